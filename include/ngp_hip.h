@@ -1,0 +1,264 @@
+/*
+ * ngp_hip.h — C-ABI of the MI355X-native Instant-NGP NeRF hot path.
+ *
+ * One shared library, libngp_hip.so (instant-ngp-rendering_amd/), exports these
+ * entry points.  Plain pointers and sizes only: no torch, tcnn or C++ types cross
+ * this boundary.  Device pointers are hipMalloc'd (or torch-allocated) HBM
+ * addresses; `ngp_stream` is a hipStream_t (0 = the null stream).
+ *
+ * Each entry names the reference interface it replaces (paths are relative to
+ * the reference checkout, fnysalehi/instant-ngp-rendering):
+ *
+ *   ngp_model_create          NerfNetwork<T>::NerfNetwork    include/neural-graphics-primitives/nerf_network.h:81
+ *                             + Testbed::reset_network        src/testbed.cu:3624 (hash-grid auto params :3680-3724,
+ *                               Trainer/Optimizer creation :3726-3727,3846)
+ *   ngp_model_encode          tcnn GridEncoding::inference_mixed_precision (called at nerf_network.h:113-118)
+ *   ngp_model_infer           NerfNetwork::inference_mixed_precision_impl   nerf_network.h:105-139
+ *   ngp_model_density         NerfNetwork::density                          nerf_network.h:270-279
+ *   ngp_train_step            Testbed::train_nerf_step        src/testbed_nerf.cu:2683-2930
+ *                             (+ Trainer::optimizer_step      src/testbed_nerf.cu:2502, unless deferred)
+ *   ngp_optimizer_step        Trainer::optimizer_step          src/testbed_nerf.cu:2502 (tcnn Ema∘ExponentialDecay∘Adam,
+ *                                                              configs/nerf/base.json:5-22)
+ *   ngp_train_read_stats      NerfCounters::update_after_training  src/testbed_nerf.cu:2422-2446
+ *   ngp_density_grid_update   Testbed::update_density_grid_nerf     src/testbed_nerf.cu:2271-2360
+ *                             + update_density_grid_mean_and_bitfield :2362-2379
+ *   ngp_render                Testbed::render_nerf / NerfTracer      src/testbed_nerf.cu:1827-1987, 1556-1761
+ *   ngp_accumulate_tonemap    CudaRenderBuffer::accumulate + tonemap src/render_buffer.cu:635-691 (kernels :232,:533)
+ *
+ * Error behaviour mirrors the reference: where the reference throws
+ * std::runtime_error (CUDA_CHECK_THROW, invalid arguments), these return a
+ * non-zero ngp_status and ngp_last_error() holds the message (thread-local).
+ * A handle is thread-compatible, not thread-safe; one handle per device.
+ */
+#ifndef NGP_HIP_H
+#define NGP_HIP_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef int ngp_status;
+#define NGP_OK 0
+#define NGP_ERR_INVALID 1
+#define NGP_ERR_HIP 2
+#define NGP_ERR_OOM 3
+#define NGP_ERR_UNSUPPORTED 4
+
+typedef struct ngp_model ngp_model;
+typedef void* ngp_stream; /* hipStream_t */
+
+/* Network + optimizer hyper-parameters (configs/nerf/base.json schema). */
+typedef struct ngp_network_config {
+	/* "encoding": HashGrid (configs/nerf/base.json:23-29) */
+	uint32_t n_levels;
+	uint32_t n_features_per_level; /* 1, 2, 4 or 8 */
+	uint32_t log2_hashmap_size;
+	uint32_t base_resolution;
+	float per_level_scale; /* resolved on the host exactly as src/testbed.cu:3710-3713 */
+	/* "network" / "rgb_network": FullyFusedMLP (configs/nerf/base.json:30-36,50-56) */
+	uint32_t n_neurons;             /* 16, 32 or 64 */
+	uint32_t density_hidden_layers; /* n_hidden_layers of "network" (1..3) */
+	uint32_t rgb_hidden_layers;     /* n_hidden_layers of "rgb_network" (1..3) */
+	/* activations (ENerfActivation, common.h:90-95) */
+	int32_t rgb_activation;     /* 0 None, 1 ReLU, 2 Logistic, 3 Exponential */
+	int32_t density_activation; /* default Exponential */
+	/* "optimizer": Ema(decay) ∘ ExponentialDecay(start, interval, base) ∘ Adam */
+	float learning_rate, beta1, beta2, epsilon, l2_reg;
+	float ema_decay;
+	uint32_t decay_start, decay_interval;
+	float decay_base;
+} ngp_network_config;
+
+/* Read-only model geometry. */
+typedef struct ngp_model_info {
+	uint64_t n_params;      /* total = n_mlp_params + n_grid_params */
+	uint64_t n_mlp_params;  /* "matrix" params first (nerf_network.h:356-371 ordering) */
+	uint64_t n_grid_params; /* hash-grid table entries x F */
+	uint32_t n_levels;
+	uint32_t n_features_per_level;
+	uint32_t encoding_width;        /* n_levels * F */
+	uint32_t padded_encoding_width; /* next multiple of 16 (tcnn alignment, nerf_network.h:82) */
+	uint32_t level_offset[32];      /* entries, GridEncoding::level_params_offset */
+	uint32_t level_size[32];
+	uint32_t level_resolution[32];
+	float level_scale[32];
+	uint32_t n_layers;             /* density layers followed by rgb layers */
+	uint32_t layer_in[8], layer_out[8];
+	uint64_t layer_param_offset[8];
+} ngp_model_info;
+
+/* Parameter buffers, all with the reference ordering [density MLP | rgb MLP | hash grid]. */
+enum {
+	NGP_PARAMS_FP32 = 0,      /* fp32 master weights (tcnn Trainer full-precision params) */
+	NGP_PARAMS_FP16 = 1,      /* fp16 training copy (network_precision_t) */
+	NGP_PARAMS_EMA_FP32 = 2,  /* Ema optimizer's running average */
+	NGP_PARAMS_INFER_FP16 = 3,/* fp16 inference params (use_inference_params=true) */
+	NGP_GRADS_FP32 = 4,       /* gradient buffer (GradientMode::Overwrite each step) */
+	NGP_ADAM_M = 5,
+	NGP_ADAM_V = 6
+};
+
+/* One training image; an array of these lives in device memory (TrainingImageMetadata,
+ * include/neural-graphics-primitives/nerf_device.cuh:44-59 + TrainingXForm common.h:179-186). */
+typedef struct ngp_image {
+	uint64_t pixels;          /* device pointer to RGBA8 (sRGB, straight alpha) rows, width*height texels */
+	uint32_t width, height;
+	float focal_length[2];    /* pixels */
+	float principal_point[2]; /* [0,1] */
+	float xform[12];          /* camera-to-world 4x3, column-major (right, up, forward, origin), NGP space */
+	int32_t lens_mode;        /* 0 Perspective (others: ELensMode, common.h:188-195) */
+	float lens_params[7];
+} ngp_image;
+
+typedef struct ngp_train_args {
+	const ngp_image* images; /* device array [n_images] */
+	uint32_t n_images;
+	uint32_t n_rays;             /* rays_per_batch (NerfCounters, adapts on the host) */
+	uint32_t n_rays_total;       /* running ray count (unused by the default sampler; kept for parity) */
+	uint32_t target_batch_size;  /* 2^18 (testbed.h:1015) */
+	uint32_t max_samples;        /* max_inference: samples the sampler may emit */
+	uint32_t training_step;      /* m_training_step before the step */
+	uint64_t rng_state, rng_inc; /* m_rng (pcg32) state; the caller advances it after the step */
+	uint32_t ray_index_offset;   /* data-parallel: this rank's first global ray index */
+	uint32_t n_rays_global;      /* data-parallel: rays over all ranks (image_idx denominator); 0 = n_rays */
+	float aabb_min[3], aabb_max[3];
+	float cone_angle_constant;
+	uint32_t max_cascade;
+	int32_t loss_type;        /* ELossType */
+	int32_t random_bg_color;  /* nerf.training.random_bg_color */
+	float background_color[3];/* sRGB, used when random_bg_color == 0 */
+	int32_t snap_to_pixel_centers;
+	int32_t train_in_linear_colors;
+	int32_t color_space;      /* EColorSpace: 0 Linear, 1 SRGB */
+	float near_distance;
+	int32_t optimize_mlp;      /* m_train_network */
+	int32_t optimize_encoding; /* m_train_encoding */
+	int32_t defer_optimizer;   /* 1: leave grads for an external all-reduce, then call ngp_optimizer_step */
+} ngp_train_args;
+
+typedef struct ngp_train_stats {
+	uint32_t n_rays;
+	uint32_t n_rays_with_samples;
+	uint32_t measured_batch_size_before_compaction; /* numsteps_counter */
+	uint32_t measured_batch_size;                   /* numsteps_counter_compacted */
+	float loss;                                     /* sum over rays of mean per-ray loss / n_rays */
+} ngp_train_stats;
+
+typedef struct ngp_grid_args {
+	const ngp_image* images; /* device array, for mark_untrained_density_grid */
+	uint32_t n_images;
+	float aabb_min[3], aabb_max[3];
+	uint32_t max_cascade;
+	float decay;                     /* nerf.training.density_grid_decay */
+	uint32_t n_uniform_samples;      /* NERF_GRID_N_CELLS * n_cascades (first 256 steps) or /4 */
+	uint32_t n_nonuniform_samples;
+	uint64_t rng_state, rng_inc;     /* nerf.training.density_grid_rng; advanced by 2^32 twice inside */
+	uint32_t ema_step;               /* m_nerf.density_grid_ema_step */
+	int32_t mark_untrained;          /* step 0 / image-count change (src/testbed_nerf.cu:2293-2309) */
+	int32_t clear_visible;           /* m_training_step == 0 */
+	int32_t use_inference_params;    /* reference passes false (:2350) */
+	uint32_t rank, world_size;       /* data-parallel: evaluate a 1/world_size slice, caller all-reduces (max) tmp */
+} ngp_grid_args;
+
+typedef struct ngp_render_args {
+	uint32_t width, height;
+	uint32_t sample_index;   /* spp index of this frame */
+	float camera[12];        /* 4x3 column-major camera-to-world (NGP space) */
+	float focal_length[2];   /* pixels */
+	float screen_center[2];
+	float near_distance;     /* m_render_near_distance */
+	float aabb_min[3], aabb_max[3];     /* render aabb (m_render_aabb) */
+	float train_aabb_min[3], train_aabb_max[3]; /* m_aabb (network input warp) */
+	float cone_angle_constant;
+	uint32_t max_cascade;
+	float min_transmittance; /* nerf.render_min_transmittance */
+	int32_t snap_to_pixel_centers;
+	int32_t use_inference_params; /* 1 = EMA params (render default) */
+	int32_t train_in_linear_colors;
+	/* row sharding for multi-GPU (config C): render rows y with (y / shard_rows) % shard_count == shard_index */
+	uint32_t shard_index, shard_count, shard_rows;
+} ngp_render_args;
+
+/* --- lifecycle -------------------------------------------------------------------- */
+ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint64_t seed, ngp_model** out);
+ngp_status ngp_model_destroy(ngp_model* model);
+ngp_status ngp_model_get_info(const ngp_model* model, ngp_model_info* info);
+ngp_status ngp_model_buffer(ngp_model* model, int kind, void** dev_ptr, size_t* bytes);
+/* After writing NGP_PARAMS_FP32 (e.g. snapshot load): refresh fp16 / EMA / inference copies. */
+ngp_status ngp_model_params_updated(ngp_model* model, int reset_optimizer, ngp_stream stream);
+ngp_status ngp_model_reset_optimizer(ngp_model* model, ngp_stream stream);
+
+/* --- network evaluation ------------------------------------------------------------ */
+/* pos: n positions in [0,1]^3, `stride` floats apart.  enc_out: [n_levels][n][F] fp16 (level-major). */
+ngp_status ngp_model_encode(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
+                            uint16_t* enc_out, int use_inference_params, ngp_stream stream);
+/* Debug/parity: corner indices [n][n_levels][8] and trilinear weights [n][n_levels][8]. */
+ngp_status ngp_model_encode_indices(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
+                                    uint32_t* idx_out, float* w_out, ngp_stream stream);
+/* coords: NerfCoordinate records (pos[3], dt, dir[3], extra...) of `floats_per_coord` floats.
+ * out: [n][4] fp16 = (rgb raw x3, density raw) (the 16-row padded output of the reference, rows 0-3). */
+ngp_status ngp_model_infer(ngp_model* model, const float* coords, uint32_t floats_per_coord, uint32_t n,
+                           uint16_t* out, int use_inference_params, ngp_stream stream);
+/* pos: n positions (stride floats). out: [n] fp16 raw density (row 0 of the density MLP output). */
+ngp_status ngp_model_density(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
+                             uint16_t* out, int use_inference_params, ngp_stream stream);
+/* Parity entry for the fused MLP backward (NerfNetwork::backward_impl, nerf_network.h:189-268):
+ * enc [n_levels][n][F] fp16, dirs [n][3] (warped to [0,1]), dL_dout [n][4] fp16 (loss-scaled),
+ * sample_weight [n] fp32 (rollover multiplicity, may be NULL). Accumulates MLP grads into
+ * NGP_GRADS_FP32 and writes dL_denc [n_levels][n][F] fp16. */
+ngp_status ngp_model_backward(ngp_model* model, const uint16_t* enc, const float* dirs, uint32_t n,
+                              const uint16_t* dL_dout, const float* sample_weight, uint16_t* dL_denc,
+                              ngp_stream stream);
+/* Parity entry for the hash-grid backward scatter: dL_denc [n_levels][n][F] fp16 -> grads. */
+ngp_status ngp_model_encode_backward(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
+                                     const uint16_t* dL_denc, ngp_stream stream);
+
+/* --- training ---------------------------------------------------------------------- */
+ngp_status ngp_train_step(ngp_model* model, const ngp_train_args* args, ngp_stream stream);
+ngp_status ngp_optimizer_step(ngp_model* model, uint32_t training_step, int optimize_mlp, int optimize_encoding,
+                              ngp_stream stream);
+ngp_status ngp_train_read_stats(ngp_model* model, ngp_train_stats* stats, ngp_stream stream);
+/* Debug/parity: device pointers to the last step's scratch (valid until the next step). */
+enum {
+	NGP_SCRATCH_RAY_NUMSTEPS = 0, /* [n_rays][2] u32: (numsteps, base) after sampling */
+	NGP_SCRATCH_COORDS = 1,       /* [max_samples][8] f32: pos3, dt, dir3, pad */
+	NGP_SCRATCH_MLP_OUT = 2,      /* [max_samples][4] f16 */
+	NGP_SCRATCH_RAY_COMPACTED = 3,/* [n_rays][2] u32: (compacted numsteps, compacted base) */
+	NGP_SCRATCH_DLOSS = 4,        /* [target_batch][4] f16 */
+	NGP_SCRATCH_LOSS = 5,         /* [n_rays] f32 */
+	NGP_SCRATCH_COMPACT_COORDS = 6/* [target_batch][8] f32 */
+};
+ngp_status ngp_train_scratch(ngp_model* model, int kind, void** dev_ptr, size_t* bytes);
+
+/* --- occupancy grid ------------------------------------------------------------------ */
+ngp_status ngp_density_grid_update(ngp_model* model, const ngp_grid_args* args, ngp_stream stream);
+/* Split form for data-parallel grids: sample+evaluate into tmp, caller all-reduces tmp (max), then finish. */
+ngp_status ngp_density_grid_evaluate(ngp_model* model, const ngp_grid_args* args, ngp_stream stream);
+ngp_status ngp_density_grid_finish(ngp_model* model, const ngp_grid_args* args, ngp_stream stream);
+/* Recompute mean + bitfield + mips from the current grid (update_density_grid_mean_and_bitfield). */
+ngp_status ngp_density_grid_bitfield(ngp_model* model, uint32_t max_cascade, ngp_stream stream);
+/* grid: [n_cascades][128^3] f32 (Morton order); bitfield: [8][128^3/8] u8; tmp: evaluation buffer;
+ * mean: 1 f32 (device). */
+ngp_status ngp_density_grid_buffers(ngp_model* model, float** grid, uint8_t** bitfield, float** tmp, float** mean);
+
+/* --- rendering --------------------------------------------------------------------- */
+/* frame: [H][W][4] f32 premultiplied RGBA, depth: [H][W] f32 (device, caller-owned);
+ * cleared and shaded for the rows this shard owns. */
+ngp_status ngp_render(ngp_model* model, const ngp_render_args* args, float* frame, float* depth, ngp_stream stream);
+/* accumulate_kernel + tonemap_kernel (render_buffer.cu:232,533): accum = running mean over spp,
+ * out = accum composited over background, exposure/tonemap(Identity), colour-space conversion. */
+ngp_status ngp_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t width, uint32_t height,
+                                  uint32_t sample_count, int color_space, float exposure,
+                                  const float* background_rgba, int output_srgb, ngp_stream stream);
+
+const char* ngp_last_error(void);
+const char* ngp_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* NGP_HIP_H */

@@ -1,0 +1,265 @@
+// density_grid.hip — occupancy-grid update for gfx950.
+//
+//  k_mark_untrained     mark_untrained_density_grid               src/testbed_nerf.cu:74-145
+//  k_grid_samples       generate_grid_samples_nerf_nonuniform     src/testbed_nerf.cu:185-214
+//  k_splat              splat_grid_samples_nerf_max_nearest_neighbor :216-232
+//  k_ema                ema_grid_samples_nerf                     :253-276
+//  k_grid_sum / mean    reduce_sum(max(v,0)/N) of update_density_grid_mean_and_bitfield :2362-2370
+//  k_grid_to_bitfield   grid_to_bitfield                          :284-308
+//  k_bitfield_max_pool  bitfield_max_pool                         :310-331
+//
+// The mean uses an exact fixed-point (2^-24) integer sum so the threshold, and
+// therefore every bitfield bit, is independent of summation order (the
+// reference's float atomics are not).
+#include "ngp_internal.h"
+
+namespace ngp {
+
+__device__ __forceinline__ m43 load_xform_g(const float* x) {
+	m43 m;
+	for (int c = 0; c < 4; ++c) m.c[c] = mk3(x[3 * c + 0], x[3 * c + 1], x[3 * c + 2]);
+	return m;
+}
+
+// inverse of the 3x3 rotation/scale part (column-major)
+__device__ __forceinline__ void inverse3(const m43& m, v3 out_rows[3]) {
+	const v3 a = m.c[0], b = m.c[1], c = m.c[2];
+	// columns a,b,c: M = [a b c]; inverse rows are (b x c, c x a, a x b) / det
+	const v3 bc = mk3(b.y * c.z - b.z * c.y, b.z * c.x - b.x * c.z, b.x * c.y - b.y * c.x);
+	const v3 ca = mk3(c.y * a.z - c.z * a.y, c.z * a.x - c.x * a.z, c.x * a.y - c.y * a.x);
+	const v3 ab = mk3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+	const float det = dot(a, bc);
+	const float inv = 1.0f / det;
+	out_rows[0] = bc * inv;
+	out_rows[1] = ca * inv;
+	out_rows[2] = ab * inv;
+}
+
+__global__ void __launch_bounds__(256) k_mark_untrained(uint32_t n_elements, float* __restrict__ grid,
+                                                        const ngp_image* __restrict__ images, uint32_t n_images,
+                                                        int clear_visible) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n_elements) return;
+	const uint32_t level = i / NERF_GRID_N_CELLS, pos_idx = i % NERF_GRID_N_CELLS;
+	const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
+	const float voxel_size = scalbnf(1.0f / (float)NERF_GRIDSIZE, (int)level);
+	const v3 pos = (mk3((float)x, (float)y, (float)z) / (float)NERF_GRIDSIZE - 0.5f) * scalbnf(1.0f, (int)level) + 0.5f;
+	const uint32_t min_count = 1;
+	uint32_t count = 0;
+	for (uint32_t j = 0; j < n_images && count < min_count; ++j) {
+		const ngp_image im = images[j];
+		if (im.lens_mode == 2 || im.lens_mode == 3 || im.lens_mode == 5) {  // FTheta, LatLong, Equirectangular
+			++count;
+			continue;
+		}
+		const m43 xf = load_xform_g(im.xform);
+		v3 inv[3];
+		inverse3(xf, inv);
+		for (uint32_t k = 0; k < 8; ++k) {
+			const v3 corner = pos + mk3((k & 1) ? voxel_size : 0.0f, (k & 2) ? voxel_size : 0.0f, (k & 4) ? voxel_size : 0.0f);
+			const v3 dir = normalize(corner - xf.c[3]);
+			if (dot(dir, xf.c[2]) < 1e-4f) continue;
+			// pos_to_uv (common_device.cuh:497-531), perspective
+			const v3 rel = corner - xf.c[3];
+			v3 cd = mk3(dot(inv[0], rel), dot(inv[1], rel), dot(inv[2], rel));
+			cd = cd / cd.z;
+			const float u = cd.x * im.focal_length[0] / (float)im.width + im.principal_point[0];
+			const float v = cd.y * im.focal_length[1] / (float)im.height + im.principal_point[1];
+			// uv_to_ray back-projection check
+			v3 rd = mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
+			            (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+			rd = normalize(rot(xf, rd));
+			if (length(rd - dir) < 1e-3f && u > 0.0f && v > 0.0f && u < 1.0f && v < 1.0f) {
+				++count;
+				break;
+			}
+		}
+	}
+	if (clear_visible || (grid[i] < 0) != (count < min_count)) grid[i] = (count >= min_count) ? 0.0f : -1.0f;
+}
+
+__global__ void __launch_bounds__(256) k_grid_samples(uint32_t n_elements, pcg32 rng, uint32_t step, aabb3 aabb,
+                                                      const float* __restrict__ grid_in, float* __restrict__ out,
+                                                      uint32_t* __restrict__ indices, uint32_t n_cascades,
+                                                      float thresh) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n_elements) return;
+	rng.advance((int64_t)i * 4);
+	const uint32_t level = (uint32_t)(rng.next_float() * (float)n_cascades) % n_cascades;
+	uint32_t idx = 0;
+	for (uint32_t j = 0; j < 10; ++j) {
+		idx = ((i + step * n_elements) * 56924617u + j * 19349663u + 96925573u) % NERF_GRID_N_CELLS;
+		idx += level * NERF_GRID_N_CELLS;
+		if (grid_in[idx] > thresh) break;
+	}
+	const uint32_t pos_idx = idx % NERF_GRID_N_CELLS;
+	const uint32_t x = morton3D_invert(pos_idx >> 0), y = morton3D_invert(pos_idx >> 1), z = morton3D_invert(pos_idx >> 2);
+	const float r0 = rng.next_float(), r1 = rng.next_float(), r2 = rng.next_float();
+	const v3 pos = ((mk3((float)x, (float)y, (float)z) + mk3(r0, r1, r2)) / (float)NERF_GRIDSIZE - 0.5f) *
+	                   scalbnf(1.0f, (int)level) + 0.5f;
+	const v3 w = aabb_relative(aabb, pos);
+	reinterpret_cast<float4*>(out)[i] = make_float4(w.x, w.y, w.z, warp_dt(MIN_CONE_STEPSIZE));
+	indices[i] = idx;
+}
+
+__global__ void __launch_bounds__(256) k_splat(uint32_t n, const uint32_t* __restrict__ indices,
+                                               const __half* __restrict__ out, float* __restrict__ grid_tmp,
+                                               int density_act) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	const float mlp = network_to_density(__half2float(out[i]), density_act);
+	const float thickness = mlp * MIN_CONE_STEPSIZE;
+	atomicMax(reinterpret_cast<uint32_t*>(grid_tmp) + indices[i], __float_as_uint(thickness));
+}
+
+__global__ void __launch_bounds__(256) k_ema(uint32_t n, float decay, float* __restrict__ grid,
+                                             const float* __restrict__ tmp) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	const float prev = grid[i];
+	grid[i] = prev < 0.0f ? prev : fmaxf(prev * decay, tmp[i]);
+}
+
+__global__ void __launch_bounds__(256) k_grid_sum(const float* __restrict__ grid, uint32_t n,
+                                                  unsigned long long* __restrict__ sum) {
+	const uint32_t i0 = blockIdx.x * 1024u + threadIdx.x;
+	unsigned long long s = 0;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const uint32_t i = i0 + 256u * k;
+		if (i < n) {
+			const float v = fminf(fmaxf(grid[i], 0.0f), 65536.0f);
+			s += (unsigned long long)(v * 16777216.0f);
+		}
+	}
+	for (int d = 32; d > 0; d >>= 1) s += __shfl_down(s, d, 64);
+	if ((threadIdx.x & 63) == 0) atomicAdd(sum, s);
+}
+
+__global__ void k_grid_mean(const unsigned long long* __restrict__ sum, float* __restrict__ mean) {
+	*mean = (float)((double)*sum / 16777216.0 / (double)NERF_GRID_N_CELLS);
+}
+
+__global__ void __launch_bounds__(256) k_grid_to_bitfield(uint32_t n_elements, uint32_t n_nonzero,
+                                                          const float* __restrict__ grid, uint8_t* __restrict__ bits,
+                                                          const float* __restrict__ mean) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n_elements) return;
+	if (i >= n_nonzero) {
+		bits[i] = 0;
+		return;
+	}
+	const float thresh = fminf(NERF_MIN_OPTICAL_THICKNESS, *mean);
+	uint8_t b = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < 8; ++j) b |= grid[i * 8 + j] > thresh ? (uint8_t)(1u << j) : (uint8_t)0;
+	bits[i] = b;
+}
+
+__global__ void __launch_bounds__(256) k_bitfield_max_pool(uint32_t n, const uint8_t* __restrict__ prev,
+                                                           uint8_t* __restrict__ next) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	uint8_t b = 0;
+#pragma unroll
+	for (uint32_t j = 0; j < 8; ++j) b |= prev[i * 8 + j] > 0 ? (uint8_t)(1u << j) : (uint8_t)0;
+	const uint32_t x = morton3D_invert(i >> 0) + NERF_GRIDSIZE / 8;
+	const uint32_t y = morton3D_invert(i >> 1) + NERF_GRIDSIZE / 8;
+	const uint32_t z = morton3D_invert(i >> 2) + NERF_GRIDSIZE / 8;
+	next[morton3D(x, y, z)] |= b;
+}
+
+void grid_reserve(ngp_model* m, uint32_t n_cascades, uint32_t n_samples) {
+	GridState& g = m->gs;
+	if (g.grid.n < (size_t)NERF_GRID_N_CELLS * n_cascades) {
+		// keep contents on growth (cascade count changes only when the dataset changes)
+		DevBuf<float> old = g.grid;
+		g.grid.ptr = nullptr;
+		g.grid.n = 0;
+		g.grid.reserve((size_t)NERF_GRID_N_CELLS * n_cascades);
+		NGP_HIP_CHECK(hipMemset(g.grid.ptr, 0, g.grid.bytes()));
+		if (old.ptr) {
+			NGP_HIP_CHECK(hipMemcpy(g.grid.ptr, old.ptr, old.bytes(), hipMemcpyDeviceToDevice));
+			old.release();
+		}
+	}
+	g.tmp.reserve((size_t)NERF_GRID_N_CELLS * n_cascades);
+	g.n_cascades = std::max(g.n_cascades, n_cascades);
+	g.positions.reserve(4 * (size_t)std::max(n_samples, 1u));
+	g.indices.reserve(std::max(n_samples, 1u));
+	g.enc.reserve((size_t)m->lt.n_levels * std::max(n_samples, 1u) * m->lt.F);
+	g.out.reserve(std::max(n_samples, 1u));
+}
+
+void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
+	GridState& g = m->gs;
+	const uint32_t n_cascades = a->max_cascade + 1;
+	const uint32_t n_elements = NERF_GRID_N_CELLS * n_cascades;
+	const uint32_t n_total = a->n_uniform_samples + a->n_nonuniform_samples;
+	grid_reserve(m, n_cascades, n_total);
+	aabb3 aabb;
+	aabb.min = mk3(a->aabb_min[0], a->aabb_min[1], a->aabb_min[2]);
+	aabb.max = mk3(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2]);
+
+	if (a->mark_untrained) {
+		k_mark_untrained<<<div_up(n_elements, 256), 256, 0, s>>>(n_elements, g.grid.ptr, a->images, a->n_images,
+		                                                         a->clear_visible);
+	}
+	NGP_HIP_CHECK(hipMemsetAsync(g.tmp.ptr, 0, sizeof(float) * n_elements, s));
+	pcg32 rng;
+	rng.state = a->rng_state;
+	rng.inc = a->rng_inc;
+	if (a->n_uniform_samples)
+		k_grid_samples<<<div_up(a->n_uniform_samples, 256), 256, 0, s>>>(a->n_uniform_samples, rng, a->ema_step, aabb,
+		                                                                  g.grid.ptr, g.positions.ptr, g.indices.ptr,
+		                                                                  n_cascades, -0.01f);
+	rng.advance();
+	if (a->n_nonuniform_samples)
+		k_grid_samples<<<div_up(a->n_nonuniform_samples, 256), 256, 0, s>>>(
+		    a->n_nonuniform_samples, rng, a->ema_step, aabb, g.grid.ptr, g.positions.ptr + 4 * (size_t)a->n_uniform_samples,
+		    g.indices.ptr + a->n_uniform_samples, n_cascades, NERF_MIN_OPTICAL_THICKNESS);
+	NGP_HIP_CHECK(hipGetLastError());
+
+	// Data-parallel: this rank evaluates a contiguous 1/world slice; tmp is max-reduced by the caller.
+	const uint32_t world = std::max(a->world_size, 1u);
+	const uint32_t per = div_up(n_total, world);
+	const uint32_t first = std::min(n_total, a->rank * per);
+	const uint32_t cnt = std::min(n_total - first, per);
+	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
+	if (cnt) {
+		launch_hashgrid_fwd(m->lt, g.positions.ptr + 4 * (size_t)first, 4, cnt, table, g.enc.ptr, cnt, s);
+		launch_mlp_density(m, frags, g.enc.ptr, cnt, cnt, g.out.ptr, s);
+		k_splat<<<div_up(cnt, 256), 256, 0, s>>>(cnt, g.indices.ptr + first, g.out.ptr, g.tmp.ptr,
+		                                        m->cfg.density_activation);
+		NGP_HIP_CHECK(hipGetLastError());
+	}
+}
+
+void run_grid_bitfield(ngp_model* m, uint32_t max_cascade, hipStream_t s) {
+	GridState& g = m->gs;
+	g.bitfield.reserve(NERF_GRID_N_CELLS / 8 * NERF_CASCADES);
+	g.mean.reserve(1);
+	g.sum.reserve(1);
+	grid_reserve(m, max_cascade + 1, 1);
+	const uint32_t N = NERF_GRID_N_CELLS;
+	NGP_HIP_CHECK(hipMemsetAsync(g.sum.ptr, 0, sizeof(unsigned long long), s));
+	k_grid_sum<<<div_up(N, 1024), 256, 0, s>>>(g.grid.ptr, N, g.sum.ptr);
+	k_grid_mean<<<1, 1, 0, s>>>(g.sum.ptr, g.mean.ptr);
+	k_grid_to_bitfield<<<div_up(N / 8 * NERF_CASCADES, 256), 256, 0, s>>>(N / 8 * NERF_CASCADES, N / 8 * (max_cascade + 1),
+	                                                                      g.grid.ptr, g.bitfield.ptr, g.mean.ptr);
+	for (uint32_t level = 1; level < NERF_CASCADES; ++level)
+		k_bitfield_max_pool<<<div_up(N / 64, 256), 256, 0, s>>>(N / 64, g.bitfield.ptr + (size_t)(level - 1) * N / 8,
+		                                                        g.bitfield.ptr + (size_t)level * N / 8);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void run_grid_finish(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
+	GridState& g = m->gs;
+	const uint32_t n_elements = NERF_GRID_N_CELLS * (a->max_cascade + 1);
+	k_ema<<<div_up(n_elements, 256), 256, 0, s>>>(n_elements, a->decay, g.grid.ptr, g.tmp.ptr);
+	NGP_HIP_CHECK(hipGetLastError());
+	run_grid_bitfield(m, a->max_cascade, s);
+}
+
+}  // namespace ngp

@@ -1,0 +1,229 @@
+// hashgrid.hip — multiresolution hash-grid encoding, forward and backward, gfx950.
+//
+// Restates tiny-cuda-nn's GridEncodingTemplated (HashGrid, Linear interpolation,
+// CoherentPrime hash) as used by NerfNetwork (include/neural-graphics-primitives/
+// nerf_network.h:82, configs/nerf/base.json:23-29).  The per-level geometry is
+// resolved once on the host (LevelTable) so host, oracle and device agree bit for
+// bit on scale/resolution/offset.
+//
+// MI355X mapping
+//  * one thread = one (sample, level); each thread issues its 8 corner gathers
+//    back to back (8 independent loads in flight per lane).
+//  * XCD-aware block order: when n_levels % 8 == 0 every workgroup of level l is
+//    placed on the XCD group b % 8 == l % 8, so each XCD's private 4 MiB L2 only
+//    ever holds the tables of n_levels/8 levels (2 MiB each at T=2^19) instead of
+//    the whole 24 MiB table.  Placement only changes speed, never results.
+//  * output is level-major [L][n][F] (fp16): a wave of 64 consecutive samples of
+//    one level writes 64*F*2 contiguous bytes.
+//  * features accumulate in fp32 (tcnn accumulates in fp16) and are rounded once.
+#include "ngp_internal.h"
+
+namespace ngp {
+
+__device__ __forceinline__ void map_block(uint32_t b, uint32_t n_chunks, uint32_t n_levels, uint32_t* level,
+                                          uint32_t* chunk) {
+	if ((n_levels & 7u) == 0) {
+		const uint32_t lpx = n_levels >> 3;
+		const uint32_t x = b & 7u, k = b >> 3;
+		*level = x + 8u * (k % lpx);
+		*chunk = k / lpx;
+	} else {
+		*level = b / n_chunks;
+		*chunk = b % n_chunks;
+	}
+}
+
+struct Corner {
+	float px, py, pz;
+	uint32_t gx, gy, gz;
+};
+
+__device__ __forceinline__ void pos_fract(float input, float scale, float* frac, uint32_t* grid) {
+	// tcnn pos_fract: pos = fmaf(scale, x, 0.5); grid = floor; frac = pos - floor
+	float p = fmaf(scale, input, 0.5f);
+	float f = floorf(p);
+	*grid = (uint32_t)(int)f;
+	*frac = p - f;
+}
+
+__device__ __forceinline__ uint32_t grid_index(uint32_t hashed, uint32_t size, uint32_t res, uint32_t x, uint32_t y,
+                                               uint32_t z) {
+	uint32_t idx;
+	if (hashed) {
+		idx = (x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u);
+	} else {
+		idx = x + y * res + z * res * res;
+	}
+	return idx % size;
+}
+
+template <uint32_t F>
+struct FeatVec;
+template <>
+struct FeatVec<1> { using T = __half; };
+template <>
+struct FeatVec<2> { using T = uint32_t; };
+template <>
+struct FeatVec<4> { using T = uint2; };
+template <>
+struct FeatVec<8> { using T = uint4; };
+
+template <uint32_t F>
+__device__ __forceinline__ void unpack(const typename FeatVec<F>::T& v, float* out) {
+	const __half* h = reinterpret_cast<const __half*>(&v);
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f) out[f] = __half2float(h[f]);
+}
+
+template <uint32_t F>
+__global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
+                                                      const __half* __restrict__ table, const LevelTable lt,
+                                                      __half* __restrict__ enc, uint32_t enc_plane, uint32_t n_chunks,
+                                                      const uint32_t* __restrict__ n_dev) {
+	uint32_t level, chunk;
+	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
+	const uint32_t i = chunk * 256u + threadIdx.x;
+	if (n_dev) n = min(n, *n_dev);
+	if (i >= n) return;
+
+	const float scale = lt.scale[level];
+	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
+	using VT = typename FeatVec<F>::T;
+	const VT* tab = reinterpret_cast<const VT*>(table + (size_t)lt.offset[level] * F);
+
+	float fx, fy, fz;
+	uint32_t gx, gy, gz;
+	pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
+	pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
+	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
+
+	VT vals[8];
+#pragma unroll
+	for (uint32_t c = 0; c < 8; ++c) {
+		const uint32_t idx = grid_index(hashed, size, res, gx + (c & 1u), gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u));
+		vals[c] = tab[idx];
+	}
+	float acc[F];
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f) acc[f] = 0.0f;
+#pragma unroll
+	for (uint32_t c = 0; c < 8; ++c) {
+		float w = 1.0f;
+		w *= (c & 1u) ? fx : 1.0f - fx;
+		w *= (c & 2u) ? fy : 1.0f - fy;
+		w *= (c & 4u) ? fz : 1.0f - fz;
+		float v[F];
+		unpack<F>(vals[c], v);
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) acc[f] = fmaf(w, v[f], acc[f]);
+	}
+	VT o;
+	__half* oh = reinterpret_cast<__half*>(&o);
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f) oh[f] = __float2half_rn(acc[f]);
+	reinterpret_cast<VT*>(enc)[(size_t)level * enc_plane + i] = o;
+}
+
+template <uint32_t F>
+__global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
+                                                      const __half* __restrict__ denc, uint32_t enc_plane,
+                                                      const LevelTable lt, float* __restrict__ grad,
+                                                      uint32_t n_chunks, const uint32_t* __restrict__ n_dev) {
+	uint32_t level, chunk;
+	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
+	const uint32_t i = chunk * 256u + threadIdx.x;
+	if (n_dev) n = min(n, *n_dev);
+	if (i >= n) return;
+
+	using VT = typename FeatVec<F>::T;
+	float g[F];
+	unpack<F>(reinterpret_cast<const VT*>(denc)[(size_t)level * enc_plane + i], g);
+	bool any = false;
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
+	if (!any) return;
+
+	const float scale = lt.scale[level];
+	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
+	float* gtab = grad + (size_t)lt.offset[level] * F;
+
+	float fx, fy, fz;
+	uint32_t gx, gy, gz;
+	pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
+	pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
+	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
+
+#pragma unroll
+	for (uint32_t c = 0; c < 8; ++c) {
+		float w = 1.0f;
+		w *= (c & 1u) ? fx : 1.0f - fx;
+		w *= (c & 2u) ? fy : 1.0f - fy;
+		w *= (c & 4u) ? fz : 1.0f - fz;
+		const uint32_t idx = grid_index(hashed, size, res, gx + (c & 1u), gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u));
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) unsafeAtomicAdd(gtab + (size_t)idx * F + f, w * g[f]);
+	}
+}
+
+__global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const float* __restrict__ pos, uint32_t stride,
+                                                          const LevelTable lt, uint32_t* __restrict__ idx_out,
+                                                          float* __restrict__ w_out) {
+	const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+	if (t >= n * lt.n_levels) return;
+	const uint32_t i = t / lt.n_levels, level = t % lt.n_levels;
+	const float scale = lt.scale[level];
+	float fx, fy, fz;
+	uint32_t gx, gy, gz;
+	pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
+	pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
+	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
+	for (uint32_t c = 0; c < 8; ++c) {
+		float w = 1.0f;
+		w *= (c & 1u) ? fx : 1.0f - fx;
+		w *= (c & 2u) ? fy : 1.0f - fy;
+		w *= (c & 4u) ? fz : 1.0f - fz;
+		const uint32_t idx = grid_index(lt.hashed[level], lt.size[level], lt.res[level], gx + (c & 1u),
+		                                gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u));
+		idx_out[((size_t)i * lt.n_levels + level) * 8 + c] = lt.offset[level] + idx;
+		w_out[((size_t)i * lt.n_levels + level) * 8 + c] = w;
+	}
+}
+
+void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
+                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev) {
+	if (n == 0) return;
+	const uint32_t n_chunks = div_up(n, 256);
+	const uint32_t blocks = n_chunks * lt.n_levels;
+	switch (lt.F) {
+		case 1: k_hashgrid_fwd<1><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 2: k_hashgrid_fwd<2><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 4: k_hashgrid_fwd<4><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 8: k_hashgrid_fwd<8><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
+	}
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
+                         uint32_t enc_plane, float* grad_table, hipStream_t s, const uint32_t* n_dev) {
+	if (n == 0) return;
+	const uint32_t n_chunks = div_up(n, 256);
+	const uint32_t blocks = n_chunks * lt.n_levels;
+	switch (lt.F) {
+		case 1: k_hashgrid_bwd<1><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 2: k_hashgrid_bwd<2><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 4: k_hashgrid_bwd<4><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 8: k_hashgrid_bwd<8><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
+	}
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
+                             float* w, hipStream_t s) {
+	if (n == 0) return;
+	k_hashgrid_indices<<<div_up((uint64_t)n * lt.n_levels, 256), 256, 0, s>>>(n, pos, stride, lt, idx, w);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ngp

@@ -1,0 +1,733 @@
+// mlp.hip — fused NeRF MLPs (density MLP + SH + rgb MLP) on gfx950 fp16 MFMA.
+//
+// Restates tiny-cuda-nn FullyFusedMLP<half, W> as composed by NerfNetwork
+// (include/neural-graphics-primitives/nerf_network.h:81-139 forward, :189-268
+// backward): enc --density MLP--> [density_out(16) | SH4(dir)(16)] --rgb MLP--> rgb.
+//
+// MI355X design
+//  * v_mfma_f32_16x16x32_f16: A = weights (16 output rows x 32 inputs), B =
+//    activations (32 inputs x 16 samples), C = 16 rows x 16 samples, fp32
+//    accumulation (tcnn accumulates in fp16 WMMA fragments).
+//  * one workgroup = 4 waves; each wave owns 32 samples (two 16-sample column
+//    tiles) and keeps their activations in a private LDS image [sample][row]
+//    (fp16, row stride padded by 16 B so the B-operand ds_read_b128 is
+//    conflict-free).  Layers chain through LDS; no activation touches HBM.
+//  * weights are packed once per optimizer step into per-lane MFMA fragments
+//    (k_pack below) and copied into LDS at kernel start: one ds_read_b128 per
+//    fragment, reused for both column tiles.
+//  * training (fwd + dgrad + wgrad in one persistent launch): weight gradients
+//    are sum_s delta[s][m] * a[s][k]; both operands are read sample-major from
+//    the four waves' LDS images with ds_read_b64_tr_b16 (hardware transpose), so
+//    one 16x16 gradient tile consumes K = 128 samples per pass, accumulates in
+//    registers across the whole persistent loop and is flushed with one fp32
+//    atomic per element per workgroup.
+#include <algorithm>
+
+#include "ngp_internal.h"
+
+namespace ngp {
+
+typedef _Float16 h8 __attribute__((ext_vector_type(8)));
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+typedef short s4 __attribute__((ext_vector_type(4)));
+typedef float f4 __attribute__((ext_vector_type(4)));
+
+constexpr int SPW = 32;         // samples per wave
+constexpr int CT = SPW / 16;    // 16-sample column tiles per wave
+constexpr int WAVES = 4;
+constexpr int BLOCK = WAVES * 64;
+constexpr int SAMPLES_PER_BLOCK = WAVES * SPW;
+constexpr int FRAG_HALVES = 512;  // 64 lanes x 8 halves
+
+template <int W_, int DH_, int RH_, int KE_>
+struct Net {
+	static constexpr int W = W_, DH = DH_, RH = RH_, KE = KE_;
+	static constexpr int Wp = (W + 31) / 32 * 32;
+	static constexpr int NL = DH + RH + 2;
+	static constexpr int ENC_ROWS = 32 * KE;
+	static constexpr int out_dim(int l) { return (l == DH || l == NL - 1) ? 16 : W; }
+	static constexpr int in_rows(int l) { return l == 0 ? ENC_ROWS : (l == DH + 1 ? 32 : Wp); }
+	static constexpr bool relu_out(int l) { return !(l == DH || l == NL - 1); }
+	static constexpr bool relu_in(int l) { return !(l == 0 || l == DH + 1); }
+	static constexpr int Mt(int l) { return out_dim(l) / 16; }
+	static constexpr int Ks(int l) { return in_rows(l) / 32; }
+	static constexpr int Ms(int l) { return (out_dim(l) + 31) / 32; }
+	static constexpr int Kt(int l) { return in_rows(l) / 16; }
+	// LDS image layouts (rows per sample); TRAIN keeps every activation for wgrad.
+	template <bool TRAIN>
+	static constexpr int rows() { return TRAIN ? ENC_ROWS + (DH + RH) * Wp + 32 : ENC_ROWS + 2 * Wp + 32; }
+	template <bool TRAIN>
+	static constexpr int x_seg() { return TRAIN ? ENC_ROWS + DH * Wp : ENC_ROWS + 2 * Wp; }
+	template <bool TRAIN>
+	static constexpr int dens_hidden(int h) { return TRAIN ? ENC_ROWS + h * Wp : ENC_ROWS + (h % 2) * Wp; }
+	template <bool TRAIN>
+	static constexpr int rgb_hidden(int r) { return TRAIN ? ENC_ROWS + DH * Wp + 32 + r * Wp : ENC_ROWS + (r % 2) * Wp; }
+	template <bool TRAIN>
+	static constexpr int seg_in(int l) {
+		return l == 0 ? 0 : (l <= DH ? dens_hidden<TRAIN>(l - 1) : (l == DH + 1 ? x_seg<TRAIN>() : rgb_hidden<TRAIN>(l - DH - 2)));
+	}
+	template <bool TRAIN>
+	static constexpr int seg_out(int l) {
+		return l < DH ? dens_hidden<TRAIN>(l) : (l == DH ? x_seg<TRAIN>() : (l < NL - 1 ? rgb_hidden<TRAIN>(l - DH - 1) : -1));
+	}
+	template <bool TRAIN>
+	static constexpr int stride() { return rows<TRAIN>() + 8; }  // halves; +16 B breaks bank aliasing
+	static constexpr int fwd_frags_upto(int L) {
+		int s = 0;
+		for (int l = 0; l < L; ++l) s += Mt(l) * Ks(l);
+		return s;
+	}
+	static constexpr int fwd_frags() { return fwd_frags_upto(NL); }
+	static constexpr int bwd_frags() {
+		int s = 0;
+		for (int l = 0; l < NL; ++l) s += Kt(l) * Ms(l);
+		return s;
+	}
+	static constexpr int fwd_off(int l) { return fwd_frags_upto(l) * FRAG_HALVES; }
+	static constexpr int bwd_off(int l) {
+		int s = fwd_frags();
+		for (int i = 0; i < l; ++i) s += Kt(i) * Ms(i);
+		return s * FRAG_HALVES;
+	}
+	// weight-gradient 16x16 tiles per layer of the [out][in] matrix
+	static constexpr int KT16(int l) { return in_rows(l) / 16; }
+	static constexpr int gtiles(int l) { return Mt(l) * KT16(l); }
+	static constexpr int gtile_base(int l) {
+		int s = 0;
+		for (int i = 0; i < l; ++i) s += gtiles(i);
+		return s;
+	}
+	static constexpr int slots() { return (gtile_base(NL) + WAVES - 1) / WAVES; }
+	static constexpr int drows() { return Wp > 32 ? Wp : 32; }
+	static constexpr int dstride() { return 2 * drows() + 8; }
+	static constexpr size_t lds_infer() { return (size_t)fwd_frags() * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<false>() * 2; }
+	static constexpr size_t lds_density() { return (size_t)fwd_frags_upto(DH + 1) * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<false>() * 2; }
+	static constexpr size_t lds_train() {
+		return (size_t)(fwd_frags() + bwd_frags()) * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<true>() * 2 +
+		       (size_t)WAVES * SPW * dstride() * 2;
+	}
+};
+
+struct MlpArgs {
+	const __half* frags;
+	const __half* enc;
+	uint32_t enc_plane;
+	const float* coords;
+	uint32_t coord_stride;
+	uint32_t n;
+	uint32_t E;        // encoding width (L*F)
+	uint32_t F;
+	uint32_t enc_pad;  // param input width of the first density layer (multiple of 16)
+	__half* out;
+	const __half* dloss;
+	const float* weight;
+	float* grads;
+	__half* denc;
+	uint64_t param_off[MAX_LAYERS];
+	uint32_t param_in[MAX_LAYERS];
+	const uint32_t* n_dev;  // optional device-side sample count (<= n)
+};
+
+__device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
+__device__ __forceinline__ h8 lds_h8(const _Float16* p) { return *reinterpret_cast<const h8*>(p); }
+__device__ __forceinline__ void lds_st_h4(_Float16* p, h4 v) { *reinterpret_cast<h4*>(p) = v; }
+__device__ __forceinline__ void lds_st_h8(_Float16* p, h8 v) { *reinterpret_cast<h8*>(p) = v; }
+__device__ __forceinline__ h4 tr_read(const _Float16* p) {
+	s4 r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s4*)(p));
+	return __builtin_bit_cast(h4, r);
+}
+__device__ __forceinline__ _Float16 u16h(uint32_t u) { return __builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu)); }
+__device__ __forceinline__ uint32_t n_chunks_of(uint32_t n) { return (n + SAMPLES_PER_BLOCK - 1) / SAMPLES_PER_BLOCK; }
+
+// This wave's SPW samples of the level-major encoding [L][plane][F] -> image rows [0, ENC_ROWS).
+template <class N, int STRIDE>
+__device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, uint32_t base, int lane) {
+	constexpr int CHUNKS = N::ENC_ROWS / 8;
+	for (int t = lane; t < SPW * CHUNKS; t += 64) {
+		const int smp = t % SPW, chunk = t / SPW;
+		const uint32_t i = base + smp;
+		const uint32_t k0 = chunk * 8;
+		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+		if (i < a.n && k0 < a.E) {
+			if (a.F == 2 && k0 + 8 <= a.E) {
+				const uint32_t* e = reinterpret_cast<const uint32_t*>(a.enc);
+#pragma unroll
+				for (int q = 0; q < 4; ++q) {
+					const uint32_t u = e[(size_t)(k0 / 2 + q) * a.enc_plane + i];
+					v[2 * q] = u16h(u);
+					v[2 * q + 1] = u16h(u >> 16);
+				}
+			} else if (a.F == 4 && k0 + 8 <= a.E) {
+				const uint2* e = reinterpret_cast<const uint2*>(a.enc);
+#pragma unroll
+				for (int q = 0; q < 2; ++q) {
+					const uint2 u = e[(size_t)(k0 / 4 + q) * a.enc_plane + i];
+					v[4 * q + 0] = u16h(u.x);
+					v[4 * q + 1] = u16h(u.x >> 16);
+					v[4 * q + 2] = u16h(u.y);
+					v[4 * q + 3] = u16h(u.y >> 16);
+				}
+			} else {
+				const uint16_t* e = reinterpret_cast<const uint16_t*>(a.enc);
+				for (int j = 0; j < 8; ++j) {
+					const uint32_t k = k0 + j;
+					if (k < a.E) {
+						const uint32_t lvl = k / a.F, f = k % a.F;
+						v[j] = __builtin_bit_cast(_Float16, e[((size_t)lvl * a.enc_plane + i) * a.F + f]);
+					}
+				}
+			}
+		}
+		lds_st_h8(img + smp * STRIDE + k0, v);
+	}
+}
+
+// Spherical harmonics, degree 4, of the warped direction (tcnn SphericalHarmonicsEncoding;
+// configs/nerf/base.json:37-49) into rows [x_seg+16, x_seg+32).
+template <int STRIDE>
+__device__ __forceinline__ void load_sh(const MlpArgs& a, _Float16* img, int x_seg, uint32_t base, int lane) {
+	for (int t = lane; t < SPW * 2; t += 64) {
+		const int smp = t % SPW, half = t / SPW;
+		const uint32_t i = base + smp;
+		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+		if (i < a.n) {
+			const float* c = a.coords + (size_t)i * a.coord_stride;
+			const float x = c[4] * 2.0f - 1.0f, y = c[5] * 2.0f - 1.0f, z = c[6] * 2.0f - 1.0f;
+			const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+			if (half == 0) {
+				v[0] = (_Float16)(0.28209479177387814f);
+				v[1] = (_Float16)(-0.48860251190291987f * y);
+				v[2] = (_Float16)(0.48860251190291987f * z);
+				v[3] = (_Float16)(-0.48860251190291987f * x);
+				v[4] = (_Float16)(1.0925484305920792f * xy);
+				v[5] = (_Float16)(-1.0925484305920792f * yz);
+				v[6] = (_Float16)(0.94617469575755997f * z2 - 0.31539156525251999f);
+				v[7] = (_Float16)(-1.0925484305920792f * xz);
+			} else {
+				v[0] = (_Float16)(0.54627421529603959f * x2 - 0.54627421529603959f * y2);
+				v[1] = (_Float16)(0.59004358992664352f * y * (-3.0f * x2 + y2));
+				v[2] = (_Float16)(2.8906114426405538f * xy * z);
+				v[3] = (_Float16)(0.45704579946446572f * y * (1.0f - 5.0f * z2));
+				v[4] = (_Float16)(0.3731763325901154f * z * (5.0f * z2 - 3.0f));
+				v[5] = (_Float16)(0.45704579946446572f * x * (1.0f - 5.0f * z2));
+				v[6] = (_Float16)(1.4453057213202769f * z * (x2 - y2));
+				v[7] = (_Float16)(0.59004358992664352f * x * (-x2 + 3.0f * y2));
+			}
+		}
+		lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, v);
+	}
+}
+
+// One forward layer for this wave's CT column tiles.  Output rows go to LDS
+// segment seg_out, or (final rgb layer) are returned in `res`.
+template <class N, bool TRAIN, int l>
+__device__ __forceinline__ void fwd_layer(const _Float16* frags, _Float16* img, int lane, f4 (&res)[CT]) {
+	constexpr int STRIDE = N::template stride<TRAIN>();
+	constexpr int MT = N::Mt(l), KS = N::Ks(l);
+	constexpr int SIN = N::template seg_in<TRAIN>(l), SOUT = N::template seg_out<TRAIN>(l);
+	const int g = lane >> 4, n = lane & 15;
+	h8 b[CT][KS];
+#pragma unroll
+	for (int c = 0; c < CT; ++c)
+#pragma unroll
+		for (int s = 0; s < KS; ++s) b[c][s] = lds_h8(img + (16 * c + n) * STRIDE + SIN + 32 * s + 8 * g);
+	const _Float16* fr = frags + N::fwd_off(l);
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		h8 a[KS];
+#pragma unroll
+		for (int s = 0; s < KS; ++s) a[s] = lds_h8(fr + ((mt * KS + s) * 64 + lane) * 8);
+#pragma unroll
+		for (int c = 0; c < CT; ++c) {
+			f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+			for (int s = 0; s < KS; ++s) acc = mfma(a[s], b[c][s], acc);
+			if constexpr (N::relu_out(l)) {
+#pragma unroll
+				for (int r = 0; r < 4; ++r) acc[r] = fmaxf(acc[r], 0.0f);
+			}
+			if constexpr (SOUT >= 0) {
+				h4 o = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
+				lds_st_h4(img + (16 * c + n) * STRIDE + SOUT + 16 * mt + 4 * g, o);
+			} else {
+				res[c] = acc;
+			}
+		}
+	}
+}
+
+template <class N, bool TRAIN, int l, int END>
+__device__ __forceinline__ void fwd_range(const _Float16* frags, _Float16* img, int lane, f4 (&res)[CT]) {
+	if constexpr (l < END) {
+		fwd_layer<N, TRAIN, l>(frags, img, lane, res);
+		fwd_range<N, TRAIN, l + 1, END>(frags, img, lane, res);
+	}
+}
+
+template <class N>
+__global__ void __launch_bounds__(BLOCK) k_mlp_infer(MlpArgs a) {
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	constexpr int STRIDE = N::template stride<false>();
+	constexpr int FH = N::fwd_frags() * FRAG_HALVES;
+	_Float16* frags = reinterpret_cast<_Float16*>(smem);
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	_Float16* img = frags + FH + wave * SPW * STRIDE;
+
+	for (int t = threadIdx.x; t < FH / 8; t += BLOCK)
+		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
+	for (int t = lane; t < SPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	__syncthreads();
+
+	const int g = lane >> 4, n = lane & 15;
+	const uint32_t n_chunks = n_chunks_of(a.n);
+	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
+		load_encoding<N, STRIDE>(a, img, base, lane);
+		load_sh<STRIDE>(a, img, N::template x_seg<false>(), base, lane);
+		f4 res[CT];
+		fwd_range<N, false, 0, N::NL>(frags, img, lane, res);
+		if (g == 0) {
+#pragma unroll
+			for (int c = 0; c < CT; ++c) {
+				const uint32_t i = base + 16 * c + n;
+				if (i < a.n) {
+					const _Float16 dens = img[(16 * c + n) * STRIDE + N::template x_seg<false>()];
+					h4 o = {(_Float16)res[c][0], (_Float16)res[c][1], (_Float16)res[c][2], dens};
+					*reinterpret_cast<h4*>(a.out + (size_t)i * 4) = o;
+				}
+			}
+		}
+	}
+}
+
+// Density only: enc -> density MLP -> row 0 (NerfNetwork::density, nerf_network.h:270-279).
+template <class N>
+__global__ void __launch_bounds__(BLOCK) k_mlp_density(MlpArgs a) {
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	constexpr int STRIDE = N::template stride<false>();
+	constexpr int FH = N::fwd_off(N::DH + 1);
+	_Float16* frags = reinterpret_cast<_Float16*>(smem);
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	_Float16* img = frags + FH + wave * SPW * STRIDE;
+	for (int t = threadIdx.x; t < FH / 8; t += BLOCK)
+		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
+	for (int t = lane; t < SPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	__syncthreads();
+	const uint32_t n_chunks = n_chunks_of(a.n);
+	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
+		load_encoding<N, STRIDE>(a, img, base, lane);
+		f4 res[CT];
+		fwd_range<N, false, 0, N::DH + 1>(frags, img, lane, res);
+		if (lane < SPW) {
+			const uint32_t i = base + lane;
+			if (i < a.n) a.out[i] = __builtin_bit_cast(__half, img[lane * STRIDE + N::template x_seg<false>()]);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Training: forward (activations kept), dgrad chain, wgrad via transposed reads.
+// ---------------------------------------------------------------------------
+template <class N, int l>
+__device__ __forceinline__ void wgrad_layer(const _Float16* imgs, const _Float16* dimgs, int wave, int lane,
+                                            f4 (&acc)[N::slots()], uint32_t enc_pad) {
+	constexpr int STRIDE = N::template stride<true>();
+	constexpr int DS = N::dstride();
+	constexpr int DCUR = ((N::NL - 1 - l) % 2) * N::drows();
+	constexpr int SIN = N::template seg_in<true>(l);
+	constexpr int KTN = N::KT16(l);
+	const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+#pragma unroll
+	for (int t = 0; t < N::gtiles(l); ++t) {
+		constexpr int dummy = 0;
+		(void)dummy;
+		const int gt = N::gtile_base(l) + t;
+		const int mt = t / KTN, kt = t % KTN;
+		if (gt % WAVES != wave) continue;
+		if (l == 0 && (uint32_t)(16 * kt) >= enc_pad) continue;
+		const int slot = gt / WAVES;
+		f4 c = acc[slot];
+#pragma unroll
+		for (int w2 = 0; w2 < WAVES; ++w2) {
+			const _Float16* ds = dimgs + w2 * SPW * DS + DCUR + 16 * mt + 4 * p;
+			const _Float16* as = imgs + w2 * SPW * STRIDE + SIN + 16 * kt + 4 * p;
+			const h4 a0 = tr_read(ds + (8 * g + q) * DS), a1 = tr_read(ds + (8 * g + 4 + q) * DS);
+			const h4 b0 = tr_read(as + (8 * g + q) * STRIDE), b1 = tr_read(as + (8 * g + 4 + q) * STRIDE);
+			const h8 A = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+			const h8 B = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+			c = mfma(A, B, c);
+		}
+		acc[slot] = c;
+	}
+}
+
+template <class N, int l>
+__device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* frags, const _Float16* img,
+                                            _Float16* dimg, int lane, uint32_t base) {
+	constexpr int STRIDE = N::template stride<true>();
+	constexpr int DS = N::dstride();
+	constexpr int DCUR = ((N::NL - 1 - l) % 2) * N::drows();
+	constexpr int DNXT = (1 - (N::NL - 1 - l) % 2) * N::drows();
+	constexpr int SIN = N::template seg_in<true>(l);
+	constexpr int MS = N::Ms(l);
+	constexpr int KT = (l == N::DH + 1) ? 1 : N::Kt(l);
+	const int g = lane >> 4, n = lane & 15;
+	h8 b[CT][MS];
+#pragma unroll
+	for (int c = 0; c < CT; ++c)
+#pragma unroll
+		for (int s = 0; s < MS; ++s) b[c][s] = lds_h8(dimg + (16 * c + n) * DS + DCUR + 32 * s + 8 * g);
+	const _Float16* fr = frags + N::bwd_off(l);
+#pragma unroll
+	for (int mt = 0; mt < KT; ++mt) {
+		h8 af[MS];
+#pragma unroll
+		for (int s = 0; s < MS; ++s) af[s] = lds_h8(fr + ((mt * MS + s) * 64 + lane) * 8);
+#pragma unroll
+		for (int c = 0; c < CT; ++c) {
+			f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+			for (int s = 0; s < MS; ++s) acc = mfma(af[s], b[c][s], acc);
+			const int smp = 16 * c + n;
+			const uint32_t i = base + smp;
+			if constexpr (N::relu_in(l)) {
+				const h4 act = *reinterpret_cast<const h4*>(img + smp * STRIDE + SIN + 16 * mt + 4 * g);
+#pragma unroll
+				for (int r = 0; r < 4; ++r) acc[r] = act[r] > (_Float16)0 ? acc[r] : 0.0f;
+			}
+			if constexpr (l == N::DH + 1) {
+				// add_density_gradient (nerf_network.h:63-74): dL/d(density raw) joins row 0
+				if (mt == 0 && g == 0 && i < a.n) {
+					const float w = a.weight ? a.weight[i] : 1.0f;
+					acc[0] += (float)__half2float(a.dloss[(size_t)i * 4 + 3]) * w;
+				}
+			}
+			if constexpr (l > 0) {
+				h4 o = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
+				lds_st_h4(dimg + smp * DS + DNXT + 16 * mt + 4 * g, o);
+			} else {
+				if (i < a.n) {
+#pragma unroll
+					for (int r = 0; r < 4; ++r) {
+						const uint32_t k = 16 * mt + 4 * g + r;
+						if (k < a.E) {
+							const uint32_t lvl = k / a.F, f = k % a.F;
+							a.denc[((size_t)lvl * a.enc_plane + i) * a.F + f] = __float2half_rn(acc[r]);
+						}
+					}
+				}
+			}
+		}
+	}
+	if constexpr (l == N::DH + 1) {
+		// density-output delta has 16 rows; rows 16..31 of the next k-step must be zero
+#pragma unroll
+		for (int c = 0; c < CT; ++c) lds_st_h4(dimg + (16 * c + n) * DS + DNXT + 16 + 4 * g, h4{0, 0, 0, 0});
+	}
+}
+
+template <class N, int l>
+__device__ __forceinline__ void bwd_range(const MlpArgs& a, const _Float16* frags, const _Float16* imgs,
+                                          _Float16* dimgs, int wave, int lane, uint32_t base,
+                                          f4 (&acc)[N::slots()]) {
+	if constexpr (l >= 0) {
+		constexpr int STRIDE = N::template stride<true>();
+		constexpr int DS = N::dstride();
+		__syncthreads();  // every wave's delta for layer l is in LDS
+		wgrad_layer<N, l>(imgs, dimgs, wave, lane, acc, a.enc_pad);
+		dgrad_layer<N, l>(a, frags, imgs + wave * SPW * STRIDE, dimgs + wave * SPW * DS, lane, base);
+		bwd_range<N, l - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
+	}
+}
+
+template <class N, int l>
+__device__ __forceinline__ void flush_range(const MlpArgs& a, int wave, int lane, const f4 (&acc)[N::slots()]) {
+	if constexpr (l < N::NL) {
+		constexpr int KTN = N::KT16(l);
+		const int g = lane >> 4, n = lane & 15;
+		const uint32_t pin = a.param_in[l];
+		float* gl = a.grads + a.param_off[l];
+#pragma unroll
+		for (int t = 0; t < N::gtiles(l); ++t) {
+			const int gt = N::gtile_base(l) + t;
+			if (gt % WAVES != wave) continue;
+			const int mt = t / KTN, kt = t % KTN;
+			const uint32_t col = 16 * kt + n;
+			if (col >= pin) continue;
+			const f4 c = acc[gt / WAVES];
+#pragma unroll
+			for (int r = 0; r < 4; ++r) {
+				const uint32_t row = 16 * mt + 4 * g + r;
+				if (row < (uint32_t)N::out_dim(l)) unsafeAtomicAdd(gl + (size_t)row * pin + col, c[r]);
+			}
+		}
+		flush_range<N, l + 1>(a, wave, lane, acc);
+	}
+}
+
+template <class N>
+__global__ void __launch_bounds__(BLOCK) k_mlp_train(MlpArgs a) {
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	constexpr int STRIDE = N::template stride<true>();
+	constexpr int DS = N::dstride();
+	constexpr int FH = (N::fwd_frags() + N::bwd_frags()) * FRAG_HALVES;
+	_Float16* frags = reinterpret_cast<_Float16*>(smem);
+	_Float16* imgs = frags + FH;
+	_Float16* dimgs = imgs + WAVES * SPW * STRIDE;
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	_Float16* img = imgs + wave * SPW * STRIDE;
+	_Float16* dimg = dimgs + wave * SPW * DS;
+
+	for (int t = threadIdx.x; t < FH / 8; t += BLOCK)
+		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
+	for (int t = lane; t < SPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	for (int t = lane; t < SPW * DS / 8; t += 64) reinterpret_cast<h8*>(dimg)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+
+	f4 acc[N::slots()];
+#pragma unroll
+	for (int s = 0; s < N::slots(); ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
+
+	const uint32_t n_chunks = n_chunks_of(a.n);
+	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
+		__syncthreads();  // previous chunk's wgrad reads of every image are done
+		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
+		load_encoding<N, STRIDE>(a, img, base, lane);
+		load_sh<STRIDE>(a, img, N::template x_seg<true>(), base, lane);
+		f4 res[CT];
+		fwd_range<N, true, 0, N::NL - 1>(frags, img, lane, res);
+		// delta of the rgb output layer: rows 0..2 = dL/drgb_raw (loss-scaled, rollover-weighted)
+		for (int t = lane; t < SPW * 4; t += 64) {
+			const int smp = t % SPW, ch = t / SPW;
+			const uint32_t i = base + smp;
+			h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+			if (ch == 0 && i < a.n) {
+				const float w = a.weight ? a.weight[i] : 1.0f;
+				const __half* d = a.dloss + (size_t)i * 4;
+				v[0] = (_Float16)(__half2float(d[0]) * w);
+				v[1] = (_Float16)(__half2float(d[1]) * w);
+				v[2] = (_Float16)(__half2float(d[2]) * w);
+			}
+			lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
+		}
+		bwd_range<N, N::NL - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
+	}
+	flush_range<N, 0>(a, wave, lane, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Weight packing: row-major fp16 params -> per-lane MFMA fragments.
+// ---------------------------------------------------------------------------
+struct PackLayer {
+	uint64_t param_off;
+	uint32_t out, in;         // param dims
+	uint32_t mt, ks, fwd_off; // forward: [mt][ks] fragments
+	uint32_t kt, ms, bwd_off; // backward (transposed): [kt][ms] fragments
+};
+struct PackArgs {
+	PackLayer L[MAX_LAYERS];
+	uint32_t n_layers;
+	uint32_t total_frags;
+};
+
+__global__ void k_pack(const __half* __restrict__ params, __half* __restrict__ out, PackArgs p) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t frag = t / 64, lane = t % 64;
+	if (frag >= p.total_frags) return;
+	const uint32_t g = lane >> 4, m = lane & 15;
+	// find the layer and direction of this fragment
+	for (uint32_t l = 0; l < p.n_layers; ++l) {
+		const PackLayer& L = p.L[l];
+		const uint32_t f0 = L.fwd_off / FRAG_HALVES, nf = L.mt * L.ks;
+		const uint32_t b0 = L.bwd_off / FRAG_HALVES, nb = L.kt * L.ms;
+		const __half* W = params + L.param_off;
+		if (frag >= f0 && frag < f0 + nf) {
+			const uint32_t idx = frag - f0, mt = idx / L.ks, s = idx % L.ks;
+			const uint32_t row = 16 * mt + m;
+			for (uint32_t j = 0; j < 8; ++j) {
+				const uint32_t col = 32 * s + 8 * g + j;
+				out[(size_t)t * 8 + j] = (row < L.out && col < L.in) ? W[(size_t)row * L.in + col] : __float2half(0.0f);
+			}
+			return;
+		}
+		if (frag >= b0 && frag < b0 + nb) {
+			const uint32_t idx = frag - b0, mt = idx / L.ms, s = idx % L.ms;
+			const uint32_t col = 16 * mt + m;  // input neuron (row of W^T)
+			for (uint32_t j = 0; j < 8; ++j) {
+				const uint32_t row = 32 * s + 8 * g + j;  // output neuron
+				out[(size_t)t * 8 + j] = (row < L.out && col < L.in) ? W[(size_t)row * L.in + col] : __float2half(0.0f);
+			}
+			return;
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Host side: variant dispatch.
+// ---------------------------------------------------------------------------
+using V0 = Net<64, 1, 2, 1>;  // lego / base.json (enc 32)
+using V1 = Net<64, 1, 2, 2>;  // enc 48..64
+using V2 = Net<16, 1, 2, 1>;  // config A
+using V3 = Net<32, 1, 2, 1>;
+using V4 = Net<64, 2, 2, 1>;
+using V5 = Net<64, 1, 1, 1>;
+using V6 = Net<64, 1, 3, 1>;
+
+int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad) {
+	const uint32_t ke = enc_pad <= 32 ? 1 : (enc_pad <= 64 ? 2 : 0);
+	if (width == 64 && dh == 1 && rh == 2 && ke == 1) return 0;
+	if (width == 64 && dh == 1 && rh == 2 && ke == 2) return 1;
+	if (width == 16 && dh == 1 && rh == 2 && ke == 1) return 2;
+	if (width == 32 && dh == 1 && rh == 2 && ke == 1) return 3;
+	if (width == 64 && dh == 2 && rh == 2 && ke == 1) return 4;
+	if (width == 64 && dh == 1 && rh == 1 && ke == 1) return 5;
+	if (width == 64 && dh == 1 && rh == 3 && ke == 1) return 6;
+	return -1;
+}
+
+template <class N>
+static void layer_geometry(const ngp_model* m, PackArgs& p) {
+	p.n_layers = N::NL;
+	for (int l = 0; l < N::NL; ++l) {
+		PackLayer& L = p.L[l];
+		L.param_off = m->layers[l].param_offset;
+		L.out = m->layers[l].out;
+		L.in = m->layers[l].in;
+		L.mt = N::Mt(l);
+		L.ks = N::Ks(l);
+		L.fwd_off = N::fwd_off(l);
+		L.kt = N::Kt(l);
+		L.ms = N::Ms(l);
+		L.bwd_off = N::bwd_off(l);
+	}
+	p.total_frags = N::fwd_frags() + N::bwd_frags();
+}
+
+#define NGP_DISPATCH(variant, ...)                      \
+	switch (variant) {                                   \
+		case 0: { using N = V0; __VA_ARGS__; } break;           \
+		case 1: { using N = V1; __VA_ARGS__; } break;           \
+		case 2: { using N = V2; __VA_ARGS__; } break;           \
+		case 3: { using N = V3; __VA_ARGS__; } break;           \
+		case 4: { using N = V4; __VA_ARGS__; } break;           \
+		case 5: { using N = V5; __VA_ARGS__; } break;           \
+		case 6: { using N = V6; __VA_ARGS__; } break;           \
+		default: throw std::runtime_error("unsupported MLP configuration"); \
+	}
+
+uint32_t mlp_frag_halves(const ngp_model* m) {
+	uint32_t r = 0;
+	NGP_DISPATCH(m->mlp_variant, r = (N::fwd_frags() + N::bwd_frags()) * FRAG_HALVES);
+	return r;
+}
+
+void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s) {
+	PackArgs p{};
+	NGP_DISPATCH(m->mlp_variant, layer_geometry<N>(m, p));
+	const uint32_t threads = p.total_frags * 64;
+	k_pack<<<div_up(threads, 256), 256, 0, s>>>(params16, frags, p);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+static int cu_count() {
+	static int n = 0;
+	if (n == 0) {
+		int dev = 0;
+		NGP_HIP_CHECK(hipGetDevice(&dev));
+		NGP_HIP_CHECK(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev));
+		if (n <= 0) n = 256;
+	}
+	return n;
+}
+
+static MlpArgs base_args(const ngp_model* m) {
+	MlpArgs a{};
+	a.E = m->enc_width;
+	a.F = m->lt.F;
+	a.enc_pad = m->enc_pad;
+	for (uint32_t l = 0; l < m->n_layers; ++l) {
+		a.param_off[l] = m->layers[l].param_offset;
+		a.param_in[l] = m->layers[l].in;
+	}
+	return a;
+}
+
+template <class N, class K>
+static void set_lds(K kernel, size_t bytes) {
+	NGP_HIP_CHECK(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
+}
+
+void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+                      const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
+                      const uint32_t* n_dev) {
+	if (n == 0) return;
+	MlpArgs a = base_args(m);
+	a.frags = frags;
+	a.enc = enc;
+	a.enc_plane = enc_plane;
+	a.coords = coords;
+	a.coord_stride = coord_stride;
+	a.n = n;
+	a.out = out;
+	a.n_dev = n_dev;
+	NGP_DISPATCH(m->mlp_variant, {
+		const size_t lds = N::lds_infer();
+		set_lds<N>(k_mlp_infer<N>, lds);
+		const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)(160 * 1024 / lds));
+		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count() * per_cu);
+		k_mlp_infer<N><<<grid, BLOCK, lds, s>>>(a);
+	});
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane, uint32_t n,
+                        __half* out, hipStream_t s, const uint32_t* n_dev) {
+	if (n == 0) return;
+	MlpArgs a = base_args(m);
+	a.frags = frags;
+	a.enc = enc;
+	a.enc_plane = enc_plane;
+	a.n = n;
+	a.out = out;
+	a.n_dev = n_dev;
+	NGP_DISPATCH(m->mlp_variant, {
+		const size_t lds = N::lds_density();
+		set_lds<N>(k_mlp_density<N>, lds);
+		const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)(160 * 1024 / lds));
+		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count() * per_cu);
+		k_mlp_density<N><<<grid, BLOCK, lds, s>>>(a);
+	});
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+                      const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
+                      const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
+                      const uint32_t* n_dev) {
+	if (n == 0) return;
+	MlpArgs a = base_args(m);
+	a.frags = frags;
+	a.enc = enc;
+	a.enc_plane = enc_plane;
+	a.coords = coords;
+	a.coord_stride = coord_stride;
+	a.n = n;
+	a.dloss = dloss;
+	a.weight = weight;
+	a.grads = grads_mlp;
+	a.denc = denc;
+	a.n_dev = n_dev;
+	NGP_DISPATCH(m->mlp_variant, {
+		const size_t lds = N::lds_train();
+		if (lds > 160 * 1024) throw std::runtime_error("MLP training LDS footprint exceeds 160 KiB");
+		set_lds<N>(k_mlp_train<N>, lds);
+		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count());
+		k_mlp_train<N><<<grid, BLOCK, lds, s>>>(a);
+	});
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ngp

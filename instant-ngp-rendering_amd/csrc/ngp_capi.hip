@@ -1,0 +1,460 @@
+// ngp_capi.hip — the C-ABI of libngp_hip.so (see include/ngp_hip.h).
+//
+// Host orchestration only: parameter layout, level tables, buffer ownership
+// and the launch sequences of the kernels in hashgrid/mlp/train/density_grid/
+// render.hip.  Every entry point converts C++ exceptions into an ngp_status +
+// thread-local message, the C-ABI analogue of the reference's
+// CUDA_CHECK_THROW -> std::runtime_error -> Python RuntimeError chain.
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "ngp_internal.h"
+
+namespace ngp {
+void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s);
+void run_grid_finish(ngp_model* m, const ngp_grid_args* a, hipStream_t s);
+void run_grid_bitfield(ngp_model* m, uint32_t max_cascade, hipStream_t s);
+void grid_reserve(ngp_model* m, uint32_t n_cascades, uint32_t n_samples);
+void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s);
+void run_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t W, uint32_t H, uint32_t spp,
+                            int color_space, float exposure, const float* bg, int output_srgb, hipStream_t s);
+}  // namespace ngp
+
+using namespace ngp;
+
+static thread_local std::string g_last_error;
+
+template <class F>
+static ngp_status guarded(F&& f) {
+	try {
+		f();
+		return NGP_OK;
+	} catch (const std::invalid_argument& e) {
+		g_last_error = e.what();
+		return NGP_ERR_INVALID;
+	} catch (const std::bad_alloc& e) {
+		g_last_error = e.what();
+		return NGP_ERR_OOM;
+	} catch (const std::exception& e) {
+		g_last_error = e.what();
+		return std::string(e.what()).rfind("HIP error", 0) == 0 ? NGP_ERR_HIP : NGP_ERR_UNSUPPORTED;
+	}
+}
+
+static void require(bool cond, const char* msg) {
+	if (!cond) throw std::invalid_argument(msg);
+}
+
+static hipStream_t S(ngp_stream s) { return reinterpret_cast<hipStream_t>(s); }
+
+// tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.
+static void build_level_table(ngp_model* m) {
+	const ngp_network_config& c = m->cfg;
+	LevelTable& lt = m->lt;
+	lt.n_levels = c.n_levels;
+	lt.F = c.n_features_per_level;
+	const float log2_pls = std::log2(c.per_level_scale);
+	uint32_t offset = 0;
+	for (uint32_t l = 0; l < c.n_levels; ++l) {
+		const float scale = std::exp2((float)l * log2_pls) * (float)c.base_resolution - 1.0f;
+		const uint32_t res = (uint32_t)std::ceil(scale) + 1;
+		const uint32_t max_params = 0xFFFFFFFFu / 2;
+		const double dense = (double)res * res * res;
+		uint32_t params = dense > (double)max_params ? max_params : res * res * res;
+		params = next_multiple(params, 8);
+		params = std::min(params, 1u << c.log2_hashmap_size);
+		lt.scale[l] = scale;
+		lt.res[l] = res;
+		lt.offset[l] = offset;
+		lt.size[l] = params;
+		lt.hashed[l] = dense > (double)params ? 1u : 0u;
+		offset += params;
+	}
+	m->n_grid_params = (uint64_t)offset * lt.F;
+}
+
+static void build_layers(ngp_model* m) {
+	const ngp_network_config& c = m->cfg;
+	const uint32_t W = c.n_neurons;
+	std::vector<std::pair<uint32_t, uint32_t>> dims;  // (out, in)
+	dims.push_back({W, m->enc_pad});
+	for (uint32_t h = 1; h < c.density_hidden_layers; ++h) dims.push_back({W, W});
+	dims.push_back({16, W});
+	m->n_density_layers = (uint32_t)dims.size();
+	dims.push_back({W, 32});  // rgb_network_input_width = next_multiple(16 + 16, 16) (nerf_network.h:93)
+	for (uint32_t h = 1; h < c.rgb_hidden_layers; ++h) dims.push_back({W, W});
+	dims.push_back({16, W});  // 3 used, padded to 16 (tcnn output alignment)
+	require(dims.size() <= MAX_LAYERS, "too many MLP layers");
+	m->n_layers = (uint32_t)dims.size();
+	uint64_t off = 0;
+	for (uint32_t l = 0; l < m->n_layers; ++l) {
+		m->layers[l].out = dims[l].first;
+		m->layers[l].in = dims[l].second;
+		m->layers[l].param_offset = off;
+		off += (uint64_t)dims[l].first * dims[l].second;
+	}
+	m->n_mlp_params = off;
+}
+
+static void upload_init_params(ngp_model* m, uint64_t seed) {
+	std::vector<float> p(m->n_params);
+	pcg32 rng(seed);
+	for (uint32_t l = 0; l < m->n_layers; ++l) {
+		const Layer& L = m->layers[l];
+		const float scale = std::sqrt(6.0f / (float)(L.in + L.out));  // Xavier uniform (tcnn FullyFusedMLP)
+		for (uint64_t i = 0; i < (uint64_t)L.in * L.out; ++i) p[L.param_offset + i] = (rng.next_float() * 2.0f - 1.0f) * scale;
+	}
+	for (uint64_t i = 0; i < m->n_grid_params; ++i) p[m->n_mlp_params + i] = (rng.next_float() * 2.0f - 1.0f) * 1e-4f;
+	NGP_HIP_CHECK(hipMemcpy(m->params32.ptr, p.data(), m->n_params * sizeof(float), hipMemcpyHostToDevice));
+}
+
+static void refresh_derived(ngp_model* m, bool reset_optimizer, hipStream_t s) {
+	launch_params_to_half(m->params32.ptr, m->params16.ptr, m->n_params, s);
+	if (reset_optimizer) {
+		NGP_HIP_CHECK(hipMemcpyAsync(m->ema32.ptr, m->params32.ptr, m->n_params * sizeof(float), hipMemcpyDeviceToDevice, s));
+		NGP_HIP_CHECK(hipMemcpyAsync(m->infer16.ptr, m->params16.ptr, m->n_params * sizeof(__half), hipMemcpyDeviceToDevice, s));
+		NGP_HIP_CHECK(hipMemsetAsync(m->adam_m.ptr, 0, m->n_params * sizeof(float), s));
+		NGP_HIP_CHECK(hipMemsetAsync(m->adam_v.ptr, 0, m->n_params * sizeof(float), s));
+		NGP_HIP_CHECK(hipMemsetAsync(m->adam_steps.ptr, 0, m->n_params * sizeof(uint32_t), s));
+		NGP_HIP_CHECK(hipMemsetAsync(m->grads.ptr, 0, m->n_params * sizeof(float), s));
+		m->ema_step = 0;
+	} else {
+		launch_params_to_half(m->ema32.ptr, m->infer16.ptr, m->n_params, s);
+	}
+	pack_mlp_fragments(m, m->params16.ptr, m->frag_train.ptr, s);
+	pack_mlp_fragments(m, m->infer16.ptr, m->frag_infer.ptr, s);
+}
+
+extern "C" {
+
+const char* ngp_last_error(void) { return g_last_error.c_str(); }
+const char* ngp_version(void) { return "ngp_hip 0.1 (gfx950)"; }
+
+ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint64_t seed, ngp_model** out) {
+	return guarded([&] {
+		require(cfg && out, "null argument");
+		require(cfg->n_levels >= 1 && cfg->n_levels <= MAX_LEVELS, "n_levels must be in [1, 32]");
+		require(cfg->n_features_per_level == 1 || cfg->n_features_per_level == 2 || cfg->n_features_per_level == 4 ||
+		            cfg->n_features_per_level == 8,
+		        "n_features_per_level must be 1, 2, 4 or 8");
+		require(cfg->log2_hashmap_size >= 4 && cfg->log2_hashmap_size <= 30, "log2_hashmap_size out of range");
+		require(cfg->per_level_scale > 0.0f, "per_level_scale must be positive");
+		NGP_HIP_CHECK(hipSetDevice(hip_device));
+		auto* m = new ngp_model();
+		try {
+			m->device = hip_device;
+			m->cfg = *cfg;
+			m->enc_width = cfg->n_levels * cfg->n_features_per_level;
+			m->enc_pad = next_multiple(m->enc_width, 16);
+			require(m->enc_pad <= 64, "encoding width (n_levels * F) must be <= 64");
+			m->mlp_variant = mlp_variant_for(cfg->n_neurons, cfg->density_hidden_layers, cfg->rgb_hidden_layers, m->enc_pad);
+			if (m->mlp_variant < 0) throw std::invalid_argument("unsupported MLP shape (n_neurons / hidden layers)");
+			build_level_table(m);
+			build_layers(m);
+			m->n_params = m->n_mlp_params + m->n_grid_params;
+			m->frag_halves = mlp_frag_halves(m);
+			m->params32.reserve(m->n_params);
+			m->params16.reserve(m->n_params);
+			m->ema32.reserve(m->n_params);
+			m->infer16.reserve(m->n_params);
+			m->grads.reserve(m->n_params);
+			m->adam_m.reserve(m->n_params);
+			m->adam_v.reserve(m->n_params);
+			m->adam_steps.reserve(m->n_params);
+			m->frag_train.reserve(m->frag_halves);
+			m->frag_infer.reserve(m->frag_halves);
+			upload_init_params(m, seed);
+			refresh_derived(m, true, 0);
+			// empty occupancy state: grid zeros, all bits set as the reference's first update would
+			grid_reserve(m, 1, 1);
+			m->gs.bitfield.reserve(NERF_GRID_N_CELLS / 8 * NERF_CASCADES);
+			m->gs.mean.reserve(1);
+			m->gs.sum.reserve(1);
+			NGP_HIP_CHECK(hipMemset(m->gs.bitfield.ptr, 0xff, m->gs.bitfield.bytes()));
+			NGP_HIP_CHECK(hipMemset(m->gs.mean.ptr, 0, sizeof(float)));
+			NGP_HIP_CHECK(hipDeviceSynchronize());
+		} catch (...) {
+			delete m;
+			throw;
+		}
+		*out = m;
+	});
+}
+
+ngp_status ngp_model_destroy(ngp_model* m) {
+	return guarded([&] {
+		if (!m) return;
+		(void)hipSetDevice(m->device);
+		(void)hipDeviceSynchronize();
+		for (auto* b : {&m->params32, &m->ema32, &m->grads, &m->adam_m, &m->adam_v}) b->release();
+		m->params16.release();
+		m->infer16.release();
+		m->adam_steps.release();
+		m->frag_train.release();
+		m->frag_infer.release();
+		TrainScratch& t = m->ts;
+		t.ray_numsteps.release(); t.ray_compacted.release(); t.ray_state.release(); t.ray_loss_state.release();
+		t.coords.release(); t.enc.release(); t.mlp_out.release(); t.ccoords.release(); t.cenc.release();
+		t.dloss.release(); t.cweight.release(); t.denc.release(); t.loss.release(); t.block_sums.release();
+		t.counters.release(); t.scan_a.release(); t.scan_b.release();
+		GridState& g = m->gs;
+		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
+		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
+		RenderScratch& r = m->rs;
+		for (int b = 0; b < 3; ++b) { r.payload[b].release(); r.rgba[b].release(); r.depth[b].release(); }
+		r.coords.release(); r.enc.release(); r.out.release(); r.counters.release();
+		if (r.host_counter.ptr) (void)hipHostFree(r.host_counter.ptr);
+		delete m;
+	});
+}
+
+ngp_status ngp_model_get_info(const ngp_model* m, ngp_model_info* info) {
+	return guarded([&] {
+		require(m && info, "null argument");
+		std::memset(info, 0, sizeof(*info));
+		info->n_params = m->n_params;
+		info->n_mlp_params = m->n_mlp_params;
+		info->n_grid_params = m->n_grid_params;
+		info->n_levels = m->lt.n_levels;
+		info->n_features_per_level = m->lt.F;
+		info->encoding_width = m->enc_width;
+		info->padded_encoding_width = m->enc_pad;
+		for (uint32_t l = 0; l < m->lt.n_levels; ++l) {
+			info->level_offset[l] = m->lt.offset[l];
+			info->level_size[l] = m->lt.size[l];
+			info->level_resolution[l] = m->lt.res[l];
+			info->level_scale[l] = m->lt.scale[l];
+		}
+		info->n_layers = m->n_layers;
+		for (uint32_t l = 0; l < m->n_layers; ++l) {
+			info->layer_in[l] = m->layers[l].in;
+			info->layer_out[l] = m->layers[l].out;
+			info->layer_param_offset[l] = m->layers[l].param_offset;
+		}
+	});
+}
+
+ngp_status ngp_model_buffer(ngp_model* m, int kind, void** ptr, size_t* bytes) {
+	return guarded([&] {
+		require(m && ptr, "null argument");
+		switch (kind) {
+			case NGP_PARAMS_FP32: *ptr = m->params32.ptr; if (bytes) *bytes = m->n_params * 4; break;
+			case NGP_PARAMS_FP16: *ptr = m->params16.ptr; if (bytes) *bytes = m->n_params * 2; break;
+			case NGP_PARAMS_EMA_FP32: *ptr = m->ema32.ptr; if (bytes) *bytes = m->n_params * 4; break;
+			case NGP_PARAMS_INFER_FP16: *ptr = m->infer16.ptr; if (bytes) *bytes = m->n_params * 2; break;
+			case NGP_GRADS_FP32: *ptr = m->grads.ptr; if (bytes) *bytes = m->n_params * 4; break;
+			case NGP_ADAM_M: *ptr = m->adam_m.ptr; if (bytes) *bytes = m->n_params * 4; break;
+			case NGP_ADAM_V: *ptr = m->adam_v.ptr; if (bytes) *bytes = m->n_params * 4; break;
+			default: throw std::invalid_argument("unknown buffer kind");
+		}
+	});
+}
+
+ngp_status ngp_model_params_updated(ngp_model* m, int reset_optimizer, ngp_stream s) {
+	return guarded([&] {
+		require(m, "null model");
+		refresh_derived(m, reset_optimizer != 0, S(s));
+	});
+}
+
+ngp_status ngp_model_reset_optimizer(ngp_model* m, ngp_stream s) {
+	return guarded([&] {
+		require(m, "null model");
+		refresh_derived(m, true, S(s));
+	});
+}
+
+ngp_status ngp_model_encode(ngp_model* m, const float* pos, uint32_t stride, uint32_t n, uint16_t* enc, int use_inf,
+                            ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (pos && enc)), "null argument");
+		require(stride >= 3, "stride must be >= 3 floats");
+		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+		launch_hashgrid_fwd(m->lt, pos, stride, n, table, reinterpret_cast<__half*>(enc), n, S(s));
+	});
+}
+
+ngp_status ngp_model_encode_indices(ngp_model* m, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
+                                    float* w, ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (pos && idx && w)), "null argument");
+		launch_hashgrid_indices(m->lt, pos, stride, n, idx, w, S(s));
+	});
+}
+
+ngp_status ngp_model_infer(ngp_model* m, const float* coords, uint32_t fpc, uint32_t n, uint16_t* out, int use_inf,
+                           ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (coords && out)), "null argument");
+		require(fpc >= 7, "floats_per_coord must be >= 7 (NerfCoordinate)");
+		if (n == 0) return;
+		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
+		TrainScratch& ts = m->ts;
+		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
+		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, n, S(s));
+		launch_mlp_infer(m, frags, ts.enc.ptr, n, coords, fpc, n, reinterpret_cast<__half*>(out), S(s));
+	});
+}
+
+ngp_status ngp_model_density(ngp_model* m, const float* pos, uint32_t stride, uint32_t n, uint16_t* out, int use_inf,
+                             ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (pos && out)), "null argument");
+		require(stride >= 3, "stride must be >= 3 floats");
+		if (n == 0) return;
+		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
+		GridState& g = m->gs;
+		g.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
+		launch_hashgrid_fwd(m->lt, pos, stride, n, table, g.enc.ptr, n, S(s));
+		launch_mlp_density(m, frags, g.enc.ptr, n, n, reinterpret_cast<__half*>(out), S(s));
+	});
+}
+
+ngp_status ngp_model_backward(ngp_model* m, const uint16_t* enc, const float* dirs, uint32_t n, const uint16_t* dloss,
+                              const float* weight, uint16_t* denc, ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (enc && dirs && dloss && denc)), "null argument");
+		if (n == 0) return;
+		// dirs are passed as [n][3]; the MLP kernel reads NerfCoordinate-like records (dir at offset 4)
+		TrainScratch& ts = m->ts;
+		ts.ccoords.reserve(8 * (size_t)n);
+		std::vector<float> tmp((size_t)n * 8, 0.0f);
+		std::vector<float> d((size_t)n * 3);
+		NGP_HIP_CHECK(hipMemcpyAsync(d.data(), dirs, d.size() * 4, hipMemcpyDeviceToHost, S(s)));
+		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
+		for (size_t i = 0; i < n; ++i)
+			for (int k = 0; k < 3; ++k) tmp[8 * i + 4 + k] = d[3 * i + k];
+		NGP_HIP_CHECK(hipMemcpyAsync(ts.ccoords.ptr, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, S(s)));
+		launch_mlp_train(m, m->frag_train.ptr, reinterpret_cast<const __half*>(enc), n, ts.ccoords.ptr, 8, n,
+		                 reinterpret_cast<const __half*>(dloss), weight, m->grads.ptr, reinterpret_cast<__half*>(denc),
+		                 S(s));
+		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
+	});
+}
+
+ngp_status ngp_model_encode_backward(ngp_model* m, const float* pos, uint32_t stride, uint32_t n, const uint16_t* denc,
+                                     ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (pos && denc)), "null argument");
+		launch_hashgrid_bwd(m->lt, pos, stride, n, reinterpret_cast<const __half*>(denc), n,
+		                    m->grads.ptr + m->n_mlp_params, S(s));
+	});
+}
+
+ngp_status ngp_train_step(ngp_model* m, const ngp_train_args* a, ngp_stream s) {
+	return guarded([&] {
+		require(m && a, "null argument");
+		require(a->images && a->n_images > 0, "training requires at least one image");
+		require(a->n_rays > 0 && a->target_batch_size > 0 && a->max_samples > 0, "empty batch");
+		require(m->gs.bitfield.ptr != nullptr, "density grid not initialised");
+		run_train_step(m, a, S(s));
+	});
+}
+
+ngp_status ngp_optimizer_step(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, ngp_stream s) {
+	return guarded([&] {
+		require(m, "null model");
+		launch_optimizer(m, step, opt_mlp, opt_enc, S(s));
+	});
+}
+
+ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s) {
+	return guarded([&] {
+		require(m && st, "null argument");
+		std::memset(st, 0, sizeof(*st));
+		if (!m->ts.counters.ptr) return;
+		uint32_t c[16];
+		NGP_HIP_CHECK(hipMemcpyAsync(c, m->ts.counters.ptr, sizeof(c), hipMemcpyDeviceToHost, S(s)));
+		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
+		st->n_rays = m->ts.last_n_rays;
+		st->measured_batch_size_before_compaction = c[0];
+		st->measured_batch_size = c[1];
+		float loss;
+		std::memcpy(&loss, &c[8], 4);
+		st->loss = loss;
+		st->n_rays_with_samples = 0;
+	});
+}
+
+ngp_status ngp_train_scratch(ngp_model* m, int kind, void** ptr, size_t* bytes) {
+	return guarded([&] {
+		require(m && ptr, "null argument");
+		TrainScratch& t = m->ts;
+		const size_t R = t.last_n_rays, B = t.last_target, MS = t.last_max_samples;
+		switch (kind) {
+			case NGP_SCRATCH_RAY_NUMSTEPS: *ptr = t.ray_numsteps.ptr; if (bytes) *bytes = R * 8; break;
+			case NGP_SCRATCH_COORDS: *ptr = t.coords.ptr; if (bytes) *bytes = MS * 32; break;
+			case NGP_SCRATCH_MLP_OUT: *ptr = t.mlp_out.ptr; if (bytes) *bytes = MS * 8; break;
+			case NGP_SCRATCH_RAY_COMPACTED: *ptr = t.ray_compacted.ptr; if (bytes) *bytes = R * 8; break;
+			case NGP_SCRATCH_DLOSS: *ptr = t.dloss.ptr; if (bytes) *bytes = B * 8; break;
+			case NGP_SCRATCH_LOSS: *ptr = t.loss.ptr; if (bytes) *bytes = R * 4; break;
+			case NGP_SCRATCH_COMPACT_COORDS: *ptr = t.ccoords.ptr; if (bytes) *bytes = B * 32; break;
+			default: throw std::invalid_argument("unknown scratch kind");
+		}
+	});
+}
+
+ngp_status ngp_density_grid_update(ngp_model* m, const ngp_grid_args* a, ngp_stream s) {
+	return guarded([&] {
+		require(m && a, "null argument");
+		require(a->max_cascade < NERF_CASCADES, "max_cascade must be < 8");
+		run_grid_evaluate(m, a, S(s));
+		run_grid_finish(m, a, S(s));
+	});
+}
+
+ngp_status ngp_density_grid_evaluate(ngp_model* m, const ngp_grid_args* a, ngp_stream s) {
+	return guarded([&] {
+		require(m && a, "null argument");
+		require(a->max_cascade < NERF_CASCADES, "max_cascade must be < 8");
+		run_grid_evaluate(m, a, S(s));
+	});
+}
+
+ngp_status ngp_density_grid_finish(ngp_model* m, const ngp_grid_args* a, ngp_stream s) {
+	return guarded([&] {
+		require(m && a, "null argument");
+		run_grid_finish(m, a, S(s));
+	});
+}
+
+ngp_status ngp_density_grid_bitfield(ngp_model* m, uint32_t max_cascade, ngp_stream s) {
+	return guarded([&] {
+		require(m, "null model");
+		require(max_cascade < NERF_CASCADES, "max_cascade must be < 8");
+		run_grid_bitfield(m, max_cascade, S(s));
+	});
+}
+
+ngp_status ngp_density_grid_buffers(ngp_model* m, float** grid, uint8_t** bitfield, float** tmp, float** mean) {
+	return guarded([&] {
+		require(m, "null model");
+		if (grid) *grid = m->gs.grid.ptr;
+		if (bitfield) *bitfield = m->gs.bitfield.ptr;
+		if (tmp) *tmp = m->gs.tmp.ptr;
+		if (mean) *mean = m->gs.mean.ptr;
+	});
+}
+
+ngp_status ngp_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth, ngp_stream s) {
+	return guarded([&] {
+		require(m && a && frame && depth, "null argument");
+		require(a->width > 0 && a->height > 0, "empty render target");
+		run_render(m, a, frame, depth, S(s));
+	});
+}
+
+ngp_status ngp_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t W, uint32_t H, uint32_t spp,
+                                  int color_space, float exposure, const float* bg, int output_srgb, ngp_stream s) {
+	return guarded([&] {
+		require(frame && accum, "null argument");
+		run_accumulate_tonemap(frame, accum, out, W, H, spp, color_space, exposure, bg, output_srgb, S(s));
+	});
+}
+
+}  // extern "C"

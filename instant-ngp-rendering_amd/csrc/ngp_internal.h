@@ -1,0 +1,172 @@
+// ngp_internal.h — model state and kernel launchers of libngp_hip.so (gfx950).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <hip/hip_fp16.h>
+
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../../include/ngp_hip.h"
+#include "ngp_math.h"
+
+namespace ngp {
+
+#define NGP_HIP_CHECK(expr)                                                                               \
+	do {                                                                                                  \
+		hipError_t _e = (expr);                                                                           \
+		if (_e != hipSuccess) {                                                                           \
+			throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(_e) + " at " + #expr); \
+		}                                                                                                 \
+	} while (0)
+
+constexpr uint32_t MAX_LEVELS = 32;
+constexpr uint32_t MAX_LAYERS = 8;
+
+// Per-level hash-grid geometry, computed once on the host (tcnn GridEncodingTemplated ctor).
+struct LevelTable {
+	uint32_t n_levels;
+	uint32_t F;
+	float scale[MAX_LEVELS];
+	uint32_t res[MAX_LEVELS];
+	uint32_t offset[MAX_LEVELS];  // in entries (each entry = F features)
+	uint32_t size[MAX_LEVELS];    // entries
+	uint32_t hashed[MAX_LEVELS];
+};
+
+struct Layer {
+	uint32_t in, out;          // logical widths (in padded to tcnn's 16-alignment)
+	uint64_t param_offset;     // into the parameter vector (row-major [out][in])
+	uint32_t frag_fwd, frag_bwd; // offsets (in halves) into the packed fragment blob
+};
+
+// Growable device buffer.
+template <typename T>
+struct DevBuf {
+	T* ptr = nullptr;
+	size_t n = 0;
+	void reserve(size_t count) {
+		if (count <= n) return;
+		if (ptr) NGP_HIP_CHECK(hipFree(ptr));
+		ptr = nullptr;
+		NGP_HIP_CHECK(hipMalloc((void**)&ptr, std::max<size_t>(count, 1) * sizeof(T)));
+		n = count;
+	}
+	void release() {
+		if (ptr) (void)hipFree(ptr);
+		ptr = nullptr;
+		n = 0;
+	}
+	size_t bytes() const { return n * sizeof(T); }
+};
+
+struct TrainScratch {
+	DevBuf<uint32_t> ray_numsteps;     // [R][2]
+	DevBuf<uint32_t> ray_compacted;    // [R][2]
+	DevBuf<float> ray_state;           // [R][8] : o, d (unnormalised), pad
+	DevBuf<float> ray_loss_state;      // [R][8]
+	DevBuf<float> coords;              // [max_samples][8]
+	DevBuf<__half> enc;                // [L][max_samples][F]
+	DevBuf<__half> mlp_out;            // [max_samples][4]
+	DevBuf<float> ccoords;             // [B][8] compacted
+	DevBuf<__half> cenc;               // [L][B][F]
+	DevBuf<__half> dloss;              // [B][4]
+	DevBuf<float> cweight;             // [B] rollover multiplicity
+	DevBuf<__half> denc;               // [L][B][F]
+	DevBuf<float> loss;                // [R]
+	DevBuf<uint32_t> block_sums;       // scan scratch
+	DevBuf<uint32_t> counters;         // [16]: 0 numsteps total, 1 compacted total, 4 clamped S, 5 clamped c, 8 loss sum
+	DevBuf<uint32_t> scan_a;           // [2R] sampler counts | bases
+	DevBuf<uint32_t> scan_b;           // [2R] compacted counts | bases
+	uint32_t last_n_rays = 0, last_target = 0, last_max_samples = 0;
+};
+
+struct GridState {
+	DevBuf<float> grid;        // [n_cascades][N]
+	DevBuf<float> tmp;         // [n_cascades][N]
+	DevBuf<uint8_t> bitfield;  // [8][N/8]
+	DevBuf<float> mean;        // [1]
+	DevBuf<unsigned long long> sum;  // [1] fixed-point accumulator
+	DevBuf<float> positions;   // [n_samples][4]
+	DevBuf<uint32_t> indices;  // [n_samples]
+	DevBuf<__half> enc;        // [L][n][F]
+	DevBuf<__half> out;        // [n]
+	uint32_t n_cascades = 0;
+};
+
+struct RenderScratch {
+	DevBuf<float> payload[3];   // [n][12]: o(3), d(3), t, max_weight, idx(bits), n_steps(bits), alive(bits), pad
+	DevBuf<float> rgba[3];      // [n][4]
+	DevBuf<float> depth[3];     // [n]
+	DevBuf<float> coords;       // [n*8][8]
+	DevBuf<__half> enc;         // [L][n*8][F]
+	DevBuf<__half> out;         // [n*8][4]
+	DevBuf<uint32_t> counters;  // [4]
+	DevBuf<uint32_t> host_counter;
+	size_t cap = 0;
+};
+
+}  // namespace ngp
+
+struct ngp_model {
+	int device = 0;
+	ngp_network_config cfg{};
+	ngp::LevelTable lt{};
+	uint32_t enc_width = 0, enc_pad = 0;
+	uint32_t n_layers = 0, n_density_layers = 0;
+	ngp::Layer layers[ngp::MAX_LAYERS];
+	uint64_t n_mlp_params = 0, n_grid_params = 0, n_params = 0;
+	uint32_t frag_halves = 0;  // packed fragment blob size
+	int mlp_variant = -1;
+
+	ngp::DevBuf<float> params32, ema32, grads, adam_m, adam_v;
+	ngp::DevBuf<__half> params16, infer16;
+	ngp::DevBuf<uint32_t> adam_steps;
+	ngp::DevBuf<__half> frag_train, frag_infer;  // packed MFMA fragments of params16 / infer16
+	uint32_t ema_step = 0;
+
+	ngp::TrainScratch ts;
+	ngp::GridState gs;
+	ngp::RenderScratch rs;
+	ngp_train_stats last_stats{};
+	bool stats_pending = false;
+	uint32_t last_n_rays = 0;
+};
+
+namespace ngp {
+
+// ---- kernel launchers (defined in the .hip files) --------------------------------------
+// hashgrid.hip
+void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
+                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr);
+void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
+                         uint32_t enc_plane, float* grad_table, hipStream_t s, const uint32_t* n_dev = nullptr);
+void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
+                             float* w, hipStream_t s);
+// mlp.hip
+int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad);
+uint32_t mlp_frag_halves(const ngp_model* m);
+void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s);
+void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+                      const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
+                      const uint32_t* n_dev = nullptr);
+void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane, uint32_t n,
+                        __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
+void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+                      const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
+                      const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
+                      const uint32_t* n_dev = nullptr);
+// train.hip
+struct SamplerParams;
+void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hipStream_t s);
+void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s);
+void launch_params_to_half(const float* src, __half* dst, size_t n, hipStream_t s);
+// device-side exclusive scan of u32 counts (n <= 2^24), totals written to *total
+void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* block_sums, uint32_t* total,
+                           hipStream_t s);
+
+inline uint32_t div_up(uint64_t a, uint64_t b) { return (uint32_t)((a + b - 1) / b); }
+inline uint32_t next_multiple(uint32_t a, uint32_t b) { return div_up(a, b) * b; }
+
+}  // namespace ngp

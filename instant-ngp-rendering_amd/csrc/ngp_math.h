@@ -1,0 +1,408 @@
+// ngp_math.h — scalar math shared by the gfx950 kernels and the host runtime.
+//
+// Everything here is __host__ __device__ so the C++ Testbed (g++) and the HIP
+// kernels (hipcc, gfx950) agree bit for bit on RNG streams, Morton codes and the
+// NeRF stepping rules.  Each helper cites the reference function it restates.
+#pragma once
+
+#include <stdint.h>
+#include <math.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define NGP_HD __host__ __device__ __forceinline__
+#else
+#define NGP_HD inline
+#endif
+
+namespace ngp {
+
+// ---------------------------------------------------------------------------
+// Constants — include/neural-graphics-primitives/nerf_device.cuh:24-42,
+// common_device.cuh:32.
+// ---------------------------------------------------------------------------
+constexpr uint32_t NERF_GRIDSIZE = 128;
+constexpr uint32_t NERF_GRID_N_CELLS = NERF_GRIDSIZE * NERF_GRIDSIZE * NERF_GRIDSIZE;
+constexpr uint32_t NERF_STEPS = 1024;
+constexpr uint32_t NERF_CASCADES = 8;
+constexpr float SQRT3 = 1.73205080757f;
+constexpr float STEPSIZE = SQRT3 / (float)NERF_STEPS;
+constexpr float MIN_CONE_STEPSIZE = STEPSIZE;
+constexpr float MAX_CONE_STEPSIZE = STEPSIZE * (float)(1u << (NERF_CASCADES - 1)) * (float)NERF_STEPS / (float)NERF_GRIDSIZE;
+constexpr uint32_t N_MAX_RANDOM_SAMPLES_PER_RAY = 16;
+constexpr float NERF_MIN_OPTICAL_THICKNESS = 0.01f;
+constexpr float MAX_DEPTH = 16384.0f;
+constexpr uint32_t BATCH_SIZE_GRANULARITY = 256;
+
+// ---------------------------------------------------------------------------
+// Small vector type (the reference uses tcnn::vec3).
+// ---------------------------------------------------------------------------
+struct v3 {
+	float x, y, z;
+};
+NGP_HD v3 mk3(float x, float y, float z) { v3 r; r.x = x; r.y = y; r.z = z; return r; }
+NGP_HD v3 mk3(float s) { return mk3(s, s, s); }
+NGP_HD v3 operator+(v3 a, v3 b) { return mk3(a.x + b.x, a.y + b.y, a.z + b.z); }
+NGP_HD v3 operator-(v3 a, v3 b) { return mk3(a.x - b.x, a.y - b.y, a.z - b.z); }
+NGP_HD v3 operator*(v3 a, v3 b) { return mk3(a.x * b.x, a.y * b.y, a.z * b.z); }
+NGP_HD v3 operator/(v3 a, v3 b) { return mk3(a.x / b.x, a.y / b.y, a.z / b.z); }
+NGP_HD v3 operator*(v3 a, float s) { return mk3(a.x * s, a.y * s, a.z * s); }
+NGP_HD v3 operator*(float s, v3 a) { return mk3(a.x * s, a.y * s, a.z * s); }
+NGP_HD v3 operator/(v3 a, float s) { return mk3(a.x / s, a.y / s, a.z / s); }
+NGP_HD v3 operator+(v3 a, float s) { return mk3(a.x + s, a.y + s, a.z + s); }
+NGP_HD v3 operator-(v3 a, float s) { return mk3(a.x - s, a.y - s, a.z - s); }
+NGP_HD float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+NGP_HD float length(v3 a) { return sqrtf(dot(a, a)); }
+NGP_HD v3 normalize(v3 a) { return a * (1.0f / length(a)); }
+NGP_HD float maxc(v3 a) { return fmaxf(fmaxf(a.x, a.y), a.z); }
+NGP_HD v3 absv(v3 a) { return mk3(fabsf(a.x), fabsf(a.y), fabsf(a.z)); }
+
+// Column-major 4x3 camera matrix, columns = right, up, forward, origin
+// (tcnn mat4x3 as used by Testbed, common.h TrainingXForm).
+struct m43 {
+	v3 c[4];
+};
+NGP_HD v3 rot(const m43& m, v3 d) { return m.c[0] * d.x + m.c[1] * d.y + m.c[2] * d.z; }
+
+// ---------------------------------------------------------------------------
+// PCG32 (tiny-cuda-nn `pcg32`, W. Jakob's pcg32.h); default_rng_t in
+// include/neural-graphics-primitives/random_val.cuh:26.
+// ---------------------------------------------------------------------------
+struct pcg32 {
+	uint64_t state, inc;
+	NGP_HD pcg32() : state(0x853c49e6748fea9bULL), inc(0xda3e39cb94b95bdbULL) {}
+	NGP_HD explicit pcg32(uint64_t initstate, uint64_t initseq = 1u) { seed(initstate, initseq); }
+	NGP_HD void seed(uint64_t initstate, uint64_t initseq = 1u) {
+		state = 0u;
+		inc = (initseq << 1u) | 1u;
+		next_uint();
+		state += initstate;
+		next_uint();
+	}
+	NGP_HD uint32_t next_uint() {
+		uint64_t oldstate = state;
+		state = oldstate * 0x5851f42d4c957f2dULL + inc;
+		uint32_t xorshifted = (uint32_t)(((oldstate >> 18u) ^ oldstate) >> 27u);
+		uint32_t r = (uint32_t)(oldstate >> 59u);
+		return (xorshifted >> r) | (xorshifted << ((~r + 1u) & 31));
+	}
+	NGP_HD float next_float() {
+		union { uint32_t u; float f; } x;
+		x.u = (next_uint() >> 9) | 0x3f800000u;
+		return x.f - 1.0f;
+	}
+	NGP_HD void advance(int64_t delta_ = (1ll << 32)) {
+		uint64_t cur_mult = 0x5851f42d4c957f2dULL, cur_plus = inc, acc_mult = 1u, acc_plus = 0u;
+		uint64_t delta = (uint64_t)delta_;
+		while (delta > 0) {
+			if (delta & 1) {
+				acc_mult *= cur_mult;
+				acc_plus = acc_plus * cur_mult + cur_plus;
+			}
+			cur_plus = (cur_mult + 1) * cur_plus;
+			cur_mult *= cur_mult;
+			delta /= 2;
+		}
+		state = acc_mult * state + acc_plus;
+	}
+};
+
+// ---------------------------------------------------------------------------
+// Morton codes (tcnn morton3D / morton3D_invert), used at nerf_device.cuh:327,
+// src/testbed_nerf.cu:86-88,206-208,326-330.
+// ---------------------------------------------------------------------------
+NGP_HD uint32_t expand_bits(uint32_t v) {
+	v = (v * 0x00010001u) & 0xFF0000FFu;
+	v = (v * 0x00000101u) & 0x0F00F00Fu;
+	v = (v * 0x00000011u) & 0xC30C30C3u;
+	v = (v * 0x00000005u) & 0x49249249u;
+	return v;
+}
+NGP_HD uint32_t morton3D(uint32_t x, uint32_t y, uint32_t z) {
+	return (expand_bits(x)) | (expand_bits(y) << 1) | (expand_bits(z) << 2);
+}
+NGP_HD uint32_t morton3D_invert(uint32_t x) {
+	x = x & 0x49249249u;
+	x = (x | (x >> 2)) & 0xc30c30c3u;
+	x = (x | (x >> 4)) & 0x0f00f00fu;
+	x = (x | (x >> 8)) & 0xff0000ffu;
+	x = (x | (x >> 16)) & 0x0000ffffu;
+	return x;
+}
+
+// ---------------------------------------------------------------------------
+// Low-discrepancy sequence — random_val.cuh:162-325 (Burley 2019 scrambled Sobol).
+// Only the dimensions the NeRF path uses (0 and 1) are needed.
+// ---------------------------------------------------------------------------
+NGP_HD uint32_t sobol_dim(uint32_t index, uint32_t dim) {
+	// dim 0: van der Corput (bit reversal); dim 1: direction numbers of
+	// random_val.cuh:176-179 (0x80000000, 0xc0000000, 0xa0000000, ...), which are
+	// the Pascal-triangle-mod-2 matrix: v_k = v_{k-1} ^ (v_{k-1} >> 1).
+	uint32_t X = 0;
+	uint32_t v = 0x80000000u;
+	for (uint32_t bit = 0; bit < 32; ++bit) {
+		uint32_t dirn = dim == 0 ? (0x80000000u >> bit) : v;
+		if ((index >> bit) & 1u) X ^= dirn;
+		v = v ^ (v >> 1);
+	}
+	return X;
+}
+NGP_HD uint32_t hash_combine(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+NGP_HD uint32_t reverse_bits(uint32_t x) {
+	x = (((x & 0xaaaaaaaau) >> 1) | ((x & 0x55555555u) << 1));
+	x = (((x & 0xccccccccu) >> 2) | ((x & 0x33333333u) << 2));
+	x = (((x & 0xf0f0f0f0u) >> 4) | ((x & 0x0f0f0f0fu) << 4));
+	x = (((x & 0xff00ff00u) >> 8) | ((x & 0x00ff00ffu) << 8));
+	return ((x >> 16) | (x << 16));
+}
+NGP_HD uint32_t laine_karras_permutation(uint32_t x, uint32_t seed) {
+	x += seed;
+	x ^= x * 0x6c50b47cu;
+	x ^= x * 0xb82f1e52u;
+	x ^= x * 0xc7afe638u;
+	x ^= x * 0x8d22f6e6u;
+	return x;
+}
+NGP_HD uint32_t nested_uniform_scramble_base2(uint32_t x, uint32_t seed) {
+	return reverse_bits(laine_karras_permutation(reverse_bits(x), seed));
+}
+// ld_random_val (random_val.cuh:287-291)
+NGP_HD float ld_random_val(uint32_t index, uint32_t seed, uint32_t dim = 0) {
+	const float S = (float)(1.0 / (double)(1ull << 32));
+	index = nested_uniform_scramble_base2(index, seed);
+	return (float)nested_uniform_scramble_base2(sobol_dim(index, dim), hash_combine(seed, dim)) * S;
+}
+// ld_random_val_2d (random_val.cuh:266-285)
+NGP_HD void ld_random_val_2d(uint32_t index, uint32_t seed, float* x, float* y) {
+	const float S = (float)(1.0 / (double)(1ull << 32));
+	index = nested_uniform_scramble_base2(index, seed);
+	*x = (float)nested_uniform_scramble_base2(sobol_dim(index, 0), hash_combine(seed, 0)) * S;
+	*y = (float)nested_uniform_scramble_base2(sobol_dim(index, 1), hash_combine(seed, 1)) * S;
+}
+NGP_HD float fractf(float x) { return x - floorf(x); }
+// ld_random_pixel_offset (random_val.cuh:320-325)
+NGP_HD void ld_random_pixel_offset(uint32_t spp, float* ox, float* oy) {
+	float ax, ay, bx, by;
+	ld_random_val_2d(0, 0xdeadbeefu, &ax, &ay);
+	ld_random_val_2d(spp, 0xdeadbeefu, &bx, &by);
+	*ox = fractf(0.5f - ax + bx);
+	*oy = fractf(0.5f - ay + by);
+}
+
+// ---------------------------------------------------------------------------
+// Colour helpers — common_device.cuh:34-80.
+// ---------------------------------------------------------------------------
+NGP_HD float srgb_to_linear(float srgb) {
+	return srgb <= 0.04045f ? srgb / 12.92f : powf((srgb + 0.055f) / 1.055f, 2.4f);
+}
+NGP_HD float linear_to_srgb(float lin) {
+	return lin < 0.0031308f ? 12.92f * lin : 1.055f * powf(lin, 0.41666f) - 0.055f;
+}
+NGP_HD float logistic(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// ---------------------------------------------------------------------------
+// Axis-aligned box — bounding_box.cuh:95-97,172-230.
+// ---------------------------------------------------------------------------
+struct aabb3 {
+	v3 min, max;
+};
+NGP_HD bool aabb_contains(const aabb3& b, v3 p) {
+	return p.x >= b.min.x && p.x <= b.max.x && p.y >= b.min.y && p.y <= b.max.y && p.z >= b.min.z && p.z <= b.max.z;
+}
+NGP_HD v3 aabb_relative(const aabb3& b, v3 p) { return (p - b.min) / (b.max - b.min); }
+NGP_HD void ray_intersect(const aabb3& b, v3 pos, v3 dir, float* t0, float* t1) {
+	const float FMAX = 3.402823466e+38f;
+	float tmin = (b.min.x - pos.x) / dir.x, tmax = (b.max.x - pos.x) / dir.x;
+	if (tmin > tmax) { float t = tmin; tmin = tmax; tmax = t; }
+	float tymin = (b.min.y - pos.y) / dir.y, tymax = (b.max.y - pos.y) / dir.y;
+	if (tymin > tymax) { float t = tymin; tymin = tymax; tymax = t; }
+	if (tmin > tymax || tymin > tmax) { *t0 = FMAX; *t1 = FMAX; return; }
+	if (tymin > tmin) tmin = tymin;
+	if (tymax < tmax) tmax = tymax;
+	float tzmin = (b.min.z - pos.z) / dir.z, tzmax = (b.max.z - pos.z) / dir.z;
+	if (tzmin > tzmax) { float t = tzmin; tzmin = tzmax; tzmax = t; }
+	if (tmin > tzmax || tzmin > tmax) { *t0 = FMAX; *t1 = FMAX; return; }
+	if (tzmin > tmin) tmin = tzmin;
+	if (tzmax < tmax) tmax = tzmax;
+	*t0 = tmin;
+	*t1 = tmax;
+}
+
+// ---------------------------------------------------------------------------
+// Warps — nerf_device.cuh:265-314.
+// ---------------------------------------------------------------------------
+NGP_HD v3 warp_direction(v3 d) { return (d + 1.0f) * 0.5f; }
+NGP_HD float warp_dt(float dt) {
+	float max_stepsize = MIN_CONE_STEPSIZE * (float)(1u << (NERF_CASCADES - 1));
+	return (dt - MIN_CONE_STEPSIZE) / (max_stepsize - MIN_CONE_STEPSIZE);
+}
+NGP_HD float unwarp_dt(float dt) {
+	float max_stepsize = MIN_CONE_STEPSIZE * (float)(1u << (NERF_CASCADES - 1));
+	return dt * (max_stepsize - MIN_CONE_STEPSIZE) + MIN_CONE_STEPSIZE;
+}
+NGP_HD v3 unwarp_position(v3 p, const aabb3& b) { return b.min + p * (b.max - b.min); }
+
+// ---------------------------------------------------------------------------
+// Occupancy grid — nerf_device.cuh:316-357.
+// ---------------------------------------------------------------------------
+NGP_HD uint32_t cascaded_grid_idx_at(v3 pos, uint32_t mip) {
+	float mip_scale = scalbnf(1.0f, -(int)mip);
+	pos = pos - 0.5f;
+	pos = pos * mip_scale;
+	pos = pos + 0.5f;
+	int ix = (int)(pos.x * (float)NERF_GRIDSIZE);
+	int iy = (int)(pos.y * (float)NERF_GRIDSIZE);
+	int iz = (int)(pos.z * (float)NERF_GRIDSIZE);
+	if (ix < 0 || ix >= (int)NERF_GRIDSIZE || iy < 0 || iy >= (int)NERF_GRIDSIZE || iz < 0 || iz >= (int)NERF_GRIDSIZE) {
+		return 0xFFFFFFFFu;
+	}
+	return morton3D((uint32_t)ix, (uint32_t)iy, (uint32_t)iz);
+}
+NGP_HD bool density_grid_occupied_at(v3 pos, const uint8_t* bitfield, uint32_t mip) {
+	uint32_t idx = cascaded_grid_idx_at(pos, mip);
+	if (idx == 0xFFFFFFFFu) return false;
+	return bitfield[idx / 8 + (NERF_GRID_N_CELLS / 8) * mip] & (1u << (idx % 8));
+}
+
+// ---------------------------------------------------------------------------
+// Exponential (cone) stepping — nerf_device.cuh:359-459.
+// ---------------------------------------------------------------------------
+NGP_HD float signf_(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
+NGP_HD float distance_to_next_voxel(v3 pos, v3 dir, v3 idir, float res) {
+	v3 p = (pos - 0.5f) * res;
+	float tx = (floorf(p.x + 0.5f + 0.5f * signf_(dir.x)) - p.x) * idir.x;
+	float ty = (floorf(p.y + 0.5f + 0.5f * signf_(dir.y)) - p.y) * idir.y;
+	float tz = (floorf(p.z + 0.5f + 0.5f * signf_(dir.z)) - p.z) * idir.z;
+	float t = fminf(fminf(tx, ty), tz);
+	return fmaxf(t / res, 0.0f);
+}
+NGP_HD float to_stepping_space(float t, float cone_angle) {
+	if (cone_angle <= 1e-5f) return t / MIN_CONE_STEPSIZE;
+	float log1p_c = logf(1.0f + cone_angle);
+	float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	float at = expf(a * log1p_c);
+	float bt = expf(b * log1p_c);
+	if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
+	else if (t <= bt) return logf(t) / log1p_c;
+	else return (t - bt) / MAX_CONE_STEPSIZE + b;
+}
+NGP_HD float from_stepping_space(float n, float cone_angle) {
+	if (cone_angle <= 1e-5f) return n * MIN_CONE_STEPSIZE;
+	float log1p_c = logf(1.0f + cone_angle);
+	float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
+	float at = expf(a * log1p_c);
+	float bt = expf(b * log1p_c);
+	if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
+	else if (n <= b) return expf(n * log1p_c);
+	else return (n - b) * MAX_CONE_STEPSIZE + bt;
+}
+NGP_HD float advance_n_steps(float t, float cone_angle, float n) {
+	return from_stepping_space(to_stepping_space(t, cone_angle) + n, cone_angle);
+}
+NGP_HD float calc_dt(float t, float cone_angle) { return advance_n_steps(t, cone_angle, 1.0f) - t; }
+NGP_HD float advance_to_next_voxel(float t, float cone_angle, v3 pos, v3 dir, v3 idir, uint32_t mip) {
+	float res = scalbnf((float)NERF_GRIDSIZE, -(int)mip);
+	float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
+	t = to_stepping_space(t, cone_angle);
+	t_target = to_stepping_space(t_target, cone_angle);
+	return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone_angle);
+}
+NGP_HD uint32_t mip_from_pos(v3 pos, uint32_t max_cascade = NERF_CASCADES - 1) {
+	int exponent;
+	float maxval = maxc(absv(pos - 0.5f));
+	frexpf(maxval, &exponent);
+	int m = exponent + 1;
+	m = m < 0 ? 0 : (m > (int)max_cascade ? (int)max_cascade : m);
+	return (uint32_t)m;
+}
+NGP_HD uint32_t mip_from_dt(float dt, v3 pos, uint32_t max_cascade = NERF_CASCADES - 1) {
+	uint32_t mip = mip_from_pos(pos, max_cascade);
+	dt *= 2.0f * (float)NERF_GRIDSIZE;
+	if (dt < 1.0f) return mip;
+	int exponent;
+	frexpf(dt, &exponent);
+	int m = exponent < (int)mip ? (int)mip : exponent;   // clamp((int)mip, exponent, max)
+	m = m > (int)max_cascade ? (int)max_cascade : m;
+	return (uint32_t)m;
+}
+// if_unoccupied_advance_to_next_occupied_voxel (nerf_device.cuh:461-494), identity
+// render_aabb_to_local, MIP_FROM_DT=false.
+NGP_HD float if_unoccupied_advance_to_next_occupied_voxel(float t, float cone_angle, v3 o, v3 d, v3 idir,
+		const uint8_t* bitfield, uint32_t min_mip, uint32_t max_mip, const aabb3& aabb) {
+	while (true) {
+		v3 pos = o + d * t;
+		if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return MAX_DEPTH;
+		uint32_t mip = mip_from_pos(pos);
+		mip = mip < min_mip ? min_mip : (mip > max_mip ? max_mip : mip);
+		if (!bitfield || density_grid_occupied_at(pos, bitfield, mip)) return t;
+		while (mip < max_mip && !density_grid_occupied_at(pos, bitfield, mip + 1)) ++mip;
+		t = advance_to_next_voxel(t, cone_angle, pos, d, idir, mip);
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Image sampling helpers — nerf_device.cuh:552-598, common_device.cuh:730-806.
+// ---------------------------------------------------------------------------
+NGP_HD uint32_t image_idx(uint32_t base_idx, uint32_t n_rays, uint32_t n_training_images) {
+	return (uint32_t)((((uint64_t)base_idx) * n_training_images) / n_rays) % n_training_images;
+}
+
+// Loss (nerf_device.cuh:74-142,600-615). loss_type matches ELossType (common.h:79-87).
+enum LossType : int { LOSS_L2 = 0, LOSS_L1 = 1, LOSS_MAPE = 2, LOSS_SMAPE = 3, LOSS_HUBER = 4, LOSS_LOGL1 = 5, LOSS_RELL2 = 6 };
+NGP_HD void loss_and_gradient(float target, float pred, int loss_type, float* loss, float* grad) {
+	float diff = pred - target;
+	switch (loss_type) {
+		case LOSS_RELL2: { float den = pred * pred + 1e-2f; *loss = diff * diff / den; *grad = 2.0f * diff / den; } break;
+		case LOSS_L1: { *loss = fabsf(diff); *grad = copysignf(1.0f, diff); } break;
+		case LOSS_MAPE: { float den = fabsf(pred) + 1e-2f; *loss = fabsf(diff) / den; *grad = copysignf(1.0f / den, diff); } break;
+		case LOSS_SMAPE: { float den = 0.5f * (fabsf(pred) + fabsf(target)) + 1e-2f; *loss = fabsf(diff) / den; *grad = copysignf(1.0f / den, diff); } break;
+		case LOSS_HUBER: {
+			const float alpha = 0.1f;
+			float ad = fabsf(diff);
+			float sq = 0.5f / alpha * diff * diff;
+			*loss = (ad > alpha ? (ad - 0.5f * alpha) : sq) / 5.0f;
+			*grad = (ad > alpha ? (diff > 0 ? 1.0f : -1.0f) : (diff / alpha)) / 5.0f;
+		} break;
+		case LOSS_LOGL1: { float dv = fabsf(diff) + 1.0f; *loss = logf(dv); *grad = copysignf(1.0f / dv, diff); } break;
+		default: { *loss = diff * diff; *grad = 2.0f * diff; } break;
+	}
+}
+
+// Activations (nerf_device.cuh:203-254). ENerfActivation: None, ReLU, Logistic, Exponential.
+enum Activation : int { ACT_NONE = 0, ACT_RELU = 1, ACT_LOGISTIC = 2, ACT_EXP = 3 };
+NGP_HD float network_to_rgb(float v, int act) {
+	switch (act) {
+		case ACT_RELU: return v > 0.0f ? v : 0.0f;
+		case ACT_LOGISTIC: return logistic(v);
+		case ACT_EXP: return expf(fminf(fmaxf(v, -10.0f), 10.0f));
+		default: return v;
+	}
+}
+NGP_HD float network_to_rgb_derivative(float v, int act) {
+	switch (act) {
+		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
+		case ACT_LOGISTIC: { float d = logistic(v); return d * (1 - d); }
+		case ACT_EXP: return expf(fminf(fmaxf(v, -10.0f), 10.0f));
+		default: return 1.0f;
+	}
+}
+NGP_HD float network_to_density(float v, int act) {
+	switch (act) {
+		case ACT_RELU: return v > 0.0f ? v : 0.0f;
+		case ACT_LOGISTIC: return logistic(v);
+		case ACT_EXP: return expf(v);
+		default: return v;
+	}
+}
+NGP_HD float network_to_density_derivative(float v, int act) {
+	switch (act) {
+		case ACT_RELU: return v > 0.0f ? 1.0f : 0.0f;
+		case ACT_LOGISTIC: { float d = logistic(v); return d * (1 - d); }
+		case ACT_EXP: return expf(fminf(fmaxf(v, -15.0f), 15.0f));
+		default: return 1.0f;
+	}
+}
+
+}  // namespace ngp

@@ -1,0 +1,384 @@
+// render.hip — NeRF volume renderer (NerfTracer) for gfx950.
+//
+//  k_render_init    init_rays_with_payload_kernel_nerf + advance_pos_nerf  src/testbed_nerf.cu:1376-1489, 333-381
+//  k_compact        compact_kernel_nerf                                     :1351-1374 (wave ballot + prefix,
+//                                                                            one atomic per wave)
+//  k_generate       generate_next_nerf_network_inputs                       :421-469
+//  k_composite      composite_kernel_nerf (Shade mode)                      :471-677
+//  k_shade          shade_kernel_nerf                                       :1309-1349
+//  k_accum_tonemap  accumulate_kernel + tonemap_kernel                      src/render_buffer.cu:232-266, 533-565
+//
+// Every ray's result depends only on its own sample sequence (the compaction
+// only regroups rays), so the image is deterministic per pixel and matches the
+// oracle's straight per-ray march whatever order the waves claim slots in.
+#include "ngp_internal.h"
+
+namespace ngp {
+
+struct Payload {
+	float o[3];
+	float d[3];
+	float t;
+	float max_weight;
+	uint32_t idx;
+	uint32_t n_steps;
+	uint32_t alive;
+	uint32_t pad;
+};
+static_assert(sizeof(Payload) == 48, "payload layout");
+
+struct RenderK {
+	uint32_t W, H;
+	uint32_t sample_index;
+	m43 cam;
+	float fx, fy, scx, scy;
+	float near_distance;
+	aabb3 aabb, train_aabb;
+	float cone_angle;
+	uint32_t max_mip;
+	float min_transmittance;
+	int snap;
+	int linear_colors;
+	int rgb_act, density_act;
+	uint32_t shard_index, shard_count, shard_rows;
+	uint32_t n_local;
+	const uint8_t* bitfield;
+};
+
+__device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32_t yl) {
+	const uint32_t blk = yl / k.shard_rows, within = yl % k.shard_rows;
+	return (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
+}
+
+__global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
+                                                     float* __restrict__ depth, float4* __restrict__ frame,
+                                                     float* __restrict__ depth_buffer) {
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= k.n_local) return;
+	const uint32_t x = r % k.W, yl = r / k.W;
+	const uint32_t y = local_to_global_row(k, yl);
+	const uint32_t idx = x + k.W * y;
+	rgba[r] = make_float4(0.f, 0.f, 0.f, 0.f);
+	depth[r] = 0.0f;
+	frame[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+	depth_buffer[idx] = MAX_DEPTH;
+
+	float ox, oy;
+	ld_random_pixel_offset(k.snap ? 0u : k.sample_index, &ox, &oy);
+	const float u = ((float)x + ox) / (float)k.W, v = ((float)y + oy) / (float)k.H;
+	v3 dir = mk3((u - k.scx) * (float)k.W / k.fx, (v - k.scy) * (float)k.H / k.fy, 1.0f);
+	dir = rot(k.cam, dir);
+	v3 origin = k.cam.c[3] + dir * k.near_distance;
+
+	Payload p;
+	p.max_weight = 0.0f;
+	p.idx = idx;
+	p.n_steps = 0;
+	p.pad = 0;
+	dir = normalize(dir);
+	float t0, t1;
+	ray_intersect(k.aabb, origin, dir, &t0, &t1);
+	float t = fmaxf(t0, 0.0f) + 1e-6f;
+	p.o[0] = origin.x; p.o[1] = origin.y; p.o[2] = origin.z;
+	p.d[0] = dir.x; p.d[1] = dir.y; p.d[2] = dir.z;
+	p.t = t;
+	p.alive = aabb_contains(k.aabb, origin + dir * t) ? 1u : 0u;
+	if (p.alive) {
+		// advance_pos_nerf: jitter the start and skip empty space
+		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
+		t = advance_n_steps(t, k.cone_angle, ld_random_val(k.sample_index, idx * 786433u));
+		t = if_unoccupied_advance_to_next_occupied_voxel(t, k.cone_angle, origin, dir, idir, k.bitfield, 0, k.max_mip, k.aabb);
+		if (t >= MAX_DEPTH) p.alive = 0;
+		else p.t = t;
+	}
+	payloads[r] = p;
+}
+
+__global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __restrict__ sp, const float4* __restrict__ srgba,
+                                                 const float* __restrict__ sdepth, Payload* __restrict__ dp,
+                                                 float4* __restrict__ drgba, float* __restrict__ ddepth,
+                                                 Payload* __restrict__ hp, float4* __restrict__ hrgba,
+                                                 float* __restrict__ hdepth, uint32_t* __restrict__ counters) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const int lane = threadIdx.x & 63;
+	bool alive = false, hit = false;
+	Payload p;
+	float4 c;
+	float dd = 0.0f;
+	if (i < n) {
+		p = sp[i];
+		c = srgba[i];
+		dd = sdepth[i];
+		alive = p.alive != 0;
+		hit = !alive && c.w > 0.001f;
+	}
+	const unsigned long long ma = __ballot(alive), mh = __ballot(hit);
+	const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+	uint32_t base_a = 0, base_h = 0;
+	if (lane == 0) {
+		base_a = ma ? atomicAdd(&counters[0], (uint32_t)__popcll(ma)) : 0u;
+		base_h = mh ? atomicAdd(&counters[1], (uint32_t)__popcll(mh)) : 0u;
+	}
+	base_a = __shfl(base_a, 0, 64);
+	base_h = __shfl(base_h, 0, 64);
+	if (alive) {
+		const uint32_t o = base_a + __popcll(ma & below);
+		dp[o] = p;
+		drgba[o] = c;
+		ddepth[o] = dd;
+	} else if (hit) {
+		const uint32_t o = base_h + __popcll(mh & below);
+		hp[o] = p;
+		hrgba[o] = c;
+		hdepth[o] = dd;
+	}
+}
+
+__global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
+                                                  float* __restrict__ coords, uint32_t n_steps) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n_alive) return;
+	Payload& p = payloads[i];
+	if (!p.alive) return;
+	const v3 o = mk3(p.o[0], p.o[1], p.o[2]), d = mk3(p.d[0], p.d[1], p.d[2]);
+	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	const v3 wdir = warp_direction(d);
+	float t = p.t;
+	for (uint32_t j = 0; j < n_steps; ++j) {
+		t = if_unoccupied_advance_to_next_occupied_voxel(t, k.cone_angle, o, d, idir, k.bitfield, 0, k.max_mip, k.aabb);
+		if (t >= MAX_DEPTH) {
+			p.n_steps = j;
+			return;
+		}
+		const float dt = calc_dt(t, k.cone_angle);
+		const v3 wp = aabb_relative(k.train_aabb, o + d * t);
+		float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)j * n_alive));
+		c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+		c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+		t += dt;
+	}
+	p.t = t;
+	p.n_steps = n_steps;
+}
+
+__global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, uint32_t current_step,
+                                                   Payload* __restrict__ payloads, float4* __restrict__ rgba,
+                                                   float* __restrict__ depth, const float* __restrict__ coords,
+                                                   const __half* __restrict__ out, uint32_t n_steps) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n_alive) return;
+	Payload& p = payloads[i];
+	if (!p.alive) return;
+	float4 c = rgba[i];
+	float local_depth = depth[i];
+	const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
+	const uint32_t actual = p.n_steps;
+	uint32_t j = 0;
+	for (; j < actual; ++j) {
+		const size_t s = (size_t)i + (size_t)j * n_alive;
+		const __half* o = out + 4 * s;
+		const float* crd = coords + 8 * s;
+		const v3 pos = unwarp_position(mk3(crd[0], crd[1], crd[2]), k.train_aabb);
+		const float T = 1.0f - c.w;
+		const float dt = unwarp_dt(crd[3]);
+		const float alpha = 1.0f - __expf(-network_to_density(__half2float(o[3]), k.density_act) * dt);
+		const float weight = alpha * T;
+		const v3 rgb = mk3(network_to_rgb(__half2float(o[0]), k.rgb_act), network_to_rgb(__half2float(o[1]), k.rgb_act),
+		                   network_to_rgb(__half2float(o[2]), k.rgb_act));
+		c.x += rgb.x * weight;
+		c.y += rgb.y * weight;
+		c.z += rgb.z * weight;
+		c.w += weight;
+		if (weight > p.max_weight) {
+			p.max_weight = weight;
+			local_depth = dot(cam_fwd, pos - cam_pos);
+		}
+		if (c.w > (1.0f - k.min_transmittance)) {
+			const float inv = 1.0f / c.w;
+			c.x *= inv;
+			c.y *= inv;
+			c.z *= inv;
+			c.w *= inv;
+			break;
+		}
+	}
+	if (j < n_steps) {
+		p.alive = 0;
+		p.n_steps = j + current_step;
+	}
+	rgba[i] = c;
+	depth[i] = local_depth;
+}
+
+__global__ void __launch_bounds__(256) k_shade(uint32_t n, const Payload* __restrict__ hp, const float4* __restrict__ hrgba,
+                                               const float* __restrict__ hdepth, int linear_colors,
+                                               float4* __restrict__ frame, float* __restrict__ depth_buffer) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	const uint32_t idx = hp[i].idx;
+	float4 t = hrgba[i];
+	if (!linear_colors) {
+		t.x = srgb_to_linear(t.x);
+		t.y = srgb_to_linear(t.y);
+		t.z = srgb_to_linear(t.z);
+	}
+	const float4 f = frame[idx];
+	frame[idx] = make_float4(t.x + f.x * (1.0f - t.w), t.y + f.y * (1.0f - t.w), t.z + f.z * (1.0f - t.w),
+	                         t.w + f.w * (1.0f - t.w));
+	if (t.w > 0.2f) depth_buffer[idx] = hdepth[i];
+}
+
+__global__ void __launch_bounds__(256) k_accum_tonemap(uint32_t W, uint32_t H, const float4* __restrict__ frame,
+                                                       float4* __restrict__ accum, float4* __restrict__ out,
+                                                       float sample_count, int color_space, float exposure,
+                                                       float4 bg, int output_srgb) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= W * H) return;
+	float4 color = frame[i];
+	float4 tmp = sample_count == 0.0f ? make_float4(0.f, 0.f, 0.f, 0.f) : accum[i];
+	if (color_space == 1) {
+		color.x = linear_to_srgb(color.x);
+		color.y = linear_to_srgb(color.y);
+		color.z = linear_to_srgb(color.z);
+	}
+	tmp.x = (tmp.x * sample_count + color.x) / (sample_count + 1.0f);
+	tmp.y = (tmp.y * sample_count + color.y) / (sample_count + 1.0f);
+	tmp.z = (tmp.z * sample_count + color.z) / (sample_count + 1.0f);
+	tmp.w = (tmp.w * sample_count + color.w) / (sample_count + 1.0f);
+	accum[i] = tmp;
+	if (!out) return;
+	if (color_space != 1) {
+		bg.x = srgb_to_linear(bg.x);
+		bg.y = srgb_to_linear(bg.y);
+		bg.z = srgb_to_linear(bg.z);
+	}
+	float4 c = tmp;
+	const float weight = (1.0f - c.w) * bg.w;
+	c.x += bg.x * weight;
+	c.y += bg.y * weight;
+	c.z += bg.z * weight;
+	c.w += weight;
+	if (color_space == 1) {
+		c.x = srgb_to_linear(c.x);
+		c.y = srgb_to_linear(c.y);
+		c.z = srgb_to_linear(c.z);
+	}
+	const float e = powf(2.0f, exposure);
+	c.x *= e;
+	c.y *= e;
+	c.z *= e;
+	if (output_srgb) {
+		c.x = linear_to_srgb(c.x);
+		c.y = linear_to_srgb(c.y);
+		c.z = linear_to_srgb(c.z);
+	}
+	out[i] = c;
+}
+
+static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t rows) {
+	uint32_t n = 0;
+	for (uint32_t y = 0; y < H; ++y)
+		if ((y / rows) % count == idx) ++n;
+	return n;
+}
+
+void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s) {
+	RenderScratch& rs = m->rs;
+	RenderK k{};
+	k.W = a->width;
+	k.H = a->height;
+	k.sample_index = a->sample_index;
+	for (int c = 0; c < 4; ++c) k.cam.c[c] = mk3(a->camera[3 * c], a->camera[3 * c + 1], a->camera[3 * c + 2]);
+	k.fx = a->focal_length[0];
+	k.fy = a->focal_length[1];
+	k.scx = a->screen_center[0];
+	k.scy = a->screen_center[1];
+	k.near_distance = a->near_distance;
+	k.aabb.min = mk3(a->aabb_min[0], a->aabb_min[1], a->aabb_min[2]);
+	k.aabb.max = mk3(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2]);
+	k.train_aabb.min = mk3(a->train_aabb_min[0], a->train_aabb_min[1], a->train_aabb_min[2]);
+	k.train_aabb.max = mk3(a->train_aabb_max[0], a->train_aabb_max[1], a->train_aabb_max[2]);
+	k.cone_angle = a->cone_angle_constant;
+	k.max_mip = a->max_cascade;
+	k.min_transmittance = a->min_transmittance;
+	k.snap = a->snap_to_pixel_centers;
+	k.linear_colors = a->train_in_linear_colors;
+	k.rgb_act = m->cfg.rgb_activation;
+	k.density_act = m->cfg.density_activation;
+	k.shard_count = std::max(a->shard_count, 1u);
+	k.shard_index = a->shard_index % k.shard_count;
+	k.shard_rows = std::max(a->shard_rows, 1u);
+	k.bitfield = m->gs.bitfield.ptr;
+	const uint32_t H_local = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
+	const uint32_t n = k.W * H_local;
+	k.n_local = n;
+	if (n == 0) return;
+	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
+
+	const size_t max_samples = std::max<size_t>((size_t)n, (size_t)2 * 1024 * 1024) + 256;
+	for (int b = 0; b < 3; ++b) {
+		rs.payload[b].reserve((size_t)n * 12);
+		rs.rgba[b].reserve((size_t)n * 4);
+		rs.depth[b].reserve(n);
+	}
+	rs.coords.reserve(8 * max_samples);
+	rs.enc.reserve((size_t)m->lt.n_levels * max_samples * m->lt.F);
+	rs.out.reserve(4 * max_samples);
+	rs.counters.reserve(4);
+	if (!rs.host_counter.ptr) {
+		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 4 * sizeof(uint32_t), hipHostMallocDefault));
+		rs.host_counter.n = 4;
+	}
+	auto P = [&](int b) { return reinterpret_cast<Payload*>(rs.payload[b].ptr); };
+	auto C = [&](int b) { return reinterpret_cast<float4*>(rs.rgba[b].ptr); };
+
+	k_render_init<<<div_up(n, 256), 256, 0, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer);
+	NGP_HIP_CHECK(hipGetLastError());
+	NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, 4 * sizeof(uint32_t), s));
+
+	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
+	uint32_t n_alive = n;
+	uint32_t db = 0;
+	const uint32_t MARCH_ITER = 10000;
+	for (uint32_t it = 1; it < MARCH_ITER;) {
+		const int cur = (db + 1) % 2, tmp = db % 2;
+		++db;
+		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
+		k_compact<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(tmp), C(tmp), rs.depth[tmp].ptr, P(cur), C(cur),
+		                                               rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr, rs.counters.ptr);
+		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		n_alive = rs.host_counter.ptr[0];
+		if (n_alive == 0) break;
+		const uint32_t target = 2 * 1024 * 1024;
+		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), 8u);
+		k_generate<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
+		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
+		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s);
+		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s);
+		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, it, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
+		                                                 rs.out.ptr, n_steps);
+		NGP_HIP_CHECK(hipGetLastError());
+		it += n_steps;
+	}
+	NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+	NGP_HIP_CHECK(hipStreamSynchronize(s));
+	const uint32_t n_hit = rs.host_counter.ptr[1];
+	if (n_hit)
+		k_shade<<<div_up(n_hit, 256), 256, 0, s>>>(n_hit, P(2), C(2), rs.depth[2].ptr, k.linear_colors,
+		                                           reinterpret_cast<float4*>(frame), depth_buffer);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void run_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t W, uint32_t H, uint32_t spp,
+                            int color_space, float exposure, const float* bg, int output_srgb, hipStream_t s) {
+	const float4 b = bg ? make_float4(bg[0], bg[1], bg[2], bg[3]) : make_float4(0.f, 0.f, 0.f, 1.f);
+	k_accum_tonemap<<<div_up((uint64_t)W * H, 256), 256, 0, s>>>(W, H, reinterpret_cast<const float4*>(frame),
+	                                                             reinterpret_cast<float4*>(accum),
+	                                                             reinterpret_cast<float4*>(out), (float)spp, color_space,
+	                                                             exposure, b, output_srgb);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+}  // namespace ngp

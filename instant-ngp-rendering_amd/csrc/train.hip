@@ -1,0 +1,648 @@
+// train.hip — NeRF training-step kernels for gfx950.
+//
+//  k_sample_count / k_sample_write   generate_training_samples_nerf   src/testbed_nerf.cu:679-838
+//  k_loss_composite / k_loss_emit    compute_loss_kernel_train_nerf   src/testbed_nerf.cu:841-1160
+//  k_rollover_weight                 tcnn fill_rollover_and_rescale   src/testbed_nerf.cu:2862-2870
+//  k_optimizer                       tcnn Ema∘ExponentialDecay∘Adam   src/testbed_nerf.cu:2502
+//
+// The reference claims output slots with global atomicAdd (numsteps_counter,
+// ray_counter, numsteps_counter_compacted), so its sample order depends on
+// scheduling.  Here every compaction is an exclusive prefix sum over the ray
+// index (wave prefix via DPP shuffles -> workgroup -> grid), i.e. the same
+// rule the reference applies ("claim `numsteps` slots, drop the ray if
+// base + numsteps > cap") taken in ray-index order: deterministic, and
+// bit-identical to the scalar oracle.
+#include "ngp_internal.h"
+
+namespace ngp {
+
+// ---------------------------------------------------------------------------
+// Exclusive scan (deterministic): 1024 elements per workgroup.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ uint32_t wave_inclusive_scan(uint32_t v) {
+	const int lane = threadIdx.x & 63;
+#pragma unroll
+	for (int d = 1; d < 64; d <<= 1) {
+		const uint32_t u = __shfl_up(v, d, 64);
+		if (lane >= d) v += u;
+	}
+	return v;
+}
+
+__global__ void __launch_bounds__(256) k_scan_local(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                    uint32_t n, uint32_t* __restrict__ block_sums) {
+	__shared__ uint32_t wsum[4];
+	const uint32_t base = blockIdx.x * 1024u + threadIdx.x * 4u;
+	uint32_t v[4];
+#pragma unroll
+	for (int k = 0; k < 4; ++k) v[k] = base + k < n ? in[base + k] : 0u;
+	const uint32_t tsum = v[0] + v[1] + v[2] + v[3];
+	const uint32_t incl = wave_inclusive_scan(tsum);
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	if (lane == 63) wsum[wave] = incl;
+	__syncthreads();
+	uint32_t woff = 0;
+	for (int w = 0; w < wave; ++w) woff += wsum[w];
+	uint32_t run = woff + incl - tsum;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		if (base + k < n) out[base + k] = run;
+		run += v[k];
+	}
+	if (threadIdx.x == 255) block_sums[blockIdx.x] = woff + incl;
+}
+
+__global__ void __launch_bounds__(1024) k_scan_blocks(uint32_t* __restrict__ block_sums, uint32_t n_blocks,
+                                                      uint32_t* __restrict__ total) {
+	__shared__ uint32_t wsum[16];
+	__shared__ uint32_t carry;
+	if (threadIdx.x == 0) carry = 0;
+	__syncthreads();
+	for (uint32_t b0 = 0; b0 < n_blocks; b0 += 1024) {
+		const uint32_t i = b0 + threadIdx.x;
+		const uint32_t v = i < n_blocks ? block_sums[i] : 0u;
+		const uint32_t incl = wave_inclusive_scan(v);
+		const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+		if (lane == 63) wsum[wave] = incl;
+		__syncthreads();
+		uint32_t woff = carry;
+		for (int w = 0; w < wave; ++w) woff += wsum[w];
+		if (i < n_blocks) block_sums[i] = woff + incl - v;
+		__syncthreads();
+		if (threadIdx.x == 1023) carry = woff + incl;
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) *total = carry;
+}
+
+__global__ void k_scan_add(uint32_t* __restrict__ out, uint32_t n, const uint32_t* __restrict__ block_sums) {
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	if (i < n) out[i] += block_sums[i / 1024u];
+}
+
+void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* block_sums, uint32_t* total,
+                           hipStream_t s) {
+	const uint32_t nb = div_up(n, 1024);
+	if (nb == 0) {
+		NGP_HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), s));
+		return;
+	}
+	k_scan_local<<<nb, 256, 0, s>>>(in, out, n, block_sums);
+	k_scan_blocks<<<1, 1024, 0, s>>>(block_sums, nb, total);
+	k_scan_add<<<div_up(n, 256), 256, 0, s>>>(out, n, block_sums);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+// ---------------------------------------------------------------------------
+// Camera rays (uv_to_ray, common_device.cuh:393-460; perspective lens).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ m43 load_xform(const float* x) {
+	m43 m;
+	for (int c = 0; c < 4; ++c) m.c[c] = mk3(x[3 * c + 0], x[3 * c + 1], x[3 * c + 2]);
+	return m;
+}
+
+__device__ __forceinline__ uint32_t read_texel(const ngp_image& im, float u, float v) {
+	int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
+	px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
+	py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
+	return reinterpret_cast<const uint32_t*>(im.pixels)[(size_t)px + (size_t)py * im.width];
+}
+
+// read_rgba (common_device.cuh:774-793), Byte images: sRGB -> linear, premultiplied; mask colour -> -1
+__device__ __forceinline__ void texel_rgba(uint32_t t, float* rgba) {
+	if (t == 0x00FF00FFu) {
+		rgba[0] = rgba[1] = rgba[2] = rgba[3] = -1.0f;
+		return;
+	}
+	const float a = (float)((t >> 24) & 0xffu) * (1.0f / 255.0f);
+	rgba[0] = srgb_to_linear((float)(t & 0xffu) * (1.0f / 255.0f)) * a;
+	rgba[1] = srgb_to_linear((float)((t >> 8) & 0xffu) * (1.0f / 255.0f)) * a;
+	rgba[2] = srgb_to_linear((float)((t >> 16) & 0xffu) * (1.0f / 255.0f)) * a;
+	rgba[3] = a;
+}
+
+struct SamplerArgs {
+	const ngp_image* images;
+	uint32_t n_images;
+	uint32_t n_rays;
+	uint32_t n_rays_global;
+	uint32_t ray_offset;
+	uint32_t max_samples;
+	pcg32 rng;
+	aabb3 aabb;
+	float cone_angle;
+	uint32_t max_mip;
+	int snap;
+	const uint8_t* bitfield;
+	uint32_t* numsteps;  // [R][2]
+	uint32_t* counts;    // [R]
+	uint32_t* bases;     // [R]
+	float* ray_state;    // [R][8]
+	float* coords;       // [max][8]
+};
+
+// Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777).
+__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* startt) {
+	const uint32_t img = image_idx(gi, a.n_rays_global, a.n_images);
+	const ngp_image im = a.images[img];
+	pcg32 rng = a.rng;
+	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
+	float u = rng.next_float(), v = rng.next_float();
+	if (a.snap) {
+		int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
+		px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
+		py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
+		u = ((float)px + 0.5f) / (float)im.width;
+		v = ((float)py + 0.5f) / (float)im.height;
+	}
+	float rgba[4];
+	texel_rgba(read_texel(im, u, v), rgba);
+	if (rgba[0] < 0.0f) return false;
+	(void)rng.next_float();  // motionblur_time
+	const m43 xf = load_xform(im.xform);
+	v3 dir = mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
+	             (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+	dir = rot(xf, dir);
+	*o = xf.c[3];
+	*d = normalize(dir);
+	float t0, t1;
+	ray_intersect(a.aabb, *o, *d, &t0, &t1);
+	t0 = fmaxf(t0, 0.0f);
+	*startt = advance_n_steps(t0, a.cone_angle, rng.next_float());
+	return true;
+}
+
+__global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n_rays) return;
+	v3 o, d;
+	float t;
+	uint32_t j = 0;
+	if (training_ray(a, a.ray_offset + i, &o, &d, &t)) {
+		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		v3 pos;
+		while (aabb_contains(a.aabb, pos = o + d * t) && j < NERF_STEPS) {
+			const float dt = calc_dt(t, a.cone_angle);
+			const uint32_t mip = mip_from_dt(dt, pos, a.max_mip);
+			if (density_grid_occupied_at(pos, a.bitfield, mip)) {
+				++j;
+				t += dt;
+			} else {
+				t = advance_to_next_voxel(t, a.cone_angle, pos, d, idir, mip);
+			}
+		}
+	}
+	a.counts[i] = j;
+}
+
+__global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n_rays) return;
+	const uint32_t n = a.counts[i], base = a.bases[i];
+	if (n == 0 || base + n > a.max_samples) {
+		a.numsteps[2 * i + 0] = 0;
+		a.numsteps[2 * i + 1] = 0;
+		return;
+	}
+	v3 o, d;
+	float t;
+	training_ray(a, a.ray_offset + i, &o, &d, &t);
+	a.numsteps[2 * i + 0] = n;
+	a.numsteps[2 * i + 1] = base;
+	float* rs = a.ray_state + 8 * (size_t)i;
+	rs[0] = o.x; rs[1] = o.y; rs[2] = o.z;
+	rs[3] = d.x; rs[4] = d.y; rs[5] = d.z;
+	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	const v3 wdir = warp_direction(d);
+	uint32_t j = 0;
+	v3 pos;
+	while (aabb_contains(a.aabb, pos = o + d * t) && j < n) {
+		const float dt = calc_dt(t, a.cone_angle);
+		const uint32_t mip = mip_from_dt(dt, pos, a.max_mip);
+		if (density_grid_occupied_at(pos, a.bitfield, mip)) {
+			const v3 wp = aabb_relative(a.aabb, pos);
+			float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + j));
+			c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+			c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+			++j;
+			t += dt;
+		} else {
+			t = advance_to_next_voxel(t, a.cone_angle, pos, d, idir, mip);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Loss: composite (pass 1), prefix sum, emit compacted samples + dL/dout (pass 2).
+// ---------------------------------------------------------------------------
+struct LossArgs {
+	const ngp_image* images;
+	uint32_t n_images;
+	uint32_t n_rays;
+	uint32_t n_rays_global;
+	uint32_t ray_offset;
+	pcg32 rng;
+	aabb3 aabb;
+	int snap;
+	int loss_type;
+	int random_bg;
+	v3 bg;
+	int linear_colors;
+	int color_space;
+	int rgb_act, density_act;
+	float near_distance;
+	uint32_t max_compacted;
+	uint32_t target_batch;
+	const uint32_t* numsteps;
+	const float* ray_state;
+	const float* coords;
+	const __half* mlp_out;
+	const __half* enc;
+	uint32_t enc_plane;
+	uint32_t n_levels, F;
+	uint32_t* ccounts;     // [R] compacted count (pre-cap)
+	uint32_t* cbases;      // [R]
+	float* loss_state;     // [R][8]: grad xyz, rgb_ray xyz, mean_loss, pad
+	uint32_t* compacted;   // [R][2]
+	float* loss_out;       // [R]
+	float* ccoords;        // [B][8]
+	__half* cenc;          // [L][B][F]
+	__half* dloss;         // [B][4]
+	const float* mean_density;
+};
+
+__global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n_rays) return;
+	const uint32_t numsteps = a.numsteps[2 * i + 0], base = a.numsteps[2 * i + 1];
+	if (numsteps == 0) {
+		a.ccounts[i] = 0;
+		return;
+	}
+	float T = 1.0f;
+	v3 rgb_ray = mk3(0.0f);
+	uint32_t c = 0;
+	for (; c < numsteps; ++c) {
+		if (T < 1e-4f) break;
+		const __half* o = a.mlp_out + 4 * (size_t)(base + c);
+		const float* crd = a.coords + 8 * (size_t)(base + c);
+		const v3 rgb = mk3(network_to_rgb(__half2float(o[0]), a.rgb_act), network_to_rgb(__half2float(o[1]), a.rgb_act),
+		                   network_to_rgb(__half2float(o[2]), a.rgb_act));
+		const float dt = unwarp_dt(crd[3]);
+		const float density = network_to_density(__half2float(o[3]), a.density_act);
+		const float alpha = 1.0f - __expf(-density * dt);
+		const float weight = alpha * T;
+		rgb_ray = rgb_ray + rgb * weight;
+		T *= (1.0f - alpha);
+	}
+
+	// Same RNG stream as the sampler -> same pixel and background colour (testbed_nerf.cu:938-955).
+	const uint32_t gi = a.ray_offset + i;
+	pcg32 rng = a.rng;
+	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
+	const uint32_t img = image_idx(gi, a.n_rays_global, a.n_images);
+	const ngp_image im = a.images[img];
+	float u = rng.next_float(), v = rng.next_float();
+	if (a.snap) {
+		int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
+		px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
+		py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
+		u = ((float)px + 0.5f) / (float)im.width;
+		v = ((float)py + 0.5f) / (float)im.height;
+	}
+	rng.advance(1);  // motionblur_time
+	v3 bg = a.bg;
+	if (a.random_bg) {
+		const float r0 = rng.next_float(), r1 = rng.next_float(), r2 = rng.next_float();
+		bg = mk3(r0, r1, r2);
+	}
+	bg = mk3(srgb_to_linear(bg.x), srgb_to_linear(bg.y), srgb_to_linear(bg.z));
+	float tex[4];
+	texel_rgba(read_texel(im, u, v), tex);
+	v3 target;
+	if (a.linear_colors || a.color_space == 0) {
+		target = mk3(tex[0], tex[1], tex[2]) + bg * (1.0f - tex[3]);
+		if (!a.linear_colors) {
+			target = mk3(linear_to_srgb(target.x), linear_to_srgb(target.y), linear_to_srgb(target.z));
+			bg = mk3(linear_to_srgb(bg.x), linear_to_srgb(bg.y), linear_to_srgb(bg.z));
+		}
+	} else {
+		bg = mk3(linear_to_srgb(bg.x), linear_to_srgb(bg.y), linear_to_srgb(bg.z));
+		if (tex[3] > 0.0f) {
+			const v3 s = mk3(linear_to_srgb(tex[0] / tex[3]), linear_to_srgb(tex[1] / tex[3]), linear_to_srgb(tex[2] / tex[3]));
+			target = s * tex[3] + bg * (1.0f - tex[3]);
+		} else {
+			target = bg;
+		}
+	}
+	if (c == numsteps) rgb_ray = rgb_ray + bg * T;
+	float lx, ly, lz, gx, gy, gz;
+	loss_and_gradient(target.x, rgb_ray.x, a.loss_type, &lx, &gx);
+	loss_and_gradient(target.y, rgb_ray.y, a.loss_type, &ly, &gy);
+	loss_and_gradient(target.z, rgb_ray.z, a.loss_type, &lz, &gz);
+	float* ls = a.loss_state + 8 * (size_t)i;
+	ls[0] = gx; ls[1] = gy; ls[2] = gz;
+	ls[3] = rgb_ray.x; ls[4] = rgb_ray.y; ls[5] = rgb_ray.z;
+	ls[6] = (lx + ly + lz) / 3.0f;
+	a.ccounts[i] = c;
+}
+
+__global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n_rays) return;
+	const uint32_t n = a.ccounts[i], cbase = a.cbases[i];
+	const uint32_t cn = n == 0 ? 0 : min(a.max_compacted - min(a.max_compacted, cbase), n);
+	a.compacted[2 * i + 0] = cn;
+	a.compacted[2 * i + 1] = cbase;
+	if (cn == 0) {
+		a.loss_out[i] = 0.0f;
+		return;
+	}
+	const uint32_t base = a.numsteps[2 * i + 1];
+	const float* ls = a.loss_state + 8 * (size_t)i;
+	const v3 grad = mk3(ls[0], ls[1], ls[2]);
+	const v3 rgb_ray = mk3(ls[3], ls[4], ls[5]);
+	a.loss_out[i] = ls[6] / (float)a.n_rays_global;
+	const float loss_scale = 128.0f / (float)a.n_rays_global;  // LOSS_SCALE / n_rays (testbed_nerf.cu:1056)
+	const float output_l2_reg = a.rgb_act == ACT_EXP ? 1e-4f : 0.0f;
+	const float output_l1_reg_density = *a.mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
+	const v3 ray_o = mk3(a.ray_state[8 * (size_t)i + 0], a.ray_state[8 * (size_t)i + 1], a.ray_state[8 * (size_t)i + 2]);
+
+	v3 rgb_ray2 = mk3(0.0f);
+	float T = 1.0f;
+	for (uint32_t j = 0; j < cn; ++j) {
+		const size_t src = base + j, dst = cbase + j;
+		const float4* ci = reinterpret_cast<const float4*>(a.coords + 8 * src);
+		const float4 c0 = ci[0], c1 = ci[1];
+		float4* co = reinterpret_cast<float4*>(a.ccoords + 8 * dst);
+		co[0] = c0;
+		co[1] = c1;
+		for (uint32_t l = 0; l < a.n_levels; ++l) {
+			const __half* es = a.enc + ((size_t)l * a.enc_plane + src) * a.F;
+			__half* ed = a.cenc + ((size_t)l * a.target_batch + dst) * a.F;
+			for (uint32_t f = 0; f < a.F; ++f) ed[f] = es[f];
+		}
+		const v3 pos = unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb);
+		const float depth = length(pos - ray_o);
+		const float dt = unwarp_dt(c0.w);
+		const __half* o = a.mlp_out + 4 * src;
+		const float o0 = __half2float(o[0]), o1 = __half2float(o[1]), o2 = __half2float(o[2]), o3 = __half2float(o[3]);
+		const v3 rgb = mk3(network_to_rgb(o0, a.rgb_act), network_to_rgb(o1, a.rgb_act), network_to_rgb(o2, a.rgb_act));
+		const float density = network_to_density(o3, a.density_act);
+		const float alpha = 1.0f - __expf(-density * dt);
+		const float weight = alpha * T;
+		rgb_ray2 = rgb_ray2 + rgb * weight;
+		T *= (1.0f - alpha);
+		const v3 suffix = rgb_ray - rgb_ray2;
+		const v3 dloss_by_drgb = grad * weight;
+		__half* dl = a.dloss + 4 * dst;
+		dl[0] = __float2half(loss_scale * (dloss_by_drgb.x * network_to_rgb_derivative(o0, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o0)));
+		dl[1] = __float2half(loss_scale * (dloss_by_drgb.y * network_to_rgb_derivative(o1, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o1)));
+		dl[2] = __float2half(loss_scale * (dloss_by_drgb.z * network_to_rgb_derivative(o2, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o2)));
+		const float density_derivative = network_to_density_derivative(o3, a.density_act);
+		const float dloss_by_dmlp = density_derivative * (dt * dot(grad, rgb * T - suffix));
+		dl[3] = __float2half(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
+		                     (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
+	}
+}
+
+// Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
+// c < B is repeated floor((B-1-j)/c) more times, each copy scaled by c/B.
+__global__ void k_rollover_weight(const uint32_t* __restrict__ total_ptr, uint32_t target, float* __restrict__ w) {
+	const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
+	const uint32_t c = min(*total_ptr, target);
+	if (j >= c) return;
+	const uint32_t copies = (target - 1 - j) / c;
+	w[j] = 1.0f + (float)copies * ((float)c / (float)target);
+}
+
+__global__ void k_clamp_count(const uint32_t* __restrict__ in, uint32_t cap, uint32_t* __restrict__ out) {
+	if (threadIdx.x == 0 && blockIdx.x == 0) *out = min(*in, cap);
+}
+
+// Sum of per-ray losses (deterministic two-level reduction).
+__global__ void __launch_bounds__(1024) k_sum_floats(const float* __restrict__ v, uint32_t n, float* __restrict__ out) {
+	__shared__ float part[1024];
+	float s = 0.0f;
+	for (uint32_t i = threadIdx.x; i < n; i += 1024) s += v[i];
+	part[threadIdx.x] = s;
+	__syncthreads();
+	for (int d = 512; d > 0; d >>= 1) {
+		if ((int)threadIdx.x < d) part[threadIdx.x] += part[threadIdx.x + d];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) *out = part[0];
+}
+
+// ---------------------------------------------------------------------------
+// Optimizer: Ema( ExponentialDecay( Adam ) ) in one pass over the parameters.
+// ---------------------------------------------------------------------------
+struct OptArgs {
+	uint64_t n, n_mlp;
+	float lr, beta1, beta2, eps, l2_reg, loss_scale;
+	float ema_decay, ema_debias_old, ema_debias_new;
+	int opt_mlp, opt_enc;
+	float* w32;
+	__half* w16;
+	float* grad;
+	float* m;
+	float* v;
+	uint32_t* steps;
+	float* ema32;
+	__half* ema16;
+};
+
+__global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n) return;
+	const float graw = a.grad[i];
+	float w = a.w32[i];
+	const bool is_mlp = i < a.n_mlp;
+	bool update = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
+	if (update) {
+		float g = graw / a.loss_scale;
+		if (is_mlp) g += a.l2_reg * w;
+		const float m = a.m[i] = a.beta1 * a.m[i] + (1.0f - a.beta1) * g;
+		const float v = a.v[i] = a.beta2 * a.v[i] + (1.0f - a.beta2) * g * g;
+		const uint32_t step = ++a.steps[i];
+		const float lr = a.lr * sqrtf(1.0f - powf(a.beta2, (float)step)) / (1.0f - powf(a.beta1, (float)step));
+		w = w - (lr / (sqrtf(v) + a.eps)) * m;
+		a.w32[i] = w;
+		a.w16[i] = __float2half(w);
+	}
+	if (graw != 0.0f) a.grad[i] = 0.0f;  // GradientMode::Overwrite for the next step
+	const float e = (a.ema32[i] * a.ema_decay * a.ema_debias_old + w * (1.0f - a.ema_decay)) / a.ema_debias_new;
+	a.ema32[i] = e;
+	a.ema16[i] = __float2half(e);
+}
+
+__global__ void k_to_half(const float* __restrict__ src, __half* __restrict__ dst, uint64_t n) {
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) dst[i] = __float2half(src[i]);
+}
+
+void launch_params_to_half(const float* src, __half* dst, size_t n, hipStream_t s) {
+	if (!n) return;
+	k_to_half<<<div_up(n, 256), 256, 0, s>>>(src, dst, n);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hipStream_t s) {
+	const ngp_network_config& c = m->cfg;
+	OptArgs a{};
+	a.n = m->n_params;
+	a.n_mlp = m->n_mlp_params;
+	// ExponentialDecay (configs/nerf/base.json:9-14): lr *= base at decay_start + k*interval
+	float lr = c.learning_rate;
+	if (c.decay_interval > 0 && step >= c.decay_start) {
+		const uint32_t k = (step - c.decay_start) / c.decay_interval + 1;
+		lr = c.learning_rate * powf(c.decay_base, (float)k);
+	}
+	a.lr = lr;
+	a.beta1 = c.beta1;
+	a.beta2 = c.beta2;
+	a.eps = c.epsilon;
+	a.l2_reg = c.l2_reg;
+	a.loss_scale = 128.0f;
+	a.ema_decay = c.ema_decay;
+	a.ema_debias_old = 1.0f - powf(c.ema_decay, (float)m->ema_step);
+	a.ema_debias_new = 1.0f - powf(c.ema_decay, (float)(m->ema_step + 1));
+	a.opt_mlp = opt_mlp;
+	a.opt_enc = opt_enc;
+	a.w32 = m->params32.ptr;
+	a.w16 = m->params16.ptr;
+	a.grad = m->grads.ptr;
+	a.m = m->adam_m.ptr;
+	a.v = m->adam_v.ptr;
+	a.steps = m->adam_steps.ptr;
+	a.ema32 = m->ema32.ptr;
+	a.ema16 = m->infer16.ptr;
+	k_optimizer<<<div_up(a.n, 256), 256, 0, s>>>(a);
+	NGP_HIP_CHECK(hipGetLastError());
+	++m->ema_step;
+	pack_mlp_fragments(m, m->params16.ptr, m->frag_train.ptr, s);
+	pack_mlp_fragments(m, m->infer16.ptr, m->frag_infer.ptr, s);
+}
+
+// ---------------------------------------------------------------------------
+// Host orchestration of one training step (Testbed::train_nerf_step).
+// ---------------------------------------------------------------------------
+void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
+	TrainScratch& ts = m->ts;
+	const uint32_t R = t->n_rays, B = t->target_batch_size, MS = t->max_samples;
+	const uint32_t L = m->lt.n_levels, F = m->lt.F;
+	ts.ray_numsteps.reserve(2 * (size_t)R);
+	ts.ray_compacted.reserve(2 * (size_t)R);
+	ts.ray_state.reserve(8 * (size_t)R);
+	ts.ray_loss_state.reserve(8 * (size_t)R);
+	ts.loss.reserve(R);
+	ts.coords.reserve(8 * (size_t)MS);
+	ts.enc.reserve((size_t)L * MS * F);
+	ts.mlp_out.reserve(4 * (size_t)MS);
+	ts.ccoords.reserve(8 * (size_t)B);
+	ts.cenc.reserve((size_t)L * B * F);
+	ts.dloss.reserve(4 * (size_t)B);
+	ts.cweight.reserve(B);
+	ts.denc.reserve((size_t)L * B * F);
+	ts.block_sums.reserve(div_up(std::max(R, 1u), 1024) + 16);
+	ts.counters.reserve(16);
+	ts.scan_a.reserve(2 * (size_t)R);
+	ts.scan_b.reserve(2 * (size_t)R);
+	DevBuf<uint32_t>& counts = ts.scan_a;
+	ts.last_n_rays = R;
+	ts.last_target = B;
+	ts.last_max_samples = MS;
+
+	NGP_HIP_CHECK(hipMemsetAsync(ts.counters.ptr, 0, 16 * sizeof(uint32_t), s));
+
+	SamplerArgs sa{};
+	sa.images = t->images;
+	sa.n_images = t->n_images;
+	sa.n_rays = R;
+	sa.n_rays_global = t->n_rays_global ? t->n_rays_global : R;
+	sa.ray_offset = t->ray_index_offset;
+	sa.max_samples = MS;
+	sa.rng.state = t->rng_state;
+	sa.rng.inc = t->rng_inc;
+	sa.aabb.min = mk3(t->aabb_min[0], t->aabb_min[1], t->aabb_min[2]);
+	sa.aabb.max = mk3(t->aabb_max[0], t->aabb_max[1], t->aabb_max[2]);
+	sa.cone_angle = t->cone_angle_constant;
+	sa.max_mip = t->max_cascade;
+	sa.snap = t->snap_to_pixel_centers;
+	sa.bitfield = m->gs.bitfield.ptr;
+	sa.numsteps = ts.ray_numsteps.ptr;
+	sa.counts = counts.ptr;
+	sa.bases = counts.ptr + R;
+	sa.ray_state = ts.ray_state.ptr;
+	sa.coords = ts.coords.ptr;
+	const uint32_t rb = div_up(R, 256);
+	k_sample_count<<<rb, 256, 0, s>>>(sa);
+	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
+	k_sample_write<<<rb, 256, 0, s>>>(sa);
+	NGP_HIP_CHECK(hipGetLastError());
+
+	// network inference over every emitted sample (NerfNetwork::inference_mixed_precision, training params)
+	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
+	launch_hashgrid_fwd(m->lt, ts.coords.ptr, 8, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
+	                    ts.counters.ptr + 4);
+	launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
+	                 ts.counters.ptr + 4);
+
+	LossArgs la{};
+	la.images = t->images;
+	la.n_images = t->n_images;
+	la.n_rays = R;
+	la.n_rays_global = sa.n_rays_global;
+	la.ray_offset = t->ray_index_offset;
+	la.rng = sa.rng;
+	la.aabb = sa.aabb;
+	la.snap = t->snap_to_pixel_centers;
+	la.loss_type = t->loss_type;
+	la.random_bg = t->random_bg_color;
+	la.bg = mk3(t->background_color[0], t->background_color[1], t->background_color[2]);
+	la.linear_colors = t->train_in_linear_colors;
+	la.color_space = t->color_space;
+	la.rgb_act = m->cfg.rgb_activation;
+	la.density_act = m->cfg.density_activation;
+	la.near_distance = t->near_distance;
+	la.max_compacted = B;
+	la.target_batch = B;
+	la.numsteps = ts.ray_numsteps.ptr;
+	la.ray_state = ts.ray_state.ptr;
+	la.coords = ts.coords.ptr;
+	la.mlp_out = ts.mlp_out.ptr;
+	la.enc = ts.enc.ptr;
+	la.enc_plane = MS;
+	la.n_levels = L;
+	la.F = F;
+	la.ccounts = ts.scan_b.ptr;
+	la.cbases = ts.scan_b.ptr + R;
+	la.loss_state = ts.ray_loss_state.ptr;
+	la.compacted = ts.ray_compacted.ptr;
+	la.loss_out = ts.loss.ptr;
+	la.ccoords = ts.ccoords.ptr;
+	la.cenc = ts.cenc.ptr;
+	la.dloss = ts.dloss.ptr;
+	la.mean_density = m->gs.mean.ptr;
+	k_loss_composite<<<rb, 256, 0, s>>>(la);
+	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
+	k_loss_emit<<<rb, 256, 0, s>>>(la);
+	NGP_HIP_CHECK(hipGetLastError());
+
+	// compacted batch size c = min(total, B); rollover multiplicity
+	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
+	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
+	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
+
+	// fused MLP forward+backward, then hash-grid scatter (Trainer::training_step)
+	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, B, ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
+	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5);
+	launch_hashgrid_bwd(m->lt, ts.ccoords.ptr, 8, B, ts.denc.ptr, B, m->grads.ptr + m->n_mlp_params, s,
+	                    ts.counters.ptr + 5);
+
+	if (!t->defer_optimizer) launch_optimizer(m, t->training_step, t->optimize_mlp, t->optimize_encoding, s);
+	m->stats_pending = true;
+}
+
+}  // namespace ngp

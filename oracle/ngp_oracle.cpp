@@ -1,0 +1,1254 @@
+// ngp_oracle.cpp — TEST INFRASTRUCTURE ONLY.
+//
+// Scalar CPU restatement of the Instant-NGP NeRF hot path of the reference
+// (fnysalehi/instant-ngp-rendering).  Only tests/, __graft_entry__.smoke() and
+// bench.py's cpu_baseline leg may load this library; the product path
+// (libngp_hip.so) never calls it.
+//
+// Parity status: the reference cannot be compiled here (CUDA sources, no nvcc,
+// empty tiny-cuda-nn submodule) and ships no tests or golden vectors, so the
+// tcnn-side pieces (hash grid, SH, MLP, Adam/Ema) are restated from the public
+// tiny-cuda-nn algorithm -> "parity unpinned" for those.
+// The in-tree pieces (sampler, compositing/loss, occupancy grid, tracer) follow
+// the cited reference lines; pcg32, Sobol and SH are pinned by published
+// known-answer values in tests/test_oracle.py.
+//
+// Deliberate, documented deviations shared with the HIP path:
+//  * sample/ray compaction is by exclusive prefix sum in ray-index order
+//    instead of atomicAdd order (same cap rule, deterministic);
+//  * hash-grid features and MLP products accumulate in fp32 (tcnn: fp16);
+//  * the rollover copies of fill_rollover_and_rescale are folded into a
+//    per-sample multiplicity weight (mathematically identical gradient);
+//  * the occupancy mean is an exact 2^-24 fixed-point sum.
+//
+// Built by oracle/Makefile with g++ -O2 -ffp-contract=off (no fast-math).
+#include <algorithm>
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+#include "../include/ngp_hip.h"
+
+namespace oref {
+
+// ---------------------------------------------------------------------------
+// fp16 <-> fp32 (IEEE binary16, round to nearest even)
+// ---------------------------------------------------------------------------
+static float h2f(uint16_t h) {
+	const uint32_t s = (uint32_t)(h >> 15) << 31, e = (h >> 10) & 0x1f, m = h & 0x3ff;
+	uint32_t b;
+	if (e == 0) {
+		if (m == 0) b = s;
+		else {  // subnormal
+			float f = (float)m * (1.0f / 16777216.0f);
+			std::memcpy(&b, &f, 4);
+			b |= s;
+		}
+	} else if (e == 31) b = s | 0x7f800000u | (m << 13);
+	else b = s | ((e + 112) << 23) | (m << 13);
+	float f;
+	std::memcpy(&f, &b, 4);
+	return f;
+}
+static uint16_t f2h(float f) {
+	uint32_t x;
+	std::memcpy(&x, &f, 4);
+	const uint32_t sign = (x >> 16) & 0x8000u;
+	const uint32_t absx = x & 0x7fffffffu;
+	if (absx >= 0x7f800000u) return (uint16_t)(sign | 0x7c00u | (absx > 0x7f800000u ? 0x200u : 0u));
+	if (absx >= 0x477ff000u) return (uint16_t)(sign | 0x7c00u);  // overflow -> inf (>= 65520)
+	if (absx < 0x38800000u) {  // subnormal half or zero
+		float af;
+		std::memcpy(&af, &absx, 4);
+		const float scaled = af * 16777216.0f;  // 2^24
+		uint32_t q = (uint32_t)std::nearbyint(scaled);
+		return (uint16_t)(sign | q);
+	}
+	uint32_t mant = absx & 0x7fffffu;
+	uint32_t exp = (absx >> 23) - 112;
+	uint32_t r = (exp << 10) | (mant >> 13);
+	const uint32_t rem = mant & 0x1fffu;
+	if (rem > 0x1000u || (rem == 0x1000u && (r & 1u))) ++r;
+	return (uint16_t)(sign | r);
+}
+static float rh(float f) { return h2f(f2h(f)); }
+
+// ---------------------------------------------------------------------------
+// Small vector math (tcnn vec3 semantics, component-wise IEEE float)
+// ---------------------------------------------------------------------------
+struct V3 {
+	float x, y, z;
+};
+static V3 v(float x, float y, float z) { return {x, y, z}; }
+static V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
+static V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
+static V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+static V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
+static float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
+static float len(V3 a) { return std::sqrt(dot(a, a)); }
+static V3 normalize(V3 a) { return a * (1.0f / len(a)); }
+
+struct Box {
+	V3 mn, mx;
+	bool contains(V3 p) const { return p.x >= mn.x && p.x <= mx.x && p.y >= mn.y && p.y <= mx.y && p.z >= mn.z && p.z <= mx.z; }
+	V3 rel(V3 p) const { return (p - mn) / (mx - mn); }
+	// bounding_box.cuh:172-219
+	void intersect(V3 o, V3 d, float* t0, float* t1) const {
+		const float FMAX = 3.402823466e+38f;
+		float tmin = (mn.x - o.x) / d.x, tmax = (mx.x - o.x) / d.x;
+		if (tmin > tmax) std::swap(tmin, tmax);
+		float tymin = (mn.y - o.y) / d.y, tymax = (mx.y - o.y) / d.y;
+		if (tymin > tymax) std::swap(tymin, tymax);
+		if (tmin > tymax || tymin > tmax) { *t0 = *t1 = FMAX; return; }
+		if (tymin > tmin) tmin = tymin;
+		if (tymax < tmax) tmax = tymax;
+		float tzmin = (mn.z - o.z) / d.z, tzmax = (mx.z - o.z) / d.z;
+		if (tzmin > tzmax) std::swap(tzmin, tzmax);
+		if (tmin > tzmax || tzmin > tmax) { *t0 = *t1 = FMAX; return; }
+		if (tzmin > tmin) tmin = tzmin;
+		if (tzmax < tmax) tmax = tzmax;
+		*t0 = tmin;
+		*t1 = tmax;
+	}
+};
+
+// ---------------------------------------------------------------------------
+// pcg32 (tcnn/pcg32.h; default_rng_t, random_val.cuh:26)
+// ---------------------------------------------------------------------------
+struct Pcg {
+	uint64_t state = 0x853c49e6748fea9bULL, inc = 0xda3e39cb94b95bdbULL;
+	void seed(uint64_t s, uint64_t q = 1) {
+		state = 0;
+		inc = (q << 1) | 1;
+		next();
+		state += s;
+		next();
+	}
+	uint32_t next() {
+		const uint64_t old = state;
+		state = old * 0x5851f42d4c957f2dULL + inc;
+		const uint32_t xs = (uint32_t)(((old >> 18u) ^ old) >> 27u);
+		const uint32_t rot = (uint32_t)(old >> 59u);
+		return (xs >> rot) | (xs << ((-(int32_t)rot) & 31));
+	}
+	float nextf() {
+		uint32_t u = (next() >> 9) | 0x3f800000u;
+		float f;
+		std::memcpy(&f, &u, 4);
+		return f - 1.0f;
+	}
+	void advance(int64_t delta_ = (1ll << 32)) {
+		uint64_t cm = 0x5851f42d4c957f2dULL, cp = inc, am = 1, ap = 0, delta = (uint64_t)delta_;
+		while (delta > 0) {
+			if (delta & 1) {
+				am *= cm;
+				ap = ap * cm + cp;
+			}
+			cp = (cm + 1) * cp;
+			cm *= cm;
+			delta /= 2;
+		}
+		state = am * state + ap;
+	}
+};
+
+// ---------------------------------------------------------------------------
+// Sobol / Laine-Karras (random_val.cuh:162-325): only dims 0 and 1.
+// ---------------------------------------------------------------------------
+static const uint32_t SOBOL_DIM1_FIRST8[8] = {0x80000000u, 0xc0000000u, 0xa0000000u, 0xf0000000u,
+                                              0x88000000u, 0xcc000000u, 0xaa000000u, 0xff000000u};
+static uint32_t sobol(uint32_t index, uint32_t dim) {
+	uint32_t X = 0, dirn = 0x80000000u;
+	for (uint32_t bit = 0; bit < 32; ++bit) {
+		const uint32_t d = dim == 0 ? (0x80000000u >> bit) : dirn;
+		if (bit < 8 && dim == 1 && d != SOBOL_DIM1_FIRST8[bit]) throw std::logic_error("sobol table");
+		if ((index >> bit) & 1) X ^= d;
+		dirn ^= dirn >> 1;
+	}
+	return X;
+}
+static uint32_t rev(uint32_t x) {
+	uint32_t r = 0;
+	for (int i = 0; i < 32; ++i) r |= ((x >> i) & 1u) << (31 - i);
+	return r;
+}
+static uint32_t lk(uint32_t x, uint32_t seed) {
+	x += seed;
+	x ^= x * 0x6c50b47cu;
+	x ^= x * 0xb82f1e52u;
+	x ^= x * 0xc7afe638u;
+	x ^= x * 0x8d22f6e6u;
+	return x;
+}
+static uint32_t scramble(uint32_t x, uint32_t seed) { return rev(lk(rev(x), seed)); }
+static uint32_t hcomb(uint32_t seed, uint32_t v) { return seed ^ (v + (seed << 6) + (seed >> 2)); }
+static float ldval(uint32_t index, uint32_t seed, uint32_t dim) {
+	index = scramble(index, seed);
+	return (float)scramble(sobol(index, dim), hcomb(seed, dim)) * (float)(1.0 / 4294967296.0);
+}
+static float fract(float x) { return x - std::floor(x); }
+static void pixel_offset(uint32_t spp, float* ox, float* oy) {
+	*ox = fract(0.5f - ldval(0, 0xdeadbeefu, 0) + ldval(spp, 0xdeadbeefu, 0));
+	*oy = fract(0.5f - ldval(0, 0xdeadbeefu, 1) + ldval(spp, 0xdeadbeefu, 1));
+}
+
+// ---------------------------------------------------------------------------
+// Morton (tcnn morton3D)
+// ---------------------------------------------------------------------------
+static uint32_t morton(uint32_t x, uint32_t y, uint32_t z) {
+	uint32_t r = 0;
+	for (int b = 0; b < 10; ++b) r |= ((x >> b) & 1u) << (3 * b) | ((y >> b) & 1u) << (3 * b + 1) | ((z >> b) & 1u) << (3 * b + 2);
+	return r;
+}
+static uint32_t morton_inv(uint32_t m) {
+	uint32_t r = 0;
+	for (int b = 0; b < 10; ++b) r |= ((m >> (3 * b)) & 1u) << b;
+	return r;
+}
+
+// ---------------------------------------------------------------------------
+// NeRF constants and stepping (nerf_device.cuh:24-42, 359-494)
+// ---------------------------------------------------------------------------
+static const uint32_t GRID = 128, CELLS = GRID * GRID * GRID, STEPS = 1024, CASCADES = 8;
+static const float SQRT3_ = 1.73205080757f;
+static const float MIN_STEP = SQRT3_ / 1024.0f;
+static const float MAX_STEP = MIN_STEP * 128.0f * 1024.0f / 128.0f;
+static const float MAXD = 16384.0f;
+
+static float sgn(float x) { return x > 0 ? 1.0f : (x < 0 ? -1.0f : 0.0f); }
+static float to_step(float t, float c) {
+	if (c <= 1e-5f) return t / MIN_STEP;
+	const float l = std::log(1.0f + c);
+	const float a = (std::log(MIN_STEP) - std::log(l)) / l, b = (std::log(MAX_STEP) - std::log(l)) / l;
+	const float at = std::exp(a * l), bt = std::exp(b * l);
+	if (t <= at) return (t - at) / MIN_STEP + a;
+	if (t <= bt) return std::log(t) / l;
+	return (t - bt) / MAX_STEP + b;
+}
+static float from_step(float n, float c) {
+	if (c <= 1e-5f) return n * MIN_STEP;
+	const float l = std::log(1.0f + c);
+	const float a = (std::log(MIN_STEP) - std::log(l)) / l, b = (std::log(MAX_STEP) - std::log(l)) / l;
+	const float at = std::exp(a * l), bt = std::exp(b * l);
+	if (n <= a) return (n - a) * MIN_STEP + at;
+	if (n <= b) return std::exp(n * l);
+	return (n - b) * MAX_STEP + bt;
+}
+static float adv_n(float t, float c, float n) { return from_step(to_step(t, c) + n, c); }
+static float calc_dt(float t, float c) { return adv_n(t, c, 1.0f) - t; }
+static float dist_next_voxel(V3 p0, V3 d, V3 idir, float res) {
+	const V3 p = (p0 - v(0.5f, 0.5f, 0.5f)) * res;
+	const float tx = (std::floor(p.x + 0.5f + 0.5f * sgn(d.x)) - p.x) * idir.x;
+	const float ty = (std::floor(p.y + 0.5f + 0.5f * sgn(d.y)) - p.y) * idir.y;
+	const float tz = (std::floor(p.z + 0.5f + 0.5f * sgn(d.z)) - p.z) * idir.z;
+	return std::max(std::min(std::min(tx, ty), tz) / res, 0.0f);
+}
+static float adv_voxel(float t, float c, V3 pos, V3 d, V3 idir, uint32_t mip) {
+	const float res = std::scalbn((float)GRID, -(int)mip);
+	float tt = t + dist_next_voxel(pos, d, idir, res);
+	t = to_step(t, c);
+	tt = to_step(tt, c);
+	return from_step(t + std::ceil(std::max(tt - t, 0.5f)), c);
+}
+static uint32_t mip_pos(V3 p, uint32_t maxc = CASCADES - 1) {
+	int e;
+	std::frexp(std::max(std::max(std::fabs(p.x - 0.5f), std::fabs(p.y - 0.5f)), std::fabs(p.z - 0.5f)), &e);
+	return (uint32_t)std::min(std::max(e + 1, 0), (int)maxc);
+}
+static uint32_t mip_dt(float dt, V3 p, uint32_t maxc) {
+	const uint32_t mip = mip_pos(p, maxc);
+	dt *= 2.0f * GRID;
+	if (dt < 1.0f) return mip;
+	int e;
+	std::frexp(dt, &e);
+	return (uint32_t)std::min(std::max((int)mip, e), (int)maxc);
+}
+static uint32_t grid_idx(V3 p, uint32_t mip) {
+	const float s = std::scalbn(1.0f, -(int)mip);
+	p = p - v(0.5f, 0.5f, 0.5f);
+	p = p * s;
+	p = p + v(0.5f, 0.5f, 0.5f);
+	const int ix = (int)(p.x * (float)GRID), iy = (int)(p.y * (float)GRID), iz = (int)(p.z * (float)GRID);
+	if (ix < 0 || ix >= (int)GRID || iy < 0 || iy >= (int)GRID || iz < 0 || iz >= (int)GRID) return 0xFFFFFFFFu;
+	return morton((uint32_t)ix, (uint32_t)iy, (uint32_t)iz);
+}
+static bool occupied(V3 p, const uint8_t* bits, uint32_t mip) {
+	const uint32_t i = grid_idx(p, mip);
+	if (i == 0xFFFFFFFFu) return false;
+	return bits[i / 8 + CELLS / 8 * mip] & (1u << (i % 8));
+}
+static float skip_empty(float t, float c, V3 o, V3 d, V3 idir, const uint8_t* bits, uint32_t maxm, const Box& b) {
+	while (true) {
+		const V3 pos = o + d * t;
+		if (t >= MAXD || !b.contains(pos)) return MAXD;
+		uint32_t mip = std::min(mip_pos(pos), maxm);
+		if (!bits || occupied(pos, bits, mip)) return t;
+		while (mip < maxm && !occupied(pos, bits, mip + 1)) ++mip;
+		t = adv_voxel(t, c, pos, d, idir, mip);
+	}
+}
+static float warp_dt(float dt) { return (dt - MIN_STEP) / (MIN_STEP * 128.0f - MIN_STEP); }
+static float unwarp_dt(float w) { return w * (MIN_STEP * 128.0f - MIN_STEP) + MIN_STEP; }
+
+// ---------------------------------------------------------------------------
+// Colour, activations, losses (common_device.cuh:34-80, nerf_device.cuh:74-263,600-615)
+// ---------------------------------------------------------------------------
+static float s2l(float s) { return s <= 0.04045f ? s / 12.92f : std::pow((s + 0.055f) / 1.055f, 2.4f); }
+static float l2s(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * std::pow(l, 0.41666f) - 0.055f; }
+static float logistic(float x) { return 1.0f / (1.0f + std::exp(-x)); }
+static float to_rgb(float x, int a) {
+	switch (a) {
+		case 1: return x > 0 ? x : 0;
+		case 2: return logistic(x);
+		case 3: return std::exp(std::min(std::max(x, -10.0f), 10.0f));
+		default: return x;
+	}
+}
+static float to_rgb_d(float x, int a) {
+	switch (a) {
+		case 1: return x > 0 ? 1.0f : 0.0f;
+		case 2: { const float d = logistic(x); return d * (1 - d); }
+		case 3: return std::exp(std::min(std::max(x, -10.0f), 10.0f));
+		default: return 1.0f;
+	}
+}
+static float to_density(float x, int a) {
+	switch (a) {
+		case 1: return x > 0 ? x : 0;
+		case 2: return logistic(x);
+		case 3: return std::exp(x);
+		default: return x;
+	}
+}
+static float to_density_d(float x, int a) {
+	switch (a) {
+		case 1: return x > 0 ? 1.0f : 0.0f;
+		case 2: { const float d = logistic(x); return d * (1 - d); }
+		case 3: return std::exp(std::min(std::max(x, -15.0f), 15.0f));
+		default: return 1.0f;
+	}
+}
+static void lossg(float target, float pred, int type, float* l, float* g) {
+	const float d = pred - target;
+	switch (type) {
+		case 6: { const float den = pred * pred + 1e-2f; *l = d * d / den; *g = 2 * d / den; } break;
+		case 1: *l = std::fabs(d); *g = std::copysign(1.0f, d); break;
+		case 2: { const float den = std::fabs(pred) + 1e-2f; *l = std::fabs(d) / den; *g = std::copysign(1.0f / den, d); } break;
+		case 3: { const float den = 0.5f * (std::fabs(pred) + std::fabs(target)) + 1e-2f; *l = std::fabs(d) / den; *g = std::copysign(1.0f / den, d); } break;
+		case 4: {
+			const float ad = std::fabs(d), sq = 0.5f / 0.1f * d * d;
+			*l = (ad > 0.1f ? ad - 0.05f : sq) / 5.0f;
+			*g = (ad > 0.1f ? (d > 0 ? 1.0f : -1.0f) : d / 0.1f) / 5.0f;
+		} break;
+		case 5: { const float dv = std::fabs(d) + 1.0f; *l = std::log(dv); *g = std::copysign(1.0f / dv, d); } break;
+		default: *l = d * d; *g = 2 * d; break;
+	}
+}
+
+// ---------------------------------------------------------------------------
+// Model
+// ---------------------------------------------------------------------------
+struct Layer {
+	uint32_t out, in;
+	uint64_t off;
+	bool relu_out, relu_in;
+};
+
+struct Model {
+	ngp_network_config cfg{};
+	uint32_t L = 0, F = 0, E = 0, Epad = 0;
+	std::vector<float> scale;
+	std::vector<uint32_t> res, offset, size, hashed;
+	std::vector<Layer> layers;
+	uint32_t n_density_layers = 0;
+	uint64_t n_mlp = 0, n_grid = 0, n = 0;
+	std::vector<float> p32, ema32, grads, m, vv;
+	std::vector<uint16_t> p16, inf16;
+	std::vector<uint32_t> steps;
+	uint32_t ema_step = 0;
+	// occupancy
+	std::vector<float> grid, tmp;
+	std::vector<uint8_t> bits;
+	float mean = 0.0f;
+	// last training step scratch (ngp_train_scratch mirror)
+	std::vector<uint32_t> ray_numsteps, ray_compacted;
+	std::vector<float> coords, ccoords, loss;
+	std::vector<uint16_t> mlp_out, dloss;
+	uint32_t total_samples = 0, total_compacted = 0;
+	float loss_sum = 0.0f;
+};
+
+// tcnn GridEncodingTemplated ctor; hash-grid auto params in src/testbed.cu:3680-3724
+static void build(Model& M) {
+	const auto& c = M.cfg;
+	M.L = c.n_levels;
+	M.F = c.n_features_per_level;
+	M.E = M.L * M.F;
+	M.Epad = (M.E + 15) / 16 * 16;
+	const float lg = std::log2(c.per_level_scale);
+	uint32_t off = 0;
+	for (uint32_t l = 0; l < M.L; ++l) {
+		const float s = std::exp2((float)l * lg) * (float)c.base_resolution - 1.0f;
+		const uint32_t r = (uint32_t)std::ceil(s) + 1;
+		const double dense = (double)r * r * r;
+		uint32_t p = dense > (double)(0xFFFFFFFFu / 2) ? 0xFFFFFFFFu / 2 : r * r * r;
+		p = (p + 7) / 8 * 8;
+		p = std::min(p, 1u << c.log2_hashmap_size);
+		M.scale.push_back(s);
+		M.res.push_back(r);
+		M.offset.push_back(off);
+		M.size.push_back(p);
+		M.hashed.push_back(dense > (double)p ? 1u : 0u);
+		off += p;
+	}
+	M.n_grid = (uint64_t)off * M.F;
+	const uint32_t W = c.n_neurons;
+	auto add = [&](uint32_t out, uint32_t in, bool ro, bool ri) { M.layers.push_back({out, in, 0, ro, ri}); };
+	add(W, M.Epad, true, false);
+	for (uint32_t h = 1; h < c.density_hidden_layers; ++h) add(W, W, true, true);
+	add(16, W, false, true);
+	M.n_density_layers = (uint32_t)M.layers.size();
+	add(W, 32, true, false);
+	for (uint32_t h = 1; h < c.rgb_hidden_layers; ++h) add(W, W, true, true);
+	add(16, W, false, true);
+	uint64_t o = 0;
+	for (auto& Ly : M.layers) {
+		Ly.off = o;
+		o += (uint64_t)Ly.out * Ly.in;
+	}
+	M.n_mlp = o;
+	M.n = M.n_mlp + M.n_grid;
+	M.p32.assign(M.n, 0.0f);
+	M.ema32.assign(M.n, 0.0f);
+	M.grads.assign(M.n, 0.0f);
+	M.m.assign(M.n, 0.0f);
+	M.vv.assign(M.n, 0.0f);
+	M.p16.assign(M.n, 0);
+	M.inf16.assign(M.n, 0);
+	M.steps.assign(M.n, 0);
+	M.grid.assign(CELLS, 0.0f);
+	M.bits.assign(CELLS / 8 * CASCADES, 0xff);
+}
+
+// ---- hash grid (tcnn grid.h: pos_fract, grid_index with CoherentPrime hash) -----------------
+static uint32_t hg_index(const Model& M, uint32_t l, uint32_t x, uint32_t y, uint32_t z) {
+	uint32_t idx;
+	if (M.hashed[l]) idx = (x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u);
+	else idx = x + y * M.res[l] + z * M.res[l] * M.res[l];
+	return idx % M.size[l];
+}
+static void hg_corners(const Model& M, uint32_t l, const float* p, uint32_t idx[8], float w[8]) {
+	float fr[3];
+	uint32_t g[3];
+	for (int d = 0; d < 3; ++d) {
+		const float q = std::fma(M.scale[l], p[d], 0.5f);
+		const float f = std::floor(q);
+		g[d] = (uint32_t)(int)f;
+		fr[d] = q - f;
+	}
+	for (uint32_t c = 0; c < 8; ++c) {
+		float ww = 1.0f;
+		ww *= (c & 1) ? fr[0] : 1.0f - fr[0];
+		ww *= (c & 2) ? fr[1] : 1.0f - fr[1];
+		ww *= (c & 4) ? fr[2] : 1.0f - fr[2];
+		idx[c] = hg_index(M, l, g[0] + (c & 1), g[1] + ((c >> 1) & 1), g[2] + ((c >> 2) & 1));
+		w[c] = ww;
+	}
+}
+// enc: [L][n][F] (fp16-rounded floats)
+static void hg_forward(const Model& M, const uint16_t* params, const float* pos, uint32_t stride, uint32_t n, float* enc) {
+	const uint16_t* tab = params + M.n_mlp;
+	for (uint32_t i = 0; i < n; ++i)
+		for (uint32_t l = 0; l < M.L; ++l) {
+			uint32_t idx[8];
+			float w[8];
+			hg_corners(M, l, pos + (size_t)i * stride, idx, w);
+			for (uint32_t f = 0; f < M.F; ++f) {
+				float acc = 0.0f;
+				for (int c = 0; c < 8; ++c) acc = std::fma(w[c], h2f(tab[((size_t)M.offset[l] + idx[c]) * M.F + f]), acc);
+				enc[((size_t)l * n + i) * M.F + f] = rh(acc);
+			}
+		}
+}
+static void hg_backward(Model& M, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
+	float* g = M.grads.data() + M.n_mlp;
+	for (uint32_t i = 0; i < n; ++i)
+		for (uint32_t l = 0; l < M.L; ++l) {
+			bool any = false;
+			for (uint32_t f = 0; f < M.F; ++f) any |= denc[((size_t)l * n + i) * M.F + f] != 0.0f;
+			if (!any) continue;
+			uint32_t idx[8];
+			float w[8];
+			hg_corners(M, l, pos + (size_t)i * stride, idx, w);
+			for (int c = 0; c < 8; ++c)
+				for (uint32_t f = 0; f < M.F; ++f)
+					g[((size_t)M.offset[l] + idx[c]) * M.F + f] += w[c] * denc[((size_t)l * n + i) * M.F + f];
+		}
+}
+
+// ---- spherical harmonics degree 4 (tcnn SphericalHarmonicsEncoding) --------------------------
+static void sh4(const float* wdir, float* o) {
+	const float x = wdir[0] * 2.0f - 1.0f, y = wdir[1] * 2.0f - 1.0f, z = wdir[2] * 2.0f - 1.0f;
+	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+	o[0] = 0.28209479177387814f;
+	o[1] = -0.48860251190291987f * y;
+	o[2] = 0.48860251190291987f * z;
+	o[3] = -0.48860251190291987f * x;
+	o[4] = 1.0925484305920792f * xy;
+	o[5] = -1.0925484305920792f * yz;
+	o[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+	o[7] = -1.0925484305920792f * xz;
+	o[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+	o[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+	o[10] = 2.8906114426405538f * xy * z;
+	o[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+	o[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+	o[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+	o[14] = 1.4453057213202769f * z * (x2 - y2);
+	o[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+	for (int k = 0; k < 16; ++k) o[k] = rh(o[k]);
+}
+
+// ---- MLP (NerfNetwork: density MLP -> [density_out | SH] -> rgb MLP), fp16 I/O, fp32 sums ------
+struct Acts {
+	std::vector<std::vector<float>> a;  // a[l] = input of layer l (fp16-rounded), a[NL] = final output
+};
+static void layer_fwd(const Model& M, const uint16_t* P, const Layer& Ly, const std::vector<float>& in, std::vector<float>& out,
+                      bool round) {
+	out.assign(Ly.out, 0.0f);
+	const uint16_t* W = P + Ly.off;
+	for (uint32_t r = 0; r < Ly.out; ++r) {
+		float acc = 0.0f;
+		for (uint32_t k = 0; k < Ly.in; ++k) acc += h2f(W[(size_t)r * Ly.in + k]) * in[k];
+		if (Ly.relu_out) acc = std::max(acc, 0.0f);
+		out[r] = round ? rh(acc) : acc;
+	}
+}
+static void mlp_forward_one(const Model& M, const uint16_t* P, const float* enc_col /*E*/, const float* wdir, Acts& A) {
+	const uint32_t NL = (uint32_t)M.layers.size();
+	A.a.assign(NL + 1, {});
+	A.a[0].assign(M.Epad, 0.0f);
+	for (uint32_t k = 0; k < M.E; ++k) A.a[0][k] = enc_col[k];
+	for (uint32_t l = 0; l < NL; ++l) {
+		if (l == M.n_density_layers) {
+			// rgb input = [density_out(16) | SH(16)]
+			std::vector<float> x(32);
+			for (int k = 0; k < 16; ++k) x[k] = A.a[l][k];
+			float sh[16];
+			sh4(wdir, sh);
+			for (int k = 0; k < 16; ++k) x[16 + k] = sh[k];
+			A.a[l] = x;
+		}
+		layer_fwd(M, P, M.layers[l], A.a[l], A.a[l + 1], true);
+	}
+}
+static void gather_enc(const Model& M, const float* enc, uint32_t n, uint32_t i, float* col) {
+	for (uint32_t k = 0; k < M.E; ++k) col[k] = enc[((size_t)(k / M.F) * n + i) * M.F + (k % M.F)];
+}
+// out: [n][4] = rgb raw (3) + density raw (fp16-rounded)
+static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, const float* coords, uint32_t cs, uint32_t n,
+                        float* out) {
+	std::vector<float> col(M.E);
+	Acts A;
+	for (uint32_t i = 0; i < n; ++i) {
+		gather_enc(M, enc, n, i, col.data());
+		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A);
+		const uint32_t NL = (uint32_t)M.layers.size();
+		out[4 * i + 0] = A.a[NL][0];
+		out[4 * i + 1] = A.a[NL][1];
+		out[4 * i + 2] = A.a[NL][2];
+		out[4 * i + 3] = A.a[M.n_density_layers][0];  // density_out row 0 (first rgb-layer input)
+	}
+}
+// NerfNetwork::backward_impl (nerf_network.h:189-268): rgb MLP bwd -> add_density_gradient -> density MLP bwd
+static void mlp_backward(Model& M, const uint16_t* P, const float* enc, const float* coords, uint32_t cs, uint32_t n,
+                         const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc) {
+	const uint32_t NL = (uint32_t)M.layers.size();
+	std::vector<float> col(M.E);
+	Acts A;
+	for (uint32_t i = 0; i < n; ++i) {
+		gather_enc(M, enc, n, i, col.data());
+		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A);
+		const float w = weight ? weight[i] : 1.0f;
+		std::vector<float> delta(16, 0.0f);
+		for (int r = 0; r < 3; ++r) delta[r] = rh(dl[4 * i + r] * w);
+		for (int l = (int)NL - 1; l >= 0; --l) {
+			const Layer& Ly = M.layers[l];
+			const std::vector<float>& in = A.a[l];
+			const uint16_t* W = P + Ly.off;
+			float* G = M.grads.data() + Ly.off;
+			for (uint32_t r = 0; r < Ly.out; ++r)
+				for (uint32_t k = 0; k < Ly.in; ++k) G[(size_t)r * Ly.in + k] += delta[r] * in[k];
+			const uint32_t nin = (l == (int)M.n_density_layers) ? 16 : Ly.in;
+			std::vector<float> nd(nin, 0.0f);
+			for (uint32_t k = 0; k < nin; ++k) {
+				float acc = 0.0f;
+				for (uint32_t r = 0; r < Ly.out; ++r) acc += h2f(W[(size_t)r * Ly.in + k]) * delta[r];
+				if (Ly.relu_in && !(in[k] > 0.0f)) acc = 0.0f;
+				if (l == (int)M.n_density_layers && k == 0) acc += h2f(f2h(dl[4 * i + 3])) * w;
+				nd[k] = rh(acc);
+			}
+			if (l == 0) {
+				for (uint32_t k = 0; k < M.E; ++k) denc[((size_t)(k / M.F) * n + i) * M.F + (k % M.F)] = nd[k];
+			}
+			delta = nd;
+		}
+	}
+}
+
+// ---- optimizer: Ema(ExponentialDecay(Adam)) (tcnn; configs/nerf/base.json:5-22) --------------
+static void optimizer(Model& M, uint32_t step, int opt_mlp, int opt_enc) {
+	const auto& c = M.cfg;
+	float lr = c.learning_rate;
+	if (c.decay_interval > 0 && step >= c.decay_start) lr = c.learning_rate * std::pow(c.decay_base, (float)((step - c.decay_start) / c.decay_interval + 1));
+	const float dold = 1.0f - std::pow(c.ema_decay, (float)M.ema_step), dnew = 1.0f - std::pow(c.ema_decay, (float)(M.ema_step + 1));
+	for (uint64_t i = 0; i < M.n; ++i) {
+		const float graw = M.grads[i];
+		float w = M.p32[i];
+		const bool mlp = i < M.n_mlp;
+		if (mlp ? (bool)opt_mlp : (opt_enc && graw != 0.0f)) {
+			float g = graw / 128.0f;
+			if (mlp) g += c.l2_reg * w;
+			M.m[i] = c.beta1 * M.m[i] + (1.0f - c.beta1) * g;
+			M.vv[i] = c.beta2 * M.vv[i] + (1.0f - c.beta2) * g * g;
+			const uint32_t s = ++M.steps[i];
+			const float l = lr * std::sqrt(1.0f - std::pow(c.beta2, (float)s)) / (1.0f - std::pow(c.beta1, (float)s));
+			w = w - (l / (std::sqrt(M.vv[i]) + c.epsilon)) * M.m[i];
+			M.p32[i] = w;
+			M.p16[i] = f2h(w);
+		}
+		M.grads[i] = 0.0f;
+		const float e = (M.ema32[i] * c.ema_decay * dold + w * (1.0f - c.ema_decay)) / dnew;
+		M.ema32[i] = e;
+		M.inf16[i] = f2h(e);
+	}
+	++M.ema_step;
+}
+
+// ---- training images ------------------------------------------------------------------------
+struct Cam {
+	V3 c[4];
+};
+static Cam cam_of(const float* x) {
+	Cam m;
+	for (int k = 0; k < 4; ++k) m.c[k] = v(x[3 * k], x[3 * k + 1], x[3 * k + 2]);
+	return m;
+}
+static V3 rot(const Cam& m, V3 d) { return m.c[0] * d.x + m.c[1] * d.y + m.c[2] * d.z; }
+static uint32_t texel(const ngp_image& im, float u, float vv) {
+	const int px = std::min(std::max((int)(u * (float)im.width), 0), (int)im.width - 1);
+	const int py = std::min(std::max((int)(vv * (float)im.height), 0), (int)im.height - 1);
+	return reinterpret_cast<const uint32_t*>(im.pixels)[(size_t)px + (size_t)py * im.width];
+}
+static void rgba_of(uint32_t t, float* o) {
+	if (t == 0x00FF00FFu) { o[0] = o[1] = o[2] = o[3] = -1.0f; return; }
+	const float a = (float)((t >> 24) & 0xff) * (1.0f / 255.0f);
+	o[0] = s2l((float)(t & 0xff) * (1.0f / 255.0f)) * a;
+	o[1] = s2l((float)((t >> 8) & 0xff) * (1.0f / 255.0f)) * a;
+	o[2] = s2l((float)((t >> 16) & 0xff) * (1.0f / 255.0f)) * a;
+	o[3] = a;
+}
+static uint32_t image_index(uint32_t i, uint32_t n_rays, uint32_t n_img) {
+	return (uint32_t)((((uint64_t)i) * n_img) / n_rays) % n_img;  // nerf_device.cuh:597
+}
+static void pixel_uv(Pcg& rng, const ngp_image& im, int snap, float* u, float* vv) {
+	*u = rng.nextf();
+	*vv = rng.nextf();
+	if (snap) {  // nerf_device.cuh:570-572
+		const int px = std::min(std::max((int)(*u * (float)im.width), 0), (int)im.width - 1);
+		const int py = std::min(std::max((int)(*vv * (float)im.height), 0), (int)im.height - 1);
+		*u = ((float)px + 0.5f) / (float)im.width;
+		*vv = ((float)py + 0.5f) / (float)im.height;
+	}
+}
+
+// generate_training_samples_nerf (src/testbed_nerf.cu:679-838), per-ray.
+static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st) {
+	const ngp_image& im = a.images[image_index(gi, nrg, a.n_images)];
+	Pcg rng;
+	rng.state = a.rng_state;
+	rng.inc = a.rng_inc;
+	rng.advance((int64_t)gi * 16);
+	float u, vv;
+	pixel_uv(rng, im, a.snap_to_pixel_centers, &u, &vv);
+	float rgba[4];
+	rgba_of(texel(im, u, vv), rgba);
+	if (rgba[0] < 0.0f) return false;
+	(void)rng.nextf();  // motionblur_time
+	const Cam x = cam_of(im.xform);
+	V3 dir = v((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
+	           (vv - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+	dir = rot(x, dir);
+	*o = x.c[3];
+	*d = normalize(dir);
+	const Box b{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	float t0, t1;
+	b.intersect(*o, *d, &t0, &t1);
+	t0 = std::max(t0, 0.0f);
+	*st = adv_n(t0, a.cone_angle_constant, rng.nextf());
+	return true;
+}
+
+static void train_step(Model& M, const ngp_train_args& a) {
+	const uint32_t R = a.n_rays, B = a.target_batch_size, MS = a.max_samples;
+	const uint32_t nrg = a.n_rays_global ? a.n_rays_global : R;
+	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	const float cone = a.cone_angle_constant;
+	// pass 1: count (testbed_nerf.cu:779-799)
+	std::vector<uint32_t> cnt(R, 0);
+	std::vector<V3> ro(R), rd(R);
+	std::vector<float> rst(R);
+	for (uint32_t i = 0; i < R; ++i) {
+		V3 o, d;
+		float t;
+		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t)) continue;
+		ro[i] = o; rd[i] = d; rst[i] = t;
+		const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		uint32_t j = 0;
+		V3 pos;
+		while (box.contains(pos = o + d * t) && j < STEPS) {
+			const float dt = calc_dt(t, cone);
+			const uint32_t mip = mip_dt(dt, pos, a.max_cascade);
+			if (occupied(pos, M.bits.data(), mip)) { ++j; t += dt; }
+			else t = adv_voxel(t, cone, pos, d, idir, mip);
+		}
+		cnt[i] = j;
+	}
+	// prefix-sum slot claim in ray order; drop if base + n > cap (testbed_nerf.cu:800-803)
+	M.ray_numsteps.assign(2 * (size_t)R, 0);
+	M.coords.assign(8 * (size_t)MS, 0.0f);
+	uint32_t base = 0;
+	for (uint32_t i = 0; i < R; ++i) {
+		const uint32_t n = cnt[i];
+		const uint32_t b = base;
+		base += n;
+		if (n == 0 || b + n > MS) continue;
+		M.ray_numsteps[2 * i] = n;
+		M.ray_numsteps[2 * i + 1] = b;
+		// pass 2: write coordinates (testbed_nerf.cu:814-830)
+		const V3 o = ro[i], d = rd[i], idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		const V3 wd = v((d.x + 1.0f) * 0.5f, (d.y + 1.0f) * 0.5f, (d.z + 1.0f) * 0.5f);
+		float t = rst[i];
+		uint32_t j = 0;
+		V3 pos;
+		while (box.contains(pos = o + d * t) && j < n) {
+			const float dt = calc_dt(t, cone);
+			const uint32_t mip = mip_dt(dt, pos, a.max_cascade);
+			if (occupied(pos, M.bits.data(), mip)) {
+				const V3 w = box.rel(pos);
+				float* c = &M.coords[8 * (size_t)(b + j)];
+				c[0] = w.x; c[1] = w.y; c[2] = w.z; c[3] = warp_dt(dt);
+				c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
+				++j;
+				t += dt;
+			} else t = adv_voxel(t, cone, pos, d, idir, mip);
+		}
+	}
+	M.total_samples = base;
+	const uint32_t S = std::min(base, MS);
+	// inference over the emitted samples with the training params (testbed_nerf.cu:2800-2802)
+	std::vector<float> enc((size_t)M.L * S * M.F), out(4 * (size_t)S);
+	hg_forward(M, M.p16.data(), M.coords.data(), 8, S, enc.data());
+	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data());
+	M.mlp_out.assign(4 * (size_t)MS, 0);
+	for (size_t k = 0; k < out.size(); ++k) M.mlp_out[k] = f2h(out[k]);
+
+	// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1119)
+	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
+	std::vector<uint32_t> cc(R, 0);
+	std::vector<float> lstate(8 * (size_t)R, 0.0f);
+	for (uint32_t i = 0; i < R; ++i) {
+		const uint32_t ns = M.ray_numsteps[2 * i], b0 = M.ray_numsteps[2 * i + 1];
+		if (ns == 0) continue;
+		float T = 1.0f;
+		float rr = 0, rg = 0, rb = 0;
+		uint32_t c = 0;
+		for (; c < ns; ++c) {
+			if (T < 1e-4f) break;
+			const float* o = &out[4 * (size_t)(b0 + c)];
+			const float dt = unwarp_dt(M.coords[8 * (size_t)(b0 + c) + 3]);
+			const float alpha = 1.0f - std::exp(-to_density(o[3], dact) * dt);
+			const float w = alpha * T;
+			rr += w * to_rgb(o[0], ract);
+			rg += w * to_rgb(o[1], ract);
+			rb += w * to_rgb(o[2], ract);
+			T *= 1.0f - alpha;
+		}
+		const uint32_t gi = a.ray_index_offset + i;
+		Pcg rng;
+		rng.state = a.rng_state;
+		rng.inc = a.rng_inc;
+		rng.advance((int64_t)gi * 16);
+		const ngp_image& im = a.images[image_index(gi, nrg, a.n_images)];
+		float u, vv;
+		pixel_uv(rng, im, a.snap_to_pixel_centers, &u, &vv);
+		rng.advance(1);
+		V3 bg = v(a.background_color[0], a.background_color[1], a.background_color[2]);
+		if (a.random_bg_color) {
+			const float x0 = rng.nextf(), x1 = rng.nextf(), x2 = rng.nextf();
+			bg = v(x0, x1, x2);
+		}
+		bg = v(s2l(bg.x), s2l(bg.y), s2l(bg.z));
+		float tex[4];
+		rgba_of(texel(im, u, vv), tex);
+		V3 tgt;
+		if (a.train_in_linear_colors || a.color_space == 0) {
+			tgt = v(tex[0], tex[1], tex[2]) + bg * (1.0f - tex[3]);
+			if (!a.train_in_linear_colors) {
+				tgt = v(l2s(tgt.x), l2s(tgt.y), l2s(tgt.z));
+				bg = v(l2s(bg.x), l2s(bg.y), l2s(bg.z));
+			}
+		} else {
+			bg = v(l2s(bg.x), l2s(bg.y), l2s(bg.z));
+			tgt = tex[3] > 0 ? v(l2s(tex[0] / tex[3]), l2s(tex[1] / tex[3]), l2s(tex[2] / tex[3])) * tex[3] + bg * (1.0f - tex[3]) : bg;
+		}
+		if (c == ns) { rr += T * bg.x; rg += T * bg.y; rb += T * bg.z; }
+		float lx, ly, lz, gx, gy, gz;
+		lossg(tgt.x, rr, a.loss_type, &lx, &gx);
+		lossg(tgt.y, rg, a.loss_type, &ly, &gy);
+		lossg(tgt.z, rb, a.loss_type, &lz, &gz);
+		float* ls = &lstate[8 * (size_t)i];
+		ls[0] = gx; ls[1] = gy; ls[2] = gz; ls[3] = rr; ls[4] = rg; ls[5] = rb; ls[6] = (lx + ly + lz) / 3.0f;
+		cc[i] = c;
+	}
+	M.ray_compacted.assign(2 * (size_t)R, 0);
+	M.loss.assign(R, 0.0f);
+	M.ccoords.assign(8 * (size_t)B, 0.0f);
+	M.dloss.assign(4 * (size_t)B, 0);
+	std::vector<float> cenc((size_t)M.L * B * M.F, 0.0f);
+	const float loss_scale = 128.0f / (float)nrg;
+	const float l2r = ract == 3 ? 1e-4f : 0.0f;
+	const float l1d = M.mean < 0.01f ? 1e-4f : 0.0f;
+	uint32_t cbase = 0;
+	for (uint32_t i = 0; i < R; ++i) {
+		const uint32_t c = cc[i], cb = cbase;
+		cbase += c;
+		const uint32_t cn = c == 0 ? 0 : std::min(B - std::min(B, cb), c);
+		M.ray_compacted[2 * i] = cn;
+		M.ray_compacted[2 * i + 1] = cb;
+		if (cn == 0) continue;
+		const float* ls = &lstate[8 * (size_t)i];
+		M.loss[i] = ls[6] / (float)nrg;
+		const uint32_t b0 = M.ray_numsteps[2 * i + 1];
+		const V3 o = ro[i];
+		float T = 1.0f, r2 = 0, g2 = 0, b2 = 0;
+		for (uint32_t j = 0; j < cn; ++j) {
+			const size_t s = b0 + j, dst = cb + j;
+			for (int k = 0; k < 8; ++k) M.ccoords[8 * dst + k] = M.coords[8 * s + k];
+			for (uint32_t l = 0; l < M.L; ++l)
+				for (uint32_t f = 0; f < M.F; ++f) cenc[((size_t)l * B + dst) * M.F + f] = enc[((size_t)l * S + s) * M.F + f];
+			const float* cw = &M.coords[8 * s];
+			const V3 pos = box.mn + v(cw[0] * (box.mx.x - box.mn.x), cw[1] * (box.mx.y - box.mn.y), cw[2] * (box.mx.z - box.mn.z));
+			const float depth = len(pos - o);
+			const float dt = unwarp_dt(cw[3]);
+			const float* ob = &out[4 * s];
+			const float rgb[3] = {to_rgb(ob[0], ract), to_rgb(ob[1], ract), to_rgb(ob[2], ract)};
+			const float alpha = 1.0f - std::exp(-to_density(ob[3], dact) * dt);
+			const float w = alpha * T;
+			r2 += w * rgb[0]; g2 += w * rgb[1]; b2 += w * rgb[2];
+			T *= 1.0f - alpha;
+			const float suf[3] = {ls[3] - r2, ls[4] - g2, ls[5] - b2};
+			uint16_t* dl = &M.dloss[4 * dst];
+			for (int k = 0; k < 3; ++k) dl[k] = f2h(loss_scale * (w * ls[k] * to_rgb_d(ob[k], ract) + std::max(0.0f, l2r * ob[k])));
+			const float ddm = to_density_d(ob[3], dact) * (dt * (ls[0] * (T * rgb[0] - suf[0]) + ls[1] * (T * rgb[1] - suf[1]) + ls[2] * (T * rgb[2] - suf[2])));
+			dl[3] = f2h(loss_scale * ddm + (ob[3] < 0.0f ? -l1d : 0.0f) + (ob[3] > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
+		}
+	}
+	M.total_compacted = cbase;
+	M.loss_sum = 0.0f;
+	for (float l : M.loss) M.loss_sum += l;
+
+	// Trainer::training_step on the compacted batch; rollover folded into a multiplicity weight
+	const uint32_t C = std::min(cbase, B);
+	std::vector<float> wts(C), dlf(4 * (size_t)C), denc((size_t)M.L * C * M.F, 0.0f), ce((size_t)M.L * C * M.F);
+	for (uint32_t j = 0; j < C; ++j) wts[j] = 1.0f + (float)((B - 1 - j) / C) * ((float)C / (float)B);
+	for (uint32_t j = 0; j < 4 * C; ++j) dlf[j] = h2f(M.dloss[j]);
+	for (uint32_t l = 0; l < M.L; ++l)
+		for (uint32_t j = 0; j < C; ++j)
+			for (uint32_t f = 0; f < M.F; ++f) ce[((size_t)l * C + j) * M.F + f] = cenc[((size_t)l * B + j) * M.F + f];
+	mlp_backward(M, M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data());
+	hg_backward(M, M.ccoords.data(), 8, C, denc.data());
+	if (!a.defer_optimizer) optimizer(M, a.training_step, a.optimize_mlp, a.optimize_encoding);
+}
+
+// ---- occupancy grid (testbed_nerf.cu:74-331, 2271-2379) ------------------------------------
+static void mark_untrained(Model& M, const ngp_grid_args& a, uint32_t n_elem) {
+	for (uint32_t i = 0; i < n_elem; ++i) {
+		const uint32_t level = i / CELLS, pi = i % CELLS;
+		const float vs = std::scalbn(1.0f / GRID, (int)level);
+		const V3 pos = (v((float)morton_inv(pi), (float)morton_inv(pi >> 1), (float)morton_inv(pi >> 2)) * (1.0f / GRID) - v(0.5f, 0.5f, 0.5f)) * std::scalbn(1.0f, (int)level) + v(0.5f, 0.5f, 0.5f);
+		uint32_t count = 0;
+		for (uint32_t j = 0; j < a.n_images && count < 1; ++j) {
+			const ngp_image& im = a.images[j];
+			if (im.lens_mode == 2 || im.lens_mode == 3 || im.lens_mode == 5) { ++count; continue; }
+			const Cam x = cam_of(im.xform);
+			const V3 A = x.c[0], Bv = x.c[1], Cc = x.c[2];
+			const V3 bc = v(Bv.y * Cc.z - Bv.z * Cc.y, Bv.z * Cc.x - Bv.x * Cc.z, Bv.x * Cc.y - Bv.y * Cc.x);
+			const V3 ca = v(Cc.y * A.z - Cc.z * A.y, Cc.z * A.x - Cc.x * A.z, Cc.x * A.y - Cc.y * A.x);
+			const V3 ab = v(A.y * Bv.z - A.z * Bv.y, A.z * Bv.x - A.x * Bv.z, A.x * Bv.y - A.y * Bv.x);
+			const float inv = 1.0f / dot(A, bc);
+			for (uint32_t k = 0; k < 8; ++k) {
+				const V3 corner = pos + v((k & 1) ? vs : 0, (k & 2) ? vs : 0, (k & 4) ? vs : 0);
+				const V3 dir = normalize(corner - x.c[3]);
+				if (dot(dir, x.c[2]) < 1e-4f) continue;
+				const V3 rel = corner - x.c[3];
+				V3 cd = v(dot(bc * inv, rel), dot(ca * inv, rel), dot(ab * inv, rel));
+				cd = cd * (1.0f / cd.z);
+				const float u = cd.x * im.focal_length[0] / (float)im.width + im.principal_point[0];
+				const float vv = cd.y * im.focal_length[1] / (float)im.height + im.principal_point[1];
+				V3 rd = v((u - im.principal_point[0]) * (float)im.width / im.focal_length[0], (vv - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+				rd = normalize(rot(x, rd));
+				if (len(rd - dir) < 1e-3f && u > 0 && vv > 0 && u < 1 && vv < 1) { ++count; break; }
+			}
+		}
+		if (a.clear_visible || (M.grid[i] < 0) != (count < 1)) M.grid[i] = count >= 1 ? 0.0f : -1.0f;
+	}
+}
+
+static void bitfield_update(Model& M, uint32_t max_cascade) {
+	unsigned long long sum = 0;
+	for (uint32_t i = 0; i < CELLS; ++i) sum += (unsigned long long)(std::min(std::max(M.grid[i], 0.0f), 65536.0f) * 16777216.0f);
+	M.mean = (float)((double)sum / 16777216.0 / (double)CELLS);
+	const float thresh = std::min(0.01f, M.mean);
+	M.bits.assign(CELLS / 8 * CASCADES, 0);
+	for (uint32_t i = 0; i < CELLS / 8 * (max_cascade + 1); ++i) {
+		uint8_t b = 0;
+		for (uint32_t j = 0; j < 8; ++j) b |= M.grid[i * 8 + j] > thresh ? (uint8_t)(1u << j) : 0;
+		M.bits[i] = b;
+	}
+	for (uint32_t level = 1; level < CASCADES; ++level) {
+		const uint8_t* prev = &M.bits[(size_t)(level - 1) * CELLS / 8];
+		uint8_t* next = &M.bits[(size_t)level * CELLS / 8];
+		for (uint32_t i = 0; i < CELLS / 64; ++i) {
+			uint8_t b = 0;
+			for (uint32_t j = 0; j < 8; ++j) b |= prev[i * 8 + j] > 0 ? (uint8_t)(1u << j) : 0;
+			next[morton(morton_inv(i) + 16, morton_inv(i >> 1) + 16, morton_inv(i >> 2) + 16)] |= b;
+		}
+	}
+}
+
+static void grid_update(Model& M, const ngp_grid_args& a) {
+	const uint32_t nc = a.max_cascade + 1, ne = CELLS * nc;
+	if (M.grid.size() < ne) M.grid.resize(ne, 0.0f);
+	if (a.mark_untrained) mark_untrained(M, a, ne);
+	M.tmp.assign(ne, 0.0f);
+	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	Pcg rng;
+	rng.state = a.rng_state;
+	rng.inc = a.rng_inc;
+	const uint32_t ntot = a.n_uniform_samples + a.n_nonuniform_samples;
+	std::vector<float> pos(4 * (size_t)ntot);
+	std::vector<uint32_t> idxs(ntot);
+	for (int pass = 0; pass < 2; ++pass) {
+		const uint32_t n = pass == 0 ? a.n_uniform_samples : a.n_nonuniform_samples;
+		const float thresh = pass == 0 ? -0.01f : 0.01f;
+		const uint32_t first = pass == 0 ? 0 : a.n_uniform_samples;
+		for (uint32_t i = 0; i < n; ++i) {
+			Pcg r = rng;
+			r.advance((int64_t)i * 4);
+			const uint32_t level = (uint32_t)(r.nextf() * (float)nc) % nc;
+			uint32_t idx = 0;
+			for (uint32_t j = 0; j < 10; ++j) {
+				idx = ((i + a.ema_step * n) * 56924617u + j * 19349663u + 96925573u) % CELLS;
+				idx += level * CELLS;
+				if (M.grid[idx] > thresh) break;
+			}
+			const uint32_t pi = idx % CELLS;
+			const float r0 = r.nextf(), r1 = r.nextf(), r2 = r.nextf();
+			const V3 p = (v(((float)morton_inv(pi) + r0) / GRID, ((float)morton_inv(pi >> 1) + r1) / GRID, ((float)morton_inv(pi >> 2) + r2) / GRID) - v(0.5f, 0.5f, 0.5f)) * std::scalbn(1.0f, (int)level) + v(0.5f, 0.5f, 0.5f);
+			const V3 w = box.rel(p);
+			float* q = &pos[4 * (size_t)(first + i)];
+			q[0] = w.x; q[1] = w.y; q[2] = w.z; q[3] = warp_dt(MIN_STEP);
+			idxs[first + i] = idx;
+		}
+		rng.advance();
+	}
+	// density (NerfNetwork::density, training params) and max-splat
+	const std::vector<uint16_t>& P = a.use_inference_params ? M.inf16 : M.p16;
+	std::vector<float> enc((size_t)M.L * ntot * M.F);
+	hg_forward(M, P.data(), pos.data(), 4, ntot, enc.data());
+	std::vector<float> col(M.E);
+	Acts A;
+	for (uint32_t i = 0; i < ntot; ++i) {
+		gather_enc(M, enc.data(), ntot, i, col.data());
+		// density MLP only
+		std::vector<float> x(M.Epad, 0.0f), y;
+		for (uint32_t k = 0; k < M.E; ++k) x[k] = col[k];
+		for (uint32_t l = 0; l < M.n_density_layers; ++l) {
+			layer_fwd(M, P.data(), M.layers[l], x, y, true);
+			x = y;
+		}
+		const float th = to_density(x[0], M.cfg.density_activation) * MIN_STEP;
+		M.tmp[idxs[i]] = std::max(M.tmp[idxs[i]], th);
+	}
+	for (uint32_t i = 0; i < ne; ++i) {
+		const float prev = M.grid[i];
+		M.grid[i] = prev < 0.0f ? prev : std::max(prev * a.decay, M.tmp[i]);
+	}
+	bitfield_update(M, a.max_cascade);
+}
+
+// ---- tracer (render_nerf, NerfTracer::trace; per ray, chunking-invariant) ---------------------
+static void render(const Model& M, const ngp_render_args& a, float* frame, float* depthbuf) {
+	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	const Box tbox{v(a.train_aabb_min[0], a.train_aabb_min[1], a.train_aabb_min[2]), v(a.train_aabb_max[0], a.train_aabb_max[1], a.train_aabb_max[2])};
+	const Cam cam = cam_of(a.camera);
+	const uint16_t* P = a.use_inference_params ? M.inf16.data() : M.p16.data();
+	const float cone = a.cone_angle_constant;
+	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
+	const uint32_t sc = std::max(a.shard_count, 1u), sr = std::max(a.shard_rows, 1u), si = a.shard_index % sc;
+	float ox, oy;
+	pixel_offset(a.snap_to_pixel_centers ? 0 : a.sample_index, &ox, &oy);
+	std::vector<float> enc(M.L * M.F), col(M.E), out(4);
+	for (uint32_t y = 0; y < a.height; ++y) {
+		if ((y / sr) % sc != si) continue;
+		for (uint32_t x = 0; x < a.width; ++x) {
+			const uint32_t idx = x + a.width * y;
+			float* fb = frame + 4 * (size_t)idx;
+			fb[0] = fb[1] = fb[2] = fb[3] = 0.0f;
+			depthbuf[idx] = MAXD;
+			const float u = ((float)x + ox) / (float)a.width, vv = ((float)y + oy) / (float)a.height;
+			V3 d = v((u - a.screen_center[0]) * (float)a.width / a.focal_length[0], (vv - a.screen_center[1]) * (float)a.height / a.focal_length[1], 1.0f);
+			d = rot(cam, d);
+			const V3 o = cam.c[3] + d * a.near_distance;
+			d = normalize(d);
+			float t0, t1;
+			box.intersect(o, d, &t0, &t1);
+			float t = std::max(t0, 0.0f) + 1e-6f;
+			if (!box.contains(o + d * t)) continue;
+			const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+			t = adv_n(t, cone, ldval(a.sample_index, idx * 786433u, 0));
+			t = skip_empty(t, cone, o, d, idir, M.bits.data(), a.max_cascade, box);
+			if (t >= MAXD) continue;
+			float c[4] = {0, 0, 0, 0}, maxw = 0.0f, dep = 0.0f;
+			const V3 wd = v((d.x + 1) * 0.5f, (d.y + 1) * 0.5f, (d.z + 1) * 0.5f);
+			for (uint32_t step = 0; step < 10000; ++step) {
+				t = skip_empty(t, cone, o, d, idir, M.bits.data(), a.max_cascade, box);
+				if (t >= MAXD) break;
+				const float dt = calc_dt(t, cone);
+				const V3 w = tbox.rel(o + d * t);
+				float coord[8] = {w.x, w.y, w.z, warp_dt(dt), wd.x, wd.y, wd.z, 0.0f};
+				hg_forward(M, P, coord, 8, 1, enc.data());
+				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data());
+				t += dt;
+				const V3 pos = tbox.mn + v(coord[0] * (tbox.mx.x - tbox.mn.x), coord[1] * (tbox.mx.y - tbox.mn.y), coord[2] * (tbox.mx.z - tbox.mn.z));
+				const float T = 1.0f - c[3];
+				const float alpha = 1.0f - std::exp(-to_density(out[3], dact) * unwarp_dt(coord[3]));
+				const float wgt = alpha * T;
+				c[0] += to_rgb(out[0], ract) * wgt;
+				c[1] += to_rgb(out[1], ract) * wgt;
+				c[2] += to_rgb(out[2], ract) * wgt;
+				c[3] += wgt;
+				if (wgt > maxw) { maxw = wgt; dep = dot(cam.c[2], pos - cam.c[3]); }
+				if (c[3] > 1.0f - a.min_transmittance) {
+					const float inv = 1.0f / c[3];
+					for (int k = 0; k < 4; ++k) c[k] *= inv;
+					break;
+				}
+			}
+			if (!(c[3] > 0.001f)) continue;  // compact_kernel_nerf drops near-transparent rays
+			if (!a.train_in_linear_colors) for (int k = 0; k < 3; ++k) c[k] = s2l(c[k]);
+			for (int k = 0; k < 4; ++k) fb[k] = c[k];
+			if (c[3] > 0.2f) depthbuf[idx] = dep;
+		}
+	}
+}
+
+}  // namespace oref
+
+using namespace oref;
+
+static thread_local std::string g_err;
+template <class F>
+static int guard(F&& f) {
+	try { f(); return 0; } catch (const std::exception& e) { g_err = e.what(); return 1; }
+}
+
+extern "C" {
+
+const char* oref_last_error(void) { return g_err.c_str(); }
+
+// Known-answer helpers
+void oref_pcg32(uint64_t seed, uint64_t seq, uint32_t n, uint32_t* out) {
+	Pcg r;
+	r.seed(seed, seq);
+	for (uint32_t i = 0; i < n; ++i) out[i] = r.next();
+}
+void oref_pcg32_floats_advanced(uint64_t state, uint64_t inc, int64_t adv, uint32_t n, float* out) {
+	Pcg r;
+	r.state = state;
+	r.inc = inc;
+	r.advance(adv);
+	for (uint32_t i = 0; i < n; ++i) out[i] = r.nextf();
+}
+float oref_ld_random_val(uint32_t index, uint32_t seed, uint32_t dim) { return ldval(index, seed, dim); }
+uint32_t oref_sobol(uint32_t index, uint32_t dim) { return sobol(index, dim); }
+uint32_t oref_morton3D(uint32_t x, uint32_t y, uint32_t z) { return morton(x, y, z); }
+void oref_sh4(const float* wdir, float* out) { sh4(wdir, out); }
+uint16_t oref_f2h(float f) { return f2h(f); }
+float oref_h2f(uint16_t h) { return h2f(h); }
+
+void* oref_model_create(const ngp_network_config* cfg) {
+	auto* M = new Model();
+	M->cfg = *cfg;
+	build(*M);
+	return M;
+}
+void oref_model_destroy(void* m) { delete static_cast<Model*>(m); }
+uint64_t oref_model_n_params(void* m) { return static_cast<Model*>(m)->n; }
+uint64_t oref_model_n_mlp_params(void* m) { return static_cast<Model*>(m)->n_mlp; }
+void oref_model_level_table(void* m, float* scale, uint32_t* res, uint32_t* offset, uint32_t* size, uint32_t* hashed) {
+	Model& M = *static_cast<Model*>(m);
+	for (uint32_t l = 0; l < M.L; ++l) {
+		scale[l] = M.scale[l]; res[l] = M.res[l]; offset[l] = M.offset[l]; size[l] = M.size[l]; hashed[l] = M.hashed[l];
+	}
+}
+// set fp32 master params; fp16 copies derived; optimizer reset (EMA = params)
+void oref_model_set_params(void* m, const float* p) {
+	Model& M = *static_cast<Model*>(m);
+	for (uint64_t i = 0; i < M.n; ++i) {
+		M.p32[i] = p[i];
+		M.p16[i] = f2h(p[i]);
+		M.ema32[i] = p[i];
+		M.inf16[i] = M.p16[i];
+		M.m[i] = M.vv[i] = 0.0f;
+		M.steps[i] = 0;
+		M.grads[i] = 0.0f;
+	}
+	M.ema_step = 0;
+}
+void oref_model_get(void* m, int kind, void* out) {
+	Model& M = *static_cast<Model*>(m);
+	switch (kind) {
+		case NGP_PARAMS_FP32: std::memcpy(out, M.p32.data(), M.n * 4); break;
+		case NGP_PARAMS_FP16: std::memcpy(out, M.p16.data(), M.n * 2); break;
+		case NGP_PARAMS_EMA_FP32: std::memcpy(out, M.ema32.data(), M.n * 4); break;
+		case NGP_PARAMS_INFER_FP16: std::memcpy(out, M.inf16.data(), M.n * 2); break;
+		case NGP_GRADS_FP32: std::memcpy(out, M.grads.data(), M.n * 4); break;
+		default: break;
+	}
+}
+void oref_zero_grads(void* m) { auto& M = *static_cast<Model*>(m); std::fill(M.grads.begin(), M.grads.end(), 0.0f); }
+
+void oref_encode(void* m, const float* pos, uint32_t stride, uint32_t n, float* enc, int use_inf) {
+	Model& M = *static_cast<Model*>(m);
+	hg_forward(M, use_inf ? M.inf16.data() : M.p16.data(), pos, stride, n, enc);
+}
+void oref_encode_indices(void* m, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx, float* w) {
+	Model& M = *static_cast<Model*>(m);
+	for (uint32_t i = 0; i < n; ++i)
+		for (uint32_t l = 0; l < M.L; ++l) {
+			uint32_t ix[8];
+			float ww[8];
+			hg_corners(M, l, pos + (size_t)i * stride, ix, ww);
+			for (int c = 0; c < 8; ++c) {
+				idx[((size_t)i * M.L + l) * 8 + c] = M.offset[l] + ix[c];
+				w[((size_t)i * M.L + l) * 8 + c] = ww[c];
+			}
+		}
+}
+void oref_infer(void* m, const float* coords, uint32_t fpc, uint32_t n, float* out, int use_inf) {
+	Model& M = *static_cast<Model*>(m);
+	const uint16_t* P = use_inf ? M.inf16.data() : M.p16.data();
+	std::vector<float> enc((size_t)M.L * n * M.F);
+	hg_forward(M, P, coords, fpc, n, enc.data());
+	mlp_forward(M, P, enc.data(), coords, fpc, n, out);
+}
+void oref_mlp_forward_enc(void* m, const float* enc, const float* coords, uint32_t fpc, uint32_t n, float* out) {
+	Model& M = *static_cast<Model*>(m);
+	mlp_forward(M, M.p16.data(), enc, coords, fpc, n, out);
+}
+void oref_density(void* m, const float* pos, uint32_t stride, uint32_t n, float* out, int use_inf) {
+	Model& M = *static_cast<Model*>(m);
+	const uint16_t* P = use_inf ? M.inf16.data() : M.p16.data();
+	std::vector<float> enc((size_t)M.L * n * M.F), col(M.E);
+	hg_forward(M, P, pos, stride, n, enc.data());
+	for (uint32_t i = 0; i < n; ++i) {
+		gather_enc(M, enc.data(), n, i, col.data());
+		std::vector<float> x(M.Epad, 0.0f), y;
+		for (uint32_t k = 0; k < M.E; ++k) x[k] = col[k];
+		for (uint32_t l = 0; l < M.n_density_layers; ++l) { layer_fwd(M, P, M.layers[l], x, y, true); x = y; }
+		out[i] = x[0];
+	}
+}
+// enc [L][n][F] floats (fp16 values), dirs [n][3] warped, dloss [n][4] (fp16 values)
+void oref_backward(void* m, const float* enc, const float* dirs, uint32_t n, const float* dloss, const float* weight, float* denc) {
+	Model& M = *static_cast<Model*>(m);
+	std::vector<float> coords(8 * (size_t)n, 0.0f);
+	for (uint32_t i = 0; i < n; ++i) for (int k = 0; k < 3; ++k) coords[8 * i + 4 + k] = dirs[3 * i + k];
+	mlp_backward(M, M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc);
+}
+void oref_encode_backward(void* m, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
+	hg_backward(*static_cast<Model*>(m), pos, stride, n, denc);
+}
+int oref_train_step(void* m, const ngp_train_args* a) { return guard([&] { train_step(*static_cast<Model*>(m), *a); }); }
+void oref_optimizer_step(void* m, uint32_t step, int opt_mlp, int opt_enc) { optimizer(*static_cast<Model*>(m), step, opt_mlp, opt_enc); }
+void oref_train_stats(void* m, ngp_train_stats* s) {
+	Model& M = *static_cast<Model*>(m);
+	std::memset(s, 0, sizeof(*s));
+	s->n_rays = (uint32_t)M.loss.size();
+	s->measured_batch_size_before_compaction = M.total_samples;
+	s->measured_batch_size = M.total_compacted;
+	s->loss = M.loss_sum;
+}
+// scratch mirrors of ngp_train_scratch (host copies)
+size_t oref_train_scratch(void* m, int kind, void* out) {
+	Model& M = *static_cast<Model*>(m);
+	auto cp = [&](const void* src, size_t bytes) { if (out) std::memcpy(out, src, bytes); return bytes; };
+	switch (kind) {
+		case NGP_SCRATCH_RAY_NUMSTEPS: return cp(M.ray_numsteps.data(), M.ray_numsteps.size() * 4);
+		case NGP_SCRATCH_COORDS: return cp(M.coords.data(), M.coords.size() * 4);
+		case NGP_SCRATCH_MLP_OUT: return cp(M.mlp_out.data(), M.mlp_out.size() * 2);
+		case NGP_SCRATCH_RAY_COMPACTED: return cp(M.ray_compacted.data(), M.ray_compacted.size() * 4);
+		case NGP_SCRATCH_DLOSS: return cp(M.dloss.data(), M.dloss.size() * 2);
+		case NGP_SCRATCH_LOSS: return cp(M.loss.data(), M.loss.size() * 4);
+		case NGP_SCRATCH_COMPACT_COORDS: return cp(M.ccoords.data(), M.ccoords.size() * 4);
+		default: return 0;
+	}
+}
+int oref_density_grid_update(void* m, const ngp_grid_args* a) { return guard([&] { grid_update(*static_cast<Model*>(m), *a); }); }
+void oref_density_grid_bitfield(void* m, uint32_t max_cascade) { bitfield_update(*static_cast<Model*>(m), max_cascade); }
+void oref_density_grid_set(void* m, const float* grid, uint32_t n) {
+	Model& M = *static_cast<Model*>(m);
+	M.grid.assign(grid, grid + n);
+}
+void oref_density_grid_get(void* m, float* grid, uint8_t* bits, float* mean) {
+	Model& M = *static_cast<Model*>(m);
+	if (grid) std::memcpy(grid, M.grid.data(), M.grid.size() * 4);
+	if (bits) std::memcpy(bits, M.bits.data(), M.bits.size());
+	if (mean) *mean = M.mean;
+}
+void oref_set_bitfield(void* m, const uint8_t* bits) {
+	Model& M = *static_cast<Model*>(m);
+	M.bits.assign(bits, bits + CELLS / 8 * CASCADES);
+}
+int oref_render(void* m, const ngp_render_args* a, float* frame, float* depth) {
+	return guard([&] { render(*static_cast<Model*>(m), *a, frame, depth); });
+}
+// accumulate_kernel + tonemap_kernel for one pixel buffer (render_buffer.cu:232-266,533-565)
+void oref_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t W, uint32_t H, uint32_t spp,
+                             int color_space, float exposure, const float* bg_in, int output_srgb) {
+	for (size_t i = 0; i < (size_t)W * H; ++i) {
+		float c[4], t[4];
+		for (int k = 0; k < 4; ++k) { c[k] = frame[4 * i + k]; t[k] = spp == 0 ? 0.0f : accum[4 * i + k]; }
+		if (color_space == 1) for (int k = 0; k < 3; ++k) c[k] = l2s(c[k]);
+		for (int k = 0; k < 4; ++k) t[k] = (t[k] * (float)spp + c[k]) / ((float)spp + 1.0f);
+		for (int k = 0; k < 4; ++k) accum[4 * i + k] = t[k];
+		if (!out) continue;
+		float bg[4] = {bg_in[0], bg_in[1], bg_in[2], bg_in[3]};
+		if (color_space != 1) for (int k = 0; k < 3; ++k) bg[k] = s2l(bg[k]);
+		const float w = (1.0f - t[3]) * bg[3];
+		for (int k = 0; k < 3; ++k) t[k] += bg[k] * w;
+		t[3] += w;
+		if (color_space == 1) for (int k = 0; k < 3; ++k) t[k] = s2l(t[k]);
+		const float e = std::pow(2.0f, exposure);
+		for (int k = 0; k < 3; ++k) t[k] *= e;
+		if (output_srgb) for (int k = 0; k < 3; ++k) t[k] = l2s(t[k]);
+		for (int k = 0; k < 4; ++k) out[4 * i + k] = t[k];
+	}
+}
+
+}  // extern "C"

@@ -1,0 +1,203 @@
+"""ctypes binding of oracle/liboracle.so — TEST INFRASTRUCTURE ONLY.
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg load this.
+"""
+import ctypes as C
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "instant-ngp-rendering_amd"))
+import ngp_abi as A  # noqa: E402
+
+LIB_PATH = os.path.join(ROOT, "oracle", "liboracle.so")
+
+_PROTOS = {
+    "oref_pcg32": (None, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]),
+    "oref_pcg32_floats_advanced": (None, [C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32, C.c_void_p]),
+    "oref_ld_random_val": (C.c_float, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "oref_sobol": (C.c_uint32, [C.c_uint32, C.c_uint32]),
+    "oref_morton3D": (C.c_uint32, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "oref_sh4": (None, [C.c_void_p, C.c_void_p]),
+    "oref_f2h": (C.c_uint16, [C.c_float]),
+    "oref_h2f": (C.c_float, [C.c_uint16]),
+    "oref_model_create": (C.c_void_p, [C.POINTER(A.NetworkConfig)]),
+    "oref_model_destroy": (None, [C.c_void_p]),
+    "oref_model_n_params": (C.c_uint64, [C.c_void_p]),
+    "oref_model_n_mlp_params": (C.c_uint64, [C.c_void_p]),
+    "oref_model_level_table": (None, [C.c_void_p] + [C.c_void_p] * 5),
+    "oref_model_set_params": (None, [C.c_void_p, C.c_void_p]),
+    "oref_model_get": (None, [C.c_void_p, C.c_int, C.c_void_p]),
+    "oref_zero_grads": (None, [C.c_void_p]),
+    "oref_encode": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
+    "oref_encode_indices": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
+    "oref_infer": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
+    "oref_mlp_forward_enc": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "oref_density": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
+    "oref_backward": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "oref_encode_backward": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
+    "oref_train_step": (C.c_int, [C.c_void_p, C.POINTER(A.TrainArgs)]),
+    "oref_optimizer_step": (None, [C.c_void_p, C.c_uint32, C.c_int, C.c_int]),
+    "oref_train_stats": (None, [C.c_void_p, C.POINTER(A.TrainStats)]),
+    "oref_train_scratch": (C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p]),
+    "oref_density_grid_update": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
+    "oref_density_grid_bitfield": (None, [C.c_void_p, C.c_uint32]),
+    "oref_density_grid_set": (None, [C.c_void_p, C.c_void_p, C.c_uint32]),
+    "oref_density_grid_get": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "oref_set_bitfield": (None, [C.c_void_p, C.c_void_p]),
+    "oref_render": (C.c_int, [C.c_void_p, C.POINTER(A.RenderArgs), C.c_void_p, C.c_void_p]),
+    "oref_accumulate_tonemap": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
+                                       C.c_int, C.c_float, C.c_void_p, C.c_int]),
+    "oref_last_error": (C.c_char_p, []),
+}
+
+_lib = None
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            subprocess.check_call(["make", "-C", os.path.join(ROOT, "oracle")], stdout=subprocess.DEVNULL)
+        lib = C.CDLL(LIB_PATH)
+        for name, (res, args) in _PROTOS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def ptr(a):
+    return a.ctypes.data_as(C.c_void_p)
+
+
+class Oracle:
+    """Scalar CPU model mirroring the C-ABI model handle."""
+
+    def __init__(self, cfg):
+        self.lib = load()
+        self.cfg = cfg
+        self.h = self.lib.oref_model_create(C.byref(cfg))
+        self.n_params = int(self.lib.oref_model_n_params(self.h))
+        self.n_mlp = int(self.lib.oref_model_n_mlp_params(self.h))
+        self.L = cfg.n_levels
+        self.F = cfg.n_features_per_level
+
+    def __del__(self):
+        try:
+            self.lib.oref_model_destroy(self.h)
+        except Exception:
+            pass
+
+    def level_table(self):
+        L = self.L
+        s = np.zeros(L, np.float32)
+        r, o, z, h = (np.zeros(L, np.uint32) for _ in range(4))
+        self.lib.oref_model_level_table(self.h, ptr(s), ptr(r), ptr(o), ptr(z), ptr(h))
+        return s, r, o, z, h
+
+    def set_params(self, p):
+        p = np.ascontiguousarray(p, np.float32)
+        assert p.size == self.n_params
+        self.lib.oref_model_set_params(self.h, ptr(p))
+
+    def get(self, kind):
+        dt = np.uint16 if kind in (A.PARAMS_FP16, A.PARAMS_INFER_FP16) else np.float32
+        out = np.zeros(self.n_params, dt)
+        self.lib.oref_model_get(self.h, kind, ptr(out))
+        return out
+
+    def encode(self, pos, use_inf=False):
+        pos = np.ascontiguousarray(pos, np.float32)
+        n, stride = pos.shape
+        enc = np.zeros((self.L, n, self.F), np.float32)
+        self.lib.oref_encode(self.h, ptr(pos), stride, n, ptr(enc), int(use_inf))
+        return enc
+
+    def encode_indices(self, pos):
+        pos = np.ascontiguousarray(pos, np.float32)
+        n, stride = pos.shape
+        idx = np.zeros((n, self.L, 8), np.uint32)
+        w = np.zeros((n, self.L, 8), np.float32)
+        self.lib.oref_encode_indices(self.h, ptr(pos), stride, n, ptr(idx), ptr(w))
+        return idx, w
+
+    def infer(self, coords, use_inf=False):
+        coords = np.ascontiguousarray(coords, np.float32)
+        n, fpc = coords.shape
+        out = np.zeros((n, 4), np.float32)
+        self.lib.oref_infer(self.h, ptr(coords), fpc, n, ptr(out), int(use_inf))
+        return out
+
+    def density(self, pos, use_inf=False):
+        pos = np.ascontiguousarray(pos, np.float32)
+        n, stride = pos.shape
+        out = np.zeros(n, np.float32)
+        self.lib.oref_density(self.h, ptr(pos), stride, n, ptr(out), int(use_inf))
+        return out
+
+    def backward(self, enc, dirs, dloss, weight=None):
+        enc = np.ascontiguousarray(enc, np.float32)
+        dirs = np.ascontiguousarray(dirs, np.float32)
+        dloss = np.ascontiguousarray(dloss, np.float32)
+        n = dirs.shape[0]
+        denc = np.zeros((self.L, n, self.F), np.float32)
+        w = None if weight is None else np.ascontiguousarray(weight, np.float32)
+        self.lib.oref_backward(self.h, ptr(enc), ptr(dirs), n, ptr(dloss), None if w is None else ptr(w), ptr(denc))
+        return denc
+
+    def encode_backward(self, pos, denc):
+        pos = np.ascontiguousarray(pos, np.float32)
+        denc = np.ascontiguousarray(denc, np.float32)
+        self.lib.oref_encode_backward(self.h, ptr(pos), pos.shape[1], pos.shape[0], ptr(denc))
+
+    def train_step(self, args):
+        if self.lib.oref_train_step(self.h, C.byref(args)) != 0:
+            raise RuntimeError(self.lib.oref_last_error().decode())
+
+    def optimizer_step(self, step, opt_mlp=1, opt_enc=1):
+        self.lib.oref_optimizer_step(self.h, step, opt_mlp, opt_enc)
+
+    def stats(self):
+        s = A.TrainStats()
+        self.lib.oref_train_stats(self.h, C.byref(s))
+        return s
+
+    def scratch(self, kind, dtype):
+        nbytes = self.lib.oref_train_scratch(self.h, kind, None)
+        out = np.zeros(nbytes // np.dtype(dtype).itemsize, dtype)
+        self.lib.oref_train_scratch(self.h, kind, ptr(out))
+        return out
+
+    def grid_update(self, args):
+        if self.lib.oref_density_grid_update(self.h, C.byref(args)) != 0:
+            raise RuntimeError(self.lib.oref_last_error().decode())
+
+    def grid_set(self, grid):
+        grid = np.ascontiguousarray(grid, np.float32)
+        self.lib.oref_density_grid_set(self.h, ptr(grid), grid.size)
+
+    def grid_bitfield(self, max_cascade):
+        self.lib.oref_density_grid_bitfield(self.h, max_cascade)
+
+    def grid_get(self, n_cells):
+        grid = np.zeros(n_cells, np.float32)
+        bits = np.zeros(128 ** 3 // 8 * 8, np.uint8)
+        mean = C.c_float()
+        self.lib.oref_density_grid_get(self.h, ptr(grid), ptr(bits), C.byref(mean))
+        return grid, bits, mean.value
+
+    def set_bitfield(self, bits):
+        bits = np.ascontiguousarray(bits, np.uint8)
+        self.lib.oref_set_bitfield(self.h, ptr(bits))
+
+    def render(self, args):
+        frame = np.zeros((args.height, args.width, 4), np.float32)
+        depth = np.zeros((args.height, args.width), np.float32)
+        if self.lib.oref_render(self.h, C.byref(args), ptr(frame), ptr(depth)) != 0:
+            raise RuntimeError(self.lib.oref_last_error().decode())
+        return frame, depth

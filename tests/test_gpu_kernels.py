@@ -1,0 +1,132 @@
+"""HIP kernels vs the scalar oracle, through the C-ABI (needs an MI355X).
+
+Tolerances: hash indices and trilinear weights bit-exact; hash features
+bit-exact (both accumulate with fmaf in corner order); MLP outputs within a
+few fp16 ulps (MFMA sums 32 products per instruction in its own order, the
+oracle sums sequentially); gradients within 1e-2 relative of the gradient norm.
+"""
+import numpy as np
+import pytest
+
+import ngp_abi as A
+from oracle_abi import Oracle
+
+pytestmark = pytest.mark.gpu
+
+CONFIGS = {
+    "B_L16F2T19": dict(n_levels=16, F=2, log2_T=19, n_neurons=64),
+    "base_L8F4T19": dict(n_levels=8, F=4, log2_T=19, n_neurons=64),
+    "A_L4F2T14": dict(n_levels=4, F=2, log2_T=14, n_neurons=16),
+    "E_L16F2T22": dict(n_levels=16, F=2, log2_T=22, n_neurons=64, aabb_scale=64),
+}
+
+
+def make(name, seed=0, grid_scale=0.5):
+    from gpu_util import GpuModel, random_params
+    cfg = A.default_config(**CONFIGS[name])
+    g = GpuModel(cfg)
+    o = Oracle(cfg)
+    rng = np.random.default_rng(seed)
+    p = random_params(g.n_params, g.n_mlp, g.info, rng, grid_scale)
+    g.set_params(p)
+    o.set_params(p)
+    return g, o, rng
+
+
+def random_coords(rng, n):
+    c = np.zeros((n, 7), np.float32)
+    c[:, :3] = rng.uniform(0, 1, (n, 3))
+    c[:, 3] = rng.uniform(0, 0.05, n)
+    d = rng.normal(size=(n, 3))
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    c[:, 4:7] = (d + 1) * 0.5
+    return c
+
+
+@pytest.mark.parametrize("name", list(CONFIGS))
+def test_hashgrid_indices_and_features_bit_exact(name):
+    g, o, rng = make(name)
+    try:
+        pos = rng.uniform(0, 1, (4096, 3)).astype(np.float32)
+        pos[:8] = [[0, 0, 0], [1, 1, 1], [0.5, 0.5, 0.5], [1, 0, 1], [0.999999, 1e-7, 0.5], [0.25, 0.75, 0.125],
+                   [0.0625, 0.0625, 0.0625], [1 / 3, 2 / 3, 1 / 7]]
+        gi, gw = g.encode_indices(pos)
+        oi, ow = o.encode_indices(pos)
+        np.testing.assert_array_equal(gi, oi)
+        np.testing.assert_array_equal(gw, ow)
+        ge = g.encode(pos).astype(np.float32)
+        oe = o.encode(pos)
+        np.testing.assert_array_equal(ge, oe)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("name", ["B_L16F2T19", "base_L8F4T19", "A_L4F2T14"])
+def test_infer_matches_oracle(name):
+    g, o, rng = make(name)
+    try:
+        coords = random_coords(rng, 3000)
+        go = g.infer(coords)
+        oo = o.infer(coords)
+        assert np.isfinite(go).all()
+        err = np.abs(go - oo)
+        tol = 4e-3 + 8e-3 * np.abs(oo)
+        assert (err <= tol).mean() > 0.999, f"max err {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
+        assert np.abs(go - oo).mean() < 1e-3
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
+def test_density_matches_oracle_and_infer(name):
+    g, o, rng = make(name)
+    try:
+        coords = random_coords(rng, 2000)
+        gd = g.density(coords[:, :3])
+        od = o.density(coords[:, :3])
+        np.testing.assert_allclose(gd, od, atol=4e-3, rtol=8e-3)
+        # density head of the full network equals NerfNetwork::density
+        gi = g.infer(coords)
+        np.testing.assert_array_equal(gi[:, 3], gd)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
+def test_mlp_backward_matches_oracle(name):
+    g, o, rng = make(name)
+    try:
+        n = 1000
+        coords = random_coords(rng, n)
+        enc = o.encode(coords[:, :3])  # fp16 values
+        dl = (rng.normal(0, 1e-2, (n, 4))).astype(np.float16).astype(np.float32)
+        w = rng.uniform(1, 2, n).astype(np.float32)
+        g.zero_grads()
+        gd = g.backward(enc, coords[:, 4:7], dl, w)
+        od = o.backward(enc, coords[:, 4:7], dl, w)
+        gg = g.get(A.GRADS_FP32)[: g.n_mlp]
+        og = o.get(A.GRADS_FP32)[: o.n_mlp]
+        rel = np.linalg.norm(gg - og) / np.linalg.norm(og)
+        assert rel < 1e-2, rel
+        dr = np.linalg.norm(gd - od) / max(np.linalg.norm(od), 1e-12)
+        assert dr < 1e-2, dr
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("name", ["B_L16F2T19", "base_L8F4T19"])
+def test_hashgrid_backward_matches_oracle(name):
+    g, o, rng = make(name)
+    try:
+        n = 2000
+        pos = rng.uniform(0, 1, (n, 3)).astype(np.float32)
+        denc = rng.normal(0, 1, (g.L, n, g.F)).astype(np.float16)
+        g.zero_grads()
+        g.encode_backward(pos, denc)
+        o.encode_backward(pos, denc.astype(np.float32))
+        gg = g.get(A.GRADS_FP32)[g.n_mlp:]
+        og = o.get(A.GRADS_FP32)[o.n_mlp:]
+        np.testing.assert_array_equal(gg != 0, og != 0)
+        np.testing.assert_allclose(gg, og, atol=1e-5, rtol=1e-4)
+    finally:
+        g.close()
