@@ -254,6 +254,30 @@ ngp_status ngp_accumulate_tonemap(const float* frame, float* accum, float* out, 
                                   uint32_t sample_count, int color_space, float exposure,
                                   const float* background_rgba, int output_srgb, ngp_stream stream);
 
+/* --- kernel timers (no reference counterpart: instrumentation for bench.py) ---------- */
+/* When enabled, each hot-path launch group is bracketed by HIP events on the stream it
+ * runs on; ngp_timing_read() synchronises those events and returns the summed duration,
+ * the number of launches and the algorithmic units processed (samples for encode/MLP,
+ * rays for sampler/loss/march, parameters for the optimizer).  Training-step units are
+ * known only on the device; they are attributed when ngp_train_read_stats() reads them. */
+enum {
+	NGP_TIMER_TRAIN_SAMPLER = 0,    /* generate_training_samples_nerf (rays)            */
+	NGP_TIMER_TRAIN_ENCODE = 1,     /* hash-grid forward over all samples (samples)     */
+	NGP_TIMER_TRAIN_MLP_INFER = 2,  /* fused MLP inference over all samples (samples)   */
+	NGP_TIMER_TRAIN_LOSS = 3,       /* compute_loss_kernel_train_nerf + compaction (rays)*/
+	NGP_TIMER_TRAIN_MLP_BWD = 4,    /* fused MLP fwd+bwd on the compacted batch (samples)*/
+	NGP_TIMER_TRAIN_ENCODE_BWD = 5, /* hash-grid backward scatter (samples)             */
+	NGP_TIMER_OPTIMIZER = 6,        /* Ema/ExponentialDecay/Adam step (params)          */
+	NGP_TIMER_GRID_UPDATE = 7,      /* density-grid evaluate + EMA + bitfield (cells)   */
+	NGP_TIMER_RENDER_ENCODE = 8,    /* render: hash-grid forward (samples)              */
+	NGP_TIMER_RENDER_MLP = 9,       /* render: fused MLP inference (samples)            */
+	NGP_TIMER_RENDER_MARCH = 10,    /* render: init/compact/generate/composite (rays)   */
+	NGP_TIMER_COUNT = 11
+};
+ngp_status ngp_timing_enable(ngp_model* model, int enable);
+ngp_status ngp_timing_read(ngp_model* model, int timer, double* total_ms, uint64_t* units, uint32_t* launches,
+                           int reset);
+
 const char* ngp_last_error(void);
 const char* ngp_version(void);
 

@@ -207,6 +207,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		for (int b = 0; b < 3; ++b) { r.payload[b].release(); r.rgba[b].release(); r.depth[b].release(); }
 		r.coords.release(); r.enc.release(); r.out.release(); r.counters.release();
 		if (r.host_counter.ptr) (void)hipHostFree(r.host_counter.ptr);
+		m->timers.release();
 		delete m;
 	});
 }
@@ -374,6 +375,15 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		st->n_rays = m->ts.last_n_rays;
 		st->measured_batch_size_before_compaction = c[0];
 		st->measured_batch_size = c[1];
+		KernelTimers& tm = m->timers;
+		if (tm.train_units_pending) {
+			const uint64_t all = std::min(c[0], m->ts.last_max_samples), comp = std::min(c[1], m->ts.last_target);
+			tm.units[NGP_TIMER_TRAIN_ENCODE] += all;
+			tm.units[NGP_TIMER_TRAIN_MLP_INFER] += all;
+			tm.units[NGP_TIMER_TRAIN_MLP_BWD] += comp;
+			tm.units[NGP_TIMER_TRAIN_ENCODE_BWD] += comp;
+			tm.train_units_pending = false;
+		}
 		float loss;
 		std::memcpy(&loss, &c[8], 4);
 		st->loss = loss;
@@ -403,8 +413,10 @@ ngp_status ngp_density_grid_update(ngp_model* m, const ngp_grid_args* a, ngp_str
 	return guarded([&] {
 		require(m && a, "null argument");
 		require(a->max_cascade < NERF_CASCADES, "max_cascade must be < 8");
+		m->timers.begin(NGP_TIMER_GRID_UPDATE, S(s));
 		run_grid_evaluate(m, a, S(s));
 		run_grid_finish(m, a, S(s));
+		m->timers.end(NGP_TIMER_GRID_UPDATE, S(s), (uint64_t)a->n_uniform_samples + a->n_nonuniform_samples);
 	});
 }
 
@@ -454,6 +466,30 @@ ngp_status ngp_accumulate_tonemap(const float* frame, float* accum, float* out, 
 	return guarded([&] {
 		require(frame && accum, "null argument");
 		run_accumulate_tonemap(frame, accum, out, W, H, spp, color_space, exposure, bg, output_srgb, S(s));
+	});
+}
+
+ngp_status ngp_timing_enable(ngp_model* m, int enable) {
+	return guarded([&] {
+		require(m, "null model");
+		m->timers.enabled = enable != 0;
+	});
+}
+
+ngp_status ngp_timing_read(ngp_model* m, int timer, double* total_ms, uint64_t* units, uint32_t* launches, int reset) {
+	return guarded([&] {
+		require(m, "null model");
+		require(timer >= 0 && timer < NGP_TIMER_COUNT, "unknown timer");
+		KernelTimers& t = m->timers;
+		t.collect();
+		if (total_ms) *total_ms = t.ms[timer];
+		if (units) *units = t.units[timer];
+		if (launches) *launches = t.launches[timer];
+		if (reset) {
+			t.ms[timer] = 0.0;
+			t.units[timer] = 0;
+			t.launches[timer] = 0;
+		}
 	});
 }
 

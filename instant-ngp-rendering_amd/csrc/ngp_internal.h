@@ -21,6 +21,67 @@ namespace ngp {
 		}                                                                                                 \
 	} while (0)
 
+// HIP-event timers around launch groups (ngp_timing_enable / ngp_timing_read).
+struct KernelTimers {
+	struct Pending {
+		int slot;
+		hipEvent_t a, b;
+	};
+	bool enabled = false;
+	bool train_units_pending = false;
+	std::vector<hipEvent_t> pool;
+	std::vector<Pending> pending;
+	hipEvent_t open[NGP_TIMER_COUNT] = {};
+	double ms[NGP_TIMER_COUNT] = {};
+	uint64_t units[NGP_TIMER_COUNT] = {};
+	uint32_t launches[NGP_TIMER_COUNT] = {};
+
+	hipEvent_t take() {
+		if (pool.empty()) {
+			hipEvent_t e;
+			NGP_HIP_CHECK(hipEventCreate(&e));
+			return e;
+		}
+		hipEvent_t e = pool.back();
+		pool.pop_back();
+		return e;
+	}
+	void begin(int slot, hipStream_t s) {
+		if (!enabled) return;
+		open[slot] = take();
+		NGP_HIP_CHECK(hipEventRecord(open[slot], s));
+	}
+	void end(int slot, hipStream_t s, uint64_t u = 0) {
+		if (!enabled || !open[slot]) return;
+		hipEvent_t e = take();
+		NGP_HIP_CHECK(hipEventRecord(e, s));
+		pending.push_back({slot, open[slot], e});
+		open[slot] = nullptr;
+		units[slot] += u;
+		++launches[slot];
+	}
+	void collect() {
+		for (const Pending& p : pending) {
+			NGP_HIP_CHECK(hipEventSynchronize(p.b));
+			float t = 0.f;
+			NGP_HIP_CHECK(hipEventElapsedTime(&t, p.a, p.b));
+			ms[p.slot] += t;
+			pool.push_back(p.a);
+			pool.push_back(p.b);
+		}
+		pending.clear();
+	}
+	void release() {
+		for (const Pending& p : pending) {
+			(void)hipEventDestroy(p.a);
+			(void)hipEventDestroy(p.b);
+		}
+		for (hipEvent_t e : pool) (void)hipEventDestroy(e);
+		pending.clear();
+		pool.clear();
+	}
+};
+
 constexpr uint32_t MAX_LEVELS = 32;
 constexpr uint32_t MAX_LAYERS = 8;
 
@@ -131,6 +192,7 @@ struct ngp_model {
 	ngp::RenderScratch rs;
 	ngp_train_stats last_stats{};
 	bool stats_pending = false;
+	ngp::KernelTimers timers;
 	uint32_t last_n_rays = 0;
 };
 

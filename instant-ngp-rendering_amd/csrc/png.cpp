@@ -1,0 +1,116 @@
+// png.cpp — minimal PNG decoder on zlib (the reference decodes with stb_image, src/nerf_loader.cu:520-560).
+#include "png.h"
+
+#include <zlib.h>
+
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <fstream>
+#include <iterator>
+
+namespace ngp {
+
+static uint32_t be32(const uint8_t* p) { return (uint32_t)p[0] << 24 | (uint32_t)p[1] << 16 | (uint32_t)p[2] << 8 | p[3]; }
+
+static int paeth(int a, int b, int c) {
+	const int p = a + b - c, pa = std::abs(p - a), pb = std::abs(p - b), pc = std::abs(p - c);
+	if (pa <= pb && pa <= pc) return a;
+	return pb <= pc ? b : c;
+}
+
+bool decode_png_memory(const uint8_t* d, size_t size, std::vector<uint8_t>& rgba, int& width, int& height,
+                       std::string& err) {
+	static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
+	if (size < 8 || std::memcmp(d, sig, 8) != 0) { err = "not a PNG file"; return false; }
+	size_t pos = 8;
+	uint32_t w = 0, h = 0;
+	int depth = 0, ctype = 0, interlace = 0;
+	std::vector<uint8_t> idat, plte, trns;
+	while (pos + 12 <= size) {
+		const uint32_t len = be32(d + pos);
+		const char* type = (const char*)d + pos + 4;
+		const uint8_t* body = d + pos + 8;
+		if (pos + 12 + len > size) { err = "truncated chunk"; return false; }
+		if (!std::strncmp(type, "IHDR", 4)) {
+			w = be32(body);
+			h = be32(body + 4);
+			depth = body[8];
+			ctype = body[9];
+			interlace = body[12];
+		} else if (!std::strncmp(type, "IDAT", 4)) idat.insert(idat.end(), body, body + len);
+		else if (!std::strncmp(type, "PLTE", 4)) plte.assign(body, body + len);
+		else if (!std::strncmp(type, "tRNS", 4)) trns.assign(body, body + len);
+		else if (!std::strncmp(type, "IEND", 4)) break;
+		pos += 12 + len;
+	}
+	if (!w || !h) { err = "missing IHDR"; return false; }
+	if (interlace) { err = "interlaced PNG unsupported"; return false; }
+	if (!(depth == 8 || depth == 16)) { err = "unsupported bit depth"; return false; }
+	int channels;
+	switch (ctype) {
+		case 0: channels = 1; break;
+		case 2: channels = 3; break;
+		case 3: channels = 1; if (depth != 8) { err = "palette depth"; return false; } break;
+		case 4: channels = 2; break;
+		case 6: channels = 4; break;
+		default: err = "unsupported color type"; return false;
+	}
+	const size_t bpp = (size_t)channels * (depth / 8);
+	const size_t stride = bpp * w;
+	std::vector<uint8_t> raw((stride + 1) * h);
+	uLongf out_len = (uLongf)raw.size();
+	if (uncompress(raw.data(), &out_len, idat.data(), (uLong)idat.size()) != Z_OK || out_len != raw.size()) {
+		err = "zlib inflate failed";
+		return false;
+	}
+	std::vector<uint8_t> img(stride * h);
+	for (uint32_t y = 0; y < h; ++y) {
+		const uint8_t f = raw[y * (stride + 1)];
+		const uint8_t* src = &raw[y * (stride + 1) + 1];
+		uint8_t* cur = &img[y * stride];
+		const uint8_t* prev = y ? &img[(y - 1) * stride] : nullptr;
+		for (size_t x = 0; x < stride; ++x) {
+			const int a = x >= bpp ? cur[x - bpp] : 0, b = prev ? prev[x] : 0, c = (prev && x >= bpp) ? prev[x - bpp] : 0;
+			int v = src[x];
+			switch (f) {
+				case 0: break;
+				case 1: v += a; break;
+				case 2: v += b; break;
+				case 3: v += (a + b) / 2; break;
+				case 4: v += paeth(a, b, c); break;
+				default: err = "bad filter"; return false;
+			}
+			cur[x] = (uint8_t)v;
+		}
+	}
+	width = (int)w;
+	height = (int)h;
+	rgba.assign((size_t)w * h * 4, 255);
+	const int step = depth / 8;  // 16-bit: keep the high byte
+	for (size_t i = 0; i < (size_t)w * h; ++i) {
+		const uint8_t* p = &img[i * bpp];
+		uint8_t* o = &rgba[i * 4];
+		switch (ctype) {
+			case 0: o[0] = o[1] = o[2] = p[0]; break;
+			case 2: o[0] = p[0]; o[1] = p[step]; o[2] = p[2 * step]; break;
+			case 3: {
+				const uint8_t k = p[0];
+				if ((size_t)k * 3 + 2 < plte.size()) { o[0] = plte[k * 3]; o[1] = plte[k * 3 + 1]; o[2] = plte[k * 3 + 2]; }
+				o[3] = k < trns.size() ? trns[k] : 255;
+			} break;
+			case 4: o[0] = o[1] = o[2] = p[0]; o[3] = p[step]; break;
+			case 6: o[0] = p[0]; o[1] = p[step]; o[2] = p[2 * step]; o[3] = p[3 * step]; break;
+		}
+	}
+	return true;
+}
+
+bool decode_png_file(const std::string& path, std::vector<uint8_t>& rgba, int& width, int& height, std::string& err) {
+	std::ifstream f(path, std::ios::binary);
+	if (!f) { err = "cannot open " + path; return false; }
+	std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+	return decode_png_memory(buf.data(), buf.size(), rgba, width, height, err);
+}
+
+}  // namespace ngp

@@ -1,0 +1,481 @@
+// pyngp.cpp — Python module `pyngp` over the MI355X Testbed.
+//
+// Mirrors the NeRF-relevant surface of the reference's bindings (src/python_api.cu:263-720):
+// same class/enum/attribute names and argument defaults, so scripts/run.py-style drivers
+// (`ngp.Testbed()`, `load_training_data`, `frame()`, `render(w, h, spp, linear)`, ...) run
+// unchanged.  GUI/VR/SDF/Image/Volume members are absent by design.
+#include <pybind11/functional.h>
+#include <pybind11/numpy.h>
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <cstring>
+#include <limits>
+
+#include "testbed.h"
+
+namespace py = pybind11;
+using namespace ngp;
+
+namespace {
+
+ETestbedMode mode_from_string(const std::string& s) {
+	std::string l = s;
+	for (auto& c : l) c = (char)std::tolower((unsigned char)c);
+	if (l == "nerf") return ETestbedMode::Nerf;
+	if (l == "sdf") return ETestbedMode::Sdf;
+	if (l == "image") return ETestbedMode::Image;
+	if (l == "volume") return ETestbedMode::Volume;
+	return ETestbedMode::None;
+}
+
+// mode_from_scene (src/common_host.cu:146-164)
+ETestbedMode mode_from_scene(const std::string& scene) {
+	auto ends = [&](const char* e) {
+		const size_t n = std::strlen(e);
+		if (scene.size() < n) return false;
+		for (size_t i = 0; i < n; ++i)
+			if (std::tolower((unsigned char)scene[scene.size() - n + i]) != e[i]) return false;
+		return true;
+	};
+	struct stat_probe {
+		static bool is_dir(const std::string& p) {
+			py::module_ os = py::module_::import("os");
+			return os.attr("path").attr("isdir")(p).cast<bool>();
+		}
+	};
+	if (stat_probe::is_dir(scene) || ends(".json")) return ETestbedMode::Nerf;
+	if (ends(".obj") || ends(".stl")) return ETestbedMode::Sdf;
+	if (ends(".nvdb")) return ETestbedMode::Volume;
+	if (ends(".exr") || ends(".bin") || ends(".png") || ends(".jpg")) return ETestbedMode::Image;
+	return ETestbedMode::None;
+}
+
+py::array_t<float> mat43_to_numpy(const Mat43& m) {
+	py::array_t<float> a({3, 4});
+	auto r = a.mutable_unchecked<2>();
+	for (int row = 0; row < 3; ++row)
+		for (int col = 0; col < 4; ++col) r(row, col) = m.m[3 * col + row];
+	return a;
+}
+
+std::array<float, 12> numpy_to_rowmajor34(py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+	if (a.ndim() != 2 || a.shape(1) != 4 || a.shape(0) < 3) throw std::runtime_error("expected a 3x4 (or 4x4) matrix");
+	std::array<float, 12> out;
+	auto r = a.unchecked<2>();
+	for (int row = 0; row < 3; ++row)
+		for (int col = 0; col < 4; ++col) out[row * 4 + col] = r(row, col);
+	return out;
+}
+
+Mat43 numpy_to_mat43(py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+	auto rm = numpy_to_rowmajor34(a);
+	Mat43 m;
+	for (int row = 0; row < 3; ++row)
+		for (int col = 0; col < 4; ++col) m.m[3 * col + row] = rm[row * 4 + col];
+	return m;
+}
+
+Json json_from_py(const py::object& o) {
+	py::module_ json = py::module_::import("json");
+	return Json::parse(json.attr("dumps")(o).cast<std::string>());
+}
+
+py::object json_to_py(const Json& j) {
+	py::module_ json = py::module_::import("json");
+	return json.attr("loads")(j.dump());
+}
+
+// Non-PNG decoder (the reference links stb_image; src/nerf_loader.cu:520-560): PIL, if importable.
+bool pil_decode(const std::string& path, std::vector<uint8_t>& rgba, int& w, int& h) {
+	py::gil_scoped_acquire gil;
+	try {
+		py::module_ image = py::module_::import("PIL.Image");
+		py::module_ np = py::module_::import("numpy");
+		py::object img = image.attr("open")(path).attr("convert")("RGBA");
+		py::array_t<uint8_t, py::array::c_style | py::array::forcecast> a = np.attr("asarray")(img);
+		h = (int)a.shape(0);
+		w = (int)a.shape(1);
+		rgba.assign(a.data(), a.data() + (size_t)w * h * 4);
+		return true;
+	} catch (const py::error_already_set&) {
+		return false;
+	}
+}
+
+// Views into the Testbed so Python can write `testbed.nerf.training.random_bg_color = False`
+// exactly like the reference (which exposes Nerf / Nerf::Training by reference).
+struct TrainingView {
+	Testbed* tb;
+};
+struct NerfView {
+	Testbed* tb;
+};
+
+struct BoundingBox {
+	vec3 min, max;
+};
+
+}  // namespace
+
+PYBIND11_MODULE(pyngp, m) {
+	m.doc() = "Instant neural graphics primitives — MI355X (gfx950) NeRF path";
+	m.def("free_temporary_memory", []() {});
+
+	py::enum_<ETestbedMode>(m, "TestbedMode")
+		.value("Nerf", ETestbedMode::Nerf)
+		.value("Sdf", ETestbedMode::Sdf)
+		.value("Image", ETestbedMode::Image)
+		.value("Volume", ETestbedMode::Volume)
+		.value("None", ETestbedMode::None)
+		.export_values();
+	m.def("mode_from_scene", &mode_from_scene);
+	m.def("mode_from_string", &mode_from_string);
+
+	py::enum_<ELossType>(m, "LossType")
+		.value("L2", ELossType::L2)
+		.value("L1", ELossType::L1)
+		.value("Mape", ELossType::Mape)
+		.value("Smape", ELossType::Smape)
+		.value("Huber", ELossType::Huber)
+		.value("SmoothL1", ELossType::Huber)
+		.value("LogL1", ELossType::LogL1)
+		.value("RelativeL2", ELossType::RelativeL2)
+		.export_values();
+	py::enum_<ENerfActivation>(m, "NerfActivation")
+		.value("None", ENerfActivation::None)
+		.value("ReLU", ENerfActivation::ReLU)
+		.value("Logistic", ENerfActivation::Logistic)
+		.value("Exponential", ENerfActivation::Exponential)
+		.export_values();
+	py::enum_<EColorSpace>(m, "ColorSpace")
+		.value("Linear", EColorSpace::Linear)
+		.value("SRGB", EColorSpace::SRGB)
+		.export_values();
+	py::enum_<ETonemapCurve>(m, "TonemapCurve")
+		.value("Identity", ETonemapCurve::Identity)
+		.value("ACES", ETonemapCurve::ACES)
+		.value("Hable", ETonemapCurve::Hable)
+		.value("Reinhard", ETonemapCurve::Reinhard)
+		.export_values();
+	py::enum_<ELensMode>(m, "LensMode")
+		.value("Perspective", ELensMode::Perspective)
+		.value("OpenCV", ELensMode::OpenCV)
+		.value("FTheta", ELensMode::FTheta)
+		.value("LatLong", ELensMode::LatLong)
+		.value("OpenCVFisheye", ELensMode::OpenCVFisheye)
+		.value("Equirectangular", ELensMode::Equirectangular)
+		.export_values();
+
+	py::class_<BoundingBox>(m, "BoundingBox")
+		.def(py::init<>())
+		.def(py::init([](vec3 a, vec3 b) { return BoundingBox{a, b}; }))
+		.def("center", [](const BoundingBox& b) {
+			return vec3{0.5f * (b.min[0] + b.max[0]), 0.5f * (b.min[1] + b.max[1]), 0.5f * (b.min[2] + b.max[2])};
+		})
+		.def("diag", [](const BoundingBox& b) { return vec3{b.max[0] - b.min[0], b.max[1] - b.min[1], b.max[2] - b.min[2]}; })
+		.def("contains", [](const BoundingBox& b, vec3 p) {
+			for (int k = 0; k < 3; ++k)
+				if (p[k] < b.min[k] || p[k] > b.max[k]) return false;
+			return true;
+		})
+		.def_readwrite("min", &BoundingBox::min)
+		.def_readwrite("max", &BoundingBox::max);
+
+	py::class_<Lens>(m, "Lens")
+		.def(py::init<>())
+		.def_readwrite("mode", &Lens::mode)
+		.def_property("params", [](const Lens& l) { return std::vector<float>(l.params, l.params + 7); },
+		              [](Lens& l, const std::vector<float>& v) {
+			              for (size_t i = 0; i < 7; ++i) l.params[i] = i < v.size() ? v[i] : 0.f;
+		              });
+
+	py::class_<TrainingImageMetadata>(m, "TrainingImageMetadata")
+		.def_readwrite("camera_distortion", &TrainingImageMetadata::lens)
+		.def_readwrite("lens", &TrainingImageMetadata::lens)
+		.def_readwrite("resolution", &TrainingImageMetadata::resolution)
+		.def_readwrite("principal_point", &TrainingImageMetadata::principal_point)
+		.def_readwrite("focal_length", &TrainingImageMetadata::focal_length);
+
+	py::class_<NerfDataset>(m, "NerfDataset")
+		.def_readonly("metadata", &NerfDataset::metadata)
+		.def_property_readonly("transforms", [](const NerfDataset& d) {
+			py::list l;
+			for (const auto& x : d.xforms) l.append(mat43_to_numpy(x));
+			return l;
+		})
+		.def_readonly("paths", &NerfDataset::paths)
+		.def_readonly("up", &NerfDataset::up)
+		.def_readonly("offset", &NerfDataset::offset)
+		.def_readonly("n_images", &NerfDataset::n_images)
+		.def_readonly("scale", &NerfDataset::scale)
+		.def_readonly("aabb_scale", &NerfDataset::aabb_scale)
+		.def_readonly("from_mitsuba", &NerfDataset::from_mitsuba)
+		.def_readonly("is_hdr", &NerfDataset::is_hdr);
+
+	py::class_<Testbed> testbed(m, "Testbed");
+
+	py::class_<NerfView> nerf(testbed, "Nerf");
+	py::class_<TrainingView>(nerf, "Training")
+#define TV_RW(name, field)                                                                                  \
+	.def_property(name, [](const TrainingView& v) { return v.tb->nerf.training.field; },                   \
+	              [](TrainingView& v, decltype(NerfTraining::field) x) { v.tb->nerf.training.field = x; })
+		TV_RW("random_bg_color", random_bg_color)
+		TV_RW("n_images_for_training", n_images_for_training)
+		TV_RW("linear_colors", linear_colors)
+		TV_RW("loss_type", loss_type)
+		TV_RW("snap_to_pixel_centers", snap_to_pixel_centers)
+		TV_RW("near_distance", near_distance)
+		TV_RW("density_grid_decay", density_grid_decay)
+		TV_RW("optimize_extrinsics", optimize_extrinsics)
+		TV_RW("optimize_distortion", optimize_distortion)
+		TV_RW("optimize_focal_length", optimize_focal_length)
+		TV_RW("optimize_exposure", optimize_exposure)
+		TV_RW("optimize_extra_dims", optimize_extra_dims)
+		TV_RW("optimize_per_image_latents", optimize_extra_dims)
+#undef TV_RW
+		.def_property_readonly("dataset", [](TrainingView& v) -> NerfDataset& { return v.tb->nerf.training.dataset; },
+		                       py::return_value_policy::reference_internal)
+		.def_property_readonly("transforms", [](TrainingView& v) {
+			py::list l;
+			for (const auto& x : v.tb->nerf.training.dataset.xforms) l.append(mat43_to_numpy(x));
+			return l;
+		})
+		.def("set_camera_intrinsics",
+		     [](TrainingView& v, int frame_idx, float fx, float fy, float cx, float cy, float k1, float k2, float p1, float p2,
+		        float k3, float k4, bool is_fisheye) {
+			     if (k1 != 0 || k2 != 0 || p1 != 0 || p2 != 0 || k3 != 0 || k4 != 0 || is_fisheye)
+				     throw std::runtime_error("lens distortion is not implemented on the MI355X path (perspective only)");
+			     v.tb->set_camera_intrinsics(frame_idx, fx, fy, cx, cy);
+		     },
+		     py::arg("frame_idx"), py::arg("fx") = 0.f, py::arg("fy") = 0.f, py::arg("cx") = -0.5f, py::arg("cy") = -0.5f,
+		     py::arg("k1") = 0.f, py::arg("k2") = 0.f, py::arg("p1") = 0.f, py::arg("p2") = 0.f, py::arg("k3") = 0.f,
+		     py::arg("k4") = 0.f, py::arg("is_fisheye") = false)
+		.def("set_camera_extrinsics",
+		     [](TrainingView& v, int frame_idx, py::array_t<float, py::array::c_style | py::array::forcecast> c2w, bool convert) {
+			     auto rm = numpy_to_rowmajor34(c2w);
+			     v.tb->set_camera_extrinsics(frame_idx, rm.data(), convert);
+		     },
+		     py::arg("frame_idx"), py::arg("camera_to_world"), py::arg("convert_to_ngp") = true)
+		.def("get_camera_extrinsics", [](TrainingView& v, int i) { return mat43_to_numpy(v.tb->get_camera_extrinsics(i)); },
+		     py::arg("frame_idx"))
+		.def("set_image",
+		     [](TrainingView& v, int frame_idx, py::array_t<float, py::array::c_style | py::array::forcecast> img,
+		        py::object depth_img, float depth_scale) {
+			     if (img.ndim() != 3 || img.shape(2) != 4) throw std::runtime_error("image should be (H,W,4)");
+			     if (!depth_img.is_none()) throw std::runtime_error("depth supervision is not implemented on the MI355X path");
+			     (void)depth_scale;
+			     v.tb->set_image(frame_idx, img.data(), (int)img.shape(1), (int)img.shape(0));
+		     },
+		     py::arg("frame_idx"), py::arg("img"), py::arg("depth_img") = py::none(), py::arg("depth_scale") = 1.0f)
+		.def("set_image_rgba8",
+		     [](TrainingView& v, int frame_idx, py::array_t<uint8_t, py::array::c_style | py::array::forcecast> img) {
+			     if (img.ndim() != 3 || img.shape(2) != 4) throw std::runtime_error("image should be (H,W,4) uint8");
+			     v.tb->set_image_rgba8(frame_idx, img.data(), (int)img.shape(1), (int)img.shape(0));
+		     },
+		     py::arg("frame_idx"), py::arg("img"));
+
+	nerf
+#define NV_RW(name, field) \
+	.def_property(name, [](const NerfView& v) { return v.tb->nerf.field; }, [](NerfView& v, decltype(Nerf::field) x) { v.tb->nerf.field = x; })
+		NV_RW("rgb_activation", rgb_activation)
+		NV_RW("density_activation", density_activation)
+		NV_RW("sharpen", sharpen)
+		NV_RW("render_with_lens_distortion", render_with_lens_distortion)
+		NV_RW("render_with_camera_distortion", render_with_lens_distortion)
+		NV_RW("render_min_transmittance", render_min_transmittance)
+		NV_RW("rendering_min_transmittance", render_min_transmittance)
+		NV_RW("cone_angle_constant", cone_angle_constant)
+		NV_RW("visualize_cameras", visualize_cameras)
+#undef NV_RW
+		.def_property_readonly("max_cascade", [](const NerfView& v) { return v.tb->nerf.max_cascade; })
+		.def_property_readonly("training", py::cpp_function([](NerfView& v) { return TrainingView{v.tb}; }, py::keep_alive<0, 1>()));
+
+	testbed
+		.def(py::init([](ETestbedMode mode) {
+			     auto* t = new Testbed(mode);
+			     t->image_decoder = &pil_decode;
+			     // configs/ ship next to the extension (the reference resolves root_dir()/configs/<mode>/)
+			     py::module_ os = py::module_::import("os");
+			     t->root_dir = os.attr("path").attr("dirname")(py::module_::import("pyngp").attr("__file__")).cast<std::string>();
+			     return t;
+		     }),
+		     py::arg("mode") = ETestbedMode::None)
+		.def_readonly("mode", &Testbed::mode)
+		.def("create_empty_nerf_dataset", &Testbed::create_empty_nerf_dataset, py::arg("n_images"), py::arg("aabb_scale") = 1,
+		     py::arg("is_hdr") = false)
+		.def("load_training_data", &Testbed::load_training_data, py::call_guard<py::gil_scoped_release>(), py::arg("path"))
+		.def("clear_training_data", [](Testbed& t) {
+			t.training_data_available = false;
+			t.nerf.training.dataset.metadata.clear();
+		})
+		.def("init_window", [](Testbed&, int, int, bool, bool) { throw std::runtime_error("No GUI on the MI355X build (headless only)."); },
+		     py::arg("width"), py::arg("height"), py::arg("hidden") = false, py::arg("second_window") = false)
+		.def("want_repl", [](Testbed&) { return false; })
+		.def("frame", &Testbed::frame, py::call_guard<py::gil_scoped_release>())
+		.def("render",
+		     [](Testbed& t, int width, int height, int spp, bool linear, float start_t, float end_t, float fps, float shutter) {
+			     (void)start_t, (void)end_t, (void)fps, (void)shutter;  // camera paths are out of scope
+			     std::vector<float> img;
+			     {
+				     py::gil_scoped_release rel;
+				     img = t.render(width, height, spp, linear);
+			     }
+			     py::array_t<float> a({height, width, 4});
+			     std::memcpy(a.mutable_data(), img.data(), img.size() * sizeof(float));
+			     return a;
+		     },
+		     py::arg("width") = 1920, py::arg("height") = 1080, py::arg("spp") = 1, py::arg("linear") = true,
+		     py::arg("start_t") = -1.f, py::arg("end_t") = -1.f, py::arg("fps") = 30.f, py::arg("shutter_fraction") = 1.0f)
+		.def("render_shard",
+		     [](Testbed& t, int width, int height, int spp, bool linear, uint32_t shard_index, uint32_t shard_count,
+		        uint32_t shard_rows) {
+			     std::vector<float> img;
+			     {
+				     py::gil_scoped_release rel;
+				     img = t.render(width, height, spp, linear, shard_index, shard_count, shard_rows);
+			     }
+			     py::array_t<float> a({height, width, 4});
+			     std::memcpy(a.mutable_data(), img.data(), img.size() * sizeof(float));
+			     return a;
+		     },
+		     py::arg("width"), py::arg("height"), py::arg("spp"), py::arg("linear"), py::arg("shard_index"),
+		     py::arg("shard_count"), py::arg("shard_rows") = 8u)
+		.def("render_to_device",
+		     [](Testbed& t, int width, int height, int spp, bool linear, uint32_t shard_index, uint32_t shard_count,
+		        uint32_t shard_rows) {
+			     py::gil_scoped_release rel;
+			     t.render(width, height, spp, linear, shard_index, shard_count, shard_rows, false);
+			     return (uintptr_t)t.render_frame_buffer();
+		     },
+		     "Render into the device frame buffer only (no PCIe readback); returns its device address.",
+		     py::arg("width") = 1920, py::arg("height") = 1080, py::arg("spp") = 1, py::arg("linear") = true,
+		     py::arg("shard_index") = 0u, py::arg("shard_count") = 1u, py::arg("shard_rows") = 8u)
+		.def("train", &Testbed::train, py::call_guard<py::gil_scoped_release>(), py::arg("batch_size"))
+		.def("reset", &Testbed::reset_network, py::arg("reset_density_grid") = true)
+		.def("reset_accumulation", [](Testbed& t, bool, bool) { t.reset_accumulation(); }, py::arg("due_to_camera_movement") = false,
+		     py::arg("immediate_redraw") = true)
+		.def("reload_network_from_file", &Testbed::reload_network_from_file, py::arg("path") = "")
+		.def("reload_network_from_json",
+		     [](Testbed& t, py::object j, const std::string& base) { t.reload_network_from_json(json_from_py(j), base); },
+		     py::arg("json"), py::arg("config_base_path") = "")
+		.def_property_readonly("network_config", [](const Testbed& t) { return json_to_py(t.network_config()); })
+		.def("n_params", [](const Testbed& t) -> size_t {
+			if (!t.model()) return 0;
+			ngp_model_info i{};
+			ngp_model_get_info(t.model(), &i);
+			return i.n_params;
+		})
+		.def("n_encoding_params", [](const Testbed& t) -> size_t {
+			if (!t.model()) return 0;
+			ngp_model_info i{};
+			ngp_model_get_info(t.model(), &i);
+			return i.n_params - i.n_mlp_params;
+		})
+		.def("save_snapshot", &Testbed::save_snapshot, py::arg("path"), py::arg("include_optimizer_state") = false,
+		     py::arg("compress") = true)
+		.def("load_snapshot", &Testbed::load_snapshot, py::arg("path"))
+		.def("load_file", &Testbed::load_file, py::arg("path"))
+		.def_readwrite("background_color", &Testbed::background_color)
+		.def_readwrite("shall_train", &Testbed::shall_train)
+		.def_readwrite("shall_train_encoding", &Testbed::train_encoding)
+		.def_readwrite("shall_train_network", &Testbed::train_network)
+		.def_readwrite("render_groundtruth", &Testbed::render_ground_truth)
+		.def_readwrite("render_ground_truth", &Testbed::render_ground_truth)
+		.def_readwrite("render_near_distance", &Testbed::render_near_distance)
+		.def_readwrite("exposure", &Testbed::exposure)
+		.def_property("scale", [](const Testbed& t) { return t.scale; },
+		              [](Testbed& t, float s) {
+			              // Testbed::set_scale: move the camera along the view direction, keeping look_at fixed
+			              const float prev = t.scale;
+			              for (int k = 0; k < 3; ++k) t.camera.m[9 + k] += (prev - s) * t.camera.m[6 + k];
+			              t.scale = s;
+		              })
+		.def_property("aabb", [](const Testbed& t) { return BoundingBox{t.aabb_min, t.aabb_max}; },
+		              [](Testbed& t, const BoundingBox& b) {
+			              t.aabb_min = b.min;
+			              t.aabb_max = b.max;
+		              })
+		.def_property("fov", &Testbed::fov, &Testbed::set_fov)
+		.def_readwrite("fov_axis", &Testbed::fov_axis)
+		.def_readwrite("zoom", &Testbed::zoom)
+		.def_readwrite("screen_center", &Testbed::screen_center)
+		.def_readwrite("relative_focal_length", &Testbed::relative_focal_length)
+		.def_readwrite("training_batch_size", &Testbed::training_batch_size)
+		.def("set_nerf_camera_matrix",
+		     [](Testbed& t, py::array_t<float, py::array::c_style | py::array::forcecast> c) {
+			     auto rm = numpy_to_rowmajor34(c);
+			     t.camera = t.nerf.training.dataset.nerf_matrix_to_ngp(rm.data());
+		     })
+		.def("set_camera_to_training_view", &Testbed::set_camera_to_training_view)
+		.def("first_training_view", [](Testbed& t) { t.set_camera_to_training_view(0); })
+		.def("last_training_view", [](Testbed& t) { t.set_camera_to_training_view((int)t.nerf.training.dataset.n_images - 1); })
+		.def("previous_training_view", [](Testbed& t) {
+			const int n = (int)t.nerf.training.dataset.n_images;
+			t.set_camera_to_training_view((t.nerf.training.view + n - 1) % std::max(n, 1));
+		})
+		.def("next_training_view", [](Testbed& t) {
+			const int n = (int)t.nerf.training.dataset.n_images;
+			t.set_camera_to_training_view((t.nerf.training.view + 1) % std::max(n, 1));
+		})
+		.def("reset_camera", &Testbed::reset_camera)
+		.def_property("camera_matrix", [](const Testbed& t) { return mat43_to_numpy(t.camera); },
+		              [](Testbed& t, py::array_t<float, py::array::c_style | py::array::forcecast> a) { t.camera = numpy_to_mat43(a); })
+		.def_property("view_dir", [](const Testbed& t) { return t.camera.col(2); },
+		              [](Testbed& t, vec3 d) {
+			              // Testbed::set_view_dir: re-orthonormalise right/down around the new forward
+			              const float n = std::sqrt(d[0] * d[0] + d[1] * d[1] + d[2] * d[2]);
+			              for (auto& x : d) x /= n;
+			              const vec3 look = {t.camera.m[9] + d[0] * t.scale, t.camera.m[10] + d[1] * t.scale, t.camera.m[11] + d[2] * t.scale};
+			              (void)look;
+			              t.camera.set_col(2, d);
+		              })
+		.def_property("look_at",
+		              [](const Testbed& t) {
+			              return vec3{t.camera.m[9] + t.camera.m[6] * t.scale, t.camera.m[10] + t.camera.m[7] * t.scale,
+			                          t.camera.m[11] + t.camera.m[8] * t.scale};
+		              },
+		              [](Testbed& t, vec3 p) {
+			              for (int k = 0; k < 3; ++k) t.camera.m[9 + k] = p[k] - t.camera.m[6 + k] * t.scale;
+		              })
+		.def_property_readonly("loss", [](const Testbed& t) { return t.loss; })
+		.def_readonly("training_step", &Testbed::training_step)
+		.def_readwrite("color_space", &Testbed::color_space)
+		.def_readwrite("tonemap_curve", &Testbed::tonemap_curve)
+		.def_readwrite("snap_to_pixel_centers", &Testbed::snap_to_pixel_centers)
+		.def_readwrite("root_dir", &Testbed::root_dir)
+		.def_readwrite("seed", &Testbed::seed)
+		.def_readonly("data_path", &Testbed::data_path)
+		.def_readonly("training_ms", &Testbed::training_ms)
+		.def_readonly("training_prep_ms", &Testbed::training_prep_ms)
+		.def_readonly("render_ms", &Testbed::render_ms)
+		.def_property_readonly("nerf", py::cpp_function([](Testbed& t) { return NerfView{&t}; }, py::keep_alive<0, 1>()))
+		.def("density_grid", [](const Testbed& t) {
+			auto g = t.density_grid();
+			return py::array_t<float>(g.size(), g.data());
+		})
+		.def("density_grid_bitfield", [](const Testbed& t) {
+			auto b = t.density_grid_bitfield();
+			return py::array_t<uint8_t>(b.size(), b.data());
+		})
+		.def("last_train_stats", [](const Testbed& t) {
+			const ngp_train_stats s = t.last_stats();
+			py::dict d;
+			d["loss"] = s.loss;
+			d["measured_batch_size"] = s.measured_batch_size;
+			d["measured_batch_size_before_compaction"] = s.measured_batch_size_before_compaction;
+			d["rays_per_batch"] = t.nerf.training.counters_rgb.rays_per_batch;
+			d["n_rays"] = s.n_rays;
+			return d;
+		})
+		.def("sync", &Testbed::sync)
+		.def_property_readonly("model_handle", [](const Testbed& t) { return (uintptr_t)t.model(); })
+		.def_property_readonly("stream_handle", [](const Testbed& t) { return (uintptr_t)t.stream(); })
+		// multi-GPU: one Testbed per rank (torchrun); gradients/grid all-reduced over RCCL
+		.def_static("nccl_unique_id", []() { return py::bytes(Testbed::nccl_unique_id()); })
+		.def("init_distributed",
+		     [](Testbed& t, int rank, int world, py::bytes uid) { t.init_distributed(rank, world, std::string(uid)); },
+		     py::arg("rank"), py::arg("world_size"), py::arg("unique_id"))
+		.def_property_readonly("rank", &Testbed::rank)
+		.def_property_readonly("world_size", &Testbed::world_size);
+}

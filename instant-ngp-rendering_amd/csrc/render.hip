@@ -332,7 +332,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	auto P = [&](int b) { return reinterpret_cast<Payload*>(rs.payload[b].ptr); };
 	auto C = [&](int b) { return reinterpret_cast<float4*>(rs.rgba[b].ptr); };
 
+	KernelTimers& tm = m->timers;
+	tm.begin(NGP_TIMER_RENDER_MARCH, s);
 	k_render_init<<<div_up(n, 256), 256, 0, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer);
+	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
 	NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, 4 * sizeof(uint32_t), s));
 
@@ -345,20 +348,30 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const int cur = (db + 1) % 2, tmp = db % 2;
 		++db;
 		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
+		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_compact<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(tmp), C(tmp), rs.depth[tmp].ptr, P(cur), C(cur),
 		                                               rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr, rs.counters.ptr);
+		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 		NGP_HIP_CHECK(hipStreamSynchronize(s));
 		n_alive = rs.host_counter.ptr[0];
 		if (n_alive == 0) break;
 		const uint32_t target = 2 * 1024 * 1024;
 		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), 8u);
+		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_generate<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
+		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
+		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
 		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s);
+		tm.end(NGP_TIMER_RENDER_ENCODE, s, n_elements);
+		tm.begin(NGP_TIMER_RENDER_MLP, s);
 		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s);
+		tm.end(NGP_TIMER_RENDER_MLP, s, n_elements);
+		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, it, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
 		                                                 rs.out.ptr, n_steps);
+		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
 		it += n_steps;
 	}

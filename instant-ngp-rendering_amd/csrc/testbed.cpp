@@ -1,0 +1,1126 @@
+// testbed.cpp — host Testbed for the MI355X NeRF path.  Every device operation is a
+// call into libngp_hip.so (include/ngp_hip.h); this file holds only the host-side
+// orchestration the reference keeps in src/testbed.cu / src/testbed_nerf.cu.
+#include "testbed.h"
+
+#include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cctype>
+#include <iterator>
+#include <chrono>
+#include <cmath>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <dirent.h>
+#include <fstream>
+#include <sstream>
+#include <stdexcept>
+#include <sys/stat.h>
+
+#include "ngp_math.h"
+#include "png.h"
+
+namespace ngp {
+
+namespace {
+
+constexpr float PI_F = 3.14159265358979323846f;
+constexpr float LOSS_SCALE = 128.0f;  // testbed.h:390
+
+void ck(ngp_status s) {
+	if (s != NGP_OK) throw std::runtime_error(ngp_last_error());
+}
+void hk(hipError_t e, const char* what) {
+	if (e != hipSuccess) throw std::runtime_error(std::string("HIP error ") + hipGetErrorString(e) + " in " + what);
+}
+void nk(ncclResult_t r, const char* what) {
+	if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r) + " in " + what);
+}
+
+bool file_exists(const std::string& p) {
+	struct stat st;
+	return stat(p.c_str(), &st) == 0;
+}
+bool is_directory(const std::string& p) {
+	struct stat st;
+	return stat(p.c_str(), &st) == 0 && S_ISDIR(st.st_mode);
+}
+std::string parent_path(const std::string& p) {
+	const size_t k = p.find_last_of('/');
+	return k == std::string::npos ? std::string(".") : p.substr(0, k);
+}
+std::string extension(const std::string& p) {
+	const size_t s = p.find_last_of('/');
+	const size_t k = p.find_last_of('.');
+	if (k == std::string::npos || (s != std::string::npos && k < s)) return "";
+	std::string e = p.substr(k + 1);
+	std::transform(e.begin(), e.end(), e.begin(), ::tolower);
+	return e;
+}
+std::string basename_of(const std::string& p) {
+	const size_t k = p.find_last_of('/');
+	return k == std::string::npos ? p : p.substr(k + 1);
+}
+std::string read_text(const std::string& path) {
+	std::ifstream f(path);
+	if (!f) throw std::runtime_error("Could not open '" + path + "'.");
+	std::stringstream ss;
+	ss << f.rdbuf();
+	return ss.str();
+}
+float fov_to_focal_length(int resolution, float degrees) { return 0.5f * (float)resolution / std::tan(0.5f * degrees * PI_F / 180.0f); }
+float focal_length_to_fov(float resolution, float focal) { return 2.0f * 180.0f / PI_F * std::atan(resolution / (focal * 2.0f)); }
+
+uint32_t next_multiple_host(uint32_t a, uint32_t b) { return (a + b - 1) / b * b; }
+
+float srgb_to_linear_h(float s) { return s <= 0.04045f ? s / 12.92f : std::pow((s + 0.055f) / 1.055f, 2.4f); }
+float linear_to_srgb_h(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * std::pow(l, 0.41666f) - 0.055f; }
+
+}  // namespace
+
+// SI::natural-style comparison key: digit runs compare numerically.
+std::string natural_sort_key(const std::string& s) {
+	std::string out;
+	for (size_t i = 0; i < s.size();) {
+		if (std::isdigit((unsigned char)s[i])) {
+			size_t j = i;
+			while (j < s.size() && std::isdigit((unsigned char)s[j])) ++j;
+			std::string digits = s.substr(i, j - i);
+			digits.erase(0, std::min(digits.find_first_not_of('0'), digits.size() - 1));
+			out += (char)('0' + std::min<size_t>(digits.size(), 9));
+			out += digits;
+			i = j;
+		} else out += s[i++];
+	}
+	return out;
+}
+
+// nerf_loader.h:95-116 (non-Mitsuba): flip y/z columns, scale + offset, cycle axes xyz <- yzx.
+Mat43 NerfDataset::nerf_matrix_to_ngp(const float* r, bool scale_columns) const {
+	float c[4][3];
+	for (int col = 0; col < 4; ++col)
+		for (int row = 0; row < 3; ++row) c[col][row] = r[row * 4 + col];
+	for (int row = 0; row < 3; ++row) {
+		c[0][row] *= scale_columns ? scale : 1.f;
+		c[1][row] *= scale_columns ? -scale : -1.f;
+		c[2][row] *= scale_columns ? -scale : -1.f;
+		c[3][row] = c[3][row] * scale + offset[row];
+	}
+	Mat43 m;
+	for (int col = 0; col < 4; ++col) {
+		m.m[3 * col + 0] = c[col][1];
+		m.m[3 * col + 1] = c[col][2];
+		m.m[3 * col + 2] = c[col][0];
+	}
+	return m;
+}
+
+Mat43 NerfDataset::ngp_matrix_to_nerf(const Mat43& in, bool scale_columns) const {
+	Mat43 m;
+	for (int col = 0; col < 4; ++col) {
+		m.m[3 * col + 0] = in.m[3 * col + 2];
+		m.m[3 * col + 1] = in.m[3 * col + 0];
+		m.m[3 * col + 2] = in.m[3 * col + 1];
+	}
+	for (int row = 0; row < 3; ++row) {
+		m.m[0 * 3 + row] *= scale_columns ? 1.f / scale : 1.f;
+		m.m[1 * 3 + row] *= scale_columns ? -1.f / scale : -1.f;
+		m.m[2 * 3 + row] *= scale_columns ? -1.f / scale : -1.f;
+		m.m[3 * 3 + row] = (m.m[3 * 3 + row] - offset[row]) / scale;
+	}
+	return m;
+}
+
+Testbed::Testbed(ETestbedMode m) {
+	int device = 0;
+	if (const char* lr = std::getenv("LOCAL_RANK")) device = std::atoi(lr);
+	int n_dev = 0;
+	hk(hipGetDeviceCount(&n_dev), "hipGetDeviceCount");
+	if (n_dev <= 0) throw std::runtime_error("Testbed requires an AMD GPU (no HIP device found).");
+	device = device % n_dev;
+	hk(hipSetDevice(device), "hipSetDevice");
+	hipStream_t s;
+	hk(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+	m_stream = s;
+	// Testbed constructor default network config (src/testbed.cu:3954-3980)
+	m_network_config = Json::parse(R"({
+		"loss": {"otype": "L2"},
+		"optimizer": {"otype": "Adam", "learning_rate": 1e-3, "beta1": 0.9, "beta2": 0.99, "epsilon": 1e-15, "l2_reg": 1e-6},
+		"encoding": {"otype": "HashGrid", "n_levels": 16, "n_features_per_level": 2, "log2_hashmap_size": 19, "base_resolution": 16},
+		"network": {"otype": "FullyFusedMLP", "n_neurons": 64, "n_layers": 2, "activation": "ReLU", "output_activation": "None"}
+	})");
+	mode = m;
+	reset_camera();
+}
+
+Testbed::~Testbed() {
+	try {
+		sync();
+	} catch (...) {
+	}
+	if (m_model) ngp_model_destroy(m_model);
+	free_device_dataset();
+	for (float* p : {m_frame, m_depth, m_accum, m_out})
+		if (p) (void)hipFree(p);
+	if (m_red_buf) (void)hipFree(m_red_buf);
+	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
+	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
+}
+
+void Testbed::sync() const { hk(hipStreamSynchronize((hipStream_t)m_stream), "hipStreamSynchronize"); }
+
+// ---------------------------------------------------------------------------
+// Data
+// ---------------------------------------------------------------------------
+void Testbed::load_file(const std::string& path) {
+	const std::string ext = extension(path);
+	if (ext == "ingp" || ext == "msgpack" || ext == "ngpmi") {
+		load_snapshot(path);
+		return;
+	}
+	if (ext == "json" && path.find("transforms") == std::string::npos && file_exists(path)) {
+		const Json j = Json::parse(read_text(path));
+		if (!j.contains("frames")) {
+			reload_network_from_file(path);
+			return;
+		}
+	}
+	load_training_data(path);
+}
+
+void Testbed::load_training_data(const std::string& path) {
+	if (!file_exists(path)) throw std::runtime_error("Data path '" + path + "' does not exist.");
+	// mode_from_scene (src/common_host.cu:146-164)
+	ETestbedMode scene_mode = ETestbedMode::None;
+	const std::string ext = extension(path);
+	if (is_directory(path) || ext == "json") scene_mode = ETestbedMode::Nerf;
+	if (path.find("geometry") != std::string::npos) scene_mode = ETestbedMode::Geometry;
+	if (ext == "obj" || ext == "stl") scene_mode = ETestbedMode::Sdf;
+	if (ext == "nvdb") scene_mode = ETestbedMode::Volume;
+	if (ext == "exr" || ext == "bin" || ext == "png" || ext == "jpg") scene_mode = ETestbedMode::Image;
+	if (scene_mode == ETestbedMode::None) throw std::runtime_error("Unknown scene format for path '" + path + "'.");
+	if (scene_mode != ETestbedMode::Nerf)
+		throw std::runtime_error("This build implements the NeRF primitive only (SDF/Image/Volume/Geometry are out of scope).");
+	if (mode != ETestbedMode::Nerf) {
+		// Testbed::set_mode (src/testbed.cu:165-218): drop mode-specific state and the network
+		if (m_model) {
+			sync();
+			ngp_model_destroy(m_model);
+			m_model = nullptr;
+		}
+		nerf = Nerf{};
+		free_device_dataset();
+		training_data_available = false;
+		mode = ETestbedMode::Nerf;
+		reset_camera();
+	}
+	data_path = path;
+
+	std::vector<std::string> json_paths;
+	if (is_directory(path)) {
+		DIR* d = opendir(path.c_str());
+		if (d) {
+			while (dirent* e = readdir(d)) {
+				const std::string f = path + "/" + e->d_name;
+				if (!is_directory(f) && extension(f) == "json") json_paths.push_back(f);
+			}
+			closedir(d);
+		}
+		std::sort(json_paths.begin(), json_paths.end());
+	} else {
+		json_paths.push_back(path);
+	}
+	if (json_paths.empty()) throw std::runtime_error("Cannot load NeRF data from an empty set of paths.");
+
+	// ngp::load_nerf (src/nerf_loader.cu:273-743)
+	const int prev_aabb_scale = nerf.training.dataset.aabb_scale;
+	NerfDataset ds;
+	ds.scale = 0.33f;
+	ds.offset = {0.5f, 0.5f, 0.5f};
+	static const char* formats[] = {"png", "jpg", "jpeg", "bmp", "gif", "tga", "pic", "pnm", "psd", "exr"};
+	for (const std::string& jp : json_paths) {
+		const Json j = Json::parse(read_text(jp));
+		if (!j.contains("frames") || !j["frames"].is_array()) continue;
+		const std::string base = parent_path(jp);
+		if (j.contains("scale")) ds.scale = (float)j["scale"].num();
+		if (j.contains("aabb_scale")) ds.aabb_scale = (int)j["aabb_scale"].num();
+		if (j.contains("offset")) {
+			if (j["offset"].is_array()) ds.offset = {(float)j["offset"][0].num(), (float)j["offset"][1].num(), (float)j["offset"][2].num()};
+			else ds.offset = {(float)j["offset"].num(), (float)j["offset"].num(), (float)j["offset"].num()};
+		}
+		if (j.contains("aabb")) {
+			const Json& a = j["aabb"];
+			float len = 1e-6f;
+			for (int k = 0; k < 3; ++k) len = std::max(len, std::fabs((float)a[1][k].num() - (float)a[0][k].num()));
+			ds.scale = 1.f / len;
+			for (int k = 0; k < 3; ++k) ds.offset[k] = (((float)a[1][k].num() + (float)a[0][k].num()) * 0.5f) * -ds.scale + 0.5f;
+		}
+		if (j.contains("up")) ds.up = {(float)j["up"][1].num(), (float)j["up"][2].num(), (float)j["up"][0].num()};
+		// frames sorted naturally by file_path (src/nerf_loader.cu:347-349)
+		std::vector<Json> frames = j["frames"].elements();
+		std::stable_sort(frames.begin(), frames.end(), [](const Json& a, const Json& b) {
+			return natural_sort_key(a.value("file_path", std::string())) < natural_sort_key(b.value("file_path", std::string()));
+		});
+		if (j.contains("n_frames")) frames.resize(std::min(frames.size(), (size_t)j["n_frames"].num()));
+		// read_lens / principal point (src/nerf_loader.cu:175-220)
+		auto read_lens = [](const Json& src, Lens& lens, vec2& pp) {
+			const ELensMode opencv = src.value("is_fisheye", false) ? ELensMode::OpenCVFisheye : ELensMode::OpenCV;
+			ELensMode mode_l = ELensMode::Perspective;
+			auto par = [&](const char* n, int idx) {
+				if (src.contains(n)) {
+					lens.params[idx] = (float)src[n].num();
+					if (lens.params[idx] != 0.f) mode_l = opencv;
+				}
+			};
+			par("k1", 0); par("k2", 1); par("k3", 2); par("k4", 3); par("p1", 2); par("p2", 3);
+			if (src.contains("cx")) pp[0] = (float)src["cx"].num() / (float)src["w"].num();
+			if (src.contains("cy")) pp[1] = (float)src["cy"].num() / (float)src["h"].num();
+			if (src.contains("latlong")) mode_l = ELensMode::LatLong;
+			if (src.contains("equirectangular")) mode_l = ELensMode::Equirectangular;
+			if (mode_l != ELensMode::Perspective) lens.mode = mode_l;
+		};
+		auto read_focal = [](const Json& src, vec2& fl, int rx, int ry) {
+			auto one = [&](int res, const std::string& axis) -> float {
+				if (src.contains(axis + "_fov")) return fov_to_focal_length(res, (float)src[axis + "_fov"].num());
+				if (src.contains("fl_" + axis)) return (float)src["fl_" + axis].num();
+				if (src.contains("camera_angle_" + axis)) return fov_to_focal_length(res, (float)src["camera_angle_" + axis].num() * 180.f / PI_F);
+				return 0.f;
+			};
+			const float x = one(rx, "x"), y = one(ry, "y");
+			if (x != 0) { fl = {x, y != 0 ? y : x}; return true; }
+			if (y != 0) { fl = {y, y}; return true; }
+			return false;
+		};
+		Lens lens;
+		vec2 pp = {0.5f, 0.5f};
+		read_lens(j, lens, pp);
+		for (const Json& fr : frames) {
+			std::string fp = fr.value("file_path", std::string());
+			std::replace(fp.begin(), fp.end(), '\\', '/');
+			std::string p = (!fp.empty() && fp[0] == '/') ? fp : base + "/" + fp;
+			if (extension(p).empty() && !file_exists(p)) {
+				for (const char* f : formats)
+					if (file_exists(p + "." + f)) { p = p + "." + f; break; }
+			}
+			if (!file_exists(p)) throw std::runtime_error("Could not find image file '" + p + "'.");
+			std::vector<uint8_t> rgba;
+			int w = 0, h = 0;
+			std::string err;
+			if (!decode_png_file(p, rgba, w, h, err)) {
+				if (!image_decoder || !image_decoder(p, rgba, w, h))
+					throw std::runtime_error("Could not open image file: " + p + " (" + err + ")");
+			}
+			TrainingImageMetadata md;
+			md.resolution = {w, h};
+			md.principal_point = pp;
+			md.lens = lens;
+			bool got = read_focal(j, md.focal_length, w, h);
+			got |= read_focal(fr, md.focal_length, w, h);
+			if (!got) throw std::runtime_error("Couldn't read fov.");
+			read_lens(fr, md.lens, md.principal_point);
+			const Json& tm = fr.contains("transform_matrix_start") ? fr["transform_matrix_start"] : fr["transform_matrix"];
+			float r[12];
+			for (int row = 0; row < 3; ++row)
+				for (int col = 0; col < 4; ++col) r[row * 4 + col] = (float)tm[row][col].num();
+			ds.xforms.push_back(ds.nerf_matrix_to_ngp(r));
+			ds.metadata.push_back(md);
+			ds.paths.push_back(fp);
+			ds.pixels.push_back(std::move(rgba));
+		}
+	}
+	ds.n_images = ds.metadata.size();
+	if (ds.n_images == 0) throw std::invalid_argument("No training images were found for NeRF training!");
+	nerf.training.dataset = std::move(ds);
+	if (nerf.training.dataset.aabb_scale != prev_aabb_scale && m_model) reset_network();
+	load_nerf_post();
+	training_data_available = true;
+}
+
+void Testbed::create_empty_nerf_dataset(size_t n_images, int aabb_scale, bool is_hdr) {
+	data_path.clear();
+	mode = ETestbedMode::Nerf;
+	NerfDataset ds;
+	ds.n_images = n_images;
+	ds.aabb_scale = aabb_scale;
+	ds.is_hdr = is_hdr;
+	ds.scale = 1.0f;
+	ds.offset = {0.f, 0.f, 0.f};
+	ds.metadata.resize(n_images);
+	ds.xforms.resize(n_images);
+	ds.paths.resize(n_images);
+	ds.pixels.resize(n_images);
+	nerf.training.dataset = std::move(ds);
+	load_nerf_post();
+	nerf.training.n_images_for_training = 0;
+	training_data_available = true;
+}
+
+// Testbed::load_nerf_post (src/testbed_nerf.cu:2151-2238)
+void Testbed::load_nerf_post() {
+	NerfDataset& ds = nerf.training.dataset;
+	nerf.rgb_activation = ds.is_hdr ? ENerfActivation::Exponential : ENerfActivation::Logistic;
+	nerf.training.n_images_for_training = (int)ds.n_images;
+	if (!ds.metadata.empty()) screen_center = {1.f - ds.metadata[0].principal_point[0], 1.f - ds.metadata[0].principal_point[1]};
+	if (ds.aabb_scale <= 0 || (ds.aabb_scale & (ds.aabb_scale - 1)))
+		throw std::runtime_error("NeRF dataset's `aabb_scale` must be a power of two, but is " + std::to_string(ds.aabb_scale) + ".");
+	const int max_aabb_scale = 1 << (NERF_CASCADES - 1);
+	if (ds.aabb_scale > max_aabb_scale) throw std::runtime_error("NeRF dataset must have `aabb_scale <= 128`.");
+	const float half = 0.5f * (float)std::min(max_aabb_scale, ds.aabb_scale);
+	aabb_min = {0.5f - half, 0.5f - half, 0.5f - half};
+	aabb_max = {0.5f + half, 0.5f + half, 0.5f + half};
+	nerf.max_cascade = 0;
+	while ((1 << nerf.max_cascade) < ds.aabb_scale) ++nerf.max_cascade;
+	nerf.cone_angle_constant = ds.aabb_scale <= 1 ? 0.0f : (1.0f / 256.0f);
+	m_dataset_dirty = true;
+}
+
+void Testbed::set_image_rgba8(int frame_idx, const uint8_t* rgba, int width, int height) {
+	NerfDataset& ds = nerf.training.dataset;
+	if (frame_idx < 0 || (size_t)frame_idx >= ds.n_images) throw std::runtime_error("Invalid frame index");
+	ds.pixels[frame_idx].assign(rgba, rgba + (size_t)width * height * 4);
+	ds.metadata[frame_idx].resolution = {width, height};
+	m_dataset_dirty = true;
+}
+
+// Nerf::Training::set_image (python_api.cu): float RGBA (linear, premultiplied) -> RGBA8 sRGB straight alpha.
+void Testbed::set_image(int frame_idx, const float* rgba, int width, int height) {
+	std::vector<uint8_t> px((size_t)width * height * 4);
+	for (size_t i = 0; i < (size_t)width * height; ++i) {
+		const float a = std::min(std::max(rgba[4 * i + 3], 0.f), 1.f);
+		for (int k = 0; k < 3; ++k) {
+			const float lin = a > 0 ? rgba[4 * i + k] / a : 0.f;
+			px[4 * i + k] = (uint8_t)std::lround(std::min(std::max(linear_to_srgb_h(lin), 0.f), 1.f) * 255.f);
+		}
+		px[4 * i + 3] = (uint8_t)std::lround(a * 255.f);
+	}
+	set_image_rgba8(frame_idx, px.data(), width, height);
+}
+
+void Testbed::set_camera_extrinsics(int frame_idx, const float* c2w, bool convert_to_ngp) {
+	NerfDataset& ds = nerf.training.dataset;
+	if (frame_idx < 0 || (size_t)frame_idx >= ds.n_images) throw std::runtime_error("Invalid frame index");
+	if (convert_to_ngp) ds.xforms[frame_idx] = ds.nerf_matrix_to_ngp(c2w);
+	else {
+		Mat43 m;
+		for (int col = 0; col < 4; ++col)
+			for (int row = 0; row < 3; ++row) m.m[3 * col + row] = c2w[row * 4 + col];
+		ds.xforms[frame_idx] = m;
+	}
+	m_dataset_dirty = true;
+}
+
+Mat43 Testbed::get_camera_extrinsics(int frame_idx) const {
+	const NerfDataset& ds = nerf.training.dataset;
+	if (frame_idx < 0 || (size_t)frame_idx >= ds.n_images) throw std::runtime_error("Invalid frame index");
+	return ds.ngp_matrix_to_nerf(ds.xforms[frame_idx]);
+}
+
+// Nerf::Training::set_camera_intrinsics (src/testbed_nerf.cu:1989-2010)
+void Testbed::set_camera_intrinsics(int frame_idx, float fx, float fy, float cx, float cy) {
+	NerfDataset& ds = nerf.training.dataset;
+	if (frame_idx < 0 || (size_t)frame_idx >= ds.n_images) return;
+	if (fx <= 0.f) fx = fy;
+	if (fy <= 0.f) fy = fx;
+	auto& m = ds.metadata[frame_idx];
+	cx = cx < 0.f ? -cx : cx / (float)m.resolution[0];
+	cy = cy < 0.f ? -cy : cy / (float)m.resolution[1];
+	m.lens = Lens{};
+	m.focal_length = {fx, fy};
+	m.principal_point = {cx, cy};
+	m_dataset_dirty = true;
+}
+
+void Testbed::free_device_dataset() {
+	for (void* p : m_dev_pixels) (void)hipFree(p);
+	m_dev_pixels.clear();
+	if (m_dev_meta) (void)hipFree(m_dev_meta);
+	m_dev_meta = nullptr;
+}
+
+void Testbed::upload_metadata() {
+	const NerfDataset& ds = nerf.training.dataset;
+	std::vector<ngp_image> meta(ds.n_images);
+	for (size_t i = 0; i < ds.n_images; ++i) {
+		ngp_image& im = meta[i];
+		std::memset(&im, 0, sizeof(im));
+		im.pixels = (uint64_t)(uintptr_t)m_dev_pixels[i];
+		im.width = (uint32_t)ds.metadata[i].resolution[0];
+		im.height = (uint32_t)ds.metadata[i].resolution[1];
+		for (int k = 0; k < 2; ++k) {
+			im.focal_length[k] = ds.metadata[i].focal_length[k];
+			im.principal_point[k] = ds.metadata[i].principal_point[k];
+		}
+		std::memcpy(im.xform, ds.xforms[i].m, sizeof(im.xform));
+		im.lens_mode = (int32_t)ds.metadata[i].lens.mode;
+		std::memcpy(im.lens_params, ds.metadata[i].lens.params, sizeof(im.lens_params));
+	}
+	if (!m_dev_meta) hk(hipMalloc(&m_dev_meta, std::max<size_t>(1, meta.size()) * sizeof(ngp_image)), "hipMalloc meta");
+	hk(hipMemcpy(m_dev_meta, meta.data(), meta.size() * sizeof(ngp_image), hipMemcpyHostToDevice), "upload meta");
+}
+
+void Testbed::upload_dataset() {
+	if (!m_dataset_dirty) return;
+	const NerfDataset& ds = nerf.training.dataset;
+	for (size_t i = 0; i < ds.n_images; ++i)
+		if (ds.pixels[i].empty()) throw std::runtime_error("Training image " + std::to_string(i) + " has no pixels.");
+	free_device_dataset();
+	m_dev_pixels.resize(ds.n_images, nullptr);
+	for (size_t i = 0; i < ds.n_images; ++i) {
+		hk(hipMalloc(&m_dev_pixels[i], ds.pixels[i].size()), "hipMalloc image");
+		hk(hipMemcpy(m_dev_pixels[i], ds.pixels[i].data(), ds.pixels[i].size(), hipMemcpyHostToDevice), "upload image");
+	}
+	upload_metadata();
+	m_dataset_dirty = false;
+}
+
+// ---------------------------------------------------------------------------
+// Network configuration
+// ---------------------------------------------------------------------------
+std::string Testbed::find_network_config(const std::string& path) const {
+	if (file_exists(path)) return path;
+	// configs/<mode>/<name>, looked up next to the package and under root_dir (src/testbed.cu find_network_config)
+	const std::string name = basename_of(path);
+	std::vector<std::string> roots;
+	if (!root_dir.empty()) roots.push_back(root_dir + "/configs/nerf/");
+	if (const char* env = std::getenv("NGP_CONFIG_DIR")) roots.push_back(std::string(env) + "/");
+	for (const std::string& r : roots) {
+		if (file_exists(r + path)) return r + path;
+		if (file_exists(r + name)) return r + name;
+	}
+	return path;
+}
+
+Json Testbed::load_network_config(const std::string& path) const {
+	if (!file_exists(path)) throw std::runtime_error("Network config '" + path + "' does not exist.");
+	Json j = Json::parse(read_text(path));
+	// merge_parent_network_config (src/testbed.cu:86-97)
+	if (j.contains("parent")) {
+		const std::string pp = parent_path(path) + "/" + j["parent"].str();
+		Json parent = load_network_config(pp);
+		parent.merge_patch(j);
+		j = parent;
+	}
+	return j;
+}
+
+void Testbed::reload_network_from_file(const std::string& path) {
+	if (!path.empty()) network_config_path = path;
+	if (mode == ETestbedMode::None) return;
+	const std::string full = find_network_config(network_config_path);
+	if (file_exists(full)) m_network_config = load_network_config(full);
+	reset_network();
+}
+
+void Testbed::reload_network_from_json(const Json& json, const std::string& config_base_path) {
+	Json j = json;
+	if (j.contains("parent")) {
+		Json parent = load_network_config(find_network_config(config_base_path.empty() ? j["parent"].str()
+		                                                                              : config_base_path + "/" + j["parent"].str()));
+		parent.merge_patch(j);
+		j = parent;
+	}
+	m_network_config = j;
+	reset_network();
+}
+
+static int loss_type_from_string(const std::string& s) {
+	std::string l = s;
+	std::transform(l.begin(), l.end(), l.begin(), ::tolower);
+	if (l == "l2") return 0;
+	if (l == "l1") return 1;
+	if (l == "mape") return 2;
+	if (l == "smape") return 3;
+	if (l == "huber" || l == "smoothl1") return 4;
+	if (l == "logl1") return 5;
+	if (l == "relativel2") return 6;
+	throw std::runtime_error("Unknown loss type.");
+}
+
+// Testbed::reset_network (src/testbed.cu:3624-3868), NeRF branch.
+void Testbed::reset_network(bool clear_density_grid) {
+	pcg32 rng(seed);
+	nerf.training.counters_rgb = NerfCounters{};
+	nerf.training.counters_rgb.rays_per_batch = 1 << 12;
+	pcg32 grid_rng(rng.next_uint());
+	m_rng_state = rng.state;
+	m_rng_inc = rng.inc;
+	nerf.training.density_grid_rng_state = grid_rng.state;
+	nerf.training.density_grid_rng_inc = grid_rng.inc;
+	training_step = 0;
+	loss = 0.f;
+	const Json& cfg = m_network_config;
+	nerf.training.loss_type = (ELossType)loss_type_from_string(cfg["loss"].value("otype", std::string("L2")));
+	build_model(cfg);
+	if (clear_density_grid) nerf.density_grid_ema_step = 0;
+}
+
+void Testbed::build_model(const Json& cfg) {
+	if (mode != ETestbedMode::Nerf) throw std::runtime_error("reset_network: only the NeRF mode is implemented.");
+	const Json& enc = cfg["encoding"];
+	std::string etype = enc.value("otype", std::string("HashGrid"));
+	std::transform(etype.begin(), etype.end(), etype.begin(), ::tolower);
+	if (etype.find("grid") == std::string::npos)
+		throw std::runtime_error("Only the HashGrid encoding is implemented on MI355X (got '" + etype + "').");
+	ngp_network_config c{};
+	c.n_features_per_level = (uint32_t)enc.value("n_features_per_level", 2.0);
+	c.n_levels = enc.contains("n_features") && enc["n_features"].num() > 0 ? (uint32_t)enc["n_features"].num() / c.n_features_per_level
+	                                                                       : (uint32_t)enc.value("n_levels", 16.0);
+	c.log2_hashmap_size = (uint32_t)enc.value("log2_hashmap_size", 15.0);
+	c.base_resolution = (uint32_t)enc.value("base_resolution", 0.0);
+	if (!c.base_resolution) c.base_resolution = 1u << (c.log2_hashmap_size / 3);
+	float pls = (float)enc.value("per_level_scale", 0.0);
+	if (pls <= 0.f && c.n_levels > 1) {
+		const float desired = 2048.0f;  // src/testbed.cu:3702
+		pls = std::exp(std::log(desired * (float)nerf.training.dataset.aabb_scale / (float)c.base_resolution) / (float)(c.n_levels - 1));
+	}
+	c.per_level_scale = pls > 0 ? pls : 1.0f;
+	const Json& net = cfg["network"];
+	const Json& rgb = cfg.contains("rgb_network") ? cfg["rgb_network"] : cfg["network"];
+	c.n_neurons = (uint32_t)net.value("n_neurons", 64.0);
+	c.density_hidden_layers = (uint32_t)(net.contains("n_hidden_layers") ? net["n_hidden_layers"].num() : std::max(1.0, net.value("n_layers", 2.0) - 1.0));
+	c.rgb_hidden_layers = (uint32_t)(rgb.contains("n_hidden_layers") ? rgb["n_hidden_layers"].num() : 2.0);
+	if ((uint32_t)rgb.value("n_neurons", (double)c.n_neurons) != c.n_neurons)
+		throw std::runtime_error("density and rgb MLPs must share n_neurons on this build");
+	c.rgb_activation = (int32_t)nerf.rgb_activation;
+	c.density_activation = (int32_t)nerf.density_activation;
+	// optimizer chain: [Ema] -> [ExponentialDecay] -> Adam (configs/nerf/base.json:5-22)
+	c.ema_decay = 0.0f;
+	c.decay_start = 0xFFFFFFFFu;
+	c.decay_interval = 0;
+	c.decay_base = 1.0f;
+	const Json* opt = &cfg["optimizer"];
+	while (opt->is_object()) {
+		std::string ot = opt->value("otype", std::string("Adam"));
+		if (ot == "Ema") c.ema_decay = (float)opt->value("decay", 0.99);
+		else if (ot == "ExponentialDecay") {
+			c.decay_start = (uint32_t)opt->value("decay_start", 0.0);
+			c.decay_interval = (uint32_t)opt->value("decay_interval", 10000.0);
+			c.decay_base = (float)opt->value("decay_base", 0.33);
+		} else if (ot == "Adam") {
+			c.learning_rate = (float)opt->value("learning_rate", 1e-3);
+			c.beta1 = (float)opt->value("beta1", 0.9);
+			c.beta2 = (float)opt->value("beta2", 0.99);
+			c.epsilon = (float)opt->value("epsilon", 1e-8);
+			c.l2_reg = (float)opt->value("l2_reg", 1e-8);
+		} else throw std::runtime_error("Unsupported optimizer '" + ot + "' (Ema/ExponentialDecay/Adam implemented)");
+		if (!opt->contains("nested")) break;
+		opt = &(*opt)["nested"];
+	}
+	if (c.ema_decay == 0.0f) c.ema_decay = 0.0f;  // no Ema: inference params track the weights exactly
+	int device = 0;
+	hk(hipGetDevice(&device), "hipGetDevice");
+	if (m_model) {
+		sync();
+		ck(ngp_model_destroy(m_model));
+		m_model = nullptr;
+	}
+	ck(ngp_model_create(device, &c, seed, &m_model));
+}
+
+// ---------------------------------------------------------------------------
+// Training
+// ---------------------------------------------------------------------------
+void Testbed::update_density_grid(uint32_t n_uniform, uint32_t n_nonuniform) {
+	upload_dataset();
+	ngp_grid_args g{};
+	g.images = (const ngp_image*)m_dev_meta;
+	g.n_images = (uint32_t)nerf.training.n_images_for_training;
+	for (int k = 0; k < 3; ++k) { g.aabb_min[k] = aabb_min[k]; g.aabb_max[k] = aabb_max[k]; }
+	g.max_cascade = nerf.max_cascade;
+	g.decay = nerf.training.density_grid_decay;
+	g.n_uniform_samples = n_uniform;
+	g.n_nonuniform_samples = n_nonuniform;
+	g.rng_state = nerf.training.density_grid_rng_state;
+	g.rng_inc = nerf.training.density_grid_rng_inc;
+	g.ema_step = nerf.density_grid_ema_step;
+	const bool changed = nerf.training.n_images_for_training != nerf.training.n_images_for_training_prev;
+	g.mark_untrained = (training_step == 0 || changed) ? 1 : 0;
+	g.clear_visible = training_step == 0 ? 1 : 0;
+	nerf.training.n_images_for_training_prev = nerf.training.n_images_for_training;
+	if (training_step == 0) nerf.density_grid_ema_step = 0, g.ema_step = 0;
+	g.use_inference_params = 0;
+	g.rank = (uint32_t)m_rank;
+	g.world_size = (uint32_t)m_world;
+	if (m_world > 1) {
+		ck(ngp_density_grid_evaluate(m_model, &g, m_stream));
+		float *grid, *tmp;
+		ck(ngp_density_grid_buffers(m_model, &grid, nullptr, &tmp, nullptr));
+		allreduce_f32(tmp, (size_t)NERF_GRID_N_CELLS * (nerf.max_cascade + 1), true);
+		ck(ngp_density_grid_finish(m_model, &g, m_stream));
+	} else {
+		ck(ngp_density_grid_update(m_model, &g, m_stream));
+	}
+	pcg32 r;
+	r.state = nerf.training.density_grid_rng_state;
+	r.inc = nerf.training.density_grid_rng_inc;
+	r.advance();
+	r.advance();
+	nerf.training.density_grid_rng_state = r.state;
+	++nerf.density_grid_ema_step;
+}
+
+void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
+	if (nerf.training.n_images_for_training == 0) return;
+	upload_dataset();
+	NerfCounters& ctr = nerf.training.counters_rgb;
+	const uint32_t max_samples = batch * 16;
+	uint32_t max_inference;
+	if (ctr.measured_batch_size_before_compaction == 0) ctr.measured_batch_size_before_compaction = max_inference = max_samples;
+	else max_inference = next_multiple_host(std::min(ctr.measured_batch_size_before_compaction, max_samples), BATCH_SIZE_GRANULARITY);
+	if (training_step == 0) ctr.n_rays_total = 0;
+
+	ngp_train_args a{};
+	a.images = (const ngp_image*)m_dev_meta;
+	a.n_images = (uint32_t)nerf.training.n_images_for_training;
+	a.n_rays = ctr.rays_per_batch;
+	a.n_rays_total = ctr.n_rays_total;
+	a.target_batch_size = batch;
+	a.max_samples = max_inference;
+	a.training_step = training_step;
+	a.rng_state = m_rng_state;
+	a.rng_inc = m_rng_inc;
+	a.ray_index_offset = (uint32_t)m_rank * ctr.rays_per_batch;
+	a.n_rays_global = ctr.rays_per_batch * (uint32_t)m_world;
+	for (int k = 0; k < 3; ++k) { a.aabb_min[k] = aabb_min[k]; a.aabb_max[k] = aabb_max[k]; }
+	a.cone_angle_constant = nerf.cone_angle_constant;
+	a.max_cascade = nerf.max_cascade;
+	a.loss_type = (int32_t)nerf.training.loss_type;
+	a.random_bg_color = nerf.training.random_bg_color;
+	for (int k = 0; k < 3; ++k) a.background_color[k] = background_color[k];
+	a.snap_to_pixel_centers = nerf.training.snap_to_pixel_centers;
+	a.train_in_linear_colors = nerf.training.linear_colors;
+	a.color_space = (int32_t)color_space;
+	a.near_distance = nerf.training.near_distance;
+	a.optimize_mlp = train_network;
+	a.optimize_encoding = train_encoding;
+	a.defer_optimizer = m_world > 1 ? 1 : 0;
+	ctr.n_rays_total += ctr.rays_per_batch;
+	ck(ngp_train_step(m_model, &a, m_stream));
+	if (m_world > 1) {
+		void* g = nullptr;
+		size_t bytes = 0;
+		ck(ngp_model_buffer(m_model, NGP_GRADS_FP32, &g, &bytes));
+		allreduce_f32((float*)g, bytes / sizeof(float), false);
+		ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
+	}
+	++training_step;
+	// m_rng.advance() (src/testbed_nerf.cu:2925)
+	pcg32 r;
+	r.state = m_rng_state;
+	r.inc = m_rng_inc;
+	r.advance();
+	m_rng_state = r.state;
+
+	// NerfCounters::update_after_training (src/testbed_nerf.cu:2422-2446)
+	ngp_train_stats st{};
+	ck(ngp_train_read_stats(m_model, &st, m_stream));
+	if (m_world > 1) {
+		float v[3] = {(float)st.measured_batch_size, (float)st.measured_batch_size_before_compaction, st.loss};
+		float* dv = (float*)m_red_buf;
+		hk(hipMemcpyAsync(dv, v, sizeof(v), hipMemcpyHostToDevice, (hipStream_t)m_stream), "stats h2d");
+		allreduce_f32(dv, 3, false);
+		hk(hipMemcpyAsync(v, dv, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "stats d2h");
+		sync();
+		st.measured_batch_size = (uint32_t)(v[0] / (float)m_world);
+		st.measured_batch_size_before_compaction = (uint32_t)(v[1] / (float)m_world);
+		st.loss = v[2];
+	}
+	m_last_stats = st;
+	ctr.measured_batch_size = st.measured_batch_size;
+	ctr.measured_batch_size_before_compaction = st.measured_batch_size_before_compaction;
+	if (st.measured_batch_size_before_compaction == 0 || st.measured_batch_size == 0) {
+		ctr.measured_batch_size = ctr.measured_batch_size_before_compaction = 0;
+		loss = 0.f;
+		std::fprintf(stderr, "Nerf training generated 0 samples. Aborting training.\n");
+		shall_train = false;
+		return;
+	}
+	if (get_loss_scalar) loss = st.loss * (float)st.measured_batch_size / (float)batch;
+	uint32_t rpb = (uint32_t)((float)ctr.rays_per_batch * (float)batch / (float)st.measured_batch_size);
+	ctr.rays_per_batch = std::min(next_multiple_host(rpb, BATCH_SIZE_GRANULARITY), 1u << 18);
+}
+
+void Testbed::train(uint32_t batch_size) {
+	if (!training_data_available) {
+		shall_train = false;
+		return;
+	}
+	if (mode == ETestbedMode::None) throw std::runtime_error("Cannot train without a mode.");
+	if (!m_model) {
+		reload_network_from_file();
+		if (!m_model) throw std::runtime_error("Unable to create a neural network trainer.");
+	}
+	reset_accumulation();
+	// density-grid cadence (src/testbed.cu:4060) + training_prep_nerf (src/testbed_nerf.cu:2933-2946)
+	const uint32_t n_prep_to_skip = std::min(std::max(training_step / 16u, 1u), 16u);
+	if (training_step % n_prep_to_skip == 0) {
+		const auto t0 = std::chrono::steady_clock::now();
+		const uint32_t nc = nerf.max_cascade + 1;
+		if (training_step < 256) update_density_grid(NERF_GRID_N_CELLS * nc, 0);
+		else update_density_grid(NERF_GRID_N_CELLS / 4 * nc, NERF_GRID_N_CELLS / 4 * nc);
+		sync();
+		training_prep_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count() / n_prep_to_skip;
+	}
+	const bool get_loss_scalar = training_step % 16 == 0;
+	const auto t0 = std::chrono::steady_clock::now();
+	train_nerf(batch_size, get_loss_scalar);
+	sync();
+	training_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+}
+
+bool Testbed::frame() {
+	if (shall_train) train(training_batch_size);
+	return true;
+}
+
+// ---------------------------------------------------------------------------
+// Rendering
+// ---------------------------------------------------------------------------
+void Testbed::reset_camera() {
+	fov_axis = 1;
+	zoom = 1.0f;
+	screen_center = {0.5f, 0.5f};
+	set_fov(50.625f);
+	scale = 1.5f;
+	// src/testbed.cu:504-511: rows (1,0,0,.5), (0,-1,0,.5), (0,0,-1,.5) transposed -> columns
+	const float m[12] = {1, 0, 0, 0, -1, 0, 0, 0, -1, 0.5f, 0.5f, 0.5f};
+	std::memcpy(camera.m, m, sizeof(m));
+	// m_camera[3] -= m_scale * view_dir()
+	for (int k = 0; k < 3; ++k) camera.m[9 + k] -= scale * camera.m[6 + k];
+	m_spp = 0;
+}
+
+float Testbed::fov() const { return focal_length_to_fov(1.0f, relative_focal_length[fov_axis]); }
+void Testbed::set_fov(float degrees) {
+	const float f = fov_to_focal_length(1, degrees);
+	relative_focal_length = {f, f};
+}
+
+void Testbed::set_camera_to_training_view(int trainview) {
+	const NerfDataset& ds = nerf.training.dataset;
+	if (trainview < 0 || (size_t)trainview >= ds.n_images) throw std::runtime_error("Invalid training view.");
+	camera = ds.xforms[trainview];
+	const auto& md = ds.metadata[trainview];
+	relative_focal_length = {md.focal_length[0] / (float)md.resolution[fov_axis], md.focal_length[1] / (float)md.resolution[fov_axis]};
+	nerf.render_with_lens_distortion = true;
+	screen_center = {1.0f - md.principal_point[0], 1.0f - md.principal_point[1]};
+	nerf.training.view = trainview;
+	m_spp = 0;
+}
+
+void Testbed::ensure_render_buffers(size_t n) {
+	if (n <= m_render_cap) return;
+	for (float** p : {&m_frame, &m_accum, &m_out}) {
+		if (*p) (void)hipFree(*p);
+		hk(hipMalloc((void**)p, n * 4 * sizeof(float)), "hipMalloc frame");
+	}
+	if (m_depth) (void)hipFree(m_depth);
+	hk(hipMalloc((void**)&m_depth, n * sizeof(float)), "hipMalloc depth");
+	m_render_cap = n;
+}
+
+std::vector<float> Testbed::render(int width, int height, int spp, bool linear, uint32_t shard_index,
+                                   uint32_t shard_count, uint32_t shard_rows, bool copy_to_host) {
+	if (width <= 0 || height <= 0) throw std::runtime_error("render: invalid resolution");
+	const size_t n = (size_t)width * height;
+	std::vector<float> out(copy_to_host ? n * 4 : 0, 0.0f);
+	const vec2 sc = {(0.5f - screen_center[0]) * zoom + 0.5f, (0.5f - screen_center[1]) * zoom + 0.5f};
+	const int res_axis = fov_axis == 0 ? width : height;
+	const vec2 focal = {relative_focal_length[0] * (float)res_axis * zoom, relative_focal_length[1] * (float)res_axis * zoom};
+
+	if (render_ground_truth && nerf.training.dataset.n_images > 0) {
+		out.assign(n * 4, 0.0f);
+		// overlay_image_kernel with ground-truth alpha 1 (src/render_buffer.cu:348-416), then tonemap to linear/sRGB
+		const NerfDataset& ds = nerf.training.dataset;
+		const int v = std::min(std::max(nerf.training.view, 0), (int)ds.n_images - 1);
+		const auto& px = ds.pixels[v];
+		const int iw = ds.metadata[v].resolution[0], ih = ds.metadata[v].resolution[1];
+		const float sca = (float)(fov_axis == 0 ? iw : ih) / (float)res_axis;
+		vec4 bg = background_color;
+		if (color_space != EColorSpace::SRGB)
+			for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear_h(bg[k]);
+		for (int y = 0; y < height; ++y)
+			for (int x = 0; x < width; ++x) {
+				float fx = x + 0.5f, fy = y + 0.5f;
+				fx -= width * 0.5f; fx /= zoom; fx += screen_center[0] * width;
+				fy -= height * 0.5f; fy /= zoom; fy += screen_center[1] * height;
+				const float u = (fx - width * 0.5f) * sca + iw * 0.5f, vv = (fy - height * 0.5f) * sca + ih * 0.5f;
+				const int sx = (int)std::floor(u), sy = (int)std::floor(vv);
+				float c[4] = {0, 0, 0, 0};
+				if (!px.empty() && sx >= 0 && sy >= 0 && sx < iw && sy < ih) {
+					const uint8_t* p = &px[((size_t)sy * iw + sx) * 4];
+					const float a = p[3] / 255.f;
+					for (int k = 0; k < 3; ++k) c[k] = srgb_to_linear_h(p[k] / 255.f) * a;
+					c[3] = a;
+				}
+				if (color_space == EColorSpace::SRGB) {
+					for (int k = 0; k < 3; ++k) c[k] = c[3] > 0 ? linear_to_srgb_h(c[k] / c[3]) * c[3] : 0.f;
+				}
+				const float w = (1 - c[3]) * bg[3];
+				for (int k = 0; k < 3; ++k) c[k] += bg[k] * w;
+				c[3] += w;
+				if (color_space == EColorSpace::SRGB)
+					for (int k = 0; k < 3; ++k) c[k] = srgb_to_linear_h(c[k]);
+				const float e = std::pow(2.0f, exposure);
+				for (int k = 0; k < 3; ++k) {
+					c[k] *= e;
+					if (!linear) c[k] = linear_to_srgb_h(c[k]);
+				}
+				std::memcpy(&out[((size_t)y * width + x) * 4], c, sizeof(c));
+			}
+		return out;
+	}
+	if (!m_model) throw std::runtime_error("render: no network (load training data or a snapshot first)");
+	const auto t0 = std::chrono::steady_clock::now();
+	ensure_render_buffers(n);
+	ngp_render_args r{};
+	r.width = (uint32_t)width;
+	r.height = (uint32_t)height;
+	std::memcpy(r.camera, camera.m, sizeof(r.camera));
+	r.focal_length[0] = focal[0];
+	r.focal_length[1] = focal[1];
+	r.screen_center[0] = sc[0];
+	r.screen_center[1] = sc[1];
+	r.near_distance = render_near_distance;
+	for (int k = 0; k < 3; ++k) {
+		r.aabb_min[k] = r.train_aabb_min[k] = aabb_min[k];
+		r.aabb_max[k] = r.train_aabb_max[k] = aabb_max[k];
+	}
+	r.cone_angle_constant = nerf.cone_angle_constant;
+	r.max_cascade = nerf.max_cascade;
+	r.min_transmittance = nerf.render_min_transmittance;
+	r.snap_to_pixel_centers = snap_to_pixel_centers;
+	r.use_inference_params = 1;
+	r.train_in_linear_colors = nerf.training.linear_colors;
+	r.shard_index = shard_index;
+	r.shard_count = std::max(shard_count, 1u);
+	r.shard_rows = std::max(shard_rows, 1u);
+	const float bg[4] = {background_color[0], background_color[1], background_color[2], background_color[3]};
+	m_spp = 0;
+	for (int i = 0; i < std::max(spp, 1); ++i) {
+		r.sample_index = (uint32_t)i;
+		ck(ngp_render(m_model, &r, m_frame, m_depth, m_stream));
+		const bool last = i == std::max(spp, 1) - 1;
+		ck(ngp_accumulate_tonemap(m_frame, m_accum, last ? m_out : nullptr, r.width, r.height, m_spp,
+		                          (int)color_space, exposure, bg, linear ? 0 : 1, m_stream));
+		++m_spp;
+	}
+	if (copy_to_host) hk(hipMemcpyAsync(out.data(), m_out, n * 4 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "render d2h");
+	sync();
+	render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+	return out;
+}
+
+std::vector<float> Testbed::density_grid() const {
+	std::vector<float> g((size_t)NERF_GRID_N_CELLS * (nerf.max_cascade + 1));
+	if (!m_model) return g;
+	float* dg = nullptr;
+	ck(ngp_density_grid_buffers(m_model, &dg, nullptr, nullptr, nullptr));
+	sync();
+	hk(hipMemcpy(g.data(), dg, g.size() * 4, hipMemcpyDeviceToHost), "grid d2h");
+	return g;
+}
+
+std::vector<uint8_t> Testbed::density_grid_bitfield() const {
+	std::vector<uint8_t> b(NERF_GRID_N_CELLS / 8 * NERF_CASCADES);
+	if (!m_model) return b;
+	uint8_t* db = nullptr;
+	ck(ngp_density_grid_buffers(m_model, nullptr, &db, nullptr, nullptr));
+	sync();
+	hk(hipMemcpy(b.data(), db, b.size(), hipMemcpyDeviceToHost), "bitfield d2h");
+	return b;
+}
+
+// ---------------------------------------------------------------------------
+// Snapshots: versioned binary container (header JSON + params [+ optimizer] + grid), zlib'd.
+// ---------------------------------------------------------------------------
+static const char SNAP_MAGIC[8] = {'N', 'G', 'P', 'M', 'I', '3', '5', '5'};
+static const uint32_t SNAPSHOT_FORMAT_VERSION = 1;
+
+void Testbed::save_snapshot(const std::string& path, bool include_optimizer_state, bool compress) {
+	if (!m_model) throw std::runtime_error("save_snapshot: no network");
+	sync();
+	ngp_model_info info{};
+	ck(ngp_model_get_info(m_model, &info));
+	auto grab = [&](int kind, size_t elem) {
+		void* p = nullptr;
+		size_t bytes = 0;
+		ck(ngp_model_buffer(m_model, kind, &p, &bytes));
+		std::vector<uint8_t> h(bytes);
+		hk(hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost), "snapshot d2h");
+		(void)elem;
+		return h;
+	};
+	Json hdr = Json::object();
+	hdr["version"] = Json((double)SNAPSHOT_FORMAT_VERSION);
+	hdr["network_config"] = m_network_config;
+	hdr["training_step"] = Json((double)training_step);
+	hdr["aabb_scale"] = Json((double)nerf.training.dataset.aabb_scale);
+	hdr["max_cascade"] = Json((double)nerf.max_cascade);
+	hdr["density_grid_ema_step"] = Json((double)nerf.density_grid_ema_step);
+	hdr["rgb_activation"] = Json((double)(int)nerf.rgb_activation);
+	hdr["density_activation"] = Json((double)(int)nerf.density_activation);
+	hdr["n_params"] = Json((double)info.n_params);
+	hdr["include_optimizer_state"] = Json(include_optimizer_state);
+	hdr["dataset_scale"] = Json((double)nerf.training.dataset.scale);
+	Json off = Json::array();
+	for (float o : nerf.training.dataset.offset) off.push_back(Json((double)o));
+	hdr["dataset_offset"] = off;
+	const std::string h = hdr.dump();
+	std::vector<uint8_t> blob;
+	auto put = [&](const void* p, size_t n) { const uint8_t* b = (const uint8_t*)p; blob.insert(blob.end(), b, b + n); };
+	const uint64_t hlen = h.size();
+	put(&hlen, 8);
+	put(h.data(), h.size());
+	auto params = grab(NGP_PARAMS_FP32, 4);
+	put(params.data(), params.size());
+	auto ema = grab(NGP_PARAMS_EMA_FP32, 4);
+	put(ema.data(), ema.size());
+	if (include_optimizer_state) {
+		auto m = grab(NGP_ADAM_M, 4);
+		put(m.data(), m.size());
+		auto v = grab(NGP_ADAM_V, 4);
+		put(v.data(), v.size());
+	}
+	auto grid = density_grid();
+	put(grid.data(), grid.size() * 4);
+	FILE* f = std::fopen(path.c_str(), "wb");
+	if (!f) throw std::runtime_error("Could not open '" + path + "' for writing.");
+	std::fwrite(SNAP_MAGIC, 1, 8, f);
+	const uint32_t flags = compress ? 1u : 0u;
+	std::fwrite(&SNAPSHOT_FORMAT_VERSION, 4, 1, f);
+	std::fwrite(&flags, 4, 1, f);
+	const uint64_t raw = blob.size();
+	std::fwrite(&raw, 8, 1, f);
+	if (compress) {
+		uLongf clen = compressBound((uLong)blob.size());
+		std::vector<uint8_t> c(clen);
+		if (compress2(c.data(), &clen, blob.data(), (uLong)blob.size(), Z_BEST_SPEED) != Z_OK) {
+			std::fclose(f);
+			throw std::runtime_error("snapshot compression failed");
+		}
+		std::fwrite(c.data(), 1, clen, f);
+	} else {
+		std::fwrite(blob.data(), 1, blob.size(), f);
+	}
+	std::fclose(f);
+}
+
+void Testbed::load_snapshot(const std::string& path) {
+	std::ifstream f(path, std::ios::binary);
+	if (!f) throw std::runtime_error("Snapshot '" + path + "' does not exist.");
+	std::vector<uint8_t> file((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+	if (file.size() < 24 || std::memcmp(file.data(), SNAP_MAGIC, 8) != 0)
+		throw std::runtime_error("'" + path + "' is not an MI355X NGP snapshot (the CUDA .ingp/msgpack reader is not implemented yet).");
+	uint32_t version, flags;
+	uint64_t raw;
+	std::memcpy(&version, &file[8], 4);
+	std::memcpy(&flags, &file[12], 4);
+	std::memcpy(&raw, &file[16], 8);
+	if (version != SNAPSHOT_FORMAT_VERSION) throw std::runtime_error("Unsupported snapshot version " + std::to_string(version));
+	std::vector<uint8_t> blob(raw);
+	if (flags & 1u) {
+		uLongf len = (uLongf)raw;
+		if (uncompress(blob.data(), &len, file.data() + 24, (uLong)(file.size() - 24)) != Z_OK || len != raw)
+			throw std::runtime_error("snapshot decompression failed");
+	} else {
+		std::memcpy(blob.data(), file.data() + 24, raw);
+	}
+	size_t pos = 0;
+	auto take = [&](void* dst, size_t n) {
+		if (pos + n > blob.size()) throw std::runtime_error("truncated snapshot");
+		std::memcpy(dst, &blob[pos], n);
+		pos += n;
+	};
+	uint64_t hlen;
+	take(&hlen, 8);
+	std::string h(hlen, '\0');
+	take(&h[0], hlen);
+	const Json hdr = Json::parse(h);
+	mode = ETestbedMode::Nerf;
+	nerf.training.dataset.aabb_scale = (int)hdr["aabb_scale"].num();
+	nerf.training.dataset.scale = (float)hdr.value("dataset_scale", 0.33);
+	if (hdr.contains("dataset_offset"))
+		for (int k = 0; k < 3; ++k) nerf.training.dataset.offset[k] = (float)hdr["dataset_offset"][k].num();
+	nerf.rgb_activation = (ENerfActivation)(int)hdr["rgb_activation"].num();
+	nerf.density_activation = (ENerfActivation)(int)hdr["density_activation"].num();
+	{
+		// aabb / cascades as load_nerf_post would set them
+		const int s = nerf.training.dataset.aabb_scale;
+		const float half = 0.5f * (float)std::min(128, s);
+		aabb_min = {0.5f - half, 0.5f - half, 0.5f - half};
+		aabb_max = {0.5f + half, 0.5f + half, 0.5f + half};
+		nerf.max_cascade = 0;
+		while ((1 << nerf.max_cascade) < s) ++nerf.max_cascade;
+		nerf.cone_angle_constant = s <= 1 ? 0.0f : (1.0f / 256.0f);
+	}
+	m_network_config = hdr["network_config"];
+	reset_network(false);
+	const size_t n_params = (size_t)hdr["n_params"].num();
+	ngp_model_info info{};
+	ck(ngp_model_get_info(m_model, &info));
+	if (info.n_params != n_params) throw std::runtime_error("snapshot parameter count does not match its network config");
+	auto put_buf = [&](int kind) {
+		void* p = nullptr;
+		size_t bytes = 0;
+		ck(ngp_model_buffer(m_model, kind, &p, &bytes));
+		std::vector<uint8_t> tmp(bytes);
+		take(tmp.data(), bytes);
+		hk(hipMemcpy(p, tmp.data(), bytes, hipMemcpyHostToDevice), "snapshot h2d");
+	};
+	put_buf(NGP_PARAMS_FP32);
+	ck(ngp_model_params_updated(m_model, 1, m_stream));
+	sync();
+	put_buf(NGP_PARAMS_EMA_FP32);
+	if (hdr.value("include_optimizer_state", false)) {
+		put_buf(NGP_ADAM_M);
+		put_buf(NGP_ADAM_V);
+	}
+	ck(ngp_model_params_updated(m_model, 0, m_stream));
+	std::vector<float> grid((size_t)NERF_GRID_N_CELLS * (nerf.max_cascade + 1));
+	take(grid.data(), grid.size() * 4);
+	// grid buffer is sized by the first bitfield pass
+	ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));
+	sync();
+	float* dg = nullptr;
+	ck(ngp_density_grid_buffers(m_model, &dg, nullptr, nullptr, nullptr));
+	hk(hipMemcpy(dg, grid.data(), grid.size() * 4, hipMemcpyHostToDevice), "grid h2d");
+	ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));
+	sync();
+	training_step = (uint32_t)hdr["training_step"].num();
+	nerf.density_grid_ema_step = (uint32_t)hdr.value("density_grid_ema_step", 0.0);
+}
+
+// ---------------------------------------------------------------------------
+// Multi-GPU (RCCL over xGMI)
+// ---------------------------------------------------------------------------
+std::string Testbed::nccl_unique_id() {
+	ncclUniqueId id;
+	nk(ncclGetUniqueId(&id), "ncclGetUniqueId");
+	return std::string(id.internal, sizeof(id.internal));
+}
+
+void Testbed::init_distributed(int rank, int world_size, const std::string& uid) {
+	if (world_size <= 1) return;
+	if (uid.size() != sizeof(ncclUniqueId::internal)) throw std::runtime_error("init_distributed: bad ncclUniqueId");
+	ncclUniqueId id;
+	std::memcpy(id.internal, uid.data(), uid.size());
+	ncclComm_t comm;
+	nk(ncclCommInitRank(&comm, world_size, id, rank), "ncclCommInitRank");
+	m_comm = comm;
+	m_rank = rank;
+	m_world = world_size;
+	hk(hipMalloc(&m_red_buf, 64), "hipMalloc reduction scratch");
+}
+
+void Testbed::allreduce_f32(float* dev, size_t n, bool max_op) {
+	if (m_world <= 1) return;
+	nk(ncclAllReduce(dev, dev, n, ncclFloat32, max_op ? ncclMax : ncclSum, (ncclComm_t)m_comm, (hipStream_t)m_stream),
+	   "ncclAllReduce");
+}
+
+}  // namespace ngp

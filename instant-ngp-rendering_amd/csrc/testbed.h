@@ -1,0 +1,228 @@
+// testbed.h — host-side Testbed for the MI355X NeRF path (no device code).
+//
+// Mirrors the reference Testbed's NeRF surface (include/neural-graphics-primitives/
+// testbed.h, src/testbed.cu, src/testbed_nerf.cu): dataset loading, network
+// (re)configuration, train()/frame(), render(), snapshots, camera helpers.  All
+// GPU work goes through the C-ABI of libngp_hip.so (include/ngp_hip.h).
+#pragma once
+
+#include <array>
+#include <cstdint>
+#include <functional>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/ngp_hip.h"
+#include "json.h"
+
+namespace ngp {
+
+enum class ETestbedMode : int { Nerf, Sdf, Image, Volume, Geometry, None };
+enum class EColorSpace : int { Linear, SRGB, VisPosNeg };
+enum class ELossType : int { L2, L1, Mape, Smape, Huber, LogL1, RelativeL2 };
+enum class ENerfActivation : int { None, ReLU, Logistic, Exponential };
+enum class ELensMode : int { Perspective, OpenCV, FTheta, LatLong, OpenCVFisheye, Equirectangular };
+enum class ETonemapCurve : int { Identity, ACES, Hable, Reinhard };
+
+using vec2 = std::array<float, 2>;
+using vec3 = std::array<float, 3>;
+using vec4 = std::array<float, 4>;
+using ivec2 = std::array<int, 2>;
+
+// Column-major 4x3 camera-to-world (right, down, forward, origin) in NGP space.
+struct Mat43 {
+	float m[12] = {1, 0, 0, 0, 1, 0, 0, 0, 1, 0, 0, 0};
+	vec3 col(int c) const { return {m[3 * c], m[3 * c + 1], m[3 * c + 2]}; }
+	void set_col(int c, const vec3& v) { m[3 * c] = v[0]; m[3 * c + 1] = v[1]; m[3 * c + 2] = v[2]; }
+};
+
+struct Lens {
+	ELensMode mode = ELensMode::Perspective;
+	float params[7] = {};
+};
+
+struct TrainingImageMetadata {
+	ivec2 resolution = {0, 0};
+	vec2 focal_length = {1000.f, 1000.f};
+	vec2 principal_point = {0.5f, 0.5f};
+	Lens lens;
+};
+
+struct NerfDataset {
+	std::vector<TrainingImageMetadata> metadata;
+	std::vector<Mat43> xforms;
+	std::vector<std::string> paths;
+	std::vector<std::vector<uint8_t>> pixels;  // RGBA8, sRGB, straight alpha (EImageDataType::Byte)
+	vec3 up = {0.f, 1.f, 0.f};
+	vec3 offset = {0.5f, 0.5f, 0.5f};
+	float scale = 0.33f;
+	int aabb_scale = 1;
+	bool is_hdr = false;
+	bool from_mitsuba = false;
+	size_t n_images = 0;
+	// nerf_loader.h:95-116
+	Mat43 nerf_matrix_to_ngp(const float* nerf_3x4_rowmajor, bool scale_columns = false) const;
+	Mat43 ngp_matrix_to_nerf(const Mat43& m, bool scale_columns = false) const;
+};
+
+struct NerfCounters {
+	uint32_t rays_per_batch = 1 << 12;
+	uint32_t n_rays_total = 0;
+	uint32_t measured_batch_size = 0;
+	uint32_t measured_batch_size_before_compaction = 0;
+};
+
+struct NerfTraining {
+	NerfDataset dataset;
+	int n_images_for_training = 0;
+	int n_images_for_training_prev = 0;
+	bool random_bg_color = true;
+	bool linear_colors = false;
+	ELossType loss_type = ELossType::L2;
+	bool snap_to_pixel_centers = true;
+	float near_distance = 0.1f;
+	float density_grid_decay = 0.95f;
+	bool optimize_extrinsics = false, optimize_distortion = false, optimize_focal_length = false,
+	     optimize_exposure = false, optimize_extra_dims = false;
+	int view = 0;
+	NerfCounters counters_rgb;
+	uint64_t density_grid_rng_state = 0, density_grid_rng_inc = 0;
+};
+
+struct Nerf {
+	NerfTraining training;
+	uint32_t max_cascade = 0;
+	ENerfActivation rgb_activation = ENerfActivation::Exponential;
+	ENerfActivation density_activation = ENerfActivation::Exponential;
+	float cone_angle_constant = 1.f / 256.f;
+	float render_min_transmittance = 0.01f;
+	bool render_with_lens_distortion = false;
+	float sharpen = 0.f;
+	uint32_t density_grid_ema_step = 0;
+	bool visualize_cameras = false;
+};
+
+class Testbed {
+public:
+	explicit Testbed(ETestbedMode mode = ETestbedMode::None);
+	~Testbed();
+	Testbed(const Testbed&) = delete;
+	Testbed& operator=(const Testbed&) = delete;
+
+	// --- data (Testbed::load_training_data src/testbed.cu:125, load_nerf src/testbed_nerf.cu:2240) ---
+	void load_training_data(const std::string& path);
+	void load_file(const std::string& path);
+	void create_empty_nerf_dataset(size_t n_images, int aabb_scale = 1, bool is_hdr = false);
+	void set_image(int frame_idx, const float* rgba, int width, int height);  // linear premultiplied float RGBA
+	void set_image_rgba8(int frame_idx, const uint8_t* rgba, int width, int height);
+	void set_camera_extrinsics(int frame_idx, const float* c2w_3x4_rowmajor, bool convert_to_ngp = true);
+	Mat43 get_camera_extrinsics(int frame_idx) const;
+	void set_camera_intrinsics(int frame_idx, float fx, float fy = 0.f, float cx = -0.5f, float cy = -0.5f);
+	std::function<bool(const std::string&, std::vector<uint8_t>&, int&, int&)> image_decoder;  // non-PNG fallback
+
+	// --- network (reload_network_from_file src/testbed.cu:274, reset_network :3624) ---
+	void reload_network_from_file(const std::string& path = "");
+	void reload_network_from_json(const Json& json, const std::string& config_base_path = "");
+	void reset_network(bool clear_density_grid = true);
+	Json network_config() const { return m_network_config; }
+
+	// --- training (train src/testbed.cu:4020, frame :3380) ---
+	void train(uint32_t batch_size);
+	bool frame();
+	void reset_accumulation() { m_spp = 0; }
+
+	// --- rendering (render_to_cpu src/python_api.cu:124) ---
+	// copy_to_host=false leaves the tonemapped frame in HBM (render_frame_buffer()) and returns {}.
+	std::vector<float> render(int width, int height, int spp, bool linear, uint32_t shard_index = 0,
+	                          uint32_t shard_count = 1, uint32_t shard_rows = 8, bool copy_to_host = true);
+	const float* render_frame_buffer() const { return m_out; }
+	void set_camera_to_training_view(int trainview);
+	void reset_camera();
+	float fov() const;
+	void set_fov(float degrees);
+
+	// --- snapshots (save_snapshot src/testbed.cu:4775, load_snapshot :4841) ---
+	void save_snapshot(const std::string& path, bool include_optimizer_state = false, bool compress = true);
+	void load_snapshot(const std::string& path);
+
+	// --- multi-GPU: one Testbed per rank, gradients all-reduced over RCCL/xGMI ---
+	void init_distributed(int rank, int world_size, const std::string& nccl_unique_id);
+	static std::string nccl_unique_id();
+	int rank() const { return m_rank; }
+	int world_size() const { return m_world; }
+
+	ngp_model* model() const { return m_model; }
+	void* stream() const { return m_stream; }
+	void sync() const;
+	ngp_train_stats last_stats() const { return m_last_stats; }
+	std::vector<float> density_grid() const;
+	std::vector<uint8_t> density_grid_bitfield() const;
+
+	// --- state (public like the reference's pybind-exposed members) ---
+	ETestbedMode mode = ETestbedMode::None;
+	Nerf nerf;
+	bool shall_train = false;
+	bool train_encoding = true, train_network = true;
+	uint32_t training_batch_size = 1 << 18;
+	uint32_t training_step = 0;
+	float loss = 0.0f;  // Ema m_loss_scalar (val) of src/testbed.cu:4106-4108
+	vec4 background_color = {0.f, 0.f, 0.f, 1.f};
+	bool snap_to_pixel_centers = false;
+	bool render_ground_truth = false;
+	Mat43 camera;
+	vec2 relative_focal_length = {1.f, 1.f};
+	uint32_t fov_axis = 1;
+	float zoom = 1.f;
+	vec2 screen_center = {0.5f, 0.5f};
+	float scale = 1.5f;
+	float exposure = 0.f;
+	EColorSpace color_space = EColorSpace::Linear;
+	ETonemapCurve tonemap_curve = ETonemapCurve::Identity;
+	float render_near_distance = 0.f;
+	uint64_t seed = 1337;
+	std::string root_dir;
+	std::string data_path;
+	std::string network_config_path = "base.json";
+	bool training_data_available = false;
+	vec3 aabb_min = {0.f, 0.f, 0.f}, aabb_max = {1.f, 1.f, 1.f};
+	double training_ms = 0.0, training_prep_ms = 0.0, render_ms = 0.0;
+
+private:
+	void load_nerf_post();
+	void upload_dataset();
+	void upload_metadata();
+	void update_density_grid(uint32_t n_uniform, uint32_t n_nonuniform);
+	void train_nerf(uint32_t batch_size, bool get_loss_scalar);
+	std::string find_network_config(const std::string& path) const;
+	Json load_network_config(const std::string& path) const;
+	void build_model(const Json& config);
+	void free_device_dataset();
+	void ensure_render_buffers(size_t n_pixels);
+	void allreduce_f32(float* dev, size_t n, bool max_op);
+
+	ngp_model* m_model = nullptr;
+	void* m_stream = nullptr;
+	Json m_network_config;
+	uint64_t m_rng_state = 0, m_rng_inc = 0;
+	// device dataset
+	std::vector<void*> m_dev_pixels;
+	void* m_dev_meta = nullptr;
+	bool m_dataset_dirty = true;
+	// render buffers
+	float* m_frame = nullptr;
+	float* m_depth = nullptr;
+	float* m_accum = nullptr;
+	float* m_out = nullptr;
+	size_t m_render_cap = 0;
+	uint32_t m_spp = 0;
+	ngp_train_stats m_last_stats{};
+	// distributed
+	int m_rank = 0, m_world = 1;
+	void* m_comm = nullptr;
+	void* m_red_buf = nullptr;
+};
+
+std::string natural_sort_key(const std::string& s);
+
+}  // namespace ngp

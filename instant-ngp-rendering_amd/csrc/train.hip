@@ -518,7 +518,9 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.steps = m->adam_steps.ptr;
 	a.ema32 = m->ema32.ptr;
 	a.ema16 = m->infer16.ptr;
+	m->timers.begin(NGP_TIMER_OPTIMIZER, s);
 	k_optimizer<<<div_up(a.n, 256), 256, 0, s>>>(a);
+	m->timers.end(NGP_TIMER_OPTIMIZER, s, a.n);
 	NGP_HIP_CHECK(hipGetLastError());
 	++m->ema_step;
 	pack_mlp_fragments(m, m->params16.ptr, m->frag_train.ptr, s);
@@ -577,17 +579,24 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
 	const uint32_t rb = div_up(R, 256);
+	KernelTimers& tm = m->timers;
+	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
 	k_sample_count<<<rb, 256, 0, s>>>(sa);
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
 	k_sample_write<<<rb, 256, 0, s>>>(sa);
 	NGP_HIP_CHECK(hipGetLastError());
+	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
+	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 
 	// network inference over every emitted sample (NerfNetwork::inference_mixed_precision, training params)
-	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
+	tm.begin(NGP_TIMER_TRAIN_ENCODE, s);
 	launch_hashgrid_fwd(m->lt, ts.coords.ptr, 8, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
 	                    ts.counters.ptr + 4);
+	tm.end(NGP_TIMER_TRAIN_ENCODE, s);
+	tm.begin(NGP_TIMER_TRAIN_MLP_INFER, s);
 	launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
 	                 ts.counters.ptr + 4);
+	tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
 
 	LossArgs la{};
 	la.images = t->images;
@@ -625,6 +634,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.cenc = ts.cenc.ptr;
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
+	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
 	k_loss_composite<<<rb, 256, 0, s>>>(la);
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
 	k_loss_emit<<<rb, 256, 0, s>>>(la);
@@ -634,12 +644,18 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
 	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
+	tm.end(NGP_TIMER_TRAIN_LOSS, s, R);
 
 	// fused MLP forward+backward, then hash-grid scatter (Trainer::training_step)
+	tm.begin(NGP_TIMER_TRAIN_MLP_BWD, s);
 	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, B, ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5);
+	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
+	tm.begin(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	launch_hashgrid_bwd(m->lt, ts.ccoords.ptr, 8, B, ts.denc.ptr, B, m->grads.ptr + m->n_mlp_params, s,
 	                    ts.counters.ptr + 5);
+	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
+	tm.train_units_pending = tm.enabled;
 
 	if (!t->defer_optimizer) launch_optimizer(m, t->training_step, t->optimize_mlp, t->optimize_encoding, s);
 	m->stats_pending = true;

@@ -93,6 +93,10 @@ PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M
 SCRATCH_RAY_NUMSTEPS, SCRATCH_COORDS, SCRATCH_MLP_OUT, SCRATCH_RAY_COMPACTED, SCRATCH_DLOSS, SCRATCH_LOSS, \
     SCRATCH_COMPACT_COORDS = range(7)
 
+TIMERS = ["train_sampler", "train_encode", "train_mlp_infer", "train_loss", "train_mlp_bwd", "train_encode_bwd",
+          "optimizer", "grid_update", "render_encode", "render_mlp", "render_march"]
+TIMER = {name: i for i, name in enumerate(TIMERS)}
+
 EXPORTS = {
     "ngp_model_create": (C.c_int, [C.c_int, C.POINTER(NetworkConfig), C.c_uint64, C.POINTER(C.c_void_p)]),
     "ngp_model_destroy": (C.c_int, [C.c_void_p]),
@@ -121,6 +125,9 @@ EXPORTS = {
     "ngp_render": (C.c_int, [C.c_void_p, C.POINTER(RenderArgs), C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngp_accumulate_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_int, C.c_float, C.POINTER(C.c_float), C.c_int, C.c_void_p]),
+    "ngp_timing_enable": (C.c_int, [C.c_void_p, C.c_int]),
+    "ngp_timing_read": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_double), C.POINTER(C.c_uint64),
+                                  C.POINTER(C.c_uint32), C.c_int]),
     "ngp_last_error": (C.c_char_p, []),
     "ngp_version": (C.c_char_p, []),
 }

@@ -1132,6 +1132,10 @@ void oref_model_get(void* m, int kind, void* out) {
 	}
 }
 void oref_zero_grads(void* m) { auto& M = *static_cast<Model*>(m); std::fill(M.grads.begin(), M.grads.end(), 0.0f); }
+void oref_model_set_grads(void* m, const float* g) {
+	Model& M = *static_cast<Model*>(m);
+	std::memcpy(M.grads.data(), g, M.n * 4);
+}
 
 void oref_encode(void* m, const float* pos, uint32_t stride, uint32_t n, float* enc, int use_inf) {
 	Model& M = *static_cast<Model*>(m);

@@ -32,6 +32,7 @@ _PROTOS = {
     "oref_model_set_params": (None, [C.c_void_p, C.c_void_p]),
     "oref_model_get": (None, [C.c_void_p, C.c_int, C.c_void_p]),
     "oref_zero_grads": (None, [C.c_void_p]),
+    "oref_model_set_grads": (None, [C.c_void_p, C.c_void_p]),
     "oref_encode": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
     "oref_encode_indices": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     "oref_infer": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
@@ -110,6 +111,11 @@ class Oracle:
         out = np.zeros(self.n_params, dt)
         self.lib.oref_model_get(self.h, kind, ptr(out))
         return out
+
+    def set_grads(self, g):
+        g = np.ascontiguousarray(g, np.float32)
+        assert g.size == self.n_params
+        self.lib.oref_model_set_grads(self.h, ptr(g))
 
     def encode(self, pos, use_inf=False):
         pos = np.ascontiguousarray(pos, np.float32)

@@ -1,0 +1,203 @@
+"""End-to-end parity of the HIP training step, optimizer, occupancy grid and
+tracer against the scalar oracle (needs an MI355X).
+
+Bit-exact: ray sample counts and bases, sample coordinates, occupancy bitfield
+and mean for a given grid.  Tolerance: network outputs and everything that
+flows from them (fp16 MFMA vs sequential fp32 sums): loss-gradient rows and
+weight gradients within 2e-2 of the norm, rendered RGB within 1e-3 mean L1
+(north_star), occupancy values within 1e-2 relative.
+"""
+import ctypes as C
+
+import numpy as np
+import pytest
+import torch
+
+import ngp_abi as A
+from gpu_util import GpuModel, cuda_memcpy_d2h, cuda_memcpy_h2d, random_params, stream
+from oracle_abi import Oracle
+from scene_util import (DeviceDataset, HostDataset, grid_args, make_views, render_args, sphere_bitfield,
+                        train_args)
+
+pytestmark = pytest.mark.gpu
+
+CELLS = 128 ** 3
+
+
+def pair(cfg_kw, seed=0, grid_scale=0.5):
+    cfg = A.default_config(**cfg_kw)
+    g, o = GpuModel(cfg), Oracle(cfg)
+    rng = np.random.default_rng(seed)
+    p = random_params(g.n_params, g.n_mlp, g.info, rng, grid_scale)
+    g.set_params(p)
+    o.set_params(p)
+    return g, o, rng
+
+
+def gpu_scratch(g, kind, dtype, count=None):
+    p, n = C.c_void_p(), C.c_size_t()
+    A.check(g.lib.ngp_train_scratch(g.h, kind, C.byref(p), C.byref(n)))
+    out = np.zeros(n.value // np.dtype(dtype).itemsize if count is None else count, dtype)
+    cuda_memcpy_d2h(out, p.value)
+    return out
+
+
+def gpu_grid_buffers(g):
+    grid, bits, tmp, mean = C.c_void_p(), C.c_void_p(), C.c_void_p(), C.c_void_p()
+    A.check(g.lib.ngp_density_grid_buffers(g.h, C.byref(grid), C.byref(bits), C.byref(tmp), C.byref(mean)))
+    return grid.value, bits.value, tmp.value, mean.value
+
+
+def set_bitfield_both(g, o, grid, max_cascade=0):
+    o.grid_set(grid)
+    o.grid_bitfield(max_cascade)
+    gp, bp, _, _ = gpu_grid_buffers(g)
+    cuda_memcpy_h2d(gp, grid.astype(np.float32))
+    A.check(g.lib.ngp_density_grid_bitfield(g.h, max_cascade, stream()))
+    torch.cuda.synchronize()
+
+
+CFG_A = dict(n_levels=4, F=2, log2_T=14, n_neurons=16)
+CFG_B = dict(n_levels=16, F=2, log2_T=19, n_neurons=64)
+
+
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
+def test_train_step_matches_oracle(cfg_kw):
+    g, o, rng = pair(cfg_kw)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        grid = sphere_bitfield(0.32)
+        set_bitfield_both(g, o, grid)
+        R, B, MS = 384, 4096, 1 << 15
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+
+        gst = A.TrainStats()
+        A.check(g.lib.ngp_train_read_stats(g.h, C.byref(gst), stream()))
+        ost = o.stats()
+        assert gst.measured_batch_size_before_compaction == ost.measured_batch_size_before_compaction > 0
+
+        g_ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        o_ns = o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        np.testing.assert_array_equal(g_ns, o_ns)
+        # only slots claimed by kept rays hold samples (dropped rays leave a tail gap)
+        owned = np.zeros(MS, bool)
+        for n, b in o_ns:
+            owned[b:b + n] = True
+        assert owned.sum() > 1000
+        g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
+        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
+        np.testing.assert_array_equal(g_c, o_c)
+
+        g_out = gpu_scratch(g, A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][owned].astype(np.float32)
+        o_out = o.scratch(A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][owned].astype(np.float32)
+        assert np.abs(g_out - o_out).mean() < 2e-3
+
+        g_cp = gpu_scratch(g, A.SCRATCH_RAY_COMPACTED, np.uint32).reshape(-1, 2)
+        o_cp = o.scratch(A.SCRATCH_RAY_COMPACTED, np.uint32).reshape(-1, 2)
+        assert (g_cp[:, 0] == o_cp[:, 0]).mean() > 0.98
+        same = np.all(g_cp == o_cp) and gst.measured_batch_size == ost.measured_batch_size
+        np.testing.assert_allclose(gst.loss, ost.loss, rtol=2e-2)
+        if same:
+            C_ = min(ost.measured_batch_size, B)
+            g_dl = gpu_scratch(g, A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[:C_].astype(np.float32)
+            o_dl = o.scratch(A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[:C_].astype(np.float32)
+            assert np.linalg.norm(g_dl - o_dl) / np.linalg.norm(o_dl) < 2e-2
+            gg, og = g.get(A.GRADS_FP32), o.get(A.GRADS_FP32)
+            for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
+                rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
+                assert rel < 5e-2, rel
+    finally:
+        g.close()
+
+
+def test_optimizer_matches_oracle():
+    g, o, rng = pair(CFG_B)
+    try:
+        for step in (0, 1, 20000):
+            grads = np.zeros(g.n_params, np.float32)
+            grads[: g.n_mlp] = rng.normal(0, 1, g.n_mlp)
+            idx = rng.choice(g.n_params - g.n_mlp, 50000, replace=False) + g.n_mlp
+            grads[idx] = rng.normal(0, 1, idx.size)
+            gp, _ = g.buffer(A.GRADS_FP32)
+            cuda_memcpy_h2d(gp, grads)
+            o.set_grads(grads)
+            A.check(g.lib.ngp_optimizer_step(g.h, step, 1, 1, stream()))
+            torch.cuda.synchronize()
+            o.optimizer_step(step, 1, 1)
+        for kind in (A.PARAMS_FP32, A.PARAMS_EMA_FP32):
+            np.testing.assert_allclose(g.get(kind), o.get(kind), rtol=1e-5, atol=1e-7)
+        assert not g.get(A.GRADS_FP32).any()  # GradientMode::Overwrite: zeroed for the next step
+    finally:
+        g.close()
+
+
+def test_bitfield_and_mean_bit_exact():
+    g, o, rng = pair(CFG_A)
+    try:
+        grid = rng.exponential(0.01, CELLS).astype(np.float32)
+        grid[rng.random(CELLS) < 0.1] = -1.0
+        set_bitfield_both(g, o, grid)
+        _, bp, _, mp = gpu_grid_buffers(g)
+        gb = np.zeros(CELLS // 8 * 8, np.uint8)
+        cuda_memcpy_d2h(gb, bp)
+        gm = np.zeros(1, np.float32)
+        cuda_memcpy_d2h(gm, mp)
+        _, ob, om = o.grid_get(CELLS)
+        assert gm[0] == np.float32(om)
+        np.testing.assert_array_equal(gb, ob)
+    finally:
+        g.close()
+
+
+def test_density_grid_update_matches_oracle():
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        for step, (nu, nn) in enumerate([(CELLS, 0), (CELLS // 4, CELLS // 4)]):
+            ga = grid_args(dd.ptr, dd.n, nu, nn, ema_step=step, mark=int(step == 0), clear=int(step == 0))
+            oa = grid_args(hd.ptr, hd.n, nu, nn, ema_step=step, mark=int(step == 0), clear=int(step == 0))
+            A.check(g.lib.ngp_density_grid_update(g.h, C.byref(ga), stream()))
+            torch.cuda.synchronize()
+            o.grid_update(oa)
+        gp, bp, _, mp = gpu_grid_buffers(g)
+        gg = np.zeros(CELLS, np.float32)
+        cuda_memcpy_d2h(gg, gp)
+        og, ob, om = o.grid_get(CELLS)
+        np.testing.assert_array_equal(gg < 0, og < 0)  # mark_untrained decisions
+        np.testing.assert_allclose(gg, og, rtol=1e-2, atol=1e-6)
+        gb = np.zeros(CELLS // 8 * 8, np.uint8)
+        cuda_memcpy_d2h(gb, bp)
+        assert (np.unpackbits(gb) == np.unpackbits(ob)).mean() > 0.999
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("spp,snap,shard", [(0, 1, (0, 1, 8)), (3, 0, (1, 2, 8))])
+def test_render_matches_oracle(spp, snap, shard):
+    g, o, rng = pair(CFG_A, grid_scale=1.0)
+    try:
+        set_bitfield_both(g, o, sphere_bitfield(0.3))
+        W, H = 40, 32
+        cam = make_views(1, 8, 8)[1][0]
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        ra = render_args(W, H, cam, focal, spp=spp, snap=snap, shard=shard)
+        frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+        depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+        A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()),
+                                 stream()))
+        torch.cuda.synchronize()
+        gf = frame.cpu().numpy().reshape(H, W, 4)
+        of, od = o.render(ra)
+        rows = [y for y in range(H) if (y // shard[2]) % shard[1] == shard[0]]
+        assert (of[rows, :, 3] > 0.01).mean() > 0.2  # the sphere is in view
+        l1 = np.abs(gf[rows] - of[rows]).mean()
+        assert l1 < 1e-3, l1
+    finally:
+        g.close()
