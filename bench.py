@@ -86,6 +86,7 @@ def make_dataset(ngp, tb, n_views, res, device):
         tb.nerf.training.set_image_rgba8(i, imgs[i])
         tb.nerf.training.set_camera_extrinsics(i, cams[i], convert_to_ngp=False)
         tb.nerf.training.set_camera_intrinsics(i, fx=focal, fy=focal)
+    tb.nerf.training.n_images_for_training = n_views  # as the reference's create_empty_nerf_dataset callers do
     return cams, imgs, focal
 
 

@@ -124,6 +124,12 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 	reinterpret_cast<VT*>(enc)[(size_t)level * enc_plane + i] = o;
 }
 
+// Backward scatter.  Lanes of a wave hold consecutive samples of the compacted batch,
+// i.e. consecutive points along the same rays, so at the coarse levels neighbouring
+// lanes very often add into the same corner.  Runs of equal indices are summed across
+// lanes first (segmented shuffle scan) and only the last lane of each run issues the
+// global float atomic: the per-address contention that dominates the coarse levels
+// disappears, and waves without any run take the plain path.
 template <uint32_t F>
 __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ denc, uint32_t enc_plane,
@@ -133,25 +139,36 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
 	const uint32_t i = chunk * 256u + threadIdx.x;
 	if (n_dev) n = min(n, *n_dev);
-	if (i >= n) return;
+	if (chunk * 256u >= n) return;  // whole block idle (block-uniform)
+	const int lane = threadIdx.x & 63;
 
 	using VT = typename FeatVec<F>::T;
 	float g[F];
-	unpack<F>(reinterpret_cast<const VT*>(denc)[(size_t)level * enc_plane + i], g);
-	bool any = false;
+	bool active = i < n;
+	if (active) {
+		unpack<F>(reinterpret_cast<const VT*>(denc)[(size_t)level * enc_plane + i], g);
+		bool any = false;
 #pragma unroll
-	for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
-	if (!any) return;
+		for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
+		active = any;
+	} else {
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) g[f] = 0.0f;
+	}
+	if (__ballot(active) == 0ull) return;  // wave-uniform
 
 	const float scale = lt.scale[level];
 	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
 	float* gtab = grad + (size_t)lt.offset[level] * F;
 
-	float fx, fy, fz;
-	uint32_t gx, gy, gz;
-	pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
-	pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
-	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
+	float fx = 0.f, fy = 0.f, fz = 0.f;
+	uint32_t gx = 0, gy = 0, gz = 0;
+	if (active) {
+		pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
+		pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
+		pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
+	}
+	const unsigned long long lanes_below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 
 #pragma unroll
 	for (uint32_t c = 0; c < 8; ++c) {
@@ -159,9 +176,36 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 		w *= (c & 1u) ? fx : 1.0f - fx;
 		w *= (c & 2u) ? fy : 1.0f - fy;
 		w *= (c & 4u) ? fz : 1.0f - fz;
-		const uint32_t idx = grid_index(hashed, size, res, gx + (c & 1u), gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u));
+		const uint32_t idx = active ? grid_index(hashed, size, res, gx + (c & 1u), gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u))
+		                            : 0xFFFFFFFFu - (uint32_t)lane;  // inactive lanes never merge
+		float v[F];
 #pragma unroll
-		for (uint32_t f = 0; f < F; ++f) unsafeAtomicAdd(gtab + (size_t)idx * F + f, w * g[f]);
+		for (uint32_t f = 0; f < F; ++f) v[f] = w * g[f];
+		const uint32_t prev = __shfl_up(idx, 1, 64);
+		const bool head = lane == 0 || prev != idx;
+		const unsigned long long heads = __ballot(head);
+		if (~heads == 0ull) {
+			if (active) {
+#pragma unroll
+				for (uint32_t f = 0; f < F; ++f) unsafeAtomicAdd(gtab + (size_t)idx * F + f, v[f]);
+			}
+			continue;
+		}
+		// run start of this lane = highest head at or below it
+		const int start = 63 - __clzll(heads & (lanes_below | (1ull << lane)));
+#pragma unroll
+		for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) {
+				const float t = __shfl_up(v[f], off, 64);
+				if (lane - off >= start) v[f] += t;
+			}
+		}
+		const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
+		if (active && tail) {
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) unsafeAtomicAdd(gtab + (size_t)idx * F + f, v[f]);
+		}
 	}
 }
 

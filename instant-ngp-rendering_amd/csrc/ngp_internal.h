@@ -134,6 +134,7 @@ struct TrainScratch {
 	DevBuf<__half> cenc;               // [L][B][F]
 	DevBuf<__half> dloss;              // [B][4]
 	DevBuf<float> cweight;             // [B] rollover multiplicity
+	DevBuf<uint32_t> csrc;             // [B] compacted sample -> source sample index
 	DevBuf<__half> denc;               // [L][B][F]
 	DevBuf<float> loss;                // [R]
 	DevBuf<uint32_t> block_sums;       // scan scratch

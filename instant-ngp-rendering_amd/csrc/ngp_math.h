@@ -264,51 +264,86 @@ NGP_HD bool density_grid_occupied_at(v3 pos, const uint8_t* bitfield, uint32_t m
 	return bitfield[idx / 8 + (NERF_GRID_N_CELLS / 8) * mip] & (1u << (idx % 8));
 }
 
-// ---------------------------------------------------------------------------
-// Exponential (cone) stepping — nerf_device.cuh:359-459.
-// ---------------------------------------------------------------------------
+// Same lookup through a one-word cache: a 64-bit word of the Morton-ordered bitfield
+// covers a 4x4x4 block of cells, so a marching ray re-reads memory only when it leaves
+// that block.  Returns exactly what density_grid_occupied_at returns.
+struct OccCache {
+	uint32_t key;
+	uint64_t bits;
+};
+NGP_HD OccCache occ_cache_init() {
+	OccCache c;
+	c.key = 0xFFFFFFFFu;
+	c.bits = 0;
+	return c;
+}
+NGP_HD bool density_grid_occupied_cached(v3 pos, const uint8_t* bitfield, uint32_t mip, OccCache& c) {
+	uint32_t idx = cascaded_grid_idx_at(pos, mip);
+	if (idx == 0xFFFFFFFFu) return false;
+	const uint32_t key = (NERF_GRID_N_CELLS / 64) * mip + idx / 64;
+	if (key != c.key) {
+		c.key = key;
+		c.bits = reinterpret_cast<const uint64_t*>(bitfield)[key];
+	}
+	return (c.bits >> (idx % 64)) & 1ull;
+}
+
 NGP_HD float signf_(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
-NGP_HD float distance_to_next_voxel(v3 pos, v3 dir, v3 idir, float res) {
-	v3 p = (pos - 0.5f) * res;
-	float tx = (floorf(p.x + 0.5f + 0.5f * signf_(dir.x)) - p.x) * idir.x;
-	float ty = (floorf(p.y + 0.5f + 0.5f * signf_(dir.y)) - p.y) * idir.y;
-	float tz = (floorf(p.z + 0.5f + 0.5f * signf_(dir.z)) - p.z) * idir.z;
-	float t = fminf(fminf(tx, ty), tz);
-	return fmaxf(t / res, 0.0f);
+
+// ---------------------------------------------------------------------------
+// Stepping lattice.  A ray's candidate samples sit at n0 + k (k = 0, 1, ...) in the
+// reference's "stepping space" (uniform steps of MIN_CONE_STEPSIZE for cone_angle 0,
+// geometric steps otherwise; nerf_device.cuh:359-459).  A lattice point is a sample
+// when it lies in the AABB and its occupancy cell is set.  The reference reaches the
+// same points by chaining t += calc_dt(t) and advance_to_next_voxel(); defining them
+// as n0 + k lets a wave test 64 lattice points of one ray at once (training sampler)
+// and lets the render skip an empty cell in one jump whose exactness is verified.
+// Division by constants is a multiply by the reciprocal (the reference is built
+// with --use_fast_math, CMakeLists.txt:82); the log-regime constants are resolved
+// once per launch (make_stepping) instead of per call.
+// ---------------------------------------------------------------------------
+constexpr float INV_MIN_CONE_STEPSIZE = 1.0f / MIN_CONE_STEPSIZE;
+constexpr float INV_MAX_CONE_STEPSIZE = 1.0f / MAX_CONE_STEPSIZE;
+struct Stepping {
+	float cone, l, inv_l, a, b, at, bt;
+};
+inline Stepping make_stepping(float cone) {
+	Stepping s;
+	s.cone = cone;
+	if (cone <= 1e-5f) {
+		s.l = s.inv_l = s.a = s.b = s.at = s.bt = 0.0f;
+		return s;
+	}
+	s.l = logf(1.0f + cone);
+	s.inv_l = 1.0f / s.l;
+	s.a = (logf(MIN_CONE_STEPSIZE) - logf(s.l)) * s.inv_l;
+	s.b = (logf(MAX_CONE_STEPSIZE) - logf(s.l)) * s.inv_l;
+	s.at = expf(s.a * s.l);
+	s.bt = expf(s.b * s.l);
+	return s;
 }
-NGP_HD float to_stepping_space(float t, float cone_angle) {
-	if (cone_angle <= 1e-5f) return t / MIN_CONE_STEPSIZE;
-	float log1p_c = logf(1.0f + cone_angle);
-	float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	float at = expf(a * log1p_c);
-	float bt = expf(b * log1p_c);
-	if (t <= at) return (t - at) / MIN_CONE_STEPSIZE + a;
-	else if (t <= bt) return logf(t) / log1p_c;
-	else return (t - bt) / MAX_CONE_STEPSIZE + b;
+NGP_HD float step_to(const Stepping& s, float t) {
+	if (s.cone <= 1e-5f) return t * INV_MIN_CONE_STEPSIZE;
+	if (t <= s.at) return (t - s.at) * INV_MIN_CONE_STEPSIZE + s.a;
+	if (t <= s.bt) return logf(t) * s.inv_l;
+	return (t - s.bt) * INV_MAX_CONE_STEPSIZE + s.b;
 }
-NGP_HD float from_stepping_space(float n, float cone_angle) {
-	if (cone_angle <= 1e-5f) return n * MIN_CONE_STEPSIZE;
-	float log1p_c = logf(1.0f + cone_angle);
-	float a = (logf(MIN_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	float b = (logf(MAX_CONE_STEPSIZE) - logf(log1p_c)) / log1p_c;
-	float at = expf(a * log1p_c);
-	float bt = expf(b * log1p_c);
-	if (n <= a) return (n - a) * MIN_CONE_STEPSIZE + at;
-	else if (n <= b) return expf(n * log1p_c);
-	else return (n - b) * MAX_CONE_STEPSIZE + bt;
+NGP_HD float step_from(const Stepping& s, float n) {
+	if (s.cone <= 1e-5f) return n * MIN_CONE_STEPSIZE;
+	if (n <= s.a) return (n - s.a) * MIN_CONE_STEPSIZE + s.at;
+	if (n <= s.b) return expf(n * s.l);
+	return (n - s.b) * MAX_CONE_STEPSIZE + s.bt;
 }
-NGP_HD float advance_n_steps(float t, float cone_angle, float n) {
-	return from_stepping_space(to_stepping_space(t, cone_angle) + n, cone_angle);
+// distance to the boundary of the current cell at resolution 128 * 2^-mip (power-of-two scales: exact)
+NGP_HD float distance_to_next_cell(v3 pos, v3 dir, v3 idir, uint32_t mip) {
+	const float res = scalbnf((float)NERF_GRIDSIZE, -(int)mip), inv_res = scalbnf(1.0f / (float)NERF_GRIDSIZE, (int)mip);
+	const v3 p = (pos - 0.5f) * res;
+	const float tx = (floorf(p.x + 0.5f + 0.5f * signf_(dir.x)) - p.x) * idir.x;
+	const float ty = (floorf(p.y + 0.5f + 0.5f * signf_(dir.y)) - p.y) * idir.y;
+	const float tz = (floorf(p.z + 0.5f + 0.5f * signf_(dir.z)) - p.z) * idir.z;
+	return fmaxf(fminf(fminf(tx, ty), tz) * inv_res, 0.0f);
 }
-NGP_HD float calc_dt(float t, float cone_angle) { return advance_n_steps(t, cone_angle, 1.0f) - t; }
-NGP_HD float advance_to_next_voxel(float t, float cone_angle, v3 pos, v3 dir, v3 idir, uint32_t mip) {
-	float res = scalbnf((float)NERF_GRIDSIZE, -(int)mip);
-	float t_target = t + distance_to_next_voxel(pos, dir, idir, res);
-	t = to_stepping_space(t, cone_angle);
-	t_target = to_stepping_space(t_target, cone_angle);
-	return from_stepping_space(t + ceilf(fmaxf(t_target - t, 0.5f)), cone_angle);
-}
+
 NGP_HD uint32_t mip_from_pos(v3 pos, uint32_t max_cascade = NERF_CASCADES - 1) {
 	int exponent;
 	float maxval = maxc(absv(pos - 0.5f));
@@ -327,18 +362,46 @@ NGP_HD uint32_t mip_from_dt(float dt, v3 pos, uint32_t max_cascade = NERF_CASCAD
 	m = m > (int)max_cascade ? (int)max_cascade : m;
 	return (uint32_t)m;
 }
-// if_unoccupied_advance_to_next_occupied_voxel (nerf_device.cuh:461-494), identity
-// render_aabb_to_local, MIP_FROM_DT=false.
-NGP_HD float if_unoccupied_advance_to_next_occupied_voxel(float t, float cone_angle, v3 o, v3 d, v3 idir,
-		const uint8_t* bitfield, uint32_t min_mip, uint32_t max_mip, const aabb3& aabb) {
+
+// Render march (if_unoccupied_advance_to_next_occupied_voxel, nerf_device.cuh:461-494, on
+// the lattice): moves *n to the first lattice point at or after it whose cell (at
+// clamp(mip_from_pos, 0, max_mip)) is occupied; false once the ray leaves the AABB.
+// An empty cell is skipped in one jump to the first lattice point past its far face
+// (at the coarsest empty mip, as the reference does) -- or, when the whole Morton
+// block of 4x4x4 cells around it is empty (one zero 64-bit bitfield word), past the
+// block's far face.  The jump is taken only if the lattice point just before the
+// landing point is still inside the skipped cell/block, so every skipped point
+// provably lies in empty space and the result equals testing the points one by one.
+NGP_HD bool next_occupied_lattice_point(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
+                                        uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
+	float n = *n_io;
 	while (true) {
-		v3 pos = o + d * t;
-		if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return MAX_DEPTH;
+		const float t = step_from(st, n);
+		const v3 pos = o + d * t;
+		if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) {
+			*n_io = n;
+			return false;
+		}
 		uint32_t mip = mip_from_pos(pos);
-		mip = mip < min_mip ? min_mip : (mip > max_mip ? max_mip : mip);
-		if (!bitfield || density_grid_occupied_at(pos, bitfield, mip)) return t;
-		while (mip < max_mip && !density_grid_occupied_at(pos, bitfield, mip + 1)) ++mip;
-		t = advance_to_next_voxel(t, cone_angle, pos, d, idir, mip);
+		mip = mip > max_mip ? max_mip : mip;
+		if (density_grid_occupied_cached(pos, bitfield, mip, cache)) {
+			*n_io = n;
+			return true;
+		}
+		while (mip < max_mip && !density_grid_occupied_cached(pos, bitfield, mip + 1, cache)) ++mip;
+		// the cached word now covers the 4x4x4-cell block around pos at `mip`: if it is all
+		// zero, jump over the whole block (cells of 4x the size), else over the one cell
+		const uint32_t cell = cascaded_grid_idx_at(pos, mip);
+		(void)density_grid_occupied_cached(pos, bitfield, mip, cache);
+		const uint32_t shift = (cell != 0xFFFFFFFFu && cache.bits == 0ull) ? 6u : 0u;
+		const uint32_t here = cell >> shift;
+		const float n_far = step_to(st, t + distance_to_next_cell(pos, d, idir, mip + (shift ? 2u : 0u)));
+		float nn = n + ceilf(fmaxf(n_far - n, 0.5f));
+		if (nn - n > 1.0f) {
+			const v3 last = o + d * step_from(st, nn - 1.0f);
+			if ((cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
+		}
+		n = nn;
 	}
 }
 

@@ -18,7 +18,7 @@ namespace ngp {
 struct Payload {
 	float o[3];
 	float d[3];
-	float t;
+	float n;  // next lattice point to test (stepping space)
 	float max_weight;
 	uint32_t idx;
 	uint32_t n_steps;
@@ -34,7 +34,7 @@ struct RenderK {
 	float fx, fy, scx, scy;
 	float near_distance;
 	aabb3 aabb, train_aabb;
-	float cone_angle;
+	Stepping st;
 	uint32_t max_mip;
 	float min_transmittance;
 	int snap;
@@ -78,18 +78,18 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 	dir = normalize(dir);
 	float t0, t1;
 	ray_intersect(k.aabb, origin, dir, &t0, &t1);
-	float t = fmaxf(t0, 0.0f) + 1e-6f;
+	const float t = fmaxf(t0, 0.0f) + 1e-6f;
 	p.o[0] = origin.x; p.o[1] = origin.y; p.o[2] = origin.z;
 	p.d[0] = dir.x; p.d[1] = dir.y; p.d[2] = dir.z;
-	p.t = t;
+	p.n = 0.0f;
 	p.alive = aabb_contains(k.aabb, origin + dir * t) ? 1u : 0u;
 	if (p.alive) {
 		// advance_pos_nerf: jitter the start and skip empty space
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
-		t = advance_n_steps(t, k.cone_angle, ld_random_val(k.sample_index, idx * 786433u));
-		t = if_unoccupied_advance_to_next_occupied_voxel(t, k.cone_angle, origin, dir, idir, k.bitfield, 0, k.max_mip, k.aabb);
-		if (t >= MAX_DEPTH) p.alive = 0;
-		else p.t = t;
+		float n = step_to(k.st, t) + ld_random_val(k.sample_index, idx * 786433u);
+		OccCache occ = occ_cache_init();
+		p.alive = next_occupied_lattice_point(&n, k.st, origin, dir, idir, k.bitfield, k.max_mip, k.aabb, occ) ? 1u : 0u;
+		p.n = n;
 	}
 	payloads[r] = p;
 }
@@ -143,21 +143,22 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 	const v3 o = mk3(p.o[0], p.o[1], p.o[2]), d = mk3(p.d[0], p.d[1], p.d[2]);
 	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 	const v3 wdir = warp_direction(d);
-	float t = p.t;
+	float n = p.n;
+	OccCache occ = occ_cache_init();
 	for (uint32_t j = 0; j < n_steps; ++j) {
-		t = if_unoccupied_advance_to_next_occupied_voxel(t, k.cone_angle, o, d, idir, k.bitfield, 0, k.max_mip, k.aabb);
-		if (t >= MAX_DEPTH) {
+		if (!next_occupied_lattice_point(&n, k.st, o, d, idir, k.bitfield, k.max_mip, k.aabb, occ)) {
 			p.n_steps = j;
 			return;
 		}
-		const float dt = calc_dt(t, k.cone_angle);
+		const float t = step_from(k.st, n);
+		const float dt = step_from(k.st, n + 1.0f) - t;
 		const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 		float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)j * n_alive));
 		c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
 		c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
-		t += dt;
+		n += 1.0f;
 	}
-	p.t = t;
+	p.n = n;
 	p.n_steps = n_steps;
 }
 
@@ -298,7 +299,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.aabb.max = mk3(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2]);
 	k.train_aabb.min = mk3(a->train_aabb_min[0], a->train_aabb_min[1], a->train_aabb_min[2]);
 	k.train_aabb.max = mk3(a->train_aabb_max[0], a->train_aabb_max[1], a->train_aabb_max[2]);
-	k.cone_angle = a->cone_angle_constant;
+	k.st = make_stepping(a->cone_angle_constant);
 	k.max_mip = a->max_cascade;
 	k.min_transmittance = a->min_transmittance;
 	k.snap = a->snap_to_pixel_centers;
@@ -357,7 +358,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		n_alive = rs.host_counter.ptr[0];
 		if (n_alive == 0) break;
 		const uint32_t target = 2 * 1024 * 1024;
-		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), 8u);
+		// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
+		// every ray composites its own samples in order and stops at the same one whatever the chunking
+		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), 32u);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_generate<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);

@@ -499,7 +499,8 @@ Json Testbed::load_network_config(const std::string& path) const {
 	Json j = Json::parse(read_text(path));
 	// merge_parent_network_config (src/testbed.cu:86-97)
 	if (j.contains("parent")) {
-		const std::string pp = parent_path(path) + "/" + j["parent"].str();
+		const std::string& par = j["parent"].str();
+		const std::string pp = (!par.empty() && par[0] == '/') ? par : parent_path(path) + "/" + par;
 		Json parent = load_network_config(pp);
 		parent.merge_patch(j);
 		j = parent;

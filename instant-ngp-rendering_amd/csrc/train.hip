@@ -12,6 +12,8 @@
 // rule the reference applies ("claim `numsteps` slots, drop the ray if
 // base + numsteps > cap") taken in ray-index order: deterministic, and
 // bit-identical to the scalar oracle.
+#include <type_traits>
+
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -131,7 +133,7 @@ struct SamplerArgs {
 	uint32_t max_samples;
 	pcg32 rng;
 	aabb3 aabb;
-	float cone_angle;
+	Stepping st;
 	uint32_t max_mip;
 	int snap;
 	const uint8_t* bitfield;
@@ -142,8 +144,9 @@ struct SamplerArgs {
 	float* coords;       // [max][8]
 };
 
-// Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777).
-__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* startt) {
+// Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777);
+// *n0 = first lattice point (stepping space) = entry + jitter.
+__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0) {
 	const uint32_t img = image_idx(gi, a.n_rays_global, a.n_images);
 	const ngp_image im = a.images[img];
 	pcg32 rng = a.rng;
@@ -169,67 +172,97 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 	float t0, t1;
 	ray_intersect(a.aabb, *o, *d, &t0, &t1);
 	t0 = fmaxf(t0, 0.0f);
-	*startt = advance_n_steps(t0, a.cone_angle, rng.next_float());
+	*n0 = step_to(a.st, t0) + rng.next_float();
 	return true;
 }
 
-__global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	if (i >= a.n_rays) return;
-	v3 o, d;
-	float t;
-	uint32_t j = 0;
-	if (training_ray(a, a.ray_offset + i, &o, &d, &t)) {
-		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-		v3 pos;
-		while (aabb_contains(a.aabb, pos = o + d * t) && j < NERF_STEPS) {
-			const float dt = calc_dt(t, a.cone_angle);
-			const uint32_t mip = mip_from_dt(dt, pos, a.max_mip);
-			if (density_grid_occupied_at(pos, a.bitfield, mip)) {
-				++j;
-				t += dt;
-			} else {
-				t = advance_to_next_voxel(t, a.cone_angle, pos, d, idir, mip);
-			}
-		}
-	}
-	a.counts[i] = j;
+// Lattice point k of a training ray: inside the AABB? a sample (occupied at mip_from_dt)?
+struct LatticePoint {
+	bool inside, occupied;
+	float t, dt;
+	v3 pos;
+};
+__device__ __forceinline__ LatticePoint training_lattice_point(const SamplerArgs& a, v3 o, v3 d, float n0, uint32_t k) {
+	LatticePoint p;
+	const float n = n0 + (float)k;
+	p.t = step_from(a.st, n);
+	p.dt = step_from(a.st, n + 1.0f) - p.t;
+	p.pos = o + d * p.t;
+	p.inside = aabb_contains(a.aabb, p.pos);
+	p.occupied = p.inside && density_grid_occupied_at(p.pos, a.bitfield, mip_from_dt(p.dt, p.pos, a.max_mip));
+	return p;
 }
 
+// generate_training_samples_nerf (testbed_nerf.cu:679-839), pass 1: one wave per ray,
+// 64 lattice points per iteration; the count stops at the first point outside the
+// AABB or at NERF_STEPS samples, like the reference's sequential loop.
+__global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63u;
+	if (i >= a.n_rays) return;  // wave-uniform
+	v3 o, d;
+	float n0;
+	uint32_t count = 0;
+	if (training_ray(a, a.ray_offset + i, &o, &d, &n0)) {
+		for (uint32_t kb = 0;; kb += 64) {
+			const LatticePoint p = training_lattice_point(a, o, d, n0, kb + lane);
+			const unsigned long long out = __ballot(!p.inside);
+			const unsigned long long valid = out ? ((1ull << (__ffsll((long long)out) - 1)) - 1ull) : ~0ull;
+			const uint32_t c = __popcll(__ballot(p.occupied) & valid);
+			if (count + c >= NERF_STEPS) {
+				count = NERF_STEPS;
+				break;
+			}
+			count += c;
+			if (out) break;
+		}
+	}
+	if (lane == 0) a.counts[i] = count;
+}
+
+// pass 2: same walk, each sample written at base + (its rank among the ray's samples);
+// consecutive lanes write consecutive 32-byte coordinates.
 __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63u;
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.counts[i], base = a.bases[i];
 	if (n == 0 || base + n > a.max_samples) {
-		a.numsteps[2 * i + 0] = 0;
-		a.numsteps[2 * i + 1] = 0;
+		if (lane == 0) {
+			a.numsteps[2 * i + 0] = 0;
+			a.numsteps[2 * i + 1] = 0;
+		}
 		return;
 	}
 	v3 o, d;
-	float t;
-	training_ray(a, a.ray_offset + i, &o, &d, &t);
-	a.numsteps[2 * i + 0] = n;
-	a.numsteps[2 * i + 1] = base;
-	float* rs = a.ray_state + 8 * (size_t)i;
-	rs[0] = o.x; rs[1] = o.y; rs[2] = o.z;
-	rs[3] = d.x; rs[4] = d.y; rs[5] = d.z;
-	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	float n0;
+	training_ray(a, a.ray_offset + i, &o, &d, &n0);
+	if (lane == 0) {
+		a.numsteps[2 * i + 0] = n;
+		a.numsteps[2 * i + 1] = base;
+		float* rs = a.ray_state + 8 * (size_t)i;
+		rs[0] = o.x; rs[1] = o.y; rs[2] = o.z;
+		rs[3] = d.x; rs[4] = d.y; rs[5] = d.z;
+	}
 	const v3 wdir = warp_direction(d);
+	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 	uint32_t j = 0;
-	v3 pos;
-	while (aabb_contains(a.aabb, pos = o + d * t) && j < n) {
-		const float dt = calc_dt(t, a.cone_angle);
-		const uint32_t mip = mip_from_dt(dt, pos, a.max_mip);
-		if (density_grid_occupied_at(pos, a.bitfield, mip)) {
-			const v3 wp = aabb_relative(a.aabb, pos);
-			float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + j));
-			c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-			c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
-			++j;
-			t += dt;
-		} else {
-			t = advance_to_next_voxel(t, a.cone_angle, pos, d, idir, mip);
+	for (uint32_t kb = 0; j < n; kb += 64) {
+		const LatticePoint p = training_lattice_point(a, o, d, n0, kb + lane);
+		const unsigned long long out = __ballot(!p.inside);
+		const unsigned long long valid = out ? ((1ull << (__ffsll((long long)out) - 1)) - 1ull) : ~0ull;
+		const unsigned long long m = __ballot(p.occupied) & valid;
+		if ((m >> lane) & 1ull) {
+			const uint32_t r = j + __popcll(m & below);
+			if (r < n) {
+				const v3 wp = aabb_relative(a.aabb, p.pos);
+				float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + r));
+				c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
+				c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+			}
 		}
+		j += __popcll(m);
+		if (out) break;
 	}
 }
 
@@ -266,8 +299,7 @@ struct LossArgs {
 	float* loss_state;     // [R][8]: grad xyz, rgb_ray xyz, mean_loss, pad
 	uint32_t* compacted;   // [R][2]
 	float* loss_out;       // [R]
-	float* ccoords;        // [B][8]
-	__half* cenc;          // [L][B][F]
+	uint32_t* csrc;        // [B] compacted -> source sample
 	__half* dloss;         // [B][4]
 	const float* mean_density;
 };
@@ -373,20 +405,13 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 	float T = 1.0f;
 	for (uint32_t j = 0; j < cn; ++j) {
 		const size_t src = base + j, dst = cbase + j;
-		const float4* ci = reinterpret_cast<const float4*>(a.coords + 8 * src);
-		const float4 c0 = ci[0], c1 = ci[1];
-		float4* co = reinterpret_cast<float4*>(a.ccoords + 8 * dst);
-		co[0] = c0;
-		co[1] = c1;
-		for (uint32_t l = 0; l < a.n_levels; ++l) {
-			const __half* es = a.enc + ((size_t)l * a.enc_plane + src) * a.F;
-			__half* ed = a.cenc + ((size_t)l * a.target_batch + dst) * a.F;
-			for (uint32_t f = 0; f < a.F; ++f) ed[f] = es[f];
-		}
+		a.csrc[dst] = (uint32_t)src;
+		const float4 c0 = *reinterpret_cast<const float4*>(a.coords + 8 * src);
 		const v3 pos = unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb);
 		const float depth = length(pos - ray_o);
 		const float dt = unwarp_dt(c0.w);
-		const __half* o = a.mlp_out + 4 * src;
+		const uint2 ob = *reinterpret_cast<const uint2*>(a.mlp_out + 4 * src);
+		const __half* o = reinterpret_cast<const __half*>(&ob);
 		const float o0 = __half2float(o[0]), o1 = __half2float(o[1]), o2 = __half2float(o[2]), o3 = __half2float(o[3]);
 		const v3 rgb = mk3(network_to_rgb(o0, a.rgb_act), network_to_rgb(o1, a.rgb_act), network_to_rgb(o2, a.rgb_act));
 		const float density = network_to_density(o3, a.density_act);
@@ -396,7 +421,7 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		T *= (1.0f - alpha);
 		const v3 suffix = rgb_ray - rgb_ray2;
 		const v3 dloss_by_drgb = grad * weight;
-		__half* dl = a.dloss + 4 * dst;
+		__half dl[4];
 		dl[0] = __float2half(loss_scale * (dloss_by_drgb.x * network_to_rgb_derivative(o0, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o0)));
 		dl[1] = __float2half(loss_scale * (dloss_by_drgb.y * network_to_rgb_derivative(o1, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o1)));
 		dl[2] = __float2half(loss_scale * (dloss_by_drgb.z * network_to_rgb_derivative(o2, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o2)));
@@ -404,7 +429,29 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		const float dloss_by_dmlp = density_derivative * (dt * dot(grad, rgb * T - suffix));
 		dl[3] = __float2half(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
 		                     (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
+		*reinterpret_cast<uint2*>(a.dloss + 4 * dst) = *reinterpret_cast<const uint2*>(dl);
 	}
+}
+
+// Gather the compacted batch (coords + per-level features) in compacted order: one
+// thread per compacted sample, so every level plane is written by contiguous lanes.
+template <uint32_t F>
+__global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ csrc,
+                                                          const float* __restrict__ coords, const __half* __restrict__ enc,
+                                                          uint32_t enc_plane, uint32_t n_levels, float* __restrict__ ccoords,
+                                                          __half* __restrict__ cenc, uint32_t target) {
+	const uint32_t dst = blockIdx.x * 256u + threadIdx.x;
+	if (dst >= *n_ptr) return;
+	const uint32_t src = csrc[dst];
+	const float4* ci = reinterpret_cast<const float4*>(coords + 8 * (size_t)src);
+	float4* co = reinterpret_cast<float4*>(ccoords + 8 * (size_t)dst);
+	co[0] = ci[0];
+	co[1] = ci[1];
+	using VT = typename std::conditional<F == 1, uint16_t, typename std::conditional<F == 2, uint32_t,
+	                                     typename std::conditional<F == 4, uint2, uint4>::type>::type>::type;
+	const VT* es = reinterpret_cast<const VT*>(enc);
+	VT* ed = reinterpret_cast<VT*>(cenc);
+	for (uint32_t l = 0; l < n_levels; ++l) ed[(size_t)l * target + dst] = es[(size_t)l * enc_plane + src];
 }
 
 // Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
@@ -546,6 +593,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.cenc.reserve((size_t)L * B * F);
 	ts.dloss.reserve(4 * (size_t)B);
 	ts.cweight.reserve(B);
+	ts.csrc.reserve(B);
 	ts.denc.reserve((size_t)L * B * F);
 	ts.block_sums.reserve(div_up(std::max(R, 1u), 1024) + 16);
 	ts.counters.reserve(16);
@@ -569,7 +617,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.rng.inc = t->rng_inc;
 	sa.aabb.min = mk3(t->aabb_min[0], t->aabb_min[1], t->aabb_min[2]);
 	sa.aabb.max = mk3(t->aabb_max[0], t->aabb_max[1], t->aabb_max[2]);
-	sa.cone_angle = t->cone_angle_constant;
+	sa.st = make_stepping(t->cone_angle_constant);
 	sa.max_mip = t->max_cascade;
 	sa.snap = t->snap_to_pixel_centers;
 	sa.bitfield = m->gs.bitfield.ptr;
@@ -581,9 +629,9 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	const uint32_t rb = div_up(R, 256);
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
-	k_sample_count<<<rb, 256, 0, s>>>(sa);
+	k_sample_count<<<div_up(R, 4), 256, 0, s>>>(sa);
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
-	k_sample_write<<<rb, 256, 0, s>>>(sa);
+	k_sample_write<<<div_up(R, 4), 256, 0, s>>>(sa);
 	NGP_HIP_CHECK(hipGetLastError());
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
@@ -630,8 +678,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.loss_state = ts.ray_loss_state.ptr;
 	la.compacted = ts.ray_compacted.ptr;
 	la.loss_out = ts.loss.ptr;
-	la.ccoords = ts.ccoords.ptr;
-	la.cenc = ts.cenc.ptr;
+	la.csrc = ts.csrc.ptr;
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
@@ -642,6 +689,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 
 	// compacted batch size c = min(total, B); rollover multiplicity
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
+	switch (F) {
+		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
+		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
+		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
+		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
+	}
 	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
 	tm.end(NGP_TIMER_TRAIN_LOSS, s, R);

@@ -219,39 +219,44 @@ static const float MAX_STEP = MIN_STEP * 128.0f * 1024.0f / 128.0f;
 static const float MAXD = 16384.0f;
 
 static float sgn(float x) { return x > 0 ? 1.0f : (x < 0 ? -1.0f : 0.0f); }
-static float to_step(float t, float c) {
-	if (c <= 1e-5f) return t / MIN_STEP;
-	const float l = std::log(1.0f + c);
-	const float a = (std::log(MIN_STEP) - std::log(l)) / l, b = (std::log(MAX_STEP) - std::log(l)) / l;
-	const float at = std::exp(a * l), bt = std::exp(b * l);
-	if (t <= at) return (t - at) / MIN_STEP + a;
-	if (t <= bt) return std::log(t) / l;
-	return (t - bt) / MAX_STEP + b;
+// Stepping lattice (see ngp_math.h "Stepping lattice"): samples sit at n0 + k in stepping
+// space; constants of the log regime resolved once; divisions by constants are
+// multiplies by the reciprocal (the reference builds with --use_fast_math).
+static const float INV_MIN_STEP = 1.0f / MIN_STEP;
+static const float INV_MAX_STEP = 1.0f / MAX_STEP;
+struct Stepping {
+	float cone, l, inv_l, a, b, at, bt;
+};
+static Stepping make_stepping(float cone) {
+	Stepping s{cone, 0, 0, 0, 0, 0, 0};
+	if (cone <= 1e-5f) return s;
+	s.l = logf(1.0f + cone);
+	s.inv_l = 1.0f / s.l;
+	s.a = (logf(MIN_STEP) - logf(s.l)) * s.inv_l;
+	s.b = (logf(MAX_STEP) - logf(s.l)) * s.inv_l;
+	s.at = expf(s.a * s.l);
+	s.bt = expf(s.b * s.l);
+	return s;
 }
-static float from_step(float n, float c) {
-	if (c <= 1e-5f) return n * MIN_STEP;
-	const float l = std::log(1.0f + c);
-	const float a = (std::log(MIN_STEP) - std::log(l)) / l, b = (std::log(MAX_STEP) - std::log(l)) / l;
-	const float at = std::exp(a * l), bt = std::exp(b * l);
-	if (n <= a) return (n - a) * MIN_STEP + at;
-	if (n <= b) return std::exp(n * l);
-	return (n - b) * MAX_STEP + bt;
+static float lat_to(const Stepping& s, float t) {
+	if (s.cone <= 1e-5f) return t * INV_MIN_STEP;
+	if (t <= s.at) return (t - s.at) * INV_MIN_STEP + s.a;
+	if (t <= s.bt) return logf(t) * s.inv_l;
+	return (t - s.bt) * INV_MAX_STEP + s.b;
 }
-static float adv_n(float t, float c, float n) { return from_step(to_step(t, c) + n, c); }
-static float calc_dt(float t, float c) { return adv_n(t, c, 1.0f) - t; }
-static float dist_next_voxel(V3 p0, V3 d, V3 idir, float res) {
-	const V3 p = (p0 - v(0.5f, 0.5f, 0.5f)) * res;
+static float lat_from(const Stepping& s, float n) {
+	if (s.cone <= 1e-5f) return n * MIN_STEP;
+	if (n <= s.a) return (n - s.a) * MIN_STEP + s.at;
+	if (n <= s.b) return expf(n * s.l);
+	return (n - s.b) * MAX_STEP + s.bt;
+}
+static float dist_next_cell(V3 pos, V3 d, V3 idir, uint32_t mip) {
+	const float res = std::scalbn((float)GRID, -(int)mip), inv_res = std::scalbn(1.0f / (float)GRID, (int)mip);
+	const V3 p = (pos - v(0.5f, 0.5f, 0.5f)) * res;
 	const float tx = (std::floor(p.x + 0.5f + 0.5f * sgn(d.x)) - p.x) * idir.x;
 	const float ty = (std::floor(p.y + 0.5f + 0.5f * sgn(d.y)) - p.y) * idir.y;
 	const float tz = (std::floor(p.z + 0.5f + 0.5f * sgn(d.z)) - p.z) * idir.z;
-	return std::max(std::min(std::min(tx, ty), tz) / res, 0.0f);
-}
-static float adv_voxel(float t, float c, V3 pos, V3 d, V3 idir, uint32_t mip) {
-	const float res = std::scalbn((float)GRID, -(int)mip);
-	float tt = t + dist_next_voxel(pos, d, idir, res);
-	t = to_step(t, c);
-	tt = to_step(tt, c);
-	return from_step(t + std::ceil(std::max(tt - t, 0.5f)), c);
+	return std::max(std::min(std::min(tx, ty), tz) * inv_res, 0.0f);
 }
 static uint32_t mip_pos(V3 p, uint32_t maxc = CASCADES - 1) {
 	int e;
@@ -280,14 +285,30 @@ static bool occupied(V3 p, const uint8_t* bits, uint32_t mip) {
 	if (i == 0xFFFFFFFFu) return false;
 	return bits[i / 8 + CELLS / 8 * mip] & (1u << (i % 8));
 }
-static float skip_empty(float t, float c, V3 o, V3 d, V3 idir, const uint8_t* bits, uint32_t maxm, const Box& b) {
+// First occupied lattice point at or after *n (render march); an empty cell is jumped over
+// only when the lattice point before the landing point is still inside it.
+static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, const uint8_t* bits, uint32_t maxm,
+                          const Box& b) {
+	float n = *n_io;
 	while (true) {
+		const float t = lat_from(st, n);
 		const V3 pos = o + d * t;
-		if (t >= MAXD || !b.contains(pos)) return MAXD;
+		if (t >= MAXD || !b.contains(pos)) { *n_io = n; return false; }
 		uint32_t mip = std::min(mip_pos(pos), maxm);
-		if (!bits || occupied(pos, bits, mip)) return t;
+		if (occupied(pos, bits, mip)) { *n_io = n; return true; }
 		while (mip < maxm && !occupied(pos, bits, mip + 1)) ++mip;
-		t = adv_voxel(t, c, pos, d, idir, mip);
+		// whole 4x4x4 Morton block empty (its 64-bit word is zero)? jump the block, else the cell
+		const uint32_t cell = grid_idx(pos, mip);
+		uint64_t word = 1;
+		if (cell != 0xFFFFFFFFu) std::memcpy(&word, &bits[(size_t)CELLS / 8 * mip + (cell / 64) * 8], 8);
+		const uint32_t shift = word == 0 ? 6u : 0u;
+		const float n_far = lat_to(st, t + dist_next_cell(pos, d, idir, mip + (shift ? 2u : 0u)));
+		float nn = n + std::ceil(std::max(n_far - n, 0.5f));
+		if (nn - n > 1.0f) {
+			const V3 last = o + d * lat_from(st, nn - 1.0f);
+			if ((grid_idx(last, mip) >> shift) != (cell >> shift)) nn = n + 1.0f;
+		}
+		n = nn;
 	}
 }
 static float warp_dt(float dt) { return (dt - MIN_STEP) / (MIN_STEP * 128.0f - MIN_STEP); }
@@ -688,7 +709,7 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	float t0, t1;
 	b.intersect(*o, *d, &t0, &t1);
 	t0 = std::max(t0, 0.0f);
-	*st = adv_n(t0, a.cone_angle_constant, rng.nextf());
+	*st = lat_to(make_stepping(a.cone_angle_constant), t0) + rng.nextf();  // n0: first lattice point
 	return true;
 }
 
@@ -696,7 +717,16 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	const uint32_t R = a.n_rays, B = a.target_batch_size, MS = a.max_samples;
 	const uint32_t nrg = a.n_rays_global ? a.n_rays_global : R;
 	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
-	const float cone = a.cone_angle_constant;
+	const Stepping stp = make_stepping(a.cone_angle_constant);
+	// lattice point k of a ray: n0 + k (stepping space); a sample if inside the AABB and occupied
+	auto lattice = [&](V3 o, V3 d, float n0, uint32_t k, float* t, float* dt, V3* pos) {
+		const float n = n0 + (float)k;
+		*t = lat_from(stp, n);
+		*dt = lat_from(stp, n + 1.0f) - *t;
+		*pos = o + d * *t;
+		if (!box.contains(*pos)) return -1;
+		return occupied(*pos, M.bits.data(), mip_dt(*dt, *pos, a.max_cascade)) ? 1 : 0;
+	};
 	// pass 1: count (testbed_nerf.cu:779-799)
 	std::vector<uint32_t> cnt(R, 0);
 	std::vector<V3> ro(R), rd(R);
@@ -706,14 +736,13 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		float t;
 		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t)) continue;
 		ro[i] = o; rd[i] = d; rst[i] = t;
-		const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		uint32_t j = 0;
-		V3 pos;
-		while (box.contains(pos = o + d * t) && j < STEPS) {
-			const float dt = calc_dt(t, cone);
-			const uint32_t mip = mip_dt(dt, pos, a.max_cascade);
-			if (occupied(pos, M.bits.data(), mip)) { ++j; t += dt; }
-			else t = adv_voxel(t, cone, pos, d, idir, mip);
+		for (uint32_t k = 0; j < STEPS; ++k) {
+			float tt, dt;
+			V3 pos;
+			const int r = lattice(o, d, t, k, &tt, &dt, &pos);
+			if (r < 0) break;
+			j += (uint32_t)r;
 		}
 		cnt[i] = j;
 	}
@@ -729,22 +758,20 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		M.ray_numsteps[2 * i] = n;
 		M.ray_numsteps[2 * i + 1] = b;
 		// pass 2: write coordinates (testbed_nerf.cu:814-830)
-		const V3 o = ro[i], d = rd[i], idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		const V3 o = ro[i], d = rd[i];
 		const V3 wd = v((d.x + 1.0f) * 0.5f, (d.y + 1.0f) * 0.5f, (d.z + 1.0f) * 0.5f);
-		float t = rst[i];
 		uint32_t j = 0;
-		V3 pos;
-		while (box.contains(pos = o + d * t) && j < n) {
-			const float dt = calc_dt(t, cone);
-			const uint32_t mip = mip_dt(dt, pos, a.max_cascade);
-			if (occupied(pos, M.bits.data(), mip)) {
-				const V3 w = box.rel(pos);
-				float* c = &M.coords[8 * (size_t)(b + j)];
-				c[0] = w.x; c[1] = w.y; c[2] = w.z; c[3] = warp_dt(dt);
-				c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
-				++j;
-				t += dt;
-			} else t = adv_voxel(t, cone, pos, d, idir, mip);
+		for (uint32_t k = 0; j < n; ++k) {
+			float t, dt;
+			V3 pos;
+			const int r = lattice(o, d, rst[i], k, &t, &dt, &pos);
+			if (r < 0) break;
+			if (r == 0) continue;
+			const V3 w = box.rel(pos);
+			float* c = &M.coords[8 * (size_t)(b + j)];
+			c[0] = w.x; c[1] = w.y; c[2] = w.z; c[3] = warp_dt(dt);
+			c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
+			++j;
 		}
 	}
 	M.total_samples = base;
@@ -997,7 +1024,7 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 	const Box tbox{v(a.train_aabb_min[0], a.train_aabb_min[1], a.train_aabb_min[2]), v(a.train_aabb_max[0], a.train_aabb_max[1], a.train_aabb_max[2])};
 	const Cam cam = cam_of(a.camera);
 	const uint16_t* P = a.use_inference_params ? M.inf16.data() : M.p16.data();
-	const float cone = a.cone_angle_constant;
+	const Stepping stp = make_stepping(a.cone_angle_constant);
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	const uint32_t sc = std::max(a.shard_count, 1u), sr = std::max(a.shard_rows, 1u), si = a.shard_index % sc;
 	float ox, oy;
@@ -1020,20 +1047,19 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			float t = std::max(t0, 0.0f) + 1e-6f;
 			if (!box.contains(o + d * t)) continue;
 			const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-			t = adv_n(t, cone, ldval(a.sample_index, idx * 786433u, 0));
-			t = skip_empty(t, cone, o, d, idir, M.bits.data(), a.max_cascade, box);
-			if (t >= MAXD) continue;
+			float n = lat_to(stp, t) + ldval(a.sample_index, idx * 786433u, 0);
+			if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), a.max_cascade, box)) continue;
 			float c[4] = {0, 0, 0, 0}, maxw = 0.0f, dep = 0.0f;
 			const V3 wd = v((d.x + 1) * 0.5f, (d.y + 1) * 0.5f, (d.z + 1) * 0.5f);
 			for (uint32_t step = 0; step < 10000; ++step) {
-				t = skip_empty(t, cone, o, d, idir, M.bits.data(), a.max_cascade, box);
-				if (t >= MAXD) break;
-				const float dt = calc_dt(t, cone);
+				if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), a.max_cascade, box)) break;
+				const float t = lat_from(stp, n);
+				const float dt = lat_from(stp, n + 1.0f) - t;
 				const V3 w = tbox.rel(o + d * t);
 				float coord[8] = {w.x, w.y, w.z, warp_dt(dt), wd.x, wd.y, wd.z, 0.0f};
 				hg_forward(M, P, coord, 8, 1, enc.data());
 				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data());
-				t += dt;
+				n += 1.0f;
 				const V3 pos = tbox.mn + v(coord[0] * (tbox.mx.x - tbox.mn.x), coord[1] * (tbox.mx.y - tbox.mn.y), coord[2] * (tbox.mx.z - tbox.mn.z));
 				const float T = 1.0f - c[3];
 				const float alpha = 1.0f - std::exp(-to_density(out[3], dact) * unwarp_dt(coord[3]));
