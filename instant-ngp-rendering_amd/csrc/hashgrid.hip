@@ -46,15 +46,15 @@ __device__ __forceinline__ void pos_fract(float input, float scale, float* frac,
 	*frac = p - f;
 }
 
+// tcnn grid_index: CoherentPrime hash for hashed levels, dense stride otherwise, modulo the
+// level size.  Hashed levels have size 2^T (a mask); a dense index is below 2*size (corner
+// coordinates reach res, so res + res^2 + res^3 < 2 res^3 <= 2 size), so the modulo is
+// one conditional subtraction -- same value as idx % size, no integer division.
 __device__ __forceinline__ uint32_t grid_index(uint32_t hashed, uint32_t size, uint32_t res, uint32_t x, uint32_t y,
                                                uint32_t z) {
-	uint32_t idx;
-	if (hashed) {
-		idx = (x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u);
-	} else {
-		idx = x + y * res + z * res * res;
-	}
-	return idx % size;
+	if (hashed) return ((x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u)) & (size - 1u);
+	const uint32_t idx = x + y * res + z * res * res;
+	return idx >= size ? idx - size : idx;
 }
 
 template <uint32_t F>
@@ -68,11 +68,70 @@ struct FeatVec<4> { using T = uint2; };
 template <>
 struct FeatVec<8> { using T = uint4; };
 
+// Two consecutive table entries (an aligned pair), used to fetch the x / x+1 corners with
+// one load when they share it (dense index even, or hashed with x even: index ^ 1).
+template <uint32_t F>
+struct PairVec;
+template <>
+struct PairVec<1> { using T = uint32_t; };
+template <>
+struct PairVec<2> { using T = uint2; };
+template <>
+struct PairVec<4> { using T = uint4; };
+
 template <uint32_t F>
 __device__ __forceinline__ void unpack(const typename FeatVec<F>::T& v, float* out) {
 	const __half* h = reinterpret_cast<const __half*>(&v);
 #pragma unroll
 	for (uint32_t f = 0; f < F; ++f) out[f] = __half2float(h[f]);
+}
+
+template <bool HASHED>
+__device__ __forceinline__ uint32_t corner_index(uint32_t size, uint32_t res, uint32_t x, uint32_t y, uint32_t z) {
+	if (HASHED) return ((x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u)) & (size - 1u);
+	const uint32_t idx = x + y * res + z * res * res;
+	return idx >= size ? idx - size : idx;
+}
+
+// The 8 corner entries of a cell, all loads issued before any is consumed.  x-pairs share
+// one aligned pair load when both corners fall in it (dense index even, or hashed with x
+// even: index ^ 1); only the other lanes issue the second corner's own load, which cuts
+// the L2 requests of a level by about a quarter.
+template <uint32_t F, bool HASHED>
+__device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __restrict__ tab, uint32_t size, uint32_t res,
+                                               uint32_t gx, uint32_t gy, uint32_t gz, typename FeatVec<F>::T* vals) {
+	using VT = typename FeatVec<F>::T;
+	uint32_t i0[4], i1[4];
+#pragma unroll
+	for (uint32_t q = 0; q < 4; ++q) {
+		const uint32_t yy = gy + (q & 1u), zz = gz + (q >> 1);
+		i0[q] = corner_index<HASHED>(size, res, gx, yy, zz);
+		i1[q] = corner_index<HASHED>(size, res, gx + 1u, yy, zz);
+	}
+	if constexpr (F <= 4) {
+		using PT = typename PairVec<F>::T;
+		const PT* ptab = reinterpret_cast<const PT*>(tab);
+		PT pr[4];
+		VT lone[4];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) pr[q] = ptab[i0[q] >> 1];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q)
+			if ((i1[q] ^ i0[q]) != 1u) lone[q] = tab[i1[q]];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) {
+			const VT* pv = reinterpret_cast<const VT*>(&pr[q]);
+			const VT a = pv[0], b = pv[1];
+			vals[2 * q] = (i0[q] & 1u) ? b : a;
+			vals[2 * q + 1] = (i1[q] ^ i0[q]) != 1u ? lone[q] : ((i1[q] & 1u) ? b : a);
+		}
+	} else {
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) {
+			vals[2 * q] = tab[i0[q]];
+			vals[2 * q + 1] = tab[i1[q]];
+		}
+	}
 }
 
 template <uint32_t F>
@@ -98,11 +157,8 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
 
 	VT vals[8];
-#pragma unroll
-	for (uint32_t c = 0; c < 8; ++c) {
-		const uint32_t idx = grid_index(hashed, size, res, gx + (c & 1u), gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u));
-		vals[c] = tab[idx];
-	}
+	if (hashed) gather_corners<F, true>(tab, size, res, gx, gy, gz, vals);
+	else gather_corners<F, false>(tab, size, res, gx, gy, gz, vals);
 	float acc[F];
 #pragma unroll
 	for (uint32_t f = 0; f < F; ++f) acc[f] = 0.0f;

@@ -166,6 +166,7 @@ struct RenderScratch {
 	DevBuf<__half> out;         // [n*8][4]
 	DevBuf<uint32_t> counters;  // [4]
 	DevBuf<uint32_t> host_counter;
+	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
 	size_t cap = 0;
 };
 

@@ -290,6 +290,11 @@ NGP_HD bool density_grid_occupied_cached(v3 pos, const uint8_t* bitfield, uint32
 
 NGP_HD float signf_(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 
+// Occupancy summary per mip: 4096 bits "any cell of this 8^3 Morton block set"
+// (block = idx >> 9) followed by 64 bits for 32^3 blocks (idx >> 15).  Derived from
+// the bitfield; lets the render march leap over large empty regions.
+constexpr uint32_t OCC_SUMMARY_BYTES = 512 + 8;
+
 // ---------------------------------------------------------------------------
 // Stepping lattice.  A ray's candidate samples sit at n0 + k (k = 0, 1, ...) in the
 // reference's "stepping space" (uniform steps of MIN_CONE_STEPSIZE for cone_angle 0,
@@ -368,40 +373,55 @@ NGP_HD uint32_t mip_from_dt(float dt, v3 pos, uint32_t max_cascade = NERF_CASCAD
 // clamp(mip_from_pos, 0, max_mip)) is occupied; false once the ray leaves the AABB.
 // An empty cell is skipped in one jump to the first lattice point past its far face
 // (at the coarsest empty mip, as the reference does) -- or, when the whole Morton
-// block of 4x4x4 cells around it is empty (one zero 64-bit bitfield word), past the
-// block's far face.  The jump is taken only if the lattice point just before the
+// block of 4^3 cells around it is empty (one zero 64-bit bitfield word), past the
+// far face of the largest empty aligned block of 4^3, 8^3 or 32^3 cells (summary
+// bits, see occupancy_summary below).  The jump is taken only if the lattice point just before the
 // landing point is still inside the skipped cell/block, so every skipped point
 // provably lies in empty space and the result equals testing the points one by one.
+enum LatticeStep : int { LATTICE_OCCUPIED = 0, LATTICE_SKIPPED = 1, LATTICE_EXIT = 2 };
+// One step of the march at lattice point *n_io: occupied (left unchanged), exited the
+// AABB, or skipped (moved to the next candidate point).  Kept as a single step so a
+// wave's lanes can interleave sampling and skipping without serialising on each other.
+NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
+                        const uint8_t* summary, uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
+	const float n = *n_io;
+	const float t = step_from(st, n);
+	const v3 pos = o + d * t;
+	if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return LATTICE_EXIT;
+	uint32_t mip = mip_from_pos(pos);
+	mip = mip > max_mip ? max_mip : mip;
+	if (density_grid_occupied_cached(pos, bitfield, mip, cache)) return LATTICE_OCCUPIED;
+	while (mip < max_mip && !density_grid_occupied_cached(pos, bitfield, mip + 1, cache)) ++mip;
+	// the cached word now covers the 4x4x4-cell block around pos at `mip`: if it is all
+	// zero, jump over the largest empty aligned block, else over the one cell
+	const uint32_t cell = cascaded_grid_idx_at(pos, mip);
+	(void)density_grid_occupied_cached(pos, bitfield, mip, cache);
+	uint32_t shift = 0;
+	if (cell != 0xFFFFFFFFu && cache.bits == 0ull) {
+		shift = 6;  // 4^3 cells empty
+		const uint8_t* sm = summary + OCC_SUMMARY_BYTES * mip;
+		const uint32_t b1 = cell >> 9, b2 = cell >> 15;
+		if (!((sm[b1 >> 3] >> (b1 & 7u)) & 1u)) {
+			shift = 9;  // 8^3 cells empty
+			if (!((sm[512 + (b2 >> 3)] >> (b2 & 7u)) & 1u)) shift = 15;  // 32^3 cells empty
+		}
+	}
+	const uint32_t here = cell >> shift;
+	const float n_far = step_to(st, t + distance_to_next_cell(pos, d, idir, mip + shift / 3u));
+	float nn = n + ceilf(fmaxf(n_far - n, 0.5f));
+	if (nn - n > 1.0f) {
+		const v3 last = o + d * step_from(st, nn - 1.0f);
+		if ((cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
+	}
+	*n_io = nn;
+	return LATTICE_SKIPPED;
+}
+
 NGP_HD bool next_occupied_lattice_point(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
-                                        uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
-	float n = *n_io;
+                                        const uint8_t* summary, uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
 	while (true) {
-		const float t = step_from(st, n);
-		const v3 pos = o + d * t;
-		if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) {
-			*n_io = n;
-			return false;
-		}
-		uint32_t mip = mip_from_pos(pos);
-		mip = mip > max_mip ? max_mip : mip;
-		if (density_grid_occupied_cached(pos, bitfield, mip, cache)) {
-			*n_io = n;
-			return true;
-		}
-		while (mip < max_mip && !density_grid_occupied_cached(pos, bitfield, mip + 1, cache)) ++mip;
-		// the cached word now covers the 4x4x4-cell block around pos at `mip`: if it is all
-		// zero, jump over the whole block (cells of 4x the size), else over the one cell
-		const uint32_t cell = cascaded_grid_idx_at(pos, mip);
-		(void)density_grid_occupied_cached(pos, bitfield, mip, cache);
-		const uint32_t shift = (cell != 0xFFFFFFFFu && cache.bits == 0ull) ? 6u : 0u;
-		const uint32_t here = cell >> shift;
-		const float n_far = step_to(st, t + distance_to_next_cell(pos, d, idir, mip + (shift ? 2u : 0u)));
-		float nn = n + ceilf(fmaxf(n_far - n, 0.5f));
-		if (nn - n > 1.0f) {
-			const v3 last = o + d * step_from(st, nn - 1.0f);
-			if ((cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
-		}
-		n = nn;
+		const int r = lattice_step(n_io, st, o, d, idir, bitfield, summary, max_mip, aabb, cache);
+		if (r != LATTICE_SKIPPED) return r == LATTICE_OCCUPIED;
 	}
 }
 

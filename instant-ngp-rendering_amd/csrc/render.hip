@@ -43,6 +43,7 @@ struct RenderK {
 	uint32_t shard_index, shard_count, shard_rows;
 	uint32_t n_local;
 	const uint8_t* bitfield;
+	const uint8_t* summary;
 };
 
 __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32_t yl) {
@@ -50,16 +51,62 @@ __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32
 	return (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
 }
 
+__device__ __forceinline__ void init_ray_body(const RenderK& k, uint32_t r, Payload* pp, float4* __restrict__ frame,
+                                              float* __restrict__ depth_buffer);
+
+// Stream compaction slot for a 256-thread block: ballot per wave, LDS prefix over the four
+// waves, ONE global atomic per block and flag (instead of one per wave).  Returns the
+// output index of this thread (valid only where flag is set).  Order within a block is
+// deterministic; order between blocks is not (results never depend on it: every ray
+// carries its own pixel index).
+__device__ __forceinline__ void block_append2(bool fa, bool fb, uint32_t* counter_a, uint32_t* counter_b, uint32_t* ia,
+                                              uint32_t* ib) {
+	__shared__ uint32_t wa[4], wb[4], base[2];
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	const unsigned long long ma = __ballot(fa), mb = __ballot(fb);
+	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+	if (lane == 0) {
+		wa[w] = (uint32_t)__popcll(ma);
+		wb[w] = (uint32_t)__popcll(mb);
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const uint32_t ta = wa[0] + wa[1] + wa[2] + wa[3], tb = wb[0] + wb[1] + wb[2] + wb[3];
+		base[0] = ta ? atomicAdd(counter_a, ta) : 0u;
+		base[1] = tb ? atomicAdd(counter_b, tb) : 0u;
+	}
+	__syncthreads();
+	uint32_t pa = base[0], pb = base[1];
+	for (uint32_t k = 0; k < w; ++k) {
+		pa += wa[k];
+		pb += wb[k];
+	}
+	*ia = pa + (uint32_t)__popcll(ma & below);
+	*ib = pb + (uint32_t)__popcll(mb & below);
+}
+
 __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
                                                      float* __restrict__ depth, float4* __restrict__ frame,
-                                                     float* __restrict__ depth_buffer) {
+                                                     float* __restrict__ depth_buffer, uint32_t* __restrict__ counters) {
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
-	if (r >= k.n_local) return;
+	Payload p;
+	p.alive = 0;
+	if (r < k.n_local) init_ray_body(k, r, &p, frame, depth_buffer);
+	uint32_t slot, unused;
+	block_append2(p.alive != 0, false, &counters[0], &counters[3], &slot, &unused);
+	if (p.alive) {
+		payloads[slot] = p;
+		rgba[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
+		depth[slot] = 0.0f;
+	}
+}
+
+// init_rays_with_payload_kernel_nerf + advance_pos_nerf for local ray r
+__device__ __forceinline__ void init_ray_body(const RenderK& k, uint32_t r, Payload* pp, float4* __restrict__ frame,
+                                              float* __restrict__ depth_buffer) {
 	const uint32_t x = r % k.W, yl = r / k.W;
 	const uint32_t y = local_to_global_row(k, yl);
 	const uint32_t idx = x + k.W * y;
-	rgba[r] = make_float4(0.f, 0.f, 0.f, 0.f);
-	depth[r] = 0.0f;
 	frame[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
 	depth_buffer[idx] = MAX_DEPTH;
 
@@ -88,10 +135,28 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
 		float n = step_to(k.st, t) + ld_random_val(k.sample_index, idx * 786433u);
 		OccCache occ = occ_cache_init();
-		p.alive = next_occupied_lattice_point(&n, k.st, origin, dir, idir, k.bitfield, k.max_mip, k.aabb, occ) ? 1u : 0u;
+		p.alive = next_occupied_lattice_point(&n, k.st, origin, dir, idir, k.bitfield, k.summary, k.max_mip, k.aabb, occ) ? 1u : 0u;
 		p.n = n;
 	}
-	payloads[r] = p;
+	*pp = p;
+}
+
+// Occupancy summary (see ngp_math.h): one thread per 8^3 block; a wave covers 64
+// consecutive blocks = one 32^3 block, so both levels come from ballots.
+__global__ void __launch_bounds__(256) k_occupancy_summary(const uint8_t* __restrict__ bitfield, uint8_t* __restrict__ summary) {
+	const uint32_t g = blockIdx.x * 256u + threadIdx.x;  // [mip][4096]
+	const uint32_t mip = g >> 12, b1 = g & 4095u;
+	const uint64_t* w = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8)) + (size_t)b1 * 8;
+	uint64_t any = 0;
+#pragma unroll
+	for (int j = 0; j < 8; ++j) any |= w[j];
+	const unsigned long long m = __ballot(any != 0ull);
+	uint8_t* sm = summary + (size_t)OCC_SUMMARY_BYTES * mip;
+	if ((threadIdx.x & 63u) == 0) {
+		*reinterpret_cast<unsigned long long*>(sm + (b1 >> 3)) = m;
+		const uint32_t b2 = b1 >> 6;
+		if (m) atomicOr(reinterpret_cast<uint32_t*>(sm + 512) + (b2 >> 5), 1u << (b2 & 31u));
+	}
 }
 
 __global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __restrict__ sp, const float4* __restrict__ srgba,
@@ -100,7 +165,6 @@ __global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __re
                                                  Payload* __restrict__ hp, float4* __restrict__ hrgba,
                                                  float* __restrict__ hdepth, uint32_t* __restrict__ counters) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	const int lane = threadIdx.x & 63;
 	bool alive = false, hit = false;
 	Payload p;
 	float4 c;
@@ -112,25 +176,33 @@ __global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __re
 		alive = p.alive != 0;
 		hit = !alive && c.w > 0.001f;
 	}
-	const unsigned long long ma = __ballot(alive), mh = __ballot(hit);
-	const unsigned long long below = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-	uint32_t base_a = 0, base_h = 0;
-	if (lane == 0) {
-		base_a = ma ? atomicAdd(&counters[0], (uint32_t)__popcll(ma)) : 0u;
-		base_h = mh ? atomicAdd(&counters[1], (uint32_t)__popcll(mh)) : 0u;
-	}
-	base_a = __shfl(base_a, 0, 64);
-	base_h = __shfl(base_h, 0, 64);
+	uint32_t oa, oh;
+	block_append2(alive, hit, &counters[0], &counters[1], &oa, &oh);
 	if (alive) {
-		const uint32_t o = base_a + __popcll(ma & below);
-		dp[o] = p;
-		drgba[o] = c;
-		ddepth[o] = dd;
+		dp[oa] = p;
+		drgba[oa] = c;
+		ddepth[oa] = dd;
 	} else if (hit) {
-		const uint32_t o = base_h + __popcll(mh & below);
-		hp[o] = p;
-		hrgba[o] = c;
-		hdepth[o] = dd;
+		hp[oh] = p;
+		hrgba[oh] = c;
+		hdepth[oh] = dd;
+	}
+}
+
+// After MARCH_ITER passes: rays still marching are finished with what they accumulated.
+__global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __restrict__ sp, const float4* __restrict__ srgba,
+                                                const float* __restrict__ sdepth, Payload* __restrict__ hp,
+                                                float4* __restrict__ hrgba, float* __restrict__ hdepth,
+                                                uint32_t* __restrict__ counters) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	bool hit = false;
+	if (i < n) hit = srgba[i].w > 0.001f;
+	uint32_t oh, unused;
+	block_append2(hit, false, &counters[1], &counters[3], &oh, &unused);
+	if (hit) {
+		hp[oh] = sp[i];
+		hrgba[oh] = srgba[i];
+		hdepth[oh] = sdepth[i];
 	}
 }
 
@@ -145,18 +217,25 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 	const v3 wdir = warp_direction(d);
 	float n = p.n;
 	OccCache occ = occ_cache_init();
-	for (uint32_t j = 0; j < n_steps; ++j) {
-		if (!next_occupied_lattice_point(&n, k.st, o, d, idir, k.bitfield, k.max_mip, k.aabb, occ)) {
+	// one flat loop: every iteration either emits a sample or skips, per lane, so lanes
+	// that are skipping empty space never hold up lanes that are sampling (and vice versa)
+	uint32_t j = 0;
+	while (j < n_steps) {
+		const int r = lattice_step(&n, k.st, o, d, idir, k.bitfield, k.summary, k.max_mip, k.aabb, occ);
+		if (r == LATTICE_EXIT) {
 			p.n_steps = j;
 			return;
 		}
-		const float t = step_from(k.st, n);
-		const float dt = step_from(k.st, n + 1.0f) - t;
-		const v3 wp = aabb_relative(k.train_aabb, o + d * t);
-		float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)j * n_alive));
-		c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-		c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
-		n += 1.0f;
+		if (r == LATTICE_OCCUPIED) {
+			const float t = step_from(k.st, n);
+			const float dt = step_from(k.st, n + 1.0f) - t;
+			const v3 wp = aabb_relative(k.train_aabb, o + d * t);
+			float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)j * n_alive));
+			c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+			c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+			n += 1.0f;
+			++j;
+		}
 	}
 	p.n = n;
 	p.n_steps = n_steps;
@@ -283,6 +362,13 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 	return n;
 }
 
+// NGP_RENDER_STEPS_PER_PASS overrides the per-pass sample cap (tuning knob; results do not depend on it)
+static uint32_t max_steps_per_pass() {
+	const char* e = getenv("NGP_RENDER_STEPS_PER_PASS");
+	const int v = e ? atoi(e) : 0;
+	return v > 0 ? (uint32_t)v : 32u;
+}
+
 void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s) {
 	RenderScratch& rs = m->rs;
 	RenderK k{};
@@ -310,6 +396,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);
 	k.bitfield = m->gs.bitfield.ptr;
+	rs.summary.reserve(OCC_SUMMARY_BYTES * NERF_CASCADES / 4 + 1);
+	k.summary = reinterpret_cast<const uint8_t*>(rs.summary.ptr);
 	const uint32_t H_local = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	const uint32_t n = k.W * H_local;
 	k.n_local = n;
@@ -335,32 +423,29 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
-	k_render_init<<<div_up(n, 256), 256, 0, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer);
+	for (uint32_t mip = 0; mip < NERF_CASCADES; ++mip)
+		NGP_HIP_CHECK(hipMemsetAsync(rs.summary.ptr + (OCC_SUMMARY_BYTES * mip + 512) / 4, 0, 8, s));
+	k_occupancy_summary<<<NERF_CASCADES * 4096 / 256, 256, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr));
+	NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, 4 * sizeof(uint32_t), s));
+	k_render_init<<<div_up(n, 256), 256, 0, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
+	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
-	NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, 4 * sizeof(uint32_t), s));
+	NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+	NGP_HIP_CHECK(hipStreamSynchronize(s));
+	uint32_t n_alive = rs.host_counter.ptr[0];
 
+	// NerfTracer::trace (testbed_nerf.cu:1639-1755): generate -> infer -> composite -> compact,
+	// alive rays ping-pong between buffers 0/1, finished rays with colour append to buffer 2.
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
-	uint32_t n_alive = n;
-	uint32_t db = 0;
+	int cur = 0;
 	const uint32_t MARCH_ITER = 10000;
-	for (uint32_t it = 1; it < MARCH_ITER;) {
-		const int cur = (db + 1) % 2, tmp = db % 2;
-		++db;
-		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
-		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_compact<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(tmp), C(tmp), rs.depth[tmp].ptr, P(cur), C(cur),
-		                                               rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr, rs.counters.ptr);
-		tm.end(NGP_TIMER_RENDER_MARCH, s);
-		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		NGP_HIP_CHECK(hipStreamSynchronize(s));
-		n_alive = rs.host_counter.ptr[0];
-		if (n_alive == 0) break;
+	for (uint32_t it = 1; it < MARCH_ITER && n_alive > 0;) {
 		const uint32_t target = 2 * 1024 * 1024;
 		// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
 		// every ray composites its own samples in order and stops at the same one whatever the chunking
-		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), 32u);
+		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), max_steps_per_pass());
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_generate<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
@@ -374,9 +459,22 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, it, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
 		                                                 rs.out.ptr, n_steps);
+		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
+		k_compact<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(1 - cur), C(1 - cur),
+		                                               rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr, rs.counters.ptr);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
+		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		n_alive = rs.host_counter.ptr[0];
+		cur = 1 - cur;
 		it += n_steps;
+	}
+	if (n_alive > 0) {
+		// march budget exhausted: still-alive rays are shaded with what they accumulated
+		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
+		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,
+		                                              rs.counters.ptr);
 	}
 	NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 	NGP_HIP_CHECK(hipStreamSynchronize(s));

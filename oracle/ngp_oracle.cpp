@@ -285,10 +285,26 @@ static bool occupied(V3 p, const uint8_t* bits, uint32_t mip) {
 	if (i == 0xFFFFFFFFu) return false;
 	return bits[i / 8 + CELLS / 8 * mip] & (1u << (i % 8));
 }
+// Occupancy summary per mip (ngp_math.h OCC_SUMMARY_BYTES): 4096 bits for 8^3 Morton blocks
+// (cell >> 9), then 64 bits for 32^3 blocks (cell >> 15).
+static const uint32_t SUMMARY_BYTES = 512 + 8;
+static std::vector<uint8_t> occ_summary(const uint8_t* bits) {
+	std::vector<uint8_t> sm((size_t)SUMMARY_BYTES * CASCADES, 0);
+	for (uint32_t mip = 0; mip < CASCADES; ++mip)
+		for (uint32_t b1 = 0; b1 < 4096; ++b1) {
+			bool any = false;
+			for (uint32_t k = 0; k < 64; ++k) any |= bits[(size_t)CELLS / 8 * mip + b1 * 64 + k] != 0;
+			if (!any) continue;
+			sm[SUMMARY_BYTES * mip + (b1 >> 3)] |= (uint8_t)(1u << (b1 & 7));
+			sm[SUMMARY_BYTES * mip + 512 + (b1 >> 9)] |= (uint8_t)(1u << ((b1 >> 6) & 7));
+		}
+	return sm;
+}
+
 // First occupied lattice point at or after *n (render march); an empty cell is jumped over
 // only when the lattice point before the landing point is still inside it.
-static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, const uint8_t* bits, uint32_t maxm,
-                          const Box& b) {
+static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, const uint8_t* bits,
+                          const uint8_t* summary, uint32_t maxm, const Box& b) {
 	float n = *n_io;
 	while (true) {
 		const float t = lat_from(st, n);
@@ -301,8 +317,17 @@ static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, 
 		const uint32_t cell = grid_idx(pos, mip);
 		uint64_t word = 1;
 		if (cell != 0xFFFFFFFFu) std::memcpy(&word, &bits[(size_t)CELLS / 8 * mip + (cell / 64) * 8], 8);
-		const uint32_t shift = word == 0 ? 6u : 0u;
-		const float n_far = lat_to(st, t + dist_next_cell(pos, d, idir, mip + (shift ? 2u : 0u)));
+		uint32_t shift = 0;
+		if (word == 0) {
+			shift = 6;
+			const uint8_t* sm = summary + SUMMARY_BYTES * mip;
+			const uint32_t b1 = cell >> 9, b2 = cell >> 15;
+			if (!((sm[b1 >> 3] >> (b1 & 7u)) & 1u)) {
+				shift = 9;
+				if (!((sm[512 + (b2 >> 3)] >> (b2 & 7u)) & 1u)) shift = 15;
+			}
+		}
+		const float n_far = lat_to(st, t + dist_next_cell(pos, d, idir, mip + shift / 3u));
 		float nn = n + std::ceil(std::max(n_far - n, 0.5f));
 		if (nn - n > 1.0f) {
 			const V3 last = o + d * lat_from(st, nn - 1.0f);
@@ -1025,6 +1050,7 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 	const Cam cam = cam_of(a.camera);
 	const uint16_t* P = a.use_inference_params ? M.inf16.data() : M.p16.data();
 	const Stepping stp = make_stepping(a.cone_angle_constant);
+	const std::vector<uint8_t> summary = occ_summary(M.bits.data());
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	const uint32_t sc = std::max(a.shard_count, 1u), sr = std::max(a.shard_rows, 1u), si = a.shard_index % sc;
 	float ox, oy;
@@ -1048,11 +1074,11 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			if (!box.contains(o + d * t)) continue;
 			const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 			float n = lat_to(stp, t) + ldval(a.sample_index, idx * 786433u, 0);
-			if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), a.max_cascade, box)) continue;
+			if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), summary.data(), a.max_cascade, box)) continue;
 			float c[4] = {0, 0, 0, 0}, maxw = 0.0f, dep = 0.0f;
 			const V3 wd = v((d.x + 1) * 0.5f, (d.y + 1) * 0.5f, (d.z + 1) * 0.5f);
 			for (uint32_t step = 0; step < 10000; ++step) {
-				if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), a.max_cascade, box)) break;
+				if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), summary.data(), a.max_cascade, box)) break;
 				const float t = lat_from(stp, n);
 				const float dt = lat_from(stp, n + 1.0f) - t;
 				const V3 w = tbox.rel(o + d * t);
