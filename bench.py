@@ -46,6 +46,8 @@ def parse():
     p.add_argument("--cpu-baseline", type=int, default=1)
     p.add_argument("--cpu-rows", type=int, default=8, help="1080p rows rendered by the CPU oracle sample")
     p.add_argument("--cpu-rays", type=int, default=512, help="training rays in the CPU oracle sample")
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+                   help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
 
 
@@ -88,6 +90,27 @@ def make_dataset(ngp, tb, n_views, res, device):
         tb.nerf.training.set_camera_intrinsics(i, fx=focal, fy=focal)
     tb.nerf.training.n_images_for_training = n_views  # as the reference's create_empty_nerf_dataset callers do
     return cams, imgs, focal
+
+
+# timer -> kernel whose PMC counters describe it
+TIMER_KERNEL = {"train_encode": ("k_hashgrid_fwd<", ", 0>"), "render_encode": ("k_hashgrid_fwd<", ", 1>"),
+                "train_encode_bwd": ("k_hashgrid_bwd<", ""), "train_mlp_infer": ("k_mlp_infer<", ""),
+                "render_mlp": ("k_mlp_infer<", ""), "train_mlp_bwd": ("k_mlp_train<", ""), "optimizer": ("k_optimizer", "")}
+
+
+def pmc_traffic(path, timer, units_per_launch):
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary (or None)."""
+    if not os.path.exists(path) or timer not in TIMER_KERNEL:
+        return None
+    data = json.load(open(path))
+    prefix, suffix = TIMER_KERNEL[timer]
+    for name, e in data.items():
+        if prefix not in name or not name.endswith(suffix):
+            continue
+        if "fetch_bytes_per_sample" in e:
+            return round((e["fetch_bytes_per_sample"] + e["write_bytes_per_sample"]) * units_per_launch)
+        return round(e.get("fetch_bytes_per_launch", 0) + e.get("write_bytes_per_launch", 0))
+    return None
 
 
 def read_timers(abi, lib, handle):
@@ -263,6 +286,7 @@ def main():
         "us_per_launch": round(1000.0 * ms / launches, 2),
     }
     roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
+    roofline["traffic"] = pmc_traffic(args.traffic_json, dom, units / launches)
 
     cpu = None
     if rank == 0 and world == 1 and args.cpu_baseline:

@@ -134,7 +134,8 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 	}
 }
 
-template <uint32_t F>
+// SITE only names the call site in profiles (0 training, 1 render, 2 density grid / API).
+template <uint32_t F, int SITE>
 __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ table, const LevelTable lt,
                                                       __half* __restrict__ enc, uint32_t enc_plane, uint32_t n_chunks,
@@ -289,18 +290,26 @@ __global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const floa
 	}
 }
 
-void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev) {
-	if (n == 0) return;
+template <int SITE>
+static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
+                            __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev) {
 	const uint32_t n_chunks = div_up(n, 256);
 	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
-		case 1: k_hashgrid_fwd<1><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 2: k_hashgrid_fwd<2><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 4: k_hashgrid_fwd<4><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 8: k_hashgrid_fwd<8><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 1: k_hashgrid_fwd<1, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 2: k_hashgrid_fwd<2, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 4: k_hashgrid_fwd<4, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 8: k_hashgrid_fwd<8, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
 		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
 	}
+}
+
+void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
+                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, int site) {
+	if (n == 0) return;
+	if (site == 0) launch_fwd_site<0>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev);
+	else if (site == 1) launch_fwd_site<1>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev);
+	else launch_fwd_site<2>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev);
 	NGP_HIP_CHECK(hipGetLastError());
 }
 

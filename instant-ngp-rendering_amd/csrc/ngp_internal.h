@@ -202,8 +202,9 @@ namespace ngp {
 
 // ---- kernel launchers (defined in the .hip files) --------------------------------------
 // hashgrid.hip
+// site: 0 training step, 1 render, 2 density grid / API (names the kernel instance in profiles)
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr);
+                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2);
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                          uint32_t enc_plane, float* grad_table, hipStream_t s, const uint32_t* n_dev = nullptr);
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,

@@ -451,7 +451,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
-		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s);
+		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s, nullptr, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MLP, s);
 		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s);

@@ -639,7 +639,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// network inference over every emitted sample (NerfNetwork::inference_mixed_precision, training params)
 	tm.begin(NGP_TIMER_TRAIN_ENCODE, s);
 	launch_hashgrid_fwd(m->lt, ts.coords.ptr, 8, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
-	                    ts.counters.ptr + 4);
+	                    ts.counters.ptr + 4, 0);
 	tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 	tm.begin(NGP_TIMER_TRAIN_MLP_INFER, s);
 	launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,

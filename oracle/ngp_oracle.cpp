@@ -982,7 +982,10 @@ static void bitfield_update(Model& M, uint32_t max_cascade) {
 	}
 }
 
-static void grid_update(Model& M, const ngp_grid_args& a) {
+// Sampling + density evaluation + max-splat into tmp.  Data-parallel form: this rank
+// evaluates the contiguous 1/world_size slice of the samples (as density_grid.hip does);
+// the caller max-reduces tmp over ranks before grid_finish.
+static void grid_evaluate(Model& M, const ngp_grid_args& a) {
 	const uint32_t nc = a.max_cascade + 1, ne = CELLS * nc;
 	if (M.grid.size() < ne) M.grid.resize(ne, 0.0f);
 	if (a.mark_untrained) mark_untrained(M, a, ne);
@@ -1018,13 +1021,16 @@ static void grid_update(Model& M, const ngp_grid_args& a) {
 		}
 		rng.advance();
 	}
-	// density (NerfNetwork::density, training params) and max-splat
+	// density (NerfNetwork::density, training params) and max-splat over this rank's slice
+	const uint32_t world = std::max(a.world_size, 1u);
+	const uint32_t per = (ntot + world - 1) / world;
+	const uint32_t first = std::min(ntot, a.rank * per), cnt = std::min(ntot - first, per);
 	const std::vector<uint16_t>& P = a.use_inference_params ? M.inf16 : M.p16;
 	std::vector<float> enc((size_t)M.L * ntot * M.F);
 	hg_forward(M, P.data(), pos.data(), 4, ntot, enc.data());
 	std::vector<float> col(M.E);
 	Acts A;
-	for (uint32_t i = 0; i < ntot; ++i) {
+	for (uint32_t i = first; i < first + cnt; ++i) {
 		gather_enc(M, enc.data(), ntot, i, col.data());
 		// density MLP only
 		std::vector<float> x(M.Epad, 0.0f), y;
@@ -1036,6 +1042,11 @@ static void grid_update(Model& M, const ngp_grid_args& a) {
 		const float th = to_density(x[0], M.cfg.density_activation) * MIN_STEP;
 		M.tmp[idxs[i]] = std::max(M.tmp[idxs[i]], th);
 	}
+}
+
+// EMA of the grid with tmp + mean/bitfield (ema_grid_samples_nerf, update_density_grid_mean_and_bitfield)
+static void grid_finish(Model& M, const ngp_grid_args& a) {
+	const uint32_t ne = CELLS * (a.max_cascade + 1);
 	for (uint32_t i = 0; i < ne; ++i) {
 		const float prev = M.grid[i];
 		M.grid[i] = prev < 0.0f ? prev : std::max(prev * a.decay, M.tmp[i]);
@@ -1265,7 +1276,20 @@ size_t oref_train_scratch(void* m, int kind, void* out) {
 		default: return 0;
 	}
 }
-int oref_density_grid_update(void* m, const ngp_grid_args* a) { return guard([&] { grid_update(*static_cast<Model*>(m), *a); }); }
+int oref_density_grid_update(void* m, const ngp_grid_args* a) {
+	return guard([&] {
+		grid_evaluate(*static_cast<Model*>(m), *a);
+		grid_finish(*static_cast<Model*>(m), *a);
+	});
+}
+int oref_density_grid_evaluate(void* m, const ngp_grid_args* a) { return guard([&] { grid_evaluate(*static_cast<Model*>(m), *a); }); }
+int oref_density_grid_finish(void* m, const ngp_grid_args* a) { return guard([&] { grid_finish(*static_cast<Model*>(m), *a); }); }
+// evaluation buffer (n floats) for the data-parallel max all-reduce
+void oref_density_grid_tmp(void* m, float* io, uint32_t n, int write) {
+	Model& M = *static_cast<Model*>(m);
+	if (write) M.tmp.assign(io, io + n);
+	else std::copy(M.tmp.begin(), M.tmp.begin() + std::min<size_t>(n, M.tmp.size()), io);
+}
 void oref_density_grid_bitfield(void* m, uint32_t max_cascade) { bitfield_update(*static_cast<Model*>(m), max_cascade); }
 void oref_density_grid_set(void* m, const float* grid, uint32_t n) {
 	Model& M = *static_cast<Model*>(m);

@@ -46,6 +46,9 @@ _PROTOS = {
     "oref_train_scratch": (C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p]),
     "oref_density_grid_update": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
     "oref_density_grid_bitfield": (None, [C.c_void_p, C.c_uint32]),
+    "oref_density_grid_evaluate": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
+    "oref_density_grid_finish": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
+    "oref_density_grid_tmp": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]),
     "oref_density_grid_set": (None, [C.c_void_p, C.c_void_p, C.c_uint32]),
     "oref_density_grid_get": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "oref_set_bitfield": (None, [C.c_void_p, C.c_void_p]),
@@ -182,6 +185,23 @@ class Oracle:
     def grid_update(self, args):
         if self.lib.oref_density_grid_update(self.h, C.byref(args)) != 0:
             raise RuntimeError(self.lib.oref_last_error().decode())
+
+    def grid_evaluate(self, args):
+        if self.lib.oref_density_grid_evaluate(self.h, C.byref(args)) != 0:
+            raise RuntimeError(self.lib.oref_last_error().decode())
+
+    def grid_finish(self, args):
+        if self.lib.oref_density_grid_finish(self.h, C.byref(args)) != 0:
+            raise RuntimeError(self.lib.oref_last_error().decode())
+
+    def grid_tmp(self, n, values=None):
+        """Read (values None) or write the density-evaluation buffer used by the DP max all-reduce."""
+        if values is None:
+            out = np.zeros(n, np.float32)
+            self.lib.oref_density_grid_tmp(self.h, ptr(out), n, 0)
+            return out
+        values = np.ascontiguousarray(values, np.float32)
+        self.lib.oref_density_grid_tmp(self.h, ptr(values), values.size, 1)
 
     def grid_set(self, grid):
         grid = np.ascontiguousarray(grid, np.float32)
