@@ -112,21 +112,3 @@ def test_level_tables(L, F, T, aabb, entries, dense_res):
     assert r[-1] == (2048 * aabb if T != 22 else 131072) or r[-1] >= 2048
     assert o.n_params == o.n_mlp + entries * F
     assert o.n_mlp == 3072 + 7168 if cfg.n_neurons == 64 else True
-
-
-def test_golden_fixtures_roundtrip():
-    """Committed golden vectors (tests/golden/*.npz, made by tests/golden/make_golden.py) still match."""
-    path = os.path.join(GOLDEN, "encode_L16F2T19.npz")
-    if not os.path.exists(path):
-        pytest.skip("golden fixtures not generated")
-    g = np.load(path)
-    cfg = A.default_config(**json.loads(str(g["cfg"])))
-    o = Oracle(cfg)
-    o.set_params(g["params"])
-    idx, w = o.encode_indices(g["pos"])
-    np.testing.assert_array_equal(idx, g["idx"])
-    np.testing.assert_array_equal(w, g["w"])
-    enc = o.encode(g["pos"])
-    np.testing.assert_array_equal(enc, g["enc"])
-    out = o.infer(g["coords"])
-    np.testing.assert_array_equal(out, g["out"])
