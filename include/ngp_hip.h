@@ -96,9 +96,12 @@ enum {
 	NGP_PARAMS_FP16 = 1,      /* fp16 training copy (network_precision_t) */
 	NGP_PARAMS_EMA_FP32 = 2,  /* Ema optimizer's running average */
 	NGP_PARAMS_INFER_FP16 = 3,/* fp16 inference params (use_inference_params=true) */
-	NGP_GRADS_FP32 = 4,       /* gradient buffer (GradientMode::Overwrite each step) */
+	NGP_GRADS_FP32 = 4,       /* gradient buffer (GradientMode::Overwrite each step); the MLP part
+	                             [0, n_mlp_params) is used, hash-grid gradients live in GRID_FP16 */
 	NGP_ADAM_M = 5,
-	NGP_ADAM_V = 6
+	NGP_ADAM_V = 6,
+	NGP_GRADS_GRID_FP16 = 7   /* hash-grid gradients [n_params - n_mlp_params], fp16, accumulated with
+	                             packed half2 atomics like tcnn's GridEncoding backward */
 };
 
 /* One training image; an array of these lives in device memory (TrainingImageMetadata,

@@ -10,9 +10,9 @@
 //  * one thread = one (sample, level); each thread issues its 8 corner gathers
 //    back to back (8 independent loads in flight per lane).
 //  * XCD-aware block order: when n_levels % 8 == 0 every workgroup of level l is
-//    placed on the XCD group b % 8 == l % 8, so each XCD's private 4 MiB L2 only
-//    ever holds the tables of n_levels/8 levels (2 MiB each at T=2^19) instead of
-//    the whole 24 MiB table.  Placement only changes speed, never results.
+//    placed on the XCD group b % 8 == l % 8, and the levels an XCD owns run one
+//    after the other, so each XCD's private 4 MiB L2 holds one level's table (2 MiB
+//    at T=2^19) instead of the whole 24 MiB table.  Placement only changes speed.
 //  * output is level-major [L][n][F] (fp16): a wave of 64 consecutive samples of
 //    one level writes 64*F*2 contiguous bytes.
 //  * features accumulate in fp32 (tcnn accumulates in fp16) and are rounded once.
@@ -23,10 +23,12 @@ namespace ngp {
 __device__ __forceinline__ void map_block(uint32_t b, uint32_t n_chunks, uint32_t n_levels, uint32_t* level,
                                           uint32_t* chunk) {
 	if ((n_levels & 7u) == 0) {
-		const uint32_t lpx = n_levels >> 3;
+		// workgroups are dispatched round-robin over the 8 XCDs: XCD x runs level x for the
+		// first n_chunks of its workgroups, then level x + 8, ... -- one level's table
+		// (<= 2 MiB at T=2^19) at a time in each XCD's 4 MiB L2
 		const uint32_t x = b & 7u, k = b >> 3;
-		*level = x + 8u * (k % lpx);
-		*chunk = k / lpx;
+		*level = x + 8u * (k / n_chunks);
+		*chunk = k % n_chunks;
 	} else {
 		*level = b / n_chunks;
 		*chunk = b % n_chunks;
@@ -181,6 +183,26 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 	reinterpret_cast<VT*>(enc)[(size_t)level * enc_plane + i] = o;
 }
 
+// Hash-grid gradients are fp16 and accumulated with packed half2 atomics
+// (global_atomic_pk_add_f16, no return), as tcnn's GridEncoding backward does with
+// atomicAdd(__half2): one memory-side atomic per entry instead of one per feature.
+// F = 1 adds (v, 0) or (0, v) to the aligned pair holding the entry.
+typedef _Float16 half2_vec __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void atomic_add_half2(__half* p, float a, float b) {
+	const half2_vec v = {(_Float16)a, (_Float16)b};
+	__builtin_amdgcn_global_atomic_fadd_v2f16((__attribute__((address_space(1))) half2_vec*)p, v);
+}
+template <uint32_t F>
+__device__ __forceinline__ void scatter_add(__half* gtab, uint32_t idx, const float* v) {
+	if constexpr (F == 1) {
+		if (idx & 1u) atomic_add_half2(gtab + (idx - 1u), 0.0f, v[0]);
+		else atomic_add_half2(gtab + idx, v[0], 0.0f);
+	} else {
+#pragma unroll
+		for (uint32_t f = 0; f < F; f += 2) atomic_add_half2(gtab + (size_t)idx * F + f, v[f], v[f + 1]);
+	}
+}
+
 // Backward scatter.  Lanes of a wave hold consecutive samples of the compacted batch,
 // i.e. consecutive points along the same rays, so at the coarse levels neighbouring
 // lanes very often add into the same corner.  Runs of equal indices are summed across
@@ -190,7 +212,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 template <uint32_t F>
 __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ denc, uint32_t enc_plane,
-                                                      const LevelTable lt, float* __restrict__ grad,
+                                                      const LevelTable lt, __half* __restrict__ grad,
                                                       uint32_t n_chunks, const uint32_t* __restrict__ n_dev) {
 	uint32_t level, chunk;
 	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
@@ -216,7 +238,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 
 	const float scale = lt.scale[level];
 	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
-	float* gtab = grad + (size_t)lt.offset[level] * F;
+	__half* gtab = grad + (size_t)lt.offset[level] * F;
 
 	float fx = 0.f, fy = 0.f, fz = 0.f;
 	uint32_t gx = 0, gy = 0, gz = 0;
@@ -243,8 +265,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 		const unsigned long long heads = __ballot(head);
 		if (~heads == 0ull) {
 			if (active) {
-#pragma unroll
-				for (uint32_t f = 0; f < F; ++f) unsafeAtomicAdd(gtab + (size_t)idx * F + f, v[f]);
+				scatter_add<F>(gtab, idx, v);
 			}
 			continue;
 		}
@@ -260,8 +281,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 		}
 		const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
 		if (active && tail) {
-#pragma unroll
-			for (uint32_t f = 0; f < F; ++f) unsafeAtomicAdd(gtab + (size_t)idx * F + f, v[f]);
+			scatter_add<F>(gtab, idx, v);
 		}
 	}
 }
@@ -314,7 +334,7 @@ void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride
 }
 
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                         uint32_t enc_plane, float* grad_table, hipStream_t s, const uint32_t* n_dev) {
+                         uint32_t enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev) {
 	if (n == 0) return;
 	const uint32_t n_chunks = div_up(n, 256);
 	const uint32_t blocks = n_chunks * lt.n_levels;

@@ -120,6 +120,7 @@ static void refresh_derived(ngp_model* m, bool reset_optimizer, hipStream_t s) {
 		NGP_HIP_CHECK(hipMemsetAsync(m->adam_v.ptr, 0, m->n_params * sizeof(float), s));
 		NGP_HIP_CHECK(hipMemsetAsync(m->adam_steps.ptr, 0, m->n_params * sizeof(uint32_t), s));
 		NGP_HIP_CHECK(hipMemsetAsync(m->grads.ptr, 0, m->n_params * sizeof(float), s));
+		NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads16.ptr, 0, m->n_grid_params * sizeof(__half), s));
 		m->ema_step = 0;
 	} else {
 		launch_params_to_half(m->ema32.ptr, m->infer16.ptr, m->n_params, s);
@@ -161,6 +162,7 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 			m->ema32.reserve(m->n_params);
 			m->infer16.reserve(m->n_params);
 			m->grads.reserve(m->n_params);
+			m->grid_grads16.reserve(m->n_grid_params);
 			m->adam_m.reserve(m->n_params);
 			m->adam_v.reserve(m->n_params);
 			m->adam_steps.reserve(m->n_params);
@@ -190,6 +192,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		(void)hipSetDevice(m->device);
 		(void)hipDeviceSynchronize();
 		for (auto* b : {&m->params32, &m->ema32, &m->grads, &m->adam_m, &m->adam_v}) b->release();
+		m->grid_grads16.release();
 		m->params16.release();
 		m->infer16.release();
 		m->adam_steps.release();
@@ -249,6 +252,7 @@ ngp_status ngp_model_buffer(ngp_model* m, int kind, void** ptr, size_t* bytes) {
 			case NGP_GRADS_FP32: *ptr = m->grads.ptr; if (bytes) *bytes = m->n_params * 4; break;
 			case NGP_ADAM_M: *ptr = m->adam_m.ptr; if (bytes) *bytes = m->n_params * 4; break;
 			case NGP_ADAM_V: *ptr = m->adam_v.ptr; if (bytes) *bytes = m->n_params * 4; break;
+			case NGP_GRADS_GRID_FP16: *ptr = m->grid_grads16.ptr; if (bytes) *bytes = m->n_grid_params * 2; break;
 			default: throw std::invalid_argument("unknown buffer kind");
 		}
 	});
@@ -343,7 +347,7 @@ ngp_status ngp_model_encode_backward(ngp_model* m, const float* pos, uint32_t st
 	return guarded([&] {
 		require(m && (n == 0 || (pos && denc)), "null argument");
 		launch_hashgrid_bwd(m->lt, pos, stride, n, reinterpret_cast<const __half*>(denc), n,
-		                    m->grads.ptr + m->n_mlp_params, S(s));
+		                    m->grid_grads16.ptr, S(s));
 	});
 }
 

@@ -184,6 +184,7 @@ struct ngp_model {
 	int mlp_variant = -1;
 
 	ngp::DevBuf<float> params32, ema32, grads, adam_m, adam_v;
+	ngp::DevBuf<__half> grid_grads16;  // hash-grid gradients (fp16, packed atomics)
 	ngp::DevBuf<__half> params16, infer16;
 	ngp::DevBuf<uint32_t> adam_steps;
 	ngp::DevBuf<__half> frag_train, frag_infer;  // packed MFMA fragments of params16 / infer16
@@ -206,7 +207,7 @@ namespace ngp {
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
                          __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2);
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                         uint32_t enc_plane, float* grad_table, hipStream_t s, const uint32_t* n_dev = nullptr);
+                         uint32_t enc_plane, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr);
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
                              float* w, hipStream_t s);
 // mlp.hip

@@ -702,10 +702,16 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	ctr.n_rays_total += ctr.rays_per_batch;
 	ck(ngp_train_step(m_model, &a, m_stream));
 	if (m_world > 1) {
-		void* g = nullptr;
-		size_t bytes = 0;
+		// MLP gradients (fp32) and hash-grid gradients (fp16) are summed over ranks
+		void *g = nullptr, *g16 = nullptr;
+		size_t bytes = 0, bytes16 = 0;
+		ngp_model_info info{};
+		ck(ngp_model_get_info(m_model, &info));
 		ck(ngp_model_buffer(m_model, NGP_GRADS_FP32, &g, &bytes));
-		allreduce_f32((float*)g, bytes / sizeof(float), false);
+		ck(ngp_model_buffer(m_model, NGP_GRADS_GRID_FP16, &g16, &bytes16));
+		allreduce_f32((float*)g, info.n_mlp_params, false);
+		nk(ncclAllReduce(g16, g16, bytes16 / 2, ncclFloat16, ncclSum, (ncclComm_t)m_comm, (hipStream_t)m_stream),
+		   "ncclAllReduce(grid grads)");
 		ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 	}
 	++training_step;

@@ -492,7 +492,8 @@ struct OptArgs {
 	int opt_mlp, opt_enc;
 	float* w32;
 	__half* w16;
-	float* grad;
+	float* grad;      // MLP gradients (fp32), [0, n_mlp)
+	__half* grad16;   // hash-grid gradients (fp16), [n_mlp, n)
 	float* m;
 	float* v;
 	uint32_t* steps;
@@ -503,9 +504,9 @@ struct OptArgs {
 __global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
 	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
 	if (i >= a.n) return;
-	const float graw = a.grad[i];
-	float w = a.w32[i];
 	const bool is_mlp = i < a.n_mlp;
+	const float graw = is_mlp ? a.grad[i] : __half2float(a.grad16[i - a.n_mlp]);
+	float w = a.w32[i];
 	bool update = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
 	if (update) {
 		float g = graw / a.loss_scale;
@@ -518,7 +519,10 @@ __global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
 		a.w32[i] = w;
 		a.w16[i] = __float2half(w);
 	}
-	if (graw != 0.0f) a.grad[i] = 0.0f;  // GradientMode::Overwrite for the next step
+	if (graw != 0.0f) {  // GradientMode::Overwrite for the next step
+		if (is_mlp) a.grad[i] = 0.0f;
+		else a.grad16[i - a.n_mlp] = __float2half(0.0f);
+	}
 	const float e = (a.ema32[i] * a.ema_decay * a.ema_debias_old + w * (1.0f - a.ema_decay)) / a.ema_debias_new;
 	a.ema32[i] = e;
 	a.ema16[i] = __float2half(e);
@@ -560,6 +564,7 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.w32 = m->params32.ptr;
 	a.w16 = m->params16.ptr;
 	a.grad = m->grads.ptr;
+	a.grad16 = m->grid_grads16.ptr;
 	a.m = m->adam_m.ptr;
 	a.v = m->adam_v.ptr;
 	a.steps = m->adam_steps.ptr;
@@ -705,7 +710,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
 	tm.begin(NGP_TIMER_TRAIN_ENCODE_BWD, s);
-	launch_hashgrid_bwd(m->lt, ts.ccoords.ptr, 8, B, ts.denc.ptr, B, m->grads.ptr + m->n_mlp_params, s,
+	launch_hashgrid_bwd(m->lt, ts.ccoords.ptr, 8, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	tm.train_units_pending = tm.enabled;

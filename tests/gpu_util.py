@@ -58,15 +58,36 @@ class GpuModel:
 
     def get(self, kind, n=None):
         ptr, nbytes = self.buffer(kind)
-        dt = np.uint16 if kind in (A.PARAMS_FP16, A.PARAMS_INFER_FP16) else np.float32
+        dt = np.uint16 if kind in (A.PARAMS_FP16, A.PARAMS_INFER_FP16, A.GRADS_GRID_FP16) else np.float32
         out = np.zeros(nbytes // np.dtype(dt).itemsize, dt)
         torch.cuda.synchronize()
         cuda_memcpy_d2h(out, ptr)
         return out
 
     def zero_grads(self):
-        ptr, nbytes = self.buffer(A.GRADS_FP32)
-        cuda_memset(ptr, nbytes)
+        for kind in (A.GRADS_FP32, A.GRADS_GRID_FP16):
+            ptr, nbytes = self.buffer(kind)
+            cuda_memset(ptr, nbytes)
+
+    def grads(self):
+        """All gradients in parameter order as fp32: MLP (fp32 buffer) + hash grid (fp16 buffer)."""
+        g = self.get(A.GRADS_FP32)
+        g[self.n_mlp:] = self.get(A.GRADS_GRID_FP16).view(np.float16).astype(np.float32)
+        return g
+
+    def set_grads(self, grads):
+        """Write fp32 MLP gradients and fp16 grid gradients; returns what the device holds (fp32)."""
+        grads = np.ascontiguousarray(grads, np.float32)
+        p, _ = self.buffer(A.GRADS_FP32)
+        g32 = grads.copy()
+        g32[self.n_mlp:] = 0.0  # the fp32 buffer's grid part is unused
+        cuda_memcpy_h2d(p, g32)
+        g16 = grads[self.n_mlp:].astype(np.float16)
+        p16, _ = self.buffer(A.GRADS_GRID_FP16)
+        cuda_memcpy_h2d(p16, g16.view(np.uint16))
+        out = grads.copy()
+        out[self.n_mlp:] = g16.astype(np.float32)
+        return out
 
     def encode(self, pos, use_inf=False):
         pos = np.ascontiguousarray(pos, np.float32)

@@ -124,9 +124,13 @@ def test_hashgrid_backward_matches_oracle(name):
         g.zero_grads()
         g.encode_backward(pos, denc)
         o.encode_backward(pos, denc.astype(np.float32))
-        gg = g.get(A.GRADS_FP32)[g.n_mlp:]
+        gg = g.grads()[g.n_mlp:]
         og = o.get(A.GRADS_FP32)[o.n_mlp:]
-        np.testing.assert_array_equal(gg != 0, og != 0)
-        np.testing.assert_allclose(gg, og, atol=1e-5, rtol=1e-4)
+        # fp16 packed atomics (tcnn GridEncoding): per-entry sums rounded to half at each add
+        assert np.linalg.norm(gg - og) / np.linalg.norm(og) < 2e-3
+        big = np.abs(og) > 1e-2
+        close = np.abs(gg[big] - og[big]) <= 5e-2 * np.abs(og[big])
+        assert close.mean() > 0.999, (close.mean(), np.abs(gg - og).max())
+        assert ((gg != 0) == (og != 0)).mean() > 0.9999
     finally:
         g.close()

@@ -108,7 +108,7 @@ def test_train_step_matches_oracle(cfg_kw):
             g_dl = gpu_scratch(g, A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[:C_].astype(np.float32)
             o_dl = o.scratch(A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[:C_].astype(np.float32)
             assert np.linalg.norm(g_dl - o_dl) / np.linalg.norm(o_dl) < 2e-2
-            gg, og = g.get(A.GRADS_FP32), o.get(A.GRADS_FP32)
+            gg, og = g.grads(), o.get(A.GRADS_FP32)
             for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
                 rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
                 assert rel < 5e-2, rel
@@ -124,15 +124,14 @@ def test_optimizer_matches_oracle():
             grads[: g.n_mlp] = rng.normal(0, 1, g.n_mlp)
             idx = rng.choice(g.n_params - g.n_mlp, 50000, replace=False) + g.n_mlp
             grads[idx] = rng.normal(0, 1, idx.size)
-            gp, _ = g.buffer(A.GRADS_FP32)
-            cuda_memcpy_h2d(gp, grads)
-            o.set_grads(grads)
+            o.set_grads(g.set_grads(grads))  # grid part as the fp16 the device holds
             A.check(g.lib.ngp_optimizer_step(g.h, step, 1, 1, stream()))
             torch.cuda.synchronize()
             o.optimizer_step(step, 1, 1)
         for kind in (A.PARAMS_FP32, A.PARAMS_EMA_FP32):
             np.testing.assert_allclose(g.get(kind), o.get(kind), rtol=1e-5, atol=1e-7)
         assert not g.get(A.GRADS_FP32).any()  # GradientMode::Overwrite: zeroed for the next step
+        assert not g.get(A.GRADS_GRID_FP16).any()
     finally:
         g.close()
 
