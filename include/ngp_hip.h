@@ -277,7 +277,9 @@ enum {
 	NGP_TIMER_RENDER_MARCH = 10,    /* render: init/compact/generate/composite (rays)   */
 	NGP_TIMER_COUNT = 11
 };
-ngp_status ngp_timing_enable(ngp_model* model, int enable);
+/* mask: bit k enables timer k (-1 = all, 0 = off); events cost a few microseconds of GPU
+ * time each, so a timed run enables only the timers it reports. */
+ngp_status ngp_timing_enable(ngp_model* model, int mask);
 ngp_status ngp_timing_read(ngp_model* model, int timer, double* total_ms, uint64_t* units, uint32_t* launches,
                            int reset);
 

@@ -473,10 +473,10 @@ ngp_status ngp_accumulate_tonemap(const float* frame, float* accum, float* out, 
 	});
 }
 
-ngp_status ngp_timing_enable(ngp_model* m, int enable) {
+ngp_status ngp_timing_enable(ngp_model* m, int mask) {
 	return guarded([&] {
 		require(m, "null model");
-		m->timers.enabled = enable != 0;
+		m->timers.mask = (uint32_t)mask & ((1u << NGP_TIMER_COUNT) - 1u);
 	});
 }
 

@@ -27,7 +27,7 @@ struct KernelTimers {
 		int slot;
 		hipEvent_t a, b;
 	};
-	bool enabled = false;
+	uint32_t mask = 0;  // bit k: timer k records events
 	bool train_units_pending = false;
 	std::vector<hipEvent_t> pool;
 	std::vector<Pending> pending;
@@ -46,13 +46,14 @@ struct KernelTimers {
 		pool.pop_back();
 		return e;
 	}
+	bool on(int slot) const { return (mask >> slot) & 1u; }
 	void begin(int slot, hipStream_t s) {
-		if (!enabled) return;
+		if (!on(slot)) return;
 		open[slot] = take();
 		NGP_HIP_CHECK(hipEventRecord(open[slot], s));
 	}
 	void end(int slot, hipStream_t s, uint64_t u = 0) {
-		if (!enabled || !open[slot]) return;
+		if (!on(slot) || !open[slot]) return;
 		hipEvent_t e = take();
 		NGP_HIP_CHECK(hipEventRecord(e, s));
 		pending.push_back({slot, open[slot], e});

@@ -290,10 +290,31 @@ NGP_HD bool density_grid_occupied_cached(v3 pos, const uint8_t* bitfield, uint32
 
 NGP_HD float signf_(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
 
-// Occupancy summary per mip: 4096 bits "any cell of this 8^3 Morton block set"
-// (block = idx >> 9) followed by 64 bits for 32^3 blocks (idx >> 15).  Derived from
-// the bitfield; lets the render march leap over large empty regions.
-constexpr uint32_t OCC_SUMMARY_BYTES = 512 + 8;
+// Occupancy summary per mip, derived from the bitfield (render.hip k_occupancy_summary):
+// level A = 32768 bits, one per 4^3-cell Morton block (cell >> 6: "its 64-bit bitfield
+// word is non-zero"), level B = 4096 bits per 8^3 block (cell >> 9), level C = 64 bits
+// per 32^3 block (cell >> 15).  4.6 KB per mip: the render kernels keep it in LDS, so
+// empty space is crossed without touching the bitfield at all.
+constexpr uint32_t OCC_SUMMARY_A = 0, OCC_SUMMARY_B = 4096, OCC_SUMMARY_C = 4096 + 512;
+constexpr uint32_t OCC_SUMMARY_BYTES = 4096 + 512 + 16;  // level C padded: 16-byte staging copies
+static_assert(OCC_SUMMARY_BYTES % 16 == 0, "summary is staged into LDS in 16-byte pieces");
+NGP_HD bool summary_bit(const uint8_t* sm, uint32_t level_base, uint32_t b) {
+	return (sm[level_base + (b >> 3)] >> (b & 7u)) & 1u;
+}
+// density_grid_occupied_at through the summary (level A) and the one-word cache
+NGP_HD bool occupied_summarised(v3 pos, const uint8_t* bitfield, const uint8_t* summary, uint32_t mip, OccCache& c,
+                                uint32_t* cell_out) {
+	const uint32_t cell = cascaded_grid_idx_at(pos, mip);
+	*cell_out = cell;
+	if (cell == 0xFFFFFFFFu) return false;
+	if (!summary_bit(summary + OCC_SUMMARY_BYTES * mip, OCC_SUMMARY_A, cell >> 6)) return false;
+	const uint32_t key = (NERF_GRID_N_CELLS / 64) * mip + cell / 64;
+	if (key != c.key) {
+		c.key = key;
+		c.bits = reinterpret_cast<const uint64_t*>(bitfield)[key];
+	}
+	return (c.bits >> (cell % 64)) & 1ull;
+}
 
 // ---------------------------------------------------------------------------
 // Stepping lattice.  A ray's candidate samples sit at n0 + k (k = 0, 1, ...) in the
@@ -372,10 +393,9 @@ NGP_HD uint32_t mip_from_dt(float dt, v3 pos, uint32_t max_cascade = NERF_CASCAD
 // the lattice): moves *n to the first lattice point at or after it whose cell (at
 // clamp(mip_from_pos, 0, max_mip)) is occupied; false once the ray leaves the AABB.
 // An empty cell is skipped in one jump to the first lattice point past its far face
-// (at the coarsest empty mip, as the reference does) -- or, when the whole Morton
-// block of 4^3 cells around it is empty (one zero 64-bit bitfield word), past the
-// far face of the largest empty aligned block of 4^3, 8^3 or 32^3 cells (summary
-// bits, see occupancy_summary below).  The jump is taken only if the lattice point just before the
+// (at the coarsest empty mip, as the reference does) -- or past the far face of the
+// largest empty aligned Morton block of 4^3, 8^3 or 32^3 cells around it (occupancy
+// summary above).  The jump is taken only if the lattice point just before the
 // landing point is still inside the skipped cell/block, so every skipped point
 // provably lies in empty space and the result equals testing the points one by one.
 enum LatticeStep : int { LATTICE_OCCUPIED = 0, LATTICE_SKIPPED = 1, LATTICE_EXIT = 2 };
@@ -390,20 +410,24 @@ NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, co
 	if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return LATTICE_EXIT;
 	uint32_t mip = mip_from_pos(pos);
 	mip = mip > max_mip ? max_mip : mip;
-	if (density_grid_occupied_cached(pos, bitfield, mip, cache)) return LATTICE_OCCUPIED;
-	while (mip < max_mip && !density_grid_occupied_cached(pos, bitfield, mip + 1, cache)) ++mip;
-	// the cached word now covers the 4x4x4-cell block around pos at `mip`: if it is all
-	// zero, jump over the largest empty aligned block, else over the one cell
-	const uint32_t cell = cascaded_grid_idx_at(pos, mip);
-	(void)density_grid_occupied_cached(pos, bitfield, mip, cache);
+	uint32_t cell;
+	if (occupied_summarised(pos, bitfield, summary, mip, cache, &cell)) return LATTICE_OCCUPIED;
+	while (mip < max_mip) {  // coarsest empty mip, as the reference climbs
+		uint32_t up;
+		if (occupied_summarised(pos, bitfield, summary, mip + 1, cache, &up)) break;
+		++mip;
+		cell = up;
+	}
+	// jump over the largest empty aligned block around pos at `mip`: 1, 4^3, 8^3 or 32^3 cells
 	uint32_t shift = 0;
-	if (cell != 0xFFFFFFFFu && cache.bits == 0ull) {
-		shift = 6;  // 4^3 cells empty
+	if (cell != 0xFFFFFFFFu) {
 		const uint8_t* sm = summary + OCC_SUMMARY_BYTES * mip;
-		const uint32_t b1 = cell >> 9, b2 = cell >> 15;
-		if (!((sm[b1 >> 3] >> (b1 & 7u)) & 1u)) {
-			shift = 9;  // 8^3 cells empty
-			if (!((sm[512 + (b2 >> 3)] >> (b2 & 7u)) & 1u)) shift = 15;  // 32^3 cells empty
+		if (!summary_bit(sm, OCC_SUMMARY_A, cell >> 6)) {
+			shift = 6;
+			if (!summary_bit(sm, OCC_SUMMARY_B, cell >> 9)) {
+				shift = 9;
+				if (!summary_bit(sm, OCC_SUMMARY_C, cell >> 15)) shift = 15;
+			}
 		}
 	}
 	const uint32_t here = cell >> shift;

@@ -51,8 +51,18 @@ __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32
 	return (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
 }
 
-__device__ __forceinline__ void init_ray_body(const RenderK& k, uint32_t r, Payload* pp, float4* __restrict__ frame,
-                                              float* __restrict__ depth_buffer);
+// Copies the summaries of mips [0, max_mip] into LDS (all threads of the block).
+__device__ __forceinline__ const uint8_t* stage_summary(const uint8_t* __restrict__ g, uint32_t max_mip) {
+	extern __shared__ uint4 s_summary[];
+	const uint32_t n16 = (max_mip + 1) * OCC_SUMMARY_BYTES / 16;
+	const uint4* src = reinterpret_cast<const uint4*>(g);
+	for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) s_summary[k] = src[k];
+	__syncthreads();
+	return reinterpret_cast<const uint8_t*>(s_summary);
+}
+
+__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t r, Payload* pp,
+                                              float4* __restrict__ frame, float* __restrict__ depth_buffer);
 
 // Stream compaction slot for a 256-thread block: ballot per wave, LDS prefix over the four
 // waves, ONE global atomic per block and flag (instead of one per wave).  Returns the
@@ -88,10 +98,11 @@ __device__ __forceinline__ void block_append2(bool fa, bool fb, uint32_t* counte
 __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
                                                      float* __restrict__ depth, float4* __restrict__ frame,
                                                      float* __restrict__ depth_buffer, uint32_t* __restrict__ counters) {
+	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	Payload p;
 	p.alive = 0;
-	if (r < k.n_local) init_ray_body(k, r, &p, frame, depth_buffer);
+	if (r < k.n_local) init_ray_body(k, summary, r, &p, frame, depth_buffer);
 	uint32_t slot, unused;
 	block_append2(p.alive != 0, false, &counters[0], &counters[3], &slot, &unused);
 	if (p.alive) {
@@ -102,8 +113,8 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 }
 
 // init_rays_with_payload_kernel_nerf + advance_pos_nerf for local ray r
-__device__ __forceinline__ void init_ray_body(const RenderK& k, uint32_t r, Payload* pp, float4* __restrict__ frame,
-                                              float* __restrict__ depth_buffer) {
+__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t r, Payload* pp,
+                                              float4* __restrict__ frame, float* __restrict__ depth_buffer) {
 	const uint32_t x = r % k.W, yl = r / k.W;
 	const uint32_t y = local_to_global_row(k, yl);
 	const uint32_t idx = x + k.W * y;
@@ -135,29 +146,32 @@ __device__ __forceinline__ void init_ray_body(const RenderK& k, uint32_t r, Payl
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
 		float n = step_to(k.st, t) + ld_random_val(k.sample_index, idx * 786433u);
 		OccCache occ = occ_cache_init();
-		p.alive = next_occupied_lattice_point(&n, k.st, origin, dir, idir, k.bitfield, k.summary, k.max_mip, k.aabb, occ) ? 1u : 0u;
+		p.alive = next_occupied_lattice_point(&n, k.st, origin, dir, idir, k.bitfield, summary, k.max_mip, k.aabb, occ) ? 1u : 0u;
 		p.n = n;
 	}
 	*pp = p;
 }
 
-// Occupancy summary (see ngp_math.h): one thread per 8^3 block; a wave covers 64
-// consecutive blocks = one 32^3 block, so both levels come from ballots.
+// Occupancy summary (ngp_math.h OCC_SUMMARY_*): one thread per 64-bit bitfield word
+// (4^3 block); a wave covers 64 consecutive words = eight 8^3 blocks, so levels A and B
+// come from one ballot; level C (32^3 = 8 waves) is OR-ed in with an atomic.
 __global__ void __launch_bounds__(256) k_occupancy_summary(const uint8_t* __restrict__ bitfield, uint8_t* __restrict__ summary) {
-	const uint32_t g = blockIdx.x * 256u + threadIdx.x;  // [mip][4096]
-	const uint32_t mip = g >> 12, b1 = g & 4095u;
-	const uint64_t* w = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8)) + (size_t)b1 * 8;
-	uint64_t any = 0;
-#pragma unroll
-	for (int j = 0; j < 8; ++j) any |= w[j];
-	const unsigned long long m = __ballot(any != 0ull);
+	const uint32_t g = blockIdx.x * 256u + threadIdx.x;  // [mip][32768 words]
+	const uint32_t mip = g >> 15, wi = g & 32767u;
+	const uint64_t w = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8))[wi];
+	const unsigned long long a = __ballot(w != 0ull);
 	uint8_t* sm = summary + (size_t)OCC_SUMMARY_BYTES * mip;
 	if ((threadIdx.x & 63u) == 0) {
-		*reinterpret_cast<unsigned long long*>(sm + (b1 >> 3)) = m;
-		const uint32_t b2 = b1 >> 6;
-		if (m) atomicOr(reinterpret_cast<uint32_t*>(sm + 512) + (b2 >> 5), 1u << (b2 & 31u));
+		*reinterpret_cast<unsigned long long*>(sm + OCC_SUMMARY_A + (wi >> 3)) = a;
+		uint8_t b = 0;
+		for (uint32_t k = 0; k < 8; ++k) b |= ((a >> (8 * k)) & 0xffull) ? (uint8_t)(1u << k) : (uint8_t)0;
+		sm[OCC_SUMMARY_B + (wi >> 6)] = b;
+		const uint32_t c = wi >> 9;  // 32^3 block
+		if (a) atomicOr(reinterpret_cast<uint32_t*>(sm + OCC_SUMMARY_C) + (c >> 5), 1u << (c & 31u));
 	}
 }
+
+
 
 __global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                  const float* __restrict__ sdepth, Payload* __restrict__ dp,
@@ -208,6 +222,7 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 
 __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
                                                   float* __restrict__ coords, uint32_t n_steps) {
+	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= n_alive) return;
 	Payload& p = payloads[i];
@@ -221,7 +236,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 	// that are skipping empty space never hold up lanes that are sampling (and vice versa)
 	uint32_t j = 0;
 	while (j < n_steps) {
-		const int r = lattice_step(&n, k.st, o, d, idir, k.bitfield, k.summary, k.max_mip, k.aabb, occ);
+		const int r = lattice_step(&n, k.st, o, d, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
 		if (r == LATTICE_EXIT) {
 			p.n_steps = j;
 			return;
@@ -396,7 +411,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);
 	k.bitfield = m->gs.bitfield.ptr;
-	rs.summary.reserve(OCC_SUMMARY_BYTES * NERF_CASCADES / 4 + 1);
+	rs.summary.reserve(OCC_SUMMARY_BYTES * NERF_CASCADES / 4);
 	k.summary = reinterpret_cast<const uint8_t*>(rs.summary.ptr);
 	const uint32_t H_local = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	const uint32_t n = k.W * H_local;
@@ -424,10 +439,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
 	for (uint32_t mip = 0; mip < NERF_CASCADES; ++mip)
-		NGP_HIP_CHECK(hipMemsetAsync(rs.summary.ptr + (OCC_SUMMARY_BYTES * mip + 512) / 4, 0, 8, s));
-	k_occupancy_summary<<<NERF_CASCADES * 4096 / 256, 256, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr));
+		NGP_HIP_CHECK(hipMemsetAsync(rs.summary.ptr + (OCC_SUMMARY_BYTES * mip + OCC_SUMMARY_C) / 4, 0, 8, s));
+	k_occupancy_summary<<<NERF_CASCADES * 32768 / 256, 256, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr));
+	const size_t lds = (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
 	NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, 4 * sizeof(uint32_t), s));
-	k_render_init<<<div_up(n, 256), 256, 0, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
+	k_render_init<<<div_up(n, 256), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
 	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
@@ -447,7 +463,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// every ray composites its own samples in order and stops at the same one whatever the chunking
 		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), max_steps_per_pass());
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_generate<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
+		k_generate<<<div_up(n_alive, 256), 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);

@@ -713,7 +713,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	launch_hashgrid_bwd(m->lt, ts.ccoords.ptr, 8, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
-	tm.train_units_pending = tm.enabled;
+	tm.train_units_pending = tm.mask != 0;
 
 	if (!t->defer_optimizer) launch_optimizer(m, t->training_step, t->optimize_mlp, t->optimize_encoding, s);
 	m->stats_pending = true;

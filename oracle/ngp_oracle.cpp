@@ -285,21 +285,24 @@ static bool occupied(V3 p, const uint8_t* bits, uint32_t mip) {
 	if (i == 0xFFFFFFFFu) return false;
 	return bits[i / 8 + CELLS / 8 * mip] & (1u << (i % 8));
 }
-// Occupancy summary per mip (ngp_math.h OCC_SUMMARY_BYTES): 4096 bits for 8^3 Morton blocks
-// (cell >> 9), then 64 bits for 32^3 blocks (cell >> 15).
-static const uint32_t SUMMARY_BYTES = 512 + 8;
+// Occupancy summary per mip (ngp_math.h OCC_SUMMARY_*): level A 32768 bits (4^3 blocks,
+// cell >> 6), level B 4096 bits (8^3 blocks, cell >> 9), level C 64 bits (32^3, cell >> 15).
+static const uint32_t SUM_A = 0, SUM_B = 4096, SUM_C = 4096 + 512, SUMMARY_BYTES = 4096 + 512 + 8;
 static std::vector<uint8_t> occ_summary(const uint8_t* bits) {
 	std::vector<uint8_t> sm((size_t)SUMMARY_BYTES * CASCADES, 0);
 	for (uint32_t mip = 0; mip < CASCADES; ++mip)
-		for (uint32_t b1 = 0; b1 < 4096; ++b1) {
+		for (uint32_t w = 0; w < 32768; ++w) {
 			bool any = false;
-			for (uint32_t k = 0; k < 64; ++k) any |= bits[(size_t)CELLS / 8 * mip + b1 * 64 + k] != 0;
+			for (uint32_t k = 0; k < 8; ++k) any |= bits[(size_t)CELLS / 8 * mip + w * 8 + k] != 0;
 			if (!any) continue;
-			sm[SUMMARY_BYTES * mip + (b1 >> 3)] |= (uint8_t)(1u << (b1 & 7));
-			sm[SUMMARY_BYTES * mip + 512 + (b1 >> 9)] |= (uint8_t)(1u << ((b1 >> 6) & 7));
+			uint8_t* s = &sm[(size_t)SUMMARY_BYTES * mip];
+			s[SUM_A + (w >> 3)] |= (uint8_t)(1u << (w & 7));
+			s[SUM_B + (w >> 6)] |= (uint8_t)(1u << ((w >> 3) & 7));
+			s[SUM_C + (w >> 12)] |= (uint8_t)(1u << ((w >> 9) & 7));
 		}
 	return sm;
 }
+static bool sum_bit(const uint8_t* sm, uint32_t base, uint32_t b) { return (sm[base + (b >> 3)] >> (b & 7u)) & 1u; }
 
 // First occupied lattice point at or after *n (render march); an empty cell is jumped over
 // only when the lattice point before the landing point is still inside it.
@@ -313,18 +316,17 @@ static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, 
 		uint32_t mip = std::min(mip_pos(pos), maxm);
 		if (occupied(pos, bits, mip)) { *n_io = n; return true; }
 		while (mip < maxm && !occupied(pos, bits, mip + 1)) ++mip;
-		// whole 4x4x4 Morton block empty (its 64-bit word is zero)? jump the block, else the cell
+		// largest empty aligned Morton block around pos at `mip`: 1, 4^3, 8^3 or 32^3 cells
 		const uint32_t cell = grid_idx(pos, mip);
-		uint64_t word = 1;
-		if (cell != 0xFFFFFFFFu) std::memcpy(&word, &bits[(size_t)CELLS / 8 * mip + (cell / 64) * 8], 8);
 		uint32_t shift = 0;
-		if (word == 0) {
-			shift = 6;
-			const uint8_t* sm = summary + SUMMARY_BYTES * mip;
-			const uint32_t b1 = cell >> 9, b2 = cell >> 15;
-			if (!((sm[b1 >> 3] >> (b1 & 7u)) & 1u)) {
-				shift = 9;
-				if (!((sm[512 + (b2 >> 3)] >> (b2 & 7u)) & 1u)) shift = 15;
+		if (cell != 0xFFFFFFFFu) {
+			const uint8_t* sm = summary + (size_t)SUMMARY_BYTES * mip;
+			if (!sum_bit(sm, SUM_A, cell >> 6)) {
+				shift = 6;
+				if (!sum_bit(sm, SUM_B, cell >> 9)) {
+					shift = 9;
+					if (!sum_bit(sm, SUM_C, cell >> 15)) shift = 15;
+				}
 			}
 		}
 		const float n_far = lat_to(st, t + dist_next_cell(pos, d, idir, mip + shift / 3u));

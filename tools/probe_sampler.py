@@ -20,7 +20,7 @@ g.set_params(random_params(g.n_params, g.n_mlp, g.info, rng, 0.5))
 imgs, cams, focal = make_views(16, 64, 64)
 dd = DeviceDataset(imgs, cams, focal)
 lib = g.lib
-A.check(lib.ngp_timing_enable(g.h, 1))
+A.check(lib.ngp_timing_enable(g.h, -1))
 CELLS = 128 ** 3
 for name, grid in [("full", np.ones(CELLS, np.float32)), ("sphere0.3", sphere_bitfield(0.3)),
                    ("sphere0.1", sphere_bitfield(0.1)), ("empty", np.zeros(CELLS, np.float32))]:
