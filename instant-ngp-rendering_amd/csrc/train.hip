@@ -304,29 +304,78 @@ struct LossArgs {
 	const float* mean_density;
 };
 
+// Wave scans over the 64 lanes (inclusive).
+__device__ __forceinline__ float wave_scan_add(float v, uint32_t lane) {
+#pragma unroll
+	for (uint32_t off = 1; off < 64; off <<= 1) {
+		const float t = __shfl_up(v, off, 64);
+		if (lane >= off) v += t;
+	}
+	return v;
+}
+__device__ __forceinline__ float wave_scan_mul(float v, uint32_t lane) {
+#pragma unroll
+	for (uint32_t off = 1; off < 64; off <<= 1) {
+		const float t = __shfl_up(v, off, 64);
+		if (lane >= off) v *= t;
+	}
+	return v;
+}
+
+// One compacted-batch sample as the compositor sees it.
+struct LossSample {
+	v3 rgb;
+	float alpha, dt;
+	float raw[4];
+};
+__device__ __forceinline__ LossSample loss_sample(const LossArgs& a, size_t src) {
+	LossSample q;
+	const uint2 ob = *reinterpret_cast<const uint2*>(a.mlp_out + 4 * src);
+	const __half* o = reinterpret_cast<const __half*>(&ob);
+	for (int k = 0; k < 4; ++k) q.raw[k] = __half2float(o[k]);
+	q.rgb = mk3(network_to_rgb(q.raw[0], a.rgb_act), network_to_rgb(q.raw[1], a.rgb_act), network_to_rgb(q.raw[2], a.rgb_act));
+	q.dt = unwarp_dt(a.coords[8 * src + 3]);
+	q.alpha = 1.0f - __expf(-network_to_density(q.raw[3], a.density_act) * q.dt);
+	return q;
+}
+
+// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1160), pass 1: one wave per ray,
+// 64 samples per iteration.  Transmittance T_j = prod_{i<j}(1 - alpha_i) comes from a
+// multiplicative wave scan, the colour from an additive one; the ray stops at the first
+// sample with T_j < 1e-4 (the reference's sequential test), found with a ballot.
 __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	if (i >= a.n_rays) return;
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63u;
+	if (i >= a.n_rays) return;  // wave-uniform
 	const uint32_t numsteps = a.numsteps[2 * i + 0], base = a.numsteps[2 * i + 1];
 	if (numsteps == 0) {
-		a.ccounts[i] = 0;
+		if (lane == 0) a.ccounts[i] = 0;
 		return;
 	}
 	float T = 1.0f;
 	v3 rgb_ray = mk3(0.0f);
-	uint32_t c = 0;
-	for (; c < numsteps; ++c) {
-		if (T < 1e-4f) break;
-		const __half* o = a.mlp_out + 4 * (size_t)(base + c);
-		const float* crd = a.coords + 8 * (size_t)(base + c);
-		const v3 rgb = mk3(network_to_rgb(__half2float(o[0]), a.rgb_act), network_to_rgb(__half2float(o[1]), a.rgb_act),
-		                   network_to_rgb(__half2float(o[2]), a.rgb_act));
-		const float dt = unwarp_dt(crd[3]);
-		const float density = network_to_density(__half2float(o[3]), a.density_act);
-		const float alpha = 1.0f - __expf(-density * dt);
-		const float weight = alpha * T;
-		rgb_ray = rgb_ray + rgb * weight;
-		T *= (1.0f - alpha);
+	uint32_t c = numsteps;
+	for (uint32_t kb = 0; kb < numsteps; kb += 64) {
+		const uint32_t j = kb + lane;
+		const bool active = j < numsteps;
+		LossSample q;
+		if (active) q = loss_sample(a, (size_t)base + j);
+		else { q.alpha = 0.0f; q.rgb = mk3(0.0f); }
+		const float incl = wave_scan_mul(1.0f - q.alpha, lane);
+		float excl = __shfl_up(incl, 1, 64);
+		if (lane == 0) excl = 1.0f;
+		const float Tj = T * excl;
+		const unsigned long long term = __ballot(active && Tj < 1e-4f);
+		const uint32_t first = term ? (uint32_t)(__ffsll((long long)term) - 1) : 64u;
+		const float w = (active && lane < first) ? q.alpha * Tj : 0.0f;
+		rgb_ray.x += __shfl(wave_scan_add(q.rgb.x * w, lane), 63, 64);
+		rgb_ray.y += __shfl(wave_scan_add(q.rgb.y * w, lane), 63, 64);
+		rgb_ray.z += __shfl(wave_scan_add(q.rgb.z * w, lane), 63, 64);
+		if (term) {
+			c = kb + first;
+			break;
+		}
+		T *= __shfl(incl, 63, 64);
 	}
 
 	// Same RNG stream as the sampler -> same pixel and background colour (testbed_nerf.cu:938-955).
@@ -369,6 +418,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 		}
 	}
 	if (c == numsteps) rgb_ray = rgb_ray + bg * T;
+	if (lane != 0) return;
 	float lx, ly, lz, gx, gy, gz;
 	loss_and_gradient(target.x, rgb_ray.x, a.loss_type, &lx, &gx);
 	loss_and_gradient(target.y, rgb_ray.y, a.loss_type, &ly, &gy);
@@ -380,56 +430,70 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	a.ccounts[i] = c;
 }
 
+// pass 2: recomposite the kept samples of the ray (one wave, 64 per iteration) and write
+// dL/d(raw network output) with the suffix trick (testbed_nerf.cu:1061-1119) plus the
+// compacted-slot -> source-sample map; consecutive lanes write consecutive slots.
 __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
+	const uint32_t lane = threadIdx.x & 63u;
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.ccounts[i], cbase = a.cbases[i];
 	const uint32_t cn = n == 0 ? 0 : min(a.max_compacted - min(a.max_compacted, cbase), n);
-	a.compacted[2 * i + 0] = cn;
-	a.compacted[2 * i + 1] = cbase;
+	if (lane == 0) {
+		a.compacted[2 * i + 0] = cn;
+		a.compacted[2 * i + 1] = cbase;
+	}
 	if (cn == 0) {
-		a.loss_out[i] = 0.0f;
+		if (lane == 0) a.loss_out[i] = 0.0f;
 		return;
 	}
 	const uint32_t base = a.numsteps[2 * i + 1];
 	const float* ls = a.loss_state + 8 * (size_t)i;
 	const v3 grad = mk3(ls[0], ls[1], ls[2]);
 	const v3 rgb_ray = mk3(ls[3], ls[4], ls[5]);
-	a.loss_out[i] = ls[6] / (float)a.n_rays_global;
+	if (lane == 0) a.loss_out[i] = ls[6] / (float)a.n_rays_global;
 	const float loss_scale = 128.0f / (float)a.n_rays_global;  // LOSS_SCALE / n_rays (testbed_nerf.cu:1056)
 	const float output_l2_reg = a.rgb_act == ACT_EXP ? 1e-4f : 0.0f;
 	const float output_l1_reg_density = *a.mean_density < NERF_MIN_OPTICAL_THICKNESS ? 1e-4f : 0.0f;
 	const v3 ray_o = mk3(a.ray_state[8 * (size_t)i + 0], a.ray_state[8 * (size_t)i + 1], a.ray_state[8 * (size_t)i + 2]);
 
-	v3 rgb_ray2 = mk3(0.0f);
+	v3 acc = mk3(0.0f);
 	float T = 1.0f;
-	for (uint32_t j = 0; j < cn; ++j) {
-		const size_t src = base + j, dst = cbase + j;
-		a.csrc[dst] = (uint32_t)src;
-		const float4 c0 = *reinterpret_cast<const float4*>(a.coords + 8 * src);
-		const v3 pos = unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb);
-		const float depth = length(pos - ray_o);
-		const float dt = unwarp_dt(c0.w);
-		const uint2 ob = *reinterpret_cast<const uint2*>(a.mlp_out + 4 * src);
-		const __half* o = reinterpret_cast<const __half*>(&ob);
-		const float o0 = __half2float(o[0]), o1 = __half2float(o[1]), o2 = __half2float(o[2]), o3 = __half2float(o[3]);
-		const v3 rgb = mk3(network_to_rgb(o0, a.rgb_act), network_to_rgb(o1, a.rgb_act), network_to_rgb(o2, a.rgb_act));
-		const float density = network_to_density(o3, a.density_act);
-		const float alpha = 1.0f - __expf(-density * dt);
-		const float weight = alpha * T;
-		rgb_ray2 = rgb_ray2 + rgb * weight;
-		T *= (1.0f - alpha);
-		const v3 suffix = rgb_ray - rgb_ray2;
-		const v3 dloss_by_drgb = grad * weight;
-		__half dl[4];
-		dl[0] = __float2half(loss_scale * (dloss_by_drgb.x * network_to_rgb_derivative(o0, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o0)));
-		dl[1] = __float2half(loss_scale * (dloss_by_drgb.y * network_to_rgb_derivative(o1, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o1)));
-		dl[2] = __float2half(loss_scale * (dloss_by_drgb.z * network_to_rgb_derivative(o2, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o2)));
-		const float density_derivative = network_to_density_derivative(o3, a.density_act);
-		const float dloss_by_dmlp = density_derivative * (dt * dot(grad, rgb * T - suffix));
-		dl[3] = __float2half(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
-		                     (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
-		*reinterpret_cast<uint2*>(a.dloss + 4 * dst) = *reinterpret_cast<const uint2*>(dl);
+	for (uint32_t kb = 0; kb < cn; kb += 64) {
+		const uint32_t j = kb + lane;
+		const bool active = j < cn;
+		const size_t src = (size_t)base + j, dst = (size_t)cbase + j;
+		LossSample q;
+		if (active) q = loss_sample(a, src);
+		else { q.alpha = 0.0f; q.rgb = mk3(0.0f); q.dt = 0.0f; q.raw[0] = q.raw[1] = q.raw[2] = q.raw[3] = 0.0f; }
+		const float incl = wave_scan_mul(1.0f - q.alpha, lane);
+		float excl = __shfl_up(incl, 1, 64);
+		if (lane == 0) excl = 1.0f;
+		const float Tj = T * excl, Tnext = T * incl;
+		const float weight = q.alpha * Tj;
+		const v3 pre = mk3(wave_scan_add(q.rgb.x * weight, lane), wave_scan_add(q.rgb.y * weight, lane),
+		                   wave_scan_add(q.rgb.z * weight, lane));
+		const v3 rgb_ray2 = acc + pre;
+		if (active) {
+			a.csrc[dst] = (uint32_t)src;
+			const float4 c0 = *reinterpret_cast<const float4*>(a.coords + 8 * src);
+			const v3 pos = unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb);
+			const float depth = length(pos - ray_o);
+			const v3 suffix = rgb_ray - rgb_ray2;
+			const v3 dloss_by_drgb = grad * weight;
+			const float o0 = q.raw[0], o1 = q.raw[1], o2 = q.raw[2], o3 = q.raw[3];
+			__half dl[4];
+			dl[0] = __float2half(loss_scale * (dloss_by_drgb.x * network_to_rgb_derivative(o0, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o0)));
+			dl[1] = __float2half(loss_scale * (dloss_by_drgb.y * network_to_rgb_derivative(o1, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o1)));
+			dl[2] = __float2half(loss_scale * (dloss_by_drgb.z * network_to_rgb_derivative(o2, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o2)));
+			const float density_derivative = network_to_density_derivative(o3, a.density_act);
+			const float dloss_by_dmlp = density_derivative * (q.dt * dot(grad, q.rgb * Tnext - suffix));
+			dl[3] = __float2half(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
+			                     (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
+			*reinterpret_cast<uint2*>(a.dloss + 4 * dst) = *reinterpret_cast<const uint2*>(dl);
+		}
+		acc = acc + mk3(__shfl(pre.x, 63, 64), __shfl(pre.y, 63, 64), __shfl(pre.z, 63, 64));
+		T *= __shfl(incl, 63, 64);
 	}
 }
 
@@ -631,7 +695,6 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.bases = counts.ptr + R;
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
-	const uint32_t rb = div_up(R, 256);
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
 	k_sample_count<<<div_up(R, 4), 256, 0, s>>>(sa);
@@ -687,9 +750,9 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
-	k_loss_composite<<<rb, 256, 0, s>>>(la);
+	k_loss_composite<<<div_up(R, 4), 256, 0, s>>>(la);
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
-	k_loss_emit<<<rb, 256, 0, s>>>(la);
+	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
 	NGP_HIP_CHECK(hipGetLastError());
 
 	// compacted batch size c = min(total, B); rollover multiplicity
