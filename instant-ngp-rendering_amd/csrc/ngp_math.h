@@ -292,15 +292,16 @@ NGP_HD float signf_(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f
 
 // Occupancy summary per mip, derived from the bitfield (render.hip k_occupancy_summary):
 // level A = 32768 bits, one per 4^3-cell Morton block (cell >> 6: "its 64-bit bitfield
-// word is non-zero"), level B = 4096 bits per 8^3 block (cell >> 9), level C = 64 bits
+// word is non-zero"), level B = 4096 bits per 8^3 block (cell >> 9), level C = one byte
 // per 32^3 block (cell >> 15).  4.6 KB per mip: the render kernels keep it in LDS, so
 // empty space is crossed without touching the bitfield at all.
 constexpr uint32_t OCC_SUMMARY_A = 0, OCC_SUMMARY_B = 4096, OCC_SUMMARY_C = 4096 + 512;
-constexpr uint32_t OCC_SUMMARY_BYTES = 4096 + 512 + 16;  // level C padded: 16-byte staging copies
+constexpr uint32_t OCC_SUMMARY_BYTES = 4096 + 512 + 64;
 static_assert(OCC_SUMMARY_BYTES % 16 == 0, "summary is staged into LDS in 16-byte pieces");
 NGP_HD bool summary_bit(const uint8_t* sm, uint32_t level_base, uint32_t b) {
 	return (sm[level_base + (b >> 3)] >> (b & 7u)) & 1u;
 }
+NGP_HD bool summary_c(const uint8_t* sm, uint32_t b) { return sm[OCC_SUMMARY_C + b] != 0; }
 // density_grid_occupied_at through the summary (level A) and the one-word cache
 NGP_HD bool occupied_summarised(v3 pos, const uint8_t* bitfield, const uint8_t* summary, uint32_t mip, OccCache& c,
                                 uint32_t* cell_out) {
@@ -396,8 +397,9 @@ NGP_HD uint32_t mip_from_dt(float dt, v3 pos, uint32_t max_cascade = NERF_CASCAD
 // (at the coarsest empty mip, as the reference does) -- or past the far face of the
 // largest empty aligned Morton block of 4^3, 8^3 or 32^3 cells around it (occupancy
 // summary above).  The jump is taken only if the lattice point just before the
-// landing point is still inside the skipped cell/block, so every skipped point
-// provably lies in empty space and the result equals testing the points one by one.
+// landing point is still inside the skipped cell/block (or already outside the AABB),
+// so every skipped point lies in empty space or outside the volume and the result
+// equals testing the points one by one.
 enum LatticeStep : int { LATTICE_OCCUPIED = 0, LATTICE_SKIPPED = 1, LATTICE_EXIT = 2 };
 // One step of the march at lattice point *n_io: occupied (left unchanged), exited the
 // AABB, or skipped (moved to the next candidate point).  Kept as a single step so a
@@ -426,7 +428,7 @@ NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, co
 			shift = 6;
 			if (!summary_bit(sm, OCC_SUMMARY_B, cell >> 9)) {
 				shift = 9;
-				if (!summary_bit(sm, OCC_SUMMARY_C, cell >> 15)) shift = 15;
+				if (!summary_c(sm, cell >> 15)) shift = 15;
 			}
 		}
 	}
@@ -434,8 +436,10 @@ NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, co
 	const float n_far = step_to(st, t + distance_to_next_cell(pos, d, idir, mip + shift / 3u));
 	float nn = n + ceilf(fmaxf(n_far - n, 0.5f));
 	if (nn - n > 1.0f) {
+		// the jump stands if the point before the landing point is still in the skipped
+		// cell/block, or already outside the AABB (the ray leaves the volume inside the block)
 		const v3 last = o + d * step_from(st, nn - 1.0f);
-		if ((cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
+		if (aabb_contains(aabb, last) && (cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
 	}
 	*n_io = nn;
 	return LATTICE_SKIPPED;

@@ -152,22 +152,31 @@ __device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* s
 	*pp = p;
 }
 
-// Occupancy summary (ngp_math.h OCC_SUMMARY_*): one thread per 64-bit bitfield word
-// (4^3 block); a wave covers 64 consecutive words = eight 8^3 blocks, so levels A and B
-// come from one ballot; level C (32^3 = 8 waves) is OR-ed in with an atomic.
-__global__ void __launch_bounds__(256) k_occupancy_summary(const uint8_t* __restrict__ bitfield, uint8_t* __restrict__ summary) {
-	const uint32_t g = blockIdx.x * 256u + threadIdx.x;  // [mip][32768 words]
-	const uint32_t mip = g >> 15, wi = g & 32767u;
-	const uint64_t w = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8))[wi];
-	const unsigned long long a = __ballot(w != 0ull);
+// Occupancy summary (ngp_math.h OCC_SUMMARY_*): one workgroup of 512 threads per 32^3
+// block = 512 bitfield words; a wave's 64 words are eight 8^3 blocks, so levels A and B
+// come from one ballot and level C from the eight waves' ballots in LDS.  Block 0 also
+// zeroes the tracer's counters (this kernel runs first in every render).
+__global__ void __launch_bounds__(512) k_occupancy_summary(const uint8_t* __restrict__ bitfield, uint8_t* __restrict__ summary,
+                                                           uint32_t* __restrict__ counters) {
+	__shared__ uint32_t any_wave[8];
+	const uint32_t g = blockIdx.x * 512u + threadIdx.x;  // [mip][32768 words]
+	const uint32_t mip = g >> 15, wi = g & 32767u, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	if (g < 4) counters[g] = 0;
+	const uint64_t word = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8))[wi];
+	const unsigned long long a = __ballot(word != 0ull);
 	uint8_t* sm = summary + (size_t)OCC_SUMMARY_BYTES * mip;
-	if ((threadIdx.x & 63u) == 0) {
+	if (lane == 0) {
 		*reinterpret_cast<unsigned long long*>(sm + OCC_SUMMARY_A + (wi >> 3)) = a;
 		uint8_t b = 0;
 		for (uint32_t k = 0; k < 8; ++k) b |= ((a >> (8 * k)) & 0xffull) ? (uint8_t)(1u << k) : (uint8_t)0;
 		sm[OCC_SUMMARY_B + (wi >> 6)] = b;
-		const uint32_t c = wi >> 9;  // 32^3 block
-		if (a) atomicOr(reinterpret_cast<uint32_t*>(sm + OCC_SUMMARY_C) + (c >> 5), 1u << (c & 31u));
+		any_wave[w] = a != 0ull;
+	}
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint32_t c = 0;
+		for (uint32_t k = 0; k < 8; ++k) c |= any_wave[k];
+		sm[OCC_SUMMARY_C + (wi >> 9)] = (uint8_t)c;
 	}
 }
 
@@ -177,7 +186,8 @@ __global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __re
                                                  const float* __restrict__ sdepth, Payload* __restrict__ dp,
                                                  float4* __restrict__ drgba, float* __restrict__ ddepth,
                                                  Payload* __restrict__ hp, float4* __restrict__ hrgba,
-                                                 float* __restrict__ hdepth, uint32_t* __restrict__ counters) {
+                                                 float* __restrict__ hdepth, uint32_t* __restrict__ alive_counter,
+                                                 uint32_t* __restrict__ hit_counter) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	bool alive = false, hit = false;
 	Payload p;
@@ -191,7 +201,7 @@ __global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __re
 		hit = !alive && c.w > 0.001f;
 	}
 	uint32_t oa, oh;
-	block_append2(alive, hit, &counters[0], &counters[1], &oa, &oh);
+	block_append2(alive, hit, alive_counter, hit_counter, &oa, &oh);
 	if (alive) {
 		dp[oa] = p;
 		drgba[oa] = c;
@@ -212,7 +222,7 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 	bool hit = false;
 	if (i < n) hit = srgba[i].w > 0.001f;
 	uint32_t oh, unused;
-	block_append2(hit, false, &counters[1], &counters[3], &oh, &unused);
+	block_append2(hit, false, &counters[2], &counters[3], &oh, &unused);
 	if (hit) {
 		hp[oh] = sp[i];
 		hrgba[oh] = srgba[i];
@@ -221,7 +231,9 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 }
 
 __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
-                                                  float* __restrict__ coords, uint32_t n_steps) {
+                                                  float* __restrict__ coords, uint32_t n_steps,
+                                                  uint32_t* __restrict__ next_alive_counter) {
+	if (blockIdx.x == 0 && threadIdx.x == 0) *next_alive_counter = 0;  // filled by this pass's k_compact
 	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= n_alive) return;
@@ -438,11 +450,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
-	for (uint32_t mip = 0; mip < NERF_CASCADES; ++mip)
-		NGP_HIP_CHECK(hipMemsetAsync(rs.summary.ptr + (OCC_SUMMARY_BYTES * mip + OCC_SUMMARY_C) / 4, 0, 8, s));
-	k_occupancy_summary<<<NERF_CASCADES * 32768 / 256, 256, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr));
+	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
+	                                                                rs.counters.ptr);
 	const size_t lds = (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
-	NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, 4 * sizeof(uint32_t), s));
 	k_render_init<<<div_up(n, 256), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
 	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
@@ -456,6 +466,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
 	int cur = 0;
+	uint32_t pass = 0, n_hit = 0;
 	const uint32_t MARCH_ITER = 10000;
 	for (uint32_t it = 1; it < MARCH_ITER && n_alive > 0;) {
 		const uint32_t target = 2 * 1024 * 1024;
@@ -463,7 +474,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// every ray composites its own samples in order and stops at the same one whatever the chunking
 		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), max_steps_per_pass());
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_generate<<<div_up(n_alive, 256), 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps);
+		// alive counters alternate between counters[0] and [1]: the host has already read the
+		// one this pass overwrites; counters[2] accumulates the finished rays with colour
+		uint32_t* alive_out = rs.counters.ptr + (pass + 1) % 2;
+		k_generate<<<div_up(n_alive, 256), 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
@@ -475,26 +489,27 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, it, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
 		                                                 rs.out.ptr, n_steps);
-		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
 		k_compact<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(1 - cur), C(1 - cur),
-		                                               rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr, rs.counters.ptr);
+		                                               rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr, alive_out,
+		                                               rs.counters.ptr + 2);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
-		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 		NGP_HIP_CHECK(hipStreamSynchronize(s));
-		n_alive = rs.host_counter.ptr[0];
+		n_alive = rs.host_counter.ptr[(pass + 1) % 2];
+		n_hit = rs.host_counter.ptr[2];
 		cur = 1 - cur;
 		it += n_steps;
+		++pass;
 	}
 	if (n_alive > 0) {
 		// march budget exhausted: still-alive rays are shaded with what they accumulated
-		NGP_HIP_CHECK(hipMemsetAsync(rs.counters.ptr, 0, sizeof(uint32_t), s));
 		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,
 		                                              rs.counters.ptr);
+		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		n_hit = rs.host_counter.ptr[2];
 	}
-	NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-	NGP_HIP_CHECK(hipStreamSynchronize(s));
-	const uint32_t n_hit = rs.host_counter.ptr[1];
 	if (n_hit)
 		k_shade<<<div_up(n_hit, 256), 256, 0, s>>>(n_hit, P(2), C(2), rs.depth[2].ptr, k.linear_colors,
 		                                           reinterpret_cast<float4*>(frame), depth_buffer);

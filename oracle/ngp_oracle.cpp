@@ -333,7 +333,7 @@ static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, 
 		float nn = n + std::ceil(std::max(n_far - n, 0.5f));
 		if (nn - n > 1.0f) {
 			const V3 last = o + d * lat_from(st, nn - 1.0f);
-			if ((grid_idx(last, mip) >> shift) != (cell >> shift)) nn = n + 1.0f;
+			if (b.contains(last) && (grid_idx(last, mip) >> shift) != (cell >> shift)) nn = n + 1.0f;
 		}
 		n = nn;
 	}

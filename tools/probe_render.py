@@ -26,7 +26,7 @@ for i in range(int(sys.argv[1]) if len(sys.argv) > 1 else 500):
     tb.train(1 << 18)
 lib = A.load()
 h = C.c_void_p(tb.model_handle)
-A.check(lib.ngp_timing_enable(h, -1))
+A.check(lib.ngp_timing_enable(h, int(os.environ.get("TIMER_MASK", "-1"))))
 tb.set_camera_to_training_view(3)
 for cap in (1, 4, 8, 16, 32, 64, 128):
     os.environ["NGP_RENDER_STEPS_PER_PASS"] = str(cap)
