@@ -230,42 +230,79 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 	}
 }
 
+// generate_next_nerf_network_inputs (testbed_nerf.cu:421-469): the next n_steps samples
+// of every alive ray.  G lanes cooperate on one ray: each iteration they test G
+// consecutive lattice points at once (ballots give the occupied ones in order and the
+// first exit), and an all-empty round jumps on from the last lane's verified skip.
+// G = 1 for the big early passes (one lane per ray, flat loop), up to 64 for the last
+// few thousand rays, whose long serial marches otherwise dominate the tail passes.
+template <uint32_t G>
 __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
                                                   float* __restrict__ coords, uint32_t n_steps,
                                                   uint32_t* __restrict__ next_alive_counter) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) *next_alive_counter = 0;  // filled by this pass's k_compact
 	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	if (i >= n_alive) return;
-	Payload& p = payloads[i];
-	if (!p.alive) return;
-	const v3 o = mk3(p.o[0], p.o[1], p.o[2]), d = mk3(p.d[0], p.d[1], p.d[2]);
-	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-	const v3 wdir = warp_direction(d);
-	float n = p.n;
+	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
+	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
+	const uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G;
+	Payload* p = payloads + (i < n_alive ? i : 0);
+	bool running = i < n_alive && p->alive;  // group-uniform
+	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f), wdir = mk3(0.0f);
+	float n = 0.0f;
+	if (running) {
+		o = mk3(p->o[0], p->o[1], p->o[2]);
+		d = mk3(p->d[0], p->d[1], p->d[2]);
+		idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		wdir = warp_direction(d);
+		n = p->n;
+	}
 	OccCache occ = occ_cache_init();
-	// one flat loop: every iteration either emits a sample or skips, per lane, so lanes
-	// that are skipping empty space never hold up lanes that are sampling (and vice versa)
 	uint32_t j = 0;
-	while (j < n_steps) {
-		const int r = lattice_step(&n, k.st, o, d, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
-		if (r == LATTICE_EXIT) {
-			p.n_steps = j;
-			return;
+	bool exited = false;
+	while (__ballot(running) != 0ull) {
+		float nr = n + (float)r;
+		int st = LATTICE_EXIT;
+		if (running) st = lattice_step(&nr, k.st, o, d, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
+		const unsigned long long m_exit = __ballot(running && st == LATTICE_EXIT) & gmask;
+		const unsigned long long m_occ = __ballot(running && st == LATTICE_OCCUPIED) & gmask;
+		const float n_last = __shfl(st == LATTICE_SKIPPED ? nr : n + (float)G, g0 + G - 1, 64);
+		if (!running) continue;
+		const uint32_t fe = m_exit ? (uint32_t)(__ffsll((long long)m_exit) - 1) : 64u;
+		const unsigned long long emit = m_occ & (fe >= 64 ? ~0ull : ((1ull << fe) - 1ull));
+		const uint32_t cnt = __popcll(emit), room = n_steps - j;
+		if ((emit >> lane) & 1ull) {
+			const uint32_t rank = __popcll(emit & ((1ull << lane) - 1ull));
+			if (rank < room) {
+				const float pn = n + (float)r;
+				const float t = step_from(k.st, pn);
+				const float dt = step_from(k.st, pn + 1.0f) - t;
+				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
+				float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)(j + rank) * n_alive));
+				c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+				c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+			}
 		}
-		if (r == LATTICE_OCCUPIED) {
-			const float t = step_from(k.st, n);
-			const float dt = step_from(k.st, n + 1.0f) - t;
-			const v3 wp = aabb_relative(k.train_aabb, o + d * t);
-			float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)j * n_alive));
-			c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-			c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
-			n += 1.0f;
-			++j;
+		if (cnt >= room) {
+			unsigned long long m = emit;  // the room-th emitted lane carries the last sample
+			for (uint32_t t = 1; t < room; ++t) m &= m - 1ull;
+			n += (float)((uint32_t)(__ffsll((long long)m) - 1) - g0 + 1u);
+			j = n_steps;
+			running = false;
+		} else {
+			j += cnt;
+			if (m_exit) {
+				exited = true;
+				running = false;
+			} else {
+				n = n_last;
+			}
 		}
 	}
-	p.n = n;
-	p.n_steps = n_steps;
+	if (i < n_alive && p->alive && r == 0) {
+		p->n_steps = j;
+		if (!exited) p->n = n;
+	}
 }
 
 __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, uint32_t current_step,
@@ -390,6 +427,13 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 }
 
 // NGP_RENDER_STEPS_PER_PASS overrides the per-pass sample cap (tuning knob; results do not depend on it)
+// NGP_RENDER_LANES overrides the lane budget that picks lanes-per-ray in k_generate
+static uint32_t lanes_target() {
+	const char* e = getenv("NGP_RENDER_LANES");
+	const long v = e ? atol(e) : 0;
+	return v > 0 ? (uint32_t)v : 1u << 20;
+}
+
 static uint32_t max_steps_per_pass() {
 	const char* e = getenv("NGP_RENDER_STEPS_PER_PASS");
 	const int v = e ? atoi(e) : 0;
@@ -477,7 +521,16 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// alive counters alternate between counters[0] and [1]: the host has already read the
 		// one this pass overwrites; counters[2] accumulates the finished rays with colour
 		uint32_t* alive_out = rs.counters.ptr + (pass + 1) % 2;
-		k_generate<<<div_up(n_alive, 256), 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out);
+		// lanes per ray: enough rays in flight for ~64k lanes, never fewer than one lane per ray
+		const uint32_t want = lanes_target() / std::max(n_alive, 1u);
+		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
+		const uint32_t gblocks = div_up((uint64_t)n_alive * G, 256);
+		switch (G) {
+			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
+			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
+			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
+			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
+		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
