@@ -65,7 +65,7 @@ def kernel_models(cfg):
     L, F = cfg["n_levels"], cfg["F"]
     macs = mlp_macs_per_sample(cfg)
     enc_fwd_bytes = L * 8 * F * 2 + 12 + L * F * 2  # 8 corner gathers (fp16) per level + pos + encoded output
-    enc_bwd_bytes = L * 8 * F * 4 * 2 + 12 + L * F * 2  # fp32 atomic RMW per corner + pos + dL/denc
+    enc_bwd_bytes = L * 8 * F * 2 * 2 + 12 + L * F * 2  # fp16 packed atomic RMW per corner + pos + dL/denc
     return {
         "train_encode": ("hbm", enc_fwd_bytes),
         "render_encode": ("hbm", enc_fwd_bytes),

@@ -4,6 +4,7 @@
 #include <map>
 #include <memory>
 #include <stdexcept>
+#include <cstdint>
 #include <string>
 #include <vector>
 
@@ -11,7 +12,7 @@ namespace ngp {
 
 class Json {
 public:
-	enum Type { Null, Bool, Number, String, Array, Object };
+	enum Type { Null, Bool, Number, String, Array, Object, Binary };
 
 	Json() = default;
 	Json(bool b) : m_type(Bool), m_bool(b) {}
@@ -22,6 +23,7 @@ public:
 	Json(std::string s) : m_type(String), m_str(std::move(s)) {}
 
 	static Json array() { Json j; j.m_type = Array; return j; }
+	static Json binary(std::vector<uint8_t> bytes) { Json j; j.m_type = Binary; j.m_bin = std::move(bytes); return j; }
 	static Json object() { Json j; j.m_type = Object; return j; }
 	static Json parse(const std::string& text);
 
@@ -32,6 +34,8 @@ public:
 	bool is_number() const { return m_type == Number; }
 	bool is_string() const { return m_type == String; }
 	bool is_bool() const { return m_type == Bool; }
+	bool is_binary() const { return m_type == Binary; }
+	const std::vector<uint8_t>& bin() const;
 
 	double num() const;
 	bool boolean() const;
@@ -44,6 +48,7 @@ public:
 	const Json& operator[](size_t i) const;
 	const Json& operator[](int i) const { return (*this)[(size_t)i]; }
 	void push_back(Json v);
+	void erase(const std::string& k) { m_obj.erase(k); }
 	const std::map<std::string, Json>& items() const { return m_obj; }
 	const std::vector<Json>& elements() const { return m_arr; }
 
@@ -55,13 +60,19 @@ public:
 
 	// RFC 7386 merge patch (nlohmann::json::merge_patch), used for "parent" configs.
 	void merge_patch(const Json& patch);
-	std::string dump() const;
+	std::string dump() const;  // binary values dump as {"binary_bytes": n}
+
+	// MessagePack (nlohmann::json::to_msgpack / from_msgpack), incl. bin and ext as Binary:
+	// the container of the reference's .msgpack / .ingp snapshots (src/testbed.cu:4775-4838).
+	std::vector<uint8_t> to_msgpack() const;
+	static Json from_msgpack(const uint8_t* data, size_t size);
 
 private:
 	Type m_type = Null;
 	bool m_bool = false;
 	double m_num = 0.0;
 	std::string m_str;
+	std::vector<uint8_t> m_bin;
 	std::vector<Json> m_arr;
 	std::map<std::string, Json> m_obj;
 };

@@ -77,6 +77,46 @@ float focal_length_to_fov(float resolution, float focal) { return 2.0f * 180.0f 
 
 uint32_t next_multiple_host(uint32_t a, uint32_t b) { return (a + b - 1) / b * b; }
 
+// IEEE binary16 <-> binary32 (round to nearest even), for the snapshot's fp16 arrays
+uint16_t f32_to_f16(float f) {
+	uint32_t x;
+	std::memcpy(&x, &f, 4);
+	const uint32_t sign = (x >> 16) & 0x8000u;
+	const int32_t e = (int32_t)((x >> 23) & 0xff) - 127 + 15;
+	uint32_t mant = x & 0x7fffffu;
+	if (((x >> 23) & 0xff) == 0xff) return (uint16_t)(sign | 0x7c00u | (mant ? 0x200u : 0u));
+	if (e >= 31) return (uint16_t)(sign | 0x7c00u);
+	if (e <= 0) {
+		if (e < -10) return (uint16_t)sign;
+		mant |= 0x800000u;
+		const uint32_t shift = (uint32_t)(14 - e);
+		uint32_t h = mant >> shift;
+		const uint32_t rem = mant & ((1u << shift) - 1u), half = 1u << (shift - 1);
+		if (rem > half || (rem == half && (h & 1u))) ++h;
+		return (uint16_t)(sign | h);
+	}
+	uint32_t h = ((uint32_t)e << 10) | (mant >> 13);
+	const uint32_t rem = mant & 0x1fffu;
+	if (rem > 0x1000u || (rem == 0x1000u && (h & 1u))) ++h;
+	return (uint16_t)(sign | h);
+}
+float f16_to_f32(uint16_t h) {
+	const uint32_t sign = (uint32_t)(h & 0x8000u) << 16;
+	uint32_t e = (h >> 10) & 0x1fu, m = h & 0x3ffu, x;
+	if (e == 0) {
+		if (m == 0) x = sign;
+		else {
+			e = 127 - 15 + 1;
+			while (!(m & 0x400u)) { m <<= 1; --e; }
+			x = sign | (e << 23) | ((m & 0x3ffu) << 13);
+		}
+	} else if (e == 31) x = sign | 0x7f800000u | (m << 13);
+	else x = sign | ((e + 127 - 15) << 23) | (m << 13);
+	float f;
+	std::memcpy(&f, &x, 4);
+	return f;
+}
+
 float srgb_to_linear_h(float s) { return s <= 0.04045f ? s / 12.92f : std::pow((s + 0.055f) / 1.055f, 2.4f); }
 float linear_to_srgb_h(float l) { return l < 0.0031308f ? 12.92f * l : 1.055f * std::pow(l, 0.41666f) - 0.055f; }
 
@@ -178,7 +218,7 @@ void Testbed::sync() const { hk(hipStreamSynchronize((hipStream_t)m_stream), "hi
 // ---------------------------------------------------------------------------
 void Testbed::load_file(const std::string& path) {
 	const std::string ext = extension(path);
-	if (ext == "ingp" || ext == "msgpack" || ext == "ngpmi") {
+	if (ext == "ingp" || ext == "msgpack") {
 		load_snapshot(path);
 		return;
 	}
@@ -943,120 +983,175 @@ std::vector<uint8_t> Testbed::density_grid_bitfield() const {
 }
 
 // ---------------------------------------------------------------------------
-// Snapshots: versioned binary container (header JSON + params [+ optimizer] + grid), zlib'd.
+// Snapshots (Testbed::save_snapshot / load_snapshot, src/testbed.cu:4772-4978): the network
+// config with a "snapshot" object, as MessagePack; zlib-compressed for ".ingp".  Keys the
+// reference reads are written in its layout (tcnn Trainer::serialize: n_params,
+// params_type "__half", params_binary = inference params; density_grid_binary fp16;
+// nerf.aabb_scale / rgb counters; training_step, loss, camera ...).  The exact fp32
+// master / EMA weights and the Adam state ride along under "mi355x" so a resumed run
+// continues bit for bit; a reader that does not know the key ignores it.
 // ---------------------------------------------------------------------------
-static const char SNAP_MAGIC[8] = {'N', 'G', 'P', 'M', 'I', '3', '5', '5'};
 static const uint32_t SNAPSHOT_FORMAT_VERSION = 1;
+
+static std::vector<uint8_t> device_bytes(const void* p, size_t bytes) {
+	std::vector<uint8_t> h(bytes);
+	hk(hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost), "snapshot d2h");
+	return h;
+}
+
+static std::vector<uint8_t> zlib_inflate(const std::vector<uint8_t>& in) {
+	z_stream zs{};
+	if (inflateInit(&zs) != Z_OK) throw std::runtime_error("zlib inflateInit failed");
+	std::vector<uint8_t> out;
+	std::vector<uint8_t> buf(1 << 20);
+	zs.next_in = const_cast<Bytef*>(in.data());
+	zs.avail_in = (uInt)in.size();
+	int rc = Z_OK;
+	while (rc != Z_STREAM_END) {
+		zs.next_out = buf.data();
+		zs.avail_out = (uInt)buf.size();
+		rc = inflate(&zs, Z_NO_FLUSH);
+		if (rc != Z_OK && rc != Z_STREAM_END) {
+			inflateEnd(&zs);
+			throw std::runtime_error("snapshot decompression failed");
+		}
+		out.insert(out.end(), buf.data(), buf.data() + (buf.size() - zs.avail_out));
+		if (rc == Z_OK && zs.avail_in == 0 && zs.avail_out != 0) break;
+	}
+	inflateEnd(&zs);
+	return out;
+}
+
+static Json vec_json(const float* v, int n) {
+	Json a = Json::array();
+	for (int k = 0; k < n; ++k) a.push_back(Json((double)v[k]));
+	return a;
+}
 
 void Testbed::save_snapshot(const std::string& path, bool include_optimizer_state, bool compress) {
 	if (!m_model) throw std::runtime_error("save_snapshot: no network");
 	sync();
 	ngp_model_info info{};
 	ck(ngp_model_get_info(m_model, &info));
-	auto grab = [&](int kind, size_t elem) {
+	auto buf = [&](int kind) {
 		void* p = nullptr;
 		size_t bytes = 0;
 		ck(ngp_model_buffer(m_model, kind, &p, &bytes));
-		std::vector<uint8_t> h(bytes);
-		hk(hipMemcpy(h.data(), p, bytes, hipMemcpyDeviceToHost), "snapshot d2h");
-		(void)elem;
-		return h;
+		return device_bytes(p, bytes);
 	};
-	Json hdr = Json::object();
-	hdr["version"] = Json((double)SNAPSHOT_FORMAT_VERSION);
-	hdr["network_config"] = m_network_config;
-	hdr["training_step"] = Json((double)training_step);
-	hdr["aabb_scale"] = Json((double)nerf.training.dataset.aabb_scale);
-	hdr["max_cascade"] = Json((double)nerf.max_cascade);
-	hdr["density_grid_ema_step"] = Json((double)nerf.density_grid_ema_step);
-	hdr["rgb_activation"] = Json((double)(int)nerf.rgb_activation);
-	hdr["density_activation"] = Json((double)(int)nerf.density_activation);
-	hdr["n_params"] = Json((double)info.n_params);
-	hdr["include_optimizer_state"] = Json(include_optimizer_state);
-	hdr["dataset_scale"] = Json((double)nerf.training.dataset.scale);
-	Json off = Json::array();
-	for (float o : nerf.training.dataset.offset) off.push_back(Json((double)o));
-	hdr["dataset_offset"] = off;
-	const std::string h = hdr.dump();
-	std::vector<uint8_t> blob;
-	auto put = [&](const void* p, size_t n) { const uint8_t* b = (const uint8_t*)p; blob.insert(blob.end(), b, b + n); };
-	const uint64_t hlen = h.size();
-	put(&hlen, 8);
-	put(h.data(), h.size());
-	auto params = grab(NGP_PARAMS_FP32, 4);
-	put(params.data(), params.size());
-	auto ema = grab(NGP_PARAMS_EMA_FP32, 4);
-	put(ema.data(), ema.size());
+	Json root = m_network_config;
+	Json snap = Json::object();
+	snap["n_params"] = Json((double)info.n_params);
+	snap["params_type"] = Json("__half");
+	snap["params_binary"] = Json::binary(buf(NGP_PARAMS_INFER_FP16));
+	Json exact = Json::object();
+	exact["params_fp32_binary"] = Json::binary(buf(NGP_PARAMS_FP32));
+	exact["params_ema_fp32_binary"] = Json::binary(buf(NGP_PARAMS_EMA_FP32));
+	exact["n_mlp_params"] = Json((double)info.n_mlp_params);
 	if (include_optimizer_state) {
-		auto m = grab(NGP_ADAM_M, 4);
-		put(m.data(), m.size());
-		auto v = grab(NGP_ADAM_V, 4);
-		put(v.data(), v.size());
+		exact["adam_m_binary"] = Json::binary(buf(NGP_ADAM_M));
+		exact["adam_v_binary"] = Json::binary(buf(NGP_ADAM_V));
 	}
-	auto grid = density_grid();
-	put(grid.data(), grid.size() * 4);
-	FILE* f = std::fopen(path.c_str(), "wb");
-	if (!f) throw std::runtime_error("Could not open '" + path + "' for writing.");
-	std::fwrite(SNAP_MAGIC, 1, 8, f);
-	const uint32_t flags = compress ? 1u : 0u;
-	std::fwrite(&SNAPSHOT_FORMAT_VERSION, 4, 1, f);
-	std::fwrite(&flags, 4, 1, f);
-	const uint64_t raw = blob.size();
-	std::fwrite(&raw, 8, 1, f);
-	if (compress) {
-		uLongf clen = compressBound((uLong)blob.size());
-		std::vector<uint8_t> c(clen);
-		if (compress2(c.data(), &clen, blob.data(), (uLong)blob.size(), Z_BEST_SPEED) != Z_OK) {
-			std::fclose(f);
-			throw std::runtime_error("snapshot compression failed");
+	snap["mi355x"] = exact;
+	snap["version"] = Json((double)SNAPSHOT_FORMAT_VERSION);
+	snap["mode"] = Json("Nerf");
+	snap["density_grid_size"] = Json((double)NERF_GRIDSIZE);
+	{
+		const std::vector<float> grid = density_grid();
+		std::vector<uint8_t> g16(grid.size() * 2);
+		for (size_t k = 0; k < grid.size(); ++k) {
+			const uint16_t h = f32_to_f16(grid[k]);
+			std::memcpy(&g16[2 * k], &h, 2);
 		}
-		std::fwrite(c.data(), 1, clen, f);
-	} else {
-		std::fwrite(blob.data(), 1, blob.size(), f);
+		snap["density_grid_binary"] = Json::binary(std::move(g16));
 	}
-	std::fclose(f);
+	Json nj = Json::object();
+	nj["aabb_scale"] = Json((double)nerf.training.dataset.aabb_scale);
+	Json rgb = Json::object();
+	rgb["rays_per_batch"] = Json((double)nerf.training.counters_rgb.rays_per_batch);
+	rgb["measured_batch_size"] = Json((double)nerf.training.counters_rgb.measured_batch_size);
+	rgb["measured_batch_size_before_compaction"] = Json((double)nerf.training.counters_rgb.measured_batch_size_before_compaction);
+	nj["rgb"] = rgb;
+	Json ds = Json::object();
+	ds["aabb_scale"] = Json((double)nerf.training.dataset.aabb_scale);
+	ds["scale"] = Json((double)nerf.training.dataset.scale);
+	ds["offset"] = vec_json(nerf.training.dataset.offset.data(), 3);
+	ds["up"] = vec_json(nerf.training.dataset.up.data(), 3);
+	ds["is_hdr"] = Json(nerf.training.dataset.is_hdr);
+	ds["n_images"] = Json((double)nerf.training.dataset.n_images);
+	nj["dataset"] = ds;
+	nj["rgb_activation"] = Json((double)(int)nerf.rgb_activation);
+	nj["density_activation"] = Json((double)(int)nerf.density_activation);
+	nj["density_grid_ema_step"] = Json((double)nerf.density_grid_ema_step);
+	snap["nerf"] = nj;
+	snap["training_step"] = Json((double)training_step);
+	snap["loss"] = Json((double)loss);
+	Json aabb = Json::object();
+	aabb["min"] = vec_json(aabb_min.data(), 3);
+	aabb["max"] = vec_json(aabb_max.data(), 3);
+	snap["aabb"] = aabb;
+	snap["exposure"] = Json((double)exposure);
+	snap["background_color"] = vec_json(background_color.data(), 4);
+	Json cam = Json::object();
+	Json mat = Json::array();
+	for (int c = 0; c < 4; ++c) mat.push_back(vec_json(&camera.m[3 * c], 3));  // 4 columns of 3 (mat4x3)
+	cam["matrix"] = mat;
+	cam["fov_axis"] = Json((double)fov_axis);
+	cam["relative_focal_length"] = vec_json(relative_focal_length.data(), 2);
+	cam["screen_center"] = vec_json(screen_center.data(), 2);
+	cam["zoom"] = Json((double)zoom);
+	cam["scale"] = Json((double)scale);
+	snap["camera"] = cam;
+	root["snapshot"] = snap;
+
+	std::vector<uint8_t> bytes = root.to_msgpack();
+	if (extension(path) == "ingp") {
+		uLongf clen = compressBound((uLong)bytes.size());
+		std::vector<uint8_t> c(clen);
+		if (compress2(c.data(), &clen, bytes.data(), (uLong)bytes.size(), compress ? Z_DEFAULT_COMPRESSION : Z_NO_COMPRESSION) != Z_OK)
+			throw std::runtime_error("snapshot compression failed");
+		c.resize(clen);
+		bytes.swap(c);
+	}
+	std::ofstream f(path, std::ios::binary);
+	if (!f) throw std::runtime_error("Could not open '" + path + "' for writing.");
+	f.write(reinterpret_cast<const char*>(bytes.data()), (std::streamsize)bytes.size());
 }
 
-void Testbed::load_snapshot(const std::string& path) {
+Json Testbed::read_snapshot_file(const std::string& path) {
 	std::ifstream f(path, std::ios::binary);
 	if (!f) throw std::runtime_error("Snapshot '" + path + "' does not exist.");
 	std::vector<uint8_t> file((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
-	if (file.size() < 24 || std::memcmp(file.data(), SNAP_MAGIC, 8) != 0)
-		throw std::runtime_error("'" + path + "' is not an MI355X NGP snapshot (the CUDA .ingp/msgpack reader is not implemented yet).");
-	uint32_t version, flags;
-	uint64_t raw;
-	std::memcpy(&version, &file[8], 4);
-	std::memcpy(&flags, &file[12], 4);
-	std::memcpy(&raw, &file[16], 8);
-	if (version != SNAPSHOT_FORMAT_VERSION) throw std::runtime_error("Unsupported snapshot version " + std::to_string(version));
-	std::vector<uint8_t> blob(raw);
-	if (flags & 1u) {
-		uLongf len = (uLongf)raw;
-		if (uncompress(blob.data(), &len, file.data() + 24, (uLong)(file.size() - 24)) != Z_OK || len != raw)
-			throw std::runtime_error("snapshot decompression failed");
-	} else {
-		std::memcpy(blob.data(), file.data() + 24, raw);
+	// zstr auto-detection: a zlib stream starts with 0x78 (CMF deflate/32K window); raw msgpack of
+	// a config object starts with a map marker (0x8X / 0xde / 0xdf)
+	if (file.size() >= 2 && file[0] == 0x78 && ((file[0] << 8) | file[1]) % 31 == 0) file = zlib_inflate(file);
+	return Json::from_msgpack(file.data(), file.size());
+}
+
+void Testbed::load_snapshot(const std::string& path) {
+	Json root = read_snapshot_file(path);
+	if (!root.contains("snapshot")) throw std::runtime_error("File '" + path + "' does not contain a snapshot.");
+	const Json snap = root["snapshot"];
+	if (snap.value("version", 0.0) < (double)SNAPSHOT_FORMAT_VERSION)
+		throw std::runtime_error("Snapshot uses an old format and can not be loaded.");
+	if (snap.contains("mode") && snap["mode"].str() != "Nerf")
+		throw std::runtime_error("Only NeRF snapshots are supported by this build (mode '" + snap["mode"].str() + "').");
+	if ((uint32_t)snap.value("density_grid_size", (double)NERF_GRIDSIZE) != NERF_GRIDSIZE)
+		throw std::runtime_error("Incompatible grid size.");
+	if (mode != ETestbedMode::Nerf) {
+		nerf = Nerf{};
+		mode = ETestbedMode::Nerf;
 	}
-	size_t pos = 0;
-	auto take = [&](void* dst, size_t n) {
-		if (pos + n > blob.size()) throw std::runtime_error("truncated snapshot");
-		std::memcpy(dst, &blob[pos], n);
-		pos += n;
-	};
-	uint64_t hlen;
-	take(&hlen, 8);
-	std::string h(hlen, '\0');
-	take(&h[0], hlen);
-	const Json hdr = Json::parse(h);
-	mode = ETestbedMode::Nerf;
-	nerf.training.dataset.aabb_scale = (int)hdr["aabb_scale"].num();
-	nerf.training.dataset.scale = (float)hdr.value("dataset_scale", 0.33);
-	if (hdr.contains("dataset_offset"))
-		for (int k = 0; k < 3; ++k) nerf.training.dataset.offset[k] = (float)hdr["dataset_offset"][k].num();
-	nerf.rgb_activation = (ENerfActivation)(int)hdr["rgb_activation"].num();
-	nerf.density_activation = (ENerfActivation)(int)hdr["density_activation"].num();
-	{
-		// aabb / cascades as load_nerf_post would set them
+	const Json& nj = snap["nerf"];
+	if (nj.contains("aabb_scale")) nerf.training.dataset.aabb_scale = (int)nj["aabb_scale"].num();
+	if (!training_data_available && nj.contains("dataset")) {
+		const Json& ds = nj["dataset"];
+		nerf.training.dataset.scale = (float)ds.value("scale", 0.33);
+		if (ds.contains("offset"))
+			for (int k = 0; k < 3; ++k) nerf.training.dataset.offset[k] = (float)ds["offset"][k].num();
+		nerf.training.dataset.is_hdr = ds.value("is_hdr", false);
+	}
+	{  // load_nerf_post: aabb, cascades, cone angle, activations
 		const int s = nerf.training.dataset.aabb_scale;
 		const float half = 0.5f * (float)std::min(128, s);
 		aabb_min = {0.5f - half, 0.5f - half, 0.5f - half};
@@ -1064,42 +1159,110 @@ void Testbed::load_snapshot(const std::string& path) {
 		nerf.max_cascade = 0;
 		while ((1 << nerf.max_cascade) < s) ++nerf.max_cascade;
 		nerf.cone_angle_constant = s <= 1 ? 0.0f : (1.0f / 256.0f);
+		nerf.rgb_activation = nerf.training.dataset.is_hdr ? ENerfActivation::Exponential : ENerfActivation::Logistic;
 	}
-	m_network_config = hdr["network_config"];
+	if (nj.contains("rgb_activation")) nerf.rgb_activation = (ENerfActivation)(int)nj["rgb_activation"].num();
+	if (nj.contains("density_activation")) nerf.density_activation = (ENerfActivation)(int)nj["density_activation"].num();
+	if (nj.contains("rgb")) {
+		nerf.training.counters_rgb.rays_per_batch = (uint32_t)nj["rgb"].value("rays_per_batch", 4096.0);
+		nerf.training.counters_rgb.measured_batch_size = (uint32_t)nj["rgb"].value("measured_batch_size", 0.0);
+		nerf.training.counters_rgb.measured_batch_size_before_compaction =
+		    (uint32_t)nj["rgb"].value("measured_batch_size_before_compaction", 0.0);
+	}
+	exposure = (float)snap.value("exposure", (double)exposure);
+	if (snap.contains("background_color"))
+		for (int k = 0; k < 4; ++k) background_color[k] = (float)snap["background_color"][k].num();
+	if (snap.contains("camera")) {
+		const Json& cam = snap["camera"];
+		if (cam.contains("matrix") && cam["matrix"].size() == 4)
+			for (int c = 0; c < 4; ++c)
+				for (int r = 0; r < 3; ++r) camera.m[3 * c + r] = (float)cam["matrix"][c][r].num();
+		fov_axis = (uint32_t)cam.value("fov_axis", (double)fov_axis);
+		if (cam.contains("relative_focal_length"))
+			for (int k = 0; k < 2; ++k) relative_focal_length[k] = (float)cam["relative_focal_length"][k].num();
+		if (cam.contains("screen_center"))
+			for (int k = 0; k < 2; ++k) screen_center[k] = (float)cam["screen_center"][k].num();
+		zoom = (float)cam.value("zoom", (double)zoom);
+		scale = (float)cam.value("scale", (double)scale);
+	}
+
+	const uint32_t saved_step = (uint32_t)snap.value("training_step", 0.0);
+	const float saved_loss = (float)snap.value("loss", 0.0);
+	const uint32_t saved_counters_rpb = nerf.training.counters_rgb.rays_per_batch;
+	const NerfCounters saved_counters = nerf.training.counters_rgb;
+	root.erase("snapshot");
+	m_network_config = root;
 	reset_network(false);
-	const size_t n_params = (size_t)hdr["n_params"].num();
+	nerf.training.counters_rgb = saved_counters;
+	nerf.training.counters_rgb.rays_per_batch = saved_counters_rpb;
+
 	ngp_model_info info{};
 	ck(ngp_model_get_info(m_model, &info));
-	if (info.n_params != n_params) throw std::runtime_error("snapshot parameter count does not match its network config");
-	auto put_buf = [&](int kind) {
+	auto upload = [&](int kind, const std::vector<uint8_t>& src) {
 		void* p = nullptr;
 		size_t bytes = 0;
 		ck(ngp_model_buffer(m_model, kind, &p, &bytes));
-		std::vector<uint8_t> tmp(bytes);
-		take(tmp.data(), bytes);
-		hk(hipMemcpy(p, tmp.data(), bytes, hipMemcpyHostToDevice), "snapshot h2d");
+		if (src.size() != bytes) throw std::runtime_error("snapshot buffer size does not match its network config");
+		hk(hipMemcpy(p, src.data(), bytes, hipMemcpyHostToDevice), "snapshot h2d");
 	};
-	put_buf(NGP_PARAMS_FP32);
-	ck(ngp_model_params_updated(m_model, 1, m_stream));
-	sync();
-	put_buf(NGP_PARAMS_EMA_FP32);
-	if (hdr.value("include_optimizer_state", false)) {
-		put_buf(NGP_ADAM_M);
-		put_buf(NGP_ADAM_V);
+	const Json& exact = snap["mi355x"];
+	if (exact.contains("params_fp32_binary")) {
+		upload(NGP_PARAMS_FP32, exact["params_fp32_binary"].bin());
+		ck(ngp_model_params_updated(m_model, 1, m_stream));
+		sync();
+		upload(NGP_PARAMS_EMA_FP32, exact["params_ema_fp32_binary"].bin());
+		if (exact.contains("adam_m_binary")) {
+			upload(NGP_ADAM_M, exact["adam_m_binary"].bin());
+			upload(NGP_ADAM_V, exact["adam_v_binary"].bin());
+		}
+		ck(ngp_model_params_updated(m_model, 0, m_stream));
+	} else {
+		// tcnn Trainer::deserialize: params_binary in params_type precision -> full-precision params
+		const std::string type = snap.value("params_type", std::string("__half"));
+		const std::vector<uint8_t>& b = snap["params_binary"].bin();
+		std::vector<float> p32(info.n_params);
+		if (type == "float") {
+			if (b.size() != p32.size() * 4) throw std::runtime_error("snapshot params_binary has the wrong size");
+			std::memcpy(p32.data(), b.data(), b.size());
+		} else if (type == "__half") {
+			if (b.size() != p32.size() * 2) throw std::runtime_error("snapshot params_binary has the wrong size");
+			for (size_t k = 0; k < p32.size(); ++k) {
+				uint16_t h;
+				std::memcpy(&h, &b[2 * k], 2);
+				p32[k] = f16_to_f32(h);
+			}
+		} else {
+			throw std::runtime_error("unsupported snapshot params_type '" + type + "'");
+		}
+		std::vector<uint8_t> raw(p32.size() * 4);
+		std::memcpy(raw.data(), p32.data(), raw.size());
+		upload(NGP_PARAMS_FP32, raw);
+		ck(ngp_model_params_updated(m_model, 1, m_stream));
 	}
-	ck(ngp_model_params_updated(m_model, 0, m_stream));
-	std::vector<float> grid((size_t)NERF_GRID_N_CELLS * (nerf.max_cascade + 1));
-	take(grid.data(), grid.size() * 4);
-	// grid buffer is sized by the first bitfield pass
-	ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));
 	sync();
-	float* dg = nullptr;
-	ck(ngp_density_grid_buffers(m_model, &dg, nullptr, nullptr, nullptr));
-	hk(hipMemcpy(dg, grid.data(), grid.size() * 4, hipMemcpyHostToDevice), "grid h2d");
-	ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));
-	sync();
-	training_step = (uint32_t)hdr["training_step"].num();
-	nerf.density_grid_ema_step = (uint32_t)hdr.value("density_grid_ema_step", 0.0);
+
+	const std::vector<uint8_t>& g16 = snap["density_grid_binary"].bin();
+	const size_t n_cells = (size_t)NERF_GRID_N_CELLS * (nerf.max_cascade + 1);
+	if (!g16.empty()) {
+		if (g16.size() != n_cells * 2) throw std::runtime_error("Incompatible number of grid cascades.");
+		std::vector<float> grid(n_cells);
+		for (size_t k = 0; k < n_cells; ++k) {
+			uint16_t h;
+			std::memcpy(&h, &g16[2 * k], 2);
+			grid[k] = f16_to_f32(h);
+		}
+		ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));  // sizes the grid buffers
+		sync();
+		float* dg = nullptr;
+		ck(ngp_density_grid_buffers(m_model, &dg, nullptr, nullptr, nullptr));
+		hk(hipMemcpy(dg, grid.data(), grid.size() * 4, hipMemcpyHostToDevice), "grid h2d");
+		ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));
+		sync();
+	}
+	training_step = saved_step;
+	loss = saved_loss;
+	nerf.density_grid_ema_step = (uint32_t)nj.value("density_grid_ema_step", 0.0);
+	network_config_path = path;
 }
 
 // ---------------------------------------------------------------------------

@@ -145,6 +145,7 @@ public:
 	// --- snapshots (save_snapshot src/testbed.cu:4775, load_snapshot :4841) ---
 	void save_snapshot(const std::string& path, bool include_optimizer_state = false, bool compress = true);
 	void load_snapshot(const std::string& path);
+	static Json read_snapshot_file(const std::string& path);  // msgpack, zlib-inflated if compressed
 
 	// --- multi-GPU: one Testbed per rank, gradients all-reduced over RCCL/xGMI ---
 	void init_distributed(int rank, int world_size, const std::string& nccl_unique_id);

@@ -86,6 +86,42 @@ def test_train_render_snapshot(scene, tmp_path):
     assert tb2.training_step == 300
     np.testing.assert_array_equal(tb.density_grid_bitfield(), tb2.density_grid_bitfield())
 
+    # the file is the reference's layout (src/testbed.cu:4772-4830): zlib(msgpack(config + "snapshot"))
+    import msgpack
+    import zlib
+    with open(snap, "rb") as f:
+        root_obj = msgpack.unpackb(zlib.decompress(f.read()), raw=False, strict_map_key=False)
+    sn = root_obj["snapshot"]
+    assert root_obj["encoding"]["n_levels"] == 4 and "network" in root_obj
+    assert sn["params_type"] == "__half" and sn["n_params"] == tb.n_params()
+    assert len(sn["params_binary"]) == 2 * tb.n_params()
+    assert len(sn["density_grid_binary"]) == 2 * 128 ** 3 and sn["density_grid_size"] == 128
+    assert sn["nerf"]["aabb_scale"] == 1 and sn["training_step"] == 300 and sn["version"] >= 1
+
+    # a snapshot with only the reference's keys (fp16 params, no exact-state extension), uncompressed
+    del sn["mi355x"]
+    plain = str(tmp_path / "model_plain.msgpack")
+    with open(plain, "wb") as f:
+        f.write(msgpack.packb(root_obj, use_bin_type=True))
+    ngp3, tb3 = new_testbed()
+    tb3.load_snapshot(plain)
+    tb3.background_color = [0.0, 0.0, 0.0, 1.0]
+    tb3.camera_matrix = tb.camera_matrix
+    tb3.relative_focal_length = tb.relative_focal_length
+    tb3.screen_center = tb.screen_center
+    np.testing.assert_array_equal(img, tb3.render(64, 64, 2, True))
+
+    # optimizer state included; the resumed testbed keeps training
+    snap_opt = str(tmp_path / "model_opt.msgpack")
+    tb.save_snapshot(snap_opt, True)
+    ngp4, tb4 = new_testbed()
+    tb4.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb4.load_snapshot(snap_opt)
+    tb4.shall_train = True
+    while tb4.training_step < 340:
+        tb4.frame()
+    assert np.isfinite(tb4.loss) and tb4.loss < 2 * np.mean(losses[-4:])
+
 
 def test_network_config_parent_merge(tmp_path):
     ngp, tb = new_testbed()
