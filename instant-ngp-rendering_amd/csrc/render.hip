@@ -42,6 +42,7 @@ struct RenderK {
 	int rgb_act, density_act;
 	uint32_t shard_index, shard_count, shard_rows;
 	uint32_t n_local;
+	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
 	const uint8_t* bitfield;
 	const uint8_t* summary;
 };
@@ -61,8 +62,8 @@ __device__ __forceinline__ const uint8_t* stage_summary(const uint8_t* __restric
 	return reinterpret_cast<const uint8_t*>(s_summary);
 }
 
-__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t r, Payload* pp,
-                                              float4* __restrict__ frame, float* __restrict__ depth_buffer);
+__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
+                                              Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer);
 
 // Stream compaction slot for a 256-thread block: ballot per wave, LDS prefix over the four
 // waves, ONE global atomic per block and flag (instead of one per wave).  Returns the
@@ -99,10 +100,13 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
                                                      float* __restrict__ depth, float4* __restrict__ frame,
                                                      float* __restrict__ depth_buffer, uint32_t* __restrict__ counters) {
 	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
+	// rays are numbered in 8x8 pixel tiles: a wave's 64 rays are a square patch, so at a
+	// given step their samples are close in space (hash-grid gathers share cache lines)
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t tile = r >> 6, x = (tile % k.tiles_x) * 8u + (r & 7u), yl = (tile / k.tiles_x) * 8u + ((r >> 3) & 7u);
 	Payload p;
 	p.alive = 0;
-	if (r < k.n_local) init_ray_body(k, summary, r, &p, frame, depth_buffer);
+	if (x < k.W && yl < k.h_local) init_ray_body(k, summary, x, yl, &p, frame, depth_buffer);
 	uint32_t slot, unused;
 	block_append2(p.alive != 0, false, &counters[0], &counters[3], &slot, &unused);
 	if (p.alive) {
@@ -112,10 +116,9 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 	}
 }
 
-// init_rays_with_payload_kernel_nerf + advance_pos_nerf for local ray r
-__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t r, Payload* pp,
-                                              float4* __restrict__ frame, float* __restrict__ depth_buffer) {
-	const uint32_t x = r % k.W, yl = r / k.W;
+// init_rays_with_payload_kernel_nerf + advance_pos_nerf for pixel x of local row yl
+__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
+                                              Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer) {
 	const uint32_t y = local_to_global_row(k, yl);
 	const uint32_t idx = x + k.W * y;
 	frame[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -472,6 +475,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const uint32_t H_local = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	const uint32_t n = k.W * H_local;
 	k.n_local = n;
+	k.h_local = H_local;
+	k.tiles_x = div_up(k.W, 8u);
+	const uint32_t n_tiled = k.tiles_x * 8u * div_up(H_local, 8u) * 8u;
 	if (n == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
 
@@ -497,7 +503,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
 	                                                                rs.counters.ptr);
 	const size_t lds = (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
-	k_render_init<<<div_up(n, 256), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
+	k_render_init<<<div_up(n_tiled, 256u), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
 	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
