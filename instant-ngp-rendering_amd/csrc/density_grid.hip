@@ -239,6 +239,7 @@ void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 void run_grid_bitfield(ngp_model* m, uint32_t max_cascade, hipStream_t s) {
 	GridState& g = m->gs;
 	g.bitfield.reserve(NERF_GRID_N_CELLS / 8 * NERF_CASCADES);
+	++g.version;
 	g.mean.reserve(1);
 	g.sum.reserve(1);
 	grid_reserve(m, max_cascade + 1, 1);

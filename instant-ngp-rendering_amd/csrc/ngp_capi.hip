@@ -176,6 +176,7 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 			m->gs.mean.reserve(1);
 			m->gs.sum.reserve(1);
 			NGP_HIP_CHECK(hipMemset(m->gs.bitfield.ptr, 0xff, m->gs.bitfield.bytes()));
+			++m->gs.version;
 			NGP_HIP_CHECK(hipMemset(m->gs.mean.ptr, 0, sizeof(float)));
 			NGP_HIP_CHECK(hipDeviceSynchronize());
 		} catch (...) {
@@ -451,7 +452,10 @@ ngp_status ngp_density_grid_buffers(ngp_model* m, float** grid, uint8_t** bitfie
 	return guarded([&] {
 		require(m, "null model");
 		if (grid) *grid = m->gs.grid.ptr;
-		if (bitfield) *bitfield = m->gs.bitfield.ptr;
+		if (bitfield) {
+			*bitfield = m->gs.bitfield.ptr;
+			++m->gs.version;  // the caller may write through it
+		}
 		if (tmp) *tmp = m->gs.tmp.ptr;
 		if (mean) *mean = m->gs.mean.ptr;
 	});

@@ -156,6 +156,7 @@ struct GridState {
 	DevBuf<__half> enc;        // [L][n][F]
 	DevBuf<__half> out;        // [n]
 	uint32_t n_cascades = 0;
+	uint64_t version = 0;  // bumped whenever the bitfield may have changed (render caches derive from it)
 };
 
 struct RenderScratch {
@@ -168,6 +169,10 @@ struct RenderScratch {
 	DevBuf<uint32_t> counters;  // [4]
 	DevBuf<uint32_t> host_counter;
 	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
+	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
+	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
+	uint64_t df_version = ~0ull;
+	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;
 };
 

@@ -445,6 +445,82 @@ NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, co
 	return LATTICE_SKIPPED;
 }
 
+// Octant distance fields (render.hip k_df_*): for each mip, ray octant o (bit k set = the
+// direction's component k is negative) and cell c, D = the Chebyshev distance from c to the
+// nearest occupied cell of that mip lying in the octant's closed orthant from c (0 = c is
+// occupied).  The box of cells c + s*[0, D-1]^3 (s = the octant's signs) is then empty, and a
+// ray heading into octant o leaves it only through its far faces.  Cells beyond the grid count
+// as occupied below max_mip (the next mip takes over there) and as empty at max_mip (outside
+// the AABB).  Layout: [mip][octant][z][y][x] bytes, 255 = capped.
+constexpr uint32_t DF_BYTES_PER_FIELD = NERF_GRID_N_CELLS;
+NGP_HD uint32_t ray_octant(v3 d) { return (d.x < 0.0f ? 1u : 0u) | (d.y < 0.0f ? 2u : 0u) | (d.z < 0.0f ? 4u : 0u); }
+// integer cell coordinates of pos at `mip` (cascaded_grid_idx_at without the Morton code)
+NGP_HD bool cascaded_cell_at(v3 pos, uint32_t mip, int* ix, int* iy, int* iz) {
+	const float mip_scale = scalbnf(1.0f, -(int)mip);
+	const v3 q = (pos - 0.5f) * mip_scale + 0.5f;
+	*ix = (int)(q.x * (float)NERF_GRIDSIZE);
+	*iy = (int)(q.y * (float)NERF_GRIDSIZE);
+	*iz = (int)(q.z * (float)NERF_GRIDSIZE);
+	return *ix >= 0 && *ix < (int)NERF_GRIDSIZE && *iy >= 0 && *iy < (int)NERF_GRIDSIZE && *iz >= 0 && *iz < (int)NERF_GRIDSIZE;
+}
+NGP_HD uint32_t df_index(uint32_t mip, uint32_t oct, int ix, int iy, int iz) {
+	return (mip * 8u + oct) * DF_BYTES_PER_FIELD + ((uint32_t)iz * NERF_GRIDSIZE + (uint32_t)iy) * NERF_GRIDSIZE + (uint32_t)ix;
+}
+// lattice_step through the octant distance fields: same result as lattice_step (the point is
+// occupied iff D = 0 at its mip; the coarsest empty mip is climbed as the reference does), but
+// an empty cell is left through the far faces of its empty D-box in one verified jump.
+NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, uint32_t oct, const uint8_t* df,
+                           uint32_t max_mip, const aabb3& aabb) {
+	const float n = *n_io;
+	const float t = step_from(st, n);
+	const v3 pos = o + d * t;
+	if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return LATTICE_EXIT;
+	uint32_t mip = mip_from_pos(pos);
+	mip = mip > max_mip ? max_mip : mip;
+	int cx, cy, cz;
+	if (!cascaded_cell_at(pos, mip, &cx, &cy, &cz)) {
+		*n_io = n + 1.0f;
+		return LATTICE_SKIPPED;
+	}
+	uint32_t D = df[df_index(mip, oct, cx, cy, cz)];
+	if (D == 0u) return LATTICE_OCCUPIED;
+	while (mip < max_mip) {  // coarsest empty mip, as the reference climbs
+		int ux, uy, uz;
+		if (!cascaded_cell_at(pos, mip + 1, &ux, &uy, &uz)) break;
+		const uint32_t Du = df[df_index(mip + 1, oct, ux, uy, uz)];
+		if (Du == 0u) break;
+		++mip;
+		D = Du;
+		cx = ux;
+		cy = uy;
+		cz = uz;
+	}
+	const float res = scalbnf((float)NERF_GRIDSIZE, -(int)mip), inv_res = scalbnf(1.0f / (float)NERF_GRIDSIZE, (int)mip);
+	const v3 p = (pos - 0.5f) * res;  // cell coordinates - 64
+	const float fd = (float)D;
+	const float fx = d.x < 0.0f ? (float)(cx - 64) + 1.0f - fd : (float)(cx - 64) + fd;
+	const float fy = d.y < 0.0f ? (float)(cy - 64) + 1.0f - fd : (float)(cy - 64) + fd;
+	const float fz = d.z < 0.0f ? (float)(cz - 64) + 1.0f - fd : (float)(cz - 64) + fd;
+	const float exit = fmaxf(fminf(fminf((fx - p.x) * idir.x, (fy - p.y) * idir.y), (fz - p.z) * idir.z) * inv_res, 0.0f);
+	const float n_far = step_to(st, t + exit);
+	float nn = n + ceilf(fmaxf(n_far - n, 0.5f));
+	if (nn - n > 1.0f) {
+		// the jump stands if the point before the landing point is still in the empty box, or
+		// already outside the AABB (the box is convex: every point in between is in it too)
+		const v3 last = o + d * step_from(st, nn - 1.0f);
+		if (aabb_contains(aabb, last)) {
+			int qx, qy, qz;
+			const bool in_grid = cascaded_cell_at(last, mip, &qx, &qy, &qz);
+			const int ex = d.x < 0.0f ? cx - qx : qx - cx, ey = d.y < 0.0f ? cy - qy : qy - cy,
+			          ez = d.z < 0.0f ? cz - qz : qz - cz;
+			const int lim = (int)D - 1;
+			if (!in_grid || ex < 0 || ex > lim || ey < 0 || ey > lim || ez < 0 || ez > lim) nn = n + 1.0f;
+		}
+	}
+	*n_io = nn;
+	return LATTICE_SKIPPED;
+}
+
 NGP_HD bool next_occupied_lattice_point(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
                                         const uint8_t* summary, uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
 	while (true) {

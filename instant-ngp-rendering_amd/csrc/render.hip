@@ -1,16 +1,17 @@
 // render.hip — NeRF volume renderer (NerfTracer) for gfx950.
 //
 //  k_render_init    init_rays_with_payload_kernel_nerf + advance_pos_nerf  src/testbed_nerf.cu:1376-1489, 333-381
-//  k_compact        compact_kernel_nerf                                     :1351-1374 (wave ballot + prefix,
-//                                                                            one atomic per wave)
 //  k_generate       generate_next_nerf_network_inputs                       :421-469
-//  k_composite      composite_kernel_nerf (Shade mode)                      :471-677
+//  k_composite      composite_kernel_nerf (Shade mode) + compact_kernel_nerf :471-677, 1351-1374 (block
+//                                                                            ballot + prefix, one atomic per block)
 //  k_shade          shade_kernel_nerf                                       :1309-1349
 //  k_accum_tonemap  accumulate_kernel + tonemap_kernel                      src/render_buffer.cu:232-266, 533-565
 //
 // Every ray's result depends only on its own sample sequence (the compaction
 // only regroups rays), so the image is deterministic per pixel and matches the
 // oracle's straight per-ray march whatever order the waves claim slots in.
+#include <cstring>
+
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -45,6 +46,8 @@ struct RenderK {
 	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
 	const uint8_t* bitfield;
 	const uint8_t* summary;
+	const uint8_t* df;  // octant distance fields (null: occupancy-summary block skipping)
+	uint32_t* dbg;  // NGP_RENDER_DEBUG: [init lattice steps, init alive, generate iterations, samples, samples composited]
 };
 
 __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32_t yl) {
@@ -149,8 +152,20 @@ __device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* s
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
 		float n = step_to(k.st, t) + ld_random_val(k.sample_index, idx * 786433u);
 		OccCache occ = occ_cache_init();
-		p.alive = next_occupied_lattice_point(&n, k.st, origin, dir, idir, k.bitfield, summary, k.max_mip, k.aabb, occ) ? 1u : 0u;
+		const uint32_t oct = ray_octant(dir);
+		int st;
+		uint32_t steps = 0;
+		do {
+			st = k.df ? lattice_step_df(&n, k.st, origin, dir, idir, oct, k.df, k.max_mip, k.aabb)
+			          : lattice_step(&n, k.st, origin, dir, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
+			++steps;
+		} while (st == LATTICE_SKIPPED);
+		p.alive = st == LATTICE_OCCUPIED ? 1u : 0u;
 		p.n = n;
+		if (k.dbg) {
+			atomicAdd(&k.dbg[0], steps);
+			atomicAdd(&k.dbg[1], p.alive);
+		}
 	}
 	*pp = p;
 }
@@ -185,35 +200,67 @@ __global__ void __launch_bounds__(512) k_occupancy_summary(const uint8_t* __rest
 
 
 
-__global__ void __launch_bounds__(256) k_compact(uint32_t n, const Payload* __restrict__ sp, const float4* __restrict__ srgba,
-                                                 const float* __restrict__ sdepth, Payload* __restrict__ dp,
-                                                 float4* __restrict__ drgba, float* __restrict__ ddepth,
-                                                 Payload* __restrict__ hp, float4* __restrict__ hrgba,
-                                                 float* __restrict__ hdepth, uint32_t* __restrict__ alive_counter,
-                                                 uint32_t* __restrict__ hit_counter) {
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	bool alive = false, hit = false;
-	Payload p;
-	float4 c;
-	float dd = 0.0f;
-	if (i < n) {
-		p = sp[i];
-		c = srgba[i];
-		dd = sdepth[i];
-		alive = p.alive != 0;
-		hit = !alive && c.w > 0.001f;
+// Octant distance fields (ngp_math.h lattice_step_df), three separable exact passes of the
+// Chebyshev transform restricted to an orthant: D = min over occupied c' of max_k |c'_k - c_k|
+// = min_z' max(dz, min_y' max(dy, min_x' dx)).  Rebuilt only when the bitfield changes.
+// Pass x: one thread per (mip, x-sign, z, y) line, a sweep toward the line's start.
+__global__ void __launch_bounds__(256) k_df_x(const uint8_t* __restrict__ bitfield, uint8_t* __restrict__ fx, uint32_t max_mip) {
+	const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t mip = g >> 15;
+	if (mip > max_mip) return;
+	const uint32_t sneg = (g >> 14) & 1u, y = g & 127u, z = (g >> 7) & 127u;
+	const uint8_t* bits = bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8);
+	uint8_t* out = fx + (size_t)(mip * 2u + sneg) * DF_BYTES_PER_FIELD + (z * NERF_GRIDSIZE + y) * NERF_GRIDSIZE;
+	uint32_t dist = mip < max_mip ? 0u : 254u;  // beyond the grid: the next mip (occupied) / outside the AABB
+	for (uint32_t k = 0; k < NERF_GRIDSIZE; ++k) {
+		const uint32_t x = sneg ? k : NERF_GRIDSIZE - 1u - k;  // positive direction looks at x' >= x
+		const uint32_t c = morton3D(x, y, z);
+		dist = ((bits[c >> 3] >> (c & 7u)) & 1u) ? 0u : min(dist + 1u, 255u);
+		out[x] = (uint8_t)dist;
 	}
-	uint32_t oa, oh;
-	block_append2(alive, hit, alive_counter, hit_counter, &oa, &oh);
-	if (alive) {
-		dp[oa] = p;
-		drgba[oa] = c;
-		ddepth[oa] = dd;
-	} else if (hit) {
-		hp[oh] = p;
-		hrgba[oh] = c;
-		hdepth[oh] = dd;
+}
+
+// Passes y and z: one thread per cell and sign combination; h = min_k max(k, f(c + s k)),
+// stopping once k reaches the best value so far (the loop is as long as the answer).
+template <uint32_t AXIS>
+__global__ void __launch_bounds__(256) k_df_yz(const uint8_t* __restrict__ fin, uint8_t* __restrict__ fout, uint32_t max_mip) {
+	constexpr uint32_t NV_IN = AXIS == 1 ? 2u : 4u;  // sign combinations of the input / output
+	const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t cell = g & (DF_BYTES_PER_FIELD - 1u), v = (g >> 21) & (2u * NV_IN - 1u);
+	const uint32_t mip = g >> (AXIS == 1 ? 23 : 24);
+	if (mip > max_mip) return;
+	const uint32_t x = cell & 127u, y = (cell >> 7) & 127u, z = cell >> 14;
+	const uint8_t* f = fin + (size_t)(mip * NV_IN + (v & (NV_IN - 1u))) * DF_BYTES_PER_FIELD;
+	const bool neg = (v >> (AXIS == 1 ? 1 : 2)) & 1u;
+	const int c0 = AXIS == 1 ? (int)y : (int)z;
+	const uint32_t stride = AXIS == 1 ? NERF_GRIDSIZE : NERF_GRIDSIZE * NERF_GRIDSIZE;
+	uint32_t h = f[cell];
+	for (uint32_t k = 1; k < h; ++k) {
+		const int c = neg ? c0 - (int)k : c0 + (int)k;
+		if (c < 0 || c >= (int)NERF_GRIDSIZE) {
+			if (mip < max_mip) h = k;
+			break;
+		}
+		const uint32_t fk = f[(uint32_t)((int)cell + (c - c0) * (int)stride)];
+		h = min(h, max(k, fk));
 	}
+	fout[(size_t)(mip * 2u * NV_IN + v) * DF_BYTES_PER_FIELD + cell] = (uint8_t)h;
+	(void)x;
+}
+
+static void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s) {
+	RenderScratch& rs = m->rs;
+	if (rs.df_version == m->gs.version && rs.df_max_mip == max_mip) return;
+	const size_t nm = max_mip + 1;
+	rs.df.reserve(nm * 8 * DF_BYTES_PER_FIELD);
+	rs.df_x.reserve(nm * 2 * DF_BYTES_PER_FIELD);
+	rs.df_xy.reserve(nm * 4 * DF_BYTES_PER_FIELD);
+	k_df_x<<<div_up(nm * 2 * NERF_GRIDSIZE * NERF_GRIDSIZE, 256), 256, 0, s>>>(m->gs.bitfield.ptr, rs.df_x.ptr, max_mip);
+	k_df_yz<1><<<div_up(nm * 4 * DF_BYTES_PER_FIELD, 256), 256, 0, s>>>(rs.df_x.ptr, rs.df_xy.ptr, max_mip);
+	k_df_yz<2><<<div_up(nm * 8 * DF_BYTES_PER_FIELD, 256), 256, 0, s>>>(rs.df_xy.ptr, rs.df.ptr, max_mip);
+	NGP_HIP_CHECK(hipGetLastError());
+	rs.df_version = m->gs.version;
+	rs.df_max_mip = max_mip;
 }
 
 // After MARCH_ITER passes: rays still marching are finished with what they accumulated.
@@ -243,8 +290,8 @@ template <uint32_t G>
 __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
                                                   float* __restrict__ coords, uint32_t n_steps,
                                                   uint32_t* __restrict__ next_alive_counter) {
-	if (blockIdx.x == 0 && threadIdx.x == 0) *next_alive_counter = 0;  // filled by this pass's k_compact
-	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
+	if (blockIdx.x == 0 && threadIdx.x == 0) *next_alive_counter = 0;  // filled by this pass's k_composite
+	const uint8_t* summary = k.df ? nullptr : stage_summary(k.summary, k.max_mip);
 	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
 	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
@@ -261,12 +308,16 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 		n = p->n;
 	}
 	OccCache occ = occ_cache_init();
-	uint32_t j = 0;
+	const uint32_t oct = ray_octant(d);
+	uint32_t j = 0, iters = 0;
 	bool exited = false;
 	while (__ballot(running) != 0ull) {
+		iters += running;
 		float nr = n + (float)r;
 		int st = LATTICE_EXIT;
-		if (running) st = lattice_step(&nr, k.st, o, d, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
+		if (running)
+			st = k.df ? lattice_step_df(&nr, k.st, o, d, idir, oct, k.df, k.max_mip, k.aabb)
+			          : lattice_step(&nr, k.st, o, d, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
 		const unsigned long long m_exit = __ballot(running && st == LATTICE_EXIT) & gmask;
 		const unsigned long long m_occ = __ballot(running && st == LATTICE_OCCUPIED) & gmask;
 		const float n_last = __shfl(st == LATTICE_SKIPPED ? nr : n + (float)G, g0 + G - 1, 64);
@@ -302,59 +353,90 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 			}
 		}
 	}
+	if (k.dbg && i < n_alive && r == 0) {
+		atomicAdd(&k.dbg[2], iters);
+		atomicAdd(&k.dbg[3], j);
+	}
 	if (i < n_alive && p->alive && r == 0) {
 		p->n_steps = j;
 		if (!exited) p->n = n;
 	}
 }
 
+// composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
+// each thread composites its ray's samples of this pass in order, then the block appends the
+// ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
 __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, uint32_t current_step,
-                                                   Payload* __restrict__ payloads, float4* __restrict__ rgba,
-                                                   float* __restrict__ depth, const float* __restrict__ coords,
-                                                   const __half* __restrict__ out, uint32_t n_steps) {
+                                                   const Payload* __restrict__ sp, const float4* __restrict__ srgba,
+                                                   const float* __restrict__ sdepth, const float* __restrict__ coords,
+                                                   const __half* __restrict__ out, uint32_t n_steps,
+                                                   Payload* __restrict__ dp, float4* __restrict__ drgba,
+                                                   float* __restrict__ ddepth, Payload* __restrict__ hp,
+                                                   float4* __restrict__ hrgba, float* __restrict__ hdepth,
+                                                   uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	if (i >= n_alive) return;
-	Payload& p = payloads[i];
-	if (!p.alive) return;
-	float4 c = rgba[i];
-	float local_depth = depth[i];
-	const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
-	const uint32_t actual = p.n_steps;
-	uint32_t j = 0;
-	for (; j < actual; ++j) {
-		const size_t s = (size_t)i + (size_t)j * n_alive;
-		const __half* o = out + 4 * s;
-		const float* crd = coords + 8 * s;
-		const v3 pos = unwarp_position(mk3(crd[0], crd[1], crd[2]), k.train_aabb);
-		const float T = 1.0f - c.w;
-		const float dt = unwarp_dt(crd[3]);
-		const float alpha = 1.0f - __expf(-network_to_density(__half2float(o[3]), k.density_act) * dt);
-		const float weight = alpha * T;
-		const v3 rgb = mk3(network_to_rgb(__half2float(o[0]), k.rgb_act), network_to_rgb(__half2float(o[1]), k.rgb_act),
-		                   network_to_rgb(__half2float(o[2]), k.rgb_act));
-		c.x += rgb.x * weight;
-		c.y += rgb.y * weight;
-		c.z += rgb.z * weight;
-		c.w += weight;
-		if (weight > p.max_weight) {
-			p.max_weight = weight;
-			local_depth = dot(cam_fwd, pos - cam_pos);
+	Payload p;
+	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+	float local_depth = 0.0f;
+	bool alive = false;
+	if (i < n_alive) {
+		p = sp[i];
+		c = srgba[i];
+		local_depth = sdepth[i];
+		alive = p.alive != 0;
+	}
+	if (alive) {
+		const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
+		const uint32_t actual = p.n_steps;
+		uint32_t j = 0;
+		for (; j < actual; ++j) {
+			const size_t s = (size_t)i + (size_t)j * n_alive;
+			const uint2 o2 = *reinterpret_cast<const uint2*>(out + 4 * s);
+			const float4 crd = *reinterpret_cast<const float4*>(coords + 8 * s);
+			const __half2 rg = *reinterpret_cast<const __half2*>(&o2.x), bs = *reinterpret_cast<const __half2*>(&o2.y);
+			const float T = 1.0f - c.w;
+			const float dt = unwarp_dt(crd.w);
+			const float alpha = 1.0f - __expf(-network_to_density(__high2float(bs), k.density_act) * dt);
+			const float weight = alpha * T;
+			const v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
+			                   network_to_rgb(__low2float(bs), k.rgb_act));
+			c.x += rgb.x * weight;
+			c.y += rgb.y * weight;
+			c.z += rgb.z * weight;
+			c.w += weight;
+			if (weight > p.max_weight) {
+				p.max_weight = weight;
+				const v3 pos = unwarp_position(mk3(crd.x, crd.y, crd.z), k.train_aabb);
+				local_depth = dot(cam_fwd, pos - cam_pos);
+			}
+			if (c.w > (1.0f - k.min_transmittance)) {
+				const float inv = 1.0f / c.w;
+				c.x *= inv;
+				c.y *= inv;
+				c.z *= inv;
+				c.w *= inv;
+				break;
+			}
 		}
-		if (c.w > (1.0f - k.min_transmittance)) {
-			const float inv = 1.0f / c.w;
-			c.x *= inv;
-			c.y *= inv;
-			c.z *= inv;
-			c.w *= inv;
-			break;
+		if (k.dbg) atomicAdd(&k.dbg[4], j < actual ? j + 1 : actual);
+		if (j < n_steps) {
+			alive = false;
+			p.alive = 0;
+			p.n_steps = j + current_step;
 		}
 	}
-	if (j < n_steps) {
-		p.alive = 0;
-		p.n_steps = j + current_step;
+	const bool hit = i < n_alive && !alive && c.w > 0.001f;
+	uint32_t oa, oh;
+	block_append2(alive, hit, alive_counter, hit_counter, &oa, &oh);
+	if (alive) {
+		dp[oa] = p;
+		drgba[oa] = c;
+		ddepth[oa] = local_depth;
+	} else if (hit) {
+		hp[oh] = p;
+		hrgba[oh] = c;
+		hdepth[oh] = local_depth;
 	}
-	rgba[i] = c;
-	depth[i] = local_depth;
 }
 
 __global__ void __launch_bounds__(256) k_shade(uint32_t n, const Payload* __restrict__ hp, const float4* __restrict__ hrgba,
@@ -490,7 +572,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	rs.coords.reserve(8 * max_samples);
 	rs.enc.reserve((size_t)m->lt.n_levels * max_samples * m->lt.F);
 	rs.out.reserve(4 * max_samples);
-	rs.counters.reserve(4);
+	rs.counters.reserve(16);
+	static const bool debug = getenv("NGP_RENDER_DEBUG") != nullptr;
+	k.dbg = debug ? rs.counters.ptr + 8 : nullptr;
+	if (debug) NGP_HIP_CHECK(hipMemsetAsync(k.dbg, 0, 8 * sizeof(uint32_t), s));
 	if (!rs.host_counter.ptr) {
 		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 4 * sizeof(uint32_t), hipHostMallocDefault));
 		rs.host_counter.n = 4;
@@ -500,9 +585,14 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
+	static const bool block_skipping = getenv("NGP_RENDER_SKIP") && !strcmp(getenv("NGP_RENDER_SKIP"), "blocks");
+	if (!block_skipping) {
+		build_distance_fields(m, k.max_mip, s);
+		k.df = rs.df.ptr;
+	}
 	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
 	                                                                rs.counters.ptr);
-	const size_t lds = (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
+	const size_t lds = k.df ? 0 : (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
 	k_render_init<<<div_up(n_tiled, 256u), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
 	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
@@ -547,10 +637,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.end(NGP_TIMER_RENDER_MLP, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, it, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
-		                                                 rs.out.ptr, n_steps);
-		k_compact<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(1 - cur), C(1 - cur),
-		                                               rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr, alive_out,
-		                                               rs.counters.ptr + 2);
+		                                                 rs.out.ptr, n_steps, P(1 - cur), C(1 - cur), rs.depth[1 - cur].ptr,
+		                                                 P(2), C(2), rs.depth[2].ptr, alive_out, rs.counters.ptr + 2);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
 		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -568,6 +656,15 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
 		NGP_HIP_CHECK(hipStreamSynchronize(s));
 		n_hit = rs.host_counter.ptr[2];
+	}
+	if (debug) {
+		uint32_t d[8];
+		NGP_HIP_CHECK(hipMemcpyAsync(d, k.dbg, sizeof(d), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		fprintf(stderr,
+		        "[render] rays %u init: alive %u lattice steps %.2f/ray | passes %u generate iterations %u samples %u "
+		        "composited %u (%.1f%%)\n",
+		        n, d[1], (double)d[0] / n, pass, d[2], d[3], d[4], 100.0 * d[4] / std::max(d[3], 1u));
 	}
 	if (n_hit)
 		k_shade<<<div_up(n_hit, 256), 256, 0, s>>>(n_hit, P(2), C(2), rs.depth[2].ptr, k.linear_colors,

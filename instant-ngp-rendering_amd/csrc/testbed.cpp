@@ -1064,6 +1064,11 @@ void Testbed::save_snapshot(const std::string& path, bool include_optimizer_stat
 			std::memcpy(&g16[2 * k], &h, 2);
 		}
 		snap["density_grid_binary"] = Json::binary(std::move(g16));
+		// the exact fp32 grid: the reference re-derives the bitfield from the fp16 copy, which can
+		// flip cells sitting on the threshold; resuming from this one reproduces renders bit for bit
+		std::vector<uint8_t> g32(grid.size() * 4);
+		std::memcpy(g32.data(), grid.data(), g32.size());
+		snap["mi355x"]["density_grid_fp32_binary"] = Json::binary(std::move(g32));
 	}
 	Json nj = Json::object();
 	nj["aabb_scale"] = Json((double)nerf.training.dataset.aabb_scale);
@@ -1246,10 +1251,14 @@ void Testbed::load_snapshot(const std::string& path) {
 	if (!g16.empty()) {
 		if (g16.size() != n_cells * 2) throw std::runtime_error("Incompatible number of grid cascades.");
 		std::vector<float> grid(n_cells);
-		for (size_t k = 0; k < n_cells; ++k) {
-			uint16_t h;
-			std::memcpy(&h, &g16[2 * k], 2);
-			grid[k] = f16_to_f32(h);
+		if (exact.contains("density_grid_fp32_binary") && exact["density_grid_fp32_binary"].bin().size() == n_cells * 4) {
+			std::memcpy(grid.data(), exact["density_grid_fp32_binary"].bin().data(), n_cells * 4);
+		} else {
+			for (size_t k = 0; k < n_cells; ++k) {
+				uint16_t h;
+				std::memcpy(&h, &g16[2 * k], 2);
+				grid[k] = f16_to_f32(h);
+			}
 		}
 		ck(ngp_density_grid_bitfield(m_model, nerf.max_cascade, m_stream));  // sizes the grid buffers
 		sync();

@@ -200,3 +200,41 @@ def test_render_matches_oracle(spp, snap, shard):
         assert l1 < 1e-3, l1
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("aabb_scale", [1, 4])
+def test_render_floaters_matches_oracle(aabb_scale):
+    """Sparse random occupancy (floaters) over several cascades: the render's empty-space
+    jumps (octant distance fields) must land on exactly the lattice points the oracle's
+    point-by-point march samples."""
+    g, o, rng = pair(CFG_A, grid_scale=1.0)
+    try:
+        max_cascade = max(0, int(np.log2(aabb_scale)))
+        nc = max_cascade + 1
+        grid = np.where(rng.random(CELLS * nc) < 0.004, 1.0, 0.0).astype(np.float32)
+        grid[:CELLS] = np.maximum(grid[:CELLS], sphere_bitfield(0.2))
+        A.check(g.lib.ngp_density_grid_bitfield(g.h, max_cascade, stream()))  # sizes the grid for nc cascades
+        torch.cuda.synchronize()
+        o.grid_set(grid)
+        o.grid_bitfield(max_cascade)
+        gp, _, _, _ = gpu_grid_buffers(g)
+        cuda_memcpy_h2d(gp, grid)
+        A.check(g.lib.ngp_density_grid_bitfield(g.h, max_cascade, stream()))
+        torch.cuda.synchronize()
+        W, H = 48, 40
+        cam = make_views(1, 8, 8)[1][0]
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        ra = render_args(W, H, cam, focal, spp=1, snap=0, aabb_scale=aabb_scale)
+        frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+        depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+        A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()),
+                                 stream()))
+        torch.cuda.synchronize()
+        gf = frame.cpu().numpy().reshape(H, W, 4)
+        of, od = o.render(ra)
+        assert (of[..., 3] > 0.01).mean() > 0.1
+        assert ((gf[..., 3] > 0.01) != (of[..., 3] > 0.01)).mean() < 0.01
+        l1 = np.abs(gf - of).mean()
+        assert l1 < 1e-3, l1
+    finally:
+        g.close()

@@ -109,7 +109,10 @@ def test_train_render_snapshot(scene, tmp_path):
     tb3.camera_matrix = tb.camera_matrix
     tb3.relative_focal_length = tb.relative_focal_length
     tb3.screen_center = tb.screen_center
-    np.testing.assert_array_equal(img, tb3.render(64, 64, 2, True))
+    # params are the same halves; the bitfield is re-derived from the fp16 grid (as the reference
+    # does, src/testbed.cu:4885-4893), which may flip threshold cells: near-identical, not bit-exact
+    img3 = tb3.render(64, 64, 2, True)
+    assert np.mean(np.abs(img3 - img)) < 1e-4 and np.mean(img3 == img) > 0.99
 
     # optimizer state included; the resumed testbed keeps training
     snap_opt = str(tmp_path / "model_opt.msgpack")
