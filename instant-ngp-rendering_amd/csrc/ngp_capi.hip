@@ -194,6 +194,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		(void)hipDeviceSynchronize();
 		for (auto* b : {&m->params32, &m->ema32, &m->grads, &m->adam_m, &m->adam_v}) b->release();
 		m->grid_grads16.release();
+		if (m->sync_event) (void)hipEventDestroy(m->sync_event);
 		m->params16.release();
 		m->infer16.release();
 		m->adam_steps.release();
@@ -376,7 +377,7 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		if (!m->ts.counters.ptr) return;
 		uint32_t c[16];
 		NGP_HIP_CHECK(hipMemcpyAsync(c, m->ts.counters.ptr, sizeof(c), hipMemcpyDeviceToHost, S(s)));
-		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
+		wait_stream(m, S(s));
 		st->n_rays = m->ts.last_n_rays;
 		st->measured_batch_size_before_compaction = c[0];
 		st->measured_batch_size = c[1];

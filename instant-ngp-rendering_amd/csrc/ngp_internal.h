@@ -202,6 +202,7 @@ struct ngp_model {
 	ngp_train_stats last_stats{};
 	bool stats_pending = false;
 	ngp::KernelTimers timers;
+	hipEvent_t sync_event = nullptr;  // host read-backs spin on it (ngp::wait_stream)
 	uint32_t last_n_rays = 0;
 };
 
@@ -210,6 +211,17 @@ namespace ngp {
 // ---- kernel launchers (defined in the .hip files) --------------------------------------
 // hashgrid.hip
 // site: 0 training step, 1 render, 2 density grid / API (names the kernel instance in profiles)
+// Waits for everything enqueued on s by spinning on an event: the per-pass counter
+// read-backs are short, and a blocking wait costs tens of microseconds of wake-up.
+inline void wait_stream(ngp_model* m, hipStream_t s) {
+	if (!m->sync_event) NGP_HIP_CHECK(hipEventCreateWithFlags(&m->sync_event, hipEventDisableTiming));
+	NGP_HIP_CHECK(hipEventRecord(m->sync_event, s));
+	hipError_t e;
+	while ((e = hipEventQuery(m->sync_event)) == hipErrorNotReady) {
+	}
+	NGP_HIP_CHECK(e);
+}
+
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
                          __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2);
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,

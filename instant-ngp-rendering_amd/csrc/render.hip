@@ -388,34 +388,49 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, 
 	if (alive) {
 		const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
 		const uint32_t actual = p.n_steps;
-		uint32_t j = 0;
-		for (; j < actual; ++j) {
-			const size_t s = (size_t)i + (size_t)j * n_alive;
-			const uint2 o2 = *reinterpret_cast<const uint2*>(out + 4 * s);
-			const float4 crd = *reinterpret_cast<const float4*>(coords + 8 * s);
-			const __half2 rg = *reinterpret_cast<const __half2*>(&o2.x), bs = *reinterpret_cast<const __half2*>(&o2.y);
-			const float T = 1.0f - c.w;
-			const float dt = unwarp_dt(crd.w);
-			const float alpha = 1.0f - __expf(-network_to_density(__high2float(bs), k.density_act) * dt);
-			const float weight = alpha * T;
-			const v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
-			                   network_to_rgb(__low2float(bs), k.rgb_act));
-			c.x += rgb.x * weight;
-			c.y += rgb.y * weight;
-			c.z += rgb.z * weight;
-			c.w += weight;
-			if (weight > p.max_weight) {
-				p.max_weight = weight;
-				const v3 pos = unwarp_position(mk3(crd.x, crd.y, crd.z), k.train_aabb);
-				local_depth = dot(cam_fwd, pos - cam_pos);
+		// samples are loaded 4 ahead of their use (the loop is otherwise one dependent
+		// global-load latency per sample; the tail passes run up to 32 per ray)
+		uint32_t j = actual;
+		bool done = false;
+		for (uint32_t j0 = 0; j0 < actual && !done; j0 += 4) {
+			uint2 o2[4];
+			float4 crd[4];
+#pragma unroll
+			for (uint32_t u = 0; u < 4; ++u) {
+				if (j0 + u < actual) {
+					const size_t s = (size_t)i + (size_t)(j0 + u) * n_alive;
+					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
+					crd[u] = *reinterpret_cast<const float4*>(coords + 8 * s);
+				}
 			}
-			if (c.w > (1.0f - k.min_transmittance)) {
-				const float inv = 1.0f / c.w;
-				c.x *= inv;
-				c.y *= inv;
-				c.z *= inv;
-				c.w *= inv;
-				break;
+#pragma unroll
+			for (uint32_t u = 0; u < 4; ++u) {
+				if (done || j0 + u >= actual) continue;
+				const __half2 rg = *reinterpret_cast<const __half2*>(&o2[u].x), bs = *reinterpret_cast<const __half2*>(&o2[u].y);
+				const float T = 1.0f - c.w;
+				const float dt = unwarp_dt(crd[u].w);
+				const float alpha = 1.0f - __expf(-network_to_density(__high2float(bs), k.density_act) * dt);
+				const float weight = alpha * T;
+				const v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
+				                   network_to_rgb(__low2float(bs), k.rgb_act));
+				c.x += rgb.x * weight;
+				c.y += rgb.y * weight;
+				c.z += rgb.z * weight;
+				c.w += weight;
+				if (weight > p.max_weight) {
+					p.max_weight = weight;
+					const v3 pos = unwarp_position(mk3(crd[u].x, crd[u].y, crd[u].z), k.train_aabb);
+					local_depth = dot(cam_fwd, pos - cam_pos);
+				}
+				if (c.w > (1.0f - k.min_transmittance)) {
+					const float inv = 1.0f / c.w;
+					c.x *= inv;
+					c.y *= inv;
+					c.z *= inv;
+					c.w *= inv;
+					j = j0 + u;
+					done = true;
+				}
 			}
 		}
 		if (k.dbg) atomicAdd(&k.dbg[4], j < actual ? j + 1 : actual);
@@ -598,7 +613,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
 	NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-	NGP_HIP_CHECK(hipStreamSynchronize(s));
+	wait_stream(m, s);
 	uint32_t n_alive = rs.host_counter.ptr[0];
 
 	// NerfTracer::trace (testbed_nerf.cu:1639-1755): generate -> infer -> composite -> compact,
@@ -642,7 +657,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
 		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		wait_stream(m, s);
 		n_alive = rs.host_counter.ptr[(pass + 1) % 2];
 		n_hit = rs.host_counter.ptr[2];
 		cur = 1 - cur;
@@ -654,13 +669,13 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,
 		                                              rs.counters.ptr);
 		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		wait_stream(m, s);
 		n_hit = rs.host_counter.ptr[2];
 	}
 	if (debug) {
 		uint32_t d[8];
 		NGP_HIP_CHECK(hipMemcpyAsync(d, k.dbg, sizeof(d), hipMemcpyDeviceToHost, s));
-		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		wait_stream(m, s);
 		fprintf(stderr,
 		        "[render] rays %u init: alive %u lattice steps %.2f/ray | passes %u generate iterations %u samples %u "
 		        "composited %u (%.1f%%)\n",
