@@ -84,6 +84,10 @@ struct Net {
 		return s;
 	}
 	static constexpr int fwd_off(int l) { return fwd_frags_upto(l) * FRAG_HALVES; }
+	// register-resident inference fragments (k_mlp_infer_rf): the forward fragments again,
+	// with the K order of every layer after the first permuted to the C-register layout
+	static constexpr int rfwd_off(int l) { return (fwd_frags() + bwd_frags() + fwd_frags_upto(l)) * FRAG_HALVES; }
+	static constexpr int all_frags() { return 2 * fwd_frags() + bwd_frags(); }
 	static constexpr int bwd_off(int l) {
 		int s = fwd_frags();
 		for (int i = 0; i < l; ++i) s += Kt(i) * Ms(i);
@@ -126,6 +130,7 @@ struct MlpArgs {
 	uint64_t param_off[MAX_LAYERS];
 	uint32_t param_in[MAX_LAYERS];
 	const uint32_t* n_dev;  // optional device-side sample count (<= n)
+	uint32_t enc_bytes, coord_bytes;  // buffer-resource extents (register-resident inference)
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -329,6 +334,254 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_density(MlpArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Register-resident inference (no LDS).  For v_mfma_f32_16x16x32_f16 lane (g, n) holds
+// C[4g + r][n] (r < 4) of a 16-row output tile and B[8g + j][n] (j < 8) of a 32-row
+// input step.  Two consecutive output tiles 2s, 2s+1 therefore ARE the next layer's
+// K-step s once the K order is permuted: position 8g + j <-> input row
+// 32s + (j < 4 ? 4g + j : 16 + 4g + j - 4).  k_pack applies that permutation to the
+// weights (rfwd fragments), so a layer's fp32 accumulators become the next layer's
+// fp16 B operands in place, and all weight fragments live in VGPRs for the whole
+// persistent loop.  Each wave streams tiles of 16*CT samples and prefetches the next
+// tile's encoding and direction while the current one runs through the MFMAs.
+// ---------------------------------------------------------------------------
+template <class N, int CT_>
+struct RawTile {
+	uint32_t e[CT_][8 * N::KE];  // encoding halves of this lane's K slots, packed in pairs where F >= 2
+	float d[CT_][3];
+};
+
+// Buffer resource over a device array (raw buffer, 32-bit byte offsets; reads past
+// num_records return 0).
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint32_t bytes) {
+	return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), (short)0, (int)bytes, 0x00020000);
+}
+
+// Loads this lane's share of a tile: encoding features 32s + 8g .. +7 of sample
+// base + 16c + n (level planes of the [L][plane][F] encoding) and its direction.
+template <class N, int CT_, int FF>
+__device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t enc_rs, __amdgpu_buffer_rsrc_t crd_rs,
+                                        uint32_t base, int g, int n, RawTile<N, CT_>& r, bool want_dir) {
+#pragma unroll
+	for (int c = 0; c < CT_; ++c) {
+		const uint32_t i = base + 16 * c + n;
+#pragma unroll
+		for (int s = 0; s < N::KE; ++s) {
+			const uint32_t k0 = 32 * s + 8 * g;
+			if constexpr (FF == 2) {
+#pragma unroll
+				for (int q = 0; q < 4; ++q) {
+					const uint32_t lvl = k0 / 2 + q;  // levels past E read as 0 (their weights are 0 too)
+					r.e[c][4 * s + q] = 2 * lvl < a.E ? __builtin_amdgcn_raw_buffer_load_b32(enc_rs, 4 * (lvl * a.enc_plane + i), 0, 0) : 0u;
+				}
+			} else if constexpr (FF == 4) {
+#pragma unroll
+				for (int q = 0; q < 2; ++q) {
+					const uint32_t lvl = k0 / 4 + q;
+					uint2 u = make_uint2(0u, 0u);
+					if (4 * lvl < a.E) {
+						const auto v = __builtin_amdgcn_raw_buffer_load_b64(enc_rs, 8 * (lvl * a.enc_plane + i), 0, 0);
+						u = make_uint2(v[0], v[1]);
+					}
+					r.e[c][4 * s + 2 * q] = u.x;
+					r.e[c][4 * s + 2 * q + 1] = u.y;
+				}
+			} else {
+				const uint16_t* e = reinterpret_cast<const uint16_t*>(a.enc);
+#pragma unroll
+				for (int q = 0; q < 4; ++q) {
+					uint32_t pair = 0;
+#pragma unroll
+					for (int h = 0; h < 2; ++h) {
+						const uint32_t k = k0 + 2 * q + h;
+						if (i < a.n && k < a.E) {
+							const uint32_t lvl = k / a.F, f = k % a.F;
+							pair |= (uint32_t)e[((size_t)lvl * a.enc_plane + i) * a.F + f] << (16 * h);
+						}
+					}
+					r.e[c][4 * s + q] = pair;
+				}
+			}
+		}
+		if (want_dir) {
+			const uint32_t o = 4 * (i * a.coord_stride + 4);
+			r.d[c][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o, 0, 0));
+			r.d[c][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o + 4, 0, 0));
+			r.d[c][2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o + 8, 0, 0));
+		}
+	}
+}
+
+__device__ __forceinline__ h8 pack_h8(uint32_t u0, uint32_t u1, uint32_t u2, uint32_t u3) {
+	const uint4 v = make_uint4(u0, u1, u2, u3);
+	return __builtin_bit_cast(h8, v);
+}
+__device__ __forceinline__ h8 c_to_b(const f4& lo, const f4& hi) {
+	return h8{(_Float16)lo[0], (_Float16)lo[1], (_Float16)lo[2], (_Float16)lo[3],
+	          (_Float16)hi[0], (_Float16)hi[1], (_Float16)hi[2], (_Float16)hi[3]};
+}
+
+// SH degree 4 components 4g .. 4g+3 of the warped direction (same formulas as load_sh)
+__device__ __forceinline__ void sh4_slice(const float* dw, int g, float (&o)[4]) {
+	const float x = dw[0] * 2.0f - 1.0f, y = dw[1] * 2.0f - 1.0f, z = dw[2] * 2.0f - 1.0f;
+	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+	float v[16];
+	v[0] = 0.28209479177387814f;
+	v[1] = -0.48860251190291987f * y;
+	v[2] = 0.48860251190291987f * z;
+	v[3] = -0.48860251190291987f * x;
+	v[4] = 1.0925484305920792f * xy;
+	v[5] = -1.0925484305920792f * yz;
+	v[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+	v[7] = -1.0925484305920792f * xz;
+	v[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+	v[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+	v[10] = 2.8906114426405538f * xy * z;
+	v[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+	v[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+	v[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+	v[14] = 1.4453057213202769f * z * (x2 - y2);
+	v[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+#pragma unroll
+	for (int r = 0; r < 4; ++r) o[r] = g == 0 ? v[r] : g == 1 ? v[4 + r] : g == 2 ? v[8 + r] : v[12 + r];
+}
+
+// one layer: B operands in (KS steps) -> C tiles out (MT tiles), weights w[frag]
+template <class N, int l, int CT_>
+__device__ __forceinline__ void rf_layer(const h8* w, const h8 (&bin)[CT_][2], f4 (&cout)[CT_][4]) {
+	constexpr int MT = N::Mt(l), KS = N::Ks(l), F0 = N::fwd_frags_upto(l);
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+		for (int c = 0; c < CT_; ++c) {
+			f4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+			for (int s = 0; s < KS; ++s) acc = mfma(w[(F0 + mt * KS + s) * 64], bin[c][s], acc);
+			cout[c][mt] = acc;  // ReLU (hidden layers) is applied by rf_chain on the packed halves
+		}
+}
+
+// C tiles of a hidden layer -> ReLU'd B operands of the next layer (missing tiles are
+// zero).  ReLU commutes with the rounding to fp16, so it runs on the packed halves.
+template <int MT, int CT_>
+__device__ __forceinline__ void rf_chain(const f4 (&cin)[CT_][4], h8 (&bout)[CT_][2]) {
+	const f4 z = {0.f, 0.f, 0.f, 0.f};
+	typedef _Float16 h2v __attribute__((ext_vector_type(2)));
+#pragma unroll
+	for (int c = 0; c < CT_; ++c)
+#pragma unroll
+		for (int s = 0; s < 2; ++s)
+			if (2 * s < MT) {
+				h8 v = c_to_b(cin[c][2 * s], 2 * s + 1 < MT ? cin[c][2 * s + 1] : z);
+#pragma unroll
+				for (int q = 0; q < 4; ++q) {
+					h2v p = {v[2 * q], v[2 * q + 1]};
+					p = __builtin_elementwise_max(p, h2v{(_Float16)0, (_Float16)0});
+					v[2 * q] = p[0];
+					v[2 * q + 1] = p[1];
+				}
+				bout[c][s] = v;
+			}
+}
+
+template <class N, int l, int END, int CT_>
+__device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4 (&c)[CT_][4]) {
+	if constexpr (l < END) {
+		rf_layer<N, l, CT_>(w, b, c);
+		rf_chain<N::Mt(l), CT_>(c, b);
+		rf_hidden_range<N, l + 1, END, CT_>(w, b, c);
+	}
+}
+
+// The tile pipeline is PF deep: every wave keeps PF tiles' loads in flight (register
+// ring, statically indexed by unrolling the loop PF times) -- the kernel is bound by
+// memory latency x bytes in flight, not by the MFMAs (20 per 16 samples).  Weight
+// fragments are read from LDS (one copy per workgroup) to leave the VGPRs to the ring.
+template <class N, int CT_, int PF, bool DENSITY_ONLY>
+__device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const RawTile<N, CT_>& cur, uint32_t base, int g,
+                                        int n) {
+	h8 b[CT_][2];
+	f4 c[CT_][4];
+#pragma unroll
+	for (int cc = 0; cc < CT_; ++cc)
+#pragma unroll
+		for (int s = 0; s < N::KE; ++s)
+			b[cc][s] = pack_h8(cur.e[cc][4 * s], cur.e[cc][4 * s + 1], cur.e[cc][4 * s + 2], cur.e[cc][4 * s + 3]);
+	rf_hidden_range<N, 0, N::DH, CT_>(w, b, c);
+	rf_layer<N, N::DH, CT_>(w, b, c);
+	if constexpr (DENSITY_ONLY) {
+		if (g == 0) {
+#pragma unroll
+			for (int cc = 0; cc < CT_; ++cc) {
+				const uint32_t i = base + 16 * cc + n;
+				if (i < a.n) a.out[i] = __builtin_bit_cast(__half, (_Float16)c[cc][0][0]);
+			}
+		}
+	} else {
+		_Float16 dens[CT_];
+#pragma unroll
+		for (int cc = 0; cc < CT_; ++cc) {
+			dens[cc] = (_Float16)c[cc][0][0];
+			float sh[4];
+			sh4_slice(cur.d[cc], g, sh);
+			const f4 shv = {sh[0], sh[1], sh[2], sh[3]};
+			b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
+		}
+		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
+		rf_layer<N, N::NL - 1, CT_>(w, b, c);
+		if (g == 0) {
+#pragma unroll
+			for (int cc = 0; cc < CT_; ++cc) {
+				const uint32_t i = base + 16 * cc + n;
+				if (i < a.n) {
+					const h4 o = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], dens[cc]};
+					*reinterpret_cast<h4*>(a.out + (size_t)i * 4) = o;
+				}
+			}
+		}
+	}
+}
+
+template <class N, int CT_, int PF, bool DENSITY_ONLY, int FF>
+__global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
+	static_assert(N::KE <= 2 && N::Wp <= 64, "register layout assumes <= 2 K-steps per layer");
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	constexpr int NF = DENSITY_ONLY ? N::fwd_frags_upto(N::DH + 1) : N::fwd_frags();
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	h8* w = reinterpret_cast<h8*>(smem);  // [frag][lane]
+	{
+		const h8* src = reinterpret_cast<const h8*>(a.frags + N::rfwd_off(0));
+		for (int t = threadIdx.x; t < NF * 64; t += BLOCK) w[t] = src[t];
+	}
+	__syncthreads();
+	const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+	const h8* wl = w + lane;  // fragment f of this lane: wl[f * 64]
+	constexpr uint32_t TS = 16 * CT_;
+	const uint32_t n_tiles = (a.n + TS - 1) / TS;
+	const uint32_t stride = gridDim.x * WAVES;
+	const uint32_t t0 = blockIdx.x * WAVES + (threadIdx.x >> 6);
+	const __amdgpu_buffer_rsrc_t enc_rs = make_rsrc(a.enc, a.enc_bytes);
+	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
+	RawTile<N, CT_> ring[PF];
+#pragma unroll
+	for (int q = 0; q < PF; ++q) {
+		const uint32_t t = t0 + q * stride;
+		if (t < n_tiles) rf_load<N, CT_, FF>(a, enc_rs, crd_rs, t * TS, g, n, ring[q], !DENSITY_ONLY);
+	}
+	for (uint32_t tb = t0; tb < n_tiles; tb += PF * stride) {
+#pragma unroll
+		for (int q = 0; q < PF; ++q) {
+			const uint32_t t = tb + q * stride;
+			if (t < n_tiles) {
+				RawTile<N, CT_> cur = ring[q];
+				const uint32_t tn = t + PF * stride;
+				if (tn < n_tiles) rf_load<N, CT_, FF>(a, enc_rs, crd_rs, tn * TS, g, n, ring[q], !DENSITY_ONLY);
+				rf_tile<N, CT_, PF, DENSITY_ONLY>(a, wl, cur, t * TS, g, n);
+			}
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
 // Training: forward (activations kept), dgrad chain, wgrad via transposed reads.
 // ---------------------------------------------------------------------------
 template <class N, int l>
@@ -526,6 +779,7 @@ struct PackLayer {
 	uint32_t out, in;         // param dims
 	uint32_t mt, ks, fwd_off; // forward: [mt][ks] fragments
 	uint32_t kt, ms, bwd_off; // backward (transposed): [kt][ms] fragments
+	uint32_t rfwd_off;        // register-resident forward: [mt][ks], K permuted for l > 0
 };
 struct PackArgs {
 	PackLayer L[MAX_LAYERS];
@@ -549,6 +803,16 @@ __global__ void k_pack(const __half* __restrict__ params, __half* __restrict__ o
 			const uint32_t row = 16 * mt + m;
 			for (uint32_t j = 0; j < 8; ++j) {
 				const uint32_t col = 32 * s + 8 * g + j;
+				out[(size_t)t * 8 + j] = (row < L.out && col < L.in) ? W[(size_t)row * L.in + col] : __float2half(0.0f);
+			}
+			return;
+		}
+		const uint32_t r0 = L.rfwd_off / FRAG_HALVES;
+		if (frag >= r0 && frag < r0 + nf) {
+			const uint32_t idx = frag - r0, mt = idx / L.ks, s = idx % L.ks;
+			const uint32_t row = 16 * mt + m;
+			for (uint32_t j = 0; j < 8; ++j) {
+				const uint32_t col = 32 * s + (l == 0 ? 8 * g + j : (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4)));
 				out[(size_t)t * 8 + j] = (row < L.out && col < L.in) ? W[(size_t)row * L.in + col] : __float2half(0.0f);
 			}
 			return;
@@ -602,8 +866,9 @@ static void layer_geometry(const ngp_model* m, PackArgs& p) {
 		L.kt = N::Kt(l);
 		L.ms = N::Ms(l);
 		L.bwd_off = N::bwd_off(l);
+		L.rfwd_off = N::rfwd_off(l);
 	}
-	p.total_frags = N::fwd_frags() + N::bwd_frags();
+	p.total_frags = N::all_frags();
 }
 
 #define NGP_DISPATCH(variant, ...)                      \
@@ -620,7 +885,7 @@ static void layer_geometry(const ngp_model* m, PackArgs& p) {
 
 uint32_t mlp_frag_halves(const ngp_model* m) {
 	uint32_t r = 0;
-	NGP_DISPATCH(m->mlp_variant, r = (N::fwd_frags() + N::bwd_frags()) * FRAG_HALVES);
+	NGP_DISPATCH(m->mlp_variant, r = N::all_frags() * FRAG_HALVES);
 	return r;
 }
 
@@ -673,12 +938,14 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.n = n;
 	a.out = out;
 	a.n_dev = n_dev;
+	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_plane * 2, 0xffffffffu);
+	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * coord_stride * 4, 0xffffffffu);
 	NGP_DISPATCH(m->mlp_variant, {
-		const size_t lds = N::lds_infer();
-		set_lds<N>(k_mlp_infer<N>, lds);
-		const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)(160 * 1024 / lds));
-		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count() * per_cu);
-		k_mlp_infer<N><<<grid, BLOCK, lds, s>>>(a);
+		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
+		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);
+		if (a.F == 2) k_mlp_infer_rf<N, 1, 2, false, 2><<<grid, BLOCK, lds, s>>>(a);
+		else if (a.F == 4) k_mlp_infer_rf<N, 1, 2, false, 4><<<grid, BLOCK, lds, s>>>(a);
+		else k_mlp_infer_rf<N, 1, 2, false, 0><<<grid, BLOCK, lds, s>>>(a);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }
@@ -693,12 +960,13 @@ void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* e
 	a.n = n;
 	a.out = out;
 	a.n_dev = n_dev;
+	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_plane * 2, 0xffffffffu);
 	NGP_DISPATCH(m->mlp_variant, {
-		const size_t lds = N::lds_density();
-		set_lds<N>(k_mlp_density<N>, lds);
-		const uint32_t per_cu = std::max<uint32_t>(1, (uint32_t)(160 * 1024 / lds));
-		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count() * per_cu);
-		k_mlp_density<N><<<grid, BLOCK, lds, s>>>(a);
+		const size_t lds = (size_t)N::fwd_frags_upto(N::DH + 1) * FRAG_HALVES * 2;
+		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);
+		if (a.F == 2) k_mlp_infer_rf<N, 1, 2, true, 2><<<grid, BLOCK, lds, s>>>(a);
+		else if (a.F == 4) k_mlp_infer_rf<N, 1, 2, true, 4><<<grid, BLOCK, lds, s>>>(a);
+		else k_mlp_infer_rf<N, 1, 2, true, 0><<<grid, BLOCK, lds, s>>>(a);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }
