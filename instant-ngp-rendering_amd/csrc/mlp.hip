@@ -370,20 +370,17 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 			if constexpr (FF == 2) {
 #pragma unroll
 				for (int q = 0; q < 4; ++q) {
-					const uint32_t lvl = k0 / 2 + q;  // levels past E read as 0 (their weights are 0 too)
-					r.e[c][4 * s + q] = 2 * lvl < a.E ? __builtin_amdgcn_raw_buffer_load_b32(enc_rs, 4 * (lvl * a.enc_plane + i), 0, 0) : 0u;
+					// levels past the encoding lie past the buffer's extent: the load returns 0
+					const uint32_t lvl = k0 / 2 + q;
+					r.e[c][4 * s + q] = __builtin_amdgcn_raw_buffer_load_b32(enc_rs, 4 * (lvl * a.enc_plane + i), 0, 0);
 				}
 			} else if constexpr (FF == 4) {
 #pragma unroll
 				for (int q = 0; q < 2; ++q) {
 					const uint32_t lvl = k0 / 4 + q;
-					uint2 u = make_uint2(0u, 0u);
-					if (4 * lvl < a.E) {
-						const auto v = __builtin_amdgcn_raw_buffer_load_b64(enc_rs, 8 * (lvl * a.enc_plane + i), 0, 0);
-						u = make_uint2(v[0], v[1]);
-					}
-					r.e[c][4 * s + 2 * q] = u.x;
-					r.e[c][4 * s + 2 * q + 1] = u.y;
+					const auto v = __builtin_amdgcn_raw_buffer_load_b64(enc_rs, 8 * (lvl * a.enc_plane + i), 0, 0);
+					r.e[c][4 * s + 2 * q] = v[0];
+					r.e[c][4 * s + 2 * q + 1] = v[1];
 				}
 			} else {
 				const uint16_t* e = reinterpret_cast<const uint16_t*>(a.enc);
@@ -420,7 +417,9 @@ __device__ __forceinline__ h8 c_to_b(const f4& lo, const f4& hi) {
 	          (_Float16)hi[0], (_Float16)hi[1], (_Float16)hi[2], (_Float16)hi[3]};
 }
 
-// SH degree 4 components 4g .. 4g+3 of the warped direction (same formulas as load_sh)
+// SH degree 4 components 4g .. 4g+3 of the warped direction (same formulas as load_sh).
+// The compiler turns the g-select into four short divergent paths, which measured
+// cheaper than computing all 16 components and blending.
 __device__ __forceinline__ void sh4_slice(const float* dw, int g, float (&o)[4]) {
 	const float x = dw[0] * 2.0f - 1.0f, y = dw[1] * 2.0f - 1.0f, z = dw[2] * 2.0f - 1.0f;
 	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
@@ -558,7 +557,8 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	constexpr uint32_t TS = 16 * CT_;
 	const uint32_t n_tiles = (a.n + TS - 1) / TS;
 	const uint32_t stride = gridDim.x * WAVES;
-	const uint32_t t0 = blockIdx.x * WAVES + (threadIdx.x >> 6);
+	// wave-uniform tile index (scalar registers: the ring's guards are scalar branches)
+	const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
 	const __amdgpu_buffer_rsrc_t enc_rs = make_rsrc(a.enc, a.enc_bytes);
 	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
 	RawTile<N, CT_> ring[PF];
