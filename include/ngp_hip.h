@@ -140,6 +140,14 @@ typedef struct ngp_train_args {
 	int32_t optimize_mlp;      /* m_train_network */
 	int32_t optimize_encoding; /* m_train_encoding */
 	int32_t defer_optimizer;   /* 1: leave grads for an external all-reduce, then call ngp_optimizer_step */
+	/* error map (Nerf::Training::ErrorMap, nerf.h:50-59; compute_loss_kernel_train_nerf
+	 * src/testbed_nerf.cu:1028-1054; nerf_random_image_pos_training / image_idx nerf_device.cuh:552-598) */
+	float* error_map;           /* device [n_images][res_y][res_x] f32: += each ray's mean loss, bilinear; null = off */
+	uint32_t error_map_res[2];  /* x, y */
+	const float* cdf_x_cond_y;  /* device [n_images][cdf_res_y][cdf_res_x]: sample_focal_plane_proportional_to_error; null = uniform */
+	const float* cdf_y;         /* device [n_images][cdf_res_y] */
+	const float* cdf_img;       /* device [n_images] normalised image CDF: sample_image_proportional_to_error; null = uniform */
+	uint32_t cdf_res[2];        /* x, y */
 } ngp_train_args;
 
 typedef struct ngp_train_stats {
@@ -246,6 +254,14 @@ ngp_status ngp_density_grid_bitfield(ngp_model* model, uint32_t max_cascade, ngp
 /* grid: [n_cascades][128^3] f32 (Morton order); bitfield: [8][128^3/8] u8; tmp: evaluation buffer;
  * mean: 1 f32 (device). */
 ngp_status ngp_density_grid_buffers(ngp_model* model, float** grid, uint8_t** bitfield, float** tmp, float** mean);
+
+/* --- error map ------------------------------------------------------------------------ */
+/* construct_cdf_2d + construct_cdf_1d (src/testbed_nerf.cu:1493-1546): per image, the row-wise
+ * conditional CDFs of the error map (MIN_PDF 0.01 mixed in), the row CDF, and cdf_img[i] = the
+ * image's unnormalised total (the caller normalises it on the host, src/testbed_nerf.cu:2553-2567).
+ * All arrays are device pointers; no model needed. */
+ngp_status ngp_error_map_build_cdf(const float* error_map, uint32_t n_images, uint32_t res_x, uint32_t res_y,
+                                   float* cdf_x_cond_y, float* cdf_y, float* cdf_img, ngp_stream stream);
 
 /* --- rendering --------------------------------------------------------------------- */
 /* frame: [H][W][4] f32 premultiplied RGBA, depth: [H][W] f32 (device, caller-owned);

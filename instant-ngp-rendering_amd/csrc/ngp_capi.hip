@@ -19,6 +19,8 @@ void run_grid_finish(ngp_model* m, const ngp_grid_args* a, hipStream_t s);
 void run_grid_bitfield(ngp_model* m, uint32_t max_cascade, hipStream_t s);
 void grid_reserve(ngp_model* m, uint32_t n_cascades, uint32_t n_samples);
 void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s);
+void run_error_map_cdf(const float* error_map, uint32_t n_images, uint32_t rx, uint32_t ry, float* cdf_x_cond_y,
+                       float* cdf_y, float* cdf_img, hipStream_t s);
 void run_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t W, uint32_t H, uint32_t spp,
                             int color_space, float exposure, const float* bg, int output_srgb, hipStream_t s);
 }  // namespace ngp
@@ -459,6 +461,14 @@ ngp_status ngp_density_grid_buffers(ngp_model* m, float** grid, uint8_t** bitfie
 		}
 		if (tmp) *tmp = m->gs.tmp.ptr;
 		if (mean) *mean = m->gs.mean.ptr;
+	});
+}
+
+ngp_status ngp_error_map_build_cdf(const float* error_map, uint32_t n_images, uint32_t res_x, uint32_t res_y,
+                                   float* cdf_x_cond_y, float* cdf_y, float* cdf_img, ngp_stream s) {
+	return guarded([&] {
+		require(n_images == 0 || (error_map && cdf_x_cond_y && cdf_y && cdf_img), "null argument");
+		run_error_map_cdf(error_map, n_images, res_x, res_y, cdf_x_cond_y, cdf_y, cdf_img, S(s));
 	});
 }
 

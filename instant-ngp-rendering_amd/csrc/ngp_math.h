@@ -536,6 +536,54 @@ NGP_HD uint32_t image_idx(uint32_t base_idx, uint32_t n_rays, uint32_t n_trainin
 	return (uint32_t)((((uint64_t)base_idx) * n_training_images) / n_rays) % n_training_images;
 }
 
+// binary_search (common.h:207-230): first index with data[i] >= val, clamped to length-1.
+NGP_HD uint32_t cdf_search(float val, const float* data, uint32_t length) {
+	if (length == 0) return 0;
+	uint32_t first = 0, count = length;
+	while (count > 0) {
+		const uint32_t step = count / 2, it = first + step;
+		if (data[it] < val) {
+			first = it + 1;
+			count -= step + 1;
+		} else {
+			count = step;
+		}
+	}
+	return first < length - 1 ? first : length - 1;
+}
+
+// Error-map importance sampling (nerf_device.cuh:495-525, 577-593).
+struct ErrorCdf {
+	const float* x_cond_y;  // [img][ry][rx]
+	const float* y;         // [img][ry]
+	const float* img;       // [n_images]
+	uint32_t rx, ry;
+};
+constexpr float UNIFORM_SAMPLING_FRACTION = 0.5f;
+constexpr float MIN_PDF = 0.01f;  // construct_cdf_2d/1d mixing (src/testbed_nerf.cu:1491)
+constexpr float MIN_PMF = 0.1f;   // image CDF mixing (src/testbed_nerf.cu:2563)
+// sample_cdf_2d: half the samples stay uniform, the rest follow the image's error CDF
+// (*pdf is left untouched on the uniform half, as in the reference)
+NGP_HD void sample_cdf_2d(float* u, float* v, uint32_t img, const ErrorCdf& c, float* pdf) {
+	if (*u < UNIFORM_SAMPLING_FRACTION) {
+		*u = *u * (1.0f / UNIFORM_SAMPLING_FRACTION);
+		return;
+	}
+	const float su = (*u - UNIFORM_SAMPLING_FRACTION) * (1.0f / (1.0f - UNIFORM_SAMPLING_FRACTION));
+	const float* cy = c.y + (size_t)img * c.ry;
+	const uint32_t y = cdf_search(*v, cy, c.ry);
+	float prev = y > 0 ? cy[y - 1] : 0.0f;
+	const float sv = (*v - prev) / (cy[y] - prev);
+	const float* cx = c.x_cond_y + ((size_t)img * c.ry + y) * c.rx;
+	const uint32_t x = cdf_search(su, cx, c.rx);
+	prev = x > 0 ? cx[x - 1] : 0.0f;
+	const float pmf_x = cx[x] - prev;
+	const float sx = (su - prev) / pmf_x;
+	*pdf = pmf_x * (cy[y] - (y > 0 ? cy[y - 1] : 0.0f)) * (float)(c.rx * c.ry);
+	*u = ((float)x + sx) / (float)c.rx;
+	*v = ((float)y + sv) / (float)c.ry;
+}
+
 // Loss (nerf_device.cuh:74-142,600-615). loss_type matches ELossType (common.h:79-87).
 enum LossType : int { LOSS_L2 = 0, LOSS_L1 = 1, LOSS_MAPE = 2, LOSS_SMAPE = 3, LOSS_HUBER = 4, LOSS_LOGL1 = 5, LOSS_RELL2 = 6 };
 NGP_HD void loss_and_gradient(float target, float pred, int loss_type, float* loss, float* grad) {

@@ -233,7 +233,22 @@ PYBIND11_MODULE(pyngp, m) {
 		TV_RW("optimize_exposure", optimize_exposure)
 		TV_RW("optimize_extra_dims", optimize_extra_dims)
 		TV_RW("optimize_per_image_latents", optimize_extra_dims)
+		TV_RW("sample_focal_plane_proportional_to_error", sample_focal_plane_proportional_to_error)
+		TV_RW("sample_image_proportional_to_error", sample_image_proportional_to_error)
+		TV_RW("include_sharpness_in_error", include_sharpness_in_error)
+		TV_RW("n_steps_between_error_map_updates", n_steps_between_error_map_updates)
 #undef TV_RW
+		// additions: the accumulated error map and the image pmf of the last CDF update
+		.def_property_readonly("error_map", [](TrainingView& v) {
+			const auto& tr = v.tb->nerf.training;
+			std::vector<float> h = v.tb->error_map_data();
+			const py::ssize_t ni = h.empty() ? 0 : (py::ssize_t)tr.dataset.n_images;
+			py::array_t<float> out({ni, (py::ssize_t)tr.error_map.resolution[1], (py::ssize_t)tr.error_map.resolution[0]});
+			if (!h.empty()) std::memcpy(out.mutable_data(), h.data(), h.size() * sizeof(float));
+			return out;
+		})
+		.def_property_readonly("error_map_pmf_img", [](TrainingView& v) { return v.tb->nerf.training.error_map.pmf_img_cpu; })
+		.def_property_readonly("error_map_cdf_valid", [](TrainingView& v) { return v.tb->nerf.training.error_map.is_cdf_valid; })
 		.def_property_readonly("dataset", [](TrainingView& v) -> NerfDataset& { return v.tb->nerf.training.dataset; },
 		                       py::return_value_policy::reference_internal)
 		.def_property_readonly("transforms", [](TrainingView& v) {

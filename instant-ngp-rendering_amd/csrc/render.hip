@@ -22,10 +22,11 @@ struct Payload {
 	float n;  // next lattice point to test (stepping space)
 	float max_weight;
 	uint32_t idx;
-	uint32_t n_steps;
-	uint32_t alive;
-	uint32_t pad;
+	uint32_t n_steps;   // samples written this pass; bit 31: the ray left the AABB
+	uint32_t base;      // first sample slot of this pass (samples are ray-major)
+	float alpha_last;   // alpha of the last composited sample (next pass's sample budget)
 };
+constexpr uint32_t PAYLOAD_EXITED = 0x80000000u;
 static_assert(sizeof(Payload) == 48, "payload layout");
 
 struct RenderK {
@@ -47,6 +48,8 @@ struct RenderK {
 	const uint8_t* bitfield;
 	const uint8_t* summary;
 	const uint8_t* df;  // octant distance fields (null: occupancy-summary block skipping)
+	int budget;         // per-ray sample budgets (sample_budget); 0: every ray gets n_steps
+	float budget_scale;
 	uint32_t* dbg;  // NGP_RENDER_DEBUG: [init lattice steps, init alive, generate iterations, samples, samples composited]
 };
 
@@ -65,7 +68,7 @@ __device__ __forceinline__ const uint8_t* stage_summary(const uint8_t* __restric
 	return reinterpret_cast<const uint8_t*>(s_summary);
 }
 
-__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
+__device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
                                               Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer);
 
 // Stream compaction slot for a 256-thread block: ballot per wave, LDS prefix over the four
@@ -99,6 +102,29 @@ __device__ __forceinline__ void block_append2(bool fa, bool fb, uint32_t* counte
 	*ib = pb + (uint32_t)__popcll(mb & below);
 }
 
+// Reserves cnt consecutive slots of *counter for every thread of a 256-thread block: wave
+// scans, LDS totals, ONE atomic per block.  Returns this thread's first slot.
+__device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t* counter) {
+	__shared__ uint32_t wsum[4], bbase;
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	uint32_t x = cnt;
+#pragma unroll
+	for (uint32_t o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o, 64);
+		if (lane >= o) x += y;
+	}
+	if (lane == 63) wsum[w] = x;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+		bbase = t ? atomicAdd(counter, t) : 0u;
+	}
+	__syncthreads();
+	uint32_t b = bbase;
+	for (uint32_t k = 0; k < w; ++k) b += wsum[k];
+	return b + x - cnt;
+}
+
 __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
                                                      float* __restrict__ depth, float4* __restrict__ frame,
                                                      float* __restrict__ depth_buffer, uint32_t* __restrict__ counters) {
@@ -108,11 +134,11 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
 	const uint32_t tile = r >> 6, x = (tile % k.tiles_x) * 8u + (r & 7u), yl = (tile / k.tiles_x) * 8u + ((r >> 3) & 7u);
 	Payload p;
-	p.alive = 0;
-	if (x < k.W && yl < k.h_local) init_ray_body(k, summary, x, yl, &p, frame, depth_buffer);
+	bool alive = false;
+	if (x < k.W && yl < k.h_local) alive = init_ray_body(k, summary, x, yl, &p, frame, depth_buffer);
 	uint32_t slot, unused;
-	block_append2(p.alive != 0, false, &counters[0], &counters[3], &slot, &unused);
-	if (p.alive) {
+	block_append2(alive, false, &counters[0], &counters[3], &slot, &unused);
+	if (alive) {
 		payloads[slot] = p;
 		rgba[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
 		depth[slot] = 0.0f;
@@ -120,7 +146,7 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 }
 
 // init_rays_with_payload_kernel_nerf + advance_pos_nerf for pixel x of local row yl
-__device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
+__device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
                                               Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer) {
 	const uint32_t y = local_to_global_row(k, yl);
 	const uint32_t idx = x + k.W * y;
@@ -138,7 +164,8 @@ __device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* s
 	p.max_weight = 0.0f;
 	p.idx = idx;
 	p.n_steps = 0;
-	p.pad = 0;
+	p.base = 0;
+	p.alpha_last = 0.0f;
 	dir = normalize(dir);
 	float t0, t1;
 	ray_intersect(k.aabb, origin, dir, &t0, &t1);
@@ -146,8 +173,8 @@ __device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* s
 	p.o[0] = origin.x; p.o[1] = origin.y; p.o[2] = origin.z;
 	p.d[0] = dir.x; p.d[1] = dir.y; p.d[2] = dir.z;
 	p.n = 0.0f;
-	p.alive = aabb_contains(k.aabb, origin + dir * t) ? 1u : 0u;
-	if (p.alive) {
+	bool alive = aabb_contains(k.aabb, origin + dir * t);
+	if (alive) {
 		// advance_pos_nerf: jitter the start and skip empty space
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
 		float n = step_to(k.st, t) + ld_random_val(k.sample_index, idx * 786433u);
@@ -160,14 +187,15 @@ __device__ __forceinline__ void init_ray_body(const RenderK& k, const uint8_t* s
 			          : lattice_step(&n, k.st, origin, dir, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
 			++steps;
 		} while (st == LATTICE_SKIPPED);
-		p.alive = st == LATTICE_OCCUPIED ? 1u : 0u;
+		alive = st == LATTICE_OCCUPIED;
 		p.n = n;
 		if (k.dbg) {
 			atomicAdd(&k.dbg[0], steps);
-			atomicAdd(&k.dbg[1], p.alive);
+			atomicAdd(&k.dbg[1], alive ? 1u : 0u);
 		}
 	}
 	*pp = p;
+	return alive;
 }
 
 // Occupancy summary (ngp_math.h OCC_SUMMARY_*): one workgroup of 512 threads per 32^3
@@ -179,7 +207,7 @@ __global__ void __launch_bounds__(512) k_occupancy_summary(const uint8_t* __rest
 	__shared__ uint32_t any_wave[8];
 	const uint32_t g = blockIdx.x * 512u + threadIdx.x;  // [mip][32768 words]
 	const uint32_t mip = g >> 15, wi = g & 32767u, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-	if (g < 4) counters[g] = 0;
+	if (g < 8) counters[g] = 0;
 	const uint64_t word = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8))[wi];
 	const unsigned long long a = __ballot(word != 0ull);
 	uint8_t* sm = summary + (size_t)OCC_SUMMARY_BYTES * mip;
@@ -280,24 +308,44 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 	}
 }
 
-// generate_next_nerf_network_inputs (testbed_nerf.cu:421-469): the next n_steps samples
-// of every alive ray.  G lanes cooperate on one ray: each iteration they test G
-// consecutive lattice points at once (ballots give the occupied ones in order and the
-// first exit), and an all-empty round jumps on from the last lane's verified skip.
-// G = 1 for the big early passes (one lane per ray, flat loop), up to 64 for the last
-// few thousand rays, whose long serial marches otherwise dominate the tail passes.
+// Samples a ray gets this pass: up to n_steps, fewer when its transmittance is already low
+// -- enough to reach min_transmittance at the opacity of its last sample, with headroom.
+// A short estimate only costs the ray another pass; samples past a ray's termination are
+// the ones a fixed per-pass count wastes (the reference uses a fixed count, capped at 8).
+__device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, float alpha_last, uint32_t n_steps) {
+	if (!k.budget || T >= 1.0f || alpha_last <= 1e-4f) return n_steps;
+	if (T <= k.min_transmittance || alpha_last >= 0.999f) return 1u;
+	const float est = __logf(k.min_transmittance / T) / __logf(1.0f - alpha_last);
+	const float b = ceilf(est * k.budget_scale) + 1.0f;
+	return b >= (float)n_steps ? n_steps : (uint32_t)fmaxf(b, 1.0f);
+}
+
+// generate_next_nerf_network_inputs (testbed_nerf.cu:421-469): the next samples of every
+// alive ray.  Each ray first reserves its budget of sample slots (one atomic per block),
+// so the pass's samples are ray-major and packed; the encode and MLP read the total from
+// the device.  G lanes cooperate on one ray: each iteration they test G consecutive
+// lattice points at once (ballots give the occupied ones in order and the first exit),
+// and an all-empty round jumps on from the last lane's verified skip.  G = 1 for the big
+// early passes (one lane per ray, flat loop), up to 64 for the last few thousand rays,
+// whose long serial marches otherwise dominate the tail passes.
 template <uint32_t G>
 __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
-                                                  float* __restrict__ coords, uint32_t n_steps,
-                                                  uint32_t* __restrict__ next_alive_counter) {
+                                                  const float4* __restrict__ rgba, float* __restrict__ coords,
+                                                  uint32_t n_steps, uint32_t* __restrict__ next_alive_counter,
+                                                  uint32_t* __restrict__ sample_counter) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) *next_alive_counter = 0;  // filled by this pass's k_composite
 	const uint8_t* summary = k.df ? nullptr : stage_summary(k.summary, k.max_mip);
 	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
 	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
 	const uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G;
-	Payload* p = payloads + (i < n_alive ? i : 0);
-	bool running = i < n_alive && p->alive;  // group-uniform
+	const bool valid = i < n_alive;  // group-uniform
+	Payload* p = payloads + (valid ? i : 0);
+	uint32_t budget = 0;
+	if (valid) budget = sample_budget(k, 1.0f - rgba[i].w, p->alpha_last, n_steps);
+	uint32_t base = block_reserve(r == 0 ? budget : 0u, sample_counter);
+	if (G > 1) base = __shfl(base, g0, 64);
+	bool running = valid;
 	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f), wdir = mk3(0.0f);
 	float n = 0.0f;
 	if (running) {
@@ -324,7 +372,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 		if (!running) continue;
 		const uint32_t fe = m_exit ? (uint32_t)(__ffsll((long long)m_exit) - 1) : 64u;
 		const unsigned long long emit = m_occ & (fe >= 64 ? ~0ull : ((1ull << fe) - 1ull));
-		const uint32_t cnt = __popcll(emit), room = n_steps - j;
+		const uint32_t cnt = __popcll(emit), room = budget - j;
 		if ((emit >> lane) & 1ull) {
 			const uint32_t rank = __popcll(emit & ((1ull << lane) - 1ull));
 			if (rank < room) {
@@ -332,7 +380,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 				const float t = step_from(k.st, pn);
 				const float dt = step_from(k.st, pn + 1.0f) - t;
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
-				float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)i + (size_t)(j + rank) * n_alive));
+				float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)base + j + rank));
 				c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
 				c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
 			}
@@ -341,7 +389,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 			unsigned long long m = emit;  // the room-th emitted lane carries the last sample
 			for (uint32_t t = 1; t < room; ++t) m &= m - 1ull;
 			n += (float)((uint32_t)(__ffsll((long long)m) - 1) - g0 + 1u);
-			j = n_steps;
+			j = budget;
 			running = false;
 		} else {
 			j += cnt;
@@ -353,12 +401,23 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 			}
 		}
 	}
-	if (k.dbg && i < n_alive && r == 0) {
+	if (valid) {
+		// reserved slots the ray did not fill (it left the volume) still go through the
+		// encoder: give them an in-range position
+		for (uint32_t q = j + r; q < budget; q += G) {
+			float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)base + q));
+			c[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+			c[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+		}
+	}
+	if (k.dbg && valid && r == 0) {
 		atomicAdd(&k.dbg[2], iters);
 		atomicAdd(&k.dbg[3], j);
+		atomicAdd(&k.dbg[5], budget);
 	}
-	if (i < n_alive && p->alive && r == 0) {
-		p->n_steps = j;
+	if (valid && r == 0) {
+		p->n_steps = j | (exited ? PAYLOAD_EXITED : 0u);
+		p->base = base;
 		if (!exited) p->n = n;
 	}
 }
@@ -366,14 +425,16 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
-__global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, uint32_t current_step,
+__global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                    const float* __restrict__ sdepth, const float* __restrict__ coords,
-                                                   const __half* __restrict__ out, uint32_t n_steps,
+                                                   const __half* __restrict__ out,
                                                    Payload* __restrict__ dp, float4* __restrict__ drgba,
                                                    float* __restrict__ ddepth, Payload* __restrict__ hp,
                                                    float4* __restrict__ hrgba, float* __restrict__ hdepth,
-                                                   uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter) {
+                                                   uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter,
+                                                   uint32_t* __restrict__ next_sample_counter) {
+	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	Payload p;
 	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -383,22 +444,24 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, 
 		p = sp[i];
 		c = srgba[i];
 		local_depth = sdepth[i];
-		alive = p.alive != 0;
+		alive = true;
 	}
 	if (alive) {
 		const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
-		const uint32_t actual = p.n_steps;
+		const uint32_t actual = p.n_steps & ~PAYLOAD_EXITED;
+		const size_t sbase = p.base;
 		// samples are loaded 4 ahead of their use (the loop is otherwise one dependent
 		// global-load latency per sample; the tail passes run up to 32 per ray)
-		uint32_t j = actual;
 		bool done = false;
+		uint32_t used = actual;
+		float alpha_last = p.alpha_last;
 		for (uint32_t j0 = 0; j0 < actual && !done; j0 += 4) {
 			uint2 o2[4];
 			float4 crd[4];
 #pragma unroll
 			for (uint32_t u = 0; u < 4; ++u) {
 				if (j0 + u < actual) {
-					const size_t s = (size_t)i + (size_t)(j0 + u) * n_alive;
+					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
 					crd[u] = *reinterpret_cast<const float4*>(coords + 8 * s);
 				}
@@ -413,6 +476,7 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, 
 				const float weight = alpha * T;
 				const v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
 				                   network_to_rgb(__low2float(bs), k.rgb_act));
+				alpha_last = alpha;
 				c.x += rgb.x * weight;
 				c.y += rgb.y * weight;
 				c.z += rgb.z * weight;
@@ -428,17 +492,15 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive, 
 					c.y *= inv;
 					c.z *= inv;
 					c.w *= inv;
-					j = j0 + u;
+					used = j0 + u + 1;
 					done = true;
 				}
 			}
 		}
-		if (k.dbg) atomicAdd(&k.dbg[4], j < actual ? j + 1 : actual);
-		if (j < n_steps) {
-			alive = false;
-			p.alive = 0;
-			p.n_steps = j + current_step;
-		}
+		if (k.dbg) atomicAdd(&k.dbg[4], used);
+		p.alpha_last = alpha_last;
+		// finished: opaque enough, or the ray left the volume during this pass
+		if (done || (p.n_steps & PAYLOAD_EXITED)) alive = false;
 	}
 	const bool hit = i < n_alive && !alive && c.w > 0.001f;
 	uint32_t oa, oh;
@@ -600,6 +662,12 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
+	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (off by default: with one
+	// host read-back per pass the extra passes cost what the saved samples gain)
+	static const char* budget_env = getenv("NGP_RENDER_BUDGET");
+	k.budget = budget_env && strcmp(budget_env, "off") != 0;
+	k.budget_scale = k.budget ? (float)atof(budget_env) : 1.5f;
+	if (!(k.budget_scale > 0.0f)) k.budget_scale = 1.5f;
 	static const bool block_skipping = getenv("NGP_RENDER_SKIP") && !strcmp(getenv("NGP_RENDER_SKIP"), "blocks");
 	if (!block_skipping) {
 		build_distance_fields(m, k.max_mip, s);
@@ -636,24 +704,27 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t want = lanes_target() / std::max(n_alive, 1u);
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
 		const uint32_t gblocks = div_up((uint64_t)n_alive * G, 256);
+		uint32_t* samples = rs.counters.ptr + 4 + pass % 2;  // zeroed by the previous kernel of the chain
+		uint32_t* samples_next = rs.counters.ptr + 4 + (pass + 1) % 2;
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
-			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
-			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
-			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), rs.coords.ptr, n_steps, alive_out); break;
+			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
+			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
+			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
+			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
+		// sized for the most samples the pass can reserve; the kernels read the actual total
 		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
-		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s, nullptr, 1);
+		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MLP, s);
-		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s);
+		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s, samples);
 		tm.end(NGP_TIMER_RENDER_MLP, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, it, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
-		                                                 rs.out.ptr, n_steps, P(1 - cur), C(1 - cur), rs.depth[1 - cur].ptr,
-		                                                 P(2), C(2), rs.depth[2].ptr, alive_out, rs.counters.ptr + 2);
+		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
+		                                                 rs.out.ptr, P(1 - cur), C(1 - cur), rs.depth[1 - cur].ptr,
+		                                                 P(2), C(2), rs.depth[2].ptr, alive_out, rs.counters.ptr + 2, samples_next);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
 		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -677,9 +748,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		NGP_HIP_CHECK(hipMemcpyAsync(d, k.dbg, sizeof(d), hipMemcpyDeviceToHost, s));
 		wait_stream(m, s);
 		fprintf(stderr,
-		        "[render] rays %u init: alive %u lattice steps %.2f/ray | passes %u generate iterations %u samples %u "
-		        "composited %u (%.1f%%)\n",
-		        n, d[1], (double)d[0] / n, pass, d[2], d[3], d[4], 100.0 * d[4] / std::max(d[3], 1u));
+		        "[render] rays %u init: alive %u lattice steps %.2f/ray | passes %u generate iterations %u slots %u "
+		        "samples %u composited %u (%.1f%% of slots)\n",
+		        n, d[1], (double)d[0] / n, pass, d[2], d[5], d[3], d[4], 100.0 * d[4] / std::max(d[5], 1u));
 	}
 	if (n_hit)
 		k_shade<<<div_up(n_hit, 256), 256, 0, s>>>(n_hit, P(2), C(2), rs.depth[2].ptr, k.linear_colors,

@@ -207,6 +207,8 @@ Testbed::~Testbed() {
 	for (float* p : {m_frame, m_depth, m_accum, m_out})
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
+	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img})
+		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
 }
@@ -586,6 +588,10 @@ void Testbed::reset_network(bool clear_density_grid) {
 	pcg32 rng(seed);
 	nerf.training.counters_rgb = NerfCounters{};
 	nerf.training.counters_rgb.rays_per_batch = 1 << 12;
+	nerf.training.n_steps_since_error_map_update = 0;  // src/testbed.cu:3636-3639
+	nerf.training.n_rays_since_error_map_update = 0;
+	nerf.training.n_steps_between_error_map_updates = 128;
+	nerf.training.error_map.is_cdf_valid = false;
 	pcg32 grid_rng(rng.next_uint());
 	m_rng_state = rng.state;
 	m_rng_inc = rng.inc;
@@ -706,6 +712,12 @@ void Testbed::update_density_grid(uint32_t n_uniform, uint32_t n_nonuniform) {
 
 void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (nerf.training.n_images_for_training == 0) return;
+	{
+		const NerfTraining& t = nerf.training;
+		if (t.optimize_extrinsics || t.optimize_distortion || t.optimize_focal_length || t.optimize_exposure ||
+		    t.optimize_extra_dims)
+			throw std::runtime_error("camera / exposure / latent optimisation is not implemented by this build");
+	}
 	upload_dataset();
 	NerfCounters& ctr = nerf.training.counters_rgb;
 	const uint32_t max_samples = batch * 16;
@@ -713,6 +725,23 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (ctr.measured_batch_size_before_compaction == 0) ctr.measured_batch_size_before_compaction = max_inference = max_samples;
 	else max_inference = next_multiple_host(std::min(ctr.measured_batch_size_before_compaction, max_samples), BATCH_SIZE_GRANULARITY);
 	if (training_step == 0) ctr.n_rays_total = 0;
+
+	// error map (re)allocation at the start of each accumulation period (src/testbed_nerf.cu:2486-2492)
+	NerfTraining& tr = nerf.training;
+	if (tr.n_steps_since_error_map_update == 0 && !tr.dataset.metadata.empty()) {
+		const uint32_t n_samples_per_image = (uint32_t)(((uint64_t)tr.n_steps_between_error_map_updates * ctr.rays_per_batch) /
+		                                                std::max<size_t>(tr.dataset.n_images, 1));
+		const ivec2 res = tr.dataset.metadata[0].resolution;
+		const int r = (int)(std::sqrt(std::sqrt((float)n_samples_per_image)) * 3.5f);
+		tr.error_map.resolution = {std::min(r, res[0]), std::min(r, res[1])};
+		const size_t n = (size_t)tr.error_map.resolution[0] * tr.error_map.resolution[1] * tr.dataset.n_images;
+		if (n > m_err_cap) {
+			if (m_err) (void)hipFree(m_err);
+			hk(hipMalloc((void**)&m_err, std::max<size_t>(n, 1) * sizeof(float)), "hipMalloc error map");
+			m_err_cap = n;
+		}
+		hk(hipMemsetAsync(m_err, 0, std::max<size_t>(n, 1) * sizeof(float), (hipStream_t)m_stream), "error map clear");
+	}
 
 	ngp_train_args a{};
 	a.images = (const ngp_image*)m_dev_meta;
@@ -739,7 +768,23 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.optimize_mlp = train_network;
 	a.optimize_encoding = train_encoding;
 	a.defer_optimizer = m_world > 1 ? 1 : 0;
+	if (m_err && tr.error_map.resolution[0] > 0 && tr.error_map.resolution[1] > 0) {
+		a.error_map = m_err;  // accumulate_error is always on (src/testbed_nerf.cu:2756)
+		a.error_map_res[0] = (uint32_t)tr.error_map.resolution[0];
+		a.error_map_res[1] = (uint32_t)tr.error_map.resolution[1];
+	}
+	if (tr.error_map.is_cdf_valid) {
+		if (tr.include_sharpness_in_error) throw std::runtime_error("include_sharpness_in_error is not supported by this build");
+		if (tr.sample_focal_plane_proportional_to_error) {
+			a.cdf_x_cond_y = m_cdf_x;
+			a.cdf_y = m_cdf_y;
+		}
+		if (tr.sample_image_proportional_to_error) a.cdf_img = m_cdf_img;
+		a.cdf_res[0] = (uint32_t)tr.error_map.cdf_resolution[0];
+		a.cdf_res[1] = (uint32_t)tr.error_map.cdf_resolution[1];
+	}
 	ctr.n_rays_total += ctr.rays_per_batch;
+	tr.n_rays_since_error_map_update += ctr.rays_per_batch;
 	ck(ngp_train_step(m_model, &a, m_stream));
 	if (m_world > 1) {
 		// MLP gradients (fp32) and hash-grid gradients (fp16) are summed over ranks
@@ -755,6 +800,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 		ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 	}
 	++training_step;
+	// CDFs from the error map, every n_steps_between_error_map_updates (x1.5 each time)
+	if (++tr.n_steps_since_error_map_update >= tr.n_steps_between_error_map_updates) update_error_map_cdf();
 	// m_rng.advance() (src/testbed_nerf.cu:2925)
 	pcg32 r;
 	r.state = m_rng_state;
@@ -789,6 +836,64 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (get_loss_scalar) loss = st.loss * (float)st.measured_batch_size / (float)batch;
 	uint32_t rpb = (uint32_t)((float)ctr.rays_per_batch * (float)batch / (float)st.measured_batch_size);
 	ctr.rays_per_batch = std::min(next_multiple_host(rpb, BATCH_SIZE_GRANULARITY), 1u << 18);
+}
+
+// src/testbed_nerf.cu:2523-2575: construct_cdf_2d/1d on the device, the image CDF on the host
+void Testbed::update_error_map_cdf() {
+	NerfTraining& tr = nerf.training;
+	const uint32_t n_images = (uint32_t)tr.dataset.n_images;
+	const ivec2 res = tr.error_map.resolution;
+	if (!m_err || n_images == 0 || res[0] <= 0 || res[1] <= 0) return;
+	const size_t n = (size_t)res[0] * res[1] * n_images;
+	// data parallel: every rank deposited the errors of its own rays
+	if (m_world > 1) allreduce_f32(m_err, n, false);
+	tr.error_map.cdf_resolution = res;
+	if (n > m_cdf_cap) {
+		if (m_cdf_x) (void)hipFree(m_cdf_x);
+		hk(hipMalloc((void**)&m_cdf_x, n * sizeof(float)), "hipMalloc cdf_x_cond_y");
+		m_cdf_cap = n;
+	}
+	const size_t ny = (size_t)res[1] * n_images;
+	if (ny + n_images > m_cdf_img_cap) {
+		if (m_cdf_y) (void)hipFree(m_cdf_y);
+		if (m_cdf_img) (void)hipFree(m_cdf_img);
+		hk(hipMalloc((void**)&m_cdf_y, ny * sizeof(float)), "hipMalloc cdf_y");
+		hk(hipMalloc((void**)&m_cdf_img, n_images * sizeof(float)), "hipMalloc cdf_img");
+		m_cdf_img_cap = ny + n_images;
+	}
+	ck(ngp_error_map_build_cdf(m_err, n_images, (uint32_t)res[0], (uint32_t)res[1], m_cdf_x, m_cdf_y, m_cdf_img, m_stream));
+	// image CDF on the CPU ("single-threaded anyway", src/testbed_nerf.cu:2552-2567)
+	std::vector<float> pmf(n_images), cdf(n_images);
+	hk(hipMemcpyAsync(pmf.data(), m_cdf_img, n_images * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "cdf_img d2h");
+	sync();
+	float cum = 0.0f;
+	for (uint32_t i = 0; i < n_images; ++i) {
+		cum += pmf[i];
+		cdf[i] = cum;
+	}
+	const float norm = 1.0f / cum;
+	for (uint32_t i = 0; i < n_images; ++i) {
+		pmf[i] = (1.0f - MIN_PMF) * pmf[i] * norm + MIN_PMF / (float)n_images;
+		cdf[i] = (1.0f - MIN_PMF) * cdf[i] * norm + MIN_PMF * (float)(i + 1) / (float)n_images;
+	}
+	tr.error_map.pmf_img_cpu = pmf;
+	hk(hipMemcpyAsync(m_cdf_img, cdf.data(), n_images * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "cdf_img h2d");
+	sync();
+	tr.n_steps_since_error_map_update = 0;
+	tr.n_rays_since_error_map_update = 0;
+	tr.error_map.is_cdf_valid = true;
+	tr.n_steps_between_error_map_updates = (uint32_t)((float)tr.n_steps_between_error_map_updates * 1.5f);
+}
+
+std::vector<float> Testbed::error_map_data() {
+	const NerfTraining& tr = nerf.training;
+	const size_t n = (size_t)tr.error_map.resolution[0] * tr.error_map.resolution[1] * tr.dataset.n_images;
+	std::vector<float> h(m_err ? n : 0);
+	if (!h.empty()) {
+		hk(hipMemcpyAsync(h.data(), m_err, n * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "error map d2h");
+		sync();
+	}
+	return h;
 }
 
 void Testbed::train(uint32_t batch_size) {

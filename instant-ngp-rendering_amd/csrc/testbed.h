@@ -88,6 +88,20 @@ struct NerfTraining {
 	int view = 0;
 	NerfCounters counters_rgb;
 	uint64_t density_grid_rng_state = 0, density_grid_rng_inc = 0;
+	// Nerf::Training::ErrorMap and its cadence (nerf.h:50-59, 112-118): the per-image error map
+	// is always accumulated; sampling follows it only when asked to
+	struct ErrorMap {
+		ivec2 resolution = {16, 16};
+		ivec2 cdf_resolution = {16, 16};
+		bool is_cdf_valid = false;
+		std::vector<float> pmf_img_cpu;
+	} error_map;
+	bool sample_focal_plane_proportional_to_error = false;
+	bool sample_image_proportional_to_error = false;
+	bool include_sharpness_in_error = false;  // not supported (no per-image sharpness data)
+	uint32_t n_steps_between_error_map_updates = 128;
+	uint32_t n_steps_since_error_map_update = 0;
+	uint32_t n_rays_since_error_map_update = 0;
 };
 
 struct Nerf {
@@ -145,6 +159,7 @@ public:
 	// --- snapshots (save_snapshot src/testbed.cu:4775, load_snapshot :4841) ---
 	void save_snapshot(const std::string& path, bool include_optimizer_state = false, bool compress = true);
 	void load_snapshot(const std::string& path);
+	std::vector<float> error_map_data();  // [n_images][res.y][res.x] accumulated since the last CDF update
 	static Json read_snapshot_file(const std::string& path);  // msgpack, zlib-inflated if compressed
 
 	// --- multi-GPU: one Testbed per rank, gradients all-reduced over RCCL/xGMI ---
@@ -202,8 +217,16 @@ private:
 	void ensure_render_buffers(size_t n_pixels);
 	void allreduce_f32(float* dev, size_t n, bool max_op);
 
+	void update_error_map_cdf();
+
 	ngp_model* m_model = nullptr;
 	void* m_stream = nullptr;
+	// error map (device): data [n_images][res.y][res.x], CDFs at cdf_resolution
+	float* m_err = nullptr;
+	float* m_cdf_x = nullptr;
+	float* m_cdf_y = nullptr;
+	float* m_cdf_img = nullptr;
+	size_t m_err_cap = 0, m_cdf_cap = 0, m_cdf_img_cap = 0;
 	Json m_network_config;
 	uint64_t m_rng_state = 0, m_rng_inc = 0;
 	// device dataset

@@ -136,6 +136,7 @@ struct SamplerArgs {
 	Stepping st;
 	uint32_t max_mip;
 	int snap;
+	ErrorCdf cdf;  // error-map importance sampling (null pointers: uniform)
 	const uint8_t* bitfield;
 	uint32_t* numsteps;  // [R][2]
 	uint32_t* counts;    // [R]
@@ -144,21 +145,46 @@ struct SamplerArgs {
 	float* coords;       // [max][8]
 };
 
-// Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777);
-// *n0 = first lattice point (stepping space) = entry + jitter.
-__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0) {
-	const uint32_t img = image_idx(gi, a.n_rays_global, a.n_images);
-	const ngp_image im = a.images[img];
-	pcg32 rng = a.rng;
-	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
+// Image and pixel of global training ray gi from its pcg32 stream (already advanced to
+// the ray): image_idx and nerf_random_image_pos_training (nerf_device.cuh:552-598),
+// proportional to the error map when its CDFs are given.
+// *pdf = img_pdf * uv_pdf, the importance-sampling density the reference divides the loss by
+// (src/testbed_nerf.cu:1010).
+__device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint32_t n_images, uint32_t gi,
+                                                  uint32_t n_rays_global, const ErrorCdf& cdf, int snap, pcg32& rng,
+                                                  float* uo, float* vo, float* pdf = nullptr) {
+	uint32_t img;
+	float img_pdf = 1.0f, uv_pdf = 1.0f;
+	if (cdf.img) {
+		img = cdf_search(ld_random_val(gi, 0xdeadbeefu), cdf.img, n_images);
+		img_pdf = (cdf.img[img] - (img > 0 ? cdf.img[img - 1] : 0.0f)) * (float)n_images;
+	} else {
+		img = image_idx(gi, n_rays_global, n_images);
+	}
+	const ngp_image& im = images[img];
 	float u = rng.next_float(), v = rng.next_float();
-	if (a.snap) {
+	if (cdf.x_cond_y) sample_cdf_2d(&u, &v, img, cdf, &uv_pdf);
+	if (pdf) *pdf = img_pdf * uv_pdf;
+	if (snap) {
 		int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
 		px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
 		py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
 		u = ((float)px + 0.5f) / (float)im.width;
 		v = ((float)py + 0.5f) / (float)im.height;
 	}
+	*uo = u;
+	*vo = v;
+	return img;
+}
+
+// Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777);
+// *n0 = first lattice point (stepping space) = entry + jitter.
+__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0) {
+	pcg32 rng = a.rng;
+	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
+	float u, v;
+	const uint32_t img = training_pixel(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v);
+	const ngp_image im = a.images[img];
 	float rgba[4];
 	texel_rgba(read_texel(im, u, v), rgba);
 	if (rgba[0] < 0.0f) return false;
@@ -271,6 +297,9 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 // ---------------------------------------------------------------------------
 struct LossArgs {
 	const ngp_image* images;
+	ErrorCdf cdf;
+	float* error_map;
+	uint32_t error_map_rx, error_map_ry;
 	uint32_t n_images;
 	uint32_t n_rays;
 	uint32_t n_rays_global;
@@ -382,16 +411,9 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	const uint32_t gi = a.ray_offset + i;
 	pcg32 rng = a.rng;
 	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
-	const uint32_t img = image_idx(gi, a.n_rays_global, a.n_images);
+	float u, v, pdf;
+	const uint32_t img = training_pixel(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v, &pdf);
 	const ngp_image im = a.images[img];
-	float u = rng.next_float(), v = rng.next_float();
-	if (a.snap) {
-		int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
-		px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
-		py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
-		u = ((float)px + 0.5f) / (float)im.width;
-		v = ((float)py + 0.5f) / (float)im.height;
-	}
 	rng.advance(1);  // motionblur_time
 	v3 bg = a.bg;
 	if (a.random_bg) {
@@ -424,9 +446,10 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	loss_and_gradient(target.y, rgb_ray.y, a.loss_type, &ly, &gy);
 	loss_and_gradient(target.z, rgb_ray.z, a.loss_type, &lz, &gz);
 	float* ls = a.loss_state + 8 * (size_t)i;
+	const float mean_loss = (lx / pdf + ly / pdf + lz / pdf) / 3.0f;  // lg.loss /= img_pdf * uv_pdf; mean(lg.loss)
 	ls[0] = gx; ls[1] = gy; ls[2] = gz;
 	ls[3] = rgb_ray.x; ls[4] = rgb_ray.y; ls[5] = rgb_ray.z;
-	ls[6] = (lx + ly + lz) / 3.0f;
+	ls[6] = mean_loss;
 	a.ccounts[i] = c;
 }
 
@@ -446,6 +469,29 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 	if (cn == 0) {
 		if (lane == 0) a.loss_out[i] = 0.0f;
 		return;
+	}
+	if (a.error_map && lane == 0) {
+		// bilinear deposit of the ray's mean loss (src/testbed_nerf.cu:1028-1054; rays without
+		// compacted samples returned before it); the corner clamp uses the image
+		// resolution, as the reference does
+		const uint32_t gi = a.ray_offset + i;
+		pcg32 rng = a.rng;
+		rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
+		float u, v;
+		const uint32_t img = training_pixel(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v);
+		const ngp_image& im = a.images[img];
+		const float mean_loss = a.loss_state[8 * (size_t)i + 6];
+		const float rx = (float)a.error_map_rx, ry = (float)a.error_map_ry;
+		const float px = fminf(fmaxf(u * rx - 0.5f, 0.0f), rx - (1.0f + 1e-4f));
+		const float py = fminf(fmaxf(v * ry - 0.5f, 0.0f), ry - (1.0f + 1e-4f));
+		const int ix = (int)px, iy = (int)py;
+		const float wx = px - (float)ix, wy = py - (float)iy;
+		const int cx = min(max(ix, 0), (int)im.width - 2), cy = min(max(iy, 0), (int)im.height - 2);
+		float* e = a.error_map + (size_t)img * a.error_map_rx * a.error_map_ry;
+		atomicAdd(&e[cy * a.error_map_rx + cx], (1.0f - wx) * (1.0f - wy) * mean_loss);
+		atomicAdd(&e[cy * a.error_map_rx + cx + 1], wx * (1.0f - wy) * mean_loss);
+		atomicAdd(&e[(cy + 1) * a.error_map_rx + cx], (1.0f - wx) * wy * mean_loss);
+		atomicAdd(&e[(cy + 1) * a.error_map_rx + cx + 1], wx * wy * mean_loss);
 	}
 	const uint32_t base = a.numsteps[2 * i + 1];
 	const float* ls = a.loss_state + 8 * (size_t)i;
@@ -646,6 +692,49 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 // ---------------------------------------------------------------------------
 // Host orchestration of one training step (Testbed::train_nerf_step).
 // ---------------------------------------------------------------------------
+// construct_cdf_2d (src/testbed_nerf.cu:1493-1521): one thread per (image, row)
+__global__ void __launch_bounds__(256) k_cdf_2d(uint32_t n_images, uint32_t height, uint32_t width,
+                                                const float* __restrict__ data, float* __restrict__ cdf_x_cond_y,
+                                                float* __restrict__ cdf_y) {
+	const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+	if (t >= n_images * height) return;
+	const uint32_t img = t / height, y = t % height;
+	const size_t off = ((size_t)img * height + y) * width;
+	float cum = 0.0f;
+	for (uint32_t x = 0; x < width; ++x) {
+		cum += data[off + x] + 1e-10f;
+		cdf_x_cond_y[off + x] = cum;
+	}
+	cdf_y[(size_t)img * height + y] = cum;
+	const float norm = 1.0f / cum;
+	for (uint32_t x = 0; x < width; ++x)
+		cdf_x_cond_y[off + x] = (1.0f - MIN_PDF) * cdf_x_cond_y[off + x] * norm + MIN_PDF * (float)(x + 1) / (float)width;
+}
+
+// construct_cdf_1d (src/testbed_nerf.cu:1523-1546): one thread per image
+__global__ void __launch_bounds__(256) k_cdf_1d(uint32_t n_images, uint32_t height, float* __restrict__ cdf_y,
+                                                float* __restrict__ cdf_img) {
+	const uint32_t img = blockIdx.x * 256u + threadIdx.x;
+	if (img >= n_images) return;
+	float* cy = cdf_y + (size_t)img * height;
+	float cum = 0.0f;
+	for (uint32_t y = 0; y < height; ++y) {
+		cum += cy[y];
+		cy[y] = cum;
+	}
+	cdf_img[img] = cum;
+	const float norm = 1.0f / cum;
+	for (uint32_t y = 0; y < height; ++y) cy[y] = (1.0f - MIN_PDF) * cy[y] * norm + MIN_PDF * (float)(y + 1) / (float)height;
+}
+
+void run_error_map_cdf(const float* error_map, uint32_t n_images, uint32_t rx, uint32_t ry, float* cdf_x_cond_y,
+                       float* cdf_y, float* cdf_img, hipStream_t s) {
+	if (n_images == 0 || rx == 0 || ry == 0) return;
+	k_cdf_2d<<<div_up((uint64_t)n_images * ry, 256), 256, 0, s>>>(n_images, ry, rx, error_map, cdf_x_cond_y, cdf_y);
+	k_cdf_1d<<<div_up(n_images, 256), 256, 0, s>>>(n_images, ry, cdf_y, cdf_img);
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
 void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	TrainScratch& ts = m->ts;
 	const uint32_t R = t->n_rays, B = t->target_batch_size, MS = t->max_samples;
@@ -689,6 +778,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.st = make_stepping(t->cone_angle_constant);
 	sa.max_mip = t->max_cascade;
 	sa.snap = t->snap_to_pixel_centers;
+	sa.cdf = ErrorCdf{t->cdf_x_cond_y, t->cdf_y, t->cdf_img, t->cdf_res[0], t->cdf_res[1]};
 	sa.bitfield = m->gs.bitfield.ptr;
 	sa.numsteps = ts.ray_numsteps.ptr;
 	sa.counts = counts.ptr;
@@ -723,6 +813,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.rng = sa.rng;
 	la.aabb = sa.aabb;
 	la.snap = t->snap_to_pixel_centers;
+	la.cdf = sa.cdf;
+	la.error_map = t->error_map;
+	la.error_map_rx = t->error_map_res[0];
+	la.error_map_ry = t->error_map_res[1];
 	la.loss_type = t->loss_type;
 	la.random_bg = t->random_bg_color;
 	la.bg = mk3(t->background_color[0], t->background_color[1], t->background_color[2]);

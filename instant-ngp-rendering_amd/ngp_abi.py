@@ -55,6 +55,8 @@ class TrainArgs(C.Structure):
         ("background_color", C.c_float * 3), ("snap_to_pixel_centers", C.c_int32),
         ("train_in_linear_colors", C.c_int32), ("color_space", C.c_int32), ("near_distance", C.c_float),
         ("optimize_mlp", C.c_int32), ("optimize_encoding", C.c_int32), ("defer_optimizer", C.c_int32),
+        ("error_map", C.c_void_p), ("error_map_res", C.c_uint32 * 2), ("cdf_x_cond_y", C.c_void_p),
+        ("cdf_y", C.c_void_p), ("cdf_img", C.c_void_p), ("cdf_res", C.c_uint32 * 2),
     ]
 
 
@@ -122,6 +124,8 @@ EXPORTS = {
     "ngp_density_grid_bitfield": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "ngp_density_grid_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                            C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "ngp_error_map_build_cdf": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p]),
     "ngp_render": (C.c_int, [C.c_void_p, C.POINTER(RenderArgs), C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngp_accumulate_tonemap": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                          C.c_int, C.c_float, C.POINTER(C.c_float), C.c_int, C.c_void_p]),

@@ -702,26 +702,77 @@ static void rgba_of(uint32_t t, float* o) {
 static uint32_t image_index(uint32_t i, uint32_t n_rays, uint32_t n_img) {
 	return (uint32_t)((((uint64_t)i) * n_img) / n_rays) % n_img;  // nerf_device.cuh:597
 }
-static void pixel_uv(Pcg& rng, const ngp_image& im, int snap, float* u, float* vv) {
-	*u = rng.nextf();
-	*vv = rng.nextf();
-	if (snap) {  // nerf_device.cuh:570-572
-		const int px = std::min(std::max((int)(*u * (float)im.width), 0), (int)im.width - 1);
-		const int py = std::min(std::max((int)(*vv * (float)im.height), 0), (int)im.height - 1);
-		*u = ((float)px + 0.5f) / (float)im.width;
-		*vv = ((float)py + 0.5f) / (float)im.height;
+// binary_search (common.h:207-230): first index with data[i] >= val, clamped to length-1
+static uint32_t cdf_search(float val, const float* data, uint32_t length) {
+	if (length == 0) return 0;
+	uint32_t first = 0, count = length;
+	while (count > 0) {
+		const uint32_t step = count / 2, it = first + step;
+		if (data[it] < val) {
+			first = it + 1;
+			count -= step + 1;
+		} else {
+			count = step;
+		}
 	}
+	return std::min(first, length - 1);
+}
+
+
+// image_idx + nerf_random_image_pos_training with the error-map CDFs (nerf_device.cuh:495-598);
+// *pdf = img_pdf * uv_pdf (uv_pdf stays 1 on the uniform half of sample_cdf_2d).
+static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, Pcg& rng, float* u, float* vv, float* pdf) {
+	uint32_t img;
+	float img_pdf = 1.0f, uv_pdf = 1.0f;
+	if (a.cdf_img) {
+		img = cdf_search(ldval(gi, 0xdeadbeefu, 0), a.cdf_img, a.n_images);  // ld_random_val (random_val.cuh:287-291)
+		img_pdf = (a.cdf_img[img] - (img > 0 ? a.cdf_img[img - 1] : 0.0f)) * (float)a.n_images;
+	} else {
+		img = image_index(gi, nrg, a.n_images);
+	}
+	const ngp_image& im = a.images[img];
+	float x = rng.nextf(), y = rng.nextf();
+	if (a.cdf_x_cond_y) {
+		const uint32_t rx = a.cdf_res[0], ry = a.cdf_res[1];
+		if (x < 0.5f) {
+			x = x * 2.0f;
+		} else {
+			const float su = (x - 0.5f) * 2.0f;
+			const float* cy = a.cdf_y + (size_t)img * ry;
+			const uint32_t yi = cdf_search(y, cy, ry);
+			float prev = yi > 0 ? cy[yi - 1] : 0.0f;
+			const float pmf_y = cy[yi] - prev;
+			const float sv = (y - prev) / pmf_y;
+			const float* cx = a.cdf_x_cond_y + ((size_t)img * ry + yi) * rx;
+			const uint32_t xi = cdf_search(su, cx, rx);
+			prev = xi > 0 ? cx[xi - 1] : 0.0f;
+			const float pmf_x = cx[xi] - prev;
+			const float sx = (su - prev) / pmf_x;
+			uv_pdf = pmf_x * pmf_y * (float)(rx * ry);
+			x = ((float)xi + sx) / (float)rx;
+			y = ((float)yi + sv) / (float)ry;
+		}
+	}
+	if (a.snap_to_pixel_centers) {  // nerf_device.cuh:570-572
+		const int px = std::min(std::max((int)(x * (float)im.width), 0), (int)im.width - 1);
+		const int py = std::min(std::max((int)(y * (float)im.height), 0), (int)im.height - 1);
+		x = ((float)px + 0.5f) / (float)im.width;
+		y = ((float)py + 0.5f) / (float)im.height;
+	}
+	*u = x;
+	*vv = y;
+	if (pdf) *pdf = img_pdf * uv_pdf;
+	return img;
 }
 
 // generate_training_samples_nerf (src/testbed_nerf.cu:679-838), per-ray.
 static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st) {
-	const ngp_image& im = a.images[image_index(gi, nrg, a.n_images)];
 	Pcg rng;
 	rng.state = a.rng_state;
 	rng.inc = a.rng_inc;
 	rng.advance((int64_t)gi * 16);
 	float u, vv;
-	pixel_uv(rng, im, a.snap_to_pixel_centers, &u, &vv);
+	const ngp_image& im = a.images[pick_pixel(a, gi, nrg, rng, &u, &vv, nullptr)];
 	float rgba[4];
 	rgba_of(texel(im, u, vv), rgba);
 	if (rgba[0] < 0.0f) return false;
@@ -836,9 +887,8 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		rng.state = a.rng_state;
 		rng.inc = a.rng_inc;
 		rng.advance((int64_t)gi * 16);
-		const ngp_image& im = a.images[image_index(gi, nrg, a.n_images)];
-		float u, vv;
-		pixel_uv(rng, im, a.snap_to_pixel_centers, &u, &vv);
+		float u, vv, pdf;
+		const ngp_image& im = a.images[pick_pixel(a, gi, nrg, rng, &u, &vv, &pdf)];
 		rng.advance(1);
 		V3 bg = v(a.background_color[0], a.background_color[1], a.background_color[2]);
 		if (a.random_bg_color) {
@@ -865,7 +915,8 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		lossg(tgt.y, rg, a.loss_type, &ly, &gy);
 		lossg(tgt.z, rb, a.loss_type, &lz, &gz);
 		float* ls = &lstate[8 * (size_t)i];
-		ls[0] = gx; ls[1] = gy; ls[2] = gz; ls[3] = rr; ls[4] = rg; ls[5] = rb; ls[6] = (lx + ly + lz) / 3.0f;
+		ls[0] = gx; ls[1] = gy; ls[2] = gz; ls[3] = rr; ls[4] = rg; ls[5] = rb;
+		ls[6] = (lx / pdf + ly / pdf + lz / pdf) / 3.0f;  // lg.loss /= img_pdf * uv_pdf (src/testbed_nerf.cu:1010)
 		cc[i] = c;
 	}
 	M.ray_compacted.assign(2 * (size_t)R, 0);
@@ -886,6 +937,28 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		if (cn == 0) continue;
 		const float* ls = &lstate[8 * (size_t)i];
 		M.loss[i] = ls[6] / (float)nrg;
+		if (a.error_map) {  // bilinear error deposit (src/testbed_nerf.cu:1028-1054)
+			const uint32_t gi = a.ray_index_offset + i;
+			Pcg rng;
+			rng.state = a.rng_state;
+			rng.inc = a.rng_inc;
+			rng.advance((int64_t)gi * 16);
+			float u, vv;
+			const uint32_t img = pick_pixel(a, gi, nrg, rng, &u, &vv, nullptr);
+			const ngp_image& im = a.images[img];
+			const uint32_t ex = a.error_map_res[0], ey = a.error_map_res[1];
+			const float px = std::min(std::max(u * (float)ex - 0.5f, 0.0f), (float)ex - (1.0f + 1e-4f));
+			const float py = std::min(std::max(vv * (float)ey - 0.5f, 0.0f), (float)ey - (1.0f + 1e-4f));
+			const int ix = (int)px, iy = (int)py;
+			const float wx = px - (float)ix, wy = py - (float)iy;
+			const int cx = std::min(std::max(ix, 0), (int)im.width - 2), cy = std::min(std::max(iy, 0), (int)im.height - 2);
+			float* e = a.error_map + (size_t)img * ex * ey;
+			const float ml = ls[6];
+			e[cy * ex + cx] += (1.0f - wx) * (1.0f - wy) * ml;
+			e[cy * ex + cx + 1] += wx * (1.0f - wy) * ml;
+			e[(cy + 1) * ex + cx] += (1.0f - wx) * wy * ml;
+			e[(cy + 1) * ex + cx + 1] += wx * wy * ml;
+		}
 		const uint32_t b0 = M.ray_numsteps[2 * i + 1];
 		const V3 o = ro[i];
 		float T = 1.0f, r2 = 0, g2 = 0, b2 = 0;
@@ -1150,6 +1223,45 @@ void oref_pcg32_floats_advanced(uint64_t state, uint64_t inc, int64_t adv, uint3
 	for (uint32_t i = 0; i < n; ++i) out[i] = r.nextf();
 }
 float oref_ld_random_val(uint32_t index, uint32_t seed, uint32_t dim) { return ldval(index, seed, dim); }
+
+// the training ray's image and pixel (image_idx + nerf_random_image_pos_training, with the
+// error-map CDFs when given) -- exposed for the sampling tests
+uint32_t oref_pick_pixel(const ngp_train_args* a, uint32_t gi, float* u, float* v, float* pdf) {
+	Pcg rng;
+	rng.state = a->rng_state;
+	rng.inc = a->rng_inc;
+	rng.advance((int64_t)gi * 16);
+	return pick_pixel(*a, gi, a->n_rays_global ? a->n_rays_global : a->n_rays, rng, u, v, pdf);
+}
+
+// construct_cdf_2d / construct_cdf_1d (src/testbed_nerf.cu:1493-1546), host arrays
+void oref_error_map_build_cdf(const float* data, uint32_t n_images, uint32_t rx, uint32_t ry, float* cdf_x_cond_y,
+                              float* cdf_y, float* cdf_img) {
+	const float MIN_PDF = 0.01f;
+	for (uint32_t img = 0; img < n_images; ++img) {
+		for (uint32_t y = 0; y < ry; ++y) {
+			const size_t off = ((size_t)img * ry + y) * rx;
+			float cum = 0.0f;
+			for (uint32_t x = 0; x < rx; ++x) {
+				cum += data[off + x] + 1e-10f;
+				cdf_x_cond_y[off + x] = cum;
+			}
+			cdf_y[(size_t)img * ry + y] = cum;
+			const float norm = 1.0f / cum;
+			for (uint32_t x = 0; x < rx; ++x)
+				cdf_x_cond_y[off + x] = (1.0f - MIN_PDF) * cdf_x_cond_y[off + x] * norm + MIN_PDF * (float)(x + 1) / (float)rx;
+		}
+		float* cy = cdf_y + (size_t)img * ry;
+		float cum = 0.0f;
+		for (uint32_t y = 0; y < ry; ++y) {
+			cum += cy[y];
+			cy[y] = cum;
+		}
+		cdf_img[img] = cum;
+		const float norm = 1.0f / cum;
+		for (uint32_t y = 0; y < ry; ++y) cy[y] = (1.0f - MIN_PDF) * cy[y] * norm + MIN_PDF * (float)(y + 1) / (float)ry;
+	}
+}
 uint32_t oref_sobol(uint32_t index, uint32_t dim) { return sobol(index, dim); }
 uint32_t oref_morton3D(uint32_t x, uint32_t y, uint32_t z) { return morton(x, y, z); }
 void oref_sh4(const float* wdir, float* out) { sh4(wdir, out); }

@@ -238,3 +238,70 @@ def test_render_floaters_matches_oracle(aabb_scale):
         assert l1 < 1e-3, l1
     finally:
         g.close()
+
+
+def test_error_map_cdf_matches_oracle():
+    from oracle_abi import load, ptr
+    rng = np.random.default_rng(11)
+    err = rng.exponential(1.0, (6, 9, 14)).astype(np.float32)
+    d_err = torch.from_numpy(err).cuda()
+    d_cx, d_cy, d_ci = torch.zeros_like(d_err), torch.zeros(6, 9, device="cuda"), torch.zeros(6, device="cuda")
+    lib = A.load()
+    A.check(lib.ngp_error_map_build_cdf(C.c_void_p(d_err.data_ptr()), 6, 14, 9, C.c_void_p(d_cx.data_ptr()),
+                                        C.c_void_p(d_cy.data_ptr()), C.c_void_p(d_ci.data_ptr()), stream()))
+    torch.cuda.synchronize()
+    cx, cy, ci = np.zeros_like(err), np.zeros((6, 9), np.float32), np.zeros(6, np.float32)
+    load().oref_error_map_build_cdf(ptr(err), 6, 14, 9, ptr(cx), ptr(cy), ptr(ci))
+    np.testing.assert_allclose(d_cx.cpu().numpy(), cx, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(d_cy.cpu().numpy(), cy, rtol=1e-6, atol=1e-7)
+    np.testing.assert_allclose(d_ci.cpu().numpy(), ci, rtol=1e-6)
+
+
+def test_train_step_error_map_matches_oracle():
+    """Importance sampling from error-map CDFs (image and pixel) is bit-exact against the
+    oracle (sample counts and coordinates), and the error deposits agree within the fp16
+    network tolerance."""
+    from error_map_util import build_cdf_numpy, normalise_image_cdf
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        emap = rng.exponential(1.0, (6, 5, 7)).astype(np.float32)
+        emap[1] *= 20.0
+        cx, cy, tot = build_cdf_numpy(emap)
+        _, cimg = normalise_image_cdf(tot)
+        R, B, MS = 384, 4096, 1 << 15
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        d_cx, d_cy, d_ci = (torch.from_numpy(x).cuda() for x in (cx, cy, cimg))
+        d_err = torch.zeros(6, 8, 8, device="cuda")
+        h_err = np.zeros((6, 8, 8), np.float32)
+        ga.cdf_x_cond_y, ga.cdf_y, ga.cdf_img = d_cx.data_ptr(), d_cy.data_ptr(), d_ci.data_ptr()
+        oa.cdf_x_cond_y, oa.cdf_y, oa.cdf_img = cx.ctypes.data, cy.ctypes.data, cimg.ctypes.data
+        ga.error_map, oa.error_map = d_err.data_ptr(), h_err.ctypes.data
+        for a in (ga, oa):
+            a.cdf_res[0], a.cdf_res[1] = 7, 5
+            a.error_map_res[0], a.error_map_res[1] = 8, 8
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+        g_ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        o_ns = o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        np.testing.assert_array_equal(g_ns, o_ns)
+        owned = np.zeros(MS, bool)
+        for n, b in o_ns:
+            owned[b:b + n] = True
+        assert owned.sum() > 1000
+        g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
+        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
+        np.testing.assert_array_equal(g_c, o_c)
+        ge = d_err.cpu().numpy()
+        assert h_err.sum() > 0
+        assert np.abs(ge - h_err).sum() / h_err.sum() < 3e-2
+        gst = A.TrainStats()
+        A.check(g.lib.ngp_train_read_stats(g.h, C.byref(gst), stream()))
+        np.testing.assert_allclose(gst.loss, o.stats().loss, rtol=2e-2)
+    finally:
+        g.close()

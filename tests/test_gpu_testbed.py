@@ -147,3 +147,30 @@ def test_errors_are_loud():
     tb.shall_train = True
     tb.train(1 << 18)  # no usable data: the reference clears shall_train and returns (src/testbed.cu:4021-4024)
     assert not tb.shall_train
+
+
+def test_error_map_importance_sampling(scene):
+    """The error map accumulates every step; after n_steps_between_error_map_updates its CDFs
+    drive image / pixel sampling (src/testbed_nerf.cu:2486-2575) and training still converges."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    tr = tb.nerf.training
+    tr.n_steps_between_error_map_updates = 16
+    tr.sample_focal_plane_proportional_to_error = True
+    tr.sample_image_proportional_to_error = True
+    tb.shall_train = True
+    while tb.training_step < 15:
+        tb.frame()
+    em = tr.error_map
+    assert em.shape[0] == 12 and em.shape[1] == em.shape[2] and em.sum() > 0 and not tr.error_map_cdf_valid
+    losses = []
+    while tb.training_step < 300:
+        tb.frame()
+        losses.append(tb.loss)
+    assert tr.error_map_cdf_valid
+    pmf = np.asarray(tr.error_map_pmf_img)
+    assert pmf.shape == (12,) and abs(pmf.sum() - 1.0) < 1e-4 and pmf.min() >= 0.1 / 12 - 1e-6
+    assert tr.n_steps_between_error_map_updates > 16  # grows x1.5 per update
+    assert np.isfinite(losses).all() and np.mean(losses[-16:]) < 0.6 * np.mean(losses[:16])
