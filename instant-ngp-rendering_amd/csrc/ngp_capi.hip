@@ -214,6 +214,8 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		for (int b = 0; b < 3; ++b) { r.payload[b].release(); r.rgba[b].release(); r.depth[b].release(); }
 		r.coords.release(); r.enc.release(); r.out.release(); r.counters.release(); r.summary.release();
 		if (r.host_counter.ptr) (void)hipHostFree(r.host_counter.ptr);
+		for (auto& e : r.events)
+			if (e) (void)hipEventDestroy(e);
 		m->timers.release();
 		delete m;
 	});

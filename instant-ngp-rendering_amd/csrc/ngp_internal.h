@@ -171,6 +171,7 @@ struct RenderScratch {
 	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
+	hipEvent_t events[2] = {nullptr, nullptr};  // per-pass counter read-backs
 	uint64_t df_version = ~0ull;
 	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;

@@ -329,11 +329,20 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 // early passes (one lane per ray, flat loop), up to 64 for the last few thousand rays,
 // whose long serial marches otherwise dominate the tail passes.
 template <uint32_t G>
-__global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, Payload* __restrict__ payloads,
-                                                  const float4* __restrict__ rgba, float* __restrict__ coords,
-                                                  uint32_t n_steps, uint32_t* __restrict__ next_alive_counter,
-                                                  uint32_t* __restrict__ sample_counter) {
-	if (blockIdx.x == 0 && threadIdx.x == 0) *next_alive_counter = 0;  // filled by this pass's k_composite
+__global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
+                                                  Payload* __restrict__ payloads, const float4* __restrict__ rgba,
+                                                  float* __restrict__ coords, uint32_t target, uint32_t max_steps,
+                                                  uint32_t* __restrict__ next_alive_counter,
+                                                  uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out) {
+	// the pass is sized on the device: the host enqueues passes ahead of their read-backs
+	const uint32_t n_alive = *alive_counter;
+	// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
+	// every ray composites its own samples in order and stops at the same one whatever the chunking
+	const uint32_t n_steps = min(max(target / max(n_alive, 1u), 1u), max_steps);
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		*next_alive_counter = 0;  // filled by this pass's k_composite
+		*steps_out = n_alive ? n_steps : 0u;
+	}
 	const uint8_t* summary = k.df ? nullptr : stage_summary(k.summary, k.max_mip);
 	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
@@ -425,7 +434,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, uint32_t n_alive, P
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
-__global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive,
+__global__ void __launch_bounds__(256) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                    const float* __restrict__ sdepth, const float* __restrict__ coords,
                                                    const __half* __restrict__ out,
@@ -435,6 +444,7 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, uint32_t n_alive,
                                                    uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter,
                                                    uint32_t* __restrict__ next_sample_counter) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
+	const uint32_t n_alive = *alive_in;
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	Payload p;
 	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -654,8 +664,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.dbg = debug ? rs.counters.ptr + 8 : nullptr;
 	if (debug) NGP_HIP_CHECK(hipMemsetAsync(k.dbg, 0, 8 * sizeof(uint32_t), s));
 	if (!rs.host_counter.ptr) {
-		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 4 * sizeof(uint32_t), hipHostMallocDefault));
-		rs.host_counter.n = 4;
+		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 16 * sizeof(uint32_t), hipHostMallocDefault));
+		rs.host_counter.n = 16;
 	}
 	auto P = [&](int b) { return reinterpret_cast<Payload*>(rs.payload[b].ptr); };
 	auto C = [&](int b) { return reinterpret_cast<float4*>(rs.rgba[b].ptr); };
@@ -680,41 +690,58 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
-	NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 2 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-	wait_stream(m, s);
-	uint32_t n_alive = rs.host_counter.ptr[0];
 
-	// NerfTracer::trace (testbed_nerf.cu:1639-1755): generate -> infer -> composite -> compact,
+	// NerfTracer::trace (testbed_nerf.cu:1639-1755): generate -> infer -> composite(+compact),
 	// alive rays ping-pong between buffers 0/1, finished rays with colour append to buffer 2.
+	// Counters (device): [0]/[1] alive rays in/out, [2] finished rays, [4]/[5] sample slots,
+	// [6]/[7] samples per ray of the pass.  The host does not wait for a pass before
+	// enqueuing the next: kernels read the counts from the device, and launches are sized by
+	// the count read back one pass earlier (alive counts only shrink).  The loop stops once a
+	// read-back shows no alive rays (the pass enqueued meanwhile runs empty).
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
+	const uint32_t target = 2 * 1024 * 1024, cap = max_steps_per_pass();
+	if (!rs.events[0]) {
+		for (auto& e : rs.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+	}
+	uint32_t* hc = rs.host_counter.ptr;  // pinned [2 slots][8]
+	auto read_back = [&](uint32_t pass) {
+		uint32_t* slot = hc + 8 * (pass % 2);
+		NGP_HIP_CHECK(hipMemcpyAsync(slot, rs.counters.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipEventRecord(rs.events[pass % 2], s));
+	};
+	auto wait_slot = [&](uint32_t pass) -> const uint32_t* {
+		hipError_t e;
+		while ((e = hipEventQuery(rs.events[pass % 2])) == hipErrorNotReady) {
+		}
+		NGP_HIP_CHECK(e);
+		return hc + 8 * (pass % 2);
+	};
 	int cur = 0;
-	uint32_t pass = 0, n_hit = 0;
+	uint32_t pass = 0, steps_done = 0;
+	uint32_t n_alive_ub = n;  // upper bound on the alive rays entering the next pass
 	const uint32_t MARCH_ITER = 10000;
-	for (uint32_t it = 1; it < MARCH_ITER && n_alive > 0;) {
-		const uint32_t target = 2 * 1024 * 1024;
-		// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
-		// every ray composites its own samples in order and stops at the same one whatever the chunking
-		const uint32_t n_steps = std::min<uint32_t>(std::max<uint32_t>(target / n_alive, 1u), max_steps_per_pass());
+	while (true) {
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		// alive counters alternate between counters[0] and [1]: the host has already read the
-		// one this pass overwrites; counters[2] accumulates the finished rays with colour
+		uint32_t* alive_in = rs.counters.ptr + pass % 2;
 		uint32_t* alive_out = rs.counters.ptr + (pass + 1) % 2;
-		// lanes per ray: enough rays in flight for ~64k lanes, never fewer than one lane per ray
-		const uint32_t want = lanes_target() / std::max(n_alive, 1u);
-		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
-		const uint32_t gblocks = div_up((uint64_t)n_alive * G, 256);
 		uint32_t* samples = rs.counters.ptr + 4 + pass % 2;  // zeroed by the previous kernel of the chain
 		uint32_t* samples_next = rs.counters.ptr + 4 + (pass + 1) % 2;
+		uint32_t* steps_out = rs.counters.ptr + 6 + pass % 2;
+		// lanes per ray: enough rays in flight for ~1M lanes, never fewer than one lane per ray
+		const uint32_t want = lanes_target() / std::max(n_alive_ub, 1u);
+		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
+		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 256));
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
-			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
-			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
-			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, n_alive, P(cur), C(cur), rs.coords.ptr, n_steps, alive_out, samples); break;
+			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
+			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
+			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
+			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
-		const uint32_t n_elements = next_multiple(n_alive * n_steps, BATCH_SIZE_GRANULARITY);
+		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap, std::max(target, n_alive_ub));
+		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
 		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s, n_elements);
@@ -722,26 +749,32 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s, samples);
 		tm.end(NGP_TIMER_RENDER_MLP, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_composite<<<div_up(n_alive, 256), 256, 0, s>>>(k, n_alive, P(cur), C(cur), rs.depth[cur].ptr, rs.coords.ptr,
-		                                                 rs.out.ptr, P(1 - cur), C(1 - cur), rs.depth[1 - cur].ptr,
-		                                                 P(2), C(2), rs.depth[2].ptr, alive_out, rs.counters.ptr + 2, samples_next);
+		k_composite<<<std::max(1u, div_up(n_alive_ub, 256)), 256, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
+		                                                                  rs.coords.ptr, rs.out.ptr, P(1 - cur), C(1 - cur),
+		                                                                  rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr,
+		                                                                  alive_out, rs.counters.ptr + 2, samples_next);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
-		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		wait_stream(m, s);
-		n_alive = rs.host_counter.ptr[(pass + 1) % 2];
-		n_hit = rs.host_counter.ptr[2];
+		read_back(pass);
 		cur = 1 - cur;
-		it += n_steps;
 		++pass;
+		// the read-back of the previous pass bounds the next one
+		if (pass >= 2) {
+			const uint32_t* c = wait_slot(pass - 2);
+			steps_done += c[6 + (pass - 2) % 2];
+			n_alive_ub = std::min(n_alive_ub, c[(pass - 1) % 2]);
+			if (n_alive_ub == 0 || steps_done >= MARCH_ITER) break;
+		}
 	}
+	const uint32_t* last = wait_slot(pass - 1);
+	uint32_t n_alive = last[pass % 2];
+	uint32_t n_hit = last[2];
 	if (n_alive > 0) {
 		// march budget exhausted: still-alive rays are shaded with what they accumulated
 		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,
 		                                              rs.counters.ptr);
-		NGP_HIP_CHECK(hipMemcpyAsync(rs.host_counter.ptr, rs.counters.ptr, 4 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		wait_stream(m, s);
-		n_hit = rs.host_counter.ptr[2];
+		read_back(pass);
+		n_hit = wait_slot(pass)[2];
 	}
 	if (debug) {
 		uint32_t d[8];
