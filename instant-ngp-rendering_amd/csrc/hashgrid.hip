@@ -56,7 +56,10 @@ __device__ __forceinline__ uint32_t grid_index(uint32_t hashed, uint32_t size, u
                                                uint32_t z) {
 	if (hashed) return ((x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u)) & (size - 1u);
 	const uint32_t idx = x + y * res + z * res * res;
-	return idx >= size ? idx - size : idx;
+	// tcnn: index % size.  Positions in [0, 1] overshoot by less than one table size (the
+	// +1 corners), so one subtraction suffices; the modulo keeps any other input in range.
+	if (idx < size) return idx;
+	return idx - size < size ? idx - size : idx % size;
 }
 
 template <uint32_t F>
@@ -92,7 +95,10 @@ template <bool HASHED>
 __device__ __forceinline__ uint32_t corner_index(uint32_t size, uint32_t res, uint32_t x, uint32_t y, uint32_t z) {
 	if (HASHED) return ((x * 1u) ^ (y * 2654435761u) ^ (z * 805459861u)) & (size - 1u);
 	const uint32_t idx = x + y * res + z * res * res;
-	return idx >= size ? idx - size : idx;
+	// tcnn: index % size.  Positions in [0, 1] overshoot by less than one table size (the
+	// +1 corners), so one subtraction suffices; the modulo keeps any other input in range.
+	if (idx < size) return idx;
+	return idx - size < size ? idx - size : idx % size;
 }
 
 // The 8 corner entries of a cell, all loads issued before any is consumed.  x-pairs share

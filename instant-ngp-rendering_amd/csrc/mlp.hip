@@ -131,6 +131,7 @@ struct MlpArgs {
 	uint32_t param_in[MAX_LAYERS];
 	const uint32_t* n_dev;  // optional device-side sample count (<= n)
 	uint32_t enc_bytes, coord_bytes;  // buffer-resource extents (register-resident inference)
+	uint32_t dir_offset;              // float offset of the direction in a coords record
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -400,7 +401,7 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 			}
 		}
 		if (want_dir) {
-			const uint32_t o = 4 * (i * a.coord_stride + 4);
+			const uint32_t o = 4 * (i * a.coord_stride + a.dir_offset);
 			r.d[c][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o, 0, 0));
 			r.d[c][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o + 4, 0, 0));
 			r.d[c][2] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o + 8, 0, 0));
@@ -927,7 +928,7 @@ static void set_lds(K kernel, size_t bytes) {
 
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev) {
+                      const uint32_t* n_dev, uint32_t dir_offset) {
 	if (n == 0) return;
 	MlpArgs a = base_args(m);
 	a.frags = frags;
@@ -940,6 +941,7 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.n_dev = n_dev;
 	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_plane * 2, 0xffffffffu);
 	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * coord_stride * 4, 0xffffffffu);
+	a.dir_offset = dir_offset;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);

@@ -132,6 +132,8 @@ struct TrainScratch {
 	DevBuf<__half> enc;                // [L][max_samples][F]
 	DevBuf<__half> mlp_out;            // [max_samples][4]
 	DevBuf<float> ccoords;             // [B][8] compacted
+	DevBuf<float> pos4;                // [max_samples][4]: pos + dt rows for the encoder
+	DevBuf<float> cpos4;               // [B][4] compacted, for the encoder backward
 	DevBuf<__half> cenc;               // [L][B][F]
 	DevBuf<__half> dloss;              // [B][4]
 	DevBuf<float> cweight;             // [B] rollover multiplicity
@@ -233,9 +235,11 @@ void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t st
 int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad);
 uint32_t mlp_frag_halves(const ngp_model* m);
 void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s);
+// coords: per-sample records of coord_stride floats holding the warped direction at
+// dir_offset (NerfCoordinate: 4; the renderer's separate direction rows: 0)
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev = nullptr);
+                      const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4);
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
 void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,

@@ -331,7 +331,8 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 template <uint32_t G>
 __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
-                                                  float* __restrict__ coords, uint32_t target, uint32_t max_steps,
+                                                  float4* __restrict__ posdt, float4* __restrict__ dirs,
+                                                  uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out) {
 	// the pass is sized on the device: the host enqueues passes ahead of their read-backs
@@ -389,9 +390,9 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __r
 				const float t = step_from(k.st, pn);
 				const float dt = step_from(k.st, pn + 1.0f) - t;
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
-				float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)base + j + rank));
-				c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+				const size_t slot = (size_t)base + j + rank;
+				posdt[slot] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+				dirs[slot] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
 			}
 		}
 		if (cnt >= room) {
@@ -414,9 +415,8 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __r
 		// reserved slots the ray did not fill (it left the volume) still go through the
 		// encoder: give them an in-range position
 		for (uint32_t q = j + r; q < budget; q += G) {
-			float4* c = reinterpret_cast<float4*>(coords + 8 * ((size_t)base + q));
-			c[0] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
-			c[1] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+			posdt[(size_t)base + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+			dirs[(size_t)base + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 		}
 	}
 	if (k.dbg && valid && r == 0) {
@@ -436,7 +436,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __r
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
 __global__ void __launch_bounds__(256) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
-                                                   const float* __restrict__ sdepth, const float* __restrict__ coords,
+                                                   const float* __restrict__ sdepth, const float4* __restrict__ posdt,
                                                    const __half* __restrict__ out,
                                                    Payload* __restrict__ dp, float4* __restrict__ drgba,
                                                    float* __restrict__ ddepth, Payload* __restrict__ hp,
@@ -473,7 +473,7 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, const uint32_t* __
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
-					crd[u] = *reinterpret_cast<const float4*>(coords + 8 * s);
+					crd[u] = posdt[s];
 				}
 			}
 #pragma unroll
@@ -656,7 +656,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		rs.rgba[b].reserve((size_t)n * 4);
 		rs.depth[b].reserve(n);
 	}
-	rs.coords.reserve(8 * max_samples);
+	rs.coords.reserve(8 * max_samples);  // [0, 4*max): pos + warped dt rows, [4*max, 8*max): direction rows
 	rs.enc.reserve((size_t)m->lt.n_levels * max_samples * m->lt.F);
 	rs.out.reserve(4 * max_samples);
 	rs.counters.reserve(16);
@@ -705,6 +705,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		for (auto& e : rs.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 	}
 	uint32_t* hc = rs.host_counter.ptr;  // pinned [2 slots][8]
+	// sample records in two row arrays: the encoder reads 16-B position rows once per level
+	float4* posdt = reinterpret_cast<float4*>(rs.coords.ptr);
+	float4* dirs = posdt + max_samples;
 	auto read_back = [&](uint32_t pass) {
 		uint32_t* slot = hc + 8 * (pass % 2);
 		NGP_HIP_CHECK(hipMemcpyAsync(slot, rs.counters.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -733,24 +736,25 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
 		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 256));
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
-			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
-			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
-			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), rs.coords.ptr, target, cap, alive_out, samples, steps_out); break;
+			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
+			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
+			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
+			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
 		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap, std::max(target, n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
-		launch_hashgrid_fwd(m->lt, rs.coords.ptr, 8, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
+		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MLP, s);
-		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, rs.coords.ptr, 8, n_elements, rs.out.ptr, s, samples);
+		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, reinterpret_cast<const float*>(dirs), 4, n_elements, rs.out.ptr, s,
+		                 samples, 0);
 		tm.end(NGP_TIMER_RENDER_MLP, s, n_elements);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<std::max(1u, div_up(n_alive_ub, 256)), 256, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
-		                                                                  rs.coords.ptr, rs.out.ptr, P(1 - cur), C(1 - cur),
+		                                                                  posdt, rs.out.ptr, P(1 - cur), C(1 - cur),
 		                                                                  rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr,
 		                                                                  alive_out, rs.counters.ptr + 2, samples_next);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);

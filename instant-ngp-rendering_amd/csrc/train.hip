@@ -143,6 +143,7 @@ struct SamplerArgs {
 	uint32_t* bases;     // [R]
 	float* ray_state;    // [R][8]
 	float* coords;       // [max][8]
+	float4* pos4;        // [max]: pos + warped dt again, 16-B rows the encoder reads once per level
 };
 
 // Image and pixel of global training ray gi from its pcg32 stream (already advanced to
@@ -283,8 +284,10 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 			if (r < n) {
 				const v3 wp = aabb_relative(a.aabb, p.pos);
 				float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + r));
-				c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
+				const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
+				c[0] = pd;
 				c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+				a.pos4[base + r] = pd;
 			}
 		}
 		j += __popcll(m);
@@ -549,14 +552,16 @@ template <uint32_t F>
 __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ csrc,
                                                           const float* __restrict__ coords, const __half* __restrict__ enc,
                                                           uint32_t enc_plane, uint32_t n_levels, float* __restrict__ ccoords,
-                                                          __half* __restrict__ cenc, uint32_t target) {
+                                                          float4* __restrict__ cpos4, __half* __restrict__ cenc, uint32_t target) {
 	const uint32_t dst = blockIdx.x * 256u + threadIdx.x;
 	if (dst >= *n_ptr) return;
 	const uint32_t src = csrc[dst];
 	const float4* ci = reinterpret_cast<const float4*>(coords + 8 * (size_t)src);
 	float4* co = reinterpret_cast<float4*>(ccoords + 8 * (size_t)dst);
-	co[0] = ci[0];
+	const float4 c0 = ci[0];
+	co[0] = c0;
 	co[1] = ci[1];
+	cpos4[dst] = c0;
 	using VT = typename std::conditional<F == 1, uint16_t, typename std::conditional<F == 2, uint32_t,
 	                                     typename std::conditional<F == 4, uint2, uint4>::type>::type>::type;
 	const VT* es = reinterpret_cast<const VT*>(enc);
@@ -748,6 +753,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.enc.reserve((size_t)L * MS * F);
 	ts.mlp_out.reserve(4 * (size_t)MS);
 	ts.ccoords.reserve(8 * (size_t)B);
+	ts.pos4.reserve(4 * (size_t)MS);
+	ts.cpos4.reserve(4 * (size_t)B);
 	ts.cenc.reserve((size_t)L * B * F);
 	ts.dloss.reserve(4 * (size_t)B);
 	ts.cweight.reserve(B);
@@ -785,6 +792,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.bases = counts.ptr + R;
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
+	sa.pos4 = reinterpret_cast<float4*>(ts.pos4.ptr);
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
 	k_sample_count<<<div_up(R, 4), 256, 0, s>>>(sa);
@@ -796,7 +804,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 
 	// network inference over every emitted sample (NerfNetwork::inference_mixed_precision, training params)
 	tm.begin(NGP_TIMER_TRAIN_ENCODE, s);
-	launch_hashgrid_fwd(m->lt, ts.coords.ptr, 8, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
+	launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
 	                    ts.counters.ptr + 4, 0);
 	tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 	tm.begin(NGP_TIMER_TRAIN_MLP_INFER, s);
@@ -852,10 +860,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// compacted batch size c = min(total, B); rollover multiplicity
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
 	switch (F) {
-		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
-		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
-		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
-		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, ts.cenc.ptr, B); break;
+		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
+		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
+		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
+		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
 	}
 	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
@@ -867,7 +875,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
 	tm.begin(NGP_TIMER_TRAIN_ENCODE_BWD, s);
-	launch_hashgrid_bwd(m->lt, ts.ccoords.ptr, 8, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
+	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	tm.train_units_pending = tm.mask != 0;
