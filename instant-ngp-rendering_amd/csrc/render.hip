@@ -609,7 +609,7 @@ static uint32_t lanes_target() {
 static uint32_t max_steps_per_pass() {
 	const char* e = getenv("NGP_RENDER_STEPS_PER_PASS");
 	const int v = e ? atoi(e) : 0;
-	return v > 0 ? (uint32_t)v : 32u;
+	return v > 0 ? (uint32_t)v : 16u;
 }
 
 void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s) {
@@ -672,11 +672,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
-	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (off by default: with one
-	// host read-back per pass the extra passes cost what the saved samples gain)
+	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (default 1.5) or "off"
 	static const char* budget_env = getenv("NGP_RENDER_BUDGET");
-	k.budget = budget_env && strcmp(budget_env, "off") != 0;
-	k.budget_scale = k.budget ? (float)atof(budget_env) : 1.5f;
+	k.budget = !(budget_env && strcmp(budget_env, "off") == 0);
+	k.budget_scale = budget_env && k.budget ? (float)atof(budget_env) : 1.5f;
 	if (!(k.budget_scale > 0.0f)) k.budget_scale = 1.5f;
 	static const bool block_skipping = getenv("NGP_RENDER_SKIP") && !strcmp(getenv("NGP_RENDER_SKIP"), "blocks");
 	if (!block_skipping) {
