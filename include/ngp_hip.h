@@ -191,6 +191,9 @@ typedef struct ngp_render_args {
 	int32_t train_in_linear_colors;
 	/* row sharding for multi-GPU (config C): render rows y with (y / shard_rows) % shard_count == shard_index */
 	uint32_t shard_index, shard_count, shard_rows;
+	/* Nerf::render_lens when render_with_lens_distortion (src/testbed_nerf.cu:1859): ELensMode + params */
+	int32_t lens_mode;
+	float lens_params[7];
 } ngp_render_args;
 
 /* --- lifecycle -------------------------------------------------------------------- */

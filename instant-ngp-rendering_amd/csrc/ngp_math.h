@@ -65,6 +65,99 @@ struct m43 {
 NGP_HD v3 rot(const m43& m, v3 d) { return m.c[0] * d.x + m.c[1] * d.y + m.c[2] * d.z; }
 
 // ---------------------------------------------------------------------------
+// Camera lenses — uv_to_ray's direction part (common_device.cuh:248-460).  Modes follow
+// ELensMode (common.h:188-195): 0 Perspective, 1 OpenCV, 2 FTheta, 3 LatLong,
+// 4 OpenCVFisheye, 5 Equirectangular.  params[7]: k1 k2 p1 p2 (OpenCV), k1 k2 k3 k4
+// (fisheye), r0..r4 w h (F-Theta).
+// ---------------------------------------------------------------------------
+enum LensMode : int { LENS_PERSPECTIVE = 0, LENS_OPENCV = 1, LENS_FTHETA = 2, LENS_LATLONG = 3, LENS_OPENCV_FISHEYE = 4,
+                      LENS_EQUIRECTANGULAR = 5 };
+constexpr float NGP_PI = 3.14159265358979323846f;
+
+NGP_HD void opencv_delta(const float* k, float u, float v, float* du, float* dv) {
+	const float u2 = u * u, uv = u * v, v2 = v * v, r2 = u2 + v2;
+	const float radial = k[0] * r2 + k[1] * r2 * r2;
+	*du = u * radial + 2.0f * k[2] * uv + k[3] * (r2 + 2.0f * u2);
+	*dv = v * radial + 2.0f * k[3] * uv + k[2] * (r2 + 2.0f * v2);
+}
+NGP_HD void opencv_fisheye_delta(const float* k, float u, float v, float* du, float* dv) {
+	const float r = sqrtf(u * u + v * v);
+	if (r > 2.220446049250313e-16f) {  // numeric_limits<double>::epsilon() as float
+		const float theta = atanf(r), t2 = theta * theta, t4 = t2 * t2, t6 = t4 * t2, t8 = t4 * t4;
+		const float thetad = theta * (1.0f + k[0] * t2 + k[1] * t4 + k[2] * t6 + k[3] * t8);
+		*du = u * thetad / r - u;
+		*dv = v * thetad / r - v;
+	} else {
+		*du = 0.0f;
+		*dv = 0.0f;
+	}
+}
+// iterative_lens_undistortion: Newton with a central-difference Jacobian, <= 100 steps
+template <int MODE>
+NGP_HD void iterative_undistortion(const float* k, float* u, float* v) {
+	const float x0 = *u, y0 = *v;
+	float x = x0, y = y0;
+	for (uint32_t i = 0; i < 100; ++i) {
+		const float s0 = fmaxf(1.1920929e-7f, fabsf(1e-6f * x)), s1 = fmaxf(1.1920929e-7f, fabsf(1e-6f * y));
+		float dx, dy, a0, b0, a1, b1, c0, d0, c1, d1;
+		auto f = [&](float px, float py, float* ox, float* oy) {
+			if (MODE == LENS_OPENCV) opencv_delta(k, px, py, ox, oy);
+			else opencv_fisheye_delta(k, px, py, ox, oy);
+		};
+		f(x, y, &dx, &dy);
+		f(x - s0, y, &a0, &b0);
+		f(x + s0, y, &a1, &b1);
+		f(x, y - s1, &c0, &d0);
+		f(x, y + s1, &c1, &d1);
+		// J (column-major as in the reference): J[0][0] = d(x+dx)/dx, J[1][0] = d(x+dx)/dy, ...
+		const float j00 = 1.0f + (a1 - a0) / (2.0f * s0), j10 = (c1 - c0) / (2.0f * s1);
+		const float j01 = (b1 - b0) / (2.0f * s0), j11 = 1.0f + (d1 - d0) / (2.0f * s1);
+		const float rx = x + dx - x0, ry = y + dy - y0;
+		// inverse(J) * r with glm's mat2 inverse: 1/det * [[j11, -j01], [-j10, j00]] (columns)
+		const float det = j00 * j11 - j10 * j01;
+		const float inv = 1.0f / det;
+		const float sx = (j11 * inv) * rx + (-j10 * inv) * ry;
+		const float sy = (-j01 * inv) * rx + (j00 * inv) * ry;
+		x -= sx;
+		y -= sy;
+		if (sx * sx + sy * sy < 1e-10f) break;
+	}
+	*u = x;
+	*v = y;
+}
+// Camera-space ray direction of screen position uv (not normalised); false: no ray (F-Theta
+// beyond its field of view -- the sampler then uses the camera axis, as the reference does)
+NGP_HD bool lens_direction(float u, float v, float res_x, float res_y, float fx, float fy, float cx, float cy, int mode,
+                           const float* k, v3* dir) {
+	if (mode == LENS_FTHETA) {
+		const float xpix = (u - cx) * k[5], ypix = (v - cy) * k[6];
+		const float norm = sqrtf(xpix * xpix + ypix * ypix);
+		const float alpha = k[0] + norm * (k[1] + norm * (k[2] + norm * (k[3] + norm * k[4])));
+		float sa = sinf(alpha), ca = cosf(alpha);
+		if (ca <= 1.17549435e-38f || norm == 0.0f) return false;
+		sa *= 1.0f / norm;
+		*dir = mk3(sa * xpix, sa * ypix, ca);
+		return true;
+	}
+	if (mode == LENS_LATLONG) {
+		const float theta = (v - 0.5f) * NGP_PI, phi = (u - 0.5f) * NGP_PI * 2.0f;
+		const float st = sinf(theta), ct = cosf(theta), sp = sinf(phi), cp = cosf(phi);
+		*dir = mk3(sp * ct, st, cp * ct);
+		return true;
+	}
+	if (mode == LENS_EQUIRECTANGULAR) {
+		const float ct = (v - 0.5f) * 2.0f, st = sqrtf(fmaxf(1.0f - ct * ct, 0.0f)), phi = (u - 0.5f) * NGP_PI * 2.0f;
+		*dir = mk3(sinf(phi) * st, ct, cosf(phi) * st);
+		return true;
+	}
+	float x = (u - cx) * res_x / fx, y = (v - cy) * res_y / fy;
+	if (mode == LENS_OPENCV) iterative_undistortion<LENS_OPENCV>(k, &x, &y);
+	else if (mode == LENS_OPENCV_FISHEYE) iterative_undistortion<LENS_OPENCV_FISHEYE>(k, &x, &y);
+	*dir = mk3(x, y, 1.0f);
+	return true;
+}
+
+// ---------------------------------------------------------------------------
 // PCG32 (tiny-cuda-nn `pcg32`, W. Jakob's pcg32.h); default_rng_t in
 // include/neural-graphics-primitives/random_val.cuh:26.
 // ---------------------------------------------------------------------------

@@ -259,9 +259,7 @@ PYBIND11_MODULE(pyngp, m) {
 		.def("set_camera_intrinsics",
 		     [](TrainingView& v, int frame_idx, float fx, float fy, float cx, float cy, float k1, float k2, float p1, float p2,
 		        float k3, float k4, bool is_fisheye) {
-			     if (k1 != 0 || k2 != 0 || p1 != 0 || p2 != 0 || k3 != 0 || k4 != 0 || is_fisheye)
-				     throw std::runtime_error("lens distortion is not implemented on the MI355X path (perspective only)");
-			     v.tb->set_camera_intrinsics(frame_idx, fx, fy, cx, cy);
+			     v.tb->set_camera_intrinsics(frame_idx, fx, fy, cx, cy, k1, k2, p1, p2, k3, k4, is_fisheye);
 		     },
 		     py::arg("frame_idx"), py::arg("fx") = 0.f, py::arg("fy") = 0.f, py::arg("cx") = -0.5f, py::arg("cy") = -0.5f,
 		     py::arg("k1") = 0.f, py::arg("k2") = 0.f, py::arg("p1") = 0.f, py::arg("p2") = 0.f, py::arg("k3") = 0.f,
@@ -298,6 +296,8 @@ PYBIND11_MODULE(pyngp, m) {
 		NV_RW("sharpen", sharpen)
 		NV_RW("render_with_lens_distortion", render_with_lens_distortion)
 		NV_RW("render_with_camera_distortion", render_with_lens_distortion)
+		NV_RW("render_lens", render_lens)
+		NV_RW("render_distortion", render_lens)
 		NV_RW("render_min_transmittance", render_min_transmittance)
 		NV_RW("rendering_min_transmittance", render_min_transmittance)
 		NV_RW("cone_angle_constant", cone_angle_constant)

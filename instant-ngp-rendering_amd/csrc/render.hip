@@ -44,6 +44,8 @@ struct RenderK {
 	int rgb_act, density_act;
 	uint32_t shard_index, shard_count, shard_rows;
 	uint32_t n_local;
+	int lens_mode;
+	float lens_params[7];
 	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
 	const uint8_t* bitfield;
 	const uint8_t* summary;
@@ -156,7 +158,12 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 	float ox, oy;
 	ld_random_pixel_offset(k.snap ? 0u : k.sample_index, &ox, &oy);
 	const float u = ((float)x + ox) / (float)k.W, v = ((float)y + oy) / (float)k.H;
-	v3 dir = mk3((u - k.scx) * (float)k.W / k.fx, (v - k.scy) * (float)k.H / k.fy, 1.0f);
+	v3 dir;
+	if (!lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
+		*pp = Payload{};  // uv_to_ray returned Ray::invalid(): the pixel stays empty
+		pp->idx = idx;
+		return false;
+	}
 	dir = rot(k.cam, dir);
 	v3 origin = k.cam.c[3] + dir * k.near_distance;
 
@@ -635,6 +642,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.linear_colors = a->train_in_linear_colors;
 	k.rgb_act = m->cfg.rgb_activation;
 	k.density_act = m->cfg.density_activation;
+	k.lens_mode = a->lens_mode;
+	for (int q = 0; q < 7; ++q) k.lens_params[q] = a->lens_params[q];
 	k.shard_count = std::max(a->shard_count, 1u);
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);

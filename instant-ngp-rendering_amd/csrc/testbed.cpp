@@ -406,7 +406,10 @@ void Testbed::load_nerf_post() {
 	NerfDataset& ds = nerf.training.dataset;
 	nerf.rgb_activation = ds.is_hdr ? ENerfActivation::Exponential : ENerfActivation::Logistic;
 	nerf.training.n_images_for_training = (int)ds.n_images;
-	if (!ds.metadata.empty()) screen_center = {1.f - ds.metadata[0].principal_point[0], 1.f - ds.metadata[0].principal_point[1]};
+	if (!ds.metadata.empty()) {
+		screen_center = {1.f - ds.metadata[0].principal_point[0], 1.f - ds.metadata[0].principal_point[1]};
+		nerf.render_lens = ds.metadata[0].lens;  // src/testbed_nerf.cu:2202
+	}
 	if (ds.aabb_scale <= 0 || (ds.aabb_scale & (ds.aabb_scale - 1)))
 		throw std::runtime_error("NeRF dataset's `aabb_scale` must be a power of two, but is " + std::to_string(ds.aabb_scale) + ".");
 	const int max_aabb_scale = 1 << (NERF_CASCADES - 1);
@@ -462,7 +465,9 @@ Mat43 Testbed::get_camera_extrinsics(int frame_idx) const {
 }
 
 // Nerf::Training::set_camera_intrinsics (src/testbed_nerf.cu:1989-2010)
-void Testbed::set_camera_intrinsics(int frame_idx, float fx, float fy, float cx, float cy) {
+// Nerf::Training::set_camera_intrinsics (src/testbed_nerf.cu:1989-2010)
+void Testbed::set_camera_intrinsics(int frame_idx, float fx, float fy, float cx, float cy, float k1, float k2, float p1,
+                                    float p2, float k3, float k4, bool is_fisheye) {
 	NerfDataset& ds = nerf.training.dataset;
 	if (frame_idx < 0 || (size_t)frame_idx >= ds.n_images) return;
 	if (fx <= 0.f) fx = fy;
@@ -471,6 +476,11 @@ void Testbed::set_camera_intrinsics(int frame_idx, float fx, float fy, float cx,
 	cx = cx < 0.f ? -cx : cx / (float)m.resolution[0];
 	cy = cy < 0.f ? -cy : cy / (float)m.resolution[1];
 	m.lens = Lens{};
+	if (k1 != 0.f || k2 != 0.f || k3 != 0.f || k4 != 0.f || p1 != 0.f || p2 != 0.f) {
+		m.lens.mode = is_fisheye ? ELensMode::OpenCVFisheye : ELensMode::OpenCV;
+		const float prm[4] = {k1, k2, is_fisheye ? k3 : p1, is_fisheye ? k4 : p2};
+		for (int q = 0; q < 4; ++q) m.lens.params[q] = prm[q];
+	}
 	m.focal_length = {fx, fy};
 	m.principal_point = {cx, cy};
 	m_dataset_dirty = true;
@@ -959,6 +969,7 @@ void Testbed::set_camera_to_training_view(int trainview) {
 	const auto& md = ds.metadata[trainview];
 	relative_focal_length = {md.focal_length[0] / (float)md.resolution[fov_axis], md.focal_length[1] / (float)md.resolution[fov_axis]};
 	nerf.render_with_lens_distortion = true;
+	nerf.render_lens = md.lens;  // src/testbed.cu:477-478
 	screen_center = {1.0f - md.principal_point[0], 1.0f - md.principal_point[1]};
 	nerf.training.view = trainview;
 	m_spp = 0;
@@ -1051,6 +1062,10 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 	r.shard_index = shard_index;
 	r.shard_count = std::max(shard_count, 1u);
 	r.shard_rows = std::max(shard_rows, 1u);
+	if (nerf.render_with_lens_distortion) {
+		r.lens_mode = (int32_t)nerf.render_lens.mode;
+		std::memcpy(r.lens_params, nerf.render_lens.params, sizeof(r.lens_params));
+	}
 	const float bg[4] = {background_color[0], background_color[1], background_color[2], background_color[3]};
 	m_spp = 0;
 	for (int i = 0; i < std::max(spp, 1); ++i) {

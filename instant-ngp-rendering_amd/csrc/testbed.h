@@ -112,6 +112,7 @@ struct Nerf {
 	float cone_angle_constant = 1.f / 256.f;
 	float render_min_transmittance = 0.01f;
 	bool render_with_lens_distortion = false;
+	Lens render_lens;  // applied to rendered rays when render_with_lens_distortion (src/testbed_nerf.cu:1859)
 	float sharpen = 0.f;
 	uint32_t density_grid_ema_step = 0;
 	bool visualize_cameras = false;
@@ -132,7 +133,8 @@ public:
 	void set_image_rgba8(int frame_idx, const uint8_t* rgba, int width, int height);
 	void set_camera_extrinsics(int frame_idx, const float* c2w_3x4_rowmajor, bool convert_to_ngp = true);
 	Mat43 get_camera_extrinsics(int frame_idx) const;
-	void set_camera_intrinsics(int frame_idx, float fx, float fy = 0.f, float cx = -0.5f, float cy = -0.5f);
+	void set_camera_intrinsics(int frame_idx, float fx, float fy = 0.f, float cx = -0.5f, float cy = -0.5f, float k1 = 0.f, float k2 = 0.f,
+	                           float p1 = 0.f, float p2 = 0.f, float k3 = 0.f, float k4 = 0.f, bool is_fisheye = false);
 	std::function<bool(const std::string&, std::vector<uint8_t>&, int&, int&)> image_decoder;  // non-PNG fallback
 
 	// --- network (reload_network_from_file src/testbed.cu:274, reset_network :3624) ---

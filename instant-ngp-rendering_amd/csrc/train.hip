@@ -96,7 +96,7 @@ void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32
 }
 
 // ---------------------------------------------------------------------------
-// Camera rays (uv_to_ray, common_device.cuh:393-460; perspective lens).
+// Camera rays (uv_to_ray, common_device.cuh:393-460; lenses: ngp_math.h lens_direction).
 // ---------------------------------------------------------------------------
 __device__ __forceinline__ m43 load_xform(const float* x) {
 	m43 m;
@@ -191,9 +191,12 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 	if (rgba[0] < 0.0f) return false;
 	(void)rng.next_float();  // motionblur_time
 	const m43 xf = load_xform(im.xform);
-	v3 dir = mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
-	             (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
-	dir = rot(xf, dir);
+	v3 dir;
+	if (lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
+	                   im.principal_point[1], im.lens_mode, im.lens_params, &dir))
+		dir = rot(xf, dir);
+	else
+		dir = xf.c[2];  // no ray through this pixel: the camera axis (src/testbed_nerf.cu:762-764)
 	*o = xf.c[3];
 	*d = normalize(dir);
 	float t0, t1;

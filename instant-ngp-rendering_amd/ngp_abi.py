@@ -86,7 +86,7 @@ class RenderArgs(C.Structure):
         ("train_aabb_max", C.c_float * 3), ("cone_angle_constant", C.c_float), ("max_cascade", C.c_uint32),
         ("min_transmittance", C.c_float), ("snap_to_pixel_centers", C.c_int32), ("use_inference_params", C.c_int32),
         ("train_in_linear_colors", C.c_int32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
-        ("shard_rows", C.c_uint32),
+        ("shard_rows", C.c_uint32), ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7),
     ]
 
 

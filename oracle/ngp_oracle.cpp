@@ -702,6 +702,82 @@ static void rgba_of(uint32_t t, float* o) {
 static uint32_t image_index(uint32_t i, uint32_t n_rays, uint32_t n_img) {
 	return (uint32_t)((((uint64_t)i) * n_img) / n_rays) % n_img;  // nerf_device.cuh:597
 }
+// Lens models of uv_to_ray (common_device.cuh:248-460): ELensMode 0 Perspective, 1 OpenCV,
+// 2 FTheta, 3 LatLong, 4 OpenCVFisheye, 5 Equirectangular.
+static void lens_delta(int mode, const float* k, float u, float v, float* du, float* dv) {
+	if (mode == 1) {  // opencv_lens_distortion_delta
+		const float u2 = u * u, uv = u * v, v2 = v * v, r2 = u2 + v2;
+		const float radial = k[0] * r2 + k[1] * r2 * r2;
+		*du = u * radial + 2.0f * k[2] * uv + k[3] * (r2 + 2.0f * u2);
+		*dv = v * radial + 2.0f * k[3] * uv + k[2] * (r2 + 2.0f * v2);
+		return;
+	}
+	// opencv_fisheye_lens_distortion_delta
+	const float r = std::sqrt(u * u + v * v);
+	if (r > 2.220446049250313e-16f) {
+		const float th = std::atan(r), t2 = th * th, t4 = t2 * t2, t6 = t4 * t2, t8 = t4 * t4;
+		const float thd = th * (1.0f + k[0] * t2 + k[1] * t4 + k[2] * t6 + k[3] * t8);
+		*du = u * thd / r - u;
+		*dv = v * thd / r - v;
+	} else {
+		*du = *dv = 0.0f;
+	}
+}
+// iterative_lens_undistortion: Newton, central-difference Jacobian, <= 100 steps
+static void undistort(int mode, const float* k, float* u, float* v) {
+	const float x0 = *u, y0 = *v;
+	float x = x0, y = y0;
+	for (int it = 0; it < 100; ++it) {
+		const float s0 = std::max(1.1920929e-7f, std::fabs(1e-6f * x)), s1 = std::max(1.1920929e-7f, std::fabs(1e-6f * y));
+		float dx, dy, a0, b0, a1, b1, c0, d0, c1, d1;
+		lens_delta(mode, k, x, y, &dx, &dy);
+		lens_delta(mode, k, x - s0, y, &a0, &b0);
+		lens_delta(mode, k, x + s0, y, &a1, &b1);
+		lens_delta(mode, k, x, y - s1, &c0, &d0);
+		lens_delta(mode, k, x, y + s1, &c1, &d1);
+		const float j00 = 1.0f + (a1 - a0) / (2.0f * s0), j10 = (c1 - c0) / (2.0f * s1);
+		const float j01 = (b1 - b0) / (2.0f * s0), j11 = 1.0f + (d1 - d0) / (2.0f * s1);
+		const float rx = x + dx - x0, ry = y + dy - y0;
+		const float inv = 1.0f / (j00 * j11 - j10 * j01);
+		const float sx = (j11 * inv) * rx + (-j10 * inv) * ry, sy = (-j01 * inv) * rx + (j00 * inv) * ry;
+		x -= sx;
+		y -= sy;
+		if (sx * sx + sy * sy < 1e-10f) break;
+	}
+	*u = x;
+	*v = y;
+}
+// camera-space direction of screen position (u, v); false = invalid ray (F-Theta)
+static bool lens_dir(float u, float vv, float rx, float ry, float fx, float fy, float cx, float cy, int mode, const float* k,
+                     V3* d) {
+	const float PI_F = 3.14159265358979323846f;
+	if (mode == 2) {
+		const float xp = (u - cx) * k[5], yp = (vv - cy) * k[6];
+		const float nrm = std::sqrt(xp * xp + yp * yp);
+		const float al = k[0] + nrm * (k[1] + nrm * (k[2] + nrm * (k[3] + nrm * k[4])));
+		float sa = std::sin(al);
+		const float ca = std::cos(al);
+		if (ca <= 1.17549435e-38f || nrm == 0.0f) return false;
+		sa *= 1.0f / nrm;
+		*d = v(sa * xp, sa * yp, ca);
+		return true;
+	}
+	if (mode == 3) {  // latlong_to_dir
+		const float th = (vv - 0.5f) * PI_F, ph = (u - 0.5f) * PI_F * 2.0f;
+		*d = v(std::sin(ph) * std::cos(th), std::sin(th), std::cos(ph) * std::cos(th));
+		return true;
+	}
+	if (mode == 5) {  // equirectangular_to_dir
+		const float ct = (vv - 0.5f) * 2.0f, st = std::sqrt(std::max(1.0f - ct * ct, 0.0f)), ph = (u - 0.5f) * PI_F * 2.0f;
+		*d = v(std::sin(ph) * st, ct, std::cos(ph) * st);
+		return true;
+	}
+	float x = (u - cx) * rx / fx, y = (vv - cy) * ry / fy;
+	if (mode == 1 || mode == 4) undistort(mode, k, &x, &y);
+	*d = v(x, y, 1.0f);
+	return true;
+}
+
 // binary_search (common.h:207-230): first index with data[i] >= val, clamped to length-1
 static uint32_t cdf_search(float val, const float* data, uint32_t length) {
 	if (length == 0) return 0;
@@ -778,9 +854,12 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	if (rgba[0] < 0.0f) return false;
 	(void)rng.nextf();  // motionblur_time
 	const Cam x = cam_of(im.xform);
-	V3 dir = v((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
-	           (vv - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
-	dir = rot(x, dir);
+	V3 dir;
+	if (lens_dir(u, vv, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
+	             im.principal_point[1], im.lens_mode, im.lens_params, &dir))
+		dir = rot(x, dir);
+	else
+		dir = x.c[2];  // src/testbed_nerf.cu:762-764
 	*o = x.c[3];
 	*d = normalize(dir);
 	const Box b{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
@@ -1150,7 +1229,10 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			fb[0] = fb[1] = fb[2] = fb[3] = 0.0f;
 			depthbuf[idx] = MAXD;
 			const float u = ((float)x + ox) / (float)a.width, vv = ((float)y + oy) / (float)a.height;
-			V3 d = v((u - a.screen_center[0]) * (float)a.width / a.focal_length[0], (vv - a.screen_center[1]) * (float)a.height / a.focal_length[1], 1.0f);
+			V3 d;
+			if (!lens_dir(u, vv, (float)a.width, (float)a.height, a.focal_length[0], a.focal_length[1], a.screen_center[0],
+			              a.screen_center[1], a.lens_mode, a.lens_params, &d))
+				continue;  // invalid ray: the pixel stays empty
 			d = rot(cam, d);
 			const V3 o = cam.c[3] + d * a.near_distance;
 			d = normalize(d);
@@ -1223,6 +1305,17 @@ void oref_pcg32_floats_advanced(uint64_t state, uint64_t inc, int64_t adv, uint3
 	for (uint32_t i = 0; i < n; ++i) out[i] = r.nextf();
 }
 float oref_ld_random_val(uint32_t index, uint32_t seed, uint32_t dim) { return ldval(index, seed, dim); }
+
+// camera-space direction of a screen position under a lens (uv_to_ray's direction part)
+int oref_lens_direction(float u, float v, float rx, float ry, float fx, float fy, float cx, float cy, int mode,
+                        const float* params, float* dir3) {
+	V3 d;
+	const bool ok = lens_dir(u, v, rx, ry, fx, fy, cx, cy, mode, params, &d);
+	dir3[0] = d.x;
+	dir3[1] = d.y;
+	dir3[2] = d.z;
+	return ok ? 1 : 0;
+}
 
 // the training ray's image and pixel (image_idx + nerf_random_image_pos_training, with the
 // error-map CDFs when given) -- exposed for the sampling tests

@@ -19,6 +19,7 @@ _PROTOS = {
     "oref_pcg32": (None, [C.c_uint64, C.c_uint64, C.c_uint32, C.c_void_p]),
     "oref_pcg32_floats_advanced": (None, [C.c_uint64, C.c_uint64, C.c_int64, C.c_uint32, C.c_void_p]),
     "oref_ld_random_val": (C.c_float, [C.c_uint32, C.c_uint32, C.c_uint32]),
+    "oref_lens_direction": (C.c_int, [C.c_float] * 8 + [C.c_int, C.c_void_p, C.c_void_p]),
     "oref_pick_pixel": (C.c_uint32, [C.c_void_p, C.c_uint32, C.POINTER(C.c_float), C.POINTER(C.c_float),
                                      C.POINTER(C.c_float)]),
     "oref_error_map_build_cdf": (None, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,

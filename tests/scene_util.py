@@ -41,7 +41,7 @@ def make_views(n_images=6, W=24, H=24, seed=0):
     return imgs, cams, focal
 
 
-def image_structs(imgs, cams, focal, pointers):
+def image_structs(imgs, cams, focal, pointers, lens=(0, ())):
     n = len(imgs)
     arr = (A.Image * n)()
     for i in range(n):
@@ -53,14 +53,16 @@ def image_structs(imgs, cams, focal, pointers):
         xf = np.asarray(cams[i], np.float32).T.reshape(-1)  # column-major 4x3
         for k in range(12):
             arr[i].xform[k] = float(xf[k])
-        arr[i].lens_mode = 0
+        arr[i].lens_mode = lens[0]
+        for k, val in enumerate(lens[1]):
+            arr[i].lens_params[k] = float(val)
     return arr
 
 
 class HostDataset:
-    def __init__(self, imgs, cams, focal):
+    def __init__(self, imgs, cams, focal, lens=(0, ())):
         self.imgs = [np.ascontiguousarray(im) for im in imgs]
-        self.arr = image_structs(imgs, cams, focal, [im.ctypes.data for im in self.imgs])
+        self.arr = image_structs(imgs, cams, focal, [im.ctypes.data for im in self.imgs], lens)
         self.n = len(imgs)
 
     @property
@@ -69,10 +71,10 @@ class HostDataset:
 
 
 class DeviceDataset:
-    def __init__(self, imgs, cams, focal):
+    def __init__(self, imgs, cams, focal, lens=(0, ())):
         import torch
         self.pix = [torch.from_numpy(np.ascontiguousarray(im)).cuda() for im in imgs]
-        arr = image_structs(imgs, cams, focal, [p.data_ptr() for p in self.pix])
+        arr = image_structs(imgs, cams, focal, [p.data_ptr() for p in self.pix], lens)
         self.meta = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
         self.n = len(imgs)
 
