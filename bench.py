@@ -94,12 +94,16 @@ def make_dataset(ngp, tb, n_views, res, device):
 
 # timer -> kernel whose PMC counters describe it
 TIMER_KERNEL = {"train_encode": ("k_hashgrid_fwd<", ", 0>"), "render_encode": ("k_hashgrid_fwd<", ", 1>"),
-                "train_encode_bwd": ("k_hashgrid_bwd<", ""), "train_mlp_infer": ("k_mlp_infer<", ""),
-                "render_mlp": ("k_mlp_infer<", ""), "train_mlp_bwd": ("k_mlp_train<", ""), "optimizer": ("k_optimizer", "")}
+                "train_encode_bwd": ("k_hashgrid_bwd<", ""), "train_mlp_infer": ("k_mlp_infer_rf<", ", false, 2>"),
+                "render_mlp": ("k_mlp_infer_rf<", ", false, 2>"), "train_mlp_bwd": ("k_mlp_train<", ""),
+                "optimizer": ("k_optimizer", "")}
 
 
 def pmc_traffic(path, timer, units_per_launch):
-    """HBM bytes per launch of the dominant kernel from the committed PMC summary (or None)."""
+    """HBM bytes per launch of the dominant kernel from the committed PMC summary (or None).
+    The PMC run profiles the same workload, so its mean bytes per launch are used directly
+    (launch grids are sized by upper bounds, so per-sample figures from the grid size would
+    undercount)."""
     if not os.path.exists(path) or timer not in TIMER_KERNEL:
         return None
     data = json.load(open(path))
@@ -107,8 +111,6 @@ def pmc_traffic(path, timer, units_per_launch):
     for name, e in data.items():
         if prefix not in name or not name.endswith(suffix):
             continue
-        if "fetch_bytes_per_sample" in e:
-            return round((e["fetch_bytes_per_sample"] + e["write_bytes_per_sample"]) * units_per_launch)
         return round(e.get("fetch_bytes_per_launch", 0) + e.get("write_bytes_per_launch", 0))
     return None
 

@@ -61,6 +61,9 @@ struct KernelTimers {
 		units[slot] += u;
 		++launches[slot];
 	}
+	void add_units(int slot, uint64_t u) {
+		if (on(slot)) units[slot] += u;
+	}
 	void collect() {
 		for (const Pending& p : pending) {
 			NGP_HIP_CHECK(hipEventSynchronize(p.b));

