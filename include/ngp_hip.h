@@ -148,6 +148,7 @@ typedef struct ngp_train_args {
 	const float* cdf_y;         /* device [n_images][cdf_res_y] */
 	const float* cdf_img;       /* device [n_images] normalised image CDF: sample_image_proportional_to_error; null = uniform */
 	uint32_t cdf_res[2];        /* x, y */
+	int32_t has_lens;           /* 1 if any image has a non-pinhole lens (selects the general sampler kernels) */
 } ngp_train_args;
 
 typedef struct ngp_train_stats {

@@ -70,6 +70,7 @@ __device__ __forceinline__ const uint8_t* stage_summary(const uint8_t* __restric
 	return reinterpret_cast<const uint8_t*>(s_summary);
 }
 
+template <bool LENS>
 __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
                                               Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer);
 
@@ -127,6 +128,7 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t* counte
 	return b + x - cnt;
 }
 
+template <bool LENS>
 __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
                                                      float* __restrict__ depth, float4* __restrict__ frame,
                                                      float* __restrict__ depth_buffer, uint32_t* __restrict__ counters) {
@@ -137,7 +139,7 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 	const uint32_t tile = r >> 6, x = (tile % k.tiles_x) * 8u + (r & 7u), yl = (tile / k.tiles_x) * 8u + ((r >> 3) & 7u);
 	Payload p;
 	bool alive = false;
-	if (x < k.W && yl < k.h_local) alive = init_ray_body(k, summary, x, yl, &p, frame, depth_buffer);
+	if (x < k.W && yl < k.h_local) alive = init_ray_body<LENS>(k, summary, x, yl, &p, frame, depth_buffer);
 	uint32_t slot, unused;
 	block_append2(alive, false, &counters[0], &counters[3], &slot, &unused);
 	if (alive) {
@@ -148,6 +150,7 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 }
 
 // init_rays_with_payload_kernel_nerf + advance_pos_nerf for pixel x of local row yl
+template <bool LENS>
 __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
                                               Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer) {
 	const uint32_t y = local_to_global_row(k, yl);
@@ -158,8 +161,8 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 	float ox, oy;
 	ld_random_pixel_offset(k.snap ? 0u : k.sample_index, &ox, &oy);
 	const float u = ((float)x + ox) / (float)k.W, v = ((float)y + oy) / (float)k.H;
-	v3 dir;
-	if (!lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
+	v3 dir = mk3((u - k.scx) * (float)k.W / k.fx, (v - k.scy) * (float)k.H / k.fy, 1.0f);
+	if (LENS && !lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
 		*pp = Payload{};  // uv_to_ray returned Ray::invalid(): the pixel stays empty
 		pp->idx = idx;
 		return false;
@@ -694,7 +697,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
 	                                                                rs.counters.ptr);
 	const size_t lds = k.df ? 0 : (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
-	k_render_init<<<div_up(n_tiled, 256u), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
+	(k.lens_mode != LENS_PERSPECTIVE ? k_render_init<true> : k_render_init<false>)<<<div_up(n_tiled, 256u), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
 	                                             rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());

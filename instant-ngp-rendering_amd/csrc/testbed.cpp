@@ -778,6 +778,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.optimize_mlp = train_network;
 	a.optimize_encoding = train_encoding;
 	a.defer_optimizer = m_world > 1 ? 1 : 0;
+	for (size_t i = 0; i < tr.dataset.metadata.size(); ++i)
+		if (tr.dataset.metadata[i].lens.mode != ELensMode::Perspective) a.has_lens = 1;
 	if (m_err && tr.error_map.resolution[0] > 0 && tr.error_map.resolution[1] > 0) {
 		a.error_map = m_err;  // accumulate_error is always on (src/testbed_nerf.cu:2756)
 		a.error_map_res[0] = (uint32_t)tr.error_map.resolution[0];

@@ -151,12 +151,15 @@ struct SamplerArgs {
 // proportional to the error map when its CDFs are given.
 // *pdf = img_pdf * uv_pdf, the importance-sampling density the reference divides the loss by
 // (src/testbed_nerf.cu:1010).
+// GENERAL: error-map CDFs and non-pinhole lenses may be present (a separate kernel instance,
+// so the common pinhole / uniform case keeps its register budget).
+template <bool GENERAL>
 __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint32_t n_images, uint32_t gi,
                                                   uint32_t n_rays_global, const ErrorCdf& cdf, int snap, pcg32& rng,
                                                   float* uo, float* vo, float* pdf = nullptr) {
 	uint32_t img;
 	float img_pdf = 1.0f, uv_pdf = 1.0f;
-	if (cdf.img) {
+	if (GENERAL && cdf.img) {
 		img = cdf_search(ld_random_val(gi, 0xdeadbeefu), cdf.img, n_images);
 		img_pdf = (cdf.img[img] - (img > 0 ? cdf.img[img - 1] : 0.0f)) * (float)n_images;
 	} else {
@@ -164,7 +167,7 @@ __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint
 	}
 	const ngp_image& im = images[img];
 	float u = rng.next_float(), v = rng.next_float();
-	if (cdf.x_cond_y) sample_cdf_2d(&u, &v, img, cdf, &uv_pdf);
+	if (GENERAL && cdf.x_cond_y) sample_cdf_2d(&u, &v, img, cdf, &uv_pdf);
 	if (pdf) *pdf = img_pdf * uv_pdf;
 	if (snap) {
 		int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
@@ -180,11 +183,12 @@ __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint
 
 // Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777);
 // *n0 = first lattice point (stepping space) = entry + jitter.
+template <bool GENERAL>
 __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0) {
 	pcg32 rng = a.rng;
 	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
 	float u, v;
-	const uint32_t img = training_pixel(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v);
+	const uint32_t img = training_pixel<GENERAL>(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v);
 	const ngp_image im = a.images[img];
 	float rgba[4];
 	texel_rgba(read_texel(im, u, v), rgba);
@@ -192,11 +196,15 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 	(void)rng.next_float();  // motionblur_time
 	const m43 xf = load_xform(im.xform);
 	v3 dir;
-	if (lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
-	                   im.principal_point[1], im.lens_mode, im.lens_params, &dir))
+	if (!GENERAL) {
+		dir = rot(xf, mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
+		                  (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f));
+	} else if (lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1],
+	                          im.principal_point[0], im.principal_point[1], im.lens_mode, im.lens_params, &dir)) {
 		dir = rot(xf, dir);
-	else
+	} else {
 		dir = xf.c[2];  // no ray through this pixel: the camera axis (src/testbed_nerf.cu:762-764)
+	}
 	*o = xf.c[3];
 	*d = normalize(dir);
 	float t0, t1;
@@ -226,6 +234,7 @@ __device__ __forceinline__ LatticePoint training_lattice_point(const SamplerArgs
 // generate_training_samples_nerf (testbed_nerf.cu:679-839), pass 1: one wave per ray,
 // 64 lattice points per iteration; the count stops at the first point outside the
 // AABB or at NERF_STEPS samples, like the reference's sequential loop.
+template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
 	const uint32_t lane = threadIdx.x & 63u;
@@ -233,7 +242,7 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	v3 o, d;
 	float n0;
 	uint32_t count = 0;
-	if (training_ray(a, a.ray_offset + i, &o, &d, &n0)) {
+	if (training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0)) {
 		for (uint32_t kb = 0;; kb += 64) {
 			const LatticePoint p = training_lattice_point(a, o, d, n0, kb + lane);
 			const unsigned long long out = __ballot(!p.inside);
@@ -252,6 +261,7 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 
 // pass 2: same walk, each sample written at base + (its rank among the ray's samples);
 // consecutive lanes write consecutive 32-byte coordinates.
+template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
 	const uint32_t lane = threadIdx.x & 63u;
@@ -266,7 +276,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	}
 	v3 o, d;
 	float n0;
-	training_ray(a, a.ray_offset + i, &o, &d, &n0);
+	training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0);
 	if (lane == 0) {
 		a.numsteps[2 * i + 0] = n;
 		a.numsteps[2 * i + 1] = base;
@@ -323,7 +333,7 @@ struct LossArgs {
 	uint32_t max_compacted;
 	uint32_t target_batch;
 	const uint32_t* numsteps;
-	const float* ray_state;
+	float* ray_state;        // [R][8]: o, d (sampler), u, v of the pixel (k_loss_composite)
 	const float* coords;
 	const __half* mlp_out;
 	const __half* enc;
@@ -378,6 +388,7 @@ __device__ __forceinline__ LossSample loss_sample(const LossArgs& a, size_t src)
 // 64 samples per iteration.  Transmittance T_j = prod_{i<j}(1 - alpha_i) comes from a
 // multiplicative wave scan, the colour from an additive one; the ray stops at the first
 // sample with T_j < 1e-4 (the reference's sequential test), found with a ballot.
+template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
 	const uint32_t lane = threadIdx.x & 63u;
@@ -418,7 +429,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	pcg32 rng = a.rng;
 	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
 	float u, v, pdf;
-	const uint32_t img = training_pixel(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v, &pdf);
+	const uint32_t img = training_pixel<GENERAL>(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v, &pdf);
 	const ngp_image im = a.images[img];
 	rng.advance(1);  // motionblur_time
 	v3 bg = a.bg;
@@ -456,6 +467,9 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	ls[0] = gx; ls[1] = gy; ls[2] = gz;
 	ls[3] = rgb_ray.x; ls[4] = rgb_ray.y; ls[5] = rgb_ray.z;
 	ls[6] = mean_loss;
+	ls[7] = __uint_as_float(img);  // the error deposit (k_loss_emit) reuses the pixel
+	a.ray_state[8 * (size_t)i + 6] = u;
+	a.ray_state[8 * (size_t)i + 7] = v;
 	a.ccounts[i] = c;
 }
 
@@ -480,11 +494,8 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		// bilinear deposit of the ray's mean loss (src/testbed_nerf.cu:1028-1054; rays without
 		// compacted samples returned before it); the corner clamp uses the image
 		// resolution, as the reference does
-		const uint32_t gi = a.ray_offset + i;
-		pcg32 rng = a.rng;
-		rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
-		float u, v;
-		const uint32_t img = training_pixel(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v);
+		const float u = a.ray_state[8 * (size_t)i + 6], v = a.ray_state[8 * (size_t)i + 7];
+		const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
 		const ngp_image& im = a.images[img];
 		const float mean_loss = a.loss_state[8 * (size_t)i + 6];
 		const float rx = (float)a.error_map_rx, ry = (float)a.error_map_ry;
@@ -798,9 +809,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.pos4 = reinterpret_cast<float4*>(ts.pos4.ptr);
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
-	k_sample_count<<<div_up(R, 4), 256, 0, s>>>(sa);
+	const bool general = t->cdf_img || t->cdf_x_cond_y || t->has_lens;
+	if (general) k_sample_count<true><<<div_up(R, 4), 256, 0, s>>>(sa);
+	else k_sample_count<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
-	k_sample_write<<<div_up(R, 4), 256, 0, s>>>(sa);
+	if (general) k_sample_write<true><<<div_up(R, 4), 256, 0, s>>>(sa);
+	else k_sample_write<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	NGP_HIP_CHECK(hipGetLastError());
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
@@ -855,7 +869,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
-	k_loss_composite<<<div_up(R, 4), 256, 0, s>>>(la);
+	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
+	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
 	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
 	NGP_HIP_CHECK(hipGetLastError());

@@ -56,7 +56,7 @@ class TrainArgs(C.Structure):
         ("train_in_linear_colors", C.c_int32), ("color_space", C.c_int32), ("near_distance", C.c_float),
         ("optimize_mlp", C.c_int32), ("optimize_encoding", C.c_int32), ("defer_optimizer", C.c_int32),
         ("error_map", C.c_void_p), ("error_map_res", C.c_uint32 * 2), ("cdf_x_cond_y", C.c_void_p),
-        ("cdf_y", C.c_void_p), ("cdf_img", C.c_void_p), ("cdf_res", C.c_uint32 * 2),
+        ("cdf_y", C.c_void_p), ("cdf_img", C.c_void_p), ("cdf_res", C.c_uint32 * 2), ("has_lens", C.c_int32),
     ]
 
 

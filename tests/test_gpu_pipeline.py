@@ -322,6 +322,7 @@ def test_train_sampler_lens_matches_oracle(lens):
         R, B, MS = 384, 4096, 1 << 15
         ga = train_args(dd.ptr, dd.n, R, B, MS)
         oa = train_args(hd.ptr, hd.n, R, B, MS)
+        ga.has_lens = 1
         g.zero_grads()
         A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
         torch.cuda.synchronize()
