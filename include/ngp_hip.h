@@ -149,6 +149,9 @@ typedef struct ngp_train_args {
 	const float* cdf_img;       /* device [n_images] normalised image CDF: sample_image_proportional_to_error; null = uniform */
 	uint32_t cdf_res[2];        /* x, y */
 	int32_t has_lens;           /* 1 if any image has a non-pinhole lens (selects the general sampler kernels) */
+	/* per-image exposure (Nerf::Training::cam_exposure, src/testbed_nerf.cu:966-985, 1121-1134) */
+	const float* exposure;      /* device [n_images][3] log2 scale of the target colours; null = 0 */
+	float* exposure_gradient;   /* device [n_images][3] += dL/dexposure of the kept rays; null = off */
 } ngp_train_args;
 
 typedef struct ngp_train_stats {

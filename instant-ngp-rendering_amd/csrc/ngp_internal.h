@@ -131,6 +131,7 @@ struct TrainScratch {
 	DevBuf<uint32_t> ray_compacted;    // [R][2]
 	DevBuf<float> ray_state;           // [R][8] : o, d (unnormalised), pad
 	DevBuf<float> ray_loss_state;      // [R][8]
+	DevBuf<float> ray_aux;             // [R][4] per-ray dL/dexposure
 	DevBuf<float> coords;              // [max_samples][8]
 	DevBuf<__half> enc;                // [L][max_samples][F]
 	DevBuf<__half> mlp_out;            // [max_samples][4]

@@ -285,6 +285,10 @@ NGP_HD void ld_random_pixel_offset(uint32_t spp, float* ox, float* oy) {
 // ---------------------------------------------------------------------------
 // Colour helpers — common_device.cuh:34-80.
 // ---------------------------------------------------------------------------
+// srgb_to_linear_derivative (common_device.cuh:46-52)
+NGP_HD float srgb_to_linear_derivative(float srgb) {
+	return srgb <= 0.04045f ? 1.0f / 12.92f : 2.4f / 1.055f * powf((srgb + 0.055f) / 1.055f, 1.4f);
+}
 NGP_HD float srgb_to_linear(float srgb) {
 	return srgb <= 0.04045f ? srgb / 12.92f : powf((srgb + 0.055f) / 1.055f, 2.4f);
 }

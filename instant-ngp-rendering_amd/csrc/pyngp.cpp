@@ -237,6 +237,8 @@ PYBIND11_MODULE(pyngp, m) {
 		TV_RW("sample_image_proportional_to_error", sample_image_proportional_to_error)
 		TV_RW("include_sharpness_in_error", include_sharpness_in_error)
 		TV_RW("n_steps_between_error_map_updates", n_steps_between_error_map_updates)
+		TV_RW("n_steps_between_cam_updates", n_steps_between_cam_updates)
+		TV_RW("exposure_l2_reg", exposure_l2_reg)
 #undef TV_RW
 		// additions: the accumulated error map and the image pmf of the last CDF update
 		.def_property_readonly("error_map", [](TrainingView& v) {
@@ -246,6 +248,11 @@ PYBIND11_MODULE(pyngp, m) {
 			py::array_t<float> out({ni, (py::ssize_t)tr.error_map.resolution[1], (py::ssize_t)tr.error_map.resolution[0]});
 			if (!h.empty()) std::memcpy(out.mutable_data(), h.data(), h.size() * sizeof(float));
 			return out;
+		})
+		.def_property_readonly("cam_exposure", [](TrainingView& v) {
+			py::list l;
+			for (const auto& o : v.tb->nerf.training.cam_exposure) l.append(py::make_tuple(o.variable[0], o.variable[1], o.variable[2]));
+			return l;
 		})
 		.def_property_readonly("error_map_pmf_img", [](TrainingView& v) { return v.tb->nerf.training.error_map.pmf_img_cpu; })
 		.def_property_readonly("error_map_cdf_valid", [](TrainingView& v) { return v.tb->nerf.training.error_map.is_cdf_valid; })

@@ -207,7 +207,7 @@ Testbed::~Testbed() {
 	for (float* p : {m_frame, m_depth, m_accum, m_out})
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
-	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img})
+	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
@@ -602,6 +602,7 @@ void Testbed::reset_network(bool clear_density_grid) {
 	nerf.training.n_rays_since_error_map_update = 0;
 	nerf.training.n_steps_between_error_map_updates = 128;
 	nerf.training.error_map.is_cdf_valid = false;
+	nerf.training.n_steps_since_cam_update = 0;
 	pcg32 grid_rng(rng.next_uint());
 	m_rng_state = rng.state;
 	m_rng_inc = rng.inc;
@@ -676,6 +677,7 @@ void Testbed::build_model(const Json& cfg) {
 		m_model = nullptr;
 	}
 	ck(ngp_model_create(device, &c, seed, &m_model));
+	m_net_cfg = c;
 }
 
 // ---------------------------------------------------------------------------
@@ -724,9 +726,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (nerf.training.n_images_for_training == 0) return;
 	{
 		const NerfTraining& t = nerf.training;
-		if (t.optimize_extrinsics || t.optimize_distortion || t.optimize_focal_length || t.optimize_exposure ||
-		    t.optimize_extra_dims)
-			throw std::runtime_error("camera / exposure / latent optimisation is not implemented by this build");
+		if (t.optimize_extrinsics || t.optimize_distortion || t.optimize_focal_length || t.optimize_extra_dims)
+			throw std::runtime_error("camera pose / focal / distortion / latent optimisation is not implemented by this build");
 	}
 	upload_dataset();
 	NerfCounters& ctr = nerf.training.counters_rgb;
@@ -753,8 +754,27 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 		hk(hipMemsetAsync(m_err, 0, std::max<size_t>(n, 1) * sizeof(float), (hipStream_t)m_stream), "error map clear");
 	}
 
+	// per-image exposure: always applied to the targets, optimised on request (src/testbed_nerf.cu:2468-2473)
+	const size_t n_img = tr.dataset.n_images;
+	if (tr.cam_exposure.size() != n_img) tr.cam_exposure.assign(n_img, NerfTraining::Adam3{});
+	if (n_img * 3 > m_exp_cap) {
+		if (m_exp) (void)hipFree(m_exp);
+		if (m_exp_grad) (void)hipFree(m_exp_grad);
+		hk(hipMalloc((void**)&m_exp, n_img * 3 * sizeof(float)), "hipMalloc exposure");
+		hk(hipMalloc((void**)&m_exp_grad, n_img * 3 * sizeof(float)), "hipMalloc exposure gradient");
+		m_exp_cap = n_img * 3;
+		std::vector<float> e(n_img * 3);
+		for (size_t i = 0; i < n_img; ++i)
+			for (int k = 0; k < 3; ++k) e[3 * i + k] = tr.cam_exposure[i].variable[k];
+		hk(hipMemcpyAsync(m_exp, e.data(), e.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "exposure h2d");
+	}
+	if (tr.n_steps_since_cam_update == 0)
+		hk(hipMemsetAsync(m_exp_grad, 0, n_img * 3 * sizeof(float), (hipStream_t)m_stream), "exposure gradient clear");
+
 	ngp_train_args a{};
 	a.images = (const ngp_image*)m_dev_meta;
+	a.exposure = m_exp;
+	a.exposure_gradient = tr.optimize_exposure ? m_exp_grad : nullptr;
 	a.n_images = (uint32_t)nerf.training.n_images_for_training;
 	a.n_rays = ctr.rays_per_batch;
 	a.n_rays_total = ctr.n_rays_total;
@@ -814,6 +834,9 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	++training_step;
 	// CDFs from the error map, every n_steps_between_error_map_updates (x1.5 each time)
 	if (++tr.n_steps_since_error_map_update >= tr.n_steps_between_error_map_updates) update_error_map_cdf();
+	// camera parameters every n_steps_between_cam_updates (src/testbed_nerf.cu:2577-2680)
+	++tr.n_steps_since_cam_update;
+	if (tr.optimize_exposure && tr.n_steps_since_cam_update >= tr.n_steps_between_cam_updates) update_cam_exposure();
 	// m_rng.advance() (src/testbed_nerf.cu:2925)
 	pcg32 r;
 	r.state = m_rng_state;
@@ -895,6 +918,51 @@ void Testbed::update_error_map_cdf() {
 	tr.n_rays_since_error_map_update = 0;
 	tr.error_map.is_cdf_valid = true;
 	tr.n_steps_between_error_map_updates = (uint32_t)((float)tr.n_steps_between_error_map_updates * 1.5f);
+}
+
+// m_optimizer->learning_rate(): Adam's rate under the ExponentialDecay of the config
+float Testbed::current_learning_rate() const {
+	const ngp_network_config& c = m_net_cfg;
+	float lr = c.learning_rate;
+	if (c.decay_interval > 0 && training_step >= c.decay_start)
+		lr = c.learning_rate * std::pow(c.decay_base, (float)((training_step - c.decay_start) / c.decay_interval + 1));
+	return lr;
+}
+
+// Exposure branch of the camera update (src/testbed_nerf.cu:2650-2677): per-image Adam
+// (AdamOptimizer<vec3>, adam_optimizer.h:129-152) at the network's learning rate, then the
+// mean exposure is subtracted so the scene brightness stays anchored.
+void Testbed::update_cam_exposure() {
+	NerfTraining& tr = nerf.training;
+	const uint32_t n = (uint32_t)tr.n_images_for_training;
+	const size_t n_img = tr.dataset.n_images;
+	std::vector<float> g(n_img * 3);
+	if (m_world > 1) allreduce_f32(m_exp_grad, n_img * 3, false);
+	hk(hipMemcpyAsync(g.data(), m_exp_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "exposure gradient d2h");
+	sync();
+	const float per_camera_loss_scale = (float)n / 128.0f / (float)tr.n_steps_between_cam_updates;
+	const float lr_base = current_learning_rate();
+	float mean[3] = {0.f, 0.f, 0.f};
+	for (uint32_t i = 0; i < n; ++i) {
+		NerfTraining::Adam3& o = tr.cam_exposure[i];
+		++o.iter;
+		const float beta1 = 0.9f, beta2 = 0.99f, eps = 1e-8f;
+		const float lr = lr_base * std::sqrt(1.0f - std::pow(beta2, (float)o.iter)) / (1.0f - std::pow(beta1, (float)o.iter));
+		for (int k = 0; k < 3; ++k) {
+			const float grad = g[3 * i + k] * per_camera_loss_scale + o.variable[k] * tr.exposure_l2_reg;
+			o.m[k] = beta1 * o.m[k] + (1.0f - beta1) * grad;
+			o.v[k] = beta2 * o.v[k] + (1.0f - beta2) * grad * grad;
+			o.variable[k] -= lr * o.m[k] / (std::sqrt(o.v[k]) + eps);
+			mean[k] += o.variable[k];
+		}
+	}
+	std::vector<float> e(n_img * 3, 0.0f);
+	for (uint32_t i = 0; i < n; ++i)
+		for (int k = 0; k < 3; ++k) e[3 * i + k] = tr.cam_exposure[i].variable[k] -= mean[k] / (float)n;
+	for (size_t i = n; i < n_img; ++i)
+		for (int k = 0; k < 3; ++k) e[3 * i + k] = tr.cam_exposure[i].variable[k];
+	hk(hipMemcpyAsync(m_exp, e.data(), e.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "exposure h2d");
+	tr.n_steps_since_cam_update = 0;
 }
 
 std::vector<float> Testbed::error_map_data() {

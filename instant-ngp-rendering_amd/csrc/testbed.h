@@ -99,6 +99,15 @@ struct NerfTraining {
 	bool sample_focal_plane_proportional_to_error = false;
 	bool sample_image_proportional_to_error = false;
 	bool include_sharpness_in_error = false;  // not supported (no per-image sharpness data)
+	// per-image exposure optimisation (Nerf::Training::cam_exposure, nerf.h:65-79, 87-91)
+	struct Adam3 {
+		vec3 variable = {0.f, 0.f, 0.f}, m = {0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f};
+		uint32_t iter = 0;
+	};
+	std::vector<Adam3> cam_exposure;
+	float exposure_l2_reg = 0.0f;
+	uint32_t n_steps_between_cam_updates = 16;
+	uint32_t n_steps_since_cam_update = 0;
 	uint32_t n_steps_between_error_map_updates = 128;
 	uint32_t n_steps_since_error_map_update = 0;
 	uint32_t n_rays_since_error_map_update = 0;
@@ -224,6 +233,12 @@ private:
 	ngp_model* m_model = nullptr;
 	void* m_stream = nullptr;
 	// error map (device): data [n_images][res.y][res.x], CDFs at cdf_resolution
+	float* m_exp = nullptr;       // [n_images][3] log2 exposure (device)
+	float* m_exp_grad = nullptr;  // [n_images][3]
+	size_t m_exp_cap = 0;
+	ngp_network_config m_net_cfg{};
+	void update_cam_exposure();
+	float current_learning_rate() const;
 	float* m_err = nullptr;
 	float* m_cdf_x = nullptr;
 	float* m_cdf_y = nullptr;

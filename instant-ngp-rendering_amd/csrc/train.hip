@@ -156,7 +156,7 @@ struct SamplerArgs {
 template <bool GENERAL>
 __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint32_t n_images, uint32_t gi,
                                                   uint32_t n_rays_global, const ErrorCdf& cdf, int snap, pcg32& rng,
-                                                  float* uo, float* vo, float* pdf = nullptr) {
+                                                  float* uo, float* vo, float* pdf = nullptr, float* uv_pdf_out = nullptr) {
 	uint32_t img;
 	float img_pdf = 1.0f, uv_pdf = 1.0f;
 	if (GENERAL && cdf.img) {
@@ -169,6 +169,7 @@ __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint
 	float u = rng.next_float(), v = rng.next_float();
 	if (GENERAL && cdf.x_cond_y) sample_cdf_2d(&u, &v, img, cdf, &uv_pdf);
 	if (pdf) *pdf = img_pdf * uv_pdf;
+	if (uv_pdf_out) *uv_pdf_out = uv_pdf;
 	if (snap) {
 		int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
 		px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
@@ -314,6 +315,9 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 struct LossArgs {
 	const ngp_image* images;
 	ErrorCdf cdf;
+	const float* exposure;     // [n_images][3] log2 exposure (null: 0)
+	float* exposure_grad;      // [n_images][3] (null: off)
+	float4* ray_aux;           // [R]: the ray's dL/dexposure, deposited by k_loss_emit if the ray is kept
 	float* error_map;
 	uint32_t error_map_rx, error_map_ry;
 	uint32_t n_images;
@@ -428,8 +432,9 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	const uint32_t gi = a.ray_offset + i;
 	pcg32 rng = a.rng;
 	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
-	float u, v, pdf;
-	const uint32_t img = training_pixel<GENERAL>(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v, &pdf);
+	float u, v, pdf, uv_pdf;
+	const uint32_t img =
+	    training_pixel<GENERAL>(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v, &pdf, &uv_pdf);
 	const ngp_image im = a.images[img];
 	rng.advance(1);  // motionblur_time
 	v3 bg = a.bg;
@@ -440,6 +445,14 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	bg = mk3(srgb_to_linear(bg.x), srgb_to_linear(bg.y), srgb_to_linear(bg.z));
 	float tex[4];
 	texel_rgba(read_texel(im, u, v), tex);
+	v3 es = mk3(1.0f);  // exposure_scale = 2^exposure[img]
+	if (a.exposure) {
+		const float* e = a.exposure + 3 * (size_t)img;
+		es = mk3(expf(0.6931471805599453f * e[0]), expf(0.6931471805599453f * e[1]), expf(0.6931471805599453f * e[2]));
+	}
+	tex[0] *= es.x;
+	tex[1] *= es.y;
+	tex[2] *= es.z;
 	v3 target;
 	if (a.linear_colors || a.color_space == 0) {
 		target = mk3(tex[0], tex[1], tex[2]) + bg * (1.0f - tex[3]);
@@ -468,6 +481,16 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	ls[3] = rgb_ray.x; ls[4] = rgb_ray.y; ls[5] = rgb_ray.z;
 	ls[6] = mean_loss;
 	ls[7] = __uint_as_float(img);  // the error deposit (k_loss_emit) reuses the pixel
+	if (a.exposure_grad) {
+		// symmetric loss: dL/dtarget = -dL/dprediction (src/testbed_nerf.cu:1121-1134)
+		v3 dgt = mk3(-gx / uv_pdf, -gy / uv_pdf, -gz / uv_pdf);
+		if (!a.linear_colors)
+			dgt = mk3(dgt.x / srgb_to_linear_derivative(target.x), dgt.y / srgb_to_linear_derivative(target.y),
+			          dgt.z / srgb_to_linear_derivative(target.z));
+		const float ls_scale = 128.0f / (float)a.n_rays_global;  // LOSS_SCALE / n_rays
+		a.ray_aux[i] = make_float4(ls_scale * dgt.x * es.x * 0.6931471805599453f, ls_scale * dgt.y * es.y * 0.6931471805599453f,
+		                           ls_scale * dgt.z * es.z * 0.6931471805599453f, 0.0f);
+	}
 	a.ray_state[8 * (size_t)i + 6] = u;
 	a.ray_state[8 * (size_t)i + 7] = v;
 	a.ccounts[i] = c;
@@ -489,6 +512,13 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 	if (cn == 0) {
 		if (lane == 0) a.loss_out[i] = 0.0f;
 		return;
+	}
+	if (a.exposure_grad && lane == 0) {
+		const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
+		const float4 g = a.ray_aux[i];
+		atomicAdd(&a.exposure_grad[3 * (size_t)img + 0], g.x);
+		atomicAdd(&a.exposure_grad[3 * (size_t)img + 1], g.y);
+		atomicAdd(&a.exposure_grad[3 * (size_t)img + 2], g.z);
 	}
 	if (a.error_map && lane == 0) {
 		// bilinear deposit of the ray's mean loss (src/testbed_nerf.cu:1028-1054; rays without
@@ -840,6 +870,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.snap = t->snap_to_pixel_centers;
 	la.cdf = sa.cdf;
 	la.error_map = t->error_map;
+	la.exposure = t->exposure;
+	la.exposure_grad = t->exposure_gradient;
+	ts.ray_aux.reserve(4 * (size_t)R);
+	la.ray_aux = reinterpret_cast<float4*>(ts.ray_aux.ptr);
 	la.error_map_rx = t->error_map_res[0];
 	la.error_map_ry = t->error_map_res[1];
 	la.loss_type = t->loss_type;

@@ -797,7 +797,8 @@ static uint32_t cdf_search(float val, const float* data, uint32_t length) {
 
 // image_idx + nerf_random_image_pos_training with the error-map CDFs (nerf_device.cuh:495-598);
 // *pdf = img_pdf * uv_pdf (uv_pdf stays 1 on the uniform half of sample_cdf_2d).
-static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, Pcg& rng, float* u, float* vv, float* pdf) {
+static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, Pcg& rng, float* u, float* vv, float* pdf,
+                           float* uv_pdf_out = nullptr) {
 	uint32_t img;
 	float img_pdf = 1.0f, uv_pdf = 1.0f;
 	if (a.cdf_img) {
@@ -838,6 +839,7 @@ static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, P
 	*u = x;
 	*vv = y;
 	if (pdf) *pdf = img_pdf * uv_pdf;
+	if (uv_pdf_out) *uv_pdf_out = uv_pdf;
 	return img;
 }
 
@@ -943,7 +945,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1119)
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	std::vector<uint32_t> cc(R, 0);
-	std::vector<float> lstate(8 * (size_t)R, 0.0f);
+	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f);
 	for (uint32_t i = 0; i < R; ++i) {
 		const uint32_t ns = M.ray_numsteps[2 * i], b0 = M.ray_numsteps[2 * i + 1];
 		if (ns == 0) continue;
@@ -966,8 +968,9 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		rng.state = a.rng_state;
 		rng.inc = a.rng_inc;
 		rng.advance((int64_t)gi * 16);
-		float u, vv, pdf;
-		const ngp_image& im = a.images[pick_pixel(a, gi, nrg, rng, &u, &vv, &pdf)];
+		float u, vv, pdf, uv_pdf;
+		const uint32_t img = pick_pixel(a, gi, nrg, rng, &u, &vv, &pdf, &uv_pdf);
+		const ngp_image& im = a.images[img];
 		rng.advance(1);
 		V3 bg = v(a.background_color[0], a.background_color[1], a.background_color[2]);
 		if (a.random_bg_color) {
@@ -977,6 +980,10 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		bg = v(s2l(bg.x), s2l(bg.y), s2l(bg.z));
 		float tex[4];
 		rgba_of(texel(im, u, vv), tex);
+		float es[3] = {1.0f, 1.0f, 1.0f};  // exposure_scale = 2^exposure[img] (src/testbed_nerf.cu:966)
+		if (a.exposure)
+			for (int k = 0; k < 3; ++k) es[k] = std::exp(0.6931471805599453f * a.exposure[3 * img + k]);
+		for (int k = 0; k < 3; ++k) tex[k] *= es[k];
 		V3 tgt;
 		if (a.train_in_linear_colors || a.color_space == 0) {
 			tgt = v(tex[0], tex[1], tex[2]) + bg * (1.0f - tex[3]);
@@ -996,6 +1003,18 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		float* ls = &lstate[8 * (size_t)i];
 		ls[0] = gx; ls[1] = gy; ls[2] = gz; ls[3] = rr; ls[4] = rg; ls[5] = rb;
 		ls[6] = (lx / pdf + ly / pdf + lz / pdf) / 3.0f;  // lg.loss /= img_pdf * uv_pdf (src/testbed_nerf.cu:1010)
+		ls[7] = (float)img;
+		if (a.exposure_gradient) {  // src/testbed_nerf.cu:1121-1134, deposited below for kept rays
+			const float g[3] = {gx, gy, gz}, t3[3] = {tgt.x, tgt.y, tgt.z};
+			for (int k = 0; k < 3; ++k) {
+				float d = -g[k] / uv_pdf;
+				if (!a.train_in_linear_colors) {
+					const float sd = t3[k] <= 0.04045f ? 1.0f / 12.92f : 2.4f / 1.055f * std::pow((t3[k] + 0.055f) / 1.055f, 1.4f);
+					d = d / sd;
+				}
+				expg[3 * (size_t)i + k] = (128.0f / (float)nrg) * d * es[k] * 0.6931471805599453f;
+			}
+		}
 		cc[i] = c;
 	}
 	M.ray_compacted.assign(2 * (size_t)R, 0);
@@ -1016,6 +1035,8 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		if (cn == 0) continue;
 		const float* ls = &lstate[8 * (size_t)i];
 		M.loss[i] = ls[6] / (float)nrg;
+		if (a.exposure_gradient)
+			for (int k = 0; k < 3; ++k) a.exposure_gradient[3 * (size_t)ls[7] + k] += expg[3 * (size_t)i + k];
 		if (a.error_map) {  // bilinear error deposit (src/testbed_nerf.cu:1028-1054)
 			const uint32_t gi = a.ray_index_offset + i;
 			Pcg rng;

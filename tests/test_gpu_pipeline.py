@@ -368,3 +368,35 @@ def test_render_lens_matches_oracle():
         assert np.abs(gf - of).mean() < 1e-3
     finally:
         g.close()
+
+
+def test_train_step_exposure_matches_oracle():
+    """Per-image exposure scales the targets (2^e) and yields dL/dexposure for the kept rays
+    (src/testbed_nerf.cu:966-985, 1121-1134): loss and gradient against the oracle."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 384, 4096, 1 << 15
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        exp_h = rng.uniform(-0.5, 0.5, (6, 3)).astype(np.float32)
+        grad_h = np.zeros((6, 3), np.float32)
+        exp_d, grad_d = torch.from_numpy(exp_h).cuda(), torch.zeros(6, 3, device="cuda")
+        ga.exposure, ga.exposure_gradient = exp_d.data_ptr(), grad_d.data_ptr()
+        oa.exposure, oa.exposure_gradient = exp_h.ctypes.data, grad_h.ctypes.data
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+        np.testing.assert_array_equal(gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32),
+                                      o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32))
+        gst = A.TrainStats()
+        A.check(g.lib.ngp_train_read_stats(g.h, C.byref(gst), stream()))
+        np.testing.assert_allclose(gst.loss, o.stats().loss, rtol=2e-2)
+        gg = grad_d.cpu().numpy()
+        assert np.abs(grad_h).sum() > 0
+        assert np.linalg.norm(gg - grad_h) / np.linalg.norm(grad_h) < 5e-2
+    finally:
+        g.close()

@@ -174,3 +174,26 @@ def test_error_map_importance_sampling(scene):
     assert pmf.shape == (12,) and abs(pmf.sum() - 1.0) < 1e-4 and pmf.min() >= 0.1 / 12 - 1e-6
     assert tr.n_steps_between_error_map_updates > 16  # grows x1.5 per update
     assert np.isfinite(losses).all() and np.mean(losses[-16:]) < 0.6 * np.mean(losses[:16])
+
+
+def test_exposure_optimisation(scene):
+    """optimize_exposure: per-image Adam on dL/dexposure every n_steps_between_cam_updates,
+    re-centred to zero mean (src/testbed_nerf.cu:2650-2677)."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    tr = tb.nerf.training
+    tr.optimize_exposure = True
+    tb.shall_train = True
+    losses = []
+    while tb.training_step < 200:
+        tb.frame()
+        losses.append(tb.loss)
+    e = np.asarray(tr.cam_exposure)
+    assert e.shape == (12, 3) and np.abs(e).max() > 0
+    np.testing.assert_allclose(e.mean(axis=0), 0.0, atol=1e-5)
+    assert np.isfinite(losses).all() and np.mean(losses[-16:]) < 0.6 * np.mean(losses[:16])
+    tr.optimize_extrinsics = True
+    with pytest.raises(RuntimeError):
+        tb.frame()
