@@ -209,12 +209,15 @@ __device__ __forceinline__ void scatter_add(__half* gtab, uint32_t idx, const fl
 	}
 }
 
-// Backward scatter.  Lanes of a wave hold consecutive samples of the compacted batch,
-// i.e. consecutive points along the same rays, so at the coarse levels neighbouring
-// lanes very often add into the same corner.  Runs of equal indices are summed across
-// lanes first (segmented shuffle scan) and only the last lane of each run issues the
-// global float atomic: the per-address contention that dominates the coarse levels
-// disappears, and waves without any run take the plain path.
+// Backward scatter.  Two lanes per (sample, level): lane 2s+h adds the four corners
+// x + h of sample s, so in every atomic instruction the x and x+1 corners of a sample sit
+// in adjacent lanes -- adjacent table entries (hashed: index ^ (x ^ (x+1)); dense: +1),
+// nearly always in the same 64-byte line, which the memory-side atomic unit takes as one
+// request instead of two.  Lanes of a parity hold consecutive samples of the compacted
+// batch, i.e. consecutive points along the same rays, so at coarse levels they often add
+// into the same corner: runs of equal indices (lane, lane+2, ...) are summed with a
+// segmented shuffle scan and only the last lane of each run issues the atomic.
+constexpr uint32_t BWD_SAMPLES_PER_BLOCK = 128;
 template <uint32_t F>
 __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ denc, uint32_t enc_plane,
@@ -222,9 +225,9 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
                                                       uint32_t n_chunks, const uint32_t* __restrict__ n_dev) {
 	uint32_t level, chunk;
 	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
-	const uint32_t i = chunk * 256u + threadIdx.x;
+	const uint32_t i = chunk * BWD_SAMPLES_PER_BLOCK + (threadIdx.x >> 1), h = threadIdx.x & 1u;
 	if (n_dev) n = min(n, *n_dev);
-	if (chunk * 256u >= n) return;  // whole block idle (block-uniform)
+	if (chunk * BWD_SAMPLES_PER_BLOCK >= n) return;  // whole block idle (block-uniform)
 	const int lane = threadIdx.x & 63;
 
 	using VT = typename FeatVec<F>::T;
@@ -253,44 +256,43 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 		pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
 		pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
 	}
-	const unsigned long long lanes_below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+	const float wx = h ? fx : 1.0f - fx;
+	// lanes of this lane's parity at or below it
+	const unsigned long long parity = (lane & 1) ? 0xAAAAAAAAAAAAAAAAull : 0x5555555555555555ull;
+	const unsigned long long at_or_below = (lane == 63 ? ~0ull : ((2ull << lane) - 1ull)) & parity;
 
 #pragma unroll
-	for (uint32_t c = 0; c < 8; ++c) {
-		float w = 1.0f;
-		w *= (c & 1u) ? fx : 1.0f - fx;
-		w *= (c & 2u) ? fy : 1.0f - fy;
-		w *= (c & 4u) ? fz : 1.0f - fz;
-		const uint32_t idx = active ? grid_index(hashed, size, res, gx + (c & 1u), gy + ((c >> 1) & 1u), gz + ((c >> 2) & 1u))
+	for (uint32_t c = 0; c < 4; ++c) {
+		float w = wx;
+		w *= (c & 1u) ? fy : 1.0f - fy;
+		w *= (c & 2u) ? fz : 1.0f - fz;
+		const uint32_t idx = active ? grid_index(hashed, size, res, gx + h, gy + (c & 1u), gz + ((c >> 1) & 1u))
 		                            : 0xFFFFFFFFu - (uint32_t)lane;  // inactive lanes never merge
 		float v[F];
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) v[f] = w * g[f];
-		const uint32_t prev = __shfl_up(idx, 1, 64);
-		const bool head = lane == 0 || prev != idx;
+		const uint32_t prev = __shfl_up(idx, 2, 64);
+		const bool head = lane < 2 || prev != idx;
 		const unsigned long long heads = __ballot(head);
 		if (~heads == 0ull) {
-			if (active) {
-				scatter_add<F>(gtab, idx, v);
-			}
+			if (active) scatter_add<F>(gtab, idx, v);
 			continue;
 		}
-		// run start of this lane = highest head at or below it
-		const int start = 63 - __clzll(heads & (lanes_below | (1ull << lane)));
+		// run start of this lane = highest head of its parity at or below it
+		const int start = 63 - __clzll(heads & at_or_below);
 #pragma unroll
-		for (int off = 1; off < 64; off <<= 1) {
+		for (int off = 2; off < 64; off <<= 1) {
 #pragma unroll
 			for (uint32_t f = 0; f < F; ++f) {
 				const float t = __shfl_up(v[f], off, 64);
 				if (lane - off >= start) v[f] += t;
 			}
 		}
-		const bool tail = lane == 63 || ((heads >> (lane + 1)) & 1ull);
-		if (active && tail) {
-			scatter_add<F>(gtab, idx, v);
-		}
+		const bool tail = lane >= 62 || ((heads >> (lane + 2)) & 1ull);
+		if (active && tail) scatter_add<F>(gtab, idx, v);
 	}
 }
+
 
 __global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                           const LevelTable lt, uint32_t* __restrict__ idx_out,
@@ -342,7 +344,7 @@ void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                          uint32_t enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev) {
 	if (n == 0) return;
-	const uint32_t n_chunks = div_up(n, 256);
+	const uint32_t n_chunks = div_up(n, BWD_SAMPLES_PER_BLOCK);
 	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
 		case 1: k_hashgrid_bwd<1><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
