@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--width", type=int, default=1920)
     p.add_argument("--height", type=int, default=1080)
     p.add_argument("--cpu-baseline", type=int, default=1)
+    p.add_argument("--kernel-timer", type=int, default=1,
+                   help="time the dominant kernel in the timed run (0: diagnostic runs without timer events)")
     p.add_argument("--cpu-rows", type=int, default=8, help="1080p rows rendered by the CPU oracle sample")
     p.add_argument("--cpu-rays", type=int, default=512, help="training rays in the CPU oracle sample")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
@@ -253,7 +255,7 @@ def main():
     calib = read_timers(A, lib, h)
     modeled = [k for k in models if calib.get(k, (0, 0, 0))[2] > 0]
     dom = max(modeled, key=lambda k: calib[k][0]) if modeled else "render_encode"
-    A.check(lib.ngp_timing_enable(C.c_void_p(h), 1 << A.TIMER[dom]))
+    A.check(lib.ngp_timing_enable(C.c_void_p(h), (1 << A.TIMER[dom]) if args.kernel_timer else 0))
     read_timers(A, lib, h)  # reset
 
     barrier()
@@ -293,7 +295,7 @@ def main():
                 entry["frac"] = round(rate / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)
         kernels[name] = entry
     bound, per_unit = models[dom]
-    ms, units, launches = timers[dom]
+    ms, units, launches = timers[dom] if args.kernel_timer else calib[dom]
     achieved = units * per_unit / launches / (ms / launches / 1000.0)
     roofline = {
         "kernel": dom,

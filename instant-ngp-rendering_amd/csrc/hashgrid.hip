@@ -324,10 +324,10 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 	const uint32_t n_chunks = div_up(n, 256);
 	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
-		case 1: k_hashgrid_fwd<1, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 2: k_hashgrid_fwd<2, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 4: k_hashgrid_fwd<4, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 8: k_hashgrid_fwd<8, SITE><<<blocks, 256, 0, s>>>(n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 1: launch_timed(k_hashgrid_fwd<1, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 2: launch_timed(k_hashgrid_fwd<2, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 4: launch_timed(k_hashgrid_fwd<4, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 8: launch_timed(k_hashgrid_fwd<8, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
 		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
 	}
 }
@@ -347,10 +347,10 @@ void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride
 	const uint32_t n_chunks = div_up(n, BWD_SAMPLES_PER_BLOCK);
 	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
-		case 1: k_hashgrid_bwd<1><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
-		case 2: k_hashgrid_bwd<2><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
-		case 4: k_hashgrid_bwd<4><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
-		case 8: k_hashgrid_bwd<8><<<blocks, 256, 0, s>>>(n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 1: launch_timed(k_hashgrid_bwd<1>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 2: launch_timed(k_hashgrid_bwd<2>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 4: launch_timed(k_hashgrid_bwd<4>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 8: launch_timed(k_hashgrid_bwd<8>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
 		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
 	}
 	NGP_HIP_CHECK(hipGetLastError());

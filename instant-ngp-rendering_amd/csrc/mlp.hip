@@ -945,9 +945,9 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);
-		if (a.F == 2) k_mlp_infer_rf<N, 1, 2, false, 2><<<grid, BLOCK, lds, s>>>(a);
-		else if (a.F == 4) k_mlp_infer_rf<N, 1, 2, false, 4><<<grid, BLOCK, lds, s>>>(a);
-		else k_mlp_infer_rf<N, 1, 2, false, 0><<<grid, BLOCK, lds, s>>>(a);
+		if (a.F == 2) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 2>, grid, BLOCK, lds, s, a);
+		else if (a.F == 4) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 4>, grid, BLOCK, lds, s, a);
+		else launch_timed(k_mlp_infer_rf<N, 1, 2, false, 0>, grid, BLOCK, lds, s, a);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }
@@ -995,7 +995,7 @@ void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc
 		if (lds > 160 * 1024) throw std::runtime_error("MLP training LDS footprint exceeds 160 KiB");
 		set_lds<N>(k_mlp_train<N>, lds);
 		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count());
-		k_mlp_train<N><<<grid, BLOCK, lds, s>>>(a);
+		launch_timed(k_mlp_train<N>, grid, BLOCK, lds, s, a);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }

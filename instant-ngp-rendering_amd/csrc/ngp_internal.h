@@ -3,6 +3,7 @@
 
 #include <hip/hip_runtime.h>
 #include <hip/hip_fp16.h>
+#include <hip/hip_ext.h>
 
 #include <stdexcept>
 #include <string>
@@ -21,7 +22,25 @@ namespace ngp {
 		}                                                                                                 \
 	} while (0)
 
-// HIP-event timers around launch groups (ngp_timing_enable / ngp_timing_read).
+// Start/stop events bound to the next launch_timed() dispatch on this thread
+// (hipExtLaunchKernelGGL): the timestamps come from the kernel's own dispatch packet, so a
+// timed kernel costs no marker packets (each hipEventRecord drains the queue, ~5 us).
+struct LaunchEvents {
+	hipEvent_t a = nullptr, b = nullptr;
+};
+inline thread_local LaunchEvents g_launch_events;
+
+template <class K, class... Args>
+inline void launch_timed(K kernel, dim3 grid, dim3 block, uint32_t lds, hipStream_t s, Args... args) {
+	const LaunchEvents e = g_launch_events;
+	g_launch_events = LaunchEvents{};
+	if (e.a) hipExtLaunchKernelGGL(kernel, grid, block, lds, s, e.a, e.b, 0u, args...);
+	else kernel<<<grid, block, lds, s>>>(args...);
+}
+
+// HIP-event timers around launch groups (ngp_timing_enable / ngp_timing_read).  A group
+// that is exactly one launch_timed() kernel is opened with begin_kernel(): its events ride
+// on that dispatch instead of being recorded around it.
 struct KernelTimers {
 	struct Pending {
 		int slot;
@@ -32,6 +51,7 @@ struct KernelTimers {
 	std::vector<hipEvent_t> pool;
 	std::vector<Pending> pending;
 	hipEvent_t open[NGP_TIMER_COUNT] = {};
+	hipEvent_t open_stop[NGP_TIMER_COUNT] = {};  // begin_kernel(): stop event of the bound dispatch
 	double ms[NGP_TIMER_COUNT] = {};
 	uint64_t units[NGP_TIMER_COUNT] = {};
 	uint32_t launches[NGP_TIMER_COUNT] = {};
@@ -52,8 +72,27 @@ struct KernelTimers {
 		open[slot] = take();
 		NGP_HIP_CHECK(hipEventRecord(open[slot], s));
 	}
+	void begin_kernel(int slot) {
+		if (!on(slot)) return;
+		open[slot] = take();
+		open_stop[slot] = take();
+		g_launch_events = LaunchEvents{open[slot], open_stop[slot]};
+	}
 	void end(int slot, hipStream_t s, uint64_t u = 0) {
 		if (!on(slot) || !open[slot]) return;
+		if (open_stop[slot]) {
+			if (g_launch_events.a == open[slot]) {  // nothing was launched (n == 0): no sample
+				g_launch_events = LaunchEvents{};
+				pool.push_back(open[slot]);
+				pool.push_back(open_stop[slot]);
+			} else {
+				pending.push_back({slot, open[slot], open_stop[slot]});
+				units[slot] += u;
+				++launches[slot];
+			}
+			open[slot] = open_stop[slot] = nullptr;
+			return;
+		}
 		hipEvent_t e = take();
 		NGP_HIP_CHECK(hipEventRecord(e, s));
 		pending.push_back({slot, open[slot], e});
@@ -173,7 +212,9 @@ struct RenderScratch {
 	DevBuf<__half> enc;         // [L][n*8][F]
 	DevBuf<__half> out;         // [n*8][4]
 	DevBuf<uint32_t> counters;  // [4]
-	DevBuf<uint32_t> host_counter;
+	DevBuf<uint32_t> host_counter;  // pinned, fine-grained (hipHostMalloc): per-pass counters
+	uint32_t* host_counter_dev = nullptr;  // its device address
+	uint32_t pass_tag = 0;          // tags of published passes (monotonic across renders)
 	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]

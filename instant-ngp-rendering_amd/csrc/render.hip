@@ -318,6 +318,22 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 	}
 }
 
+// Publishes the tracer's counters [0, 8) of the previous pass to pinned host memory, so the
+// host learns a pass's sizes by polling instead of enqueueing a copy and an event after
+// every pass (each costs a queue drain).  Called by the first 8 threads of the first
+// workgroup of the next pass's k_generate (the previous pass's kernels have all finished,
+// and the counters it reads are not touched by this launch), or by k_publish after the
+// last pass.  Each counter goes out as one 8-byte store (tag << 32 | value): the host
+// waits until all eight words carry the pass's tag, so no store ordering -- and no fence --
+// is needed.
+__device__ __forceinline__ void publish_counters(const uint32_t* counters, unsigned long long* host, uint32_t tag) {
+	const uint32_t v = __hip_atomic_load(counters + threadIdx.x, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+	__hip_atomic_store(host + threadIdx.x, ((unsigned long long)tag << 32) | v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+__global__ void k_publish(const uint32_t* __restrict__ counters, unsigned long long* host, uint32_t tag) {
+	if (threadIdx.x < 8) publish_counters(counters, host, tag);
+}
+
 // Samples a ray gets this pass: up to n_steps, fewer when its transmittance is already low
 // -- enough to reach min_transmittance at the opacity of its last sample, with headroom.
 // A short estimate only costs the ray another pass; samples past a ray's termination are
@@ -344,7 +360,11 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __r
                                                   float4* __restrict__ posdt, float4* __restrict__ dirs,
                                                   uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
-                                                  uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out) {
+                                                  uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
+                                                  const uint32_t* counters, unsigned long long* host_prev, uint32_t tag_prev) {
+	// the previous pass's counters, before this block zeroes next_alive_counter / steps_out
+	if (host_prev && blockIdx.x == 0 && threadIdx.x < 8) publish_counters(counters, host_prev, tag_prev);
+	__syncthreads();
 	// the pass is sized on the device: the host enqueues passes ahead of their read-backs
 	const uint32_t n_alive = *alive_counter;
 	// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
@@ -676,8 +696,13 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.dbg = debug ? rs.counters.ptr + 8 : nullptr;
 	if (debug) NGP_HIP_CHECK(hipMemsetAsync(k.dbg, 0, 8 * sizeof(uint32_t), s));
 	if (!rs.host_counter.ptr) {
-		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 16 * sizeof(uint32_t), hipHostMallocDefault));
-		rs.host_counter.n = 16;
+		// [2][16] unpacked pass counters, [32, 40) copy-back slot, [64, 96) the published
+		// words ([2 slots][8] x (tag << 32 | value));
+		// fine-grained (coherent) so the kernel's system-scope stores reach the polling host
+		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 96 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+		std::memset(rs.host_counter.ptr, 0, 96 * sizeof(uint32_t));
+		rs.host_counter.n = 96;
+		NGP_HIP_CHECK(hipHostGetDevicePointer((void**)&rs.host_counter_dev, rs.host_counter.ptr, 0));
 	}
 	auto P = [&](int b) { return reinterpret_cast<Payload*>(rs.payload[b].ptr); };
 	auto C = [&](int b) { return reinterpret_cast<float4*>(rs.rgba[b].ptr); };
@@ -715,23 +740,45 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	if (!rs.events[0]) {
 		for (auto& e : rs.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 	}
-	uint32_t* hc = rs.host_counter.ptr;  // pinned [2 slots][8]
+	uint32_t* hc = rs.host_counter.ptr;  // pinned (layout at its allocation)
 	// sample records in two row arrays: the encoder reads 16-B position rows once per level
 	float4* posdt = reinterpret_cast<float4*>(rs.coords.ptr);
 	float4* dirs = posdt + max_samples;
-	auto read_back = [&](uint32_t pass) {
-		uint32_t* slot = hc + 8 * (pass % 2);
-		NGP_HIP_CHECK(hipMemcpyAsync(slot, rs.counters.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		NGP_HIP_CHECK(hipEventRecord(rs.events[pass % 2], s));
-	};
-	auto wait_slot = [&](uint32_t pass) -> const uint32_t* {
+	// copy-back (only after k_retire): counters -> slot [32, 40), then an event
+	auto read_back = [&]() -> const uint32_t* {
+		NGP_HIP_CHECK(hipMemcpyAsync(hc + 32, rs.counters.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipEventRecord(rs.events[0], s));
 		hipError_t e;
-		while ((e = hipEventQuery(rs.events[pass % 2])) == hipErrorNotReady) {
+		while ((e = hipEventQuery(rs.events[0])) == hipErrorNotReady) {
 		}
 		NGP_HIP_CHECK(e);
-		return hc + 8 * (pass % 2);
+		return hc + 32;
 	};
-	auto consume = [&](uint32_t pass) -> const uint32_t* {  // every pass's read-back is consumed once
+	// pass p's counters, published (k_generate of pass p + 1, or k_publish) as (tag << 32 | value) words with tag
+	// base_tag + p + 1; unpacked into hc[16 * (p % 2) ...]
+	const uint32_t base_tag = rs.pass_tag;
+	volatile unsigned long long* pub = reinterpret_cast<volatile unsigned long long*>(hc + 64);
+	unsigned long long* pub_dev = reinterpret_cast<unsigned long long*>(rs.host_counter_dev + 64);
+	auto wait_slot = [&](uint32_t pass) -> const uint32_t* {
+		volatile unsigned long long* w = pub + 8 * (pass % 2);
+		const uint32_t want = base_tag + pass + 1;
+		uint32_t* out = hc + 16 * (pass % 2);
+		for (uint32_t q = 0, spin = 1; q < 8; ++spin) {
+			const unsigned long long v = w[q];
+			if ((uint32_t)(v >> 32) == want) {
+				out[q++] = (uint32_t)v;
+				continue;
+			}
+			if ((spin & 4095u) == 0) {
+				const hipError_t e = hipStreamQuery(s);
+				if (e != hipSuccess && e != hipErrorNotReady) NGP_HIP_CHECK(e);
+				if (e == hipSuccess && (uint32_t)(w[q] >> 32) != want)
+					throw std::runtime_error("render: pass counters were not published");
+			}
+		}
+		return out;
+	};
+	auto consume = [&](uint32_t pass) -> const uint32_t* {  // every pass's counters are consumed once
 		const uint32_t* c = wait_slot(pass);
 		tm.add_units(NGP_TIMER_RENDER_ENCODE, c[4 + pass % 2]);
 		tm.add_units(NGP_TIMER_RENDER_MLP, c[4 + pass % 2]);
@@ -752,20 +799,22 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t want = lanes_target() / std::max(n_alive_ub, 1u);
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
 		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 256));
+		unsigned long long* host_prev = pass > 0 ? pub_dev + 8 * ((pass - 1) % 2) : nullptr;
+		const uint32_t tag_prev = base_tag + pass;  // = tag of pass - 1
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
-			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
-			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
-			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out); break;
+			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
 		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap, std::max(target, n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
-		tm.begin(NGP_TIMER_RENDER_ENCODE, s);
+		tm.begin_kernel(NGP_TIMER_RENDER_ENCODE);
 		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s);  // units: the pass's sample count, added at its read-back
-		tm.begin(NGP_TIMER_RENDER_MLP, s);
+		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
 		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, reinterpret_cast<const float*>(dirs), 4, n_elements, rs.out.ptr, s,
 		                 samples, 0);
 		tm.end(NGP_TIMER_RENDER_MLP, s);
@@ -776,7 +825,6 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		                                                                  alive_out, rs.counters.ptr + 2, samples_next);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
-		read_back(pass);
 		cur = 1 - cur;
 		++pass;
 		// the read-back of the previous pass bounds the next one
@@ -787,6 +835,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			if (n_alive_ub == 0 || steps_done >= MARCH_ITER) break;
 		}
 	}
+	k_publish<<<1, 64, 0, s>>>(rs.counters.ptr, pub_dev + 8 * ((pass - 1) % 2), base_tag + pass);
+	NGP_HIP_CHECK(hipGetLastError());
 	const uint32_t* last = consume(pass - 1);
 	uint32_t n_alive = last[pass % 2];
 	uint32_t n_hit = last[2];
@@ -794,9 +844,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// march budget exhausted: still-alive rays are shaded with what they accumulated
 		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,
 		                                              rs.counters.ptr);
-		read_back(pass);
-		n_hit = wait_slot(pass)[2];
+		n_hit = read_back()[2];
 	}
+	rs.pass_tag = base_tag + pass;
 	if (debug) {
 		uint32_t d[8];
 		NGP_HIP_CHECK(hipMemcpyAsync(d, k.dbg, sizeof(d), hipMemcpyDeviceToHost, s));

@@ -729,8 +729,8 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.steps = m->adam_steps.ptr;
 	a.ema32 = m->ema32.ptr;
 	a.ema16 = m->infer16.ptr;
-	m->timers.begin(NGP_TIMER_OPTIMIZER, s);
-	k_optimizer<<<div_up(a.n, 256), 256, 0, s>>>(a);
+	m->timers.begin_kernel(NGP_TIMER_OPTIMIZER);
+	launch_timed(k_optimizer, div_up(a.n, 256), 256, 0, s, a);
 	m->timers.end(NGP_TIMER_OPTIMIZER, s, a.n);
 	NGP_HIP_CHECK(hipGetLastError());
 	++m->ema_step;
@@ -850,11 +850,11 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 
 	// network inference over every emitted sample (NerfNetwork::inference_mixed_precision, training params)
-	tm.begin(NGP_TIMER_TRAIN_ENCODE, s);
+	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
 	launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
 	                    ts.counters.ptr + 4, 0);
 	tm.end(NGP_TIMER_TRAIN_ENCODE, s);
-	tm.begin(NGP_TIMER_TRAIN_MLP_INFER, s);
+	tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
 	launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
 	                 ts.counters.ptr + 4);
 	tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
@@ -908,6 +908,35 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
 	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
 	NGP_HIP_CHECK(hipGetLastError());
+	static const bool train_debug = getenv("NGP_TRAIN_DEBUG") != nullptr;
+	if (train_debug) {
+		// samples per ray emitted vs composited before termination, and what a chunked
+		// (early-terminated) forward would evaluate under a few chunk schedules
+		std::vector<uint32_t> ns(2 * (size_t)R), cc(R);
+		NGP_HIP_CHECK(hipMemcpyAsync(ns.data(), ts.ray_numsteps.ptr, ns.size() * 4, hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipMemcpyAsync(cc.data(), la.ccounts, cc.size() * 4, hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipStreamSynchronize(s));
+		const uint32_t sched[4][4] = {{8, 16, 32, 1024}, {16, 32, 1024, 0}, {16, 48, 1024, 0}, {32, 1024, 0, 0}};
+		uint64_t sn = 0, sc = 0, ev[4] = {0, 0, 0, 0}, full = 0;
+		for (uint32_t i = 0; i < R; ++i) {
+			const uint32_t n = ns[2 * i], c = cc[i];
+			sn += n;
+			sc += std::min(c, n);
+			full += (c >= n);
+			for (int q = 0; q < 4; ++q) {
+				uint32_t e = 0;
+				for (int p = 0; p < 4 && sched[q][p]; ++p) {
+					e = std::min(n, sched[q][p]);
+					if (c < e || e == n) break;  // terminated inside the evaluated range
+				}
+				ev[q] += e;
+			}
+		}
+		fprintf(stderr, "[train] rays %u samples %llu composited %llu (%.1f%%) rays-unterminated %llu | chunked eval "
+		        "8/16/32/all %llu, 16/32/all %llu, 16/48/all %llu, 32/all %llu\n", R, (unsigned long long)sn,
+		        (unsigned long long)sc, 100.0 * sc / std::max<uint64_t>(sn, 1), (unsigned long long)full,
+		        (unsigned long long)ev[0], (unsigned long long)ev[1], (unsigned long long)ev[2], (unsigned long long)ev[3]);
+	}
 
 	// compacted batch size c = min(total, B); rollover multiplicity
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
@@ -922,11 +951,11 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	tm.end(NGP_TIMER_TRAIN_LOSS, s, R);
 
 	// fused MLP forward+backward, then hash-grid scatter (Trainer::training_step)
-	tm.begin(NGP_TIMER_TRAIN_MLP_BWD, s);
+	tm.begin_kernel(NGP_TIMER_TRAIN_MLP_BWD);
 	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, B, ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
-	tm.begin(NGP_TIMER_TRAIN_ENCODE_BWD, s);
+	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
 	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
