@@ -243,11 +243,14 @@ ngp_status ngp_train_read_stats(ngp_model* model, ngp_train_stats* stats, ngp_st
 enum {
 	NGP_SCRATCH_RAY_NUMSTEPS = 0, /* [n_rays][2] u32: (numsteps, base) after sampling */
 	NGP_SCRATCH_COORDS = 1,       /* [max_samples][8] f32: pos3, dt, dir3, pad */
-	NGP_SCRATCH_MLP_OUT = 2,      /* [max_samples][4] f16 */
+	NGP_SCRATCH_MLP_OUT = 2,      /* [max_samples][4] f16; the first RAY_EVALUATED samples of each ray */
 	NGP_SCRATCH_RAY_COMPACTED = 3,/* [n_rays][2] u32: (compacted numsteps, compacted base) */
 	NGP_SCRATCH_DLOSS = 4,        /* [target_batch][4] f16 */
 	NGP_SCRATCH_LOSS = 5,         /* [n_rays] f32 */
-	NGP_SCRATCH_COMPACT_COORDS = 6/* [target_batch][8] f32 */
+	NGP_SCRATCH_COMPACT_COORDS = 6,/* [target_batch][8] f32 */
+	NGP_SCRATCH_RAY_EVALUATED = 7 /* [n_rays] u32: samples of the ray the forward evaluated (bit 31 set); it
+	                                 stops once the transmittance is below the loss's threshold. Null when
+	                                 every sample was evaluated (NGP_TRAIN_CHUNKED=0) */
 };
 ngp_status ngp_train_scratch(ngp_model* model, int kind, void** dev_ptr, size_t* bytes);
 

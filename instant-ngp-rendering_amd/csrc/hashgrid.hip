@@ -142,18 +142,31 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 	}
 }
 
+template <uint32_t F>
+__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const float* __restrict__ pos, uint32_t stride,
+                                           const __half* __restrict__ table, const LevelTable& lt,
+                                           __half* __restrict__ enc, uint32_t enc_plane);
+
 // SITE only names the call site in profiles (0 training, 1 render, 2 density grid / API).
 template <uint32_t F, int SITE>
 __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ table, const LevelTable lt,
                                                       __half* __restrict__ enc, uint32_t enc_plane, uint32_t n_chunks,
                                                       const uint32_t* __restrict__ n_dev) {
-	uint32_t level, chunk;
-	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
-	const uint32_t i = chunk * 256u + threadIdx.x;
+	uint32_t level, chunk0;
+	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk0);
 	if (n_dev) n = min(n, *n_dev);
-	if (i >= n) return;
+	// n_chunks per level are launched; they stride over the chunks the count covers
+	for (uint32_t chunk = chunk0; chunk * 256u < n; chunk += n_chunks) {
+		const uint32_t i = chunk * 256u + threadIdx.x;
+		if (i < n) encode_one<F>(i, level, pos, stride, table, lt, enc, enc_plane);
+	}
+}
 
+template <uint32_t F>
+__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const float* __restrict__ pos, uint32_t stride,
+                                           const __half* __restrict__ table, const LevelTable& lt,
+                                           __half* __restrict__ enc, uint32_t enc_plane) {
 	const float scale = lt.scale[level];
 	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
 	using VT = typename FeatVec<F>::T;
@@ -320,8 +333,9 @@ __global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const floa
 
 template <int SITE>
 static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                            __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev) {
-	const uint32_t n_chunks = div_up(n, 256);
+                            __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, uint32_t max_chunks) {
+	uint32_t n_chunks = div_up(n, 256);
+	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
 	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
 		case 1: launch_timed(k_hashgrid_fwd<1, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
@@ -333,11 +347,12 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 }
 
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, int site) {
+                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, int site,
+                         uint32_t max_chunks) {
 	if (n == 0) return;
-	if (site == 0) launch_fwd_site<0>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev);
-	else if (site == 1) launch_fwd_site<1>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev);
-	else launch_fwd_site<2>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev);
+	if (site == 0) launch_fwd_site<0>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev, max_chunks);
+	else if (site == 1) launch_fwd_site<1>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev, max_chunks);
+	else launch_fwd_site<2>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev, max_chunks);
 	NGP_HIP_CHECK(hipGetLastError());
 }
 

@@ -208,6 +208,8 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		t.pos4.release(); t.cpos4.release(); t.ray_aux.release();
 		t.dloss.release(); t.cweight.release(); t.csrc.release(); t.denc.release(); t.loss.release(); t.block_sums.release();
 		t.counters.release(); t.scan_a.release(); t.scan_b.release();
+		t.epos.release(); t.edir.release(); t.eenc.release(); t.eout.release(); t.eidx.release();
+		t.ray_T.release(); t.ray_eval.release(); t.ray_ebase.release();
 		GridState& g = m->gs;
 		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
@@ -387,8 +389,12 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		st->measured_batch_size_before_compaction = c[0];
 		st->measured_batch_size = c[1];
 		KernelTimers& tm = m->timers;
+		if (m->ts.chunked)
+			for (int p = 0; p < 3; ++p) m->ts.last_rows[p] = c[12 + p];
 		if (tm.train_units_pending) {
-			const uint64_t all = std::min(c[0], m->ts.last_max_samples), comp = std::min(c[1], m->ts.last_target);
+			// samples the forward evaluated: all emitted ones, or the chunks' rows
+			const uint64_t all = m->ts.chunked ? (uint64_t)c[12] + c[13] + c[14] : std::min(c[0], m->ts.last_max_samples);
+			const uint64_t comp = std::min(c[1], m->ts.last_target);
 			tm.units[NGP_TIMER_TRAIN_ENCODE] += all;
 			tm.units[NGP_TIMER_TRAIN_MLP_INFER] += all;
 			tm.units[NGP_TIMER_TRAIN_MLP_BWD] += comp;
@@ -415,6 +421,10 @@ ngp_status ngp_train_scratch(ngp_model* m, int kind, void** ptr, size_t* bytes) 
 			case NGP_SCRATCH_DLOSS: *ptr = t.dloss.ptr; if (bytes) *bytes = B * 8; break;
 			case NGP_SCRATCH_LOSS: *ptr = t.loss.ptr; if (bytes) *bytes = R * 4; break;
 			case NGP_SCRATCH_COMPACT_COORDS: *ptr = t.ccoords.ptr; if (bytes) *bytes = B * 32; break;
+			case NGP_SCRATCH_RAY_EVALUATED:
+				*ptr = t.chunked ? t.ray_eval.ptr : nullptr;
+				if (bytes) *bytes = t.chunked ? R * 4 : 0;
+				break;
 			default: throw std::invalid_argument("unknown scratch kind");
 		}
 	});

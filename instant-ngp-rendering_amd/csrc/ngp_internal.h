@@ -184,9 +184,19 @@ struct TrainScratch {
 	DevBuf<__half> denc;               // [L][B][F]
 	DevBuf<float> loss;                // [R]
 	DevBuf<uint32_t> block_sums;       // scan scratch
-	DevBuf<uint32_t> counters;         // [16]: 0 numsteps total, 1 compacted total, 4 clamped S, 5 clamped c, 8 loss sum
+	DevBuf<uint32_t> counters;         // [16]: 0 numsteps total, 1 compacted total, 4 clamped S, 5 clamped c, 8 loss sum,
+	                                   //       12..14 evaluation rows of the forward chunks
 	DevBuf<uint32_t> scan_a;           // [2R] sampler counts | bases
 	DevBuf<uint32_t> scan_b;           // [2R] compacted counts | bases
+	// early-terminated forward (k_train_chunk): evaluation rows of the chunks, per-ray state
+	DevBuf<float> epos, edir;          // [MSE][4] pos + warped dt | warped direction
+	DevBuf<__half> eenc;               // [L][MSE][F]
+	DevBuf<__half> eout;               // [MSE][4]
+	DevBuf<uint32_t> eidx;             // [MS] sample -> evaluation row
+	DevBuf<float> ray_T;               // [R]
+	DevBuf<uint32_t> ray_eval, ray_ebase;  // [R]
+	bool chunked = false;              // last step ran the chunked forward
+	uint32_t last_rows[3] = {0, 0, 0}; // evaluation rows of each chunk in the last read-back step
 	uint32_t last_n_rays = 0, last_target = 0, last_max_samples = 0;
 };
 
@@ -270,8 +280,12 @@ inline void wait_stream(ngp_model* m, hipStream_t s) {
 	NGP_HIP_CHECK(e);
 }
 
+// n: bound on the samples (the device count *n_dev, when given, is the actual one).  max_chunks
+// > 0 caps the 256-sample chunks launched per level; the blocks then loop over the chunks
+// up to the device count (for large bounds that are rarely reached).
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2);
+                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2,
+                         uint32_t max_chunks = 0);
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                          uint32_t enc_plane, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr);
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,

@@ -12,6 +12,7 @@
 // rule the reference applies ("claim `numsteps` slots, drop the ray if
 // base + numsteps > cap") taken in ray-index order: deterministic, and
 // bit-identical to the scalar oracle.
+#include <cstring>
 #include <type_traits>
 
 #include "ngp_internal.h"
@@ -310,6 +311,170 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Early-terminated forward.  The reference runs the network over every sample the
+// sampler emitted (src/testbed_nerf.cu:2797-2802), but compute_loss_kernel_train_nerf
+// reads a ray's samples only up to the one where its transmittance falls below 1e-4
+// (:905-916) -- on a converged scene ~85 % of the samples lie behind that point.  Here
+// the forward runs over chunks of each ray's samples ([0, 16), [16, 48), [48, n)): after
+// a chunk, a ray whose transmittance is below half the loss kernel's threshold stops.
+// Every sample the loss kernels read is evaluated, with exactly the same network inputs,
+// so the loss, the compaction and the gradients do not change (the margin absorbs the
+// different association of the transmittance product).
+// ---------------------------------------------------------------------------
+constexpr uint32_t TRAIN_CHUNKS = 3;
+constexpr uint32_t TRAIN_CHUNK_END[TRAIN_CHUNKS] = {16, 48, NERF_STEPS};
+constexpr float TRAIN_CHUNK_STOP_T = 0.5e-4f;
+constexpr uint32_t RAY_EVAL_DONE = 0x80000000u;
+
+struct ChunkArgs {
+	uint32_t n_rays;
+	const uint32_t* numsteps;  // [R][2] samples, first sample (sampler)
+	const float* coords;       // [MS][8] sampler rows
+	const float4* pos4;        // [MS]
+	float4* epos;              // [MSE] evaluation rows: pos + warped dt
+	float4* edir;              // [MSE] warped direction
+	const __half* eout;        // [MSE][4] network outputs of the evaluation rows
+	__half* mlp_out;           // [MS][4] outputs scattered back to the sampler layout
+	uint32_t* eidx;            // [MS] sample -> evaluation row (the compacted gather reads the encoding there)
+	float* ray_T;              // [R] transmittance before the ray's next unevaluated sample
+	uint32_t* ray_eval;        // [R] samples evaluated and scattered; | RAY_EVAL_DONE once the ray stopped
+	uint32_t* ray_ebase;       // [R] evaluation row of the ray's current chunk
+	uint32_t* rows;            // evaluation rows claimed for the next chunk
+	uint32_t prev_lo, lo, hi;  // previous chunk [prev_lo, lo); next chunk [lo, hi) (lo == hi: none)
+	uint32_t eval_offset;      // evaluation row of the next chunk's first claim
+	int first, last;
+	int density_act;
+};
+
+// Block-cooperative row loop: thread t owns cnt rows (k = 0..cnt-1); the block's rows are
+// dealt to its 256 threads in order, so consecutive lanes move consecutive rows.
+template <class Op>
+__device__ __forceinline__ void block_rows(uint32_t cnt, uint32_t* s_off, Op op) {
+	__shared__ uint32_t wsum[4];
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	uint32_t x = cnt;
+#pragma unroll
+	for (uint32_t o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o, 64);
+		if (lane >= o) x += y;
+	}
+	if (lane == 63) wsum[w] = x;
+	__syncthreads();
+	uint32_t off = x - cnt;
+	for (uint32_t k = 0; k < w; ++k) off += wsum[k];
+	s_off[threadIdx.x] = off;
+	if (threadIdx.x == 255) s_off[256] = off + cnt;
+	__syncthreads();
+	const uint32_t total = s_off[256];
+	for (uint32_t r = threadIdx.x; r < total; r += 256) {
+		uint32_t lo = 0, hi = 256;  // owner: last t with s_off[t] <= r
+		while (hi - lo > 1) {
+			const uint32_t mid = (lo + hi) >> 1;
+			if (s_off[mid] <= r) lo = mid;
+			else hi = mid;
+		}
+		op(lo, r - s_off[lo]);
+	}
+	__syncthreads();
+}
+
+// One chunk step: composite the previous chunk's outputs (transmittance only) and scatter
+// them to the sampler layout, then claim evaluation rows for the next chunk of every ray
+// still marching and gather its network inputs.  The last step only scatters.
+__global__ void __launch_bounds__(256) k_train_chunk(ChunkArgs a) {
+	__shared__ uint32_t s_off[257], s_src[256], s_dst[256];
+	__shared__ uint32_t s_base;
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const bool valid = i < a.n_rays;
+	uint32_t n = 0, base = 0;
+	if (valid) {
+		n = a.numsteps[2 * i];
+		base = a.numsteps[2 * i + 1];
+	}
+	float T = 1.0f;
+	bool alive = valid && n > 0;
+	uint32_t ev = 0, scatter = 0;
+	if (!a.first) {
+		const uint32_t e = valid ? a.ray_eval[i] : RAY_EVAL_DONE;
+		alive = alive && !(e & RAY_EVAL_DONE) && e == a.prev_lo;
+	}
+	const bool entered = a.first ? valid : alive;  // this step owns the ray's state
+	if (!a.first) {
+		if (alive) {
+			T = a.ray_T[i];
+			const uint32_t ebase = a.ray_ebase[i];
+			const uint32_t end = min(n, a.lo);
+			uint32_t j = a.prev_lo;
+			if (!a.last) {
+				for (; j < end; ++j) {
+					if (T < TRAIN_CHUNK_STOP_T) break;  // the loss kernel stops at or before sample j
+					const uint2 ob = *reinterpret_cast<const uint2*>(a.eout + 4 * (size_t)(ebase + j - a.prev_lo));
+					const float raw = __half2float(reinterpret_cast<const __half*>(&ob)[3]);
+					const float dt = unwarp_dt(a.epos[ebase + j - a.prev_lo].w);
+					T *= __expf(-network_to_density(raw, a.density_act) * dt);  // 1 - alpha
+				}
+			} else {
+				j = end;
+			}
+			scatter = j - a.prev_lo;
+			ev = j;
+			// stopped inside the chunk, at its end with T already below the margin, or out of samples
+			if (j < end || T < TRAIN_CHUNK_STOP_T || end == n) alive = false;
+			s_src[threadIdx.x] = base + a.prev_lo;
+			s_dst[threadIdx.x] = ebase;
+		}
+	}
+	if (!a.first) {
+		// previous chunk's outputs back to the sampler layout (rows [prev_lo, prev_lo + scatter))
+		block_rows(scatter, s_off, [&](uint32_t t, uint32_t k) {
+			const uint32_t src = s_src[t] + k, e = s_dst[t] + k;
+			*reinterpret_cast<uint2*>(a.mlp_out + 4 * (size_t)src) = *reinterpret_cast<const uint2*>(a.eout + 4 * (size_t)e);
+			a.eidx[src] = e;
+		});
+	}
+	uint32_t claim = 0;
+	if (alive && a.hi > a.lo) claim = min(n, a.hi) - a.lo;
+	if (entered) {
+		if (claim) {
+			a.ray_T[i] = T;
+			a.ray_eval[i] = a.lo;
+		} else {
+			a.ray_eval[i] = ev | RAY_EVAL_DONE;
+		}
+	}
+	if (a.hi <= a.lo) return;  // last step: nothing to gather (block-uniform)
+	// claim rows for the next chunk: one atomic per block
+	__syncthreads();
+	{
+		__shared__ uint32_t wtot[4];
+		const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+		uint32_t x = claim;
+#pragma unroll
+		for (uint32_t o = 1; o < 64; o <<= 1) {
+			const uint32_t y = __shfl_up(x, o, 64);
+			if (lane >= o) x += y;
+		}
+		if (lane == 63) wtot[w] = x;
+		__syncthreads();
+		if (threadIdx.x == 0) {
+			const uint32_t t = wtot[0] + wtot[1] + wtot[2] + wtot[3];
+			s_base = t ? atomicAdd(a.rows, t) : 0u;
+		}
+		__syncthreads();
+		uint32_t off = s_base + x - claim;
+		for (uint32_t k = 0; k < w; ++k) off += wtot[k];
+		if (claim) a.ray_ebase[i] = a.eval_offset + off;
+		s_src[threadIdx.x] = base + a.lo;
+		s_dst[threadIdx.x] = a.eval_offset + off;
+	}
+	block_rows(claim, s_off, [&](uint32_t t, uint32_t k) {
+		const uint32_t src = s_src[t] + k, e = s_dst[t] + k;
+		a.epos[e] = a.pos4[src];
+		a.edir[e] = reinterpret_cast<const float4*>(a.coords + 8 * (size_t)src)[1];
+	});
+}
+
+// ---------------------------------------------------------------------------
 // Loss: composite (pass 1), prefix sum, emit compacted samples + dL/dout (pass 2).
 // ---------------------------------------------------------------------------
 struct LossArgs {
@@ -351,6 +516,7 @@ struct LossArgs {
 	uint32_t* csrc;        // [B] compacted -> source sample
 	__half* dloss;         // [B][4]
 	const float* mean_density;
+	const uint32_t* ray_eval;  // [R] samples the chunked forward evaluated (null: all of them)
 };
 
 // Wave scans over the 64 lanes (inclusive).
@@ -405,11 +571,13 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	float T = 1.0f;
 	v3 rgb_ray = mk3(0.0f);
 	uint32_t c = numsteps;
+	// the chunked forward evaluated at least every sample before this ray's stop
+	const uint32_t evaluated = a.ray_eval ? (a.ray_eval[i] & ~RAY_EVAL_DONE) : numsteps;
 	for (uint32_t kb = 0; kb < numsteps; kb += 64) {
 		const uint32_t j = kb + lane;
 		const bool active = j < numsteps;
 		LossSample q;
-		if (active) q = loss_sample(a, (size_t)base + j);
+		if (active && j < evaluated) q = loss_sample(a, (size_t)base + j);
 		else { q.alpha = 0.0f; q.rgb = mk3(0.0f); }
 		const float incl = wave_scan_mul(1.0f - q.alpha, lane);
 		float excl = __shfl_up(incl, 1, 64);
@@ -596,10 +764,12 @@ template <uint32_t F>
 __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ csrc,
                                                           const float* __restrict__ coords, const __half* __restrict__ enc,
                                                           uint32_t enc_plane, uint32_t n_levels, float* __restrict__ ccoords,
-                                                          float4* __restrict__ cpos4, __half* __restrict__ cenc, uint32_t target) {
+                                                          float4* __restrict__ cpos4, __half* __restrict__ cenc, uint32_t target,
+                                                          const uint32_t* __restrict__ eidx) {
 	const uint32_t dst = blockIdx.x * 256u + threadIdx.x;
 	if (dst >= *n_ptr) return;
 	const uint32_t src = csrc[dst];
+	const uint32_t esrc = eidx ? eidx[src] : src;  // row of the sample's encoding
 	const float4* ci = reinterpret_cast<const float4*>(coords + 8 * (size_t)src);
 	float4* co = reinterpret_cast<float4*>(ccoords + 8 * (size_t)dst);
 	const float4 c0 = ci[0];
@@ -610,7 +780,7 @@ __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __rest
 	                                     typename std::conditional<F == 4, uint2, uint4>::type>::type>::type;
 	const VT* es = reinterpret_cast<const VT*>(enc);
 	VT* ed = reinterpret_cast<VT*>(cenc);
-	for (uint32_t l = 0; l < n_levels; ++l) ed[(size_t)l * target + dst] = es[(size_t)l * enc_plane + src];
+	for (uint32_t l = 0; l < n_levels; ++l) ed[(size_t)l * target + dst] = es[(size_t)l * enc_plane + esrc];
 }
 
 // Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
@@ -849,15 +1019,79 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 
-	// network inference over every emitted sample (NerfNetwork::inference_mixed_precision, training params)
-	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
-	launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, m->params16.ptr + m->n_mlp_params, ts.enc.ptr, MS, s,
-	                    ts.counters.ptr + 4, 0);
-	tm.end(NGP_TIMER_TRAIN_ENCODE, s);
-	tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
-	launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
-	                 ts.counters.ptr + 4);
-	tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
+	// network inference with the training params (NerfNetwork::inference_mixed_precision): over
+	// every emitted sample as the reference does (NGP_TRAIN_CHUNKED=0), or chunk by chunk up to
+	// each ray's stop (k_train_chunk) -- the loss kernels read the same outputs either way
+	const char* chunk_env = getenv("NGP_TRAIN_CHUNKED");  // read per step (tests switch it)
+	const bool chunk_off = chunk_env && !strcmp(chunk_env, "0");
+	const __half* table = m->params16.ptr + m->n_mlp_params;
+	const __half* enc_rows = ts.enc.ptr;
+	uint32_t enc_plane = MS;
+	const uint32_t* eidx = nullptr;
+	ts.chunked = !chunk_off;
+	if (chunk_off) {
+		tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
+		launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, table, ts.enc.ptr, MS, s, ts.counters.ptr + 4, 0);
+		tm.end(NGP_TIMER_TRAIN_ENCODE, s);
+		tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
+		launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
+		                 ts.counters.ptr + 4);
+		tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
+	} else {
+		// evaluation rows: chunk p of every ray lands in [off[p], off[p] + cap[p])
+		const uint32_t cap[TRAIN_CHUNKS] = {std::min(16 * R, MS), std::min(32 * R, MS), MS};
+		const uint32_t off[TRAIN_CHUNKS] = {0, cap[0], cap[0] + cap[1]};
+		const uint32_t MSE = off[2] + cap[2];
+		ts.epos.reserve(4 * (size_t)MSE);
+		ts.edir.reserve(4 * (size_t)MSE);
+		ts.eenc.reserve((size_t)L * MSE * F);
+		ts.eout.reserve(4 * (size_t)MSE);
+		ts.eidx.reserve(MS);
+		ts.ray_T.reserve(R);
+		ts.ray_eval.reserve(R);
+		ts.ray_ebase.reserve(R);
+		ChunkArgs c{};
+		c.n_rays = R;
+		c.numsteps = ts.ray_numsteps.ptr;
+		c.coords = ts.coords.ptr;
+		c.pos4 = reinterpret_cast<const float4*>(ts.pos4.ptr);
+		c.epos = reinterpret_cast<float4*>(ts.epos.ptr);
+		c.edir = reinterpret_cast<float4*>(ts.edir.ptr);
+		c.eout = ts.eout.ptr;
+		c.mlp_out = ts.mlp_out.ptr;
+		c.eidx = ts.eidx.ptr;
+		c.ray_T = ts.ray_T.ptr;
+		c.ray_eval = ts.ray_eval.ptr;
+		c.ray_ebase = ts.ray_ebase.ptr;
+		c.density_act = m->cfg.density_activation;
+		for (uint32_t p = 0; p <= TRAIN_CHUNKS; ++p) {
+			c.first = p == 0;
+			c.last = p == TRAIN_CHUNKS;
+			c.prev_lo = p >= 2 ? TRAIN_CHUNK_END[p - 2] : 0u;
+			c.lo = p == 0 ? 0u : TRAIN_CHUNK_END[p - 1];
+			c.hi = p < TRAIN_CHUNKS ? TRAIN_CHUNK_END[p] : c.lo;
+			c.rows = ts.counters.ptr + 12 + std::min(p, TRAIN_CHUNKS - 1);
+			c.eval_offset = p < TRAIN_CHUNKS ? off[p] : 0u;
+			k_train_chunk<<<div_up(R, 256), 256, 0, s>>>(c);
+			NGP_HIP_CHECK(hipGetLastError());
+			if (p == TRAIN_CHUNKS) break;
+			// launch about as many encoder chunks as the last step's rows needed; blocks loop
+			// over the rest if there are more
+			const uint32_t lr = ts.last_rows[p];
+			const uint32_t max_chunks = lr ? div_up((uint64_t)lr + lr / 4, 256) + 16 : 0u;
+			tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
+			launch_hashgrid_fwd(m->lt, ts.epos.ptr + 4 * (size_t)off[p], 4, cap[p], table, ts.eenc.ptr + (size_t)off[p] * F,
+			                    MSE, s, c.rows, 0, max_chunks);
+			tm.end(NGP_TIMER_TRAIN_ENCODE, s);
+			tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
+			launch_mlp_infer(m, m->frag_train.ptr, ts.eenc.ptr + (size_t)off[p] * F, MSE, ts.edir.ptr + 4 * (size_t)off[p], 4,
+			                 cap[p], ts.eout.ptr + 4 * (size_t)off[p], s, c.rows, 0);
+			tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
+		}
+		enc_rows = ts.eenc.ptr;
+		enc_plane = MSE;
+		eidx = ts.eidx.ptr;
+	}
 
 	LossArgs la{};
 	la.images = t->images;
@@ -902,6 +1136,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.csrc = ts.csrc.ptr;
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
+	la.ray_eval = ts.chunked ? ts.ray_eval.ptr : nullptr;
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
 	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
 	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);
@@ -941,10 +1176,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// compacted batch size c = min(total, B); rollover multiplicity
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
 	switch (F) {
-		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
-		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
-		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
-		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, ts.enc.ptr, MS, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B); break;
+		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
 	}
 	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));

@@ -94,7 +94,7 @@ class RenderArgs(C.Structure):
 # enums (include/ngp_hip.h)
 PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M, ADAM_V, GRADS_GRID_FP16 = range(8)
 SCRATCH_RAY_NUMSTEPS, SCRATCH_COORDS, SCRATCH_MLP_OUT, SCRATCH_RAY_COMPACTED, SCRATCH_DLOSS, SCRATCH_LOSS, \
-    SCRATCH_COMPACT_COORDS = range(7)
+    SCRATCH_COMPACT_COORDS, SCRATCH_RAY_EVALUATED = range(8)
 
 TIMERS = ["train_sampler", "train_encode", "train_mlp_infer", "train_loss", "train_mlp_bwd", "train_encode_bwd",
           "optimizer", "grid_update", "render_encode", "render_mlp", "render_march"]

@@ -37,6 +37,8 @@ def pair(cfg_kw, seed=0, grid_scale=0.5):
 def gpu_scratch(g, kind, dtype, count=None):
     p, n = C.c_void_p(), C.c_size_t()
     A.check(g.lib.ngp_train_scratch(g.h, kind, C.byref(p), C.byref(n)))
+    if n.value == 0 and count is None:
+        return np.zeros(0, dtype)
     out = np.zeros(n.value // np.dtype(dtype).itemsize if count is None else count, dtype)
     cuda_memcpy_d2h(out, p.value)
     return out
@@ -94,12 +96,21 @@ def test_train_step_matches_oracle(cfg_kw):
         o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
         np.testing.assert_array_equal(g_c, o_c)
 
-        g_out = gpu_scratch(g, A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][owned].astype(np.float32)
-        o_out = o.scratch(A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][owned].astype(np.float32)
-        assert np.abs(g_out - o_out).mean() < 2e-3
-
+        # the chunked forward evaluates each ray up to its stop (at least every sample the
+        # loss composites); the oracle evaluates every sample, as the reference does
+        ev = gpu_scratch(g, A.SCRATCH_RAY_EVALUATED, np.uint32) & 0x7FFFFFFF
         g_cp = gpu_scratch(g, A.SCRATCH_RAY_COMPACTED, np.uint32).reshape(-1, 2)
         o_cp = o.scratch(A.SCRATCH_RAY_COMPACTED, np.uint32).reshape(-1, 2)
+        evaluated = np.zeros(MS, bool)
+        for r, (n, b) in enumerate(o_ns):
+            evaluated[b:b + (min(n, ev[r]) if ev.size else n)] = True
+        if ev.size:
+            assert np.all(ev[:R] >= o_cp[:, 0]) and np.all(ev[:R] <= o_ns[:, 0])
+        assert evaluated.sum() > 500
+        g_out = gpu_scratch(g, A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][evaluated].astype(np.float32)
+        o_out = o.scratch(A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][evaluated].astype(np.float32)
+        assert np.abs(g_out - o_out).mean() < 2e-3
+
         assert (g_cp[:, 0] == o_cp[:, 0]).mean() > 0.98
         same = np.all(g_cp == o_cp) and gst.measured_batch_size == ost.measured_batch_size
         np.testing.assert_allclose(gst.loss, ost.loss, rtol=2e-2)
@@ -112,6 +123,46 @@ def test_train_step_matches_oracle(cfg_kw):
             for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
                 rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
                 assert rel < 5e-2, rel
+    finally:
+        g.close()
+
+
+def test_chunked_forward_matches_full_forward(monkeypatch):
+    """The early-terminated (chunked) forward leaves the loss, the compaction and dL/dout
+    bit-identical to evaluating every sample (the reference's inference over the whole
+    pre-compaction batch); gradients agree up to float-atomic ordering."""
+    g, o, rng = pair(CFG_B, grid_scale=2.0)  # dense enough that most rays stop early
+    try:
+        imgs, cams, focal = make_views(6, 32, 32)
+        dd = DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.35))
+        R, B, MS = 2048, 1 << 14, 1 << 17
+        out = {}
+        for mode in ("0", "1"):
+            monkeypatch.setenv("NGP_TRAIN_CHUNKED", mode)
+            g.zero_grads()
+            A.check(g.lib.ngp_train_step(g.h, C.byref(train_args(dd.ptr, dd.n, R, B, MS)), stream()))
+            torch.cuda.synchronize()
+            st = A.TrainStats()
+            A.check(g.lib.ngp_train_read_stats(g.h, C.byref(st), stream()))
+            out[mode] = dict(
+                stats=(st.measured_batch_size, st.measured_batch_size_before_compaction, st.loss),
+                cp=gpu_scratch(g, A.SCRATCH_RAY_COMPACTED, np.uint32).copy(),
+                loss=gpu_scratch(g, A.SCRATCH_LOSS, np.float32).copy(),
+                dl=gpu_scratch(g, A.SCRATCH_DLOSS, np.float16)[: 4 * min(st.measured_batch_size, B)].copy(),
+                grads=g.grads().copy(),
+                ev=gpu_scratch(g, A.SCRATCH_RAY_EVALUATED, np.uint32).copy())
+        full, ch = out["0"], out["1"]
+        assert full["ev"].size == 0 and ch["ev"].size == R
+        n_eval = int((ch["ev"] & 0x7FFFFFFF).sum())
+        assert n_eval < full["stats"][1]  # fewer samples evaluated than emitted
+        assert full["stats"] == ch["stats"]
+        np.testing.assert_array_equal(full["cp"], ch["cp"])
+        np.testing.assert_array_equal(full["loss"], ch["loss"])
+        np.testing.assert_array_equal(full["dl"], ch["dl"])
+        for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
+            rel = np.linalg.norm(full["grads"][sl] - ch["grads"][sl]) / np.linalg.norm(full["grads"][sl])
+            assert rel < 1e-2, rel
     finally:
         g.close()
 
