@@ -10,6 +10,7 @@
 // Every ray's result depends only on its own sample sequence (the compaction
 // only regroups rays), so the image is deterministic per pixel and matches the
 // oracle's straight per-ray march whatever order the waves claim slots in.
+#include <chrono>
 #include <cstring>
 
 #include "ngp_internal.h"
@@ -258,32 +259,45 @@ __global__ void __launch_bounds__(256) k_df_x(const uint8_t* __restrict__ bitfie
 	}
 }
 
-// Passes y and z: one thread per cell and sign combination; h = min_k max(k, f(c + s k)),
-// stopping once k reaches the best value so far (the loop is as long as the answer).
+// Passes y and z: h = min_k max(k, f(c + s k)) for both signs s, stopping once k reaches
+// the best value so far (the loop is as long as the answer).  One workgroup per (mip, input
+// field, other coordinate, half of the x range): the 128 x 64 slab of lines is staged in
+// LDS, so the long loops over empty space read LDS instead of strided global bytes.
 template <uint32_t AXIS>
 __global__ void __launch_bounds__(256) k_df_yz(const uint8_t* __restrict__ fin, uint8_t* __restrict__ fout, uint32_t max_mip) {
-	constexpr uint32_t NV_IN = AXIS == 1 ? 2u : 4u;  // sign combinations of the input / output
-	const uint32_t g = blockIdx.x * 256u + threadIdx.x;
-	const uint32_t cell = g & (DF_BYTES_PER_FIELD - 1u), v = (g >> 21) & (2u * NV_IN - 1u);
-	const uint32_t mip = g >> (AXIS == 1 ? 23 : 24);
-	if (mip > max_mip) return;
-	const uint32_t x = cell & 127u, y = (cell >> 7) & 127u, z = cell >> 14;
-	const uint8_t* f = fin + (size_t)(mip * NV_IN + (v & (NV_IN - 1u))) * DF_BYTES_PER_FIELD;
-	const bool neg = (v >> (AXIS == 1 ? 1 : 2)) & 1u;
-	const int c0 = AXIS == 1 ? (int)y : (int)z;
-	const uint32_t stride = AXIS == 1 ? NERF_GRIDSIZE : NERF_GRIDSIZE * NERF_GRIDSIZE;
-	uint32_t h = f[cell];
-	for (uint32_t k = 1; k < h; ++k) {
-		const int c = neg ? c0 - (int)k : c0 + (int)k;
-		if (c < 0 || c >= (int)NERF_GRIDSIZE) {
-			if (mip < max_mip) h = k;
-			break;
+	constexpr uint32_t NV_IN = AXIS == 1 ? 2u : 4u;  // sign combinations of the input (output: 2x)
+	__shared__ uint8_t slab[NERF_GRIDSIZE][64];       // [coordinate along AXIS][x - x0]
+	uint32_t b = blockIdx.x;
+	const uint32_t x0 = (b & 1u) * 64u;
+	b >>= 1;
+	const uint32_t other = b & (NERF_GRIDSIZE - 1u);  // z (AXIS 1) or y (AXIS 2)
+	b >>= 7;
+	const uint32_t vin = b % NV_IN, mip = b / NV_IN;
+	if (mip > max_mip) return;  // block-uniform
+	const uint8_t* f = fin + (size_t)(mip * NV_IN + vin) * DF_BYTES_PER_FIELD;
+	auto cell_of = [&](uint32_t c, uint32_t x) {
+		return AXIS == 1 ? (other * NERF_GRIDSIZE + c) * NERF_GRIDSIZE + x : (c * NERF_GRIDSIZE + other) * NERF_GRIDSIZE + x;
+	};
+	for (uint32_t t = threadIdx.x; t < NERF_GRIDSIZE * 64u; t += 256u) slab[t >> 6][t & 63u] = f[cell_of(t >> 6, x0 + (t & 63u))];
+	__syncthreads();
+	for (uint32_t t = threadIdx.x; t < NERF_GRIDSIZE * 64u; t += 256u) {
+		const uint32_t c0 = t >> 6, xl = t & 63u;
+		const uint32_t h0 = slab[c0][xl];
+#pragma unroll
+		for (uint32_t neg = 0; neg < 2; ++neg) {
+			uint32_t h = h0;
+			for (uint32_t k = 1; k < h; ++k) {
+				const int c = neg ? (int)c0 - (int)k : (int)c0 + (int)k;
+				if (c < 0 || c >= (int)NERF_GRIDSIZE) {
+					if (mip < max_mip) h = k;  // beyond the grid: the next mip (occupied)
+					break;
+				}
+				h = min(h, max(k, (uint32_t)slab[c][xl]));
+			}
+			const uint32_t v = vin + (neg ? NV_IN : 0u);  // output field: input signs + this axis' sign
+			fout[(size_t)(mip * 2u * NV_IN + v) * DF_BYTES_PER_FIELD + cell_of(c0, x0 + xl)] = (uint8_t)h;
 		}
-		const uint32_t fk = f[(uint32_t)((int)cell + (c - c0) * (int)stride)];
-		h = min(h, max(k, fk));
 	}
-	fout[(size_t)(mip * 2u * NV_IN + v) * DF_BYTES_PER_FIELD + cell] = (uint8_t)h;
-	(void)x;
 }
 
 static void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s) {
@@ -294,8 +308,8 @@ static void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s)
 	rs.df_x.reserve(nm * 2 * DF_BYTES_PER_FIELD);
 	rs.df_xy.reserve(nm * 4 * DF_BYTES_PER_FIELD);
 	k_df_x<<<div_up(nm * 2 * NERF_GRIDSIZE * NERF_GRIDSIZE, 256), 256, 0, s>>>(m->gs.bitfield.ptr, rs.df_x.ptr, max_mip);
-	k_df_yz<1><<<div_up(nm * 4 * DF_BYTES_PER_FIELD, 256), 256, 0, s>>>(rs.df_x.ptr, rs.df_xy.ptr, max_mip);
-	k_df_yz<2><<<div_up(nm * 8 * DF_BYTES_PER_FIELD, 256), 256, 0, s>>>(rs.df_xy.ptr, rs.df.ptr, max_mip);
+	k_df_yz<1><<<(uint32_t)nm * 2u * NERF_GRIDSIZE * 2u, 256, 0, s>>>(rs.df_x.ptr, rs.df_xy.ptr, max_mip);
+	k_df_yz<2><<<(uint32_t)nm * 4u * NERF_GRIDSIZE * 2u, 256, 0, s>>>(rs.df_xy.ptr, rs.df.ptr, max_mip);
 	NGP_HIP_CHECK(hipGetLastError());
 	rs.df_version = m->gs.version;
 	rs.df_max_mip = max_mip;
@@ -763,13 +777,16 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		volatile unsigned long long* w = pub + 8 * (pass % 2);
 		const uint32_t want = base_tag + pass + 1;
 		uint32_t* out = hc + 16 * (pass % 2);
+		// no stream queries while spinning (each one enqueues a marker that drains the queue);
+		// only after seconds without the tag is the stream asked whether it failed
+		const auto t0 = std::chrono::steady_clock::now();
 		for (uint32_t q = 0, spin = 1; q < 8; ++spin) {
 			const unsigned long long v = w[q];
 			if ((uint32_t)(v >> 32) == want) {
 				out[q++] = (uint32_t)v;
 				continue;
 			}
-			if ((spin & 4095u) == 0) {
+			if ((spin & 65535u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
 				const hipError_t e = hipStreamQuery(s);
 				if (e != hipSuccess && e != hipErrorNotReady) NGP_HIP_CHECK(e);
 				if (e == hipSuccess && (uint32_t)(w[q] >> 32) != want)
