@@ -16,6 +16,8 @@
 //  * output is level-major [L][n][F] (fp16): a wave of 64 consecutive samples of
 //    one level writes 64*F*2 contiguous bytes.
 //  * features accumulate in fp32 (tcnn accumulates in fp16) and are rounded once.
+#include <cstring>
+
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -101,11 +103,17 @@ __device__ __forceinline__ uint32_t corner_index(uint32_t size, uint32_t res, ui
 	return idx - size < size ? idx - size : idx % size;
 }
 
-// The 8 corner entries of a cell, all loads issued before any is consumed.  x-pairs share
-// one aligned pair load when both corners fall in it (dense index even, or hashed with x
-// even: index ^ 1); only the other lanes issue the second corner's own load, which cuts
-// the L2 requests of a level by about a quarter.
-template <uint32_t F, bool HASHED>
+// The 8 corner entries of a cell, all loads issued before any is consumed.  The x / x+1
+// corners share one aligned load when both fall in it: a 16-B quad of entries (F = 2;
+// the x+1 corner is in it unless x (hashed) or the index (dense) is 3 mod 4), else a pair
+// (dense index even, or hashed with x even: index ^ 1); only the other lanes issue the
+// second corner's own load.  The encoder is bound by the texture addresser (TA busy ~87 %
+// of a render launch): fewer lanes in the lone-corner loads is what makes it faster.
+__device__ __forceinline__ uint32_t quad_pick(const uint4& v, uint32_t k) {
+	return k == 0 ? v.x : (k == 1 ? v.y : (k == 2 ? v.z : v.w));
+}
+
+template <uint32_t F, bool HASHED, bool QUAD = false>
 __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __restrict__ tab, uint32_t size, uint32_t res,
                                                uint32_t gx, uint32_t gy, uint32_t gz, typename FeatVec<F>::T* vals) {
 	using VT = typename FeatVec<F>::T;
@@ -116,7 +124,23 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 		i0[q] = corner_index<HASHED>(size, res, gx, yy, zz);
 		i1[q] = corner_index<HASHED>(size, res, gx + 1u, yy, zz);
 	}
-	if constexpr (F <= 4) {
+	if constexpr (QUAD && F == 2) {
+		// aligned 16-B quads of entries: the x+1 corner shares the x corner's quad unless x
+		// (hashed) or the index (dense) is 3 mod 4 -- a quarter of the lanes load it alone
+		const uint4* qtab = reinterpret_cast<const uint4*>(tab);
+		uint4 qd[4];
+		uint32_t lone[4];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) qd[q] = qtab[i0[q] >> 2];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q)
+			if ((i1[q] >> 2) != (i0[q] >> 2)) lone[q] = tab[i1[q]];
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) {
+			vals[2 * q] = quad_pick(qd[q], i0[q] & 3u);
+			vals[2 * q + 1] = (i1[q] >> 2) != (i0[q] >> 2) ? lone[q] : quad_pick(qd[q], i1[q] & 3u);
+		}
+	} else if constexpr (F <= 4) {
 		using PT = typename PairVec<F>::T;
 		const PT* ptab = reinterpret_cast<const PT*>(tab);
 		PT pr[4];
@@ -142,13 +166,13 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 	}
 }
 
-template <uint32_t F>
+template <uint32_t F, bool QUAD>
 __device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const float* __restrict__ pos, uint32_t stride,
                                            const __half* __restrict__ table, const LevelTable& lt,
                                            __half* __restrict__ enc, uint32_t enc_plane);
 
 // SITE only names the call site in profiles (0 training, 1 render, 2 density grid / API).
-template <uint32_t F, int SITE>
+template <uint32_t F, int SITE, bool QUAD>
 __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ table, const LevelTable lt,
                                                       __half* __restrict__ enc, uint32_t enc_plane, uint32_t n_chunks,
@@ -159,11 +183,11 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 	// n_chunks per level are launched; they stride over the chunks the count covers
 	for (uint32_t chunk = chunk0; chunk * 256u < n; chunk += n_chunks) {
 		const uint32_t i = chunk * 256u + threadIdx.x;
-		if (i < n) encode_one<F>(i, level, pos, stride, table, lt, enc, enc_plane);
+		if (i < n) encode_one<F, QUAD>(i, level, pos, stride, table, lt, enc, enc_plane);
 	}
 }
 
-template <uint32_t F>
+template <uint32_t F, bool QUAD>
 __device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const float* __restrict__ pos, uint32_t stride,
                                            const __half* __restrict__ table, const LevelTable& lt,
                                            __half* __restrict__ enc, uint32_t enc_plane) {
@@ -179,8 +203,8 @@ __device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const flo
 	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
 
 	VT vals[8];
-	if (hashed) gather_corners<F, true>(tab, size, res, gx, gy, gz, vals);
-	else gather_corners<F, false>(tab, size, res, gx, gy, gz, vals);
+	if (hashed) gather_corners<F, true, QUAD>(tab, size, res, gx, gy, gz, vals);
+	else gather_corners<F, false, QUAD>(tab, size, res, gx, gy, gz, vals);
 	float acc[F];
 #pragma unroll
 	for (uint32_t f = 0; f < F; ++f) acc[f] = 0.0f;
@@ -337,11 +361,17 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 	uint32_t n_chunks = div_up(n, 256);
 	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
 	const uint32_t blocks = n_chunks * lt.n_levels;
+	// 16-B quad gathers for F = 2 (NGP_ENC_GATHER=pair: 8-B pair gathers)
+	static const bool quad = !(getenv("NGP_ENC_GATHER") && !strcmp(getenv("NGP_ENC_GATHER"), "pair"));
+	if (quad && lt.F == 2) {
+		launch_timed(k_hashgrid_fwd<2, SITE, true>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev);
+		return;
+	}
 	switch (lt.F) {
-		case 1: launch_timed(k_hashgrid_fwd<1, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 2: launch_timed(k_hashgrid_fwd<2, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 4: launch_timed(k_hashgrid_fwd<4, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 8: launch_timed(k_hashgrid_fwd<8, SITE>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 1: launch_timed(k_hashgrid_fwd<1, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 2: launch_timed(k_hashgrid_fwd<2, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 4: launch_timed(k_hashgrid_fwd<4, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 8: launch_timed(k_hashgrid_fwd<8, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
 		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
 	}
 }
