@@ -80,10 +80,12 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 // output index of this thread (valid only where flag is set).  Order within a block is
 // deterministic; order between blocks is not (results never depend on it: every ray
 // carries its own pixel index).
+// Any block size up to 1024 threads: the atomics on one counter address serialise across
+// the chip (~10 ns each), so the big render launches use large blocks to issue few of them.
 __device__ __forceinline__ void block_append2(bool fa, bool fb, uint32_t* counter_a, uint32_t* counter_b, uint32_t* ia,
                                               uint32_t* ib) {
-	__shared__ uint32_t wa[4], wb[4], base[2];
-	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	__shared__ uint32_t wa[16], wb[16], base[2];
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
 	const unsigned long long ma = __ballot(fa), mb = __ballot(fb);
 	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 	if (lane == 0) {
@@ -92,7 +94,11 @@ __device__ __forceinline__ void block_append2(bool fa, bool fb, uint32_t* counte
 	}
 	__syncthreads();
 	if (threadIdx.x == 0) {
-		const uint32_t ta = wa[0] + wa[1] + wa[2] + wa[3], tb = wb[0] + wb[1] + wb[2] + wb[3];
+		uint32_t ta = 0, tb = 0;
+		for (uint32_t k = 0; k < nw; ++k) {
+			ta += wa[k];
+			tb += wb[k];
+		}
 		base[0] = ta ? atomicAdd(counter_a, ta) : 0u;
 		base[1] = tb ? atomicAdd(counter_b, tb) : 0u;
 	}
@@ -109,8 +115,8 @@ __device__ __forceinline__ void block_append2(bool fa, bool fb, uint32_t* counte
 // Reserves cnt consecutive slots of *counter for every thread of a 256-thread block: wave
 // scans, LDS totals, ONE atomic per block.  Returns this thread's first slot.
 __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t* counter) {
-	__shared__ uint32_t wsum[4], bbase;
-	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	__shared__ uint32_t wsum[16], bbase;
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
 	uint32_t x = cnt;
 #pragma unroll
 	for (uint32_t o = 1; o < 64; o <<= 1) {
@@ -120,7 +126,8 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t* counte
 	if (lane == 63) wsum[w] = x;
 	__syncthreads();
 	if (threadIdx.x == 0) {
-		const uint32_t t = wsum[0] + wsum[1] + wsum[2] + wsum[3];
+		uint32_t t = 0;
+		for (uint32_t k = 0; k < nw; ++k) t += wsum[k];
 		bbase = t ? atomicAdd(counter, t) : 0u;
 	}
 	__syncthreads();
@@ -136,7 +143,7 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
 	// rays are numbered in 8x8 pixel tiles: a wave's 64 rays are a square patch, so at a
 	// given step their samples are close in space (hash-grid gathers share cache lines)
-	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t tile = r >> 6, x = (tile % k.tiles_x) * 8u + (r & 7u), yl = (tile / k.tiles_x) * 8u + ((r >> 3) & 7u);
 	Payload p;
 	bool alive = false;
@@ -259,45 +266,32 @@ __global__ void __launch_bounds__(256) k_df_x(const uint8_t* __restrict__ bitfie
 	}
 }
 
-// Passes y and z: h = min_k max(k, f(c + s k)) for both signs s, stopping once k reaches
-// the best value so far (the loop is as long as the answer).  One workgroup per (mip, input
-// field, other coordinate, half of the x range): the 128 x 64 slab of lines is staged in
-// LDS, so the long loops over empty space read LDS instead of strided global bytes.
+// Passes y and z: one thread per cell and sign combination; h = min_k max(k, f(c + s k)),
+// stopping once k reaches the best value so far (the loop is as long as the answer).
 template <uint32_t AXIS>
 __global__ void __launch_bounds__(256) k_df_yz(const uint8_t* __restrict__ fin, uint8_t* __restrict__ fout, uint32_t max_mip) {
-	constexpr uint32_t NV_IN = AXIS == 1 ? 2u : 4u;  // sign combinations of the input (output: 2x)
-	__shared__ uint8_t slab[NERF_GRIDSIZE][64];       // [coordinate along AXIS][x - x0]
-	uint32_t b = blockIdx.x;
-	const uint32_t x0 = (b & 1u) * 64u;
-	b >>= 1;
-	const uint32_t other = b & (NERF_GRIDSIZE - 1u);  // z (AXIS 1) or y (AXIS 2)
-	b >>= 7;
-	const uint32_t vin = b % NV_IN, mip = b / NV_IN;
-	if (mip > max_mip) return;  // block-uniform
-	const uint8_t* f = fin + (size_t)(mip * NV_IN + vin) * DF_BYTES_PER_FIELD;
-	auto cell_of = [&](uint32_t c, uint32_t x) {
-		return AXIS == 1 ? (other * NERF_GRIDSIZE + c) * NERF_GRIDSIZE + x : (c * NERF_GRIDSIZE + other) * NERF_GRIDSIZE + x;
-	};
-	for (uint32_t t = threadIdx.x; t < NERF_GRIDSIZE * 64u; t += 256u) slab[t >> 6][t & 63u] = f[cell_of(t >> 6, x0 + (t & 63u))];
-	__syncthreads();
-	for (uint32_t t = threadIdx.x; t < NERF_GRIDSIZE * 64u; t += 256u) {
-		const uint32_t c0 = t >> 6, xl = t & 63u;
-		const uint32_t h0 = slab[c0][xl];
-#pragma unroll
-		for (uint32_t neg = 0; neg < 2; ++neg) {
-			uint32_t h = h0;
-			for (uint32_t k = 1; k < h; ++k) {
-				const int c = neg ? (int)c0 - (int)k : (int)c0 + (int)k;
-				if (c < 0 || c >= (int)NERF_GRIDSIZE) {
-					if (mip < max_mip) h = k;  // beyond the grid: the next mip (occupied)
-					break;
-				}
-				h = min(h, max(k, (uint32_t)slab[c][xl]));
-			}
-			const uint32_t v = vin + (neg ? NV_IN : 0u);  // output field: input signs + this axis' sign
-			fout[(size_t)(mip * 2u * NV_IN + v) * DF_BYTES_PER_FIELD + cell_of(c0, x0 + xl)] = (uint8_t)h;
+	constexpr uint32_t NV_IN = AXIS == 1 ? 2u : 4u;  // sign combinations of the input / output
+	const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t cell = g & (DF_BYTES_PER_FIELD - 1u), v = (g >> 21) & (2u * NV_IN - 1u);
+	const uint32_t mip = g >> (AXIS == 1 ? 23 : 24);
+	if (mip > max_mip) return;
+	const uint32_t x = cell & 127u, y = (cell >> 7) & 127u, z = cell >> 14;
+	const uint8_t* f = fin + (size_t)(mip * NV_IN + (v & (NV_IN - 1u))) * DF_BYTES_PER_FIELD;
+	const bool neg = (v >> (AXIS == 1 ? 1 : 2)) & 1u;
+	const int c0 = AXIS == 1 ? (int)y : (int)z;
+	const uint32_t stride = AXIS == 1 ? NERF_GRIDSIZE : NERF_GRIDSIZE * NERF_GRIDSIZE;
+	uint32_t h = f[cell];
+	for (uint32_t k = 1; k < h; ++k) {
+		const int c = neg ? c0 - (int)k : c0 + (int)k;
+		if (c < 0 || c >= (int)NERF_GRIDSIZE) {
+			if (mip < max_mip) h = k;
+			break;
 		}
+		const uint32_t fk = f[(uint32_t)((int)cell + (c - c0) * (int)stride)];
+		h = min(h, max(k, fk));
 	}
+	fout[(size_t)(mip * 2u * NV_IN + v) * DF_BYTES_PER_FIELD + cell] = (uint8_t)h;
+	(void)x;
 }
 
 static void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s) {
@@ -308,8 +302,8 @@ static void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s)
 	rs.df_x.reserve(nm * 2 * DF_BYTES_PER_FIELD);
 	rs.df_xy.reserve(nm * 4 * DF_BYTES_PER_FIELD);
 	k_df_x<<<div_up(nm * 2 * NERF_GRIDSIZE * NERF_GRIDSIZE, 256), 256, 0, s>>>(m->gs.bitfield.ptr, rs.df_x.ptr, max_mip);
-	k_df_yz<1><<<(uint32_t)nm * 2u * NERF_GRIDSIZE * 2u, 256, 0, s>>>(rs.df_x.ptr, rs.df_xy.ptr, max_mip);
-	k_df_yz<2><<<(uint32_t)nm * 4u * NERF_GRIDSIZE * 2u, 256, 0, s>>>(rs.df_xy.ptr, rs.df.ptr, max_mip);
+	k_df_yz<1><<<div_up(nm * 4 * DF_BYTES_PER_FIELD, 256), 256, 0, s>>>(rs.df_x.ptr, rs.df_xy.ptr, max_mip);
+	k_df_yz<2><<<div_up(nm * 8 * DF_BYTES_PER_FIELD, 256), 256, 0, s>>>(rs.df_xy.ptr, rs.df.ptr, max_mip);
 	NGP_HIP_CHECK(hipGetLastError());
 	rs.df_version = m->gs.version;
 	rs.df_max_mip = max_mip;
@@ -369,7 +363,7 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 // early passes (one lane per ray, flat loop), up to 64 for the last few thousand rays,
 // whose long serial marches otherwise dominate the tail passes.
 template <uint32_t G>
-__global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
+__global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
                                                   float4* __restrict__ posdt, float4* __restrict__ dirs,
                                                   uint32_t target, uint32_t max_steps,
@@ -392,7 +386,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __r
 	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
 	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
-	const uint32_t i = (blockIdx.x * 256u + threadIdx.x) / G;
+	const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
 	const bool valid = i < n_alive;  // group-uniform
 	Payload* p = payloads + (valid ? i : 0);
 	uint32_t budget = 0;
@@ -478,7 +472,7 @@ __global__ void __launch_bounds__(256) k_generate(RenderK k, const uint32_t* __r
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
-__global__ void __launch_bounds__(256) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
+__global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                    const float* __restrict__ sdepth, const float4* __restrict__ posdt,
                                                    const __half* __restrict__ out,
@@ -489,7 +483,7 @@ __global__ void __launch_bounds__(256) k_composite(RenderK k, const uint32_t* __
                                                    uint32_t* __restrict__ next_sample_counter) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
 	const uint32_t n_alive = *alive_in;
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
 	Payload p;
 	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
 	float local_depth = 0.0f;
@@ -736,8 +730,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
 	                                                                rs.counters.ptr);
 	const size_t lds = k.df ? 0 : (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
-	(k.lens_mode != LENS_PERSPECTIVE ? k_render_init<true> : k_render_init<false>)<<<div_up(n_tiled, 256u), 256, lds, s>>>(k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
-	                                             rs.counters.ptr);
+	(k.lens_mode != LENS_PERSPECTIVE ? k_render_init<true> : k_render_init<false>)<<<div_up(n_tiled, 256u), 256, lds, s>>>(
+	    k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, rs.counters.ptr);
 	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
 	NGP_HIP_CHECK(hipGetLastError());
 
@@ -815,20 +809,37 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// lanes per ray: enough rays in flight for ~1M lanes, never fewer than one lane per ray
 		const uint32_t want = lanes_target() / std::max(n_alive_ub, 1u);
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
-		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 256));
+		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 512));
 		unsigned long long* host_prev = pass > 0 ? pub_dev + 8 * ((pass - 1) % 2) : nullptr;
 		const uint32_t tag_prev = base_tag + pass;  // = tag of pass - 1
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, 256, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 1: k_generate<1><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
 		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap, std::max(target, n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin_kernel(NGP_TIMER_RENDER_ENCODE);
+		static const char* dump = getenv("NGP_RENDER_DUMP");  // diagnostic: pass-0 samples + alive payloads
+		if (dump && pass == 0) {
+			uint32_t c[8];
+			NGP_HIP_CHECK(hipMemcpyAsync(c, rs.counters.ptr, sizeof(c), hipMemcpyDeviceToHost, s));
+			NGP_HIP_CHECK(hipStreamSynchronize(s));
+			std::vector<float> pd((size_t)c[4] * 4);
+			std::vector<Payload> pl(c[0]);
+			NGP_HIP_CHECK(hipMemcpy(pd.data(), posdt, pd.size() * 4, hipMemcpyDeviceToHost));
+			NGP_HIP_CHECK(hipMemcpy(pl.data(), P(cur), pl.size() * sizeof(Payload), hipMemcpyDeviceToHost));
+			FILE* f = fopen(dump, "wb");
+			if (f) {
+				fwrite(c, 4, 8, f);
+				fwrite(pd.data(), 4, pd.size(), f);
+				fwrite(pl.data(), sizeof(Payload), pl.size(), f);
+				fclose(f);
+			}
+		}
 		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s);  // units: the pass's sample count, added at its read-back
 		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
@@ -836,7 +847,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		                 samples, 0);
 		tm.end(NGP_TIMER_RENDER_MLP, s);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_composite<<<std::max(1u, div_up(n_alive_ub, 256)), 256, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
+		k_composite<<<std::max(1u, div_up(n_alive_ub, 1024)), 1024, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
 		                                                                  posdt, rs.out.ptr, P(1 - cur), C(1 - cur),
 		                                                                  rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr,
 		                                                                  alive_out, rs.counters.ptr + 2, samples_next);
