@@ -94,11 +94,11 @@ def make_dataset(ngp, tb, n_views, res, device):
     return cams, imgs, focal
 
 
-# timer -> kernel whose PMC counters describe it
-TIMER_KERNEL = {"train_encode": ("k_hashgrid_fwd<", ", 0>"), "render_encode": ("k_hashgrid_fwd<", ", 1>"),
-                "train_encode_bwd": ("k_hashgrid_bwd<", ""), "train_mlp_infer": ("k_mlp_infer_rf<", ", false, 2>"),
-                "render_mlp": ("k_mlp_infer_rf<", ", false, 2>"), "train_mlp_bwd": ("k_mlp_train<", ""),
-                "optimizer": ("k_optimizer", "")}
+# timer -> kernel (name pattern) whose PMC counters describe it
+TIMER_KERNEL = {"train_encode": r"k_hashgrid_fwd<\d+u, 0(, (true|false))?>", "render_encode": r"k_hashgrid_fwd<\d+u, 1(, (true|false))?>",
+                "train_encode_bwd": r"k_hashgrid_bwd<", "train_mlp_infer": r"k_mlp_infer_rf<.*, false, \d>$",
+                "render_mlp": r"k_mlp_infer_rf<.*, false, \d>$", "train_mlp_bwd": r"k_mlp_train<",
+                "optimizer": r"k_optimizer"}
 
 
 def pmc_traffic(path, timer, units_per_launch):
@@ -108,10 +108,11 @@ def pmc_traffic(path, timer, units_per_launch):
     undercount)."""
     if not os.path.exists(path) or timer not in TIMER_KERNEL:
         return None
+    import re
+
     data = json.load(open(path))
-    prefix, suffix = TIMER_KERNEL[timer]
     for name, e in data.items():
-        if prefix not in name or not name.endswith(suffix):
+        if not re.search(TIMER_KERNEL[timer], name):
             continue
         return round(e.get("fetch_bytes_per_launch", 0) + e.get("write_bytes_per_launch", 0))
     return None
