@@ -167,28 +167,43 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 }
 
 template <uint32_t F, bool QUAD>
-__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const float* __restrict__ pos, uint32_t stride,
+__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, float px, float py, float pz,
                                            const __half* __restrict__ table, const LevelTable& lt,
                                            __half* __restrict__ enc, uint32_t enc_plane);
 
-// SITE only names the call site in profiles (0 training, 1 render, 2 density grid / API).
-template <uint32_t F, int SITE, bool QUAD>
+// SITE names the call site in profiles (0 training, 1 render, 2 density grid / API).  A
+// thread encodes LPT levels of one sample (l, l + L/LPT, ...), so the position row is
+// loaded once per LPT levels: the encoder is bound by the texture addresser's per-lane
+// work, which this cuts by a seventh at LPT = 4 -- more than the XCD-private L2 locality
+// of one level per block (kept for LPT <= 2: levels l and l + L/2 share an XCD) is worth.  Render slots that a ray
+// reserved but did not fill carry x = -1 (k_generate): they get zero features, no gathers.
+template <uint32_t F, int SITE, bool QUAD, uint32_t LPT>
 __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ table, const LevelTable lt,
                                                       __half* __restrict__ enc, uint32_t enc_plane, uint32_t n_chunks,
                                                       const uint32_t* __restrict__ n_dev) {
-	uint32_t level, chunk0;
-	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk0);
+	uint32_t level0, chunk0;
+	const uint32_t groups = lt.n_levels / LPT;
+	map_block(blockIdx.x, n_chunks, groups, &level0, &chunk0);
 	if (n_dev) n = min(n, *n_dev);
-	// n_chunks per level are launched; they stride over the chunks the count covers
+	// n_chunks per level group are launched; they stride over the chunks the count covers
 	for (uint32_t chunk = chunk0; chunk * 256u < n; chunk += n_chunks) {
 		const uint32_t i = chunk * 256u + threadIdx.x;
-		if (i < n) encode_one<F, QUAD>(i, level, pos, stride, table, lt, enc, enc_plane);
+		if (i >= n) continue;
+		const float px = pos[(size_t)i * stride + 0], py = pos[(size_t)i * stride + 1], pz = pos[(size_t)i * stride + 2];
+		if (SITE == 1 && px < 0.0f) {
+			using VT = typename FeatVec<F>::T;
+#pragma unroll
+			for (uint32_t q = 0; q < LPT; ++q) reinterpret_cast<VT*>(enc)[(size_t)(level0 + q * groups) * enc_plane + i] = VT{};
+			continue;
+		}
+#pragma unroll
+		for (uint32_t q = 0; q < LPT; ++q) encode_one<F, QUAD>(i, level0 + q * groups, px, py, pz, table, lt, enc, enc_plane);
 	}
 }
 
 template <uint32_t F, bool QUAD>
-__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const float* __restrict__ pos, uint32_t stride,
+__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, float px, float py, float pz,
                                            const __half* __restrict__ table, const LevelTable& lt,
                                            __half* __restrict__ enc, uint32_t enc_plane) {
 	const float scale = lt.scale[level];
@@ -198,9 +213,9 @@ __device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, const flo
 
 	float fx, fy, fz;
 	uint32_t gx, gy, gz;
-	pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
-	pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
-	pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
+	pos_fract(px, scale, &fx, &gx);
+	pos_fract(py, scale, &fy, &gy);
+	pos_fract(pz, scale, &fz, &gz);
 
 	VT vals[8];
 	if (hashed) gather_corners<F, true, QUAD>(tab, size, res, gx, gy, gz, vals);
@@ -360,18 +375,29 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
                             __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, uint32_t max_chunks) {
 	uint32_t n_chunks = div_up(n, 256);
 	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
-	const uint32_t blocks = n_chunks * lt.n_levels;
-	// 16-B quad gathers for F = 2 (NGP_ENC_GATHER=pair: 8-B pair gathers)
+	// 16-B quad gathers for F = 2 (NGP_ENC_GATHER=pair: 8-B pair gathers); four levels per
+	// thread (l, l + L/4, ...; NGP_ENC_LPT=2: two, on one XCD; =1: one level per thread)
 	static const bool quad = !(getenv("NGP_ENC_GATHER") && !strcmp(getenv("NGP_ENC_GATHER"), "pair"));
+	static const int lpt = getenv("NGP_ENC_LPT") ? atoi(getenv("NGP_ENC_LPT")) : 4;
+	const bool lpt1 = lpt == 1;
 	if (quad && lt.F == 2) {
-		launch_timed(k_hashgrid_fwd<2, SITE, true>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev);
+		if (lpt == 4 && lt.n_levels % 4 == 0)
+			launch_timed(k_hashgrid_fwd<2, SITE, true, 4>, n_chunks * lt.n_levels / 4, 256, 0, s, n, pos, stride, table, lt, enc,
+			             enc_plane, n_chunks, n_dev);
+		else if (!lpt1 && lt.n_levels % 16 == 0)
+			launch_timed(k_hashgrid_fwd<2, SITE, true, 2>, n_chunks * lt.n_levels / 2, 256, 0, s, n, pos, stride, table, lt, enc,
+			             enc_plane, n_chunks, n_dev);
+		else
+			launch_timed(k_hashgrid_fwd<2, SITE, true, 1>, n_chunks * lt.n_levels, 256, 0, s, n, pos, stride, table, lt, enc,
+			             enc_plane, n_chunks, n_dev);
 		return;
 	}
+	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
-		case 1: launch_timed(k_hashgrid_fwd<1, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 2: launch_timed(k_hashgrid_fwd<2, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 4: launch_timed(k_hashgrid_fwd<4, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
-		case 8: launch_timed(k_hashgrid_fwd<8, SITE, false>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 1: launch_timed(k_hashgrid_fwd<1, SITE, false, 1>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 2: launch_timed(k_hashgrid_fwd<2, SITE, false, 1>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 4: launch_timed(k_hashgrid_fwd<4, SITE, false, 1>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
+		case 8: launch_timed(k_hashgrid_fwd<8, SITE, false, 1>, blocks, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane, n_chunks, n_dev); break;
 		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
 	}
 }

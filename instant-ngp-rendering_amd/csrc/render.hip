@@ -450,10 +450,10 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 		}
 	}
 	if (valid) {
-		// reserved slots the ray did not fill (it left the volume) still go through the
-		// encoder: give them an in-range position
+		// reserved slots the ray did not fill (it left the volume) still go through the encoder
+		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
 		for (uint32_t q = j + r; q < budget; q += G) {
-			posdt[(size_t)base + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+			posdt[(size_t)base + q] = make_float4(-1.0f, -1.0f, -1.0f, 0.0f);
 			dirs[(size_t)base + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
 		}
 	}
