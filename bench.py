@@ -95,7 +95,7 @@ def make_dataset(ngp, tb, n_views, res, device):
 
 
 # timer -> kernel (name pattern) whose PMC counters describe it
-TIMER_KERNEL = {"train_encode": r"k_hashgrid_fwd<\d+u, 0(, (true|false))?>", "render_encode": r"k_hashgrid_fwd<\d+u, 1(, (true|false))?>",
+TIMER_KERNEL = {"train_encode": r"k_hashgrid_fwd<\d+u, 0[,>]", "render_encode": r"k_hashgrid_fwd<\d+u, 1[,>]",
                 "train_encode_bwd": r"k_hashgrid_bwd<", "train_mlp_infer": r"k_mlp_infer_rf<.*, false, \d>$",
                 "render_mlp": r"k_mlp_infer_rf<.*, false, \d>$", "train_mlp_bwd": r"k_mlp_train<",
                 "optimizer": r"k_optimizer"}
