@@ -152,6 +152,11 @@ typedef struct ngp_train_args {
 	/* per-image exposure (Nerf::Training::cam_exposure, src/testbed_nerf.cu:966-985, 1121-1134) */
 	const float* exposure;      /* device [n_images][3] log2 scale of the target colours; null = 0 */
 	float* exposure_gradient;   /* device [n_images][3] += dL/dexposure of the kept rays; null = off */
+	/* extrinsics (compute_cam_gradient_train_nerf, src/testbed_nerf.cu:1163-1269): device [n_images][3]
+	 * += the kept rays' origin gradient (translation) and cross(dir, dir gradient) (rotation, angle-axis),
+	 * divided by the pixel pdf; null = off */
+	float* cam_pos_gradient;
+	float* cam_rot_gradient;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {

@@ -346,6 +346,77 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 }
 
 
+// dL/d(position) through the grid (tcnn GridEncoding backward with input gradients, used by the
+// camera gradients): dL/dx_d = sum_l scale_l sum_c dw_c/df_d sum_f dL/denc[l][f] table[c][f].
+// One thread per sample, the training-parameter table; divided by the sample's rollover weight
+// (the dL/denc carry it) so it is the gradient of the sample's own row.
+template <uint32_t F>
+__global__ void __launch_bounds__(256) k_hashgrid_input_grad(uint32_t n, const float* __restrict__ pos, uint32_t stride,
+                                                             const __half* __restrict__ denc, uint32_t enc_plane,
+                                                             const __half* __restrict__ table, const LevelTable lt,
+                                                             const float* __restrict__ weight, float* __restrict__ dpos,
+                                                             const uint32_t* __restrict__ n_dev) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (n_dev) n = min(n, *n_dev);
+	if (i >= n) return;
+	using VT = typename FeatVec<F>::T;
+	const float px = pos[(size_t)i * stride + 0], py = pos[(size_t)i * stride + 1], pz = pos[(size_t)i * stride + 2];
+	float dx = 0.0f, dy = 0.0f, dz = 0.0f;
+	for (uint32_t level = 0; level < lt.n_levels; ++level) {
+		float g[F];
+		unpack<F>(reinterpret_cast<const VT*>(denc)[(size_t)level * enc_plane + i], g);
+		bool any = false;
+#pragma unroll
+		for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
+		if (!any) continue;
+		const float scale = lt.scale[level];
+		const uint32_t res = lt.res[level], size = lt.size[level];
+		const VT* tab = reinterpret_cast<const VT*>(table + (size_t)lt.offset[level] * F);
+		float fx, fy, fz;
+		uint32_t gx, gy, gz;
+		pos_fract(px, scale, &fx, &gx);
+		pos_fract(py, scale, &fy, &gy);
+		pos_fract(pz, scale, &fz, &gz);
+		VT vals[8];
+		if (lt.hashed[level]) gather_corners<F, true>(tab, size, res, gx, gy, gz, vals);
+		else gather_corners<F, false>(tab, size, res, gx, gy, gz, vals);
+		float lx = 0.0f, ly = 0.0f, lz = 0.0f;
+#pragma unroll
+		for (uint32_t c = 0; c < 8; ++c) {
+			float v[F];
+			unpack<F>(vals[c], v);
+			float dot = 0.0f;
+#pragma unroll
+			for (uint32_t f = 0; f < F; ++f) dot = fmaf(g[f], v[f], dot);
+			const float wx = (c & 1u) ? fx : 1.0f - fx, wy = (c & 2u) ? fy : 1.0f - fy, wz = (c & 4u) ? fz : 1.0f - fz;
+			lx += dot * ((c & 1u) ? 1.0f : -1.0f) * wy * wz;
+			ly += dot * ((c & 2u) ? 1.0f : -1.0f) * wx * wz;
+			lz += dot * ((c & 4u) ? 1.0f : -1.0f) * wx * wy;
+		}
+		dx = fmaf(scale, lx, dx);
+		dy = fmaf(scale, ly, dy);
+		dz = fmaf(scale, lz, dz);
+	}
+	const float inv = weight ? 1.0f / weight[i] : 1.0f;
+	dpos[3 * (size_t)i + 0] = dx * inv;
+	dpos[3 * (size_t)i + 1] = dy * inv;
+	dpos[3 * (size_t)i + 2] = dz * inv;
+}
+
+void launch_hashgrid_input_grad(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
+                                uint32_t enc_plane, const __half* table, const float* weight, float* dpos, hipStream_t s,
+                                const uint32_t* n_dev) {
+	if (n == 0) return;
+	switch (lt.F) {
+		case 1: k_hashgrid_input_grad<1><<<div_up(n, 256), 256, 0, s>>>(n, pos, stride, denc, enc_plane, table, lt, weight, dpos, n_dev); break;
+		case 2: k_hashgrid_input_grad<2><<<div_up(n, 256), 256, 0, s>>>(n, pos, stride, denc, enc_plane, table, lt, weight, dpos, n_dev); break;
+		case 4: k_hashgrid_input_grad<4><<<div_up(n, 256), 256, 0, s>>>(n, pos, stride, denc, enc_plane, table, lt, weight, dpos, n_dev); break;
+		case 8: k_hashgrid_input_grad<8><<<div_up(n, 256), 256, 0, s>>>(n, pos, stride, denc, enc_plane, table, lt, weight, dpos, n_dev); break;
+		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
+	}
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
 __global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                           const LevelTable lt, uint32_t* __restrict__ idx_out,
                                                           float* __restrict__ w_out) {

@@ -130,6 +130,7 @@ struct MlpArgs {
 	uint64_t param_off[MAX_LAYERS];
 	uint32_t param_in[MAX_LAYERS];
 	const uint32_t* n_dev;  // optional device-side sample count (<= n)
+	float* dsh;             // optional [n][16] dL/d(SH inputs) (camera gradients)
 	uint32_t enc_bytes, coord_bytes;  // buffer-resource extents (register-resident inference)
 	uint32_t dir_offset;              // float offset of the direction in a coords record
 };
@@ -627,7 +628,8 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	constexpr int DNXT = (1 - (N::NL - 1 - l) % 2) * N::drows();
 	constexpr int SIN = N::template seg_in<true>(l);
 	constexpr int MS = N::Ms(l);
-	constexpr int KT = (l == N::DH + 1) ? 1 : N::Kt(l);
+	// the rgb network's input: the 16 density-output rows, then (for the camera gradients) the 16 SH rows
+	constexpr int KT = N::Kt(l);
 	const int g = lane >> 4, n = lane & 15;
 	h8 b[CT][MS];
 #pragma unroll
@@ -637,6 +639,7 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	const _Float16* fr = frags + N::bwd_off(l);
 #pragma unroll
 	for (int mt = 0; mt < KT; ++mt) {
+		if (l == N::DH + 1 && mt == 1 && !a.dsh) break;
 		h8 af[MS];
 #pragma unroll
 		for (int s = 0; s < MS; ++s) af[s] = lds_h8(fr + ((mt * MS + s) * 64 + lane) * 8);
@@ -659,7 +662,13 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 					acc[0] += (float)__half2float(a.dloss[(size_t)i * 4 + 3]) * w;
 				}
 			}
-			if constexpr (l > 0) {
+			if (l == N::DH + 1 && mt == 1) {
+				// dL/d(SH) of the sample's own row: the deltas carry its rollover weight
+				if (i < a.n) {
+					const float inv = a.weight ? 1.0f / a.weight[i] : 1.0f;
+					*reinterpret_cast<float4*>(a.dsh + (size_t)i * 16 + 4 * g) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+				}
+			} else if constexpr (l > 0) {
 				h4 o = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
 				lds_st_h4(dimg + smp * DS + DNXT + 16 * mt + 4 * g, o);
 			} else {
@@ -976,9 +985,10 @@ void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* e
 void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
-                      const uint32_t* n_dev) {
+                      const uint32_t* n_dev, float* dsh) {
 	if (n == 0) return;
 	MlpArgs a = base_args(m);
+	a.dsh = dsh;
 	a.frags = frags;
 	a.enc = enc;
 	a.enc_plane = enc_plane;

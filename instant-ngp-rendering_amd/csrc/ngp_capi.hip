@@ -209,7 +209,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		t.dloss.release(); t.cweight.release(); t.csrc.release(); t.denc.release(); t.loss.release(); t.block_sums.release();
 		t.counters.release(); t.scan_a.release(); t.scan_b.release();
 		t.epos.release(); t.edir.release(); t.eenc.release(); t.eout.release(); t.eidx.release();
-		t.ray_T.release(); t.ray_eval.release(); t.ray_ebase.release();
+		t.ray_T.release(); t.ray_eval.release(); t.ray_ebase.release(); t.dsh.release(); t.dpos.release();
 		GridState& g = m->gs;
 		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();

@@ -195,6 +195,8 @@ struct TrainScratch {
 	DevBuf<uint32_t> eidx;             // [MS] sample -> evaluation row
 	DevBuf<float> ray_T;               // [R]
 	DevBuf<uint32_t> ray_eval, ray_ebase;  // [R]
+	DevBuf<float> dsh;                 // [B][16] dL/d(SH inputs) of the compacted batch (extrinsics)
+	DevBuf<float> dpos;                // [B][3] dL/d(warped position) of the compacted batch (extrinsics)
 	bool chunked = false;              // last step ran the chunked forward
 	uint32_t last_rows[3] = {0, 0, 0}; // evaluation rows of each chunk in the last read-back step
 	uint32_t last_n_rays = 0, last_target = 0, last_max_samples = 0;
@@ -301,10 +303,16 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
                       const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4);
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
+// dsh (optional): [n][16] dL/d(SH inputs of the rgb network), of the sample's own row (divided
+// by its rollover weight), for the camera gradients
 void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
-                      const uint32_t* n_dev = nullptr);
+                      const uint32_t* n_dev = nullptr, float* dsh = nullptr);
+// dL/d(warped position) through the grid of the first *n_dev samples (dpos [n][3]), divided by weight
+void launch_hashgrid_input_grad(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
+                                uint32_t enc_plane, const __half* table, const float* weight, float* dpos, hipStream_t s,
+                                const uint32_t* n_dev);
 // train.hip
 struct SamplerParams;
 void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hipStream_t s);

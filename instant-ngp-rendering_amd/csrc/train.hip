@@ -517,6 +517,7 @@ struct LossArgs {
 	__half* dloss;         // [B][4]
 	const float* mean_density;
 	const uint32_t* ray_eval;  // [R] samples the chunked forward evaluated (null: all of them)
+	int store_uv_pdf;          // camera gradients: ray_aux[i].w = the pixel's pdf
 };
 
 // Wave scans over the 64 lanes (inclusive).
@@ -659,6 +660,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 		a.ray_aux[i] = make_float4(ls_scale * dgt.x * es.x * 0.6931471805599453f, ls_scale * dgt.y * es.y * 0.6931471805599453f,
 		                           ls_scale * dgt.z * es.z * 0.6931471805599453f, 0.0f);
 	}
+	if (a.store_uv_pdf) a.ray_aux[i].w = uv_pdf;
 	a.ray_state[8 * (size_t)i + 6] = u;
 	a.ray_state[8 * (size_t)i + 7] = v;
 	a.ccounts[i] = c;
@@ -756,6 +758,93 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		acc = acc + mk3(__shfl(pre.x, 63, 64), __shfl(pre.y, 63, 64), __shfl(pre.z, 63, 64));
 		T *= __shfl(incl, 63, 64);
 	}
+}
+
+// ---------------------------------------------------------------------------
+// Camera extrinsics gradient: compute_cam_gradient_train_nerf (src/testbed_nerf.cu:1163-1269).
+// Per ray, over its compacted samples: the position gradient (dL/d warped position ÷ the
+// AABB size) adds to the origin gradient and, times the sample's distance from the origin,
+// to the direction gradient, together with dL/d direction through the SH encoding (the
+// warp's 0.5 and the SH input's 2x - 1 cancel).  Image translation += origin gradient,
+// rotation += cross(dir, dir gradient), each divided by the pixel pdf.
+// ---------------------------------------------------------------------------
+// dL/d(x, y, z) of the degree-4 SH basis (sh4_slice, mlp.hip) at (x, y, z) = 2 wd - 1
+__device__ __forceinline__ v3 sh4_input_grad(const float* wd, const float* dsh) {
+	const float x = wd[0] * 2.0f - 1.0f, y = wd[1] * 2.0f - 1.0f, z = wd[2] * 2.0f - 1.0f;
+	const float x2 = x * x, y2 = y * y, z2 = z * z;
+	float gx = 0.0f, gy = 0.0f, gz = 0.0f;
+	gy += dsh[1] * -0.48860251190291987f;
+	gz += dsh[2] * 0.48860251190291987f;
+	gx += dsh[3] * -0.48860251190291987f;
+	gx += dsh[4] * 1.0925484305920792f * y;
+	gy += dsh[4] * 1.0925484305920792f * x;
+	gy += dsh[5] * -1.0925484305920792f * z;
+	gz += dsh[5] * -1.0925484305920792f * y;
+	gz += dsh[6] * 2.0f * 0.94617469575755997f * z;
+	gx += dsh[7] * -1.0925484305920792f * z;
+	gz += dsh[7] * -1.0925484305920792f * x;
+	gx += dsh[8] * 2.0f * 0.54627421529603959f * x;
+	gy += dsh[8] * -2.0f * 0.54627421529603959f * y;
+	gx += dsh[9] * 0.59004358992664352f * (-6.0f * x * y);
+	gy += dsh[9] * 0.59004358992664352f * (-3.0f * x2 + 3.0f * y2);
+	gx += dsh[10] * 2.8906114426405538f * y * z;
+	gy += dsh[10] * 2.8906114426405538f * x * z;
+	gz += dsh[10] * 2.8906114426405538f * x * y;
+	gy += dsh[11] * 0.45704579946446572f * (1.0f - 5.0f * z2);
+	gz += dsh[11] * 0.45704579946446572f * (-10.0f * y * z);
+	gz += dsh[12] * 0.3731763325901154f * (15.0f * z2 - 3.0f);
+	gx += dsh[13] * 0.45704579946446572f * (1.0f - 5.0f * z2);
+	gz += dsh[13] * 0.45704579946446572f * (-10.0f * x * z);
+	gx += dsh[14] * 1.4453057213202769f * 2.0f * x * z;
+	gy += dsh[14] * 1.4453057213202769f * -2.0f * y * z;
+	gz += dsh[14] * 1.4453057213202769f * (x2 - y2);
+	gx += dsh[15] * 0.59004358992664352f * (-3.0f * x2 + 3.0f * y2);
+	gy += dsh[15] * 0.59004358992664352f * (6.0f * x * y);
+	return mk3(gx, gy, gz);
+}
+
+struct CamGradArgs {
+	uint32_t n_rays;
+	aabb3 aabb;
+	const uint32_t* compacted;   // [R][2] (count, base) in the compacted batch
+	const float* ray_state;      // [R][8] o, d
+	const float* loss_state;     // [R][8]: [7] image
+	const float4* ray_aux;       // [R]: w = pixel pdf
+	const float* ccoords;        // [B][8]
+	const float* dpos;           // [B][3]
+	const float* dsh;            // [B][16]
+	float* cam_pos_gradient;     // [n_images][3]
+	float* cam_rot_gradient;     // [n_images][3]
+};
+
+__global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n_rays) return;
+	const uint32_t cn = a.compacted[2 * i], cbase = a.compacted[2 * i + 1];
+	if (cn == 0) return;
+	const float* rs = a.ray_state + 8 * (size_t)i;
+	const v3 o = mk3(rs[0], rs[1], rs[2]), d = mk3(rs[3], rs[4], rs[5]);
+	const v3 inv_diag = mk3(1.0f / (a.aabb.max.x - a.aabb.min.x), 1.0f / (a.aabb.max.y - a.aabb.min.y),
+	                        1.0f / (a.aabb.max.z - a.aabb.min.z));
+	v3 go = mk3(0.0f), gd = mk3(0.0f);
+	for (uint32_t j = 0; j < cn; ++j) {
+		const size_t s = (size_t)cbase + j;
+		const float* c = a.ccoords + 8 * s;
+		const v3 pg = mk3(a.dpos[3 * s], a.dpos[3 * s + 1], a.dpos[3 * s + 2]) * inv_diag;
+		go = go + pg;
+		const v3 pos = unwarp_position(mk3(c[0], c[1], c[2]), a.aabb);
+		const float t = length(pos - o);
+		gd = gd + pg * t + sh4_input_grad(c + 4, a.dsh + 16 * s);
+	}
+	const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
+	const float inv_pdf = 1.0f / a.ray_aux[i].w;
+	const v3 aa = mk3(d.y * gd.z - d.z * gd.y, d.z * gd.x - d.x * gd.z, d.x * gd.y - d.y * gd.x);
+	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 0], go.x * inv_pdf);
+	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 1], go.y * inv_pdf);
+	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 2], go.z * inv_pdf);
+	atomicAdd(&a.cam_rot_gradient[3 * (size_t)img + 0], aa.x * inv_pdf);
+	atomicAdd(&a.cam_rot_gradient[3 * (size_t)img + 1], aa.y * inv_pdf);
+	atomicAdd(&a.cam_rot_gradient[3 * (size_t)img + 2], aa.z * inv_pdf);
 }
 
 // Gather the compacted batch (coords + per-level features) in compacted order: one
@@ -1137,6 +1226,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
 	la.ray_eval = ts.chunked ? ts.ray_eval.ptr : nullptr;
+	const bool cam = t->cam_pos_gradient && t->cam_rot_gradient;
+	la.store_uv_pdf = cam ? 1 : 0;
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
 	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
 	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);
@@ -1187,13 +1278,37 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 
 	// fused MLP forward+backward, then hash-grid scatter (Trainer::training_step)
 	tm.begin_kernel(NGP_TIMER_TRAIN_MLP_BWD);
+	if (cam) {
+		ts.dsh.reserve(16 * (size_t)B);
+		ts.dpos.reserve(3 * (size_t)B);
+	}
 	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, B, ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
-	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5);
+	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
 	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
 	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
+	if (cam) {
+		// input gradients of the compacted samples (Trainer::training_step with dL_dinput), then
+		// compute_cam_gradient_train_nerf per ray
+		launch_hashgrid_input_grad(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, B, m->params16.ptr + m->n_mlp_params,
+		                           ts.cweight.ptr, ts.dpos.ptr, s, ts.counters.ptr + 5);
+		CamGradArgs ca{};
+		ca.n_rays = R;
+		ca.aabb = sa.aabb;
+		ca.compacted = ts.ray_compacted.ptr;
+		ca.ray_state = ts.ray_state.ptr;
+		ca.loss_state = ts.ray_loss_state.ptr;
+		ca.ray_aux = reinterpret_cast<const float4*>(ts.ray_aux.ptr);
+		ca.ccoords = ts.ccoords.ptr;
+		ca.dpos = ts.dpos.ptr;
+		ca.dsh = ts.dsh.ptr;
+		ca.cam_pos_gradient = t->cam_pos_gradient;
+		ca.cam_rot_gradient = t->cam_rot_gradient;
+		k_cam_gradient<<<div_up(R, 256), 256, 0, s>>>(ca);
+		NGP_HIP_CHECK(hipGetLastError());
+	}
 	tm.train_units_pending = tm.mask != 0;
 
 	if (!t->defer_optimizer) launch_optimizer(m, t->training_step, t->optimize_mlp, t->optimize_encoding, s);

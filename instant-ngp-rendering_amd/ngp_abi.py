@@ -58,6 +58,7 @@ class TrainArgs(C.Structure):
         ("error_map", C.c_void_p), ("error_map_res", C.c_uint32 * 2), ("cdf_x_cond_y", C.c_void_p),
         ("cdf_y", C.c_void_p), ("cdf_img", C.c_void_p), ("cdf_res", C.c_uint32 * 2), ("has_lens", C.c_int32),
         ("exposure", C.c_void_p), ("exposure_gradient", C.c_void_p),
+        ("cam_pos_gradient", C.c_void_p), ("cam_rot_gradient", C.c_void_p),
     ]
 
 

@@ -537,6 +537,44 @@ static void hg_backward(Model& M, const float* pos, uint32_t stride, uint32_t n,
 		}
 }
 
+// dL/d(position) through the grid (tcnn GridEncoding input gradient, linear interpolation):
+// dL/dx_d = sum_l scale_l sum_c (c_d ? 1 : -1) prod_{e != d} w_e sum_f dL/denc[l][f] table[c][f]; ÷ weight
+static void hg_input_grad(const Model& M, const uint16_t* params, const float* pos, uint32_t stride, uint32_t n,
+                          const float* denc, const float* weight, float* dpos) {
+	const uint16_t* tab = params + M.n_mlp;
+	for (uint32_t i = 0; i < n; ++i) {
+		float g3[3] = {0.0f, 0.0f, 0.0f};
+		const float* p = pos + (size_t)i * stride;
+		for (uint32_t l = 0; l < M.L; ++l) {
+			bool any = false;
+			for (uint32_t f = 0; f < M.F; ++f) any |= denc[((size_t)l * n + i) * M.F + f] != 0.0f;
+			if (!any) continue;
+			float fr[3];
+			uint32_t gc[3];
+			for (int d = 0; d < 3; ++d) {
+				const float q = std::fma(M.scale[l], p[d], 0.5f);
+				const float fl = std::floor(q);
+				gc[d] = (uint32_t)(int)fl;
+				fr[d] = q - fl;
+			}
+			float lg[3] = {0.0f, 0.0f, 0.0f};
+			for (uint32_t c = 0; c < 8; ++c) {
+				const uint32_t idx = hg_index(M, l, gc[0] + (c & 1), gc[1] + ((c >> 1) & 1), gc[2] + ((c >> 2) & 1));
+				float dotv = 0.0f;
+				for (uint32_t f = 0; f < M.F; ++f)
+					dotv += denc[((size_t)l * n + i) * M.F + f] * h2f(tab[((size_t)M.offset[l] + idx) * M.F + f]);
+				const float w[3] = {(c & 1) ? fr[0] : 1.0f - fr[0], (c & 2) ? fr[1] : 1.0f - fr[1], (c & 4) ? fr[2] : 1.0f - fr[2]};
+				lg[0] += dotv * ((c & 1) ? 1.0f : -1.0f) * w[1] * w[2];
+				lg[1] += dotv * ((c & 2) ? 1.0f : -1.0f) * w[0] * w[2];
+				lg[2] += dotv * ((c & 4) ? 1.0f : -1.0f) * w[0] * w[1];
+			}
+			for (int d = 0; d < 3; ++d) g3[d] += M.scale[l] * lg[d];
+		}
+		const float w = weight ? weight[i] : 1.0f;
+		for (int d = 0; d < 3; ++d) dpos[3 * (size_t)i + d] = g3[d] / w;
+	}
+}
+
 // ---- spherical harmonics degree 4 (tcnn SphericalHarmonicsEncoding) --------------------------
 static void sh4(const float* wdir, float* o) {
 	const float x = wdir[0] * 2.0f - 1.0f, y = wdir[1] * 2.0f - 1.0f, z = wdir[2] * 2.0f - 1.0f;
@@ -558,6 +596,24 @@ static void sh4(const float* wdir, float* o) {
 	o[14] = 1.4453057213202769f * z * (x2 - y2);
 	o[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
 	for (int k = 0; k < 16; ++k) o[k] = rh(o[k]);
+}
+
+// dL/d(x, y, z) of the SH basis above at (x, y, z) = 2 wdir - 1 (the derivative of each formula)
+static V3 sh4_input_grad(const float* wdir, const float* g) {
+	const float x = wdir[0] * 2.0f - 1.0f, y = wdir[1] * 2.0f - 1.0f, z = wdir[2] * 2.0f - 1.0f;
+	const float x2 = x * x, y2 = y * y, z2 = z * z;
+	const float a1 = 0.48860251190291987f, a4 = 1.0925484305920792f, a6 = 0.94617469575755997f, a8 = 0.54627421529603959f,
+	            a9 = 0.59004358992664352f, a10 = 2.8906114426405538f, a11 = 0.45704579946446572f, a12 = 0.3731763325901154f,
+	            a14 = 1.4453057213202769f;
+	const float gx = -a1 * g[3] + a4 * y * g[4] - a4 * z * g[7] + 2.0f * a8 * x * g[8] - 6.0f * a9 * x * y * g[9] +
+	                 a10 * y * z * g[10] + a11 * (1.0f - 5.0f * z2) * g[13] + 2.0f * a14 * x * z * g[14] +
+	                 a9 * (3.0f * y2 - 3.0f * x2) * g[15];
+	const float gy = -a1 * g[1] + a4 * x * g[4] - a4 * z * g[5] - 2.0f * a8 * y * g[8] + a9 * (3.0f * y2 - 3.0f * x2) * g[9] +
+	                 a10 * x * z * g[10] + a11 * (1.0f - 5.0f * z2) * g[11] - 2.0f * a14 * y * z * g[14] + 6.0f * a9 * x * y * g[15];
+	const float gz = a1 * g[2] - a4 * y * g[5] + 2.0f * a6 * z * g[6] - a4 * x * g[7] + a10 * x * y * g[10] -
+	                 10.0f * a11 * y * z * g[11] + a12 * (15.0f * z2 - 3.0f) * g[12] - 10.0f * a11 * x * z * g[13] +
+	                 a14 * (x2 - y2) * g[14];
+	return v(gx, gy, gz);
 }
 
 // ---- MLP (NerfNetwork: density MLP -> [density_out | SH] -> rgb MLP), fp16 I/O, fp32 sums ------
@@ -612,8 +668,10 @@ static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, con
 	}
 }
 // NerfNetwork::backward_impl (nerf_network.h:189-268): rgb MLP bwd -> add_density_gradient -> density MLP bwd
+// dsh (optional, [n][16]): dL/d(SH inputs) of the sample's own row (÷ its rollover weight), for the
+// camera gradients (tcnn's input gradient through the Composite encoding's SH part)
 static void mlp_backward(Model& M, const uint16_t* P, const float* enc, const float* coords, uint32_t cs, uint32_t n,
-                         const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc) {
+                         const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc, float* dsh = nullptr) {
 	const uint32_t NL = (uint32_t)M.layers.size();
 	std::vector<float> col(M.E);
 	Acts A;
@@ -639,6 +697,12 @@ static void mlp_backward(Model& M, const uint16_t* P, const float* enc, const fl
 				if (l == (int)M.n_density_layers && k == 0) acc += h2f(f2h(dl[4 * i + 3])) * w;
 				nd[k] = rh(acc);
 			}
+			if (dsh && l == (int)M.n_density_layers)
+				for (uint32_t k = 16; k < 32; ++k) {
+					float acc = 0.0f;
+					for (uint32_t r = 0; r < Ly.out; ++r) acc += h2f(W[(size_t)r * Ly.in + k]) * delta[r];
+					dsh[16 * (size_t)i + (k - 16)] = acc / w;
+				}
 			if (l == 0) {
 				for (uint32_t k = 0; k < M.E; ++k) denc[((size_t)(k / M.F) * n + i) * M.F + (k % M.F)] = nd[k];
 			}
@@ -945,7 +1009,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1119)
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	std::vector<uint32_t> cc(R, 0);
-	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f);
+	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f), ray_uv_pdf(R, 1.0f);
 	for (uint32_t i = 0; i < R; ++i) {
 		const uint32_t ns = M.ray_numsteps[2 * i], b0 = M.ray_numsteps[2 * i + 1];
 		if (ns == 0) continue;
@@ -970,6 +1034,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		rng.advance((int64_t)gi * 16);
 		float u, vv, pdf, uv_pdf;
 		const uint32_t img = pick_pixel(a, gi, nrg, rng, &u, &vv, &pdf, &uv_pdf);
+		ray_uv_pdf[i] = uv_pdf;
 		const ngp_image& im = a.images[img];
 		rng.advance(1);
 		V3 bg = v(a.background_color[0], a.background_color[1], a.background_color[2]);
@@ -1096,8 +1161,39 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	for (uint32_t l = 0; l < M.L; ++l)
 		for (uint32_t j = 0; j < C; ++j)
 			for (uint32_t f = 0; f < M.F; ++f) ce[((size_t)l * C + j) * M.F + f] = cenc[((size_t)l * B + j) * M.F + f];
-	mlp_backward(M, M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data());
+	const bool cam = a.cam_pos_gradient && a.cam_rot_gradient;
+	std::vector<float> dsh(cam ? 16 * (size_t)C : 0), dpos(cam ? 3 * (size_t)C : 0);
+	mlp_backward(M, M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
+	             cam ? dsh.data() : nullptr);
+	if (cam) hg_input_grad(M, M.p16.data(), M.ccoords.data(), 8, C, denc.data(), wts.data(), dpos.data());
 	hg_backward(M, M.ccoords.data(), 8, C, denc.data());
+	if (cam) {
+		// compute_cam_gradient_train_nerf (src/testbed_nerf.cu:1163-1269), extrinsics part
+		const V3 diag = box.mx - box.mn;
+		for (uint32_t i = 0; i < R; ++i) {
+			const uint32_t cn = M.ray_compacted[2 * i], cb = M.ray_compacted[2 * i + 1];
+			if (cn == 0) continue;
+			const V3 o = ro[i], d = rd[i];
+			V3 go = v(0, 0, 0), gd = v(0, 0, 0);
+			for (uint32_t j = 0; j < cn; ++j) {
+				const size_t s2 = (size_t)cb + j;
+				const float* c = &M.ccoords[8 * s2];
+				const V3 pg = v(dpos[3 * s2] / diag.x, dpos[3 * s2 + 1] / diag.y, dpos[3 * s2 + 2] / diag.z);
+				go = go + pg;
+				const V3 pos = box.mn + v(c[0] * diag.x, c[1] * diag.y, c[2] * diag.z);
+				gd = gd + pg * len(pos - o) + sh4_input_grad(c + 4, &dsh[16 * s2]);
+			}
+			const uint32_t img = (uint32_t)lstate[8 * (size_t)i + 7];
+			const V3 aa = v(d.y * gd.z - d.z * gd.y, d.z * gd.x - d.x * gd.z, d.x * gd.y - d.y * gd.x);
+			const float p = ray_uv_pdf[i];
+			a.cam_pos_gradient[3 * img + 0] += go.x / p;
+			a.cam_pos_gradient[3 * img + 1] += go.y / p;
+			a.cam_pos_gradient[3 * img + 2] += go.z / p;
+			a.cam_rot_gradient[3 * img + 0] += aa.x / p;
+			a.cam_rot_gradient[3 * img + 1] += aa.y / p;
+			a.cam_rot_gradient[3 * img + 2] += aa.z / p;
+		}
+	}
 	if (!a.defer_optimizer) optimizer(M, a.training_step, a.optimize_mlp, a.optimize_encoding);
 }
 

@@ -451,3 +451,35 @@ def test_train_step_exposure_matches_oracle():
         assert np.linalg.norm(gg - grad_h) / np.linalg.norm(grad_h) < 5e-2
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
+def test_train_step_cam_gradient_matches_oracle(cfg_kw):
+    """compute_cam_gradient_train_nerf (src/testbed_nerf.cu:1163-1269): per-image translation and
+    rotation (angle-axis) gradients from the input gradients of the compacted samples -- through
+    the hash grid for the position, through the SH encoding for the direction -- against the
+    oracle's scalar restatement."""
+    g, o, rng = pair(cfg_kw)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 384, 4096, 1 << 15
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        pos_h, rot_h = np.zeros((6, 3), np.float32), np.zeros((6, 3), np.float32)
+        pos_d, rot_d = torch.zeros(6, 3, device="cuda"), torch.zeros(6, 3, device="cuda")
+        ga.cam_pos_gradient, ga.cam_rot_gradient = pos_d.data_ptr(), rot_d.data_ptr()
+        oa.cam_pos_gradient, oa.cam_rot_gradient = pos_h.ctypes.data, rot_h.ctypes.data
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+        np.testing.assert_array_equal(gpu_scratch(g, A.SCRATCH_RAY_COMPACTED, np.uint32),
+                                      o.scratch(A.SCRATCH_RAY_COMPACTED, np.uint32))
+        for gd, oh in ((pos_d, pos_h), (rot_d, rot_h)):
+            gg = gd.cpu().numpy()
+            assert np.abs(oh).sum() > 0
+            assert np.linalg.norm(gg - oh) / np.linalg.norm(oh) < 5e-2, (gg, oh)
+    finally:
+        g.close()
