@@ -239,6 +239,9 @@ PYBIND11_MODULE(pyngp, m) {
 		TV_RW("n_steps_between_error_map_updates", n_steps_between_error_map_updates)
 		TV_RW("n_steps_between_cam_updates", n_steps_between_cam_updates)
 		TV_RW("exposure_l2_reg", exposure_l2_reg)
+		TV_RW("extrinsic_l2_reg", extrinsic_l2_reg)
+		TV_RW("extrinsic_learning_rate", extrinsic_learning_rate)
+		TV_RW("intrinsic_l2_reg", intrinsic_l2_reg)
 #undef TV_RW
 		// additions: the accumulated error map and the image pmf of the last CDF update
 		.def_property_readonly("error_map", [](TrainingView& v) {
@@ -254,13 +257,27 @@ PYBIND11_MODULE(pyngp, m) {
 			for (const auto& o : v.tb->nerf.training.cam_exposure) l.append(py::make_tuple(o.variable[0], o.variable[1], o.variable[2]));
 			return l;
 		})
+		.def_property_readonly("cam_pos_offset", [](TrainingView& v) {
+			py::list l;
+			for (const auto& o : v.tb->nerf.training.cam_pos_offset) l.append(py::make_tuple(o.variable[0], o.variable[1], o.variable[2]));
+			return l;
+		})
+		.def_property_readonly("cam_rot_offset", [](TrainingView& v) {
+			py::list l;
+			for (const auto& o : v.tb->nerf.training.cam_rot_offset) l.append(py::make_tuple(o.variable[0], o.variable[1], o.variable[2]));
+			return l;
+		})
+		.def_property_readonly("cam_focal_length_offset", [](TrainingView& v) {
+			const auto& o = v.tb->nerf.training.cam_focal_length_offset;
+			return py::make_tuple(o.variable[0], o.variable[1]);
+		})
 		.def_property_readonly("error_map_pmf_img", [](TrainingView& v) { return v.tb->nerf.training.error_map.pmf_img_cpu; })
 		.def_property_readonly("error_map_cdf_valid", [](TrainingView& v) { return v.tb->nerf.training.error_map.is_cdf_valid; })
 		.def_property_readonly("dataset", [](TrainingView& v) -> NerfDataset& { return v.tb->nerf.training.dataset; },
 		                       py::return_value_policy::reference_internal)
 		.def_property_readonly("transforms", [](TrainingView& v) {
 			py::list l;
-			for (const auto& x : v.tb->nerf.training.dataset.xforms) l.append(mat43_to_numpy(x));
+			for (size_t i = 0; i < v.tb->nerf.training.dataset.xforms.size(); ++i) l.append(mat43_to_numpy(v.tb->training_transform(i)));
 			return l;
 		})
 		.def("set_camera_intrinsics",

@@ -1,6 +1,7 @@
 // testbed.cpp — host Testbed for the MI355X NeRF path.  Every device operation is a
 // call into libngp_hip.so (include/ngp_hip.h); this file holds only the host-side
 // orchestration the reference keeps in src/testbed.cu / src/testbed_nerf.cu.
+#include <array>
 #include "testbed.h"
 
 #include <hip/hip_runtime_api.h>
@@ -207,7 +208,7 @@ Testbed::~Testbed() {
 	for (float* p : {m_frame, m_depth, m_accum, m_out})
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
-	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad})
+	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
@@ -461,7 +462,7 @@ void Testbed::set_camera_extrinsics(int frame_idx, const float* c2w, bool conver
 Mat43 Testbed::get_camera_extrinsics(int frame_idx) const {
 	const NerfDataset& ds = nerf.training.dataset;
 	if (frame_idx < 0 || (size_t)frame_idx >= ds.n_images) throw std::runtime_error("Invalid frame index");
-	return ds.ngp_matrix_to_nerf(ds.xforms[frame_idx]);
+	return ds.ngp_matrix_to_nerf(training_transform((size_t)frame_idx));  // offsets applied (src/testbed_nerf.cu:2089-2094)
 }
 
 // Nerf::Training::set_camera_intrinsics (src/testbed_nerf.cu:1989-2010)
@@ -493,6 +494,50 @@ void Testbed::free_device_dataset() {
 	m_dev_meta = nullptr;
 }
 
+// rotmat / rotvec (tcnn vec.h): Rodrigues rotation of angle |r| about r / |r|, and its inverse.
+static std::array<float, 9> rotmat(const vec3& r) {  // row-major 3x3
+	const double th = std::sqrt((double)r[0] * r[0] + (double)r[1] * r[1] + (double)r[2] * r[2]);
+	std::array<float, 9> R{1, 0, 0, 0, 1, 0, 0, 0, 1};
+	if (th < 1e-12) return R;
+	const double x = r[0] / th, y = r[1] / th, z = r[2] / th, c = std::cos(th), s = std::sin(th), C = 1.0 - c;
+	R = {(float)(c + x * x * C), (float)(x * y * C - z * s), (float)(x * z * C + y * s),
+	     (float)(y * x * C + z * s), (float)(c + y * y * C), (float)(y * z * C - x * s),
+	     (float)(z * x * C - y * s), (float)(z * y * C + x * s), (float)(c + z * z * C)};
+	return R;
+}
+static vec3 rotvec(const std::array<float, 9>& R) {
+	const double tr = (double)R[0] + R[4] + R[8];
+	const double c = std::min(1.0, std::max(-1.0, (tr - 1.0) * 0.5));
+	const double th = std::acos(c);
+	if (th < 1e-12) return {0.f, 0.f, 0.f};
+	const double k = th / (2.0 * std::sin(th));
+	return {(float)((R[7] - R[5]) * k), (float)((R[2] - R[6]) * k), (float)((R[3] - R[1]) * k)};
+}
+static std::array<float, 9> matmul3(const std::array<float, 9>& A, const std::array<float, 9>& B) {
+	std::array<float, 9> C{};
+	for (int i = 0; i < 3; ++i)
+		for (int j = 0; j < 3; ++j) C[3 * i + j] = A[3 * i] * B[j] + A[3 * i + 1] * B[3 + j] + A[3 * i + 2] * B[6 + j];
+	return C;
+}
+
+// NerfDataset transform with the optimised extrinsic offsets (Nerf::Training::update_transforms,
+// src/testbed_nerf.cu:2112-2140): rotation = rotmat(rot offset) * R, translation += pos offset.
+Mat43 Testbed::training_transform(size_t i) const {
+	const NerfTraining& tr = nerf.training;
+	Mat43 x = tr.dataset.xforms[i];
+	if (i < tr.cam_rot_offset.size()) {
+		const std::array<float, 9> Rm = rotmat(tr.cam_rot_offset[i].variable);
+		Mat43 y = x;
+		for (int c = 0; c < 3; ++c)
+			for (int r = 0; r < 3; ++r)
+				y.m[3 * c + r] = Rm[3 * r] * x.m[3 * c] + Rm[3 * r + 1] * x.m[3 * c + 1] + Rm[3 * r + 2] * x.m[3 * c + 2];
+		x = y;
+	}
+	if (i < tr.cam_pos_offset.size())
+		for (int r = 0; r < 3; ++r) x.m[9 + r] += tr.cam_pos_offset[i].variable[r];
+	return x;
+}
+
 void Testbed::upload_metadata() {
 	const NerfDataset& ds = nerf.training.dataset;
 	std::vector<ngp_image> meta(ds.n_images);
@@ -506,7 +551,7 @@ void Testbed::upload_metadata() {
 			im.focal_length[k] = ds.metadata[i].focal_length[k];
 			im.principal_point[k] = ds.metadata[i].principal_point[k];
 		}
-		std::memcpy(im.xform, ds.xforms[i].m, sizeof(im.xform));
+		std::memcpy(im.xform, training_transform(i).m, sizeof(im.xform));
 		im.lens_mode = (int32_t)ds.metadata[i].lens.mode;
 		std::memcpy(im.lens_params, ds.metadata[i].lens.params, sizeof(im.lens_params));
 	}
@@ -726,8 +771,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (nerf.training.n_images_for_training == 0) return;
 	{
 		const NerfTraining& t = nerf.training;
-		if (t.optimize_extrinsics || t.optimize_distortion || t.optimize_focal_length || t.optimize_extra_dims)
-			throw std::runtime_error("camera pose / focal / distortion / latent optimisation is not implemented by this build");
+		if (t.optimize_distortion || t.optimize_extra_dims)
+			throw std::runtime_error("distortion-map / latent optimisation is not implemented by this build");
 	}
 	upload_dataset();
 	NerfCounters& ctr = nerf.training.counters_rgb;
@@ -770,11 +815,26 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	}
 	if (tr.n_steps_since_cam_update == 0)
 		hk(hipMemsetAsync(m_exp_grad, 0, n_img * 3 * sizeof(float), (hipStream_t)m_stream), "exposure gradient clear");
+	// extrinsic offsets and their gradients (src/testbed_nerf.cu:2158-2167, 2468-2471)
+	if (tr.cam_pos_offset.size() != n_img) tr.cam_pos_offset.assign(n_img, NerfTraining::Adam3{});
+	if (tr.cam_rot_offset.size() != n_img) tr.cam_rot_offset.assign(n_img, NerfTraining::Adam3{});
+	if (tr.optimize_extrinsics) {
+		if (n_img * 6 > m_cam_grad_cap) {
+			if (m_cam_grad) (void)hipFree(m_cam_grad);
+			hk(hipMalloc((void**)&m_cam_grad, n_img * 6 * sizeof(float)), "hipMalloc camera gradients");
+			m_cam_grad_cap = n_img * 6;
+			hk(hipMemsetAsync(m_cam_grad, 0, n_img * 6 * sizeof(float), (hipStream_t)m_stream), "camera gradient clear");
+		}
+		if (tr.n_steps_since_cam_update == 0)
+			hk(hipMemsetAsync(m_cam_grad, 0, n_img * 6 * sizeof(float), (hipStream_t)m_stream), "camera gradient clear");
+	}
 
 	ngp_train_args a{};
 	a.images = (const ngp_image*)m_dev_meta;
 	a.exposure = m_exp;
 	a.exposure_gradient = tr.optimize_exposure ? m_exp_grad : nullptr;
+	a.cam_pos_gradient = tr.optimize_extrinsics ? m_cam_grad : nullptr;
+	a.cam_rot_gradient = tr.optimize_extrinsics ? m_cam_grad + 3 * n_img : nullptr;
 	a.n_images = (uint32_t)nerf.training.n_images_for_training;
 	a.n_rays = ctr.rays_per_batch;
 	a.n_rays_total = ctr.n_rays_total;
@@ -836,7 +896,13 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (++tr.n_steps_since_error_map_update >= tr.n_steps_between_error_map_updates) update_error_map_cdf();
 	// camera parameters every n_steps_between_cam_updates (src/testbed_nerf.cu:2577-2680)
 	++tr.n_steps_since_cam_update;
-	if (tr.optimize_exposure && tr.n_steps_since_cam_update >= tr.n_steps_between_cam_updates) update_cam_exposure();
+	const bool train_camera = tr.optimize_extrinsics || tr.optimize_focal_length || tr.optimize_exposure;
+	if (train_camera && tr.n_steps_since_cam_update >= tr.n_steps_between_cam_updates) {
+		if (tr.optimize_extrinsics) update_cam_extrinsics();
+		if (tr.optimize_focal_length) update_cam_focal_length();
+		if (tr.optimize_exposure) update_cam_exposure();
+		tr.n_steps_since_cam_update = 0;
+	}
 	// m_rng.advance() (src/testbed_nerf.cu:2925)
 	pcg32 r;
 	r.state = m_rng_state;
@@ -962,7 +1028,59 @@ void Testbed::update_cam_exposure() {
 	for (size_t i = n; i < n_img; ++i)
 		for (int k = 0; k < 3; ++k) e[3 * i + k] = tr.cam_exposure[i].variable[k];
 	hk(hipMemcpyAsync(m_exp, e.data(), e.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "exposure h2d");
-	tr.n_steps_since_cam_update = 0;
+}
+
+// Extrinsics branch of the camera update (src/testbed_nerf.cu:2605-2628): per-image Adam on the
+// translation offset and rotation-Adam on the angle-axis offset (lr = max(extrinsic_lr *
+// 0.33^(step / 128), network lr / 1000), L2 on the offsets), then the transforms are rebuilt.
+void Testbed::update_cam_extrinsics() {
+	NerfTraining& tr = nerf.training;
+	const uint32_t n = (uint32_t)tr.n_images_for_training;
+	const size_t n_img = tr.dataset.n_images;
+	if (m_world > 1) allreduce_f32(m_cam_grad, n_img * 6, false);
+	std::vector<float> g(n_img * 6);
+	hk(hipMemcpyAsync(g.data(), m_cam_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "camera gradient d2h");
+	sync();
+	const float per_camera_loss_scale = (float)n / 128.0f / (float)tr.n_steps_between_cam_updates;
+	const float lr_floor = current_learning_rate() / 1000.0f;
+	const float beta1 = 0.9f, beta2 = 0.99f, eps = 1e-8f;
+	for (uint32_t i = 0; i < n; ++i) {
+		for (int kind = 0; kind < 2; ++kind) {
+			NerfTraining::Adam3& o = kind == 0 ? tr.cam_pos_offset[i] : tr.cam_rot_offset[i];
+			const float lr_set = std::max(tr.extrinsic_learning_rate * std::pow(0.33f, (float)(o.iter / 128)), lr_floor);
+			++o.iter;
+			const float lr = lr_set * std::sqrt(1.0f - std::pow(beta2, (float)o.iter)) / (1.0f - std::pow(beta1, (float)o.iter));
+			vec3 step{};
+			for (int k = 0; k < 3; ++k) {
+				const float grad = g[(size_t)kind * 3 * n_img + 3 * i + k] * per_camera_loss_scale + o.variable[k] * tr.extrinsic_l2_reg;
+				o.m[k] = beta1 * o.m[k] + (1.0f - beta1) * grad;
+				o.v[k] = beta2 * o.v[k] + (1.0f - beta2) * grad * grad;
+				step[k] = lr * o.m[k] / (std::sqrt(o.v[k]) + eps);
+			}
+			if (kind == 0) {
+				for (int k = 0; k < 3; ++k) o.variable[k] -= step[k];
+			} else {  // RotationAdamOptimizer::step: variable = rotvec(rotmat(-step) * rotmat(variable))
+				o.variable = rotvec(matmul3(rotmat({-step[0], -step[1], -step[2]}), rotmat(o.variable)));
+			}
+		}
+	}
+	upload_metadata();  // update_transforms
+}
+
+// Focal-length branch (src/testbed_nerf.cu:2639-2648): Adam with lr max(1e-3 * 0.33^(step / 128),
+// network lr / 1000) on the L2-regularised offset; the gradient term is zero (see testbed.h).
+void Testbed::update_cam_focal_length() {
+	NerfTraining::Adam2& o = nerf.training.cam_focal_length_offset;
+	const float lr_set = std::max(1e-3f * std::pow(0.33f, (float)(o.iter / 128)), current_learning_rate() / 1000.0f);
+	++o.iter;
+	const float beta1 = 0.9f, beta2 = 0.99f, eps = 1e-8f;
+	const float lr = lr_set * std::sqrt(1.0f - std::pow(beta2, (float)o.iter)) / (1.0f - std::pow(beta1, (float)o.iter));
+	for (int k = 0; k < 2; ++k) {
+		const float grad = o.variable[k] * nerf.training.intrinsic_l2_reg;
+		o.m[k] = beta1 * o.m[k] + (1.0f - beta1) * grad;
+		o.v[k] = beta2 * o.v[k] + (1.0f - beta2) * grad * grad;
+		o.variable[k] -= lr * o.m[k] / (std::sqrt(o.v[k]) + eps);
+	}
 }
 
 std::vector<float> Testbed::error_map_data() {

@@ -106,6 +106,19 @@ struct NerfTraining {
 	};
 	std::vector<Adam3> cam_exposure;
 	float exposure_l2_reg = 0.0f;
+	// extrinsics (Nerf::Training::cam_pos_offset / cam_rot_offset, nerf.h:65-67, 88-89): per-image
+	// translation offset (AdamOptimizer<vec3>) and angle-axis rotation offset (RotationAdamOptimizer,
+	// adam_optimizer.h:222-247) applied to the dataset transforms (update_transforms)
+	std::vector<Adam3> cam_pos_offset, cam_rot_offset;
+	float extrinsic_l2_reg = 1e-4f, extrinsic_learning_rate = 1e-3f;
+	// focal length (cam_focal_length_offset, intrinsic_l2_reg 1e-4): the reference's gradient kernel
+	// never writes cam_focal_length_gradient (src/testbed_nerf.cu:1163-1269), so the offset only
+	// sees its L2 term -- from 0 it stays 0
+	struct Adam2 {
+		vec2 variable = {0.f, 0.f}, m = {0.f, 0.f}, v = {0.f, 0.f};
+		uint32_t iter = 0;
+	} cam_focal_length_offset;
+	float intrinsic_l2_reg = 1e-4f;
 	uint32_t n_steps_between_cam_updates = 16;
 	uint32_t n_steps_since_cam_update = 0;
 	uint32_t n_steps_between_error_map_updates = 128;
@@ -142,6 +155,8 @@ public:
 	void set_image_rgba8(int frame_idx, const uint8_t* rgba, int width, int height);
 	void set_camera_extrinsics(int frame_idx, const float* c2w_3x4_rowmajor, bool convert_to_ngp = true);
 	Mat43 get_camera_extrinsics(int frame_idx) const;
+	// dataset transform with the extrinsic offsets applied (Nerf::Training::transforms)
+	Mat43 training_transform(size_t i) const;
 	void set_camera_intrinsics(int frame_idx, float fx, float fy = 0.f, float cx = -0.5f, float cy = -0.5f, float k1 = 0.f, float k2 = 0.f,
 	                           float p1 = 0.f, float p2 = 0.f, float k3 = 0.f, float k4 = 0.f, bool is_fisheye = false);
 	std::function<bool(const std::string&, std::vector<uint8_t>&, int&, int&)> image_decoder;  // non-PNG fallback
@@ -238,6 +253,10 @@ private:
 	size_t m_exp_cap = 0;
 	ngp_network_config m_net_cfg{};
 	void update_cam_exposure();
+	void update_cam_extrinsics();
+	void update_cam_focal_length();
+	float* m_cam_grad = nullptr;  // [2][n_images][3]: translation, rotation gradients (device)
+	size_t m_cam_grad_cap = 0;
 	float current_learning_rate() const;
 	float* m_err = nullptr;
 	float* m_cdf_x = nullptr;

@@ -194,6 +194,68 @@ def test_exposure_optimisation(scene):
     assert e.shape == (12, 3) and np.abs(e).max() > 0
     np.testing.assert_allclose(e.mean(axis=0), 0.0, atol=1e-5)
     assert np.isfinite(losses).all() and np.mean(losses[-16:]) < 0.6 * np.mean(losses[:16])
-    tr.optimize_extrinsics = True
+    tr.optimize_extra_dims = True
     with pytest.raises(RuntimeError):
         tb.frame()
+
+
+def _rotvec(R):
+    c = np.clip((np.trace(R) - 1.0) / 2.0, -1.0, 1.0)
+    th = np.arccos(c)
+    if th < 1e-12:
+        return np.zeros(3)
+    return th / (2 * np.sin(th)) * np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
+
+
+def _rotmat(r):
+    th = np.linalg.norm(r)
+    if th < 1e-12:
+        return np.eye(3)
+    k = r / th
+    K = np.array([[0, -k[2], k[1]], [k[2], 0, -k[0]], [-k[1], k[0], 0]])
+    return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
+
+
+def test_extrinsic_optimisation_recovers_perturbed_pose(scene):
+    """optimize_extrinsics: per-image Adam on the translation offset and rotation-Adam on the
+    angle-axis offset every n_steps_between_cam_updates (src/testbed_nerf.cu:2605-2628), applied
+    as rotmat(rot) * R, t + pos (Nerf::Training::update_transforms, :2096-2140). A scene trained
+    on the true poses pulls a translated training camera back toward its true position."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    tr = tb.nerf.training
+    tb.shall_train = True
+    while tb.training_step < 300:
+        tb.frame()
+    k = 4
+    start = [np.asarray(tr.get_camera_extrinsics(i), dtype=np.float64) for i in range(12)]
+    true = start[k]
+    moved = true.copy()
+    moved[:, 3] += np.array([0.06, -0.04, 0.05])
+    tr.set_camera_extrinsics(k, moved.astype(np.float32), True)
+    np.testing.assert_allclose(tr.get_camera_extrinsics(k), moved, atol=1e-5)
+    tr.optimize_extrinsics = True
+    tr.extrinsic_learning_rate = 3e-3
+    losses = []
+    while tb.training_step < 1100:
+        tb.frame()
+        losses.append(tb.loss)
+    assert np.isfinite(losses).all()
+    pos = np.asarray(tr.cam_pos_offset)
+    rot = np.asarray(tr.cam_rot_offset)
+    assert pos.shape == (12, 3) and rot.shape == (12, 3)
+    assert np.isfinite(pos).all() and np.isfinite(rot).all() and np.abs(pos[k]).max() > 0
+    assert tr.cam_focal_length_offset == (0.0, 0.0)
+    # the returned pose is the dataset pose with the offsets applied (ngp space: R' = rotmat(r) R)
+    cur = np.asarray(tr.get_camera_extrinsics(k), dtype=np.float64)
+    R = cur[:, :3]
+    np.testing.assert_allclose(R.T @ R, np.eye(3), atol=1e-4)
+    err_before = np.linalg.norm(moved[:, 3] - true[:, 3])
+    err_after = np.linalg.norm(cur[:, 3] - true[:, 3])
+    print(f"pose error {err_before:.4f} -> {err_after:.4f}; pos offset {pos[k]}, rot offset {rot[k]}")
+    assert err_after < 0.8 * err_before
+    # untouched cameras stay close to their true poses
+    others = [np.linalg.norm(np.asarray(tr.get_camera_extrinsics(i))[:, 3] - start[i][:, 3]) for i in range(12) if i != k]
+    assert max(others) < 0.5 * err_before
