@@ -648,6 +648,11 @@ void Testbed::reset_network(bool clear_density_grid) {
 	nerf.training.n_steps_between_error_map_updates = 128;
 	nerf.training.error_map.is_cdf_valid = false;
 	nerf.training.n_steps_since_cam_update = 0;
+	// reset_camera_extrinsics (src/testbed.cu:3642)
+	nerf.training.cam_pos_offset.assign(nerf.training.dataset.n_images, NerfTraining::Adam3{});
+	nerf.training.cam_rot_offset.assign(nerf.training.dataset.n_images, NerfTraining::Adam3{});
+	nerf.training.cam_focal_length_offset = NerfTraining::Adam2{};
+	if (training_data_available) m_dataset_dirty = true;
 	pcg32 grid_rng(rng.next_uint());
 	m_rng_state = rng.state;
 	m_rng_inc = rng.inc;
@@ -1393,6 +1398,26 @@ void Testbed::save_snapshot(const std::string& path, bool include_optimizer_stat
 	ds["is_hdr"] = Json(nerf.training.dataset.is_hdr);
 	ds["n_images"] = Json((double)nerf.training.dataset.n_images);
 	nj["dataset"] = ds;
+	// per-image extrinsic offsets as the reference's AdamOptimizer to_json objects
+	// (src/testbed.cu:4793-4794, adam_optimizer.h:172-183)
+	auto adam_json = [](const std::vector<NerfTraining::Adam3>& v) {
+		Json a = Json::array();
+		for (const auto& o : v) {
+			Json j = Json::object();
+			j["iter"] = Json((double)o.iter);
+			j["first_moment"] = vec_json(o.m.data(), 3);
+			j["second_moment"] = vec_json(o.v.data(), 3);
+			j["variable"] = vec_json(o.variable.data(), 3);
+			j["learning_rate"] = Json(1e-4);
+			j["epsilon"] = Json(1e-8);
+			j["beta1"] = Json(0.9);
+			j["beta2"] = Json(0.99);
+			a.push_back(std::move(j));
+		}
+		return a;
+	};
+	nj["cam_pos_offset"] = adam_json(nerf.training.cam_pos_offset);
+	nj["cam_rot_offset"] = adam_json(nerf.training.cam_rot_offset);
 	nj["rgb_activation"] = Json((double)(int)nerf.rgb_activation);
 	nj["density_activation"] = Json((double)(int)nerf.density_activation);
 	nj["density_grid_ema_step"] = Json((double)nerf.density_grid_ema_step);
@@ -1508,6 +1533,27 @@ void Testbed::load_snapshot(const std::string& path) {
 	reset_network(false);
 	nerf.training.counters_rgb = saved_counters;
 	nerf.training.counters_rgb.rays_per_batch = saved_counters_rpb;
+	// dataset-specific optimised extrinsics (src/testbed.cu:4940-4951): restored when the
+	// snapshot's dataset has the loaded dataset's image count
+	if (training_data_available && nj.contains("dataset") &&
+	    (size_t)nj["dataset"].value("n_images", -1.0) == nerf.training.dataset.n_images) {
+		auto load_adam = [&](const char* key, std::vector<NerfTraining::Adam3>& v) {
+			if (!nj.contains(key) || nj[key].size() != nerf.training.dataset.n_images) return;
+			v.assign(nerf.training.dataset.n_images, NerfTraining::Adam3{});
+			for (size_t i = 0; i < v.size(); ++i) {
+				const Json& j = nj[key][i];
+				v[i].iter = (uint32_t)j.value("iter", 0.0);
+				for (int k = 0; k < 3; ++k) {
+					v[i].m[k] = (float)j["first_moment"][k].num();
+					v[i].v[k] = (float)j["second_moment"][k].num();
+					v[i].variable[k] = (float)j["variable"][k].num();
+				}
+			}
+		};
+		load_adam("cam_pos_offset", nerf.training.cam_pos_offset);
+		load_adam("cam_rot_offset", nerf.training.cam_rot_offset);
+		m_dataset_dirty = true;  // update_transforms
+	}
 
 	ngp_model_info info{};
 	ck(ngp_model_get_info(m_model, &info));

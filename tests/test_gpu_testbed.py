@@ -216,7 +216,7 @@ def _rotmat(r):
     return np.eye(3) + np.sin(th) * K + (1 - np.cos(th)) * K @ K
 
 
-def test_extrinsic_optimisation_recovers_perturbed_pose(scene):
+def test_extrinsic_optimisation_recovers_perturbed_pose(scene, tmp_path):
     """optimize_extrinsics: per-image Adam on the translation offset and rotation-Adam on the
     angle-axis offset every n_steps_between_cam_updates (src/testbed_nerf.cu:2605-2628), applied
     as rotmat(rot) * R, t + pos (Nerf::Training::update_transforms, :2096-2140). A scene trained
@@ -259,3 +259,12 @@ def test_extrinsic_optimisation_recovers_perturbed_pose(scene):
     # untouched cameras stay close to their true poses
     others = [np.linalg.norm(np.asarray(tr.get_camera_extrinsics(i))[:, 3] - start[i][:, 3]) for i in range(12) if i != k]
     assert max(others) < 0.5 * err_before
+    # the offsets ride in the snapshot (src/testbed.cu:4793-4794, 4944-4950)
+    snap = str(tmp_path / "cam.ingp")
+    tb.save_snapshot(snap, False)
+    _, tb2 = new_testbed()
+    tb2.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb2.nerf.training.set_camera_extrinsics(k, moved.astype(np.float32), True)
+    tb2.load_snapshot(snap)
+    np.testing.assert_allclose(np.asarray(tb2.nerf.training.cam_pos_offset), pos, atol=1e-7)
+    np.testing.assert_allclose(tb2.nerf.training.get_camera_extrinsics(k), cur, atol=1e-6)
