@@ -228,8 +228,8 @@ void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
 	if (cnt) {
-		launch_hashgrid_fwd(m->lt, g.positions.ptr + 4 * (size_t)first, 4, cnt, table, g.enc.ptr, cnt, s);
-		launch_mlp_density(m, frags, g.enc.ptr, cnt, cnt, g.out.ptr, s);
+		launch_hashgrid_fwd(m->lt, g.positions.ptr + 4 * (size_t)first, 4, cnt, table, g.enc.ptr, internal_layout(m, cnt), s);
+		launch_mlp_density(m, frags, g.enc.ptr, internal_layout(m, cnt), cnt, g.out.ptr, s);
 		k_splat<<<div_up(cnt, 256), 256, 0, s>>>(cnt, g.indices.ptr + first, g.out.ptr, g.tmp.ptr,
 		                                        m->cfg.density_activation);
 		NGP_HIP_CHECK(hipGetLastError());

@@ -13,8 +13,9 @@
 //    placed on the XCD group b % 8 == l % 8, and the levels an XCD owns run one
 //    after the other, so each XCD's private 4 MiB L2 holds one level's table (2 MiB
 //    at T=2^19) instead of the whole 24 MiB table.  Placement only changes speed.
-//  * output is level-major [L][n][F] (fp16): a wave of 64 consecutive samples of
-//    one level writes 64*F*2 contiguous bytes.
+//  * output is an EncLayout (ngp_internal.h): level-major [L][n][F] at the C-ABI, planes
+//    of four levels [L/4][n][4][F] inside the pipelines -- a wave of 64 consecutive samples
+//    writes 64 contiguous 16-B planes (F = 2).
 //  * features accumulate in fp32 (tcnn accumulates in fp16) and are rounded once.
 #include <cstring>
 
@@ -167,45 +168,64 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 }
 
 template <uint32_t F, bool QUAD>
-__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, float px, float py, float pz,
-                                           const __half* __restrict__ table, const LevelTable& lt,
-                                           __half* __restrict__ enc, uint32_t enc_plane);
+__device__ __forceinline__ typename FeatVec<F>::T encode_one(uint32_t level, float px, float py, float pz,
+                                                             const __half* __restrict__ table, const LevelTable& lt);
+
+// four levels' feature vectors of one sample: one plane of an EncLayout with lsh = 2
+template <uint32_t F>
+struct alignas(4 * sizeof(typename FeatVec<F>::T)) Plane4 {
+	typename FeatVec<F>::T v[4];
+};
 
 // SITE names the call site in profiles (0 training, 1 render, 2 density grid / API).  A
-// thread encodes LPT levels of one sample (l, l + L/LPT, ...), so the position row is
-// loaded once per LPT levels: the encoder is bound by the texture addresser's per-lane
-// work, which this cuts by a seventh at LPT = 4 -- more than the XCD-private L2 locality
-// of one level per block (kept for LPT <= 2: levels l and l + L/2 share an XCD) is worth.  Render slots that a ray
-// reserved but did not fill carry x = -1 (k_generate): they get zero features, no gathers.
+// thread encodes LPT levels of one sample (l, l + L/LPT, ...), so the position row is loaded
+// once per LPT levels: the encoder is bound by the texture addresser's per-lane work, which
+// this cuts by a seventh at LPT = 4 -- more than the XCD-private L2 locality of one level per
+// block is worth.  Strided levels keep a mix of coarse and fine tables in flight (four
+// consecutive fine levels at once measured ~15 % slower: L2 working set).  With LPT = 4 and
+// the plane layout (EncLayout lsh = 2) the four results are one plane: one 16-B store
+// (F = 2) instead of four 4-B stores.  Render slots that a ray reserved but did not fill
+// carry x = -1 (k_generate): they get zero features, no gathers.
 template <uint32_t F, int SITE, bool QUAD, uint32_t LPT>
 __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
                                                       const __half* __restrict__ table, const LevelTable lt,
-                                                      __half* __restrict__ enc, uint32_t enc_plane, uint32_t n_chunks,
+                                                      __half* __restrict__ enc, EncLayout lay, uint32_t n_chunks,
                                                       const uint32_t* __restrict__ n_dev) {
-	uint32_t level0, chunk0;
+	uint32_t grp, chunk0;
 	const uint32_t groups = lt.n_levels / LPT;
-	map_block(blockIdx.x, n_chunks, groups, &level0, &chunk0);
+	map_block(blockIdx.x, n_chunks, groups, &grp, &chunk0);
 	if (n_dev) n = min(n, *n_dev);
+	using VT = typename FeatVec<F>::T;
 	// n_chunks per level group are launched; they stride over the chunks the count covers
 	for (uint32_t chunk = chunk0; chunk * 256u < n; chunk += n_chunks) {
 		const uint32_t i = chunk * 256u + threadIdx.x;
 		if (i >= n) continue;
 		const float px = pos[(size_t)i * stride + 0], py = pos[(size_t)i * stride + 1], pz = pos[(size_t)i * stride + 2];
+		VT o[LPT];
 		if (SITE == 1 && px < 0.0f) {
-			using VT = typename FeatVec<F>::T;
 #pragma unroll
-			for (uint32_t q = 0; q < LPT; ++q) reinterpret_cast<VT*>(enc)[(size_t)(level0 + q * groups) * enc_plane + i] = VT{};
-			continue;
+			for (uint32_t q = 0; q < LPT; ++q) o[q] = VT{};
+		} else {
+#pragma unroll
+			for (uint32_t q = 0; q < LPT; ++q) o[q] = encode_one<F, QUAD>(grp + q * groups, px, py, pz, table, lt);
+		}
+		if constexpr (LPT == 4) {
+			if (lay.lsh == 2) {
+				Plane4<F> pv;
+#pragma unroll
+				for (uint32_t q = 0; q < 4; ++q) pv.v[q] = o[q];
+				reinterpret_cast<Plane4<F>*>(enc)[(size_t)grp * lay.plane + i] = pv;
+				continue;
+			}
 		}
 #pragma unroll
-		for (uint32_t q = 0; q < LPT; ++q) encode_one<F, QUAD>(i, level0 + q * groups, px, py, pz, table, lt, enc, enc_plane);
+		for (uint32_t q = 0; q < LPT; ++q) reinterpret_cast<VT*>(enc)[lay.vec(grp + q * groups, i)] = o[q];
 	}
 }
 
 template <uint32_t F, bool QUAD>
-__device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, float px, float py, float pz,
-                                           const __half* __restrict__ table, const LevelTable& lt,
-                                           __half* __restrict__ enc, uint32_t enc_plane) {
+__device__ __forceinline__ typename FeatVec<F>::T encode_one(uint32_t level, float px, float py, float pz,
+                                                             const __half* __restrict__ table, const LevelTable& lt) {
 	const float scale = lt.scale[level];
 	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
 	using VT = typename FeatVec<F>::T;
@@ -237,8 +257,14 @@ __device__ __forceinline__ void encode_one(uint32_t i, uint32_t level, float px,
 	VT o;
 	__half* oh = reinterpret_cast<__half*>(&o);
 #pragma unroll
-	for (uint32_t f = 0; f < F; ++f) oh[f] = __float2half_rn(acc[f]);
-	reinterpret_cast<VT*>(enc)[(size_t)level * enc_plane + i] = o;
+	for (uint32_t f = 0; f < F; ++f) {
+		// round to fp32 first, then to fp16, as tcnn and the oracle do: without the barrier the
+		// last fmaf and the conversion fold into v_fma_mixlo_f16 (one rounding), which differs
+		// from the two roundings when the fp32 sum lies on an fp16 tie
+		__asm__("" : "+v"(acc[f]));
+		oh[f] = __float2half_rn(acc[f]);
+	}
+	return o;
 }
 
 // Hash-grid gradients are fp16 and accumulated with packed half2 atomics
@@ -272,7 +298,7 @@ __device__ __forceinline__ void scatter_add(__half* gtab, uint32_t idx, const fl
 constexpr uint32_t BWD_SAMPLES_PER_BLOCK = 128;
 template <uint32_t F>
 __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
-                                                      const __half* __restrict__ denc, uint32_t enc_plane,
+                                                      const __half* __restrict__ denc, EncLayout lay,
                                                       const LevelTable lt, __half* __restrict__ grad,
                                                       uint32_t n_chunks, const uint32_t* __restrict__ n_dev) {
 	uint32_t level, chunk;
@@ -286,7 +312,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 	float g[F];
 	bool active = i < n;
 	if (active) {
-		unpack<F>(reinterpret_cast<const VT*>(denc)[(size_t)level * enc_plane + i], g);
+		unpack<F>(reinterpret_cast<const VT*>(denc)[lay.vec(level, i)], g);
 		bool any = false;
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
@@ -352,7 +378,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 // (the dL/denc carry it) so it is the gradient of the sample's own row.
 template <uint32_t F>
 __global__ void __launch_bounds__(256) k_hashgrid_input_grad(uint32_t n, const float* __restrict__ pos, uint32_t stride,
-                                                             const __half* __restrict__ denc, uint32_t enc_plane,
+                                                             const __half* __restrict__ denc, EncLayout lay,
                                                              const __half* __restrict__ table, const LevelTable lt,
                                                              const float* __restrict__ weight, float* __restrict__ dpos,
                                                              const uint32_t* __restrict__ n_dev) {
@@ -364,7 +390,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_input_grad(uint32_t n, const f
 	float dx = 0.0f, dy = 0.0f, dz = 0.0f;
 	for (uint32_t level = 0; level < lt.n_levels; ++level) {
 		float g[F];
-		unpack<F>(reinterpret_cast<const VT*>(denc)[(size_t)level * enc_plane + i], g);
+		unpack<F>(reinterpret_cast<const VT*>(denc)[lay.vec(level, i)], g);
 		bool any = false;
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
@@ -404,7 +430,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_input_grad(uint32_t n, const f
 }
 
 void launch_hashgrid_input_grad(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                                uint32_t enc_plane, const __half* table, const float* weight, float* dpos, hipStream_t s,
+                                EncLayout enc_plane, const __half* table, const float* weight, float* dpos, hipStream_t s,
                                 const uint32_t* n_dev) {
 	if (n == 0) return;
 	switch (lt.F) {
@@ -443,7 +469,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const floa
 
 template <int SITE>
 static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                            __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, uint32_t max_chunks) {
+                            __half* enc, EncLayout enc_plane, hipStream_t s, const uint32_t* n_dev, uint32_t max_chunks) {
 	uint32_t n_chunks = div_up(n, 256);
 	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
 	// 16-B quad gathers for F = 2 (NGP_ENC_GATHER=pair: 8-B pair gathers); four levels per
@@ -474,7 +500,7 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 }
 
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev, int site,
+                         __half* enc, EncLayout enc_plane, hipStream_t s, const uint32_t* n_dev, int site,
                          uint32_t max_chunks) {
 	if (n == 0) return;
 	if (site == 0) launch_fwd_site<0>(lt, pos, stride, n, table, enc, enc_plane, s, n_dev, max_chunks);
@@ -484,7 +510,7 @@ void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride
 }
 
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                         uint32_t enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev) {
+                         EncLayout enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev) {
 	if (n == 0) return;
 	const uint32_t n_chunks = div_up(n, BWD_SAMPLES_PER_BLOCK);
 	const uint32_t blocks = n_chunks * lt.n_levels;

@@ -23,6 +23,8 @@
 //    atomic per element per workgroup.
 #include <algorithm>
 
+#include <cstring>
+
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -116,6 +118,7 @@ struct MlpArgs {
 	const __half* frags;
 	const __half* enc;
 	uint32_t enc_plane;
+	uint32_t enc_lsh, enc_gsh;  // EncLayout{enc_plane, enc_lsh, enc_gsh} of enc (denc: level-major)
 	const float* coords;
 	uint32_t coord_stride;
 	uint32_t n;
@@ -133,6 +136,7 @@ struct MlpArgs {
 	float* dsh;             // optional [n][16] dL/d(SH inputs) (camera gradients)
 	uint32_t enc_bytes, coord_bytes;  // buffer-resource extents (register-resident inference)
 	uint32_t dir_offset;              // float offset of the direction in a coords record
+	const __half* sh;                 // optional [n][16] precomputed SH inputs (renderer), instead of directions
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -146,7 +150,7 @@ __device__ __forceinline__ h4 tr_read(const _Float16* p) {
 __device__ __forceinline__ _Float16 u16h(uint32_t u) { return __builtin_bit_cast(_Float16, (uint16_t)(u & 0xffffu)); }
 __device__ __forceinline__ uint32_t n_chunks_of(uint32_t n) { return (n + SAMPLES_PER_BLOCK - 1) / SAMPLES_PER_BLOCK; }
 
-// This wave's SPW samples of the level-major encoding [L][plane][F] -> image rows [0, ENC_ROWS).
+// This wave's SPW samples of the encoding (EncLayout) -> image rows [0, ENC_ROWS).
 template <class N, int STRIDE>
 __device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, uint32_t base, int lane) {
 	constexpr int CHUNKS = N::ENC_ROWS / 8;
@@ -156,11 +160,12 @@ __device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, u
 		const uint32_t k0 = chunk * 8;
 		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 		if (i < a.n && k0 < a.E) {
+			const EncLayout lay{a.enc_plane, a.enc_lsh, a.enc_gsh};
 			if (a.F == 2 && k0 + 8 <= a.E) {
 				const uint32_t* e = reinterpret_cast<const uint32_t*>(a.enc);
 #pragma unroll
 				for (int q = 0; q < 4; ++q) {
-					const uint32_t u = e[(size_t)(k0 / 2 + q) * a.enc_plane + i];
+					const uint32_t u = e[lay.vec(k0 / 2 + q, i)];
 					v[2 * q] = u16h(u);
 					v[2 * q + 1] = u16h(u >> 16);
 				}
@@ -168,7 +173,7 @@ __device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, u
 				const uint2* e = reinterpret_cast<const uint2*>(a.enc);
 #pragma unroll
 				for (int q = 0; q < 2; ++q) {
-					const uint2 u = e[(size_t)(k0 / 4 + q) * a.enc_plane + i];
+					const uint2 u = e[lay.vec(k0 / 4 + q, i)];
 					v[4 * q + 0] = u16h(u.x);
 					v[4 * q + 1] = u16h(u.x >> 16);
 					v[4 * q + 2] = u16h(u.y);
@@ -180,7 +185,7 @@ __device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, u
 					const uint32_t k = k0 + j;
 					if (k < a.E) {
 						const uint32_t lvl = k / a.F, f = k % a.F;
-						v[j] = __builtin_bit_cast(_Float16, e[((size_t)lvl * a.enc_plane + i) * a.F + f]);
+						v[j] = __builtin_bit_cast(_Float16, e[lay.vec(lvl, i) * a.F + f]);
 					}
 				}
 			}
@@ -349,7 +354,8 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_density(MlpArgs a) {
 template <class N, int CT_>
 struct RawTile {
 	uint32_t e[CT_][8 * N::KE];  // encoding halves of this lane's K slots, packed in pairs where F >= 2
-	float d[CT_][3];
+	float d[CT_][3];             // warped direction, or
+	uint32_t h[CT_][2];          // SH inputs 4g .. 4g+3 (precomputed rows)
 };
 
 // Buffer resource over a device array (raw buffer, 32-bit byte offsets; reads past
@@ -359,8 +365,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 }
 
 // Loads this lane's share of a tile: encoding features 32s + 8g .. +7 of sample
-// base + 16c + n (level planes of the [L][plane][F] encoding) and its direction.
-template <class N, int CT_, int FF>
+// base + 16c + n and its direction.  FF: 2 / 4 = F of a level-major encoding (one load per
+// level), 12 / 14 = F = 2 / 4 in four-level planes (EncLayout lsh = 2: one 16-B load per
+// K step; the K order is then the planes' and k_pack permutes the first layer to match),
+// 0 = any layout, element by element.  SHIN: the direction inputs are precomputed SH rows
+// (8 B per lane group) instead of a direction the lane expands itself.
+template <class N, int CT_, int FF, bool SHIN>
 __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t enc_rs, __amdgpu_buffer_rsrc_t crd_rs,
                                         uint32_t base, int g, int n, RawTile<N, CT_>& r, bool want_dir) {
 #pragma unroll
@@ -369,7 +379,19 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 #pragma unroll
 		for (int s = 0; s < N::KE; ++s) {
 			const uint32_t k0 = 32 * s + 8 * g;
-			if constexpr (FF == 2) {
+			if constexpr (FF == 12) {
+				// K positions 32s + 8g .. +7 = plane 4s + g (levels 4s + g + qG, q < 4); planes past
+				// the encoding lie past the buffer's extent: the load returns 0
+				const auto v = __builtin_amdgcn_raw_buffer_load_b128(enc_rs, 16 * ((4 * s + g) * a.enc_plane + i), 0, 0);
+#pragma unroll
+				for (int q = 0; q < 4; ++q) r.e[c][4 * s + q] = v[q];
+			} else if constexpr (FF == 14) {
+				// K positions 32s + 8g .. +7 = half g & 1 of plane 2s + g/2
+				const uint32_t o = 32 * ((2 * s + (g >> 1)) * a.enc_plane + i) + 16 * (g & 1);
+				const auto v = __builtin_amdgcn_raw_buffer_load_b128(enc_rs, o, 0, 0);
+#pragma unroll
+				for (int q = 0; q < 4; ++q) r.e[c][4 * s + q] = v[q];
+			} else if constexpr (FF == 2) {
 #pragma unroll
 				for (int q = 0; q < 4; ++q) {
 					// levels past the encoding lie past the buffer's extent: the load returns 0
@@ -386,6 +408,7 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 				}
 			} else {
 				const uint16_t* e = reinterpret_cast<const uint16_t*>(a.enc);
+				const EncLayout lay{a.enc_plane, a.enc_lsh, a.enc_gsh};
 #pragma unroll
 				for (int q = 0; q < 4; ++q) {
 					uint32_t pair = 0;
@@ -394,14 +417,18 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 						const uint32_t k = k0 + 2 * q + h;
 						if (i < a.n && k < a.E) {
 							const uint32_t lvl = k / a.F, f = k % a.F;
-							pair |= (uint32_t)e[((size_t)lvl * a.enc_plane + i) * a.F + f] << (16 * h);
+							pair |= (uint32_t)e[lay.vec(lvl, i) * a.F + f] << (16 * h);
 						}
 					}
 					r.e[c][4 * s + q] = pair;
 				}
 			}
 		}
-		if (want_dir) {
+		if (want_dir && SHIN) {
+			const auto v = __builtin_amdgcn_raw_buffer_load_b64(crd_rs, 32 * i + 8 * g, 0, 0);
+			r.h[c][0] = v[0];
+			r.h[c][1] = v[1];
+		} else if (want_dir) {
 			const uint32_t o = 4 * (i * a.coord_stride + a.dir_offset);
 			r.d[c][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o, 0, 0));
 			r.d[c][1] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o + 4, 0, 0));
@@ -423,25 +450,8 @@ __device__ __forceinline__ h8 c_to_b(const f4& lo, const f4& hi) {
 // The compiler turns the g-select into four short divergent paths, which measured
 // cheaper than computing all 16 components and blending.
 __device__ __forceinline__ void sh4_slice(const float* dw, int g, float (&o)[4]) {
-	const float x = dw[0] * 2.0f - 1.0f, y = dw[1] * 2.0f - 1.0f, z = dw[2] * 2.0f - 1.0f;
-	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
 	float v[16];
-	v[0] = 0.28209479177387814f;
-	v[1] = -0.48860251190291987f * y;
-	v[2] = 0.48860251190291987f * z;
-	v[3] = -0.48860251190291987f * x;
-	v[4] = 1.0925484305920792f * xy;
-	v[5] = -1.0925484305920792f * yz;
-	v[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
-	v[7] = -1.0925484305920792f * xz;
-	v[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
-	v[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
-	v[10] = 2.8906114426405538f * xy * z;
-	v[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
-	v[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
-	v[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
-	v[14] = 1.4453057213202769f * z * (x2 - y2);
-	v[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+	sh_deg4(dw[0], dw[1], dw[2], v);
 #pragma unroll
 	for (int r = 0; r < 4; ++r) o[r] = g == 0 ? v[r] : g == 1 ? v[4 + r] : g == 2 ? v[8 + r] : v[12 + r];
 }
@@ -497,7 +507,7 @@ __device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4
 // ring, statically indexed by unrolling the loop PF times) -- the kernel is bound by
 // memory latency x bytes in flight, not by the MFMAs (20 per 16 samples).  Weight
 // fragments are read from LDS (one copy per workgroup) to leave the VGPRs to the ring.
-template <class N, int CT_, int PF, bool DENSITY_ONLY>
+template <class N, int CT_, int PF, bool DENSITY_ONLY, bool SHIN>
 __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const RawTile<N, CT_>& cur, uint32_t base, int g,
                                         int n) {
 	h8 b[CT_][2];
@@ -522,10 +532,16 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 #pragma unroll
 		for (int cc = 0; cc < CT_; ++cc) {
 			dens[cc] = (_Float16)c[cc][0][0];
-			float sh[4];
-			sh4_slice(cur.d[cc], g, sh);
-			const f4 shv = {sh[0], sh[1], sh[2], sh[3]};
-			b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
+			if constexpr (SHIN) {
+				const h4 lo = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], (_Float16)c[cc][0][3]};
+				const uint2 lu = __builtin_bit_cast(uint2, lo);
+				b[cc][0] = pack_h8(lu.x, lu.y, cur.h[cc][0], cur.h[cc][1]);  // rgb input: [density out 16 | SH 16]
+			} else {
+				float sh[4];
+				sh4_slice(cur.d[cc], g, sh);
+				const f4 shv = {sh[0], sh[1], sh[2], sh[3]};
+				b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
+			}
 		}
 		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
 		rf_layer<N, N::NL - 1, CT_>(w, b, c);
@@ -542,7 +558,7 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 	}
 }
 
-template <class N, int CT_, int PF, bool DENSITY_ONLY, int FF>
+template <class N, int CT_, int PF, bool DENSITY_ONLY, int FF, bool SHIN = false>
 __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	static_assert(N::KE <= 2 && N::Wp <= 64, "register layout assumes <= 2 K-steps per layer");
 	if (a.n_dev) a.n = min(a.n, *a.n_dev);
@@ -562,12 +578,12 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	// wave-uniform tile index (scalar registers: the ring's guards are scalar branches)
 	const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
 	const __amdgpu_buffer_rsrc_t enc_rs = make_rsrc(a.enc, a.enc_bytes);
-	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
+	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(SHIN ? (const void*)a.sh : (const void*)a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
 	RawTile<N, CT_> ring[PF];
 #pragma unroll
 	for (int q = 0; q < PF; ++q) {
 		const uint32_t t = t0 + q * stride;
-		if (t < n_tiles) rf_load<N, CT_, FF>(a, enc_rs, crd_rs, t * TS, g, n, ring[q], !DENSITY_ONLY);
+		if (t < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, t * TS, g, n, ring[q], !DENSITY_ONLY);
 	}
 	for (uint32_t tb = t0; tb < n_tiles; tb += PF * stride) {
 #pragma unroll
@@ -576,8 +592,8 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 			if (t < n_tiles) {
 				RawTile<N, CT_> cur = ring[q];
 				const uint32_t tn = t + PF * stride;
-				if (tn < n_tiles) rf_load<N, CT_, FF>(a, enc_rs, crd_rs, tn * TS, g, n, ring[q], !DENSITY_ONLY);
-				rf_tile<N, CT_, PF, DENSITY_ONLY>(a, wl, cur, t * TS, g, n);
+				if (tn < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, tn * TS, g, n, ring[q], !DENSITY_ONLY);
+				rf_tile<N, CT_, PF, DENSITY_ONLY, SHIN>(a, wl, cur, t * TS, g, n);
 			}
 		}
 	}
@@ -678,7 +694,7 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 						const uint32_t k = 16 * mt + 4 * g + r;
 						if (k < a.E) {
 							const uint32_t lvl = k / a.F, f = k % a.F;
-							a.denc[((size_t)lvl * a.enc_plane + i) * a.F + f] = __float2half_rn(acc[r]);
+							a.denc[((size_t)lvl * a.enc_plane + i) * a.F + f] = __float2half_rn(acc[r]);  // level-major
 						}
 					}
 				}
@@ -795,7 +811,28 @@ struct PackArgs {
 	PackLayer L[MAX_LAYERS];
 	uint32_t n_layers;
 	uint32_t total_frags;
+	uint32_t plane_f, gsh;  // first-layer K order of the register-resident path: planes (F = 2 / 4) or natural (0)
 };
+
+// Input column of K position k of the first layer for k_mlp_infer_rf's plane loads
+// (EncLayout lsh = 2, G = 2^gsh planes; plane p holds levels p + qG): F = 2: k = 32s + 8g + 2q
+// + f reads plane 4s + g slot q; F = 4: k = 32s + 8g + 4r + f reads plane 2s + g/2 slot
+// 2(g & 1) + r.  ~0u: no such plane (the load returns 0; the weight is 0).
+__device__ __forceinline__ uint32_t plane_col(uint32_t k, uint32_t F, uint32_t gsh) {
+	const uint32_t s = k / 32, g = (k % 32) / 8, G = 1u << gsh;
+	uint32_t p, slot, f;
+	if (F == 2) {
+		p = 4 * s + g;
+		slot = (k % 8) / 2;
+		f = k % 2;
+	} else {
+		p = 2 * s + g / 2;
+		slot = 2 * (g & 1) + (k % 8) / 4;
+		f = k % 4;
+	}
+	if (p >= G) return ~0u;
+	return (p + slot * G) * F + f;
+}
 
 __global__ void k_pack(const __half* __restrict__ params, __half* __restrict__ out, PackArgs p) {
 	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -822,7 +859,8 @@ __global__ void k_pack(const __half* __restrict__ params, __half* __restrict__ o
 			const uint32_t idx = frag - r0, mt = idx / L.ks, s = idx % L.ks;
 			const uint32_t row = 16 * mt + m;
 			for (uint32_t j = 0; j < 8; ++j) {
-				const uint32_t col = 32 * s + (l == 0 ? 8 * g + j : (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4)));
+				uint32_t col = 32 * s + (l == 0 ? 8 * g + j : (j < 4 ? 4 * g + j : 16 + 4 * g + (j - 4)));
+				if (l == 0 && p.plane_f) col = plane_col(col, p.plane_f, p.gsh);
 				out[(size_t)t * 8 + j] = (row < L.out && col < L.in) ? W[(size_t)row * L.in + col] : __float2half(0.0f);
 			}
 			return;
@@ -902,6 +940,8 @@ uint32_t mlp_frag_halves(const ngp_model* m) {
 void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s) {
 	PackArgs p{};
 	NGP_DISPATCH(m->mlp_variant, layer_geometry<N>(m, p));
+	p.plane_f = m->enc_lsh == 2 && (m->lt.F == 2 || m->lt.F == 4) ? m->lt.F : 0u;
+	p.gsh = m->enc_gsh;
 	const uint32_t threads = p.total_frags * 64;
 	k_pack<<<div_up(threads, 256), 256, 0, s>>>(params16, frags, p);
 	NGP_HIP_CHECK(hipGetLastError());
@@ -935,54 +975,75 @@ static void set_lds(K kernel, size_t bytes) {
 	NGP_HIP_CHECK(hipFuncSetAttribute((const void*)kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes));
 }
 
-void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev, uint32_t dir_offset) {
+                      const uint32_t* n_dev, uint32_t dir_offset, const __half* sh) {
 	if (n == 0) return;
+	if (enc_layout.lsh != m->enc_lsh) throw std::runtime_error("encoding layout differs from the packed first layer's");
 	MlpArgs a = base_args(m);
 	a.frags = frags;
 	a.enc = enc;
-	a.enc_plane = enc_plane;
+	a.enc_plane = enc_layout.plane;
+	a.enc_lsh = enc_layout.lsh;
+	a.enc_gsh = enc_layout.gsh;
 	a.coords = coords;
 	a.coord_stride = coord_stride;
 	a.n = n;
 	a.out = out;
 	a.n_dev = n_dev;
-	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_plane * 2, 0xffffffffu);
-	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * coord_stride * 4, 0xffffffffu);
+	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_layout.plane * 2, 0xffffffffu);
+	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * (sh ? 8 : coord_stride) * 4, 0xffffffffu);
 	a.dir_offset = dir_offset;
+	a.sh = sh;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);
-		if (a.F == 2) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 2>, grid, BLOCK, lds, s, a);
-		else if (a.F == 4) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 4>, grid, BLOCK, lds, s, a);
+		const bool pl = a.enc_lsh == 2;
+		// tile shape of the renderer's path (NGP_MLP_TILE=CT,PF: tiles per wave step, prefetch depth; A/B)
+		static const int tile = getenv("NGP_MLP_TILE") ? atoi(getenv("NGP_MLP_TILE")) * 10 + atoi(strchr(getenv("NGP_MLP_TILE"), ',') ? strchr(getenv("NGP_MLP_TILE"), ',') + 1 : "2") : 12;
+		if (sh && a.F == 2 && pl && tile == 22) launch_timed(k_mlp_infer_rf<N, 2, 2, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * 5), BLOCK, lds, s, a);
+		else if (sh && a.F == 2 && pl && tile == 21) launch_timed(k_mlp_infer_rf<N, 2, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * 5), BLOCK, lds, s, a);
+		else if (sh && a.F == 2 && pl && tile == 13) launch_timed(k_mlp_infer_rf<N, 1, 3, false, 12, true>, grid, BLOCK, lds, s, a);
+		else if (sh && a.F == 2 && pl && tile == 11) launch_timed(k_mlp_infer_rf<N, 1, 1, false, 12, true>, grid, BLOCK, lds, s, a);
+		else if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);
+		else if (sh) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 0, true>, grid, BLOCK, lds, s, a);
+		else if (a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12>, grid, BLOCK, lds, s, a);
+		else if (a.F == 4 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 14>, grid, BLOCK, lds, s, a);
+		else if (a.F == 2 && !pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 2>, grid, BLOCK, lds, s, a);
+		else if (a.F == 4 && !pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 4>, grid, BLOCK, lds, s, a);
 		else launch_timed(k_mlp_infer_rf<N, 1, 2, false, 0>, grid, BLOCK, lds, s, a);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }
 
-void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane, uint32_t n,
+void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev) {
 	if (n == 0) return;
+	if (enc_layout.lsh != m->enc_lsh) throw std::runtime_error("encoding layout differs from the packed first layer's");
 	MlpArgs a = base_args(m);
 	a.frags = frags;
 	a.enc = enc;
-	a.enc_plane = enc_plane;
+	a.enc_plane = enc_layout.plane;
+	a.enc_lsh = enc_layout.lsh;
+	a.enc_gsh = enc_layout.gsh;
 	a.n = n;
 	a.out = out;
 	a.n_dev = n_dev;
-	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_plane * 2, 0xffffffffu);
+	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_layout.plane * 2, 0xffffffffu);
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags_upto(N::DH + 1) * FRAG_HALVES * 2;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);
-		if (a.F == 2) k_mlp_infer_rf<N, 1, 2, true, 2><<<grid, BLOCK, lds, s>>>(a);
-		else if (a.F == 4) k_mlp_infer_rf<N, 1, 2, true, 4><<<grid, BLOCK, lds, s>>>(a);
+		const bool pl = a.enc_lsh == 2;
+		if (a.F == 2 && pl) k_mlp_infer_rf<N, 1, 2, true, 12><<<grid, BLOCK, lds, s>>>(a);
+		else if (a.F == 4 && pl) k_mlp_infer_rf<N, 1, 2, true, 14><<<grid, BLOCK, lds, s>>>(a);
+		else if (a.F == 2 && !pl) k_mlp_infer_rf<N, 1, 2, true, 2><<<grid, BLOCK, lds, s>>>(a);
+		else if (a.F == 4 && !pl) k_mlp_infer_rf<N, 1, 2, true, 4><<<grid, BLOCK, lds, s>>>(a);
 		else k_mlp_infer_rf<N, 1, 2, true, 0><<<grid, BLOCK, lds, s>>>(a);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }
 
-void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
                       const uint32_t* n_dev, float* dsh) {
@@ -991,7 +1052,9 @@ void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc
 	a.dsh = dsh;
 	a.frags = frags;
 	a.enc = enc;
-	a.enc_plane = enc_plane;
+	a.enc_plane = enc_layout.plane;
+	a.enc_lsh = enc_layout.lsh;
+	a.enc_gsh = enc_layout.gsh;
 	a.coords = coords;
 	a.coord_stride = coord_stride;
 	a.n = n;

@@ -7,6 +7,7 @@
 // CUDA_CHECK_THROW -> std::runtime_error -> Python RuntimeError chain.
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -152,6 +153,13 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 			m->cfg = *cfg;
 			m->enc_width = cfg->n_levels * cfg->n_features_per_level;
 			m->enc_pad = next_multiple(m->enc_width, 16);
+			{  // NGP_ENC_LAYOUT=level keeps the level-major layout internally too (A/B)
+				const char* e = std::getenv("NGP_ENC_LAYOUT");
+				const uint32_t G = cfg->n_levels / 4;
+				const bool pow2 = cfg->n_levels % 4 == 0 && G && (G & (G - 1)) == 0;
+				m->enc_lsh = (pow2 && !(e && std::strcmp(e, "level") == 0)) ? 2u : 0u;
+				m->enc_gsh = m->enc_lsh ? (uint32_t)__builtin_ctz(G) : 0u;
+			}
 			require(m->enc_pad <= 64, "encoding width (n_levels * F) must be <= 64");
 			m->mlp_variant = mlp_variant_for(cfg->n_neurons, cfg->density_hidden_layers, cfg->rgb_hidden_layers, m->enc_pad);
 			if (m->mlp_variant < 0) throw std::invalid_argument("unsupported MLP shape (n_neurons / hidden layers)");
@@ -287,7 +295,7 @@ ngp_status ngp_model_encode(ngp_model* m, const float* pos, uint32_t stride, uin
 		require(m && (n == 0 || (pos && enc)), "null argument");
 		require(stride >= 3, "stride must be >= 3 floats");
 		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
-		launch_hashgrid_fwd(m->lt, pos, stride, n, table, reinterpret_cast<__half*>(enc), n, S(s));
+		launch_hashgrid_fwd(m->lt, pos, stride, n, table, reinterpret_cast<__half*>(enc), EncLayout{n, 0}, S(s));
 	});
 }
 
@@ -309,8 +317,8 @@ ngp_status ngp_model_infer(ngp_model* m, const float* coords, uint32_t fpc, uint
 		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
 		TrainScratch& ts = m->ts;
 		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
-		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, n, S(s));
-		launch_mlp_infer(m, frags, ts.enc.ptr, n, coords, fpc, n, reinterpret_cast<__half*>(out), S(s));
+		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, internal_layout(m, n), S(s));
+		launch_mlp_infer(m, frags, ts.enc.ptr, internal_layout(m, n), coords, fpc, n, reinterpret_cast<__half*>(out), S(s));
 	});
 }
 
@@ -324,8 +332,8 @@ ngp_status ngp_model_density(ngp_model* m, const float* pos, uint32_t stride, ui
 		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
 		GridState& g = m->gs;
 		g.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
-		launch_hashgrid_fwd(m->lt, pos, stride, n, table, g.enc.ptr, n, S(s));
-		launch_mlp_density(m, frags, g.enc.ptr, n, n, reinterpret_cast<__half*>(out), S(s));
+		launch_hashgrid_fwd(m->lt, pos, stride, n, table, g.enc.ptr, internal_layout(m, n), S(s));
+		launch_mlp_density(m, frags, g.enc.ptr, internal_layout(m, n), n, reinterpret_cast<__half*>(out), S(s));
 	});
 }
 
@@ -344,7 +352,7 @@ ngp_status ngp_model_backward(ngp_model* m, const uint16_t* enc, const float* di
 		for (size_t i = 0; i < n; ++i)
 			for (int k = 0; k < 3; ++k) tmp[8 * i + 4 + k] = d[3 * i + k];
 		NGP_HIP_CHECK(hipMemcpyAsync(ts.ccoords.ptr, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, S(s)));
-		launch_mlp_train(m, m->frag_train.ptr, reinterpret_cast<const __half*>(enc), n, ts.ccoords.ptr, 8, n,
+		launch_mlp_train(m, m->frag_train.ptr, reinterpret_cast<const __half*>(enc), EncLayout{n, 0}, ts.ccoords.ptr, 8, n,
 		                 reinterpret_cast<const __half*>(dloss), weight, m->grads.ptr, reinterpret_cast<__half*>(denc),
 		                 S(s));
 		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
@@ -355,7 +363,7 @@ ngp_status ngp_model_encode_backward(ngp_model* m, const float* pos, uint32_t st
                                      ngp_stream s) {
 	return guarded([&] {
 		require(m && (n == 0 || (pos && denc)), "null argument");
-		launch_hashgrid_bwd(m->lt, pos, stride, n, reinterpret_cast<const __half*>(denc), n,
+		launch_hashgrid_bwd(m->lt, pos, stride, n, reinterpret_cast<const __half*>(denc), EncLayout{n, 0},
 		                    m->grid_grads16.ptr, S(s));
 	});
 }

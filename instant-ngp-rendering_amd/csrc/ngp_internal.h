@@ -139,6 +139,47 @@ struct LevelTable {
 	uint32_t hashed[MAX_LEVELS];
 };
 
+// Layout of an fp16 encoding buffer (n samples, L levels, F features).
+//  * lsh = 0: level-major [L][plane][F], the C-ABI layout.
+//  * lsh = 2: [G][plane][4][F] with G = L / 4 = 2^gsh planes; plane p holds levels p, p + G,
+//    p + 2G, p + 3G -- the four levels one encoder thread computes (k_hashgrid_fwd, LPT = 4),
+//    written with one 16-B store (F = 2), and one MLP lane group's share of a 32-deep K step,
+//    read with one 16-B load (k_mlp_infer_rf; k_pack permutes the first layer's K to match).
+// The internal pipelines use lsh = 2 when L / 4 is a power of two; gradients w.r.t. the
+// encoding (dL/denc) stay level-major.
+struct EncLayout {
+	uint32_t plane = 0;  // samples per plane (row pitch)
+	uint32_t lsh = 0;    // 0 or 2
+	uint32_t gsh = 0;    // log2 planes (lsh = 2)
+	__host__ __device__ size_t vec(uint32_t level, uint32_t i) const {
+		if (lsh == 0) return (size_t)level * plane + i;
+		return ((size_t)((level & ((1u << gsh) - 1u)) * plane + i) << 2) | (level >> gsh);
+	}
+};
+
+// Spherical harmonics of degree 4 of a warped direction in [0, 1]^3 (tcnn
+// SphericalHarmonicsEncoding, configs/nerf/base.json:37-49): the rgb network's 16 inputs.
+__device__ __forceinline__ void sh_deg4(float dx, float dy, float dz, float (&v)[16]) {
+	const float x = dx * 2.0f - 1.0f, y = dy * 2.0f - 1.0f, z = dz * 2.0f - 1.0f;
+	const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
+	v[0] = 0.28209479177387814f;
+	v[1] = -0.48860251190291987f * y;
+	v[2] = 0.48860251190291987f * z;
+	v[3] = -0.48860251190291987f * x;
+	v[4] = 1.0925484305920792f * xy;
+	v[5] = -1.0925484305920792f * yz;
+	v[6] = 0.94617469575755997f * z2 - 0.31539156525251999f;
+	v[7] = -1.0925484305920792f * xz;
+	v[8] = 0.54627421529603959f * x2 - 0.54627421529603959f * y2;
+	v[9] = 0.59004358992664352f * y * (-3.0f * x2 + y2);
+	v[10] = 2.8906114426405538f * xy * z;
+	v[11] = 0.45704579946446572f * y * (1.0f - 5.0f * z2);
+	v[12] = 0.3731763325901154f * z * (5.0f * z2 - 3.0f);
+	v[13] = 0.45704579946446572f * x * (1.0f - 5.0f * z2);
+	v[14] = 1.4453057213202769f * z * (x2 - y2);
+	v[15] = 0.59004358992664352f * x * (-x2 + 3.0f * y2);
+}
+
 struct Layer {
 	uint32_t in, out;          // logical widths (in padded to tcnn's 16-alignment)
 	uint64_t param_offset;     // into the parameter vector (row-major [out][in])
@@ -243,6 +284,7 @@ struct ngp_model {
 	ngp_network_config cfg{};
 	ngp::LevelTable lt{};
 	uint32_t enc_width = 0, enc_pad = 0;
+	uint32_t enc_lsh = 0, enc_gsh = 0;  // EncLayout of the internal encoding buffers
 	uint32_t n_layers = 0, n_density_layers = 0;
 	ngp::Layer layers[ngp::MAX_LAYERS];
 	uint64_t n_mlp_params = 0, n_grid_params = 0, n_params = 0;
@@ -286,10 +328,10 @@ inline void wait_stream(ngp_model* m, hipStream_t s) {
 // > 0 caps the 256-sample chunks launched per level; the blocks then loop over the chunks
 // up to the device count (for large bounds that are rarely reached).
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
-                         __half* enc, uint32_t enc_plane, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2,
+                         __half* enc, EncLayout enc_layout, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2,
                          uint32_t max_chunks = 0);
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                         uint32_t enc_plane, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr);
+                         EncLayout enc_layout, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr);
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
                              float* w, hipStream_t s);
 // mlp.hip
@@ -297,22 +339,24 @@ int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad);
 uint32_t mlp_frag_halves(const ngp_model* m);
 void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s);
 // coords: per-sample records of coord_stride floats holding the warped direction at
-// dir_offset (NerfCoordinate: 4; the renderer's separate direction rows: 0)
-void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+// dir_offset (NerfCoordinate: 4); sh (optional): [n][16] fp16 SH rows used instead
+void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4);
-void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane, uint32_t n,
+                      const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr);
+void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
 // dsh (optional): [n][16] dL/d(SH inputs of the rgb network), of the sample's own row (divided
 // by its rollover weight), for the camera gradients
-void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, uint32_t enc_plane,
+void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
                       const uint32_t* n_dev = nullptr, float* dsh = nullptr);
 // dL/d(warped position) through the grid of the first *n_dev samples (dpos [n][3]), divided by weight
 void launch_hashgrid_input_grad(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                                uint32_t enc_plane, const __half* table, const float* weight, float* dpos, hipStream_t s,
+                                EncLayout enc_layout, const __half* table, const float* weight, float* dpos, hipStream_t s,
                                 const uint32_t* n_dev);
+// layout of the encoding buffers the pipelines keep internally (C-ABI buffers: EncLayout{n, 0})
+inline EncLayout internal_layout(const ngp_model* m, uint32_t plane) { return EncLayout{plane, m->enc_lsh, m->enc_gsh}; }
 // train.hip
 struct SamplerParams;
 void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hipStream_t s);

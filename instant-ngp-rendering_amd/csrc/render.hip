@@ -365,7 +365,7 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 template <uint32_t G>
 __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
-                                                  float4* __restrict__ posdt, float4* __restrict__ dirs,
+                                                  float4* __restrict__ posdt, uint4* __restrict__ shrows,
                                                   uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
@@ -394,14 +394,26 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 	uint32_t base = block_reserve(r == 0 ? budget : 0u, sample_counter);
 	if (G > 1) base = __shfl(base, g0, 64);
 	bool running = valid;
-	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f), wdir = mk3(0.0f);
+	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f);
+	uint4 sh_lo = make_uint4(0u, 0u, 0u, 0u), sh_hi = sh_lo;  // the ray's 16 SH inputs (fp16)
 	float n = 0.0f;
 	if (running) {
 		o = mk3(p->o[0], p->o[1], p->o[2]);
 		d = mk3(p->d[0], p->d[1], p->d[2]);
 		idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-		wdir = warp_direction(d);
 		n = p->n;
+		// the rgb network's direction inputs, once per ray instead of once per sample in the MLP
+		const v3 wdir = warp_direction(d);
+		float v[16];
+		sh_deg4(wdir.x, wdir.y, wdir.z, v);
+		uint32_t u[8];
+#pragma unroll
+		for (int q = 0; q < 8; ++q) {
+			const _Float16 lo = (_Float16)v[2 * q], hi = (_Float16)v[2 * q + 1];
+			u[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
+		}
+		sh_lo = make_uint4(u[0], u[1], u[2], u[3]);
+		sh_hi = make_uint4(u[4], u[5], u[6], u[7]);
 	}
 	OccCache occ = occ_cache_init();
 	const uint32_t oct = ray_octant(d);
@@ -430,7 +442,8 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 				const size_t slot = (size_t)base + j + rank;
 				posdt[slot] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				dirs[slot] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+				shrows[2 * slot] = sh_lo;
+				shrows[2 * slot + 1] = sh_hi;
 			}
 		}
 		if (cnt >= room) {
@@ -454,7 +467,8 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
 		for (uint32_t q = j + r; q < budget; q += G) {
 			posdt[(size_t)base + q] = make_float4(-1.0f, -1.0f, -1.0f, 0.0f);
-			dirs[(size_t)base + q] = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+			shrows[2 * ((size_t)base + q)] = make_uint4(0u, 0u, 0u, 0u);
+			shrows[2 * ((size_t)base + q) + 1] = make_uint4(0u, 0u, 0u, 0u);
 		}
 	}
 	if (k.dbg && valid && r == 0) {
@@ -696,7 +710,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		rs.rgba[b].reserve((size_t)n * 4);
 		rs.depth[b].reserve(n);
 	}
-	rs.coords.reserve(8 * max_samples);  // [0, 4*max): pos + warped dt rows, [4*max, 8*max): direction rows
+	rs.coords.reserve(12 * max_samples);  // [0, 4*max): pos + warped dt rows, [4*max, 12*max): SH rows (16 fp16)
 	rs.enc.reserve((size_t)m->lt.n_levels * max_samples * m->lt.F);
 	rs.out.reserve(4 * max_samples);
 	rs.counters.reserve(16);
@@ -751,7 +765,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	uint32_t* hc = rs.host_counter.ptr;  // pinned (layout at its allocation)
 	// sample records in two row arrays: the encoder reads 16-B position rows once per level
 	float4* posdt = reinterpret_cast<float4*>(rs.coords.ptr);
-	float4* dirs = posdt + max_samples;
+	uint4* shrows = reinterpret_cast<uint4*>(posdt + max_samples);
 	// copy-back (only after k_retire): counters -> slot [32, 40), then an event
 	auto read_back = [&]() -> const uint32_t* {
 		NGP_HIP_CHECK(hipMemcpyAsync(hc + 32, rs.counters.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
@@ -813,10 +827,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		unsigned long long* host_prev = pass > 0 ? pub_dev + 8 * ((pass - 1) % 2) : nullptr;
 		const uint32_t tag_prev = base_tag + pass;  // = tag of pass - 1
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, dirs, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 1: k_generate<1><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
@@ -840,11 +854,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 				fclose(f);
 			}
 		}
-		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, n_elements, s, samples, 1);
+		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, internal_layout(m, n_elements), s, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, s);  // units: the pass's sample count, added at its read-back
 		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
-		launch_mlp_infer(m, frags, rs.enc.ptr, n_elements, reinterpret_cast<const float*>(dirs), 4, n_elements, rs.out.ptr, s,
-		                 samples, 0);
+		launch_mlp_infer(m, frags, rs.enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, rs.out.ptr, s,
+		                 samples, 0, reinterpret_cast<const __half*>(shrows));
 		tm.end(NGP_TIMER_RENDER_MLP, s);
 		tm.begin(NGP_TIMER_RENDER_MARCH, s);
 		k_composite<<<std::max(1u, div_up(n_alive_ub, 1024)), 1024, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,

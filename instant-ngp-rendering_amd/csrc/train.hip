@@ -505,8 +505,6 @@ struct LossArgs {
 	float* ray_state;        // [R][8]: o, d (sampler), u, v of the pixel (k_loss_composite)
 	const float* coords;
 	const __half* mlp_out;
-	const __half* enc;
-	uint32_t enc_plane;
 	uint32_t n_levels, F;
 	uint32_t* ccounts;     // [R] compacted count (pre-cap)
 	uint32_t* cbases;      // [R]
@@ -852,7 +850,7 @@ __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 template <uint32_t F>
 __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ csrc,
                                                           const float* __restrict__ coords, const __half* __restrict__ enc,
-                                                          uint32_t enc_plane, uint32_t n_levels, float* __restrict__ ccoords,
+                                                          EncLayout src_layout, EncLayout dst_layout, uint32_t n_levels, float* __restrict__ ccoords,
                                                           float4* __restrict__ cpos4, __half* __restrict__ cenc, uint32_t target,
                                                           const uint32_t* __restrict__ eidx) {
 	const uint32_t dst = blockIdx.x * 256u + threadIdx.x;
@@ -869,7 +867,16 @@ __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __rest
 	                                     typename std::conditional<F == 4, uint2, uint4>::type>::type>::type;
 	const VT* es = reinterpret_cast<const VT*>(enc);
 	VT* ed = reinterpret_cast<VT*>(cenc);
-	for (uint32_t l = 0; l < n_levels; ++l) ed[(size_t)l * target + dst] = es[(size_t)l * enc_plane + esrc];
+	if (src_layout.lsh == 2 && dst_layout.lsh == 2) {
+		// whole planes: four levels' features in one vector
+		struct alignas(4 * sizeof(VT)) Plane { VT v[4]; };
+		const Plane* ps = reinterpret_cast<const Plane*>(enc);
+		Plane* pd = reinterpret_cast<Plane*>(cenc);
+		for (uint32_t l = 0; l < n_levels; l += 4)
+			pd[(size_t)(l >> 2) * dst_layout.plane + dst] = ps[(size_t)(l >> 2) * src_layout.plane + esrc];
+	} else {
+		for (uint32_t l = 0; l < n_levels; ++l) ed[dst_layout.vec(l, dst)] = es[src_layout.vec(l, esrc)];
+	}
 }
 
 // Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
@@ -1115,15 +1122,15 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	const bool chunk_off = chunk_env && !strcmp(chunk_env, "0");
 	const __half* table = m->params16.ptr + m->n_mlp_params;
 	const __half* enc_rows = ts.enc.ptr;
-	uint32_t enc_plane = MS;
+	EncLayout enc_layout = internal_layout(m, MS);
 	const uint32_t* eidx = nullptr;
 	ts.chunked = !chunk_off;
 	if (chunk_off) {
 		tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
-		launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, table, ts.enc.ptr, MS, s, ts.counters.ptr + 4, 0);
+		launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, table, ts.enc.ptr, enc_layout, s, ts.counters.ptr + 4, 0);
 		tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 		tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
-		launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, MS, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
+		launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, enc_layout, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
 		                 ts.counters.ptr + 4);
 		tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
 	} else {
@@ -1169,16 +1176,18 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			const uint32_t lr = ts.last_rows[p];
 			const uint32_t max_chunks = lr ? div_up((uint64_t)lr + lr / 4, 256) + 16 : 0u;
 			tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
-			launch_hashgrid_fwd(m->lt, ts.epos.ptr + 4 * (size_t)off[p], 4, cap[p], table, ts.eenc.ptr + (size_t)off[p] * F,
-			                    MSE, s, c.rows, 0, max_chunks);
+			// chunk p's rows start at sample off[p] of every plane
+			__half* eenc_p = ts.eenc.ptr + ((size_t)off[p] * F << m->enc_lsh);
+			launch_hashgrid_fwd(m->lt, ts.epos.ptr + 4 * (size_t)off[p], 4, cap[p], table, eenc_p, internal_layout(m, MSE), s,
+			                    c.rows, 0, max_chunks);
 			tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 			tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
-			launch_mlp_infer(m, m->frag_train.ptr, ts.eenc.ptr + (size_t)off[p] * F, MSE, ts.edir.ptr + 4 * (size_t)off[p], 4,
+			launch_mlp_infer(m, m->frag_train.ptr, eenc_p, internal_layout(m, MSE), ts.edir.ptr + 4 * (size_t)off[p], 4,
 			                 cap[p], ts.eout.ptr + 4 * (size_t)off[p], s, c.rows, 0);
 			tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
 		}
 		enc_rows = ts.eenc.ptr;
-		enc_plane = MSE;
+		enc_layout = internal_layout(m, MSE);
 		eidx = ts.eidx.ptr;
 	}
 
@@ -1213,8 +1222,6 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.ray_state = ts.ray_state.ptr;
 	la.coords = ts.coords.ptr;
 	la.mlp_out = ts.mlp_out.ptr;
-	la.enc = ts.enc.ptr;
-	la.enc_plane = MS;
 	la.n_levels = L;
 	la.F = F;
 	la.ccounts = ts.scan_b.ptr;
@@ -1267,10 +1274,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// compacted batch size c = min(total, B); rollover multiplicity
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
 	switch (F) {
-		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
-		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
-		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
-		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_plane, L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
 	}
 	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
@@ -1282,17 +1289,17 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		ts.dsh.reserve(16 * (size_t)B);
 		ts.dpos.reserve(3 * (size_t)B);
 	}
-	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, B, ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
+	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, internal_layout(m, B), ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
 	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
-	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, B, m->grid_grads16.ptr, s,
+	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	if (cam) {
 		// input gradients of the compacted samples (Trainer::training_step with dL_dinput), then
 		// compute_cam_gradient_train_nerf per ray
-		launch_hashgrid_input_grad(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, B, m->params16.ptr + m->n_mlp_params,
+		launch_hashgrid_input_grad(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->params16.ptr + m->n_mlp_params,
 		                           ts.cweight.ptr, ts.dpos.ptr, s, ts.counters.ptr + 5);
 		CamGradArgs ca{};
 		ca.n_rays = R;
