@@ -76,7 +76,20 @@ def kernel_models(cfg):
         "render_mlp": ("mfma", 2 * macs),
         "train_mlp_bwd": ("mfma", 6 * macs),  # fwd + dgrad + wgrad
         "optimizer": ("hbm", 44),  # w32,g,m,v,step in; w32,w16,m,v,step,ema32,ema16 out
+        # init/generate/composite/shade: 28 B per filled sample + 36 B per ray;
+        # units are rays, the per-sample part comes from the render's filled-sample count
+        "render_march": ("hbm", None),
     }
+
+
+MARCH_B_PER_SAMPLE, MARCH_B_PER_RAY = 28, 36
+
+
+def model_bytes(name, per_unit, units, timers):
+    """Algorithmic bytes (or flops) of a timer's launches."""
+    if name == "render_march":
+        return units * MARCH_B_PER_RAY + timers["render_encode"][1] * MARCH_B_PER_SAMPLE
+    return units * per_unit
 
 
 def make_dataset(ngp, tb, n_views, res, device):
@@ -127,32 +140,27 @@ def read_timers(abi, lib, handle):
     return out
 
 
-def cpu_baseline(args, tb, cams, imgs, focal, cfg_abi, W, H):
-    """Scalar oracle (1 core) on a bounded sample: one training step of --cpu-rays rays
-    and --cpu-rows rows of the 1080p frame, with the GPU's trained weights and grid."""
+def cpu_baseline(args, tb, cams, imgs, focal, view, W, H):
+    """Scalar oracle (1 core) on a bounded sample: one training step of --cpu-rays rays and
+    --cpu-rows rows of the 1080p frame, with the GPU's trained weights (EMA inference weights
+    for the render, as the GPU renders) and density grid.  The same rows of the GPU's frame are
+    compared with the oracle's (north_star: rendered RGB within 1e-3 mean L1) -> "parity"."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    import ngp_abi as A
-    from oracle_abi import Oracle
-    from scene_util import HostDataset, pcg_seed, render_args, train_args
+    from scene_util import HostDataset, oracle_frame_rows, testbed_oracle, train_args
 
-    o = Oracle(cfg_abi)
-    lib = A.load()
-    h = C.c_void_p(tb.model_handle)
-    p, n = C.c_void_p(), C.c_size_t()
-    A.check(lib.ngp_model_buffer(h, A.PARAMS_FP32, C.byref(p), C.byref(n)))
-    import torch
+    tb.set_camera_to_training_view(view)
+    gpu_frame = tb.render(W, H, 1, True)  # the timed workload's frame, copied to the host
+    o = testbed_oracle(tb)
 
-    params = torch.empty(n.value // 4, dtype=torch.float32, device="cuda")
-    hip = C.CDLL("libamdhip64.so")
-    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
-    tb.sync()
-    hip.hipMemcpy(C.c_void_p(params.data_ptr()), p, n.value, 3)
-    params = params.cpu().numpy()
-    o.set_params(params)
-    grid = tb.density_grid()
-    o.grid_set(grid)
-    o.grid_bitfield(0)
+    rows = args.cpu_rows
+    block = H // (2 * rows)
+    t0 = time.perf_counter()
+    ref = oracle_frame_rows(o, tb, W, H, [block], rows)
+    t_render = time.perf_counter() - t0
+    ys = sorted(ref)
+    l1 = float(np.abs(gpu_frame[ys, :, :3] - np.stack([ref[y] for y in ys])[..., :3]).mean())
 
+    # the training step last: its optimizer step changes the oracle's weights
     n_sub = min(len(imgs), 8)
     hd = HostDataset(imgs[:n_sub], cams[:n_sub], focal)
     R = args.cpu_rays
@@ -161,25 +169,39 @@ def cpu_baseline(args, tb, cams, imgs, focal, cfg_abi, W, H):
     o.train_step(ta)
     o.optimizer_step(0, 1, 1)
     t_train = time.perf_counter() - t0
-
-    tb.set_camera_to_training_view(0)
-    cam = np.asarray(tb.camera_matrix, np.float32)
-    f = tb.relative_focal_length[1] * H
-    rows = args.cpu_rows
-    ra = render_args(W, H, cam, f, spp=0, snap=0, shard=(H // (2 * rows), H // rows, rows), min_transmittance=0.01)
-    t0 = time.perf_counter()
-    o.render(ra)
-    t_render = time.perf_counter() - t0
-    rays = R + W * rows
+    rays = R + W * len(ys)
     secs = t_train + t_render
-    return {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-            "sample": f"scalar oracle: 1 train step of {R} rays (+Adam over {params.size} params) in {t_train:.2f}s "
-                      f"+ {rows} rows of a {W}x{H} frame ({W * rows} rays) in {t_render:.2f}s, same weights/grid"}
+    cpu = {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
+           "sample": f"scalar oracle: 1 train step of {R} rays (+Adam over {o.n_params} params) in {t_train:.2f}s "
+                     f"+ {len(ys)} rows of the {W}x{H} frame ({W * len(ys)} rays) in {t_render:.2f}s, same weights/grid"}
+    parity = {"rgb_mean_l1_vs_oracle": l1, "rows": [ys[0], ys[-1]], "tolerance": 1e-3, "ok": l1 < 1e-3,
+              "object_pixels_frac": float((gpu_frame[ys, :, 3] > 0.01).mean())}
+    return cpu, parity
+
+
+def launch_ranks(args):
+    """--gpus N without a torchrun environment: start N ranks as a CHILD torchrun (nothing here has
+    touched the GPU yet), relay its output and exit with its status."""
+    import socket
+    import subprocess
+
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
 
 
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
+    if world != args.gpus and "WORLD_SIZE" in os.environ and args.gpus != 1:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
 
@@ -279,6 +301,27 @@ def main():
         dist.all_reduce(r, op=dist.ReduceOp.SUM)
         rays = int(r.item())
 
+    # config C (BASELINE configs[2]): ONE 1080p frame per step, row-sharded over the ranks in
+    # 8-row blocks and gathered to rank 0 over RCCL -- strong scaling of inference
+    config_c = None
+    if world > 1:
+        tb.set_camera_to_training_view(3 % args.views)
+        for _ in range(2):
+            tb.render_distributed(W, H, 1, True, False)
+        barrier()
+        t0 = time.perf_counter()
+        for _ in range(args.steps):
+            tb.render_distributed(W, H, 1, True, False)
+        barrier()
+        tc = time.perf_counter() - t0
+        t = torch.tensor([tc], dtype=torch.float64)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        tc = float(t.item())
+        config_c = {"workload": f"one {W}x{H} spp1 frame per step, 8-row blocks interleaved over {world} ranks, "
+                                "gathered to rank 0 (RCCL send/recv)",
+                    "Mrays_s": round(W * H * args.steps / tc / 1e6, 3), "ms_per_frame": round(1e3 * tc / args.steps, 3),
+                    "scaling": "strong"}
+
     kernels = {}
     for name, (ms, units, launches) in calib.items():
         if launches == 0:
@@ -287,7 +330,7 @@ def main():
                  "us_per_launch": round(1000.0 * ms / launches, 2)}
         if name in models and ms > 0:
             bound, per_unit = models[name]
-            rate = units * per_unit / (ms / 1000.0)
+            rate = model_bytes(name, per_unit, units, calib) / (ms / 1000.0)
             if bound == "hbm":
                 entry["GB/s"] = round(rate / 1e9, 1)
                 entry["frac"] = round(rate / 1e9 / HBM_PEAK_GBS, 4)
@@ -296,8 +339,12 @@ def main():
                 entry["frac"] = round(rate / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)
         kernels[name] = entry
     bound, per_unit = models[dom]
-    ms, units, launches = timers[dom] if args.kernel_timer else calib[dom]
-    achieved = units * per_unit / launches / (ms / launches / 1000.0)
+    tsrc = timers if args.kernel_timer else calib
+    ms, units, launches = tsrc[dom]
+    work = model_bytes(dom, per_unit, units, tsrc)
+    if per_unit is None:
+        per_unit = f"{MARCH_B_PER_SAMPLE} B/filled sample + {MARCH_B_PER_RAY} B/ray"
+    achieved = work / launches / (ms / launches / 1000.0)
     roofline = {
         "kernel": dom,
         "bound": bound,
@@ -307,18 +354,15 @@ def main():
         "traffic": None,
         "per_unit": per_unit,
         "units_per_launch": round(units / launches),
+        "bytes_or_flops_per_launch": round(work / launches),
         "us_per_launch": round(1000.0 * ms / launches, 2),
     }
     roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
     roofline["traffic"] = pmc_traffic(args.traffic_json, dom, units / launches)
 
-    cpu = None
+    cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        from ngp_abi import default_config
-
-        cfg_abi = default_config(n_levels=mcfg["n_levels"], F=mcfg["F"], log2_T=int(enc["log2_hashmap_size"]),
-                                 n_neurons=mcfg["W"], density_hidden=mcfg["dh"], rgb_hidden=mcfg["rh"])
-        cpu = cpu_baseline(args, tb, cams, imgs, focal, cfg_abi, W, H)
+        cpu, parity = cpu_baseline(args, tb, cams, imgs, focal, view, W, H)
 
     value = rays / elapsed / 1e6
     if rank == 0:
@@ -341,12 +385,14 @@ def main():
                        "parallelism": f"dp{world} (RCCL grad all-reduce) + per-rank 1080p view"},
             "roofline": roofline,
             "cpu_baseline": cpu,
+            "parity": parity,
             "split": {"train_Mrays_s": round(split["train_rays"] / split["train_s"] / 1e6, 3),
                       "render_Mrays_s": round(split["render_rays"] / split["render_s"] / 1e6, 3),
                       "train_ms_per_step": round(1e3 * split["train_s"] / args.steps, 3),
                       "render_ms_per_frame": round(1e3 * split["render_s"] / args.steps, 3),
                       "note": "rank 0; per-part wall time inside the timed region (SURVEY 8(d) counts train and inference separately)"},
             "kernels_calibration": kernels,
+            "config_c": config_c,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

@@ -20,6 +20,8 @@
  *   ngp_optimizer_step        Trainer::optimizer_step          src/testbed_nerf.cu:2502 (tcnn Ema∘ExponentialDecay∘Adam,
  *                                                              configs/nerf/base.json:5-22)
  *   ngp_train_read_stats      NerfCounters::update_after_training  src/testbed_nerf.cu:2422-2446
+ *   ngp_allreduce_grads       (no reference counterpart: multi-GPU training is not supported upstream,
+ *                             README.md:250-252) -- the data-parallel gradient reduction of SURVEY 8(e)
  *   ngp_density_grid_update   Testbed::update_density_grid_nerf     src/testbed_nerf.cu:2271-2360
  *                             + update_density_grid_mean_and_bitfield :2362-2379
  *   ngp_render                Testbed::render_nerf / NerfTracer      src/testbed_nerf.cu:1827-1987, 1556-1761
@@ -157,6 +159,11 @@ typedef struct ngp_train_args {
 	 * divided by the pixel pdf; null = off */
 	float* cam_pos_gradient;
 	float* cam_rot_gradient;
+	/* 1: run the network over every emitted sample before the loss, as the reference does
+	 * (src/testbed_nerf.cu:2797-2802); 0: the early-terminated chunked forward, which evaluates
+	 * each ray only up to its transmittance stop (identical loss/compaction/gradients, see
+	 * train_stats.forward_early_stop_violations) */
+	int32_t full_forward;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {
@@ -165,6 +172,10 @@ typedef struct ngp_train_stats {
 	uint32_t measured_batch_size_before_compaction; /* numsteps_counter */
 	uint32_t measured_batch_size;                   /* numsteps_counter_compacted */
 	float loss;                                     /* sum over rays of mean per-ray loss / n_rays */
+	/* rays whose loss composite needed a sample the chunked forward had not evaluated (the
+	 * chunk stop and the loss stop disagree); must be 0 -- the Testbed switches to the full
+	 * forward for the rest of the run if it is not */
+	uint32_t forward_early_stop_violations;
 } ngp_train_stats;
 
 typedef struct ngp_grid_args {
@@ -244,6 +255,10 @@ ngp_status ngp_train_step(ngp_model* model, const ngp_train_args* args, ngp_stre
 ngp_status ngp_optimizer_step(ngp_model* model, uint32_t training_step, int optimize_mlp, int optimize_encoding,
                               ngp_stream stream);
 ngp_status ngp_train_read_stats(ngp_model* model, ngp_train_stats* stats, ngp_stream stream);
+/* Data-parallel training: sum the model's gradients over an RCCL communicator (an ncclComm_t):
+ * the fp32 MLP gradients and the fp16 hash-grid gradients, in one group on `stream`.  Call it
+ * between ngp_train_step (defer_optimizer = 1) and ngp_optimizer_step on every rank. */
+ngp_status ngp_allreduce_grads(ngp_model* model, void* nccl_comm, ngp_stream stream);
 /* Debug/parity: device pointers to the last step's scratch (valid until the next step). */
 enum {
 	NGP_SCRATCH_RAY_NUMSTEPS = 0, /* [n_rays][2] u32: (numsteps, base) after sampling */

@@ -12,6 +12,8 @@
 #include <string>
 #include <vector>
 
+#include <rccl/rccl.h>
+
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -385,6 +387,23 @@ ngp_status ngp_optimizer_step(ngp_model* m, uint32_t step, int opt_mlp, int opt_
 	});
 }
 
+ngp_status ngp_allreduce_grads(ngp_model* m, void* comm, ngp_stream s) {
+	return guarded([&] {
+		require(m && comm, "null argument");
+		const ncclComm_t c = (ncclComm_t)comm;
+		auto nk = [](ncclResult_t r, const char* what) {
+			if (r != ncclSuccess) throw std::runtime_error(std::string("RCCL error ") + ncclGetErrorString(r) + " in " + what);
+		};
+		// one group: the 41 KB fp32 MLP gradients and the fp16 hash-grid gradients (the buffer the
+		// packed atomics write) -- summed, so every rank's optimizer step sees the global gradient
+		nk(ncclGroupStart(), "ncclGroupStart");
+		nk(ncclAllReduce(m->grads.ptr, m->grads.ptr, m->n_mlp_params, ncclFloat32, ncclSum, c, S(s)), "ncclAllReduce(mlp grads)");
+		nk(ncclAllReduce(m->grid_grads16.ptr, m->grid_grads16.ptr, m->n_params - m->n_mlp_params, ncclFloat16, ncclSum, c, S(s)),
+		   "ncclAllReduce(grid grads)");
+		nk(ncclGroupEnd(), "ncclGroupEnd");
+	});
+}
+
 ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s) {
 	return guarded([&] {
 		require(m && st, "null argument");
@@ -413,6 +432,7 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		std::memcpy(&loss, &c[8], 4);
 		st->loss = loss;
 		st->n_rays_with_samples = 0;
+		st->forward_early_stop_violations = c[9];
 	});
 }
 

@@ -100,9 +100,9 @@ struct KernelTimers {
 		units[slot] += u;
 		++launches[slot];
 	}
-	void add_units(int slot, uint64_t u) {
-		if (on(slot)) units[slot] += u;
-	}
+	// units are counted even while the slot's events are off (the march's roofline needs the
+	// render's sample count when only the march timer runs)
+	void add_units(int slot, uint64_t u) { units[slot] += u; }
 	void collect() {
 		for (const Pending& p : pending) {
 			NGP_HIP_CHECK(hipEventSynchronize(p.b));

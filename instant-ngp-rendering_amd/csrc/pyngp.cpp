@@ -399,6 +399,7 @@ PYBIND11_MODULE(pyngp, m) {
 		     [](Testbed& t, py::object j, const std::string& base) { t.reload_network_from_json(json_from_py(j), base); },
 		     py::arg("json"), py::arg("config_base_path") = "")
 		.def_property_readonly("network_config", [](const Testbed& t) { return json_to_py(t.network_config()); })
+		.def_property_readonly("per_level_scale", [](const Testbed& t) { return t.network_abi_config().per_level_scale; })
 		.def("n_params", [](const Testbed& t) -> size_t {
 			if (!t.model()) return 0;
 			ngp_model_info i{};
@@ -441,6 +442,7 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("screen_center", &Testbed::screen_center)
 		.def_readwrite("relative_focal_length", &Testbed::relative_focal_length)
 		.def_readwrite("training_batch_size", &Testbed::training_batch_size)
+		.def_readwrite("train_full_forward", &Testbed::train_full_forward)
 		.def("set_nerf_camera_matrix",
 		     [](Testbed& t, py::array_t<float, py::array::c_style | py::array::forcecast> c) {
 			     auto rm = numpy_to_rowmajor34(c);
@@ -505,6 +507,8 @@ PYBIND11_MODULE(pyngp, m) {
 			d["measured_batch_size_before_compaction"] = s.measured_batch_size_before_compaction;
 			d["rays_per_batch"] = t.nerf.training.counters_rgb.rays_per_batch;
 			d["n_rays"] = s.n_rays;
+			d["forward_early_stop_violations"] = s.forward_early_stop_violations;
+			d["forward_early_stop_violations_total"] = t.forward_early_stop_violations;
 			return d;
 		})
 		.def("sync", &Testbed::sync)
@@ -515,6 +519,36 @@ PYBIND11_MODULE(pyngp, m) {
 		.def("init_distributed",
 		     [](Testbed& t, int rank, int world, py::bytes uid) { t.init_distributed(rank, world, std::string(uid)); },
 		     py::arg("rank"), py::arg("world_size"), py::arg("unique_id"))
+		.def("init_distributed_host",
+		     [](Testbed& t, int rank, int world, py::function fn) {
+			     // fn(array, op) reduces a host numpy array in place (op "sum" / "max"); called with the GIL
+			     // re-acquired, since train() / frame() release it
+			     auto hold = std::make_shared<py::function>(std::move(fn));
+			     t.init_distributed_host(rank, world, [hold](void* p, size_t n, int dtype, int op) {
+				     py::gil_scoped_acquire gil;
+				     py::array a = dtype == 0 ? py::array(py::dtype("float32"), {(py::ssize_t)n}, {(py::ssize_t)4}, p, py::none())
+				                              : py::array(py::dtype("float16"), {(py::ssize_t)n}, {(py::ssize_t)2}, p, py::none());
+				     (*hold)(a, op ? "max" : "sum");
+			     });
+		     },
+		     "Data-parallel Testbed whose collectives are staged through host memory and reduced by fn "
+		     "(test backend: several processes sharing one GPU over torch.distributed/gloo).",
+		     py::arg("rank"), py::arg("world_size"), py::arg("allreduce"))
+		.def("render_distributed",
+		     [](Testbed& t, int width, int height, int spp, bool linear, bool copy_to_host) -> py::object {
+			     std::vector<float> img;
+			     {
+				     py::gil_scoped_release rel;
+				     img = t.render_distributed(width, height, spp, linear, copy_to_host);
+			     }
+			     if (img.empty()) return py::none();
+			     py::array_t<float> a({height, width, 4});
+			     std::memcpy(a.mutable_data(), img.data(), img.size() * sizeof(float));
+			     return a;
+		     },
+		     "One frame row-sharded over the ranks and gathered to rank 0 (None on the other ranks).",
+		     py::arg("width") = 1920, py::arg("height") = 1080, py::arg("spp") = 1, py::arg("linear") = true,
+		     py::arg("copy_to_host") = true)
 		.def_property_readonly("rank", &Testbed::rank)
 		.def_property_readonly("world_size", &Testbed::world_size);
 }

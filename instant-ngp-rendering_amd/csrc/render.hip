@@ -136,6 +136,21 @@ __device__ __forceinline__ uint32_t block_reserve(uint32_t cnt, uint32_t* counte
 	return b + x - cnt;
 }
 
+// Adds v over the whole block to *counter with one atomic (all threads of the block call it).
+__device__ __forceinline__ void block_add(uint32_t v, uint32_t* counter) {
+	__shared__ uint32_t ws[16];
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6, nw = blockDim.x >> 6;
+#pragma unroll
+	for (uint32_t o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+	if (lane == 0) ws[w] = v;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint32_t t = 0;
+		for (uint32_t k = 0; k < nw; ++k) t += ws[k];
+		if (t) atomicAdd(counter, t);
+	}
+}
+
 template <bool LENS>
 __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
                                                      float* __restrict__ depth, float4* __restrict__ frame,
@@ -494,7 +509,8 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
                                                    float* __restrict__ ddepth, Payload* __restrict__ hp,
                                                    float4* __restrict__ hrgba, float* __restrict__ hdepth,
                                                    uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter,
-                                                   uint32_t* __restrict__ next_sample_counter) {
+                                                   uint32_t* __restrict__ next_sample_counter,
+                                                   uint32_t* __restrict__ filled_counter) {
 	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
 	const uint32_t n_alive = *alive_in;
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -502,6 +518,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
 	float local_depth = 0.0f;
 	bool alive = false;
+	uint32_t filled = 0;
 	if (i < n_alive) {
 		p = sp[i];
 		c = srgba[i];
@@ -511,6 +528,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 	if (alive) {
 		const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
 		const uint32_t actual = p.n_steps & ~PAYLOAD_EXITED;
+		filled = actual;
 		const size_t sbase = p.base;
 		// samples are loaded 4 ahead of their use (the loop is otherwise one dependent
 		// global-load latency per sample; the tail passes run up to 32 per ray)
@@ -565,6 +583,9 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		if (done || (p.n_steps & PAYLOAD_EXITED)) alive = false;
 	}
 	const bool hit = i < n_alive && !alive && c.w > 0.001f;
+	// samples the rays actually filled this pass (reserved slots past an exit are not counted):
+	// the frame's network-evaluated sample count for the roofline
+	block_add(filled, filled_counter);
 	uint32_t oa, oh;
 	block_append2(alive, hit, alive_counter, hit_counter, &oa, &oh);
 	if (alive) {
@@ -803,12 +824,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		return out;
 	};
-	auto consume = [&](uint32_t pass) -> const uint32_t* {  // every pass's counters are consumed once
-		const uint32_t* c = wait_slot(pass);
-		tm.add_units(NGP_TIMER_RENDER_ENCODE, c[4 + pass % 2]);
-		tm.add_units(NGP_TIMER_RENDER_MLP, c[4 + pass % 2]);
-		return c;
-	};
+	auto consume = [&](uint32_t pass) -> const uint32_t* { return wait_slot(pass); };
 	int cur = 0;
 	uint32_t pass = 0, steps_done = 0;
 	uint32_t n_alive_ub = n;  // upper bound on the alive rays entering the next pass
@@ -864,7 +880,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		k_composite<<<std::max(1u, div_up(n_alive_ub, 1024)), 1024, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
 		                                                                  posdt, rs.out.ptr, P(1 - cur), C(1 - cur),
 		                                                                  rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr,
-		                                                                  alive_out, rs.counters.ptr + 2, samples_next);
+		                                                                  alive_out, rs.counters.ptr + 2, samples_next,
+                                                                  rs.counters.ptr + 3);
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		NGP_HIP_CHECK(hipGetLastError());
 		cur = 1 - cur;
@@ -882,6 +899,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const uint32_t* last = consume(pass - 1);
 	uint32_t n_alive = last[pass % 2];
 	uint32_t n_hit = last[2];
+	// [3]: filled samples of the whole frame (the encoder / MLP skip the unfilled slots' work)
+	tm.add_units(NGP_TIMER_RENDER_ENCODE, last[3]);
+	tm.add_units(NGP_TIMER_RENDER_MLP, last[3]);
 	if (n_alive > 0) {
 		// march budget exhausted: still-alive rays are shaded with what they accumulated
 		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,

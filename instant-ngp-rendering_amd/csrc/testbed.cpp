@@ -208,6 +208,7 @@ Testbed::~Testbed() {
 	for (float* p : {m_frame, m_depth, m_accum, m_out})
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
+	if (m_pack) (void)hipFree(m_pack);
 	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
@@ -863,6 +864,7 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.optimize_mlp = train_network;
 	a.optimize_encoding = train_encoding;
 	a.defer_optimizer = m_world > 1 ? 1 : 0;
+	a.full_forward = train_full_forward ? 1 : 0;
 	for (size_t i = 0; i < tr.dataset.metadata.size(); ++i)
 		if (tr.dataset.metadata[i].lens.mode != ELensMode::Perspective) a.has_lens = 1;
 	if (m_err && tr.error_map.resolution[0] > 0 && tr.error_map.resolution[1] > 0) {
@@ -885,15 +887,18 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	ck(ngp_train_step(m_model, &a, m_stream));
 	if (m_world > 1) {
 		// MLP gradients (fp32) and hash-grid gradients (fp16) are summed over ranks
-		void *g = nullptr, *g16 = nullptr;
-		size_t bytes = 0, bytes16 = 0;
-		ngp_model_info info{};
-		ck(ngp_model_get_info(m_model, &info));
-		ck(ngp_model_buffer(m_model, NGP_GRADS_FP32, &g, &bytes));
-		ck(ngp_model_buffer(m_model, NGP_GRADS_GRID_FP16, &g16, &bytes16));
-		allreduce_f32((float*)g, info.n_mlp_params, false);
-		nk(ncclAllReduce(g16, g16, bytes16 / 2, ncclFloat16, ncclSum, (ncclComm_t)m_comm, (hipStream_t)m_stream),
-		   "ncclAllReduce(grid grads)");
+		if (m_comm) {
+			ck(ngp_allreduce_grads(m_model, m_comm, m_stream));
+		} else {
+			void *g = nullptr, *g16 = nullptr;
+			size_t bytes = 0, bytes16 = 0;
+			ngp_model_info info{};
+			ck(ngp_model_get_info(m_model, &info));
+			ck(ngp_model_buffer(m_model, NGP_GRADS_FP32, &g, &bytes));
+			ck(ngp_model_buffer(m_model, NGP_GRADS_GRID_FP16, &g16, &bytes16));
+			allreduce_dev(g, info.n_mlp_params, 0, false);
+			allreduce_dev(g16, bytes16 / 2, 1, false);
+		}
 		ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 	}
 	++training_step;
@@ -928,6 +933,13 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 		st.measured_batch_size = (uint32_t)(v[0] / (float)m_world);
 		st.measured_batch_size_before_compaction = (uint32_t)(v[1] / (float)m_world);
 		st.loss = v[2];
+	}
+	if (st.forward_early_stop_violations) {
+		forward_early_stop_violations += st.forward_early_stop_violations;
+		if (!train_full_forward)
+			std::fprintf(stderr, "Nerf training: the chunked forward missed samples of %u rays; switching to the full forward.\n",
+			             st.forward_early_stop_violations);
+		train_full_forward = true;
 	}
 	m_last_stats = st;
 	ctr.measured_batch_size = st.measured_batch_size;
@@ -1650,10 +1662,106 @@ void Testbed::init_distributed(int rank, int world_size, const std::string& uid)
 	hk(hipMalloc(&m_red_buf, 64), "hipMalloc reduction scratch");
 }
 
-void Testbed::allreduce_f32(float* dev, size_t n, bool max_op) {
-	if (m_world <= 1) return;
-	nk(ncclAllReduce(dev, dev, n, ncclFloat32, max_op ? ncclMax : ncclSum, (ncclComm_t)m_comm, (hipStream_t)m_stream),
-	   "ncclAllReduce");
+// Rows of an H-row frame that shard `idx` of `count` owns in blocks of `rows` (ngp_render_args).
+static std::vector<std::pair<uint32_t, uint32_t>> owned_row_runs(uint32_t H, uint32_t idx, uint32_t count, uint32_t rows) {
+	std::vector<std::pair<uint32_t, uint32_t>> runs;  // (first row, n rows)
+	for (uint32_t b = idx; b * rows < H; b += count) runs.push_back({b * rows, std::min(rows, H - b * rows)});
+	return runs;
+}
+
+std::vector<float> Testbed::render_distributed(int width, int height, int spp, bool linear, bool copy_to_host) {
+	const uint32_t R = 8;
+	if (m_world <= 1) return render(width, height, spp, linear, 0, 1, R, copy_to_host);
+	render(width, height, spp, linear, (uint32_t)m_rank, (uint32_t)m_world, R, false);
+	const size_t row_bytes = (size_t)width * 4 * sizeof(float);
+	hipStream_t s = (hipStream_t)m_stream;
+	// pack this rank's rows (contiguous in shard order), then rank 0 receives every rank's pack
+	std::vector<size_t> pack_rows(m_world);
+	for (int r = 0; r < m_world; ++r)
+		for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)r, (uint32_t)m_world, R)) pack_rows[r] += run.second;
+	const size_t cap = *std::max_element(pack_rows.begin(), pack_rows.end()) * row_bytes * (m_rank == 0 ? (size_t)m_world : 1);
+	if (cap > m_pack_cap) {
+		if (m_pack) (void)hipFree(m_pack);
+		hk(hipMalloc((void**)&m_pack, cap), "hipMalloc pack");
+		m_pack_cap = cap;
+	}
+	const size_t slot = *std::max_element(pack_rows.begin(), pack_rows.end()) * row_bytes;
+	if (m_rank != 0) {
+		size_t off = 0;
+		for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)m_rank, (uint32_t)m_world, R)) {
+			hk(hipMemcpyAsync((char*)m_pack + off, (const char*)m_out + run.first * row_bytes, run.second * row_bytes,
+			                  hipMemcpyDeviceToDevice, s), "pack rows");
+			off += run.second * row_bytes;
+		}
+	}
+	if (!m_comm) {
+		// host-staged test backend: owned rows over a zero frame, summed over the ranks
+		std::vector<float> full((size_t)width * height * 4, 0.0f);
+		for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)m_rank, (uint32_t)m_world, R))
+			hk(hipMemcpyAsync((char*)full.data() + run.first * row_bytes, (const char*)m_out + run.first * row_bytes,
+			                  run.second * row_bytes, hipMemcpyDeviceToHost, s), "rows d2h");
+		sync();
+		m_host_allreduce(full.data(), full.size(), 0, 0);
+		if (m_rank != 0) return {};
+		hk(hipMemcpyAsync(m_out, full.data(), full.size() * sizeof(float), hipMemcpyHostToDevice, s), "frame h2d");
+		sync();
+		if (!copy_to_host) full.clear();
+		return full;
+	}
+	nk(ncclGroupStart(), "ncclGroupStart");
+	if (m_rank == 0) {
+		for (int r = 1; r < m_world; ++r)
+			nk(ncclRecv((char*)m_pack + r * slot, pack_rows[r] * row_bytes, ncclChar, r, (ncclComm_t)m_comm, s), "ncclRecv rows");
+	} else {
+		nk(ncclSend(m_pack, pack_rows[m_rank] * row_bytes, ncclChar, 0, (ncclComm_t)m_comm, s), "ncclSend rows");
+	}
+	nk(ncclGroupEnd(), "ncclGroupEnd");
+	std::vector<float> out;
+	if (m_rank == 0) {
+		for (int r = 1; r < m_world; ++r) {
+			size_t off = 0;
+			for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)r, (uint32_t)m_world, R)) {
+				hk(hipMemcpyAsync((char*)m_out + run.first * row_bytes, (const char*)m_pack + r * slot + off,
+				                  run.second * row_bytes, hipMemcpyDeviceToDevice, s), "unpack rows");
+				off += run.second * row_bytes;
+			}
+		}
+		if (copy_to_host) {
+			out.resize((size_t)width * height * 4);
+			hk(hipMemcpyAsync(out.data(), m_out, out.size() * sizeof(float), hipMemcpyDeviceToHost, s), "frame d2h");
+		}
+	}
+	sync();
+	return out;
+}
+
+void Testbed::allreduce_f32(float* dev, size_t n, bool max_op) { allreduce_dev(dev, n, 0, max_op); }
+
+void Testbed::allreduce_dev(void* dev, size_t n, int dtype, bool max_op) {
+	if (m_world <= 1 || n == 0) return;
+	if (m_comm) {
+		nk(ncclAllReduce(dev, dev, n, dtype == 0 ? ncclFloat32 : ncclFloat16, max_op ? ncclMax : ncclSum, (ncclComm_t)m_comm,
+		                 (hipStream_t)m_stream),
+		   "ncclAllReduce");
+		return;
+	}
+	if (!m_host_allreduce) throw std::runtime_error("distributed Testbed without a collective backend");
+	const size_t bytes = n * (dtype == 0 ? 4 : 2);
+	std::vector<uint8_t> h(bytes);
+	hk(hipMemcpyAsync(h.data(), dev, bytes, hipMemcpyDeviceToHost, (hipStream_t)m_stream), "allreduce d2h");
+	sync();
+	m_host_allreduce(h.data(), n, dtype, max_op ? 1 : 0);
+	hk(hipMemcpyAsync(dev, h.data(), bytes, hipMemcpyHostToDevice, (hipStream_t)m_stream), "allreduce h2d");
+	sync();
+}
+
+void Testbed::init_distributed_host(int rank, int world_size, HostAllReduce fn) {
+	if (world_size <= 1) return;
+	if (!fn) throw std::runtime_error("init_distributed_host: no all-reduce function");
+	m_host_allreduce = std::move(fn);
+	m_rank = rank;
+	m_world = world_size;
+	if (!m_red_buf) hk(hipMalloc(&m_red_buf, 64), "hipMalloc reduction scratch");
 }
 
 }  // namespace ngp

@@ -166,6 +166,7 @@ public:
 	void reload_network_from_json(const Json& json, const std::string& config_base_path = "");
 	void reset_network(bool clear_density_grid = true);
 	Json network_config() const { return m_network_config; }
+	const ngp_network_config& network_abi_config() const { return m_net_cfg; }  // the resolved C-ABI config
 
 	// --- training (train src/testbed.cu:4020, frame :3380) ---
 	void train(uint32_t batch_size);
@@ -190,7 +191,16 @@ public:
 
 	// --- multi-GPU: one Testbed per rank, gradients all-reduced over RCCL/xGMI ---
 	void init_distributed(int rank, int world_size, const std::string& nccl_unique_id);
+	// Test backend: the same data-parallel path with every collective staged through host memory
+	// and a caller-supplied all-reduce (e.g. torch.distributed over gloo), so several processes can
+	// share one GPU.  fn(host_ptr, n, dtype 0 f32 / 1 f16, op 0 sum / 1 max) reduces in place.
+	using HostAllReduce = std::function<void(void*, size_t, int, int)>;
+	void init_distributed_host(int rank, int world_size, HostAllReduce fn);
 	static std::string nccl_unique_id();
+	// config C: one frame row-sharded over the ranks (8-row blocks, interleaved) and gathered into
+	// rank 0's frame buffer over RCCL (the reference's aux-device copy-back, src/testbed.cu:5089-5090).
+	// Every rank calls it; rank 0 returns the frame (copy_to_host) and holds it in render_frame_buffer().
+	std::vector<float> render_distributed(int width, int height, int spp, bool linear, bool copy_to_host = true);
 	int rank() const { return m_rank; }
 	int world_size() const { return m_world; }
 
@@ -207,6 +217,11 @@ public:
 	bool shall_train = false;
 	bool train_encoding = true, train_network = true;
 	uint32_t training_batch_size = 1 << 18;
+	// evaluate every emitted sample before the loss (the reference's forward) instead of the
+	// early-terminated chunked forward; switched on automatically if the chunked forward ever
+	// misses a sample the loss needs (ngp_train_stats::forward_early_stop_violations)
+	bool train_full_forward = false;
+	uint64_t forward_early_stop_violations = 0;
 	uint32_t training_step = 0;
 	float loss = 0.0f;  // Ema m_loss_scalar (val) of src/testbed.cu:4106-4108
 	vec4 background_color = {0.f, 0.f, 0.f, 1.f};
@@ -242,6 +257,8 @@ private:
 	void free_device_dataset();
 	void ensure_render_buffers(size_t n_pixels);
 	void allreduce_f32(float* dev, size_t n, bool max_op);
+	void allreduce_dev(void* dev, size_t n, int dtype, bool max_op);  // RCCL or the host-staged backend
+	HostAllReduce m_host_allreduce;
 
 	void update_error_map_cdf();
 
@@ -281,6 +298,8 @@ private:
 	int m_rank = 0, m_world = 1;
 	void* m_comm = nullptr;
 	void* m_red_buf = nullptr;
+	float* m_pack = nullptr;  // owned rows of a sharded frame, packed for the gather
+	size_t m_pack_cap = 0;
 };
 
 std::string natural_sort_key(const std::string& s);

@@ -515,6 +515,7 @@ struct LossArgs {
 	__half* dloss;         // [B][4]
 	const float* mean_density;
 	const uint32_t* ray_eval;  // [R] samples the chunked forward evaluated (null: all of them)
+	uint32_t* violations;      // rays whose composite reached past the evaluated samples (must stay 0)
 	int store_uv_pdf;          // camera gradients: ray_aux[i].w = the pixel's pdf
 };
 
@@ -594,6 +595,8 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 		}
 		T *= __shfl(incl, 63, 64);
 	}
+	// runtime guard of the chunked forward: every sample before the stop must have been evaluated
+	if (lane == 0 && a.ray_eval && evaluated < c) atomicAdd(a.violations, 1u);
 
 	// Same RNG stream as the sampler -> same pixel and background colour (testbed_nerf.cu:938-955).
 	const uint32_t gi = a.ray_offset + i;
@@ -1119,7 +1122,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// every emitted sample as the reference does (NGP_TRAIN_CHUNKED=0), or chunk by chunk up to
 	// each ray's stop (k_train_chunk) -- the loss kernels read the same outputs either way
 	const char* chunk_env = getenv("NGP_TRAIN_CHUNKED");  // read per step (tests switch it)
-	const bool chunk_off = chunk_env && !strcmp(chunk_env, "0");
+	const bool chunk_off = t->full_forward || (chunk_env && !strcmp(chunk_env, "0"));
 	const __half* table = m->params16.ptr + m->n_mlp_params;
 	const __half* enc_rows = ts.enc.ptr;
 	EncLayout enc_layout = internal_layout(m, MS);
@@ -1233,6 +1236,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.dloss = ts.dloss.ptr;
 	la.mean_density = m->gs.mean.ptr;
 	la.ray_eval = ts.chunked ? ts.ray_eval.ptr : nullptr;
+	la.violations = ts.counters.ptr + 9;
 	const bool cam = t->cam_pos_gradient && t->cam_rot_gradient;
 	la.store_uv_pdf = cam ? 1 : 0;
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);

@@ -58,7 +58,7 @@ class TrainArgs(C.Structure):
         ("error_map", C.c_void_p), ("error_map_res", C.c_uint32 * 2), ("cdf_x_cond_y", C.c_void_p),
         ("cdf_y", C.c_void_p), ("cdf_img", C.c_void_p), ("cdf_res", C.c_uint32 * 2), ("has_lens", C.c_int32),
         ("exposure", C.c_void_p), ("exposure_gradient", C.c_void_p),
-        ("cam_pos_gradient", C.c_void_p), ("cam_rot_gradient", C.c_void_p),
+        ("cam_pos_gradient", C.c_void_p), ("cam_rot_gradient", C.c_void_p), ("full_forward", C.c_int32),
     ]
 
 
@@ -66,7 +66,7 @@ class TrainStats(C.Structure):
     _fields_ = [
         ("n_rays", C.c_uint32), ("n_rays_with_samples", C.c_uint32),
         ("measured_batch_size_before_compaction", C.c_uint32), ("measured_batch_size", C.c_uint32),
-        ("loss", C.c_float),
+        ("loss", C.c_float), ("forward_early_stop_violations", C.c_uint32),
     ]
 
 
@@ -119,6 +119,7 @@ EXPORTS = {
     "ngp_train_step": (C.c_int, [C.c_void_p, C.POINTER(TrainArgs), C.c_void_p]),
     "ngp_optimizer_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_void_p]),
     "ngp_train_read_stats": (C.c_int, [C.c_void_p, C.POINTER(TrainStats), C.c_void_p]),
+    "ngp_allreduce_grads": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngp_train_scratch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "ngp_density_grid_update": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),
     "ngp_density_grid_evaluate": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),

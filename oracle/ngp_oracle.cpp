@@ -1507,6 +1507,14 @@ void oref_model_set_params(void* m, const float* p) {
 	}
 	M.ema_step = 0;
 }
+// the EMA weights of a trained model: the fp16 inference params (use_inference_params) derived from them
+void oref_model_set_inference_params(void* m, const float* ema) {
+	Model& M = *static_cast<Model*>(m);
+	for (uint64_t i = 0; i < M.n; ++i) {
+		M.ema32[i] = ema[i];
+		M.inf16[i] = f2h(ema[i]);
+	}
+}
 void oref_model_get(void* m, int kind, void* out) {
 	Model& M = *static_cast<Model*>(m);
 	switch (kind) {

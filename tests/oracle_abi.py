@@ -36,6 +36,7 @@ _PROTOS = {
     "oref_model_level_table": (None, [C.c_void_p] + [C.c_void_p] * 5),
     "oref_model_set_params": (None, [C.c_void_p, C.c_void_p]),
     "oref_model_get": (None, [C.c_void_p, C.c_int, C.c_void_p]),
+    "oref_model_set_inference_params": (None, [C.c_void_p, C.c_void_p]),
     "oref_zero_grads": (None, [C.c_void_p]),
     "oref_model_set_grads": (None, [C.c_void_p, C.c_void_p]),
     "oref_encode": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
@@ -113,6 +114,12 @@ class Oracle:
         p = np.ascontiguousarray(p, np.float32)
         assert p.size == self.n_params
         self.lib.oref_model_set_params(self.h, ptr(p))
+
+    def set_inference_params(self, ema):
+        """EMA weights (fp32) -> the fp16 inference params renders and use_inference_params read."""
+        ema = np.ascontiguousarray(ema, np.float32)
+        assert ema.size == self.n_params
+        self.lib.oref_model_set_inference_params(self.h, ptr(ema))
 
     def get(self, kind):
         dt = np.uint16 if kind in (A.PARAMS_FP16, A.PARAMS_INFER_FP16) else np.float32

@@ -167,3 +167,85 @@ def sphere_bitfield(radius=0.3, center=(0.5, 0.5, 0.5)):
     d = np.linalg.norm(p - np.asarray(center, np.float32), axis=-1)
     grid = np.where(d < radius, 1.0, 0.0).astype(np.float32)
     return grid
+
+
+def testbed_abi_config(tb):
+    """The C-ABI network config of a pyngp Testbed's current network (for the oracle)."""
+    cfg = tb.network_config
+    enc = cfg["encoding"]
+    c = A.default_config(n_levels=int(enc["n_levels"]), F=int(enc["n_features_per_level"]),
+                         log2_T=int(enc["log2_hashmap_size"]), base_res=int(enc.get("base_resolution", 16)),
+                         n_neurons=int(cfg["network"]["n_neurons"]),
+                         density_hidden=int(cfg["network"]["n_hidden_layers"]),
+                         rgb_hidden=int(cfg["rgb_network"]["n_hidden_layers"]),
+                         aabb_scale=int(tb.nerf.training.dataset.aabb_scale))
+    c.per_level_scale = float(tb.per_level_scale)  # exactly as the Testbed resolved it
+    return c
+
+
+def testbed_oracle(tb):
+    """CPU oracle holding a Testbed's trained state: fp32 weights, the EMA inference weights the
+    renderer reads, the density grid and its bitfield (test infrastructure only)."""
+    from oracle_abi import Oracle
+    o = Oracle(testbed_abi_config(tb))
+    lib = A.load()
+    h = C.c_void_p(tb.model_handle)
+    tb.sync()
+
+    def fetch(kind):
+        p, n = C.c_void_p(), C.c_size_t()
+        A.check(lib.ngp_model_buffer(h, kind, C.byref(p), C.byref(n)))
+        out = np.zeros(n.value // 4, np.float32)
+        hip = C.CDLL("libamdhip64.so")
+        hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+        assert hip.hipMemcpy(out.ctypes.data_as(C.c_void_p), p, n.value, 2) == 0
+        return out
+    o.set_params(fetch(A.PARAMS_FP32))
+    o.set_inference_params(fetch(A.PARAMS_EMA_FP32))
+    o.grid_set(tb.density_grid())
+    o.set_bitfield(tb.density_grid_bitfield())  # the occupancy the GPU marches (bitfield parity is tested apart)
+    return o
+
+
+def testbed_render_args(tb, W, H, shard=(0, 1, 8), sample_index=0):
+    """ngp_render_args exactly as Testbed::render builds them from the Testbed's camera state."""
+    r = A.RenderArgs()
+    r.width, r.height, r.sample_index = W, H, sample_index
+    cam = np.asarray(tb.camera_matrix, np.float32)  # 3x4, columns right/down/forward/origin (NGP space)
+    xf = cam.T.reshape(-1)
+    for k in range(12):
+        r.camera[k] = float(xf[k])
+    zoom = float(tb.zoom)
+    res_axis = W if tb.fov_axis == 0 else H
+    rf = tb.relative_focal_length
+    r.focal_length[0], r.focal_length[1] = rf[0] * res_axis * zoom, rf[1] * res_axis * zoom
+    sc = tb.screen_center
+    r.screen_center[0], r.screen_center[1] = (0.5 - sc[0]) * zoom + 0.5, (0.5 - sc[1]) * zoom + 0.5
+    r.near_distance = float(tb.render_near_distance)
+    bb = tb.aabb
+    for k in range(3):
+        r.aabb_min[k] = r.train_aabb_min[k] = bb.min[k]
+        r.aabb_max[k] = r.train_aabb_max[k] = bb.max[k]
+    r.cone_angle_constant = float(tb.nerf.cone_angle_constant)
+    r.max_cascade = int(tb.nerf.max_cascade)
+    r.min_transmittance = float(tb.nerf.render_min_transmittance)
+    r.snap_to_pixel_centers = int(tb.snap_to_pixel_centers)
+    r.use_inference_params = 1
+    r.train_in_linear_colors = int(tb.nerf.training.linear_colors)
+    r.shard_index, r.shard_count, r.shard_rows = shard
+    if tb.nerf.render_with_lens_distortion:
+        lens = tb.nerf.render_lens
+        r.lens_mode = int(lens.mode)
+        for k, v in enumerate(lens.params):
+            r.lens_params[k] = float(v)
+    return r
+
+
+def oracle_frame_rows(o, tb, W, H, blocks, rows=8):
+    """Render the 8-row blocks `blocks` of a W x H frame with the oracle; returns {row: rgba}."""
+    out = {}
+    for b in blocks:
+        fr, _ = o.render(testbed_render_args(tb, W, H, shard=(b, H // rows, rows)))
+        for y in range(b * rows, min(H, (b + 1) * rows)):
+            out[y] = fr[y]
+    return out

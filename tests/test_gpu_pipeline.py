@@ -111,18 +111,22 @@ def test_train_step_matches_oracle(cfg_kw):
         o_out = o.scratch(A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][evaluated].astype(np.float32)
         assert np.abs(g_out - o_out).mean() < 2e-3
 
-        assert (g_cp[:, 0] == o_cp[:, 0]).mean() > 0.98
-        same = np.all(g_cp == o_cp) and gst.measured_batch_size == ost.measured_batch_size
+        # compaction: the stop index depends on fp16 network outputs, so a ray may keep one sample
+        # more or less than the oracle; dL/dout is compared on every ray whose (count, base) match
+        match = np.all(g_cp == o_cp, axis=1) & (o_cp[:, 0] > 0)
+        assert match.mean() > 0.9 * (o_cp[:, 0] > 0).mean()
         np.testing.assert_allclose(gst.loss, ost.loss, rtol=2e-2)
-        if same:
-            C_ = min(ost.measured_batch_size, B)
-            g_dl = gpu_scratch(g, A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[:C_].astype(np.float32)
-            o_dl = o.scratch(A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[:C_].astype(np.float32)
-            assert np.linalg.norm(g_dl - o_dl) / np.linalg.norm(o_dl) < 2e-2
-            gg, og = g.grads(), o.get(A.GRADS_FP32)
-            for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
-                rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
-                assert rel < 5e-2, rel
+        assert gst.forward_early_stop_violations == 0
+        rows = np.concatenate([np.arange(b, b + n) for n, b in o_cp[match] if b + n <= B])
+        assert rows.size > 500
+        g_dl = gpu_scratch(g, A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[rows].astype(np.float32)
+        o_dl = o.scratch(A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[rows].astype(np.float32)
+        assert np.linalg.norm(g_dl - o_dl) / np.linalg.norm(o_dl) < 2e-2
+        # weight gradients over the whole batch (a mismatching ray changes them by one sample)
+        gg, og = g.grads(), o.get(A.GRADS_FP32)
+        for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
+            rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
+            assert rel < 5e-2, rel
     finally:
         g.close()
 
@@ -229,9 +233,13 @@ def test_density_grid_update_matches_oracle():
         g.close()
 
 
-@pytest.mark.parametrize("spp,snap,shard", [(0, 1, (0, 1, 8)), (3, 0, (1, 2, 8))])
-def test_render_matches_oracle(spp, snap, shard):
-    g, o, rng = pair(CFG_A, grid_scale=1.0)
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
+@pytest.mark.parametrize("spp,snap,shard", [(0, 1, (0, 1, 8)), (1, 0, (0, 1, 8)), (3, 0, (1, 2, 8))])
+def test_render_matches_oracle(spp, snap, shard, cfg_kw):
+    """NerfTracer::trace (src/testbed_nerf.cu:1639-1761) incl. the render network instance: config A
+    (L4, 16-wide) and config B (L16F2T19, 64-wide density + rgb MLPs: the SH-row MLP instance and the
+    render-site encoder that produce the headline number)."""
+    g, o, rng = pair(cfg_kw, grid_scale=1.0)
     try:
         set_bitfield_both(g, o, sphere_bitfield(0.3))
         W, H = 40, 32
@@ -253,12 +261,13 @@ def test_render_matches_oracle(spp, snap, shard):
         g.close()
 
 
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
 @pytest.mark.parametrize("aabb_scale", [1, 4])
-def test_render_floaters_matches_oracle(aabb_scale):
+def test_render_floaters_matches_oracle(aabb_scale, cfg_kw):
     """Sparse random occupancy (floaters) over several cascades: the render's empty-space
     jumps (octant distance fields) must land on exactly the lattice points the oracle's
     point-by-point march samples."""
-    g, o, rng = pair(CFG_A, grid_scale=1.0)
+    g, o, rng = pair(cfg_kw, grid_scale=1.0)
     try:
         max_cascade = max(0, int(np.log2(aabb_scale)))
         nc = max_cascade + 1
@@ -481,5 +490,61 @@ def test_train_step_cam_gradient_matches_oracle(cfg_kw):
             gg = gd.cpu().numpy()
             assert np.abs(oh).sum() > 0
             assert np.linalg.norm(gg - oh) / np.linalg.norm(oh) < 5e-2, (gg, oh)
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("spp,color_space,srgb", [(0, 0, 0), (2, 0, 1), (1, 1, 0)])
+def test_accumulate_tonemap_matches_oracle(spp, color_space, srgb):
+    """accumulate_kernel + tonemap_kernel (src/render_buffer.cu:232-266, 533-565): running spp mean,
+    background blend, colour-space conversion and exposure against the oracle's restatement."""
+    from oracle_abi import load, ptr
+    rng = np.random.default_rng(5 + spp)
+    W, H = 37, 23
+    frame = rng.uniform(0, 1, (H, W, 4)).astype(np.float32)
+    frame[..., :3] *= frame[..., 3:4]
+    accum0 = rng.uniform(0, 1, (H, W, 4)).astype(np.float32)
+    bg = np.array([0.2, 0.4, 0.9, 0.7], np.float32)
+    exposure = 0.35
+    d_frame, d_acc = torch.from_numpy(frame).cuda(), torch.from_numpy(accum0.copy()).cuda()
+    d_out = torch.zeros_like(d_frame)
+    lib = A.load()
+    A.check(lib.ngp_accumulate_tonemap(C.c_void_p(d_frame.data_ptr()), C.c_void_p(d_acc.data_ptr()),
+                                       C.c_void_p(d_out.data_ptr()), W, H, spp, color_space, exposure,
+                                       bg.ctypes.data_as(C.POINTER(C.c_float)), srgb, stream()))
+    torch.cuda.synchronize()
+    acc, out = accum0.copy(), np.zeros_like(frame)
+    load().oref_accumulate_tonemap(ptr(frame), ptr(acc), ptr(out), W, H, spp, color_space, exposure, ptr(bg), srgb)
+    np.testing.assert_allclose(d_acc.cpu().numpy(), acc, rtol=1e-5, atol=1e-6)
+    np.testing.assert_allclose(d_out.cpu().numpy(), out, rtol=1e-4, atol=1e-5)
+
+
+def test_train_step_ray_offset_is_a_slice_of_the_global_batch():
+    """Data-parallel ray split: rank r's step over rays [r R, (r+1) R) of the shared
+    pcg32 stream (ray_index_offset, n_rays_global) samples exactly what the single-GPU step over
+    2R rays samples for those rays -- counts, and coordinates bit for bit."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        dd = DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 256, 1 << 16, 1 << 16
+
+        def run(n_rays, offset, n_global):
+            a = train_args(dd.ptr, dd.n, n_rays, B, MS)
+            a.ray_index_offset, a.n_rays_global = offset, n_global
+            g.zero_grads()
+            A.check(g.lib.ngp_train_step(g.h, C.byref(a), stream()))
+            torch.cuda.synchronize()
+            ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2).copy()
+            co = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+            return ns, [co[b:b + n, :7].copy() for n, b in ns]
+
+        ns_full, c_full = run(2 * R, 0, 2 * R)
+        ns_hi, c_hi = run(R, R, 2 * R)
+        np.testing.assert_array_equal(ns_hi[:, 0], ns_full[R:, 0])
+        assert ns_hi[:, 0].sum() > 500
+        for a_, b_ in zip(c_hi, c_full[R:]):
+            np.testing.assert_array_equal(a_, b_)
     finally:
         g.close()
