@@ -38,6 +38,8 @@ def parse():
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--pretrain", type=int, default=1500, help="untimed training steps before warmup (grid converges)")
     p.add_argument("--config", default="lego_L16F2.json")
+    p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"),
+                   help="transforms.json of the scene to train on, or 'synthetic' for the procedural lego-shaped one")
     p.add_argument("--batch", type=int, default=1 << 18)
     p.add_argument("--views", type=int, default=100)
     p.add_argument("--train-res", type=int, default=800)
@@ -92,18 +94,27 @@ def model_bytes(name, per_unit, units, timers):
     return units * per_unit
 
 
-def make_dataset(ngp, tb, n_views, res, device):
+def make_dataset(ngp, tb, args, device):
+    """The bench scene: a transforms.json through the Testbed's loader (default: the reference's
+    data/nerf/test/dataset, SURVEY 8(d)'s stand-in for lego), or the procedural lego-shaped scene.
+    Returns (cams [3x4 NGP], RGBA8 images, focal) for the CPU oracle's sample."""
+    if args.scene != "synthetic":
+        tb.load_training_data(args.scene)
+        ds = tb.nerf.training.dataset
+        cams = [np.asarray(x, np.float32) for x in ds.transforms]
+        imgs = np.stack([ds.image(i) for i in range(ds.n_images)])
+        return cams, imgs, float(ds.metadata[0].focal_length[0])
     import synthetic
 
-    cams = synthetic.hemisphere_cameras(n_views, seed=0)
-    focal = synthetic.focal_from_angle(res)
-    imgs = synthetic.render_views(cams, res, res, focal, device=device)
-    tb.create_empty_nerf_dataset(n_views, aabb_scale=1)
-    for i in range(n_views):
+    cams = synthetic.hemisphere_cameras(args.views, seed=0)
+    focal = synthetic.focal_from_angle(args.train_res)
+    imgs = synthetic.render_views(cams, args.train_res, args.train_res, focal, device=device)
+    tb.create_empty_nerf_dataset(args.views, aabb_scale=1)
+    for i in range(args.views):
         tb.nerf.training.set_image_rgba8(i, imgs[i])
         tb.nerf.training.set_camera_extrinsics(i, cams[i], convert_to_ngp=False)
         tb.nerf.training.set_camera_intrinsics(i, fx=focal, fy=focal)
-    tb.nerf.training.n_images_for_training = n_views  # as the reference's create_empty_nerf_dataset callers do
+    tb.nerf.training.n_images_for_training = args.views  # as the reference's create_empty_nerf_dataset callers do
     return cams, imgs, focal
 
 
@@ -218,7 +229,8 @@ def main():
     import pyngp as ngp
 
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
-    cams, imgs, focal = make_dataset(ngp, tb, args.views, args.train_res, f"cuda:{local_rank}")
+    cams, imgs, focal = make_dataset(ngp, tb, args, f"cuda:{local_rank}")
+    n_views = len(cams)
     tb.reload_network_from_file(args.config)
     if world > 1:
         uid = [ngp.Testbed.nccl_unique_id() if rank == 0 else None]
@@ -240,7 +252,7 @@ def main():
             print(f"# pretrain {i + 1}/{args.pretrain} loss {tb.loss:.5f} "
                   f"rays/batch {tb.last_train_stats()['rays_per_batch']} ({time.perf_counter() - t_pre:.1f}s)",
                   file=sys.stderr, flush=True)
-    view = (rank * 7 + 3) % args.views
+    view = (rank * 7 + 3) % n_views
 
     split = {"train_s": 0.0, "render_s": 0.0, "train_rays": 0, "render_rays": 0}
 
@@ -305,7 +317,7 @@ def main():
     # 8-row blocks and gathered to rank 0 over RCCL -- strong scaling of inference
     config_c = None
     if world > 1:
-        tb.set_camera_to_training_view(3 % args.views)
+        tb.set_camera_to_training_view(3 % n_views)
         for _ in range(2):
             tb.render_distributed(W, H, 1, True, False)
         barrier()
@@ -378,8 +390,11 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "f16-mfma/f32-accum",
-            "data": f"synthetic lego-shaped scene ({args.views} views {args.train_res}x{args.train_res} RGBA8, "
-                    f"random-init weights trained {args.pretrain} steps before timing)",
+            "data": (f"real scene {os.path.relpath(args.scene, ROOT)} ({n_views} views {imgs.shape[2]}x{imgs.shape[1]} "
+                     f"RGBA8; the reference's data/nerf/test/dataset, nerf_synthetic/lego is not available offline)"
+                     if args.scene != "synthetic" else
+                     f"synthetic lego-shaped scene ({n_views} views {args.train_res}x{args.train_res} RGBA8)")
+                    + f", random-init weights trained {args.pretrain} steps before timing",
             "config": {"workload": "lego L16F2T19 MLP 64 (1x density + 2x rgb hidden): Testbed.train(2^18) "
                                    f"+ {W}x{H} spp1 render per step", "batch": args.batch, "config_file": args.config,
                        "parallelism": f"dp{world} (RCCL grad all-reduce) + per-rank 1080p view"},

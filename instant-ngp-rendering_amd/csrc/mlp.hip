@@ -1006,6 +1006,9 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		else if (sh && a.F == 2 && pl && tile == 13) launch_timed(k_mlp_infer_rf<N, 1, 3, false, 12, true>, grid, BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl && tile == 11) launch_timed(k_mlp_infer_rf<N, 1, 1, false, 12, true>, grid, BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);
+		else if (sh && a.F == 4 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 14, true>, grid, BLOCK, lds, s, a);
+		// element-wise loads read K in natural order: only valid where k_pack did not permute the
+		// first layer to the plane order (plane_f == 0)
 		else if (sh) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 0, true>, grid, BLOCK, lds, s, a);
 		else if (a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12>, grid, BLOCK, lds, s, a);
 		else if (a.F == 4 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 14>, grid, BLOCK, lds, s, a);

@@ -211,7 +211,21 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readonly("scale", &NerfDataset::scale)
 		.def_readonly("aabb_scale", &NerfDataset::aabb_scale)
 		.def_readonly("from_mitsuba", &NerfDataset::from_mitsuba)
-		.def_readonly("is_hdr", &NerfDataset::is_hdr);
+		.def_readonly("is_hdr", &NerfDataset::is_hdr)
+		.def("image", [](const NerfDataset& d, size_t i) {
+			if (i >= d.n_images) throw std::runtime_error("Invalid frame index");
+			const auto& md = d.metadata[i];
+			py::array_t<uint8_t> a({md.resolution[1], md.resolution[0], 4});
+			if (d.pixels[i].size() != (size_t)md.resolution[0] * md.resolution[1] * 4) throw std::runtime_error("image has no pixels");
+			std::memcpy(a.mutable_data(), d.pixels[i].data(), d.pixels[i].size());
+			return a;
+		}, "RGBA8 (sRGB, straight alpha) pixels of image i, as stored for training");
+
+	// ngp::load_nerf without a Testbed (no GPU needed): the dataset front end on its own
+	m.def("load_nerf_dataset", [](const std::string& path) {
+		py::gil_scoped_release rel;
+		return load_nerf(path, &pil_decode);
+	}, py::arg("path"));
 
 	py::class_<Testbed> testbed(m, "Testbed");
 

@@ -236,34 +236,11 @@ void Testbed::load_file(const std::string& path) {
 	load_training_data(path);
 }
 
-void Testbed::load_training_data(const std::string& path) {
+// ngp::load_nerf (src/nerf_loader.cu:273-743) on the host: every transforms json of `path` (a
+// file, or all *.json of a directory), frames naturally sorted, sharpness-filtered, decoded to
+// RGBA8 and converted to NGP space.  No device work (the Testbed uploads on first use).
+NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder) {
 	if (!file_exists(path)) throw std::runtime_error("Data path '" + path + "' does not exist.");
-	// mode_from_scene (src/common_host.cu:146-164)
-	ETestbedMode scene_mode = ETestbedMode::None;
-	const std::string ext = extension(path);
-	if (is_directory(path) || ext == "json") scene_mode = ETestbedMode::Nerf;
-	if (path.find("geometry") != std::string::npos) scene_mode = ETestbedMode::Geometry;
-	if (ext == "obj" || ext == "stl") scene_mode = ETestbedMode::Sdf;
-	if (ext == "nvdb") scene_mode = ETestbedMode::Volume;
-	if (ext == "exr" || ext == "bin" || ext == "png" || ext == "jpg") scene_mode = ETestbedMode::Image;
-	if (scene_mode == ETestbedMode::None) throw std::runtime_error("Unknown scene format for path '" + path + "'.");
-	if (scene_mode != ETestbedMode::Nerf)
-		throw std::runtime_error("This build implements the NeRF primitive only (SDF/Image/Volume/Geometry are out of scope).");
-	if (mode != ETestbedMode::Nerf) {
-		// Testbed::set_mode (src/testbed.cu:165-218): drop mode-specific state and the network
-		if (m_model) {
-			sync();
-			ngp_model_destroy(m_model);
-			m_model = nullptr;
-		}
-		nerf = Nerf{};
-		free_device_dataset();
-		training_data_available = false;
-		mode = ETestbedMode::Nerf;
-		reset_camera();
-	}
-	data_path = path;
-
 	std::vector<std::string> json_paths;
 	if (is_directory(path)) {
 		DIR* d = opendir(path.c_str());
@@ -281,7 +258,6 @@ void Testbed::load_training_data(const std::string& path) {
 	if (json_paths.empty()) throw std::runtime_error("Cannot load NeRF data from an empty set of paths.");
 
 	// ngp::load_nerf (src/nerf_loader.cu:273-743)
-	const int prev_aabb_scale = nerf.training.dataset.aabb_scale;
 	NerfDataset ds;
 	ds.scale = 0.33f;
 	ds.offset = {0.5f, 0.5f, 0.5f};
@@ -310,6 +286,30 @@ void Testbed::load_training_data(const std::string& path) {
 			return natural_sort_key(a.value("file_path", std::string())) < natural_sort_key(b.value("file_path", std::string()));
 		});
 		if (j.contains("n_frames")) frames.resize(std::min(frames.size(), (size_t)j["n_frames"].num()));
+		for (Json& fr : frames)
+			if (fr.contains("file_path")) {
+				std::string fp = fr["file_path"].str();
+				std::replace(fp.begin(), fp.end(), '\\', '/');
+				fr["file_path"] = Json(fp);
+			}
+		// frames with a sharpness record (src/nerf_loader.cu:364-387): keep a frame if its image file
+		// exists and it is sharper than sharpness_discard_threshold x the mean of its neighbours
+		// [i-3, i+3) (the reference's window, including its 0/0 for a single frame)
+		if (!frames.empty() && frames[0].contains("sharpness")) {
+			const float thr = (float)j.value("sharpness_discard_threshold", 0.0);
+			const int n = (int)frames.size();
+			std::vector<Json> kept;
+			for (int i = 0; i < n; ++i) {
+				float mean = 0.0f;
+				const int a = std::max(0, i - 3), b = std::min(i + 3, n - 1);
+				for (int k = a; k < b; ++k) mean += (float)frames[k].value("sharpness", 1.0);
+				mean /= (float)(b - a);
+				const std::string fp = frames[i].value("file_path", std::string());
+				const std::string p = (!fp.empty() && fp[0] == '/') ? fp : base + "/" + fp;
+				if (file_exists(p) && (float)frames[i].value("sharpness", 1.0) > thr * mean) kept.push_back(frames[i]);
+			}
+			frames.swap(kept);
+		}
 		// read_lens / principal point (src/nerf_loader.cu:175-220)
 		auto read_lens = [](const Json& src, Lens& lens, vec2& pp) {
 			const ELensMode opencv = src.value("is_fisheye", false) ? ELensMode::OpenCVFisheye : ELensMode::OpenCV;
@@ -323,6 +323,13 @@ void Testbed::load_training_data(const std::string& path) {
 			par("k1", 0); par("k2", 1); par("k3", 2); par("k4", 3); par("p1", 2); par("p2", 3);
 			if (src.contains("cx")) pp[0] = (float)src["cx"].num() / (float)src["w"].num();
 			if (src.contains("cy")) pp[1] = (float)src["cy"].num() / (float)src["h"].num();
+			if (src.contains("ftheta_p0")) {
+				const char* names[5] = {"ftheta_p0", "ftheta_p1", "ftheta_p2", "ftheta_p3", "ftheta_p4"};
+				for (int q = 0; q < 5; ++q) lens.params[q] = (float)src[names[q]].num();
+				lens.params[5] = (float)src["w"].num();
+				lens.params[6] = (float)src["h"].num();
+				mode_l = ELensMode::FTheta;
+			}
 			if (src.contains("latlong")) mode_l = ELensMode::LatLong;
 			if (src.contains("equirectangular")) mode_l = ELensMode::Equirectangular;
 			if (mode_l != ELensMode::Perspective) lens.mode = mode_l;
@@ -378,6 +385,39 @@ void Testbed::load_training_data(const std::string& path) {
 	}
 	ds.n_images = ds.metadata.size();
 	if (ds.n_images == 0) throw std::invalid_argument("No training images were found for NeRF training!");
+	return ds;
+}
+
+void Testbed::load_training_data(const std::string& path) {
+	if (!file_exists(path)) throw std::runtime_error("Data path '" + path + "' does not exist.");
+	// mode_from_scene (src/common_host.cu:146-164)
+	ETestbedMode scene_mode = ETestbedMode::None;
+	const std::string ext = extension(path);
+	if (is_directory(path) || ext == "json") scene_mode = ETestbedMode::Nerf;
+	if (path.find("geometry") != std::string::npos) scene_mode = ETestbedMode::Geometry;
+	if (ext == "obj" || ext == "stl") scene_mode = ETestbedMode::Sdf;
+	if (ext == "nvdb") scene_mode = ETestbedMode::Volume;
+	if (ext == "exr" || ext == "bin" || ext == "png" || ext == "jpg") scene_mode = ETestbedMode::Image;
+	if (scene_mode == ETestbedMode::None) throw std::runtime_error("Unknown scene format for path '" + path + "'.");
+	if (scene_mode != ETestbedMode::Nerf)
+		throw std::runtime_error("This build implements the NeRF primitive only (SDF/Image/Volume/Geometry are out of scope).");
+	if (mode != ETestbedMode::Nerf) {
+		// Testbed::set_mode (src/testbed.cu:165-218): drop mode-specific state and the network
+		if (m_model) {
+			sync();
+			ngp_model_destroy(m_model);
+			m_model = nullptr;
+		}
+		nerf = Nerf{};
+		free_device_dataset();
+		training_data_available = false;
+		mode = ETestbedMode::Nerf;
+		reset_camera();
+	}
+	data_path = path;
+
+	const int prev_aabb_scale = nerf.training.dataset.aabb_scale;
+	NerfDataset ds = load_nerf(path, image_decoder);
 	nerf.training.dataset = std::move(ds);
 	if (nerf.training.dataset.aabb_scale != prev_aabb_scale && m_model) reset_network();
 	load_nerf_post();
@@ -1213,9 +1253,11 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 			for (int k = 0; k < 3; ++k) bg[k] = srgb_to_linear_h(bg[k]);
 		for (int y = 0; y < height; ++y)
 			for (int x = 0; x < width; ++x) {
+				// the reference overlays the image about the frame centre, vec2(0.5) -- not the camera's
+				// screen centre (src/testbed.cu:4597-4608, render_buffer.cu:373-380)
 				float fx = x + 0.5f, fy = y + 0.5f;
-				fx -= width * 0.5f; fx /= zoom; fx += screen_center[0] * width;
-				fy -= height * 0.5f; fy /= zoom; fy += screen_center[1] * height;
+				fx -= width * 0.5f; fx /= zoom; fx += 0.5f * width;
+				fy -= height * 0.5f; fy /= zoom; fy += 0.5f * height;
 				const float u = (fx - width * 0.5f) * sca + iw * 0.5f, vv = (fy - height * 0.5f) * sca + ih * 0.5f;
 				const int sx = (int)std::floor(u), sy = (int)std::floor(vv);
 				float c[4] = {0, 0, 0, 0};
@@ -1233,9 +1275,10 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 				c[3] += w;
 				if (color_space == EColorSpace::SRGB)
 					for (int k = 0; k < 3; ++k) c[k] = srgb_to_linear_h(c[k]);
-				const float e = std::pow(2.0f, exposure);
 				for (int k = 0; k < 3; ++k) {
-					c[k] *= e;
+					// exposure + the view's optimised exposure (src/testbed.cu:4599)
+					const float ev = (size_t)v < nerf.training.cam_exposure.size() ? nerf.training.cam_exposure[v].variable[k] : 0.0f;
+					c[k] *= std::pow(2.0f, exposure + ev);
 					if (!linear) c[k] = linear_to_srgb_h(c[k]);
 				}
 				std::memcpy(&out[((size_t)y * width + x) * 4], c, sizeof(c));

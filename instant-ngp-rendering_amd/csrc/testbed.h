@@ -303,5 +303,8 @@ private:
 };
 
 std::string natural_sort_key(const std::string& s);
+// non-PNG images (JPG, ...): decoder(path, rgba8_out, width, height) -> success
+using ImageDecoder = std::function<bool(const std::string&, std::vector<uint8_t>&, int&, int&)>;
+NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder = nullptr);
 
 }  // namespace ngp

@@ -61,6 +61,7 @@ def set_bitfield_both(g, o, grid, max_cascade=0):
 
 CFG_A = dict(n_levels=4, F=2, log2_T=14, n_neurons=16)
 CFG_B = dict(n_levels=16, F=2, log2_T=19, n_neurons=64)
+CFG_F4 = dict(n_levels=8, F=4, log2_T=19, n_neurons=64)  # the fork's configs/nerf/base.json (L8 F4)
 
 
 @pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
@@ -233,7 +234,7 @@ def test_density_grid_update_matches_oracle():
         g.close()
 
 
-@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B, CFG_F4], ids=["A", "B", "F4"])
 @pytest.mark.parametrize("spp,snap,shard", [(0, 1, (0, 1, 8)), (1, 0, (0, 1, 8)), (3, 0, (1, 2, 8))])
 def test_render_matches_oracle(spp, snap, shard, cfg_kw):
     """NerfTracer::trace (src/testbed_nerf.cu:1639-1761) incl. the render network instance: config A
@@ -261,7 +262,7 @@ def test_render_matches_oracle(spp, snap, shard, cfg_kw):
         g.close()
 
 
-@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B, CFG_F4], ids=["A", "B", "F4"])
 @pytest.mark.parametrize("aabb_scale", [1, 4])
 def test_render_floaters_matches_oracle(aabb_scale, cfg_kw):
     """Sparse random occupancy (floaters) over several cascades: the render's empty-space

@@ -46,6 +46,14 @@ def test_load_training_data_matches_scene(scene):
     a = imgs[5][..., 3:4] / 255.0
     expect = imgs[5][..., :3] / 255.0 * a
     assert np.abs(gt[..., :3] - expect).max() < 2.0 / 255.0
+    # an off-centre principal point moves the rendered rays (screen centre = 1 - pp) but not the
+    # ground-truth overlay, which the reference draws about the frame centre (src/testbed.cu:4597-4608)
+    f = S.focal_from_angle(64)
+    tb.nerf.training.set_camera_intrinsics(5, fx=f, fy=f, cx=41.0, cy=27.0)
+    tb.set_camera_to_training_view(5)
+    np.testing.assert_allclose(tb.screen_center, [1 - 41.0 / 64, 1 - 27.0 / 64], rtol=1e-6)
+    gt2 = tb.render(64, 64, 1, False)
+    np.testing.assert_array_equal(gt2, gt)
 
 
 def test_train_render_snapshot(scene, tmp_path):
@@ -126,7 +134,8 @@ def test_train_render_snapshot(scene, tmp_path):
     assert np.isfinite(tb4.loss) and tb4.loss < 2 * np.mean(losses[-4:])
 
 
-def test_render_1080p_rows_match_oracle(scene):
+@pytest.mark.parametrize("config", ["lego_L16F2.json", "base.json"])
+def test_render_1080p_rows_match_oracle(scene, config):
     """north_star parity at the lego config: a network of BASELINE config B (L16 F2 T2^19, 64-wide
     density + rgb MLPs) trained on a scene through the Testbed renders a full 1920x1080 frame; the
     oracle renders three 8-row blocks of it with the same EMA inference weights and density grid.
@@ -135,7 +144,7 @@ def test_render_1080p_rows_match_oracle(scene):
     root, cams, imgs = scene
     ngp, tb = new_testbed()
     tb.load_training_data(os.path.join(root, "transforms_train.json"))
-    tb.reload_network_from_file("lego_L16F2.json")
+    tb.reload_network_from_file(config)
     tb.shall_train = True
     while tb.training_step < 200:
         tb.frame()

@@ -1,0 +1,101 @@
+"""The NeRF dataset front end (ngp::load_nerf, src/nerf_loader.cu:273-743) on the reference's own
+datasets, on the CPU (pyngp.load_nerf_dataset needs no GPU):
+
+* data/nerf/fox -- the reference's transforms.json verbatim: JPG frames, OpenCV lens (k1, k2, p1,
+  p2), per-axis focal lengths, principal point cx/w, cy/h, aabb_scale 4, and 17 listed frames
+  whose files are absent (skipped by the sharpness/exists filter, nerf_loader.cu:364-387);
+* data/nerf/test/dataset -- the reference's BlenderNeRF scene (half resolution, see
+  tools/make_real_data.py), aabb_scale 1, opaque RGBA.
+
+Transforms are checked against an independent numpy restatement of nerf_matrix_to_ngp
+(nerf_loader.h:100-120); focal lengths, lens parameters and the frame set against the json.
+"""
+import json
+import os
+import re
+
+import numpy as np
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FOX = os.path.join(ROOT, "data", "nerf", "fox")
+TEST = os.path.join(ROOT, "data", "nerf", "test", "dataset")
+
+
+def natural_key(s):
+    return [int(t) if t.isdigit() else t for t in re.split(r"(\d+)", s)]
+
+
+def nerf_to_ngp(m, scale=0.33, offset=(0.5, 0.5, 0.5)):
+    x = np.asarray(m, np.float64)[:3, :4].copy()
+    x[:, 1] *= -1
+    x[:, 2] *= -1
+    x[:, 3] = x[:, 3] * scale + np.asarray(offset)
+    return x[[1, 2, 0], :]  # cycle axes xyz <- yzx
+
+
+@pytest.fixture(scope="module")
+def ngp():
+    import pyngp
+    return pyngp
+
+
+def test_fox_transforms_opencv_lens_and_missing_frames(ngp):
+    meta = json.load(open(os.path.join(FOX, "transforms.json")))
+    frames = sorted(meta["frames"], key=lambda f: natural_key(f["file_path"]))
+    present = [f for f in frames if os.path.exists(os.path.join(FOX, f["file_path"]))]
+    assert len(frames) == 67 and len(present) == 50
+    d = ngp.load_nerf_dataset(os.path.join(FOX, "transforms.json"))
+    assert d.n_images == 50 and d.aabb_scale == 4
+    assert list(d.paths) == [f["file_path"] for f in present]
+    for i, f in enumerate(present):
+        np.testing.assert_allclose(d.transforms[i], nerf_to_ngp(f["transform_matrix"]), atol=2e-6)
+    md = d.metadata[0]
+    assert list(md.resolution) == [1080, 1920]
+    np.testing.assert_allclose(md.focal_length, [meta["fl_x"], meta["fl_y"]], rtol=1e-6)
+    np.testing.assert_allclose(md.principal_point, [meta["cx"] / meta["w"], meta["cy"] / meta["h"]], rtol=1e-6)
+    assert md.lens.mode == ngp.LensMode.OpenCV
+    np.testing.assert_allclose(md.lens.params[:4], [meta["k1"], meta["k2"], meta["p1"], meta["p2"]], rtol=1e-6)
+    # JPG decode (PIL through the Testbed's decoder hook; stb_image in the reference)
+    from PIL import Image
+    img = d.image(0)
+    ref = np.asarray(Image.open(os.path.join(FOX, present[0]["file_path"])).convert("RGBA"))
+    np.testing.assert_array_equal(img, ref)
+
+
+def test_test_dataset_split_and_intrinsics(ngp):
+    d = ngp.load_nerf_dataset(os.path.join(TEST, "transforms_train.json"))
+    t = ngp.load_nerf_dataset(os.path.join(TEST, "transforms_test.json"))
+    assert d.n_images == 45 and t.n_images == 5 and d.aabb_scale == 1
+    assert not set(d.paths) & set(t.paths)
+    meta = json.load(open(os.path.join(TEST, "transforms_train.json")))
+    md = d.metadata[3]
+    assert list(md.resolution) == [360, 640]
+    np.testing.assert_allclose(md.focal_length, [meta["fl_x"], meta["fl_y"]], rtol=1e-6)
+    np.testing.assert_allclose(md.principal_point, [0.5, 0.5], rtol=1e-6)
+    assert md.lens.mode == ngp.LensMode.Perspective
+    frames = sorted(meta["frames"], key=lambda f: natural_key(f["file_path"]))
+    for i in (0, 17, 44):
+        np.testing.assert_allclose(d.transforms[i], nerf_to_ngp(frames[i]["transform_matrix"]), atol=2e-6)
+    img = d.image(0)
+    assert img.shape == (640, 360, 4) and img[..., 3].min() == 255
+
+
+def test_directory_merges_every_json(ngp):
+    """A scene directory loads every *.json in it (src/testbed_nerf.cu:2243-2248)."""
+    d = ngp.load_nerf_dataset(TEST)
+    assert d.n_images == 45 + 5 + 50  # transforms_all + transforms_test + transforms_train
+
+
+def test_missing_files_and_empty_sets_raise(ngp, tmp_path):
+    with pytest.raises(RuntimeError, match="does not exist"):
+        ngp.load_nerf_dataset(str(tmp_path / "nope.json"))
+    (tmp_path / "t.json").write_text(json.dumps({"camera_angle_x": 0.7, "frames": [
+        {"file_path": "missing.png", "transform_matrix": np.eye(4).tolist()}]}))
+    with pytest.raises(RuntimeError, match="Could not find image file"):
+        ngp.load_nerf_dataset(str(tmp_path / "t.json"))
+    # with a sharpness record, frames whose files are absent are dropped instead
+    (tmp_path / "s.json").write_text(json.dumps({"camera_angle_x": 0.7, "frames": [
+        {"file_path": "missing.png", "sharpness": 3.0, "transform_matrix": np.eye(4).tolist()}]}))
+    with pytest.raises((RuntimeError, ValueError), match="No training images"):
+        ngp.load_nerf_dataset(str(tmp_path / "s.json"))

@@ -1,0 +1,61 @@
+"""Builds data/nerf/{test,fox} from the reference checkout's own datasets (run in the build
+container, where /root/reference exists; the outputs are committed and travel to the GPU box).
+
+* data/nerf/test/dataset: the reference's BlenderNeRF scene (data/nerf/test/dataset, 50 RGBA
+  720x1280 frames, alpha 255 everywhere, aabb_scale 1) at half resolution (360x640, Lanczos),
+  stored as RGB PNG (lossless for an opaque image), intrinsics (fl_x/fl_y/cx/cy/w/h) halved.
+  Split for the quality protocol: every 10th frame (0005, 0015, ...) -> transforms_test.json,
+  the other 45 -> transforms_train.json.
+* data/nerf/fox: the reference's transforms.json verbatim and its 50 JPG frames as shipped (17
+  listed frames are absent from the reference checkout; the loader skips them exactly as
+  nerf_loader.cu:364-387 does for files that do not exist).
+"""
+import json
+import os
+import shutil
+import sys
+
+from PIL import Image
+
+REF = "/root/reference/data/nerf"
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+OUT = os.path.join(ROOT, "data", "nerf")
+
+
+def make_test():
+    src = os.path.join(REF, "test", "dataset")
+    dst = os.path.join(OUT, "test", "dataset")
+    os.makedirs(os.path.join(dst, "train"), exist_ok=True)
+    meta = json.load(open(os.path.join(src, "transforms_train.json")))
+    for k in ("fl_x", "fl_y", "cx", "cy", "w", "h"):
+        meta[k] = meta[k] * 0.5
+    frames = sorted(meta["frames"], key=lambda f: f["file_path"])
+    for fr in frames:
+        name = os.path.basename(fr["file_path"])
+        im = Image.open(os.path.join(src, fr["file_path"]))
+        w, h = im.size
+        im = im.resize((w // 2, h // 2), Image.LANCZOS).convert("RGB")
+        im.save(os.path.join(dst, "train", name), "PNG", optimize=True)
+    test = [f for i, f in enumerate(frames) if i % 10 == 4]
+    train = [f for i, f in enumerate(frames) if i % 10 != 4]
+    for name, fr in (("transforms_train.json", train), ("transforms_test.json", test), ("transforms_all.json", frames)):
+        m = dict(meta)
+        m["frames"] = fr
+        json.dump(m, open(os.path.join(dst, name), "w"), indent=1)
+    shutil.copy(os.path.join(src, "log.txt"), os.path.join(dst, "log.txt"))
+
+
+def make_fox():
+    src = os.path.join(REF, "fox")
+    dst = os.path.join(OUT, "fox")
+    os.makedirs(os.path.join(dst, "images"), exist_ok=True)
+    shutil.copy(os.path.join(src, "transforms.json"), os.path.join(dst, "transforms.json"))
+    for name in sorted(os.listdir(os.path.join(src, "images"))):
+        shutil.copy(os.path.join(src, "images", name), os.path.join(dst, "images", name))
+
+
+if __name__ == "__main__":
+    if not os.path.isdir(REF):
+        sys.exit("the reference checkout is not here (build container only)")
+    make_test()
+    make_fox()

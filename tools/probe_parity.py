@@ -15,7 +15,8 @@ from scene_util import oracle_frame_rows, testbed_oracle  # noqa: E402
 
 torch.cuda.set_device(0)
 tb = ngp.Testbed(ngp.TestbedMode.Nerf)
-cams, imgs, focal = bench.make_dataset(ngp, tb, 100, 800, "cuda:0")
+import argparse
+cams, imgs, focal = bench.make_dataset(ngp, tb, argparse.Namespace(scene="synthetic", views=100, train_res=800), "cuda:0")
 tb.reload_network_from_file("lego_L16F2.json")
 tb.shall_train = True
 W, H = 1920, 1080
