@@ -217,25 +217,65 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 }
 
 // Lattice point k of a training ray: inside the AABB? a sample (occupied at mip_from_dt)?
+// If it is inside but empty, the reference leaves the cell: advance_to_next_voxel at that
+// mip (nerf_device.cuh:444-453) -> `jump` lattice steps (>= 1) to the first point past
+// the cell's far face.
 struct LatticePoint {
 	bool inside, occupied;
 	float t, dt;
 	v3 pos;
+	uint32_t jump;
 };
-__device__ __forceinline__ LatticePoint training_lattice_point(const SamplerArgs& a, v3 o, v3 d, float n0, uint32_t k) {
+__device__ __forceinline__ LatticePoint training_lattice_point(const SamplerArgs& a, v3 o, v3 d, v3 idir, float n0,
+                                                              uint32_t k) {
 	LatticePoint p;
 	const float n = n0 + (float)k;
 	p.t = step_from(a.st, n);
 	p.dt = step_from(a.st, n + 1.0f) - p.t;
 	p.pos = o + d * p.t;
 	p.inside = aabb_contains(a.aabb, p.pos);
-	p.occupied = p.inside && density_grid_occupied_at(p.pos, a.bitfield, mip_from_dt(p.dt, p.pos, a.max_mip));
+	const uint32_t mip = mip_from_dt(p.dt, p.pos, a.max_mip);
+	p.occupied = p.inside && density_grid_occupied_at(p.pos, a.bitfield, mip);
+	p.jump = 1;
+	if (p.inside && !p.occupied) {
+		const float n_far = step_to(a.st, p.t + distance_to_next_cell(p.pos, d, idir, mip));
+		p.jump = (uint32_t)fminf(ceilf(fmaxf(n_far - n, 0.5f)), 1048576.0f);
+	}
 	return p;
 }
 
-// generate_training_samples_nerf (testbed_nerf.cu:679-839), pass 1: one wave per ray,
-// 64 lattice points per iteration; the count stops at the first point outside the
-// AABB or at NERF_STEPS samples, like the reference's sequential loop.
+// generate_training_samples_nerf's walk (testbed_nerf.cu:779-795, 814-830) over 64 lattice
+// points of one ray at a time (one per lane): the reference's chain -- a sample at every
+// occupied point it visits, a jump past the cell of every empty one, stop at the first
+// visited point outside the AABB -- run as a scalar loop over the batch's ballots (one
+// iteration per run of samples or per jump).  Returns the batch's sample lanes; *cur = the
+// lattice offset (from this batch's first point) of the next point to visit; *exited once
+// the ray has left the AABB.
+__device__ __forceinline__ unsigned long long training_walk_batch(const LatticePoint& p, uint32_t lane, uint32_t* cur_io,
+                                                                  bool* exited) {
+	const unsigned long long occ = __ballot(p.occupied), in = __ballot(p.inside);
+	unsigned long long samp = 0;
+	uint32_t cur = *cur_io;
+	while (cur < 64u) {
+		if (!((in >> cur) & 1ull)) {
+			*exited = true;
+			break;
+		}
+		if ((occ >> cur) & 1ull) {
+			const unsigned long long rest = ~occ >> cur;  // run of occupied points from cur
+			const uint32_t run = rest ? (uint32_t)(__ffsll((long long)rest) - 1) : 64u - cur;
+			samp |= (run >= 64u ? ~0ull : ((1ull << run) - 1ull)) << cur;
+			cur += run;
+		} else {
+			cur += (uint32_t)__builtin_amdgcn_readlane((int)p.jump, (int)cur);
+		}
+	}
+	*cur_io = cur;
+	(void)lane;
+	return samp;
+}
+
+// pass 1: count the ray's samples (<= NERF_STEPS), one wave per ray.
 template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -245,17 +285,17 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	float n0;
 	uint32_t count = 0;
 	if (training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0)) {
-		for (uint32_t kb = 0;; kb += 64) {
-			const LatticePoint p = training_lattice_point(a, o, d, n0, kb + lane);
-			const unsigned long long out = __ballot(!p.inside);
-			const unsigned long long valid = out ? ((1ull << (__ffsll((long long)out) - 1)) - 1ull) : ~0ull;
-			const uint32_t c = __popcll(__ballot(p.occupied) & valid);
+		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		bool exited = false;
+		for (uint32_t kb = 0, cur = 0; !exited; kb += 64, cur -= 64) {
+			if (cur >= 64u) continue;  // a jump past this whole batch
+			const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + lane);
+			const uint32_t c = __popcll(training_walk_batch(p, lane, &cur, &exited));
 			if (count + c >= NERF_STEPS) {
 				count = NERF_STEPS;
 				break;
 			}
 			count += c;
-			if (out) break;
 		}
 	}
 	if (lane == 0) a.counts[i] = count;
@@ -287,13 +327,14 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 		rs[3] = d.x; rs[4] = d.y; rs[5] = d.z;
 	}
 	const v3 wdir = warp_direction(d);
+	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 	uint32_t j = 0;
-	for (uint32_t kb = 0; j < n; kb += 64) {
-		const LatticePoint p = training_lattice_point(a, o, d, n0, kb + lane);
-		const unsigned long long out = __ballot(!p.inside);
-		const unsigned long long valid = out ? ((1ull << (__ffsll((long long)out) - 1)) - 1ull) : ~0ull;
-		const unsigned long long m = __ballot(p.occupied) & valid;
+	bool exited = false;
+	for (uint32_t kb = 0, cur = 0; j < n && !exited; kb += 64, cur -= 64) {
+		if (cur >= 64u) continue;
+		const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + lane);
+		const unsigned long long m = training_walk_batch(p, lane, &cur, &exited);
 		if ((m >> lane) & 1ull) {
 			const uint32_t r = j + __popcll(m & below);
 			if (r < n) {
@@ -306,7 +347,6 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 			}
 		}
 		j += __popcll(m);
-		if (out) break;
 	}
 }
 

@@ -256,7 +256,7 @@ static float dist_next_cell(V3 pos, V3 d, V3 idir, uint32_t mip) {
 	const float tx = (std::floor(p.x + 0.5f + 0.5f * sgn(d.x)) - p.x) * idir.x;
 	const float ty = (std::floor(p.y + 0.5f + 0.5f * sgn(d.y)) - p.y) * idir.y;
 	const float tz = (std::floor(p.z + 0.5f + 0.5f * sgn(d.z)) - p.z) * idir.z;
-	return std::max(std::min(std::min(tx, ty), tz) * inv_res, 0.0f);
+	return std::fmax(std::fmin(std::fmin(tx, ty), tz) * inv_res, 0.0f);
 }
 static uint32_t mip_pos(V3 p, uint32_t maxc = CASCADES - 1) {
 	int e;
@@ -907,8 +907,11 @@ static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, P
 	return img;
 }
 
-// generate_training_samples_nerf (src/testbed_nerf.cu:679-838), per-ray.
-static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st) {
+// generate_training_samples_nerf (src/testbed_nerf.cu:679-838), per-ray: origin, direction,
+// first lattice point n0 = to_stepping_space(t_entry) + random; t_entry and the random offset
+// are returned too (the literal transcription below starts from them).
+static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st, float* t_entry = nullptr,
+                      float* jitter = nullptr) {
 	Pcg rng;
 	rng.state = a.rng_state;
 	rng.inc = a.rng_inc;
@@ -932,8 +935,69 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	float t0, t1;
 	b.intersect(*o, *d, &t0, &t1);
 	t0 = std::max(t0, 0.0f);
-	*st = lat_to(make_stepping(a.cone_angle_constant), t0) + rng.nextf();  // n0: first lattice point
+	const float r = rng.nextf();
+	*st = lat_to(make_stepping(a.cone_angle_constant), t0) + r;  // n0: first lattice point
+	if (t_entry) *t_entry = t0;
+	if (jitter) *jitter = r;
 	return true;
+}
+
+// The reference's sampling walk (testbed_nerf.cu:779-795) on the stepping lattice: at lattice
+// point n0 + k, a sample if the cell at mip_from_dt is occupied (next point k + 1), else
+// advance_to_next_voxel at that mip (nerf_device.cuh:444-453): jump to the first lattice point
+// past the cell's far face; stop at the first visited point outside the AABB or after `cap`
+// samples.  visit(j, k, t, dt, pos) for sample j.
+template <class Visit>
+static uint32_t training_walk(const Stepping& stp, const Box& box, const uint8_t* bits, uint32_t maxc, V3 o, V3 d, float n0,
+                              uint32_t cap, Visit visit) {
+	const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	uint32_t j = 0;
+	for (uint32_t k = 0; j < cap;) {
+		const float n = n0 + (float)k;
+		const float t = lat_from(stp, n), dt = lat_from(stp, n + 1.0f) - t;
+		const V3 pos = o + d * t;
+		if (!box.contains(pos)) break;
+		const uint32_t mip = mip_dt(dt, pos, maxc);
+		if (occupied(pos, bits, mip)) {
+			visit(j, k, t, dt, pos);
+			++j;
+			++k;
+		} else {
+			const float n_far = lat_to(stp, t + dist_next_cell(pos, d, idir, mip));
+			k += (uint32_t)std::fmin(std::ceil(std::fmax(n_far - n, 0.5f)), 1048576.0f);
+		}
+	}
+	return j;
+}
+
+// ---- literal transcription of the reference's stepping (nerf_device.cuh:378-453), for the
+// parity test of the lattice walk: chained t, no lattice, the reference's own divisions. ----
+static float ref_to_stepping_space(float t, float cone) {
+	if (cone <= 1e-5f) return t / MIN_STEP;
+	const float log1p_c = logf(1.0f + cone);
+	const float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c, b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
+	const float at = expf(a * log1p_c), bt = expf(b * log1p_c);
+	if (t <= at) return (t - at) / MIN_STEP + a;
+	if (t <= bt) return logf(t) / log1p_c;
+	return (t - bt) / MAX_STEP + b;
+}
+static float ref_from_stepping_space(float n, float cone) {
+	if (cone <= 1e-5f) return n * MIN_STEP;
+	const float log1p_c = logf(1.0f + cone);
+	const float a = (logf(MIN_STEP) - logf(log1p_c)) / log1p_c, b = (logf(MAX_STEP) - logf(log1p_c)) / log1p_c;
+	const float at = expf(a * log1p_c), bt = expf(b * log1p_c);
+	if (n <= a) return (n - a) * MIN_STEP + at;
+	if (n <= b) return expf(n * log1p_c);
+	return (n - b) * MAX_STEP + bt;
+}
+static float ref_advance_n_steps(float t, float cone, float n) {
+	return ref_from_stepping_space(ref_to_stepping_space(t, cone) + n, cone);
+}
+static float ref_calc_dt(float t, float cone) { return ref_advance_n_steps(t, cone, 1.0f) - t; }
+static float ref_advance_to_next_voxel(float t, float cone, V3 pos, V3 dir, V3 idir, uint32_t mip) {
+	const float t_target = t + dist_next_cell(pos, dir, idir, mip);
+	const float ts = ref_to_stepping_space(t, cone), tt = ref_to_stepping_space(t_target, cone);
+	return ref_from_stepping_space(ts + std::ceil(std::fmax(tt - ts, 0.5f)), cone);
 }
 
 static void train_step(Model& M, const ngp_train_args& a) {
@@ -941,15 +1005,6 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	const uint32_t nrg = a.n_rays_global ? a.n_rays_global : R;
 	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
 	const Stepping stp = make_stepping(a.cone_angle_constant);
-	// lattice point k of a ray: n0 + k (stepping space); a sample if inside the AABB and occupied
-	auto lattice = [&](V3 o, V3 d, float n0, uint32_t k, float* t, float* dt, V3* pos) {
-		const float n = n0 + (float)k;
-		*t = lat_from(stp, n);
-		*dt = lat_from(stp, n + 1.0f) - *t;
-		*pos = o + d * *t;
-		if (!box.contains(*pos)) return -1;
-		return occupied(*pos, M.bits.data(), mip_dt(*dt, *pos, a.max_cascade)) ? 1 : 0;
-	};
 	// pass 1: count (testbed_nerf.cu:779-799)
 	std::vector<uint32_t> cnt(R, 0);
 	std::vector<V3> ro(R), rd(R);
@@ -959,15 +1014,8 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		float t;
 		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t)) continue;
 		ro[i] = o; rd[i] = d; rst[i] = t;
-		uint32_t j = 0;
-		for (uint32_t k = 0; j < STEPS; ++k) {
-			float tt, dt;
-			V3 pos;
-			const int r = lattice(o, d, t, k, &tt, &dt, &pos);
-			if (r < 0) break;
-			j += (uint32_t)r;
-		}
-		cnt[i] = j;
+		cnt[i] = training_walk(stp, box, M.bits.data(), a.max_cascade, o, d, t, STEPS,
+		                       [](uint32_t, uint32_t, float, float, V3) {});
 	}
 	// prefix-sum slot claim in ray order; drop if base + n > cap (testbed_nerf.cu:800-803)
 	M.ray_numsteps.assign(2 * (size_t)R, 0);
@@ -981,21 +1029,15 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		M.ray_numsteps[2 * i] = n;
 		M.ray_numsteps[2 * i + 1] = b;
 		// pass 2: write coordinates (testbed_nerf.cu:814-830)
-		const V3 o = ro[i], d = rd[i];
+		const V3 d = rd[i];
 		const V3 wd = v((d.x + 1.0f) * 0.5f, (d.y + 1.0f) * 0.5f, (d.z + 1.0f) * 0.5f);
-		uint32_t j = 0;
-		for (uint32_t k = 0; j < n; ++k) {
-			float t, dt;
-			V3 pos;
-			const int r = lattice(o, d, rst[i], k, &t, &dt, &pos);
-			if (r < 0) break;
-			if (r == 0) continue;
-			const V3 w = box.rel(pos);
-			float* c = &M.coords[8 * (size_t)(b + j)];
-			c[0] = w.x; c[1] = w.y; c[2] = w.z; c[3] = warp_dt(dt);
-			c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
-			++j;
-		}
+		training_walk(stp, box, M.bits.data(), a.max_cascade, ro[i], d, rst[i], n,
+		              [&](uint32_t j, uint32_t, float, float dt, V3 pos) {
+			              const V3 w = box.rel(pos);
+			              float* c = &M.coords[8 * (size_t)(b + j)];
+			              c[0] = w.x; c[1] = w.y; c[2] = w.z; c[3] = warp_dt(dt);
+			              c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
+		              });
 	}
 	M.total_samples = base;
 	const uint32_t S = std::min(base, MS);
@@ -1583,6 +1625,40 @@ void oref_backward(void* m, const float* enc, const float* dirs, uint32_t n, con
 void oref_encode_backward(void* m, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
 	hg_backward(*static_cast<Model*>(m), pos, stride, n, denc);
 }
+// Test hook: training ray i's sample parameters -- mode 0: the lattice walk (fast path), as
+// stepping-space positions n0 + k; mode 1: the literal transcription of the reference's loop
+// (chained t += calc_dt(t), advance_to_next_voxel), as stepping-space positions to(t).
+// Returns the sample count (<= cap), writes min(count, cap) values and *n0 (the lattice origin).
+uint32_t oref_train_ray_samples(void* m, const ngp_train_args* a, uint32_t i, int mode, float* out, uint32_t cap, float* n0_out) {
+	Model& M = *static_cast<Model*>(m);
+	const uint32_t nrg = a->n_rays_global ? a->n_rays_global : a->n_rays;
+	const Box box{v(a->aabb_min[0], a->aabb_min[1], a->aabb_min[2]), v(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2])};
+	const Stepping stp = make_stepping(a->cone_angle_constant);
+	V3 o, d;
+	float n0, t0, r;
+	if (!train_ray(*a, a->ray_index_offset + i, nrg, &o, &d, &n0, &t0, &r)) return 0;
+	if (n0_out) *n0_out = n0;
+	if (mode == 0)
+		return training_walk(stp, box, M.bits.data(), a->max_cascade, o, d, n0, std::min(cap, STEPS),
+		                     [&](uint32_t j, uint32_t k, float, float, V3) { out[j] = n0 + (float)k; });
+	const float cone = a->cone_angle_constant;
+	const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	float t = ref_advance_n_steps(t0, cone, r);
+	uint32_t j = 0;
+	V3 pos;
+	while (box.contains(pos = o + d * t) && j < std::min(cap, STEPS)) {
+		const float dt = ref_calc_dt(t, cone);
+		const uint32_t mip = mip_dt(dt, pos, a->max_cascade);
+		if (occupied(pos, M.bits.data(), mip)) {
+			out[j++] = ref_to_stepping_space(t, cone);
+			t += dt;
+		} else {
+			t = ref_advance_to_next_voxel(t, cone, pos, d, idir, mip);
+		}
+	}
+	return j;
+}
+
 int oref_train_step(void* m, const ngp_train_args* a) { return guard([&] { train_step(*static_cast<Model*>(m), *a); }); }
 void oref_optimizer_step(void* m, uint32_t step, int opt_mlp, int opt_enc) { optimizer(*static_cast<Model*>(m), step, opt_mlp, opt_enc); }
 void oref_train_stats(void* m, ngp_train_stats* s) {

@@ -47,6 +47,8 @@ _PROTOS = {
     "oref_backward": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
     "oref_encode_backward": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     "oref_train_step": (C.c_int, [C.c_void_p, C.POINTER(A.TrainArgs)]),
+    "oref_train_ray_samples": (C.c_uint32, [C.c_void_p, C.POINTER(A.TrainArgs), C.c_uint32, C.c_int, C.c_void_p,
+                                            C.c_uint32, C.POINTER(C.c_float)]),
     "oref_optimizer_step": (None, [C.c_void_p, C.c_uint32, C.c_int, C.c_int]),
     "oref_train_stats": (None, [C.c_void_p, C.POINTER(A.TrainStats)]),
     "oref_train_scratch": (C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p]),
@@ -179,6 +181,14 @@ class Oracle:
     def train_step(self, args):
         if self.lib.oref_train_step(self.h, C.byref(args)) != 0:
             raise RuntimeError(self.lib.oref_last_error().decode())
+
+    def train_ray_samples(self, args, i, literal=False, cap=1024):
+        """Stepping-space positions of training ray i's samples: the lattice walk (fast path) or the
+        literal transcription of the reference's loop; and the ray's lattice origin n0."""
+        out = np.zeros(cap, np.float32)
+        n0 = C.c_float()
+        n = self.lib.oref_train_ray_samples(self.h, C.byref(args), i, int(literal), ptr(out), cap, C.byref(n0))
+        return out[:n].copy(), n0.value
 
     def optimizer_step(self, step, opt_mlp=1, opt_enc=1):
         self.lib.oref_optimizer_step(self.h, step, opt_mlp, opt_enc)
