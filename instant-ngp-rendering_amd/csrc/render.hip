@@ -676,13 +676,33 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 static uint32_t lanes_target() {
 	const char* e = getenv("NGP_RENDER_LANES");
 	const long v = e ? atol(e) : 0;
-	return v > 0 ? (uint32_t)v : 1u << 20;
+	return v > 0 ? (uint32_t)v : 8u << 20;
+}
+
+// NGP_RENDER_TARGET overrides the per-pass sample budget (tuning knob; results do not depend on it)
+static uint32_t pass_sample_target() {
+	const char* e = getenv("NGP_RENDER_TARGET");
+	const long v = e ? atol(e) : 0;
+	// <= 16M: the MLP reads the encodings through raw buffers with 32-bit byte offsets (64 B/sample)
+	return (uint32_t)std::min<long>(v > 0 ? v : 16l << 20, 16l << 20);
+}
+
+// NGP_RENDER_FIRST_STEPS: the per-ray cap of the first pass; the cap doubles every pass up to
+// NGP_RENDER_STEPS_PER_PASS.  A ray's slots past its termination are wasted encoder and MLP
+// work: most rays of a surface scene stop within a few samples of their first occupied one,
+// while rays through a volume need many, so short first passes and geometric growth keep the
+// waste and the pass count both low.  Inside the cap each ray's budget also follows its
+// transmittance and the opacity of its last sample (sample_budget).
+static uint32_t first_pass_steps() {
+	const char* e = getenv("NGP_RENDER_FIRST_STEPS");
+	const int v = e ? atoi(e) : 0;
+	return v > 0 ? (uint32_t)v : 4u;
 }
 
 static uint32_t max_steps_per_pass() {
 	const char* e = getenv("NGP_RENDER_STEPS_PER_PASS");
 	const int v = e ? atoi(e) : 0;
-	return v > 0 ? (uint32_t)v : 16u;
+	return v > 0 ? (uint32_t)v : 32u;
 }
 
 void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s) {
@@ -725,7 +745,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	if (n == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
 
-	const size_t max_samples = std::max<size_t>((size_t)n, (size_t)2 * 1024 * 1024) + 256;
+	const uint32_t target = pass_sample_target(), cap = max_steps_per_pass(), cap0 = std::min(first_pass_steps(), cap);
+	// the most slots one pass can reserve (see `bound` below): small frames stay small
+	const size_t max_samples = std::min<size_t>((size_t)n * cap, std::max<size_t>((size_t)n, (size_t)target)) + 256;
 	for (int b = 0; b < 3; ++b) {
 		rs.payload[b].reserve((size_t)n * 12);
 		rs.rgba[b].reserve((size_t)n * 4);
@@ -779,7 +801,6 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// read-back shows no alive rays (the pass enqueued meanwhile runs empty).
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
-	const uint32_t target = 2 * 1024 * 1024, cap = max_steps_per_pass();
 	if (!rs.events[0]) {
 		for (auto& e : rs.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 	}
@@ -842,15 +863,16 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 512));
 		unsigned long long* host_prev = pass > 0 ? pub_dev + 8 * ((pass - 1) % 2) : nullptr;
 		const uint32_t tag_prev = base_tag + pass;  // = tag of pass - 1
+		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 1: k_generate<1><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, s);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
-		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap, std::max(target, n_alive_ub));
+		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap_p, std::max(target, n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin_kernel(NGP_TIMER_RENDER_ENCODE);
 		static const char* dump = getenv("NGP_RENDER_DUMP");  // diagnostic: pass-0 samples + alive payloads
