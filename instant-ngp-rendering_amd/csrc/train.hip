@@ -386,46 +386,28 @@ struct ChunkArgs {
 	int density_act;
 };
 
-// Block-cooperative row loop: thread t owns cnt rows (k = 0..cnt-1); the block's rows are
-// dealt to its 256 threads in order, so consecutive lanes move consecutive rows.
-template <class Op>
-__device__ __forceinline__ void block_rows(uint32_t cnt, uint32_t* s_off, Op op) {
-	__shared__ uint32_t wsum[4];
-	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-	uint32_t x = cnt;
-#pragma unroll
-	for (uint32_t o = 1; o < 64; o <<= 1) {
-		const uint32_t y = __shfl_up(x, o, 64);
-		if (lane >= o) x += y;
-	}
-	if (lane == 63) wsum[w] = x;
-	__syncthreads();
-	uint32_t off = x - cnt;
-	for (uint32_t k = 0; k < w; ++k) off += wsum[k];
-	s_off[threadIdx.x] = off;
-	if (threadIdx.x == 255) s_off[256] = off + cnt;
-	__syncthreads();
-	const uint32_t total = s_off[256];
-	for (uint32_t r = threadIdx.x; r < total; r += 256) {
-		uint32_t lo = 0, hi = 256;  // owner: last t with s_off[t] <= r
-		while (hi - lo > 1) {
-			const uint32_t mid = (lo + hi) >> 1;
-			if (s_off[mid] <= r) lo = mid;
-			else hi = mid;
-		}
-		op(lo, r - s_off[lo]);
-	}
-	__syncthreads();
-}
-
 // One chunk step: composite the previous chunk's outputs (transmittance only) and scatter
 // them to the sampler layout, then claim evaluation rows for the next chunk of every ray
 // still marching and gather its network inputs.  The last step only scatters.
-__global__ void __launch_bounds__(256) k_train_chunk(ChunkArgs a) {
-	__shared__ uint32_t s_off[257], s_src[256], s_dst[256];
+//
+// G lanes per ray (1024-thread blocks, 1024 / G rays each; the host picks G so a launch has
+// ~100k+ lanes whether a batch holds 2k long rays of a volume or 35k short ones of a surface
+// scene).  The group composites G samples per round: an inclusive product scan of the
+// per-sample factors exp(-sigma dt) gives every lane the transmittance before its sample, and
+// the ray stops at the first sample where that is below the margin (the sequential loop's
+// stop; the product's association differs, which the 2x margin below the loss kernel's
+// threshold absorbs).  Row copies are coalesced within the group; the rows of the next chunk
+// are claimed with one atomic per block.
+template <uint32_t G>
+__global__ void __launch_bounds__(1024) k_train_chunk(ChunkArgs a) {
+	constexpr uint32_t RPB = 1024u / G;
+	__shared__ uint32_t wtot[16];
 	__shared__ uint32_t s_base;
-	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	const bool valid = i < a.n_rays;
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	const uint32_t r = lane % G, g0 = lane - r;
+	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
+	const uint32_t i = blockIdx.x * RPB + threadIdx.x / G;
+	const bool valid = i < a.n_rays;  // group-uniform
 	uint32_t n = 0, base = 0;
 	if (valid) {
 		n = a.numsteps[2 * i];
@@ -433,48 +415,64 @@ __global__ void __launch_bounds__(256) k_train_chunk(ChunkArgs a) {
 	}
 	float T = 1.0f;
 	bool alive = valid && n > 0;
-	uint32_t ev = 0, scatter = 0;
+	uint32_t ev = 0;
 	if (!a.first) {
 		const uint32_t e = valid ? a.ray_eval[i] : RAY_EVAL_DONE;
 		alive = alive && !(e & RAY_EVAL_DONE) && e == a.prev_lo;
 	}
 	const bool entered = a.first ? valid : alive;  // this step owns the ray's state
-	if (!a.first) {
-		if (alive) {
-			T = a.ray_T[i];
-			const uint32_t ebase = a.ray_ebase[i];
-			const uint32_t end = min(n, a.lo);
-			uint32_t j = a.prev_lo;
-			if (!a.last) {
-				for (; j < end; ++j) {
-					if (T < TRAIN_CHUNK_STOP_T) break;  // the loss kernel stops at or before sample j
-					const uint2 ob = *reinterpret_cast<const uint2*>(a.eout + 4 * (size_t)(ebase + j - a.prev_lo));
+	if (!a.first && alive) {
+		T = a.ray_T[i];
+		const uint32_t ebase = a.ray_ebase[i];
+		const uint32_t end = min(n, a.lo);
+		uint32_t j = a.prev_lo;
+		if (!a.last) {
+			while (j < end) {  // group-uniform
+				const uint32_t jj = j + r;
+				float f = 1.0f;
+				if (jj < end) {
+					const size_t e = ebase + jj - a.prev_lo;
+					const uint2 ob = *reinterpret_cast<const uint2*>(a.eout + 4 * e);
 					const float raw = __half2float(reinterpret_cast<const __half*>(&ob)[3]);
-					const float dt = unwarp_dt(a.epos[ebase + j - a.prev_lo].w);
-					T *= __expf(-network_to_density(raw, a.density_act) * dt);  // 1 - alpha
+					const float dt = unwarp_dt(a.epos[e].w);
+					f = __expf(-network_to_density(raw, a.density_act) * dt);  // 1 - alpha
 				}
-			} else {
-				j = end;
+				float incl = f;
+#pragma unroll
+				for (uint32_t o = 1; o < G; o <<= 1) {
+					const float y = __shfl_up(incl, o, G);
+					if (r >= o) incl *= y;
+				}
+				const float prev = __shfl_up(incl, 1, G);
+				const float Tb = r == 0 ? T : T * prev;  // transmittance before sample jj
+				const unsigned long long below = __ballot(jj < end && Tb < TRAIN_CHUNK_STOP_T) & gmask;
+				if (below) {  // the loss kernel stops at or before the first such sample
+					const uint32_t k = (uint32_t)(__ffsll((long long)below) - 1) - g0;
+					T = __shfl(Tb, g0 + k, 64);
+					j += k;
+					break;
+				}
+				const uint32_t m = min(G, end - j);
+				T *= __shfl(incl, g0 + m - 1, 64);
+				j += m;
 			}
-			scatter = j - a.prev_lo;
-			ev = j;
-			// stopped inside the chunk, at its end with T already below the margin, or out of samples
-			if (j < end || T < TRAIN_CHUNK_STOP_T || end == n) alive = false;
-			s_src[threadIdx.x] = base + a.prev_lo;
-			s_dst[threadIdx.x] = ebase;
+		} else {
+			j = end;
 		}
-	}
-	if (!a.first) {
-		// previous chunk's outputs back to the sampler layout (rows [prev_lo, prev_lo + scatter))
-		block_rows(scatter, s_off, [&](uint32_t t, uint32_t k) {
-			const uint32_t src = s_src[t] + k, e = s_dst[t] + k;
+		const uint32_t scatter = j - a.prev_lo;
+		ev = j;
+		// stopped inside the chunk, at its end with T already below the margin, or out of samples
+		if (j < end || T < TRAIN_CHUNK_STOP_T || end == n) alive = false;
+		// the chunk's outputs back to the sampler layout (rows [prev_lo, j))
+		for (uint32_t k = r; k < scatter; k += G) {
+			const uint32_t src = base + a.prev_lo + k, e = ebase + k;
 			*reinterpret_cast<uint2*>(a.mlp_out + 4 * (size_t)src) = *reinterpret_cast<const uint2*>(a.eout + 4 * (size_t)e);
 			a.eidx[src] = e;
-		});
+		}
 	}
 	uint32_t claim = 0;
 	if (alive && a.hi > a.lo) claim = min(n, a.hi) - a.lo;
-	if (entered) {
+	if (entered && r == 0) {
 		if (claim) {
 			a.ray_T[i] = T;
 			a.ray_eval[i] = a.lo;
@@ -483,35 +481,33 @@ __global__ void __launch_bounds__(256) k_train_chunk(ChunkArgs a) {
 		}
 	}
 	if (a.hi <= a.lo) return;  // last step: nothing to gather (block-uniform)
-	// claim rows for the next chunk: one atomic per block
-	__syncthreads();
-	{
-		__shared__ uint32_t wtot[4];
-		const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-		uint32_t x = claim;
+	// claim rows for the next chunk: wave scan over the groups' leaders, one atomic per block
+	const uint32_t mine = r == 0 ? claim : 0u;
+	uint32_t x = mine;
 #pragma unroll
-		for (uint32_t o = 1; o < 64; o <<= 1) {
-			const uint32_t y = __shfl_up(x, o, 64);
-			if (lane >= o) x += y;
-		}
-		if (lane == 63) wtot[w] = x;
-		__syncthreads();
-		if (threadIdx.x == 0) {
-			const uint32_t t = wtot[0] + wtot[1] + wtot[2] + wtot[3];
-			s_base = t ? atomicAdd(a.rows, t) : 0u;
-		}
-		__syncthreads();
-		uint32_t off = s_base + x - claim;
-		for (uint32_t k = 0; k < w; ++k) off += wtot[k];
-		if (claim) a.ray_ebase[i] = a.eval_offset + off;
-		s_src[threadIdx.x] = base + a.lo;
-		s_dst[threadIdx.x] = a.eval_offset + off;
+	for (uint32_t o = 1; o < 64; o <<= 1) {
+		const uint32_t y = __shfl_up(x, o, 64);
+		if (lane >= o) x += y;
 	}
-	block_rows(claim, s_off, [&](uint32_t t, uint32_t k) {
-		const uint32_t src = s_src[t] + k, e = s_dst[t] + k;
-		a.epos[e] = a.pos4[src];
-		a.edir[e] = reinterpret_cast<const float4*>(a.coords + 8 * (size_t)src)[1];
-	});
+	if (lane == 63) wtot[w] = x;
+	__syncthreads();
+	if (threadIdx.x == 0) {
+		uint32_t t = 0;
+		for (uint32_t k = 0; k < 16; ++k) t += wtot[k];
+		s_base = t ? atomicAdd(a.rows, t) : 0u;
+	}
+	__syncthreads();
+	// exclusive offset of the group's leader
+	uint32_t off = s_base + __shfl(x - mine, g0, 64);
+	for (uint32_t k = 0; k < w; ++k) off += wtot[k];
+	if (claim == 0) return;
+	const uint32_t e0 = a.eval_offset + off;
+	if (r == 0) a.ray_ebase[i] = e0;
+	for (uint32_t k = r; k < claim; k += G) {
+		const uint32_t src = base + a.lo + k;
+		a.epos[e0 + k] = a.pos4[src];
+		a.edir[e0 + k] = reinterpret_cast<const float4*>(a.coords + 8 * (size_t)src)[1];
+	}
 }
 
 // ---------------------------------------------------------------------------
@@ -1211,7 +1207,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			c.hi = p < TRAIN_CHUNKS ? TRAIN_CHUNK_END[p] : c.lo;
 			c.rows = ts.counters.ptr + 12 + std::min(p, TRAIN_CHUNKS - 1);
 			c.eval_offset = p < TRAIN_CHUNKS ? off[p] : 0u;
-			k_train_chunk<<<div_up(R, 256), 256, 0, s>>>(c);
+			// lanes per ray: ~100k+ lanes per launch (2k rays of a volume scene: 64; 35k rays of a surface scene: 4)
+			if (R <= 4096) k_train_chunk<64><<<div_up(R, 16), 1024, 0, s>>>(c);
+			else if (R <= 16384) k_train_chunk<16><<<div_up(R, 64), 1024, 0, s>>>(c);
+			else k_train_chunk<4><<<div_up(R, 256), 1024, 0, s>>>(c);
 			NGP_HIP_CHECK(hipGetLastError());
 			if (p == TRAIN_CHUNKS) break;
 			// launch about as many encoder chunks as the last step's rows needed; blocks loop
