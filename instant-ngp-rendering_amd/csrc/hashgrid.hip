@@ -125,7 +125,32 @@ __device__ __forceinline__ void gather_corners(const typename FeatVec<F>::T* __r
 		i0[q] = corner_index<HASHED>(size, res, gx, yy, zz);
 		i1[q] = corner_index<HASHED>(size, res, gx + 1u, yy, zz);
 	}
-	if constexpr (QUAD && F == 2) {
+	if constexpr (QUAD && F == 2 && !HASHED) {
+		// dense level: the x+1 corner is the next entry (unless the index wraps at the level's
+		// end), so one 8-B load at the x corner's entry fetches both -- 4 load instructions per
+		// level instead of 4 quads + 4 masked lone loads (the encoder is bound by the texture
+		// addresser's work per load instruction).  4-B aligned 8-B global loads are legal on
+		// gfx950 (the compiler emits them for 4-B aligned memcpy).
+		bool adj = true;
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) adj &= i1[q] == i0[q] + 1u;
+		uint2 pr[4];
+		if (adj) {
+#pragma unroll
+			for (uint32_t q = 0; q < 4; ++q) __builtin_memcpy(&pr[q], tab + i0[q], sizeof(uint2));
+		}
+		if (__ballot(!adj)) {  // a wrapped index (at most a few lanes, rarely any)
+			if (!adj) {
+#pragma unroll
+				for (uint32_t q = 0; q < 4; ++q) pr[q] = make_uint2(tab[i0[q]], tab[i1[q]]);
+			}
+		}
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) {
+			vals[2 * q] = pr[q].x;
+			vals[2 * q + 1] = pr[q].y;
+		}
+	} else if constexpr (QUAD && F == 2) {
 		// aligned 16-B quads of entries: the x+1 corner shares the x corner's quad unless x
 		// (hashed) or the index (dense) is 3 mod 4 -- a quarter of the lanes load it alone
 		const uint4* qtab = reinterpret_cast<const uint4*>(tab);
