@@ -151,40 +151,49 @@ def read_timers(abi, lib, handle):
     return out
 
 
-def cpu_baseline(args, tb, cams, imgs, focal, view, W, H):
-    """Scalar oracle (1 core) on a bounded sample: one training step of --cpu-rays rays and
-    --cpu-rows rows of the 1080p frame, with the GPU's trained weights (EMA inference weights
-    for the render, as the GPU renders) and density grid.  The same rows of the GPU's frame are
-    compared with the oracle's (north_star: rendered RGB within 1e-3 mean L1) -> "parity"."""
+def cpu_baseline(args, tb, cams, imgs, focal, view, W, H, calib, n_cal):
+    """The scalar C++ oracle (tests/cpu_baseline.py) on bounded samples, timed single-threaded and
+    with OpenMP on min(16, hardware_concurrency) threads (the GPU box's CPU share):
+      * value: one training step of --cpu-rays rays + --cpu-rows rows of the 1080p frame with the
+        GPU's trained weights (EMA inference weights for the render, as the GPU renders) and grid,
+        all-core; the same rows of the GPU's frame are compared with the oracle's (north_star:
+        rendered RGB within 1e-3 mean L1) -> "parity";
+      * config A (BASELINE configs[0]) end to end: 16 training steps + a 64x64 render;
+      * config B per kernel at 2^15 samples, extrapolated to one bench step."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
-    from scene_util import HostDataset, oracle_frame_rows, testbed_oracle, train_args
+    import cpu_baseline as cb
+    from scene_util import HostDataset, testbed_oracle
 
     tb.set_camera_to_training_view(view)
     gpu_frame = tb.render(W, H, 1, True)  # the timed workload's frame, copied to the host
     o = testbed_oracle(tb)
-
-    rows = args.cpu_rows
-    block = H // (2 * rows)
-    t0 = time.perf_counter()
-    ref = oracle_frame_rows(o, tb, W, H, [block], rows)
-    t_render = time.perf_counter() - t0
-    ys = sorted(ref)
-    l1 = float(np.abs(gpu_frame[ys, :, :3] - np.stack([ref[y] for y in ys])[..., :3]).mean())
-
-    # the training step last: its optimizer step changes the oracle's weights
+    hw, nth = cb.threads_for_box()
     n_sub = min(len(imgs), 8)
     hd = HostDataset(imgs[:n_sub], cams[:n_sub], focal)
     R = args.cpu_rays
-    ta = train_args(hd.ptr, hd.n, R, 1 << 14, 16 * (1 << 14))
-    t0 = time.perf_counter()
-    o.train_step(ta)
-    o.optimizer_step(0, 1, 1)
-    t_train = time.perf_counter() - t0
-    rays = R + W * len(ys)
-    secs = t_train + t_render
-    cpu = {"value": rays / secs / 1e6, "unit": "Mrays/s", "cores": 1, "kind": "port",
-           "sample": f"scalar oracle: 1 train step of {R} rays (+Adam over {o.n_params} params) in {t_train:.2f}s "
-                     f"+ {len(ys)} rows of the {W}x{H} frame ({W * len(ys)} rays) in {t_render:.2f}s, same weights/grid"}
+    # all-core first: its rows are the parity check (the training step after them moves the weights)
+    t_train, t_render, rays, ref = cb.bench_sample(o, tb, W, H, args.cpu_rows, hd, R, nth)
+    ys = sorted(ref)
+    l1 = float(np.abs(gpu_frame[ys, :, :3] - np.stack([ref[y] for y in ys])[..., :3]).mean())
+    t1_train, t1_render, _, _ = cb.bench_sample(o, tb, W, H, args.cpu_rows, hd, R, 1)
+    cfg_a = {"single_thread": cb.config_a_end_to_end(1), "all_core": cb.config_a_end_to_end(nth)}
+    train_samples = calib["train_mlp_infer"][1] / max(n_cal, 1)
+    render_samples = calib["render_encode"][1] / max(n_cal, 1)
+    train_rays = calib["train_sampler"][1] / max(n_cal, 1)
+    cfg_b = {}
+    for label, th in (("single_thread", 1), ("all_core", nth)):
+        e = cb.config_b_kernels(o, th, train_samples, render_samples, n=1 << 15)
+        e["Mrays_s_extrapolated"] = (train_rays + W * H) / e["extrapolated_s_per_step"] / 1e6
+        cfg_b[label] = e
+    cpu = {"value": rays / (t_train + t_render) / 1e6, "unit": "Mrays/s", "cores": nth, "kind": "port",
+           "sample": f"scalar C++ oracle, OpenMP on {nth} threads (hardware_concurrency {hw}): 1 train step of {R} rays "
+                     f"(+Adam over {o.n_params} params) in {t_train:.2f}s + {len(ys)} rows of the {W}x{H} frame "
+                     f"({W * len(ys)} rays) in {t_render:.2f}s, same weights/grid as the GPU",
+           "hardware_concurrency": hw,
+           "single_thread": {"value": rays / (t1_train + t1_render) / 1e6, "cores": 1, "train_s": round(t1_train, 3),
+                             "render_s": round(t1_render, 3)},
+           "config_a_end_to_end": cfg_a,
+           "config_b_per_kernel_extrapolated": cfg_b}
     parity = {"rgb_mean_l1_vs_oracle": l1, "rows": [ys[0], ys[-1]], "tolerance": 1e-3, "ok": l1 < 1e-3,
               "object_pixels_frac": float((gpu_frame[ys, :, 3] > 0.01).mean())}
     return cpu, parity
@@ -374,7 +383,7 @@ def main():
 
     cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_baseline:
-        cpu, parity = cpu_baseline(args, tb, cams, imgs, focal, view, W, H)
+        cpu, parity = cpu_baseline(args, tb, cams, imgs, focal, view, W, H, calib, n_cal)
 
     value = rays / elapsed / 1e6
     if rank == 0:

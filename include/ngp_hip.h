@@ -14,6 +14,7 @@
  *                               Trainer/Optimizer creation :3726-3727,3846)
  *   ngp_model_encode          tcnn GridEncoding::inference_mixed_precision (called at nerf_network.h:113-118)
  *   ngp_model_infer           NerfNetwork::inference_mixed_precision_impl   nerf_network.h:105-139
+ *   ngp_model_infer_padded    the same, 16-row padded output in the reference's CM / RM layouts
  *   ngp_model_density         NerfNetwork::density                          nerf_network.h:270-279
  *   ngp_train_step            Testbed::train_nerf_step        src/testbed_nerf.cu:2683-2930
  *                             (+ Trainer::optimizer_step      src/testbed_nerf.cu:2502, unless deferred)
@@ -72,6 +73,10 @@ typedef struct ngp_network_config {
 	float ema_decay;
 	uint32_t decay_start, decay_interval;
 	float decay_base;
+	/* NerfNetwork's n_extra_dims (nerf_network.h:81, the dataset's per-image latent code width,
+	 * appended to the rgb network's input): must be 0 -- extra-dims optimisation
+	 * (optimize_extra_dims, default off) is not implemented (ngp_model_create fails otherwise) */
+	uint32_t n_extra_dims;
 } ngp_network_config;
 
 /* Read-only model geometry. */
@@ -236,6 +241,14 @@ ngp_status ngp_model_encode_indices(ngp_model* model, const float* pos, uint32_t
  * out: [n][4] fp16 = (rgb raw x3, density raw) (the 16-row padded output of the reference, rows 0-3). */
 ngp_status ngp_model_infer(ngp_model* model, const float* coords, uint32_t floats_per_coord, uint32_t n,
                            uint16_t* out, int use_inference_params, ngp_stream stream);
+/* The reference's full network output: padded_output_width() = 16 fp16 rows per sample (rows 0-2
+ * rgb raw, row 3 density raw -- extract_density, nerf_network.h:32-43, 132-138 -- rows 4-15 the rgb
+ * network's remaining outputs), column-major as training reads it (src/testbed_nerf.cu:2801:
+ * sample i's 16 rows at out[i * out_stride], out_stride >= 16) or row-major as the renderer reads
+ * it (:1720: row r of sample i at out[r * out_stride + i], out_stride >= n). */
+ngp_status ngp_model_infer_padded(ngp_model* model, const float* coords, uint32_t floats_per_coord, uint32_t n,
+                                  uint16_t* out, uint32_t out_stride, int layout_rm, int use_inference_params,
+                                  ngp_stream stream);
 /* pos: n positions (stride floats). out: [n] fp16 raw density (row 0 of the density MLP output). */
 ngp_status ngp_model_density(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
                              uint16_t* out, int use_inference_params, ngp_stream stream);

@@ -137,6 +137,9 @@ struct MlpArgs {
 	uint32_t enc_bytes, coord_bytes;  // buffer-resource extents (register-resident inference)
 	uint32_t dir_offset;              // float offset of the direction in a coords record
 	const __half* sh;                 // optional [n][16] precomputed SH inputs (renderer), instead of directions
+	uint32_t out_mode, out_stride;    // 0: out [n][4]; 1 / 2: the reference's 16-row output, column- / row-major
+	float* partials;                  // k_mlp_train: [workgroup][n_mlp_params] weight-gradient partials
+	uint32_t n_mlp;                   // MLP parameter count (partials row pitch)
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -545,13 +548,33 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 		}
 		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
 		rf_layer<N, N::NL - 1, CT_>(w, b, c);
-		if (g == 0) {
+		if (a.out_mode == 0) {
+			if (g == 0) {
+#pragma unroll
+				for (int cc = 0; cc < CT_; ++cc) {
+					const uint32_t i = base + 16 * cc + n;
+					if (i < a.n) {
+						const h4 o = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], dens[cc]};
+						*reinterpret_cast<h4*>(a.out + (size_t)i * 4) = o;
+					}
+				}
+			}
+		} else {
+			// all 16 output rows: lane group g holds rows 4g .. 4g+3; row 3 is the density (extract_density)
 #pragma unroll
 			for (int cc = 0; cc < CT_; ++cc) {
 				const uint32_t i = base + 16 * cc + n;
-				if (i < a.n) {
-					const h4 o = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], dens[cc]};
-					*reinterpret_cast<h4*>(a.out + (size_t)i * 4) = o;
+				if (i >= a.n) continue;
+				h4 o = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], (_Float16)c[cc][0][3]};
+				if (g == 0) o[3] = dens[cc];
+				if (a.out_mode == 1) {
+					*reinterpret_cast<h4*>(a.out + (size_t)i * a.out_stride + 4 * g) = o;
+				} else {
+#pragma unroll
+					for (int r = 0; r < 4; ++r) {
+							const _Float16 v = o[r];  // (a bit_cast of the vector element itself read element 0)
+							a.out[(size_t)(4 * g + r) * a.out_stride + i] = __builtin_bit_cast(__half, v);
+						}
 				}
 			}
 		}
@@ -722,13 +745,16 @@ __device__ __forceinline__ void bwd_range(const MlpArgs& a, const _Float16* frag
 	}
 }
 
+// The workgroup's weight gradients -> its row of the partials (plain stores: every weight is
+// in exactly one tile); k_mlp_reduce sums the rows in a fixed order.  Replaces one fp32 atomic
+// per weight and workgroup onto the same 10k addresses (256-way contention at the L2).
 template <class N, int l>
 __device__ __forceinline__ void flush_range(const MlpArgs& a, int wave, int lane, const f4 (&acc)[N::slots()]) {
 	if constexpr (l < N::NL) {
 		constexpr int KTN = N::KT16(l);
 		const int g = lane >> 4, n = lane & 15;
 		const uint32_t pin = a.param_in[l];
-		float* gl = a.grads + a.param_off[l];
+		float* gl = a.partials + (size_t)blockIdx.x * a.n_mlp + a.param_off[l];
 #pragma unroll
 		for (int t = 0; t < N::gtiles(l); ++t) {
 			const int gt = N::gtile_base(l) + t;
@@ -740,10 +766,109 @@ __device__ __forceinline__ void flush_range(const MlpArgs& a, int wave, int lane
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
 				const uint32_t row = 16 * mt + 4 * g + r;
-				if (row < (uint32_t)N::out_dim(l)) unsafeAtomicAdd(gl + (size_t)row * pin + col, c[r]);
+				if (row < (uint32_t)N::out_dim(l)) gl[(size_t)row * pin + col] = c[r];
 			}
 		}
 		flush_range<N, l + 1>(a, wave, lane, acc);
+	}
+}
+
+// Sum of the workgroups' partials into the fp32 MLP gradients: 16 lanes per weight, each
+// adding 1/16 of the rows, then a shuffle reduction -- a fixed order, so the MLP gradients are
+// deterministic.
+__global__ void __launch_bounds__(256) k_mlp_reduce(const float* __restrict__ partials, uint32_t rows, uint32_t n,
+                                                    float* __restrict__ grads) {
+	const uint32_t t = blockIdx.x * 256u + threadIdx.x;
+	const uint32_t j = t >> 4, q = t & 15u;
+	float s = 0.0f;
+	if (j < n) {
+#pragma unroll 4
+		for (uint32_t r = q; r < rows; r += 16) s += partials[(size_t)r * n + j];
+	}
+#pragma unroll
+	for (uint32_t o = 8; o > 0; o >>= 1) s += __shfl_xor(s, o, 16);
+	if (j < n && q == 0) grads[j] += s;
+}
+
+// Next chunk's global inputs, fetched into registers while the current chunk runs (F = 2
+// encodings with whole 8-half K chunks; other shapes load directly): the raw encoding words,
+// the warped direction and the loss gradient of this lane's rows.
+struct TrainPrefetch {
+	uint32_t e[2][4];
+	float d[3];
+	uint2 dl;
+	float w;
+};
+
+template <class N>
+__device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int lane, TrainPrefetch& p) {
+	constexpr int CHUNKS = N::ENC_ROWS / 8;
+	const EncLayout lay{a.enc_plane, a.enc_lsh, a.enc_gsh};
+	const uint32_t* e = reinterpret_cast<const uint32_t*>(a.enc);
+#pragma unroll
+	for (int it = 0; it < 2; ++it) {
+		const int t = lane + 64 * it, smp = t % SPW, chunk = t / SPW;
+		const uint32_t i = base + smp, k0 = chunk * 8;
+		const bool ok = t < SPW * CHUNKS && i < a.n && k0 < a.E;
+#pragma unroll
+		for (int q = 0; q < 4; ++q) p.e[it][q] = ok ? e[lay.vec(k0 / 2 + q, i)] : 0u;
+	}
+	const uint32_t i = base + (lane % SPW);
+	const bool in = i < a.n;
+	const float* c = a.coords + (size_t)(in ? i : 0) * a.coord_stride;
+#pragma unroll
+	for (int k = 0; k < 3; ++k) p.d[k] = in ? c[4 + k] : 0.5f;
+	p.dl = make_uint2(0u, 0u);
+	p.w = 1.0f;
+	if (lane < SPW && in) {
+		p.dl = *reinterpret_cast<const uint2*>(a.dloss + (size_t)i * 4);
+		if (a.weight) p.w = a.weight[i];
+	}
+}
+
+// The prefetched inputs -> this wave's LDS images (encoding rows, SH rows, output-layer delta),
+// the same values load_encoding / load_sh / the delta loop store.
+template <class N, int STRIDE, int DS>
+__device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefetch& p, _Float16* img, _Float16* dimg,
+                                             int x_seg, uint32_t base, int lane) {
+	constexpr int CHUNKS = N::ENC_ROWS / 8;
+#pragma unroll
+	for (int it = 0; it < 2; ++it) {
+		const int t = lane + 64 * it;
+		if (t < SPW * CHUNKS) {
+			const int smp = t % SPW, chunk = t / SPW;
+			h8 v;
+#pragma unroll
+			for (int q = 0; q < 4; ++q) {
+				v[2 * q] = u16h(p.e[it][q]);
+				v[2 * q + 1] = u16h(p.e[it][q] >> 16);
+			}
+			lds_st_h8(img + smp * STRIDE + chunk * 8, v);
+		}
+	}
+	{
+		// lane = half * SPW + sample: SH components 8 half .. 8 half + 7 of the warped direction
+		const int smp = lane % SPW, half = lane / SPW;
+		const bool in = base + smp < a.n;
+		float v[16];
+		sh_deg4(p.d[0], p.d[1], p.d[2], v);
+		h8 o;
+#pragma unroll
+		for (int k = 0; k < 8; ++k) o[k] = in ? (_Float16)(half ? v[8 + k] : v[k]) : (_Float16)0;
+		lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, o);
+	}
+	for (int t = lane; t < SPW * 4; t += 64) {
+		const int smp = t % SPW, ch = t / SPW;
+		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+		const uint2 dl = make_uint2(__shfl(p.dl.x, smp, 64), __shfl(p.dl.y, smp, 64));
+		const float w = __shfl(p.w, smp, 64);
+		if (ch == 0) {
+			const __half* d = reinterpret_cast<const __half*>(&dl);
+			v[0] = (_Float16)(__half2float(d[0]) * w);
+			v[1] = (_Float16)(__half2float(d[1]) * w);
+			v[2] = (_Float16)(__half2float(d[2]) * w);
+		}
+		lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
 	}
 }
 
@@ -771,27 +896,37 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_train(MlpArgs a) {
 	for (int s = 0; s < N::slots(); ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
 
 	const uint32_t n_chunks = n_chunks_of(a.n);
+	// F = 2 with whole K chunks: the next chunk's inputs are fetched during the current one
+	const bool pref = a.F == 2 && (a.E % 8) == 0 && N::ENC_ROWS / 8 * SPW <= 128;
+	TrainPrefetch pf;
+	if (pref && blockIdx.x < n_chunks) train_fetch<N>(a, blockIdx.x * SAMPLES_PER_BLOCK + wave * SPW, lane, pf);
 	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
 		__syncthreads();  // previous chunk's wgrad reads of every image are done
 		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
-		load_encoding<N, STRIDE>(a, img, base, lane);
-		load_sh<STRIDE>(a, img, N::template x_seg<true>(), base, lane);
+		if (pref) {
+			train_commit<N, STRIDE, DS>(a, pf, img, dimg, N::template x_seg<true>(), base, lane);
+			const uint32_t nxt = chunk + gridDim.x;
+			if (nxt < n_chunks) train_fetch<N>(a, nxt * SAMPLES_PER_BLOCK + wave * SPW, lane, pf);
+		} else {
+			load_encoding<N, STRIDE>(a, img, base, lane);
+			load_sh<STRIDE>(a, img, N::template x_seg<true>(), base, lane);
+			// delta of the rgb output layer: rows 0..2 = dL/drgb_raw (loss-scaled, rollover-weighted)
+			for (int t = lane; t < SPW * 4; t += 64) {
+				const int smp = t % SPW, ch = t / SPW;
+				const uint32_t i = base + smp;
+				h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+				if (ch == 0 && i < a.n) {
+					const float w = a.weight ? a.weight[i] : 1.0f;
+					const __half* d = a.dloss + (size_t)i * 4;
+					v[0] = (_Float16)(__half2float(d[0]) * w);
+					v[1] = (_Float16)(__half2float(d[1]) * w);
+					v[2] = (_Float16)(__half2float(d[2]) * w);
+				}
+				lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
+			}
+		}
 		f4 res[CT];
 		fwd_range<N, true, 0, N::NL - 1>(frags, img, lane, res);
-		// delta of the rgb output layer: rows 0..2 = dL/drgb_raw (loss-scaled, rollover-weighted)
-		for (int t = lane; t < SPW * 4; t += 64) {
-			const int smp = t % SPW, ch = t / SPW;
-			const uint32_t i = base + smp;
-			h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-			if (ch == 0 && i < a.n) {
-				const float w = a.weight ? a.weight[i] : 1.0f;
-				const __half* d = a.dloss + (size_t)i * 4;
-				v[0] = (_Float16)(__half2float(d[0]) * w);
-				v[1] = (_Float16)(__half2float(d[1]) * w);
-				v[2] = (_Float16)(__half2float(d[2]) * w);
-			}
-			lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
-		}
 		bwd_range<N, N::NL - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
 	}
 	flush_range<N, 0>(a, wave, lane, acc);
@@ -977,7 +1112,7 @@ static void set_lds(K kernel, size_t bytes) {
 
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev, uint32_t dir_offset, const __half* sh) {
+                      const uint32_t* n_dev, uint32_t dir_offset, const __half* sh, uint32_t out_mode, uint32_t out_stride) {
 	if (n == 0) return;
 	if (enc_layout.lsh != m->enc_lsh) throw std::runtime_error("encoding layout differs from the packed first layer's");
 	MlpArgs a = base_args(m);
@@ -995,6 +1130,8 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * (sh ? 8 : coord_stride) * 4, 0xffffffffu);
 	a.dir_offset = dir_offset;
 	a.sh = sh;
+	a.out_mode = out_mode;
+	a.out_stride = out_stride;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * 5);
@@ -1071,7 +1208,11 @@ void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc
 		if (lds > 160 * 1024) throw std::runtime_error("MLP training LDS footprint exceeds 160 KiB");
 		set_lds<N>(k_mlp_train<N>, lds);
 		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count());
+		m->mlp_partials.reserve((size_t)cu_count() * m->n_mlp_params);
+		a.partials = m->mlp_partials.ptr;
+		a.n_mlp = m->n_mlp_params;
 		launch_timed(k_mlp_train<N>, grid, BLOCK, lds, s, a);
+		k_mlp_reduce<<<div_up(16 * m->n_mlp_params, 256), 256, 0, s>>>(m->mlp_partials.ptr, grid, m->n_mlp_params, grads_mlp);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }

@@ -148,6 +148,7 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 		        "n_features_per_level must be 1, 2, 4 or 8");
 		require(cfg->log2_hashmap_size >= 4 && cfg->log2_hashmap_size <= 30, "log2_hashmap_size out of range");
 		require(cfg->per_level_scale > 0.0f, "per_level_scale must be positive");
+		require(cfg->n_extra_dims == 0, "n_extra_dims > 0 (per-image latent codes, optimize_extra_dims) is not supported");
 		NGP_HIP_CHECK(hipSetDevice(hip_device));
 		auto* m = new ngp_model();
 		try {
@@ -321,6 +322,23 @@ ngp_status ngp_model_infer(ngp_model* m, const float* coords, uint32_t fpc, uint
 		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
 		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, internal_layout(m, n), S(s));
 		launch_mlp_infer(m, frags, ts.enc.ptr, internal_layout(m, n), coords, fpc, n, reinterpret_cast<__half*>(out), S(s));
+	});
+}
+
+ngp_status ngp_model_infer_padded(ngp_model* m, const float* coords, uint32_t fpc, uint32_t n, uint16_t* out,
+                                  uint32_t out_stride, int layout_rm, int use_inf, ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (coords && out)), "null argument");
+		require(fpc >= 7, "floats_per_coord must be >= 7 (NerfCoordinate)");
+		require(layout_rm ? out_stride >= n : out_stride >= 16, "out_stride too small for 16 output rows");
+		if (n == 0) return;
+		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
+		TrainScratch& ts = m->ts;
+		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
+		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, internal_layout(m, n), S(s));
+		launch_mlp_infer(m, frags, ts.enc.ptr, internal_layout(m, n), coords, fpc, n, reinterpret_cast<__half*>(out), S(s),
+		                 nullptr, 4, nullptr, layout_rm ? 2u : 1u, out_stride);
 	});
 }
 

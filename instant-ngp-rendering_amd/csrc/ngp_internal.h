@@ -296,6 +296,7 @@ struct ngp_model {
 	ngp::DevBuf<__half> params16, infer16;
 	ngp::DevBuf<uint32_t> adam_steps;
 	ngp::DevBuf<__half> frag_train, frag_infer;  // packed MFMA fragments of params16 / infer16
+	mutable ngp::DevBuf<float> mlp_partials;      // [workgroup][n_mlp_params] weight-gradient partials of k_mlp_train
 	uint32_t ema_step = 0;
 
 	ngp::TrainScratch ts;
@@ -342,7 +343,8 @@ void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frag
 // dir_offset (NerfCoordinate: 4); sh (optional): [n][16] fp16 SH rows used instead
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr);
+                      const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr,
+                      uint32_t out_mode = 0, uint32_t out_stride = 4);
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
 // dsh (optional): [n][16] dL/d(SH inputs of the rgb network), of the sample's own row (divided

@@ -21,6 +21,7 @@ class NetworkConfig(C.Structure):
         ("learning_rate", C.c_float), ("beta1", C.c_float), ("beta2", C.c_float), ("epsilon", C.c_float),
         ("l2_reg", C.c_float), ("ema_decay", C.c_float),
         ("decay_start", C.c_uint32), ("decay_interval", C.c_uint32), ("decay_base", C.c_float),
+        ("n_extra_dims", C.c_uint32),
     ]
 
 
@@ -112,6 +113,8 @@ EXPORTS = {
     "ngp_model_encode_indices": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.c_void_p]),
     "ngp_model_infer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]),
+    "ngp_model_infer_padded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int,
+                                         C.c_int, C.c_void_p]),
     "ngp_model_density": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]),
     "ngp_model_backward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),

@@ -22,6 +22,8 @@
 //  * the occupancy mean is an exact 2^-24 fixed-point sum.
 //
 // Built by oracle/Makefile with g++ -O2 -ffp-contract=off (no fast-math).
+#include <omp.h>
+#include <thread>
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -509,6 +511,8 @@ static void hg_corners(const Model& M, uint32_t l, const float* p, uint32_t idx[
 // enc: [L][n][F] (fp16-rounded floats)
 static void hg_forward(const Model& M, const uint16_t* params, const float* pos, uint32_t stride, uint32_t n, float* enc) {
 	const uint16_t* tab = params + M.n_mlp;
+	// samples are independent (the all-core CPU baseline; 1 thread unless oref_set_threads)
+#pragma omp parallel for schedule(static)
 	for (uint32_t i = 0; i < n; ++i)
 		for (uint32_t l = 0; l < M.L; ++l) {
 			uint32_t idx[8];
@@ -655,8 +659,11 @@ static void gather_enc(const Model& M, const float* enc, uint32_t n, uint32_t i,
 // out: [n][4] = rgb raw (3) + density raw (fp16-rounded)
 static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, const float* coords, uint32_t cs, uint32_t n,
                         float* out) {
+#pragma omp parallel
+	{
 	std::vector<float> col(M.E);
 	Acts A;
+#pragma omp for schedule(static)
 	for (uint32_t i = 0; i < n; ++i) {
 		gather_enc(M, enc, n, i, col.data());
 		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A);
@@ -665,6 +672,7 @@ static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, con
 		out[4 * i + 1] = A.a[NL][1];
 		out[4 * i + 2] = A.a[NL][2];
 		out[4 * i + 3] = A.a[M.n_density_layers][0];  // density_out row 0 (first rgb-layer input)
+	}
 	}
 }
 // NerfNetwork::backward_impl (nerf_network.h:189-268): rgb MLP bwd -> add_density_gradient -> density MLP bwd
@@ -1379,7 +1387,11 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 	const uint32_t sc = std::max(a.shard_count, 1u), sr = std::max(a.shard_rows, 1u), si = a.shard_index % sc;
 	float ox, oy;
 	pixel_offset(a.snap_to_pixel_centers ? 0 : a.sample_index, &ox, &oy);
+	// rows are independent (the all-core CPU baseline); dynamic: rows differ in cost
+#pragma omp parallel
+	{
 	std::vector<float> enc(M.L * M.F), col(M.E), out(4);
+#pragma omp for schedule(dynamic, 1)
 	for (uint32_t y = 0; y < a.height; ++y) {
 		if ((y / sr) % sc != si) continue;
 		for (uint32_t x = 0; x < a.width; ++x) {
@@ -1434,6 +1446,7 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			if (c[3] > 0.2f) depthbuf[idx] = dep;
 		}
 	}
+	}
 }
 
 }  // namespace oref
@@ -1447,6 +1460,11 @@ static int guard(F&& f) {
 }
 
 extern "C" {
+
+// threads of the parallel loops (render rows, encoding, inference); 1 by default so the tests
+// run the scalar oracle; the bench's all-core CPU baseline raises it
+void oref_set_threads(int n) { omp_set_num_threads(n > 0 ? n : 1); }
+uint32_t oref_hardware_concurrency(void) { return std::thread::hardware_concurrency(); }
 
 const char* oref_last_error(void) { return g_err.c_str(); }
 
@@ -1597,6 +1615,21 @@ void oref_infer(void* m, const float* coords, uint32_t fpc, uint32_t n, float* o
 	std::vector<float> enc((size_t)M.L * n * M.F);
 	hg_forward(M, P, coords, fpc, n, enc.data());
 	mlp_forward(M, P, enc.data(), coords, fpc, n, out);
+}
+// the reference's padded network output: 16 rows per sample, row 3 = density (extract_density)
+void oref_infer_padded(void* m, const float* coords, uint32_t fpc, uint32_t n, float* out16, int use_inf) {
+	Model& M = *static_cast<Model*>(m);
+	const uint16_t* P = use_inf ? M.inf16.data() : M.p16.data();
+	std::vector<float> enc((size_t)M.L * n * M.F), col(M.E);
+	hg_forward(M, P, coords, fpc, n, enc.data());
+	Acts A;
+	const uint32_t NL = (uint32_t)M.layers.size();
+	for (uint32_t i = 0; i < n; ++i) {
+		gather_enc(M, enc.data(), n, i, col.data());
+		mlp_forward_one(M, P, col.data(), coords + (size_t)i * fpc + 4, A);
+		for (uint32_t r = 0; r < 16; ++r) out16[16 * (size_t)i + r] = A.a[NL][r];
+		out16[16 * (size_t)i + 3] = A.a[M.n_density_layers][0];
+	}
 }
 void oref_mlp_forward_enc(void* m, const float* enc, const float* coords, uint32_t fpc, uint32_t n, float* out) {
 	Model& M = *static_cast<Model*>(m);

@@ -117,6 +117,20 @@ class GpuModel:
         torch.cuda.synchronize()
         return out.float().cpu().numpy().reshape(n, 4)
 
+    def infer_padded(self, coords, layout_rm, use_inf=False, pad=0):
+        """ngp_model_infer_padded: [n][16] (column-major, stride 16 + pad) or [16][n + pad] (row-major),
+        returned as [n][16]."""
+        coords = np.ascontiguousarray(coords, np.float32)
+        n, fpc = coords.shape
+        c = dev(coords)
+        stride = n + pad if layout_rm else 16 + pad
+        out = torch.full(((16 if layout_rm else n) * stride,), float("nan"), dtype=torch.float16, device="cuda")
+        A.check(self.lib.ngp_model_infer_padded(self.h, vp(c), fpc, n, vp(out), stride, int(layout_rm), int(use_inf),
+                                                stream()))
+        torch.cuda.synchronize()
+        o = out.float().cpu().numpy()
+        return o.reshape(16, stride)[:, :n].T.copy() if layout_rm else o.reshape(n, stride)[:, :16].copy()
+
     def density(self, pos, use_inf=False):
         pos = np.ascontiguousarray(pos, np.float32)
         n, stride = pos.shape

@@ -64,6 +64,9 @@ _PROTOS = {
     "oref_accumulate_tonemap": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                        C.c_int, C.c_float, C.c_void_p, C.c_int]),
     "oref_last_error": (C.c_char_p, []),
+    "oref_set_threads": (None, [C.c_int]),
+    "oref_infer_padded": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
+    "oref_hardware_concurrency": (C.c_uint32, []),
 }
 
 _lib = None
@@ -79,6 +82,7 @@ def load():
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        lib.oref_set_threads(1)  # the scalar oracle; the bench's all-core baseline raises it
         _lib = lib
     return _lib
 
@@ -154,6 +158,14 @@ class Oracle:
         n, fpc = coords.shape
         out = np.zeros((n, 4), np.float32)
         self.lib.oref_infer(self.h, ptr(coords), fpc, n, ptr(out), int(use_inf))
+        return out
+
+    def infer_padded(self, coords, use_inf=False):
+        """[n][16] network output (row 3 = density), as the reference's padded output."""
+        coords = np.ascontiguousarray(coords, np.float32)
+        n, fpc = coords.shape
+        out = np.zeros((n, 16), np.float32)
+        self.lib.oref_infer_padded(self.h, ptr(coords), fpc, n, ptr(out), int(use_inf))
         return out
 
     def density(self, pos, use_inf=False):

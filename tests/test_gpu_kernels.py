@@ -77,6 +77,38 @@ def test_infer_matches_oracle(name):
         g.close()
 
 
+@pytest.mark.parametrize("layout_rm", [0, 1])
+@pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
+def test_infer_padded_output_matches_oracle(name, layout_rm):
+    """The reference's 16-row padded network output (padded_output_width(), row 3 = density via
+    extract_density, nerf_network.h:32-43,132-138), column-major as training reads it
+    (src/testbed_nerf.cu:2801) and row-major as the renderer does (:1720), with a row stride
+    larger than the minimum; rows 0-3 equal the compact output bit for bit."""
+    g, o, rng = make(name)
+    try:
+        coords = random_coords(rng, 2500)
+        gp = g.infer_padded(coords, layout_rm, pad=7)
+        op = o.infer_padded(coords)
+        assert np.isfinite(gp).all()
+        err = np.abs(gp - op)
+        tol = 4e-3 + 8e-3 * np.abs(op)
+        assert (err <= tol).mean() > 0.999, f"max err {err.max()} at {np.unravel_index(err.argmax(), err.shape)}"
+        np.testing.assert_array_equal(gp[:, :4], g.infer(coords))
+        # the 16-row rgb output tile is the rgb network's real output, not padding
+        assert np.abs(op[:, 4:]).max() > 0
+    finally:
+        g.close()
+
+
+def test_extra_dims_are_refused():
+    """n_extra_dims > 0 (per-image latent codes) is not implemented: model creation fails loudly."""
+    from gpu_util import GpuModel
+    cfg = A.default_config(**CONFIGS["A_L4F2T14"])
+    cfg.n_extra_dims = 4
+    with pytest.raises(RuntimeError, match="n_extra_dims"):
+        GpuModel(cfg)
+
+
 @pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
 def test_density_matches_oracle_and_infer(name):
     g, o, rng = make(name)
