@@ -50,7 +50,7 @@ def parse():
                    help="time the dominant kernel in the timed run (0: diagnostic runs without timer events)")
     p.add_argument("--cpu-rows", type=int, default=8, help="1080p rows rendered by the CPU oracle sample")
     p.add_argument("--cpu-rays", type=int, default=512, help="training rays in the CPU oracle sample")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"),
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
 
@@ -120,8 +120,8 @@ def make_dataset(ngp, tb, args, device):
 
 # timer -> kernel (name pattern) whose PMC counters describe it
 TIMER_KERNEL = {"train_encode": r"k_hashgrid_fwd<\d+u, 0[,>]", "render_encode": r"k_hashgrid_fwd<\d+u, 1[,>]",
-                "train_encode_bwd": r"k_hashgrid_bwd<", "train_mlp_infer": r"k_mlp_infer_rf<.*, false, \d>$",
-                "render_mlp": r"k_mlp_infer_rf<.*, false, \d>$", "train_mlp_bwd": r"k_mlp_train<",
+                "train_encode_bwd": r"k_hashgrid_bwd<", "train_mlp_infer": r"k_mlp_infer_rf<.*, false, \d+, false>$",
+                "render_mlp": r"k_mlp_infer_rf<.*, true>$", "train_mlp_bwd": r"k_mlp_train<",
                 "optimizer": r"k_optimizer"}
 
 
@@ -138,7 +138,10 @@ def pmc_traffic(path, timer, units_per_launch):
     for name, e in data.items():
         if not re.search(TIMER_KERNEL[timer], name):
             continue
-        return round(e.get("fetch_bytes_per_launch", 0) + e.get("write_bytes_per_launch", 0))
+        # FETCH corrected by the measured ratio of the kernel's read shape (tools/fetch_calib.sh) where
+        # the summary carries it, as reported otherwise; WRITE as reported (exact per the guide)
+        fetch = e.get("fetch_bytes_per_launch_corrected", e.get("fetch_bytes_per_launch", 0))
+        return round(fetch + e.get("write_bytes_per_launch", 0))
     return None
 
 
