@@ -121,6 +121,10 @@ typedef struct ngp_image {
 	float xform[12];          /* camera-to-world 4x3, column-major (right, up, forward, origin), NGP space */
 	int32_t lens_mode;        /* 0 Perspective (others: ELensMode, common.h:188-195) */
 	float lens_params[7];
+	/* depth supervision target (TrainingImageMetadata::depth, nerf_device.cuh:44-59): device pointer to
+	 * width*height f32 depths along the optical axis, already multiplied by integer_depth_scale and the
+	 * dataset scale (src/nerf_loader.cu:73-82, 728); 0 = no depth for this image */
+	uint64_t depth;
 } ngp_image;
 
 typedef struct ngp_train_args {
@@ -169,6 +173,11 @@ typedef struct ngp_train_args {
 	 * each ray only up to its transmittance stop (identical loss/compaction/gradients, see
 	 * train_stats.forward_early_stop_violations) */
 	int32_t full_forward;
+	/* depth supervision (compute_loss_kernel_train_nerf, src/testbed_nerf.cu:1013-1015, 1098-1103):
+	 * with lambda > 0, rays of images with depth add lambda * d loss(target depth, composited depth)
+	 * to dL/d(density) through the depth suffix; depth_loss_type is an ELossType (default L1) */
+	float depth_supervision_lambda;
+	int32_t depth_loss_type;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {

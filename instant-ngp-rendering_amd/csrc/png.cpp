@@ -19,8 +19,65 @@ static int paeth(int a, int b, int c) {
 	return pb <= pc ? b : c;
 }
 
+// Unfiltered sample bytes of a non-interlaced PNG (big-endian 16-bit samples kept as bytes).
+struct RawPng {
+	std::vector<uint8_t> img, plte, trns;
+	uint32_t w = 0, h = 0;
+	int depth = 0, ctype = 0, channels = 0;
+	size_t bpp = 0;
+};
+static bool decode_png_raw(const uint8_t* d, size_t size, RawPng& out, std::string& err);
+
 bool decode_png_memory(const uint8_t* d, size_t size, std::vector<uint8_t>& rgba, int& width, int& height,
                        std::string& err) {
+	RawPng r;
+	if (!decode_png_raw(d, size, r, err)) return false;
+	const uint32_t w = r.w, h = r.h;
+	const int ctype = r.ctype, depth = r.depth;
+	const size_t bpp = r.bpp;
+	const std::vector<uint8_t>& img = r.img;
+	const std::vector<uint8_t>& plte = r.plte;
+	const std::vector<uint8_t>& trns = r.trns;
+	width = (int)w;
+	height = (int)h;
+	rgba.assign((size_t)w * h * 4, 255);
+	const int step = depth / 8;  // 16-bit: keep the high byte
+	for (size_t i = 0; i < (size_t)w * h; ++i) {
+		const uint8_t* p = &img[i * bpp];
+		uint8_t* o = &rgba[i * 4];
+		switch (ctype) {
+			case 0: o[0] = o[1] = o[2] = p[0]; break;
+			case 2: o[0] = p[0]; o[1] = p[step]; o[2] = p[2 * step]; break;
+			case 3: {
+				const uint8_t k = p[0];
+				if ((size_t)k * 3 + 2 < plte.size()) { o[0] = plte[k * 3]; o[1] = plte[k * 3 + 1]; o[2] = plte[k * 3 + 2]; }
+				o[3] = k < trns.size() ? trns[k] : 255;
+			} break;
+			case 4: o[0] = o[1] = o[2] = p[0]; o[3] = p[step]; break;
+			case 6: o[0] = p[0]; o[1] = p[step]; o[2] = p[2 * step]; o[3] = p[3 * step]; break;
+		}
+	}
+	return true;
+}
+
+bool decode_png16_file(const std::string& path, std::vector<uint16_t>& gray, int& width, int& height, std::string& err) {
+	std::ifstream f(path, std::ios::binary);
+	if (!f) { err = "cannot open " + path; return false; }
+	std::vector<uint8_t> buf((std::istreambuf_iterator<char>(f)), std::istreambuf_iterator<char>());
+	RawPng r;
+	if (!decode_png_raw(buf.data(), buf.size(), r, err)) return false;
+	if (r.ctype == 3) { err = "palette image as depth"; return false; }
+	width = (int)r.w;
+	height = (int)r.h;
+	gray.resize((size_t)r.w * r.h);
+	for (size_t i = 0; i < gray.size(); ++i) {
+		const uint8_t* p = &r.img[i * r.bpp];
+		gray[i] = r.depth == 16 ? (uint16_t)((p[0] << 8) | p[1]) : (uint16_t)(p[0] * 257u);
+	}
+	return true;
+}
+
+static bool decode_png_raw(const uint8_t* d, size_t size, RawPng& out, std::string& err) {
 	static const uint8_t sig[8] = {137, 80, 78, 71, 13, 10, 26, 10};
 	if (size < 8 || std::memcmp(d, sig, 8) != 0) { err = "not a PNG file"; return false; }
 	size_t pos = 8;
@@ -84,25 +141,15 @@ bool decode_png_memory(const uint8_t* d, size_t size, std::vector<uint8_t>& rgba
 			cur[x] = (uint8_t)v;
 		}
 	}
-	width = (int)w;
-	height = (int)h;
-	rgba.assign((size_t)w * h * 4, 255);
-	const int step = depth / 8;  // 16-bit: keep the high byte
-	for (size_t i = 0; i < (size_t)w * h; ++i) {
-		const uint8_t* p = &img[i * bpp];
-		uint8_t* o = &rgba[i * 4];
-		switch (ctype) {
-			case 0: o[0] = o[1] = o[2] = p[0]; break;
-			case 2: o[0] = p[0]; o[1] = p[step]; o[2] = p[2 * step]; break;
-			case 3: {
-				const uint8_t k = p[0];
-				if ((size_t)k * 3 + 2 < plte.size()) { o[0] = plte[k * 3]; o[1] = plte[k * 3 + 1]; o[2] = plte[k * 3 + 2]; }
-				o[3] = k < trns.size() ? trns[k] : 255;
-			} break;
-			case 4: o[0] = o[1] = o[2] = p[0]; o[3] = p[step]; break;
-			case 6: o[0] = p[0]; o[1] = p[step]; o[2] = p[2 * step]; o[3] = p[3 * step]; break;
-		}
-	}
+	out.w = w;
+	out.h = h;
+	out.depth = depth;
+	out.ctype = ctype;
+	out.channels = channels;
+	out.bpp = bpp;
+	out.img.swap(img);
+	out.plte.swap(plte);
+	out.trns.swap(trns);
 	return true;
 }
 

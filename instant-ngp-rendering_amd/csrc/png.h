@@ -11,5 +11,8 @@ namespace ngp {
 bool decode_png_file(const std::string& path, std::vector<uint8_t>& rgba, int& width, int& height, std::string& err);
 bool decode_png_memory(const uint8_t* data, size_t size, std::vector<uint8_t>& rgba, int& width, int& height,
                        std::string& err);
+// First channel as 16-bit values (stbi_load_16(..., 1) as the reference's depth loader calls it,
+// src/nerf_loader.cu:629: 16-bit samples as stored, 8-bit ones scaled by 257).
+bool decode_png16_file(const std::string& path, std::vector<uint16_t>& gray, int& width, int& height, std::string& err);
 
 }  // namespace ngp

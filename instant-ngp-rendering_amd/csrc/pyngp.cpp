@@ -219,7 +219,15 @@ PYBIND11_MODULE(pyngp, m) {
 			if (d.pixels[i].size() != (size_t)md.resolution[0] * md.resolution[1] * 4) throw std::runtime_error("image has no pixels");
 			std::memcpy(a.mutable_data(), d.pixels[i].data(), d.pixels[i].size());
 			return a;
-		}, "RGBA8 (sRGB, straight alpha) pixels of image i, as stored for training");
+		}, "RGBA8 (sRGB, straight alpha) pixels of image i, as stored for training")
+		.def("depth", [](const NerfDataset& d, size_t i) -> py::object {
+			if (i >= d.n_images) throw std::runtime_error("Invalid frame index");
+			if (i >= d.depths.size() || d.depths[i].empty()) return py::none();
+			const auto& md = d.metadata[i];
+			py::array_t<float> a({md.resolution[1], md.resolution[0]});
+			std::memcpy(a.mutable_data(), d.depths[i].data(), d.depths[i].size() * sizeof(float));
+			return a;
+		}, "depth targets of image i (16-bit depth x integer_depth_scale x scale), or None");
 
 	// ngp::load_nerf without a Testbed (no GPU needed): the dataset front end on its own
 	m.def("load_nerf_dataset", [](const std::string& path) {
@@ -250,6 +258,8 @@ PYBIND11_MODULE(pyngp, m) {
 		TV_RW("sample_focal_plane_proportional_to_error", sample_focal_plane_proportional_to_error)
 		TV_RW("sample_image_proportional_to_error", sample_image_proportional_to_error)
 		TV_RW("include_sharpness_in_error", include_sharpness_in_error)
+		TV_RW("depth_supervision_lambda", depth_supervision_lambda)
+		TV_RW("depth_loss_type", depth_loss_type)
 		TV_RW("n_steps_between_error_map_updates", n_steps_between_error_map_updates)
 		TV_RW("n_steps_between_cam_updates", n_steps_between_cam_updates)
 		TV_RW("exposure_l2_reg", exposure_l2_reg)

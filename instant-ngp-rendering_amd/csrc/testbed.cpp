@@ -260,6 +260,9 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 	// ngp::load_nerf (src/nerf_loader.cu:273-743)
 	NerfDataset ds;
 	ds.scale = 0.33f;
+	// depth images as loaded (16-bit) and their integer_depth_scale; scaled by the final dataset scale below
+	std::vector<std::vector<uint16_t>> depth_raw;
+	std::vector<float> depth_scales;
 	ds.offset = {0.5f, 0.5f, 0.5f};
 	static const char* formats[] = {"png", "jpg", "jpeg", "bmp", "gif", "tga", "pic", "pnm", "psd", "exr"};
 	for (const std::string& jp : json_paths) {
@@ -279,6 +282,9 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 			ds.scale = 1.f / len;
 			for (int k = 0; k < 3; ++k) ds.offset[k] = (((float)a[1][k].num() + (float)a[0][k].num()) * 0.5f) * -ds.scale + 0.5f;
 		}
+		// depth supervision inputs (src/nerf_loader.cu:419-437, 486-488)
+		const float depth_scale = (float)j.value("integer_depth_scale", -1.0);
+		const bool enable_depth_loading = j.value("enable_depth_loading", true);
 		if (j.contains("up")) ds.up = {(float)j["up"][1].num(), (float)j["up"][2].num(), (float)j["up"][0].num()};
 		// frames sorted naturally by file_path (src/nerf_loader.cu:347-349)
 		std::vector<Json> frames = j["frames"].elements();
@@ -381,7 +387,30 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 			ds.metadata.push_back(md);
 			ds.paths.push_back(fp);
 			ds.pixels.push_back(std::move(rgba));
+			// the frame's depth image (src/nerf_loader.cu:625-637): 16-bit, same resolution as the image
+			std::vector<uint16_t> dep;
+			if (enable_depth_loading && depth_scale > 0.f && fr.contains("depth_path")) {
+				std::string dpth = fr["depth_path"].str();
+				std::replace(dpth.begin(), dpth.end(), '\\', '/');
+				const std::string dp = (!dpth.empty() && dpth[0] == '/') ? dpth : base + "/" + dpth;
+				if (file_exists(dp)) {
+					int dw = 0, dh = 0;
+					std::string derr;
+					if (!decode_png16_file(dp, dep, dw, dh, derr)) throw std::runtime_error("Could not load depth image '" + dp + "'.");
+					if (dw != w || dh != h) throw std::runtime_error("Depth image " + dp + " has wrong resolution.");
+				}
+			}
+			depth_raw.push_back(std::move(dep));
+			depth_scales.push_back(depth_scale);
 		}
+	}
+	// depth targets in NGP units: depth x integer_depth_scale x the final dataset scale (src/nerf_loader.cu:728)
+	ds.depths.resize(depth_raw.size());
+	for (size_t i = 0; i < depth_raw.size(); ++i) {
+		if (depth_raw[i].empty()) continue;
+		ds.depths[i].resize(depth_raw[i].size());
+		const float sc = depth_scales[i] * ds.scale;
+		for (size_t k = 0; k < depth_raw[i].size(); ++k) ds.depths[i][k] = (float)depth_raw[i][k] * sc;
 	}
 	ds.n_images = ds.metadata.size();
 	if (ds.n_images == 0) throw std::invalid_argument("No training images were found for NeRF training!");
@@ -531,6 +560,9 @@ void Testbed::set_camera_intrinsics(int frame_idx, float fx, float fy, float cx,
 void Testbed::free_device_dataset() {
 	for (void* p : m_dev_pixels) (void)hipFree(p);
 	m_dev_pixels.clear();
+	for (void* p : m_dev_depths)
+		if (p) (void)hipFree(p);
+	m_dev_depths.clear();
 	if (m_dev_meta) (void)hipFree(m_dev_meta);
 	m_dev_meta = nullptr;
 }
@@ -586,6 +618,7 @@ void Testbed::upload_metadata() {
 		ngp_image& im = meta[i];
 		std::memset(&im, 0, sizeof(im));
 		im.pixels = (uint64_t)(uintptr_t)m_dev_pixels[i];
+		im.depth = i < m_dev_depths.size() ? (uint64_t)(uintptr_t)m_dev_depths[i] : 0;
 		im.width = (uint32_t)ds.metadata[i].resolution[0];
 		im.height = (uint32_t)ds.metadata[i].resolution[1];
 		for (int k = 0; k < 2; ++k) {
@@ -607,9 +640,15 @@ void Testbed::upload_dataset() {
 		if (ds.pixels[i].empty()) throw std::runtime_error("Training image " + std::to_string(i) + " has no pixels.");
 	free_device_dataset();
 	m_dev_pixels.resize(ds.n_images, nullptr);
+	m_dev_depths.assign(ds.n_images, nullptr);
 	for (size_t i = 0; i < ds.n_images; ++i) {
 		hk(hipMalloc(&m_dev_pixels[i], ds.pixels[i].size()), "hipMalloc image");
 		hk(hipMemcpy(m_dev_pixels[i], ds.pixels[i].data(), ds.pixels[i].size(), hipMemcpyHostToDevice), "upload image");
+		if (i < ds.depths.size() && !ds.depths[i].empty()) {
+			const size_t nb = ds.depths[i].size() * sizeof(float);
+			hk(hipMalloc(&m_dev_depths[i], nb), "hipMalloc depth");
+			hk(hipMemcpy(m_dev_depths[i], ds.depths[i].data(), nb, hipMemcpyHostToDevice), "upload depth");
+		}
 	}
 	upload_metadata();
 	m_dataset_dirty = false;
@@ -905,6 +944,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.optimize_encoding = train_encoding;
 	a.defer_optimizer = m_world > 1 ? 1 : 0;
 	a.full_forward = train_full_forward ? 1 : 0;
+	a.depth_supervision_lambda = tr.depth_supervision_lambda;
+	a.depth_loss_type = (int32_t)tr.depth_loss_type;
 	for (size_t i = 0; i < tr.dataset.metadata.size(); ++i)
 		if (tr.dataset.metadata[i].lens.mode != ELensMode::Perspective) a.has_lens = 1;
 	if (m_err && tr.error_map.resolution[0] > 0 && tr.error_map.resolution[1] > 0) {

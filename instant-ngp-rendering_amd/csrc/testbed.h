@@ -54,6 +54,9 @@ struct NerfDataset {
 	std::vector<Mat43> xforms;
 	std::vector<std::string> paths;
 	std::vector<std::vector<uint8_t>> pixels;  // RGBA8, sRGB, straight alpha (EImageDataType::Byte)
+	// per image [h][w] depth targets = 16-bit depth x integer_depth_scale x scale (src/nerf_loader.cu:73-82,
+	// 625-637, 728); empty (or missing) = no depth for that image
+	std::vector<std::vector<float>> depths;
 	vec3 up = {0.f, 1.f, 0.f};
 	vec3 offset = {0.5f, 0.5f, 0.5f};
 	float scale = 0.33f;
@@ -99,6 +102,9 @@ struct NerfTraining {
 	bool sample_focal_plane_proportional_to_error = false;
 	bool sample_image_proportional_to_error = false;
 	bool include_sharpness_in_error = false;  // not supported (no per-image sharpness data)
+	// depth supervision (nerf.h:99,125): weight of the depth loss and its type
+	float depth_supervision_lambda = 0.f;
+	ELossType depth_loss_type = ELossType::L1;
 	// per-image exposure optimisation (Nerf::Training::cam_exposure, nerf.h:65-79, 87-91)
 	struct Adam3 {
 		vec3 variable = {0.f, 0.f, 0.f}, m = {0.f, 0.f, 0.f}, v = {0.f, 0.f, 0.f};
@@ -284,6 +290,7 @@ private:
 	uint64_t m_rng_state = 0, m_rng_inc = 0;
 	// device dataset
 	std::vector<void*> m_dev_pixels;
+	std::vector<void*> m_dev_depths;  // per image f32 depth targets (null: none)
 	void* m_dev_meta = nullptr;
 	bool m_dataset_dirty = true;
 	// render buffers

@@ -553,6 +553,9 @@ struct LossArgs {
 	const uint32_t* ray_eval;  // [R] samples the chunked forward evaluated (null: all of them)
 	uint32_t* violations;      // rays whose composite reached past the evaluated samples (must stay 0)
 	int store_uv_pdf;          // camera gradients: ray_aux[i].w = the pixel's pdf
+	float depth_lambda;        // depth supervision (0: off)
+	int depth_loss_type;
+	float2* ray_depth;         // [R]: composited depth, lambda * dloss/ddepth (k_loss_composite -> k_loss_emit)
 };
 
 // Wave scans over the 64 lanes (inclusive).
@@ -590,6 +593,19 @@ __device__ __forceinline__ LossSample loss_sample(const LossArgs& a, size_t src)
 	return q;
 }
 
+// |rays_in_unnormalized[i].d| of the training ray through (u, v): the target depth is the depth
+// image's value (along the optical axis) times it (src/testbed_nerf.cu:1013); the camera's
+// rotation keeps lengths, so the camera-space direction's length is the one
+template <bool GENERAL>
+__device__ __forceinline__ float unnormalized_dir_length(const ngp_image& im, float u, float v) {
+	v3 dir = mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
+	             (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+	if (GENERAL && !lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1],
+	                               im.principal_point[0], im.principal_point[1], im.lens_mode, im.lens_params, &dir))
+		return 1.0f;  // no ray through the pixel: the camera axis (src/testbed_nerf.cu:762-764)
+	return length(dir);
+}
+
 // compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1160), pass 1: one wave per ray,
 // 64 samples per iteration.  Transmittance T_j = prod_{i<j}(1 - alpha_i) comes from a
 // multiplicative wave scan, the colour from an additive one; the ray stops at the first
@@ -606,6 +622,10 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	}
 	float T = 1.0f;
 	v3 rgb_ray = mk3(0.0f);
+	float depth_ray = 0.0f;  // depth supervision: sum of weight x distance from the origin
+	const bool depth_on = a.depth_lambda > 0.0f;
+	v3 ray_o = mk3(0.0f);
+	if (depth_on) ray_o = mk3(a.ray_state[8 * (size_t)i + 0], a.ray_state[8 * (size_t)i + 1], a.ray_state[8 * (size_t)i + 2]);
 	uint32_t c = numsteps;
 	// the chunked forward evaluated at least every sample before this ray's stop
 	const uint32_t evaluated = a.ray_eval ? (a.ray_eval[i] & ~RAY_EVAL_DONE) : numsteps;
@@ -625,6 +645,15 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 		rgb_ray.x += __shfl(wave_scan_add(q.rgb.x * w, lane), 63, 64);
 		rgb_ray.y += __shfl(wave_scan_add(q.rgb.y * w, lane), 63, 64);
 		rgb_ray.z += __shfl(wave_scan_add(q.rgb.z * w, lane), 63, 64);
+		if (depth_on) {
+			float wd = 0.0f;
+			if (w != 0.0f) {
+				const size_t src = (size_t)base + j;
+				const v3 pos = unwarp_position(mk3(a.coords[8 * src], a.coords[8 * src + 1], a.coords[8 * src + 2]), a.aabb);
+				wd = w * length(pos - ray_o);
+			}
+			depth_ray += __shfl(wave_scan_add(wd, lane), 63, 64);
+		}
 		if (term) {
 			c = kb + first;
 			break;
@@ -687,6 +716,21 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	ls[3] = rgb_ray.x; ls[4] = rgb_ray.y; ls[5] = rgb_ray.z;
 	ls[6] = mean_loss;
 	ls[7] = __uint_as_float(img);  // the error deposit (k_loss_emit) reuses the pixel
+	if (depth_on) {
+		// target depth and lambda * dloss/ddepth (src/testbed_nerf.cu:1013-1015); 0 for images without depth
+		float dlg = 0.0f;
+		if (im.depth) {
+			int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
+			px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
+			py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
+			const float target = unnormalized_dir_length<GENERAL>(im, u, v) *
+			                     reinterpret_cast<const float*>(im.depth)[(size_t)px + (size_t)py * im.width];
+			float ld, gd;
+			loss_and_gradient(target, depth_ray, a.depth_loss_type, &ld, &gd);
+			if (target > 0.0f) dlg = a.depth_lambda * gd;
+		}
+		a.ray_depth[i] = make_float2(depth_ray, dlg);
+	}
 	if (a.exposure_grad) {
 		// symmetric loss: dL/dtarget = -dL/dprediction (src/testbed_nerf.cu:1121-1134)
 		v3 dgt = mk3(-gx / uv_pdf, -gy / uv_pdf, -gz / uv_pdf);
@@ -759,6 +803,9 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 
 	v3 acc = mk3(0.0f);
 	float T = 1.0f;
+	// depth supervision: the ray's composited depth and lambda * dloss/ddepth (0: no term)
+	const float2 rdep = a.depth_lambda > 0.0f ? a.ray_depth[i] : make_float2(0.0f, 0.0f);
+	float dacc = 0.0f;
 	for (uint32_t kb = 0; kb < cn; kb += 64) {
 		const uint32_t j = kb + lane;
 		const bool active = j < cn;
@@ -774,11 +821,15 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		const v3 pre = mk3(wave_scan_add(q.rgb.x * weight, lane), wave_scan_add(q.rgb.y * weight, lane),
 		                   wave_scan_add(q.rgb.z * weight, lane));
 		const v3 rgb_ray2 = acc + pre;
+		float depth = 0.0f;
+		if (active) {
+			const float4 c0 = *reinterpret_cast<const float4*>(a.coords + 8 * src);
+			depth = length(unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb) - ray_o);
+		}
+		// depth supervision: inclusive prefix of weight x depth over the ray's samples (depth_ray2)
+		const float dpre = rdep.y != 0.0f ? wave_scan_add(weight * depth, lane) : 0.0f;
 		if (active) {
 			a.csrc[dst] = (uint32_t)src;
-			const float4 c0 = *reinterpret_cast<const float4*>(a.coords + 8 * src);
-			const v3 pos = unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb);
-			const float depth = length(pos - ray_o);
 			const v3 suffix = rgb_ray - rgb_ray2;
 			const v3 dloss_by_drgb = grad * weight;
 			const float o0 = q.raw[0], o1 = q.raw[1], o2 = q.raw[2], o3 = q.raw[3];
@@ -787,12 +838,16 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 			dl[1] = __float2half(loss_scale * (dloss_by_drgb.y * network_to_rgb_derivative(o1, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o1)));
 			dl[2] = __float2half(loss_scale * (dloss_by_drgb.z * network_to_rgb_derivative(o2, a.rgb_act) + fmaxf(0.0f, output_l2_reg * o2)));
 			const float density_derivative = network_to_density_derivative(o3, a.density_act);
-			const float dloss_by_dmlp = density_derivative * (q.dt * dot(grad, q.rgb * Tnext - suffix));
+			const float drgb = dot(grad, q.rgb * Tnext - suffix);
+			// depth_supervision = lambda dloss/ddepth x (T depth - depth suffix)  (src/testbed_nerf.cu:1098-1103)
+			const float dsum = rdep.y != 0.0f ? drgb + rdep.y * (Tnext * depth - (rdep.x - (dacc + dpre))) : drgb;
+			const float dloss_by_dmlp = density_derivative * (q.dt * dsum);
 			dl[3] = __float2half(loss_scale * dloss_by_dmlp + (o3 < 0.0f ? -output_l1_reg_density : 0.0f) +
 			                     (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
 			*reinterpret_cast<uint2*>(a.dloss + 4 * dst) = *reinterpret_cast<const uint2*>(dl);
 		}
 		acc = acc + mk3(__shfl(pre.x, 63, 64), __shfl(pre.y, 63, 64), __shfl(pre.z, 63, 64));
+		if (rdep.y != 0.0f) dacc += __shfl(dpre, 63, 64);
 		T *= __shfl(incl, 63, 64);
 	}
 }
@@ -1278,6 +1333,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.violations = ts.counters.ptr + 9;
 	const bool cam = t->cam_pos_gradient && t->cam_rot_gradient;
 	la.store_uv_pdf = cam ? 1 : 0;
+	la.depth_lambda = t->depth_supervision_lambda > 0.0f ? t->depth_supervision_lambda : 0.0f;
+	la.depth_loss_type = t->depth_loss_type;
+	if (la.depth_lambda > 0.0f) {
+		ts.ray_depth.reserve(2 * (size_t)R);
+		la.ray_depth = reinterpret_cast<float2*>(ts.ray_depth.ptr);
+	}
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
 	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
 	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);

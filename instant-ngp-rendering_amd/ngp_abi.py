@@ -41,7 +41,7 @@ class Image(C.Structure):
     _fields_ = [
         ("pixels", C.c_uint64), ("width", C.c_uint32), ("height", C.c_uint32),
         ("focal_length", C.c_float * 2), ("principal_point", C.c_float * 2), ("xform", C.c_float * 12),
-        ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7),
+        ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7), ("depth", C.c_uint64),
     ]
 
 
@@ -60,6 +60,7 @@ class TrainArgs(C.Structure):
         ("cdf_y", C.c_void_p), ("cdf_img", C.c_void_p), ("cdf_res", C.c_uint32 * 2), ("has_lens", C.c_int32),
         ("exposure", C.c_void_p), ("exposure_gradient", C.c_void_p),
         ("cam_pos_gradient", C.c_void_p), ("cam_rot_gradient", C.c_void_p), ("full_forward", C.c_int32),
+        ("depth_supervision_lambda", C.c_float), ("depth_loss_type", C.c_int32),
     ]
 
 

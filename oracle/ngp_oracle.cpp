@@ -919,7 +919,7 @@ static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, P
 // first lattice point n0 = to_stepping_space(t_entry) + random; t_entry and the random offset
 // are returned too (the literal transcription below starts from them).
 static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st, float* t_entry = nullptr,
-                      float* jitter = nullptr) {
+                      float* jitter = nullptr, float* dlen = nullptr) {
 	Pcg rng;
 	rng.state = a.rng_state;
 	rng.inc = a.rng_inc;
@@ -938,6 +938,7 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	else
 		dir = x.c[2];  // src/testbed_nerf.cu:762-764
 	*o = x.c[3];
+	if (dlen) *dlen = len(dir);  // |rays_in_unnormalized[i].d| (src/testbed_nerf.cu:1013)
 	*d = normalize(dir);
 	const Box b{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
 	float t0, t1;
@@ -1016,11 +1017,11 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	// pass 1: count (testbed_nerf.cu:779-799)
 	std::vector<uint32_t> cnt(R, 0);
 	std::vector<V3> ro(R), rd(R);
-	std::vector<float> rst(R);
+	std::vector<float> rst(R), rdl(R, 1.0f);
 	for (uint32_t i = 0; i < R; ++i) {
 		V3 o, d;
 		float t;
-		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t)) continue;
+		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t, nullptr, nullptr, &rdl[i])) continue;
 		ro[i] = o; rd[i] = d; rst[i] = t;
 		cnt[i] = training_walk(stp, box, M.bits.data(), a.max_cascade, o, d, t, STEPS,
 		                       [](uint32_t, uint32_t, float, float, V3) {});
@@ -1060,11 +1061,14 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	std::vector<uint32_t> cc(R, 0);
 	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f), ray_uv_pdf(R, 1.0f);
+	// depth supervision (src/testbed_nerf.cu:1013-1015): composited depth and lambda * dloss/ddepth per ray
+	const bool depth_on = a.depth_supervision_lambda > 0.0f;
+	std::vector<float> ray_depth(R, 0.0f), ray_dlg(R, 0.0f);
 	for (uint32_t i = 0; i < R; ++i) {
 		const uint32_t ns = M.ray_numsteps[2 * i], b0 = M.ray_numsteps[2 * i + 1];
 		if (ns == 0) continue;
 		float T = 1.0f;
-		float rr = 0, rg = 0, rb = 0;
+		float rr = 0, rg = 0, rb = 0, dray = 0;
 		uint32_t c = 0;
 		for (; c < ns; ++c) {
 			if (T < 1e-4f) break;
@@ -1075,6 +1079,11 @@ static void train_step(Model& M, const ngp_train_args& a) {
 			rr += w * to_rgb(o[0], ract);
 			rg += w * to_rgb(o[1], ract);
 			rb += w * to_rgb(o[2], ract);
+			if (depth_on) {
+				const float* cw = &M.coords[8 * (size_t)(b0 + c)];
+				const V3 pos = box.mn + v(cw[0] * (box.mx.x - box.mn.x), cw[1] * (box.mx.y - box.mn.y), cw[2] * (box.mx.z - box.mn.z));
+				dray += w * len(pos - ro[i]);
+			}
 			T *= 1.0f - alpha;
 		}
 		const uint32_t gi = a.ray_index_offset + i;
@@ -1119,6 +1128,15 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		ls[0] = gx; ls[1] = gy; ls[2] = gz; ls[3] = rr; ls[4] = rg; ls[5] = rb;
 		ls[6] = (lx / pdf + ly / pdf + lz / pdf) / 3.0f;  // lg.loss /= img_pdf * uv_pdf (src/testbed_nerf.cu:1010)
 		ls[7] = (float)img;
+		if (depth_on && im.depth) {
+			const int px = std::min(std::max((int)(u * (float)im.width), 0), (int)im.width - 1);
+			const int py = std::min(std::max((int)(vv * (float)im.height), 0), (int)im.height - 1);
+			const float target = rdl[i] * reinterpret_cast<const float*>(im.depth)[(size_t)px + (size_t)py * im.width];
+			float ld, gd;
+			lossg(target, dray, a.depth_loss_type, &ld, &gd);
+			ray_depth[i] = dray;
+			ray_dlg[i] = target > 0.0f ? a.depth_supervision_lambda * gd : 0.0f;
+		}
 		if (a.exposure_gradient) {  // src/testbed_nerf.cu:1121-1134, deposited below for kept rays
 			const float g[3] = {gx, gy, gz}, t3[3] = {tgt.x, tgt.y, tgt.z};
 			for (int k = 0; k < 3; ++k) {
@@ -1176,7 +1194,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		}
 		const uint32_t b0 = M.ray_numsteps[2 * i + 1];
 		const V3 o = ro[i];
-		float T = 1.0f, r2 = 0, g2 = 0, b2 = 0;
+		float T = 1.0f, r2 = 0, g2 = 0, b2 = 0, d2 = 0;
 		for (uint32_t j = 0; j < cn; ++j) {
 			const size_t s = b0 + j, dst = cb + j;
 			for (int k = 0; k < 8; ++k) M.ccoords[8 * dst + k] = M.coords[8 * s + k];
@@ -1195,7 +1213,9 @@ static void train_step(Model& M, const ngp_train_args& a) {
 			const float suf[3] = {ls[3] - r2, ls[4] - g2, ls[5] - b2};
 			uint16_t* dl = &M.dloss[4 * dst];
 			for (int k = 0; k < 3; ++k) dl[k] = f2h(loss_scale * (w * ls[k] * to_rgb_d(ob[k], ract) + std::max(0.0f, l2r * ob[k])));
-			const float ddm = to_density_d(ob[3], dact) * (dt * (ls[0] * (T * rgb[0] - suf[0]) + ls[1] * (T * rgb[1] - suf[1]) + ls[2] * (T * rgb[2] - suf[2])));
+			d2 += w * depth;
+			const float dsup = ray_dlg[i] * (T * depth - (ray_depth[i] - d2));  // depth_supervision (:1098-1100)
+			const float ddm = to_density_d(ob[3], dact) * (dt * (ls[0] * (T * rgb[0] - suf[0]) + ls[1] * (T * rgb[1] - suf[1]) + ls[2] * (T * rgb[2] - suf[2]) + dsup));
 			dl[3] = f2h(loss_scale * ddm + (ob[3] < 0.0f ? -l1d : 0.0f) + (ob[3] > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
 		}
 	}

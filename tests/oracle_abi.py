@@ -133,6 +133,9 @@ class Oracle:
         self.lib.oref_model_get(self.h, kind, ptr(out))
         return out
 
+    def zero_grads(self):
+        self.lib.oref_zero_grads(self.h)
+
     def set_grads(self, g):
         g = np.ascontiguousarray(g, np.float32)
         assert g.size == self.n_params

@@ -41,7 +41,7 @@ def make_views(n_images=6, W=24, H=24, seed=0):
     return imgs, cams, focal
 
 
-def image_structs(imgs, cams, focal, pointers, lens=(0, ())):
+def image_structs(imgs, cams, focal, pointers, lens=(0, ()), depth_pointers=None):
     n = len(imgs)
     arr = (A.Image * n)()
     for i in range(n):
@@ -53,6 +53,7 @@ def image_structs(imgs, cams, focal, pointers, lens=(0, ())):
         xf = np.asarray(cams[i], np.float32).T.reshape(-1)  # column-major 4x3
         for k in range(12):
             arr[i].xform[k] = float(xf[k])
+        arr[i].depth = int(depth_pointers[i]) if depth_pointers is not None and depth_pointers[i] else 0
         arr[i].lens_mode = lens[0]
         for k, val in enumerate(lens[1]):
             arr[i].lens_params[k] = float(val)
@@ -60,9 +61,12 @@ def image_structs(imgs, cams, focal, pointers, lens=(0, ())):
 
 
 class HostDataset:
-    def __init__(self, imgs, cams, focal, lens=(0, ())):
+    def __init__(self, imgs, cams, focal, lens=(0, ()), depths=None):
+        """depths: optional per-image [H][W] f32 depth targets (None entries: no depth)."""
         self.imgs = [np.ascontiguousarray(im) for im in imgs]
-        self.arr = image_structs(imgs, cams, focal, [im.ctypes.data for im in self.imgs], lens)
+        self.depths = [None if d is None else np.ascontiguousarray(d, np.float32) for d in depths] if depths else None
+        dp = [0 if d is None else d.ctypes.data for d in self.depths] if self.depths else None
+        self.arr = image_structs(imgs, cams, focal, [im.ctypes.data for im in self.imgs], lens, dp)
         self.n = len(imgs)
 
     @property
@@ -71,10 +75,13 @@ class HostDataset:
 
 
 class DeviceDataset:
-    def __init__(self, imgs, cams, focal, lens=(0, ())):
+    def __init__(self, imgs, cams, focal, lens=(0, ()), depths=None):
         import torch
         self.pix = [torch.from_numpy(np.ascontiguousarray(im)).cuda() for im in imgs]
-        arr = image_structs(imgs, cams, focal, [p.data_ptr() for p in self.pix], lens)
+        self.depths = [None if d is None else torch.from_numpy(np.ascontiguousarray(d, np.float32)).cuda() for d in depths] \
+            if depths else None
+        dp = [0 if d is None else d.data_ptr() for d in self.depths] if self.depths else None
+        arr = image_structs(imgs, cams, focal, [p.data_ptr() for p in self.pix], lens, dp)
         self.meta = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
         self.n = len(imgs)
 

@@ -503,6 +503,54 @@ def test_train_step_exposure_matches_oracle():
         g.close()
 
 
+@pytest.mark.parametrize("loss_type", [1, 0], ids=["L1", "L2"])
+def test_train_step_depth_supervision_matches_oracle(loss_type):
+    """Depth supervision (compute_loss_kernel_train_nerf, src/testbed_nerf.cu:1013-1015, 1098-1103):
+    images with a depth target add lambda * dloss(|d_unnormalised| x depth(uv), composited depth)
+    to dL/d(density) through the depth suffix; images without one add nothing.  dL/dout of the
+    kept rays and the weight gradients against the oracle, and the density gradient must differ
+    from the same step without supervision."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        depths = [rng.uniform(0.8, 2.5, (24, 24)).astype(np.float32) if k % 2 == 0 else None for k in range(6)]
+        hd, dd = HostDataset(imgs, cams, focal, depths=depths), DeviceDataset(imgs, cams, focal, depths=depths)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 384, 4096, 1 << 15
+        out = {}
+        for lam in (0.0, 0.3):
+            ga = train_args(dd.ptr, dd.n, R, B, MS)
+            oa = train_args(hd.ptr, hd.n, R, B, MS)
+            for a_ in (ga, oa):
+                a_.depth_supervision_lambda, a_.depth_loss_type = lam, loss_type
+            g.zero_grads()
+            o.zero_grads()
+            A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+            torch.cuda.synchronize()
+            o.train_step(oa)
+            g_cp = gpu_scratch(g, A.SCRATCH_RAY_COMPACTED, np.uint32).reshape(-1, 2)
+            o_cp = o.scratch(A.SCRATCH_RAY_COMPACTED, np.uint32).reshape(-1, 2)
+            match = np.all(g_cp == o_cp, axis=1) & (o_cp[:, 0] > 0)
+            assert match.mean() > 0.9 * (o_cp[:, 0] > 0).mean()
+            rows = np.concatenate([np.arange(b, b + n) for n, b in o_cp[match] if b + n <= B])
+            g_dl = gpu_scratch(g, A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[rows].astype(np.float32)
+            o_dl = o.scratch(A.SCRATCH_DLOSS, np.float16).reshape(-1, 4)[rows].astype(np.float32)
+            assert np.linalg.norm(g_dl - o_dl) / np.linalg.norm(o_dl) < 2e-2
+            gg, og = g.grads(), o.get(A.GRADS_FP32)
+            rel = np.linalg.norm(gg - og) / np.linalg.norm(og)
+            assert rel < 5e-2, rel
+            out[lam] = (rows, o_dl)
+        r0, d0 = out[0.0]
+        r1, d1 = out[0.3]
+        common = np.intersect1d(r0, r1)
+        i0, i1 = np.searchsorted(r0, common), np.searchsorted(r1, common)
+        # the depth term changes dL/d(density) (column 3), never the colour columns
+        np.testing.assert_array_equal(d0[i0, :3], d1[i1, :3])
+        assert np.abs(d0[i0, 3] - d1[i1, 3]).max() > 0
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B], ids=["A", "B"])
 def test_train_step_cam_gradient_matches_oracle(cfg_kw):
     """compute_cam_gradient_train_nerf (src/testbed_nerf.cu:1163-1269): per-image translation and

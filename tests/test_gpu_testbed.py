@@ -311,3 +311,66 @@ def test_extrinsic_optimisation_recovers_perturbed_pose(scene, tmp_path):
     tb2.load_snapshot(snap)
     np.testing.assert_allclose(np.asarray(tb2.nerf.training.cam_pos_offset), pos, atol=1e-7)
     np.testing.assert_allclose(tb2.nerf.training.get_camera_extrinsics(k), cur, atol=1e-6)
+
+
+def test_depth_supervision_through_the_testbed(scene, tmp_path):
+    """transforms.json depth_path + integer_depth_scale (src/nerf_loader.cu:486-488, 625-637) ->
+    the Testbed uploads the scaled depth targets with the images, and depth_supervision_lambda > 0
+    adds the depth term to the density gradients (src/testbed_nerf.cu:1098-1103).  From one
+    snapshot, one training step's MLP update (deterministic: fixed-order gradient reduction) differs
+    between lambda 1 and lambda 0 on the scene with depth images, and is bit-identical between
+    lambda 1 and lambda 0 on the scene without them."""
+    import shutil
+    from test_gpu_distributed import _params
+    from test_loader import _write_png16_gray
+    root, cams, imgs = scene
+    src = json.load(open(os.path.join(root, "transforms_train.json")))
+    droot = tmp_path / "with_depth"
+    droot.mkdir()
+    rng = np.random.default_rng(0)
+    for k, f in enumerate(src["frames"]):
+        p = f["file_path"] + ("" if f["file_path"].endswith(".png") else ".png")
+        os.makedirs(os.path.dirname(str(droot / p)), exist_ok=True)
+        shutil.copy(os.path.join(root, p), str(droot / p))
+        _write_png16_gray(str(droot / f"depth_{k}.png"), rng.integers(3000, 9000, (64, 64)).astype(np.uint16))
+        f["depth_path"] = f"depth_{k}.png"
+    src["integer_depth_scale"] = 1e-3
+    (droot / "transforms_train.json").write_text(json.dumps(src))
+
+    snap = str(tmp_path / "start.ingp")
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    tb.shall_train = True
+    while tb.training_step < 60:
+        tb.frame()
+    tb.save_snapshot(snap, True)
+    n_mlp = None
+    after = {}
+    for label, path, lam in (("plain_l0", os.path.join(root, "transforms_train.json"), 0.0),
+                             ("plain_l1", os.path.join(root, "transforms_train.json"), 1.0),
+                             ("depth_l0", str(droot / "transforms_train.json"), 0.0),
+                             ("depth_l1", str(droot / "transforms_train.json"), 1.0)):
+        ngp, tb = new_testbed()
+        tb.load_training_data(path)
+        tb.reload_network_from_file("tiny_L4F2.json")
+        tb.load_snapshot(snap)
+        ds = tb.nerf.training.dataset
+        assert (ds.depth(0) is not None) == label.startswith("depth")
+        if label.startswith("depth"):
+            np.testing.assert_allclose(ds.depth(0).mean(), 6.0e-3 * 1000 * ds.scale, rtol=0.05)
+        tb.nerf.training.depth_supervision_lambda = lam
+        tb.shall_train = True
+        start = tb.training_step
+        tb.frame()
+        assert tb.training_step == start + 1
+        if n_mlp is None:
+            import ctypes as C
+            import ngp_abi as A
+            info = A.ModelInfo()
+            A.check(A.load().ngp_model_get_info(C.c_void_p(tb.model_handle), C.byref(info)))
+            n_mlp = int(info.n_mlp_params)
+        after[label] = _params(tb)[:n_mlp]
+    assert np.isfinite(after["depth_l1"]).all()
+    np.testing.assert_array_equal(after["plain_l1"], after["plain_l0"])
+    assert np.abs(after["depth_l1"] - after["depth_l0"]).max() > 0, "depth supervision had no effect"

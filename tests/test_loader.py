@@ -99,3 +99,48 @@ def test_missing_files_and_empty_sets_raise(ngp, tmp_path):
         {"file_path": "missing.png", "sharpness": 3.0, "transform_matrix": np.eye(4).tolist()}]}))
     with pytest.raises((RuntimeError, ValueError), match="No training images"):
         ngp.load_nerf_dataset(str(tmp_path / "s.json"))
+
+
+def _write_png16_gray(path, arr):
+    """Minimal 16-bit grayscale PNG writer (zlib, filter 0) for the depth fixtures."""
+    import struct
+    import zlib
+    h, w = arr.shape
+    raw = b"".join(b"\x00" + arr[y].astype(">u2").tobytes() for y in range(h))
+
+    def chunk(t, data):
+        return struct.pack(">I", len(data)) + t + data + struct.pack(">I", zlib.crc32(t + data) & 0xFFFFFFFF)
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 16, 0, 0, 0, 0))
+                + chunk(b"IDAT", zlib.compress(raw)) + chunk(b"IEND", b""))
+
+
+def test_depth_images_load_scaled(ngp, tmp_path):
+    """Depth supervision inputs (src/nerf_loader.cu:419-437, 486-488, 625-637, 728): a frame's
+    depth_path is a 16-bit image of the frame's resolution, scaled by integer_depth_scale and the
+    dataset scale; frames without one, a missing file, or enable_depth_loading false give no depth;
+    a wrong resolution is an error."""
+    from PIL import Image
+    w, h = 6, 4
+    rgb = np.zeros((h, w, 4), np.uint8)
+    rgb[..., 3] = 255
+    for k in range(3):
+        Image.fromarray(rgb).save(tmp_path / f"img{k}.png")
+    dep = (np.arange(w * h).reshape(h, w) * 997 % 60000).astype(np.uint16)
+    _write_png16_gray(str(tmp_path / "d0.png"), dep)
+    frames = [{"file_path": f"img{k}.png", "transform_matrix": np.eye(4).tolist()} for k in range(3)]
+    frames[0]["depth_path"] = "d0.png"
+    frames[1]["depth_path"] = "missing.png"
+    meta = {"camera_angle_x": 0.7, "integer_depth_scale": 1e-3, "scale": 0.5, "frames": frames}
+    (tmp_path / "transforms.json").write_text(json.dumps(meta))
+    d = ngp.load_nerf_dataset(str(tmp_path / "transforms.json"))
+    np.testing.assert_allclose(d.depth(0), dep.astype(np.float32) * np.float32(1e-3 * 0.5), rtol=1e-6)
+    assert d.depth(1) is None and d.depth(2) is None
+    meta["enable_depth_loading"] = False
+    (tmp_path / "transforms.json").write_text(json.dumps(meta))
+    assert ngp.load_nerf_dataset(str(tmp_path / "transforms.json")).depth(0) is None
+    meta["enable_depth_loading"] = True
+    _write_png16_gray(str(tmp_path / "d0.png"), dep[:, :3])
+    (tmp_path / "transforms.json").write_text(json.dumps(meta))
+    with pytest.raises(RuntimeError, match="wrong resolution"):
+        ngp.load_nerf_dataset(str(tmp_path / "transforms.json"))
