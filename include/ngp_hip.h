@@ -178,6 +178,15 @@ typedef struct ngp_train_args {
 	 * to dL/d(density) through the depth suffix; depth_loss_type is an ELossType (default L1) */
 	float depth_supervision_lambda;
 	int32_t depth_loss_type;
+	/* sharpness-weighted error deposits (include_sharpness_in_error, src/testbed_nerf.cu:1036-1044,
+	 * 2453-2464): sharpness_data = device [n_images][res_y][res_x] variance of the Laplacian of the
+	 * images' luma (compute_sharpness, src/nerf_loader.cu:111-151); sharpness_grid = device
+	 * [8 cascades][128^3] f32 running max (Morton order), zeroed when sharpness_grid_clear, else
+	 * decayed by 0.95 at the start of the step; null = off */
+	const float* sharpness_data;
+	uint32_t sharpness_res[2];
+	float* sharpness_grid;
+	int32_t sharpness_grid_clear;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {

@@ -212,6 +212,7 @@ struct TrainScratch {
 	DevBuf<float> ray_state;           // [R][8] : o, d (unnormalised), pad
 	DevBuf<float> ray_loss_state;      // [R][8]
 	DevBuf<float> ray_depth;           // [R][2] depth supervision: composited depth, lambda * dloss/ddepth
+	DevBuf<float> ray_hit;             // [R][4] sharpness: composited hit point
 	DevBuf<float> ray_aux;             // [R][4] per-ray dL/dexposure
 	DevBuf<float> coords;              // [max_samples][8]
 	DevBuf<__half> enc;                // [L][max_samples][F]

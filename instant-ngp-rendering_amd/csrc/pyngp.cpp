@@ -227,7 +227,14 @@ PYBIND11_MODULE(pyngp, m) {
 			py::array_t<float> a({md.resolution[1], md.resolution[0]});
 			std::memcpy(a.mutable_data(), d.depths[i].data(), d.depths[i].size() * sizeof(float));
 			return a;
-		}, "depth targets of image i (16-bit depth x integer_depth_scale x scale), or None");
+		}, "depth targets of image i (16-bit depth x integer_depth_scale x scale), or None")
+		.def("sharpness", [](const NerfDataset& d, size_t i) {
+			if (i >= d.n_images) throw std::runtime_error("Invalid frame index");
+			const std::vector<float> s = d.sharpness(i);
+			py::array_t<float> a({72, 128});
+			std::memcpy(a.mutable_data(), s.data(), s.size() * sizeof(float));
+			return a;
+		}, "compute_sharpness of image i: [72][128] variance of the Laplacian of the luma per tile");
 
 	// ngp::load_nerf without a Testbed (no GPU needed): the dataset front end on its own
 	m.def("load_nerf_dataset", [](const std::string& path) {

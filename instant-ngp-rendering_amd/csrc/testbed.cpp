@@ -209,7 +209,7 @@ Testbed::~Testbed() {
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
 	if (m_pack) (void)hipFree(m_pack);
-	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad})
+	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
@@ -557,7 +557,46 @@ void Testbed::set_camera_intrinsics(int frame_idx, float fx, float fy, float cx,
 	m_dataset_dirty = true;
 }
 
+// compute_sharpness (src/nerf_loader.cu:111-151) on the host, from the stored RGBA8 sRGB pixels as
+// read_rgba sees them (linear, premultiplied).  A tile narrower than a pixel (images below 128 x 72)
+// gets 0 where the reference divides by zero.
+std::vector<float> NerfDataset::sharpness(size_t i) const {
+	constexpr int SX = 128, SY = 72;
+	std::vector<float> out((size_t)SX * SY, 0.0f);
+	if (i >= pixels.size() || pixels[i].empty()) return out;
+	const int W = metadata[i].resolution[0], H = metadata[i].resolution[1];
+	const uint8_t* px = pixels[i].data();
+	auto s2l = [](float c) { return c <= 0.04045f ? c / 12.92f : std::pow((c + 0.055f) / 1.055f, 2.4f); };
+	auto luma = [&](int x, int y) {
+		const uint8_t* p = px + 4 * ((size_t)y * W + x);
+		const float a = p[3] * (1.0f / 255.0f);
+		const float r = s2l(p[0] * (1.0f / 255.0f)) * a, g = s2l(p[1] * (1.0f / 255.0f)) * a, b = s2l(p[2] * (1.0f / 255.0f)) * a;
+		return r * 0.2126f + g * 0.7152f + b * 0.0722f;
+	};
+	for (int y = 0; y < SY; ++y)
+		for (int x = 0; x < SX; ++x) {
+			int x1 = (x * W) / SX, x2 = ((x + 1) * W) / SX, y1 = (y * H) / SY, y2 = ((y + 1) * H) / SY;
+			x1 = std::max(x1, 1); y1 = std::max(y1, 1);
+			x2 = std::min(x2, W - 2); y2 = std::min(y2, H - 2);
+			if (x2 <= x1 || y2 <= y1) continue;
+			float tot_lap = 0.f, tot_lap2 = 0.f;
+			const float scal = 1.f / (float)((x2 - x1) * (y2 - y1));
+			for (int yy = y1; yy < y2; ++yy)
+				for (int xx = x1; xx < x2; ++xx) {
+					const float lap = luma(xx, yy) * 4.f - luma(xx, yy - 1) - luma(xx + 1, yy) - luma(xx, yy + 1) - luma(xx - 1, yy);
+					tot_lap += lap;
+					tot_lap2 += lap * lap;
+				}
+			tot_lap *= scal;
+			tot_lap2 *= scal;
+			out[(size_t)y * SX + x] = tot_lap2 - tot_lap * tot_lap;
+		}
+	return out;
+}
+
 void Testbed::free_device_dataset() {
+	if (m_dev_sharpness) (void)hipFree(m_dev_sharpness);
+	m_dev_sharpness = nullptr;
 	for (void* p : m_dev_pixels) (void)hipFree(p);
 	m_dev_pixels.clear();
 	for (void* p : m_dev_depths)
@@ -953,8 +992,27 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 		a.error_map_res[0] = (uint32_t)tr.error_map.resolution[0];
 		a.error_map_res[1] = (uint32_t)tr.error_map.resolution[1];
 	}
+	if (tr.include_sharpness_in_error && a.error_map) {
+		// dataset sharpness (computed on first use) and the running-max grid (src/testbed_nerf.cu:2453-2464)
+		const size_t per = (size_t)128 * 72;
+		if (!m_dev_sharpness) {
+			std::vector<float> all(per * tr.dataset.n_images);
+			for (size_t i = 0; i < tr.dataset.n_images; ++i) {
+				const std::vector<float> sh = tr.dataset.sharpness(i);
+				std::copy(sh.begin(), sh.end(), all.begin() + per * i);
+			}
+			hk(hipMalloc((void**)&m_dev_sharpness, std::max<size_t>(all.size(), 1) * sizeof(float)), "hipMalloc sharpness");
+			hk(hipMemcpy(m_dev_sharpness, all.data(), all.size() * sizeof(float), hipMemcpyHostToDevice), "upload sharpness");
+		}
+		const bool fresh = !m_sharp_grid;
+		if (fresh) hk(hipMalloc((void**)&m_sharp_grid, (size_t)128 * 128 * 128 * 8 * sizeof(float)), "hipMalloc sharpness grid");
+		a.sharpness_data = m_dev_sharpness;
+		a.sharpness_res[0] = 128;
+		a.sharpness_res[1] = 72;
+		a.sharpness_grid = m_sharp_grid;
+		a.sharpness_grid_clear = (fresh || training_step == 0) ? 1 : 0;
+	}
 	if (tr.error_map.is_cdf_valid) {
-		if (tr.include_sharpness_in_error) throw std::runtime_error("include_sharpness_in_error is not supported by this build");
 		if (tr.sample_focal_plane_proportional_to_error) {
 			a.cdf_x_cond_y = m_cdf_x;
 			a.cdf_y = m_cdf_y;

@@ -66,6 +66,9 @@ struct NerfDataset {
 	size_t n_images = 0;
 	// nerf_loader.h:95-116
 	Mat43 nerf_matrix_to_ngp(const float* nerf_3x4_rowmajor, bool scale_columns = false) const;
+	// compute_sharpness (src/nerf_loader.cu:111-151) of image i: [72][128] variance of the Laplacian of
+	// the luma of the linear, premultiplied pixels per tile (sharpness_resolution {128, 72}, :156)
+	std::vector<float> sharpness(size_t i) const;
 	Mat43 ngp_matrix_to_nerf(const Mat43& m, bool scale_columns = false) const;
 };
 
@@ -292,6 +295,8 @@ private:
 	std::vector<void*> m_dev_pixels;
 	std::vector<void*> m_dev_depths;  // per image f32 depth targets (null: none)
 	void* m_dev_meta = nullptr;
+	float* m_dev_sharpness = nullptr;  // [n_images][72][128] (include_sharpness_in_error)
+	float* m_sharp_grid = nullptr;     // [8][128^3] running max (Nerf::Training::sharpness_grid)
 	bool m_dataset_dirty = true;
 	// render buffers
 	float* m_frame = nullptr;

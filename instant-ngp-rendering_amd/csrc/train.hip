@@ -556,6 +556,12 @@ struct LossArgs {
 	float depth_lambda;        // depth supervision (0: off)
 	int depth_loss_type;
 	float2* ray_depth;         // [R]: composited depth, lambda * dloss/ddepth (k_loss_composite -> k_loss_emit)
+	// sharpness-weighted error deposits (null sharp_data: off)
+	const float* sharp_data;   // [n_images][res_y][res_x]
+	uint32_t sharp_rx, sharp_ry;
+	float* sharp_grid;         // [8][128^3] running max
+	float4* ray_hit;           // [R]: composited hit point (k_loss_composite -> k_loss_emit)
+	uint32_t max_mip;
 };
 
 // Wave scans over the 64 lanes (inclusive).
@@ -593,6 +599,12 @@ __device__ __forceinline__ LossSample loss_sample(const LossArgs& a, size_t src)
 	return q;
 }
 
+// decay_sharpness_grid_nerf (src/testbed_nerf.cu:278-282)
+__global__ void __launch_bounds__(256) k_scale_floats(float* __restrict__ x, size_t n, float f) {
+	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
+	if (i < n) x[i] *= f;
+}
+
 // |rays_in_unnormalized[i].d| of the training ray through (u, v): the target depth is the depth
 // image's value (along the optical axis) times it (src/testbed_nerf.cu:1013); the camera's
 // rotation keeps lengths, so the camera-space direction's length is the one
@@ -623,6 +635,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	float T = 1.0f;
 	v3 rgb_ray = mk3(0.0f);
 	float depth_ray = 0.0f;  // depth supervision: sum of weight x distance from the origin
+	v3 hit = mk3(0.0f);       // sharpness: sum of weight x position (the reference's hitpoint)
 	const bool depth_on = a.depth_lambda > 0.0f;
 	v3 ray_o = mk3(0.0f);
 	if (depth_on) ray_o = mk3(a.ray_state[8 * (size_t)i + 0], a.ray_state[8 * (size_t)i + 1], a.ray_state[8 * (size_t)i + 2]);
@@ -645,6 +658,16 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 		rgb_ray.x += __shfl(wave_scan_add(q.rgb.x * w, lane), 63, 64);
 		rgb_ray.y += __shfl(wave_scan_add(q.rgb.y * w, lane), 63, 64);
 		rgb_ray.z += __shfl(wave_scan_add(q.rgb.z * w, lane), 63, 64);
+		if (a.sharp_data) {
+			v3 wp = mk3(0.0f);
+			if (w != 0.0f) {
+				const size_t src = (size_t)base + j;
+				wp = unwarp_position(mk3(a.coords[8 * src], a.coords[8 * src + 1], a.coords[8 * src + 2]), a.aabb) * w;
+			}
+			hit.x += __shfl(wave_scan_add(wp.x, lane), 63, 64);
+			hit.y += __shfl(wave_scan_add(wp.y, lane), 63, 64);
+			hit.z += __shfl(wave_scan_add(wp.z, lane), 63, 64);
+		}
 		if (depth_on) {
 			float wd = 0.0f;
 			if (w != 0.0f) {
@@ -716,6 +739,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	ls[3] = rgb_ray.x; ls[4] = rgb_ray.y; ls[5] = rgb_ray.z;
 	ls[6] = mean_loss;
 	ls[7] = __uint_as_float(img);  // the error deposit (k_loss_emit) reuses the pixel
+	if (a.sharp_data) a.ray_hit[i] = make_float4(hit.x, hit.y, hit.z, 0.0f);
 	if (depth_on) {
 		// target depth and lambda * dloss/ddepth (src/testbed_nerf.cu:1013-1015); 0 for images without depth
 		float dlg = 0.0f;
@@ -778,7 +802,23 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		const float u = a.ray_state[8 * (size_t)i + 6], v = a.ray_state[8 * (size_t)i + 7];
 		const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
 		const ngp_image& im = a.images[img];
-		const float mean_loss = a.loss_state[8 * (size_t)i + 6];
+		float mean_loss = a.loss_state[8 * (size_t)i + 6];
+		if (a.sharp_data) {
+			// include_sharpness_in_error (src/testbed_nerf.cu:1039-1047): the pixel's sharpness against the
+			// running max over the grid cell of the ray's hit point (float bits order like uints for >= 0)
+			const float4 h4 = a.ray_hit[i];
+			const v3 hp = mk3(h4.x, h4.y, h4.z);
+			if (aabb_contains(a.aabb, hp)) {
+				int sx = (int)(u * (float)a.sharp_rx), sy = (int)(v * (float)a.sharp_ry);
+				sx = sx < 0 ? 0 : (sx > (int)a.sharp_rx - 1 ? (int)a.sharp_rx - 1 : sx);
+				sy = sy < 0 ? 0 : (sy > (int)a.sharp_ry - 1 ? (int)a.sharp_ry - 1 : sy);
+				const float sharp = a.sharp_data[((size_t)img * a.sharp_ry + sy) * a.sharp_rx + sx] + 1e-6f;
+				const uint32_t mip = mip_from_pos(hp, a.max_mip);
+				float* cell = a.sharp_grid + (size_t)mip * NERF_GRID_N_CELLS + cascaded_grid_idx_at(hp, mip);
+				const float old = __uint_as_float(atomicMax(reinterpret_cast<uint32_t*>(cell), __float_as_uint(sharp)));
+				mean_loss *= fmaxf(sharp / fmaxf(sharp, old), 0.01f);
+			}
+		}
 		const float rx = (float)a.error_map_rx, ry = (float)a.error_map_ry;
 		const float px = fminf(fmaxf(u * rx - 0.5f, 0.0f), rx - (1.0f + 1e-4f));
 		const float py = fminf(fmaxf(v * ry - 0.5f, 0.0f), ry - (1.0f + 1e-4f));
@@ -1334,6 +1374,19 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	const bool cam = t->cam_pos_gradient && t->cam_rot_gradient;
 	la.store_uv_pdf = cam ? 1 : 0;
 	la.depth_lambda = t->depth_supervision_lambda > 0.0f ? t->depth_supervision_lambda : 0.0f;
+	la.max_mip = t->max_cascade;
+	if (t->sharpness_data && t->sharpness_grid && t->error_map) {
+		// train_nerf (src/testbed_nerf.cu:2453-2464): clear at step 0, else decay by 0.95
+		const size_t n_cells = (size_t)NERF_GRID_N_CELLS * NERF_CASCADES;
+		if (t->sharpness_grid_clear) NGP_HIP_CHECK(hipMemsetAsync(t->sharpness_grid, 0, n_cells * sizeof(float), s));
+		else k_scale_floats<<<div_up(n_cells, 256), 256, 0, s>>>(t->sharpness_grid, n_cells, 0.95f);
+		la.sharp_data = t->sharpness_data;
+		la.sharp_rx = t->sharpness_res[0];
+		la.sharp_ry = t->sharpness_res[1];
+		la.sharp_grid = t->sharpness_grid;
+		ts.ray_hit.reserve(4 * (size_t)R);
+		la.ray_hit = reinterpret_cast<float4*>(ts.ray_hit.ptr);
+	}
 	la.depth_loss_type = t->depth_loss_type;
 	if (la.depth_lambda > 0.0f) {
 		ts.ray_depth.reserve(2 * (size_t)R);

@@ -61,6 +61,8 @@ class TrainArgs(C.Structure):
         ("exposure", C.c_void_p), ("exposure_gradient", C.c_void_p),
         ("cam_pos_gradient", C.c_void_p), ("cam_rot_gradient", C.c_void_p), ("full_forward", C.c_int32),
         ("depth_supervision_lambda", C.c_float), ("depth_loss_type", C.c_int32),
+        ("sharpness_data", C.c_void_p), ("sharpness_res", C.c_uint32 * 2), ("sharpness_grid", C.c_void_p),
+        ("sharpness_grid_clear", C.c_int32),
     ]
 
 

@@ -1063,6 +1063,13 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f), ray_uv_pdf(R, 1.0f);
 	// depth supervision (src/testbed_nerf.cu:1013-1015): composited depth and lambda * dloss/ddepth per ray
 	const bool depth_on = a.depth_supervision_lambda > 0.0f;
+	// include_sharpness_in_error (src/testbed_nerf.cu:1036-1044, 2453-2464)
+	const bool sharp_on = a.sharpness_data && a.sharpness_grid && a.error_map;
+	if (sharp_on) {
+		const size_t nc = (size_t)CELLS * CASCADES;
+		for (size_t k = 0; k < nc; ++k) a.sharpness_grid[k] = a.sharpness_grid_clear ? 0.0f : a.sharpness_grid[k] * 0.95f;
+	}
+	std::vector<V3> ray_hit(R, v(0, 0, 0));
 	std::vector<float> ray_depth(R, 0.0f), ray_dlg(R, 0.0f);
 	for (uint32_t i = 0; i < R; ++i) {
 		const uint32_t ns = M.ray_numsteps[2 * i], b0 = M.ray_numsteps[2 * i + 1];
@@ -1079,6 +1086,10 @@ static void train_step(Model& M, const ngp_train_args& a) {
 			rr += w * to_rgb(o[0], ract);
 			rg += w * to_rgb(o[1], ract);
 			rb += w * to_rgb(o[2], ract);
+			if (sharp_on) {
+				const float* cw = &M.coords[8 * (size_t)(b0 + c)];
+				ray_hit[i] = ray_hit[i] + (box.mn + v(cw[0] * (box.mx.x - box.mn.x), cw[1] * (box.mx.y - box.mn.y), cw[2] * (box.mx.z - box.mn.z))) * w;
+			}
 			if (depth_on) {
 				const float* cw = &M.coords[8 * (size_t)(b0 + c)];
 				const V3 pos = box.mn + v(cw[0] * (box.mx.x - box.mn.x), cw[1] * (box.mx.y - box.mn.y), cw[2] * (box.mx.z - box.mn.z));
@@ -1186,7 +1197,19 @@ static void train_step(Model& M, const ngp_train_args& a) {
 			const float wx = px - (float)ix, wy = py - (float)iy;
 			const int cx = std::min(std::max(ix, 0), (int)im.width - 2), cy = std::min(std::max(iy, 0), (int)im.height - 2);
 			float* e = a.error_map + (size_t)img * ex * ey;
-			const float ml = ls[6];
+			float ml = ls[6];
+			const V3 hp = ray_hit[i];
+			if (sharp_on && box.contains(hp)) {
+				const uint32_t srx = a.sharpness_res[0], sry = a.sharpness_res[1];
+				const int sx = std::min(std::max((int)(u * (float)srx), 0), (int)srx - 1);
+				const int sy = std::min(std::max((int)(vv * (float)sry), 0), (int)sry - 1);
+				const float sharp = a.sharpness_data[((size_t)img * sry + sy) * srx + sx] + 1e-6f;
+				const uint32_t mip = mip_pos(hp, a.max_cascade);
+				float& cell = a.sharpness_grid[(size_t)mip * CELLS + grid_idx(hp, mip)];
+				const float old = cell;
+				cell = std::max(old, sharp);
+				ml *= std::max(sharp / std::max(sharp, old), 0.01f);
+			}
 			e[cy * ex + cx] += (1.0f - wx) * (1.0f - wy) * ml;
 			e[cy * ex + cx + 1] += wx * (1.0f - wy) * ml;
 			e[(cy + 1) * ex + cx] += (1.0f - wx) * wy * ml;

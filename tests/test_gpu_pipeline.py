@@ -503,6 +503,58 @@ def test_train_step_exposure_matches_oracle():
         g.close()
 
 
+def test_train_step_sharpness_weighted_error_matches_oracle():
+    """include_sharpness_in_error (src/testbed_nerf.cu:1036-1047, 2453-2464): each kept ray's error
+    deposit is scaled by max(sharp / running max over its hit point's grid cell, 0.01).  From a
+    cleared grid, the running max after the step is order-independent and must equal the oracle's
+    bit for bit; from a grid pre-filled above every sharpness value the factor is sharp / cell, so
+    the error map must match the oracle's within the fp16 network tolerance, and differ from the
+    unweighted map."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 384, 4096, 1 << 15
+        n_cells = 8 * 128 ** 3
+        sharp = rng.exponential(1.0, (6, 9, 11)).astype(np.float32)
+        d_sharp = torch.from_numpy(sharp).cuda()
+        results = {}
+        for mode in ("cleared", "prefilled", "off"):
+            ga = train_args(dd.ptr, dd.n, R, B, MS)
+            oa = train_args(hd.ptr, hd.n, R, B, MS)
+            d_err, h_err = torch.zeros(6, 8, 8, device="cuda"), np.zeros((6, 8, 8), np.float32)
+            ga.error_map, oa.error_map = d_err.data_ptr(), h_err.ctypes.data
+            h_grid = np.full(n_cells, 0.0 if mode == "cleared" else 100.0, np.float32)
+            d_grid = torch.from_numpy(h_grid).cuda()
+            for a_ in (ga, oa):
+                a_.error_map_res[0], a_.error_map_res[1] = 8, 8
+                if mode != "off":
+                    a_.sharpness_res[0], a_.sharpness_res[1] = 11, 9
+                    a_.sharpness_grid_clear = 1 if mode == "cleared" else 0
+            if mode != "off":
+                ga.sharpness_data, oa.sharpness_data = d_sharp.data_ptr(), sharp.ctypes.data
+                ga.sharpness_grid, oa.sharpness_grid = d_grid.data_ptr(), h_grid.ctypes.data
+            g.zero_grads()
+            A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+            torch.cuda.synchronize()
+            o.train_step(oa)
+            results[mode] = (d_err.cpu().numpy(), h_err.copy(), d_grid.cpu().numpy(), h_grid.copy())
+        ge, he, gg, hg = results["cleared"]
+        assert (hg > 0).sum() > 10
+        # the max is order-independent; a hit point (a weighted sum, scanned on the GPU, sequential
+        # in the oracle) within float rounding of a cell face may land in the neighbouring cell
+        assert (gg != hg).sum() <= 2
+        ge, he, gg, hg = results["prefilled"]
+        np.testing.assert_array_equal(gg, hg)  # decayed by 0.95, no cell exceeded
+        assert he.sum() > 0
+        assert np.abs(ge - he).sum() / he.sum() < 3e-2
+        off = results["off"][1]
+        assert np.abs(he - off).sum() / off.sum() > 0.5  # the weighting changed the deposits
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("loss_type", [1, 0], ids=["L1", "L2"])
 def test_train_step_depth_supervision_matches_oracle(loss_type):
     """Depth supervision (compute_loss_kernel_train_nerf, src/testbed_nerf.cu:1013-1015, 1098-1103):

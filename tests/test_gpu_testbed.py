@@ -374,3 +374,25 @@ def test_depth_supervision_through_the_testbed(scene, tmp_path):
     assert np.isfinite(after["depth_l1"]).all()
     np.testing.assert_array_equal(after["plain_l1"], after["plain_l0"])
     assert np.abs(after["depth_l1"] - after["depth_l0"]).max() > 0, "depth supervision had no effect"
+
+
+def test_sharpness_weighted_error_map_through_the_testbed(scene):
+    """include_sharpness_in_error through the Testbed: the dataset's sharpness (computed on first
+    use) and the running-max grid are allocated, cleared at step 0 and decayed every step
+    (src/testbed_nerf.cu:2453-2464); training with error-map importance sampling runs and the error
+    map keeps accumulating."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    tr = tb.nerf.training
+    tr.include_sharpness_in_error = True
+    tr.sample_image_proportional_to_error = True
+    tr.sample_focal_plane_proportional_to_error = True
+    tb.shall_train = True
+    losses = []
+    while tb.training_step < 300:
+        tb.frame()
+        losses.append(tb.loss)
+    assert np.isfinite(losses).all() and losses[-1] < losses[0]
+    assert np.asarray(tr.error_map).sum() > 0

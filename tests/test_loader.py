@@ -144,3 +144,35 @@ def test_depth_images_load_scaled(ngp, tmp_path):
     (tmp_path / "transforms.json").write_text(json.dumps(meta))
     with pytest.raises(RuntimeError, match="wrong resolution"):
         ngp.load_nerf_dataset(str(tmp_path / "transforms.json"))
+
+
+def _sharpness_numpy(rgba8):
+    """compute_sharpness (src/nerf_loader.cu:111-151), restated in numpy: per tile of a 128 x 72
+    grid, the variance of the 5-point Laplacian of the luma of the linear, premultiplied pixels."""
+    c = rgba8.astype(np.float32) / np.float32(255)
+    lin = np.where(c[..., :3] <= 0.04045, c[..., :3] / 12.92, ((c[..., :3] + 0.055) / 1.055) ** 2.4).astype(np.float32)
+    lin = lin * c[..., 3:4]
+    lum = (lin[..., 0] * np.float32(0.2126) + lin[..., 1] * np.float32(0.7152) + lin[..., 2] * np.float32(0.0722)).astype(np.float64)
+    H, W = lum.shape
+    lap = np.zeros_like(lum)
+    lap[1:-1, 1:-1] = 4 * lum[1:-1, 1:-1] - lum[:-2, 1:-1] - lum[2:, 1:-1] - lum[1:-1, :-2] - lum[1:-1, 2:]
+    out = np.zeros((72, 128))
+    for y in range(72):
+        y1, y2 = max(y * H // 72, 1), min((y + 1) * H // 72, H - 2)
+        for x in range(128):
+            x1, x2 = max(x * W // 128, 1), min((x + 1) * W // 128, W - 2)
+            if x2 <= x1 or y2 <= y1:
+                continue
+            t = lap[y1:y2, x1:x2]
+            out[y, x] = (t * t).mean() - t.mean() ** 2
+    return out
+
+
+def test_sharpness_matches_numpy_restatement(ngp):
+    """The per-image sharpness of include_sharpness_in_error (compute_sharpness, 128 x 72 tiles of
+    the variance of the Laplacian) on a frame of the reference's test dataset."""
+    d = ngp.load_nerf_dataset(os.path.join(TEST, "transforms_test.json"))
+    s = d.sharpness(0)
+    ref = _sharpness_numpy(d.image(0))
+    assert s.shape == (72, 128) and ref.max() > 0
+    np.testing.assert_allclose(s, ref, rtol=2e-3, atol=1e-6 * ref.max())
