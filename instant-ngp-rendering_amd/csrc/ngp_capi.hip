@@ -224,12 +224,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		GridState& g = m->gs;
 		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
-		RenderScratch& r = m->rs;
-		for (int b = 0; b < 3; ++b) { r.payload[b].release(); r.rgba[b].release(); r.depth[b].release(); }
-		r.coords.release(); r.enc.release(); r.out.release(); r.counters.release(); r.summary.release();
-		if (r.host_counter.ptr) (void)hipHostFree(r.host_counter.ptr);
-		for (auto& e : r.events)
-			if (e) (void)hipEventDestroy(e);
+		m->rs.release();
 		m->timers.release();
 		delete m;
 	});

@@ -259,24 +259,53 @@ struct GridState {
 	uint64_t version = 0;  // bumped whenever the bitfield may have changed (render caches derive from it)
 };
 
-struct RenderScratch {
-	DevBuf<float> payload[3];   // [n][12]: o(3), d(3), t, max_weight, idx(bits), n_steps(bits), alive(bits), pad
+// One ray pipeline of the tracer: its ray set (alternate 8-row blocks of the frame when two
+// pipelines run), payload ping-pong buffers, pass scratch and counters.
+struct RenderPipeScratch {
+	DevBuf<float> payload[3];   // [n][12]: Payload (render.hip)
 	DevBuf<float> rgba[3];      // [n][4]
 	DevBuf<float> depth[3];     // [n]
-	DevBuf<float> coords;       // [n*8][8]
-	DevBuf<__half> enc;         // [L][n*8][F]
-	DevBuf<__half> out;         // [n*8][4]
-	DevBuf<uint32_t> counters;  // [4]
+	DevBuf<float> coords;       // [max_samples][4] position + warped dt, then [max_samples][8] SH rows
+	DevBuf<__half> enc;         // [L][max_samples][F]
+	DevBuf<__half> out;         // [max_samples][4]
+	DevBuf<uint32_t> counters;  // [16]
 	DevBuf<uint32_t> host_counter;  // pinned, fine-grained (hipHostMalloc): per-pass counters
 	uint32_t* host_counter_dev = nullptr;  // its device address
 	uint32_t pass_tag = 0;          // tags of published passes (monotonic across renders)
+	hipEvent_t events[2] = {nullptr, nullptr};  // per-pass counter read-backs
+	void release() {
+		for (int b = 0; b < 3; ++b) { payload[b].release(); rgba[b].release(); depth[b].release(); }
+		coords.release(); enc.release(); out.release(); counters.release();
+		if (host_counter.ptr) (void)hipHostFree(host_counter.ptr);
+		host_counter.ptr = nullptr;
+		for (auto& e : events)
+			if (e) (void)hipEventDestroy(e);
+	}
+};
+
+struct RenderScratch {
+	static constexpr int MAX_PIPES = 4;
+	RenderPipeScratch pipe[MAX_PIPES];
+	hipStream_t streams[MAX_PIPES] = {};  // pipelines 1.. run on their own streams ([0] unused: the caller's)
+	hipEvent_t fork = nullptr, join[MAX_PIPES] = {};  // caller's stream -> pipeline streams -> caller's stream
 	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
-	hipEvent_t events[2] = {nullptr, nullptr};  // per-pass counter read-backs
 	uint64_t df_version = ~0ull;
 	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;
+	void release() {
+		for (auto& p : pipe) p.release();
+		summary.release(); df.release(); df_x.release(); df_xy.release();
+		if (fork) (void)hipEventDestroy(fork);
+		fork = nullptr;
+		for (int j = 0; j < MAX_PIPES; ++j) {
+			if (join[j]) (void)hipEventDestroy(join[j]);
+			if (streams[j]) (void)hipStreamDestroy(streams[j]);
+			join[j] = nullptr;
+			streams[j] = nullptr;
+		}
+	}
 };
 
 }  // namespace ngp

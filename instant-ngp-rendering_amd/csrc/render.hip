@@ -48,6 +48,7 @@ struct RenderK {
 	int lens_mode;
 	float lens_params[7];
 	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
+	uint32_t pipe_index, pipe_count;  // this pipeline's 8-row blocks of the shard's rows
 	const uint8_t* bitfield;
 	const uint8_t* summary;
 	const uint8_t* df;  // octant distance fields (null: occupancy-summary block skipping)
@@ -57,6 +58,8 @@ struct RenderK {
 };
 
 __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32_t yl) {
+	// pipeline-local row -> shard-local row (alternate 8-row blocks) -> frame row
+	yl = ((yl >> 3) * k.pipe_count + k.pipe_index) * 8u + (yl & 7u);
 	const uint32_t blk = yl / k.shard_rows, within = yl % k.shard_rows;
 	return (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
 }
@@ -676,7 +679,7 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 static uint32_t lanes_target() {
 	const char* e = getenv("NGP_RENDER_LANES");
 	const long v = e ? atol(e) : 0;
-	return v > 0 ? (uint32_t)v : 8u << 20;
+	return v > 0 ? (uint32_t)v : 4u << 20;
 }
 
 // NGP_RENDER_TARGET overrides the per-pass sample budget (tuning knob; results do not depend on it)
@@ -684,7 +687,7 @@ static uint32_t pass_sample_target() {
 	const char* e = getenv("NGP_RENDER_TARGET");
 	const long v = e ? atol(e) : 0;
 	// <= 16M: the MLP reads the encodings through raw buffers with 32-bit byte offsets (64 B/sample)
-	return (uint32_t)std::min<long>(v > 0 ? v : 16l << 20, 16l << 20);
+	return (uint32_t)std::min<long>(v > 0 ? v : 4l << 20, 16l << 20);
 }
 
 // NGP_RENDER_FIRST_STEPS: the per-ray cap of the first pass; the cap doubles every pass up to
@@ -703,6 +706,71 @@ static uint32_t max_steps_per_pass() {
 	const char* e = getenv("NGP_RENDER_STEPS_PER_PASS");
 	const int v = e ? atoi(e) : 0;
 	return v > 0 ? (uint32_t)v : 32u;
+}
+
+// rows r < h_shard of a shard with (r / 8) % pipe_count == pipe_index
+static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_count) {
+	const uint32_t full = h_shard / 8u, rest = h_shard % 8u;
+	uint32_t n = (full / pipe_count + (full % pipe_count > pipe_index ? 1u : 0u)) * 8u;
+	if (rest && full % pipe_count == pipe_index) n += rest;
+	return n;
+}
+
+// NGP_RENDER_PIPES: ray pipelines per render (1 .. 4; default 2 for frames of >= 2^16 rays).
+// The pipelines take interleaved 8-row blocks of the frame and run their passes on their own
+// streams: one pipeline's latency-bound march kernels overlap another's encoder
+// (texture-addresser bound) and MLP (matrix cores).  Every ray composites its own samples in
+// order, so the image does not depend on the split.
+static uint32_t render_pipes(uint32_t n, uint32_t h_shard) {
+	const char* e = getenv("NGP_RENDER_PIPES");
+	if (getenv("NGP_RENDER_DUMP")) return 1;  // the diagnostic dump covers one pipeline's pass 0
+	uint32_t p = n >= (1u << 16) ? 2u : 1u;
+	if (e && atoi(e) >= 1) p = std::min<uint32_t>((uint32_t)atoi(e), RenderScratch::MAX_PIPES);
+	return std::max(1u, std::min(p, div_up(h_shard, 8u)));  // every pipeline gets rows
+}
+
+namespace {
+// One pipeline's march state (NerfTracer::trace, testbed_nerf.cu:1639-1755, for its rays).
+struct PipeRun {
+	RenderK k{};
+	RenderPipeScratch* ps = nullptr;
+	hipStream_t s = nullptr;
+	uint32_t n = 0, n_tiled = 0;
+	size_t max_samples = 0;
+	int cur = 0;
+	uint32_t pass = 0, steps_done = 0, n_alive_ub = 0, base_tag = 0;
+	bool marching = false;
+	float4* posdt = nullptr;
+	uint4* shrows = nullptr;
+	Payload* P(int b) const { return reinterpret_cast<Payload*>(ps->payload[b].ptr); }
+	float4* C(int b) const { return reinterpret_cast<float4*>(ps->rgba[b].ptr); }
+	uint32_t* hc() const { return ps->host_counter.ptr; }
+	unsigned long long* pub_dev() const { return reinterpret_cast<unsigned long long*>(ps->host_counter_dev + 64); }
+};
+}  // namespace
+
+// pass p's counters, published (k_generate of pass p + 1, or k_publish) as (tag << 32 | value)
+// words with tag base_tag + p + 1; unpacked into hc[16 * (p % 2) ...]
+static const uint32_t* wait_slot(PipeRun& pr, uint32_t pass) {
+	volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(pr.hc() + 64) + 8 * (pass % 2);
+	const uint32_t want = pr.base_tag + pass + 1;
+	uint32_t* out = pr.hc() + 16 * (pass % 2);
+	// no stream queries while spinning (each one enqueues a marker that drains the queue);
+	// only after seconds without the tag is the stream asked whether it failed
+	const auto t0 = std::chrono::steady_clock::now();
+	for (uint32_t q = 0, spin = 1; q < 8; ++spin) {
+		const unsigned long long v = w[q];
+		if ((uint32_t)(v >> 32) == want) {
+			out[q++] = (uint32_t)v;
+			continue;
+		}
+		if ((spin & 65535u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
+			const hipError_t e = hipStreamQuery(pr.s);
+			if (e != hipSuccess && e != hipErrorNotReady) NGP_HIP_CHECK(e);
+			if (e == hipSuccess && (uint32_t)(w[q] >> 32) != want) throw std::runtime_error("render: pass counters were not published");
+		}
+	}
+	return out;
 }
 
 void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s) {
@@ -734,156 +802,149 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);
 	k.bitfield = m->gs.bitfield.ptr;
+	k.tiles_x = div_up(k.W, 8u);
 	rs.summary.reserve(OCC_SUMMARY_BYTES * NERF_CASCADES / 4);
 	k.summary = reinterpret_cast<const uint8_t*>(rs.summary.ptr);
-	const uint32_t H_local = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
-	const uint32_t n = k.W * H_local;
-	k.n_local = n;
-	k.h_local = H_local;
-	k.tiles_x = div_up(k.W, 8u);
-	const uint32_t n_tiled = k.tiles_x * 8u * div_up(H_local, 8u) * 8u;
-	if (n == 0) return;
+	const uint32_t H_shard = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
+	if (k.W * H_shard == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
+	const uint32_t n_pipes = render_pipes(k.W * H_shard, H_shard);
 
 	const uint32_t target = pass_sample_target(), cap = max_steps_per_pass(), cap0 = std::min(first_pass_steps(), cap);
-	// the most slots one pass can reserve (see `bound` below): small frames stay small
-	const size_t max_samples = std::min<size_t>((size_t)n * cap, std::max<size_t>((size_t)n, (size_t)target)) + 256;
-	for (int b = 0; b < 3; ++b) {
-		rs.payload[b].reserve((size_t)n * 12);
-		rs.rgba[b].reserve((size_t)n * 4);
-		rs.depth[b].reserve(n);
-	}
-	rs.coords.reserve(12 * max_samples);  // [0, 4*max): pos + warped dt rows, [4*max, 12*max): SH rows (16 fp16)
-	rs.enc.reserve((size_t)m->lt.n_levels * max_samples * m->lt.F);
-	rs.out.reserve(4 * max_samples);
-	rs.counters.reserve(16);
 	static const bool debug = getenv("NGP_RENDER_DEBUG") != nullptr;
-	k.dbg = debug ? rs.counters.ptr + 8 : nullptr;
-	if (debug) NGP_HIP_CHECK(hipMemsetAsync(k.dbg, 0, 8 * sizeof(uint32_t), s));
-	if (!rs.host_counter.ptr) {
-		// [2][16] unpacked pass counters, [32, 40) copy-back slot, [64, 96) the published
-		// words ([2 slots][8] x (tag << 32 | value));
-		// fine-grained (coherent) so the kernel's system-scope stores reach the polling host
-		NGP_HIP_CHECK(hipHostMalloc((void**)&rs.host_counter.ptr, 96 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
-		std::memset(rs.host_counter.ptr, 0, 96 * sizeof(uint32_t));
-		rs.host_counter.n = 96;
-		NGP_HIP_CHECK(hipHostGetDevicePointer((void**)&rs.host_counter_dev, rs.host_counter.ptr, 0));
-	}
-	auto P = [&](int b) { return reinterpret_cast<Payload*>(rs.payload[b].ptr); };
-	auto C = [&](int b) { return reinterpret_cast<float4*>(rs.rgba[b].ptr); };
-
-	KernelTimers& tm = m->timers;
-	tm.begin(NGP_TIMER_RENDER_MARCH, s);
 	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (default 1.5) or "off"
 	static const char* budget_env = getenv("NGP_RENDER_BUDGET");
 	k.budget = !(budget_env && strcmp(budget_env, "off") == 0);
 	k.budget_scale = budget_env && k.budget ? (float)atof(budget_env) : 1.5f;
 	if (!(k.budget_scale > 0.0f)) k.budget_scale = 1.5f;
 	static const bool block_skipping = getenv("NGP_RENDER_SKIP") && !strcmp(getenv("NGP_RENDER_SKIP"), "blocks");
+
+	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
+	for (uint32_t j = 1; j < n_pipes; ++j) {
+		if (rs.streams[j]) continue;
+		NGP_HIP_CHECK(hipStreamCreateWithFlags(&rs.streams[j], hipStreamNonBlocking));
+		NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.join[j], hipEventDisableTiming));
+	}
+	PipeRun pipes[RenderScratch::MAX_PIPES];
+	for (uint32_t j = 0; j < n_pipes; ++j) {
+		PipeRun& pr = pipes[j];
+		pr.k = k;
+		pr.k.pipe_index = j;
+		pr.k.pipe_count = n_pipes;
+		pr.k.h_local = pipe_rows(H_shard, j, n_pipes);
+		pr.k.n_local = pr.n = k.W * pr.k.h_local;
+		pr.n_tiled = k.tiles_x * 8u * div_up(pr.k.h_local, 8u) * 8u;
+		pr.ps = &rs.pipe[j];
+		pr.s = j == 0 ? s : rs.streams[j];
+		RenderPipeScratch& ps = *pr.ps;
+		// the most slots one pass can reserve (see `bound` below): small frames stay small
+		pr.max_samples = std::min<size_t>((size_t)pr.n * cap, std::max<size_t>((size_t)pr.n, (size_t)target)) + 256;
+		for (int b = 0; b < 3; ++b) {
+			ps.payload[b].reserve((size_t)pr.n * 12);
+			ps.rgba[b].reserve((size_t)pr.n * 4);
+			ps.depth[b].reserve(pr.n);
+		}
+		ps.coords.reserve(12 * pr.max_samples);  // [0, 4*max): pos + warped dt rows, [4*max, 12*max): SH rows (16 fp16)
+		ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
+		ps.out.reserve(4 * pr.max_samples);
+		ps.counters.reserve(16);
+		if (!ps.host_counter.ptr) {
+			// [2][16] unpacked pass counters, [32, 40) copy-back slot, [64, 96) the published
+			// words ([2 slots][8] x (tag << 32 | value));
+			// fine-grained (coherent) so the kernel's system-scope stores reach the polling host
+			NGP_HIP_CHECK(hipHostMalloc((void**)&ps.host_counter.ptr, 96 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+			std::memset(ps.host_counter.ptr, 0, 96 * sizeof(uint32_t));
+			ps.host_counter.n = 96;
+			NGP_HIP_CHECK(hipHostGetDevicePointer((void**)&ps.host_counter_dev, ps.host_counter.ptr, 0));
+		}
+		if (!ps.events[0]) {
+			for (auto& e : ps.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+		}
+		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // sample records in two row arrays: the encoder
+		pr.shrows = reinterpret_cast<uint4*>(pr.posdt + pr.max_samples);  // reads 16-B position rows once per level
+		pr.base_tag = ps.pass_tag;
+		pr.n_alive_ub = pr.n;
+	}
+
+	KernelTimers& tm = m->timers;
+	tm.begin(NGP_TIMER_RENDER_MARCH, s);
+	uint32_t* dbg = debug ? rs.pipe[0].counters.ptr + 8 : nullptr;
+	if (debug) NGP_HIP_CHECK(hipMemsetAsync(dbg, 0, 8 * sizeof(uint32_t), s));
 	if (!block_skipping) {
 		build_distance_fields(m, k.max_mip, s);
 		k.df = rs.df.ptr;
 	}
+	// the summary kernel also zeroes pipeline 0's counters
 	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
-	                                                                rs.counters.ptr);
+	                                                                rs.pipe[0].counters.ptr);
+	if (n_pipes > 1) {
+		for (uint32_t j = 1; j < n_pipes; ++j) NGP_HIP_CHECK(hipMemsetAsync(rs.pipe[j].counters.ptr, 0, 8 * sizeof(uint32_t), s));
+		NGP_HIP_CHECK(hipEventRecord(rs.fork, s));
+		for (uint32_t j = 1; j < n_pipes; ++j) NGP_HIP_CHECK(hipStreamWaitEvent(rs.streams[j], rs.fork, 0));
+	}
 	const size_t lds = k.df ? 0 : (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
-	(k.lens_mode != LENS_PERSPECTIVE ? k_render_init<true> : k_render_init<false>)<<<div_up(n_tiled, 256u), 256, lds, s>>>(
-	    k, P(0), C(0), rs.depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, rs.counters.ptr);
-	tm.end(NGP_TIMER_RENDER_MARCH, s, n);
+	for (uint32_t j = 0; j < n_pipes; ++j) {
+		PipeRun& pr = pipes[j];
+		pr.k.df = k.df;
+		pr.k.dbg = dbg;
+		if (pr.n == 0) continue;
+		(k.lens_mode != LENS_PERSPECTIVE ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, lds, pr.s>>>(
+		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, pr.ps->counters.ptr);
+		pr.marching = true;
+	}
+	tm.end(NGP_TIMER_RENDER_MARCH, s, k.W * H_shard);
 	NGP_HIP_CHECK(hipGetLastError());
 
 	// NerfTracer::trace (testbed_nerf.cu:1639-1755): generate -> infer -> composite(+compact),
 	// alive rays ping-pong between buffers 0/1, finished rays with colour append to buffer 2.
-	// Counters (device): [0]/[1] alive rays in/out, [2] finished rays, [4]/[5] sample slots,
-	// [6]/[7] samples per ray of the pass.  The host does not wait for a pass before
-	// enqueuing the next: kernels read the counts from the device, and launches are sized by
-	// the count read back one pass earlier (alive counts only shrink).  The loop stops once a
-	// read-back shows no alive rays (the pass enqueued meanwhile runs empty).
+	// Counters (device): [0]/[1] alive rays in/out, [2] finished rays, [3] filled samples,
+	// [4]/[5] sample slots, [6]/[7] samples per ray of the pass.  The host does not wait for a
+	// pass before enqueuing the next: kernels read the counts from the device, and launches
+	// are sized by the count read back one pass earlier (alive counts only shrink).  A
+	// pipeline stops once a read-back shows no alive rays (the pass enqueued meanwhile runs
+	// empty).  With two pipelines the host alternates between them, so each stream holds up
+	// to two enqueued passes while the host waits on the other's read-back.
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
-	if (!rs.events[0]) {
-		for (auto& e : rs.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-	}
-	uint32_t* hc = rs.host_counter.ptr;  // pinned (layout at its allocation)
-	// sample records in two row arrays: the encoder reads 16-B position rows once per level
-	float4* posdt = reinterpret_cast<float4*>(rs.coords.ptr);
-	uint4* shrows = reinterpret_cast<uint4*>(posdt + max_samples);
-	// copy-back (only after k_retire): counters -> slot [32, 40), then an event
-	auto read_back = [&]() -> const uint32_t* {
-		NGP_HIP_CHECK(hipMemcpyAsync(hc + 32, rs.counters.ptr, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, s));
-		NGP_HIP_CHECK(hipEventRecord(rs.events[0], s));
-		hipError_t e;
-		while ((e = hipEventQuery(rs.events[0])) == hipErrorNotReady) {
-		}
-		NGP_HIP_CHECK(e);
-		return hc + 32;
-	};
-	// pass p's counters, published (k_generate of pass p + 1, or k_publish) as (tag << 32 | value) words with tag
-	// base_tag + p + 1; unpacked into hc[16 * (p % 2) ...]
-	const uint32_t base_tag = rs.pass_tag;
-	volatile unsigned long long* pub = reinterpret_cast<volatile unsigned long long*>(hc + 64);
-	unsigned long long* pub_dev = reinterpret_cast<unsigned long long*>(rs.host_counter_dev + 64);
-	auto wait_slot = [&](uint32_t pass) -> const uint32_t* {
-		volatile unsigned long long* w = pub + 8 * (pass % 2);
-		const uint32_t want = base_tag + pass + 1;
-		uint32_t* out = hc + 16 * (pass % 2);
-		// no stream queries while spinning (each one enqueues a marker that drains the queue);
-		// only after seconds without the tag is the stream asked whether it failed
-		const auto t0 = std::chrono::steady_clock::now();
-		for (uint32_t q = 0, spin = 1; q < 8; ++spin) {
-			const unsigned long long v = w[q];
-			if ((uint32_t)(v >> 32) == want) {
-				out[q++] = (uint32_t)v;
-				continue;
-			}
-			if ((spin & 65535u) == 0 && std::chrono::steady_clock::now() - t0 > std::chrono::seconds(5)) {
-				const hipError_t e = hipStreamQuery(s);
-				if (e != hipSuccess && e != hipErrorNotReady) NGP_HIP_CHECK(e);
-				if (e == hipSuccess && (uint32_t)(w[q] >> 32) != want)
-					throw std::runtime_error("render: pass counters were not published");
-			}
-		}
-		return out;
-	};
-	auto consume = [&](uint32_t pass) -> const uint32_t* { return wait_slot(pass); };
-	int cur = 0;
-	uint32_t pass = 0, steps_done = 0;
-	uint32_t n_alive_ub = n;  // upper bound on the alive rays entering the next pass
 	const uint32_t MARCH_ITER = 10000;
-	while (true) {
-		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		uint32_t* alive_in = rs.counters.ptr + pass % 2;
-		uint32_t* alive_out = rs.counters.ptr + (pass + 1) % 2;
-		uint32_t* samples = rs.counters.ptr + 4 + pass % 2;  // zeroed by the previous kernel of the chain
-		uint32_t* samples_next = rs.counters.ptr + 4 + (pass + 1) % 2;
-		uint32_t* steps_out = rs.counters.ptr + 6 + pass % 2;
+	auto enqueue_pass = [&](PipeRun& pr) {
+		const hipStream_t ps = pr.s;
+		uint32_t* counters = pr.ps->counters.ptr;
+		const uint32_t pass = pr.pass;
+		const int cur = pr.cur;
+		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
+		uint32_t* alive_in = counters + pass % 2;
+		uint32_t* alive_out = counters + (pass + 1) % 2;
+		uint32_t* samples = counters + 4 + pass % 2;  // zeroed by the previous kernel of the chain
+		uint32_t* samples_next = counters + 4 + (pass + 1) % 2;
+		uint32_t* steps_out = counters + 6 + pass % 2;
 		// lanes per ray: enough rays in flight for ~1M lanes, never fewer than one lane per ray
-		const uint32_t want = lanes_target() / std::max(n_alive_ub, 1u);
+		const uint32_t want = lanes_target() / std::max(pr.n_alive_ub, 1u);
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
-		const uint32_t gblocks = std::max(1u, div_up((uint64_t)n_alive_ub * G, 512));
-		unsigned long long* host_prev = pass > 0 ? pub_dev + 8 * ((pass - 1) % 2) : nullptr;
-		const uint32_t tag_prev = base_tag + pass;  // = tag of pass - 1
+		const uint32_t gblocks = std::max(1u, div_up((uint64_t)pr.n_alive_ub * G, 512));
+		unsigned long long* host_prev = pass > 0 ? pr.pub_dev() + 8 * ((pass - 1) % 2) : nullptr;
+		const uint32_t tag_prev = pr.base_tag + pass;  // = tag of pass - 1
 		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, 512, lds, s>>>(k, alive_in, P(cur), C(cur), posdt, shrows, target, cap_p, alive_out, samples, steps_out, rs.counters.ptr, host_prev, tag_prev); break;
+			case 1: k_generate<1><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
 		}
-		tm.end(NGP_TIMER_RENDER_MARCH, s);
+		tm.end(NGP_TIMER_RENDER_MARCH, ps);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
-		const uint64_t bound = std::min<uint64_t>((uint64_t)n_alive_ub * cap_p, std::max(target, n_alive_ub));
+		const uint64_t bound = std::min<uint64_t>((uint64_t)pr.n_alive_ub * cap_p, std::max(target, pr.n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin_kernel(NGP_TIMER_RENDER_ENCODE);
 		static const char* dump = getenv("NGP_RENDER_DUMP");  // diagnostic: pass-0 samples + alive payloads
 		if (dump && pass == 0) {
 			uint32_t c[8];
-			NGP_HIP_CHECK(hipMemcpyAsync(c, rs.counters.ptr, sizeof(c), hipMemcpyDeviceToHost, s));
-			NGP_HIP_CHECK(hipStreamSynchronize(s));
+			NGP_HIP_CHECK(hipMemcpyAsync(c, counters, sizeof(c), hipMemcpyDeviceToHost, ps));
+			NGP_HIP_CHECK(hipStreamSynchronize(ps));
 			std::vector<float> pd((size_t)c[4] * 4);
 			std::vector<Payload> pl(c[0]);
-			NGP_HIP_CHECK(hipMemcpy(pd.data(), posdt, pd.size() * 4, hipMemcpyDeviceToHost));
-			NGP_HIP_CHECK(hipMemcpy(pl.data(), P(cur), pl.size() * sizeof(Payload), hipMemcpyDeviceToHost));
+			NGP_HIP_CHECK(hipMemcpy(pd.data(), pr.posdt, pd.size() * 4, hipMemcpyDeviceToHost));
+			NGP_HIP_CHECK(hipMemcpy(pl.data(), pr.P(cur), pl.size() * sizeof(Payload), hipMemcpyDeviceToHost));
 			FILE* f = fopen(dump, "wb");
 			if (f) {
 				fwrite(c, 4, 8, f);
@@ -892,58 +953,84 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 				fclose(f);
 			}
 		}
-		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(posdt), 4, n_elements, table, rs.enc.ptr, internal_layout(m, n_elements), s, samples, 1);
-		tm.end(NGP_TIMER_RENDER_ENCODE, s);  // units: the pass's sample count, added at its read-back
+		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
+		                    internal_layout(m, n_elements), ps, samples, 1);
+		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
 		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
-		launch_mlp_infer(m, frags, rs.enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, rs.out.ptr, s,
-		                 samples, 0, reinterpret_cast<const __half*>(shrows));
-		tm.end(NGP_TIMER_RENDER_MLP, s);
-		tm.begin(NGP_TIMER_RENDER_MARCH, s);
-		k_composite<<<std::max(1u, div_up(n_alive_ub, 1024)), 1024, 0, s>>>(k, alive_in, P(cur), C(cur), rs.depth[cur].ptr,
-		                                                                  posdt, rs.out.ptr, P(1 - cur), C(1 - cur),
-		                                                                  rs.depth[1 - cur].ptr, P(2), C(2), rs.depth[2].ptr,
-		                                                                  alive_out, rs.counters.ptr + 2, samples_next,
-                                                                  rs.counters.ptr + 3);
-		tm.end(NGP_TIMER_RENDER_MARCH, s);
+		launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
+		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows));
+		tm.end(NGP_TIMER_RENDER_MLP, ps);
+		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
+		k_composite<<<std::max(1u, div_up(pr.n_alive_ub, 1024)), 1024, 0, ps>>>(
+		    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
+		    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);
+		tm.end(NGP_TIMER_RENDER_MARCH, ps);
 		NGP_HIP_CHECK(hipGetLastError());
-		cur = 1 - cur;
-		++pass;
+		pr.cur = 1 - cur;
+		++pr.pass;
 		// the read-back of the previous pass bounds the next one
-		if (pass >= 2) {
-			const uint32_t* c = consume(pass - 2);
-			steps_done += c[6 + (pass - 2) % 2];
-			n_alive_ub = std::min(n_alive_ub, c[(pass - 1) % 2]);
-			if (n_alive_ub == 0 || steps_done >= MARCH_ITER) break;
+		if (pr.pass >= 2) {
+			const uint32_t* c = wait_slot(pr, pr.pass - 2);
+			pr.steps_done += c[6 + (pr.pass - 2) % 2];
+			pr.n_alive_ub = std::min(pr.n_alive_ub, c[(pr.pass - 1) % 2]);
+			if (pr.n_alive_ub == 0 || pr.steps_done >= MARCH_ITER) pr.marching = false;
+		}
+	};
+	for (bool any = true; any;) {
+		any = false;
+		for (uint32_t j = 0; j < n_pipes; ++j) {
+			if (!pipes[j].marching) continue;
+			enqueue_pass(pipes[j]);
+			any |= pipes[j].marching;
 		}
 	}
-	k_publish<<<1, 64, 0, s>>>(rs.counters.ptr, pub_dev + 8 * ((pass - 1) % 2), base_tag + pass);
-	NGP_HIP_CHECK(hipGetLastError());
-	const uint32_t* last = consume(pass - 1);
-	uint32_t n_alive = last[pass % 2];
-	uint32_t n_hit = last[2];
-	// [3]: filled samples of the whole frame (the encoder / MLP skip the unfilled slots' work)
-	tm.add_units(NGP_TIMER_RENDER_ENCODE, last[3]);
-	tm.add_units(NGP_TIMER_RENDER_MLP, last[3]);
-	if (n_alive > 0) {
-		// march budget exhausted: still-alive rays are shaded with what they accumulated
-		k_retire<<<div_up(n_alive, 256), 256, 0, s>>>(n_alive, P(cur), C(cur), rs.depth[cur].ptr, P(2), C(2), rs.depth[2].ptr,
-		                                              rs.counters.ptr);
-		n_hit = read_back()[2];
+
+	for (uint32_t j = 0; j < n_pipes; ++j) {
+		PipeRun& pr = pipes[j];
+		if (pr.pass == 0) continue;  // no rays
+		uint32_t* counters = pr.ps->counters.ptr;
+		k_publish<<<1, 64, 0, pr.s>>>(counters, pr.pub_dev() + 8 * ((pr.pass - 1) % 2), pr.base_tag + pr.pass);
+		NGP_HIP_CHECK(hipGetLastError());
+		const uint32_t* last = wait_slot(pr, pr.pass - 1);
+		const uint32_t n_alive = last[pr.pass % 2];
+		uint32_t n_hit = last[2];
+		// [3]: filled samples of the pipeline's rays (the encoder / MLP skip the unfilled slots' work)
+		tm.add_units(NGP_TIMER_RENDER_ENCODE, last[3]);
+		tm.add_units(NGP_TIMER_RENDER_MLP, last[3]);
+		if (n_alive > 0) {
+			// march budget exhausted: still-alive rays are shaded with what they accumulated
+			k_retire<<<div_up(n_alive, 256), 256, 0, pr.s>>>(n_alive, pr.P(pr.cur), pr.C(pr.cur), pr.ps->depth[pr.cur].ptr,
+			                                                 pr.P(2), pr.C(2), pr.ps->depth[2].ptr, counters);
+			// copy-back of the counters -> slot [32, 40), then an event
+			NGP_HIP_CHECK(hipMemcpyAsync(pr.hc() + 32, counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, pr.s));
+			NGP_HIP_CHECK(hipEventRecord(pr.ps->events[0], pr.s));
+			hipError_t e;
+			while ((e = hipEventQuery(pr.ps->events[0])) == hipErrorNotReady) {
+			}
+			NGP_HIP_CHECK(e);
+			n_hit = pr.hc()[32 + 2];
+		}
+		pr.ps->pass_tag = pr.base_tag + pr.pass;
+		if (n_hit)
+			k_shade<<<div_up(n_hit, 256), 256, 0, pr.s>>>(n_hit, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, k.linear_colors,
+			                                              reinterpret_cast<float4*>(frame), depth_buffer);
+		NGP_HIP_CHECK(hipGetLastError());
 	}
-	rs.pass_tag = base_tag + pass;
+	for (uint32_t j = 1; j < n_pipes; ++j) {
+		NGP_HIP_CHECK(hipEventRecord(rs.join[j], rs.streams[j]));
+		NGP_HIP_CHECK(hipStreamWaitEvent(s, rs.join[j], 0));
+	}
 	if (debug) {
 		uint32_t d[8];
-		NGP_HIP_CHECK(hipMemcpyAsync(d, k.dbg, sizeof(d), hipMemcpyDeviceToHost, s));
+		NGP_HIP_CHECK(hipMemcpyAsync(d, dbg, sizeof(d), hipMemcpyDeviceToHost, s));
 		wait_stream(m, s);
+		const uint32_t n = k.W * H_shard;
 		fprintf(stderr,
-		        "[render] rays %u init: alive %u lattice steps %.2f/ray | passes %u generate iterations %u slots %u "
-		        "samples %u composited %u (%.1f%% of slots)\n",
-		        n, d[1], (double)d[0] / n, pass, d[2], d[5], d[3], d[4], 100.0 * d[4] / std::max(d[5], 1u));
+		        "[render] rays %u pipelines %u init: alive %u lattice steps %.2f/ray | passes %u (pipeline 0) generate iterations %u "
+		        "slots %u samples %u composited %u (%.1f%% of slots)\n",
+		        n, n_pipes, d[1], (double)d[0] / n, pipes[0].pass, d[2], d[5], d[3], d[4],
+		        100.0 * d[4] / std::max(d[5], 1u));
 	}
-	if (n_hit)
-		k_shade<<<div_up(n_hit, 256), 256, 0, s>>>(n_hit, P(2), C(2), rs.depth[2].ptr, k.linear_colors,
-		                                           reinterpret_cast<float4*>(frame), depth_buffer);
-	NGP_HIP_CHECK(hipGetLastError());
 }
 
 void run_accumulate_tonemap(const float* frame, float* accum, float* out, uint32_t W, uint32_t H, uint32_t spp,

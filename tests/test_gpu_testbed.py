@@ -277,7 +277,7 @@ def test_extrinsic_optimisation_recovers_perturbed_pose(scene, tmp_path):
     tr.optimize_extrinsics = True
     tr.extrinsic_learning_rate = 3e-3
     losses = []
-    while tb.training_step < 1100:
+    while tb.training_step < 1700:
         tb.frame()
         losses.append(tb.loss)
     assert np.isfinite(losses).all()

@@ -1,0 +1,67 @@
+"""Render-schedule A/B on one box and one set of weights (diagnostic, GPU box).
+
+Trains the bench scene once (bench.py's defaults), then renders the bench's 1080p view under
+each environment setting in turn, round-robin, so box-to-box and run-to-run spread cancel out.
+The render knobs it varies (NGP_RENDER_PIPES / TARGET / STEPS_PER_PASS / LANES /
+FIRST_STEPS) are read on every render call.
+
+Usage: python tools/render_ab.py [--rounds 4] [--frames 5] "" "NGP_RENDER_PIPES=1" "NGP_RENDER_TARGET=8388608" ...
+"""
+import argparse
+import os
+import statistics
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "instant-ngp-rendering_amd"))
+
+KNOBS = ("NGP_RENDER_PIPES", "NGP_RENDER_TARGET", "NGP_RENDER_STEPS_PER_PASS", "NGP_RENDER_LANES",
+         "NGP_RENDER_FIRST_STEPS")
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("settings", nargs="+")
+    p.add_argument("--rounds", type=int, default=4)
+    p.add_argument("--frames", type=int, default=5)
+    p.add_argument("--pretrain", type=int, default=1500)
+    p.add_argument("--config", default="lego_L16F2.json")
+    p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
+    a = p.parse_args()
+    import pyngp as ngp
+
+    tb = ngp.Testbed(ngp.TestbedMode.Nerf)
+    tb.load_training_data(a.scene)
+    tb.reload_network_from_file(a.config)
+    tb.shall_train = True
+    for i in range(a.pretrain):
+        tb.train(1 << 18)
+    n_views = tb.nerf.training.dataset.n_images
+    tb.set_camera_to_training_view(3 % n_views)
+    base = {k: os.environ.get(k) for k in KNOBS}
+    times = {s: [] for s in a.settings}
+    for r in range(a.rounds):
+        for s in a.settings:
+            for k, v in base.items():
+                if v is None:
+                    os.environ.pop(k, None)
+                else:
+                    os.environ[k] = v
+            for kv in s.split():
+                k, v = kv.split("=", 1)
+                os.environ[k] = v
+            tb.render_to_device(1920, 1080, 1, True)  # warm this setting's buffers
+            t0 = time.perf_counter()
+            for _ in range(a.frames):
+                tb.render_to_device(1920, 1080, 1, True)
+            times[s].append((time.perf_counter() - t0) / a.frames * 1e3)
+        print(f"# round {r + 1}/{a.rounds}", file=sys.stderr, flush=True)
+    for s in a.settings:
+        t = times[s]
+        print(f"{s or 'default':55s} median {statistics.median(t):7.3f} ms/frame  min {min(t):7.3f}  "
+              f"({', '.join(f'{x:.2f}' for x in t)})")
+
+
+if __name__ == "__main__":
+    main()
