@@ -263,8 +263,24 @@ __device__ __forceinline__ typename FeatVec<F>::T encode_one(uint32_t level, flo
 	pos_fract(pz, scale, &fz, &gz);
 
 	VT vals[8];
-	if (hashed) gather_corners<F, true, QUAD>(tab, size, res, gx, gy, gz, vals);
-	else gather_corners<F, false, QUAD>(tab, size, res, gx, gy, gz, vals);
+	if (hashed) {
+		gather_corners<F, true, QUAD>(tab, size, res, gx, gy, gz, vals);
+	} else if constexpr (F == 2) {
+		// dense level with corner records (render site): two 16-B loads fetch the 8 corners
+		// (the cell's z and z + 1 records) instead of four 8-B pairs -- the encoder is bound by
+		// the texture addresser's work per load instruction.  Corners outside [0, res) (only
+		// positions outside the unit cube) take the table path.
+		if (lt.rec && gx < res && gy < res && gz < res) {
+			const uint4* r = lt.rec + lt.rec_off[level] + gx + res * (gy + res * gz);
+			const uint4 a = r[0], b = r[res * res];
+			vals[0] = a.x; vals[1] = a.y; vals[2] = a.z; vals[3] = a.w;
+			vals[4] = b.x; vals[5] = b.y; vals[6] = b.z; vals[7] = b.w;
+		} else {
+			gather_corners<F, false, QUAD>(tab, size, res, gx, gy, gz, vals);
+		}
+	} else {
+		gather_corners<F, false, QUAD>(tab, size, res, gx, gy, gz, vals);
+	}
 	float acc[F];
 #pragma unroll
 	for (uint32_t f = 0; f < F; ++f) acc[f] = 0.0f;
@@ -490,6 +506,40 @@ __global__ void __launch_bounds__(256) k_hashgrid_indices(uint32_t n, const floa
 		idx_out[((size_t)i * lt.n_levels + level) * 8 + c] = lt.offset[level] + idx;
 		w_out[((size_t)i * lt.n_levels + level) * 8 + c] = w;
 	}
+}
+
+// Corner records of the dense levels (LevelTable::rec): one thread per record, four table
+// entries gathered with the encoder's own corner indexing (same modulo), one 16-B store.
+__global__ void __launch_bounds__(256) k_dense_records(const uint32_t* __restrict__ table, const LevelTable lt,
+                                                       uint4* __restrict__ rec, uint32_t total) {
+	const uint32_t g = blockIdx.x * 256u + threadIdx.x;
+	if (g >= total) return;
+	uint32_t level = 0;
+	for (uint32_t l = 0; l < lt.n_levels; ++l)
+		if (!lt.hashed[l] && lt.rec_off[l] <= g) level = l;
+	const uint32_t res = lt.res[level], size = lt.size[level], i = g - lt.rec_off[level];
+	const uint32_t x = i % res, y = (i / res) % res, z = i / (res * res);
+	const uint32_t* tab = table + lt.offset[level];
+	rec[g] = make_uint4(tab[corner_index<false>(size, res, x, y, z)], tab[corner_index<false>(size, res, x + 1u, y, z)],
+	                    tab[corner_index<false>(size, res, x, y + 1u, z)], tab[corner_index<false>(size, res, x + 1u, y + 1u, z)]);
+}
+
+LevelTable build_dense_records(ngp_model* m, const __half* table, hipStream_t s) {
+	LevelTable lt = m->lt;
+	lt.rec = nullptr;
+	const bool off = getenv("NGP_ENC_DENSE_RECORDS") && !strcmp(getenv("NGP_ENC_DENSE_RECORDS"), "0");  // A/B knob
+	if (lt.F != 2 || off) return lt;
+	uint32_t total = 0;
+	for (uint32_t l = 0; l < lt.n_levels; ++l) {
+		lt.rec_off[l] = total;
+		if (!lt.hashed[l]) total += lt.res[l] * lt.res[l] * (lt.res[l] + 1u);
+	}
+	if (total == 0) return lt;
+	m->rs.dense_rec.reserve(total);
+	k_dense_records<<<div_up(total, 256u), 256, 0, s>>>(reinterpret_cast<const uint32_t*>(table), lt, m->rs.dense_rec.ptr, total);
+	NGP_HIP_CHECK(hipGetLastError());
+	lt.rec = m->rs.dense_rec.ptr;
+	return lt;
 }
 
 template <int SITE>

@@ -137,6 +137,11 @@ struct LevelTable {
 	uint32_t offset[MAX_LEVELS];  // in entries (each entry = F features)
 	uint32_t size[MAX_LEVELS];    // entries
 	uint32_t hashed[MAX_LEVELS];
+	// optional corner records of the dense levels (render site, F = 2; build_dense_records):
+	// record (x, y, z) of level l, at rec[rec_off[l] + x + y res + z res^2] for x, y < res and
+	// z <= res, holds the entries of corners (x, y, z), (x+1, y, z), (x, y+1, z), (x+1, y+1, z)
+	const uint4* rec = nullptr;
+	uint32_t rec_off[MAX_LEVELS];
 };
 
 // Layout of an fp16 encoding buffer (n samples, L levels, F features).
@@ -289,6 +294,7 @@ struct RenderScratch {
 	hipStream_t streams[MAX_PIPES] = {};  // pipelines 1.. run on their own streams ([0] unused: the caller's)
 	hipEvent_t fork = nullptr, join[MAX_PIPES] = {};  // caller's stream -> pipeline streams -> caller's stream
 	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
+	DevBuf<uint4> dense_rec;   // corner records of the dense levels (LevelTable::rec), rebuilt per render
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
 	uint64_t df_version = ~0ull;
@@ -296,7 +302,7 @@ struct RenderScratch {
 	size_t cap = 0;
 	void release() {
 		for (auto& p : pipe) p.release();
-		summary.release(); df.release(); df_x.release(); df_xy.release();
+		summary.release(); dense_rec.release(); df.release(); df_x.release(); df_xy.release();
 		if (fork) (void)hipEventDestroy(fork);
 		fork = nullptr;
 		for (int j = 0; j < MAX_PIPES; ++j) {
@@ -359,6 +365,9 @@ inline void wait_stream(ngp_model* m, hipStream_t s) {
 // n: bound on the samples (the device count *n_dev, when given, is the actual one).  max_chunks
 // > 0 caps the 256-sample chunks launched per level; the blocks then loop over the chunks
 // up to the device count (for large bounds that are rarely reached).
+// Corner records of the dense levels of `table` (F = 2) into rs.dense_rec; returns m->lt with
+// rec / rec_off set (rec stays null when no level is dense or F != 2).
+LevelTable build_dense_records(ngp_model* m, const __half* table, hipStream_t s);
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
                          __half* enc, EncLayout enc_layout, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2,
                          uint32_t max_chunks = 0);

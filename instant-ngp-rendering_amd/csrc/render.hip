@@ -877,6 +877,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// the summary kernel also zeroes pipeline 0's counters
 	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
 	                                                                rs.pipe[0].counters.ptr);
+	// the encoder's table, and corner records of its dense levels (read by every pipeline)
+	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
+	const LevelTable lt_render = build_dense_records(m, table, s);
 	if (n_pipes > 1) {
 		for (uint32_t j = 1; j < n_pipes; ++j) NGP_HIP_CHECK(hipMemsetAsync(rs.pipe[j].counters.ptr, 0, 8 * sizeof(uint32_t), s));
 		NGP_HIP_CHECK(hipEventRecord(rs.fork, s));
@@ -904,8 +908,6 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// pipeline stops once a read-back shows no alive rays (the pass enqueued meanwhile runs
 	// empty).  With two pipelines the host alternates between them, so each stream holds up
 	// to two enqueued passes while the host waits on the other's read-back.
-	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
-	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
 	const uint32_t MARCH_ITER = 10000;
 	auto enqueue_pass = [&](PipeRun& pr) {
 		const hipStream_t ps = pr.s;
@@ -953,7 +955,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 				fclose(f);
 			}
 		}
-		launch_hashgrid_fwd(m->lt, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
+		launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
 		                    internal_layout(m, n_elements), ps, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
 		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
