@@ -26,17 +26,28 @@ def main():
     p.add_argument("--rounds", type=int, default=4)
     p.add_argument("--frames", type=int, default=5)
     p.add_argument("--pretrain", type=int, default=1500)
-    p.add_argument("--config", default="lego_L16F2.json")
+    p.add_argument("--config", default=os.path.join(ROOT, "instant-ngp-rendering_amd", "configs", "nerf", "lego_L16F2.json"))
+    p.add_argument("--snapshot", default=None, help="load this snapshot if it exists, else train and save it")
+    p.add_argument("--pkg", default=None, help="directory holding another build of pyngp + libngp_hip (tools/ab_build_old.sh)")
     p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
     a = p.parse_args()
+    if a.pkg:
+        sys.path.insert(0, os.path.abspath(a.pkg))
     import pyngp as ngp
+
+    print(f"# pyngp from {ngp.__file__}", file=sys.stderr)
 
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
     tb.load_training_data(a.scene)
     tb.reload_network_from_file(a.config)
-    tb.shall_train = True
-    for i in range(a.pretrain):
-        tb.train(1 << 18)
+    if a.snapshot and os.path.exists(a.snapshot):
+        tb.load_snapshot(a.snapshot)  # the same weights and grid as the run that wrote it
+    else:
+        tb.shall_train = True
+        for i in range(a.pretrain):
+            tb.train(1 << 18)
+        if a.snapshot:
+            tb.save_snapshot(a.snapshot, False)
     n_views = tb.nerf.training.dataset.n_images
     tb.set_camera_to_training_view(3 % n_views)
     base = {k: os.environ.get(k) for k in KNOBS}
