@@ -40,6 +40,13 @@ constexpr int WAVES = 4;
 constexpr int BLOCK = WAVES * 64;
 constexpr int SAMPLES_PER_BLOCK = WAVES * SPW;
 constexpr int FRAG_HALVES = 512;  // 64 lanes x 8 halves
+// the training kernel: 8 waves x 16 samples per workgroup (the same 128-sample chunk and
+// 146 KiB LDS images as 4 x 32, but two waves per SIMD to hide the LDS round trips)
+constexpr int TWAVES = 8;
+constexpr int TSPW = 16;
+constexpr int TCT = TSPW / 16;
+constexpr int TBLOCK = TWAVES * 64;
+static_assert(TWAVES * TSPW == SAMPLES_PER_BLOCK, "the training images hold one chunk");
 
 template <int W_, int DH_, int RH_, int KE_>
 struct Net {
@@ -104,6 +111,7 @@ struct Net {
 		return s;
 	}
 	static constexpr int slots() { return (gtile_base(NL) + WAVES - 1) / WAVES; }
+	static constexpr int tslots() { return (gtile_base(NL) + TWAVES - 1) / TWAVES; }
 	static constexpr int drows() { return Wp > 32 ? Wp : 32; }
 	static constexpr int dstride() { return 2 * drows() + 8; }
 	static constexpr size_t lds_infer() { return (size_t)fwd_frags() * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<false>() * 2; }
@@ -154,11 +162,11 @@ __device__ __forceinline__ _Float16 u16h(uint32_t u) { return __builtin_bit_cast
 __device__ __forceinline__ uint32_t n_chunks_of(uint32_t n) { return (n + SAMPLES_PER_BLOCK - 1) / SAMPLES_PER_BLOCK; }
 
 // This wave's SPW samples of the encoding (EncLayout) -> image rows [0, ENC_ROWS).
-template <class N, int STRIDE>
+template <class N, int STRIDE, int SPW_ = SPW>
 __device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, uint32_t base, int lane) {
 	constexpr int CHUNKS = N::ENC_ROWS / 8;
-	for (int t = lane; t < SPW * CHUNKS; t += 64) {
-		const int smp = t % SPW, chunk = t / SPW;
+	for (int t = lane; t < SPW_ * CHUNKS; t += 64) {
+		const int smp = t % SPW_, chunk = t / SPW_;
 		const uint32_t i = base + smp;
 		const uint32_t k0 = chunk * 8;
 		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
@@ -199,10 +207,10 @@ __device__ __forceinline__ void load_encoding(const MlpArgs& a, _Float16* img, u
 
 // Spherical harmonics, degree 4, of the warped direction (tcnn SphericalHarmonicsEncoding;
 // configs/nerf/base.json:37-49) into rows [x_seg+16, x_seg+32).
-template <int STRIDE>
+template <int STRIDE, int SPW_ = SPW>
 __device__ __forceinline__ void load_sh(const MlpArgs& a, _Float16* img, int x_seg, uint32_t base, int lane) {
-	for (int t = lane; t < SPW * 2; t += 64) {
-		const int smp = t % SPW, half = t / SPW;
+	for (int t = lane; t < SPW_ * 2; t += 64) {
+		const int smp = t % SPW_, half = t / SPW_;
 		const uint32_t i = base + smp;
 		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 		if (i < a.n) {
@@ -235,15 +243,15 @@ __device__ __forceinline__ void load_sh(const MlpArgs& a, _Float16* img, int x_s
 
 // One forward layer for this wave's CT column tiles.  Output rows go to LDS
 // segment seg_out, or (final rgb layer) are returned in `res`.
-template <class N, bool TRAIN, int l>
-__device__ __forceinline__ void fwd_layer(const _Float16* frags, _Float16* img, int lane, f4 (&res)[CT]) {
+template <class N, bool TRAIN, int l, int CT_ = CT>
+__device__ __forceinline__ void fwd_layer(const _Float16* frags, _Float16* img, int lane, f4 (&res)[CT_]) {
 	constexpr int STRIDE = N::template stride<TRAIN>();
 	constexpr int MT = N::Mt(l), KS = N::Ks(l);
 	constexpr int SIN = N::template seg_in<TRAIN>(l), SOUT = N::template seg_out<TRAIN>(l);
 	const int g = lane >> 4, n = lane & 15;
-	h8 b[CT][KS];
+	h8 b[CT_][KS];
 #pragma unroll
-	for (int c = 0; c < CT; ++c)
+	for (int c = 0; c < CT_; ++c)
 #pragma unroll
 		for (int s = 0; s < KS; ++s) b[c][s] = lds_h8(img + (16 * c + n) * STRIDE + SIN + 32 * s + 8 * g);
 	const _Float16* fr = frags + N::fwd_off(l);
@@ -253,7 +261,7 @@ __device__ __forceinline__ void fwd_layer(const _Float16* frags, _Float16* img, 
 #pragma unroll
 		for (int s = 0; s < KS; ++s) a[s] = lds_h8(fr + ((mt * KS + s) * 64 + lane) * 8);
 #pragma unroll
-		for (int c = 0; c < CT; ++c) {
+		for (int c = 0; c < CT_; ++c) {
 			f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
 			for (int s = 0; s < KS; ++s) acc = mfma(a[s], b[c][s], acc);
@@ -271,11 +279,11 @@ __device__ __forceinline__ void fwd_layer(const _Float16* frags, _Float16* img, 
 	}
 }
 
-template <class N, bool TRAIN, int l, int END>
-__device__ __forceinline__ void fwd_range(const _Float16* frags, _Float16* img, int lane, f4 (&res)[CT]) {
+template <class N, bool TRAIN, int l, int END, int CT_ = CT>
+__device__ __forceinline__ void fwd_range(const _Float16* frags, _Float16* img, int lane, f4 (&res)[CT_]) {
 	if constexpr (l < END) {
-		fwd_layer<N, TRAIN, l>(frags, img, lane, res);
-		fwd_range<N, TRAIN, l + 1, END>(frags, img, lane, res);
+		fwd_layer<N, TRAIN, l, CT_>(frags, img, lane, res);
+		fwd_range<N, TRAIN, l + 1, END, CT_>(frags, img, lane, res);
 	}
 }
 
@@ -627,7 +635,7 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 // ---------------------------------------------------------------------------
 template <class N, int l>
 __device__ __forceinline__ void wgrad_layer(const _Float16* imgs, const _Float16* dimgs, int wave, int lane,
-                                            f4 (&acc)[N::slots()], uint32_t enc_pad) {
+                                            f4 (&acc)[N::tslots()], uint32_t enc_pad) {
 	constexpr int STRIDE = N::template stride<true>();
 	constexpr int DS = N::dstride();
 	constexpr int DCUR = ((N::NL - 1 - l) % 2) * N::drows();
@@ -640,14 +648,14 @@ __device__ __forceinline__ void wgrad_layer(const _Float16* imgs, const _Float16
 		(void)dummy;
 		const int gt = N::gtile_base(l) + t;
 		const int mt = t / KTN, kt = t % KTN;
-		if (gt % WAVES != wave) continue;
+		if (gt % TWAVES != wave) continue;
 		if (l == 0 && (uint32_t)(16 * kt) >= enc_pad) continue;
-		const int slot = gt / WAVES;
+		const int slot = gt / TWAVES;
 		f4 c = acc[slot];
 #pragma unroll
-		for (int w2 = 0; w2 < WAVES; ++w2) {
-			const _Float16* ds = dimgs + w2 * SPW * DS + DCUR + 16 * mt + 4 * p;
-			const _Float16* as = imgs + w2 * SPW * STRIDE + SIN + 16 * kt + 4 * p;
+		for (int w2 = 0; w2 < TWAVES * TSPW / 32; ++w2) {  // K = 32 consecutive samples of the chunk per MFMA
+			const _Float16* ds = dimgs + w2 * 32 * DS + DCUR + 16 * mt + 4 * p;
+			const _Float16* as = imgs + w2 * 32 * STRIDE + SIN + 16 * kt + 4 * p;
 			const h4 a0 = tr_read(ds + (8 * g + q) * DS), a1 = tr_read(ds + (8 * g + 4 + q) * DS);
 			const h4 b0 = tr_read(as + (8 * g + q) * STRIDE), b1 = tr_read(as + (8 * g + 4 + q) * STRIDE);
 			const h8 A = {a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
@@ -670,9 +678,9 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	// the rgb network's input: the 16 density-output rows, then (for the camera gradients) the 16 SH rows
 	constexpr int KT = N::Kt(l);
 	const int g = lane >> 4, n = lane & 15;
-	h8 b[CT][MS];
+	h8 b[TCT][MS];
 #pragma unroll
-	for (int c = 0; c < CT; ++c)
+	for (int c = 0; c < TCT; ++c)
 #pragma unroll
 		for (int s = 0; s < MS; ++s) b[c][s] = lds_h8(dimg + (16 * c + n) * DS + DCUR + 32 * s + 8 * g);
 	const _Float16* fr = frags + N::bwd_off(l);
@@ -683,7 +691,7 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 #pragma unroll
 		for (int s = 0; s < MS; ++s) af[s] = lds_h8(fr + ((mt * MS + s) * 64 + lane) * 8);
 #pragma unroll
-		for (int c = 0; c < CT; ++c) {
+		for (int c = 0; c < TCT; ++c) {
 			f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
 			for (int s = 0; s < MS; ++s) acc = mfma(af[s], b[c][s], acc);
@@ -727,20 +735,20 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	if constexpr (l == N::DH + 1) {
 		// density-output delta has 16 rows; rows 16..31 of the next k-step must be zero
 #pragma unroll
-		for (int c = 0; c < CT; ++c) lds_st_h4(dimg + (16 * c + n) * DS + DNXT + 16 + 4 * g, h4{0, 0, 0, 0});
+		for (int c = 0; c < TCT; ++c) lds_st_h4(dimg + (16 * c + n) * DS + DNXT + 16 + 4 * g, h4{0, 0, 0, 0});
 	}
 }
 
 template <class N, int l>
 __device__ __forceinline__ void bwd_range(const MlpArgs& a, const _Float16* frags, const _Float16* imgs,
                                           _Float16* dimgs, int wave, int lane, uint32_t base,
-                                          f4 (&acc)[N::slots()]) {
+                                          f4 (&acc)[N::tslots()]) {
 	if constexpr (l >= 0) {
 		constexpr int STRIDE = N::template stride<true>();
 		constexpr int DS = N::dstride();
 		__syncthreads();  // every wave's delta for layer l is in LDS
 		wgrad_layer<N, l>(imgs, dimgs, wave, lane, acc, a.enc_pad);
-		dgrad_layer<N, l>(a, frags, imgs + wave * SPW * STRIDE, dimgs + wave * SPW * DS, lane, base);
+		dgrad_layer<N, l>(a, frags, imgs + wave * TSPW * STRIDE, dimgs + wave * TSPW * DS, lane, base);
 		bwd_range<N, l - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
 	}
 }
@@ -749,7 +757,7 @@ __device__ __forceinline__ void bwd_range(const MlpArgs& a, const _Float16* frag
 // in exactly one tile); k_mlp_reduce sums the rows in a fixed order.  Replaces one fp32 atomic
 // per weight and workgroup onto the same 10k addresses (256-way contention at the L2).
 template <class N, int l>
-__device__ __forceinline__ void flush_range(const MlpArgs& a, int wave, int lane, const f4 (&acc)[N::slots()]) {
+__device__ __forceinline__ void flush_range(const MlpArgs& a, int wave, int lane, const f4 (&acc)[N::tslots()]) {
 	if constexpr (l < N::NL) {
 		constexpr int KTN = N::KT16(l);
 		const int g = lane >> 4, n = lane & 15;
@@ -758,11 +766,11 @@ __device__ __forceinline__ void flush_range(const MlpArgs& a, int wave, int lane
 #pragma unroll
 		for (int t = 0; t < N::gtiles(l); ++t) {
 			const int gt = N::gtile_base(l) + t;
-			if (gt % WAVES != wave) continue;
+			if (gt % TWAVES != wave) continue;
 			const int mt = t / KTN, kt = t % KTN;
 			const uint32_t col = 16 * kt + n;
 			if (col >= pin) continue;
-			const f4 c = acc[gt / WAVES];
+			const f4 c = acc[gt / TWAVES];
 #pragma unroll
 			for (int r = 0; r < 4; ++r) {
 				const uint32_t row = 16 * mt + 4 * g + r;
@@ -807,20 +815,20 @@ __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int
 	const uint32_t* e = reinterpret_cast<const uint32_t*>(a.enc);
 #pragma unroll
 	for (int it = 0; it < 2; ++it) {
-		const int t = lane + 64 * it, smp = t % SPW, chunk = t / SPW;
+		const int t = lane + 64 * it, smp = t % TSPW, chunk = t / TSPW;
 		const uint32_t i = base + smp, k0 = chunk * 8;
-		const bool ok = t < SPW * CHUNKS && i < a.n && k0 < a.E;
+		const bool ok = t < TSPW * CHUNKS && i < a.n && k0 < a.E;
 #pragma unroll
 		for (int q = 0; q < 4; ++q) p.e[it][q] = ok ? e[lay.vec(k0 / 2 + q, i)] : 0u;
 	}
-	const uint32_t i = base + (lane % SPW);
+	const uint32_t i = base + (lane % TSPW);
 	const bool in = i < a.n;
 	const float* c = a.coords + (size_t)(in ? i : 0) * a.coord_stride;
 #pragma unroll
 	for (int k = 0; k < 3; ++k) p.d[k] = in ? c[4 + k] : 0.5f;
 	p.dl = make_uint2(0u, 0u);
 	p.w = 1.0f;
-	if (lane < SPW && in) {
+	if (lane < TSPW && in) {
 		p.dl = *reinterpret_cast<const uint2*>(a.dloss + (size_t)i * 4);
 		if (a.weight) p.w = a.weight[i];
 	}
@@ -835,8 +843,8 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 #pragma unroll
 	for (int it = 0; it < 2; ++it) {
 		const int t = lane + 64 * it;
-		if (t < SPW * CHUNKS) {
-			const int smp = t % SPW, chunk = t / SPW;
+		if (t < TSPW * CHUNKS) {
+			const int smp = t % TSPW, chunk = t / TSPW;
 			h8 v;
 #pragma unroll
 			for (int q = 0; q < 4; ++q) {
@@ -847,18 +855,18 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 		}
 	}
 	{
-		// lane = half * SPW + sample: SH components 8 half .. 8 half + 7 of the warped direction
-		const int smp = lane % SPW, half = lane / SPW;
+		// lane = half * TSPW + sample: SH components 8 half .. 8 half + 7 of the warped direction
+		const int smp = lane % TSPW, half = lane / TSPW;
 		const bool in = base + smp < a.n;
 		float v[16];
 		sh_deg4(p.d[0], p.d[1], p.d[2], v);
 		h8 o;
 #pragma unroll
 		for (int k = 0; k < 8; ++k) o[k] = in ? (_Float16)(half ? v[8 + k] : v[k]) : (_Float16)0;
-		lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, o);
+		if (half < 2) lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, o);
 	}
-	for (int t = lane; t < SPW * 4; t += 64) {
-		const int smp = t % SPW, ch = t / SPW;
+	for (int t = lane; t < TSPW * 4; t += 64) {
+		const int smp = t % TSPW, ch = t / TSPW;
 		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 		const uint2 dl = make_uint2(__shfl(p.dl.x, smp, 64), __shfl(p.dl.y, smp, 64));
 		const float w = __shfl(p.w, smp, 64);
@@ -873,7 +881,7 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 }
 
 template <class N>
-__global__ void __launch_bounds__(BLOCK) k_mlp_train(MlpArgs a) {
+__global__ void __launch_bounds__(TBLOCK) k_mlp_train(MlpArgs a) {
 	if (a.n_dev) a.n = min(a.n, *a.n_dev);
 	extern __shared__ __attribute__((aligned(16))) char smem[];
 	constexpr int STRIDE = N::template stride<true>();
@@ -883,36 +891,36 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_train(MlpArgs a) {
 	_Float16* imgs = frags + FH;
 	_Float16* dimgs = imgs + WAVES * SPW * STRIDE;
 	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	_Float16* img = imgs + wave * SPW * STRIDE;
-	_Float16* dimg = dimgs + wave * SPW * DS;
+	_Float16* img = imgs + wave * TSPW * STRIDE;
+	_Float16* dimg = dimgs + wave * TSPW * DS;
 
-	for (int t = threadIdx.x; t < FH / 8; t += BLOCK)
+	for (int t = threadIdx.x; t < FH / 8; t += TBLOCK)
 		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
-	for (int t = lane; t < SPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
-	for (int t = lane; t < SPW * DS / 8; t += 64) reinterpret_cast<h8*>(dimg)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	for (int t = lane; t < TSPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	for (int t = lane; t < TSPW * DS / 8; t += 64) reinterpret_cast<h8*>(dimg)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
 
-	f4 acc[N::slots()];
+	f4 acc[N::tslots()];
 #pragma unroll
-	for (int s = 0; s < N::slots(); ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
+	for (int s = 0; s < N::tslots(); ++s) acc[s] = f4{0.f, 0.f, 0.f, 0.f};
 
 	const uint32_t n_chunks = n_chunks_of(a.n);
 	// F = 2 with whole K chunks: the next chunk's inputs are fetched during the current one
-	const bool pref = a.F == 2 && (a.E % 8) == 0 && N::ENC_ROWS / 8 * SPW <= 128;
+	const bool pref = a.F == 2 && (a.E % 8) == 0 && N::ENC_ROWS / 8 * TSPW <= 128;
 	TrainPrefetch pf;
-	if (pref && blockIdx.x < n_chunks) train_fetch<N>(a, blockIdx.x * SAMPLES_PER_BLOCK + wave * SPW, lane, pf);
+	if (pref && blockIdx.x < n_chunks) train_fetch<N>(a, blockIdx.x * SAMPLES_PER_BLOCK + wave * TSPW, lane, pf);
 	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
 		__syncthreads();  // previous chunk's wgrad reads of every image are done
-		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
+		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * TSPW;
 		if (pref) {
 			train_commit<N, STRIDE, DS>(a, pf, img, dimg, N::template x_seg<true>(), base, lane);
 			const uint32_t nxt = chunk + gridDim.x;
-			if (nxt < n_chunks) train_fetch<N>(a, nxt * SAMPLES_PER_BLOCK + wave * SPW, lane, pf);
+			if (nxt < n_chunks) train_fetch<N>(a, nxt * SAMPLES_PER_BLOCK + wave * TSPW, lane, pf);
 		} else {
-			load_encoding<N, STRIDE>(a, img, base, lane);
-			load_sh<STRIDE>(a, img, N::template x_seg<true>(), base, lane);
+			load_encoding<N, STRIDE, TSPW>(a, img, base, lane);
+			load_sh<STRIDE, TSPW>(a, img, N::template x_seg<true>(), base, lane);
 			// delta of the rgb output layer: rows 0..2 = dL/drgb_raw (loss-scaled, rollover-weighted)
-			for (int t = lane; t < SPW * 4; t += 64) {
-				const int smp = t % SPW, ch = t / SPW;
+			for (int t = lane; t < TSPW * 4; t += 64) {
+				const int smp = t % TSPW, ch = t / TSPW;
 				const uint32_t i = base + smp;
 				h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 				if (ch == 0 && i < a.n) {
@@ -925,8 +933,8 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_train(MlpArgs a) {
 				lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
 			}
 		}
-		f4 res[CT];
-		fwd_range<N, true, 0, N::NL - 1>(frags, img, lane, res);
+		f4 res[TCT];
+		fwd_range<N, true, 0, N::NL - 1, TCT>(frags, img, lane, res);
 		bwd_range<N, N::NL - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
 	}
 	flush_range<N, 0>(a, wave, lane, acc);
@@ -1211,7 +1219,7 @@ void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc
 		m->mlp_partials.reserve((size_t)cu_count() * m->n_mlp_params);
 		a.partials = m->mlp_partials.ptr;
 		a.n_mlp = m->n_mlp_params;
-		launch_timed(k_mlp_train<N>, grid, BLOCK, lds, s, a);
+		launch_timed(k_mlp_train<N>, grid, TBLOCK, lds, s, a);
 		k_mlp_reduce<<<div_up(16 * m->n_mlp_params, 256), 256, 0, s>>>(m->mlp_partials.ptr, grid, m->n_mlp_params, grads_mlp);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
