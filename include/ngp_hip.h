@@ -187,6 +187,16 @@ typedef struct ngp_train_args {
 	uint32_t sharpness_res[2];
 	float* sharpness_grid;
 	int32_t sharpness_grid_clear;
+	/* learned image-plane distortion (Testbed::m_distortion, a TrainableBuffer<2, 2, float>):
+	 * distortion_map = device [res_y][res_x][2] f32 added to the camera-space ray direction's xy at the
+	 * pixel's uv, bilinear (uv_to_ray common_device.cuh:441-443, Buffer2DView::at_lerp common.h:249-266);
+	 * null = off.  distortion_gradient / distortion_gradient_weight = device [res_y][res_x][2] += the
+	 * kept rays' image-plane direction gradient / 1 (bilinear; compute_cam_gradient_train_nerf
+	 * src/testbed_nerf.cu:1234-1246, deposit_image_gradient common_device.cuh:82-115); null = off */
+	const float* distortion_map;
+	uint32_t distortion_res[2];
+	float* distortion_gradient;
+	float* distortion_gradient_weight;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {
@@ -237,6 +247,10 @@ typedef struct ngp_render_args {
 	/* Nerf::render_lens when render_with_lens_distortion (src/testbed_nerf.cu:1859): ELensMode + params */
 	int32_t lens_mode;
 	float lens_params[7];
+	/* the learned distortion map (m_distortion.inference_view(), src/testbed_nerf.cu:1854-1857) when
+	 * render_with_lens_distortion: device [res_y][res_x][2] f32; null = off */
+	const float* distortion_map;
+	uint32_t distortion_res[2];
 } ngp_render_args;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -63,6 +63,17 @@ struct m43 {
 	v3 c[4];
 };
 NGP_HD v3 rot(const m43& m, v3 d) { return m.c[0] * d.x + m.c[1] * d.y + m.c[2] * d.z; }
+// inverse(mat3(m)) * g with glm's adjugate / determinant inverse (column-major m[c][r])
+NGP_HD v3 inverse3_mul(const m43& m, v3 g) {
+	const float m00 = m.c[0].x, m01 = m.c[0].y, m02 = m.c[0].z;
+	const float m10 = m.c[1].x, m11 = m.c[1].y, m12 = m.c[1].z;
+	const float m20 = m.c[2].x, m21 = m.c[2].y, m22 = m.c[2].z;
+	const float inv_det = 1.0f / (m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) + m20 * (m01 * m12 - m11 * m02));
+	const float i00 = (m11 * m22 - m21 * m12) * inv_det, i10 = -(m10 * m22 - m20 * m12) * inv_det, i20 = (m10 * m21 - m20 * m11) * inv_det;
+	const float i01 = -(m01 * m22 - m21 * m02) * inv_det, i11 = (m00 * m22 - m20 * m02) * inv_det, i21 = -(m00 * m21 - m20 * m01) * inv_det;
+	const float i02 = (m01 * m12 - m11 * m02) * inv_det, i12 = -(m00 * m12 - m10 * m02) * inv_det, i22 = (m00 * m11 - m10 * m01) * inv_det;
+	return mk3(i00 * g.x + i10 * g.y + i20 * g.z, i01 * g.x + i11 * g.y + i21 * g.z, i02 * g.x + i12 * g.y + i22 * g.z);
+}
 
 // ---------------------------------------------------------------------------
 // Camera lenses — uv_to_ray's direction part (common_device.cuh:248-460).  Modes follow
@@ -127,6 +138,24 @@ NGP_HD void iterative_undistortion(const float* k, float* u, float* v) {
 }
 // Camera-space ray direction of screen position uv (not normalised); false: no ray (F-Theta
 // beyond its field of view -- the sampler then uses the camera axis, as the reference does)
+// Buffer2DView<const vec2>::at_lerp (common.h:249-266) of the learned distortion map
+// ([res_y][res_x][2] f32) at uv: bilinear between the texels around res * uv, clamped to the edge
+// (uv_to_ray adds it to the camera-space direction's xy, common_device.cuh:441-443).
+NGP_HD void distortion_at_lerp(const float* map, uint32_t rx, uint32_t ry, float u, float v, float* dx, float* dy) {
+	const float fx = (float)rx * u, fy = (float)ry * v;
+	const int px = (int)fx, py = (int)fy;
+	const float wx = fx - (float)px, wy = fy - (float)py;
+	const int x0 = px < 0 ? 0 : (px > (int)rx - 1 ? (int)rx - 1 : px), x1 = px + 1 < 0 ? 0 : (px + 1 > (int)rx - 1 ? (int)rx - 1 : px + 1);
+	const int y0 = py < 0 ? 0 : (py > (int)ry - 1 ? (int)ry - 1 : py), y1 = py + 1 < 0 ? 0 : (py + 1 > (int)ry - 1 ? (int)ry - 1 : py + 1);
+	const float w00 = (1.0f - wx) * (1.0f - wy), w10 = wx * (1.0f - wy), w01 = (1.0f - wx) * wy, w11 = wx * wy;
+	const float* a = map + 2 * ((size_t)y0 * rx + x0);
+	const float* b = map + 2 * ((size_t)y0 * rx + x1);
+	const float* c = map + 2 * ((size_t)y1 * rx + x0);
+	const float* d = map + 2 * ((size_t)y1 * rx + x1);
+	*dx = w00 * a[0] + w10 * b[0] + w01 * c[0] + w11 * d[0];
+	*dy = w00 * a[1] + w10 * b[1] + w01 * c[1] + w11 * d[1];
+}
+
 NGP_HD bool lens_direction(float u, float v, float res_x, float res_y, float fx, float fy, float cx, float cy, int mode,
                            const float* k, v3* dir) {
 	if (mode == LENS_FTHETA) {

@@ -543,6 +543,14 @@ PYBIND11_MODULE(pyngp, m) {
 			return d;
 		})
 		.def("sync", &Testbed::sync)
+		// the learned distortion map as a [res_y][res_x][2] array (an MI355X-side accessor for tests)
+		.def_property_readonly("distortion_map", [](const Testbed& t) {
+			const ivec2 r = t.distortion_resolution();
+			std::vector<float> p = t.distortion_map();
+			py::array_t<float> a({(py::ssize_t)r[1], (py::ssize_t)r[0], (py::ssize_t)2});
+			std::copy(p.begin(), p.end(), a.mutable_data());
+			return a;
+		})
 		.def_property_readonly("model_handle", [](const Testbed& t) { return (uintptr_t)t.model(); })
 		.def_property_readonly("stream_handle", [](const Testbed& t) { return (uintptr_t)t.stream(); })
 		// multi-GPU: one Testbed per rank (torchrun); gradients/grid all-reduced over RCCL

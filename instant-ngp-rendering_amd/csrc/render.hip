@@ -47,6 +47,8 @@ struct RenderK {
 	uint32_t n_local;
 	int lens_mode;
 	float lens_params[7];
+	const float* dmap;  // learned distortion map [dry][drx][2] (null: off; LENS instance only)
+	uint32_t drx, dry;
 	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
 	uint32_t pipe_index, pipe_count;  // this pipeline's 8-row blocks of the shard's rows
 	const uint8_t* bitfield;
@@ -192,6 +194,12 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 		*pp = Payload{};  // uv_to_ray returned Ray::invalid(): the pixel stays empty
 		pp->idx = idx;
 		return false;
+	}
+	if (LENS && k.dmap) {  // uv_to_ray: dir.xy += distortion.at_lerp(uv) (common_device.cuh:441-443)
+		float ddx, ddy;
+		distortion_at_lerp(k.dmap, k.drx, k.dry, u, v, &ddx, &ddy);
+		dir.x += ddx;
+		dir.y += ddy;
 	}
 	dir = rot(k.cam, dir);
 	v3 origin = k.cam.c[3] + dir * k.near_distance;
@@ -798,6 +806,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.density_act = m->cfg.density_activation;
 	k.lens_mode = a->lens_mode;
 	for (int q = 0; q < 7; ++q) k.lens_params[q] = a->lens_params[q];
+	if (a->distortion_map && a->distortion_res[0] && a->distortion_res[1]) {
+		k.dmap = a->distortion_map;
+		k.drx = a->distortion_res[0];
+		k.dry = a->distortion_res[1];
+	}
 	k.shard_count = std::max(a->shard_count, 1u);
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);
@@ -892,7 +905,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		pr.k.df = k.df;
 		pr.k.dbg = dbg;
 		if (pr.n == 0) continue;
-		(k.lens_mode != LENS_PERSPECTIVE ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, lds, pr.s>>>(
+		(k.lens_mode != LENS_PERSPECTIVE || k.dmap ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, lds, pr.s>>>(
 		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, pr.ps->counters.ptr);
 		pr.marching = true;
 	}

@@ -209,7 +209,7 @@ Testbed::~Testbed() {
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
 	if (m_pack) (void)hipFree(m_pack);
-	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid})
+	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid, m_dist, m_dist_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
@@ -838,6 +838,43 @@ void Testbed::build_model(const Json& cfg) {
 		opt = &(*opt)["nested"];
 	}
 	if (c.ema_decay == 0.0f) c.ema_decay = 0.0f;  // no Ema: inference params track the weights exactly
+	// the distortion map and its trainer (src/testbed.cu:3781-3792): zero map, fresh Adam
+	{
+		DistortionMap d;
+		if (cfg.contains("distortion_map")) {
+			const Json& dm = cfg["distortion_map"];
+			if (dm.contains("resolution") && dm["resolution"].is_array()) {
+				d.rx = (int)dm["resolution"][0].num();
+				d.ry = (int)dm["resolution"][1].num();
+			}
+			const Json* o = dm.contains("optimizer") ? &dm["optimizer"] : nullptr;
+			while (o && o->is_object()) {
+				const std::string ot = o->value("otype", std::string("Adam"));
+				if (ot == "ExponentialDecay") {
+					d.decay_start = (uint32_t)o->value("decay_start", 0.0);
+					d.decay_interval = (uint32_t)o->value("decay_interval", 10000.0);
+					d.decay_end = (uint32_t)o->value("decay_end", 4294967295.0);
+					d.decay_base = (float)o->value("decay_base", 0.33);
+				} else if (ot == "Adam") {
+					d.lr = (float)o->value("learning_rate", 1e-3);
+					d.beta1 = (float)o->value("beta1", 0.9);
+					d.beta2 = (float)o->value("beta2", 0.99);
+					d.eps = (float)o->value("epsilon", 1e-8);
+				} else throw std::runtime_error("distortion_map: unsupported optimizer '" + ot + "'");
+				o = o->contains("nested") ? &(*o)["nested"] : nullptr;
+			}
+		}
+		if (d.rx <= 0 || d.ry <= 0) throw std::runtime_error("distortion_map: resolution must be positive");
+		const size_t n = (size_t)d.rx * d.ry * 2;
+		d.params.assign(n, 0.0f);
+		d.m.assign(n, 0.0f);
+		d.v.assign(n, 0.0f);
+		d.steps.assign(n, 0u);
+		for (float* p : {m_dist, m_dist_grad})
+			if (p) (void)hipFree(p);
+		m_dist = m_dist_grad = nullptr;
+		m_distortion = d;
+	}
 	int device = 0;
 	hk(hipGetDevice(&device), "hipGetDevice");
 	if (m_model) {
@@ -895,8 +932,7 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (nerf.training.n_images_for_training == 0) return;
 	{
 		const NerfTraining& t = nerf.training;
-		if (t.optimize_distortion || t.optimize_extra_dims)
-			throw std::runtime_error("distortion-map / latent optimisation is not implemented by this build");
+		if (t.optimize_extra_dims) throw std::runtime_error("latent (extra dims) optimisation is not implemented by this build");
 	}
 	upload_dataset();
 	NerfCounters& ctr = nerf.training.counters_rgb;
@@ -953,8 +989,30 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 			hk(hipMemsetAsync(m_cam_grad, 0, n_img * 6 * sizeof(float), (hipStream_t)m_stream), "camera gradient clear");
 	}
 
+	// the learned distortion map (src/testbed_nerf.cu:2468-2474, 2787): applied to the training rays
+	// once it is being optimised, its gradients cleared at the start of every camera-update period
+	const size_t n_dist = m_distortion.params.size();
+	if (tr.optimize_distortion && !m_distortion.active) {
+		m_distortion.active = true;
+		hk(hipMalloc((void**)&m_dist, n_dist * sizeof(float)), "hipMalloc distortion map");
+		hk(hipMalloc((void**)&m_dist_grad, 2 * n_dist * sizeof(float)), "hipMalloc distortion gradients");
+		hk(hipMemcpyAsync(m_dist, m_distortion.params.data(), n_dist * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "distortion h2d");
+		hk(hipMemsetAsync(m_dist_grad, 0, 2 * n_dist * sizeof(float), (hipStream_t)m_stream), "distortion gradient clear");
+	}
+	if (m_distortion.active && tr.optimize_distortion && tr.n_steps_since_cam_update == 0)
+		hk(hipMemsetAsync(m_dist_grad, 0, 2 * n_dist * sizeof(float), (hipStream_t)m_stream), "distortion gradient clear");
+
 	ngp_train_args a{};
 	a.images = (const ngp_image*)m_dev_meta;
+	if (m_distortion.active) {
+		a.distortion_map = m_dist;
+		a.distortion_res[0] = (uint32_t)m_distortion.rx;
+		a.distortion_res[1] = (uint32_t)m_distortion.ry;
+		if (tr.optimize_distortion) {
+			a.distortion_gradient = m_dist_grad;
+			a.distortion_gradient_weight = m_dist_grad + n_dist;
+		}
+	}
 	a.exposure = m_exp;
 	a.exposure_gradient = tr.optimize_exposure ? m_exp_grad : nullptr;
 	a.cam_pos_gradient = tr.optimize_extrinsics ? m_cam_grad : nullptr;
@@ -1045,9 +1103,10 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (++tr.n_steps_since_error_map_update >= tr.n_steps_between_error_map_updates) update_error_map_cdf();
 	// camera parameters every n_steps_between_cam_updates (src/testbed_nerf.cu:2577-2680)
 	++tr.n_steps_since_cam_update;
-	const bool train_camera = tr.optimize_extrinsics || tr.optimize_focal_length || tr.optimize_exposure;
+	const bool train_camera = tr.optimize_extrinsics || tr.optimize_distortion || tr.optimize_focal_length || tr.optimize_exposure;
 	if (train_camera && tr.n_steps_since_cam_update >= tr.n_steps_between_cam_updates) {
 		if (tr.optimize_extrinsics) update_cam_extrinsics();
+		if (tr.optimize_distortion) update_distortion_map();
 		if (tr.optimize_focal_length) update_cam_focal_length();
 		if (tr.optimize_exposure) update_cam_exposure();
 		tr.n_steps_since_cam_update = 0;
@@ -1184,6 +1243,39 @@ void Testbed::update_cam_exposure() {
 	for (size_t i = n; i < n_img; ++i)
 		for (int k = 0; k < 3; ++k) e[3 * i + k] = tr.cam_exposure[i].variable[k];
 	hk(hipMemcpyAsync(m_exp, e.data(), e.size() * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "exposure h2d");
+}
+
+// Distortion branch of the camera update (src/testbed_nerf.cu:2630-2637): gradients divided by
+// their accumulated bilinear weights (safe_divide, :1548-1554), then one step of the map's
+// ExponentialDecay(Adam) trainer at loss scale LOSS_SCALE * n_steps_between_cam_updates.  The map
+// has no matrix parameters, so (as the network's hash grid) entries with a zero gradient are
+// skipped and no L2 term applies; the step counts are per parameter.
+void Testbed::update_distortion_map() {
+	DistortionMap& d = m_distortion;
+	const size_t n = d.params.size();
+	if (m_world > 1) allreduce_f32(m_dist_grad, 2 * n, false);
+	std::vector<float> g(2 * n);
+	hk(hipMemcpyAsync(g.data(), m_dist_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "distortion gradient d2h");
+	sync();
+	float lr = d.lr;
+	if (d.decay_interval > 0 && d.optimizer_step >= d.decay_start) {
+		const uint32_t s = std::min(d.optimizer_step, d.decay_end > 0 ? d.decay_end - 1 : 0u);
+		if (s >= d.decay_start) lr = d.lr * std::pow(d.decay_base, (float)((s - d.decay_start) / d.decay_interval + 1));
+	}
+	++d.optimizer_step;
+	const float loss_scale = 128.0f * (float)nerf.training.n_steps_between_cam_updates;
+	for (size_t i = 0; i < n; ++i) {
+		const float w = g[n + i];
+		const float graw = w > 0.0f ? g[i] / w : 0.0f;
+		if (graw == 0.0f) continue;
+		const float gs = graw / loss_scale;
+		d.m[i] = d.beta1 * d.m[i] + (1.0f - d.beta1) * gs;
+		d.v[i] = d.beta2 * d.v[i] + (1.0f - d.beta2) * gs * gs;
+		const uint32_t step = ++d.steps[i];
+		const float lr_t = lr * std::sqrt(1.0f - std::pow(d.beta2, (float)step)) / (1.0f - std::pow(d.beta1, (float)step));
+		d.params[i] = d.params[i] - (lr_t / (std::sqrt(d.v[i]) + d.eps)) * d.m[i];
+	}
+	hk(hipMemcpyAsync(m_dist, d.params.data(), n * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream), "distortion h2d");
 }
 
 // Extrinsics branch of the camera update (src/testbed_nerf.cu:2605-2628): per-image Adam on the
@@ -1412,6 +1504,11 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 	if (nerf.render_with_lens_distortion) {
 		r.lens_mode = (int32_t)nerf.render_lens.mode;
 		std::memcpy(r.lens_params, nerf.render_lens.params, sizeof(r.lens_params));
+		if (m_distortion.active) {  // m_distortion.inference_view() (src/testbed_nerf.cu:1854-1857)
+			r.distortion_map = m_dist;
+			r.distortion_res[0] = (uint32_t)m_distortion.rx;
+			r.distortion_res[1] = (uint32_t)m_distortion.ry;
+		}
 	}
 	const float bg[4] = {background_color[0], background_color[1], background_color[2], background_color[3]};
 	m_spp = 0;

@@ -216,6 +216,9 @@ public:
 	ngp_model* model() const { return m_model; }
 	void* stream() const { return m_stream; }
 	void sync() const;
+	// the learned distortion map's parameters, [res_y][res_x][2] (m_distortion.map->params())
+	std::vector<float> distortion_map() const { return m_distortion.params; }
+	ivec2 distortion_resolution() const { return {m_distortion.rx, m_distortion.ry}; }
 	ngp_train_stats last_stats() const { return m_last_stats; }
 	std::vector<float> density_grid() const;
 	std::vector<uint8_t> density_grid_bitfield() const;
@@ -282,6 +285,20 @@ private:
 	void update_cam_extrinsics();
 	void update_cam_focal_length();
 	float* m_cam_grad = nullptr;  // [2][n_images][3]: translation, rotation gradients (device)
+	// learned image-plane distortion (Testbed::m_distortion: TrainableBuffer<2, 2, float> with its own
+	// ExponentialDecay(Adam) trainer, src/testbed.cu:3781-3792, configs/nerf/base.json:57-73)
+	struct DistortionMap {
+		int rx = 32, ry = 32;
+		float lr = 1e-4f, beta1 = 0.9f, beta2 = 0.99f, eps = 1e-8f, decay_base = 0.33f;
+		uint32_t decay_start = 10000, decay_interval = 5000, decay_end = 25000;
+		std::vector<float> params, m, v;  // params start at zero (TrainableBuffer::initialize_params)
+		std::vector<uint32_t> steps;      // Adam's per-parameter step counts
+		uint32_t optimizer_step = 0;
+		bool active = false;  // applied to training rays once optimize_distortion was set (a zero map is the identity)
+	} m_distortion;
+	float* m_dist = nullptr;       // device params [ry][rx][2]
+	float* m_dist_grad = nullptr;  // device [2][ry][rx][2]: gradient, gradient weight
+	void update_distortion_map();
 	size_t m_cam_grad_cap = 0;
 	float current_learning_rate() const;
 	float* m_err = nullptr;

@@ -145,6 +145,8 @@ struct SamplerArgs {
 	float* ray_state;    // [R][8]
 	float* coords;       // [max][8]
 	float4* pos4;        // [max]: pos + warped dt again, 16-B rows the encoder reads once per level
+	const float* dmap;   // learned distortion map [dry][drx][2] (null: off; general instance only)
+	uint32_t drx, dry;
 };
 
 // Image and pixel of global training ray gi from its pcg32 stream (already advanced to
@@ -203,6 +205,12 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 		                  (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f));
 	} else if (lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1],
 	                          im.principal_point[0], im.principal_point[1], im.lens_mode, im.lens_params, &dir)) {
+		if (a.dmap) {
+			float ddx, ddy;
+			distortion_at_lerp(a.dmap, a.drx, a.dry, u, v, &ddx, &ddy);
+			dir.x += ddx;
+			dir.y += ddy;
+		}
 		dir = rot(xf, dir);
 	} else {
 		dir = xf.c[2];  // no ray through this pixel: the camera axis (src/testbed_nerf.cu:762-764)
@@ -556,6 +564,8 @@ struct LossArgs {
 	float depth_lambda;        // depth supervision (0: off)
 	int depth_loss_type;
 	float2* ray_depth;         // [R]: composited depth, lambda * dloss/ddepth (k_loss_composite -> k_loss_emit)
+	const float* dmap;         // learned distortion map (depth targets use the distorted direction's length)
+	uint32_t drx, dry;
 	// sharpness-weighted error deposits (null sharp_data: off)
 	const float* sharp_data;   // [n_images][res_y][res_x]
 	uint32_t sharp_rx, sharp_ry;
@@ -609,12 +619,19 @@ __global__ void __launch_bounds__(256) k_scale_floats(float* __restrict__ x, siz
 // image's value (along the optical axis) times it (src/testbed_nerf.cu:1013); the camera's
 // rotation keeps lengths, so the camera-space direction's length is the one
 template <bool GENERAL>
-__device__ __forceinline__ float unnormalized_dir_length(const ngp_image& im, float u, float v) {
+__device__ __forceinline__ float unnormalized_dir_length(const ngp_image& im, float u, float v, const float* dmap, uint32_t drx,
+                                                         uint32_t dry) {
 	v3 dir = mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
 	             (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
 	if (GENERAL && !lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1],
 	                               im.principal_point[0], im.principal_point[1], im.lens_mode, im.lens_params, &dir))
 		return 1.0f;  // no ray through the pixel: the camera axis (src/testbed_nerf.cu:762-764)
+	if (GENERAL && dmap) {
+		float ddx, ddy;
+		distortion_at_lerp(dmap, drx, dry, u, v, &ddx, &ddy);
+		dir.x += ddx;
+		dir.y += ddy;
+	}
 	return length(dir);
 }
 
@@ -747,7 +764,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 			int px = (int)(u * (float)im.width), py = (int)(v * (float)im.height);
 			px = px < 0 ? 0 : (px > (int)im.width - 1 ? (int)im.width - 1 : px);
 			py = py < 0 ? 0 : (py > (int)im.height - 1 ? (int)im.height - 1 : py);
-			const float target = unnormalized_dir_length<GENERAL>(im, u, v) *
+			const float target = unnormalized_dir_length<GENERAL>(im, u, v, a.dmap, a.drx, a.dry) *
 			                     reinterpret_cast<const float*>(im.depth)[(size_t)px + (size_t)py * im.width];
 			float ld, gd;
 			loss_and_gradient(target, depth_ray, a.depth_loss_type, &ld, &gd);
@@ -945,9 +962,34 @@ struct CamGradArgs {
 	const float* ccoords;        // [B][8]
 	const float* dpos;           // [B][3]
 	const float* dsh;            // [B][16]
-	float* cam_pos_gradient;     // [n_images][3]
+	float* cam_pos_gradient;     // [n_images][3] (null: off)
 	float* cam_rot_gradient;     // [n_images][3]
+	const ngp_image* images;     // the images' current transforms (distortion gradient)
+	float* dgrad;                // distortion map gradient / weight [dry][drx][2] (null: off)
+	float* dgrad_w;
+	uint32_t drx, dry;
 };
+
+// deposit_image_gradient (common_device.cuh:82-115): value into the four texels around res * uv,
+// bilinear weights, clamped to the edge; the weights into the weight buffer
+__device__ __forceinline__ void deposit_image_gradient(float gx, float gy, float* grad, float* gw, uint32_t rx, uint32_t ry,
+                                                       float u, float v) {
+	const float fx = (float)rx * u, fy = (float)ry * v;
+	const int px = (int)fx, py = (int)fy;
+	const float wx = fx - (float)px, wy = fy - (float)py;
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const float w = (k & 1 ? wx : 1.0f - wx) * (k & 2 ? wy : 1.0f - wy);
+		int x = px + (k & 1), y = py + (k >> 1);
+		x = x > (int)rx - 1 ? (int)rx - 1 : (x < 0 ? 0 : x);
+		y = y > (int)ry - 1 ? (int)ry - 1 : (y < 0 ? 0 : y);
+		const size_t o = 2 * ((size_t)x + (size_t)y * rx);
+		atomicAdd(&grad[o], gx * w);
+		atomicAdd(&gw[o], w);
+		atomicAdd(&grad[o + 1], gy * w);
+		atomicAdd(&gw[o + 1], w);
+	}
+}
 
 __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
@@ -970,6 +1012,15 @@ __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 	}
 	const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
 	const float inv_pdf = 1.0f / a.ray_aux[i].w;
+	if (a.dgrad) {
+		// the direction gradient's component orthogonal to the direction, rotated back into the
+		// camera's frame (inverse(mat3(xform)) * g), its xy splatted at the pixel (divided by the pdf)
+		const v3 og = gd - d * dot(gd, d);
+		const m43 xf = load_xform(a.images[img].xform);
+		const v3 ip = inverse3_mul(xf, og);
+		deposit_image_gradient(ip.x / a.ray_aux[i].w, ip.y / a.ray_aux[i].w, a.dgrad, a.dgrad_w, a.drx, a.dry, rs[6], rs[7]);
+	}
+	if (!a.cam_pos_gradient) return;
 	const v3 aa = mk3(d.y * gd.z - d.z * gd.y, d.z * gd.x - d.x * gd.z, d.x * gd.y - d.y * gd.x);
 	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 0], go.x * inv_pdf);
 	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 1], go.y * inv_pdf);
@@ -1237,9 +1288,14 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
 	sa.pos4 = reinterpret_cast<float4*>(ts.pos4.ptr);
+	if (t->distortion_map && t->distortion_res[0] && t->distortion_res[1]) {
+		sa.dmap = t->distortion_map;
+		sa.drx = t->distortion_res[0];
+		sa.dry = t->distortion_res[1];
+	}
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
-	const bool general = t->cdf_img || t->cdf_x_cond_y || t->has_lens;
+	const bool general = t->cdf_img || t->cdf_x_cond_y || t->has_lens || sa.dmap;
 	if (general) k_sample_count<true><<<div_up(R, 4), 256, 0, s>>>(sa);
 	else k_sample_count<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
@@ -1371,8 +1427,13 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.mean_density = m->gs.mean.ptr;
 	la.ray_eval = ts.chunked ? ts.ray_eval.ptr : nullptr;
 	la.violations = ts.counters.ptr + 9;
-	const bool cam = t->cam_pos_gradient && t->cam_rot_gradient;
+	// camera gradients: extrinsics and / or the distortion map's (compute_cam_gradient_train_nerf)
+	const bool dist_grad = sa.dmap && t->distortion_gradient && t->distortion_gradient_weight;
+	const bool cam = (t->cam_pos_gradient && t->cam_rot_gradient) || dist_grad;
 	la.store_uv_pdf = cam ? 1 : 0;
+	la.dmap = sa.dmap;
+	la.drx = sa.drx;
+	la.dry = sa.dry;
 	la.depth_lambda = t->depth_supervision_lambda > 0.0f ? t->depth_supervision_lambda : 0.0f;
 	la.max_mip = t->max_cascade;
 	if (t->sharpness_data && t->sharpness_grid && t->error_map) {
@@ -1470,6 +1531,14 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		ca.dsh = ts.dsh.ptr;
 		ca.cam_pos_gradient = t->cam_pos_gradient;
 		ca.cam_rot_gradient = t->cam_rot_gradient;
+		if (!(t->cam_pos_gradient && t->cam_rot_gradient)) ca.cam_pos_gradient = ca.cam_rot_gradient = nullptr;
+		ca.images = t->images;
+		if (dist_grad) {
+			ca.dgrad = t->distortion_gradient;
+			ca.dgrad_w = t->distortion_gradient_weight;
+			ca.drx = sa.drx;
+			ca.dry = sa.dry;
+		}
 		k_cam_gradient<<<div_up(R, 256), 256, 0, s>>>(ca);
 		NGP_HIP_CHECK(hipGetLastError());
 	}

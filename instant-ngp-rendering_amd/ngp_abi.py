@@ -63,6 +63,8 @@ class TrainArgs(C.Structure):
         ("depth_supervision_lambda", C.c_float), ("depth_loss_type", C.c_int32),
         ("sharpness_data", C.c_void_p), ("sharpness_res", C.c_uint32 * 2), ("sharpness_grid", C.c_void_p),
         ("sharpness_grid_clear", C.c_int32),
+        ("distortion_map", C.c_void_p), ("distortion_res", C.c_uint32 * 2), ("distortion_gradient", C.c_void_p),
+        ("distortion_gradient_weight", C.c_void_p),
     ]
 
 
@@ -93,6 +95,7 @@ class RenderArgs(C.Structure):
         ("min_transmittance", C.c_float), ("snap_to_pixel_centers", C.c_int32), ("use_inference_params", C.c_int32),
         ("train_in_linear_colors", C.c_int32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
         ("shard_rows", C.c_uint32), ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7),
+        ("distortion_map", C.c_void_p), ("distortion_res", C.c_uint32 * 2),
     ]
 
 

@@ -758,6 +758,37 @@ static Cam cam_of(const float* x) {
 	return m;
 }
 static V3 rot(const Cam& m, V3 d) { return m.c[0] * d.x + m.c[1] * d.y + m.c[2] * d.z; }
+
+// Buffer2DView<const vec2>::at_lerp (include/neural-graphics-primitives/common.h:249-266) of the
+// distortion map [ry][rx][2]: px = int(res * uv), weights = fraction, texels clamped to the edge;
+// uv_to_ray adds it to the camera-space direction's xy (common_device.cuh:441-443)
+static void distortion_lerp(const float* map, uint32_t rx, uint32_t ry, float u, float vv, float* dx, float* dy) {
+	const float fx = (float)rx * u, fy = (float)ry * vv;
+	const int px = (int)fx, py = (int)fy;
+	const float wx = fx - (float)px, wy = fy - (float)py;
+	auto at = [&](int x, int y, int c) {
+		x = std::min(std::max(x, 0), (int)rx - 1);
+		y = std::min(std::max(y, 0), (int)ry - 1);
+		return map[2 * ((size_t)y * rx + x) + c];
+	};
+	for (int c = 0; c < 2; ++c) {
+		const float r = (1.0f - wx) * (1.0f - wy) * at(px, py, c) + wx * (1.0f - wy) * at(px + 1, py, c) +
+		                (1.0f - wx) * wy * at(px, py + 1, c) + wx * wy * at(px + 1, py + 1, c);
+		*(c ? dy : dx) = r;
+	}
+}
+
+// inverse(mat3(m)) * g, glm's adjugate / determinant inverse (compute_cam_gradient_train_nerf
+// src/testbed_nerf.cu:1242)
+static V3 inv3_mul(const Cam& m, V3 g) {
+	const float m00 = m.c[0].x, m01 = m.c[0].y, m02 = m.c[0].z, m10 = m.c[1].x, m11 = m.c[1].y, m12 = m.c[1].z;
+	const float m20 = m.c[2].x, m21 = m.c[2].y, m22 = m.c[2].z;
+	const float id = 1.0f / (m00 * (m11 * m22 - m21 * m12) - m10 * (m01 * m22 - m21 * m02) + m20 * (m01 * m12 - m11 * m02));
+	const float i00 = (m11 * m22 - m21 * m12) * id, i10 = -(m10 * m22 - m20 * m12) * id, i20 = (m10 * m21 - m20 * m11) * id;
+	const float i01 = -(m01 * m22 - m21 * m02) * id, i11 = (m00 * m22 - m20 * m02) * id, i21 = -(m00 * m21 - m20 * m01) * id;
+	const float i02 = (m01 * m12 - m11 * m02) * id, i12 = -(m00 * m12 - m10 * m02) * id, i22 = (m00 * m11 - m10 * m01) * id;
+	return v(i00 * g.x + i10 * g.y + i20 * g.z, i01 * g.x + i11 * g.y + i21 * g.z, i02 * g.x + i12 * g.y + i22 * g.z);
+}
 static uint32_t texel(const ngp_image& im, float u, float vv) {
 	const int px = std::min(std::max((int)(u * (float)im.width), 0), (int)im.width - 1);
 	const int py = std::min(std::max((int)(vv * (float)im.height), 0), (int)im.height - 1);
@@ -933,10 +964,17 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	const Cam x = cam_of(im.xform);
 	V3 dir;
 	if (lens_dir(u, vv, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
-	             im.principal_point[1], im.lens_mode, im.lens_params, &dir))
+	             im.principal_point[1], im.lens_mode, im.lens_params, &dir)) {
+		if (a.distortion_map && a.distortion_res[0] && a.distortion_res[1]) {
+			float ddx, ddy;
+			distortion_lerp(a.distortion_map, a.distortion_res[0], a.distortion_res[1], u, vv, &ddx, &ddy);
+			dir.x += ddx;
+			dir.y += ddy;
+		}
 		dir = rot(x, dir);
-	else
+	} else {
 		dir = x.c[2];  // src/testbed_nerf.cu:762-764
+	}
 	*o = x.c[3];
 	if (dlen) *dlen = len(dir);  // |rays_in_unnormalized[i].d| (src/testbed_nerf.cu:1013)
 	*d = normalize(dir);
@@ -1060,7 +1098,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1119)
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	std::vector<uint32_t> cc(R, 0);
-	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f), ray_uv_pdf(R, 1.0f);
+	std::vector<float> lstate(8 * (size_t)R, 0.0f), expg(3 * (size_t)R, 0.0f), ray_uv_pdf(R, 1.0f), ray_uv(2 * (size_t)R, 0.0f);
 	// depth supervision (src/testbed_nerf.cu:1013-1015): composited depth and lambda * dloss/ddepth per ray
 	const bool depth_on = a.depth_supervision_lambda > 0.0f;
 	// include_sharpness_in_error (src/testbed_nerf.cu:1036-1044, 2453-2464)
@@ -1105,6 +1143,8 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		float u, vv, pdf, uv_pdf;
 		const uint32_t img = pick_pixel(a, gi, nrg, rng, &u, &vv, &pdf, &uv_pdf);
 		ray_uv_pdf[i] = uv_pdf;
+		ray_uv[2 * i] = u;
+		ray_uv[2 * i + 1] = vv;
 		const ngp_image& im = a.images[img];
 		rng.advance(1);
 		V3 bg = v(a.background_color[0], a.background_color[1], a.background_color[2]);
@@ -1254,7 +1294,10 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	for (uint32_t l = 0; l < M.L; ++l)
 		for (uint32_t j = 0; j < C; ++j)
 			for (uint32_t f = 0; f < M.F; ++f) ce[((size_t)l * C + j) * M.F + f] = cenc[((size_t)l * B + j) * M.F + f];
-	const bool cam = a.cam_pos_gradient && a.cam_rot_gradient;
+	const bool ext = a.cam_pos_gradient && a.cam_rot_gradient;
+	const bool dist = a.distortion_map && a.distortion_res[0] && a.distortion_res[1] && a.distortion_gradient &&
+	                  a.distortion_gradient_weight;
+	const bool cam = ext || dist;
 	std::vector<float> dsh(cam ? 16 * (size_t)C : 0), dpos(cam ? 3 * (size_t)C : 0);
 	mlp_backward(M, M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
 	             cam ? dsh.data() : nullptr);
@@ -1277,8 +1320,29 @@ static void train_step(Model& M, const ngp_train_args& a) {
 				gd = gd + pg * len(pos - o) + sh4_input_grad(c + 4, &dsh[16 * s2]);
 			}
 			const uint32_t img = (uint32_t)lstate[8 * (size_t)i + 7];
-			const V3 aa = v(d.y * gd.z - d.z * gd.y, d.z * gd.x - d.x * gd.z, d.x * gd.y - d.y * gd.x);
 			const float p = ray_uv_pdf[i];
+			if (dist) {
+				// the direction gradient orthogonal to the direction, in the camera's frame, splatted
+				// bilinearly at the pixel (src/testbed_nerf.cu:1234-1246, deposit_image_gradient
+				// common_device.cuh:82-115)
+				const V3 og = gd - d * dot(gd, d);
+				const V3 ip = inv3_mul(cam_of(a.images[img].xform), og);
+				const uint32_t rx = a.distortion_res[0], ry = a.distortion_res[1];
+				const float fx = (float)rx * ray_uv[2 * i], fy = (float)ry * ray_uv[2 * i + 1];
+				const int px = (int)fx, py = (int)fy;
+				const float wx = fx - (float)px, wy = fy - (float)py;
+				const float val[2] = {ip.x / p, ip.y / p};
+				for (int k = 0; k < 4; ++k) {
+					const float w = (k & 1 ? wx : 1.0f - wx) * (k & 2 ? wy : 1.0f - wy);
+					const int x = std::min(std::max(px + (k & 1), 0), (int)rx - 1), y = std::min(std::max(py + (k >> 1), 0), (int)ry - 1);
+					for (int c = 0; c < 2; ++c) {
+						a.distortion_gradient[2 * ((size_t)x + (size_t)y * rx) + c] += val[c] * w;
+						a.distortion_gradient_weight[2 * ((size_t)x + (size_t)y * rx) + c] += w;
+					}
+				}
+			}
+			if (!ext) continue;
+			const V3 aa = v(d.y * gd.z - d.z * gd.y, d.z * gd.x - d.x * gd.z, d.x * gd.y - d.y * gd.x);
 			a.cam_pos_gradient[3 * img + 0] += go.x / p;
 			a.cam_pos_gradient[3 * img + 1] += go.y / p;
 			a.cam_pos_gradient[3 * img + 2] += go.z / p;
@@ -1447,6 +1511,12 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			if (!lens_dir(u, vv, (float)a.width, (float)a.height, a.focal_length[0], a.focal_length[1], a.screen_center[0],
 			              a.screen_center[1], a.lens_mode, a.lens_params, &d))
 				continue;  // invalid ray: the pixel stays empty
+			if (a.distortion_map && a.distortion_res[0] && a.distortion_res[1]) {
+				float ddx, ddy;
+				distortion_lerp(a.distortion_map, a.distortion_res[0], a.distortion_res[1], u, vv, &ddx, &ddy);
+				d.x += ddx;
+				d.y += ddy;
+			}
 			d = rot(cam, d);
 			const V3 o = cam.c[3] + d * a.near_distance;
 			d = normalize(d);

@@ -689,3 +689,105 @@ def test_train_step_ray_offset_is_a_slice_of_the_global_batch():
             np.testing.assert_array_equal(a_, b_)
     finally:
         g.close()
+
+
+def _distortion_map(rng, rx=8, ry=6, scale=0.02):
+    return rng.uniform(-scale, scale, (ry, rx, 2)).astype(np.float32)
+
+
+def test_train_step_distortion_map_matches_oracle():
+    """The learned distortion map (uv_to_ray common_device.cuh:441-443, Buffer2DView::at_lerp
+    common.h:249-266): training rays bend by the bilinear map value at the pixel -- sample counts and
+    coordinates bit for bit against the oracle -- and compute_cam_gradient_train_nerf's distortion
+    branch (src/testbed_nerf.cu:1234-1246) splats the camera-frame image-plane direction gradient and
+    the bilinear weights (deposit_image_gradient) into the map's gradient buffers (fp32 atomics over
+    fp16 MLP gradients: 5e-2 relative)."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 384, 4096, 1 << 15
+        dmap = _distortion_map(rng)
+        ry, rx = dmap.shape[:2]
+        dmap_d = torch.from_numpy(dmap).cuda()
+        grad_h, grad_d = np.zeros((2, ry, rx, 2), np.float32), torch.zeros(2, ry, rx, 2, device="cuda")
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        for a_, m_, gp in ((ga, dmap_d.data_ptr(), grad_d.data_ptr()), (oa, dmap.ctypes.data, grad_h.ctypes.data)):
+            a_.distortion_map = m_
+            a_.distortion_res[0], a_.distortion_res[1] = rx, ry
+            a_.distortion_gradient = gp
+            a_.distortion_gradient_weight = gp + 4 * ry * rx * 2
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+        g_ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        o_ns = o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        np.testing.assert_array_equal(g_ns, o_ns)
+        g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+        n = int(o_ns[:, 0].sum())
+        np.testing.assert_array_equal(g_c[:n, :7], o_c[:n, :7])
+        np.testing.assert_array_equal(gpu_scratch(g, A.SCRATCH_RAY_COMPACTED, np.uint32),
+                                      o.scratch(A.SCRATCH_RAY_COMPACTED, np.uint32))
+        gg = grad_d.cpu().numpy()
+        # the weights are sums of bilinear weights over the same pixels: tight
+        np.testing.assert_allclose(gg[1], grad_h[1], rtol=1e-5, atol=1e-5)
+        assert grad_h[1].sum() > 10 and np.abs(grad_h[0]).sum() > 0
+        assert np.linalg.norm(gg[0] - grad_h[0]) / np.linalg.norm(grad_h[0]) < 5e-2
+        # a zero map is the identity: the same coordinates as no map at all
+        g2, o2, _ = pair(CFG_A)
+        try:
+            set_bitfield_both(g2, o2, sphere_bitfield(0.32))
+            z = torch.zeros_like(dmap_d)
+            a2 = train_args(dd.ptr, dd.n, R, B, MS)
+            a2.distortion_map = z.data_ptr()
+            a2.distortion_res[0], a2.distortion_res[1] = rx, ry
+            g2.zero_grads()
+            A.check(g2.lib.ngp_train_step(g2.h, C.byref(a2), stream()))
+            torch.cuda.synchronize()
+            o2.train_step(train_args(hd.ptr, hd.n, R, B, MS))
+            z_c = gpu_scratch(g2, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+            nz = int(o2.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)[:, 0].sum())
+            np.testing.assert_array_equal(z_c[:nz, :7], o2.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:nz, :7])
+        finally:
+            g2.close()
+    finally:
+        g.close()
+
+
+def test_render_distortion_map_matches_oracle():
+    """render_with_lens_distortion with a learned distortion map (m_distortion.inference_view(),
+    src/testbed_nerf.cu:1854-1857): rendered RGB within 1e-3 mean L1 of the oracle, and different
+    from the undistorted frame."""
+    g, o, rng = pair(CFG_A, grid_scale=1.0)
+    try:
+        set_bitfield_both(g, o, sphere_bitfield(0.3))
+        W, H = 40, 32
+        cam = make_views(1, 8, 8)[1][0]
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        dmap = _distortion_map(rng, 5, 4, 0.08)
+        dmap_d = torch.from_numpy(dmap).cuda()
+        frames = []
+        for with_map in (True, False):
+            ra = render_args(W, H, cam, focal, spp=0, snap=1)
+            if with_map:
+                ra.distortion_map = dmap_d.data_ptr()
+                ra.distortion_res[0], ra.distortion_res[1] = 5, 4
+            frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+            depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+            A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()),
+                                     stream()))
+            torch.cuda.synchronize()
+            gf = frame.cpu().numpy().reshape(H, W, 4)
+            if with_map:
+                ra.distortion_map = dmap.ctypes.data
+                of, _ = o.render(ra)
+                assert (of[..., 3] > 0.01).mean() > 0.2
+                assert np.abs(gf - of).mean() < 1e-3
+            frames.append(gf)
+        assert np.abs(frames[0] - frames[1]).mean() > 1e-3
+    finally:
+        g.close()

@@ -396,3 +396,34 @@ def test_sharpness_weighted_error_map_through_the_testbed(scene):
         losses.append(tb.loss)
     assert np.isfinite(losses).all() and losses[-1] < losses[0]
     assert np.asarray(tr.error_map).sum() > 0
+
+
+def test_distortion_map_optimisation(scene):
+    """optimize_distortion: the Testbed's distortion map (a [32][32][2] TrainableBuffer, zero at
+    start; configs/nerf/base.json:57-73) is applied to the training rays and stepped every
+    n_steps_between_cam_updates by its own ExponentialDecay(Adam) on the weight-normalised splatted
+    gradients (src/testbed_nerf.cu:2630-2637); render_with_lens_distortion renders through it."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    tr = tb.nerf.training
+    tb.shall_train = True
+    while tb.training_step < 200:
+        tb.frame()
+    assert np.abs(tb.distortion_map).max() == 0.0
+    tr.optimize_distortion = True
+    losses = []
+    while tb.training_step < 400:
+        tb.frame()
+        losses.append(tb.loss)
+    d = tb.distortion_map
+    assert d.shape == (32, 32, 2)
+    assert np.isfinite(d).all() and np.isfinite(losses).all()
+    # 12 updates of Adam at lr 1e-4 move the touched texels by at most ~12 lr
+    assert 0 < np.abs(d).max() < 2e-3
+    assert (np.abs(d) > 0).mean() > 0.05
+    tb.set_camera_to_training_view(0)
+    assert tb.nerf.render_with_lens_distortion
+    f = tb.render(64, 64, 1, True)
+    assert np.isfinite(f).all() and f[..., 3].max() > 0.1
