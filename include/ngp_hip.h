@@ -125,6 +125,12 @@ typedef struct ngp_image {
 	 * width*height f32 depths along the optical axis, already multiplied by integer_depth_scale and the
 	 * dataset scale (src/nerf_loader.cu:73-82, 728); 0 = no depth for this image */
 	uint64_t depth;
+	/* rolling shutter / motion blur (TrainingXForm::end, TrainingImageMetadata::rolling_shutter;
+	 * get_xform_given_rolling_shutter common_device.cuh:633-636): the ray's camera is
+	 * camera_slerp(xform, xform_end, A + B u + C v + D motionblur_time); all-zero = xform (the
+	 * sampler honours it in its general instance: set ngp_train_args.has_lens) */
+	float xform_end[12];
+	float rolling_shutter[4];
 } ngp_image;
 
 typedef struct ngp_train_args {
@@ -159,7 +165,7 @@ typedef struct ngp_train_args {
 	const float* cdf_y;         /* device [n_images][cdf_res_y] */
 	const float* cdf_img;       /* device [n_images] normalised image CDF: sample_image_proportional_to_error; null = uniform */
 	uint32_t cdf_res[2];        /* x, y */
-	int32_t has_lens;           /* 1 if any image has a non-pinhole lens (selects the general sampler kernels) */
+	int32_t has_lens;           /* 1 if any image has a non-pinhole lens or a rolling shutter (selects the general sampler kernels) */
 	/* per-image exposure (Nerf::Training::cam_exposure, src/testbed_nerf.cu:966-985, 1121-1134) */
 	const float* exposure;      /* device [n_images][3] log2 scale of the target colours; null = 0 */
 	float* exposure_gradient;   /* device [n_images][3] += dL/dexposure of the kept rays; null = off */
@@ -247,6 +253,11 @@ typedef struct ngp_render_args {
 	/* Nerf::render_lens when render_with_lens_distortion (src/testbed_nerf.cu:1859): ELensMode + params */
 	int32_t lens_mode;
 	float lens_params[7];
+	/* motion blur / rolling shutter of rendered rays (init_rays_with_payload_kernel_nerf,
+	 * src/testbed_nerf.cu:1416): camera_slerp(camera, camera_end, A + B u + C v + D
+	 * ld_random_val(sample_index, pixel * 72239731)); all-zero rolling_shutter = camera */
+	float camera_end[12];
+	float rolling_shutter[4];
 	/* the learned distortion map (m_distortion.inference_view(), src/testbed_nerf.cu:1854-1857) when
 	 * render_with_lens_distortion: device [res_y][res_x][2] f32; null = off */
 	const float* distortion_map;

@@ -63,6 +63,60 @@ struct m43 {
 	v3 c[4];
 };
 NGP_HD v3 rot(const m43& m, v3 d) { return m.c[0] * d.x + m.c[1] * d.y + m.c[2] * d.z; }
+// camera_slerp (common_device.cuh:628-631): rotation slerped through quaternions, translation
+// mixed.  The quaternion conversions and slerp live in tcnn's vec.h, which is absent from the
+// mount; they are restated from glm (quat_cast, slerp with the lerp fallback at cos > 1 - eps,
+// mat3_cast), so the interpolated camera is parity-unpinned beyond t = 0 (start returned exactly).
+struct q4 {
+	float w, x, y, z;
+};
+NGP_HD q4 quat_from_rot(const m43& m) {
+	const float m00 = m.c[0].x, m01 = m.c[0].y, m02 = m.c[0].z, m10 = m.c[1].x, m11 = m.c[1].y, m12 = m.c[1].z;
+	const float m20 = m.c[2].x, m21 = m.c[2].y, m22 = m.c[2].z;
+	const float fx = m00 - m11 - m22, fy = m11 - m00 - m22, fz = m22 - m00 - m11, fw = m00 + m11 + m22;
+	int bi = 0;
+	float fb = fw;
+	if (fx > fb) { fb = fx; bi = 1; }
+	if (fy > fb) { fb = fy; bi = 2; }
+	if (fz > fb) { fb = fz; bi = 3; }
+	const float bv = sqrtf(fb + 1.0f) * 0.5f, mult = 0.25f / bv;
+	q4 q;
+	if (bi == 0) q = {bv, (m12 - m21) * mult, (m20 - m02) * mult, (m01 - m10) * mult};
+	else if (bi == 1) q = {(m12 - m21) * mult, bv, (m01 + m10) * mult, (m20 + m02) * mult};
+	else if (bi == 2) q = {(m20 - m02) * mult, (m01 + m10) * mult, bv, (m12 + m21) * mult};
+	else q = {(m01 - m10) * mult, (m20 + m02) * mult, (m12 + m21) * mult, bv};
+	return q;
+}
+NGP_HD q4 quat_slerp(q4 a, q4 b, float t) {
+	float c = a.w * b.w + a.x * b.x + a.y * b.y + a.z * b.z;
+	if (c < 0.0f) {
+		b = {-b.w, -b.x, -b.y, -b.z};
+		c = -c;
+	}
+	if (c > 1.0f - 1.1920928955078125e-7f)
+		return {a.w * (1.0f - t) + b.w * t, a.x * (1.0f - t) + b.x * t, a.y * (1.0f - t) + b.y * t, a.z * (1.0f - t) + b.z * t};
+	const float ang = acosf(c), s0 = sinf((1.0f - t) * ang), s1 = sinf(t * ang), inv = 1.0f / sinf(ang);
+	return {(s0 * a.w + s1 * b.w) * inv, (s0 * a.x + s1 * b.x) * inv, (s0 * a.y + s1 * b.y) * inv, (s0 * a.z + s1 * b.z) * inv};
+}
+NGP_HD m43 camera_slerp(const m43& a, const m43& b, float t) {
+	if (t == 0.0f) return a;
+	q4 q = quat_slerp(quat_from_rot(a), quat_from_rot(b), t);
+	const float n = sqrtf(q.w * q.w + q.x * q.x + q.y * q.y + q.z * q.z), in = 1.0f / n;
+	q = {q.w * in, q.x * in, q.y * in, q.z * in};
+	const float xx = q.x * q.x, yy = q.y * q.y, zz = q.z * q.z, xz = q.x * q.z, xy = q.x * q.y, yz = q.y * q.z;
+	const float wx = q.w * q.x, wy = q.w * q.y, wz = q.w * q.z;
+	m43 r;
+	r.c[0] = mk3(1.0f - 2.0f * (yy + zz), 2.0f * (xy + wz), 2.0f * (xz - wy));
+	r.c[1] = mk3(2.0f * (xy - wz), 1.0f - 2.0f * (xx + zz), 2.0f * (yz + wx));
+	r.c[2] = mk3(2.0f * (xz + wy), 2.0f * (yz - wx), 1.0f - 2.0f * (xx + yy));
+	r.c[3] = mk3(a.c[3].x * (1.0f - t) + b.c[3].x * t, a.c[3].y * (1.0f - t) + b.c[3].y * t, a.c[3].z * (1.0f - t) + b.c[3].z * t);
+	return r;
+}
+// get_xform_given_rolling_shutter (common_device.cuh:633-636): pixel time A + B u + C v + D motionblur_time
+NGP_HD m43 xform_given_rolling_shutter(const m43& start, const m43& end, const float* rs, float u, float v, float mb) {
+	return camera_slerp(start, end, rs[0] + rs[1] * u + rs[2] * v + rs[3] * mb);
+}
+
 // inverse(mat3(m)) * g with glm's adjugate / determinant inverse (column-major m[c][r])
 NGP_HD v3 inverse3_mul(const m43& m, v3 g) {
 	const float m00 = m.c[0].x, m01 = m.c[0].y, m02 = m.c[0].z;

@@ -195,13 +195,20 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("lens", &TrainingImageMetadata::lens)
 		.def_readwrite("resolution", &TrainingImageMetadata::resolution)
 		.def_readwrite("principal_point", &TrainingImageMetadata::principal_point)
-		.def_readwrite("focal_length", &TrainingImageMetadata::focal_length);
+		.def_readwrite("focal_length", &TrainingImageMetadata::focal_length)
+		.def_readwrite("rolling_shutter", &TrainingImageMetadata::rolling_shutter);
 
 	py::class_<NerfDataset>(m, "NerfDataset")
 		.def_readonly("metadata", &NerfDataset::metadata)
 		.def_property_readonly("transforms", [](const NerfDataset& d) {
 			py::list l;
 			for (const auto& x : d.xforms) l.append(mat43_to_numpy(x));
+			return l;
+		})
+		// TrainingXForm::end per image (= the start transform unless transform_matrix_end was given)
+		.def_property_readonly("transforms_end", [](const NerfDataset& d) {
+			py::list l;
+			for (size_t i = 0; i < d.xforms.size(); ++i) l.append(mat43_to_numpy(i < d.xforms_end.size() ? d.xforms_end[i] : d.xforms[i]));
 			return l;
 		})
 		.def_readonly("paths", &NerfDataset::paths)
@@ -325,6 +332,15 @@ PYBIND11_MODULE(pyngp, m) {
 			     v.tb->set_camera_extrinsics(frame_idx, rm.data(), convert);
 		     },
 		     py::arg("frame_idx"), py::arg("camera_to_world"), py::arg("convert_to_ngp") = true)
+		.def("set_camera_extrinsics_rolling_shutter",
+		     [](TrainingView& v, int frame_idx, py::array_t<float, py::array::c_style | py::array::forcecast> start,
+		        py::array_t<float, py::array::c_style | py::array::forcecast> end, const vec4& rolling_shutter, bool convert) {
+			     auto s = numpy_to_rowmajor34(start);
+			     auto e = numpy_to_rowmajor34(end);
+			     v.tb->set_camera_extrinsics_rolling_shutter(frame_idx, s.data(), e.data(), rolling_shutter, convert);
+		     },
+		     py::arg("frame_idx"), py::arg("camera_to_world_start"), py::arg("camera_to_world_end"), py::arg("rolling_shutter"),
+		     py::arg("convert_to_ngp") = true)
 		.def("get_camera_extrinsics", [](TrainingView& v, int i) { return mat43_to_numpy(v.tb->get_camera_extrinsics(i)); },
 		     py::arg("frame_idx"))
 		.def("set_image",

@@ -47,6 +47,9 @@ struct RenderK {
 	uint32_t n_local;
 	int lens_mode;
 	float lens_params[7];
+	m43 cam_end;        // motion blur / rolling shutter: the pixel's camera slerps toward it
+	float rs[4];
+	int rs_on;
 	const float* dmap;  // learned distortion map [dry][drx][2] (null: off; LENS instance only)
 	uint32_t drx, dry;
 	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
@@ -190,6 +193,9 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 	ld_random_pixel_offset(k.snap ? 0u : k.sample_index, &ox, &oy);
 	const float u = ((float)x + ox) / (float)k.W, v = ((float)y + oy) / (float)k.H;
 	v3 dir = mk3((u - k.scx) * (float)k.W / k.fx, (v - k.scy) * (float)k.H / k.fy, 1.0f);
+	// get_xform_given_rolling_shutter (src/testbed_nerf.cu:1416)
+	const m43 cam = k.rs_on ? xform_given_rolling_shutter(k.cam, k.cam_end, k.rs, u, v, ld_random_val(k.sample_index, idx * 72239731u))
+	                        : k.cam;
 	if (LENS && !lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
 		*pp = Payload{};  // uv_to_ray returned Ray::invalid(): the pixel stays empty
 		pp->idx = idx;
@@ -201,8 +207,8 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 		dir.x += ddx;
 		dir.y += ddy;
 	}
-	dir = rot(k.cam, dir);
-	v3 origin = k.cam.c[3] + dir * k.near_distance;
+	dir = rot(cam, dir);
+	v3 origin = cam.c[3] + dir * k.near_distance;
 
 	Payload p;
 	p.max_weight = 0.0f;
@@ -806,6 +812,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.density_act = m->cfg.density_activation;
 	k.lens_mode = a->lens_mode;
 	for (int q = 0; q < 7; ++q) k.lens_params[q] = a->lens_params[q];
+	for (int c = 0; c < 4; ++c) k.cam_end.c[c] = mk3(a->camera_end[3 * c], a->camera_end[3 * c + 1], a->camera_end[3 * c + 2]);
+	for (int q = 0; q < 4; ++q) {
+		k.rs[q] = a->rolling_shutter[q];
+		k.rs_on |= a->rolling_shutter[q] != 0.0f;
+	}
 	if (a->distortion_map && a->distortion_res[0] && a->distortion_res[1]) {
 		k.dmap = a->distortion_map;
 		k.drx = a->distortion_res[0];

@@ -352,9 +352,17 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 			if (y != 0) { fl = {y, y}; return true; }
 			return false;
 		};
+		// rolling_shutter [A, B, C(, D)] (src/nerf_loader.cu:204-216), global and per frame
+		auto read_rolling_shutter = [](const Json& src, vec4& rs) {
+			if (!src.contains("rolling_shutter")) return;
+			const Json& r = src["rolling_shutter"];
+			rs = {(float)r[0].num(), (float)r[1].num(), (float)r[2].num(), r.size() >= 4 ? (float)r[3].num() : 0.f};
+		};
 		Lens lens;
 		vec2 pp = {0.5f, 0.5f};
+		vec4 rolling_shutter = {0.f, 0.f, 0.f, 0.f};
 		read_lens(j, lens, pp);
+		read_rolling_shutter(j, rolling_shutter);
 		for (const Json& fr : frames) {
 			std::string fp = fr.value("file_path", std::string());
 			std::replace(fp.begin(), fp.end(), '\\', '/');
@@ -379,11 +387,18 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 			got |= read_focal(fr, md.focal_length, w, h);
 			if (!got) throw std::runtime_error("Couldn't read fov.");
 			read_lens(fr, md.lens, md.principal_point);
+			md.rolling_shutter = rolling_shutter;
+			read_rolling_shutter(fr, md.rolling_shutter);  // per-frame override
 			const Json& tm = fr.contains("transform_matrix_start") ? fr["transform_matrix_start"] : fr["transform_matrix"];
-			float r[12];
+			const Json& tme = fr.contains("transform_matrix_end") ? fr["transform_matrix_end"] : tm;
+			float r[12], re[12];
 			for (int row = 0; row < 3; ++row)
-				for (int col = 0; col < 4; ++col) r[row * 4 + col] = (float)tm[row][col].num();
+				for (int col = 0; col < 4; ++col) {
+					r[row * 4 + col] = (float)tm[row][col].num();
+					re[row * 4 + col] = (float)tme[row][col].num();
+				}
 			ds.xforms.push_back(ds.nerf_matrix_to_ngp(r));
+			ds.xforms_end.push_back(ds.nerf_matrix_to_ngp(re));  // = start without transform_matrix_end
 			ds.metadata.push_back(md);
 			ds.paths.push_back(fp);
 			ds.pixels.push_back(std::move(rgba));
@@ -464,6 +479,7 @@ void Testbed::create_empty_nerf_dataset(size_t n_images, int aabb_scale, bool is
 	ds.offset = {0.f, 0.f, 0.f};
 	ds.metadata.resize(n_images);
 	ds.xforms.resize(n_images);
+	ds.xforms_end.clear();  // end = start
 	ds.paths.resize(n_images);
 	ds.pixels.resize(n_images);
 	nerf.training.dataset = std::move(ds);
@@ -526,6 +542,20 @@ void Testbed::set_camera_extrinsics(int frame_idx, const float* c2w, bool conver
 			for (int row = 0; row < 3; ++row) m.m[3 * col + row] = c2w[row * 4 + col];
 		ds.xforms[frame_idx] = m;
 	}
+	if ((size_t)frame_idx < ds.xforms_end.size()) ds.xforms_end[frame_idx] = ds.xforms[frame_idx];  // end = start
+	if ((size_t)frame_idx < ds.metadata.size()) ds.metadata[frame_idx].rolling_shutter = {0.f, 0.f, 0.f, 0.f};
+	m_dataset_dirty = true;
+}
+
+void Testbed::set_camera_extrinsics_rolling_shutter(int frame_idx, const float* start, const float* end, const vec4& rs,
+                                                    bool convert_to_ngp) {
+	set_camera_extrinsics(frame_idx, end, convert_to_ngp);
+	NerfDataset& ds = nerf.training.dataset;
+	const Mat43 e = ds.xforms[frame_idx];
+	set_camera_extrinsics(frame_idx, start, convert_to_ngp);
+	while (ds.xforms_end.size() < ds.xforms.size()) ds.xforms_end.push_back(ds.xforms[ds.xforms_end.size()]);
+	ds.xforms_end[frame_idx] = e;
+	ds.metadata[frame_idx].rolling_shutter = rs;
 	m_dataset_dirty = true;
 }
 
@@ -634,6 +664,24 @@ static std::array<float, 9> matmul3(const std::array<float, 9>& A, const std::ar
 
 // NerfDataset transform with the optimised extrinsic offsets (Nerf::Training::update_transforms,
 // src/testbed_nerf.cu:2112-2140): rotation = rotmat(rot offset) * R, translation += pos offset.
+Mat43 Testbed::training_transform_end(size_t i) const {
+	const NerfTraining& tr = nerf.training;
+	if (i >= tr.dataset.xforms_end.size()) return training_transform(i);
+	// the same offsets on the end transform (src/testbed_nerf.cu:2128-2134)
+	Mat43 x = tr.dataset.xforms_end[i];
+	if (i < tr.cam_rot_offset.size()) {
+		const std::array<float, 9> Rm = rotmat(tr.cam_rot_offset[i].variable);
+		Mat43 y = x;
+		for (int c = 0; c < 3; ++c)
+			for (int r = 0; r < 3; ++r)
+				y.m[3 * c + r] = Rm[3 * r] * x.m[3 * c] + Rm[3 * r + 1] * x.m[3 * c + 1] + Rm[3 * r + 2] * x.m[3 * c + 2];
+		x = y;
+	}
+	if (i < tr.cam_pos_offset.size())
+		for (int r = 0; r < 3; ++r) x.m[9 + r] += tr.cam_pos_offset[i].variable[r];
+	return x;
+}
+
 Mat43 Testbed::training_transform(size_t i) const {
 	const NerfTraining& tr = nerf.training;
 	Mat43 x = tr.dataset.xforms[i];
@@ -665,6 +713,8 @@ void Testbed::upload_metadata() {
 			im.principal_point[k] = ds.metadata[i].principal_point[k];
 		}
 		std::memcpy(im.xform, training_transform(i).m, sizeof(im.xform));
+		std::memcpy(im.xform_end, training_transform_end(i).m, sizeof(im.xform_end));
+		for (int k = 0; k < 4; ++k) im.rolling_shutter[k] = ds.metadata[i].rolling_shutter[k];
 		im.lens_mode = (int32_t)ds.metadata[i].lens.mode;
 		std::memcpy(im.lens_params, ds.metadata[i].lens.params, sizeof(im.lens_params));
 	}
@@ -1044,7 +1094,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.depth_supervision_lambda = tr.depth_supervision_lambda;
 	a.depth_loss_type = (int32_t)tr.depth_loss_type;
 	for (size_t i = 0; i < tr.dataset.metadata.size(); ++i)
-		if (tr.dataset.metadata[i].lens.mode != ELensMode::Perspective) a.has_lens = 1;
+		if (tr.dataset.metadata[i].lens.mode != ELensMode::Perspective || tr.dataset.metadata[i].rolling_shutter != vec4{0.f, 0.f, 0.f, 0.f})
+			a.has_lens = 1;  // the general sampler instance (lenses, rolling shutter)
 	if (m_err && tr.error_map.resolution[0] > 0 && tr.error_map.resolution[1] > 0) {
 		a.error_map = m_err;  // accumulate_error is always on (src/testbed_nerf.cu:2756)
 		a.error_map_res[0] = (uint32_t)tr.error_map.resolution[0];

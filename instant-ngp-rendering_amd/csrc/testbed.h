@@ -47,11 +47,13 @@ struct TrainingImageMetadata {
 	vec2 focal_length = {1000.f, 1000.f};
 	vec2 principal_point = {0.5f, 0.5f};
 	Lens lens;
+	vec4 rolling_shutter = {0.f, 0.f, 0.f, 0.f};  // pixel time A + B u + C v + D motionblur_time (nerf_loader.cu:204-216)
 };
 
 struct NerfDataset {
 	std::vector<TrainingImageMetadata> metadata;
 	std::vector<Mat43> xforms;
+	std::vector<Mat43> xforms_end;  // TrainingXForm::end where it differs from start (empty / short: end = start)
 	std::vector<std::string> paths;
 	std::vector<std::vector<uint8_t>> pixels;  // RGBA8, sRGB, straight alpha (EImageDataType::Byte)
 	// per image [h][w] depth targets = 16-bit depth x integer_depth_scale x scale (src/nerf_loader.cu:73-82,
@@ -163,9 +165,13 @@ public:
 	void set_image(int frame_idx, const float* rgba, int width, int height);  // linear premultiplied float RGBA
 	void set_image_rgba8(int frame_idx, const uint8_t* rgba, int width, int height);
 	void set_camera_extrinsics(int frame_idx, const float* c2w_3x4_rowmajor, bool convert_to_ngp = true);
+	// Nerf::Training::set_camera_extrinsics_rolling_shutter (src/testbed_nerf.cu:2012-2030)
+	void set_camera_extrinsics_rolling_shutter(int frame_idx, const float* start_3x4_rowmajor, const float* end_3x4_rowmajor,
+	                                           const vec4& rolling_shutter, bool convert_to_ngp = true);
 	Mat43 get_camera_extrinsics(int frame_idx) const;
 	// dataset transform with the extrinsic offsets applied (Nerf::Training::transforms)
 	Mat43 training_transform(size_t i) const;
+	Mat43 training_transform_end(size_t i) const;  // the end transform with the same offsets
 	void set_camera_intrinsics(int frame_idx, float fx, float fy = 0.f, float cx = -0.5f, float cy = -0.5f, float k1 = 0.f, float k2 = 0.f,
 	                           float p1 = 0.f, float p2 = 0.f, float k3 = 0.f, float k4 = 0.f, bool is_fisheye = false);
 	std::function<bool(const std::string&, std::vector<uint8_t>&, int&, int&)> image_decoder;  // non-PNG fallback

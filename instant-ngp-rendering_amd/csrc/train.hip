@@ -197,8 +197,11 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 	float rgba[4];
 	texel_rgba(read_texel(im, u, v), rgba);
 	if (rgba[0] < 0.0f) return false;
-	(void)rng.next_float();  // motionblur_time
-	const m43 xf = load_xform(im.xform);
+	const float motionblur_time = rng.next_float();
+	m43 xf = load_xform(im.xform);
+	if (GENERAL && (im.rolling_shutter[0] != 0.0f || im.rolling_shutter[1] != 0.0f || im.rolling_shutter[2] != 0.0f ||
+	                im.rolling_shutter[3] != 0.0f))
+		xf = xform_given_rolling_shutter(xf, load_xform(im.xform_end), im.rolling_shutter, u, v, motionblur_time);
 	v3 dir;
 	if (!GENERAL) {
 		dir = rot(xf, mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],

@@ -42,6 +42,7 @@ class Image(C.Structure):
         ("pixels", C.c_uint64), ("width", C.c_uint32), ("height", C.c_uint32),
         ("focal_length", C.c_float * 2), ("principal_point", C.c_float * 2), ("xform", C.c_float * 12),
         ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7), ("depth", C.c_uint64),
+        ("xform_end", C.c_float * 12), ("rolling_shutter", C.c_float * 4),
     ]
 
 
@@ -95,6 +96,7 @@ class RenderArgs(C.Structure):
         ("min_transmittance", C.c_float), ("snap_to_pixel_centers", C.c_int32), ("use_inference_params", C.c_int32),
         ("train_in_linear_colors", C.c_int32), ("shard_index", C.c_uint32), ("shard_count", C.c_uint32),
         ("shard_rows", C.c_uint32), ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7),
+        ("camera_end", C.c_float * 12), ("rolling_shutter", C.c_float * 4),
         ("distortion_map", C.c_void_p), ("distortion_res", C.c_uint32 * 2),
     ]
 

@@ -778,6 +778,50 @@ static void distortion_lerp(const float* map, uint32_t rx, uint32_t ry, float u,
 	}
 }
 
+// camera_slerp / get_xform_given_rolling_shutter (common_device.cuh:628-636).  tcnn's
+// slerp(mat3, mat3, t) is absent from the mount: restated as glm's quat_cast -> slerp (lerp when
+// cos > 1 - FLT_EPSILON) -> normalize -> mat3_cast, translation mixed; t = 0 returns the start
+// (parity unpinned beyond that).
+static Cam slerp_cam(const Cam& a, const Cam& b, float t) {
+	if (t == 0.0f) return a;
+	auto to_q = [](const Cam& m, float* q) {  // w, x, y, z
+		const float m00 = m.c[0].x, m01 = m.c[0].y, m02 = m.c[0].z, m10 = m.c[1].x, m11 = m.c[1].y, m12 = m.c[1].z;
+		const float m20 = m.c[2].x, m21 = m.c[2].y, m22 = m.c[2].z;
+		const float f[4] = {m00 + m11 + m22, m00 - m11 - m22, m11 - m00 - m22, m22 - m00 - m11};
+		int bi = 0;
+		for (int k = 1; k < 4; ++k)
+			if (f[k] > f[bi]) bi = k;
+		const float bv = std::sqrt(f[bi] + 1.0f) * 0.5f, mu = 0.25f / bv;
+		const float a12 = (m12 - m21) * mu, a20 = (m20 - m02) * mu, a01 = (m01 - m10) * mu;
+		const float s01 = (m01 + m10) * mu, s20 = (m20 + m02) * mu, s12 = (m12 + m21) * mu;
+		const float r[4][4] = {{bv, a12, a20, a01}, {a12, bv, s01, s20}, {a20, s01, bv, s12}, {a01, s20, s12, bv}};
+		for (int k = 0; k < 4; ++k) q[k] = r[bi][k];
+	};
+	float qa[4], qb[4], q[4];
+	to_q(a, qa);
+	to_q(b, qb);
+	float c = qa[0] * qb[0] + qa[1] * qb[1] + qa[2] * qb[2] + qa[3] * qb[3];
+	if (c < 0.0f) {
+		for (float& x : qb) x = -x;
+		c = -c;
+	}
+	if (c > 1.0f - 1.1920928955078125e-7f) {
+		for (int k = 0; k < 4; ++k) q[k] = qa[k] * (1.0f - t) + qb[k] * t;
+	} else {
+		const float ang = std::acos(c), s0 = std::sin((1.0f - t) * ang), s1 = std::sin(t * ang), inv = 1.0f / std::sin(ang);
+		for (int k = 0; k < 4; ++k) q[k] = (s0 * qa[k] + s1 * qb[k]) * inv;
+	}
+	const float in = 1.0f / std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2] + q[3] * q[3]);
+	const float w = q[0] * in, x = q[1] * in, y = q[2] * in, z = q[3] * in;
+	Cam r;
+	r.c[0] = v(1.0f - 2.0f * (y * y + z * z), 2.0f * (x * y + w * z), 2.0f * (x * z - w * y));
+	r.c[1] = v(2.0f * (x * y - w * z), 1.0f - 2.0f * (x * x + z * z), 2.0f * (y * z + w * x));
+	r.c[2] = v(2.0f * (x * z + w * y), 2.0f * (y * z - w * x), 1.0f - 2.0f * (x * x + y * y));
+	r.c[3] = v(a.c[3].x * (1.0f - t) + b.c[3].x * t, a.c[3].y * (1.0f - t) + b.c[3].y * t, a.c[3].z * (1.0f - t) + b.c[3].z * t);
+	return r;
+}
+static bool rs_on(const float* rs) { return rs[0] != 0.0f || rs[1] != 0.0f || rs[2] != 0.0f || rs[3] != 0.0f; }
+
 // inverse(mat3(m)) * g, glm's adjugate / determinant inverse (compute_cam_gradient_train_nerf
 // src/testbed_nerf.cu:1242)
 static V3 inv3_mul(const Cam& m, V3 g) {
@@ -960,8 +1004,11 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	float rgba[4];
 	rgba_of(texel(im, u, vv), rgba);
 	if (rgba[0] < 0.0f) return false;
-	(void)rng.nextf();  // motionblur_time
-	const Cam x = cam_of(im.xform);
+	const float mb = rng.nextf();  // motionblur_time
+	Cam x = cam_of(im.xform);
+	if (rs_on(im.rolling_shutter))
+		x = slerp_cam(x, cam_of(im.xform_end),
+		              im.rolling_shutter[0] + im.rolling_shutter[1] * u + im.rolling_shutter[2] * vv + im.rolling_shutter[3] * mb);
 	V3 dir;
 	if (lens_dir(u, vv, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
 	             im.principal_point[1], im.lens_mode, im.lens_params, &dir)) {
@@ -1517,8 +1564,13 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 				d.x += ddx;
 				d.y += ddy;
 			}
-			d = rot(cam, d);
-			const V3 o = cam.c[3] + d * a.near_distance;
+			// the pixel's camera (src/testbed_nerf.cu:1416)
+			const Cam pc = rs_on(a.rolling_shutter)
+			                   ? slerp_cam(cam, cam_of(a.camera_end), a.rolling_shutter[0] + a.rolling_shutter[1] * u + a.rolling_shutter[2] * vv +
+			                                                              a.rolling_shutter[3] * ldval(a.sample_index, idx * 72239731u, 0))
+			                   : cam;
+			d = rot(pc, d);
+			const V3 o = pc.c[3] + d * a.near_distance;
 			d = normalize(d);
 			float t0, t1;
 			box.intersect(o, d, &t0, &t1);

@@ -41,7 +41,9 @@ def make_views(n_images=6, W=24, H=24, seed=0):
     return imgs, cams, focal
 
 
-def image_structs(imgs, cams, focal, pointers, lens=(0, ()), depth_pointers=None):
+def image_structs(imgs, cams, focal, pointers, lens=(0, ()), depth_pointers=None, shutter=None):
+    """shutter: optional (cams_end, rolling_shutter[4]) -- TrainingXForm::end and the pixel-time
+    coefficients of every image (default: end = start, no rolling shutter)."""
     n = len(imgs)
     arr = (A.Image * n)()
     for i in range(n):
@@ -51,8 +53,13 @@ def image_structs(imgs, cams, focal, pointers, lens=(0, ()), depth_pointers=None
         arr[i].focal_length[0] = arr[i].focal_length[1] = float(focal)
         arr[i].principal_point[0] = arr[i].principal_point[1] = 0.5
         xf = np.asarray(cams[i], np.float32).T.reshape(-1)  # column-major 4x3
+        xe = np.asarray(shutter[0][i] if shutter else cams[i], np.float32).T.reshape(-1)
         for k in range(12):
             arr[i].xform[k] = float(xf[k])
+            arr[i].xform_end[k] = float(xe[k])
+        if shutter:
+            for k in range(4):
+                arr[i].rolling_shutter[k] = float(shutter[1][k])
         arr[i].depth = int(depth_pointers[i]) if depth_pointers is not None and depth_pointers[i] else 0
         arr[i].lens_mode = lens[0]
         for k, val in enumerate(lens[1]):
@@ -61,12 +68,12 @@ def image_structs(imgs, cams, focal, pointers, lens=(0, ()), depth_pointers=None
 
 
 class HostDataset:
-    def __init__(self, imgs, cams, focal, lens=(0, ()), depths=None):
+    def __init__(self, imgs, cams, focal, lens=(0, ()), depths=None, shutter=None):
         """depths: optional per-image [H][W] f32 depth targets (None entries: no depth)."""
         self.imgs = [np.ascontiguousarray(im) for im in imgs]
         self.depths = [None if d is None else np.ascontiguousarray(d, np.float32) for d in depths] if depths else None
         dp = [0 if d is None else d.ctypes.data for d in self.depths] if self.depths else None
-        self.arr = image_structs(imgs, cams, focal, [im.ctypes.data for im in self.imgs], lens, dp)
+        self.arr = image_structs(imgs, cams, focal, [im.ctypes.data for im in self.imgs], lens, dp, shutter)
         self.n = len(imgs)
 
     @property
@@ -75,13 +82,13 @@ class HostDataset:
 
 
 class DeviceDataset:
-    def __init__(self, imgs, cams, focal, lens=(0, ()), depths=None):
+    def __init__(self, imgs, cams, focal, lens=(0, ()), depths=None, shutter=None):
         import torch
         self.pix = [torch.from_numpy(np.ascontiguousarray(im)).cuda() for im in imgs]
         self.depths = [None if d is None else torch.from_numpy(np.ascontiguousarray(d, np.float32)).cuda() for d in depths] \
             if depths else None
         dp = [0 if d is None else d.data_ptr() for d in self.depths] if self.depths else None
-        arr = image_structs(imgs, cams, focal, [p.data_ptr() for p in self.pix], lens, dp)
+        arr = image_structs(imgs, cams, focal, [p.data_ptr() for p in self.pix], lens, dp, shutter)
         self.meta = torch.frombuffer(bytearray(bytes(arr)), dtype=torch.uint8).cuda()
         self.n = len(imgs)
 

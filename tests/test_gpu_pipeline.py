@@ -791,3 +791,90 @@ def test_render_distortion_map_matches_oracle():
         assert np.abs(frames[0] - frames[1]).mean() > 1e-3
     finally:
         g.close()
+
+
+def _rotated(cam, axis, angle, shift):
+    """cam (3x4 NGP camera-to-world) rotated about its own origin and translated."""
+    a = np.asarray(axis, np.float64) / np.linalg.norm(axis)
+    K = np.array([[0, -a[2], a[1]], [a[2], 0, -a[0]], [-a[1], a[0], 0]])
+    Rm = np.eye(3) + np.sin(angle) * K + (1 - np.cos(angle)) * K @ K
+    out = np.asarray(cam, np.float64).copy()
+    out[:, :3] = Rm @ out[:, :3]
+    out[:, 3] += shift
+    return out.astype(np.float32)
+
+
+def test_train_sampler_rolling_shutter_matches_oracle():
+    """Rolling shutter / motion blur (get_xform_given_rolling_shutter, common_device.cuh:633-636;
+    used at src/testbed_nerf.cu:726-733): each training ray's camera is the start/end transforms
+    slerped at A + B u + C v + D motionblur_time.  The quaternion slerp goes through acos / sin,
+    whose device and host implementations may differ in the last ulp: coordinates within 1e-5."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        ends = [_rotated(c, (0.3, 1.0, 0.2), 0.08, np.array([0.02, -0.01, 0.015])) for c in cams]
+        shutter = (ends, (0.1, 0.4, 0.3, 0.2))
+        hd, dd = HostDataset(imgs, cams, focal, shutter=shutter), DeviceDataset(imgs, cams, focal, shutter=shutter)
+        set_bitfield_both(g, o, sphere_bitfield(0.32))
+        R, B, MS = 384, 4096, 1 << 15
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        ga.has_lens = 1
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+        g_ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        o_ns = o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        assert (g_ns[:, 0] == o_ns[:, 0]).mean() > 0.99
+        same = np.flatnonzero(np.all(g_ns == o_ns, axis=1) & (o_ns[:, 0] > 0))
+        assert same.size > 100
+        g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+        rows = np.concatenate([np.arange(b, b + n) for n, b in o_ns[same]])
+        np.testing.assert_allclose(g_c[rows, :7], o_c[rows, :7], atol=1e-5)
+        # the shutter moves the rays: the same step without it samples elsewhere
+        g2, o2, _ = pair(CFG_A)
+        try:
+            set_bitfield_both(g2, o2, sphere_bitfield(0.32))
+            hd0 = HostDataset(imgs, cams, focal)
+            o2.train_step(train_args(hd0.ptr, hd0.n, R, B, MS))
+            p_c = o2.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)
+            p_ns = o2.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+            k = np.flatnonzero((p_ns[:, 0] > 0) & (o_ns[:, 0] > 0))[0]
+            assert not np.array_equal(p_c[p_ns[k, 1], :3], o_c[o_ns[k, 1], :3])
+        finally:
+            g2.close()
+    finally:
+        g.close()
+
+
+def test_render_motion_blur_matches_oracle():
+    """init_rays_with_payload_kernel_nerf's per-pixel camera (src/testbed_nerf.cu:1416): camera and
+    camera_end slerped at A + B u + C v + D ld_random_val(sample_index, pixel * 72239731); rendered
+    RGB within 1e-3 mean L1 of the oracle for two sample indices."""
+    g, o, rng = pair(CFG_A, grid_scale=1.0)
+    try:
+        set_bitfield_both(g, o, sphere_bitfield(0.3))
+        W, H = 40, 32
+        cam = make_views(1, 8, 8)[1][0]
+        cam_end = _rotated(cam, (0.0, 1.0, 0.3), 0.1, np.array([0.03, 0.0, -0.02]))
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        xe = np.asarray(cam_end, np.float32).T.reshape(-1)
+        for spp in (0, 3):
+            ra = render_args(W, H, cam, focal, spp=spp, snap=0)
+            for k in range(12):
+                ra.camera_end[k] = float(xe[k])
+            for k, val in enumerate((0.0, 0.2, 0.1, 1.0)):
+                ra.rolling_shutter[k] = val
+            frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+            depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+            A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()),
+                                     stream()))
+            torch.cuda.synchronize()
+            gf = frame.cpu().numpy().reshape(H, W, 4)
+            of, _ = o.render(ra)
+            assert (of[..., 3] > 0.01).mean() > 0.2
+            assert np.abs(gf - of).mean() < 1e-3
+    finally:
+        g.close()

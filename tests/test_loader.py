@@ -176,3 +176,31 @@ def test_sharpness_matches_numpy_restatement(ngp):
     ref = _sharpness_numpy(d.image(0))
     assert s.shape == (72, 128) and ref.max() > 0
     np.testing.assert_allclose(s, ref, rtol=2e-3, atol=1e-6 * ref.max())
+
+
+def test_rolling_shutter_and_end_transforms(ngp, tmp_path):
+    """Rolling shutter / motion blur inputs (src/nerf_loader.cu:204-216, 515-516, 664-699): a global
+    3- or 4-element rolling_shutter (D defaults to 0), a per-frame override, and per-frame
+    transform_matrix_start / transform_matrix_end (end = start when absent), both converted with
+    nerf_matrix_to_ngp."""
+    from PIL import Image
+    rgb = np.zeros((4, 6, 4), np.uint8)
+    rgb[..., 3] = 255
+    for k in range(3):
+        Image.fromarray(rgb).save(tmp_path / f"img{k}.png")
+    rng = np.random.default_rng(0)
+    mats = [np.vstack([rng.uniform(-1, 1, (3, 4)), [0, 0, 0, 1]]) for _ in range(4)]
+    frames = [{"file_path": "img0.png", "transform_matrix": mats[0].tolist()},
+              {"file_path": "img1.png", "transform_matrix_start": mats[1].tolist(), "transform_matrix_end": mats[2].tolist(),
+               "rolling_shutter": [0.1, 0.2, 0.3, 0.4]},
+              {"file_path": "img2.png", "transform_matrix": mats[3].tolist()}]
+    meta = {"camera_angle_x": 0.7, "rolling_shutter": [0.5, 0.25, 0.125], "frames": frames}
+    (tmp_path / "transforms.json").write_text(json.dumps(meta))
+    d = ngp.load_nerf_dataset(str(tmp_path / "transforms.json"))
+    rs = [tuple(d.metadata[i].rolling_shutter) for i in range(3)]
+    assert rs[0] == rs[2] == (0.5, 0.25, 0.125, 0.0)
+    np.testing.assert_allclose(rs[1], (0.1, 0.2, 0.3, 0.4), rtol=1e-7)
+    start, end = d.transforms, d.transforms_end
+    for i, (ms, me) in enumerate(((mats[0], mats[0]), (mats[1], mats[2]), (mats[3], mats[3]))):
+        np.testing.assert_allclose(start[i], nerf_to_ngp(ms), atol=1e-6)
+        np.testing.assert_allclose(end[i], nerf_to_ngp(me), atol=1e-6)
