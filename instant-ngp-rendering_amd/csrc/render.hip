@@ -836,11 +836,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 
 	const uint32_t target = pass_sample_target(), cap = max_steps_per_pass(), cap0 = std::min(first_pass_steps(), cap);
 	static const bool debug = getenv("NGP_RENDER_DEBUG") != nullptr;
-	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (default 1.5) or "off"
-	static const char* budget_env = getenv("NGP_RENDER_BUDGET");
+	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (default 1.0: measured 1 % faster than 1.5) or "off"
+	const char* budget_env = getenv("NGP_RENDER_BUDGET");  // read per render (A/B knob)
 	k.budget = !(budget_env && strcmp(budget_env, "off") == 0);
-	k.budget_scale = budget_env && k.budget ? (float)atof(budget_env) : 1.5f;
-	if (!(k.budget_scale > 0.0f)) k.budget_scale = 1.5f;
+	k.budget_scale = budget_env && k.budget ? (float)atof(budget_env) : 1.0f;
+	if (!(k.budget_scale > 0.0f)) k.budget_scale = 1.0f;
 	static const bool block_skipping = getenv("NGP_RENDER_SKIP") && !strcmp(getenv("NGP_RENDER_SKIP"), "blocks");
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
