@@ -1,0 +1,51 @@
+"""Per-kernel training-step timings of one build (diagnostic, GPU box): trains the bench scene with
+every kernel timer on and prints the mean launch time of each timer class.  Run it once per build
+(--pkg: a directory with another build of pyngp + libngp_hip, tools/ab_build_old.sh) to compare
+kernels on one box.
+
+Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400]
+"""
+import argparse
+import ctypes as C
+import os
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, os.path.join(ROOT, "instant-ngp-rendering_amd"))
+
+
+def main():
+    p = argparse.ArgumentParser()
+    p.add_argument("--pkg", default=None)
+    p.add_argument("--steps", type=int, default=400)
+    p.add_argument("--timed", type=int, default=100)
+    p.add_argument("--config", default=os.path.join(ROOT, "instant-ngp-rendering_amd", "configs", "nerf", "lego_L16F2.json"))
+    p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
+    a = p.parse_args()
+    if a.pkg:
+        sys.path.insert(0, os.path.abspath(a.pkg))
+    import ngp_abi as A
+    import pyngp as ngp
+
+    tb = ngp.Testbed(ngp.TestbedMode.Nerf)
+    tb.load_training_data(a.scene)
+    tb.reload_network_from_file(a.config)
+    tb.shall_train = True
+    for _ in range(a.steps):
+        tb.train(1 << 18)
+    lib = A.load(os.path.join(os.path.abspath(a.pkg), "libngp_hip.so")) if a.pkg else A.load()
+    h = C.c_void_p(tb.model_handle)
+    A.check(lib.ngp_timing_enable(h, -1))
+    for _ in range(a.timed):
+        tb.train(1 << 18)
+    tb.sync()
+    print(f"# pyngp {ngp.__file__}")
+    for name, idx in A.TIMER.items():
+        ms, units, launches = C.c_double(), C.c_uint64(), C.c_uint32()
+        A.check(lib.ngp_timing_read(h, idx, C.byref(ms), C.byref(units), C.byref(launches), 1))
+        if launches.value:
+            print(f"{name:20s} {1000.0 * ms.value / launches.value:9.2f} us/launch  {launches.value:6d} launches")
+
+
+if __name__ == "__main__":
+    main()
