@@ -878,3 +878,38 @@ def test_render_motion_blur_matches_oracle():
             assert np.abs(gf - of).mean() < 1e-3
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("pipes,shard", [(1, (0, 1, 8)), (2, (0, 1, 8)), (3, (0, 1, 8)), (4, (0, 1, 8)), (2, (1, 3, 4))],
+                         ids=["1", "2", "3", "4", "2-shard"])
+def test_render_pipelines_match_oracle(pipes, shard, monkeypatch):
+    """The renderer's ray pipelines (render.hip render_pipes: interleaved 8-row blocks of the shard's
+    rows, one stream each) against the oracle's single straight march, on config B, a frame whose
+    row count leaves partial blocks (66 rows), also under a row shard.  Every pipeline count must
+    give the same pixels (depth included)."""
+    monkeypatch.setenv("NGP_RENDER_PIPES", str(pipes))
+    g, o, rng = pair(CFG_B, grid_scale=1.0)
+    try:
+        set_bitfield_both(g, o, sphere_bitfield(0.3))
+        W, H = 72, 66
+        cam = make_views(1, 8, 8)[1][0]
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        ra = render_args(W, H, cam, focal, spp=1, snap=0, shard=shard)
+        frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+        depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+        A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()),
+                                 stream()))
+        torch.cuda.synchronize()
+        gf = frame.cpu().numpy().reshape(H, W, 4)
+        gd = depth.cpu().numpy().reshape(H, W)
+        of, od = o.render(ra)
+        od = np.asarray(od).reshape(H, W)
+        rows = [y for y in range(H) if (y // shard[2]) % shard[1] == shard[0]]
+        assert (of[rows, :, 3] > 0.01).mean() > 0.2
+        assert np.abs(gf[rows] - of[rows]).mean() < 1e-3
+        hit = of[rows, :, 3] > 0.05
+        assert hit.sum() > 50
+        # the depth of the max-weight sample: equal up to near-ties between two samples' weights
+        assert (np.abs(gd[rows][hit] - od[rows][hit]) <= 1e-3 * np.abs(od[rows][hit]) + 1e-4).mean() > 0.99
+    finally:
+        g.close()
