@@ -142,9 +142,10 @@ struct MlpArgs {
 	uint32_t param_in[MAX_LAYERS];
 	const uint32_t* n_dev;  // optional device-side sample count (<= n)
 	float* dsh;             // optional [n][16] dL/d(SH inputs) (camera gradients)
-	uint32_t enc_bytes, coord_bytes;  // buffer-resource extents (register-resident inference)
+	uint32_t enc_bytes, coord_bytes, sh_bytes;  // buffer-resource extents (register-resident inference)
 	uint32_t dir_offset;              // float offset of the direction in a coords record
-	const __half* sh;                 // optional [n][16] precomputed SH inputs (renderer), instead of directions
+	const __half* sh;                 // optional [rays][16] precomputed SH inputs (renderer), instead of directions,
+	const uint32_t* sh_ray;           //   row of sample i: sh_ray[i] (the samples of a ray share its row)
 	uint32_t out_mode, out_stride;    // 0: out [n][4]; 1 / 2: the reference's 16-row output, column- / row-major
 	float* partials;                  // k_mlp_train: [workgroup][n_mlp_params] weight-gradient partials
 	uint32_t n_mlp;                   // MLP parameter count (partials row pitch)
@@ -367,6 +368,7 @@ struct RawTile {
 	uint32_t e[CT_][8 * N::KE];  // encoding halves of this lane's K slots, packed in pairs where F >= 2
 	float d[CT_][3];             // warped direction, or
 	uint32_t h[CT_][2];          // SH inputs 4g .. 4g+3 (precomputed rows)
+	uint32_t ri[CT_];            // SHIN: the samples' SH row indices
 };
 
 // Buffer resource over a device array (raw buffer, 32-bit byte offsets; reads past
@@ -379,11 +381,28 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t make_rsrc(const void* p, uint3
 // base + 16c + n and its direction.  FF: 2 / 4 = F of a level-major encoding (one load per
 // level), 12 / 14 = F = 2 / 4 in four-level planes (EncLayout lsh = 2: one 16-B load per
 // K step; the K order is then the planes' and k_pack permutes the first layer to match),
-// 0 = any layout, element by element.  SHIN: the direction inputs are precomputed SH rows
-// (8 B per lane group) instead of a direction the lane expands itself.
+// 0 = any layout, element by element.  SHIN: the direction inputs are precomputed per-ray SH
+// rows (8 B per lane group) instead of a direction the lane expands itself: this loads the
+// samples' row indices (first, so a later wait for them leaves the encoding loads in flight);
+// sh_load fetches the rows one ring stage later.
+// the SH rows of a ring slot whose row indices were loaded one stage earlier
+template <class N, int CT_>
+__device__ __forceinline__ void sh_load(__amdgpu_buffer_rsrc_t sh_rs, int g, RawTile<N, CT_>& r) {
+#pragma unroll
+	for (int c = 0; c < CT_; ++c) {
+		const auto v = __builtin_amdgcn_raw_buffer_load_b64(sh_rs, 32 * r.ri[c] + 8 * g, 0, 0);
+		r.h[c][0] = v[0];
+		r.h[c][1] = v[1];
+	}
+}
+
 template <class N, int CT_, int FF, bool SHIN>
 __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t enc_rs, __amdgpu_buffer_rsrc_t crd_rs,
                                         uint32_t base, int g, int n, RawTile<N, CT_>& r, bool want_dir) {
+	if (want_dir && SHIN) {
+#pragma unroll
+		for (int c = 0; c < CT_; ++c) r.ri[c] = __builtin_amdgcn_raw_buffer_load_b32(crd_rs, 4 * (base + 16 * c + n), 0, 0);
+	}
 #pragma unroll
 	for (int c = 0; c < CT_; ++c) {
 		const uint32_t i = base + 16 * c + n;
@@ -436,9 +455,6 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 			}
 		}
 		if (want_dir && SHIN) {
-			const auto v = __builtin_amdgcn_raw_buffer_load_b64(crd_rs, 32 * i + 8 * g, 0, 0);
-			r.h[c][0] = v[0];
-			r.h[c][1] = v[1];
 		} else if (want_dir) {
 			const uint32_t o = 4 * (i * a.coord_stride + a.dir_offset);
 			r.d[c][0] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(crd_rs, o, 0, 0));
@@ -609,12 +625,17 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	// wave-uniform tile index (scalar registers: the ring's guards are scalar branches)
 	const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
 	const __amdgpu_buffer_rsrc_t enc_rs = make_rsrc(a.enc, a.enc_bytes);
-	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(SHIN ? (const void*)a.sh : (const void*)a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
+	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(SHIN ? (const void*)a.sh_ray : (const void*)a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
+	const __amdgpu_buffer_rsrc_t sh_rs = make_rsrc(a.sh, SHIN && !DENSITY_ONLY ? a.sh_bytes : 0u);
+	constexpr bool SHR = SHIN && !DENSITY_ONLY;
 	RawTile<N, CT_> ring[PF];
 #pragma unroll
 	for (int q = 0; q < PF; ++q) {
 		const uint32_t t = t0 + q * stride;
 		if (t < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, t * TS, g, n, ring[q], !DENSITY_ONLY);
+	}
+	if constexpr (SHR) {
+		if (t0 < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[0]);
 	}
 	for (uint32_t tb = t0; tb < n_tiles; tb += PF * stride) {
 #pragma unroll
@@ -624,6 +645,11 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 				RawTile<N, CT_> cur = ring[q];
 				const uint32_t tn = t + PF * stride;
 				if (tn < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, tn * TS, g, n, ring[q], !DENSITY_ONLY);
+				if constexpr (SHR) {
+					// SH rows of the next tile to consume (its row indices arrived a stage ago); with
+					// PF = 1 that is the tile just loaded into this slot
+					if (t + stride < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[(q + 1) % PF]);
+				}
 				rf_tile<N, CT_, PF, DENSITY_ONLY, SHIN>(a, wl, cur, t * TS, g, n);
 			}
 		}
@@ -1120,7 +1146,8 @@ static void set_lds(K kernel, size_t bytes) {
 
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
-                      const uint32_t* n_dev, uint32_t dir_offset, const __half* sh, uint32_t out_mode, uint32_t out_stride) {
+                      const uint32_t* n_dev, uint32_t dir_offset, const __half* sh, uint32_t out_mode, uint32_t out_stride,
+                      const uint32_t* sh_ray, uint32_t sh_rows) {
 	if (n == 0) return;
 	if (enc_layout.lsh != m->enc_lsh) throw std::runtime_error("encoding layout differs from the packed first layer's");
 	MlpArgs a = base_args(m);
@@ -1135,9 +1162,12 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.out = out;
 	a.n_dev = n_dev;
 	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_layout.plane * 2, 0xffffffffu);
-	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * (sh ? 8 : coord_stride) * 4, 0xffffffffu);
+	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * (sh ? 1 : coord_stride) * 4, 0xffffffffu);
 	a.dir_offset = dir_offset;
+	if (sh && !sh_ray) throw std::runtime_error("launch_mlp_infer: SH rows need their per-sample row indices");
 	a.sh = sh;
+	a.sh_ray = sh_ray;
+	a.sh_bytes = (uint32_t)std::min<uint64_t>((uint64_t)sh_rows * 32, 0xffffffffu);
 	a.out_mode = out_mode;
 	a.out_stride = out_stride;
 	NGP_DISPATCH(m->mlp_variant, {

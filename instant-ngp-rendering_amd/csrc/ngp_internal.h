@@ -384,7 +384,7 @@ void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frag
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr,
-                      uint32_t out_mode = 0, uint32_t out_stride = 4);
+                      uint32_t out_mode = 0, uint32_t out_stride = 4, const uint32_t* sh_ray = nullptr, uint32_t sh_rows = 0);
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
 // dsh (optional): [n][16] dL/d(SH inputs of the rgb network), of the sample's own row (divided

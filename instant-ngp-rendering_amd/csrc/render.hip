@@ -397,8 +397,8 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 template <uint32_t G>
 __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
-                                                  float4* __restrict__ posdt, uint4* __restrict__ shrows,
-                                                  uint32_t target, uint32_t max_steps,
+                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray,
+                                                  uint4* __restrict__ shrows, uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
                                                   const uint32_t* counters, unsigned long long* host_prev, uint32_t tag_prev) {
@@ -446,6 +446,12 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 		}
 		sh_lo = make_uint4(u[0], u[1], u[2], u[3]);
 		sh_hi = make_uint4(u[4], u[5], u[6], u[7]);
+		// one row per ray and pass (row = the ray's index in this pass's alive buffer); its sample
+		// slots carry the row index (4 B instead of 32 B of SH per slot)
+		if (r == 0) {
+			shrows[2 * (size_t)i] = sh_lo;
+			shrows[2 * (size_t)i + 1] = sh_hi;
+		}
 	}
 	OccCache occ = occ_cache_init();
 	const uint32_t oct = ray_octant(d);
@@ -474,8 +480,7 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 				const size_t slot = (size_t)base + j + rank;
 				posdt[slot] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				shrows[2 * slot] = sh_lo;
-				shrows[2 * slot + 1] = sh_hi;
+				sray[slot] = i;
 			}
 		}
 		if (cnt >= room) {
@@ -499,8 +504,7 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
 		for (uint32_t q = j + r; q < budget; q += G) {
 			posdt[(size_t)base + q] = make_float4(-1.0f, -1.0f, -1.0f, 0.0f);
-			shrows[2 * ((size_t)base + q)] = make_uint4(0u, 0u, 0u, 0u);
-			shrows[2 * ((size_t)base + q) + 1] = make_uint4(0u, 0u, 0u, 0u);
+			sray[(size_t)base + q] = i;
 		}
 	}
 	if (k.dbg && valid && r == 0) {
@@ -755,6 +759,7 @@ struct PipeRun {
 	uint32_t pass = 0, steps_done = 0, n_alive_ub = 0, base_tag = 0;
 	bool marching = false;
 	float4* posdt = nullptr;
+	uint32_t* sray = nullptr;
 	uint4* shrows = nullptr;
 	Payload* P(int b) const { return reinterpret_cast<Payload*>(ps->payload[b].ptr); }
 	float4* C(int b) const { return reinterpret_cast<float4*>(ps->rgba[b].ptr); }
@@ -862,13 +867,15 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		pr.s = j == 0 ? s : rs.streams[j];
 		RenderPipeScratch& ps = *pr.ps;
 		// the most slots one pass can reserve (see `bound` below): small frames stay small
-		pr.max_samples = std::min<size_t>((size_t)pr.n * cap, std::max<size_t>((size_t)pr.n, (size_t)target)) + 256;
+		pr.max_samples = (std::min<size_t>((size_t)pr.n * cap, std::max<size_t>((size_t)pr.n, (size_t)target)) + 256 + 63) & ~(size_t)63;
 		for (int b = 0; b < 3; ++b) {
 			ps.payload[b].reserve((size_t)pr.n * 12);
 			ps.rgba[b].reserve((size_t)pr.n * 4);
 			ps.depth[b].reserve(pr.n);
 		}
-		ps.coords.reserve(12 * pr.max_samples);  // [0, 4*max): pos + warped dt rows, [4*max, 12*max): SH rows (16 fp16)
+		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH row indices, then
+		// [rays][8]: one row of 16 fp16 SH inputs per alive ray
+		ps.coords.reserve(5 * pr.max_samples + 8 * (size_t)pr.n);
 		ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
@@ -884,8 +891,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		if (!ps.events[0]) {
 			for (auto& e : ps.events) NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableTiming));
 		}
-		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // sample records in two row arrays: the encoder
-		pr.shrows = reinterpret_cast<uint4*>(pr.posdt + pr.max_samples);  // reads 16-B position rows once per level
+		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // the encoder reads 16-B position rows once per level
+		pr.sray = reinterpret_cast<uint32_t*>(ps.coords.ptr + 4 * pr.max_samples);
+		pr.shrows = reinterpret_cast<uint4*>(ps.coords.ptr + 5 * pr.max_samples);
 		pr.base_tag = ps.pass_tag;
 		pr.n_alive_ub = pr.n;
 	}
@@ -952,10 +960,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t tag_prev = pr.base_tag + pass;  // = tag of pass - 1
 		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 1: k_generate<1><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, 512, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, ps);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
@@ -984,7 +992,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
 		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
 		launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
-		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows));
+		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, pr.n);
 		tm.end(NGP_TIMER_RENDER_MLP, ps);
 		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
 		k_composite<<<std::max(1u, div_up(pr.n_alive_ub, 1024)), 1024, 0, ps>>>(
