@@ -746,12 +746,23 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 				lds_st_h4(dimg + smp * DS + DNXT + 16 * mt + 4 * g, o);
 			} else {
 				if (i < a.n) {
+					const uint32_t k0 = 16 * mt + 4 * g;
+					if (a.F == 2 && k0 + 4 <= a.E) {
+						// F = 2: rows k0, k0+1 and k0+2, k0+3 are the two features of two levels: one
+						// 4-B store per level (level-major dL/denc), values as the element path
 #pragma unroll
-					for (int r = 0; r < 4; ++r) {
-						const uint32_t k = 16 * mt + 4 * g + r;
-						if (k < a.E) {
-							const uint32_t lvl = k / a.F, f = k % a.F;
-							a.denc[((size_t)lvl * a.enc_plane + i) * a.F + f] = __float2half_rn(acc[r]);  // level-major
+						for (int q = 0; q < 2; ++q) {
+							const __half2 v = __halves2half2(__float2half_rn(acc[2 * q]), __float2half_rn(acc[2 * q + 1]));
+							*reinterpret_cast<__half2*>(a.denc + ((size_t)(k0 / 2 + q) * a.enc_plane + i) * 2) = v;
+						}
+					} else {
+#pragma unroll
+						for (int r = 0; r < 4; ++r) {
+							const uint32_t k = k0 + r;
+							if (k < a.E) {
+								const uint32_t lvl = k / a.F, f = k % a.F;
+								a.denc[((size_t)lvl * a.enc_plane + i) * a.F + f] = __float2half_rn(acc[r]);  // level-major
+							}
 						}
 					}
 				}
