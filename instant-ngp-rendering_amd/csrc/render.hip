@@ -556,15 +556,18 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		bool done = false;
 		uint32_t used = actual;
 		float alpha_last = p.alpha_last;
+		// only each sample's dt is read in the loop (4 B instead of the 16-B row); the position of
+		// the max-weight sample -- the depth -- is read once after it
+		size_t s_max = ~(size_t)0;
 		for (uint32_t j0 = 0; j0 < actual && !done; j0 += 4) {
 			uint2 o2[4];
-			float4 crd[4];
+			float wdt[4];
 #pragma unroll
 			for (uint32_t u = 0; u < 4; ++u) {
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
-					crd[u] = posdt[s];
+					wdt[u] = reinterpret_cast<const float*>(posdt)[4 * s + 3];
 				}
 			}
 #pragma unroll
@@ -572,7 +575,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				if (done || j0 + u >= actual) continue;
 				const __half2 rg = *reinterpret_cast<const __half2*>(&o2[u].x), bs = *reinterpret_cast<const __half2*>(&o2[u].y);
 				const float T = 1.0f - c.w;
-				const float dt = unwarp_dt(crd[u].w);
+				const float dt = unwarp_dt(wdt[u]);
 				const float alpha = 1.0f - __expf(-network_to_density(__high2float(bs), k.density_act) * dt);
 				const float weight = alpha * T;
 				const v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
@@ -584,8 +587,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				c.w += weight;
 				if (weight > p.max_weight) {
 					p.max_weight = weight;
-					const v3 pos = unwarp_position(mk3(crd[u].x, crd[u].y, crd[u].z), k.train_aabb);
-					local_depth = dot(cam_fwd, pos - cam_pos);
+					s_max = sbase + j0 + u;
 				}
 				if (c.w > (1.0f - k.min_transmittance)) {
 					const float inv = 1.0f / c.w;
@@ -597,6 +599,11 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 					done = true;
 				}
 			}
+		}
+		if (s_max != ~(size_t)0) {
+			const float4 crd = posdt[s_max];
+			const v3 pos = unwarp_position(mk3(crd.x, crd.y, crd.z), k.train_aabb);
+			local_depth = dot(cam_fwd, pos - cam_pos);
 		}
 		if (k.dbg) atomicAdd(&k.dbg[4], used);
 		p.alpha_last = alpha_last;
