@@ -519,6 +519,9 @@ __global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __r
 	}
 }
 
+// samples loaded ahead of their use in k_composite
+constexpr uint32_t COMPOSITE_AHEAD = 4;  // 8 measured no better (same-weights A/B)
+
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
@@ -559,11 +562,11 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		// only each sample's dt is read in the loop (4 B instead of the 16-B row); the position of
 		// the max-weight sample -- the depth -- is read once after it
 		size_t s_max = ~(size_t)0;
-		for (uint32_t j0 = 0; j0 < actual && !done; j0 += 4) {
-			uint2 o2[4];
-			float wdt[4];
+		for (uint32_t j0 = 0; j0 < actual && !done; j0 += COMPOSITE_AHEAD) {
+			uint2 o2[COMPOSITE_AHEAD];
+			float wdt[COMPOSITE_AHEAD];
 #pragma unroll
-			for (uint32_t u = 0; u < 4; ++u) {
+			for (uint32_t u = 0; u < COMPOSITE_AHEAD; ++u) {
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
@@ -571,7 +574,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				}
 			}
 #pragma unroll
-			for (uint32_t u = 0; u < 4; ++u) {
+			for (uint32_t u = 0; u < COMPOSITE_AHEAD; ++u) {
 				if (done || j0 + u >= actual) continue;
 				const __half2 rg = *reinterpret_cast<const __half2*>(&o2[u].x), bs = *reinterpret_cast<const __half2*>(&o2[u].y);
 				const float T = 1.0f - c.w;
