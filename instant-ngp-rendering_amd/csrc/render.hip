@@ -395,7 +395,7 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 // early passes (one lane per ray, flat loop), up to 64 for the last few thousand rays,
 // whose long serial marches otherwise dominate the tail passes.
 template <uint32_t G>
-__global__ void __launch_bounds__(512) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
                                                   float4* __restrict__ posdt, uint32_t* __restrict__ sray,
                                                   uint4* __restrict__ shrows, uint32_t target, uint32_t max_steps,
