@@ -757,6 +757,18 @@ static uint32_t render_pipes(uint32_t n, uint32_t h_shard) {
 	return std::max(1u, std::min(p, div_up(h_shard, 8u)));  // every pipeline gets rows
 }
 
+// Pinned host-counter words of a pipeline: per-pass unpacked counters in HC_SLOTS slots (the
+// read-back lag, NGP_RENDER_LAG, is at most HC_SLOTS passes), a copy-back slot, and the words the
+// kernels publish.
+constexpr uint32_t HC_SLOTS = 4, HC_COPYBACK = 16 * HC_SLOTS, HC_PUBLISHED = 128, HC_WORDS = HC_PUBLISHED + 16 * HC_SLOTS;
+
+// NGP_RENDER_LAG: passes a pipeline runs ahead of its counter read-backs (2 .. HC_SLOTS, default 3)
+static uint32_t render_lag() {
+	const char* e = getenv("NGP_RENDER_LAG");
+	const int v = e ? atoi(e) : 0;
+	return v >= 2 ? std::min<uint32_t>((uint32_t)v, HC_SLOTS) : 3u;  // 3: -0.6 % against 2 (same weights)
+}
+
 namespace {
 // One pipeline's march state (NerfTracer::trace, testbed_nerf.cu:1639-1755, for its rays).
 struct PipeRun {
@@ -774,16 +786,16 @@ struct PipeRun {
 	Payload* P(int b) const { return reinterpret_cast<Payload*>(ps->payload[b].ptr); }
 	float4* C(int b) const { return reinterpret_cast<float4*>(ps->rgba[b].ptr); }
 	uint32_t* hc() const { return ps->host_counter.ptr; }
-	unsigned long long* pub_dev() const { return reinterpret_cast<unsigned long long*>(ps->host_counter_dev + 64); }
+	unsigned long long* pub_dev() const { return reinterpret_cast<unsigned long long*>(ps->host_counter_dev + HC_PUBLISHED); }
 };
 }  // namespace
 
 // pass p's counters, published (k_generate of pass p + 1, or k_publish) as (tag << 32 | value)
 // words with tag base_tag + p + 1; unpacked into hc[16 * (p % 2) ...]
 static const uint32_t* wait_slot(PipeRun& pr, uint32_t pass) {
-	volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(pr.hc() + 64) + 8 * (pass % 2);
+	volatile unsigned long long* w = reinterpret_cast<volatile unsigned long long*>(pr.hc() + HC_PUBLISHED) + 8 * (pass % HC_SLOTS);
 	const uint32_t want = pr.base_tag + pass + 1;
-	uint32_t* out = pr.hc() + 16 * (pass % 2);
+	uint32_t* out = pr.hc() + 16 * (pass % HC_SLOTS);
 	// no stream queries while spinning (each one enqueues a marker that drains the queue);
 	// only after seconds without the tag is the stream asked whether it failed
 	const auto t0 = std::chrono::steady_clock::now();
@@ -890,12 +902,12 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
 		if (!ps.host_counter.ptr) {
-			// [2][16] unpacked pass counters, [32, 40) copy-back slot, [64, 96) the published
-			// words ([2 slots][8] x (tag << 32 | value));
+			// [HC_SLOTS][16] unpacked pass counters, [HC_COPYBACK, +8) copy-back slot,
+			// [HC_PUBLISHED, +HC_SLOTS * 16) the published words ([slot][8] x (tag << 32 | value));
 			// fine-grained (coherent) so the kernel's system-scope stores reach the polling host
-			NGP_HIP_CHECK(hipHostMalloc((void**)&ps.host_counter.ptr, 96 * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
-			std::memset(ps.host_counter.ptr, 0, 96 * sizeof(uint32_t));
-			ps.host_counter.n = 96;
+			NGP_HIP_CHECK(hipHostMalloc((void**)&ps.host_counter.ptr, HC_WORDS * sizeof(uint32_t), hipHostMallocCoherent | hipHostMallocMapped));
+			std::memset(ps.host_counter.ptr, 0, HC_WORDS * sizeof(uint32_t));
+			ps.host_counter.n = HC_WORDS;
 			NGP_HIP_CHECK(hipHostGetDevicePointer((void**)&ps.host_counter_dev, ps.host_counter.ptr, 0));
 		}
 		if (!ps.events[0]) {
@@ -951,6 +963,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// empty).  With two pipelines the host alternates between them, so each stream holds up
 	// to two enqueued passes while the host waits on the other's read-back.
 	const uint32_t MARCH_ITER = 10000;
+	const uint32_t lag = render_lag();
 	auto enqueue_pass = [&](PipeRun& pr) {
 		const hipStream_t ps = pr.s;
 		uint32_t* counters = pr.ps->counters.ptr;
@@ -966,7 +979,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t want = lanes_target() / std::max(pr.n_alive_ub, 1u);
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
 		const uint32_t gblocks = std::max(1u, div_up((uint64_t)pr.n_alive_ub * G, 512));
-		unsigned long long* host_prev = pass > 0 ? pr.pub_dev() + 8 * ((pass - 1) % 2) : nullptr;
+		unsigned long long* host_prev = pass > 0 ? pr.pub_dev() + 8 * ((pass - 1) % HC_SLOTS) : nullptr;
 		const uint32_t tag_prev = pr.base_tag + pass;  // = tag of pass - 1
 		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
 		switch (G) {
@@ -1013,10 +1026,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		pr.cur = 1 - cur;
 		++pr.pass;
 		// the read-back of the previous pass bounds the next one
-		if (pr.pass >= 2) {
-			const uint32_t* c = wait_slot(pr, pr.pass - 2);
-			pr.steps_done += c[6 + (pr.pass - 2) % 2];
-			pr.n_alive_ub = std::min(pr.n_alive_ub, c[(pr.pass - 1) % 2]);
+		if (pr.pass >= lag) {
+			const uint32_t q = pr.pass - lag;  // its counters: alive out (the input of pass q + 1, a bound on every later one)
+			const uint32_t* c = wait_slot(pr, q);
+			pr.steps_done += c[6 + q % 2];
+			pr.n_alive_ub = std::min(pr.n_alive_ub, c[(q + 1) % 2]);
 			if (pr.n_alive_ub == 0 || pr.steps_done >= MARCH_ITER) pr.marching = false;
 		}
 	};
@@ -1033,7 +1047,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		PipeRun& pr = pipes[j];
 		if (pr.pass == 0) continue;  // no rays
 		uint32_t* counters = pr.ps->counters.ptr;
-		k_publish<<<1, 64, 0, pr.s>>>(counters, pr.pub_dev() + 8 * ((pr.pass - 1) % 2), pr.base_tag + pr.pass);
+		k_publish<<<1, 64, 0, pr.s>>>(counters, pr.pub_dev() + 8 * ((pr.pass - 1) % HC_SLOTS), pr.base_tag + pr.pass);
 		NGP_HIP_CHECK(hipGetLastError());
 		const uint32_t* last = wait_slot(pr, pr.pass - 1);
 		const uint32_t n_alive = last[pr.pass % 2];
@@ -1046,13 +1060,13 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			k_retire<<<div_up(n_alive, 256), 256, 0, pr.s>>>(n_alive, pr.P(pr.cur), pr.C(pr.cur), pr.ps->depth[pr.cur].ptr,
 			                                                 pr.P(2), pr.C(2), pr.ps->depth[2].ptr, counters);
 			// copy-back of the counters -> slot [32, 40), then an event
-			NGP_HIP_CHECK(hipMemcpyAsync(pr.hc() + 32, counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, pr.s));
+			NGP_HIP_CHECK(hipMemcpyAsync(pr.hc() + HC_COPYBACK, counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, pr.s));
 			NGP_HIP_CHECK(hipEventRecord(pr.ps->events[0], pr.s));
 			hipError_t e;
 			while ((e = hipEventQuery(pr.ps->events[0])) == hipErrorNotReady) {
 			}
 			NGP_HIP_CHECK(e);
-			n_hit = pr.hc()[32 + 2];
+			n_hit = pr.hc()[HC_COPYBACK + 2];
 		}
 		pr.ps->pass_tag = pr.base_tag + pr.pass;
 		if (n_hit)
