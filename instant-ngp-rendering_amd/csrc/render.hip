@@ -958,7 +958,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// Counters (device): [0]/[1] alive rays in/out, [2] finished rays, [3] filled samples,
 	// [4]/[5] sample slots, [6]/[7] samples per ray of the pass.  The host does not wait for a
 	// pass before enqueuing the next: kernels read the counts from the device, and launches
-	// are sized by the count read back one pass earlier (alive counts only shrink).  A
+	// are sized by the latest count read back (lag passes behind; alive counts only shrink).  A
 	// pipeline stops once a read-back shows no alive rays (the pass enqueued meanwhile runs
 	// empty).  With two pipelines the host alternates between them, so each stream holds up
 	// to two enqueued passes while the host waits on the other's read-back.
