@@ -16,7 +16,7 @@ import time
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "instant-ngp-rendering_amd"))
 
-KNOBS = ("NGP_RENDER_GENERATE_BLOCK", "NGP_RENDER_COMPOSITE_BLOCK", "NGP_RENDER_LAG", "NGP_RENDER_BUDGET", "NGP_ENC_DENSE_RECORDS", "NGP_RENDER_PIPES", "NGP_RENDER_TARGET", "NGP_RENDER_STEPS_PER_PASS", "NGP_RENDER_LANES",
+KNOBS = ("NGP_MLP_WG_PER_CU", "NGP_RENDER_GENERATE_BLOCK", "NGP_RENDER_COMPOSITE_BLOCK", "NGP_RENDER_LAG", "NGP_RENDER_BUDGET", "NGP_ENC_DENSE_RECORDS", "NGP_RENDER_PIPES", "NGP_RENDER_TARGET", "NGP_RENDER_STEPS_PER_PASS", "NGP_RENDER_LANES",
          "NGP_RENDER_FIRST_STEPS")
 
 
