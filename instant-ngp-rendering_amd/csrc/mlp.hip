@@ -1183,7 +1183,9 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.out_stride = out_stride;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
-		// workgroups per CU (NGP_MLP_WG_PER_CU; 8 measured 0.6 % faster per frame than 5 = the occupancy)
+		// workgroups per CU (NGP_MLP_WG_PER_CU; 8 measured 0.6 % faster per frame than 5 = the
+		// occupancy with fixed weights, +4 % bench value on one box; the other pipeline's encoder
+		// launches then share the CUs longer, which lowers their measured per-launch rate)
 		const char* wg_env = getenv("NGP_MLP_WG_PER_CU");
 		const uint32_t wg_per_cu = wg_env && atoi(wg_env) > 0 ? (uint32_t)atoi(wg_env) : 8u;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * wg_per_cu);
@@ -1224,7 +1226,9 @@ void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* e
 	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_layout.plane * 2, 0xffffffffu);
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags_upto(N::DH + 1) * FRAG_HALVES * 2;
-		// workgroups per CU (NGP_MLP_WG_PER_CU; 8 measured 0.6 % faster per frame than 5 = the occupancy)
+		// workgroups per CU (NGP_MLP_WG_PER_CU; 8 measured 0.6 % faster per frame than 5 = the
+		// occupancy with fixed weights, +4 % bench value on one box; the other pipeline's encoder
+		// launches then share the CUs longer, which lowers their measured per-launch rate)
 		const char* wg_env = getenv("NGP_MLP_WG_PER_CU");
 		const uint32_t wg_per_cu = wg_env && atoi(wg_env) > 0 ? (uint32_t)atoi(wg_env) : 8u;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * wg_per_cu);
