@@ -284,6 +284,20 @@ struct pcg32 {
 };
 
 // ---------------------------------------------------------------------------
+// tcnn ExponentialDecay (configs/nerf/base.json:9-14) in closed form: the learning rate is
+// multiplied by decay_base at decay_start, decay_start + interval, ... for optimizer steps below
+// decay_end.  PARITY UNPINNED: tcnn's optimizer source is not in the reference mount, so the exact
+// step a decay lands on (first at decay_start, none at or after decay_end) is the restated spec
+// (SURVEY App. C 6), shared by the network optimizer, the distortion map and the camera updates.
+// ---------------------------------------------------------------------------
+NGP_HD float exp_decay_learning_rate(float lr, float decay_base, uint32_t decay_start, uint32_t decay_interval,
+                                     uint32_t decay_end, uint32_t step) {
+	if (decay_interval == 0 || step < decay_start || decay_end <= decay_start) return lr;
+	const uint32_t s = step < decay_end ? step : decay_end - 1;
+	return lr * powf(decay_base, (float)((s - decay_start) / decay_interval + 1));
+}
+
+// ---------------------------------------------------------------------------
 // Morton codes (tcnn morton3D / morton3D_invert), used at nerf_device.cuh:327,
 // src/testbed_nerf.cu:86-88,206-208,326-330.
 // ---------------------------------------------------------------------------

@@ -12,6 +12,7 @@
 #include <cstring>
 #include <limits>
 
+#include "ngp_math.h"
 #include "testbed.h"
 
 namespace py = pybind11;
@@ -131,6 +132,9 @@ PYBIND11_MODULE(pyngp, m) {
 		.export_values();
 	m.def("mode_from_scene", &mode_from_scene);
 	m.def("mode_from_string", &mode_from_string);
+	// the ExponentialDecay schedule every optimizer of the Testbed uses (ngp_math.h; parity unpinned)
+	m.def("exponential_decay_learning_rate", &exp_decay_learning_rate, py::arg("learning_rate"), py::arg("decay_base"),
+	      py::arg("decay_start"), py::arg("decay_interval"), py::arg("decay_end"), py::arg("step"));
 
 	py::enum_<ELossType>(m, "LossType")
 		.value("L2", ELossType::L2)

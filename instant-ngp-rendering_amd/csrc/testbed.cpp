@@ -265,6 +265,10 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 	std::vector<float> depth_scales;
 	ds.offset = {0.5f, 0.5f, 0.5f};
 	static const char* formats[] = {"png", "jpg", "jpeg", "bmp", "gif", "tga", "pic", "pnm", "psd", "exr"};
+	// declared outside the per-json loop as in the reference (src/nerf_loader.cu:300, 419, 486-488): a
+	// value set by one json carries over to the jsons loaded after it
+	float depth_scale = -1.0f;
+	bool enable_depth_loading = true;
 	for (const std::string& jp : json_paths) {
 		const Json j = Json::parse(read_text(jp));
 		if (!j.contains("frames") || !j["frames"].is_array()) continue;
@@ -283,8 +287,8 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 			for (int k = 0; k < 3; ++k) ds.offset[k] = (((float)a[1][k].num() + (float)a[0][k].num()) * 0.5f) * -ds.scale + 0.5f;
 		}
 		// depth supervision inputs (src/nerf_loader.cu:419-437, 486-488)
-		const float depth_scale = (float)j.value("integer_depth_scale", -1.0);
-		const bool enable_depth_loading = j.value("enable_depth_loading", true);
+		if (j.contains("integer_depth_scale")) depth_scale = (float)j["integer_depth_scale"].num();
+		if (j.contains("enable_depth_loading")) enable_depth_loading = j.value("enable_depth_loading", true);
 		if (j.contains("up")) ds.up = {(float)j["up"][1].num(), (float)j["up"][2].num(), (float)j["up"][0].num()};
 		// frames sorted naturally by file_path (src/nerf_loader.cu:347-349)
 		std::vector<Json> frames = j["frames"].elements();
@@ -1255,10 +1259,7 @@ void Testbed::update_error_map_cdf() {
 // m_optimizer->learning_rate(): Adam's rate under the ExponentialDecay of the config
 float Testbed::current_learning_rate() const {
 	const ngp_network_config& c = m_net_cfg;
-	float lr = c.learning_rate;
-	if (c.decay_interval > 0 && training_step >= c.decay_start)
-		lr = c.learning_rate * std::pow(c.decay_base, (float)((training_step - c.decay_start) / c.decay_interval + 1));
-	return lr;
+	return exp_decay_learning_rate(c.learning_rate, c.decay_base, c.decay_start, c.decay_interval, 0xFFFFFFFFu, training_step);
 }
 
 // Exposure branch of the camera update (src/testbed_nerf.cu:2650-2677): per-image Adam
@@ -1308,11 +1309,7 @@ void Testbed::update_distortion_map() {
 	std::vector<float> g(2 * n);
 	hk(hipMemcpyAsync(g.data(), m_dist_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "distortion gradient d2h");
 	sync();
-	float lr = d.lr;
-	if (d.decay_interval > 0 && d.optimizer_step >= d.decay_start) {
-		const uint32_t s = std::min(d.optimizer_step, d.decay_end > 0 ? d.decay_end - 1 : 0u);
-		if (s >= d.decay_start) lr = d.lr * std::pow(d.decay_base, (float)((s - d.decay_start) / d.decay_interval + 1));
-	}
+	const float lr = exp_decay_learning_rate(d.lr, d.decay_base, d.decay_start, d.decay_interval, d.decay_end, d.optimizer_step);
 	++d.optimizer_step;
 	const float loss_scale = 128.0f * (float)nerf.training.n_steps_between_cam_updates;
 	for (size_t i = 0; i < n; ++i) {

@@ -1158,12 +1158,7 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.n = m->n_params;
 	a.n_mlp = m->n_mlp_params;
 	// ExponentialDecay (configs/nerf/base.json:9-14): lr *= base at decay_start + k*interval
-	float lr = c.learning_rate;
-	if (c.decay_interval > 0 && step >= c.decay_start) {
-		const uint32_t k = (step - c.decay_start) / c.decay_interval + 1;
-		lr = c.learning_rate * powf(c.decay_base, (float)k);
-	}
-	a.lr = lr;
+	a.lr = exp_decay_learning_rate(c.learning_rate, c.decay_base, c.decay_start, c.decay_interval, 0xFFFFFFFFu, step);
 	a.beta1 = c.beta1;
 	a.beta2 = c.beta2;
 	a.eps = c.epsilon;

@@ -146,6 +146,33 @@ def test_depth_images_load_scaled(ngp, tmp_path):
         ngp.load_nerf_dataset(str(tmp_path / "transforms.json"))
 
 
+def test_depth_settings_carry_over_between_jsons(ngp, tmp_path):
+    """A directory load reads every *.json in sorted order; integer_depth_scale and
+    enable_depth_loading live outside the reference's per-json loop (src/nerf_loader.cu:300, 419,
+    435-437, 486-488), so a value set by the first json applies to the jsons after it."""
+    from PIL import Image
+    w, h = 6, 4
+    rgb = np.zeros((h, w, 4), np.uint8)
+    rgb[..., 3] = 255
+    for k in range(2):
+        Image.fromarray(rgb).save(tmp_path / f"img{k}.png")
+    dep = (np.arange(w * h).reshape(h, w) * 131 % 50000).astype(np.uint16)
+    _write_png16_gray(str(tmp_path / "d1.png"), dep)
+    eye = np.eye(4).tolist()
+    first = {"camera_angle_x": 0.7, "integer_depth_scale": 2e-3, "scale": 0.5,
+             "frames": [{"file_path": "img0.png", "transform_matrix": eye}]}
+    second = {"camera_angle_x": 0.7, "frames": [{"file_path": "img1.png", "transform_matrix": eye, "depth_path": "d1.png"}]}
+    (tmp_path / "transforms_a.json").write_text(json.dumps(first))
+    (tmp_path / "transforms_b.json").write_text(json.dumps(second))
+    d = ngp.load_nerf_dataset(str(tmp_path))
+    assert d.n_images == 2 and d.depth(0) is None
+    np.testing.assert_allclose(d.depth(1), dep.astype(np.float32) * np.float32(2e-3 * 0.5), rtol=1e-6)
+    # enable_depth_loading false in the first json turns depth loading off for the second as well
+    first["enable_depth_loading"] = False
+    (tmp_path / "transforms_a.json").write_text(json.dumps(first))
+    assert ngp.load_nerf_dataset(str(tmp_path)).depth(1) is None
+
+
 def _sharpness_numpy(rgba8):
     """compute_sharpness (src/nerf_loader.cu:111-151), restated in numpy: per tile of a 128 x 72
     grid, the variance of the 5-point Laplacian of the luma of the linear, premultiplied pixels."""
