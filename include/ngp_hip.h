@@ -264,8 +264,30 @@ typedef struct ngp_render_args {
 	uint32_t distortion_res[2];
 } ngp_render_args;
 
+/* Launch shapes and march schedule of the gfx950 kernels (no reference counterpart).  None of
+ * them changes a result -- every ray composites its own samples in order whatever the pass
+ * split, and the kernel variants compute the same values -- only the speed.  0 = the measured
+ * default.  Per model; ngp_model_create starts from all zeros. */
+typedef struct ngp_tuning {
+	uint32_t render_pipelines;       /* ray pipelines on their own streams, 1..4; 0: 2 for frames of >= 2^16 rays */
+	uint32_t render_pass_samples;    /* a pipeline's sample-slot budget per march pass (<= 2^24); 0: 2^22 */
+	uint32_t render_lanes;           /* lane budget from which k_generate picks lanes per ray; 0: 2^22 */
+	uint32_t render_first_steps;     /* per-ray sample cap of the first pass (doubling per pass); 0: 4 */
+	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 */
+	uint32_t render_lag;             /* passes a pipeline runs ahead of its counter read-backs, 2..4; 0: 3 */
+	float render_budget_scale;       /* headroom of the per-ray transmittance budget; 0: 1.0; < 0: no budget */
+	uint32_t render_block_skipping;  /* 1: aligned-block occupancy summaries instead of octant distance fields */
+	uint32_t render_composite_block; /* k_composite workgroup size (256, 512, 1024); 0: 512 */
+	uint32_t render_generate_block;  /* k_generate workgroup size (256, 512); 0: 512 */
+	uint32_t encode_dense_records;   /* render-site corner records of the dense levels: 0 on, 1 off */
+	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: 8 */
+	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics */
+} ngp_tuning;
+
 /* --- lifecycle -------------------------------------------------------------------- */
 ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint64_t seed, ngp_model** out);
+ngp_status ngp_model_set_tuning(ngp_model* model, const ngp_tuning* tuning);
+ngp_status ngp_model_get_tuning(const ngp_model* model, ngp_tuning* tuning);
 ngp_status ngp_model_destroy(ngp_model* model);
 ngp_status ngp_model_get_info(const ngp_model* model, ngp_model_info* info);
 ngp_status ngp_model_buffer(ngp_model* model, int kind, void** dev_ptr, size_t* bytes);

@@ -527,8 +527,7 @@ __global__ void __launch_bounds__(256) k_dense_records(const uint32_t* __restric
 LevelTable build_dense_records(ngp_model* m, const __half* table, hipStream_t s) {
 	LevelTable lt = m->lt;
 	lt.rec = nullptr;
-	const bool off = getenv("NGP_ENC_DENSE_RECORDS") && !strcmp(getenv("NGP_ENC_DENSE_RECORDS"), "0");  // A/B knob
-	if (lt.F != 2 || off) return lt;
+	if (lt.F != 2 || m->tuning.encode_dense_records == 1) return lt;
 	uint32_t total = 0;
 	for (uint32_t l = 0; l < lt.n_levels; ++l) {
 		lt.rec_off[l] = total;
@@ -547,17 +546,11 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
                             __half* enc, EncLayout enc_plane, hipStream_t s, const uint32_t* n_dev, uint32_t max_chunks) {
 	uint32_t n_chunks = div_up(n, 256);
 	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
-	// 16-B quad gathers for F = 2 (NGP_ENC_GATHER=pair: 8-B pair gathers); four levels per
-	// thread (l, l + L/4, ...; NGP_ENC_LPT=2: two, on one XCD; =1: one level per thread)
-	static const bool quad = !(getenv("NGP_ENC_GATHER") && !strcmp(getenv("NGP_ENC_GATHER"), "pair"));
-	static const int lpt = getenv("NGP_ENC_LPT") ? atoi(getenv("NGP_ENC_LPT")) : 4;
-	const bool lpt1 = lpt == 1;
-	if (quad && lt.F == 2) {
-		if (lpt == 4 && lt.n_levels % 4 == 0)
+	// F = 2: 16-B quad gathers, four levels per thread (l, l + L/4, ...) where L % 4 == 0, else one
+	// (8-B pair gathers and two levels per thread measured slower)
+	if (lt.F == 2) {
+		if (lt.n_levels % 4 == 0)
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 4>, n_chunks * lt.n_levels / 4, 256, 0, s, n, pos, stride, table, lt, enc,
-			             enc_plane, n_chunks, n_dev);
-		else if (!lpt1 && lt.n_levels % 16 == 0)
-			launch_timed(k_hashgrid_fwd<2, SITE, true, 2>, n_chunks * lt.n_levels / 2, 256, 0, s, n, pos, stride, table, lt, enc,
 			             enc_plane, n_chunks, n_dev);
 		else
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 1>, n_chunks * lt.n_levels, 256, 0, s, n, pos, stride, table, lt, enc,

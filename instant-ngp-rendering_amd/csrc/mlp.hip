@@ -1183,20 +1183,15 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.out_stride = out_stride;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
-		// workgroups per CU (NGP_MLP_WG_PER_CU; 8 measured 0.6 % faster per frame than 5 = the
-		// occupancy with fixed weights, +4 % bench value on one box; the other pipeline's encoder
-		// launches then share the CUs longer, which lowers their measured per-launch rate)
-		const char* wg_env = getenv("NGP_MLP_WG_PER_CU");
-		const uint32_t wg_per_cu = wg_env && atoi(wg_env) > 0 ? (uint32_t)atoi(wg_env) : 8u;
+		// workgroups per CU (ngp_tuning.mlp_workgroups_per_cu; 8 measured 0.6 % faster per frame than
+		// 5 = the occupancy with fixed weights, +4 % bench value on one box; the other pipeline's
+		// encoder launches then share the CUs longer, which lowers their measured per-launch rate)
+		const uint32_t wg_per_cu = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : 8u;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * wg_per_cu);
 		const bool pl = a.enc_lsh == 2;
-		// tile shape of the renderer's path (NGP_MLP_TILE=CT,PF: tiles per wave step, prefetch depth; A/B)
-		static const int tile = getenv("NGP_MLP_TILE") ? atoi(getenv("NGP_MLP_TILE")) * 10 + atoi(strchr(getenv("NGP_MLP_TILE"), ',') ? strchr(getenv("NGP_MLP_TILE"), ',') + 1 : "2") : 12;
-		if (sh && a.F == 2 && pl && tile == 22) launch_timed(k_mlp_infer_rf<N, 2, 2, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * 5), BLOCK, lds, s, a);
-		else if (sh && a.F == 2 && pl && tile == 21) launch_timed(k_mlp_infer_rf<N, 2, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * 5), BLOCK, lds, s, a);
-		else if (sh && a.F == 2 && pl && tile == 13) launch_timed(k_mlp_infer_rf<N, 1, 3, false, 12, true>, grid, BLOCK, lds, s, a);
-		else if (sh && a.F == 2 && pl && tile == 11) launch_timed(k_mlp_infer_rf<N, 1, 1, false, 12, true>, grid, BLOCK, lds, s, a);
-		else if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);
+		// the renderer's path: one 16-sample tile per wave step, prefetch two ahead (2-tile steps and
+		// prefetch depths 1 / 3 measured slower)
+		if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);
 		else if (sh && a.F == 4 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 14, true>, grid, BLOCK, lds, s, a);
 		// element-wise loads read K in natural order: only valid where k_pack did not permute the
 		// first layer to the plane order (plane_f == 0)
@@ -1226,11 +1221,10 @@ void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* e
 	a.enc_bytes = (uint32_t)std::min<uint64_t>((uint64_t)m->enc_width * enc_layout.plane * 2, 0xffffffffu);
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags_upto(N::DH + 1) * FRAG_HALVES * 2;
-		// workgroups per CU (NGP_MLP_WG_PER_CU; 8 measured 0.6 % faster per frame than 5 = the
-		// occupancy with fixed weights, +4 % bench value on one box; the other pipeline's encoder
-		// launches then share the CUs longer, which lowers their measured per-launch rate)
-		const char* wg_env = getenv("NGP_MLP_WG_PER_CU");
-		const uint32_t wg_per_cu = wg_env && atoi(wg_env) > 0 ? (uint32_t)atoi(wg_env) : 8u;
+		// workgroups per CU (ngp_tuning.mlp_workgroups_per_cu; 8 measured 0.6 % faster per frame than
+		// 5 = the occupancy with fixed weights, +4 % bench value on one box; the other pipeline's
+		// encoder launches then share the CUs longer, which lowers their measured per-launch rate)
+		const uint32_t wg_per_cu = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : 8u;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * wg_per_cu);
 		const bool pl = a.enc_lsh == 2;
 		if (a.F == 2 && pl) k_mlp_infer_rf<N, 1, 2, true, 12><<<grid, BLOCK, lds, s>>>(a);

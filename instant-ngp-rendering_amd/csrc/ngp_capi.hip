@@ -156,11 +156,10 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 			m->cfg = *cfg;
 			m->enc_width = cfg->n_levels * cfg->n_features_per_level;
 			m->enc_pad = next_multiple(m->enc_width, 16);
-			{  // NGP_ENC_LAYOUT=level keeps the level-major layout internally too (A/B)
-				const char* e = std::getenv("NGP_ENC_LAYOUT");
+			{  // the plane layout of the internal encodings (ngp_internal.h EncLayout) where L/4 is a power of two
 				const uint32_t G = cfg->n_levels / 4;
 				const bool pow2 = cfg->n_levels % 4 == 0 && G && (G & (G - 1)) == 0;
-				m->enc_lsh = (pow2 && !(e && std::strcmp(e, "level") == 0)) ? 2u : 0u;
+				m->enc_lsh = pow2 ? 2u : 0u;
 				m->enc_gsh = m->enc_lsh ? (uint32_t)__builtin_ctz(G) : 0u;
 			}
 			require(m->enc_pad <= 64, "encoding width (n_levels * F) must be <= 64");
@@ -227,6 +226,29 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		m->rs.release();
 		m->timers.release();
 		delete m;
+	});
+}
+
+ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
+	return guarded([&] {
+		require(m && t, "null argument");
+		require(t->render_pipelines <= RenderScratch::MAX_PIPES, "render_pipelines must be 0..4");
+		require(t->render_pass_samples <= (16u << 20), "render_pass_samples must be <= 2^24");
+		require(t->render_lag == 0 || (t->render_lag >= 2 && t->render_lag <= 4), "render_lag must be 0 or 2..4");
+		require(t->render_composite_block == 0 || t->render_composite_block == 256 || t->render_composite_block == 512 ||
+		            t->render_composite_block == 1024,
+		        "render_composite_block must be 0, 256, 512 or 1024");
+		require(t->render_generate_block == 0 || t->render_generate_block == 256 || t->render_generate_block == 512,
+		        "render_generate_block must be 0, 256 or 512");
+		require(t->mlp_workgroups_per_cu <= 32, "mlp_workgroups_per_cu must be <= 32");
+		m->tuning = *t;
+	});
+}
+
+ngp_status ngp_model_get_tuning(const ngp_model* m, ngp_tuning* t) {
+	return guarded([&] {
+		require(m && t, "null argument");
+		*t = m->tuning;
 	});
 }
 

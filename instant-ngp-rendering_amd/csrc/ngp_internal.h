@@ -327,6 +327,7 @@ struct ngp_model {
 	uint64_t n_mlp_params = 0, n_grid_params = 0, n_params = 0;
 	uint32_t frag_halves = 0;  // packed fragment blob size
 	int mlp_variant = -1;
+	ngp_tuning tuning{};  // launch shapes / march schedule (ngp_model_set_tuning; 0 = default)
 
 	ngp::DevBuf<float> params32, ema32, grads, adam_m, adam_v;
 	ngp::DevBuf<__half> grid_grads16;  // hash-grid gradients (fp16, packed atomics)

@@ -18,6 +18,13 @@
 namespace py = pybind11;
 using namespace ngp;
 
+#define NGP_TUNING_FIELDS                                                                                              \
+	NGP_TUNING_FIELD(render_pipelines) NGP_TUNING_FIELD(render_pass_samples) NGP_TUNING_FIELD(render_lanes)          \
+	NGP_TUNING_FIELD(render_first_steps) NGP_TUNING_FIELD(render_max_steps) NGP_TUNING_FIELD(render_lag)             \
+	NGP_TUNING_FIELD(render_budget_scale) NGP_TUNING_FIELD(render_block_skipping)                                    \
+	NGP_TUNING_FIELD(render_composite_block) NGP_TUNING_FIELD(render_generate_block)                                 \
+	NGP_TUNING_FIELD(encode_dense_records) NGP_TUNING_FIELD(mlp_workgroups_per_cu) NGP_TUNING_FIELD(debug)
+
 namespace {
 
 ETestbedMode mode_from_string(const std::string& s) {
@@ -494,6 +501,30 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("relative_focal_length", &Testbed::relative_focal_length)
 		.def_readwrite("training_batch_size", &Testbed::training_batch_size)
 		.def_readwrite("train_full_forward", &Testbed::train_full_forward)
+		// ngp_tuning (include/ngp_hip.h) as a dict; unknown keys are an error, missing keys keep their value
+		.def("get_tuning",
+		     [](const Testbed& t) {
+			     const ngp_tuning& u = t.tuning();
+			     py::dict d;
+#define NGP_TUNING_FIELD(f) d[#f] = u.f;
+			     NGP_TUNING_FIELDS
+#undef NGP_TUNING_FIELD
+			     return d;
+		     })
+		.def("set_tuning",
+		     [](Testbed& t, py::dict d) {
+			     ngp_tuning u = t.tuning();
+			     for (auto kv : d) {
+				     const std::string k = py::str(kv.first);
+				     bool known = false;
+#define NGP_TUNING_FIELD(f) \
+	if (k == #f) { u.f = kv.second.cast<decltype(u.f)>(); known = true; }
+				     NGP_TUNING_FIELDS
+#undef NGP_TUNING_FIELD
+				     if (!known) throw std::invalid_argument("unknown tuning field '" + k + "'");
+			     }
+			     t.set_tuning(u);
+		     })
 		.def("set_nerf_camera_matrix",
 		     [](Testbed& t, py::array_t<float, py::array::c_style | py::array::forcecast> c) {
 			     auto rm = numpy_to_rowmajor34(c);

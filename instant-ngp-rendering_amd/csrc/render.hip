@@ -702,39 +702,22 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 	return n;
 }
 
-// NGP_RENDER_STEPS_PER_PASS overrides the per-pass sample cap (tuning knob; results do not depend on it)
-// NGP_RENDER_LANES overrides the lane budget that picks lanes-per-ray in k_generate
-static uint32_t lanes_target() {
-	const char* e = getenv("NGP_RENDER_LANES");
-	const long v = e ? atol(e) : 0;
-	return v > 0 ? (uint32_t)v : 4u << 20;
+// The march schedule (ngp_tuning; results do not depend on it):
+//  * lanes_target: the lane budget that picks lanes-per-ray in k_generate (4M);
+//  * pass_sample_target: a pipeline's sample slots per pass (4M; <= 16M: the MLP reads the
+//    encodings through raw buffers with 32-bit byte offsets, 64 B/sample);
+//  * first_pass_steps / max_steps_per_pass: the per-ray cap of the first pass doubles every pass
+//    up to the maximum (4 -> 32).  A ray's slots past its termination are wasted encoder and MLP
+//    work: most rays of a surface scene stop within a few samples of their first occupied one,
+//    while rays through a volume need many, so short first passes and geometric growth keep the
+//    waste and the pass count both low.  Inside the cap each ray's budget also follows its
+//    transmittance and the opacity of its last sample (sample_budget).
+static uint32_t lanes_target(const ngp_tuning& t) { return t.render_lanes ? t.render_lanes : 4u << 20; }
+static uint32_t pass_sample_target(const ngp_tuning& t) {
+	return std::min<uint32_t>(t.render_pass_samples ? t.render_pass_samples : 4u << 20, 16u << 20);
 }
-
-// NGP_RENDER_TARGET overrides the per-pass sample budget (tuning knob; results do not depend on it)
-static uint32_t pass_sample_target() {
-	const char* e = getenv("NGP_RENDER_TARGET");
-	const long v = e ? atol(e) : 0;
-	// <= 16M: the MLP reads the encodings through raw buffers with 32-bit byte offsets (64 B/sample)
-	return (uint32_t)std::min<long>(v > 0 ? v : 4l << 20, 16l << 20);
-}
-
-// NGP_RENDER_FIRST_STEPS: the per-ray cap of the first pass; the cap doubles every pass up to
-// NGP_RENDER_STEPS_PER_PASS.  A ray's slots past its termination are wasted encoder and MLP
-// work: most rays of a surface scene stop within a few samples of their first occupied one,
-// while rays through a volume need many, so short first passes and geometric growth keep the
-// waste and the pass count both low.  Inside the cap each ray's budget also follows its
-// transmittance and the opacity of its last sample (sample_budget).
-static uint32_t first_pass_steps() {
-	const char* e = getenv("NGP_RENDER_FIRST_STEPS");
-	const int v = e ? atoi(e) : 0;
-	return v > 0 ? (uint32_t)v : 4u;
-}
-
-static uint32_t max_steps_per_pass() {
-	const char* e = getenv("NGP_RENDER_STEPS_PER_PASS");
-	const int v = e ? atoi(e) : 0;
-	return v > 0 ? (uint32_t)v : 32u;
-}
+static uint32_t first_pass_steps(const ngp_tuning& t) { return t.render_first_steps ? t.render_first_steps : 4u; }
+static uint32_t max_steps_per_pass(const ngp_tuning& t) { return t.render_max_steps ? t.render_max_steps : 32u; }
 
 // rows r < h_shard of a shard with (r / 8) % pipe_count == pipe_index
 static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_count) {
@@ -744,29 +727,28 @@ static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_c
 	return n;
 }
 
-// NGP_RENDER_PIPES: ray pipelines per render (1 .. 4; default 2 for frames of >= 2^16 rays).
-// The pipelines take interleaved 8-row blocks of the frame and run their passes on their own
-// streams: one pipeline's latency-bound march kernels overlap another's encoder
+// Ray pipelines per render (ngp_tuning.render_pipelines, 1 .. 4; default 2 for frames of >= 2^16
+// rays).  The pipelines take interleaved 8-row blocks of the frame and run their passes on their
+// own streams: one pipeline's latency-bound march kernels overlap another's encoder
 // (texture-addresser bound) and MLP (matrix cores).  Every ray composites its own samples in
 // order, so the image does not depend on the split.
-static uint32_t render_pipes(uint32_t n, uint32_t h_shard) {
-	const char* e = getenv("NGP_RENDER_PIPES");
+static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard) {
+#ifdef NGP_DIAGNOSTICS
 	if (getenv("NGP_RENDER_DUMP")) return 1;  // the diagnostic dump covers one pipeline's pass 0
+#endif
 	uint32_t p = n >= (1u << 16) ? 2u : 1u;
-	if (e && atoi(e) >= 1) p = std::min<uint32_t>((uint32_t)atoi(e), RenderScratch::MAX_PIPES);
+	if (t.render_pipelines) p = std::min<uint32_t>(t.render_pipelines, RenderScratch::MAX_PIPES);
 	return std::max(1u, std::min(p, div_up(h_shard, 8u)));  // every pipeline gets rows
 }
 
 // Pinned host-counter words of a pipeline: per-pass unpacked counters in HC_SLOTS slots (the
-// read-back lag, NGP_RENDER_LAG, is at most HC_SLOTS passes), a copy-back slot, and the words the
+// read-back lag, ngp_tuning.render_lag, is at most HC_SLOTS passes), a copy-back slot, and the words the
 // kernels publish.
 constexpr uint32_t HC_SLOTS = 4, HC_COPYBACK = 16 * HC_SLOTS, HC_PUBLISHED = 128, HC_WORDS = HC_PUBLISHED + 16 * HC_SLOTS;
 
-// NGP_RENDER_LAG: passes a pipeline runs ahead of its counter read-backs (2 .. HC_SLOTS, default 3)
-static uint32_t render_lag() {
-	const char* e = getenv("NGP_RENDER_LAG");
-	const int v = e ? atoi(e) : 0;
-	return v >= 2 ? std::min<uint32_t>((uint32_t)v, HC_SLOTS) : 3u;  // 3: -0.6 % against 2 (same weights)
+// passes a pipeline runs ahead of its counter read-backs (ngp_tuning.render_lag, 2 .. HC_SLOTS)
+static uint32_t render_lag(const ngp_tuning& t) {
+	return t.render_lag >= 2 ? std::min<uint32_t>(t.render_lag, HC_SLOTS) : 3u;  // 3: -0.6 % against 2 (same weights)
 }
 
 namespace {
@@ -859,16 +841,15 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const uint32_t H_shard = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	if (k.W * H_shard == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
-	const uint32_t n_pipes = render_pipes(k.W * H_shard, H_shard);
+	const ngp_tuning& tu = m->tuning;
+	const uint32_t n_pipes = render_pipes(tu, k.W * H_shard, H_shard);
 
-	const uint32_t target = pass_sample_target(), cap = max_steps_per_pass(), cap0 = std::min(first_pass_steps(), cap);
-	static const bool debug = getenv("NGP_RENDER_DEBUG") != nullptr;
-	// per-ray sample budgets: NGP_RENDER_BUDGET=<headroom factor> (default 1.0: measured 1 % faster than 1.5) or "off"
-	const char* budget_env = getenv("NGP_RENDER_BUDGET");  // read per render (A/B knob)
-	k.budget = !(budget_env && strcmp(budget_env, "off") == 0);
-	k.budget_scale = budget_env && k.budget ? (float)atof(budget_env) : 1.0f;
-	if (!(k.budget_scale > 0.0f)) k.budget_scale = 1.0f;
-	static const bool block_skipping = getenv("NGP_RENDER_SKIP") && !strcmp(getenv("NGP_RENDER_SKIP"), "blocks");
+	const uint32_t target = pass_sample_target(tu), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu), cap);
+	const bool debug = (tu.debug & 1u) != 0;
+	// per-ray sample budgets: headroom factor (default 1.0: measured 1 % faster than 1.5), < 0 = off
+	k.budget = !(tu.render_budget_scale < 0.0f);
+	k.budget_scale = tu.render_budget_scale > 0.0f ? tu.render_budget_scale : 1.0f;
+	const bool block_skipping = tu.render_block_skipping != 0;
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
 	for (uint32_t j = 1; j < n_pipes; ++j) {
@@ -963,13 +944,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// empty).  With two pipelines the host alternates between them, so each stream holds up
 	// to two enqueued passes while the host waits on the other's read-back.
 	const uint32_t MARCH_ITER = 10000;
-	const uint32_t lag = render_lag();
-	// NGP_RENDER_COMPOSITE_BLOCK: k_composite workgroup size (256, 512 or 1024; 512 measured 0.5 %
-	// faster than 1024, 256 2 % slower); NGP_RENDER_GENERATE_BLOCK: k_generate's (512; 256 measured 4.5 % slower)
-	const char* cb_env = getenv("NGP_RENDER_COMPOSITE_BLOCK");
-	const uint32_t comp_block = cb_env && (atoi(cb_env) == 256 || atoi(cb_env) == 1024) ? (uint32_t)atoi(cb_env) : 512u;
-	const char* gb_env = getenv("NGP_RENDER_GENERATE_BLOCK");
-	const uint32_t gen_block = gb_env && atoi(gb_env) == 256 ? 256u : 512u;
+	const uint32_t lag = render_lag(tu);
+	// workgroup sizes: k_composite 512 (measured 0.5 % faster than 1024, 256 2 % slower), k_generate
+	// 512 (256 measured 4.5 % slower)
+	const uint32_t comp_block = tu.render_composite_block ? tu.render_composite_block : 512u;
+	const uint32_t gen_block = tu.render_generate_block ? tu.render_generate_block : 512u;
 	auto enqueue_pass = [&](PipeRun& pr) {
 		const hipStream_t ps = pr.s;
 		uint32_t* counters = pr.ps->counters.ptr;
@@ -982,7 +961,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		uint32_t* samples_next = counters + 4 + (pass + 1) % 2;
 		uint32_t* steps_out = counters + 6 + pass % 2;
 		// lanes per ray: enough rays in flight for ~1M lanes, never fewer than one lane per ray
-		const uint32_t want = lanes_target() / std::max(pr.n_alive_ub, 1u);
+		const uint32_t want = lanes_target(tu) / std::max(pr.n_alive_ub, 1u);
 		const uint32_t G = want >= 64 ? 64u : want >= 16 ? 16u : want >= 4 ? 4u : 1u;
 		const uint32_t gblocks = std::max(1u, div_up((uint64_t)pr.n_alive_ub * G, gen_block));
 		unsigned long long* host_prev = pass > 0 ? pr.pub_dev() + 8 * ((pass - 1) % HC_SLOTS) : nullptr;
@@ -999,7 +978,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint64_t bound = std::min<uint64_t>((uint64_t)pr.n_alive_ub * cap_p, std::max(target, pr.n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin_kernel(NGP_TIMER_RENDER_ENCODE);
-		static const char* dump = getenv("NGP_RENDER_DUMP");  // diagnostic: pass-0 samples + alive payloads
+#ifdef NGP_DIAGNOSTICS
+		static const char* dump = getenv("NGP_RENDER_DUMP");  // diagnostic builds only: pass-0 samples + alive payloads
 		if (dump && pass == 0) {
 			uint32_t c[8];
 			NGP_HIP_CHECK(hipMemcpyAsync(c, counters, sizeof(c), hipMemcpyDeviceToHost, ps));
@@ -1016,6 +996,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 				fclose(f);
 			}
 		}
+#endif
 		launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
 		                    internal_layout(m, n_elements), ps, samples, 1);
 		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back

@@ -937,12 +937,18 @@ void Testbed::build_model(const Json& cfg) {
 		m_model = nullptr;
 	}
 	ck(ngp_model_create(device, &c, seed, &m_model));
+	ck(ngp_model_set_tuning(m_model, &m_tuning));
 	m_net_cfg = c;
 }
 
 // ---------------------------------------------------------------------------
 // Training
 // ---------------------------------------------------------------------------
+void Testbed::set_tuning(const ngp_tuning& t) {
+	if (m_model) ck(ngp_model_set_tuning(m_model, &t));  // validates
+	m_tuning = t;
+}
+
 void Testbed::update_density_grid(uint32_t n_uniform, uint32_t n_nonuniform) {
 	upload_dataset();
 	ngp_grid_args g{};

@@ -220,6 +220,9 @@ public:
 	int world_size() const { return m_world; }
 
 	ngp_model* model() const { return m_model; }
+	// launch shapes / march schedule of the kernels (ngp_tuning; kept across network reloads)
+	const ngp_tuning& tuning() const { return m_tuning; }
+	void set_tuning(const ngp_tuning& t);
 	void* stream() const { return m_stream; }
 	void sync() const;
 	// the learned distortion map's parameters, [res_y][res_x][2] (m_distortion.map->params())
@@ -239,6 +242,7 @@ public:
 	// early-terminated chunked forward; switched on automatically if the chunked forward ever
 	// misses a sample the loss needs (ngp_train_stats::forward_early_stop_violations)
 	bool train_full_forward = false;
+	ngp_tuning m_tuning{};
 	uint64_t forward_early_stop_violations = 0;
 	uint32_t training_step = 0;
 	float loss = 0.0f;  // Ema m_loss_scalar (val) of src/testbed.cu:4106-4108

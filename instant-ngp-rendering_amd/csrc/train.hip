@@ -1304,10 +1304,9 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 
 	// network inference with the training params (NerfNetwork::inference_mixed_precision): over
-	// every emitted sample as the reference does (NGP_TRAIN_CHUNKED=0), or chunk by chunk up to
-	// each ray's stop (k_train_chunk) -- the loss kernels read the same outputs either way
-	const char* chunk_env = getenv("NGP_TRAIN_CHUNKED");  // read per step (tests switch it)
-	const bool chunk_off = t->full_forward || (chunk_env && !strcmp(chunk_env, "0"));
+	// every emitted sample as the reference does (full_forward), or chunk by chunk up to each
+	// ray's stop (k_train_chunk) -- the loss kernels read the same outputs either way
+	const bool chunk_off = t->full_forward != 0;
 	const __half* table = m->params16.ptr + m->n_mlp_params;
 	const __half* enc_rows = ts.enc.ptr;
 	EncLayout enc_layout = internal_layout(m, MS);
@@ -1457,7 +1456,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
 	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
 	NGP_HIP_CHECK(hipGetLastError());
-	static const bool train_debug = getenv("NGP_TRAIN_DEBUG") != nullptr;
+	const bool train_debug = (m->tuning.debug & 2u) != 0;
 	if (train_debug) {
 		// samples per ray emitted vs composited before termination, and what a chunked
 		// (early-terminated) forward would evaluate under a few chunk schedules

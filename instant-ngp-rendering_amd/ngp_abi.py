@@ -101,6 +101,17 @@ class RenderArgs(C.Structure):
     ]
 
 
+class Tuning(C.Structure):
+    """ngp_tuning: launch shapes / march schedule (0 = the measured default; results do not depend on them)."""
+    _fields_ = [
+        ("render_pipelines", C.c_uint32), ("render_pass_samples", C.c_uint32), ("render_lanes", C.c_uint32),
+        ("render_first_steps", C.c_uint32), ("render_max_steps", C.c_uint32), ("render_lag", C.c_uint32),
+        ("render_budget_scale", C.c_float), ("render_block_skipping", C.c_uint32),
+        ("render_composite_block", C.c_uint32), ("render_generate_block", C.c_uint32),
+        ("encode_dense_records", C.c_uint32), ("mlp_workgroups_per_cu", C.c_uint32), ("debug", C.c_uint32),
+    ]
+
+
 # enums (include/ngp_hip.h)
 PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M, ADAM_V, GRADS_GRID_FP16 = range(8)
 SCRATCH_RAY_NUMSTEPS, SCRATCH_COORDS, SCRATCH_MLP_OUT, SCRATCH_RAY_COMPACTED, SCRATCH_DLOSS, SCRATCH_LOSS, \
@@ -113,6 +124,8 @@ TIMER = {name: i for i, name in enumerate(TIMERS)}
 EXPORTS = {
     "ngp_model_create": (C.c_int, [C.c_int, C.POINTER(NetworkConfig), C.c_uint64, C.POINTER(C.c_void_p)]),
     "ngp_model_destroy": (C.c_int, [C.c_void_p]),
+    "ngp_model_set_tuning": (C.c_int, [C.c_void_p, C.POINTER(Tuning)]),
+    "ngp_model_get_tuning": (C.c_int, [C.c_void_p, C.POINTER(Tuning)]),
     "ngp_model_get_info": (C.c_int, [C.c_void_p, C.POINTER(ModelInfo)]),
     "ngp_model_buffer": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "ngp_model_params_updated": (C.c_int, [C.c_void_p, C.c_int, C.c_void_p]),

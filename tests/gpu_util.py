@@ -36,6 +36,14 @@ class GpuModel:
         self.L = cfg.n_levels
         self.F = cfg.n_features_per_level
 
+    def set_tuning(self, **kw):
+        """ngp_model_set_tuning (launch shapes / march schedule; 0 = default)."""
+        t = A.Tuning()
+        A.check(self.lib.ngp_model_get_tuning(self.h, C.byref(t)))
+        for k, v in kw.items():
+            setattr(t, k, v)
+        A.check(self.lib.ngp_model_set_tuning(self.h, C.byref(t)))
+
     def close(self):
         if self.h:
             torch.cuda.synchronize()

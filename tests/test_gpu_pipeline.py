@@ -157,7 +157,7 @@ def test_train_step_matches_oracle(cfg_kw):
         g.close()
 
 
-def test_chunked_forward_matches_full_forward(monkeypatch):
+def test_chunked_forward_matches_full_forward():
     """The early-terminated (chunked) forward leaves the loss, the compaction and dL/dout
     bit-identical to evaluating every sample (the reference's inference over the whole
     pre-compaction batch); gradients agree up to float-atomic ordering."""
@@ -169,9 +169,10 @@ def test_chunked_forward_matches_full_forward(monkeypatch):
         R, B, MS = 2048, 1 << 14, 1 << 17
         out = {}
         for mode in ("0", "1"):
-            monkeypatch.setenv("NGP_TRAIN_CHUNKED", mode)
             g.zero_grads()
-            A.check(g.lib.ngp_train_step(g.h, C.byref(train_args(dd.ptr, dd.n, R, B, MS)), stream()))
+            ta = train_args(dd.ptr, dd.n, R, B, MS)
+            ta.full_forward = 1 if mode == "0" else 0
+            A.check(g.lib.ngp_train_step(g.h, C.byref(ta), stream()))
             torch.cuda.synchronize()
             st = A.TrainStats()
             A.check(g.lib.ngp_train_read_stats(g.h, C.byref(st), stream()))
@@ -882,14 +883,14 @@ def test_render_motion_blur_matches_oracle():
 
 @pytest.mark.parametrize("pipes,shard", [(1, (0, 1, 8)), (2, (0, 1, 8)), (3, (0, 1, 8)), (4, (0, 1, 8)), (2, (1, 3, 4))],
                          ids=["1", "2", "3", "4", "2-shard"])
-def test_render_pipelines_match_oracle(pipes, shard, monkeypatch):
+def test_render_pipelines_match_oracle(pipes, shard):
     """The renderer's ray pipelines (render.hip render_pipes: interleaved 8-row blocks of the shard's
     rows, one stream each) against the oracle's single straight march, on config B, a frame whose
     row count leaves partial blocks (66 rows), also under a row shard.  Every pipeline count must
     give the same pixels (depth included)."""
-    monkeypatch.setenv("NGP_RENDER_PIPES", str(pipes))
     g, o, rng = pair(CFG_B, grid_scale=1.0)
     try:
+        g.set_tuning(render_pipelines=pipes)
         set_bitfield_both(g, o, sphere_bitfield(0.3))
         W, H = 72, 66
         cam = make_views(1, 8, 8)[1][0]

@@ -29,7 +29,7 @@ h = C.c_void_p(tb.model_handle)
 A.check(lib.ngp_timing_enable(h, int(os.environ.get("TIMER_MASK", "-1"))))
 tb.set_camera_to_training_view(3)
 for cap in [int(c) for c in os.environ.get("CAPS", "1,4,8,16,32,64,128").split(",")]:
-    os.environ["NGP_RENDER_STEPS_PER_PASS"] = str(cap)
+    tb.set_tuning({"render_max_steps": cap})
     tb.render_to_device(1920, 1080, 1, True)
     for name in A.TIMERS:
         lib.ngp_timing_read(h, A.TIMER[name], None, None, None, 1)

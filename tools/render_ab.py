@@ -1,11 +1,11 @@
 """Render-schedule A/B on one box and one set of weights (diagnostic, GPU box).
 
 Trains the bench scene once (bench.py's defaults), then renders the bench's 1080p view under
-each environment setting in turn, round-robin, so box-to-box and run-to-run spread cancel out.
-The render knobs it varies (NGP_RENDER_PIPES / TARGET / STEPS_PER_PASS / LANES /
-FIRST_STEPS) are read on every render call.
+each setting in turn, round-robin, so box-to-box and run-to-run spread cancel out.  A setting is
+a space-separated list of ngp_tuning fields (include/ngp_hip.h; Testbed.set_tuning), applied
+before its frames.
 
-Usage: python tools/render_ab.py [--rounds 4] [--frames 5] "" "NGP_RENDER_PIPES=1" "NGP_RENDER_TARGET=8388608" ...
+Usage: python tools/render_ab.py [--rounds 4] [--frames 5] "" "render_pipelines=1" "render_pass_samples=8388608" ...
 """
 import argparse
 import os
@@ -15,9 +15,6 @@ import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "instant-ngp-rendering_amd"))
-
-KNOBS = ("NGP_MLP_WG_PER_CU", "NGP_RENDER_GENERATE_BLOCK", "NGP_RENDER_COMPOSITE_BLOCK", "NGP_RENDER_LAG", "NGP_RENDER_BUDGET", "NGP_ENC_DENSE_RECORDS", "NGP_RENDER_PIPES", "NGP_RENDER_TARGET", "NGP_RENDER_STEPS_PER_PASS", "NGP_RENDER_LANES",
-         "NGP_RENDER_FIRST_STEPS")
 
 
 def main():
@@ -50,18 +47,15 @@ def main():
             tb.save_snapshot(a.snapshot, False)
     n_views = tb.nerf.training.dataset.n_images
     tb.set_camera_to_training_view(3 % n_views)
-    base = {k: os.environ.get(k) for k in KNOBS}
+    base = tb.get_tuning()
     times = {s: [] for s in a.settings}
     for r in range(a.rounds):
         for s in a.settings:
-            for k, v in base.items():
-                if v is None:
-                    os.environ.pop(k, None)
-                else:
-                    os.environ[k] = v
+            setting = dict(base)
             for kv in s.split():
                 k, v = kv.split("=", 1)
-                os.environ[k] = v
+                setting[k] = float(v) if k == "render_budget_scale" else int(v)
+            tb.set_tuning(setting)
             tb.render_to_device(1920, 1080, 1, True)  # warm this setting's buffers
             t0 = time.perf_counter()
             for _ in range(a.frames):
