@@ -107,8 +107,10 @@ enum {
 	                             [0, n_mlp_params) is used, hash-grid gradients live in GRID_FP16 */
 	NGP_ADAM_M = 5,
 	NGP_ADAM_V = 6,
-	NGP_GRADS_GRID_FP16 = 7   /* hash-grid gradients [n_params - n_mlp_params], fp16, accumulated with
+	NGP_GRADS_GRID_FP16 = 7,  /* hash-grid gradients [n_params - n_mlp_params], fp16, accumulated with
 	                             packed half2 atomics like tcnn's GridEncoding backward */
+	NGP_GRADS_GRID_FIXED64 = 8/* the same in deterministic steps: int64 fixed point, value = v * 2^-40 (allocated on the
+	                             first deterministic step; null before) */
 };
 
 /* One training image; an array of these lives in device memory (TrainingImageMetadata,
@@ -203,6 +205,21 @@ typedef struct ngp_train_args {
 	uint32_t distortion_res[2];
 	float* distortion_gradient;
 	float* distortion_gradient_weight;
+	/* data parallelism: this rank's slice of the global batch.  n_rays / ray_index_offset
+	 * are the rank's rays of the n_rays_global of the step; target_batch_size and max_samples are the
+	 * GLOBAL values.  The step calls allreduce_i32 (sum of world_size int32 device words, on `stream`)
+	 * twice -- after sampling and after the loss composite -- to learn every rank's totals, so the
+	 * sampler's max_samples cap, the compaction cap and the rollover (tcnn fill_rollover_and_rescale)
+	 * apply to the global ray order exactly as in one process training n_rays_global rays
+	 * (src/testbed_nerf.cu:779-781, 997-1003, 2862-2870).  world_size <= 1 or a null callback: one
+	 * process (rank must be 0). */
+	uint32_t rank, world_size;
+	ngp_status (*allreduce_i32)(void* user, int32_t* dev, uint32_t n, ngp_stream stream);
+	void* allreduce_user;
+	/* 1: hash-grid gradients accumulate as 64-bit fixed point (2^-40 units, NGP_GRADS_GRID_FIXED64) with
+	 * integer atomics -- order-independent sums, so a step is bit-reproducible and data-parallel ranks
+	 * sum exactly (deterministic mode); 0: packed fp16 atomics as tcnn's GridEncoding backward */
+	int32_t deterministic;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {
@@ -335,7 +352,8 @@ ngp_status ngp_optimizer_step(ngp_model* model, uint32_t training_step, int opti
 ngp_status ngp_train_read_stats(ngp_model* model, ngp_train_stats* stats, ngp_stream stream);
 /* Data-parallel training: sum the model's gradients over an RCCL communicator (an ncclComm_t):
  * the fp32 MLP gradients and the fp16 hash-grid gradients, in one group on `stream`.  Call it
- * between ngp_train_step (defer_optimizer = 1) and ngp_optimizer_step on every rank. */
+ * between ngp_train_step (defer_optimizer = 1) and ngp_optimizer_step on every rank.  After a
+ * deterministic step the hash-grid part is the int64 fixed-point buffer (an exact integer sum). */
 ngp_status ngp_allreduce_grads(ngp_model* model, void* nccl_comm, ngp_stream stream);
 /* Debug/parity: device pointers to the last step's scratch (valid until the next step). */
 enum {
@@ -346,11 +364,17 @@ enum {
 	NGP_SCRATCH_DLOSS = 4,        /* [target_batch][4] f16 */
 	NGP_SCRATCH_LOSS = 5,         /* [n_rays] f32 */
 	NGP_SCRATCH_COMPACT_COORDS = 6,/* [target_batch][8] f32 */
-	NGP_SCRATCH_RAY_EVALUATED = 7 /* [n_rays] u32: samples of the ray the forward evaluated (bit 31 set); it
+	NGP_SCRATCH_RAY_EVALUATED = 7,/* [n_rays] u32: samples of the ray the forward evaluated (bit 31 set); it
 	                                 stops once the transmittance is below the loss's threshold. Null when
-	                                 every sample was evaluated (NGP_TRAIN_CHUNKED=0) */
+	                                 every sample was evaluated (full_forward) */
+	NGP_SCRATCH_VIOLATIONS = 8    /* 1 u32: the last step's forward_early_stop_violations.  ngp_optimizer_step
+	                                 skips the whole update while it is non-zero (data-parallel callers all-reduce
+	                                 it with max first); ngp_train_discard then clears the step for a re-run */
 };
 ngp_status ngp_train_scratch(ngp_model* model, int kind, void** dev_ptr, size_t* bytes);
+/* Drops the last step's gradients (MLP and hash grid) before the step is run again -- after a chunked
+ * forward reported forward_early_stop_violations, which made its optimizer step a no-op. */
+ngp_status ngp_train_discard(ngp_model* model, ngp_stream stream);
 
 /* --- occupancy grid ------------------------------------------------------------------ */
 ngp_status ngp_density_grid_update(ngp_model* model, const ngp_grid_args* args, ngp_stream stream);

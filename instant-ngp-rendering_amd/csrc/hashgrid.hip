@@ -18,6 +18,7 @@
 //    writes 64 contiguous 16-B planes (F = 2).
 //  * features accumulate in fp32 (tcnn accumulates in fp16) and are rounded once.
 #include <cstring>
+#include <type_traits>
 
 #include "ngp_internal.h"
 
@@ -336,17 +337,26 @@ __device__ __forceinline__ void scatter_add(__half* gtab, uint32_t idx, const fl
 // batch, i.e. consecutive points along the same rays, so at coarse levels they often add
 // into the same corner: runs of equal indices (lane, lane+2, ...) are summed with a
 // segmented shuffle scan and only the last lane of each run issues the atomic.
-constexpr uint32_t BWD_SAMPLES_PER_BLOCK = 128;
+// Deterministic mode (FIXED): each corner's contribution is rounded to 2^-40 fixed point first,
+// the run sums and the memory-side atomics are 64-bit integer adds -- exact, so the result does not
+// depend on the order the waves arrive in.
 template <uint32_t F>
-__global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
-                                                      const __half* __restrict__ denc, EncLayout lay,
-                                                      const LevelTable lt, __half* __restrict__ grad,
-                                                      uint32_t n_chunks, const uint32_t* __restrict__ n_dev) {
-	uint32_t level, chunk;
-	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
+__device__ __forceinline__ void scatter_add_fixed(long long* gtab, uint32_t idx, const long long* v) {
+#pragma unroll
+	for (uint32_t f = 0; f < F; ++f)
+		if (v[f]) atomicAdd(reinterpret_cast<unsigned long long*>(gtab + (size_t)idx * F + f), (unsigned long long)v[f]);
+}
+__device__ __forceinline__ long long to_fixed(float v) {
+	const float x = fminf(fmaxf(v * GRAD_FIXED_SCALE, -9.2e18f), 9.2e18f);
+	return (long long)rintf(x);
+}
+
+constexpr uint32_t BWD_SAMPLES_PER_BLOCK = 128;
+template <uint32_t F, bool FIXED>
+__device__ __forceinline__ void hashgrid_bwd_chunk(uint32_t n, uint32_t level, uint32_t chunk, const float* __restrict__ pos,
+                                                   uint32_t stride, const __half* __restrict__ denc, const EncLayout& lay,
+                                                   const LevelTable& lt, __half* __restrict__ grad, long long* __restrict__ grad64) {
 	const uint32_t i = chunk * BWD_SAMPLES_PER_BLOCK + (threadIdx.x >> 1), h = threadIdx.x & 1u;
-	if (n_dev) n = min(n, *n_dev);
-	if (chunk * BWD_SAMPLES_PER_BLOCK >= n) return;  // whole block idle (block-uniform)
 	const int lane = threadIdx.x & 63;
 
 	using VT = typename FeatVec<F>::T;
@@ -366,7 +376,8 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 
 	const float scale = lt.scale[level];
 	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
-	__half* gtab = grad + (size_t)lt.offset[level] * F;
+	__half* gtab = FIXED ? nullptr : grad + (size_t)lt.offset[level] * F;
+	long long* gtab64 = FIXED ? grad64 + (size_t)lt.offset[level] * F : nullptr;
 
 	float fx = 0.f, fy = 0.f, fz = 0.f;
 	uint32_t gx = 0, gy = 0, gz = 0;
@@ -387,14 +398,21 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 		w *= (c & 2u) ? fz : 1.0f - fz;
 		const uint32_t idx = active ? grid_index(hashed, size, res, gx + h, gy + (c & 1u), gz + ((c >> 1) & 1u))
 		                            : 0xFFFFFFFFu - (uint32_t)lane;  // inactive lanes never merge
-		float v[F];
+		using AccT = typename std::conditional<FIXED, long long, float>::type;
+		AccT v[F];
 #pragma unroll
-		for (uint32_t f = 0; f < F; ++f) v[f] = w * g[f];
+		for (uint32_t f = 0; f < F; ++f) {
+			if constexpr (FIXED) v[f] = to_fixed(w * g[f]);
+			else v[f] = w * g[f];
+		}
 		const uint32_t prev = __shfl_up(idx, 2, 64);
 		const bool head = lane < 2 || prev != idx;
 		const unsigned long long heads = __ballot(head);
 		if (~heads == 0ull) {
-			if (active) scatter_add<F>(gtab, idx, v);
+			if (active) {
+				if constexpr (FIXED) scatter_add_fixed<F>(gtab64, idx, v);
+				else scatter_add<F>(gtab, idx, v);
+			}
 			continue;
 		}
 		// run start of this lane = highest head of its parity at or below it
@@ -403,13 +421,30 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 		for (int off = 2; off < 64; off <<= 1) {
 #pragma unroll
 			for (uint32_t f = 0; f < F; ++f) {
-				const float t = __shfl_up(v[f], off, 64);
+				const AccT t = __shfl_up(v[f], off, 64);
 				if (lane - off >= start) v[f] += t;
 			}
 		}
 		const bool tail = lane >= 62 || ((heads >> (lane + 2)) & 1ull);
-		if (active && tail) scatter_add<F>(gtab, idx, v);
+		if (active && tail) {
+			if constexpr (FIXED) scatter_add_fixed<F>(gtab64, idx, v);
+			else scatter_add<F>(gtab, idx, v);
+		}
 	}
+}
+
+// Blocks loop over chunks (n_chunks launched per level, the device count may need more)
+template <uint32_t F, bool FIXED>
+__global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* __restrict__ pos, uint32_t stride,
+                                                      const __half* __restrict__ denc, EncLayout lay,
+                                                      const LevelTable lt, __half* __restrict__ grad,
+                                                      long long* __restrict__ grad64, uint32_t n_chunks,
+                                                      const uint32_t* __restrict__ n_dev) {
+	uint32_t level, chunk;
+	map_block(blockIdx.x, n_chunks, lt.n_levels, &level, &chunk);
+	if (n_dev) n = min(n, *n_dev);
+	for (; chunk * BWD_SAMPLES_PER_BLOCK < n; chunk += n_chunks)  // block-uniform
+		hashgrid_bwd_chunk<F, FIXED>(n, level, chunk, pos, stride, denc, lay, lt, grad, grad64);
 }
 
 
@@ -577,18 +612,28 @@ void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride
 	NGP_HIP_CHECK(hipGetLastError());
 }
 
-void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                         EncLayout enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev) {
-	if (n == 0) return;
-	const uint32_t n_chunks = div_up(n, BWD_SAMPLES_PER_BLOCK);
+template <bool FIXED>
+static void launch_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
+                       EncLayout enc_plane, __half* grad16, long long* grad64, hipStream_t s, const uint32_t* n_dev,
+                       uint32_t n_chunks) {
 	const uint32_t blocks = n_chunks * lt.n_levels;
 	switch (lt.F) {
-		case 1: launch_timed(k_hashgrid_bwd<1>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
-		case 2: launch_timed(k_hashgrid_bwd<2>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
-		case 4: launch_timed(k_hashgrid_bwd<4>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
-		case 8: launch_timed(k_hashgrid_bwd<8>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad_table, n_chunks, n_dev); break;
+		case 1: launch_timed(k_hashgrid_bwd<1, FIXED>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad16, grad64, n_chunks, n_dev); break;
+		case 2: launch_timed(k_hashgrid_bwd<2, FIXED>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad16, grad64, n_chunks, n_dev); break;
+		case 4: launch_timed(k_hashgrid_bwd<4, FIXED>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad16, grad64, n_chunks, n_dev); break;
+		case 8: launch_timed(k_hashgrid_bwd<8, FIXED>, blocks, 256, 0, s, n, pos, stride, denc, enc_plane, lt, grad16, grad64, n_chunks, n_dev); break;
 		default: throw std::runtime_error("n_features_per_level must be 1, 2, 4 or 8");
 	}
+}
+
+void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
+                         EncLayout enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev, long long* grad64,
+                         uint32_t max_chunks) {
+	if (n == 0) return;
+	uint32_t n_chunks = div_up(n, BWD_SAMPLES_PER_BLOCK);
+	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
+	if (grad64) launch_bwd<true>(lt, pos, stride, n, denc, enc_plane, nullptr, grad64, s, n_dev, n_chunks);
+	else launch_bwd<false>(lt, pos, stride, n, denc, enc_plane, grad_table, nullptr, s, n_dev, n_chunks);
 	NGP_HIP_CHECK(hipGetLastError());
 }
 

@@ -206,6 +206,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		(void)hipDeviceSynchronize();
 		for (auto* b : {&m->params32, &m->ema32, &m->grads, &m->adam_m, &m->adam_v}) b->release();
 		m->grid_grads16.release();
+		m->grid_grads64.release();
 		if (m->sync_event) (void)hipEventDestroy(m->sync_event);
 		m->params16.release();
 		m->infer16.release();
@@ -217,7 +218,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		t.coords.release(); t.enc.release(); t.mlp_out.release(); t.ccoords.release(); t.cenc.release();
 		t.pos4.release(); t.cpos4.release(); t.ray_aux.release();
 		t.dloss.release(); t.cweight.release(); t.csrc.release(); t.denc.release(); t.loss.release(); t.block_sums.release();
-		t.counters.release(); t.scan_a.release(); t.scan_b.release();
+		t.counters.release(); t.scan_a.release(); t.scan_b.release(); t.dp.release();
 		t.epos.release(); t.edir.release(); t.eenc.release(); t.eout.release(); t.eidx.release();
 		t.ray_T.release(); t.ray_eval.release(); t.ray_ebase.release(); t.dsh.release(); t.dpos.release();
 		GridState& g = m->gs;
@@ -290,6 +291,7 @@ ngp_status ngp_model_buffer(ngp_model* m, int kind, void** ptr, size_t* bytes) {
 			case NGP_ADAM_M: *ptr = m->adam_m.ptr; if (bytes) *bytes = m->n_params * 4; break;
 			case NGP_ADAM_V: *ptr = m->adam_v.ptr; if (bytes) *bytes = m->n_params * 4; break;
 			case NGP_GRADS_GRID_FP16: *ptr = m->grid_grads16.ptr; if (bytes) *bytes = m->n_grid_params * 2; break;
+			case NGP_GRADS_GRID_FIXED64: *ptr = m->grid_grads64.ptr; if (bytes) *bytes = m->grid_grads64.ptr ? m->n_grid_params * 8 : 0; break;
 			default: throw std::invalid_argument("unknown buffer kind");
 		}
 	});
@@ -433,9 +435,26 @@ ngp_status ngp_allreduce_grads(ngp_model* m, void* comm, ngp_stream s) {
 		// packed atomics write) -- summed, so every rank's optimizer step sees the global gradient
 		nk(ncclGroupStart(), "ncclGroupStart");
 		nk(ncclAllReduce(m->grads.ptr, m->grads.ptr, m->n_mlp_params, ncclFloat32, ncclSum, c, S(s)), "ncclAllReduce(mlp grads)");
-		nk(ncclAllReduce(m->grid_grads16.ptr, m->grid_grads16.ptr, m->n_params - m->n_mlp_params, ncclFloat16, ncclSum, c, S(s)),
-		   "ncclAllReduce(grid grads)");
+		if (m->ts.fixed)  // deterministic step: exact integer sum of the fixed-point gradients
+			nk(ncclAllReduce(m->grid_grads64.ptr, m->grid_grads64.ptr, m->n_grid_params, ncclInt64, ncclSum, c, S(s)),
+			   "ncclAllReduce(grid grads, fixed point)");
+		else
+			nk(ncclAllReduce(m->grid_grads16.ptr, m->grid_grads16.ptr, m->n_grid_params, ncclFloat16, ncclSum, c, S(s)),
+			   "ncclAllReduce(grid grads)");
 		nk(ncclGroupEnd(), "ncclGroupEnd");
+	});
+}
+
+ngp_status ngp_train_discard(ngp_model* m, ngp_stream s) {
+	return guarded([&] {
+		require(m, "null model");
+		// the gated optimizer step was a no-op on the device, but its host-side EMA step count moved
+		if (m->ts.gated_optimizer_ran && m->ema_step > 0) --m->ema_step;
+		m->ts.gated_optimizer_ran = false;
+		NGP_HIP_CHECK(hipMemsetAsync(m->grads.ptr, 0, m->n_mlp_params * sizeof(float), S(s)));
+		NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads16.ptr, 0, m->n_grid_params * sizeof(__half), S(s)));
+		if (m->grid_grads64.ptr) NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads64.ptr, 0, m->n_grid_params * sizeof(long long), S(s)));
+		if (m->ts.counters.ptr) NGP_HIP_CHECK(hipMemsetAsync(m->ts.counters.ptr + 9, 0, sizeof(uint32_t), S(s)));
 	});
 }
 
@@ -456,7 +475,7 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		if (tm.train_units_pending) {
 			// samples the forward evaluated: all emitted ones, or the chunks' rows
 			const uint64_t all = m->ts.chunked ? (uint64_t)c[12] + c[13] + c[14] : std::min(c[0], m->ts.last_max_samples);
-			const uint64_t comp = std::min(c[1], m->ts.last_target);
+			const uint64_t comp = c[5];  // this rank's kept samples (min(total, cap))
 			tm.units[NGP_TIMER_TRAIN_ENCODE] += all;
 			tm.units[NGP_TIMER_TRAIN_MLP_INFER] += all;
 			tm.units[NGP_TIMER_TRAIN_MLP_BWD] += comp;
@@ -488,6 +507,7 @@ ngp_status ngp_train_scratch(ngp_model* m, int kind, void** ptr, size_t* bytes) 
 				*ptr = t.chunked ? t.ray_eval.ptr : nullptr;
 				if (bytes) *bytes = t.chunked ? R * 4 : 0;
 				break;
+			case NGP_SCRATCH_VIOLATIONS: *ptr = t.counters.ptr ? t.counters.ptr + 9 : nullptr; if (bytes) *bytes = 4; break;
 			default: throw std::invalid_argument("unknown scratch kind");
 		}
 	});

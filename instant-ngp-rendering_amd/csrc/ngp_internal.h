@@ -211,6 +211,12 @@ struct DevBuf {
 	size_t bytes() const { return n * sizeof(T); }
 };
 
+// Deterministic hash-grid gradients (ngp_train_args.deterministic): 64-bit fixed point in units of
+// 2^-40 -- integer sums are exact and order-independent; |gradient| < 2^23 fits, contributions below
+// 2^-41 round to zero (fp16, the default accumulation, flushes below 6e-8).
+constexpr float GRAD_FIXED_SCALE = 1099511627776.0f;          // 2^40
+constexpr float GRAD_FIXED_INV = 1.0f / 1099511627776.0f;     // 2^-40
+
 struct TrainScratch {
 	DevBuf<uint32_t> ray_numsteps;     // [R][2]
 	DevBuf<uint32_t> ray_compacted;    // [R][2]
@@ -245,7 +251,10 @@ struct TrainScratch {
 	DevBuf<uint32_t> ray_eval, ray_ebase;  // [R]
 	DevBuf<float> dsh;                 // [B][16] dL/d(SH inputs) of the compacted batch (extrinsics)
 	DevBuf<float> dpos;                // [B][3] dL/d(warped position) of the compacted batch (extrinsics)
+	DevBuf<uint32_t> dp;               // data parallel: [0,3) sample DpCaps, [4,7) compaction DpCaps, then 2 x [world] slots
 	bool chunked = false;              // last step ran the chunked forward
+	bool fixed = false;                // last step accumulated hash-grid gradients in fixed point (deterministic)
+	bool gated_optimizer_ran = false;  // an optimizer step gated by the last step's violation word was enqueued
 	uint32_t last_rows[3] = {0, 0, 0}; // evaluation rows of each chunk in the last read-back step
 	uint32_t last_n_rays = 0, last_target = 0, last_max_samples = 0;
 };
@@ -331,6 +340,7 @@ struct ngp_model {
 
 	ngp::DevBuf<float> params32, ema32, grads, adam_m, adam_v;
 	ngp::DevBuf<__half> grid_grads16;  // hash-grid gradients (fp16, packed atomics)
+	ngp::DevBuf<long long> grid_grads64;  // deterministic mode: hash-grid gradients, 2^-40 fixed point
 	ngp::DevBuf<__half> params16, infer16;
 	ngp::DevBuf<uint32_t> adam_steps;
 	ngp::DevBuf<__half> frag_train, frag_infer;  // packed MFMA fragments of params16 / infer16
@@ -372,8 +382,11 @@ LevelTable build_dense_records(ngp_model* m, const __half* table, hipStream_t s)
 void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* table,
                          __half* enc, EncLayout enc_layout, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2,
                          uint32_t max_chunks = 0);
+// grad64 non-null: deterministic fixed-point accumulation into it (grad_table16 unused).
+// max_chunks > 0: blocks loop over the device count past max_chunks 128-sample chunks.
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
-                         EncLayout enc_layout, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr);
+                         EncLayout enc_layout, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr,
+                         long long* grad64 = nullptr, uint32_t max_chunks = 0);
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
                              float* w, hipStream_t s);
 // mlp.hip

@@ -501,6 +501,10 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("relative_focal_length", &Testbed::relative_focal_length)
 		.def_readwrite("training_batch_size", &Testbed::training_batch_size)
 		.def_readwrite("train_full_forward", &Testbed::train_full_forward)
+		.def_readwrite("deterministic", &Testbed::deterministic,
+		               "Bit-reproducible training steps: hash-grid gradients summed in 64-bit fixed point "
+		               "(ngp_train_args.deterministic) instead of fp16 atomics")
+		.def_property_readonly("distributed", &Testbed::distributed)
 		// ngp_tuning (include/ngp_hip.h) as a dict; unknown keys are an error, missing keys keep their value
 		.def("get_tuning",
 		     [](const Testbed& t) {
@@ -616,8 +620,10 @@ PYBIND11_MODULE(pyngp, m) {
 			     auto hold = std::make_shared<py::function>(std::move(fn));
 			     t.init_distributed_host(rank, world, [hold](void* p, size_t n, int dtype, int op) {
 				     py::gil_scoped_acquire gil;
-				     py::array a = dtype == 0 ? py::array(py::dtype("float32"), {(py::ssize_t)n}, {(py::ssize_t)4}, p, py::none())
-				                              : py::array(py::dtype("float16"), {(py::ssize_t)n}, {(py::ssize_t)2}, p, py::none());
+				     // dtype 0 f32, 1 f16, 2 i32 (per-rank totals), 3 i64 (deterministic fixed-point gradients)
+				     static const char* names[4] = {"float32", "float16", "int32", "int64"};
+				     static const py::ssize_t sizes[4] = {4, 2, 4, 8};
+				     py::array a(py::dtype(names[dtype]), {(py::ssize_t)n}, {sizes[dtype]}, p, py::none());
 				     (*hold)(a, op ? "max" : "sum");
 			     });
 		     },

@@ -970,7 +970,7 @@ void Testbed::update_density_grid(uint32_t n_uniform, uint32_t n_nonuniform) {
 	g.use_inference_params = 0;
 	g.rank = (uint32_t)m_rank;
 	g.world_size = (uint32_t)m_world;
-	if (m_world > 1) {
+	if (distributed()) {
 		ck(ngp_density_grid_evaluate(m_model, &g, m_stream));
 		float *grid, *tmp;
 		ck(ngp_density_grid_buffers(m_model, &grid, nullptr, &tmp, nullptr));
@@ -996,6 +996,11 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	}
 	upload_dataset();
 	NerfCounters& ctr = nerf.training.counters_rgb;
+	// data parallelism: the ranks train one global batch of world x batch samples over
+	// rays_per_batch global rays, each rank its contiguous slice -- the same sample set, caps, rollover
+	// and host state as one process training with batch world x batch (ngp_train_args.world_size)
+	const uint32_t W = (uint32_t)m_world;
+	batch *= W;
 	const uint32_t max_samples = batch * 16;
 	uint32_t max_inference;
 	if (ctr.measured_batch_size_before_compaction == 0) ctr.measured_batch_size_before_compaction = max_inference = max_samples;
@@ -1078,15 +1083,23 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.cam_pos_gradient = tr.optimize_extrinsics ? m_cam_grad : nullptr;
 	a.cam_rot_gradient = tr.optimize_extrinsics ? m_cam_grad + 3 * n_img : nullptr;
 	a.n_images = (uint32_t)nerf.training.n_images_for_training;
-	a.n_rays = ctr.rays_per_batch;
+	if (ctr.rays_per_batch % W) ctr.rays_per_batch = next_multiple_host(ctr.rays_per_batch, W);
+	a.n_rays = ctr.rays_per_batch / W;
 	a.n_rays_total = ctr.n_rays_total;
 	a.target_batch_size = batch;
 	a.max_samples = max_inference;
 	a.training_step = training_step;
 	a.rng_state = m_rng_state;
 	a.rng_inc = m_rng_inc;
-	a.ray_index_offset = (uint32_t)m_rank * ctr.rays_per_batch;
-	a.n_rays_global = ctr.rays_per_batch * (uint32_t)m_world;
+	a.ray_index_offset = (uint32_t)m_rank * a.n_rays;
+	a.n_rays_global = ctr.rays_per_batch;
+	if (distributed()) {
+		a.rank = (uint32_t)m_rank;
+		a.world_size = W;
+		a.allreduce_i32 = &Testbed::dp_allreduce_i32;
+		a.allreduce_user = this;
+	}
+	a.deterministic = deterministic ? 1 : 0;
 	for (int k = 0; k < 3; ++k) { a.aabb_min[k] = aabb_min[k]; a.aabb_max[k] = aabb_max[k]; }
 	a.cone_angle_constant = nerf.cone_angle_constant;
 	a.max_cascade = nerf.max_cascade;
@@ -1099,7 +1112,7 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	a.near_distance = nerf.training.near_distance;
 	a.optimize_mlp = train_network;
 	a.optimize_encoding = train_encoding;
-	a.defer_optimizer = m_world > 1 ? 1 : 0;
+	a.defer_optimizer = distributed() ? 1 : 0;
 	a.full_forward = train_full_forward ? 1 : 0;
 	a.depth_supervision_lambda = tr.depth_supervision_lambda;
 	a.depth_loss_type = (int32_t)tr.depth_loss_type;
@@ -1142,22 +1155,44 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	}
 	ctr.n_rays_total += ctr.rays_per_batch;
 	tr.n_rays_since_error_map_update += ctr.rays_per_batch;
-	ck(ngp_train_step(m_model, &a, m_stream));
-	if (m_world > 1) {
-		// MLP gradients (fp32) and hash-grid gradients (fp16) are summed over ranks
-		if (m_comm) {
-			ck(ngp_allreduce_grads(m_model, m_comm, m_stream));
-		} else {
-			void *g = nullptr, *g16 = nullptr;
-			size_t bytes = 0, bytes16 = 0;
-			ngp_model_info info{};
-			ck(ngp_model_get_info(m_model, &info));
-			ck(ngp_model_buffer(m_model, NGP_GRADS_FP32, &g, &bytes));
-			ck(ngp_model_buffer(m_model, NGP_GRADS_GRID_FP16, &g16, &bytes16));
-			allreduce_dev(g, info.n_mlp_params, 0, false);
-			allreduce_dev(g16, bytes16 / 2, 1, false);
+	// one step: sample, forward, loss, backward; data parallel: the gradient all-reduce before the
+	// (identical) optimizer step on every rank.  The chunked forward's violation word gates the
+	// optimizer on the device (ngp_optimizer_step); every rank sees the max over the ranks.
+	ngp_train_stats st{};
+	for (int attempt = 0;; ++attempt) {
+		ck(ngp_train_step(m_model, &a, m_stream));
+		if (distributed()) {
+			if (m_comm) {
+				ck(ngp_allreduce_grads(m_model, m_comm, m_stream));
+			} else {
+				void *g = nullptr, *gg = nullptr;
+				size_t bytes = 0, gbytes = 0;
+				ngp_model_info info{};
+				ck(ngp_model_get_info(m_model, &info));
+				ck(ngp_model_buffer(m_model, NGP_GRADS_FP32, &g, &bytes));
+				ck(ngp_model_buffer(m_model, deterministic ? NGP_GRADS_GRID_FIXED64 : NGP_GRADS_GRID_FP16, &gg, &gbytes));
+				allreduce_dev(g, info.n_mlp_params, 0, false);
+				allreduce_dev(gg, info.n_grid_params, deterministic ? 3 : 1, false);
+			}
+			if (!a.full_forward) {
+				void* viol = nullptr;
+				ck(ngp_train_scratch(m_model, NGP_SCRATCH_VIOLATIONS, &viol, nullptr));
+				if (viol) allreduce_dev(viol, 1, 2, true);
+			}
+			ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 		}
-		ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
+		// NerfCounters::update_after_training (src/testbed_nerf.cu:2422-2446)
+		ck(ngp_train_read_stats(m_model, &st, m_stream));
+		if (!st.forward_early_stop_violations || a.full_forward) break;
+		// the chunked forward stopped a ray before a sample its loss needed: the step's update was
+		// skipped on the device; drop its gradients and run the step again with the full forward (its
+		// error-map / camera-gradient deposits of the first attempt stay -- such steps have not been seen)
+		forward_early_stop_violations += st.forward_early_stop_violations;
+		std::fprintf(stderr, "Nerf training: the chunked forward missed samples of %u rays; re-running the step with the full "
+		             "forward and keeping it from now on.\n", st.forward_early_stop_violations);
+		train_full_forward = true;
+		ck(ngp_train_discard(m_model, m_stream));
+		a.full_forward = 1;
 	}
 	++training_step;
 	// CDFs from the error map, every n_steps_between_error_map_updates (x1.5 each time)
@@ -1179,26 +1214,22 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	r.advance();
 	m_rng_state = r.state;
 
-	// NerfCounters::update_after_training (src/testbed_nerf.cu:2422-2446)
-	ngp_train_stats st{};
-	ck(ngp_train_read_stats(m_model, &st, m_stream));
-	if (m_world > 1) {
-		float v[3] = {(float)st.measured_batch_size, (float)st.measured_batch_size_before_compaction, st.loss};
-		float* dv = (float*)m_red_buf;
-		hk(hipMemcpyAsync(dv, v, sizeof(v), hipMemcpyHostToDevice, (hipStream_t)m_stream), "stats h2d");
-		allreduce_f32(dv, 3, false);
-		hk(hipMemcpyAsync(v, dv, sizeof(v), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "stats d2h");
+	// the global counters: sums of the ranks' sample / compacted totals (exact int32) and losses
+	if (distributed()) {
+		int32_t cnt[2] = {(int32_t)st.measured_batch_size, (int32_t)st.measured_batch_size_before_compaction};
+		float lv = st.loss;
+		int32_t* dc = (int32_t*)m_red_buf;
+		float* dl = (float*)m_red_buf + 4;
+		hk(hipMemcpyAsync(dc, cnt, sizeof(cnt), hipMemcpyHostToDevice, (hipStream_t)m_stream), "stats h2d");
+		hk(hipMemcpyAsync(dl, &lv, sizeof(lv), hipMemcpyHostToDevice, (hipStream_t)m_stream), "stats h2d");
+		allreduce_dev(dc, 2, 2, false);
+		allreduce_dev(dl, 1, 0, false);
+		hk(hipMemcpyAsync(cnt, dc, sizeof(cnt), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "stats d2h");
+		hk(hipMemcpyAsync(&lv, dl, sizeof(lv), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "stats d2h");
 		sync();
-		st.measured_batch_size = (uint32_t)(v[0] / (float)m_world);
-		st.measured_batch_size_before_compaction = (uint32_t)(v[1] / (float)m_world);
-		st.loss = v[2];
-	}
-	if (st.forward_early_stop_violations) {
-		forward_early_stop_violations += st.forward_early_stop_violations;
-		if (!train_full_forward)
-			std::fprintf(stderr, "Nerf training: the chunked forward missed samples of %u rays; switching to the full forward.\n",
-			             st.forward_early_stop_violations);
-		train_full_forward = true;
+		st.measured_batch_size = (uint32_t)cnt[0];
+		st.measured_batch_size_before_compaction = (uint32_t)cnt[1];
+		st.loss = lv;
 	}
 	m_last_stats = st;
 	ctr.measured_batch_size = st.measured_batch_size;
@@ -1212,7 +1243,10 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	}
 	if (get_loss_scalar) loss = st.loss * (float)st.measured_batch_size / (float)batch;
 	uint32_t rpb = (uint32_t)((float)ctr.rays_per_batch * (float)batch / (float)st.measured_batch_size);
-	ctr.rays_per_batch = std::min(next_multiple_host(rpb, BATCH_SIZE_GRANULARITY), 1u << 18);
+	// data parallel: rays_per_batch stays a multiple of the world size (every rank gets an equal slice);
+	// 256-granular as the reference when the world size divides 256 (1, 2, 4, 8)
+	const uint32_t gran = BATCH_SIZE_GRANULARITY % W == 0 ? BATCH_SIZE_GRANULARITY : BATCH_SIZE_GRANULARITY * W;
+	ctr.rays_per_batch = std::min(next_multiple_host(rpb, gran), next_multiple_host((1u << 18) * W, gran));
 }
 
 // src/testbed_nerf.cu:2523-2575: construct_cdf_2d/1d on the device, the image CDF on the host
@@ -1223,7 +1257,7 @@ void Testbed::update_error_map_cdf() {
 	if (!m_err || n_images == 0 || res[0] <= 0 || res[1] <= 0) return;
 	const size_t n = (size_t)res[0] * res[1] * n_images;
 	// data parallel: every rank deposited the errors of its own rays
-	if (m_world > 1) allreduce_f32(m_err, n, false);
+	if (distributed()) allreduce_f32(m_err, n, false);
 	tr.error_map.cdf_resolution = res;
 	if (n > m_cdf_cap) {
 		if (m_cdf_x) (void)hipFree(m_cdf_x);
@@ -1276,7 +1310,7 @@ void Testbed::update_cam_exposure() {
 	const uint32_t n = (uint32_t)tr.n_images_for_training;
 	const size_t n_img = tr.dataset.n_images;
 	std::vector<float> g(n_img * 3);
-	if (m_world > 1) allreduce_f32(m_exp_grad, n_img * 3, false);
+	if (distributed()) allreduce_f32(m_exp_grad, n_img * 3, false);
 	hk(hipMemcpyAsync(g.data(), m_exp_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "exposure gradient d2h");
 	sync();
 	const float per_camera_loss_scale = (float)n / 128.0f / (float)tr.n_steps_between_cam_updates;
@@ -1311,7 +1345,7 @@ void Testbed::update_cam_exposure() {
 void Testbed::update_distortion_map() {
 	DistortionMap& d = m_distortion;
 	const size_t n = d.params.size();
-	if (m_world > 1) allreduce_f32(m_dist_grad, 2 * n, false);
+	if (distributed()) allreduce_f32(m_dist_grad, 2 * n, false);
 	std::vector<float> g(2 * n);
 	hk(hipMemcpyAsync(g.data(), m_dist_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "distortion gradient d2h");
 	sync();
@@ -1339,7 +1373,7 @@ void Testbed::update_cam_extrinsics() {
 	NerfTraining& tr = nerf.training;
 	const uint32_t n = (uint32_t)tr.n_images_for_training;
 	const size_t n_img = tr.dataset.n_images;
-	if (m_world > 1) allreduce_f32(m_cam_grad, n_img * 6, false);
+	if (distributed()) allreduce_f32(m_cam_grad, n_img * 6, false);
 	std::vector<float> g(n_img * 6);
 	hk(hipMemcpyAsync(g.data(), m_cam_grad, g.size() * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "camera gradient d2h");
 	sync();
@@ -1943,7 +1977,8 @@ std::string Testbed::nccl_unique_id() {
 }
 
 void Testbed::init_distributed(int rank, int world_size, const std::string& uid) {
-	if (world_size <= 1) return;
+	if (world_size < 1 || rank < 0 || rank >= world_size) throw std::runtime_error("init_distributed: bad rank / world_size");
+	if (m_comm || m_host_allreduce) throw std::runtime_error("init_distributed: already distributed");
 	if (uid.size() != sizeof(ncclUniqueId::internal)) throw std::runtime_error("init_distributed: bad ncclUniqueId");
 	ncclUniqueId id;
 	std::memcpy(id.internal, uid.data(), uid.size());
@@ -1964,29 +1999,13 @@ static std::vector<std::pair<uint32_t, uint32_t>> owned_row_runs(uint32_t H, uin
 
 std::vector<float> Testbed::render_distributed(int width, int height, int spp, bool linear, bool copy_to_host) {
 	const uint32_t R = 8;
-	if (m_world <= 1) return render(width, height, spp, linear, 0, 1, R, copy_to_host);
+	if (!distributed()) return render(width, height, spp, linear, 0, 1, R, copy_to_host);
 	render(width, height, spp, linear, (uint32_t)m_rank, (uint32_t)m_world, R, false);
 	const size_t row_bytes = (size_t)width * 4 * sizeof(float);
 	hipStream_t s = (hipStream_t)m_stream;
-	// pack this rank's rows (contiguous in shard order), then rank 0 receives every rank's pack
 	std::vector<size_t> pack_rows(m_world);
 	for (int r = 0; r < m_world; ++r)
 		for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)r, (uint32_t)m_world, R)) pack_rows[r] += run.second;
-	const size_t cap = *std::max_element(pack_rows.begin(), pack_rows.end()) * row_bytes * (m_rank == 0 ? (size_t)m_world : 1);
-	if (cap > m_pack_cap) {
-		if (m_pack) (void)hipFree(m_pack);
-		hk(hipMalloc((void**)&m_pack, cap), "hipMalloc pack");
-		m_pack_cap = cap;
-	}
-	const size_t slot = *std::max_element(pack_rows.begin(), pack_rows.end()) * row_bytes;
-	if (m_rank != 0) {
-		size_t off = 0;
-		for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)m_rank, (uint32_t)m_world, R)) {
-			hk(hipMemcpyAsync((char*)m_pack + off, (const char*)m_out + run.first * row_bytes, run.second * row_bytes,
-			                  hipMemcpyDeviceToDevice, s), "pack rows");
-			off += run.second * row_bytes;
-		}
-	}
 	if (!m_comm) {
 		// host-staged test backend: owned rows over a zero frame, summed over the ranks
 		std::vector<float> full((size_t)width * height * 4, 0.0f);
@@ -2001,20 +2020,36 @@ std::vector<float> Testbed::render_distributed(int width, int height, int spp, b
 		if (!copy_to_host) full.clear();
 		return full;
 	}
-	nk(ncclGroupStart(), "ncclGroupStart");
-	if (m_rank == 0) {
-		for (int r = 1; r < m_world; ++r)
-			nk(ncclRecv((char*)m_pack + r * slot, pack_rows[r] * row_bytes, ncclChar, r, (ncclComm_t)m_comm, s), "ncclRecv rows");
-	} else {
-		nk(ncclSend(m_pack, pack_rows[m_rank] * row_bytes, ncclChar, 0, (ncclComm_t)m_comm, s), "ncclSend rows");
+	// every rank packs its rows (contiguous in shard order) into [0, slot) and sends them to rank 0,
+	// which receives every rank's pack -- its own too, over RCCL, so one code path serves any world
+	// size -- into slot r + 1 and unpacks them into its frame
+	const size_t slot = *std::max_element(pack_rows.begin(), pack_rows.end()) * row_bytes;
+	const size_t cap = slot * (m_rank == 0 ? (size_t)m_world + 1 : 1);
+	if (cap > m_pack_cap) {
+		if (m_pack) (void)hipFree(m_pack);
+		hk(hipMalloc((void**)&m_pack, cap), "hipMalloc pack");
+		m_pack_cap = cap;
 	}
+	{
+		size_t off = 0;
+		for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)m_rank, (uint32_t)m_world, R)) {
+			hk(hipMemcpyAsync((char*)m_pack + off, (const char*)m_out + run.first * row_bytes, run.second * row_bytes,
+			                  hipMemcpyDeviceToDevice, s), "pack rows");
+			off += run.second * row_bytes;
+		}
+	}
+	nk(ncclGroupStart(), "ncclGroupStart");
+	if (m_rank == 0)
+		for (int r = 0; r < m_world; ++r)
+			nk(ncclRecv((char*)m_pack + (r + 1) * slot, pack_rows[r] * row_bytes, ncclChar, r, (ncclComm_t)m_comm, s), "ncclRecv rows");
+	nk(ncclSend(m_pack, pack_rows[m_rank] * row_bytes, ncclChar, 0, (ncclComm_t)m_comm, s), "ncclSend rows");
 	nk(ncclGroupEnd(), "ncclGroupEnd");
 	std::vector<float> out;
 	if (m_rank == 0) {
-		for (int r = 1; r < m_world; ++r) {
+		for (int r = 0; r < m_world; ++r) {
 			size_t off = 0;
 			for (const auto& run : owned_row_runs((uint32_t)height, (uint32_t)r, (uint32_t)m_world, R)) {
-				hk(hipMemcpyAsync((char*)m_out + run.first * row_bytes, (const char*)m_pack + r * slot + off,
+				hk(hipMemcpyAsync((char*)m_out + run.first * row_bytes, (const char*)m_pack + (r + 1) * slot + off,
 				                  run.second * row_bytes, hipMemcpyDeviceToDevice, s), "unpack rows");
 				off += run.second * row_bytes;
 			}
@@ -2030,16 +2065,30 @@ std::vector<float> Testbed::render_distributed(int width, int height, int spp, b
 
 void Testbed::allreduce_f32(float* dev, size_t n, bool max_op) { allreduce_dev(dev, n, 0, max_op); }
 
+// ngp_train_args.allreduce_i32: the step's per-rank totals, on the Testbed's collective backend
+ngp_status Testbed::dp_allreduce_i32(void* user, int32_t* dev, uint32_t n, ngp_stream) {
+	try {
+		static_cast<Testbed*>(user)->allreduce_dev(dev, n, 2, false);
+		return NGP_OK;
+	} catch (const std::exception& e) {
+		std::fprintf(stderr, "data-parallel all-reduce failed: %s\n", e.what());
+		return NGP_ERR_UNSUPPORTED;
+	}
+}
+
+// dtype: 0 f32, 1 f16, 2 i32, 3 i64 (deterministic fixed-point gradients)
 void Testbed::allreduce_dev(void* dev, size_t n, int dtype, bool max_op) {
-	if (m_world <= 1 || n == 0) return;
+	if (!distributed() || n == 0) return;
+	static const size_t elem[4] = {4, 2, 4, 8};
+	if (dtype < 0 || dtype > 3) throw std::runtime_error("allreduce_dev: unknown dtype");
 	if (m_comm) {
-		nk(ncclAllReduce(dev, dev, n, dtype == 0 ? ncclFloat32 : ncclFloat16, max_op ? ncclMax : ncclSum, (ncclComm_t)m_comm,
-		                 (hipStream_t)m_stream),
+		static const ncclDataType_t types[4] = {ncclFloat32, ncclFloat16, ncclInt32, ncclInt64};
+		nk(ncclAllReduce(dev, dev, n, types[dtype], max_op ? ncclMax : ncclSum, (ncclComm_t)m_comm, (hipStream_t)m_stream),
 		   "ncclAllReduce");
 		return;
 	}
 	if (!m_host_allreduce) throw std::runtime_error("distributed Testbed without a collective backend");
-	const size_t bytes = n * (dtype == 0 ? 4 : 2);
+	const size_t bytes = n * elem[dtype];
 	std::vector<uint8_t> h(bytes);
 	hk(hipMemcpyAsync(h.data(), dev, bytes, hipMemcpyDeviceToHost, (hipStream_t)m_stream), "allreduce d2h");
 	sync();
@@ -2049,7 +2098,8 @@ void Testbed::allreduce_dev(void* dev, size_t n, int dtype, bool max_op) {
 }
 
 void Testbed::init_distributed_host(int rank, int world_size, HostAllReduce fn) {
-	if (world_size <= 1) return;
+	if (world_size < 1 || rank < 0 || rank >= world_size) throw std::runtime_error("init_distributed_host: bad rank / world_size");
+	if (m_comm || m_host_allreduce) throw std::runtime_error("init_distributed_host: already distributed");
 	if (!fn) throw std::runtime_error("init_distributed_host: no all-reduce function");
 	m_host_allreduce = std::move(fn);
 	m_rank = rank;

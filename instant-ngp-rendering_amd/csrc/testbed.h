@@ -217,6 +217,10 @@ public:
 	// Every rank calls it; rank 0 returns the frame (copy_to_host) and holds it in render_frame_buffer().
 	std::vector<float> render_distributed(int width, int height, int spp, bool linear, bool copy_to_host = true);
 	int rank() const { return m_rank; }
+	// a collective backend is set (RCCL or the host-staged one), world size 1 included
+	bool distributed() const { return m_comm != nullptr || (bool)m_host_allreduce; }
+	// deterministic hash-grid gradients (ngp_train_args.deterministic): bit-reproducible steps
+	bool deterministic = false;
 	int world_size() const { return m_world; }
 
 	ngp_model* model() const { return m_model; }
@@ -280,6 +284,7 @@ private:
 	void ensure_render_buffers(size_t n_pixels);
 	void allreduce_f32(float* dev, size_t n, bool max_op);
 	void allreduce_dev(void* dev, size_t n, int dtype, bool max_op);  // RCCL or the host-staged backend
+	static ngp_status dp_allreduce_i32(void* user, int32_t* dev, uint32_t n, ngp_stream stream);
 	HostAllReduce m_host_allreduce;
 
 	void update_error_map_cdf();

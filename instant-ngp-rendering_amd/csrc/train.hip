@@ -132,6 +132,7 @@ struct SamplerArgs {
 	uint32_t n_rays_global;
 	uint32_t ray_offset;
 	uint32_t max_samples;
+	const uint32_t* max_samples_dev;  // data parallel: this rank's share of the global cap (device); null: max_samples
 	pcg32 rng;
 	aabb3 aabb;
 	Stepping st;
@@ -320,7 +321,8 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	const uint32_t lane = threadIdx.x & 63u;
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.counts[i], base = a.bases[i];
-	if (n == 0 || base + n > a.max_samples) {
+	const uint32_t cap = a.max_samples_dev ? *a.max_samples_dev : a.max_samples;
+	if (n == 0 || base + n > cap) {
 		if (lane == 0) {
 			a.numsteps[2 * i + 0] = 0;
 			a.numsteps[2 * i + 1] = 0;
@@ -547,6 +549,7 @@ struct LossArgs {
 	int rgb_act, density_act;
 	float near_distance;
 	uint32_t max_compacted;
+	const uint32_t* max_compacted_dev;  // data parallel: this rank's share of the global cap (device); null: max_compacted
 	uint32_t target_batch;
 	const uint32_t* numsteps;
 	float* ray_state;        // [R][8]: o, d (sampler), u, v of the pixel (k_loss_composite)
@@ -799,7 +802,8 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 	const uint32_t lane = threadIdx.x & 63u;
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.ccounts[i], cbase = a.cbases[i];
-	const uint32_t cn = n == 0 ? 0 : min(a.max_compacted - min(a.max_compacted, cbase), n);
+	const uint32_t mc = a.max_compacted_dev ? *a.max_compacted_dev : a.max_compacted;
+	const uint32_t cn = n == 0 ? 0 : min(mc - min(mc, cbase), n);
 	if (lane == 0) {
 		a.compacted[2 * i + 0] = cn;
 		a.compacted[2 * i + 1] = cbase;
@@ -1068,17 +1072,51 @@ __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __rest
 }
 
 // Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
-// c < B is repeated floor((B-1-j)/c) more times, each copy scaled by c/B.
-__global__ void k_rollover_weight(const uint32_t* __restrict__ total_ptr, uint32_t target, float* __restrict__ w) {
+// c < B is repeated floor((B-1-j)/c) more times, each copy scaled by c/B.  Data parallel (dp =
+// DpCaps of the compaction): the rank's sample j is global sample base + j of the global batch.
+__global__ void k_rollover_weight(const uint32_t* __restrict__ total_ptr, uint32_t target, const uint32_t* __restrict__ dp,
+                                  float* __restrict__ w) {
 	const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-	const uint32_t c = min(*total_ptr, target);
-	if (j >= c) return;
-	const uint32_t copies = (target - 1 - j) / c;
+	uint32_t c, g, n;
+	if (dp) {
+		c = dp[1];
+		g = dp[0] + j;
+		n = min(*total_ptr, dp[2]);
+	} else {
+		c = min(*total_ptr, target);
+		g = j;
+		n = c;
+	}
+	if (j >= n) return;
+	const uint32_t copies = (target - 1 - g) / c;
 	w[j] = 1.0f + (float)copies * ((float)c / (float)target);
 }
 
-__global__ void k_clamp_count(const uint32_t* __restrict__ in, uint32_t cap, uint32_t* __restrict__ out) {
-	if (threadIdx.x == 0 && blockIdx.x == 0) *out = min(*in, cap);
+__global__ void k_clamp_count(const uint32_t* __restrict__ in, uint32_t cap, const uint32_t* __restrict__ cap_dev,
+                              uint32_t* __restrict__ out) {
+	if (threadIdx.x == 0 && blockIdx.x == 0) *out = min(*in, cap_dev ? *cap_dev : cap);
+}
+
+// Data parallelism (ngp_train_args.world_size > 1): each rank writes its total into its slot of
+// [world] words (the others zero), the caller's all-reduce sums them, and every rank derives the
+// same global prefix -- so caps and rollover follow the global ray order of one process.
+__global__ void k_dp_publish(const uint32_t* __restrict__ total, int32_t* __restrict__ slots, uint32_t world, uint32_t rank) {
+	for (uint32_t q = threadIdx.x; q < world; q += blockDim.x) slots[q] = q == rank ? (int32_t)*total : 0;
+}
+// DpCaps: [0] this rank's first global index, [1] min(global total, cap), [2] this rank's share of
+// the cap (cap - base, 0 once the ranks before it filled it)
+__global__ void k_dp_caps(const int32_t* __restrict__ slots, uint32_t world, uint32_t rank, uint32_t cap,
+                          uint32_t* __restrict__ out) {
+	if (threadIdx.x || blockIdx.x) return;
+	uint64_t base = 0, total = 0;
+	for (uint32_t q = 0; q < world; ++q) {
+		const uint64_t v = (uint32_t)slots[q];
+		if (q < rank) base += v;
+		total += v;
+	}
+	out[0] = (uint32_t)min<uint64_t>(base, 0xffffffffull);
+	out[1] = (uint32_t)min<uint64_t>(total, cap);
+	out[2] = base >= cap ? 0u : (uint32_t)(cap - base);
 }
 
 // Sum of per-ray losses (deterministic two-level reduction).
@@ -1107,6 +1145,8 @@ struct OptArgs {
 	__half* w16;
 	float* grad;      // MLP gradients (fp32), [0, n_mlp)
 	__half* grad16;   // hash-grid gradients (fp16), [n_mlp, n)
+	long long* grad64;  // deterministic steps: hash-grid gradients in 2^-40 fixed point (replaces grad16)
+	const uint32_t* skip;  // chunked forward violations of the step: non-zero = no update at all
 	float* m;
 	float* v;
 	uint32_t* steps;
@@ -1117,8 +1157,12 @@ struct OptArgs {
 __global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
 	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
 	if (i >= a.n) return;
+	// a step whose chunked forward missed samples is dropped whole; the caller re-runs it
+	// (ngp_train_discard + full_forward) -- every thread reads the same word
+	if (a.skip && *a.skip) return;
 	const bool is_mlp = i < a.n_mlp;
-	const float graw = is_mlp ? a.grad[i] : __half2float(a.grad16[i - a.n_mlp]);
+	const float graw = is_mlp ? a.grad[i]
+	                          : (a.grad64 ? (float)a.grad64[i - a.n_mlp] * GRAD_FIXED_INV : __half2float(a.grad16[i - a.n_mlp]));
 	float w = a.w32[i];
 	bool update = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
 	if (update) {
@@ -1134,6 +1178,7 @@ __global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
 	}
 	if (graw != 0.0f) {  // GradientMode::Overwrite for the next step
 		if (is_mlp) a.grad[i] = 0.0f;
+		else if (a.grad64) a.grad64[i - a.n_mlp] = 0;
 		else a.grad16[i - a.n_mlp] = __float2half(0.0f);
 	}
 	const float e = (a.ema32[i] * a.ema_decay * a.ema_debias_old + w * (1.0f - a.ema_decay)) / a.ema_debias_new;
@@ -1173,6 +1218,10 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.w16 = m->params16.ptr;
 	a.grad = m->grads.ptr;
 	a.grad16 = m->grid_grads16.ptr;
+	a.grad64 = m->ts.fixed ? m->grid_grads64.ptr : nullptr;
+	// a chunked training step's violation word gates its update (ngp_train_discard re-runs it)
+	a.skip = m->ts.chunked && m->ts.counters.ptr ? m->ts.counters.ptr + 9 : nullptr;
+	if (a.skip) m->ts.gated_optimizer_ran = true;
 	a.m = m->adam_m.ptr;
 	a.v = m->adam_v.ptr;
 	a.steps = m->adam_steps.ptr;
@@ -1261,6 +1310,33 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.last_n_rays = R;
 	ts.last_target = B;
 	ts.last_max_samples = MS;
+	ts.gated_optimizer_ran = false;
+
+	// data parallelism: caps and rollover over the global ray order (ngp_train_args.world_size)
+	const uint32_t world = t->world_size > 1 && t->allreduce_i32 ? t->world_size : 1u;
+	if (world > 1 && t->rank >= world) throw std::invalid_argument("rank must be < world_size");
+	uint32_t* dp_samples = nullptr;  // DpCaps of the sampler / the compaction (device)
+	uint32_t* dp_compact = nullptr;
+	auto dp_exchange = [&](const uint32_t* total, uint32_t* caps, int32_t* slots, uint32_t cap) {
+		k_dp_publish<<<1, 64, 0, s>>>(total, slots, world, t->rank);
+		NGP_HIP_CHECK(hipGetLastError());
+		if (t->allreduce_i32(t->allreduce_user, slots, world, s) != NGP_OK)
+			throw std::runtime_error("data-parallel training: the all-reduce of the per-rank totals failed");
+		k_dp_caps<<<1, 64, 0, s>>>(slots, world, t->rank, cap, caps);
+		NGP_HIP_CHECK(hipGetLastError());
+	};
+	if (world > 1) {
+		ts.dp.reserve(8 + 2 * (size_t)world);
+		dp_samples = ts.dp.ptr;
+		dp_compact = ts.dp.ptr + 4;
+	}
+	// deterministic hash-grid gradients: the fixed-point buffer, zeroed once (the optimizer clears
+	// what it consumed, as for the fp16 buffer)
+	ts.fixed = t->deterministic != 0;
+	if (ts.fixed && !m->grid_grads64.ptr) {
+		m->grid_grads64.reserve(m->n_grid_params);
+		NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads64.ptr, 0, m->n_grid_params * sizeof(long long), s));
+	}
 
 	NGP_HIP_CHECK(hipMemsetAsync(ts.counters.ptr, 0, 16 * sizeof(uint32_t), s));
 
@@ -1271,6 +1347,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.n_rays_global = t->n_rays_global ? t->n_rays_global : R;
 	sa.ray_offset = t->ray_index_offset;
 	sa.max_samples = MS;
+	sa.max_samples_dev = dp_samples ? dp_samples + 2 : nullptr;
 	sa.rng.state = t->rng_state;
 	sa.rng.inc = t->rng_inc;
 	sa.aabb.min = mk3(t->aabb_min[0], t->aabb_min[1], t->aabb_min[2]);
@@ -1297,10 +1374,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	if (general) k_sample_count<true><<<div_up(R, 4), 256, 0, s>>>(sa);
 	else k_sample_count<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
+	// the global sample cap (src/testbed_nerf.cu:779-781 drops rays past max_samples) over all ranks
+	if (world > 1) dp_exchange(ts.counters.ptr + 0, dp_samples, reinterpret_cast<int32_t*>(ts.dp.ptr + 8), MS);
 	if (general) k_sample_write<true><<<div_up(R, 4), 256, 0, s>>>(sa);
 	else k_sample_write<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	NGP_HIP_CHECK(hipGetLastError());
-	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, ts.counters.ptr + 4);
+	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, sa.max_samples_dev, ts.counters.ptr + 4);
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 
 	// network inference with the training params (NerfNetwork::inference_mixed_precision): over
@@ -1454,6 +1533,11 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
 	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
+	// the global compaction cap (src/testbed_nerf.cu:997-1003) over all ranks
+	if (world > 1) {
+		dp_exchange(ts.counters.ptr + 1, dp_compact, reinterpret_cast<int32_t*>(ts.dp.ptr + 8 + world), B);
+		la.max_compacted_dev = dp_compact + 2;
+	}
 	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
 	NGP_HIP_CHECK(hipGetLastError());
 	const bool train_debug = (m->tuning.debug & 2u) != 0;
@@ -1487,14 +1571,14 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	}
 
 	// compacted batch size c = min(total, B); rollover multiplicity
-	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, ts.counters.ptr + 5);
+	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, la.max_compacted_dev, ts.counters.ptr + 5);
 	switch (F) {
 		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
 		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
 		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
 		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
 	}
-	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, ts.cweight.ptr);
+	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, dp_compact, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
 	tm.end(NGP_TIMER_TRAIN_LOSS, s, R);
 
@@ -1508,8 +1592,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
 	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
+	// data parallel: launched for about this rank's share of the global batch (blocks loop past it)
+	const uint32_t bwd_chunks = world > 1 ? div_up(B / world + B / (4 * world), 128u) + 16 : 0u;
 	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->grid_grads16.ptr, s,
-	                    ts.counters.ptr + 5);
+	                    ts.counters.ptr + 5, ts.fixed ? m->grid_grads64.ptr : nullptr, bwd_chunks);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	if (cam) {
 		// input gradients of the compacted samples (Trainer::training_step with dL_dinput), then

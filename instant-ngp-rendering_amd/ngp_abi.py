@@ -66,6 +66,8 @@ class TrainArgs(C.Structure):
         ("sharpness_grid_clear", C.c_int32),
         ("distortion_map", C.c_void_p), ("distortion_res", C.c_uint32 * 2), ("distortion_gradient", C.c_void_p),
         ("distortion_gradient_weight", C.c_void_p),
+        ("rank", C.c_uint32), ("world_size", C.c_uint32), ("allreduce_i32", C.c_void_p), ("allreduce_user", C.c_void_p),
+        ("deterministic", C.c_int32),
     ]
 
 
@@ -113,9 +115,10 @@ class Tuning(C.Structure):
 
 
 # enums (include/ngp_hip.h)
-PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M, ADAM_V, GRADS_GRID_FP16 = range(8)
+PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M, ADAM_V, GRADS_GRID_FP16, \
+    GRADS_GRID_FIXED64 = range(9)
 SCRATCH_RAY_NUMSTEPS, SCRATCH_COORDS, SCRATCH_MLP_OUT, SCRATCH_RAY_COMPACTED, SCRATCH_DLOSS, SCRATCH_LOSS, \
-    SCRATCH_COMPACT_COORDS, SCRATCH_RAY_EVALUATED = range(8)
+    SCRATCH_COMPACT_COORDS, SCRATCH_RAY_EVALUATED, SCRATCH_VIOLATIONS = range(9)
 
 TIMERS = ["train_sampler", "train_encode", "train_mlp_infer", "train_loss", "train_mlp_bwd", "train_encode_bwd",
           "optimizer", "grid_update", "render_encode", "render_mlp", "render_march"]
@@ -145,6 +148,7 @@ EXPORTS = {
     "ngp_train_read_stats": (C.c_int, [C.c_void_p, C.POINTER(TrainStats), C.c_void_p]),
     "ngp_allreduce_grads": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngp_train_scratch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
+    "ngp_train_discard": (C.c_int, [C.c_void_p, C.c_void_p]),
     "ngp_density_grid_update": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),
     "ngp_density_grid_evaluate": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),
     "ngp_density_grid_finish": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),

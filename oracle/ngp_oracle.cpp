@@ -1094,8 +1094,32 @@ static float ref_advance_to_next_voxel(float t, float cone, V3 pos, V3 dir, V3 i
 	return ref_from_stepping_space(ts + std::ceil(std::fmax(tt - ts, 0.5f)), cone);
 }
 
+// Data parallelism (ngp_train_args.world_size): every rank learns all ranks' totals
+// through the caller's all-reduce (sum of [world] slots, its own slot set) and caps its share of
+// the global order: out = {first global index of this rank, min(global total, cap)}; returns the
+// rank's share of the cap.  One process: {0, min(total, cap)}, cap.
+static uint32_t dp_share(const ngp_train_args& a, uint32_t total, uint32_t cap, uint32_t out[2]) {
+	const uint32_t world = a.world_size > 1 && a.allreduce_i32 ? a.world_size : 1u;
+	if (world == 1) {
+		out[0] = 0;
+		out[1] = std::min(total, cap);
+		return cap;
+	}
+	std::vector<int32_t> slots(world, 0);
+	slots[a.rank] = (int32_t)total;
+	if (a.allreduce_i32(a.allreduce_user, slots.data(), world, nullptr) != 0) throw std::runtime_error("all-reduce failed");
+	uint64_t base = 0, sum = 0;
+	for (uint32_t q = 0; q < world; ++q) {
+		if (q < a.rank) base += (uint32_t)slots[q];
+		sum += (uint32_t)slots[q];
+	}
+	out[0] = (uint32_t)base;
+	out[1] = (uint32_t)std::min<uint64_t>(sum, cap);
+	return base >= cap ? 0u : (uint32_t)(cap - base);
+}
+
 static void train_step(Model& M, const ngp_train_args& a) {
-	const uint32_t R = a.n_rays, B = a.target_batch_size, MS = a.max_samples;
+	const uint32_t R = a.n_rays, B = a.target_batch_size;
 	const uint32_t nrg = a.n_rays_global ? a.n_rays_global : R;
 	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
 	const Stepping stp = make_stepping(a.cone_angle_constant);
@@ -1111,9 +1135,14 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		cnt[i] = training_walk(stp, box, M.bits.data(), a.max_cascade, o, d, t, STEPS,
 		                       [](uint32_t, uint32_t, float, float, V3) {});
 	}
-	// prefix-sum slot claim in ray order; drop if base + n > cap (testbed_nerf.cu:800-803)
+	// prefix-sum slot claim in ray order; drop if base + n > cap (testbed_nerf.cu:800-803) -- the cap
+	// of the global order when data parallel (this rank's share)
+	uint32_t total = 0;
+	for (uint32_t i = 0; i < R; ++i) total += cnt[i];
+	uint32_t sdp[2];
+	const uint32_t MS = dp_share(a, total, a.max_samples, sdp);
 	M.ray_numsteps.assign(2 * (size_t)R, 0);
-	M.coords.assign(8 * (size_t)MS, 0.0f);
+	M.coords.assign(8 * (size_t)a.max_samples, 0.0f);
 	uint32_t base = 0;
 	for (uint32_t i = 0; i < R; ++i) {
 		const uint32_t n = cnt[i];
@@ -1139,7 +1168,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	std::vector<float> enc((size_t)M.L * S * M.F), out(4 * (size_t)S);
 	hg_forward(M, M.p16.data(), M.coords.data(), 8, S, enc.data());
 	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data());
-	M.mlp_out.assign(4 * (size_t)MS, 0);
+	M.mlp_out.assign(4 * (size_t)a.max_samples, 0);
 	for (size_t k = 0; k < out.size(); ++k) M.mlp_out[k] = f2h(out[k]);
 
 	// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1119)
@@ -1256,11 +1285,15 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	const float loss_scale = 128.0f / (float)nrg;
 	const float l2r = ract == 3 ? 1e-4f : 0.0f;
 	const float l1d = M.mean < 0.01f ? 1e-4f : 0.0f;
+	uint32_t ctotal = 0;
+	for (uint32_t i = 0; i < R; ++i) ctotal += cc[i];
+	uint32_t cdp[2];
+	const uint32_t Bl = dp_share(a, ctotal, B, cdp);  // the compaction cap of this rank's share
 	uint32_t cbase = 0;
 	for (uint32_t i = 0; i < R; ++i) {
 		const uint32_t c = cc[i], cb = cbase;
 		cbase += c;
-		const uint32_t cn = c == 0 ? 0 : std::min(B - std::min(B, cb), c);
+		const uint32_t cn = c == 0 ? 0 : std::min(Bl - std::min(Bl, cb), c);
 		M.ray_compacted[2 * i] = cn;
 		M.ray_compacted[2 * i + 1] = cb;
 		if (cn == 0) continue;
@@ -1334,9 +1367,10 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	for (float l : M.loss) M.loss_sum += l;
 
 	// Trainer::training_step on the compacted batch; rollover folded into a multiplicity weight
-	const uint32_t C = std::min(cbase, B);
+	// (data parallel: this rank's samples are global samples cdp[0] + j of the global batch of cdp[1])
+	const uint32_t C = std::min(cbase, Bl), CG = cdp[1];
 	std::vector<float> wts(C), dlf(4 * (size_t)C), denc((size_t)M.L * C * M.F, 0.0f), ce((size_t)M.L * C * M.F);
-	for (uint32_t j = 0; j < C; ++j) wts[j] = 1.0f + (float)((B - 1 - j) / C) * ((float)C / (float)B);
+	for (uint32_t j = 0; j < C; ++j) wts[j] = 1.0f + (float)((B - 1 - (cdp[0] + j)) / CG) * ((float)CG / (float)B);
 	for (uint32_t j = 0; j < 4 * C; ++j) dlf[j] = h2f(M.dloss[j]);
 	for (uint32_t l = 0; l < M.L; ++l)
 		for (uint32_t j = 0; j < C; ++j)

@@ -9,7 +9,15 @@ row-sharded frame gathered to rank 0.
 Checks: the density grid after the split update is bit-identical to one process doing the
 whole update; after 130 steps (one error-map CDF rebuild, eight camera updates) every rank
 holds bit-identical parameters, grid and camera offsets (the replicas do not drift); the
-gathered frame equals rank 0's own full render bit for bit.
+gathered frame equals rank 0's own full render bit for bit.  And the decomposition is exact:
+two ranks of batch B train like ONE process of batch 2B (the same rays, sample / compaction caps
+and rollover over the global ray order, ngp_train_args.world_size), compared in deterministic
+mode (fixed-point hash-grid gradients, so the gradient all-reduce is an exact integer sum).
+
+The RCCL calls themselves run in test_rccl_world_size_one_matches_plain_testbed: a real RCCL
+communicator of one rank on the box's GPU drives the same data-parallel path (ncclAllReduce of the
+per-rank totals, gradients, violation word, grid evaluation, statistics; ncclSend / ncclRecv of the
+frame rows), bit-identical to a Testbed without a communicator.
 """
 import os
 import socket
@@ -57,6 +65,45 @@ def _testbed(scene_dir):
     return tb
 
 
+def _host_allreduce(dist):
+    def allreduce(arr, op):
+        t = torch.from_numpy(arr)
+        rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
+        if t.dtype == torch.float16:  # gloo reduces fp32; a 2-rank fp16 sum rounds exactly once either way
+            t32 = t.float()
+            dist.all_reduce(t32, op=rop)
+            t.copy_(t32.half())
+        else:
+            dist.all_reduce(t, op=rop)
+    return allreduce
+
+
+EQ_STEPS = 24
+
+
+def _equivalence_worker(rank, world, port, scene_dir, q):
+    """Deterministic data-parallel training: state after the first frame and after EQ_STEPS."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        tb = _testbed(scene_dir)
+        tb.init_distributed_host(rank, world, _host_allreduce(dist))
+        tb.deterministic = True
+        tb.shall_train = True
+        out = dict(rank=rank)
+        while tb.training_step < EQ_STEPS:
+            tb.frame()
+            if tb.training_step in (1, EQ_STEPS):
+                out[tb.training_step] = dict(params=_params(tb), grid=tb.density_grid(), bits=tb.density_grid_bitfield(),
+                                             stats=tb.last_train_stats())
+        q.put(out)
+    finally:
+        dist.destroy_process_group()
+
+
 def _worker(rank, world, port, scene_dir, q):
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -65,18 +112,7 @@ def _worker(rank, world, port, scene_dir, q):
     try:
         torch.cuda.set_device(0)
         tb = _testbed(scene_dir)
-
-        def allreduce(arr, op):
-            t = torch.from_numpy(arr)
-            rop = dist.ReduceOp.MAX if op == "max" else dist.ReduceOp.SUM
-            if t.dtype == torch.float16:  # gloo reduces fp32; a 2-rank fp16 sum rounds exactly once either way
-                t32 = t.float()
-                dist.all_reduce(t32, op=rop)
-                t.copy_(t32.half())
-            else:
-                dist.all_reduce(t, op=rop)
-
-        tb.init_distributed_host(rank, world, allreduce)
+        tb.init_distributed_host(rank, world, _host_allreduce(dist))
         assert tb.world_size == world and tb.rank == rank
         tr = tb.nerf.training
         tr.optimize_exposure = True
@@ -108,12 +144,11 @@ def scene(tmp_path_factory):
     return str(root)
 
 
-def test_data_parallel_testbed_two_processes_one_gpu(scene):
-    world = 2
+def _spawn(target, scene, world=2):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=_worker, args=(r, world, port, scene, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, scene, q)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -125,6 +160,12 @@ def test_data_parallel_testbed_two_processes_one_gpu(scene):
         for p in procs:
             p.join(timeout=60)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    return res
+
+
+def test_data_parallel_testbed_two_processes_one_gpu(scene):
+    world = 2
+    res = _spawn(_worker, scene, world)
     r0, r1 = res[0], res[1]
 
     # the split density-grid update (1/N of the samples per rank + max all-reduce) equals one
@@ -152,3 +193,103 @@ def test_data_parallel_testbed_two_processes_one_gpu(scene):
     assert r1["gathered"] is None
     np.testing.assert_array_equal(r0["gathered"], r0["local"])
     assert r0["local"][..., 3].max() > 0.5
+
+
+def test_two_ranks_train_like_one_process_with_twice_the_batch(scene):
+    """rank r of N owns global rays [r R, (r+1) R) of one batch; with the exact
+    decomposition the N ranks' step is one process's step of N x the batch.  Deterministic mode on
+    both sides: the hash-grid gradients are integer sums (identical), the MLP gradients sums over
+    different partitions (float association), so the parameters agree to rounding and the grid /
+    bitfield -- thresholded densities of those parameters -- agree exactly."""
+    res = _spawn(_equivalence_worker, scene)
+    torch.cuda.set_device(0)
+    tb = _testbed(scene)
+    tb.training_batch_size = 2 * BATCH
+    tb.deterministic = True
+    tb.shall_train = True
+    single = {}
+    while tb.training_step < EQ_STEPS:
+        tb.frame()
+        if tb.training_step in (1, EQ_STEPS):
+            single[tb.training_step] = dict(params=_params(tb), grid=tb.density_grid(), bits=tb.density_grid_bitfield(),
+                                            stats=tb.last_train_stats())
+    n_mlp = _n_mlp(tb)
+    for step in (1, EQ_STEPS):
+        s = single[step]
+        for r in (0, 1):
+            d = res[r][step]
+            # the global batch statistics are the single process's
+            for k in ("measured_batch_size", "measured_batch_size_before_compaction", "rays_per_batch"):
+                assert d["stats"][k] == s["stats"][k], (step, k, d["stats"][k], s["stats"][k])
+            assert d["stats"]["loss"] == pytest.approx(s["stats"]["loss"], rel=1e-5)
+            np.testing.assert_array_equal(d["bits"], s["bits"])
+            np.testing.assert_allclose(d["grid"], s["grid"], rtol=1e-4, atol=1e-6)
+            # replicas identical; against one process: MLP weights to float association, the hash grid
+            # (whose gradients are exact) to the rounding the MLP differences feed through
+            np.testing.assert_array_equal(d["params"], res[0][step]["params"])
+            np.testing.assert_allclose(d["params"][:n_mlp], s["params"][:n_mlp], rtol=1e-3, atol=1e-6)
+            np.testing.assert_allclose(d["params"][n_mlp:], s["params"][n_mlp:], rtol=1e-3, atol=1e-6)
+    # after the first step the hash-grid parameters are bit-identical (integer-summed gradients, the
+    # same Adam step); the step-1 MLP gradients only differ in association
+    np.testing.assert_array_equal(res[0][1]["params"][n_mlp:], single[1]["params"][n_mlp:])
+
+
+def _n_mlp(tb):
+    import ctypes as C
+    import ngp_abi as A
+    info = A.ModelInfo()
+    A.check(A.load().ngp_model_get_info(C.c_void_p(tb.model_handle), C.byref(info)))
+    return int(info.n_mlp_params)
+
+
+def test_rccl_world_size_one_matches_plain_testbed(scene):
+    """The RCCL path on the one GPU of the box (a world_size-1 communicator): a Testbed
+    with init_distributed(0, 1, uid) runs every data-parallel collective through RCCL -- the per-rank
+    totals (ncclInt32), the fixed-point gradient all-reduce (ngp_allreduce_grads, ncclInt64 + fp32),
+    the violation max, the density-grid max all-reduce, the statistics, and render_distributed's
+    ncclSend / ncclRecv of the frame rows -- and must match a Testbed without a communicator bit for
+    bit (deterministic mode on both)."""
+    import pyngp as ngp
+    torch.cuda.set_device(0)
+    out = {}
+    for name in ("plain", "rccl"):
+        tb = _testbed(scene)
+        if name == "rccl":
+            tb.init_distributed(0, 1, ngp.Testbed.nccl_unique_id())
+            assert tb.distributed and tb.world_size == 1
+        tb.deterministic = True
+        tb.shall_train = True
+        while tb.training_step < 50:
+            tb.frame()
+        tb.background_color = [0.0, 0.0, 0.0, 1.0]
+        tb.set_camera_to_training_view(1)
+        frame = tb.render_distributed(W, H, 1, True) if name == "rccl" else tb.render(W, H, 1, True)
+        out[name] = dict(params=_params(tb), grid=tb.density_grid(), bits=tb.density_grid_bitfield(), frame=frame,
+                         stats=tb.last_train_stats())
+        del tb
+    a, b = out["plain"], out["rccl"]
+    assert a["stats"] == b["stats"]
+    np.testing.assert_array_equal(a["params"], b["params"])
+    np.testing.assert_array_equal(a["grid"], b["grid"])
+    np.testing.assert_array_equal(a["bits"], b["bits"])
+    np.testing.assert_array_equal(a["frame"], b["frame"])
+    assert a["frame"][..., 3].max() > 0.5
+
+
+def test_deterministic_steps_are_bit_reproducible(scene):
+    """SURVEY §5 deterministic mode: two Testbeds training the same scene from the same seed end
+    bit-identical (fixed-point hash-grid gradients); the default fp16-atomic mode agrees with it to
+    fp16 accumulation error."""
+    torch.cuda.set_device(0)
+    runs = []
+    for det in (True, True, False):
+        tb = _testbed(scene)
+        tb.deterministic = det
+        tb.shall_train = True
+        while tb.training_step < 20:
+            tb.frame()
+        runs.append(_params(tb))
+        del tb
+    np.testing.assert_array_equal(runs[0], runs[1])
+    rel = np.linalg.norm(runs[0] - runs[2]) / np.linalg.norm(runs[0])
+    assert 0 < rel < 1e-2, rel
