@@ -50,6 +50,10 @@ def parse():
                    help="time the dominant kernel in the timed run (0: diagnostic runs without timer events)")
     p.add_argument("--cpu-rows", type=int, default=8, help="1080p rows rendered by the CPU oracle sample")
     p.add_argument("--cpu-rays", type=int, default=512, help="training rays in the CPU oracle sample")
+    p.add_argument("--surface-scene", type=int, default=1,
+                   help="N=1: also time the procedural lego-shaped SURFACE scene (train + 1080p render) -> surface_scene")
+    p.add_argument("--render-to-cpu", type=int, default=5,
+                   help="N=1: 1080p renders timed through render() with the read-back to host memory -> render_to_cpu")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r02_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
@@ -200,6 +204,47 @@ def cpu_baseline(args, tb, cams, imgs, focal, view, W, H, calib, n_cal):
     parity = {"rgb_mean_l1_vs_oracle": l1, "rows": [ys[0], ys[-1]], "tolerance": 1e-3, "ok": l1 < 1e-3,
               "object_pixels_frac": float((gpu_frame[ys, :, 3] > 0.01).mean())}
     return cpu, parity
+
+
+def surface_scene(args, ngp):
+    """The procedural lego-shaped surface scene (synthetic.py: 100 hemisphere views of 800x800, opaque
+    primitives) -- nerf_synthetic/lego's workload shape (a few samples per 1080p ray) next to the
+    volumetric headline scene: pretrain, then args.steps of train(2^18) + one 1080p spp1 render."""
+    sub_args = argparse.Namespace(**vars(args))
+    sub_args.scene = "synthetic"
+    tb = ngp.Testbed(ngp.TestbedMode.Nerf)
+    cams, _, _ = make_dataset(ngp, tb, sub_args, "cuda:0")
+    tb.reload_network_from_file(args.config)
+    tb.shall_train = True
+    for _ in range(args.pretrain):
+        tb.train(args.batch)
+    W, H = args.width, args.height
+    view = 3 % len(cams)
+
+    def step():
+        t0 = time.perf_counter()
+        tb.train(args.batch)
+        t1 = time.perf_counter()
+        tb.set_camera_to_training_view(view)
+        tb.render_to_device(W, H, 1, True)
+        return tb.last_train_stats()["n_rays"], t1 - t0, time.perf_counter() - t1
+
+    for _ in range(args.warmup):
+        step()
+    tb.sync()
+    rays = train_s = render_s = 0
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        r, a, b = step()
+        rays += r + W * H
+        train_s += a
+        render_s += b
+    elapsed = time.perf_counter() - t0
+    return {"Mrays_s": round(rays / elapsed / 1e6, 3), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "train_ms_per_step": round(1e3 * train_s / args.steps, 3), "render_ms_per_frame": round(1e3 * render_s / args.steps, 3),
+            "render_Mrays_s": round(W * H * args.steps / render_s / 1e6, 3),
+            "workload": f"synthetic lego-shaped surface scene ({args.views} views {args.train_res}x{args.train_res}), same network, "
+                        f"{args.pretrain} pretrain steps, then train(2^18) + {W}x{H} spp1 render per step"}
 
 
 def launch_ranks(args):
@@ -388,9 +433,36 @@ def main():
     roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
     roofline["traffic"] = pmc_traffic(args.traffic_json, dom, units / launches)
 
+    # render() as BASELINE.md:30 counts inference: the wall time of render(1920, 1080, spp) including the
+    # read-back of the float frame to host memory (render_to_cpu, src/python_api.cu:124-202) -- here into
+    # pooled page-locked numpy arrays; reported beside value, which keeps the frame in HBM
+    render_to_cpu = None
+    if world == 1 and args.render_to_cpu > 0:
+        tb.set_camera_to_training_view(view)
+        tb.render(W, H, 1, True)
+        t0 = time.perf_counter()
+        for _ in range(args.render_to_cpu):
+            img = tb.render(W, H, 1, True)
+            del img
+        tr = (time.perf_counter() - t0) / args.render_to_cpu
+        t0 = time.perf_counter()
+        for _ in range(args.render_to_cpu):
+            tb.render_to_device(W, H, 1, True)
+        td = (time.perf_counter() - t0) / args.render_to_cpu
+        render_to_cpu = {"ms_per_frame": round(1e3 * tr, 3), "Mrays_s": round(W * H / tr / 1e6, 3),
+                         "ms_per_frame_in_hbm": round(1e3 * td, 3), "readback_ms": round(1e3 * (tr - td), 3),
+                         "readback_GB_s": round(W * H * 16 / max(tr - td, 1e-9) / 1e9, 1),
+                         "note": f"{args.render_to_cpu} renders of the bench view through render() (numpy float32 "
+                                 "[H,W,4] on pooled pinned host memory) vs render_to_device()"}
+
     cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu, parity = cpu_baseline(args, tb, cams, imgs, focal, view, W, H, calib, n_cal)
+
+    surface = None
+    if world == 1 and args.surface_scene:
+        del tb
+        surface = surface_scene(args, ngp)
 
     value = rays / elapsed / 1e6
     if rank == 0:
@@ -423,6 +495,8 @@ def main():
                       "render_ms_per_frame": round(1e3 * split["render_s"] / args.steps, 3),
                       "note": "rank 0; per-part wall time inside the timed region (SURVEY 8(d) counts train and inference separately)"},
             "kernels_calibration": kernels,
+            "render_to_cpu": render_to_cpu,
+            "surface_scene": surface,
             "config_c": config_c,
         }
         print(json.dumps(line), flush=True)

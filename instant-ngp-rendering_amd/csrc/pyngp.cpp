@@ -18,6 +18,20 @@
 namespace py = pybind11;
 using namespace ngp;
 
+// An [h][w][4] float array over a pooled page-locked buffer (pinned_host_alloc); the capsule returns the
+// buffer to the pool when numpy frees the array.
+static py::array_t<float> pinned_frame(int height, int width) {
+	const size_t bytes = (size_t)height * width * 4 * sizeof(float);
+	float* p = static_cast<float*>(pinned_host_alloc(bytes));
+	auto* owner = new std::pair<void*, size_t>(p, bytes);
+	py::capsule cap(owner, [](void* o) {
+		auto* q = static_cast<std::pair<void*, size_t>*>(o);
+		pinned_host_release(q->first, q->second);
+		delete q;
+	});
+	return py::array_t<float>({(py::ssize_t)height, (py::ssize_t)width, (py::ssize_t)4}, p, cap);
+}
+
 #define NGP_TUNING_FIELDS                                                                                              \
 	NGP_TUNING_FIELD(render_pipelines) NGP_TUNING_FIELD(render_pass_samples) NGP_TUNING_FIELD(render_lanes)          \
 	NGP_TUNING_FIELD(render_first_steps) NGP_TUNING_FIELD(render_max_steps) NGP_TUNING_FIELD(render_lag)             \
@@ -413,13 +427,14 @@ PYBIND11_MODULE(pyngp, m) {
 		.def("render",
 		     [](Testbed& t, int width, int height, int spp, bool linear, float start_t, float end_t, float fps, float shutter) {
 			     (void)start_t, (void)end_t, (void)fps, (void)shutter;  // camera paths are out of scope
-			     std::vector<float> img;
+			     if (width <= 0 || height <= 0) throw std::runtime_error("render: invalid resolution");
+			     // render_to_cpu (src/python_api.cu:124-202): the frame is read back straight into the array's
+			     // page-locked memory (pooled; returned to the pool when the array is freed)
+			     py::array_t<float> a = pinned_frame(height, width);
 			     {
 				     py::gil_scoped_release rel;
-				     img = t.render(width, height, spp, linear);
+				     t.render_into(a.mutable_data(), width, height, spp, linear);
 			     }
-			     py::array_t<float> a({height, width, 4});
-			     std::memcpy(a.mutable_data(), img.data(), img.size() * sizeof(float));
 			     return a;
 		     },
 		     py::arg("width") = 1920, py::arg("height") = 1080, py::arg("spp") = 1, py::arg("linear") = true,

@@ -11,6 +11,8 @@
 #include <algorithm>
 #include <cctype>
 #include <iterator>
+#include <map>
+#include <mutex>
 #include <chrono>
 #include <cmath>
 #include <cstdio>
@@ -1510,17 +1512,52 @@ void Testbed::ensure_render_buffers(size_t n) {
 	m_render_cap = n;
 }
 
+static std::mutex g_pinned_mu;
+static std::multimap<size_t, void*> g_pinned_free;
+
+void* pinned_host_alloc(size_t bytes) {
+	{
+		std::lock_guard<std::mutex> lock(g_pinned_mu);
+		auto it = g_pinned_free.find(bytes);
+		if (it != g_pinned_free.end()) {
+			void* p = it->second;
+			g_pinned_free.erase(it);
+			return p;
+		}
+	}
+	void* p = nullptr;
+	hk(hipHostMalloc(&p, std::max<size_t>(bytes, 1), hipHostMallocDefault), "hipHostMalloc frame");
+	return p;
+}
+
+void pinned_host_release(void* p, size_t bytes) {
+	if (!p) return;
+	std::lock_guard<std::mutex> lock(g_pinned_mu);
+	if (g_pinned_free.count(bytes) < 4) {  // keep a few per size (frames of the same resolution)
+		g_pinned_free.emplace(bytes, p);
+		return;
+	}
+	(void)hipHostFree(p);
+}
+
 std::vector<float> Testbed::render(int width, int height, int spp, bool linear, uint32_t shard_index,
                                    uint32_t shard_count, uint32_t shard_rows, bool copy_to_host) {
 	if (width <= 0 || height <= 0) throw std::runtime_error("render: invalid resolution");
+	std::vector<float> out(copy_to_host ? (size_t)width * height * 4 : 0, 0.0f);
+	render_into(copy_to_host ? out.data() : nullptr, width, height, spp, linear, shard_index, shard_count, shard_rows);
+	return out;
+}
+
+void Testbed::render_into(float* host_dst, int width, int height, int spp, bool linear, uint32_t shard_index,
+                          uint32_t shard_count, uint32_t shard_rows) {
+	if (width <= 0 || height <= 0) throw std::runtime_error("render: invalid resolution");
 	const size_t n = (size_t)width * height;
-	std::vector<float> out(copy_to_host ? n * 4 : 0, 0.0f);
 	const vec2 sc = {(0.5f - screen_center[0]) * zoom + 0.5f, (0.5f - screen_center[1]) * zoom + 0.5f};
 	const int res_axis = fov_axis == 0 ? width : height;
 	const vec2 focal = {relative_focal_length[0] * (float)res_axis * zoom, relative_focal_length[1] * (float)res_axis * zoom};
 
 	if (render_ground_truth && nerf.training.dataset.n_images > 0) {
-		out.assign(n * 4, 0.0f);
+		std::vector<float> out(n * 4, 0.0f);
 		// overlay_image_kernel with ground-truth alpha 1 (src/render_buffer.cu:348-416), then tonemap to linear/sRGB
 		const NerfDataset& ds = nerf.training.dataset;
 		const int v = std::min(std::max(nerf.training.view, 0), (int)ds.n_images - 1);
@@ -1562,7 +1599,8 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 				}
 				std::memcpy(&out[((size_t)y * width + x) * 4], c, sizeof(c));
 			}
-		return out;
+		if (host_dst) std::memcpy(host_dst, out.data(), out.size() * sizeof(float));
+		return;
 	}
 	if (!m_model) throw std::runtime_error("render: no network (load training data or a snapshot first)");
 	const auto t0 = std::chrono::steady_clock::now();
@@ -1608,10 +1646,9 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 		                          (int)color_space, exposure, bg, linear ? 0 : 1, m_stream));
 		++m_spp;
 	}
-	if (copy_to_host) hk(hipMemcpyAsync(out.data(), m_out, n * 4 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "render d2h");
+	if (host_dst) hk(hipMemcpyAsync(host_dst, m_out, n * 4 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "render d2h");
 	sync();
 	render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
-	return out;
 }
 
 std::vector<float> Testbed::density_grid() const {

@@ -14,6 +14,13 @@
 #include <vector>
 
 #include "../../include/ngp_hip.h"
+
+namespace ngp {
+// Page-locked host buffers for frame read-backs, recycled through a small per-size pool (hipHostMalloc
+// costs milliseconds; a frame read-back into pageable memory runs at about a fifth of the DMA rate).
+void* pinned_host_alloc(size_t bytes);
+void pinned_host_release(void* p, size_t bytes);
+}  // namespace ngp
 #include "json.h"
 
 namespace ngp {
@@ -192,6 +199,10 @@ public:
 	// copy_to_host=false leaves the tonemapped frame in HBM (render_frame_buffer()) and returns {}.
 	std::vector<float> render(int width, int height, int spp, bool linear, uint32_t shard_index = 0,
 	                          uint32_t shard_count = 1, uint32_t shard_rows = 8, bool copy_to_host = true);
+	// the same into caller-owned host memory of width * height * 4 floats (null: stay in HBM); with a
+	// pinned buffer (pinned_host_alloc) the read-back runs at PCIe DMA rate
+	void render_into(float* host_dst, int width, int height, int spp, bool linear, uint32_t shard_index = 0,
+	                 uint32_t shard_count = 1, uint32_t shard_rows = 8);
 	const float* render_frame_buffer() const { return m_out; }
 	void set_camera_to_training_view(int trainview);
 	void reset_camera();
