@@ -218,7 +218,9 @@ typedef struct ngp_train_args {
 	void* allreduce_user;
 	/* 1: hash-grid gradients accumulate as 64-bit fixed point (2^-40 units, NGP_GRADS_GRID_FIXED64) with
 	 * integer atomics -- order-independent sums, so a step is bit-reproducible and data-parallel ranks
-	 * sum exactly (deterministic mode); 0: packed fp16 atomics as tcnn's GridEncoding backward */
+	 * sum exactly (deterministic mode); the optimizer rounds each sum to fp16 once (the
+	 * gradient buffer's precision, so the sparse skip sees the same zeros); 0: packed fp16 atomics as
+	 * tcnn's GridEncoding backward */
 	int32_t deterministic;
 } ngp_train_args;
 

@@ -1161,8 +1161,12 @@ __global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
 	// (ngp_train_discard + full_forward) -- every thread reads the same word
 	if (a.skip && *a.skip) return;
 	const bool is_mlp = i < a.n_mlp;
-	const float graw = is_mlp ? a.grad[i]
-	                          : (a.grad64 ? (float)a.grad64[i - a.n_mlp] * GRAD_FIXED_INV : __half2float(a.grad16[i - a.n_mlp]));
+	// deterministic hash-grid gradients are the exact sum rounded to fp16 once -- the precision the fp16
+	// buffer holds, so the sparse skip of zero gradients (a sum below fp16's range is zero) matches
+	float graw;
+	if (is_mlp) graw = a.grad[i];
+	else if (a.grad64) graw = __half2float(__float2half((float)a.grad64[i - a.n_mlp] * GRAD_FIXED_INV));
+	else graw = __half2float(a.grad16[i - a.n_mlp]);
 	float w = a.w32[i];
 	bool update = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
 	if (update) {
