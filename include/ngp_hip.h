@@ -281,7 +281,33 @@ typedef struct ngp_render_args {
 	 * render_with_lens_distortion: device [res_y][res_x][2] f32; null = off */
 	const float* distortion_map;
 	uint32_t distortion_res[2];
+	/* the crop box's frame (Testbed::m_render_aabb_to_local, NerfDataset::render_aabb_to_local): positions are
+	 * tested against aabb_min / aabb_max after this row-major 3x3 map (if_unoccupied_advance_to_next_occupied_voxel,
+	 * nerf_device.cuh:461-494; init_rays_with_payload_kernel_nerf, src/testbed_nerf.cu:1465-1475); all zeros =
+	 * identity */
+	float render_aabb_to_local[9];
+	/* Testbed::m_render_mode (ERenderMode, common.h:56-67) as NGP_RENDER_MODE_* below; 0 = Shade */
+	int32_t render_mode;
+	float depth_scale;          /* Depth mode: 1 / dataset scale (src/testbed_nerf.cu:1905) */
+	int32_t gbuffer_hard_edges; /* Nerf::render_gbuffer_hard_edges: Depth / Positions from the max-weight sample */
+	/* depth of field (uv_to_ray, common_device.cuh:450-456): aperture_size != 0 jitters the ray origin over a disk
+	 * on the lens and aims it at the focus plane at camera-space depth focus_z (the reference passes plane_z =
+	 * slice_plane_z + scale); Slice mode renders the density / colour slice at depth focus_z instead of tracing */
+	float aperture_size;
+	float focus_z;
 } ngp_render_args;
+
+/* ngp_render_args.render_mode (the reference's ERenderMode; Distortion and EncodingVis are GUI
+ * visualisations of this build's scope and are refused) */
+enum {
+	NGP_RENDER_MODE_SHADE = 0,
+	NGP_RENDER_MODE_AO = 1,
+	NGP_RENDER_MODE_NORMALS = 2,
+	NGP_RENDER_MODE_POSITIONS = 3,
+	NGP_RENDER_MODE_DEPTH = 4,
+	NGP_RENDER_MODE_COST = 5,
+	NGP_RENDER_MODE_SLICE = 6
+};
 
 /* Launch shapes and march schedule of the gfx950 kernels (no reference counterpart).  None of
  * them changes a result -- every ray composites its own samples in order whatever the pass

@@ -283,6 +283,9 @@ struct RenderPipeScratch {
 	DevBuf<__half> enc;         // [L][max_samples][F]
 	DevBuf<__half> out;         // [max_samples][4]
 	DevBuf<uint32_t> counters;  // [16]
+	// Normals render mode: d(raw density)/d(warped position) of the pass's samples and its scratch
+	DevBuf<__half> nrm_dloss, nrm_denc;
+	DevBuf<float> nrm, nrm_grads;
 	DevBuf<uint32_t> host_counter;  // pinned, fine-grained (hipHostMalloc): per-pass counters
 	uint32_t* host_counter_dev = nullptr;  // its device address
 	uint32_t pass_tag = 0;          // tags of published passes (monotonic across renders)
@@ -290,6 +293,7 @@ struct RenderPipeScratch {
 	void release() {
 		for (int b = 0; b < 3; ++b) { payload[b].release(); rgba[b].release(); depth[b].release(); }
 		coords.release(); enc.release(); out.release(); counters.release();
+		nrm_dloss.release(); nrm_denc.release(); nrm.release(); nrm_grads.release();
 		if (host_counter.ptr) (void)hipHostFree(host_counter.ptr);
 		host_counter.ptr = nullptr;
 		for (auto& e : events)
@@ -306,12 +310,15 @@ struct RenderScratch {
 	DevBuf<uint4> dense_rec;   // corner records of the dense levels (LevelTable::rec), rebuilt per render
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
+	DevBuf<float> slice_coords;   // Slice mode: [pixels][8] NerfCoordinate rows (pos.x NaN: no ray)
+	DevBuf<__half> slice_enc, slice_out;
 	uint64_t df_version = ~0ull;
 	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;
 	void release() {
 		for (auto& p : pipe) p.release();
 		summary.release(); dense_rec.release(); df.release(); df_x.release(); df_xy.release();
+		slice_coords.release(); slice_enc.release(); slice_out.release();
 		if (fork) (void)hipEventDestroy(fork);
 		fork = nullptr;
 		for (int j = 0; j < MAX_PIPES; ++j) {

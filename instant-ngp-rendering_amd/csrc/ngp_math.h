@@ -422,6 +422,34 @@ NGP_HD void ray_intersect(const aabb3& b, v3 pos, v3 dir, float* t0, float* t1) 
 	*t1 = tmax;
 }
 
+// The render crop box (Testbed::m_render_aabb + m_render_aabb_to_local): positions are tested in
+// the box's local frame, local = R * world (nerf_device.cuh:475, src/testbed_nerf.cu:1467-1469).
+struct RenderBox {
+	aabb3 box;
+	float R[9];  // row-major
+	int rot;     // 0: R is the identity
+};
+NGP_HD v3 rbox_local(const RenderBox& b, v3 p) {
+	if (!b.rot) return p;
+	return mk3(b.R[0] * p.x + b.R[1] * p.y + b.R[2] * p.z, b.R[3] * p.x + b.R[4] * p.y + b.R[5] * p.z,
+	           b.R[6] * p.x + b.R[7] * p.y + b.R[8] * p.z);
+}
+NGP_HD bool rbox_contains(const RenderBox& b, v3 p) { return aabb_contains(b.box, rbox_local(b, p)); }
+inline RenderBox make_render_box(const aabb3& box, const float* R) {
+	RenderBox b;
+	b.box = box;
+	bool any = false, ident = true;
+	for (int k = 0; k < 9; ++k) {
+		b.R[k] = R ? R[k] : 0.0f;
+		any |= b.R[k] != 0.0f;
+		ident &= b.R[k] == ((k % 4 == 0) ? 1.0f : 0.0f);
+	}
+	b.rot = any && !ident;
+	if (!b.rot)
+		for (int k = 0; k < 9; ++k) b.R[k] = (k % 4 == 0) ? 1.0f : 0.0f;
+	return b;
+}
+
 // ---------------------------------------------------------------------------
 // Warps — nerf_device.cuh:265-314.
 // ---------------------------------------------------------------------------
@@ -599,11 +627,11 @@ enum LatticeStep : int { LATTICE_OCCUPIED = 0, LATTICE_SKIPPED = 1, LATTICE_EXIT
 // AABB, or skipped (moved to the next candidate point).  Kept as a single step so a
 // wave's lanes can interleave sampling and skipping without serialising on each other.
 NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
-                        const uint8_t* summary, uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
+                        const uint8_t* summary, uint32_t max_mip, const RenderBox& aabb, OccCache& cache) {
 	const float n = *n_io;
 	const float t = step_from(st, n);
 	const v3 pos = o + d * t;
-	if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return LATTICE_EXIT;
+	if (t >= MAX_DEPTH || !rbox_contains(aabb, pos)) return LATTICE_EXIT;
 	uint32_t mip = mip_from_pos(pos);
 	mip = mip > max_mip ? max_mip : mip;
 	uint32_t cell;
@@ -633,7 +661,7 @@ NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, co
 		// the jump stands if the point before the landing point is still in the skipped
 		// cell/block, or already outside the AABB (the ray leaves the volume inside the block)
 		const v3 last = o + d * step_from(st, nn - 1.0f);
-		if (aabb_contains(aabb, last) && (cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
+		if (rbox_contains(aabb, last) && (cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
 	}
 	*n_io = nn;
 	return LATTICE_SKIPPED;
@@ -664,11 +692,11 @@ NGP_HD uint32_t df_index(uint32_t mip, uint32_t oct, int ix, int iy, int iz) {
 // occupied iff D = 0 at its mip; the coarsest empty mip is climbed as the reference does), but
 // an empty cell is left through the far faces of its empty D-box in one verified jump.
 NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, uint32_t oct, const uint8_t* df,
-                           uint32_t max_mip, const aabb3& aabb) {
+                           uint32_t max_mip, const RenderBox& aabb) {
 	const float n = *n_io;
 	const float t = step_from(st, n);
 	const v3 pos = o + d * t;
-	if (t >= MAX_DEPTH || !aabb_contains(aabb, pos)) return LATTICE_EXIT;
+	if (t >= MAX_DEPTH || !rbox_contains(aabb, pos)) return LATTICE_EXIT;
 	uint32_t mip = mip_from_pos(pos);
 	mip = mip > max_mip ? max_mip : mip;
 	int cx, cy, cz;
@@ -702,7 +730,7 @@ NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir,
 		// the jump stands if the point before the landing point is still in the empty box, or
 		// already outside the AABB (the box is convex: every point in between is in it too)
 		const v3 last = o + d * step_from(st, nn - 1.0f);
-		if (aabb_contains(aabb, last)) {
+		if (rbox_contains(aabb, last)) {
 			int qx, qy, qz;
 			const bool in_grid = cascaded_cell_at(last, mip, &qx, &qy, &qz);
 			const int ex = d.x < 0.0f ? cx - qx : qx - cx, ey = d.y < 0.0f ? cy - qy : qy - cy,
@@ -716,7 +744,7 @@ NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir,
 }
 
 NGP_HD bool next_occupied_lattice_point(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
-                                        const uint8_t* summary, uint32_t max_mip, const aabb3& aabb, OccCache& cache) {
+                                        const uint8_t* summary, uint32_t max_mip, const RenderBox& aabb, OccCache& cache) {
 	while (true) {
 		const int r = lattice_step(n_io, st, o, d, idir, bitfield, summary, max_mip, aabb, cache);
 		if (r != LATTICE_SKIPPED) return r == LATTICE_OCCUPIED;

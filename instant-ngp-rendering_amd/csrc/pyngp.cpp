@@ -183,6 +183,16 @@ PYBIND11_MODULE(pyngp, m) {
 		.value("Hable", ETonemapCurve::Hable)
 		.value("Reinhard", ETonemapCurve::Reinhard)
 		.export_values();
+	py::enum_<ERenderMode>(m, "RenderMode")
+		.value("AO", ERenderMode::AO)
+		.value("Shade", ERenderMode::Shade)
+		.value("Normals", ERenderMode::Normals)
+		.value("Positions", ERenderMode::Positions)
+		.value("Depth", ERenderMode::Depth)
+		.value("Distortion", ERenderMode::Distortion)
+		.value("Cost", ERenderMode::Cost)
+		.value("Slice", ERenderMode::Slice)
+		.export_values();
 	py::enum_<ELensMode>(m, "LensMode")
 		.value("Perspective", ELensMode::Perspective)
 		.value("OpenCV", ELensMode::OpenCV)
@@ -395,6 +405,7 @@ PYBIND11_MODULE(pyngp, m) {
 		NV_RW("render_lens", render_lens)
 		NV_RW("render_distortion", render_lens)
 		NV_RW("render_min_transmittance", render_min_transmittance)
+		NV_RW("render_gbuffer_hard_edges", render_gbuffer_hard_edges)
 		NV_RW("rendering_min_transmittance", render_min_transmittance)
 		NV_RW("cone_angle_constant", cone_angle_constant)
 		NV_RW("visualize_cameras", visualize_cameras)
@@ -497,6 +508,25 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("render_ground_truth", &Testbed::render_ground_truth)
 		.def_readwrite("render_near_distance", &Testbed::render_near_distance)
 		.def_readwrite("exposure", &Testbed::exposure)
+		.def_readwrite("render_mode", &Testbed::render_mode)
+		.def_readwrite("aperture_size", &Testbed::aperture_size)
+		.def_readwrite("dof", &Testbed::aperture_size)
+		.def_readwrite("slice_plane_z", &Testbed::slice_plane_z)
+		.def_property("render_aabb", [](const Testbed& t) { return BoundingBox{t.render_aabb_min, t.render_aabb_max}; },
+		              [](Testbed& t, const BoundingBox& b) {
+			              t.render_aabb_min = b.min;
+			              t.render_aabb_max = b.max;
+		              })
+		.def_property("render_aabb_to_local",
+		              [](const Testbed& t) {
+			              py::array_t<float> a({3, 3});
+			              std::memcpy(a.mutable_data(), t.render_aabb_to_local.data(), 9 * sizeof(float));
+			              return a;
+		              },
+		              [](Testbed& t, py::array_t<float, py::array::c_style | py::array::forcecast> a) {
+			              if (a.size() != 9) throw std::runtime_error("render_aabb_to_local must be a 3x3 matrix");
+			              std::memcpy(t.render_aabb_to_local.data(), a.data(), 9 * sizeof(float));
+		              })
 		.def_property("scale", [](const Testbed& t) { return t.scale; },
 		              [](Testbed& t, float s) {
 			              // Testbed::set_scale: move the camera along the view direction, keeping look_at fixed

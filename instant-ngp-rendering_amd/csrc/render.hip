@@ -36,7 +36,8 @@ struct RenderK {
 	m43 cam;
 	float fx, fy, scx, scy;
 	float near_distance;
-	aabb3 aabb, train_aabb;
+	RenderBox aabb;    // the crop box (m_render_aabb in the frame of m_render_aabb_to_local)
+	aabb3 train_aabb;  // the network's input warp (m_aabb)
 	Stepping st;
 	uint32_t max_mip;
 	float min_transmittance;
@@ -59,8 +60,47 @@ struct RenderK {
 	const uint8_t* df;  // octant distance fields (null: occupancy-summary block skipping)
 	int budget;         // per-ray sample budgets (sample_budget); 0: every ray gets n_steps
 	float budget_scale;
-	uint32_t* dbg;  // NGP_RENDER_DEBUG: [init lattice steps, init alive, generate iterations, samples, samples composited]
+	uint32_t* dbg;  // ngp_tuning.debug bit 0: [init lattice steps, init alive, generate iterations, samples, samples composited]
+	int mode;       // NGP_RENDER_MODE_*
+	float depth_scale;
+	int hard_edges;
+	float aperture, focus_z;  // depth of field (uv_to_ray, common_device.cuh:450-456)
+	const float* normals;     // Normals mode: d(raw density)/d(warped position) per sample slot of the pass, [slot][3]
 };
+
+// square2disk_shirley (random_val.cuh:112-128)
+__device__ __forceinline__ void square2disk_shirley(float a, float b, float* x, float* y) {
+	float phi, r;
+	if (a * a > b * b) {
+		r = a;
+		phi = (NGP_PI / 4.0f) * (b / a);
+	} else {
+		r = b;
+		phi = (NGP_PI / 2.0f) - (NGP_PI / 4.0f) * (a / b);
+	}
+	float s, c;
+	sincosf(phi, &s, &c);
+	*x = r * c;
+	*y = r * s;
+}
+
+// uv_to_ray's camera-space -> world ray (common_device.cuh:445-459): rotate, depth of field (the
+// origin jittered over the lens disk, the ray aimed at the focus plane), near distance.
+__device__ __forceinline__ void camera_ray(const RenderK& k, const m43& cam, v3 dir_cam, float u, float v, v3* o, v3* d) {
+	v3 dir = rot(cam, dir_cam);
+	v3 origin = cam.c[3];
+	if (k.aperture != 0.0f) {
+		const v3 lookat = origin + dir * k.focus_z;
+		const uint32_t px = (uint32_t)(int)(u * (float)k.W), py = (uint32_t)(int)(v * (float)k.H);
+		float bx, by, dx, dy;
+		ld_random_val_2d(k.sample_index, px * 19349663u + py * 96925573u, &bx, &by);
+		square2disk_shirley(bx * 2.0f - 1.0f, by * 2.0f - 1.0f, &dx, &dy);
+		origin = origin + cam.c[0] * (k.aperture * dx) + cam.c[1] * (k.aperture * dy);
+		dir = (lookat - origin) * (1.0f / k.focus_z);
+	}
+	*o = origin + dir * k.near_distance;
+	*d = dir;
+}
 
 __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32_t yl) {
 	// pipeline-local row -> shard-local row (alternate 8-row blocks) -> frame row
@@ -207,8 +247,8 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 		dir.x += ddx;
 		dir.y += ddy;
 	}
-	dir = rot(cam, dir);
-	v3 origin = cam.c[3] + dir * k.near_distance;
+	v3 origin;
+	camera_ray(k, cam, dir, u, v, &origin, &dir);
 
 	Payload p;
 	p.max_weight = 0.0f;
@@ -218,12 +258,12 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 	p.alpha_last = 0.0f;
 	dir = normalize(dir);
 	float t0, t1;
-	ray_intersect(k.aabb, origin, dir, &t0, &t1);
+	ray_intersect(k.aabb.box, rbox_local(k.aabb, origin), rbox_local(k.aabb, dir), &t0, &t1);
 	const float t = fmaxf(t0, 0.0f) + 1e-6f;
 	p.o[0] = origin.x; p.o[1] = origin.y; p.o[2] = origin.z;
 	p.d[0] = dir.x; p.d[1] = dir.y; p.d[2] = dir.z;
 	p.n = 0.0f;
-	bool alive = aabb_contains(k.aabb, origin + dir * t);
+	bool alive = rbox_contains(k.aabb, origin + dir * t);
 	if (alive) {
 		// advance_pos_nerf: jitter the start and skip empty space
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
@@ -246,6 +286,69 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 	}
 	*pp = p;
 	return alive;
+}
+
+// Slice render mode (render_nerf, src/testbed_nerf.cu:1842-1845, 1908-1932): no tracing -- every
+// pixel's ray is evaluated once, at camera-space depth focus_z (init_rays_with_payload_kernel_nerf's
+// plane_z < 0 branch, :1447-1456), with dt = MIN_CONE_STEPSIZE (generate_nerf_network_inputs_at_current
+// _position, :397-403); then compute_nerf_rgba with depth 0.01 (:405-423) and shade_kernel_nerf.
+template <bool LENS>
+__global__ void __launch_bounds__(256) k_slice_init(RenderK k, uint32_t n, float* __restrict__ coords,
+                                                    float4* __restrict__ frame, float* __restrict__ depth_buffer) {
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n) return;
+	const uint32_t x = r % k.W, yl = r / k.W;
+	const uint32_t blk = yl / k.shard_rows, within = yl % k.shard_rows;
+	const uint32_t y = (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
+	const uint32_t idx = x + k.W * y;
+	frame[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
+	depth_buffer[idx] = MAX_DEPTH;
+	float* c = coords + 8 * (size_t)r;
+	float ox, oy;
+	ld_random_pixel_offset(k.snap ? 0u : k.sample_index, &ox, &oy);
+	const float u = ((float)x + ox) / (float)k.W, v = ((float)y + oy) / (float)k.H;
+	v3 dir = mk3((u - k.scx) * (float)k.W / k.fx, (v - k.scy) * (float)k.H / k.fy, 1.0f);
+	const m43 cam = k.rs_on ? xform_given_rolling_shutter(k.cam, k.cam_end, k.rs, u, v, ld_random_val(k.sample_index, idx * 72239731u))
+	                        : k.cam;
+	if (LENS && !lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
+		c[0] = __int_as_float(0x7fc00000);  // no ray: the pixel stays empty
+		return;
+	}
+	if (LENS && k.dmap) {
+		float ddx, ddy;
+		distortion_at_lerp(k.dmap, k.drx, k.dry, u, v, &ddx, &ddy);
+		dir.x += ddx;
+		dir.y += ddy;
+	}
+	v3 o, d;
+	camera_ray(k, cam, dir, u, v, &o, &d);  // (no aperture in Slice mode)
+	const v3 pos = o + d * k.focus_z;        // t = -plane_z * |d| along the normalised direction
+	const v3 wp = aabb_relative(k.train_aabb, pos), wd = warp_direction(normalize(d));
+	c[0] = wp.x; c[1] = wp.y; c[2] = wp.z; c[3] = warp_dt(MIN_CONE_STEPSIZE);
+	c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
+	depth_buffer[idx] = k.focus_z;
+}
+
+__global__ void __launch_bounds__(256) k_slice_shade(RenderK k, uint32_t n, const float* __restrict__ coords,
+                                                     const __half* __restrict__ out, float4* __restrict__ frame) {
+	const uint32_t r = blockIdx.x * 256u + threadIdx.x;
+	if (r >= n || coords[8 * (size_t)r] != coords[8 * (size_t)r]) return;
+	const uint32_t x = r % k.W, yl = r / k.W;
+	const uint32_t blk = yl / k.shard_rows, within = yl % k.shard_rows;
+	const uint32_t y = (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
+	const uint32_t idx = x + k.W * y;
+	const __half* o = out + 4 * (size_t)r;
+	const float density = network_to_density(__half2float(o[3]), k.density_act);
+	const float alpha = fminf(fmaxf(1.0f - __expf(-density * 0.01f), 0.0f), 1.0f);
+	float4 t = make_float4(network_to_rgb(__half2float(o[0]), k.rgb_act) * alpha, network_to_rgb(__half2float(o[1]), k.rgb_act) * alpha,
+	                       network_to_rgb(__half2float(o[2]), k.rgb_act) * alpha, alpha);
+	if (!k.linear_colors) {
+		t.x = srgb_to_linear(t.x);
+		t.y = srgb_to_linear(t.y);
+		t.z = srgb_to_linear(t.z);
+	}
+	const float4 f = frame[idx];
+	frame[idx] = make_float4(t.x + f.x * (1.0f - t.w), t.y + f.y * (1.0f - t.w), t.z + f.z * (1.0f - t.w), t.w + f.w * (1.0f - t.w));
 }
 
 // Occupancy summary (ngp_math.h OCC_SUMMARY_*): one workgroup of 512 threads per 32^3
@@ -525,6 +628,11 @@ constexpr uint32_t COMPOSITE_AHEAD = 4;  // 8 measured no better (same-weights A
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
+// MODES: the render modes other than Shade (:626-638) replace a sample's colour -- AO: its alpha,
+// Positions / Depth: its position / camera depth, Normals: the normalised negative density
+// gradient; Cost counts the ray's composited samples in c.x (shade_kernel_nerf turns it into a
+// grey level, :1327-1330) as payload.n_steps = j + current_step does (:664-667).
+template <bool MODES>
 __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                    const float* __restrict__ sdepth, const float4* __restrict__ posdt,
@@ -581,12 +689,30 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				const float dt = unwarp_dt(wdt[u]);
 				const float alpha = 1.0f - __expf(-network_to_density(__high2float(bs), k.density_act) * dt);
 				const float weight = alpha * T;
-				const v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
-				                   network_to_rgb(__low2float(bs), k.rgb_act));
+				v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
+				             network_to_rgb(__low2float(bs), k.rgb_act));
+				if constexpr (MODES) {
+					const size_t s = sbase + j0 + u;
+					if (k.mode == NGP_RENDER_MODE_NORMALS) {
+						// the reference replaces the network input by its gradient (input_gradient, :1715-1717)
+						const float* g = k.normals + 3 * s;
+						const float dd = -network_to_density_derivative(__high2float(bs), k.density_act);
+						rgb = normalize(mk3(g[0] * dd, g[1] * dd, g[2] * dd));
+					} else if (k.mode == NGP_RENDER_MODE_POSITIONS || k.mode == NGP_RENDER_MODE_DEPTH) {
+						const float4 crd = posdt[s];
+						const v3 pos = unwarp_position(mk3(crd.x, crd.y, crd.z), k.train_aabb);
+						rgb = k.mode == NGP_RENDER_MODE_POSITIONS ? (pos - 0.5f) * 0.5f + 0.5f
+						                                          : mk3(dot(cam_fwd, pos - mk3(p.o[0], p.o[1], p.o[2])) * k.depth_scale);
+					} else if (k.mode == NGP_RENDER_MODE_AO) {
+						rgb = mk3(alpha);
+					}
+				}
 				alpha_last = alpha;
-				c.x += rgb.x * weight;
-				c.y += rgb.y * weight;
-				c.z += rgb.z * weight;
+				if (!MODES || k.mode != NGP_RENDER_MODE_COST) {
+					c.x += rgb.x * weight;
+					c.y += rgb.y * weight;
+					c.z += rgb.z * weight;
+				}
 				c.w += weight;
 				if (weight > p.max_weight) {
 					p.max_weight = weight;
@@ -594,9 +720,13 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				}
 				if (c.w > (1.0f - k.min_transmittance)) {
 					const float inv = 1.0f / c.w;
-					c.x *= inv;
-					c.y *= inv;
-					c.z *= inv;
+					if (!MODES || k.mode != NGP_RENDER_MODE_COST) {
+						c.x *= inv;
+						c.y *= inv;
+						c.z *= inv;
+					} else {
+						c.x += (float)(j0 + u);  // the reference's n_steps = j + current_step at the break
+					}
 					c.w *= inv;
 					used = j0 + u + 1;
 					done = true;
@@ -609,6 +739,8 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 			local_depth = dot(cam_fwd, pos - cam_pos);
 		}
 		if (k.dbg) atomicAdd(&k.dbg[4], used);
+		// Cost: a ray going on (or leaving the volume) adds all of this pass's samples
+		if (MODES && k.mode == NGP_RENDER_MODE_COST && !done) c.x += (float)actual;
 		p.alpha_last = alpha_last;
 		// finished: opaque enough, or the ray left the volume during this pass
 		if (done || (p.n_steps & PAYLOAD_EXITED)) alive = false;
@@ -630,14 +762,44 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 	}
 }
 
-__global__ void __launch_bounds__(256) k_shade(uint32_t n, const Payload* __restrict__ hp, const float4* __restrict__ hrgba,
+// Normals mode: dL/dout = d/d(raw density) for the pass's samples (fp16 [n][4])
+__global__ void k_density_unit_dloss(const uint32_t* __restrict__ n_dev, uint32_t n, __half* __restrict__ dl) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n || i >= *n_dev) return;
+	const __half z = __float2half(0.0f);
+	dl[4 * (size_t)i + 0] = z;
+	dl[4 * (size_t)i + 1] = z;
+	dl[4 * (size_t)i + 2] = z;
+	dl[4 * (size_t)i + 3] = __float2half(1.0f);
+}
+
+// shade_kernel_nerf (testbed_nerf.cu:1309-1349) with its render modes
+__global__ void __launch_bounds__(256) k_shade(RenderK k, uint32_t n, const Payload* __restrict__ hp, const float4* __restrict__ hrgba,
                                                const float* __restrict__ hdepth, int linear_colors,
                                                float4* __restrict__ frame, float* __restrict__ depth_buffer) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= n) return;
 	const uint32_t idx = hp[i].idx;
 	float4 t = hrgba[i];
-	if (!linear_colors) {
+	if (k.mode == NGP_RENDER_MODE_NORMALS) {
+		const v3 nn = normalize(mk3(t.x, t.y, t.z));
+		t.x = (0.5f * nn.x + 0.5f) * t.w;
+		t.y = (0.5f * nn.y + 0.5f) * t.w;
+		t.z = (0.5f * nn.z + 0.5f) * t.w;
+	} else if (k.mode == NGP_RENDER_MODE_COST) {
+		const float col = t.x / 128.0f;
+		t = make_float4(col, col, col, 1.0f);
+	} else if (k.hard_edges && k.mode == NGP_RENDER_MODE_DEPTH) {
+		const float dv = hdepth[i] * k.depth_scale;
+		t.x = t.y = t.z = dv;
+	} else if (k.hard_edges && k.mode == NGP_RENDER_MODE_POSITIONS) {
+		const v3 d = mk3(hp[i].d[0], hp[i].d[1], hp[i].d[2]);
+		const v3 pos = k.cam.c[3] + d * (hdepth[i] / dot(d, k.cam.c[2]));
+		t.x = (pos.x - 0.5f) * 0.5f + 0.5f;
+		t.y = (pos.y - 0.5f) * 0.5f + 0.5f;
+		t.z = (pos.z - 0.5f) * 0.5f + 0.5f;
+	}
+	if (!linear_colors && k.mode == NGP_RENDER_MODE_SHADE) {
 		t.x = srgb_to_linear(t.x);
 		t.y = srgb_to_linear(t.y);
 		t.z = srgb_to_linear(t.z);
@@ -808,8 +970,20 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.scx = a->screen_center[0];
 	k.scy = a->screen_center[1];
 	k.near_distance = a->near_distance;
-	k.aabb.min = mk3(a->aabb_min[0], a->aabb_min[1], a->aabb_min[2]);
-	k.aabb.max = mk3(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2]);
+	{
+		aabb3 box;
+		box.min = mk3(a->aabb_min[0], a->aabb_min[1], a->aabb_min[2]);
+		box.max = mk3(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2]);
+		k.aabb = make_render_box(box, a->render_aabb_to_local);
+	}
+	if (a->render_mode < NGP_RENDER_MODE_SHADE || a->render_mode > NGP_RENDER_MODE_SLICE)
+		throw std::invalid_argument("render_mode must be one of NGP_RENDER_MODE_* (Distortion / EncodingVis are not supported)");
+	k.mode = a->render_mode;
+	k.depth_scale = a->depth_scale;
+	k.hard_edges = a->gbuffer_hard_edges;
+	k.aperture = k.mode == NGP_RENDER_MODE_SLICE ? 0.0f : a->aperture_size;  // init_rays_with_payload_kernel_nerf:1427-1429
+	k.focus_z = a->focus_z;
+	if (k.aperture != 0.0f && !(k.focus_z > 0.0f)) throw std::invalid_argument("depth of field needs focus_z > 0");
 	k.train_aabb.min = mk3(a->train_aabb_min[0], a->train_aabb_min[1], a->train_aabb_min[2]);
 	k.train_aabb.max = mk3(a->train_aabb_max[0], a->train_aabb_max[1], a->train_aabb_max[2]);
 	k.st = make_stepping(a->cone_angle_constant);
@@ -841,6 +1015,21 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const uint32_t H_shard = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	if (k.W * H_shard == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
+	if (k.mode == NGP_RENDER_MODE_SLICE) {
+		const uint32_t n = k.W * H_shard;
+		rs.slice_coords.reserve(8 * (size_t)n);
+		rs.slice_enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
+		rs.slice_out.reserve(4 * (size_t)n);
+		(k.lens_mode != LENS_PERSPECTIVE || k.dmap ? k_slice_init<true> : k_slice_init<false>)<<<div_up(n, 256u), 256, 0, s>>>(
+		    k, n, rs.slice_coords.ptr, reinterpret_cast<float4*>(frame), depth_buffer);
+		const __half* tab = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+		const __half* fr = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
+		launch_hashgrid_fwd(m->lt, rs.slice_coords.ptr, 8, n, tab, rs.slice_enc.ptr, internal_layout(m, n), s);
+		launch_mlp_infer(m, fr, rs.slice_enc.ptr, internal_layout(m, n), rs.slice_coords.ptr, 8, n, rs.slice_out.ptr, s);
+		k_slice_shade<<<div_up(n, 256u), 256, 0, s>>>(k, n, rs.slice_coords.ptr, rs.slice_out.ptr, reinterpret_cast<float4*>(frame));
+		NGP_HIP_CHECK(hipGetLastError());
+		return;
+	}
 	const ngp_tuning& tu = m->tuning;
 	const uint32_t n_pipes = render_pipes(tu, k.W * H_shard, H_shard);
 
@@ -1004,10 +1193,31 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
 		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, pr.n);
 		tm.end(NGP_TIMER_RENDER_MLP, ps);
+		if (pr.k.mode == NGP_RENDER_MODE_NORMALS) {
+			// Normals (NerfTracer::trace, testbed_nerf.cu:1715-1717, network->input_gradient): the gradient of
+			// the raw density w.r.t. the warped position of every sample -- the fused MLP backward from
+			// dL/dout = (0, 0, 0, 1) (weight gradients into scratch), then the grid's input gradient
+			RenderPipeScratch& sc = *pr.ps;
+			sc.nrm_dloss.reserve(4 * (size_t)n_elements);
+			sc.nrm_denc.reserve((size_t)m->lt.n_levels * n_elements * m->lt.F);
+			sc.nrm.reserve(3 * (size_t)n_elements);
+			sc.nrm_grads.reserve(m->n_mlp_params);
+			k_density_unit_dloss<<<div_up(n_elements, 256u), 256, 0, ps>>>(samples, n_elements, sc.nrm_dloss.ptr);
+			launch_mlp_train(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), reinterpret_cast<const float*>(pr.posdt), 4,
+			                 n_elements, sc.nrm_dloss.ptr, nullptr, sc.nrm_grads.ptr, sc.nrm_denc.ptr, ps, samples);
+			launch_hashgrid_input_grad(m->lt, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, sc.nrm_denc.ptr,
+			                           EncLayout{n_elements, 0}, table, nullptr, sc.nrm.ptr, ps, samples);
+			pr.k.normals = sc.nrm.ptr;
+		}
 		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
-		k_composite<<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
-		    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
-		    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);
+		if (pr.k.mode == NGP_RENDER_MODE_SHADE)
+			k_composite<false><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
+			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
+			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);
+		else
+			k_composite<true><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
+			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
+			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);
 		tm.end(NGP_TIMER_RENDER_MARCH, ps);
 		NGP_HIP_CHECK(hipGetLastError());
 		pr.cur = 1 - cur;
@@ -1057,7 +1267,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		pr.ps->pass_tag = pr.base_tag + pr.pass;
 		if (n_hit)
-			k_shade<<<div_up(n_hit, 256), 256, 0, pr.s>>>(n_hit, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, k.linear_colors,
+			k_shade<<<div_up(n_hit, 256), 256, 0, pr.s>>>(pr.k, n_hit, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, k.linear_colors,
 			                                              reinterpret_cast<float4*>(frame), depth_buffer);
 		NGP_HIP_CHECK(hipGetLastError());
 	}

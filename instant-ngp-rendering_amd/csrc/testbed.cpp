@@ -288,6 +288,13 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 			ds.scale = 1.f / len;
 			for (int k = 0; k < 3; ++k) ds.offset[k] = (((float)a[1][k].num() + (float)a[0][k].num()) * 0.5f) * -ds.scale + 0.5f;
 		}
+		if (j.contains("render_aabb")) {  // src/nerf_loader.cu:453-456
+			const Json& ra = j["render_aabb"];
+			for (int k = 0; k < 3; ++k) {
+				ds.render_aabb_min[k] = (float)ra[0][k].num();
+				ds.render_aabb_max[k] = (float)ra[1][k].num();
+			}
+		}
 		// depth supervision inputs (src/nerf_loader.cu:419-437, 486-488)
 		if (j.contains("integer_depth_scale")) depth_scale = (float)j["integer_depth_scale"].num();
 		if (j.contains("enable_depth_loading")) enable_depth_loading = j.value("enable_depth_loading", true);
@@ -510,6 +517,17 @@ void Testbed::load_nerf_post() {
 	const float half = 0.5f * (float)std::min(max_aabb_scale, ds.aabb_scale);
 	aabb_min = {0.5f - half, 0.5f - half, 0.5f - half};
 	aabb_max = {0.5f + half, 0.5f + half, 0.5f + half};
+	// m_render_aabb = the training aabb, or the dataset's render_aabb intersected with it (src/testbed_nerf.cu:2221-2225)
+	render_aabb_min = aabb_min;
+	render_aabb_max = aabb_max;
+	render_aabb_to_local = ds.render_aabb_to_local;
+	const bool empty = ds.render_aabb_min[0] > ds.render_aabb_max[0] || ds.render_aabb_min[1] > ds.render_aabb_max[1] ||
+	                   ds.render_aabb_min[2] > ds.render_aabb_max[2];
+	if (!empty)
+		for (int k = 0; k < 3; ++k) {
+			render_aabb_min[k] = std::max(ds.render_aabb_min[k], aabb_min[k]);
+			render_aabb_max[k] = std::min(ds.render_aabb_max[k], aabb_max[k]);
+		}
 	nerf.max_cascade = 0;
 	while ((1 << nerf.max_cascade) < ds.aabb_scale) ++nerf.max_cascade;
 	nerf.cone_angle_constant = ds.aabb_scale <= 1 ? 0.0f : (1.0f / 256.0f);
@@ -1491,7 +1509,14 @@ void Testbed::set_fov(float degrees) {
 void Testbed::set_camera_to_training_view(int trainview) {
 	const NerfDataset& ds = nerf.training.dataset;
 	if (trainview < 0 || (size_t)trainview >= ds.n_images) throw std::runtime_error("Invalid training view.");
+	// m_scale keeps the old look-at point in front of the new view (src/testbed.cu:471-475)
+	const vec3 old_pos = camera.col(3), old_dir = camera.col(2);
+	const vec3 look_at = {old_pos[0] + old_dir[0] * scale, old_pos[1] + old_dir[1] * scale, old_pos[2] + old_dir[2] * scale};
 	camera = ds.xforms[trainview];
+	{
+		const vec3 p = camera.col(3), d = camera.col(2);
+		scale = std::max((look_at[0] - p[0]) * d[0] + (look_at[1] - p[1]) * d[1] + (look_at[2] - p[2]) * d[2], 0.1f);
+	}
 	const auto& md = ds.metadata[trainview];
 	relative_focal_length = {md.focal_length[0] / (float)md.resolution[fov_axis], md.focal_length[1] / (float)md.resolution[fov_axis]};
 	nerf.render_with_lens_distortion = true;
@@ -1615,9 +1640,29 @@ void Testbed::render_into(float* host_dst, int width, int height, int spp, bool 
 	r.screen_center[1] = sc[1];
 	r.near_distance = render_near_distance;
 	for (int k = 0; k < 3; ++k) {
-		r.aabb_min[k] = r.train_aabb_min[k] = aabb_min[k];
-		r.aabb_max[k] = r.train_aabb_max[k] = aabb_max[k];
+		r.aabb_min[k] = render_aabb_min[k];
+		r.aabb_max[k] = render_aabb_max[k];
+		r.train_aabb_min[k] = aabb_min[k];
+		r.train_aabb_max[k] = aabb_max[k];
 	}
+	for (int k = 0; k < 9; ++k) r.render_aabb_to_local[k] = render_aabb_to_local[k];
+	switch (render_mode) {
+		case ERenderMode::AO: r.render_mode = NGP_RENDER_MODE_AO; break;
+		case ERenderMode::Shade: r.render_mode = NGP_RENDER_MODE_SHADE; break;
+		case ERenderMode::Normals: r.render_mode = NGP_RENDER_MODE_NORMALS; break;
+		case ERenderMode::Positions: r.render_mode = NGP_RENDER_MODE_POSITIONS; break;
+		case ERenderMode::Depth: r.render_mode = NGP_RENDER_MODE_DEPTH; break;
+		case ERenderMode::Cost: r.render_mode = NGP_RENDER_MODE_COST; break;
+		case ERenderMode::Slice: r.render_mode = NGP_RENDER_MODE_SLICE; break;
+		default: throw std::runtime_error("render: render mode Distortion is a GUI visualisation and not supported by this build");
+	}
+	r.depth_scale = 1.0f / nerf.training.dataset.scale;  // src/testbed_nerf.cu:1905
+	r.gbuffer_hard_edges = nerf.render_gbuffer_hard_edges;
+	// plane_z = m_slice_plane_z + m_scale (src/testbed_nerf.cu:1842): the Slice plane, or the focus plane of the
+	// depth of field (init_rays_with_payload_kernel_nerf drops the aperture when plane_z < 0, :1427-1429)
+	const float plane_z = slice_plane_z + scale;
+	r.focus_z = plane_z;
+	r.aperture_size = plane_z < 0.0f ? 0.0f : aperture_size;
 	r.cone_angle_constant = nerf.cone_angle_constant;
 	r.max_cascade = nerf.max_cascade;
 	r.min_transmittance = nerf.render_min_transmittance;

@@ -31,6 +31,10 @@ enum class ELossType : int { L2, L1, Mape, Smape, Huber, LogL1, RelativeL2 };
 enum class ENerfActivation : int { None, ReLU, Logistic, Exponential };
 enum class ELensMode : int { Perspective, OpenCV, FTheta, LatLong, OpenCVFisheye, Equirectangular };
 enum class ETonemapCurve : int { Identity, ACES, Hable, Reinhard };
+// ERenderMode (common.h:56-67); Distortion and EncodingVis are GUI visualisations, refused by render()
+enum class ERenderMode : int { AO, Shade, Normals, Positions, Depth, Distortion, Cost, Slice };
+using mat3 = std::array<float, 9>;  // row-major
+constexpr mat3 MAT3_IDENTITY = {1, 0, 0, 0, 1, 0, 0, 0, 1};
 
 using vec2 = std::array<float, 2>;
 using vec3 = std::array<float, 3>;
@@ -70,6 +74,9 @@ struct NerfDataset {
 	vec3 offset = {0.5f, 0.5f, 0.5f};
 	float scale = 0.33f;
 	int aabb_scale = 1;
+	// transforms.json "render_aabb" (nerf_loader.cu:453-456; empty = min > max) and its frame
+	vec3 render_aabb_min = {1.f, 1.f, 1.f}, render_aabb_max = {0.f, 0.f, 0.f};
+	mat3 render_aabb_to_local = MAT3_IDENTITY;
 	bool is_hdr = false;
 	bool from_mitsuba = false;
 	size_t n_images = 0;
@@ -153,6 +160,7 @@ struct Nerf {
 	float render_min_transmittance = 0.01f;
 	bool render_with_lens_distortion = false;
 	Lens render_lens;  // applied to rendered rays when render_with_lens_distortion (src/testbed_nerf.cu:1859)
+	bool render_gbuffer_hard_edges = false;  // nerf.h:174
 	float sharpen = 0.f;
 	uint32_t density_grid_ema_step = 0;
 	bool visualize_cameras = false;
@@ -280,6 +288,12 @@ public:
 	std::string network_config_path = "base.json";
 	bool training_data_available = false;
 	vec3 aabb_min = {0.f, 0.f, 0.f}, aabb_max = {1.f, 1.f, 1.f};
+	// the render crop box (m_render_aabb, m_render_aabb_to_local; src/testbed_nerf.cu:2219-2225) and modes
+	vec3 render_aabb_min = {0.f, 0.f, 0.f}, render_aabb_max = {1.f, 1.f, 1.f};
+	mat3 render_aabb_to_local = MAT3_IDENTITY;
+	ERenderMode render_mode = ERenderMode::Shade;
+	float aperture_size = 0.f;  // m_aperture_size (depth of field)
+	float slice_plane_z = 0.f;  // m_slice_plane_z: focus / slice plane at camera depth slice_plane_z + scale
 	double training_ms = 0.0, training_prep_ms = 0.0, render_ms = 0.0;
 
 private:

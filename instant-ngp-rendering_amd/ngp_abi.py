@@ -100,6 +100,8 @@ class RenderArgs(C.Structure):
         ("shard_rows", C.c_uint32), ("lens_mode", C.c_int32), ("lens_params", C.c_float * 7),
         ("camera_end", C.c_float * 12), ("rolling_shutter", C.c_float * 4),
         ("distortion_map", C.c_void_p), ("distortion_res", C.c_uint32 * 2),
+        ("render_aabb_to_local", C.c_float * 9), ("render_mode", C.c_int32), ("depth_scale", C.c_float),
+        ("gbuffer_hard_edges", C.c_int32), ("aperture_size", C.c_float), ("focus_z", C.c_float),
     ]
 
 
@@ -119,6 +121,8 @@ PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M
     GRADS_GRID_FIXED64 = range(9)
 SCRATCH_RAY_NUMSTEPS, SCRATCH_COORDS, SCRATCH_MLP_OUT, SCRATCH_RAY_COMPACTED, SCRATCH_DLOSS, SCRATCH_LOSS, \
     SCRATCH_COMPACT_COORDS, SCRATCH_RAY_EVALUATED, SCRATCH_VIOLATIONS = range(9)
+
+RENDER_SHADE, RENDER_AO, RENDER_NORMALS, RENDER_POSITIONS, RENDER_DEPTH, RENDER_COST, RENDER_SLICE = range(7)
 
 TIMERS = ["train_sampler", "train_encode", "train_mlp_infer", "train_loss", "train_mlp_bwd", "train_encode_bwd",
           "optimizer", "grid_update", "render_encode", "render_mlp", "render_march"]

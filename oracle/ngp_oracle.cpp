@@ -88,6 +88,8 @@ static V3 v(float x, float y, float z) { return {x, y, z}; }
 static V3 operator+(V3 a, V3 b) { return {a.x + b.x, a.y + b.y, a.z + b.z}; }
 static V3 operator-(V3 a, V3 b) { return {a.x - b.x, a.y - b.y, a.z - b.z}; }
 static V3 operator*(V3 a, float s) { return {a.x * s, a.y * s, a.z * s}; }
+static V3 operator+(V3 a, float s) { return {a.x + s, a.y + s, a.z + s}; }
+static V3 operator-(V3 a, float s) { return {a.x - s, a.y - s, a.z - s}; }
 static V3 operator/(V3 a, V3 b) { return {a.x / b.x, a.y / b.y, a.z / b.z}; }
 static float dot(V3 a, V3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
 static float len(V3 a) { return std::sqrt(dot(a, a)); }
@@ -116,6 +118,31 @@ struct Box {
 		*t1 = tmax;
 	}
 };
+
+// The render crop box in its local frame: local = R * world (Testbed::m_render_aabb_to_local,
+// nerf_device.cuh:475, src/testbed_nerf.cu:1467-1469); all-zero R = identity.
+struct RBox {
+	Box b;
+	float R[9];
+	bool rot = false;
+	V3 local(V3 p) const {
+		if (!rot) return p;
+		return V3{R[0] * p.x + R[1] * p.y + R[2] * p.z, R[3] * p.x + R[4] * p.y + R[5] * p.z, R[6] * p.x + R[7] * p.y + R[8] * p.z};
+	}
+	bool contains(V3 p) const { return b.contains(local(p)); }
+};
+static RBox rbox_of(const Box& b, const float* R) {
+	RBox r;
+	r.b = b;
+	bool any = false, ident = true;
+	for (int k = 0; k < 9; ++k) {
+		r.R[k] = R[k];
+		any |= R[k] != 0.0f;
+		ident &= R[k] == ((k % 4 == 0) ? 1.0f : 0.0f);
+	}
+	r.rot = any && !ident;
+	return r;
+}
 
 // ---------------------------------------------------------------------------
 // pcg32 (tcnn/pcg32.h; default_rng_t, random_val.cuh:26)
@@ -308,8 +335,9 @@ static bool sum_bit(const uint8_t* sm, uint32_t base, uint32_t b) { return (sm[b
 
 // First occupied lattice point at or after *n (render march); an empty cell is jumped over
 // only when the lattice point before the landing point is still inside it.
+template <class B>
 static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, const uint8_t* bits,
-                          const uint8_t* summary, uint32_t maxm, const Box& b) {
+                          const uint8_t* summary, uint32_t maxm, const B& b) {
 	float n = *n_io;
 	while (true) {
 		const float t = lat_from(st, n);
@@ -678,8 +706,9 @@ static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, con
 // NerfNetwork::backward_impl (nerf_network.h:189-268): rgb MLP bwd -> add_density_gradient -> density MLP bwd
 // dsh (optional, [n][16]): dL/d(SH inputs) of the sample's own row (÷ its rollover weight), for the
 // camera gradients (tcnn's input gradient through the Composite encoding's SH part)
-static void mlp_backward(Model& M, const uint16_t* P, const float* enc, const float* coords, uint32_t cs, uint32_t n,
-                         const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc, float* dsh = nullptr) {
+static void mlp_backward(const Model& M, float* grads, const uint16_t* P, const float* enc, const float* coords, uint32_t cs,
+                         uint32_t n, const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc,
+                         float* dsh = nullptr) {
 	const uint32_t NL = (uint32_t)M.layers.size();
 	std::vector<float> col(M.E);
 	Acts A;
@@ -693,7 +722,7 @@ static void mlp_backward(Model& M, const uint16_t* P, const float* enc, const fl
 			const Layer& Ly = M.layers[l];
 			const std::vector<float>& in = A.a[l];
 			const uint16_t* W = P + Ly.off;
-			float* G = M.grads.data() + Ly.off;
+			float* G = grads + Ly.off;
 			for (uint32_t r = 0; r < Ly.out; ++r)
 				for (uint32_t k = 0; k < Ly.in; ++k) G[(size_t)r * Ly.in + k] += delta[r] * in[k];
 			const uint32_t nin = (l == (int)M.n_density_layers) ? 16 : Ly.in;
@@ -1380,7 +1409,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	                  a.distortion_gradient_weight;
 	const bool cam = ext || dist;
 	std::vector<float> dsh(cam ? 16 * (size_t)C : 0), dpos(cam ? 3 * (size_t)C : 0);
-	mlp_backward(M, M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
+	mlp_backward(M, M.grads.data(), M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
 	             cam ? dsh.data() : nullptr);
 	if (cam) hg_input_grad(M, M.p16.data(), M.ccoords.data(), 8, C, denc.data(), wts.data(), dpos.data());
 	hg_backward(M, M.ccoords.data(), 8, C, denc.data());
@@ -1564,21 +1593,53 @@ static void grid_finish(Model& M, const ngp_grid_args& a) {
 }
 
 // ---- tracer (render_nerf, NerfTracer::trace; per ray, chunking-invariant) ---------------------
+// square2disk_shirley (random_val.cuh:112-128)
+static void disk_shirley(float a, float b, float* x, float* y) {
+	const float PI = 3.14159265358979323846f;
+	float phi, r;
+	if (a * a > b * b) {
+		r = a;
+		phi = (PI / 4.0f) * (b / a);
+	} else {
+		r = b;
+		phi = (PI / 2.0f) - (PI / 4.0f) * (a / b);
+	}
+	*x = r * std::cos(phi);
+	*y = r * std::sin(phi);
+}
+
+// d(raw density)/d(warped position) of one sample (network->input_gradient, the Normals mode's input;
+// src/testbed_nerf.cu:1715-1717): MLP backward from dL/dout = (0, 0, 0, 1), then the grid's input gradient
+static V3 density_gradient(const Model& M, const uint16_t* P, const float* coord, std::vector<float>& gscratch) {
+	std::vector<float> enc(M.L * M.F), denc(M.L * M.F);
+	hg_forward(M, P, coord, 8, 1, enc.data());
+	const float dl[4] = {0.0f, 0.0f, 0.0f, 1.0f};
+	mlp_backward(M, gscratch.data(), P, enc.data(), coord, 8, 1, dl, nullptr, denc.data());
+	float g[3];
+	hg_input_grad(M, P, coord, 8, 1, denc.data(), nullptr, g);
+	return v(g[0], g[1], g[2]);
+}
+
+// render_nerf (src/testbed_nerf.cu:1827-1987): per pixel, the NerfTracer march and composite of every
+// render mode but Distortion / EncodingVis, then shade_kernel_nerf; Slice evaluates one point per pixel.
 static void render(const Model& M, const ngp_render_args& a, float* frame, float* depthbuf) {
-	const Box box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])};
+	const RBox box = rbox_of(Box{v(a.aabb_min[0], a.aabb_min[1], a.aabb_min[2]), v(a.aabb_max[0], a.aabb_max[1], a.aabb_max[2])},
+	                         a.render_aabb_to_local);
 	const Box tbox{v(a.train_aabb_min[0], a.train_aabb_min[1], a.train_aabb_min[2]), v(a.train_aabb_max[0], a.train_aabb_max[1], a.train_aabb_max[2])};
 	const Cam cam = cam_of(a.camera);
 	const uint16_t* P = a.use_inference_params ? M.inf16.data() : M.p16.data();
 	const Stepping stp = make_stepping(a.cone_angle_constant);
 	const std::vector<uint8_t> summary = occ_summary(M.bits.data());
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
+	const int mode = a.render_mode;
+	const float aperture = mode == NGP_RENDER_MODE_SLICE ? 0.0f : a.aperture_size;
 	const uint32_t sc = std::max(a.shard_count, 1u), sr = std::max(a.shard_rows, 1u), si = a.shard_index % sc;
 	float ox, oy;
 	pixel_offset(a.snap_to_pixel_centers ? 0 : a.sample_index, &ox, &oy);
 	// rows are independent (the all-core CPU baseline); dynamic: rows differ in cost
 #pragma omp parallel
 	{
-	std::vector<float> enc(M.L * M.F), col(M.E), out(4);
+	std::vector<float> enc(M.L * M.F), col(M.E), out(4), gscratch(mode == NGP_RENDER_MODE_NORMALS ? M.n_mlp : 0);
 #pragma omp for schedule(dynamic, 1)
 	for (uint32_t y = 0; y < a.height; ++y) {
 		if ((y / sr) % sc != si) continue;
@@ -1604,17 +1665,45 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			                                                              a.rolling_shutter[3] * ldval(a.sample_index, idx * 72239731u, 0))
 			                   : cam;
 			d = rot(pc, d);
-			const V3 o = pc.c[3] + d * a.near_distance;
+			V3 o = pc.c[3];
+			if (aperture != 0.0f) {  // depth of field (uv_to_ray, common_device.cuh:450-456)
+				const V3 lookat = o + d * a.focus_z;
+				const uint32_t px = (uint32_t)(int)(u * (float)a.width), py = (uint32_t)(int)(vv * (float)a.height);
+				const uint32_t seed = px * 19349663u + py * 96925573u;
+				float dx, dy;
+				disk_shirley(ldval(a.sample_index, seed, 0) * 2.0f - 1.0f, ldval(a.sample_index, seed, 1) * 2.0f - 1.0f, &dx, &dy);
+				o = o + pc.c[0] * (aperture * dx) + pc.c[1] * (aperture * dy);
+				d = (lookat - o) * (1.0f / a.focus_z);
+			}
+			o = o + d * a.near_distance;
+			if (mode == NGP_RENDER_MODE_SLICE) {
+				// one point per pixel at camera depth focus_z, compute_nerf_rgba with depth 0.01, shade (Slice)
+				const V3 pos = o + d * a.focus_z;
+				const V3 dn = normalize(d);
+				const V3 w = tbox.rel(pos);
+				float coord[8] = {w.x, w.y, w.z, warp_dt(MIN_STEP), (dn.x + 1) * 0.5f, (dn.y + 1) * 0.5f, (dn.z + 1) * 0.5f, 0.0f};
+				hg_forward(M, P, coord, 8, 1, enc.data());
+				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data());
+				const float alpha = std::min(std::max(1.0f - std::exp(-to_density(out[3], dact) * 0.01f), 0.0f), 1.0f);
+				float c[4] = {to_rgb(out[0], ract) * alpha, to_rgb(out[1], ract) * alpha, to_rgb(out[2], ract) * alpha, alpha};
+				if (!a.train_in_linear_colors) for (int k = 0; k < 3; ++k) c[k] = s2l(c[k]);
+				for (int k = 0; k < 4; ++k) fb[k] = c[k];
+				depthbuf[idx] = a.focus_z;
+				continue;
+			}
 			d = normalize(d);
 			float t0, t1;
-			box.intersect(o, d, &t0, &t1);
+			box.b.intersect(box.local(o), box.local(d), &t0, &t1);
 			float t = std::max(t0, 0.0f) + 1e-6f;
 			if (!box.contains(o + d * t)) continue;
 			const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 			float n = lat_to(stp, t) + ldval(a.sample_index, idx * 786433u, 0);
 			if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), summary.data(), a.max_cascade, box)) continue;
 			float c[4] = {0, 0, 0, 0}, maxw = 0.0f, dep = 0.0f;
+			float cost = 0.0f;
+			uint32_t j = 0;
 			const V3 wd = v((d.x + 1) * 0.5f, (d.y + 1) * 0.5f, (d.z + 1) * 0.5f);
+			bool broke = false;
 			for (uint32_t step = 0; step < 10000; ++step) {
 				if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), summary.data(), a.max_cascade, box)) break;
 				const float t = lat_from(stp, n);
@@ -1628,19 +1717,58 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 				const float T = 1.0f - c[3];
 				const float alpha = 1.0f - std::exp(-to_density(out[3], dact) * unwarp_dt(coord[3]));
 				const float wgt = alpha * T;
-				c[0] += to_rgb(out[0], ract) * wgt;
-				c[1] += to_rgb(out[1], ract) * wgt;
-				c[2] += to_rgb(out[2], ract) * wgt;
+				V3 rgb = v(to_rgb(out[0], ract), to_rgb(out[1], ract), to_rgb(out[2], ract));
+				if (mode == NGP_RENDER_MODE_NORMALS) {
+					const V3 g = density_gradient(M, P, coord, gscratch) * -to_density_d(out[3], dact);
+					rgb = normalize(g);
+				} else if (mode == NGP_RENDER_MODE_POSITIONS) {
+					rgb = (pos - 0.5f) * 0.5f + 0.5f;
+				} else if (mode == NGP_RENDER_MODE_DEPTH) {
+					const float dv = dot(cam.c[2], pos - o) * a.depth_scale;
+					rgb = v(dv, dv, dv);
+				} else if (mode == NGP_RENDER_MODE_AO) {
+					rgb = v(alpha, alpha, alpha);
+				}
+				if (mode != NGP_RENDER_MODE_COST) {
+					c[0] += rgb.x * wgt;
+					c[1] += rgb.y * wgt;
+					c[2] += rgb.z * wgt;
+				}
 				c[3] += wgt;
 				if (wgt > maxw) { maxw = wgt; dep = dot(cam.c[2], pos - cam.c[3]); }
 				if (c[3] > 1.0f - a.min_transmittance) {
 					const float inv = 1.0f / c[3];
-					for (int k = 0; k < 4; ++k) c[k] *= inv;
+					if (mode != NGP_RENDER_MODE_COST) for (int k = 0; k < 3; ++k) c[k] *= inv;
+					c[3] *= inv;
+					broke = true;
 					break;
 				}
+				++j;
 			}
+			// Cost: the reference's payload.n_steps -- the index of the terminating sample, or every
+			// composited sample of a ray that left the volume (src/testbed_nerf.cu:664-667)
+			cost = (float)j;
+			(void)broke;
 			if (!(c[3] > 0.001f)) continue;  // compact_kernel_nerf drops near-transparent rays
-			if (!a.train_in_linear_colors) for (int k = 0; k < 3; ++k) c[k] = s2l(c[k]);
+			// shade_kernel_nerf (src/testbed_nerf.cu:1309-1349)
+			if (mode == NGP_RENDER_MODE_NORMALS) {
+				const V3 nn = normalize(v(c[0], c[1], c[2]));
+				c[0] = (0.5f * nn.x + 0.5f) * c[3];
+				c[1] = (0.5f * nn.y + 0.5f) * c[3];
+				c[2] = (0.5f * nn.z + 0.5f) * c[3];
+			} else if (mode == NGP_RENDER_MODE_COST) {
+				const float cc = cost / 128.0f;
+				c[0] = c[1] = c[2] = cc;
+				c[3] = 1.0f;
+			} else if (a.gbuffer_hard_edges && mode == NGP_RENDER_MODE_DEPTH) {
+				c[0] = c[1] = c[2] = dep * a.depth_scale;
+			} else if (a.gbuffer_hard_edges && mode == NGP_RENDER_MODE_POSITIONS) {
+				const V3 p3 = cam.c[3] + d * (dep / dot(d, cam.c[2]));
+				c[0] = (p3.x - 0.5f) * 0.5f + 0.5f;
+				c[1] = (p3.y - 0.5f) * 0.5f + 0.5f;
+				c[2] = (p3.z - 0.5f) * 0.5f + 0.5f;
+			}
+			if (!a.train_in_linear_colors && mode == NGP_RENDER_MODE_SHADE) for (int k = 0; k < 3; ++k) c[k] = s2l(c[k]);
 			for (int k = 0; k < 4; ++k) fb[k] = c[k];
 			if (c[3] > 0.2f) depthbuf[idx] = dep;
 		}
@@ -1852,7 +1980,7 @@ void oref_backward(void* m, const float* enc, const float* dirs, uint32_t n, con
 	Model& M = *static_cast<Model*>(m);
 	std::vector<float> coords(8 * (size_t)n, 0.0f);
 	for (uint32_t i = 0; i < n; ++i) for (int k = 0; k < 3; ++k) coords[8 * i + 4 + k] = dirs[3 * i + k];
-	mlp_backward(M, M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc);
+	mlp_backward(M, M.grads.data(), M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc);
 }
 void oref_encode_backward(void* m, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
 	hg_backward(*static_cast<Model*>(m), pos, stride, n, denc);
