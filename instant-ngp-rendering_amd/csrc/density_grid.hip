@@ -59,15 +59,21 @@ __global__ void __launch_bounds__(256) k_mark_untrained(uint32_t n_elements, flo
 			const v3 corner = pos + mk3((k & 1) ? voxel_size : 0.0f, (k & 2) ? voxel_size : 0.0f, (k & 4) ? voxel_size : 0.0f);
 			const v3 dir = normalize(corner - xf.c[3]);
 			if (dot(dir, xf.c[2]) < 1e-4f) continue;
-			// pos_to_uv (common_device.cuh:497-531), perspective
+			// pos_to_uv (common_device.cuh:497-531): camera frame, dir /= dir.z, the lens's distortion
 			const v3 rel = corner - xf.c[3];
-			v3 cd = mk3(dot(inv[0], rel), dot(inv[1], rel), dot(inv[2], rel));
-			cd = cd / cd.z;
-			const float u = cd.x * im.focal_length[0] / (float)im.width + im.principal_point[0];
-			const float v = cd.y * im.focal_length[1] / (float)im.height + im.principal_point[1];
-			// uv_to_ray back-projection check
-			v3 rd = mk3((u - im.principal_point[0]) * (float)im.width / im.focal_length[0],
-			            (v - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+			const v3 cd = mk3(dot(inv[0], rel), dot(inv[1], rel), dot(inv[2], rel));
+			float cx = cd.x / cd.z, cy = cd.y / cd.z;
+			float du = 0.0f, dv = 0.0f;
+			if (im.lens_mode == LENS_OPENCV) opencv_delta(im.lens_params, cx, cy, &du, &dv);
+			else if (im.lens_mode == LENS_OPENCV_FISHEYE) opencv_fisheye_delta(im.lens_params, cx, cy, &du, &dv);
+			cx += du;
+			cy += dv;
+			const float u = cx * im.focal_length[0] / (float)im.width + im.principal_point[0];
+			const float v = cy * im.focal_length[1] / (float)im.height + im.principal_point[1];
+			// uv_to_ray back-projection check (pos_to_uv is not injective under lens distortion)
+			v3 rd;
+			lens_direction(u, v, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
+			               im.principal_point[1], im.lens_mode, im.lens_params, &rd);
 			rd = normalize(rot(xf, rd));
 			if (length(rd - dir) < 1e-3f && u > 0.0f && v > 0.0f && u < 1.0f && v < 1.0f) {
 				++count;

@@ -1484,12 +1484,19 @@ static void mark_untrained(Model& M, const ngp_grid_args& a, uint32_t n_elem) {
 				const V3 corner = pos + v((k & 1) ? vs : 0, (k & 2) ? vs : 0, (k & 4) ? vs : 0);
 				const V3 dir = normalize(corner - x.c[3]);
 				if (dot(dir, x.c[2]) < 1e-4f) continue;
+				// pos_to_uv (common_device.cuh:497-531) with the lens's distortion, then the uv_to_ray check
 				const V3 rel = corner - x.c[3];
-				V3 cd = v(dot(bc * inv, rel), dot(ca * inv, rel), dot(ab * inv, rel));
-				cd = cd * (1.0f / cd.z);
-				const float u = cd.x * im.focal_length[0] / (float)im.width + im.principal_point[0];
-				const float vv = cd.y * im.focal_length[1] / (float)im.height + im.principal_point[1];
-				V3 rd = v((u - im.principal_point[0]) * (float)im.width / im.focal_length[0], (vv - im.principal_point[1]) * (float)im.height / im.focal_length[1], 1.0f);
+				const V3 cd = v(dot(bc * inv, rel), dot(ca * inv, rel), dot(ab * inv, rel));
+				float cx = cd.x / cd.z, cy = cd.y / cd.z;
+				float du = 0.0f, dv = 0.0f;
+				if (im.lens_mode == 1 || im.lens_mode == 4) lens_delta(im.lens_mode, im.lens_params, cx, cy, &du, &dv);
+				cx += du;
+				cy += dv;
+				const float u = cx * im.focal_length[0] / (float)im.width + im.principal_point[0];
+				const float vv = cy * im.focal_length[1] / (float)im.height + im.principal_point[1];
+				V3 rd;
+				lens_dir(u, vv, (float)im.width, (float)im.height, im.focal_length[0], im.focal_length[1], im.principal_point[0],
+				         im.principal_point[1], im.lens_mode, im.lens_params, &rd);
 				rd = normalize(rot(x, rd));
 				if (len(rd - dir) < 1e-3f && u > 0 && vv > 0 && u < 1 && vv < 1) { ++count; break; }
 			}

@@ -236,17 +236,29 @@ def test_bitfield_and_mean_bit_exact():
         g.close()
 
 
-@pytest.mark.parametrize("aabb_scale", [1, 64])
-def test_density_grid_update_matches_oracle(aabb_scale):
-    """update_density_grid_nerf (src/testbed_nerf.cu:2271-2379): mark_untrained, uniform then
-    occupancy-biased samples, splat (atomicMax), EMA, mean and bitfield with mips -- over one
-    cascade, and over the 7 of an aabb_scale-64 scene (config E)."""
-    g, o, rng = pair(dict(CFG_A, aabb_scale=aabb_scale))
+@pytest.mark.parametrize("cfg_kw,aabb_scale,lens", [(CFG_A, 1, 0), (CFG_A, 64, 0), (CFG_E, 64, 0), (CFG_A, 4, 1)],
+                         ids=["A-aabb1", "A-aabb64", "E-aabb64", "A-aabb4-opencv"])
+def test_density_grid_update_matches_oracle(cfg_kw, aabb_scale, lens):
+    """update_density_grid_nerf (src/testbed_nerf.cu:2271-2379): mark_untrained (pos_to_uv with the
+    lens's distortion + the uv_to_ray check, :74-145), uniform then occupancy-biased samples, splat
+    (atomicMax), EMA, mean and bitfield with mips -- over one cascade, over the 7 of an aabb_scale-64
+    scene with config A's and with config E's full network (L16 F2 T=2^22, 64-wide), and with an
+    OpenCV lens.  Exact: the untrained marks (same divisions and square roots on both sides).  Pinned
+    tolerance: the network's densities differ by fp16/MFMA rounding, so a cell whose step-1 value lies
+    within that tolerance of the occupancy threshold may be picked differently by the second step's
+    occupancy-biased sampler; only such cells (and the cells their samples land in) may differ, and
+    bitfield bits only there or where a density straddles the threshold within the tolerance."""
+    kw = dict(cfg_kw)
+    kw.pop("aabb_scale", None)
+    g, o, rng = pair(dict(kw, aabb_scale=aabb_scale))
     nc = int(np.log2(aabb_scale)) + 1
+    tol = lambda ref: 1e-6 + 1e-2 * np.abs(ref)
     try:
         imgs, cams, focal = make_views(6, 24, 24)
-        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        lm = (1, (0.06, -0.08, 0.001, -0.0005)) if lens else (0, ())  # OpenCV k1 k2 p1 p2 on every view
+        hd, dd = HostDataset(imgs, cams, focal, lens=lm), DeviceDataset(imgs, cams, focal, lens=lm)
         n0 = CELLS if nc == 1 else CELLS // 2  # the CPU oracle evaluates every sample
+        og1 = None
         for step, (nu, nn) in enumerate([(n0, 0), (n0 // 4, n0 // 4)]):
             ga = grid_args(dd.ptr, dd.n, nu, nn, ema_step=step, mark=int(step == 0), clear=int(step == 0),
                            aabb_scale=aabb_scale)
@@ -255,22 +267,29 @@ def test_density_grid_update_matches_oracle(aabb_scale):
             A.check(g.lib.ngp_density_grid_update(g.h, C.byref(ga), stream()))
             torch.cuda.synchronize()
             o.grid_update(oa)
+            if step == 0:
+                og1 = o.grid_get(CELLS * nc)[0].copy()
         gp, bp, _, mp = gpu_grid_buffers(g)
         gg = np.zeros(CELLS * nc, np.float32)
         cuda_memcpy_d2h(gg, gp)
         og, ob, om = o.grid_get(CELLS * nc)
-        # mark_untrained decisions, every cascade (a voxel corner projecting onto the image border
-        # can flip with the last ulp of the device's division / sqrt)
-        assert ((gg < 0) != (og < 0)).sum() <= max(1, gg.size // 1000000)
+        # mark_untrained decisions: exact, every cascade
+        np.testing.assert_array_equal(gg < 0, og < 0)
+        assert (og < 0).mean() > 0.001 and (og >= 0).mean() > 0.01
         if nc > 1:
             assert (og[CELLS:] < 0).mean() > 0.01 and (og[CELLS:] >= 0).mean() > 0.01
-        # a flipped cell changes which cell the occupancy-biased sampler picks for it: allow a
-        # handful of knock-on differences
-        bad = np.abs(gg - og) > 1e-6 + 1e-2 * np.abs(og)
-        assert bad.sum() <= max(0, 16 * ((gg < 0) != (og < 0)).sum()), bad.sum()
+        # cells the second step's sampler may pick differently: step-1 densities within the tolerance
+        # of its threshold (0.01, generate_grid_samples_nerf_nonuniform)
+        near = np.abs(og1 - 0.01) <= tol(og1)
+        bad = np.abs(gg - og) > tol(og)
+        assert bad.sum() <= 2 * near.sum(), (bad.sum(), near.sum())
         gb = np.zeros(CELLS // 8 * 8, np.uint8)
         cuda_memcpy_d2h(gb, bp)
-        assert (np.unpackbits(gb) == np.unpackbits(ob)).mean() > 0.999
+        diff_bits = (np.unpackbits(gb) != np.unpackbits(ob)).sum()
+        thresh = min(0.01, float(om))
+        straddle = (np.abs(og - thresh) <= tol(og)) | bad
+        # a straddling cell flips its own bit and at most one pooled bit per coarser mip
+        assert diff_bits <= straddle.sum() * nc, (diff_bits, straddle.sum())
     finally:
         g.close()
 
@@ -336,6 +355,39 @@ def test_render_floaters_matches_oracle(aabb_scale, cfg_kw):
         of, od = o.render(ra)
         assert (of[..., 3] > 0.01).mean() > 0.1
         assert ((gf[..., 3] > 0.01) != (of[..., 3] > 0.01)).mean() < 0.01
+        l1 = np.abs(gf - of).mean()
+        assert l1 < 1e-3, l1
+    finally:
+        g.close()
+
+
+def test_render_config_e_full_network_matches_oracle():
+    """Config E at full width (mip-nerf360/bicycle: L16 F2 T=2^22, 64-wide MLPs, aabb_scale 64, 7
+    cascades, cone angle 1/256): the render through the T=2^22 table, cascaded occupancy with
+    floaters in every cascade, against the oracle's point-by-point march."""
+    g, o, rng = pair(CFG_E, grid_scale=1.0)
+    try:
+        max_cascade = 6
+        grid = cascaded_grid(rng, max_cascade, density=0.004, core=0.2)
+        A.check(g.lib.ngp_density_grid_bitfield(g.h, max_cascade, stream()))  # sizes the grid for 7 cascades
+        torch.cuda.synchronize()
+        o.grid_set(grid)
+        o.grid_bitfield(max_cascade)
+        gp, _, _, _ = gpu_grid_buffers(g)
+        cuda_memcpy_h2d(gp, grid)
+        A.check(g.lib.ngp_density_grid_bitfield(g.h, max_cascade, stream()))
+        torch.cuda.synchronize()
+        W, H = 48, 40
+        cam = make_views(1, 8, 8)[1][0]
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        ra = render_args(W, H, cam, focal, spp=1, snap=0, aabb_scale=64)
+        frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+        depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+        A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
+        torch.cuda.synchronize()
+        gf = frame.cpu().numpy().reshape(H, W, 4)
+        of, od = o.render(ra)
+        assert (of[..., 3] > 0.01).mean() > 0.1
         l1 = np.abs(gf - of).mean()
         assert l1 < 1e-3, l1
     finally:
