@@ -275,7 +275,7 @@ def test_density_grid_update_matches_oracle(cfg_kw, aabb_scale, lens):
         og, ob, om = o.grid_get(CELLS * nc)
         # mark_untrained decisions: exact, every cascade
         np.testing.assert_array_equal(gg < 0, og < 0)
-        assert (og < 0).mean() > 0.001 and (og >= 0).mean() > 0.01
+        assert (og < 0).any() and (og >= 0).mean() > 0.01
         if nc > 1:
             assert (og[CELLS:] < 0).mean() > 0.01 and (og[CELLS:] >= 0).mean() > 0.01
         # cells the second step's sampler may pick differently: step-1 densities within the tolerance
