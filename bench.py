@@ -432,6 +432,14 @@ def main():
     }
     roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
     roofline["traffic"] = pmc_traffic(args.traffic_json, dom, units / launches)
+    if dom == "render_encode" and split["render_s"] > 0:
+        # the same algorithmic bytes over a whole frame: one frame's encode bytes / the frame's wall time
+        frame_s = split["render_s"] / args.steps
+        per_frame = work / args.steps
+        roofline["per_frame"] = {"bytes": round(per_frame), "frame_ms": round(1e3 * frame_s, 3),
+                                 "GB/s": round(per_frame / frame_s / 1e9, 1),
+                                 "frac": round(per_frame / frame_s / 1e9 / HBM_PEAK_GBS, 4),
+                                 "note": "algorithmic encode bytes of one 1080p frame / its render() wall time in HBM"}
 
     # render() as BASELINE.md:30 counts inference: the wall time of render(1920, 1080, spp) including the
     # read-back of the float frame to host memory (render_to_cpu, src/python_api.cu:124-202) -- here into

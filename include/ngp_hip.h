@@ -222,6 +222,12 @@ typedef struct ngp_train_args {
 	 * gradient buffer's precision, so the sparse skip sees the same zeros); 0: packed fp16 atomics as
 	 * tcnn's GridEncoding backward */
 	int32_t deterministic;
+	/* Testbed::m_max_level_rand_training (src/testbed_nerf.cu:724, 949, 2797, 2805; python_api.cu:527):
+	 * every training ray draws max_level = 2 u (after its pixel, before motionblur_time -- the same
+	 * pcg32 draw in the sampler and the loss pass) and the hash-grid levels l >= max_level * L (+1e-3)
+	 * of its samples encode to zero and receive no gradient (tcnn GridEncoding::set_max_level_gpu);
+	 * the value rides in the pad float of the sample's coordinate row.  0: all levels. */
+	int32_t max_level_rand_training;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {
@@ -327,6 +333,8 @@ typedef struct ngp_tuning {
 	uint32_t encode_dense_records;   /* render-site corner records of the dense levels: 0 on, 1 off */
 	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: 8 */
 	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics */
+	uint32_t encode_levels_per_thread; /* F = 2, L = 16 hash encoder: 2 = level pairs (g, 15 - g), pair g on XCD g
+	                                      (each XCD's L2 holds two levels' tables); 0 or 4: four strided levels */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

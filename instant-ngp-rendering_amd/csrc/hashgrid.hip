@@ -222,6 +222,10 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 	map_block(blockIdx.x, n_chunks, groups, &grp, &chunk0);
 	if (n_dev) n = min(n, *n_dev);
 	using VT = typename FeatVec<F>::T;
+	// LPT = 2: the level pair (g, L - 1 - g) -- a coarse and a fine level, so with L = 16 the eight
+	// pairs cost about the same and each XCD (map_block: XCD x runs pair x) keeps two levels' tables
+	// in its L2; else levels g, g + L/LPT, ...
+	auto level_of = [&](uint32_t q) { return LPT == 2 ? (q == 0 ? grp : lt.n_levels - 1u - grp) : grp + q * groups; };
 	// n_chunks per level group are launched; they stride over the chunks the count covers
 	for (uint32_t chunk = chunk0; chunk * 256u < n; chunk += n_chunks) {
 		const uint32_t i = chunk * 256u + threadIdx.x;
@@ -231,9 +235,14 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 		if (SITE == 1 && px < 0.0f) {
 #pragma unroll
 			for (uint32_t q = 0; q < LPT; ++q) o[q] = VT{};
+		} else if (SITE == 0 && lt.max_level) {
+			// levels above the sample's max level are zero (tcnn kernel_grid with max_level_gpu)
+#pragma unroll
+			for (uint32_t q = 0; q < LPT; ++q)
+				o[q] = lt.level_cut(level_of(q), i) ? VT{} : encode_one<F, QUAD>(level_of(q), px, py, pz, table, lt);
 		} else {
 #pragma unroll
-			for (uint32_t q = 0; q < LPT; ++q) o[q] = encode_one<F, QUAD>(grp + q * groups, px, py, pz, table, lt);
+			for (uint32_t q = 0; q < LPT; ++q) o[q] = encode_one<F, QUAD>(level_of(q), px, py, pz, table, lt);
 		}
 		if constexpr (LPT == 4) {
 			if (lay.lsh == 2) {
@@ -245,7 +254,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 			}
 		}
 #pragma unroll
-		for (uint32_t q = 0; q < LPT; ++q) reinterpret_cast<VT*>(enc)[lay.vec(grp + q * groups, i)] = o[q];
+		for (uint32_t q = 0; q < LPT; ++q) reinterpret_cast<VT*>(enc)[lay.vec(level_of(q), i)] = o[q];
 	}
 }
 
@@ -362,13 +371,14 @@ __device__ __forceinline__ void hashgrid_bwd_chunk(uint32_t n, uint32_t level, u
 	using VT = typename FeatVec<F>::T;
 	float g[F];
 	bool active = i < n;
-	if (active) {
+	if (active && !lt.level_cut(level, i)) {
 		unpack<F>(reinterpret_cast<const VT*>(denc)[lay.vec(level, i)], g);
 		bool any = false;
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
 		active = any;
 	} else {
+		active = false;
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) g[f] = 0.0f;
 	}
@@ -470,7 +480,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_input_grad(uint32_t n, const f
 		bool any = false;
 #pragma unroll
 		for (uint32_t f = 0; f < F; ++f) any |= g[f] != 0.0f;
-		if (!any) continue;
+		if (!any || lt.level_cut(level, i)) continue;
 		const float scale = lt.scale[level];
 		const uint32_t res = lt.res[level], size = lt.size[level];
 		const VT* tab = reinterpret_cast<const VT*>(table + (size_t)lt.offset[level] * F);
@@ -584,7 +594,10 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 	// F = 2: 16-B quad gathers, four levels per thread (l, l + L/4, ...) where L % 4 == 0, else one
 	// (8-B pair gathers and two levels per thread measured slower)
 	if (lt.F == 2) {
-		if (lt.n_levels % 4 == 0)
+		if (lt.pairs && lt.n_levels == 16)
+			launch_timed(k_hashgrid_fwd<2, SITE, true, 2>, n_chunks * 8, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane,
+			             n_chunks, n_dev);
+		else if (lt.n_levels % 4 == 0)
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 4>, n_chunks * lt.n_levels / 4, 256, 0, s, n, pos, stride, table, lt, enc,
 			             enc_plane, n_chunks, n_dev);
 		else

@@ -242,7 +242,10 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->render_generate_block == 0 || t->render_generate_block == 256 || t->render_generate_block == 512,
 		        "render_generate_block must be 0, 256 or 512");
 		require(t->mlp_workgroups_per_cu <= 32, "mlp_workgroups_per_cu must be <= 32");
+		require(t->encode_levels_per_thread == 0 || t->encode_levels_per_thread == 2 || t->encode_levels_per_thread == 4,
+		        "encode_levels_per_thread must be 0, 2 or 4");
 		m->tuning = *t;
+		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
 	});
 }
 

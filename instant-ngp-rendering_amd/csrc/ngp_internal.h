@@ -142,6 +142,25 @@ struct LevelTable {
 	// z <= res, holds the entries of corners (x, y, z), (x+1, y, z), (x, y+1, z), (x+1, y+1, z)
 	const uint4* rec = nullptr;
 	uint32_t rec_off[MAX_LEVELS];
+	// optional per-sample max level (tcnn GridEncoding::set_max_level_gpu; training with
+	// max_level_rand_training): sample i's value at max_level[i * ml_stride]; levels at or above
+	// max_level * L + 1e-3 encode to zero and get no gradient.  null: all levels.
+	const float* max_level = nullptr;
+	uint32_t ml_stride = 0;
+	// F = 2, L = 16: encode level pairs (g, 15 - g), pair g on XCD g (ngp_tuning.encode_levels_per_thread = 2)
+	uint32_t pairs = 0;
+	__host__ __device__ bool level_cut(uint32_t level, uint32_t i) const {
+		if (!max_level) return false;
+		// tcnn: max_level = (max_level_gpu[i] * num_grid_features) / N_FEATURES_PER_LEVEL; level >= max_level + 1e-3f
+		const float ml = (max_level[(size_t)i * ml_stride] * (float)(n_levels * F)) / (float)F;
+		return (float)level >= ml + 1e-3f;
+	}
+	LevelTable with_max_level(const float* p, uint32_t stride) const {
+		LevelTable t = *this;
+		t.max_level = p;
+		t.ml_stride = stride;
+		return t;
+	}
 };
 
 // Layout of an fp16 encoding buffer (n samples, L levels, F features).

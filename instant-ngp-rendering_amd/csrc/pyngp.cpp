@@ -37,7 +37,8 @@ static py::array_t<float> pinned_frame(int height, int width) {
 	NGP_TUNING_FIELD(render_first_steps) NGP_TUNING_FIELD(render_max_steps) NGP_TUNING_FIELD(render_lag)             \
 	NGP_TUNING_FIELD(render_budget_scale) NGP_TUNING_FIELD(render_block_skipping)                                    \
 	NGP_TUNING_FIELD(render_composite_block) NGP_TUNING_FIELD(render_generate_block)                                 \
-	NGP_TUNING_FIELD(encode_dense_records) NGP_TUNING_FIELD(mlp_workgroups_per_cu) NGP_TUNING_FIELD(debug)
+	NGP_TUNING_FIELD(encode_dense_records) NGP_TUNING_FIELD(mlp_workgroups_per_cu) NGP_TUNING_FIELD(debug)                          \
+	NGP_TUNING_FIELD(encode_levels_per_thread)
 
 namespace {
 
@@ -549,6 +550,7 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("deterministic", &Testbed::deterministic,
 		               "Bit-reproducible training steps: hash-grid gradients summed in 64-bit fixed point "
 		               "(ngp_train_args.deterministic) instead of fp16 atomics")
+		.def_readwrite("max_level_rand_training", &Testbed::m_max_level_rand_training)
 		.def_property_readonly("distributed", &Testbed::distributed)
 		// ngp_tuning (include/ngp_hip.h) as a dict; unknown keys are an error, missing keys keep their value
 		.def("get_tuning",

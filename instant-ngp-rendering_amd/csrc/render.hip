@@ -1105,10 +1105,33 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
 	const LevelTable lt_render = build_dense_records(m, table, s);
+	// joins the pipeline streams back to s, also when a throw leaves this function early (work the
+	// caller enqueues on s next shares the frame, dense records and scratch with them)
+	struct StreamJoin {
+		RenderScratch& rs;
+		hipStream_t s;
+		uint32_t n = 1;
+		void join() {
+			for (uint32_t j = 1; j < n; ++j) {
+				NGP_HIP_CHECK(hipEventRecord(rs.join[j], rs.streams[j]));
+				NGP_HIP_CHECK(hipStreamWaitEvent(s, rs.join[j], 0));
+			}
+			n = 1;
+		}
+		~StreamJoin() {
+			for (uint32_t j = 1; j < n; ++j) {
+				if (hipEventRecord(rs.join[j], rs.streams[j]) == hipSuccess) (void)hipStreamWaitEvent(s, rs.join[j], 0);
+				else (void)hipStreamSynchronize(rs.streams[j]);
+			}
+		}
+	} joiner{rs, s};
 	if (n_pipes > 1) {
 		for (uint32_t j = 1; j < n_pipes; ++j) NGP_HIP_CHECK(hipMemsetAsync(rs.pipe[j].counters.ptr, 0, 8 * sizeof(uint32_t), s));
 		NGP_HIP_CHECK(hipEventRecord(rs.fork, s));
-		for (uint32_t j = 1; j < n_pipes; ++j) NGP_HIP_CHECK(hipStreamWaitEvent(rs.streams[j], rs.fork, 0));
+		for (uint32_t j = 1; j < n_pipes; ++j) {
+			NGP_HIP_CHECK(hipStreamWaitEvent(rs.streams[j], rs.fork, 0));
+			joiner.n = j + 1;
+		}
 	}
 	const size_t lds = k.df ? 0 : (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
 	for (uint32_t j = 0; j < n_pipes; ++j) {
@@ -1271,10 +1294,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			                                              reinterpret_cast<float4*>(frame), depth_buffer);
 		NGP_HIP_CHECK(hipGetLastError());
 	}
-	for (uint32_t j = 1; j < n_pipes; ++j) {
-		NGP_HIP_CHECK(hipEventRecord(rs.join[j], rs.streams[j]));
-		NGP_HIP_CHECK(hipStreamWaitEvent(s, rs.join[j], 0));
-	}
+	joiner.join();
 	if (debug) {
 		uint32_t d[8];
 		NGP_HIP_CHECK(hipMemcpyAsync(d, dbg, sizeof(d), hipMemcpyDeviceToHost, s));

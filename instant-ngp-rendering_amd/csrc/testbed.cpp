@@ -1120,6 +1120,7 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 		a.allreduce_user = this;
 	}
 	a.deterministic = deterministic ? 1 : 0;
+	a.max_level_rand_training = m_max_level_rand_training ? 1 : 0;
 	for (int k = 0; k < 3; ++k) { a.aabb_min[k] = aabb_min[k]; a.aabb_max[k] = aabb_max[k]; }
 	a.cone_angle_constant = nerf.cone_angle_constant;
 	a.max_cascade = nerf.max_cascade;

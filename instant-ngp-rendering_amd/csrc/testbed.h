@@ -240,6 +240,9 @@ public:
 	bool distributed() const { return m_comm != nullptr || (bool)m_host_allreduce; }
 	// deterministic hash-grid gradients (ngp_train_args.deterministic): bit-reproducible steps
 	bool deterministic = false;
+	// m_max_level_rand_training (testbed.h:704; src/testbed_nerf.cu:724, 949, 2797-2805): per-ray random
+	// hash-grid max level during training
+	bool m_max_level_rand_training = false;
 	int world_size() const { return m_world; }
 
 	ngp_model* model() const { return m_model; }

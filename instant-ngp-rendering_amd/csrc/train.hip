@@ -138,6 +138,7 @@ struct SamplerArgs {
 	Stepping st;
 	uint32_t max_mip;
 	int snap;
+	int max_level_rand;  // max_level_rand_training: a per-ray max level draw (src/testbed_nerf.cu:724)
 	ErrorCdf cdf;  // error-map importance sampling (null pointers: uniform)
 	const uint8_t* bitfield;
 	uint32_t* numsteps;  // [R][2]
@@ -187,9 +188,11 @@ __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint
 }
 
 // Shared by both passes: image, pixel and ray of global ray gi (testbed_nerf.cu:712-777);
-// *n0 = first lattice point (stepping space) = entry + jitter.
+// *n0 = first lattice point (stepping space) = entry + jitter; *max_level = the ray's hash-grid
+// max level (2 u with max_level_rand_training, drawn before motionblur_time; else 0 = unused).
 template <bool GENERAL>
-__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0) {
+__device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0,
+                                             float* max_level = nullptr) {
 	pcg32 rng = a.rng;
 	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
 	float u, v;
@@ -198,6 +201,8 @@ __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, 
 	float rgba[4];
 	texel_rgba(read_texel(im, u, v), rgba);
 	if (rgba[0] < 0.0f) return false;
+	const float ml = a.max_level_rand ? rng.next_float() * 2.0f : 0.0f;
+	if (max_level) *max_level = ml;
 	const float motionblur_time = rng.next_float();
 	m43 xf = load_xform(im.xform);
 	if (GENERAL && (im.rolling_shutter[0] != 0.0f || im.rolling_shutter[1] != 0.0f || im.rolling_shutter[2] != 0.0f ||
@@ -330,8 +335,8 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 		return;
 	}
 	v3 o, d;
-	float n0;
-	training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0);
+	float n0, max_level;
+	training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0, &max_level);
 	if (lane == 0) {
 		a.numsteps[2 * i + 0] = n;
 		a.numsteps[2 * i + 1] = base;
@@ -355,7 +360,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 				float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + r));
 				const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
 				c[0] = pd;
-				c[1] = make_float4(wdir.x, wdir.y, wdir.z, 0.0f);
+				c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);  // the pad float carries the max level
 				a.pos4[base + r] = pd;
 			}
 		}
@@ -541,6 +546,7 @@ struct LossArgs {
 	pcg32 rng;
 	aabb3 aabb;
 	int snap;
+	int max_level_rand;
 	int loss_type;
 	int random_bg;
 	v3 bg;
@@ -717,6 +723,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	const uint32_t img =
 	    training_pixel<GENERAL>(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v, &pdf, &uv_pdf);
 	const ngp_image im = a.images[img];
+	if (a.max_level_rand) rng.advance(1);  // max_level (testbed_nerf.cu:949)
 	rng.advance(1);  // motionblur_time
 	v3 bg = a.bg;
 	if (a.random_bg) {
@@ -1359,6 +1366,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.st = make_stepping(t->cone_angle_constant);
 	sa.max_mip = t->max_cascade;
 	sa.snap = t->snap_to_pixel_centers;
+	sa.max_level_rand = t->max_level_rand_training != 0;
 	sa.cdf = ErrorCdf{t->cdf_x_cond_y, t->cdf_y, t->cdf_img, t->cdf_res[0], t->cdf_res[1]};
 	sa.bitfield = m->gs.bitfield.ptr;
 	sa.numsteps = ts.ray_numsteps.ptr;
@@ -1390,6 +1398,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// every emitted sample as the reference does (full_forward), or chunk by chunk up to each
 	// ray's stop (k_train_chunk) -- the loss kernels read the same outputs either way
 	const bool chunk_off = t->full_forward != 0;
+	const bool ml_on = sa.max_level_rand != 0;  // hash-grid levels cut per sample (set_max_level_gpu)
+	const LevelTable lt_c = ml_on ? m->lt.with_max_level(ts.ccoords.ptr + 7, 8) : m->lt;  // compacted rows
 	const __half* table = m->params16.ptr + m->n_mlp_params;
 	const __half* enc_rows = ts.enc.ptr;
 	EncLayout enc_layout = internal_layout(m, MS);
@@ -1397,7 +1407,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.chunked = !chunk_off;
 	if (chunk_off) {
 		tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
-		launch_hashgrid_fwd(m->lt, ts.pos4.ptr, 4, MS, table, ts.enc.ptr, enc_layout, s, ts.counters.ptr + 4, 0);
+		launch_hashgrid_fwd(ml_on ? m->lt.with_max_level(ts.coords.ptr + 7, 8) : m->lt, ts.pos4.ptr, 4, MS, table, ts.enc.ptr,
+		                    enc_layout, s, ts.counters.ptr + 4, 0);
 		tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 		tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
 		launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, enc_layout, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
@@ -1451,7 +1462,9 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
 			// chunk p's rows start at sample off[p] of every plane
 			__half* eenc_p = ts.eenc.ptr + ((size_t)off[p] * F << m->enc_lsh);
-			launch_hashgrid_fwd(m->lt, ts.epos.ptr + 4 * (size_t)off[p], 4, cap[p], table, eenc_p, internal_layout(m, MSE), s,
+			// max_level_rand_training: the max level rides in the direction row's pad float
+			const LevelTable lt_p = ml_on ? m->lt.with_max_level(ts.edir.ptr + 4 * (size_t)off[p] + 3, 4) : m->lt;
+			launch_hashgrid_fwd(lt_p, ts.epos.ptr + 4 * (size_t)off[p], 4, cap[p], table, eenc_p, internal_layout(m, MSE), s,
 			                    c.rows, 0, max_chunks);
 			tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 			tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
@@ -1473,6 +1486,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.rng = sa.rng;
 	la.aabb = sa.aabb;
 	la.snap = t->snap_to_pixel_centers;
+	la.max_level_rand = sa.max_level_rand;
 	la.cdf = sa.cdf;
 	la.error_map = t->error_map;
 	la.exposure = t->exposure;
@@ -1598,13 +1612,13 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
 	// data parallel: launched for about this rank's share of the global batch (blocks loop past it)
 	const uint32_t bwd_chunks = world > 1 ? div_up(B / world + B / (4 * world), 128u) + 16 : 0u;
-	launch_hashgrid_bwd(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->grid_grads16.ptr, s,
+	launch_hashgrid_bwd(lt_c, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->grid_grads16.ptr, s,
 	                    ts.counters.ptr + 5, ts.fixed ? m->grid_grads64.ptr : nullptr, bwd_chunks);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	if (cam) {
 		// input gradients of the compacted samples (Trainer::training_step with dL_dinput), then
 		// compute_cam_gradient_train_nerf per ray
-		launch_hashgrid_input_grad(m->lt, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->params16.ptr + m->n_mlp_params,
+		launch_hashgrid_input_grad(lt_c, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->params16.ptr + m->n_mlp_params,
 		                           ts.cweight.ptr, ts.dpos.ptr, s, ts.counters.ptr + 5);
 		CamGradArgs ca{};
 		ca.n_rays = R;

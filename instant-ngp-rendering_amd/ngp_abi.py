@@ -68,6 +68,7 @@ class TrainArgs(C.Structure):
         ("distortion_gradient_weight", C.c_void_p),
         ("rank", C.c_uint32), ("world_size", C.c_uint32), ("allreduce_i32", C.c_void_p), ("allreduce_user", C.c_void_p),
         ("deterministic", C.c_int32),
+        ("max_level_rand_training", C.c_int32),
     ]
 
 
@@ -113,6 +114,7 @@ class Tuning(C.Structure):
         ("render_budget_scale", C.c_float), ("render_block_skipping", C.c_uint32),
         ("render_composite_block", C.c_uint32), ("render_generate_block", C.c_uint32),
         ("encode_dense_records", C.c_uint32), ("mlp_workgroups_per_cu", C.c_uint32), ("debug", C.c_uint32),
+        ("encode_levels_per_thread", C.c_uint32),
     ]
 
 

@@ -536,13 +536,26 @@ static void hg_corners(const Model& M, uint32_t l, const float* p, uint32_t idx[
 		w[c] = ww;
 	}
 }
+// tcnn GridEncoding::set_max_level_gpu (kernel_grid / kernel_grid_backward): sample i's levels at or
+// above max_level * (L F) / F + 1e-3 are zero and get no gradient; ml = null: all levels
+static bool hg_cut(const Model& M, const float* ml, uint32_t ml_stride, uint32_t i, uint32_t l) {
+	if (!ml) return false;
+	const float mlv = (ml[(size_t)i * ml_stride] * (float)(M.L * M.F)) / (float)M.F;
+	return (float)l >= mlv + 1e-3f;
+}
+
 // enc: [L][n][F] (fp16-rounded floats)
-static void hg_forward(const Model& M, const uint16_t* params, const float* pos, uint32_t stride, uint32_t n, float* enc) {
+static void hg_forward(const Model& M, const uint16_t* params, const float* pos, uint32_t stride, uint32_t n, float* enc,
+                       const float* ml = nullptr, uint32_t ml_stride = 0) {
 	const uint16_t* tab = params + M.n_mlp;
 	// samples are independent (the all-core CPU baseline; 1 thread unless oref_set_threads)
 #pragma omp parallel for schedule(static)
 	for (uint32_t i = 0; i < n; ++i)
 		for (uint32_t l = 0; l < M.L; ++l) {
+			if (hg_cut(M, ml, ml_stride, i, l)) {
+				for (uint32_t f = 0; f < M.F; ++f) enc[((size_t)l * n + i) * M.F + f] = 0.0f;
+				continue;
+			}
 			uint32_t idx[8];
 			float w[8];
 			hg_corners(M, l, pos + (size_t)i * stride, idx, w);
@@ -553,13 +566,14 @@ static void hg_forward(const Model& M, const uint16_t* params, const float* pos,
 			}
 		}
 }
-static void hg_backward(Model& M, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
+static void hg_backward(Model& M, const float* pos, uint32_t stride, uint32_t n, const float* denc, const float* ml = nullptr,
+                        uint32_t ml_stride = 0) {
 	float* g = M.grads.data() + M.n_mlp;
 	for (uint32_t i = 0; i < n; ++i)
 		for (uint32_t l = 0; l < M.L; ++l) {
 			bool any = false;
 			for (uint32_t f = 0; f < M.F; ++f) any |= denc[((size_t)l * n + i) * M.F + f] != 0.0f;
-			if (!any) continue;
+			if (!any || hg_cut(M, ml, ml_stride, i, l)) continue;
 			uint32_t idx[8];
 			float w[8];
 			hg_corners(M, l, pos + (size_t)i * stride, idx, w);
@@ -572,7 +586,7 @@ static void hg_backward(Model& M, const float* pos, uint32_t stride, uint32_t n,
 // dL/d(position) through the grid (tcnn GridEncoding input gradient, linear interpolation):
 // dL/dx_d = sum_l scale_l sum_c (c_d ? 1 : -1) prod_{e != d} w_e sum_f dL/denc[l][f] table[c][f]; ÷ weight
 static void hg_input_grad(const Model& M, const uint16_t* params, const float* pos, uint32_t stride, uint32_t n,
-                          const float* denc, const float* weight, float* dpos) {
+                          const float* denc, const float* weight, float* dpos, const float* ml = nullptr, uint32_t ml_stride = 0) {
 	const uint16_t* tab = params + M.n_mlp;
 	for (uint32_t i = 0; i < n; ++i) {
 		float g3[3] = {0.0f, 0.0f, 0.0f};
@@ -580,7 +594,7 @@ static void hg_input_grad(const Model& M, const uint16_t* params, const float* p
 		for (uint32_t l = 0; l < M.L; ++l) {
 			bool any = false;
 			for (uint32_t f = 0; f < M.F; ++f) any |= denc[((size_t)l * n + i) * M.F + f] != 0.0f;
-			if (!any) continue;
+			if (!any || hg_cut(M, ml, ml_stride, i, l)) continue;
 			float fr[3];
 			uint32_t gc[3];
 			for (int d = 0; d < 3; ++d) {
@@ -1023,7 +1037,7 @@ static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, P
 // first lattice point n0 = to_stepping_space(t_entry) + random; t_entry and the random offset
 // are returned too (the literal transcription below starts from them).
 static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st, float* t_entry = nullptr,
-                      float* jitter = nullptr, float* dlen = nullptr) {
+                      float* jitter = nullptr, float* dlen = nullptr, float* max_level = nullptr) {
 	Pcg rng;
 	rng.state = a.rng_state;
 	rng.inc = a.rng_inc;
@@ -1033,6 +1047,9 @@ static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o,
 	float rgba[4];
 	rgba_of(texel(im, u, vv), rgba);
 	if (rgba[0] < 0.0f) return false;
+	// max_level_rand_training (src/testbed_nerf.cu:724): drawn before motionblur_time
+	const float ml = a.max_level_rand_training ? rng.nextf() * 2.0f : 0.0f;
+	if (max_level) *max_level = ml;
 	const float mb = rng.nextf();  // motionblur_time
 	Cam x = cam_of(im.xform);
 	if (rs_on(im.rolling_shutter))
@@ -1155,11 +1172,11 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	// pass 1: count (testbed_nerf.cu:779-799)
 	std::vector<uint32_t> cnt(R, 0);
 	std::vector<V3> ro(R), rd(R);
-	std::vector<float> rst(R), rdl(R, 1.0f);
+	std::vector<float> rst(R), rdl(R, 1.0f), rml(R, 0.0f);
 	for (uint32_t i = 0; i < R; ++i) {
 		V3 o, d;
 		float t;
-		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t, nullptr, nullptr, &rdl[i])) continue;
+		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t, nullptr, nullptr, &rdl[i], &rml[i])) continue;
 		ro[i] = o; rd[i] = d; rst[i] = t;
 		cnt[i] = training_walk(stp, box, M.bits.data(), a.max_cascade, o, d, t, STEPS,
 		                       [](uint32_t, uint32_t, float, float, V3) {});
@@ -1188,14 +1205,15 @@ static void train_step(Model& M, const ngp_train_args& a) {
 			              const V3 w = box.rel(pos);
 			              float* c = &M.coords[8 * (size_t)(b + j)];
 			              c[0] = w.x; c[1] = w.y; c[2] = w.z; c[3] = warp_dt(dt);
-			              c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = 0.0f;
+			              c[4] = wd.x; c[5] = wd.y; c[6] = wd.z; c[7] = rml[i];  // pad: the ray's max level
 		              });
 	}
 	M.total_samples = base;
 	const uint32_t S = std::min(base, MS);
 	// inference over the emitted samples with the training params (testbed_nerf.cu:2800-2802)
 	std::vector<float> enc((size_t)M.L * S * M.F), out(4 * (size_t)S);
-	hg_forward(M, M.p16.data(), M.coords.data(), 8, S, enc.data());
+	const bool ml_on = a.max_level_rand_training != 0;
+	hg_forward(M, M.p16.data(), M.coords.data(), 8, S, enc.data(), ml_on ? M.coords.data() + 7 : nullptr, 8);
 	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data());
 	M.mlp_out.assign(4 * (size_t)a.max_samples, 0);
 	for (size_t k = 0; k < out.size(); ++k) M.mlp_out[k] = f2h(out[k]);
@@ -1251,6 +1269,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		ray_uv[2 * i] = u;
 		ray_uv[2 * i + 1] = vv;
 		const ngp_image& im = a.images[img];
+		if (a.max_level_rand_training) rng.advance(1);  // max_level (src/testbed_nerf.cu:949)
 		rng.advance(1);
 		V3 bg = v(a.background_color[0], a.background_color[1], a.background_color[2]);
 		if (a.random_bg_color) {
@@ -1411,8 +1430,9 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	std::vector<float> dsh(cam ? 16 * (size_t)C : 0), dpos(cam ? 3 * (size_t)C : 0);
 	mlp_backward(M, M.grads.data(), M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
 	             cam ? dsh.data() : nullptr);
-	if (cam) hg_input_grad(M, M.p16.data(), M.ccoords.data(), 8, C, denc.data(), wts.data(), dpos.data());
-	hg_backward(M, M.ccoords.data(), 8, C, denc.data());
+	const float* cml = ml_on ? M.ccoords.data() + 7 : nullptr;
+	if (cam) hg_input_grad(M, M.p16.data(), M.ccoords.data(), 8, C, denc.data(), wts.data(), dpos.data(), cml, 8);
+	hg_backward(M, M.ccoords.data(), 8, C, denc.data(), cml, 8);
 	if (cam) {
 		// compute_cam_gradient_train_nerf (src/testbed_nerf.cu:1163-1269), extrinsics part
 		const V3 diag = box.mx - box.mn;

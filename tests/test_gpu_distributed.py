@@ -231,7 +231,10 @@ def test_two_ranks_train_like_one_process_with_twice_the_batch(scene):
             # (whose gradients are exact) to the rounding the MLP differences feed through
             np.testing.assert_array_equal(d["params"], res[0][step]["params"])
             np.testing.assert_allclose(d["params"][:n_mlp], s["params"][:n_mlp], rtol=1e-3, atol=1e-6)
-            np.testing.assert_allclose(d["params"][n_mlp:], s["params"][n_mlp:], rtol=1e-3, atol=1e-6)
+            # step 2 runs on step-1 MLP weights that differ in association: a grid gradient sum close to zero
+            # can change sign, and Adam's early steps turn that into a full step (lr) of the other sign
+            far = ~np.isclose(d["params"][n_mlp:], s["params"][n_mlp:], rtol=1e-3, atol=1e-6)
+            assert far.mean() < 5e-3, (step, far.mean())
     # after the first step the hash-grid parameters are bit-identical (integer-summed gradients, the
     # same Adam step); the step-1 MLP gradients only differ in association
     np.testing.assert_array_equal(res[0][1]["params"][n_mlp:], single[1]["params"][n_mlp:])
@@ -288,15 +291,20 @@ def test_deterministic_steps_are_bit_reproducible(scene):
     bit-identical (fixed-point hash-grid gradients, fixed-order MLP reductions).  The default
     fp16-atomic mode trains the same scene to the same loss; its parameters are not comparable
     element-wise (Adam turns the rounding of near-zero gradient sums into full-size steps of either
-    sign), so only the first step -- whose gradients differ by fp16 rounding alone -- is compared."""
+    sign), so only the first step is compared: where both modes move a parameter, Adam's first update
+    (lr * sign(g)) has the same sign.  The modes do differ in WHICH parameters move: fp16 atomics round
+    every run of corner contributions to fp16, so sums of contributions below the fp16 subnormal range
+    vanish (the optimizer's sparse skip then leaves the parameter alone), while the fixed-point sum keeps
+    them until its single rounding."""
     torch.cuda.set_device(0)
     runs, first, losses = [], [], []
     for det in (True, True, False):
         tb = _testbed(scene)
         tb.deterministic = det
         tb.shall_train = True
+        init = _params(tb)
         tb.frame()
-        first.append(_params(tb))
+        first.append(_params(tb) - init)
         while tb.training_step < 100:
             tb.frame()
         runs.append(_params(tb))
@@ -304,8 +312,9 @@ def test_deterministic_steps_are_bit_reproducible(scene):
         n_mlp = _n_mlp(tb)
         del tb
     np.testing.assert_array_equal(runs[0], runs[1])
-    # one step: Adam's first update is lr * sign(g) where g != 0 -- the sign agrees except for sums that
-    # fp16 rounding moves across zero
-    d = first[0] != first[2]
-    assert d[:n_mlp].mean() < 1e-3 and d[n_mlp:].mean() < 1e-2, (d[:n_mlp].mean(), d[n_mlp:].mean())
+    np.testing.assert_array_equal(first[0], first[1])
+    both = (first[0] != 0) & (first[2] != 0)
+    assert both[:n_mlp].mean() > 0.5 and both[n_mlp:].sum() > 1000
+    agree = np.sign(first[0][both]) == np.sign(first[2][both])
+    assert agree.mean() > 0.99, agree.mean()
     assert losses[2] == pytest.approx(losses[0], rel=0.1)

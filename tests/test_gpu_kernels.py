@@ -57,6 +57,10 @@ def test_hashgrid_indices_and_features_bit_exact(name):
         ge = g.encode(pos).astype(np.float32)
         oe = o.encode(pos)
         np.testing.assert_array_equal(ge, oe)
+        if CONFIGS[name]["n_levels"] == 16 and CONFIGS[name]["F"] == 2:
+            # the level-pair encoder (ngp_tuning.encode_levels_per_thread = 2) computes the same features
+            g.set_tuning(encode_levels_per_thread=2)
+            np.testing.assert_array_equal(g.encode(pos).astype(np.float32), oe)
     finally:
         g.close()
 

@@ -75,13 +75,18 @@ def cascaded_grid(rng, max_cascade, density=0.01, core=0.3):
     return grid
 
 
-@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B, CFG_E], ids=["A", "B", "E"])
+@pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B, CFG_E, dict(CFG_B, max_level_rand=1)],
+                         ids=["A", "B", "E", "B-max-level-rand"])
 def test_train_step_matches_oracle(cfg_kw):
     """generate_training_samples_nerf + network + compute_loss_kernel_train_nerf + backward.  E:
     aabb_scale 64 (7 cascades, cone angle 1/256, T=2^22): mip_from_dt and the jumps past empty
-    cells (advance_to_next_voxel) at every cascade."""
+    cells (advance_to_next_voxel) at every cascade.  max_level_rand_training (testbed_nerf.cu:724,
+    949, 2797-2805): the per-ray max level draw shifts the ray's later random numbers (pixel jitter,
+    background), is stored bit-exact with every sample, and cuts the levels above it in the
+    forward and the backward (tcnn set_max_level_gpu)."""
     cfg_kw = dict(cfg_kw)
     aabb_scale = cfg_kw.pop("aabb_scale", 1)
+    max_level_rand = cfg_kw.pop("max_level_rand", 0)
     g, o, rng = pair(dict(cfg_kw, aabb_scale=aabb_scale))
     try:
         imgs, cams, focal = make_views(6, 24, 24)
@@ -92,6 +97,7 @@ def test_train_step_matches_oracle(cfg_kw):
         R, B, MS = 384, 4096, 1 << 15
         ga = train_args(dd.ptr, dd.n, R, B, MS, aabb_scale=aabb_scale)
         oa = train_args(hd.ptr, hd.n, R, B, MS, aabb_scale=aabb_scale)
+        ga.max_level_rand_training = oa.max_level_rand_training = max_level_rand
         g.zero_grads()
         A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
         torch.cuda.synchronize()
@@ -110,8 +116,11 @@ def test_train_step_matches_oracle(cfg_kw):
         for n, b in o_ns:
             owned[b:b + n] = True
         assert owned.sum() > 1000
-        g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
-        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7][owned]
+        g_c = gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7 + max_level_rand][owned]
+        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS, :7 + max_level_rand][owned]
+        if max_level_rand:
+            ml = o_c[:, 7]
+            assert 0 <= ml.min() and ml.max() < 2 and (ml < 1).mean() > 0.2  # some samples lose levels
         if aabb_scale == 1:
             np.testing.assert_array_equal(g_c, o_c)
         else:
@@ -390,6 +399,12 @@ def test_render_config_e_full_network_matches_oracle():
         assert (of[..., 3] > 0.01).mean() > 0.1
         l1 = np.abs(gf - of).mean()
         assert l1 < 1e-3, l1
+        # the level-pair encoder (ngp_tuning.encode_levels_per_thread = 2) renders the same frame bit for bit
+        g.set_tuning(encode_levels_per_thread=2)
+        frame.zero_()
+        A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(frame.cpu().numpy().reshape(H, W, 4), gf)
     finally:
         g.close()
 
