@@ -335,6 +335,12 @@ typedef struct ngp_tuning {
 	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics */
 	uint32_t encode_levels_per_thread; /* F = 2, L = 16 hash encoder: 2 = level pairs (g, 15 - g), pair g on XCD g
 	                                      (each XCD's L2 holds two levels' tables); 0 or 4: four strided levels */
+	uint32_t encode_streaming;       /* hash encoder cache hints: bit 0 non-temporal encoding stores (F = 2 planes),
+	                                    bit 1 non-temporal position loads, bit 2 sc1 encoding stores
+	                                    (the line leaves the L2); 0: none */
+	uint32_t render_network;         /* 1: the renderer's fused hash encoding + MLP kernel (F = 2, L = 16); 2: separate
+	                                    encoder and MLP launches; 0: the default */
+	uint32_t render_net_workgroups_per_cu; /* fused render kernel workgroups per CU; 0: 4 */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

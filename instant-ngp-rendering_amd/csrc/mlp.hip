@@ -25,6 +25,7 @@
 
 #include <cstring>
 
+#include "encode_device.h"
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -657,6 +658,80 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 }
 
 // ---------------------------------------------------------------------------
+// Fused render network (renderer, F = 2, L = 16): the hash encoding and the register-resident MLP
+// in one persistent kernel.  The separate encoder writes 64 B of features per sample that the MLP
+// reads back (12 GB per 1080p frame of the bench scene, streaming through the L2s that hold the
+// hash table); here they stay on chip.  A workgroup of RN_WAVES waves takes 16 * RN_WAVES samples
+// per round: wave w computes plane w % 4 (levels p, p + 4, p + 8, p + 12 -- the encoder's own
+// encode_one, so the features are bit-identical) of 64 samples, one sample per lane, into LDS;
+// after a barrier wave w runs the 16-sample tile w through the MLP (rf_tile), lane (g, n) taking
+// plane g of sample n as its B operand -- exactly the plane layout the first layer's K order was
+// packed for.  Other workgroups' MFMAs overlap a workgroup's gathers on the same CU.
+// ---------------------------------------------------------------------------
+struct EncIn {
+	const float4* pos;    // [n] warped position + dt (x < 0: a reserved slot the ray did not fill)
+	const __half* table;  // the encoding's fp16 parameters
+	LevelTable lt;        // F = 2, L = 16 (dense-level corner records when built)
+};
+
+constexpr int RN_WAVES = 8;
+constexpr int RN_BLOCK = RN_WAVES * 64;
+constexpr int RN_SAMPLES = 16 * RN_WAVES;
+
+template <class N>
+__global__ void __launch_bounds__(RN_BLOCK) k_render_net(MlpArgs a, EncIn e) {
+	static_assert(N::KE == 1 && N::Wp <= 64, "one 32-row K step of encoding inputs (L * F = 32)");
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	constexpr int NF = N::fwd_frags();
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	h8* w = reinterpret_cast<h8*>(smem);                                        // [frag][lane]
+	uint4* planes = reinterpret_cast<uint4*>(smem + (size_t)NF * 64 * sizeof(h8));  // [2][RN_SAMPLES][4]
+	{
+		const h8* src = reinterpret_cast<const h8*>(a.frags + N::rfwd_off(0));
+		for (int t = threadIdx.x; t < NF * 64; t += RN_BLOCK) w[t] = src[t];
+	}
+	__syncthreads();
+	const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+	const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+	const uint32_t plane = wave & 3u, half = wave >> 2;  // encode: plane of samples [64 half, 64 half + 64)
+	const h8* wl = w + lane;
+	const uint32_t rounds = (a.n + RN_SAMPLES - 1) / RN_SAMPLES;
+	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.sh_ray, a.coord_bytes);
+	const __amdgpu_buffer_rsrc_t sh_rs = make_rsrc(a.sh, a.sh_bytes);
+	uint32_t buf = 0;
+	for (uint32_t r = blockIdx.x; r < rounds; r += gridDim.x, buf ^= 1u) {
+		const uint32_t base = r * RN_SAMPLES;
+		RawTile<N, 1> cur;
+		// this wave's MLP tile: samples base + 16 wave + n; the SH row indices first
+		cur.ri[0] = __builtin_amdgcn_raw_buffer_load_b32(crd_rs, 4 * (base + 16 * wave + n), 0, 0);
+		{
+			const uint32_t i = base + 64 * half + lane;
+			uint4 v = make_uint4(0u, 0u, 0u, 0u);
+			if (i < a.n) {
+				const float4 p = e.pos[i];
+				if (p.x >= 0.0f) {
+					v.x = encode_one<2, true>(plane, p.x, p.y, p.z, e.table, e.lt);
+					v.y = encode_one<2, true>(plane + 4u, p.x, p.y, p.z, e.table, e.lt);
+					v.z = encode_one<2, true>(plane + 8u, p.x, p.y, p.z, e.table, e.lt);
+					v.w = encode_one<2, true>(plane + 12u, p.x, p.y, p.z, e.table, e.lt);
+				}
+			}
+			planes[((size_t)buf * RN_SAMPLES + 64 * half + lane) * 4 + plane] = v;
+		}
+		sh_load<N, 1>(sh_rs, g, cur);
+		// every plane of the round is in LDS (the other buffer is the next round's: a wave still in
+		// this round's MLP never races the next round's writes, which follow the next barrier)
+		__syncthreads();
+		const uint4 pv = planes[((size_t)buf * RN_SAMPLES + 16 * wave + n) * 4 + g];
+		cur.e[0][0] = pv.x;
+		cur.e[0][1] = pv.y;
+		cur.e[0][2] = pv.z;
+		cur.e[0][3] = pv.w;
+		rf_tile<N, 1, 1, false, true>(a, wl, cur, base + 16 * wave, g, n);
+	}
+}
+
+// ---------------------------------------------------------------------------
 // Training: forward (activations kept), dgrad chain, wgrad via transposed reads.
 // ---------------------------------------------------------------------------
 template <class N, int l>
@@ -1201,6 +1276,40 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		else if (a.F == 2 && !pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 2>, grid, BLOCK, lds, s, a);
 		else if (a.F == 4 && !pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 4>, grid, BLOCK, lds, s, a);
 		else launch_timed(k_mlp_infer_rf<N, 1, 2, false, 0>, grid, BLOCK, lds, s, a);
+	});
+	NGP_HIP_CHECK(hipGetLastError());
+}
+
+bool render_net_supported(const ngp_model* m) {
+	bool ok = m->lt.F == 2 && m->lt.n_levels == 16 && m->enc_lsh == 2;
+	if (ok) NGP_DISPATCH(m->mlp_variant, ok = N::KE == 1 && N::Wp <= 64);
+	return ok;
+}
+
+void launch_render_net(const ngp_model* m, const __half* frags, const LevelTable& lt, const __half* table, const float* posdt,
+                       uint32_t n, __half* out, hipStream_t s, const uint32_t* n_dev, const __half* sh, const uint32_t* sh_ray,
+                       uint32_t sh_rows) {
+	if (n == 0) return;
+	if (!render_net_supported(m)) throw std::runtime_error("launch_render_net: needs F = 2, L = 16 and the plane layout");
+	MlpArgs a = base_args(m);
+	a.frags = frags;
+	a.n = n;
+	a.out = out;
+	a.n_dev = n_dev;
+	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * 4, 0xffffffffu);
+	a.sh = sh;
+	a.sh_ray = sh_ray;
+	a.sh_bytes = (uint32_t)std::min<uint64_t>((uint64_t)sh_rows * 32, 0xffffffffu);
+	a.out_mode = 0;
+	a.out_stride = 4;
+	EncIn e{reinterpret_cast<const float4*>(posdt), table, lt};
+	NGP_DISPATCH(m->mlp_variant, {
+		if constexpr (N::KE == 1 && N::Wp <= 64) {
+			const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2 + 2 * RN_SAMPLES * 4 * sizeof(uint4);
+			const uint32_t wg_per_cu = m->tuning.render_net_workgroups_per_cu ? m->tuning.render_net_workgroups_per_cu : 4u;
+			const uint32_t grid = std::min<uint32_t>(div_up(n, RN_SAMPLES), cu_count() * wg_per_cu);
+			launch_timed(k_render_net<N>, grid, RN_BLOCK, lds, s, a, e);
+		}
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }

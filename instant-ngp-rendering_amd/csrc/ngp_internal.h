@@ -149,6 +149,8 @@ struct LevelTable {
 	uint32_t ml_stride = 0;
 	// F = 2, L = 16: encode level pairs (g, 15 - g), pair g on XCD g (ngp_tuning.encode_levels_per_thread = 2)
 	uint32_t pairs = 0;
+	// ngp_tuning.encode_streaming: bit 0 non-temporal encoding stores, bit 1 non-temporal position loads
+	uint32_t streaming = 0;
 	__host__ __device__ bool level_cut(uint32_t level, uint32_t i) const {
 		if (!max_level) return false;
 		// tcnn: max_level = (max_level_gpu[i] * num_grid_features) / N_FEATURES_PER_LEVEL; level >= max_level + 1e-3f
@@ -425,6 +427,11 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr,
                       uint32_t out_mode = 0, uint32_t out_stride = 4, const uint32_t* sh_ray = nullptr, uint32_t sh_rows = 0);
+// The renderer's fused encoding + network (k_render_net): F = 2, L = 16, the plane layout, one K step
+bool render_net_supported(const ngp_model* m);
+void launch_render_net(const ngp_model* m, const __half* frags, const LevelTable& lt, const __half* table, const float* posdt,
+                       uint32_t n, __half* out, hipStream_t s, const uint32_t* n_dev, const __half* sh, const uint32_t* sh_ray,
+                       uint32_t sh_rows);
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
 // dsh (optional): [n][16] dL/d(SH inputs of the rgb network), of the sample's own row (divided

@@ -1039,6 +1039,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.budget = !(tu.render_budget_scale < 0.0f);
 	k.budget_scale = tu.render_budget_scale > 0.0f ? tu.render_budget_scale : 1.0f;
 	const bool block_skipping = tu.render_block_skipping != 0;
+	// the fused encoding + network kernel where it applies (Normals needs the encodings for its backward)
+	const bool fused = tu.render_network == 1 && k.mode != NGP_RENDER_MODE_NORMALS && render_net_supported(m);
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
 	for (uint32_t j = 1; j < n_pipes; ++j) {
@@ -1068,7 +1070,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH row indices, then
 		// [rays][8]: one row of 16 fp16 SH inputs per alive ray
 		ps.coords.reserve(5 * pr.max_samples + 8 * (size_t)pr.n);
-		ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
+		if (!fused) ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
 		if (!ps.host_counter.ptr) {
@@ -1209,13 +1211,20 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			}
 		}
 #endif
-		launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
-		                    internal_layout(m, n_elements), ps, samples, 1);
-		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
-		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
-		launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
-		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, pr.n);
-		tm.end(NGP_TIMER_RENDER_MLP, ps);
+		if (fused) {
+			// one kernel: encoding + network (k_render_net), the features never leave the CU
+			launch_render_net(m, frags, lt_render, table, reinterpret_cast<const float*>(pr.posdt), n_elements, pr.ps->out.ptr, ps,
+			                  samples, reinterpret_cast<const __half*>(pr.shrows), pr.sray, pr.n);
+			tm.end(NGP_TIMER_RENDER_ENCODE, ps);
+		} else {
+			launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
+			                    internal_layout(m, n_elements), ps, samples, 1);
+			tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
+			tm.begin_kernel(NGP_TIMER_RENDER_MLP);
+			launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
+			                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, pr.n);
+			tm.end(NGP_TIMER_RENDER_MLP, ps);
+		}
 		if (pr.k.mode == NGP_RENDER_MODE_NORMALS) {
 			// Normals (NerfTracer::trace, testbed_nerf.cu:1715-1717, network->input_gradient): the gradient of
 			// the raw density w.r.t. the warped position of every sample -- the fused MLP backward from

@@ -114,7 +114,8 @@ class Tuning(C.Structure):
         ("render_budget_scale", C.c_float), ("render_block_skipping", C.c_uint32),
         ("render_composite_block", C.c_uint32), ("render_generate_block", C.c_uint32),
         ("encode_dense_records", C.c_uint32), ("mlp_workgroups_per_cu", C.c_uint32), ("debug", C.c_uint32),
-        ("encode_levels_per_thread", C.c_uint32),
+        ("encode_levels_per_thread", C.c_uint32), ("encode_streaming", C.c_uint32),
+        ("render_network", C.c_uint32), ("render_net_workgroups_per_cu", C.c_uint32),
     ]
 
 

@@ -399,12 +399,15 @@ def test_render_config_e_full_network_matches_oracle():
         assert (of[..., 3] > 0.01).mean() > 0.1
         l1 = np.abs(gf - of).mean()
         assert l1 < 1e-3, l1
-        # the level-pair encoder (ngp_tuning.encode_levels_per_thread = 2) renders the same frame bit for bit
-        g.set_tuning(encode_levels_per_thread=2)
-        frame.zero_()
-        A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
-        torch.cuda.synchronize()
-        np.testing.assert_array_equal(frame.cpu().numpy().reshape(H, W, 4), gf)
+        # the level-pair encoder (ngp_tuning.encode_levels_per_thread = 2), the separate encoder + MLP launches
+        # and the fused encoding + network kernel (render_network 2 / 1) render the same frame bit for bit
+        for kw in (dict(encode_levels_per_thread=2), dict(encode_levels_per_thread=0, render_network=2),
+                   dict(render_network=1)):
+            g.set_tuning(**kw)
+            frame.zero_()
+            A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
+            torch.cuda.synchronize()
+            np.testing.assert_array_equal(frame.cpu().numpy().reshape(H, W, 4), gf, err_msg=str(kw))
     finally:
         g.close()
 

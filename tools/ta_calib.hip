@@ -49,8 +49,8 @@ __global__ void __launch_bounds__(256) k_gather(const uint4* __restrict__ tab, u
 			const uint32_t h = mix(tid * 131u + (uint32_t)(it + u) * 0x9e3779b9u);
 			uint32_t slot16;  // 16-B slot index
 			if (MODE == 0) slot16 = h & mask16;
-			else if (MODE == 1) slot16 = ((mix((tid >> 4) * 977u + (uint32_t)(it + u)) & mask16) & ~3u) + ((lane & 15u) * W) / 16u;
-			else slot16 = ((mix((tid >> 6) * 977u + (uint32_t)(it + u)) & mask16) & ~63u) + (lane * W) / 16u;
+			else if (MODE == 1) slot16 = ((mix((tid >> 4) * 977u + (uint32_t)(it + u)) & mask16) & ~(uint32_t)(W - 1)) + ((lane & 15u) * W) / 16u;
+			else slot16 = ((mix((tid >> 6) * 977u + (uint32_t)(it + u)) & mask16) & ~(uint32_t)(4 * W - 1)) + (lane * W) / 16u;
 			off[u] = slot16 * 16u + (MODE == 0 ? 0u : ((lane * W) % 16u));
 		}
 		if (on) {
@@ -69,6 +69,11 @@ __global__ void __launch_bounds__(256) k_gather(const uint4* __restrict__ tab, u
 		}
 	}
 	if (acc == 0x12345678u) sink[0] = acc;
+}
+
+// XCD of every workgroup (HW_REG_XCC_ID, bits 3:0): checks the round-robin placement the encoders assume
+__global__ void k_xcc(uint32_t* __restrict__ out) {
+	if (threadIdx.x == 0) out[blockIdx.x] = (uint32_t)__builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20) & 15u;
 }
 
 template <int W, int MODE, int ACTIVE>
@@ -108,6 +113,20 @@ int main() {
 	CK(hipMalloc(&tab, big));
 	CK(hipMalloc(&sink, 64));
 	CK(hipMemset(tab, 1, big));
+	{
+		const int nb = 8192;
+		uint32_t* xd;
+		CK(hipMalloc(&xd, nb * 4));
+		k_xcc<<<nb, 64>>>(xd);
+		uint32_t h[nb];
+		CK(hipMemcpy(h, xd, sizeof(h), hipMemcpyDeviceToHost));
+		CK(hipFree(xd));
+		int same = 0;  // blocks b, b + 8 on one XCD
+		for (int b = 0; b + 8 < nb; ++b) same += h[b] == h[b + 8];
+		printf("xcc of blocks 0..15:");
+		for (int b = 0; b < 16; ++b) printf(" %u", h[b]);
+		printf("   blocks b, b+8 on the same XCD: %d of %d\n", same, nb - 8);
+	}
 	for (size_t tb : {2ull << 20, 32ull << 20}) {
 		run<4, 0, 64>("gather  4B random, 64 lanes", tab, tb, sink, cus, clk);
 		run<8, 0, 64>("gather  8B random, 64 lanes", tab, tb, sink, cus, clk);
