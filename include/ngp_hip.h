@@ -337,7 +337,7 @@ typedef struct ngp_tuning {
 	                                      (each XCD's L2 holds two levels' tables); 0 or 4: four strided levels */
 	uint32_t encode_streaming;       /* hash encoder cache hints: bit 0 non-temporal encoding stores (F = 2 planes),
 	                                    bit 1 non-temporal position loads, bit 2 sc1 encoding stores
-	                                    (the line leaves the L2); 0: none */
+	                                    (the line leaves the L2); 0: the default (bit 0); 128: none */
 	uint32_t render_network;         /* 1: the renderer's fused hash encoding + MLP kernel (F = 2, L = 16); 2: separate
 	                                    encoder and MLP launches; 0: the default */
 	uint32_t render_net_workgroups_per_cu; /* fused render kernel workgroups per CU; 0: 4 */

@@ -55,6 +55,13 @@ static void require(bool cond, const char* msg) {
 
 static hipStream_t S(ngp_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
+// ngp_tuning.encode_streaming: 0 = the default (non-temporal encoding stores: -2 % render frame
+// time, tools/render_ab.py), bit 7 = no hints
+static uint32_t encode_streaming_bits(const ngp_tuning& t) {
+	if (t.encode_streaming == 0) return 1u;
+	return t.encode_streaming & 127u;
+}
+
 // tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.
 static void build_level_table(ngp_model* m) {
 	const ngp_network_config& c = m->cfg;
@@ -79,6 +86,7 @@ static void build_level_table(ngp_model* m) {
 		offset += params;
 	}
 	m->n_grid_params = (uint64_t)offset * lt.F;
+	lt.streaming = encode_streaming_bits(m->tuning);
 }
 
 static void build_layers(ngp_model* m) {
@@ -248,7 +256,7 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->render_net_workgroups_per_cu <= 16, "render_net_workgroups_per_cu must be <= 16");
 		m->tuning = *t;
 		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
-		m->lt.streaming = t->encode_streaming;
+		m->lt.streaming = encode_streaming_bits(*t);
 	});
 }
 
