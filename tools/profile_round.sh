@@ -6,7 +6,7 @@ OUT=$PWD/gpurun_out/prof_$R
 mkdir -p "$OUT"
 REPO=$PWD
 export TMPDIR=/tmp
-STEPS="--steps 10 --warmup 3 --pretrain 1500 --cpu-baseline 0"
+STEPS="--steps 10 --warmup 3 --pretrain 1500 --cpu-baseline 0 --surface-scene 0 --render-to-cpu 0"
 tools/fetch_calib.sh > "$OUT/fetch_calib.log" 2>&1 || exit $?
 cp gpurun_out/fetch_calib/fetch_calib.json "$OUT/fetch_calib.json"
 cd /tmp
