@@ -341,6 +341,8 @@ typedef struct ngp_tuning {
 	uint32_t render_network;         /* 1: the renderer's fused hash encoding + MLP kernel (F = 2, L = 16); 2: separate
 	                                    encoder and MLP launches; 0: the default */
 	uint32_t render_net_workgroups_per_cu; /* fused render kernel workgroups per CU; 0: 4 */
+	uint32_t train_chain_walk;       /* 1: the training sampler walks the reference's voxel-jump chain also at
+	                                    aabb_scale 1 (0: the octant distance fields there; same samples) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -427,6 +427,9 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr,
                       uint32_t out_mode = 0, uint32_t out_stride = 4, const uint32_t* sh_ray = nullptr, uint32_t sh_rows = 0);
+// render.hip: the octant distance fields of the bitfield's mips [0, max_mip] into m->rs.df (rebuilt only
+// when the bitfield changed); the renderer's march and the training sampler (aabb_scale 1) read them
+void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s);
 // The renderer's fused encoding + network (k_render_net): F = 2, L = 16, the plane layout, one K step
 bool render_net_supported(const ngp_model* m);
 void launch_render_net(const ngp_model* m, const __half* frags, const LevelTable& lt, const __half* table, const float* posdt,

@@ -743,6 +743,50 @@ NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir,
 	return LATTICE_SKIPPED;
 }
 
+// The training sampler's walk through the octant distance fields, for aabb_scale 1 (one mip: there
+// the reference's advance_to_next_voxel chain, src/testbed_nerf.cu:779-795, samples exactly the
+// occupied lattice points inside the AABB, since a jump only ever leaves an empty cell).  Lattice
+// point n0 + k with k an integer offset, so sample positions are step_from(n0 + k) bit for bit as the
+// chain walk computes them: occupied -> OCCUPIED; outside the AABB -> EXIT; empty -> SKIPPED with *k
+// moved past the far faces of the cell's empty D-box, the jump verified (as in lattice_step_df) on
+// the exact lattice point before the landing one.
+NGP_HD int train_step_df(uint32_t* k_io, float n0, const Stepping& st, v3 o, v3 d, v3 idir, uint32_t oct, const uint8_t* df,
+                         const aabb3& aabb) {
+	const uint32_t k = *k_io;
+	const float n = n0 + (float)k;
+	const float t = step_from(st, n);
+	const v3 pos = o + d * t;
+	if (!aabb_contains(aabb, pos)) return LATTICE_EXIT;
+	int cx, cy, cz;
+	if (!cascaded_cell_at(pos, 0, &cx, &cy, &cz)) {
+		*k_io = k + 1u;
+		return LATTICE_SKIPPED;
+	}
+	const uint32_t D = df[df_index(0, oct, cx, cy, cz)];
+	if (D == 0u) return LATTICE_OCCUPIED;
+	const float res = (float)NERF_GRIDSIZE, inv_res = 1.0f / (float)NERF_GRIDSIZE;
+	const v3 p = (pos - 0.5f) * res;  // cell coordinates - 64
+	const float fd = (float)D;
+	const float fx = d.x < 0.0f ? (float)(cx - 64) + 1.0f - fd : (float)(cx - 64) + fd;
+	const float fy = d.y < 0.0f ? (float)(cy - 64) + 1.0f - fd : (float)(cy - 64) + fd;
+	const float fz = d.z < 0.0f ? (float)(cz - 64) + 1.0f - fd : (float)(cz - 64) + fd;
+	const float exit = fmaxf(fminf(fminf((fx - p.x) * idir.x, (fy - p.y) * idir.y), (fz - p.z) * idir.z) * inv_res, 0.0f);
+	const float n_far = step_to(st, t + exit);
+	uint32_t c = (uint32_t)fminf(ceilf(fmaxf(n_far - n, 0.5f)), 1048576.0f);
+	if (c > 1u) {
+		const v3 last = o + d * step_from(st, n0 + (float)(k + c - 1u));
+		if (aabb_contains(aabb, last)) {
+			int qx, qy, qz;
+			const bool in_grid = cascaded_cell_at(last, 0, &qx, &qy, &qz);
+			const int ex = d.x < 0.0f ? cx - qx : qx - cx, ey = d.y < 0.0f ? cy - qy : qy - cy, ez = d.z < 0.0f ? cz - qz : qz - cz;
+			const int lim = (int)D - 1;
+			if (!in_grid || ex < 0 || ex > lim || ey < 0 || ey > lim || ez < 0 || ez > lim) c = 1u;
+		}
+	}
+	*k_io = k + c;
+	return LATTICE_SKIPPED;
+}
+
 NGP_HD bool next_occupied_lattice_point(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
                                         const uint8_t* summary, uint32_t max_mip, const RenderBox& aabb, OccCache& cache) {
 	while (true) {

@@ -429,7 +429,7 @@ __global__ void __launch_bounds__(256) k_df_yz(const uint8_t* __restrict__ fin, 
 	(void)x;
 }
 
-static void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s) {
+void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s) {
 	RenderScratch& rs = m->rs;
 	if (rs.df_version == m->gs.version && rs.df_max_mip == max_mip) return;
 	const size_t nm = max_mip + 1;

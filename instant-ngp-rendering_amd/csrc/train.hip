@@ -149,6 +149,7 @@ struct SamplerArgs {
 	float4* pos4;        // [max]: pos + warped dt again, 16-B rows the encoder reads once per level
 	const float* dmap;   // learned distortion map [dry][drx][2] (null: off; general instance only)
 	uint32_t drx, dry;
+	const uint8_t* df;   // octant distance fields of mip 0 (aabb_scale 1 only; null: the jump chain)
 };
 
 // Image and pixel of global training ray gi from its pcg32 stream (already advanced to
@@ -292,6 +293,36 @@ __device__ __forceinline__ unsigned long long training_walk_batch(const LatticeP
 	return samp;
 }
 
+// aabb_scale 1 (a.df set): the ray's samples are the occupied lattice points inside the AABB (see
+// train_step_df), found 64 lattice points per round with the empty space between them crossed
+// through the octant distance fields -- a surface scene's rays cross most of the volume empty, one
+// voxel per jump in the chain walk.  visit(rank, k) for every sample in order (rank < cap); returns
+// the ray's sample count, capped.
+template <class Visit>
+__device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3 idir, float n0, uint32_t cap, uint32_t lane,
+                                            Visit visit) {
+	const uint32_t oct = ray_octant(d);
+	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+	uint32_t kb = 0, j = 0;
+	while (true) {  // wave-uniform: one ray per wave
+		uint32_t k = kb + lane;
+		const int st = train_step_df(&k, n0, a.st, o, d, idir, oct, a.df, a.aabb);
+		const unsigned long long m_exit = __ballot(st == LATTICE_EXIT), m_occ = __ballot(st == LATTICE_OCCUPIED);
+		// an all-empty round goes on from the last lane's verified skip
+		const uint32_t k_next = (uint32_t)__builtin_amdgcn_readlane((int)(st == LATTICE_SKIPPED ? k : kb + 64u), 63);
+		const uint32_t fe = m_exit ? (uint32_t)(__ffsll((long long)m_exit) - 1) : 64u;
+		const unsigned long long emit = m_occ & (fe >= 64 ? ~0ull : ((1ull << fe) - 1ull));
+		if ((emit >> lane) & 1ull) {
+			const uint32_t r = j + __popcll(emit & below);
+			if (r < cap) visit(r, kb + lane);
+		}
+		j += __popcll(emit);
+		if (j >= cap) return cap;
+		if (m_exit) return j;
+		kb = k_next;
+	}
+}
+
 // pass 1: count the ray's samples (<= NERF_STEPS), one wave per ray.
 template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
@@ -301,7 +332,11 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	v3 o, d;
 	float n0;
 	uint32_t count = 0;
-	if (training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0)) {
+	if (!training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0)) {
+	} else if (a.df) {
+		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+		count = df_walk(a, o, d, idir, n0, NERF_STEPS, lane, [](uint32_t, uint32_t) {});
+	} else {
 		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		bool exited = false;
 		for (uint32_t kb = 0, cur = 0; !exited; kb += 64, cur -= 64) {
@@ -346,6 +381,21 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	}
 	const v3 wdir = warp_direction(d);
 	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	if (a.df) {
+		df_walk(a, o, d, idir, n0, n, lane, [&](uint32_t r, uint32_t k) {
+			// the chain walk's training_lattice_point for lattice point k, bit for bit
+			const float nk = n0 + (float)k;
+			const float t = step_from(a.st, nk);
+			const float dt = step_from(a.st, nk + 1.0f) - t;
+			const v3 wp = aabb_relative(a.aabb, o + d * t);
+			float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + r));
+			const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+			c[0] = pd;
+			c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);
+			a.pos4[base + r] = pd;
+		});
+		return;
+	}
 	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 	uint32_t j = 0;
 	bool exited = false;
@@ -1367,6 +1417,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.max_mip = t->max_cascade;
 	sa.snap = t->snap_to_pixel_centers;
 	sa.max_level_rand = t->max_level_rand_training != 0;
+	// aabb_scale 1: cross empty space through the octant distance fields (shared with the renderer,
+	// rebuilt when the bitfield changed); the chain walk otherwise
+	if (t->max_cascade == 0 && m->tuning.train_chain_walk == 0) {
+		build_distance_fields(m, 0, s);
+		sa.df = m->rs.df.ptr;
+	}
 	sa.cdf = ErrorCdf{t->cdf_x_cond_y, t->cdf_y, t->cdf_img, t->cdf_res[0], t->cdf_res[1]};
 	sa.bitfield = m->gs.bitfield.ptr;
 	sa.numsteps = ts.ray_numsteps.ptr;

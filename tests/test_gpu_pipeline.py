@@ -166,6 +166,43 @@ def test_train_step_matches_oracle(cfg_kw):
         g.close()
 
 
+@pytest.mark.parametrize("density", [0.002, 0.05, 0.5])
+def test_sampler_distance_field_walk_matches_chain_walk(density):
+    """aabb_scale 1: the training sampler crosses empty space through the octant distance fields
+    (train_step_df) instead of the reference's voxel-by-voxel jump chain (ngp_tuning.train_chain_walk
+    = 1); the samples -- counts, bases, coordinates -- are identical bit for bit, and the oracle's
+    literal chain agrees, over sparse random occupancy (floaters everywhere), a solid core and a dense
+    grid."""
+    g, o, rng = pair(CFG_A)
+    try:
+        imgs, cams, focal = make_views(6, 32, 32)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        grid = np.where(rng.random(CELLS) < density, 1.0, 0.0).astype(np.float32)
+        grid = np.maximum(grid, sphere_bitfield(0.2))
+        set_bitfield_both(g, o, grid)
+        R, B, MS = 2048, 1 << 14, 1 << 18
+        out = {}
+        for chain in (1, 0):
+            g.set_tuning(train_chain_walk=chain)
+            ta = train_args(dd.ptr, dd.n, R, B, MS)
+            g.zero_grads()
+            A.check(g.lib.ngp_train_step(g.h, C.byref(ta), stream()))
+            torch.cuda.synchronize()
+            ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2).copy()
+            total = int(ns[:, 0].sum())
+            out[chain] = (ns, gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS].copy(), total)
+        np.testing.assert_array_equal(out[0][0], out[1][0])
+        assert out[0][2] > 1000
+        owned = np.zeros(MS, bool)
+        for n, b in out[0][0]:
+            owned[b:b + n] = True
+        np.testing.assert_array_equal(out[0][1][owned], out[1][1][owned])
+        o.train_step(train_args(hd.ptr, hd.n, R, B, MS))
+        np.testing.assert_array_equal(out[0][0], o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2))
+    finally:
+        g.close()
+
+
 def test_chunked_forward_matches_full_forward():
     """The early-terminated (chunked) forward leaves the loss, the compaction and dL/dout
     bit-identical to evaluating every sample (the reference's inference over the whole
