@@ -343,6 +343,8 @@ typedef struct ngp_tuning {
 	uint32_t render_net_workgroups_per_cu; /* fused render kernel workgroups per CU; 0: 4 */
 	uint32_t train_chain_walk;       /* 1: the training sampler walks the reference's voxel-jump chain also at
 	                                    aabb_scale 1 (0: the octant distance fields there; same samples) */
+	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
+	                                    by cell, coherent gathers; same grid) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -11,6 +11,8 @@
 // The mean uses an exact fixed-point (2^-24) integer sum so the threshold, and
 // therefore every bitfield bit, is independent of summation order (the
 // reference's float atomics are not).
+#include <hipcub/hipcub.hpp>
+
 #include "ngp_internal.h"
 
 namespace ngp {
@@ -197,6 +199,18 @@ void grid_reserve(ngp_model* m, uint32_t n_cascades, uint32_t n_samples) {
 	g.out.reserve(std::max(n_samples, 1u));
 }
 
+__global__ void k_iota(uint32_t n, uint32_t* __restrict__ v) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i < n) v[i] = i;
+}
+
+// positions of the samples in sorted order (16-B rows) for the encoder
+__global__ void k_gather_rows(uint32_t n, const uint32_t* __restrict__ perm, const float4* __restrict__ src,
+                              float4* __restrict__ dst) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i < n) dst[i] = src[perm[i]];
+}
+
 void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 	GridState& g = m->gs;
 	const uint32_t n_cascades = a->max_cascade + 1;
@@ -234,10 +248,32 @@ void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
 	if (cnt) {
-		launch_hashgrid_fwd(m->lt, g.positions.ptr + 4 * (size_t)first, 4, cnt, table, g.enc.ptr, internal_layout(m, cnt), s);
+		const float* pos = g.positions.ptr + 4 * (size_t)first;
+		const uint32_t* idx = g.indices.ptr + first;
+		if (m->tuning.grid_unsorted == 0) {
+			// the samples are drawn in hash order, so the encoder's gathers were incoherent (2.6x the
+			// algorithmic fetch, r02); sorted by cell index (cascade-major Morton order) neighbouring lanes
+			// share corners.  The splat is a max per cell: the result does not depend on the order.
+			const uint32_t bits = 21u + (uint32_t)std::ceil(std::log2((double)n_cascades));
+			g.skeys.reserve(cnt);
+			g.perm_in.reserve(cnt);
+			g.perm.reserve(cnt);
+			g.spos.reserve(4 * (size_t)cnt);
+			size_t tmp_bytes = 0;
+			NGP_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(nullptr, tmp_bytes, idx, g.skeys.ptr, g.perm_in.ptr, g.perm.ptr, (int)cnt,
+			                                                 0, (int)bits, s));
+			g.sort_tmp.reserve(tmp_bytes / 4 + 1);
+			k_iota<<<div_up(cnt, 256), 256, 0, s>>>(cnt, g.perm_in.ptr);
+			NGP_HIP_CHECK(hipcub::DeviceRadixSort::SortPairs(g.sort_tmp.ptr, tmp_bytes, idx, g.skeys.ptr, g.perm_in.ptr, g.perm.ptr,
+			                                                 (int)cnt, 0, (int)bits, s));
+			k_gather_rows<<<div_up(cnt, 256), 256, 0, s>>>(cnt, g.perm.ptr, reinterpret_cast<const float4*>(pos),
+			                                               reinterpret_cast<float4*>(g.spos.ptr));
+			pos = g.spos.ptr;
+			idx = g.skeys.ptr;
+		}
+		launch_hashgrid_fwd(m->lt, pos, 4, cnt, table, g.enc.ptr, internal_layout(m, cnt), s);
 		launch_mlp_density(m, frags, g.enc.ptr, internal_layout(m, cnt), cnt, g.out.ptr, s);
-		k_splat<<<div_up(cnt, 256), 256, 0, s>>>(cnt, g.indices.ptr + first, g.out.ptr, g.tmp.ptr,
-		                                        m->cfg.density_activation);
+		k_splat<<<div_up(cnt, 256), 256, 0, s>>>(cnt, idx, g.out.ptr, g.tmp.ptr, m->cfg.density_activation);
 		NGP_HIP_CHECK(hipGetLastError());
 	}
 }

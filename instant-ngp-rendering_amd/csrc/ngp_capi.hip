@@ -232,6 +232,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		GridState& g = m->gs;
 		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
+		g.skeys.release(); g.perm_in.release(); g.perm.release(); g.sort_tmp.release(); g.spos.release();
 		m->rs.release();
 		m->timers.release();
 		delete m;

@@ -290,6 +290,10 @@ struct GridState {
 	DevBuf<uint32_t> indices;  // [n_samples]
 	DevBuf<__half> enc;        // [L][n][F]
 	DevBuf<__half> out;        // [n]
+	// the evaluated samples in cell (Morton) order: sort keys / permutation in and out, the
+	// positions gathered in that order, radix-sort scratch
+	DevBuf<uint32_t> skeys, perm_in, perm, sort_tmp;
+	DevBuf<float> spos;        // [n][4]
 	uint32_t n_cascades = 0;
 	uint64_t version = 0;  // bumped whenever the bitfield may have changed (render caches derive from it)
 };

@@ -340,6 +340,37 @@ def test_density_grid_update_matches_oracle(cfg_kw, aabb_scale, lens):
         g.close()
 
 
+@pytest.mark.parametrize("aabb_scale", [1, 16])
+def test_density_grid_update_sorted_samples_match_drawing_order(aabb_scale):
+    """The grid update encodes its samples sorted by cell (coherent gathers; ngp_tuning.grid_unsorted = 0)
+    -- the splat is a max per cell, so the grid, mean and bitfield are bit-identical to evaluating them in
+    drawing order (grid_unsorted = 1)."""
+    out = {}
+    for unsorted in (1, 0):
+        g, o, rng = pair(dict(CFG_B, aabb_scale=aabb_scale), grid_scale=1.0)
+        try:
+            g.set_tuning(grid_unsorted=unsorted)
+            nc = int(np.log2(aabb_scale)) + 1
+            imgs, cams, focal = make_views(6, 24, 24)
+            dd = DeviceDataset(imgs, cams, focal)
+            for step, (nu, nn) in enumerate([(CELLS, 0), (CELLS // 4, CELLS // 4)]):
+                ga = grid_args(dd.ptr, dd.n, nu, nn, ema_step=step, mark=int(step == 0), clear=int(step == 0),
+                               aabb_scale=aabb_scale)
+                A.check(g.lib.ngp_density_grid_update(g.h, C.byref(ga), stream()))
+                torch.cuda.synchronize()
+            gp, bp, _, mp = gpu_grid_buffers(g)
+            gg = np.zeros(CELLS * nc, np.float32)
+            cuda_memcpy_d2h(gg, gp)
+            gb = np.zeros(CELLS // 8 * nc, np.uint8)
+            cuda_memcpy_d2h(gb, bp)
+            out[unsorted] = (gg, gb)
+        finally:
+            g.close()
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    np.testing.assert_array_equal(out[0][1], out[1][1])
+    assert (out[0][0] > 0).mean() > 0.01  # the update wrote densities
+
+
 @pytest.mark.parametrize("cfg_kw", [CFG_A, CFG_B, CFG_F4], ids=["A", "B", "F4"])
 @pytest.mark.parametrize("spp,snap,shard", [(0, 1, (0, 1, 8)), (1, 0, (0, 1, 8)), (3, 0, (1, 2, 8))])
 def test_render_matches_oracle(spp, snap, shard, cfg_kw):
