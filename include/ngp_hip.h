@@ -345,6 +345,8 @@ typedef struct ngp_tuning {
 	                                    aabb_scale 1 (0: the octant distance fields there; same samples) */
 	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
 	                                    by cell, coherent gathers; same grid) */
+	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16 (2-deep prefetch ring), 2 = 32,
+	                                    3 = 32 with a 2-deep ring, 4 = 64; 0: 4 */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -254,6 +254,7 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->encode_levels_per_thread == 0 || t->encode_levels_per_thread == 2 || t->encode_levels_per_thread == 4,
 		        "encode_levels_per_thread must be 0, 2 or 4");
 		require(t->render_network <= 2, "render_network must be 0, 1 or 2");
+		require(t->render_mlp_tile <= 4, "render_mlp_tile must be 0..4");
 		require(t->render_net_workgroups_per_cu <= 16, "render_net_workgroups_per_cu must be <= 16");
 		m->tuning = *t;
 		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
