@@ -347,6 +347,10 @@ typedef struct ngp_tuning {
 	                                    by cell, coherent gathers; same grid) */
 	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16 (2-deep prefetch ring), 2 = 32,
 	                                    3 = 32 with a 2-deep ring, 4 = 64; 0: 4 */
+	uint32_t encode_xcd_regions;     /* four-levels-per-thread hash encoder: 1 = each XCD encodes one contiguous eighth
+	                                    of the samples (level groups one after another), 2 = the same with the four
+	                                    level groups of a chunk back to back, 3 = off (XCD x takes every eighth
+	                                    chunk); 0: the default (1) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -61,17 +61,39 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
                                                       const __half* __restrict__ table, const LevelTable lt,
                                                       __half* __restrict__ enc, EncLayout lay, uint32_t n_chunks,
                                                       const uint32_t* __restrict__ n_dev) {
-	uint32_t grp, chunk0;
+	uint32_t grp, chunk0 = 0;
 	const uint32_t groups = lt.n_levels / LPT;
-	map_block(blockIdx.x, n_chunks, groups, &grp, &chunk0);
 	if (n_dev) n = min(n, *n_dev);
+	// n_chunks per level group are launched; they stride over the chunks the count covers
+	uint32_t c_begin, c_end = (n + 255u) >> 8, c_step = n_chunks;
+	if (LPT == 4 && lt.regions) {
+		// XCD regions (n_chunks a multiple of 8): workgroup b runs on XCD b % 8, so XCD x takes the
+		// contiguous chunk range [x R, x R + R) of the device count -- its L2 sees the cells of one
+		// eighth of the rays instead of every eighth chunk of all of them
+		const uint32_t b = blockIdx.x, K = n_chunks >> 3, R = (c_end + 7u) >> 3;
+		uint32_t x, k;
+		if (lt.regions == 1) {
+			grp = b / n_chunks;
+			x = (b % n_chunks) & 7u;
+			k = (b % n_chunks) >> 3;
+		} else {
+			x = b & 7u;
+			grp = (b >> 3) % groups;
+			k = (b >> 3) / groups;
+		}
+		c_begin = x * R + k;
+		c_end = min(c_end, x * R + R);
+		c_step = K;
+	} else {
+		map_block(blockIdx.x, n_chunks, groups, &grp, &chunk0);
+		c_begin = chunk0;
+	}
 	using VT = typename FeatVec<F>::T;
 	// LPT = 2: the level pair (g, L - 1 - g) -- a coarse and a fine level, so with L = 16 the eight
 	// pairs cost about the same and each XCD (map_block: XCD x runs pair x) keeps two levels' tables
 	// in its L2; else levels g, g + L/LPT, ...
 	auto level_of = [&](uint32_t q) { return LPT == 2 ? (q == 0 ? grp : lt.n_levels - 1u - grp) : grp + q * groups; };
-	// n_chunks per level group are launched; they stride over the chunks the count covers
-	for (uint32_t chunk = chunk0; chunk * 256u < n; chunk += n_chunks) {
+	for (uint32_t chunk = c_begin; chunk < c_end; chunk += c_step) {
 		const uint32_t i = chunk * 256u + threadIdx.x;
 		if (i >= n) continue;
 		float px, py, pz;
@@ -411,9 +433,11 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 		if (lt.pairs && lt.n_levels == 16)
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 2>, n_chunks * 8, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane,
 			             n_chunks, n_dev);
-		else if (lt.n_levels % 4 == 0)
+		else if (lt.n_levels % 4 == 0) {
+			if (lt.regions) n_chunks = div_up(n_chunks, 8u) * 8u;  // K = n_chunks / 8 workgroups per XCD and group
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 4>, n_chunks * lt.n_levels / 4, 256, 0, s, n, pos, stride, table, lt, enc,
 			             enc_plane, n_chunks, n_dev);
+		}
 		else
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 1>, n_chunks * lt.n_levels, 256, 0, s, n, pos, stride, table, lt, enc,
 			             enc_plane, n_chunks, n_dev);

@@ -57,6 +57,9 @@ static hipStream_t S(ngp_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
 // ngp_tuning.encode_streaming: 0 = the default (non-temporal encoding stores: -2 % render frame
 // time, tools/render_ab.py), bit 7 = no hints
+// ngp_tuning.encode_xcd_regions: 0 = the default (contiguous XCD regions: -1.1 % render frame time in a same-weights
+// A/B), 3 = off
+static uint32_t encode_regions(const ngp_tuning& t) { return t.encode_xcd_regions == 0 ? 1u : t.encode_xcd_regions == 3 ? 0u : t.encode_xcd_regions; }
 static uint32_t encode_streaming_bits(const ngp_tuning& t) {
 	if (t.encode_streaming == 0) return 1u;
 	return t.encode_streaming & 127u;
@@ -87,6 +90,7 @@ static void build_level_table(ngp_model* m) {
 	}
 	m->n_grid_params = (uint64_t)offset * lt.F;
 	lt.streaming = encode_streaming_bits(m->tuning);
+	lt.regions = encode_regions(m->tuning);
 }
 
 static void build_layers(ngp_model* m) {
@@ -256,9 +260,11 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->render_network <= 2, "render_network must be 0, 1 or 2");
 		require(t->render_mlp_tile <= 4, "render_mlp_tile must be 0..4");
 		require(t->render_net_workgroups_per_cu <= 16, "render_net_workgroups_per_cu must be <= 16");
+		require(t->encode_xcd_regions <= 3, "encode_xcd_regions must be 0..3");
 		m->tuning = *t;
 		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
 		m->lt.streaming = encode_streaming_bits(*t);
+		m->lt.regions = encode_regions(*t);
 	});
 }
 

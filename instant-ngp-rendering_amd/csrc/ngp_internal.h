@@ -151,6 +151,9 @@ struct LevelTable {
 	uint32_t pairs = 0;
 	// ngp_tuning.encode_streaming: bit 0 non-temporal encoding stores, bit 1 non-temporal position loads
 	uint32_t streaming = 0;
+	// ngp_tuning.encode_xcd_regions (four levels per thread): 1 = each XCD encodes a contiguous eighth of the
+	// chunks, level group by level group; 2 = the four level groups of a chunk back to back on one XCD; 0 = off
+	uint32_t regions = 0;
 	__host__ __device__ bool level_cut(uint32_t level, uint32_t i) const {
 		if (!max_level) return false;
 		// tcnn: max_level = (max_level_gpu[i] * num_grid_features) / N_FEATURES_PER_LEVEL; level >= max_level + 1e-3f

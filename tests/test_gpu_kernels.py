@@ -61,6 +61,13 @@ def test_hashgrid_indices_and_features_bit_exact(name):
             # the level-pair encoder (ngp_tuning.encode_levels_per_thread = 2) computes the same features
             g.set_tuning(encode_levels_per_thread=2)
             np.testing.assert_array_equal(g.encode(pos).astype(np.float32), oe)
+        if CONFIGS[name]["n_levels"] % 4 == 0 and CONFIGS[name]["F"] == 2:
+            # XCD-region chunk mappings (ngp_tuning.encode_xcd_regions), also on a count that is not a
+            # multiple of 8 chunks of 256
+            for r in (1, 2, 3):
+                g.set_tuning(encode_levels_per_thread=0, encode_xcd_regions=r)
+                np.testing.assert_array_equal(g.encode(pos).astype(np.float32), oe, err_msg=f"regions {r}")
+                np.testing.assert_array_equal(g.encode(pos[:3001]).astype(np.float32), oe[:, :3001], err_msg=f"regions {r}")
     finally:
         g.close()
 
