@@ -351,6 +351,13 @@ typedef struct ngp_tuning {
 	                                    of the samples (level groups one after another), 2 = the same with the four
 	                                    level groups of a chunk back to back, 3 = off (XCD x takes every eighth
 	                                    chunk); 0: the default (1) */
+	uint32_t render_pass_order;      /* ray pipelines' network launches: 1 = free-running streams, 2 = the hash-encoder
+	                                    launches of all pipelines chained in enqueue order (one encoder on the GPU at a
+	                                    time; the other pipelines' MLP and march kernels run beside it), 3 = the same
+	                                    chain over encoder + MLP; 0: the default */
+	uint32_t render_encode_wgs_per_cu; /* render hash-encoder workgroups per CU (a persistent grid striding over the
+	                                      pass's chunks, leaving CU room for the other pipelines' kernels); 0: one
+	                                      workgroup per chunk and level group */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

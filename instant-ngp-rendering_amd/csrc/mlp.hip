@@ -1202,7 +1202,7 @@ void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frag
 	NGP_HIP_CHECK(hipGetLastError());
 }
 
-static int cu_count() {
+int cu_count() {
 	static int n = 0;
 	if (n == 0) {
 		int dev = 0;

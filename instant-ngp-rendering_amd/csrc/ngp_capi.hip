@@ -261,6 +261,8 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->render_mlp_tile <= 4, "render_mlp_tile must be 0..4");
 		require(t->render_net_workgroups_per_cu <= 16, "render_net_workgroups_per_cu must be <= 16");
 		require(t->encode_xcd_regions <= 3, "encode_xcd_regions must be 0..3");
+		require(t->render_pass_order <= 3, "render_pass_order must be 0..3");
+		require(t->render_encode_wgs_per_cu <= 32, "render_encode_wgs_per_cu must be <= 32");
 		m->tuning = *t;
 		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
 		m->lt.streaming = encode_streaming_bits(*t);

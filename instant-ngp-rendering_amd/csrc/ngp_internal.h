@@ -307,7 +307,7 @@ struct RenderPipeScratch {
 	DevBuf<float> payload[3];   // [n][12]: Payload (render.hip)
 	DevBuf<float> rgba[3];      // [n][4]
 	DevBuf<float> depth[3];     // [n]
-	DevBuf<float> coords;       // [max_samples][4] position + warped dt, then [max_samples][8] SH rows
+	DevBuf<float> coords;       // [max_samples][4] position + warped dt, then [max_samples] SH row indices
 	DevBuf<__half> enc;         // [L][max_samples][F]
 	DevBuf<__half> out;         // [max_samples][4]
 	DevBuf<uint32_t> counters;  // [16]
@@ -334,8 +334,10 @@ struct RenderScratch {
 	RenderPipeScratch pipe[MAX_PIPES];
 	hipStream_t streams[MAX_PIPES] = {};  // pipelines 1.. run on their own streams ([0] unused: the caller's)
 	hipEvent_t fork = nullptr, join[MAX_PIPES] = {};  // caller's stream -> pipeline streams -> caller's stream
+	hipEvent_t chain[MAX_PIPES] = {};  // ngp_tuning.render_pass_order >= 2: a pipeline's last chained network launch
 	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
 	DevBuf<uint4> dense_rec;   // corner records of the dense levels (LevelTable::rec), rebuilt per render
+	DevBuf<uint4> shrows;      // [W * H][2]: each ray's 16 fp16 SH inputs, indexed by its pixel (k_render_init)
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
 	DevBuf<float> slice_coords;   // Slice mode: [pixels][8] NerfCoordinate rows (pos.x NaN: no ray)
@@ -345,12 +347,14 @@ struct RenderScratch {
 	size_t cap = 0;
 	void release() {
 		for (auto& p : pipe) p.release();
-		summary.release(); dense_rec.release(); df.release(); df_x.release(); df_xy.release();
+		summary.release(); dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();
 		slice_coords.release(); slice_enc.release(); slice_out.release();
 		if (fork) (void)hipEventDestroy(fork);
 		fork = nullptr;
 		for (int j = 0; j < MAX_PIPES; ++j) {
 			if (join[j]) (void)hipEventDestroy(join[j]);
+			if (chain[j]) (void)hipEventDestroy(chain[j]);
+			chain[j] = nullptr;
 			if (streams[j]) (void)hipStreamDestroy(streams[j]);
 			join[j] = nullptr;
 			streams[j] = nullptr;
@@ -418,6 +422,9 @@ void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride
                          __half* enc, EncLayout enc_layout, hipStream_t s, const uint32_t* n_dev = nullptr, int site = 2,
                          uint32_t max_chunks = 0);
 // grad64 non-null: deterministic fixed-point accumulation into it (grad_table16 unused).
+// CUs of the current device (cached)
+int cu_count();
+
 // max_chunks > 0: blocks loop over the device count past max_chunks 128-sample chunks.
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                          EncLayout enc_layout, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr,

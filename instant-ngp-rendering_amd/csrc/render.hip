@@ -199,10 +199,26 @@ __device__ __forceinline__ void block_add(uint32_t v, uint32_t* counter) {
 	}
 }
 
+// The 16 SH(4) inputs of the warped direction d as fp16 pairs (the rgb network's direction rows).
+__device__ __forceinline__ void sh_row(v3 d, uint4* lo, uint4* hi) {
+	const v3 wdir = warp_direction(d);
+	float v[16];
+	sh_deg4(wdir.x, wdir.y, wdir.z, v);
+	uint32_t u[8];
+#pragma unroll
+	for (int q = 0; q < 8; ++q) {
+		const _Float16 a = (_Float16)v[2 * q], b = (_Float16)v[2 * q + 1];
+		u[q] = (uint32_t)__builtin_bit_cast(uint16_t, a) | ((uint32_t)__builtin_bit_cast(uint16_t, b) << 16);
+	}
+	*lo = make_uint4(u[0], u[1], u[2], u[3]);
+	*hi = make_uint4(u[4], u[5], u[6], u[7]);
+}
+
 template <bool LENS>
 __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restrict__ payloads, float4* __restrict__ rgba,
                                                      float* __restrict__ depth, float4* __restrict__ frame,
-                                                     float* __restrict__ depth_buffer, uint32_t* __restrict__ counters) {
+                                                     float* __restrict__ depth_buffer, uint32_t* __restrict__ counters,
+                                                     uint4* __restrict__ shrows) {
 	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
 	// rays are numbered in 8x8 pixel tiles: a wave's 64 rays are a square patch, so at a
 	// given step their samples are close in space (hash-grid gathers share cache lines)
@@ -217,6 +233,13 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 		payloads[slot] = p;
 		rgba[slot] = make_float4(0.f, 0.f, 0.f, 0.f);
 		depth[slot] = 0.0f;
+		// the rgb network's direction inputs: one row of 16 fp16 SH values per ray and frame, indexed
+		// by its pixel (the samples of every pass carry that index), instead of once per sample in the
+		// MLP or once per ray and pass in k_generate
+		uint4 lo, hi;
+		sh_row(mk3(p.d[0], p.d[1], p.d[2]), &lo, &hi);
+		shrows[2 * (size_t)p.idx] = lo;
+		shrows[2 * (size_t)p.idx + 1] = hi;
 	}
 }
 
@@ -501,7 +524,7 @@ template <uint32_t G>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
                                                   float4* __restrict__ posdt, uint32_t* __restrict__ sray,
-                                                  uint4* __restrict__ shrows, uint32_t target, uint32_t max_steps,
+                                                  uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
                                                   const uint32_t* counters, unsigned long long* host_prev, uint32_t tag_prev) {
@@ -530,31 +553,14 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 	if (G > 1) base = __shfl(base, g0, 64);
 	bool running = valid;
 	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f);
-	uint4 sh_lo = make_uint4(0u, 0u, 0u, 0u), sh_hi = sh_lo;  // the ray's 16 SH inputs (fp16)
 	float n = 0.0f;
+	uint32_t row = 0;  // the ray's SH row (its pixel index; written once per frame by k_render_init)
 	if (running) {
 		o = mk3(p->o[0], p->o[1], p->o[2]);
 		d = mk3(p->d[0], p->d[1], p->d[2]);
 		idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		n = p->n;
-		// the rgb network's direction inputs, once per ray instead of once per sample in the MLP
-		const v3 wdir = warp_direction(d);
-		float v[16];
-		sh_deg4(wdir.x, wdir.y, wdir.z, v);
-		uint32_t u[8];
-#pragma unroll
-		for (int q = 0; q < 8; ++q) {
-			const _Float16 lo = (_Float16)v[2 * q], hi = (_Float16)v[2 * q + 1];
-			u[q] = (uint32_t)__builtin_bit_cast(uint16_t, lo) | ((uint32_t)__builtin_bit_cast(uint16_t, hi) << 16);
-		}
-		sh_lo = make_uint4(u[0], u[1], u[2], u[3]);
-		sh_hi = make_uint4(u[4], u[5], u[6], u[7]);
-		// one row per ray and pass (row = the ray's index in this pass's alive buffer); its sample
-		// slots carry the row index (4 B instead of 32 B of SH per slot)
-		if (r == 0) {
-			shrows[2 * (size_t)i] = sh_lo;
-			shrows[2 * (size_t)i + 1] = sh_hi;
-		}
+		row = p->idx;
 	}
 	OccCache occ = occ_cache_init();
 	const uint32_t oct = ray_octant(d);
@@ -583,7 +589,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 				const size_t slot = (size_t)base + j + rank;
 				posdt[slot] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				sray[slot] = i;
+				sray[slot] = row;
 			}
 		}
 		if (cnt >= room) {
@@ -607,7 +613,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
 		for (uint32_t q = j + r; q < budget; q += G) {
 			posdt[(size_t)base + q] = make_float4(-1.0f, -1.0f, -1.0f, 0.0f);
-			sray[(size_t)base + q] = i;
+			sray[(size_t)base + q] = row;
 		}
 	}
 	if (k.dbg && valid && r == 0) {
@@ -908,6 +914,10 @@ static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard) 
 // kernels publish.
 constexpr uint32_t HC_SLOTS = 4, HC_COPYBACK = 16 * HC_SLOTS, HC_PUBLISHED = 128, HC_WORDS = HC_PUBLISHED + 16 * HC_SLOTS;
 
+// ngp_tuning.render_pass_order: 1 free-running pipelines, 2 encoder launches chained across them, 3 encoder +
+// MLP chained
+static uint32_t render_pass_order(const ngp_tuning& t) { return t.render_pass_order ? t.render_pass_order : 1u; }
+
 // passes a pipeline runs ahead of its counter read-backs (ngp_tuning.render_lag, 2 .. HC_SLOTS)
 static uint32_t render_lag(const ngp_tuning& t) {
 	return t.render_lag >= 2 ? std::min<uint32_t>(t.render_lag, HC_SLOTS) : 3u;  // 3: -0.6 % against 2 (same weights)
@@ -1043,11 +1053,16 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const bool fused = tu.render_network == 1 && k.mode != NGP_RENDER_MODE_NORMALS && render_net_supported(m);
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
+	for (uint32_t j = 0; j < n_pipes; ++j)
+		if (!rs.chain[j]) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.chain[j], hipEventDisableTiming));
 	for (uint32_t j = 1; j < n_pipes; ++j) {
 		if (rs.streams[j]) continue;
 		NGP_HIP_CHECK(hipStreamCreateWithFlags(&rs.streams[j], hipStreamNonBlocking));
 		NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.join[j], hipEventDisableTiming));
 	}
+	// one SH row (16 fp16) per pixel of the frame, written by k_render_init for its alive rays
+	const uint32_t sh_rows = k.W * k.H;
+	rs.shrows.reserve(2 * (size_t)sh_rows);
 	PipeRun pipes[RenderScratch::MAX_PIPES];
 	for (uint32_t j = 0; j < n_pipes; ++j) {
 		PipeRun& pr = pipes[j];
@@ -1067,9 +1082,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			ps.rgba[b].reserve((size_t)pr.n * 4);
 			ps.depth[b].reserve(pr.n);
 		}
-		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH row indices, then
-		// [rays][8]: one row of 16 fp16 SH inputs per alive ray
-		ps.coords.reserve(5 * pr.max_samples + 8 * (size_t)pr.n);
+		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH rows (pixel indices)
+		ps.coords.reserve(5 * pr.max_samples);
 		if (!fused) ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
@@ -1087,7 +1101,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // the encoder reads 16-B position rows once per level
 		pr.sray = reinterpret_cast<uint32_t*>(ps.coords.ptr + 4 * pr.max_samples);
-		pr.shrows = reinterpret_cast<uint4*>(ps.coords.ptr + 5 * pr.max_samples);
+		pr.shrows = rs.shrows.ptr;
 		pr.base_tag = ps.pass_tag;
 		pr.n_alive_ub = pr.n;
 	}
@@ -1142,7 +1156,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		pr.k.dbg = dbg;
 		if (pr.n == 0) continue;
 		(k.lens_mode != LENS_PERSPECTIVE || k.dmap ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, lds, pr.s>>>(
-		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, pr.ps->counters.ptr);
+		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, pr.ps->counters.ptr, rs.shrows.ptr);
 		pr.marching = true;
 	}
 	tm.end(NGP_TIMER_RENDER_MARCH, s, k.W * H_shard);
@@ -1163,6 +1177,25 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// 512 (256 measured 4.5 % slower)
 	const uint32_t comp_block = tu.render_composite_block ? tu.render_composite_block : 512u;
 	const uint32_t gen_block = tu.render_generate_block ? tu.render_generate_block : 512u;
+	// network launches chained across the pipelines (ngp_tuning.render_pass_order): each pipeline's
+	// encoder (2) or encoder + MLP (3) waits for the one enqueued before it, so the pipelines take
+	// turns on the encoder instead of running their passes in lockstep
+	const uint32_t order = n_pipes > 1 ? render_pass_order(tu) : 1u;
+	int chain_last = -1;
+	// the render encoder's persistent grid (ngp_tuning.render_encode_wgs_per_cu): chunks per level group such
+	// that the launch holds that many workgroups per CU (F = 2, four levels per thread: L/4 groups)
+	const uint32_t enc_chunk_cap = tu.render_encode_wgs_per_cu
+	                                   ? std::max(8u, tu.render_encode_wgs_per_cu * (uint32_t)cu_count() / std::max(1u, m->lt.n_levels / 4) / 8u * 8u)
+	                                   : 0u;
+	auto chain_wait = [&](PipeRun& pr) {
+		const int j = (int)pr.k.pipe_index;
+		if (order >= 2 && chain_last >= 0 && chain_last != j) NGP_HIP_CHECK(hipStreamWaitEvent(pr.s, rs.chain[chain_last], 0));
+	};
+	auto chain_mark = [&](PipeRun& pr) {
+		const int j = (int)pr.k.pipe_index;
+		NGP_HIP_CHECK(hipEventRecord(rs.chain[j], pr.s));
+		chain_last = j;
+	};
 	auto enqueue_pass = [&](PipeRun& pr) {
 		const hipStream_t ps = pr.s;
 		uint32_t* counters = pr.ps->counters.ptr;
@@ -1182,10 +1215,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint32_t tag_prev = pr.base_tag + pass;  // = tag of pass - 1
 		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
 		switch (G) {
-			case 1: k_generate<1><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.shrows, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 1: k_generate<1><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 4: k_generate<4><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			case 16: k_generate<16><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+			default: k_generate<64><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
 		}
 		tm.end(NGP_TIMER_RENDER_MARCH, ps);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
@@ -1211,19 +1244,23 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			}
 		}
 #endif
+		chain_wait(pr);
 		if (fused) {
 			// one kernel: encoding + network (k_render_net), the features never leave the CU
 			launch_render_net(m, frags, lt_render, table, reinterpret_cast<const float*>(pr.posdt), n_elements, pr.ps->out.ptr, ps,
-			                  samples, reinterpret_cast<const __half*>(pr.shrows), pr.sray, pr.n);
+			                  samples, reinterpret_cast<const __half*>(pr.shrows), pr.sray, sh_rows);
 			tm.end(NGP_TIMER_RENDER_ENCODE, ps);
+			if (order >= 2) chain_mark(pr);
 		} else {
 			launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
-			                    internal_layout(m, n_elements), ps, samples, 1);
+			                    internal_layout(m, n_elements), ps, samples, 1, enc_chunk_cap);
 			tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
+			if (order == 2) chain_mark(pr);
 			tm.begin_kernel(NGP_TIMER_RENDER_MLP);
 			launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
-			                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, pr.n);
+			                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows);
 			tm.end(NGP_TIMER_RENDER_MLP, ps);
+			if (order == 3) chain_mark(pr);
 		}
 		if (pr.k.mode == NGP_RENDER_MODE_NORMALS) {
 			// Normals (NerfTracer::trace, testbed_nerf.cu:1715-1717, network->input_gradient): the gradient of

@@ -117,7 +117,8 @@ class Tuning(C.Structure):
         ("encode_levels_per_thread", C.c_uint32), ("encode_streaming", C.c_uint32),
         ("render_network", C.c_uint32), ("render_net_workgroups_per_cu", C.c_uint32),
         ("train_chain_walk", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
-        ("encode_xcd_regions", C.c_uint32),
+        ("encode_xcd_regions", C.c_uint32), ("render_pass_order", C.c_uint32),
+        ("render_encode_wgs_per_cu", C.c_uint32),
     ]
 
 

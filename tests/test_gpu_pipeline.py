@@ -469,10 +469,17 @@ def test_render_config_e_full_network_matches_oracle():
         assert l1 < 1e-3, l1
         # the level-pair encoder (ngp_tuning.encode_levels_per_thread = 2), the separate encoder + MLP launches
         # and the fused encoding + network kernel (render_network 2 / 1), and the render MLP's 16-, 32- and
-        # 64-sample steps (render_mlp_tile) and the encoder's XCD-region mappings render the same frame bit for bit
+        # 64-sample steps (render_mlp_tile), the encoder's XCD-region mappings, the network launches chained across
+        # ray pipelines (render_pass_order) and the encoder's persistent grid (render_encode_wgs_per_cu) render the
+        # same frame bit for bit
         for kw in (dict(encode_levels_per_thread=2), dict(encode_levels_per_thread=0, render_network=2),
                    dict(render_network=1), dict(render_network=2, render_mlp_tile=1), dict(render_mlp_tile=2),
-                   dict(render_mlp_tile=3), dict(render_mlp_tile=0, encode_xcd_regions=3), dict(encode_xcd_regions=2)):
+                   dict(render_mlp_tile=3), dict(render_mlp_tile=0, encode_xcd_regions=3), dict(encode_xcd_regions=2),
+                   dict(encode_xcd_regions=0, render_pipelines=2, render_pass_order=2),
+                   dict(render_pipelines=3, render_pass_order=3, render_encode_wgs_per_cu=1),
+                   dict(render_pipelines=2, render_pass_order=2, render_encode_wgs_per_cu=4),
+                   dict(render_network=1, render_pass_order=2),
+                   dict(render_network=0, render_pipelines=0, render_pass_order=0, render_encode_wgs_per_cu=0)):
             g.set_tuning(**kw)
             frame.zero_()
             A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
