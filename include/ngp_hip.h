@@ -358,6 +358,13 @@ typedef struct ngp_tuning {
 	uint32_t render_encode_wgs_per_cu; /* render hash-encoder workgroups per CU (a persistent grid striding over the
 	                                      pass's chunks, leaving CU room for the other pipelines' kernels); 0: one
 	                                      workgroup per chunk and level group */
+	uint32_t mlp_train_schedule;     /* training MLP (k_mlp_train*): 1 = 8 waves x 16 samples, wave-shared weight
+	                                    gradients with a workgroup barrier per layer; 2 = 4 waves, each owning
+	                                    32-sample steps end to end (forward, dgrad and every weight gradient), no
+	                                    barrier in the loop; 0: the default */
+	uint32_t render_slot_compaction; /* march passes: 1 = each ray stages its samples and then takes exactly the
+	                                    rows it filled (packed pass rows); 2 = rays reserve their whole budget up
+	                                    front, unfilled slots marked and skipped; 0: the default (2) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

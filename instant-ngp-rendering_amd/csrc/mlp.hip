@@ -111,6 +111,11 @@ struct Net {
 		for (int i = 0; i < l; ++i) s += gtiles(i);
 		return s;
 	}
+	static constexpr int tile_layer(int t) {
+		int l = 0;
+		while (l + 1 < NL && t >= gtile_base(l + 1)) ++l;
+		return l;
+	}
 	static constexpr int slots() { return (gtile_base(NL) + WAVES - 1) / WAVES; }
 	static constexpr int tslots() { return (gtile_base(NL) + TWAVES - 1) / TWAVES; }
 	static constexpr int drows() { return Wp > 32 ? Wp : 32; }
@@ -767,7 +772,7 @@ __device__ __forceinline__ void wgrad_layer(const _Float16* imgs, const _Float16
 	}
 }
 
-template <class N, int l>
+template <class N, int l, int CT_ = TCT>
 __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* frags, const _Float16* img,
                                             _Float16* dimg, int lane, uint32_t base) {
 	constexpr int STRIDE = N::template stride<true>();
@@ -779,9 +784,9 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	// the rgb network's input: the 16 density-output rows, then (for the camera gradients) the 16 SH rows
 	constexpr int KT = N::Kt(l);
 	const int g = lane >> 4, n = lane & 15;
-	h8 b[TCT][MS];
+	h8 b[CT_][MS];
 #pragma unroll
-	for (int c = 0; c < TCT; ++c)
+	for (int c = 0; c < CT_; ++c)
 #pragma unroll
 		for (int s = 0; s < MS; ++s) b[c][s] = lds_h8(dimg + (16 * c + n) * DS + DCUR + 32 * s + 8 * g);
 	const _Float16* fr = frags + N::bwd_off(l);
@@ -792,7 +797,7 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 #pragma unroll
 		for (int s = 0; s < MS; ++s) af[s] = lds_h8(fr + ((mt * MS + s) * 64 + lane) * 8);
 #pragma unroll
-		for (int c = 0; c < TCT; ++c) {
+		for (int c = 0; c < CT_; ++c) {
 			f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
 			for (int s = 0; s < MS; ++s) acc = mfma(af[s], b[c][s], acc);
@@ -847,7 +852,7 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	if constexpr (l == N::DH + 1) {
 		// density-output delta has 16 rows; rows 16..31 of the next k-step must be zero
 #pragma unroll
-		for (int c = 0; c < TCT; ++c) lds_st_h4(dimg + (16 * c + n) * DS + DNXT + 16 + 4 * g, h4{0, 0, 0, 0});
+		for (int c = 0; c < CT_; ++c) lds_st_h4(dimg + (16 * c + n) * DS + DNXT + 16 + 4 * g, h4{0, 0, 0, 0});
 	}
 }
 
@@ -920,27 +925,27 @@ struct TrainPrefetch {
 	float w;
 };
 
-template <class N>
+template <class N, int SPW_ = TSPW>
 __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int lane, TrainPrefetch& p) {
 	constexpr int CHUNKS = N::ENC_ROWS / 8;
 	const EncLayout lay{a.enc_plane, a.enc_lsh, a.enc_gsh};
 	const uint32_t* e = reinterpret_cast<const uint32_t*>(a.enc);
 #pragma unroll
 	for (int it = 0; it < 2; ++it) {
-		const int t = lane + 64 * it, smp = t % TSPW, chunk = t / TSPW;
+		const int t = lane + 64 * it, smp = t % SPW_, chunk = t / SPW_;
 		const uint32_t i = base + smp, k0 = chunk * 8;
-		const bool ok = t < TSPW * CHUNKS && i < a.n && k0 < a.E;
+		const bool ok = t < SPW_ * CHUNKS && i < a.n && k0 < a.E;
 #pragma unroll
 		for (int q = 0; q < 4; ++q) p.e[it][q] = ok ? e[lay.vec(k0 / 2 + q, i)] : 0u;
 	}
-	const uint32_t i = base + (lane % TSPW);
+	const uint32_t i = base + (lane % SPW_);
 	const bool in = i < a.n;
 	const float* c = a.coords + (size_t)(in ? i : 0) * a.coord_stride;
 #pragma unroll
 	for (int k = 0; k < 3; ++k) p.d[k] = in ? c[4 + k] : 0.5f;
 	p.dl = make_uint2(0u, 0u);
 	p.w = 1.0f;
-	if (lane < TSPW && in) {
+	if (lane < SPW_ && in) {
 		p.dl = *reinterpret_cast<const uint2*>(a.dloss + (size_t)i * 4);
 		if (a.weight) p.w = a.weight[i];
 	}
@@ -948,15 +953,15 @@ __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int
 
 // The prefetched inputs -> this wave's LDS images (encoding rows, SH rows, output-layer delta),
 // the same values load_encoding / load_sh / the delta loop store.
-template <class N, int STRIDE, int DS>
+template <class N, int STRIDE, int DS, int SPW_ = TSPW>
 __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefetch& p, _Float16* img, _Float16* dimg,
                                              int x_seg, uint32_t base, int lane) {
 	constexpr int CHUNKS = N::ENC_ROWS / 8;
 #pragma unroll
 	for (int it = 0; it < 2; ++it) {
 		const int t = lane + 64 * it;
-		if (t < TSPW * CHUNKS) {
-			const int smp = t % TSPW, chunk = t / TSPW;
+		if (t < SPW_ * CHUNKS) {
+			const int smp = t % SPW_, chunk = t / SPW_;
 			h8 v;
 #pragma unroll
 			for (int q = 0; q < 4; ++q) {
@@ -967,8 +972,8 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 		}
 	}
 	{
-		// lane = half * TSPW + sample: SH components 8 half .. 8 half + 7 of the warped direction
-		const int smp = lane % TSPW, half = lane / TSPW;
+		// lane = half * SPW_ + sample: SH components 8 half .. 8 half + 7 of the warped direction
+		const int smp = lane % SPW_, half = lane / SPW_;
 		const bool in = base + smp < a.n;
 		float v[16];
 		sh_deg4(p.d[0], p.d[1], p.d[2], v);
@@ -977,8 +982,8 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 		for (int k = 0; k < 8; ++k) o[k] = in ? (_Float16)(half ? v[8 + k] : v[k]) : (_Float16)0;
 		if (half < 2) lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, o);
 	}
-	for (int t = lane; t < TSPW * 4; t += 64) {
-		const int smp = t % TSPW, ch = t / TSPW;
+	for (int t = lane; t < SPW_ * 4; t += 64) {
+		const int smp = t % SPW_, ch = t / SPW_;
 		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 		const uint2 dl = make_uint2(__shfl(p.dl.x, smp, 64), __shfl(p.dl.y, smp, 64));
 		const float w = __shfl(p.w, smp, 64);
@@ -1050,6 +1055,170 @@ __global__ void __launch_bounds__(TBLOCK) k_mlp_train(MlpArgs a) {
 		bwd_range<N, N::NL - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
 	}
 	flush_range<N, 0>(a, wave, lane, acc);
+}
+
+// ---------------------------------------------------------------------------
+// Training, wave-independent schedule (k_mlp_train_w): 4 waves per workgroup (one per SIMD),
+// each wave owns 32-sample steps end to end -- forward, dgrad and the weight gradients of ALL
+// layers over its own 32 samples (K of one v_mfma_f32_16x16x32_f16), accumulated in its
+// registers over the persistent loop.  No workgroup barrier inside the loop, and the weight
+// gradient of an Mt x Kt layer reads Mt + Kt transposed fragments for Mt * Kt MFMAs (the 8-wave
+// schedule above reads 2 per MFMA and synchronises the workgroup before every layer).  The
+// four waves' accumulators are summed through LDS once, at the end, into the workgroup's row
+// of the partials (the same rows k_mlp_reduce sums in a fixed order).
+// ---------------------------------------------------------------------------
+constexpr int WWAVES = 4;
+constexpr int WSPW = 32;
+constexpr int WCT = WSPW / 16;
+constexpr int WBLOCK = WWAVES * 64;
+static_assert(WWAVES * WSPW == SAMPLES_PER_BLOCK, "the training images hold one chunk");
+
+template <class N, int l>
+__device__ __forceinline__ void wgrad_wave(const _Float16* img, const _Float16* dimg, int lane, f4 (&acc)[N::gtile_base(N::NL)],
+                                           uint32_t enc_pad) {
+	constexpr int STRIDE = N::template stride<true>();
+	constexpr int DS = N::dstride();
+	constexpr int DCUR = ((N::NL - 1 - l) % 2) * N::drows();
+	constexpr int SIN = N::template seg_in<true>(l);
+	constexpr int KTN = N::KT16(l), MT = N::Mt(l), TB = N::gtile_base(l);
+	const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
+	// A: delta^T (16 output rows x 32 samples), B: activation^T (32 samples x 16 inputs)
+	h8 A[MT];
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt) {
+		const _Float16* ds = dimg + DCUR + 16 * mt + 4 * p;
+		const h4 a0 = tr_read(ds + (8 * g + q) * DS), a1 = tr_read(ds + (8 * g + 4 + q) * DS);
+		A[mt] = h8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
+	}
+#pragma unroll
+	for (int kt = 0; kt < KTN; ++kt) {
+		if (l == 0 && (uint32_t)(16 * kt) >= enc_pad) continue;
+		const _Float16* as = img + SIN + 16 * kt + 4 * p;
+		const h4 b0 = tr_read(as + (8 * g + q) * STRIDE), b1 = tr_read(as + (8 * g + 4 + q) * STRIDE);
+		const h8 B = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
+#pragma unroll
+		for (int mt = 0; mt < MT; ++mt) acc[TB + mt * KTN + kt] = mfma(A[mt], B, acc[TB + mt * KTN + kt]);
+	}
+}
+
+template <class N, int l>
+__device__ __forceinline__ void bwd_wave(const MlpArgs& a, const _Float16* frags, const _Float16* img, _Float16* dimg, int lane,
+                                         uint32_t base, f4 (&acc)[N::gtile_base(N::NL)]) {
+	if constexpr (l >= 0) {
+		wgrad_wave<N, l>(img, dimg, lane, acc, a.enc_pad);
+		dgrad_layer<N, l, WCT>(a, frags, img, dimg, lane, base);
+		bwd_wave<N, l - 1>(a, frags, img, dimg, lane, base, acc);
+	}
+}
+
+// The reduced tile t (16 x 16 fp32, MFMA C layout: lane (g, n) holds rows 4g..4g+3 of column n)
+// -> the workgroup's partials row.
+template <class N, int t>
+__device__ __forceinline__ void store_tile(const MlpArgs& a, int lane, f4 c) {
+	constexpr int l = N::tile_layer(t);
+	constexpr int KTN = N::KT16(l);
+	constexpr int mt = (t - N::gtile_base(l)) / KTN, kt = (t - N::gtile_base(l)) % KTN;
+	const int g = lane >> 4, n = lane & 15;
+	const uint32_t pin = a.param_in[l];
+	const uint32_t col = 16 * kt + n;
+	if (col >= pin) return;
+	float* gl = a.partials + (size_t)blockIdx.x * a.n_mlp + a.param_off[l];
+#pragma unroll
+	for (int r = 0; r < 4; ++r) {
+		const uint32_t row = 16 * mt + 4 * g + r;
+		if (row < (uint32_t)N::out_dim(l)) gl[(size_t)row * pin + col] = c[r];
+	}
+}
+
+// tile R0 + I of a reduction round: wave I % 4 sums the four waves' copies (fixed order)
+template <class N, int R0, int RT, int I>
+__device__ __forceinline__ void reduce_round(const MlpArgs& a, const f4* red, int wave, int lane) {
+	if constexpr (I < RT && R0 + I < N::gtile_base(N::NL)) {
+		if (I % WWAVES == wave) {
+			f4 sum = red[I * 64 + lane];
+#pragma unroll
+			for (int w = 1; w < WWAVES; ++w) sum += red[(w * RT + I) * 64 + lane];
+			store_tile<N, R0 + I>(a, lane, sum);
+		}
+		reduce_round<N, R0, RT, I + 1>(a, red, wave, lane);
+	}
+}
+
+// rounds of RT tiles: every wave parks its RT accumulators in LDS, then the tiles are summed
+// over the four waves and stored
+template <class N, int R0, int RT>
+__device__ __forceinline__ void reduce_tiles(const MlpArgs& a, f4* red, int wave, int lane, const f4 (&acc)[N::gtile_base(N::NL)]) {
+	constexpr int NT = N::gtile_base(N::NL);
+	if constexpr (R0 < NT) {
+		__syncthreads();  // the previous round's (or the loop's) LDS reads are done
+#pragma unroll
+		for (int t = R0; t < R0 + RT && t < NT; ++t) red[(wave * RT + (t - R0)) * 64 + lane] = acc[t];
+		__syncthreads();
+		reduce_round<N, R0, RT, 0>(a, red, wave, lane);
+		reduce_tiles<N, R0 + RT, RT>(a, red, wave, lane, acc);
+	}
+}
+
+template <class N>
+__global__ void __launch_bounds__(WBLOCK) k_mlp_train_w(MlpArgs a) {
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	constexpr int STRIDE = N::template stride<true>();
+	constexpr int DS = N::dstride();
+	constexpr int FH = (N::fwd_frags() + N::bwd_frags()) * FRAG_HALVES;
+	constexpr int NT = N::gtile_base(N::NL);
+	_Float16* frags = reinterpret_cast<_Float16*>(smem);
+	_Float16* imgs = frags + FH;
+	_Float16* dimgs = imgs + WAVES * SPW * STRIDE;
+	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+	_Float16* img = imgs + wave * WSPW * STRIDE;
+	_Float16* dimg = dimgs + wave * WSPW * DS;
+
+	for (int t = threadIdx.x; t < FH / 8; t += WBLOCK)
+		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
+	for (int t = lane; t < WSPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	for (int t = lane; t < WSPW * DS / 8; t += 64) reinterpret_cast<h8*>(dimg)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
+	__syncthreads();  // the fragments are shared; from here on every wave runs on its own
+
+	f4 acc[NT];
+#pragma unroll
+	for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
+
+	const uint32_t n_steps = (a.n + WSPW - 1) / WSPW;
+	const uint32_t step_stride = gridDim.x * WWAVES;
+	const bool pref = a.F == 2 && (a.E % 8) == 0 && N::ENC_ROWS / 8 * WSPW <= 128;
+	uint32_t step = blockIdx.x * WWAVES + wave;
+	TrainPrefetch pf;
+	if (pref && step < n_steps) train_fetch<N, WSPW>(a, step * WSPW, lane, pf);
+	for (; step < n_steps; step += step_stride) {
+		const uint32_t base = step * WSPW;
+		if (pref) {
+			train_commit<N, STRIDE, DS, WSPW>(a, pf, img, dimg, N::template x_seg<true>(), base, lane);
+			if (step + step_stride < n_steps) train_fetch<N, WSPW>(a, (step + step_stride) * WSPW, lane, pf);
+		} else {
+			load_encoding<N, STRIDE, WSPW>(a, img, base, lane);
+			load_sh<STRIDE, WSPW>(a, img, N::template x_seg<true>(), base, lane);
+			for (int t = lane; t < WSPW * 4; t += 64) {
+				const int smp = t % WSPW, ch = t / WSPW;
+				const uint32_t i = base + smp;
+				h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
+				if (ch == 0 && i < a.n) {
+					const float w = a.weight ? a.weight[i] : 1.0f;
+					const __half* d = a.dloss + (size_t)i * 4;
+					v[0] = (_Float16)(__half2float(d[0]) * w);
+					v[1] = (_Float16)(__half2float(d[1]) * w);
+					v[2] = (_Float16)(__half2float(d[2]) * w);
+				}
+				lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
+			}
+		}
+		f4 res[WCT];
+		fwd_range<N, true, 0, N::NL - 1, WCT>(frags, img, lane, res);
+		bwd_wave<N, N::NL - 1>(a, frags, img, dimg, lane, base, acc);
+	}
+	constexpr int RT = 8;
+	static_assert((size_t)WWAVES * RT * 64 * 16 <= N::lds_train(), "reduction rounds fit the images");
+	reduce_tiles<N, 0, RT>(a, reinterpret_cast<f4*>(smem), wave, lane, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1377,12 +1546,17 @@ void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = N::lds_train();
 		if (lds > 160 * 1024) throw std::runtime_error("MLP training LDS footprint exceeds 160 KiB");
-		set_lds<N>(k_mlp_train<N>, lds);
 		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count());
 		m->mlp_partials.reserve((size_t)cu_count() * m->n_mlp_params);
 		a.partials = m->mlp_partials.ptr;
 		a.n_mlp = m->n_mlp_params;
-		launch_timed(k_mlp_train<N>, grid, TBLOCK, lds, s, a);
+		if (m->tuning.mlp_train_schedule == 2) {
+			set_lds<N>(k_mlp_train_w<N>, lds);
+			launch_timed(k_mlp_train_w<N>, grid, WBLOCK, lds, s, a);
+		} else {
+			set_lds<N>(k_mlp_train<N>, lds);
+			launch_timed(k_mlp_train<N>, grid, TBLOCK, lds, s, a);
+		}
 		k_mlp_reduce<<<div_up(16 * m->n_mlp_params, 256), 256, 0, s>>>(m->mlp_partials.ptr, grid, m->n_mlp_params, grads_mlp);
 	});
 	NGP_HIP_CHECK(hipGetLastError());

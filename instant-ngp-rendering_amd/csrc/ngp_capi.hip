@@ -223,6 +223,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		m->params16.release();
 		m->infer16.release();
 		m->adam_steps.release();
+		m->adam_corr.release();
 		m->frag_train.release();
 		m->frag_infer.release();
 		TrainScratch& t = m->ts;
@@ -263,6 +264,8 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->encode_xcd_regions <= 3, "encode_xcd_regions must be 0..3");
 		require(t->render_pass_order <= 3, "render_pass_order must be 0..3");
 		require(t->render_encode_wgs_per_cu <= 32, "render_encode_wgs_per_cu must be <= 32");
+		require(t->mlp_train_schedule <= 2, "mlp_train_schedule must be 0, 1 or 2");
+		require(t->render_slot_compaction <= 2, "render_slot_compaction must be 0, 1 or 2");
 		m->tuning = *t;
 		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
 		m->lt.streaming = encode_streaming_bits(*t);

@@ -308,6 +308,7 @@ struct RenderPipeScratch {
 	DevBuf<float> rgba[3];      // [n][4]
 	DevBuf<float> depth[3];     // [n]
 	DevBuf<float> coords;       // [max_samples][4] position + warped dt, then [max_samples] SH row indices
+	DevBuf<float> stage;        // [max_samples][4] slot compaction: ray i's samples of a pass at i * n_steps
 	DevBuf<__half> enc;         // [L][max_samples][F]
 	DevBuf<__half> out;         // [max_samples][4]
 	DevBuf<uint32_t> counters;  // [16]
@@ -320,7 +321,7 @@ struct RenderPipeScratch {
 	hipEvent_t events[2] = {nullptr, nullptr};  // per-pass counter read-backs
 	void release() {
 		for (int b = 0; b < 3; ++b) { payload[b].release(); rgba[b].release(); depth[b].release(); }
-		coords.release(); enc.release(); out.release(); counters.release();
+		coords.release(); stage.release(); enc.release(); out.release(); counters.release();
 		nrm_dloss.release(); nrm_denc.release(); nrm.release(); nrm_grads.release();
 		if (host_counter.ptr) (void)hipHostFree(host_counter.ptr);
 		host_counter.ptr = nullptr;
@@ -382,6 +383,11 @@ struct ngp_model {
 	ngp::DevBuf<long long> grid_grads64;  // deterministic mode: hash-grid gradients, 2^-40 fixed point
 	ngp::DevBuf<__half> params16, infer16;
 	ngp::DevBuf<uint32_t> adam_steps;
+	// Adam's bias corrections per step count n: {sqrt(1 - beta2^n), 1 - beta1^n}, entries [0, adam_corr_n)
+	// (the optimizer's powf pair was most of its instructions: it ran VALU-bound)
+	ngp::DevBuf<float> adam_corr;
+	uint32_t adam_corr_n = 0;
+	float adam_corr_b1 = 0.0f, adam_corr_b2 = 0.0f;
 	ngp::DevBuf<__half> frag_train, frag_infer;  // packed MFMA fragments of params16 / infer16
 	mutable ngp::DevBuf<float> mlp_partials;      // [workgroup][n_mlp_params] weight-gradient partials of k_mlp_train
 	uint32_t ema_step = 0;

@@ -520,10 +520,17 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 // and an all-empty round jumps on from the last lane's verified skip.  G = 1 for the big
 // early passes (one lane per ray, flat loop), up to 64 for the last few thousand rays,
 // whose long serial marches otherwise dominate the tail passes.
-template <uint32_t G>
+//
+// COMPACT (slot compaction, ngp_tuning.render_slot_compaction = 1, opt-in): a ray marches into its own
+// staging range [i * n_steps, i * n_steps + budget) first, then reserves exactly the samples it found
+// and copies them (L2-resident) to the pass's packed rows -- no reserved-but-unfilled slots (about
+// half the slots of a volumetric scene's pass: rays leave the volume inside their budget).  Measured
+// 3 % slower per frame than the up-front reservation: the unfilled slots cost the encoder (which
+// skips them) and the MLP less than the copy turn costs the latency-bound march.
+template <uint32_t G, bool COMPACT>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
-                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray,
+                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray, float4* __restrict__ stage,
                                                   uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
@@ -549,8 +556,12 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 	Payload* p = payloads + (valid ? i : 0);
 	uint32_t budget = 0;
 	if (valid) budget = sample_budget(k, 1.0f - rgba[i].w, p->alpha_last, n_steps);
-	uint32_t base = block_reserve(r == 0 ? budget : 0u, sample_counter);
-	if (G > 1) base = __shfl(base, g0, 64);
+	uint32_t base = 0;
+	if constexpr (!COMPACT) {
+		base = block_reserve(r == 0 ? budget : 0u, sample_counter);
+		if (G > 1) base = __shfl(base, g0, 64);
+	}
+	float4* const out_rows = COMPACT ? stage + (size_t)i * n_steps : posdt + base;
 	bool running = valid;
 	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f);
 	float n = 0.0f;
@@ -587,9 +598,8 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 				const float t = step_from(k.st, pn);
 				const float dt = step_from(k.st, pn + 1.0f) - t;
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
-				const size_t slot = (size_t)base + j + rank;
-				posdt[slot] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				sray[slot] = row;
+				out_rows[j + rank] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+				if constexpr (!COMPACT) sray[(size_t)base + j + rank] = row;
 			}
 		}
 		if (cnt >= room) {
@@ -608,7 +618,24 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 			}
 		}
 	}
-	if (valid) {
+	if constexpr (COMPACT) {
+		// exactly the samples found: packed rows in ray order within the block
+		base = block_reserve(valid && r == 0 ? j : 0u, sample_counter);
+		if (G > 1) base = __shfl(base, g0, 64);
+		if (valid) {
+			const float4* src = stage + (size_t)i * n_steps;
+			uint32_t q = r;
+			for (; q + 3u * G < j; q += 4u * G) {
+				const float4 a0 = src[q], a1 = src[q + G], a2 = src[q + 2u * G], a3 = src[q + 3u * G];
+				posdt[(size_t)base + q] = a0;
+				posdt[(size_t)base + q + G] = a1;
+				posdt[(size_t)base + q + 2u * G] = a2;
+				posdt[(size_t)base + q + 3u * G] = a3;
+			}
+			for (; q < j; q += G) posdt[(size_t)base + q] = src[q];
+			for (q = r; q < j; q += G) sray[(size_t)base + q] = row;
+		}
+	} else if (valid) {
 		// reserved slots the ray did not fill (it left the volume) still go through the encoder
 		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
 		for (uint32_t q = j + r; q < budget; q += G) {
@@ -935,6 +962,7 @@ struct PipeRun {
 	uint32_t pass = 0, steps_done = 0, n_alive_ub = 0, base_tag = 0;
 	bool marching = false;
 	float4* posdt = nullptr;
+	float4* stage = nullptr;
 	uint32_t* sray = nullptr;
 	uint4* shrows = nullptr;
 	Payload* P(int b) const { return reinterpret_cast<Payload*>(ps->payload[b].ptr); }
@@ -1051,6 +1079,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	const bool block_skipping = tu.render_block_skipping != 0;
 	// the fused encoding + network kernel where it applies (Normals needs the encodings for its backward)
 	const bool fused = tu.render_network == 1 && k.mode != NGP_RENDER_MODE_NORMALS && render_net_supported(m);
+	// slot compaction (ngp_tuning.render_slot_compaction: 1 on, 2 off; 0 the default: off -- 14.37 vs 13.96 ms per
+	// 1080p frame in a same-box A/B: the copy turn costs the march more than the encoder and MLP save)
+	const bool compact = tu.render_slot_compaction == 1;
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
 	for (uint32_t j = 0; j < n_pipes; ++j)
@@ -1084,6 +1115,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH rows (pixel indices)
 		ps.coords.reserve(5 * pr.max_samples);
+		if (compact) ps.stage.reserve(4 * pr.max_samples);
 		if (!fused) ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
@@ -1101,6 +1133,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // the encoder reads 16-B position rows once per level
 		pr.sray = reinterpret_cast<uint32_t*>(ps.coords.ptr + 4 * pr.max_samples);
+		pr.stage = compact ? reinterpret_cast<float4*>(ps.stage.ptr) : nullptr;
 		pr.shrows = rs.shrows.ptr;
 		pr.base_tag = ps.pass_tag;
 		pr.n_alive_ub = pr.n;
@@ -1214,12 +1247,18 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		unsigned long long* host_prev = pass > 0 ? pr.pub_dev() + 8 * ((pass - 1) % HC_SLOTS) : nullptr;
 		const uint32_t tag_prev = pr.base_tag + pass;  // = tag of pass - 1
 		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
-		switch (G) {
-			case 1: k_generate<1><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			case 4: k_generate<4><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			case 16: k_generate<16><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
-			default: k_generate<64><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev); break;
+#define NGP_GEN(GG, CC) k_generate<GG, CC><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.stage, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev)
+		switch (G * 2 + (compact ? 1 : 0)) {
+			case 2: NGP_GEN(1, false); break;
+			case 3: NGP_GEN(1, true); break;
+			case 8: NGP_GEN(4, false); break;
+			case 9: NGP_GEN(4, true); break;
+			case 32: NGP_GEN(16, false); break;
+			case 33: NGP_GEN(16, true); break;
+			case 128: NGP_GEN(64, false); break;
+			default: NGP_GEN(64, true); break;
 		}
+#undef NGP_GEN
 		tm.end(NGP_TIMER_RENDER_MARCH, ps);
 		// sized for the most samples the pass can reserve; the kernels read the actual total
 		const uint64_t bound = std::min<uint64_t>((uint64_t)pr.n_alive_ub * cap_p, std::max(target, pr.n_alive_ub));

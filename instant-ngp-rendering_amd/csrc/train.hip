@@ -1209,31 +1209,65 @@ struct OptArgs {
 	uint32_t* steps;
 	float* ema32;
 	__half* ema16;
+	const float2* corr;  // Adam bias corrections by step count, [0, corr_n) (k_adam_corr)
+	uint32_t corr_n;
 };
 
-__global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
-	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-	if (i >= a.n) return;
-	// a step whose chunked forward missed samples is dropped whole; the caller re-runs it
-	// (ngp_train_discard + full_forward) -- every thread reads the same word
-	if (a.skip && *a.skip) return;
+// {sqrt(1 - beta2^n), 1 - beta1^n} for n in [lo, hi): the expressions adam_update evaluates otherwise,
+// so a table entry and the inline evaluation are the same float
+__global__ void k_adam_corr(float beta1, float beta2, uint32_t lo, uint32_t hi, float2* __restrict__ corr) {
+	const uint32_t n = lo + blockIdx.x * 256u + threadIdx.x;
+	if (n >= hi) return;
+	corr[n] = make_float2(sqrtf(1.0f - powf(beta2, (float)n)), 1.0f - powf(beta1, (float)n));
+}
+
+// One parameter's Adam step (shared by both optimizer kernels, so their arithmetic is identical).
+__device__ __forceinline__ bool adam_update(const OptArgs& a, bool is_mlp, float graw, float& w, float& m, float& v,
+                                            uint32_t& step) {
+	const bool update = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
+	if (!update) return false;
+	float g = graw / a.loss_scale;
+	if (is_mlp) g += a.l2_reg * w;
+	m = a.beta1 * m + (1.0f - a.beta1) * g;
+	v = a.beta2 * v + (1.0f - a.beta2) * g * g;
+	step = step + 1u;
+	float lr;
+	if (step < a.corr_n) {
+		const float2 c = a.corr[step];
+		lr = a.lr * c.x / c.y;
+	} else {
+		lr = a.lr * sqrtf(1.0f - powf(a.beta2, (float)step)) / (1.0f - powf(a.beta1, (float)step));
+	}
+	w = w - (lr / (sqrtf(v) + a.eps)) * m;
+	return true;
+}
+
+__device__ __forceinline__ float ema_update(const OptArgs& a, float e, float w) {
+	return (e * a.ema_decay * a.ema_debias_old + w * (1.0f - a.ema_decay)) / a.ema_debias_new;
+}
+
+// deterministic hash-grid gradients are the exact sum rounded to fp16 once -- the precision the fp16
+// buffer holds, so the sparse skip of zero gradients (a sum below fp16's range is zero) matches
+__device__ __forceinline__ float fixed_grad(long long q) { return __half2float(__float2half((float)q * GRAD_FIXED_INV)); }
+
+__device__ __forceinline__ void optimize_one(const OptArgs& a, uint64_t i) {
 	const bool is_mlp = i < a.n_mlp;
-	// deterministic hash-grid gradients are the exact sum rounded to fp16 once -- the precision the fp16
-	// buffer holds, so the sparse skip of zero gradients (a sum below fp16's range is zero) matches
 	float graw;
 	if (is_mlp) graw = a.grad[i];
-	else if (a.grad64) graw = __half2float(__float2half((float)a.grad64[i - a.n_mlp] * GRAD_FIXED_INV));
+	else if (a.grad64) graw = fixed_grad(a.grad64[i - a.n_mlp]);
 	else graw = __half2float(a.grad16[i - a.n_mlp]);
 	float w = a.w32[i];
-	bool update = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
-	if (update) {
-		float g = graw / a.loss_scale;
-		if (is_mlp) g += a.l2_reg * w;
-		const float m = a.m[i] = a.beta1 * a.m[i] + (1.0f - a.beta1) * g;
-		const float v = a.v[i] = a.beta2 * a.v[i] + (1.0f - a.beta2) * g * g;
-		const uint32_t step = ++a.steps[i];
-		const float lr = a.lr * sqrtf(1.0f - powf(a.beta2, (float)step)) / (1.0f - powf(a.beta1, (float)step));
-		w = w - (lr / (sqrtf(v) + a.eps)) * m;
+	float m, v;
+	uint32_t st;
+	const bool is_upd = is_mlp ? (bool)a.opt_mlp : (a.opt_enc && graw != 0.0f);
+	if (is_upd) {
+		m = a.m[i];
+		v = a.v[i];
+		st = a.steps[i];
+		adam_update(a, is_mlp, graw, w, m, v, st);
+		a.m[i] = m;
+		a.v[i] = v;
+		a.steps[i] = st;
 		a.w32[i] = w;
 		a.w16[i] = __float2half(w);
 	}
@@ -1242,9 +1276,116 @@ __global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
 		else if (a.grad64) a.grad64[i - a.n_mlp] = 0;
 		else a.grad16[i - a.n_mlp] = __float2half(0.0f);
 	}
-	const float e = (a.ema32[i] * a.ema_decay * a.ema_debias_old + w * (1.0f - a.ema_decay)) / a.ema_debias_new;
+	const float e = ema_update(a, a.ema32[i], w);
 	a.ema32[i] = e;
 	a.ema16[i] = __float2half(e);
+}
+
+__global__ void __launch_bounds__(256) k_optimizer(OptArgs a) {
+	const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+	if (i >= a.n) return;
+	// a step whose chunked forward missed samples is dropped whole; the caller re-runs it
+	// (ngp_train_discard + full_forward) -- every thread reads the same word
+	if (a.skip && *a.skip) return;
+	optimize_one(a, i);
+}
+
+// The same update, 8 consecutive parameters per thread with 16-B loads and stores (the one-per-thread
+// kernel moves 2- and 4-B words per lane and reached half of the HBM rate).  Needs n_mlp % 8 == 0, so a
+// group lies wholly in the MLP or the grid part; Adam's moments and step counts are read only for groups
+// with an update (the grid's sparse skip).
+__device__ __forceinline__ void ld8(const float* p, float (&x)[8]) {
+	const float4 u = reinterpret_cast<const float4*>(p)[0], v = reinterpret_cast<const float4*>(p)[1];
+	x[0] = u.x, x[1] = u.y, x[2] = u.z, x[3] = u.w, x[4] = v.x, x[5] = v.y, x[6] = v.z, x[7] = v.w;
+}
+__device__ __forceinline__ void st8(float* p, const float (&x)[8]) {
+	reinterpret_cast<float4*>(p)[0] = make_float4(x[0], x[1], x[2], x[3]);
+	reinterpret_cast<float4*>(p)[1] = make_float4(x[4], x[5], x[6], x[7]);
+}
+__device__ __forceinline__ void st8h(__half* p, const float (&x)[8]) {
+	uint4 u;
+	uint32_t* w = reinterpret_cast<uint32_t*>(&u);
+#pragma unroll
+	for (int k = 0; k < 4; ++k) {
+		const __half2 h = __halves2half2(__float2half(x[2 * k]), __float2half(x[2 * k + 1]));
+		w[k] = *reinterpret_cast<const uint32_t*>(&h);
+	}
+	*reinterpret_cast<uint4*>(p) = u;
+}
+
+__global__ void __launch_bounds__(256) k_optimizer8(OptArgs a) {
+	const uint64_t i0 = ((uint64_t)blockIdx.x * 256u + threadIdx.x) * 8u;
+	if (i0 >= a.n) return;
+	if (a.skip && *a.skip) return;
+	if (i0 + 8 > a.n) {
+		for (uint64_t i = i0; i < a.n; ++i) optimize_one(a, i);
+		return;
+	}
+	const bool is_mlp = i0 < a.n_mlp;
+	const uint64_t gi = i0 - a.n_mlp;
+	float g[8];
+	if (is_mlp) {
+		ld8(a.grad + i0, g);
+	} else if (a.grad64) {
+		const longlong2* q = reinterpret_cast<const longlong2*>(a.grad64 + gi);
+#pragma unroll
+		for (int k = 0; k < 4; ++k) {
+			const longlong2 t = q[k];
+			g[2 * k] = fixed_grad(t.x);
+			g[2 * k + 1] = fixed_grad(t.y);
+		}
+	} else {
+		const uint4 u = *reinterpret_cast<const uint4*>(a.grad16 + gi);
+		const __half* h = reinterpret_cast<const __half*>(&u);
+#pragma unroll
+		for (int k = 0; k < 8; ++k) g[k] = __half2float(h[k]);
+	}
+	float w[8];
+	ld8(a.w32 + i0, w);
+	uint32_t upd = 0, nz = 0;
+#pragma unroll
+	for (int k = 0; k < 8; ++k) {
+		if (is_mlp ? (bool)a.opt_mlp : (a.opt_enc && g[k] != 0.0f)) upd |= 1u << k;
+		if (g[k] != 0.0f) nz |= 1u << k;
+	}
+	if (upd) {
+		float m[8], v[8];
+		ld8(a.m + i0, m);
+		ld8(a.v + i0, v);
+		uint4 s0 = reinterpret_cast<const uint4*>(a.steps + i0)[0], s1 = reinterpret_cast<const uint4*>(a.steps + i0)[1];
+		uint32_t st[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+#pragma unroll
+		for (int k = 0; k < 8; ++k) adam_update(a, is_mlp, g[k], w[k], m[k], v[k], st[k]);
+		st8(a.m + i0, m);
+		st8(a.v + i0, v);
+		reinterpret_cast<uint4*>(a.steps + i0)[0] = make_uint4(st[0], st[1], st[2], st[3]);
+		reinterpret_cast<uint4*>(a.steps + i0)[1] = make_uint4(st[4], st[5], st[6], st[7]);
+		st8(a.w32 + i0, w);
+		if (upd == 0xffu) {
+			st8h(a.w16 + i0, w);
+		} else {
+			// parameters without an update keep their fp16 copy untouched
+			uint4 old = *reinterpret_cast<const uint4*>(a.w16 + i0);
+			__half* oh = reinterpret_cast<__half*>(&old);
+#pragma unroll
+			for (int k = 0; k < 8; ++k)
+				if ((upd >> k) & 1u) oh[k] = __float2half(w[k]);
+			*reinterpret_cast<uint4*>(a.w16 + i0) = old;
+		}
+	}
+	if (nz) {  // GradientMode::Overwrite for the next step (zeros where they already are change nothing)
+		if (is_mlp) reinterpret_cast<float4*>(a.grad + i0)[0] = reinterpret_cast<float4*>(a.grad + i0)[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+		else if (a.grad64) {
+#pragma unroll
+			for (int k = 0; k < 4; ++k) reinterpret_cast<longlong2*>(a.grad64 + gi)[k] = make_longlong2(0, 0);
+		} else *reinterpret_cast<uint4*>(a.grad16 + gi) = make_uint4(0u, 0u, 0u, 0u);
+	}
+	float e[8];
+	ld8(a.ema32 + i0, e);
+#pragma unroll
+	for (int k = 0; k < 8; ++k) e[k] = ema_update(a, e[k], w[k]);
+	st8(a.ema32 + i0, e);
+	st8h(a.ema16 + i0, e);
 }
 
 __global__ void k_to_half(const float* __restrict__ src, __half* __restrict__ dst, uint64_t n) {
@@ -1288,8 +1429,29 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.steps = m->adam_steps.ptr;
 	a.ema32 = m->ema32.ptr;
 	a.ema16 = m->infer16.ptr;
+	// bias-correction table up to step + 2 (a parameter's count is at most the optimizer steps taken;
+	// larger counts, e.g. restored from a snapshot, fall back to the inline evaluation)
+	{
+		const uint32_t need = std::min<uint32_t>(step, 1u << 20) + 2u;
+		if (m->adam_corr_b1 != c.beta1 || m->adam_corr_b2 != c.beta2) m->adam_corr_n = 0;
+		if (need > m->adam_corr_n) {
+			uint32_t lo = m->adam_corr_n;
+			if ((size_t)need * 2 > m->adam_corr.n) {
+				m->adam_corr.reserve((size_t)std::max<uint32_t>(need * 2u, 1u << 16) * 2);  // grows: refill all
+				lo = 0;
+			}
+			k_adam_corr<<<div_up(need - lo, 256u), 256, 0, s>>>(c.beta1, c.beta2, lo, need, reinterpret_cast<float2*>(m->adam_corr.ptr));
+			NGP_HIP_CHECK(hipGetLastError());
+			m->adam_corr_n = need;
+			m->adam_corr_b1 = c.beta1;
+			m->adam_corr_b2 = c.beta2;
+		}
+	}
+	a.corr = reinterpret_cast<const float2*>(m->adam_corr.ptr);
+	a.corr_n = m->adam_corr_n;
 	m->timers.begin_kernel(NGP_TIMER_OPTIMIZER);
-	launch_timed(k_optimizer, div_up(a.n, 256), 256, 0, s, a);
+	if (a.n_mlp % 8 == 0) launch_timed(k_optimizer8, div_up(div_up(a.n, 8), 256), 256, 0, s, a);
+	else launch_timed(k_optimizer, div_up(a.n, 256), 256, 0, s, a);
 	m->timers.end(NGP_TIMER_OPTIMIZER, s, a.n);
 	NGP_HIP_CHECK(hipGetLastError());
 	++m->ema_step;

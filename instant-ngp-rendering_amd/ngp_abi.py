@@ -119,6 +119,8 @@ class Tuning(C.Structure):
         ("train_chain_walk", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
         ("encode_xcd_regions", C.c_uint32), ("render_pass_order", C.c_uint32),
         ("render_encode_wgs_per_cu", C.c_uint32),
+        ("mlp_train_schedule", C.c_uint32),
+        ("render_slot_compaction", C.c_uint32),
     ]
 
 

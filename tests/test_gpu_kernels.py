@@ -135,9 +135,13 @@ def test_density_matches_oracle_and_infer(name):
         g.close()
 
 
-@pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
-def test_mlp_backward_matches_oracle(name):
+@pytest.mark.parametrize("schedule", [1, 2])
+@pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14", "E_L16F2T22"])
+def test_mlp_backward_matches_oracle(name, schedule):
+    """Both training-MLP schedules (ngp_tuning.mlp_train_schedule: 8 waves with wave-shared weight
+    gradients, or 4 wave-independent waves) against the oracle's NerfNetwork backward."""
     g, o, rng = make(name)
+    g.set_tuning(mlp_train_schedule=schedule)
     try:
         n = 1000
         coords = random_coords(rng, n)
@@ -153,6 +157,32 @@ def test_mlp_backward_matches_oracle(name):
         assert rel < 1e-2, rel
         dr = np.linalg.norm(gd - od) / max(np.linalg.norm(od), 1e-12)
         assert dr < 1e-2, dr
+    finally:
+        g.close()
+
+
+@pytest.mark.parametrize("name", ["B_L16F2T19", "base_L8F4T19"])
+def test_mlp_train_schedules_agree_at_batch_size(name):
+    """At a full 2^18 batch (+ a ragged tail: every wave runs many persistent steps and the last
+    step is partial) the two training-MLP schedules give the same weight and input gradients up to
+    the fp32 association of the sums."""
+    g, o, rng = make(name)
+    try:
+        n = (1 << 18) + 77
+        coords = random_coords(rng, n)
+        enc = g.encode(coords[:, :3])
+        dl = (rng.normal(0, 1e-2, (n, 4))).astype(np.float16).astype(np.float32)
+        w = rng.uniform(1, 2, n).astype(np.float32)
+        out = []
+        for schedule in (1, 2):
+            g.set_tuning(mlp_train_schedule=schedule)
+            g.zero_grads()
+            gd = g.backward(enc, coords[:, 4:7], dl, w)
+            out.append((g.get(A.GRADS_FP32)[: g.n_mlp].copy(), gd.copy()))
+        (g1, d1), (g2, d2) = out
+        assert np.linalg.norm(g1 - g2) / np.linalg.norm(g1) < 1e-5
+        # dL/denc is per sample (no cross-sample sum): identical
+        np.testing.assert_array_equal(d1, d2)
     finally:
         g.close()
 

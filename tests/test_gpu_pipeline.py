@@ -245,13 +245,18 @@ def test_chunked_forward_matches_full_forward():
 
 
 def test_optimizer_matches_oracle():
+    """Ema(ExponentialDecay(Adam)) against the oracle: full MLP gradients, a sparse grid gradient (most
+    8-parameter groups of the vectorised kernel without an update, some partly updated)."""
     g, o, rng = pair(CFG_B)
     try:
+        p16_before = g.get(A.PARAMS_FP16)
+        touched = np.zeros(g.n_params, bool)
         for step in (0, 1, 20000):
             grads = np.zeros(g.n_params, np.float32)
             grads[: g.n_mlp] = rng.normal(0, 1, g.n_mlp)
             idx = rng.choice(g.n_params - g.n_mlp, 50000, replace=False) + g.n_mlp
             grads[idx] = rng.normal(0, 1, idx.size)
+            touched[idx] = True
             o.set_grads(g.set_grads(grads))  # grid part as the fp16 the device holds
             A.check(g.lib.ngp_optimizer_step(g.h, step, 1, 1, stream()))
             torch.cuda.synchronize()
@@ -260,6 +265,13 @@ def test_optimizer_matches_oracle():
             np.testing.assert_allclose(g.get(kind), o.get(kind), rtol=1e-5, atol=1e-7)
         assert not g.get(A.GRADS_FP32).any()  # GradientMode::Overwrite: zeroed for the next step
         assert not g.get(A.GRADS_GRID_FP16).any()
+        # fp16 copies: updated parameters = fp16(fp32), the others untouched
+        touched[: g.n_mlp] = True
+        p32, p16 = g.get(A.PARAMS_FP32)[: g.n_params], g.get(A.PARAMS_FP16)[: g.n_params]
+        np.testing.assert_array_equal(p16[touched], p32[touched].astype(np.float16).view(np.uint16))
+        np.testing.assert_array_equal(p16[~touched], p16_before[: g.n_params][~touched])
+        e32, e16 = g.get(A.PARAMS_EMA_FP32)[: g.n_params], g.get(A.PARAMS_INFER_FP16)[: g.n_params]
+        np.testing.assert_array_equal(e16, e32.astype(np.float16).view(np.uint16))
     finally:
         g.close()
 
@@ -479,7 +491,11 @@ def test_render_config_e_full_network_matches_oracle():
                    dict(render_pipelines=3, render_pass_order=3, render_encode_wgs_per_cu=1),
                    dict(render_pipelines=2, render_pass_order=2, render_encode_wgs_per_cu=4),
                    dict(render_network=1, render_pass_order=2),
-                   dict(render_network=0, render_pipelines=0, render_pass_order=0, render_encode_wgs_per_cu=0)):
+                   dict(render_network=0, render_pipelines=0, render_pass_order=0, render_encode_wgs_per_cu=0),
+                   # every ray's samples of a pass staged and compacted to packed rows instead of reserved up front
+                   dict(render_slot_compaction=1), dict(render_slot_compaction=1, render_network=1),
+                   dict(render_slot_compaction=1, render_network=0, render_pipelines=3),
+                   dict(render_slot_compaction=0, render_pipelines=0)):
             g.set_tuning(**kw)
             frame.zero_()
             A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))

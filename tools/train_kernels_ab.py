@@ -3,7 +3,8 @@ every kernel timer on and prints the mean launch time of each timer class.  Run 
 (--pkg: a directory with another build of pyngp + libngp_hip, tools/ab_build_old.sh) to compare
 kernels on one box.
 
-Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400]
+Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400] [--settings "mlp_train_schedule=1" "mlp_train_schedule=2"]
+(--settings: ngp_tuning fields per setting, timed round-robin on the same trained model)
 """
 import argparse
 import ctypes as C
@@ -19,6 +20,8 @@ def main():
     p.add_argument("--pkg", default=None)
     p.add_argument("--steps", type=int, default=400)
     p.add_argument("--timed", type=int, default=100)
+    p.add_argument("--rounds", type=int, default=3)
+    p.add_argument("--settings", nargs="*", default=[""])
     p.add_argument("--config", default=os.path.join(ROOT, "instant-ngp-rendering_amd", "configs", "nerf", "lego_L16F2.json"))
     p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
     a = p.parse_args()
@@ -35,17 +38,33 @@ def main():
         tb.train(1 << 18)
     lib = A.load(os.path.join(os.path.abspath(a.pkg), "libngp_hip.so")) if a.pkg else A.load()
     h = C.c_void_p(tb.model_handle)
-    A.check(lib.ngp_timing_enable(h, -1))
-    for _ in range(a.timed):
-        tb.train(1 << 18)
-    tb.sync()
+    base = tb.get_tuning()
     print(f"# pyngp {ngp.__file__}")
-    for name, idx in A.TIMER.items():
-        ms, units, launches = C.c_double(), C.c_uint64(), C.c_uint32()
-        A.check(lib.ngp_timing_read(h, idx, C.byref(ms), C.byref(units), C.byref(launches), 1))
-        if launches.value:
-            print(f"{name:20s} {1000.0 * ms.value / launches.value:9.2f} us/launch  {launches.value:6d} launches")
-
+    acc = {st: {} for st in a.settings}
+    for r in range(a.rounds):
+        for st in a.settings:
+            setting = dict(base)
+            for kv in st.split():
+                k, v = kv.split("=", 1)
+                setting[k] = int(v)
+            tb.set_tuning(setting)
+            tb.train(1 << 18)
+            tb.sync()
+            A.check(lib.ngp_timing_enable(h, -1))
+            for idx in A.TIMER.values():  # discard what the warm-up step accumulated
+                A.check(lib.ngp_timing_read(h, idx, None, None, None, 1))
+            for _ in range(a.timed):
+                tb.train(1 << 18)
+            tb.sync()
+            for name, idx in A.TIMER.items():
+                ms, units, launches = C.c_double(), C.c_uint64(), C.c_uint32()
+                A.check(lib.ngp_timing_read(h, idx, C.byref(ms), C.byref(units), C.byref(launches), 1))
+                if launches.value:
+                    acc[st].setdefault(name, []).append(1000.0 * ms.value / launches.value)
+    for st in a.settings:
+        print(f"## {st or 'default'}")
+        for name, v in acc[st].items():
+            print(f"{name:20s} {sorted(v)[len(v) // 2]:9.2f} us/launch (median of {len(v)} rounds: {', '.join(f'{x:.2f}' for x in v)})")
 
 if __name__ == "__main__":
     main()
