@@ -83,11 +83,74 @@ __global__ void k_scan_add(uint32_t* __restrict__ out, uint32_t n, const uint32_
 	if (i < n) out[i] += block_sums[i / 1024u];
 }
 
+// The whole scan in one workgroup (n up to SCAN_ONE_BLOCK_MAX: a training batch's rays): tiles of 16 K
+// elements staged through LDS (coalesced loads and stores), 16 consecutive elements per thread, wave
+// scans, LDS totals, a carry across tiles -- one launch instead of three launch-latency-bound ones (the
+// rays of a volume scene's batch are ~2 k, of a surface scene ~35 k).
+constexpr uint32_t SCAN_ONE_BLOCK_MAX = 1u << 17;
+__global__ void __launch_bounds__(1024) k_scan_one_block(const uint32_t* __restrict__ in, uint32_t* __restrict__ out,
+                                                         uint32_t n, uint32_t* __restrict__ total) {
+	constexpr uint32_t PER = 16, TILE = 1024 * PER;
+	__shared__ uint32_t wsum[16];
+	__shared__ uint4 stage[TILE / 4];
+	uint32_t* st = reinterpret_cast<uint32_t*>(stage);
+	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
+	uint32_t carry = 0;
+	for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
+#pragma unroll
+		for (uint32_t k = 0; k < PER; ++k) {
+			const uint32_t e = k * 1024u + threadIdx.x;
+			st[e] = t0 + e < n ? in[t0 + e] : 0u;
+		}
+		__syncthreads();
+		uint32_t v[PER], tsum = 0;
+#pragma unroll
+		for (uint32_t q = 0; q < PER / 4; ++q) {
+			const uint4 u = stage[threadIdx.x * (PER / 4) + q];
+			v[4 * q] = u.x, v[4 * q + 1] = u.y, v[4 * q + 2] = u.z, v[4 * q + 3] = u.w;
+		}
+#pragma unroll
+		for (uint32_t k = 0; k < PER; ++k) tsum += v[k];
+		const uint32_t incl = wave_inclusive_scan(tsum);
+		if (lane == 63) wsum[w] = incl;
+		__syncthreads();
+		uint32_t woff = carry, tile_total = 0;
+		for (uint32_t q = 0; q < 16; ++q) {
+			if (q < w) woff += wsum[q];
+			tile_total += wsum[q];
+		}
+		uint32_t run = woff + incl - tsum;
+#pragma unroll
+		for (uint32_t q = 0; q < PER / 4; ++q) {
+			uint4 u;
+			u.x = run, run += v[4 * q];
+			u.y = run, run += v[4 * q + 1];
+			u.z = run, run += v[4 * q + 2];
+			u.w = run, run += v[4 * q + 3];
+			stage[threadIdx.x * (PER / 4) + q] = u;
+		}
+		__syncthreads();
+#pragma unroll
+		for (uint32_t k = 0; k < PER; ++k) {
+			const uint32_t e = k * 1024u + threadIdx.x;
+			if (t0 + e < n) out[t0 + e] = st[e];
+		}
+		carry += tile_total;
+		__syncthreads();  // stage and wsum are rewritten by the next tile
+	}
+	if (threadIdx.x == 0) *total = carry;
+}
+
 void launch_exclusive_scan(const uint32_t* in, uint32_t* out, uint32_t n, uint32_t* block_sums, uint32_t* total,
                            hipStream_t s) {
 	const uint32_t nb = div_up(n, 1024);
 	if (nb == 0) {
 		NGP_HIP_CHECK(hipMemsetAsync(total, 0, sizeof(uint32_t), s));
+		return;
+	}
+	if (n <= SCAN_ONE_BLOCK_MAX) {
+		k_scan_one_block<<<1, 1024, 0, s>>>(in, out, n, total);
+		NGP_HIP_CHECK(hipGetLastError());
 		return;
 	}
 	k_scan_local<<<nb, 256, 0, s>>>(in, out, n, block_sums);
