@@ -365,6 +365,8 @@ typedef struct ngp_tuning {
 	uint32_t render_slot_compaction; /* march passes: 1 = each ray stages its samples and then takes exactly the
 	                                    rows it filled (packed pass rows); 2 = rays reserve their whole budget up
 	                                    front, unfilled slots marked and skipped; 0: the default (2) */
+	uint32_t render_skip_unfilled;   /* 1 = the render MLP skips 16-sample column tiles of slots no ray filled (marked
+	                                    by k_generate), 2 = computes every reserved slot; 0: the default */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -155,6 +155,7 @@ struct MlpArgs {
 	uint32_t out_mode, out_stride;    // 0: out [n][4]; 1 / 2: the reference's 16-row output, column- / row-major
 	float* partials;                  // k_mlp_train: [workgroup][n_mlp_params] weight-gradient partials
 	uint32_t n_mlp;                   // MLP parameter count (partials row pitch)
+	uint32_t skip_unfilled;           // SH-row inference: skip column tiles whose rows are all NO_SH_ROW
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -490,13 +491,15 @@ __device__ __forceinline__ void sh4_slice(const float* dw, int g, float (&o)[4])
 }
 
 // one layer: B operands in (KS steps) -> C tiles out (MT tiles), weights w[frag]
+// live: wave-uniform mask of the column tiles to compute (render slots no ray filled are skipped)
 template <class N, int l, int CT_>
-__device__ __forceinline__ void rf_layer(const h8* w, const h8 (&bin)[CT_][2], f4 (&cout)[CT_][4]) {
+__device__ __forceinline__ void rf_layer(const h8* w, const h8 (&bin)[CT_][2], f4 (&cout)[CT_][4], uint32_t live) {
 	constexpr int MT = N::Mt(l), KS = N::Ks(l), F0 = N::fwd_frags_upto(l);
 #pragma unroll
 	for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
 		for (int c = 0; c < CT_; ++c) {
+			if (!((live >> c) & 1u)) continue;
 			f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
 			for (int s = 0; s < KS; ++s) acc = mfma(w[(F0 + mt * KS + s) * 64], bin[c][s], acc);
@@ -528,11 +531,11 @@ __device__ __forceinline__ void rf_chain(const f4 (&cin)[CT_][4], h8 (&bout)[CT_
 }
 
 template <class N, int l, int END, int CT_>
-__device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4 (&c)[CT_][4]) {
+__device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4 (&c)[CT_][4], uint32_t live) {
 	if constexpr (l < END) {
-		rf_layer<N, l, CT_>(w, b, c);
+		rf_layer<N, l, CT_>(w, b, c, live);
 		rf_chain<N::Mt(l), CT_>(c, b);
-		rf_hidden_range<N, l + 1, END, CT_>(w, b, c);
+		rf_hidden_range<N, l + 1, END, CT_>(w, b, c, live);
 	}
 }
 
@@ -550,8 +553,19 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 #pragma unroll
 		for (int s = 0; s < N::KE; ++s)
 			b[cc][s] = pack_h8(cur.e[cc][4 * s], cur.e[cc][4 * s + 1], cur.e[cc][4 * s + 2], cur.e[cc][4 * s + 3]);
-	rf_hidden_range<N, 0, N::DH, CT_>(w, b, c);
-	rf_layer<N, N::DH, CT_>(w, b, c);
+	// SH-row inputs (renderer): a 16-sample column tile whose slots no ray filled (k_generate marks them
+	// with row NO_SH_ROW) is not computed -- k_composite reads a ray's filled samples only
+	uint32_t live = (1u << CT_) - 1u;
+	if constexpr (SHIN && !DENSITY_ONLY) {
+		if (a.skip_unfilled) {
+			live = 0;
+#pragma unroll
+			for (int cc = 0; cc < CT_; ++cc) live |= (__ballot(cur.ri[cc] != NO_SH_ROW) != 0ull ? 1u : 0u) << cc;
+			if (live == 0) return;
+		}
+	}
+	rf_hidden_range<N, 0, N::DH, CT_>(w, b, c, live);
+	rf_layer<N, N::DH, CT_>(w, b, c, live);
 	if constexpr (DENSITY_ONLY) {
 		if (g == 0) {
 #pragma unroll
@@ -576,14 +590,14 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 				b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
 			}
 		}
-		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
-		rf_layer<N, N::NL - 1, CT_>(w, b, c);
+		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c, live);
+		rf_layer<N, N::NL - 1, CT_>(w, b, c, live);
 		if (a.out_mode == 0) {
 			if (g == 0) {
 #pragma unroll
 				for (int cc = 0; cc < CT_; ++cc) {
 					const uint32_t i = base + 16 * cc + n;
-					if (i < a.n) {
+					if (i < a.n && ((live >> cc) & 1u)) {
 						const h4 o = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], dens[cc]};
 						*reinterpret_cast<h4*>(a.out + (size_t)i * 4) = o;
 					}
@@ -1402,7 +1416,7 @@ static void set_lds(K kernel, size_t bytes) {
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev, uint32_t dir_offset, const __half* sh, uint32_t out_mode, uint32_t out_stride,
-                      const uint32_t* sh_ray, uint32_t sh_rows) {
+                      const uint32_t* sh_ray, uint32_t sh_rows, bool skip_unfilled) {
 	if (n == 0) return;
 	if (enc_layout.lsh != m->enc_lsh) throw std::runtime_error("encoding layout differs from the packed first layer's");
 	MlpArgs a = base_args(m);
@@ -1425,6 +1439,7 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.sh_bytes = (uint32_t)std::min<uint64_t>((uint64_t)sh_rows * 32, 0xffffffffu);
 	a.out_mode = out_mode;
 	a.out_stride = out_stride;
+	a.skip_unfilled = skip_unfilled && sh_ray && out_mode == 0;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
 		// workgroups per CU (ngp_tuning.mlp_workgroups_per_cu; 8 measured 0.6 % faster per frame than

@@ -266,6 +266,7 @@ ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 		require(t->render_encode_wgs_per_cu <= 32, "render_encode_wgs_per_cu must be <= 32");
 		require(t->mlp_train_schedule <= 2, "mlp_train_schedule must be 0, 1 or 2");
 		require(t->render_slot_compaction <= 2, "render_slot_compaction must be 0, 1 or 2");
+		require(t->render_skip_unfilled <= 2, "render_skip_unfilled must be 0, 1 or 2");
 		m->tuning = *t;
 		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
 		m->lt.streaming = encode_streaming_bits(*t);

@@ -128,6 +128,10 @@ struct KernelTimers {
 constexpr uint32_t MAX_LEVELS = 32;
 constexpr uint32_t MAX_LAYERS = 8;
 
+// SH row index k_generate gives the render slots a ray reserved but did not fill (ngp_tuning.render_skip_unfilled):
+// the render MLP skips 16-sample column tiles made of them (their SH loads fall past the rows: zero)
+constexpr uint32_t NO_SH_ROW = 0xFFFFFFFFu;
+
 // Per-level hash-grid geometry, computed once on the host (tcnn GridEncodingTemplated ctor).
 struct LevelTable {
 	uint32_t n_levels;
@@ -446,7 +450,8 @@ void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frag
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr,
-                      uint32_t out_mode = 0, uint32_t out_stride = 4, const uint32_t* sh_ray = nullptr, uint32_t sh_rows = 0);
+                      uint32_t out_mode = 0, uint32_t out_stride = 4, const uint32_t* sh_ray = nullptr, uint32_t sh_rows = 0,
+                      bool skip_unfilled = false);
 // render.hip: the octant distance fields of the bitfield's mips [0, max_mip] into m->rs.df (rebuilt only
 // when the bitfield changed); the renderer's march and the training sampler (aabb_scale 1) read them
 void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s);

@@ -66,6 +66,7 @@ struct RenderK {
 	int hard_edges;
 	float aperture, focus_z;  // depth of field (uv_to_ray, common_device.cuh:450-456)
 	const float* normals;     // Normals mode: d(raw density)/d(warped position) per sample slot of the pass, [slot][3]
+	int mark_unfilled;        // unfilled slots get SH row NO_SH_ROW (the render MLP skips tiles of them)
 };
 
 // square2disk_shirley (random_val.cuh:112-128)
@@ -638,9 +639,10 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 	} else if (valid) {
 		// reserved slots the ray did not fill (it left the volume) still go through the encoder
 		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
+		const uint32_t tail_row = k.mark_unfilled ? NO_SH_ROW : row;
 		for (uint32_t q = j + r; q < budget; q += G) {
 			posdt[(size_t)base + q] = make_float4(-1.0f, -1.0f, -1.0f, 0.0f);
-			sray[(size_t)base + q] = row;
+			sray[(size_t)base + q] = tail_row;
 		}
 	}
 	if (k.dbg && valid && r == 0) {
@@ -1082,6 +1084,10 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// slot compaction (ngp_tuning.render_slot_compaction: 1 on, 2 off; 0 the default: off -- 14.37 vs 13.96 ms per
 	// 1080p frame in a same-box A/B: the copy turn costs the march more than the encoder and MLP save)
 	const bool compact = tu.render_slot_compaction == 1;
+	// unfilled slots marked for the render MLP to skip (ngp_tuning.render_skip_unfilled: 1 on, 2 off; 0 the
+	// default); Normals runs the MLP backward over every slot, so it keeps real rows
+	const bool skip_unfilled = tu.render_skip_unfilled != 2 && k.mode != NGP_RENDER_MODE_NORMALS;
+	k.mark_unfilled = skip_unfilled ? 1 : 0;
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
 	for (uint32_t j = 0; j < n_pipes; ++j)
@@ -1297,7 +1303,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			if (order == 2) chain_mark(pr);
 			tm.begin_kernel(NGP_TIMER_RENDER_MLP);
 			launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
-			                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows);
+			                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows, skip_unfilled);
 			tm.end(NGP_TIMER_RENDER_MLP, ps);
 			if (order == 3) chain_mark(pr);
 		}

@@ -121,6 +121,7 @@ class Tuning(C.Structure):
         ("render_encode_wgs_per_cu", C.c_uint32),
         ("mlp_train_schedule", C.c_uint32),
         ("render_slot_compaction", C.c_uint32),
+        ("render_skip_unfilled", C.c_uint32),
     ]
 
 

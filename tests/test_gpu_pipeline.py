@@ -495,7 +495,10 @@ def test_render_config_e_full_network_matches_oracle():
                    # every ray's samples of a pass staged and compacted to packed rows instead of reserved up front
                    dict(render_slot_compaction=1), dict(render_slot_compaction=1, render_network=1),
                    dict(render_slot_compaction=1, render_network=0, render_pipelines=3),
-                   dict(render_slot_compaction=0, render_pipelines=0)):
+                   dict(render_slot_compaction=0, render_pipelines=0),
+                   # the render MLP computing every reserved slot instead of skipping tiles no ray filled
+                   dict(render_skip_unfilled=2), dict(render_skip_unfilled=1, render_mlp_tile=1),
+                   dict(render_skip_unfilled=0, render_mlp_tile=0)):
             g.set_tuning(**kw)
             frame.zero_()
             A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
