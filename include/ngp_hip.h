@@ -367,6 +367,8 @@ typedef struct ngp_tuning {
 	                                    front, unfilled slots marked and skipped; 0: the default (2) */
 	uint32_t render_skip_unfilled;   /* 1 = the render MLP skips 16-sample column tiles of slots no ray filled (marked
 	                                    by k_generate), 2 = computes every reserved slot; 0: the default */
+	uint32_t render_tail_rays;       /* march passes with at most this many alive rays composite with all of a ray's
+	                                    samples of the pass loaded at once; 0: never (the default) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

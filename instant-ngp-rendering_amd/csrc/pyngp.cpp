@@ -42,7 +42,7 @@ static py::array_t<float> pinned_frame(int height, int width) {
 	NGP_TUNING_FIELD(render_network) NGP_TUNING_FIELD(render_net_workgroups_per_cu)                          \
 	NGP_TUNING_FIELD(train_chain_walk) NGP_TUNING_FIELD(grid_unsorted) NGP_TUNING_FIELD(render_mlp_tile) NGP_TUNING_FIELD(encode_xcd_regions) \
 	NGP_TUNING_FIELD(render_pass_order) NGP_TUNING_FIELD(render_encode_wgs_per_cu) \
-	NGP_TUNING_FIELD(mlp_train_schedule) NGP_TUNING_FIELD(render_slot_compaction) NGP_TUNING_FIELD(render_skip_unfilled)
+	NGP_TUNING_FIELD(mlp_train_schedule) NGP_TUNING_FIELD(render_slot_compaction) NGP_TUNING_FIELD(render_skip_unfilled) NGP_TUNING_FIELD(render_tail_rays)
 
 namespace {
 

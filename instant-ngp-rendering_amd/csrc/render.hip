@@ -659,6 +659,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 
 // samples loaded ahead of their use in k_composite
 constexpr uint32_t COMPOSITE_AHEAD = 4;  // 8 measured no better (same-weights A/B)
+// the tail passes (few rays, up to 32 samples each): every sample of the pass loaded at once, so a ray's
+// composite waits for one load round trip instead of eight (the same serial arithmetic: same image)
+constexpr uint32_t COMPOSITE_AHEAD_TAIL = 32;
 
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
@@ -667,7 +670,7 @@ constexpr uint32_t COMPOSITE_AHEAD = 4;  // 8 measured no better (same-weights A
 // Positions / Depth: its position / camera depth, Normals: the normalised negative density
 // gradient; Cost counts the ray's composited samples in c.x (shade_kernel_nerf turns it into a
 // grey level, :1327-1330) as payload.n_steps = j + current_step does (:664-667).
-template <bool MODES>
+template <bool MODES, uint32_t AHEAD = COMPOSITE_AHEAD>
 __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                    const float* __restrict__ sdepth, const float4* __restrict__ posdt,
@@ -705,11 +708,11 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		// only each sample's dt is read in the loop (4 B instead of the 16-B row); the position of
 		// the max-weight sample -- the depth -- is read once after it
 		size_t s_max = ~(size_t)0;
-		for (uint32_t j0 = 0; j0 < actual && !done; j0 += COMPOSITE_AHEAD) {
-			uint2 o2[COMPOSITE_AHEAD];
-			float wdt[COMPOSITE_AHEAD];
+		for (uint32_t j0 = 0; j0 < actual && !done; j0 += AHEAD) {
+			uint2 o2[AHEAD];
+			float wdt[AHEAD];
 #pragma unroll
-			for (uint32_t u = 0; u < COMPOSITE_AHEAD; ++u) {
+			for (uint32_t u = 0; u < AHEAD; ++u) {
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
@@ -717,7 +720,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				}
 			}
 #pragma unroll
-			for (uint32_t u = 0; u < COMPOSITE_AHEAD; ++u) {
+			for (uint32_t u = 0; u < AHEAD; ++u) {
 				if (done || j0 + u >= actual) continue;
 				const __half2 rg = *reinterpret_cast<const __half2*>(&o2[u].x), bs = *reinterpret_cast<const __half2*>(&o2[u].y);
 				const float T = 1.0f - c.w;
@@ -1324,7 +1327,15 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			pr.k.normals = sc.nrm.ptr;
 		}
 		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
-		if (pr.k.mode == NGP_RENDER_MODE_SHADE)
+		// ngp_tuning.render_tail_rays (opt-in): passes with at most this many alive rays (and a cap of >= 16 samples
+		// per ray) composite with every sample of the pass prefetched; 0: never (2^16 measured 13.62 vs 13.56 ms
+		// per frame, 2^18 13.68: the tail's composites are not what its passes wait on)
+		const uint32_t tail_rays = tu.render_tail_rays;
+		if (pr.k.mode == NGP_RENDER_MODE_SHADE && pr.n_alive_ub <= tail_rays && cap_p >= 16)
+			k_composite<false, COMPOSITE_AHEAD_TAIL><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
+			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
+			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);
+		else if (pr.k.mode == NGP_RENDER_MODE_SHADE)
 			k_composite<false><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
 			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
 			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);

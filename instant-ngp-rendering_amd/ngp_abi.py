@@ -122,6 +122,7 @@ class Tuning(C.Structure):
         ("mlp_train_schedule", C.c_uint32),
         ("render_slot_compaction", C.c_uint32),
         ("render_skip_unfilled", C.c_uint32),
+        ("render_tail_rays", C.c_uint32),
     ]
 
 

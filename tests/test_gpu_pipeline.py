@@ -498,7 +498,9 @@ def test_render_config_e_full_network_matches_oracle():
                    dict(render_slot_compaction=0, render_pipelines=0),
                    # the render MLP computing every reserved slot instead of skipping tiles no ray filled
                    dict(render_skip_unfilled=2), dict(render_skip_unfilled=1, render_mlp_tile=1),
-                   dict(render_skip_unfilled=0, render_mlp_tile=0)):
+                   dict(render_skip_unfilled=0, render_mlp_tile=0),
+                   # the tail passes' composites with all of a ray's samples prefetched (default: 4 deep)
+                   dict(render_tail_rays=65536), dict(render_tail_rays=0)):
             g.set_tuning(**kw)
             frame.zero_()
             A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))

@@ -165,10 +165,11 @@ def test_render_1080p_rows_match_oracle(scene, config):
     # the whole 1080p frame is the same with the passes' sample slots compacted or reserved up front
     # (every lane-per-ray width of k_generate runs in a 1080p march: 1, 4, 16 and 64)
     # and with the render MLP computing every reserved slot (default: tiles of unfilled slots skipped)
-    for kw in ({"render_slot_compaction": 1}, {"render_slot_compaction": 2}, {"render_slot_compaction": 0, "render_skip_unfilled": 2}):
+    for kw in ({"render_slot_compaction": 1}, {"render_slot_compaction": 2}, {"render_slot_compaction": 0, "render_skip_unfilled": 2},
+               {"render_skip_unfilled": 0, "render_tail_rays": 65536}, {"render_tail_rays": 4194304}):
         tb.set_tuning(kw)
         np.testing.assert_array_equal(tb.render(W, H, 1, True), img, err_msg=str(kw))
-    tb.set_tuning({"render_skip_unfilled": 0})
+    tb.set_tuning({"render_tail_rays": 0})
 
 
 def test_network_config_parent_merge(tmp_path):
