@@ -37,6 +37,10 @@ def parse():
     p.add_argument("--steps", type=int, default=20)
     p.add_argument("--warmup", type=int, default=5)
     p.add_argument("--pretrain", type=int, default=1500, help="untimed training steps before warmup (grid converges)")
+    p.add_argument("--deterministic-pretrain", type=int, default=1,
+                   help="pretrain with bit-reproducible hash-grid gradients (Testbed.deterministic), so every run times "
+                        "the same trained scene (its samples per 1080p frame otherwise vary by +-10 %% run to run); "
+                        "the timed steps use the default fp16-atomic path")
     p.add_argument("--config", default="lego_L16F2.json")
     p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"),
                    help="transforms.json of the scene to train on, or 'synthetic' for the procedural lego-shaped one")
@@ -216,8 +220,10 @@ def surface_scene(args, ngp):
     cams, _, _ = make_dataset(ngp, tb, sub_args, "cuda:0")
     tb.reload_network_from_file(args.config)
     tb.shall_train = True
+    tb.deterministic = bool(args.deterministic_pretrain)
     for _ in range(args.pretrain):
         tb.train(args.batch)
+    tb.deterministic = False
     W, H = args.width, args.height
     view = 3 % len(cams)
 
@@ -303,12 +309,14 @@ def main():
             dist.barrier()
 
     t_pre = time.perf_counter()
+    tb.deterministic = bool(args.deterministic_pretrain)
     for i in range(args.pretrain):
         tb.train(args.batch)
         if rank == 0 and (i + 1) % 250 == 0:
             print(f"# pretrain {i + 1}/{args.pretrain} loss {tb.loss:.5f} "
                   f"rays/batch {tb.last_train_stats()['rays_per_batch']} ({time.perf_counter() - t_pre:.1f}s)",
                   file=sys.stderr, flush=True)
+    tb.deterministic = False  # the timed steps run the default path
     view = (rank * 7 + 3) % n_views
 
     split = {"train_s": 0.0, "render_s": 0.0, "train_rays": 0, "render_rays": 0}
@@ -490,7 +498,9 @@ def main():
                      f"RGBA8; the reference's data/nerf/test/dataset, nerf_synthetic/lego is not available offline)"
                      if args.scene != "synthetic" else
                      f"synthetic lego-shaped scene ({n_views} views {args.train_res}x{args.train_res} RGBA8)")
-                    + f", random-init weights trained {args.pretrain} steps before timing",
+                    + f", random-init weights trained {args.pretrain} steps before timing"
+                    + (" (bit-reproducible hash-grid gradients: the same trained scene every run; timed steps on the "
+                       "default fp16-atomic path)" if args.deterministic_pretrain else ""),
             "config": {"workload": "lego L16F2T19 MLP 64 (1x density + 2x rgb hidden): Testbed.train(2^18) "
                                    f"+ {W}x{H} spp1 render per step", "batch": args.batch, "config_file": args.config,
                        "parallelism": f"dp{world} (RCCL grad all-reduce) + per-rank 1080p view"},

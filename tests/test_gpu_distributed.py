@@ -318,3 +318,29 @@ def test_deterministic_steps_are_bit_reproducible(scene):
     agree = np.sign(first[0][both]) == np.sign(first[2][both])
     assert agree.mean() > 0.99, agree.mean()
     assert losses[2] == pytest.approx(losses[0], rel=0.1)
+
+
+def test_deterministic_mode_switches_off_between_steps(scene):
+    """bench.py pretrains with the deterministic hash-grid gradients and times the default path: a
+    Testbed switched from one mode to the other between steps keeps training (the fixed-point and the
+    fp16 gradient buffers are each zeroed by the optimizer step that consumes them), and the switched
+    run's first deterministic steps are the deterministic run's."""
+    torch.cuda.set_device(0)
+    out = []
+    for switch in (False, True):
+        tb = _testbed(scene)
+        tb.deterministic = True
+        tb.shall_train = True
+        while tb.training_step < 40:
+            tb.frame()
+        at40 = _params(tb)
+        if switch:
+            tb.deterministic = False
+        while tb.training_step < 80:
+            tb.frame()
+        out.append((at40, _params(tb), tb.loss))
+        del tb
+    np.testing.assert_array_equal(out[0][0], out[1][0])
+    assert np.isfinite(out[1][1]).all() and np.isfinite(out[1][2])
+    assert out[1][2] == pytest.approx(out[0][2], rel=0.25)
+
