@@ -1,5 +1,3 @@
 set -o pipefail
 mkdir -p gpurun_out
-timeout -k 10 1000 bash tools/profile_round.sh r03j > gpurun_out/profile_round.log 2>&1 && \
-timeout -k 10 600 bash tools/pmc_mfma.sh r03j > gpurun_out/pmc_mfma.log 2>&1 && \
-timeout -k 10 300 python -u bench.py > gpurun_out/bench.log 2>&1
+timeout -k 10 900 python -u tools/render_ab.py --rounds 4 --frames 5 "" "render_pass_samples=5242880" "render_pass_samples=6291456" "render_pass_samples=8388608" "render_pass_samples=6291456 render_lanes=6291456" > gpurun_out/render_ab.log 2>&1
