@@ -904,7 +904,7 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 
 // The march schedule (ngp_tuning; results do not depend on it):
 //  * lanes_target: the lane budget that picks lanes-per-ray in k_generate (4M);
-//  * pass_sample_target: a pipeline's sample slots per pass (4M; <= 16M: the MLP reads the
+//  * pass_sample_target: a pipeline's sample slots per pass (5M; <= 16M: the MLP reads the
 //    encodings through raw buffers with 32-bit byte offsets, 64 B/sample);
 //  * first_pass_steps / max_steps_per_pass: the per-ray cap of the first pass doubles every pass
 //    up to the maximum (4 -> 32).  A ray's slots past its termination are wasted encoder and MLP
@@ -914,7 +914,8 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 //    transmittance and the opacity of its last sample (sample_budget).
 static uint32_t lanes_target(const ngp_tuning& t) { return t.render_lanes ? t.render_lanes : 4u << 20; }
 static uint32_t pass_sample_target(const ngp_tuning& t) {
-	return std::min<uint32_t>(t.render_pass_samples ? t.render_pass_samples : 4u << 20, 16u << 20);
+	// 5 M: 13.78 vs 13.96 ms per frame against 4 M (6 M 13.82, 8 M 13.99; same weights, profiles/r03_pass_size_ab.txt)
+	return std::min<uint32_t>(t.render_pass_samples ? t.render_pass_samples : 5u << 20, 16u << 20);
 }
 static uint32_t first_pass_steps(const ngp_tuning& t) { return t.render_first_steps ? t.render_first_steps : 4u; }
 static uint32_t max_steps_per_pass(const ngp_tuning& t) { return t.render_max_steps ? t.render_max_steps : 32u; }

@@ -5,7 +5,7 @@ each setting in turn, round-robin, so box-to-box and run-to-run spread cancel ou
 a space-separated list of ngp_tuning fields (include/ngp_hip.h; Testbed.set_tuning), applied
 before its frames.
 
-Usage: python tools/render_ab.py [--rounds 4] [--frames 5] "" "render_pipelines=1" "render_pass_samples=8388608" ...
+Usage: python tools/render_ab.py [--rounds 4] [--frames 5] [--scene synthetic] "" "render_pipelines=1" "render_pass_samples=8388608" ...
 """
 import argparse
 import os
@@ -35,7 +35,14 @@ def main():
     print(f"# pyngp from {ngp.__file__}", file=sys.stderr)
 
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
-    tb.load_training_data(a.scene)
+    if a.scene == "synthetic":
+        # bench.py's procedural lego-shaped surface scene (100 views 800x800)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import bench
+        bench.make_dataset(ngp, tb, argparse.Namespace(scene="synthetic", views=100, train_res=800), "cuda:0")
+    else:
+        tb.load_training_data(a.scene)
     tb.reload_network_from_file(a.config)
     if a.snapshot and os.path.exists(a.snapshot):
         tb.load_snapshot(a.snapshot)  # the same weights and grid as the run that wrote it
