@@ -34,6 +34,10 @@ def main():
 
     print(f"# pyngp from {ngp.__file__}", file=sys.stderr)
 
+    if a.scene == "synthetic":
+        import torch  # the scene's views are rendered with torch: its HIP runtime starts before the Testbed's
+
+        torch.cuda.set_device(0)
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
     if a.scene == "synthetic":
         # bench.py's procedural lego-shaped surface scene (100 views 800x800)
