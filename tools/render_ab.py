@@ -30,14 +30,14 @@ def main():
     a = p.parse_args()
     if a.pkg:
         sys.path.insert(0, os.path.abspath(a.pkg))
+    if a.scene == "synthetic":
+        import torch  # renders the scene's views: its HIP runtime has to start before pyngp's library loads
+
+        torch.cuda.set_device(0)
     import pyngp as ngp
 
     print(f"# pyngp from {ngp.__file__}", file=sys.stderr)
 
-    if a.scene == "synthetic":
-        import torch  # the scene's views are rendered with torch: its HIP runtime starts before the Testbed's
-
-        torch.cuda.set_device(0)
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
     if a.scene == "synthetic":
         # bench.py's procedural lego-shaped surface scene (100 views 800x800)
