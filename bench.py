@@ -26,6 +26,7 @@ import numpy as np
 ROOT = os.path.dirname(os.path.abspath(__file__))
 PKG = os.path.join(ROOT, "instant-ngp-rendering_amd")
 sys.path.insert(0, PKG)
+TESTS = os.path.join(ROOT, "tests")
 
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E (MI355X_MICROARCH.md)
 MFMA_F16_PEAK_TFLOPS = 2500.0  # dense fp16/bf16 MFMA, no sparsity (MI355X_MICROARCH.md)
@@ -112,6 +113,7 @@ def make_dataset(ngp, tb, args, device):
         cams = [np.asarray(x, np.float32) for x in ds.transforms]
         imgs = np.stack([ds.image(i) for i in range(ds.n_images)])
         return cams, imgs, float(ds.metadata[0].focal_length[0])
+    sys.path.insert(0, TESTS)  # the procedural scene generator is a test fixture
     import synthetic
 
     cams = synthetic.hemisphere_cameras(args.views, seed=0)

@@ -240,6 +240,10 @@ typedef struct ngp_train_stats {
 	 * chunk stop and the loss stop disagree); must be 0 -- the Testbed switches to the full
 	 * forward for the rest of the run if it is not */
 	uint32_t forward_early_stop_violations;
+	/* data parallelism: 1 if some rank's share of the step's samples did not fit its buffers (sized about
+	 * 2 / world_size of max_samples); the step made no update or deposits -- discard it (ngp_train_discard)
+	 * and run it again: the rank's buffers grow to the need */
+	uint32_t sample_capacity_overflow;
 } ngp_train_stats;
 
 typedef struct ngp_grid_args {
@@ -327,53 +331,32 @@ typedef struct ngp_tuning {
 	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 */
 	uint32_t render_lag;             /* passes a pipeline runs ahead of its counter read-backs, 2..4; 0: 3 */
 	float render_budget_scale;       /* headroom of the per-ray transmittance budget; 0: 1.0; < 0: no budget */
-	uint32_t render_block_skipping;  /* 1: aligned-block occupancy summaries instead of octant distance fields */
 	uint32_t render_composite_block; /* k_composite workgroup size (256, 512, 1024); 0: 512 */
 	uint32_t render_generate_block;  /* k_generate workgroup size (256, 512); 0: 512 */
 	uint32_t encode_dense_records;   /* render-site corner records of the dense levels: 0 on, 1 off */
 	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: 8 */
-	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics */
-	uint32_t encode_levels_per_thread; /* F = 2, L = 16 hash encoder: 2 = level pairs (g, 15 - g), pair g on XCD g
-	                                      (each XCD's L2 holds two levels' tables); 0 or 4: four strided levels */
-	uint32_t encode_streaming;       /* hash encoder cache hints: bit 0 non-temporal encoding stores (F = 2 planes),
-	                                    bit 1 non-temporal position loads, bit 2 sc1 encoding stores
-	                                    (the line leaves the L2); 0: the default (bit 0); 128: none */
-	uint32_t render_network;         /* 1: the renderer's fused hash encoding + MLP kernel (F = 2, L = 16); 2: separate
-	                                    encoder and MLP launches; 0: the default */
-	uint32_t render_net_workgroups_per_cu; /* fused render kernel workgroups per CU; 0: 4 */
-	uint32_t train_chain_walk;       /* 1: the training sampler walks the reference's voxel-jump chain also at
-	                                    aabb_scale 1 (0: the octant distance fields there; same samples) */
+	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics;
+	                                    bit 2: the chunked training forward stops rays at transmittance 0.999 (forces
+	                                    forward_early_stop_violations: exercises the discard-and-retry path);
+	                                    bit 3: data-parallel sample buffers start at an eighth of a rank's even share
+	                                    (forces sample_capacity_overflow and the retry with grown buffers) */
+	uint32_t encode_streaming;       /* hash encoder (F = 2 planes): 0 = non-temporal encoding stores (the default), 1 = plain */
 	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
 	                                    by cell, coherent gathers; same grid) */
-	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16 (2-deep prefetch ring), 2 = 32,
-	                                    3 = 32 with a 2-deep ring, 4 = 64; 0: 4 */
-	uint32_t encode_xcd_regions;     /* four-levels-per-thread hash encoder: 1 = each XCD encodes one contiguous eighth
-	                                    of the samples (level groups one after another), 2 = the same with the four
-	                                    level groups of a chunk back to back, 3 = off (XCD x takes every eighth
-	                                    chunk); 0: the default (1) */
-	uint32_t render_pass_order;      /* ray pipelines' network launches: 1 = free-running streams, 2 = the hash-encoder
-	                                    launches of all pipelines chained in enqueue order (one encoder on the GPU at a
-	                                    time; the other pipelines' MLP and march kernels run beside it), 3 = the same
-	                                    chain over encoder + MLP; 0: the default */
-	uint32_t render_encode_wgs_per_cu; /* render hash-encoder workgroups per CU (a persistent grid striding over the
-	                                      pass's chunks, leaving CU room for the other pipelines' kernels); 0: one
-	                                      workgroup per chunk and level group */
-	uint32_t mlp_train_schedule;     /* training MLP (k_mlp_train*): 1 = 8 waves x 16 samples, wave-shared weight
-	                                    gradients with a workgroup barrier per layer; 2 = 4 waves, each owning
-	                                    32-sample steps end to end (forward, dgrad and every weight gradient), no
-	                                    barrier in the loop; 0: the default */
-	uint32_t render_slot_compaction; /* march passes: 1 = each ray stages its samples and then takes exactly the
-	                                    rows it filled (packed pass rows); 2 = rays reserve their whole budget up
-	                                    front, unfilled slots marked and skipped; 0: the default (2) */
+	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16, 4 = 64; 0: 4 */
+	uint32_t encode_xcd_regions;     /* four-levels-per-thread hash encoder: 0 = each XCD encodes one contiguous eighth of
+	                                    the samples (the default), 1 = XCD x takes every eighth chunk */
 	uint32_t render_skip_unfilled;   /* 1 = the render MLP skips 16-sample column tiles of slots no ray filled (marked
-	                                    by k_generate), 2 = computes every reserved slot; 0: the default */
-	uint32_t render_tail_rays;       /* march passes with at most this many alive rays composite with all of a ray's
-	                                    samples of the pass loaded at once; 0: never (the default) */
+	                                    by k_generate), 2 = computes every reserved slot; 0: the default (1) */
+	uint32_t render_exit_cap;        /* 1 = a ray reserves at most the lattice points left to its AABB exit in a march
+	                                    pass, 2 = the per-ray cap alone; 0: the default */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */
 ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint64_t seed, ngp_model** out);
 ngp_status ngp_model_set_tuning(ngp_model* model, const ngp_tuning* tuning);
+/* The checks ngp_model_set_tuning applies, without a model (NGP_ERR_INVALID + ngp_last_error on a bad value). */
+ngp_status ngp_tuning_validate(const ngp_tuning* tuning);
 ngp_status ngp_model_get_tuning(const ngp_model* model, ngp_tuning* tuning);
 ngp_status ngp_model_destroy(ngp_model* model);
 ngp_status ngp_model_get_info(const ngp_model* model, ngp_model_info* info);

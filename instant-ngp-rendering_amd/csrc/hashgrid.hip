@@ -71,16 +71,8 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 		// contiguous chunk range [x R, x R + R) of the device count -- its L2 sees the cells of one
 		// eighth of the rays instead of every eighth chunk of all of them
 		const uint32_t b = blockIdx.x, K = n_chunks >> 3, R = (c_end + 7u) >> 3;
-		uint32_t x, k;
-		if (lt.regions == 1) {
-			grp = b / n_chunks;
-			x = (b % n_chunks) & 7u;
-			k = (b % n_chunks) >> 3;
-		} else {
-			x = b & 7u;
-			grp = (b >> 3) % groups;
-			k = (b >> 3) / groups;
-		}
+		grp = b / n_chunks;
+		const uint32_t x = (b % n_chunks) & 7u, k = (b % n_chunks) >> 3;
 		c_begin = x * R + k;
 		c_end = min(c_end, x * R + R);
 		c_step = K;
@@ -89,27 +81,13 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 		c_begin = chunk0;
 	}
 	using VT = typename FeatVec<F>::T;
-	// LPT = 2: the level pair (g, L - 1 - g) -- a coarse and a fine level, so with L = 16 the eight
-	// pairs cost about the same and each XCD (map_block: XCD x runs pair x) keeps two levels' tables
-	// in its L2; else levels g, g + L/LPT, ...
-	auto level_of = [&](uint32_t q) { return LPT == 2 ? (q == 0 ? grp : lt.n_levels - 1u - grp) : grp + q * groups; };
+	// levels g, g + L/LPT, ... of the sample
+	auto level_of = [&](uint32_t q) { return grp + q * groups; };
 	for (uint32_t chunk = c_begin; chunk < c_end; chunk += c_step) {
 		const uint32_t i = chunk * 256u + threadIdx.x;
 		if (i >= n) continue;
-		float px, py, pz;
-		if ((lt.streaming & 2u) && stride == 4) {
-			// 16-B position rows, read once: non-temporal, so they do not evict table lines from the L2
-			typedef float f32x4 __attribute__((ext_vector_type(4)));
-			const f32x4 r = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(pos) + i);
-			px = r.x;
-			py = r.y;
-			pz = r.z;
-		} else {
-			px = pos[(size_t)i * stride + 0];
-			py = pos[(size_t)i * stride + 1];
-			pz = pos[(size_t)i * stride + 2];
-		}
-		VT o[LPT];
+		const float px = pos[(size_t)i * stride + 0], py = pos[(size_t)i * stride + 1], pz = pos[(size_t)i * stride + 2];
+	VT o[LPT];
 		if (SITE == 1 && px < 0.0f) {
 #pragma unroll
 			for (uint32_t q = 0; q < LPT; ++q) o[q] = VT{};
@@ -128,16 +106,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
 #pragma unroll
 				for (uint32_t q = 0; q < 4; ++q) pv.v[q] = o[q];
 				if constexpr (F == 2) {
-					if (lt.streaming & 4u) {
-						// sc1 store: the line leaves the XCD's L2 (MI355X_MICROARCH.md: plain / nt stores keep it)
-						typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-						const u32x4 w = {pv.v[0], pv.v[1], pv.v[2], pv.v[3]};
-						const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc(
-						    reinterpret_cast<uint4*>(enc) + (size_t)grp * lay.plane, (short)0, 0x7FFFFFFF, 0x00020000);
-						__builtin_amdgcn_raw_buffer_store_b128(w, rs, (int)(16u * i), 0, 16);
-						continue;
-					}
-					if (lt.streaming & 1u) {
+					if (lt.streaming) {
 						// the encodings are written once and read once by the MLP: non-temporal stores
 						typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 						const u32x4 w = {pv.v[0], pv.v[1], pv.v[2], pv.v[3]};
@@ -430,10 +399,7 @@ static void launch_fwd_site(const LevelTable& lt, const float* pos, uint32_t str
 	// F = 2: 16-B quad gathers, four levels per thread (l, l + L/4, ...) where L % 4 == 0, else one
 	// (8-B pair gathers and two levels per thread measured slower)
 	if (lt.F == 2) {
-		if (lt.pairs && lt.n_levels == 16)
-			launch_timed(k_hashgrid_fwd<2, SITE, true, 2>, n_chunks * 8, 256, 0, s, n, pos, stride, table, lt, enc, enc_plane,
-			             n_chunks, n_dev);
-		else if (lt.n_levels % 4 == 0) {
+		if (lt.n_levels % 4 == 0) {
 			if (lt.regions) n_chunks = div_up(n_chunks, 8u) * 8u;  // K = n_chunks / 8 workgroups per XCD and group
 			launch_timed(k_hashgrid_fwd<2, SITE, true, 4>, n_chunks * lt.n_levels / 4, 256, 0, s, n, pos, stride, table, lt, enc,
 			             enc_plane, n_chunks, n_dev);

@@ -8,19 +8,17 @@
 //  * v_mfma_f32_16x16x32_f16: A = weights (16 output rows x 32 inputs), B =
 //    activations (32 inputs x 16 samples), C = 16 rows x 16 samples, fp32
 //    accumulation (tcnn accumulates in fp16 WMMA fragments).
-//  * one workgroup = 4 waves; each wave owns 32 samples (two 16-sample column
-//    tiles) and keeps their activations in a private LDS image [sample][row]
-//    (fp16, row stride padded by 16 B so the B-operand ds_read_b128 is
-//    conflict-free).  Layers chain through LDS; no activation touches HBM.
-//  * weights are packed once per optimizer step into per-lane MFMA fragments
-//    (k_pack below) and copied into LDS at kernel start: one ds_read_b128 per
-//    fragment, reused for both column tiles.
-//  * training (fwd + dgrad + wgrad in one persistent launch): weight gradients
-//    are sum_s delta[s][m] * a[s][k]; both operands are read sample-major from
-//    the four waves' LDS images with ds_read_b64_tr_b16 (hardware transpose), so
-//    one 16x16 gradient tile consumes K = 128 samples per pass, accumulates in
-//    registers across the whole persistent loop and is flushed with one fp32
-//    atomic per element per workgroup.
+//  * inference (k_mlp_infer_rf: render, training forward, density grid) is
+//    register-resident: a layer's C tiles are the next layer's B operands once
+//    k_pack has permuted its K order, so activations never leave the VGPRs;
+//    weight fragments live in LDS (one copy per workgroup).
+//  * training (k_mlp_train: fwd + dgrad + wgrad in one persistent launch, 8
+//    waves x 16 samples per 128-sample chunk): activations and deltas live in
+//    LDS images [sample][row] (row stride padded by 16 B: conflict-free
+//    ds_read_b128); weight gradients are sum_s delta[s][m] * a[s][k] with both
+//    operands read sample-major through ds_read_b64_tr_b16 (hardware
+//    transpose), accumulated in registers over the loop and written once per
+//    workgroup as a row of partials that k_mlp_reduce sums in a fixed order.
 #include <algorithm>
 
 #include <cstring>
@@ -120,8 +118,6 @@ struct Net {
 	static constexpr int tslots() { return (gtile_base(NL) + TWAVES - 1) / TWAVES; }
 	static constexpr int drows() { return Wp > 32 ? Wp : 32; }
 	static constexpr int dstride() { return 2 * drows() + 8; }
-	static constexpr size_t lds_infer() { return (size_t)fwd_frags() * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<false>() * 2; }
-	static constexpr size_t lds_density() { return (size_t)fwd_frags_upto(DH + 1) * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<false>() * 2; }
 	static constexpr size_t lds_train() {
 		return (size_t)(fwd_frags() + bwd_frags()) * FRAG_HALVES * 2 + (size_t)WAVES * SPW * stride<true>() * 2 +
 		       (size_t)WAVES * SPW * dstride() * 2;
@@ -222,8 +218,8 @@ __device__ __forceinline__ void load_sh(const MlpArgs& a, _Float16* img, int x_s
 		const uint32_t i = base + smp;
 		h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
 		if (i < a.n) {
-			const float* c = a.coords + (size_t)i * a.coord_stride;
-			const float x = c[4] * 2.0f - 1.0f, y = c[5] * 2.0f - 1.0f, z = c[6] * 2.0f - 1.0f;
+			const float* c = a.coords ? a.coords + (size_t)i * a.coord_stride : nullptr;
+			const float x = c ? c[4] * 2.0f - 1.0f : 0.0f, y = c ? c[5] * 2.0f - 1.0f : 0.0f, z = c ? c[6] * 2.0f - 1.0f : 0.0f;
 			const float xy = x * y, xz = x * z, yz = y * z, x2 = x * x, y2 = y * y, z2 = z * z;
 			if (half == 0) {
 				v[0] = (_Float16)(0.28209479177387814f);
@@ -292,70 +288,6 @@ __device__ __forceinline__ void fwd_range(const _Float16* frags, _Float16* img, 
 	if constexpr (l < END) {
 		fwd_layer<N, TRAIN, l, CT_>(frags, img, lane, res);
 		fwd_range<N, TRAIN, l + 1, END, CT_>(frags, img, lane, res);
-	}
-}
-
-template <class N>
-__global__ void __launch_bounds__(BLOCK) k_mlp_infer(MlpArgs a) {
-	if (a.n_dev) a.n = min(a.n, *a.n_dev);
-	extern __shared__ __attribute__((aligned(16))) char smem[];
-	constexpr int STRIDE = N::template stride<false>();
-	constexpr int FH = N::fwd_frags() * FRAG_HALVES;
-	_Float16* frags = reinterpret_cast<_Float16*>(smem);
-	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	_Float16* img = frags + FH + wave * SPW * STRIDE;
-
-	for (int t = threadIdx.x; t < FH / 8; t += BLOCK)
-		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
-	for (int t = lane; t < SPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
-	__syncthreads();
-
-	const int g = lane >> 4, n = lane & 15;
-	const uint32_t n_chunks = n_chunks_of(a.n);
-	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
-		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
-		load_encoding<N, STRIDE>(a, img, base, lane);
-		load_sh<STRIDE>(a, img, N::template x_seg<false>(), base, lane);
-		f4 res[CT];
-		fwd_range<N, false, 0, N::NL>(frags, img, lane, res);
-		if (g == 0) {
-#pragma unroll
-			for (int c = 0; c < CT; ++c) {
-				const uint32_t i = base + 16 * c + n;
-				if (i < a.n) {
-					const _Float16 dens = img[(16 * c + n) * STRIDE + N::template x_seg<false>()];
-					h4 o = {(_Float16)res[c][0], (_Float16)res[c][1], (_Float16)res[c][2], dens};
-					*reinterpret_cast<h4*>(a.out + (size_t)i * 4) = o;
-				}
-			}
-		}
-	}
-}
-
-// Density only: enc -> density MLP -> row 0 (NerfNetwork::density, nerf_network.h:270-279).
-template <class N>
-__global__ void __launch_bounds__(BLOCK) k_mlp_density(MlpArgs a) {
-	if (a.n_dev) a.n = min(a.n, *a.n_dev);
-	extern __shared__ __attribute__((aligned(16))) char smem[];
-	constexpr int STRIDE = N::template stride<false>();
-	constexpr int FH = N::fwd_off(N::DH + 1);
-	_Float16* frags = reinterpret_cast<_Float16*>(smem);
-	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	_Float16* img = frags + FH + wave * SPW * STRIDE;
-	for (int t = threadIdx.x; t < FH / 8; t += BLOCK)
-		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
-	for (int t = lane; t < SPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
-	__syncthreads();
-	const uint32_t n_chunks = n_chunks_of(a.n);
-	for (uint32_t chunk = blockIdx.x; chunk < n_chunks; chunk += gridDim.x) {
-		const uint32_t base = chunk * SAMPLES_PER_BLOCK + wave * SPW;
-		load_encoding<N, STRIDE>(a, img, base, lane);
-		f4 res[CT];
-		fwd_range<N, false, 0, N::DH + 1>(frags, img, lane, res);
-		if (lane < SPW) {
-			const uint32_t i = base + lane;
-			if (i < a.n) a.out[i] = __builtin_bit_cast(__half, img[lane * STRIDE + N::template x_seg<false>()]);
-		}
 	}
 }
 
@@ -677,80 +609,6 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 }
 
 // ---------------------------------------------------------------------------
-// Fused render network (renderer, F = 2, L = 16): the hash encoding and the register-resident MLP
-// in one persistent kernel.  The separate encoder writes 64 B of features per sample that the MLP
-// reads back (12 GB per 1080p frame of the bench scene, streaming through the L2s that hold the
-// hash table); here they stay on chip.  A workgroup of RN_WAVES waves takes 16 * RN_WAVES samples
-// per round: wave w computes plane w % 4 (levels p, p + 4, p + 8, p + 12 -- the encoder's own
-// encode_one, so the features are bit-identical) of 64 samples, one sample per lane, into LDS;
-// after a barrier wave w runs the 16-sample tile w through the MLP (rf_tile), lane (g, n) taking
-// plane g of sample n as its B operand -- exactly the plane layout the first layer's K order was
-// packed for.  Other workgroups' MFMAs overlap a workgroup's gathers on the same CU.
-// ---------------------------------------------------------------------------
-struct EncIn {
-	const float4* pos;    // [n] warped position + dt (x < 0: a reserved slot the ray did not fill)
-	const __half* table;  // the encoding's fp16 parameters
-	LevelTable lt;        // F = 2, L = 16 (dense-level corner records when built)
-};
-
-constexpr int RN_WAVES = 8;
-constexpr int RN_BLOCK = RN_WAVES * 64;
-constexpr int RN_SAMPLES = 16 * RN_WAVES;
-
-template <class N>
-__global__ void __launch_bounds__(RN_BLOCK) k_render_net(MlpArgs a, EncIn e) {
-	static_assert(N::KE == 1 && N::Wp <= 64, "one 32-row K step of encoding inputs (L * F = 32)");
-	if (a.n_dev) a.n = min(a.n, *a.n_dev);
-	constexpr int NF = N::fwd_frags();
-	extern __shared__ __attribute__((aligned(16))) char smem[];
-	h8* w = reinterpret_cast<h8*>(smem);                                        // [frag][lane]
-	uint4* planes = reinterpret_cast<uint4*>(smem + (size_t)NF * 64 * sizeof(h8));  // [2][RN_SAMPLES][4]
-	{
-		const h8* src = reinterpret_cast<const h8*>(a.frags + N::rfwd_off(0));
-		for (int t = threadIdx.x; t < NF * 64; t += RN_BLOCK) w[t] = src[t];
-	}
-	__syncthreads();
-	const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-	const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
-	const uint32_t plane = wave & 3u, half = wave >> 2;  // encode: plane of samples [64 half, 64 half + 64)
-	const h8* wl = w + lane;
-	const uint32_t rounds = (a.n + RN_SAMPLES - 1) / RN_SAMPLES;
-	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.sh_ray, a.coord_bytes);
-	const __amdgpu_buffer_rsrc_t sh_rs = make_rsrc(a.sh, a.sh_bytes);
-	uint32_t buf = 0;
-	for (uint32_t r = blockIdx.x; r < rounds; r += gridDim.x, buf ^= 1u) {
-		const uint32_t base = r * RN_SAMPLES;
-		RawTile<N, 1> cur;
-		// this wave's MLP tile: samples base + 16 wave + n; the SH row indices first
-		cur.ri[0] = __builtin_amdgcn_raw_buffer_load_b32(crd_rs, 4 * (base + 16 * wave + n), 0, 0);
-		{
-			const uint32_t i = base + 64 * half + lane;
-			uint4 v = make_uint4(0u, 0u, 0u, 0u);
-			if (i < a.n) {
-				const float4 p = e.pos[i];
-				if (p.x >= 0.0f) {
-					v.x = encode_one<2, true>(plane, p.x, p.y, p.z, e.table, e.lt);
-					v.y = encode_one<2, true>(plane + 4u, p.x, p.y, p.z, e.table, e.lt);
-					v.z = encode_one<2, true>(plane + 8u, p.x, p.y, p.z, e.table, e.lt);
-					v.w = encode_one<2, true>(plane + 12u, p.x, p.y, p.z, e.table, e.lt);
-				}
-			}
-			planes[((size_t)buf * RN_SAMPLES + 64 * half + lane) * 4 + plane] = v;
-		}
-		sh_load<N, 1>(sh_rs, g, cur);
-		// every plane of the round is in LDS (the other buffer is the next round's: a wave still in
-		// this round's MLP never races the next round's writes, which follow the next barrier)
-		__syncthreads();
-		const uint4 pv = planes[((size_t)buf * RN_SAMPLES + 16 * wave + n) * 4 + g];
-		cur.e[0][0] = pv.x;
-		cur.e[0][1] = pv.y;
-		cur.e[0][2] = pv.z;
-		cur.e[0][3] = pv.w;
-		rf_tile<N, 1, 1, false, true>(a, wl, cur, base + 16 * wave, g, n);
-	}
-}
-
-// ---------------------------------------------------------------------------
 // Training: forward (activations kept), dgrad chain, wgrad via transposed reads.
 // ---------------------------------------------------------------------------
 template <class N, int l>
@@ -878,7 +736,7 @@ __device__ __forceinline__ void bwd_range(const MlpArgs& a, const _Float16* frag
 		constexpr int STRIDE = N::template stride<true>();
 		constexpr int DS = N::dstride();
 		__syncthreads();  // every wave's delta for layer l is in LDS
-		wgrad_layer<N, l>(imgs, dimgs, wave, lane, acc, a.enc_pad);
+		if (a.grads) wgrad_layer<N, l>(imgs, dimgs, wave, lane, acc, a.enc_pad);
 		dgrad_layer<N, l>(a, frags, imgs + wave * TSPW * STRIDE, dimgs + wave * TSPW * DS, lane, base);
 		bwd_range<N, l - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
 	}
@@ -953,7 +811,7 @@ __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int
 		for (int q = 0; q < 4; ++q) p.e[it][q] = ok ? e[lay.vec(k0 / 2 + q, i)] : 0u;
 	}
 	const uint32_t i = base + (lane % SPW_);
-	const bool in = i < a.n;
+	const bool in = i < a.n && a.coords;  // no coordinates (input gradients only): the zero direction
 	const float* c = a.coords + (size_t)(in ? i : 0) * a.coord_stride;
 #pragma unroll
 	for (int k = 0; k < 3; ++k) p.d[k] = in ? c[4 + k] : 0.5f;
@@ -1068,171 +926,7 @@ __global__ void __launch_bounds__(TBLOCK) k_mlp_train(MlpArgs a) {
 		fwd_range<N, true, 0, N::NL - 1, TCT>(frags, img, lane, res);
 		bwd_range<N, N::NL - 1>(a, frags, imgs, dimgs, wave, lane, base, acc);
 	}
-	flush_range<N, 0>(a, wave, lane, acc);
-}
-
-// ---------------------------------------------------------------------------
-// Training, wave-independent schedule (k_mlp_train_w): 4 waves per workgroup (one per SIMD),
-// each wave owns 32-sample steps end to end -- forward, dgrad and the weight gradients of ALL
-// layers over its own 32 samples (K of one v_mfma_f32_16x16x32_f16), accumulated in its
-// registers over the persistent loop.  No workgroup barrier inside the loop, and the weight
-// gradient of an Mt x Kt layer reads Mt + Kt transposed fragments for Mt * Kt MFMAs (the 8-wave
-// schedule above reads 2 per MFMA and synchronises the workgroup before every layer).  The
-// four waves' accumulators are summed through LDS once, at the end, into the workgroup's row
-// of the partials (the same rows k_mlp_reduce sums in a fixed order).
-// ---------------------------------------------------------------------------
-constexpr int WWAVES = 4;
-constexpr int WSPW = 32;
-constexpr int WCT = WSPW / 16;
-constexpr int WBLOCK = WWAVES * 64;
-static_assert(WWAVES * WSPW == SAMPLES_PER_BLOCK, "the training images hold one chunk");
-
-template <class N, int l>
-__device__ __forceinline__ void wgrad_wave(const _Float16* img, const _Float16* dimg, int lane, f4 (&acc)[N::gtile_base(N::NL)],
-                                           uint32_t enc_pad) {
-	constexpr int STRIDE = N::template stride<true>();
-	constexpr int DS = N::dstride();
-	constexpr int DCUR = ((N::NL - 1 - l) % 2) * N::drows();
-	constexpr int SIN = N::template seg_in<true>(l);
-	constexpr int KTN = N::KT16(l), MT = N::Mt(l), TB = N::gtile_base(l);
-	const int g = lane >> 4, q = (lane & 15) >> 2, p = lane & 3;
-	// A: delta^T (16 output rows x 32 samples), B: activation^T (32 samples x 16 inputs)
-	h8 A[MT];
-#pragma unroll
-	for (int mt = 0; mt < MT; ++mt) {
-		const _Float16* ds = dimg + DCUR + 16 * mt + 4 * p;
-		const h4 a0 = tr_read(ds + (8 * g + q) * DS), a1 = tr_read(ds + (8 * g + 4 + q) * DS);
-		A[mt] = h8{a0[0], a0[1], a0[2], a0[3], a1[0], a1[1], a1[2], a1[3]};
-	}
-#pragma unroll
-	for (int kt = 0; kt < KTN; ++kt) {
-		if (l == 0 && (uint32_t)(16 * kt) >= enc_pad) continue;
-		const _Float16* as = img + SIN + 16 * kt + 4 * p;
-		const h4 b0 = tr_read(as + (8 * g + q) * STRIDE), b1 = tr_read(as + (8 * g + 4 + q) * STRIDE);
-		const h8 B = {b0[0], b0[1], b0[2], b0[3], b1[0], b1[1], b1[2], b1[3]};
-#pragma unroll
-		for (int mt = 0; mt < MT; ++mt) acc[TB + mt * KTN + kt] = mfma(A[mt], B, acc[TB + mt * KTN + kt]);
-	}
-}
-
-template <class N, int l>
-__device__ __forceinline__ void bwd_wave(const MlpArgs& a, const _Float16* frags, const _Float16* img, _Float16* dimg, int lane,
-                                         uint32_t base, f4 (&acc)[N::gtile_base(N::NL)]) {
-	if constexpr (l >= 0) {
-		wgrad_wave<N, l>(img, dimg, lane, acc, a.enc_pad);
-		dgrad_layer<N, l, WCT>(a, frags, img, dimg, lane, base);
-		bwd_wave<N, l - 1>(a, frags, img, dimg, lane, base, acc);
-	}
-}
-
-// The reduced tile t (16 x 16 fp32, MFMA C layout: lane (g, n) holds rows 4g..4g+3 of column n)
-// -> the workgroup's partials row.
-template <class N, int t>
-__device__ __forceinline__ void store_tile(const MlpArgs& a, int lane, f4 c) {
-	constexpr int l = N::tile_layer(t);
-	constexpr int KTN = N::KT16(l);
-	constexpr int mt = (t - N::gtile_base(l)) / KTN, kt = (t - N::gtile_base(l)) % KTN;
-	const int g = lane >> 4, n = lane & 15;
-	const uint32_t pin = a.param_in[l];
-	const uint32_t col = 16 * kt + n;
-	if (col >= pin) return;
-	float* gl = a.partials + (size_t)blockIdx.x * a.n_mlp + a.param_off[l];
-#pragma unroll
-	for (int r = 0; r < 4; ++r) {
-		const uint32_t row = 16 * mt + 4 * g + r;
-		if (row < (uint32_t)N::out_dim(l)) gl[(size_t)row * pin + col] = c[r];
-	}
-}
-
-// tile R0 + I of a reduction round: wave I % 4 sums the four waves' copies (fixed order)
-template <class N, int R0, int RT, int I>
-__device__ __forceinline__ void reduce_round(const MlpArgs& a, const f4* red, int wave, int lane) {
-	if constexpr (I < RT && R0 + I < N::gtile_base(N::NL)) {
-		if (I % WWAVES == wave) {
-			f4 sum = red[I * 64 + lane];
-#pragma unroll
-			for (int w = 1; w < WWAVES; ++w) sum += red[(w * RT + I) * 64 + lane];
-			store_tile<N, R0 + I>(a, lane, sum);
-		}
-		reduce_round<N, R0, RT, I + 1>(a, red, wave, lane);
-	}
-}
-
-// rounds of RT tiles: every wave parks its RT accumulators in LDS, then the tiles are summed
-// over the four waves and stored
-template <class N, int R0, int RT>
-__device__ __forceinline__ void reduce_tiles(const MlpArgs& a, f4* red, int wave, int lane, const f4 (&acc)[N::gtile_base(N::NL)]) {
-	constexpr int NT = N::gtile_base(N::NL);
-	if constexpr (R0 < NT) {
-		__syncthreads();  // the previous round's (or the loop's) LDS reads are done
-#pragma unroll
-		for (int t = R0; t < R0 + RT && t < NT; ++t) red[(wave * RT + (t - R0)) * 64 + lane] = acc[t];
-		__syncthreads();
-		reduce_round<N, R0, RT, 0>(a, red, wave, lane);
-		reduce_tiles<N, R0 + RT, RT>(a, red, wave, lane, acc);
-	}
-}
-
-template <class N>
-__global__ void __launch_bounds__(WBLOCK) k_mlp_train_w(MlpArgs a) {
-	if (a.n_dev) a.n = min(a.n, *a.n_dev);
-	extern __shared__ __attribute__((aligned(16))) char smem[];
-	constexpr int STRIDE = N::template stride<true>();
-	constexpr int DS = N::dstride();
-	constexpr int FH = (N::fwd_frags() + N::bwd_frags()) * FRAG_HALVES;
-	constexpr int NT = N::gtile_base(N::NL);
-	_Float16* frags = reinterpret_cast<_Float16*>(smem);
-	_Float16* imgs = frags + FH;
-	_Float16* dimgs = imgs + WAVES * SPW * STRIDE;
-	const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-	_Float16* img = imgs + wave * WSPW * STRIDE;
-	_Float16* dimg = dimgs + wave * WSPW * DS;
-
-	for (int t = threadIdx.x; t < FH / 8; t += WBLOCK)
-		reinterpret_cast<h8*>(frags)[t] = reinterpret_cast<const h8*>(a.frags)[t];
-	for (int t = lane; t < WSPW * STRIDE / 8; t += 64) reinterpret_cast<h8*>(img)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
-	for (int t = lane; t < WSPW * DS / 8; t += 64) reinterpret_cast<h8*>(dimg)[t] = h8{0, 0, 0, 0, 0, 0, 0, 0};
-	__syncthreads();  // the fragments are shared; from here on every wave runs on its own
-
-	f4 acc[NT];
-#pragma unroll
-	for (int t = 0; t < NT; ++t) acc[t] = f4{0.f, 0.f, 0.f, 0.f};
-
-	const uint32_t n_steps = (a.n + WSPW - 1) / WSPW;
-	const uint32_t step_stride = gridDim.x * WWAVES;
-	const bool pref = a.F == 2 && (a.E % 8) == 0 && N::ENC_ROWS / 8 * WSPW <= 128;
-	uint32_t step = blockIdx.x * WWAVES + wave;
-	TrainPrefetch pf;
-	if (pref && step < n_steps) train_fetch<N, WSPW>(a, step * WSPW, lane, pf);
-	for (; step < n_steps; step += step_stride) {
-		const uint32_t base = step * WSPW;
-		if (pref) {
-			train_commit<N, STRIDE, DS, WSPW>(a, pf, img, dimg, N::template x_seg<true>(), base, lane);
-			if (step + step_stride < n_steps) train_fetch<N, WSPW>(a, (step + step_stride) * WSPW, lane, pf);
-		} else {
-			load_encoding<N, STRIDE, WSPW>(a, img, base, lane);
-			load_sh<STRIDE, WSPW>(a, img, N::template x_seg<true>(), base, lane);
-			for (int t = lane; t < WSPW * 4; t += 64) {
-				const int smp = t % WSPW, ch = t / WSPW;
-				const uint32_t i = base + smp;
-				h8 v = {0, 0, 0, 0, 0, 0, 0, 0};
-				if (ch == 0 && i < a.n) {
-					const float w = a.weight ? a.weight[i] : 1.0f;
-					const __half* d = a.dloss + (size_t)i * 4;
-					v[0] = (_Float16)(__half2float(d[0]) * w);
-					v[1] = (_Float16)(__half2float(d[1]) * w);
-					v[2] = (_Float16)(__half2float(d[2]) * w);
-				}
-				lds_st_h8(dimg + smp * DS + 8 * ch, v);  // layer NL-1 uses buffer 0
-			}
-		}
-		f4 res[WCT];
-		fwd_range<N, true, 0, N::NL - 1, WCT>(frags, img, lane, res);
-		bwd_wave<N, N::NL - 1>(a, frags, img, dimg, lane, base, acc);
-	}
-	constexpr int RT = 8;
-	static_assert((size_t)WWAVES * RT * 64 * 16 <= N::lds_train(), "reduction rounds fit the images");
-	reduce_tiles<N, 0, RT>(a, reinterpret_cast<f4*>(smem), wave, lane, acc);
+	if (a.grads) flush_range<N, 0>(a, wave, lane, acc);
 }
 
 // ---------------------------------------------------------------------------
@@ -1473,40 +1167,6 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	NGP_HIP_CHECK(hipGetLastError());
 }
 
-bool render_net_supported(const ngp_model* m) {
-	bool ok = m->lt.F == 2 && m->lt.n_levels == 16 && m->enc_lsh == 2;
-	if (ok) NGP_DISPATCH(m->mlp_variant, ok = N::KE == 1 && N::Wp <= 64);
-	return ok;
-}
-
-void launch_render_net(const ngp_model* m, const __half* frags, const LevelTable& lt, const __half* table, const float* posdt,
-                       uint32_t n, __half* out, hipStream_t s, const uint32_t* n_dev, const __half* sh, const uint32_t* sh_ray,
-                       uint32_t sh_rows) {
-	if (n == 0) return;
-	if (!render_net_supported(m)) throw std::runtime_error("launch_render_net: needs F = 2, L = 16 and the plane layout");
-	MlpArgs a = base_args(m);
-	a.frags = frags;
-	a.n = n;
-	a.out = out;
-	a.n_dev = n_dev;
-	a.coord_bytes = (uint32_t)std::min<uint64_t>((uint64_t)n * 4, 0xffffffffu);
-	a.sh = sh;
-	a.sh_ray = sh_ray;
-	a.sh_bytes = (uint32_t)std::min<uint64_t>((uint64_t)sh_rows * 32, 0xffffffffu);
-	a.out_mode = 0;
-	a.out_stride = 4;
-	EncIn e{reinterpret_cast<const float4*>(posdt), table, lt};
-	NGP_DISPATCH(m->mlp_variant, {
-		if constexpr (N::KE == 1 && N::Wp <= 64) {
-			const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2 + 2 * RN_SAMPLES * 4 * sizeof(uint4);
-			const uint32_t wg_per_cu = m->tuning.render_net_workgroups_per_cu ? m->tuning.render_net_workgroups_per_cu : 4u;
-			const uint32_t grid = std::min<uint32_t>(div_up(n, RN_SAMPLES), cu_count() * wg_per_cu);
-			launch_timed(k_render_net<N>, grid, RN_BLOCK, lds, s, a, e);
-		}
-	});
-	NGP_HIP_CHECK(hipGetLastError());
-}
-
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev) {
 	if (n == 0) return;
@@ -1562,17 +1222,14 @@ void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc
 		const size_t lds = N::lds_train();
 		if (lds > 160 * 1024) throw std::runtime_error("MLP training LDS footprint exceeds 160 KiB");
 		const uint32_t grid = std::min<uint32_t>(div_up(n, SAMPLES_PER_BLOCK), cu_count());
-		m->mlp_partials.reserve((size_t)cu_count() * m->n_mlp_params);
-		a.partials = m->mlp_partials.ptr;
-		a.n_mlp = m->n_mlp_params;
-		if (m->tuning.mlp_train_schedule == 2) {
-			set_lds<N>(k_mlp_train_w<N>, lds);
-			launch_timed(k_mlp_train_w<N>, grid, WBLOCK, lds, s, a);
-		} else {
-			set_lds<N>(k_mlp_train<N>, lds);
-			launch_timed(k_mlp_train<N>, grid, TBLOCK, lds, s, a);
+		if (grads_mlp) {
+			m->mlp_partials.reserve((size_t)cu_count() * m->n_mlp_params);
+			a.partials = m->mlp_partials.ptr;
+			a.n_mlp = m->n_mlp_params;
 		}
-		k_mlp_reduce<<<div_up(16 * m->n_mlp_params, 256), 256, 0, s>>>(m->mlp_partials.ptr, grid, m->n_mlp_params, grads_mlp);
+		set_lds<N>(k_mlp_train<N>, lds);
+		launch_timed(k_mlp_train<N>, grid, TBLOCK, lds, s, a);
+		if (grads_mlp) k_mlp_reduce<<<div_up(16 * m->n_mlp_params, 256), 256, 0, s>>>(m->mlp_partials.ptr, grid, m->n_mlp_params, grads_mlp);
 	});
 	NGP_HIP_CHECK(hipGetLastError());
 }

@@ -55,14 +55,32 @@ static void require(bool cond, const char* msg) {
 
 static hipStream_t S(ngp_stream s) { return reinterpret_cast<hipStream_t>(s); }
 
-// ngp_tuning.encode_streaming: 0 = the default (non-temporal encoding stores: -2 % render frame
-// time, tools/render_ab.py), bit 7 = no hints
-// ngp_tuning.encode_xcd_regions: 0 = the default (contiguous XCD regions: -1.1 % render frame time in a same-weights
-// A/B), 3 = off
-static uint32_t encode_regions(const ngp_tuning& t) { return t.encode_xcd_regions == 0 ? 1u : t.encode_xcd_regions == 3 ? 0u : t.encode_xcd_regions; }
-static uint32_t encode_streaming_bits(const ngp_tuning& t) {
-	if (t.encode_streaming == 0) return 1u;
-	return t.encode_streaming & 127u;
+// ngp_tuning.encode_streaming: 0 = the default (non-temporal encoding stores: -2 % render frame time,
+// tools/render_ab.py), 1 = plain stores.  ngp_tuning.encode_xcd_regions: 0 = the default (contiguous XCD regions:
+// -1.1 % render frame time in a same-weights A/B), 1 = off.
+static void apply_encode_tuning(LevelTable& lt, const ngp_tuning& t) {
+	lt.streaming = t.encode_streaming == 0 ? 1u : 0u;
+	lt.regions = t.encode_xcd_regions == 0 ? 1u : 0u;
+}
+
+static void validate_tuning(const ngp_tuning* t) {
+	require(t != nullptr, "null argument");
+	require(t->render_pipelines <= RenderScratch::MAX_PIPES, "render_pipelines must be 0..4");
+	require(t->render_pass_samples <= (16u << 20), "render_pass_samples must be <= 2^24");
+	require(t->render_lag == 0 || (t->render_lag >= 2 && t->render_lag <= 4), "render_lag must be 0 or 2..4");
+	require(t->render_composite_block == 0 || t->render_composite_block == 256 || t->render_composite_block == 512 ||
+	            t->render_composite_block == 1024,
+	        "render_composite_block must be 0, 256, 512 or 1024");
+	require(t->render_generate_block == 0 || t->render_generate_block == 256 || t->render_generate_block == 512,
+	        "render_generate_block must be 0, 256 or 512");
+	require(t->encode_dense_records <= 1, "encode_dense_records must be 0 or 1");
+	require(t->mlp_workgroups_per_cu <= 32, "mlp_workgroups_per_cu must be <= 32");
+	require(t->encode_streaming <= 1, "encode_streaming must be 0 or 1");
+	require(t->grid_unsorted <= 1, "grid_unsorted must be 0 or 1");
+	require(t->render_mlp_tile == 0 || t->render_mlp_tile == 1 || t->render_mlp_tile == 4, "render_mlp_tile must be 0, 1 or 4");
+	require(t->encode_xcd_regions <= 1, "encode_xcd_regions must be 0 or 1");
+	require(t->render_skip_unfilled <= 2, "render_skip_unfilled must be 0, 1 or 2");
+	require(t->render_exit_cap <= 2, "render_exit_cap must be 0, 1 or 2");
 }
 
 // tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.
@@ -89,8 +107,7 @@ static void build_level_table(ngp_model* m) {
 		offset += params;
 	}
 	m->n_grid_params = (uint64_t)offset * lt.F;
-	lt.streaming = encode_streaming_bits(m->tuning);
-	lt.regions = encode_regions(m->tuning);
+	apply_encode_tuning(lt, m->tuning);
 }
 
 static void build_layers(ngp_model* m) {
@@ -246,32 +263,15 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 
 ngp_status ngp_model_set_tuning(ngp_model* m, const ngp_tuning* t) {
 	return guarded([&] {
-		require(m && t, "null argument");
-		require(t->render_pipelines <= RenderScratch::MAX_PIPES, "render_pipelines must be 0..4");
-		require(t->render_pass_samples <= (16u << 20), "render_pass_samples must be <= 2^24");
-		require(t->render_lag == 0 || (t->render_lag >= 2 && t->render_lag <= 4), "render_lag must be 0 or 2..4");
-		require(t->render_composite_block == 0 || t->render_composite_block == 256 || t->render_composite_block == 512 ||
-		            t->render_composite_block == 1024,
-		        "render_composite_block must be 0, 256, 512 or 1024");
-		require(t->render_generate_block == 0 || t->render_generate_block == 256 || t->render_generate_block == 512,
-		        "render_generate_block must be 0, 256 or 512");
-		require(t->mlp_workgroups_per_cu <= 32, "mlp_workgroups_per_cu must be <= 32");
-		require(t->encode_levels_per_thread == 0 || t->encode_levels_per_thread == 2 || t->encode_levels_per_thread == 4,
-		        "encode_levels_per_thread must be 0, 2 or 4");
-		require(t->render_network <= 2, "render_network must be 0, 1 or 2");
-		require(t->render_mlp_tile <= 4, "render_mlp_tile must be 0..4");
-		require(t->render_net_workgroups_per_cu <= 16, "render_net_workgroups_per_cu must be <= 16");
-		require(t->encode_xcd_regions <= 3, "encode_xcd_regions must be 0..3");
-		require(t->render_pass_order <= 3, "render_pass_order must be 0..3");
-		require(t->render_encode_wgs_per_cu <= 32, "render_encode_wgs_per_cu must be <= 32");
-		require(t->mlp_train_schedule <= 2, "mlp_train_schedule must be 0, 1 or 2");
-		require(t->render_slot_compaction <= 2, "render_slot_compaction must be 0, 1 or 2");
-		require(t->render_skip_unfilled <= 2, "render_skip_unfilled must be 0, 1 or 2");
+		require(m != nullptr, "null argument");
+		validate_tuning(t);
 		m->tuning = *t;
-		m->lt.pairs = t->encode_levels_per_thread == 2 ? 1u : 0u;
-		m->lt.streaming = encode_streaming_bits(*t);
-		m->lt.regions = encode_regions(*t);
+		apply_encode_tuning(m->lt, *t);
 	});
+}
+
+ngp_status ngp_tuning_validate(const ngp_tuning* t) {
+	return guarded([&] { validate_tuning(t); });
 }
 
 ngp_status ngp_model_get_tuning(const ngp_model* m, ngp_tuning* t) {
@@ -514,7 +514,9 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		std::memcpy(&loss, &c[8], 4);
 		st->loss = loss;
 		st->n_rays_with_samples = 0;
-		st->forward_early_stop_violations = c[9];
+		st->forward_early_stop_violations = c[9] & (VIOL_CAPACITY - 1u);
+		st->sample_capacity_overflow = (c[9] & VIOL_CAPACITY) ? 1u : 0u;
+		if (c[10]) m->ts.rank_cap_hint = next_multiple(c[10] + c[10] / 4, 4096u);  // this rank's need, with headroom
 	});
 }
 

@@ -151,12 +151,10 @@ struct LevelTable {
 	// max_level * L + 1e-3 encode to zero and get no gradient.  null: all levels.
 	const float* max_level = nullptr;
 	uint32_t ml_stride = 0;
-	// F = 2, L = 16: encode level pairs (g, 15 - g), pair g on XCD g (ngp_tuning.encode_levels_per_thread = 2)
-	uint32_t pairs = 0;
-	// ngp_tuning.encode_streaming: bit 0 non-temporal encoding stores, bit 1 non-temporal position loads
+	// 1: non-temporal encoding stores (ngp_tuning.encode_streaming = 0)
 	uint32_t streaming = 0;
-	// ngp_tuning.encode_xcd_regions (four levels per thread): 1 = each XCD encodes a contiguous eighth of the
-	// chunks, level group by level group; 2 = the four level groups of a chunk back to back on one XCD; 0 = off
+	// 1: each XCD encodes a contiguous eighth of the chunks, level group by level group (four levels per
+	// thread; ngp_tuning.encode_xcd_regions = 0); 0: XCD x takes every eighth chunk
 	uint32_t regions = 0;
 	__host__ __device__ bool level_cut(uint32_t level, uint32_t i) const {
 		if (!max_level) return false;
@@ -245,6 +243,10 @@ struct DevBuf {
 constexpr float GRAD_FIXED_SCALE = 1099511627776.0f;          // 2^40
 constexpr float GRAD_FIXED_INV = 1.0f / 1099511627776.0f;     // 2^-40
 
+// high bit of the step's violation word (counters[9]): a data-parallel rank's share of the samples did not fit
+// its buffers (k_dp_caps); the low bits count the chunked forward's early-stop violations
+constexpr uint32_t VIOL_CAPACITY = 1u << 20;
+
 struct TrainScratch {
 	DevBuf<uint32_t> ray_numsteps;     // [R][2]
 	DevBuf<uint32_t> ray_compacted;    // [R][2]
@@ -285,6 +287,8 @@ struct TrainScratch {
 	bool gated_optimizer_ran = false;  // an optimizer step gated by the last step's violation word was enqueued
 	uint32_t last_rows[3] = {0, 0, 0}; // evaluation rows of each chunk in the last read-back step
 	uint32_t last_n_rays = 0, last_target = 0, last_max_samples = 0;
+	// data parallelism: the sample capacity a step that did not fit asked for (grown on the retry)
+	uint32_t rank_cap_hint = 0;
 };
 
 struct GridState {
@@ -312,21 +316,20 @@ struct RenderPipeScratch {
 	DevBuf<float> rgba[3];      // [n][4]
 	DevBuf<float> depth[3];     // [n]
 	DevBuf<float> coords;       // [max_samples][4] position + warped dt, then [max_samples] SH row indices
-	DevBuf<float> stage;        // [max_samples][4] slot compaction: ray i's samples of a pass at i * n_steps
 	DevBuf<__half> enc;         // [L][max_samples][F]
 	DevBuf<__half> out;         // [max_samples][4]
 	DevBuf<uint32_t> counters;  // [16]
 	// Normals render mode: d(raw density)/d(warped position) of the pass's samples and its scratch
 	DevBuf<__half> nrm_dloss, nrm_denc;
-	DevBuf<float> nrm, nrm_grads;
+	DevBuf<float> nrm;
 	DevBuf<uint32_t> host_counter;  // pinned, fine-grained (hipHostMalloc): per-pass counters
 	uint32_t* host_counter_dev = nullptr;  // its device address
 	uint32_t pass_tag = 0;          // tags of published passes (monotonic across renders)
 	hipEvent_t events[2] = {nullptr, nullptr};  // per-pass counter read-backs
 	void release() {
 		for (int b = 0; b < 3; ++b) { payload[b].release(); rgba[b].release(); depth[b].release(); }
-		coords.release(); stage.release(); enc.release(); out.release(); counters.release();
-		nrm_dloss.release(); nrm_denc.release(); nrm.release(); nrm_grads.release();
+		coords.release(); enc.release(); out.release(); counters.release();
+		nrm_dloss.release(); nrm_denc.release(); nrm.release();
 		if (host_counter.ptr) (void)hipHostFree(host_counter.ptr);
 		host_counter.ptr = nullptr;
 		for (auto& e : events)
@@ -339,8 +342,6 @@ struct RenderScratch {
 	RenderPipeScratch pipe[MAX_PIPES];
 	hipStream_t streams[MAX_PIPES] = {};  // pipelines 1.. run on their own streams ([0] unused: the caller's)
 	hipEvent_t fork = nullptr, join[MAX_PIPES] = {};  // caller's stream -> pipeline streams -> caller's stream
-	hipEvent_t chain[MAX_PIPES] = {};  // ngp_tuning.render_pass_order >= 2: a pipeline's last chained network launch
-	DevBuf<uint32_t> summary;  // occupancy summary, OCC_SUMMARY_BYTES per mip
 	DevBuf<uint4> dense_rec;   // corner records of the dense levels (LevelTable::rec), rebuilt per render
 	DevBuf<uint4> shrows;      // [W * H][2]: each ray's 16 fp16 SH inputs, indexed by its pixel (k_render_init)
 	DevBuf<uint8_t> df;        // octant distance fields [mip][8][N] (ngp_math.h lattice_step_df)
@@ -352,14 +353,12 @@ struct RenderScratch {
 	size_t cap = 0;
 	void release() {
 		for (auto& p : pipe) p.release();
-		summary.release(); dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();
+		dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();
 		slice_coords.release(); slice_enc.release(); slice_out.release();
 		if (fork) (void)hipEventDestroy(fork);
 		fork = nullptr;
 		for (int j = 0; j < MAX_PIPES; ++j) {
 			if (join[j]) (void)hipEventDestroy(join[j]);
-			if (chain[j]) (void)hipEventDestroy(chain[j]);
-			chain[j] = nullptr;
 			if (streams[j]) (void)hipStreamDestroy(streams[j]);
 			join[j] = nullptr;
 			streams[j] = nullptr;
@@ -455,15 +454,11 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 // render.hip: the octant distance fields of the bitfield's mips [0, max_mip] into m->rs.df (rebuilt only
 // when the bitfield changed); the renderer's march and the training sampler (aabb_scale 1) read them
 void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s);
-// The renderer's fused encoding + network (k_render_net): F = 2, L = 16, the plane layout, one K step
-bool render_net_supported(const ngp_model* m);
-void launch_render_net(const ngp_model* m, const __half* frags, const LevelTable& lt, const __half* table, const float* posdt,
-                       uint32_t n, __half* out, hipStream_t s, const uint32_t* n_dev, const __half* sh, const uint32_t* sh_ray,
-                       uint32_t sh_rows);
 void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout, uint32_t n,
                         __half* out, hipStream_t s, const uint32_t* n_dev = nullptr);
 // dsh (optional): [n][16] dL/d(SH inputs of the rgb network), of the sample's own row (divided
-// by its rollover weight), for the camera gradients
+// by its rollover weight), for the camera gradients.  grads_mlp null: dL/denc only (no weight gradients);
+// coords null: the zero direction (for dL/dout with zero rgb rows, where the direction does not matter)
 void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,

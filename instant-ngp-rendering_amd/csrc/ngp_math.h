@@ -486,58 +486,7 @@ NGP_HD bool density_grid_occupied_at(v3 pos, const uint8_t* bitfield, uint32_t m
 	return bitfield[idx / 8 + (NERF_GRID_N_CELLS / 8) * mip] & (1u << (idx % 8));
 }
 
-// Same lookup through a one-word cache: a 64-bit word of the Morton-ordered bitfield
-// covers a 4x4x4 block of cells, so a marching ray re-reads memory only when it leaves
-// that block.  Returns exactly what density_grid_occupied_at returns.
-struct OccCache {
-	uint32_t key;
-	uint64_t bits;
-};
-NGP_HD OccCache occ_cache_init() {
-	OccCache c;
-	c.key = 0xFFFFFFFFu;
-	c.bits = 0;
-	return c;
-}
-NGP_HD bool density_grid_occupied_cached(v3 pos, const uint8_t* bitfield, uint32_t mip, OccCache& c) {
-	uint32_t idx = cascaded_grid_idx_at(pos, mip);
-	if (idx == 0xFFFFFFFFu) return false;
-	const uint32_t key = (NERF_GRID_N_CELLS / 64) * mip + idx / 64;
-	if (key != c.key) {
-		c.key = key;
-		c.bits = reinterpret_cast<const uint64_t*>(bitfield)[key];
-	}
-	return (c.bits >> (idx % 64)) & 1ull;
-}
-
 NGP_HD float signf_(float x) { return x > 0.0f ? 1.0f : (x < 0.0f ? -1.0f : 0.0f); }
-
-// Occupancy summary per mip, derived from the bitfield (render.hip k_occupancy_summary):
-// level A = 32768 bits, one per 4^3-cell Morton block (cell >> 6: "its 64-bit bitfield
-// word is non-zero"), level B = 4096 bits per 8^3 block (cell >> 9), level C = one byte
-// per 32^3 block (cell >> 15).  4.6 KB per mip: the render kernels keep it in LDS, so
-// empty space is crossed without touching the bitfield at all.
-constexpr uint32_t OCC_SUMMARY_A = 0, OCC_SUMMARY_B = 4096, OCC_SUMMARY_C = 4096 + 512;
-constexpr uint32_t OCC_SUMMARY_BYTES = 4096 + 512 + 64;
-static_assert(OCC_SUMMARY_BYTES % 16 == 0, "summary is staged into LDS in 16-byte pieces");
-NGP_HD bool summary_bit(const uint8_t* sm, uint32_t level_base, uint32_t b) {
-	return (sm[level_base + (b >> 3)] >> (b & 7u)) & 1u;
-}
-NGP_HD bool summary_c(const uint8_t* sm, uint32_t b) { return sm[OCC_SUMMARY_C + b] != 0; }
-// density_grid_occupied_at through the summary (level A) and the one-word cache
-NGP_HD bool occupied_summarised(v3 pos, const uint8_t* bitfield, const uint8_t* summary, uint32_t mip, OccCache& c,
-                                uint32_t* cell_out) {
-	const uint32_t cell = cascaded_grid_idx_at(pos, mip);
-	*cell_out = cell;
-	if (cell == 0xFFFFFFFFu) return false;
-	if (!summary_bit(summary + OCC_SUMMARY_BYTES * mip, OCC_SUMMARY_A, cell >> 6)) return false;
-	const uint32_t key = (NERF_GRID_N_CELLS / 64) * mip + cell / 64;
-	if (key != c.key) {
-		c.key = key;
-		c.bits = reinterpret_cast<const uint64_t*>(bitfield)[key];
-	}
-	return (c.bits >> (cell % 64)) & 1ull;
-}
 
 // ---------------------------------------------------------------------------
 // Stepping lattice.  A ray's candidate samples sit at n0 + k (k = 0, 1, ...) in the
@@ -612,60 +561,14 @@ NGP_HD uint32_t mip_from_dt(float dt, v3 pos, uint32_t max_cascade = NERF_CASCAD
 	return (uint32_t)m;
 }
 
-// Render march (if_unoccupied_advance_to_next_occupied_voxel, nerf_device.cuh:461-494, on
-// the lattice): moves *n to the first lattice point at or after it whose cell (at
-// clamp(mip_from_pos, 0, max_mip)) is occupied; false once the ray leaves the AABB.
-// An empty cell is skipped in one jump to the first lattice point past its far face
-// (at the coarsest empty mip, as the reference does) -- or past the far face of the
-// largest empty aligned Morton block of 4^3, 8^3 or 32^3 cells around it (occupancy
-// summary above).  The jump is taken only if the lattice point just before the
-// landing point is still inside the skipped cell/block (or already outside the AABB),
-// so every skipped point lies in empty space or outside the volume and the result
-// equals testing the points one by one.
+// Render march (if_unoccupied_advance_to_next_occupied_voxel, nerf_device.cuh:461-494, on the
+// lattice): a lattice point is a sample when it lies in the AABB and its cell at clamp(mip_from_pos,
+// 0, max_mip) is occupied; an empty cell is left in one jump past the far faces of the empty box
+// the octant distance fields give for it (at the coarsest empty mip, as the reference climbs).
+// The jump is taken only if the lattice point just before the landing point is still inside the
+// skipped box (or already outside the AABB), so every skipped point lies in empty space or outside
+// the volume and the result equals testing the points one by one.
 enum LatticeStep : int { LATTICE_OCCUPIED = 0, LATTICE_SKIPPED = 1, LATTICE_EXIT = 2 };
-// One step of the march at lattice point *n_io: occupied (left unchanged), exited the
-// AABB, or skipped (moved to the next candidate point).  Kept as a single step so a
-// wave's lanes can interleave sampling and skipping without serialising on each other.
-NGP_HD int lattice_step(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
-                        const uint8_t* summary, uint32_t max_mip, const RenderBox& aabb, OccCache& cache) {
-	const float n = *n_io;
-	const float t = step_from(st, n);
-	const v3 pos = o + d * t;
-	if (t >= MAX_DEPTH || !rbox_contains(aabb, pos)) return LATTICE_EXIT;
-	uint32_t mip = mip_from_pos(pos);
-	mip = mip > max_mip ? max_mip : mip;
-	uint32_t cell;
-	if (occupied_summarised(pos, bitfield, summary, mip, cache, &cell)) return LATTICE_OCCUPIED;
-	while (mip < max_mip) {  // coarsest empty mip, as the reference climbs
-		uint32_t up;
-		if (occupied_summarised(pos, bitfield, summary, mip + 1, cache, &up)) break;
-		++mip;
-		cell = up;
-	}
-	// jump over the largest empty aligned block around pos at `mip`: 1, 4^3, 8^3 or 32^3 cells
-	uint32_t shift = 0;
-	if (cell != 0xFFFFFFFFu) {
-		const uint8_t* sm = summary + OCC_SUMMARY_BYTES * mip;
-		if (!summary_bit(sm, OCC_SUMMARY_A, cell >> 6)) {
-			shift = 6;
-			if (!summary_bit(sm, OCC_SUMMARY_B, cell >> 9)) {
-				shift = 9;
-				if (!summary_c(sm, cell >> 15)) shift = 15;
-			}
-		}
-	}
-	const uint32_t here = cell >> shift;
-	const float n_far = step_to(st, t + distance_to_next_cell(pos, d, idir, mip + shift / 3u));
-	float nn = n + ceilf(fmaxf(n_far - n, 0.5f));
-	if (nn - n > 1.0f) {
-		// the jump stands if the point before the landing point is still in the skipped
-		// cell/block, or already outside the AABB (the ray leaves the volume inside the block)
-		const v3 last = o + d * step_from(st, nn - 1.0f);
-		if (rbox_contains(aabb, last) && (cascaded_grid_idx_at(last, mip) >> shift) != here) nn = n + 1.0f;
-	}
-	*n_io = nn;
-	return LATTICE_SKIPPED;
-}
 
 // Octant distance fields (render.hip k_df_*): for each mip, ray octant o (bit k set = the
 // direction's component k is negative) and cell c, D = the Chebyshev distance from c to the
@@ -785,14 +688,6 @@ NGP_HD int train_step_df(uint32_t* k_io, float n0, const Stepping& st, v3 o, v3 
 	}
 	*k_io = k + c;
 	return LATTICE_SKIPPED;
-}
-
-NGP_HD bool next_occupied_lattice_point(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, const uint8_t* bitfield,
-                                        const uint8_t* summary, uint32_t max_mip, const RenderBox& aabb, OccCache& cache) {
-	while (true) {
-		const int r = lattice_step(n_io, st, o, d, idir, bitfield, summary, max_mip, aabb, cache);
-		if (r != LATTICE_SKIPPED) return r == LATTICE_OCCUPIED;
-	}
 }
 
 // ---------------------------------------------------------------------------

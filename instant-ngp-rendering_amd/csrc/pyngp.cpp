@@ -35,14 +35,10 @@ static py::array_t<float> pinned_frame(int height, int width) {
 #define NGP_TUNING_FIELDS                                                                                              \
 	NGP_TUNING_FIELD(render_pipelines) NGP_TUNING_FIELD(render_pass_samples) NGP_TUNING_FIELD(render_lanes)          \
 	NGP_TUNING_FIELD(render_first_steps) NGP_TUNING_FIELD(render_max_steps) NGP_TUNING_FIELD(render_lag)             \
-	NGP_TUNING_FIELD(render_budget_scale) NGP_TUNING_FIELD(render_block_skipping)                                    \
-	NGP_TUNING_FIELD(render_composite_block) NGP_TUNING_FIELD(render_generate_block)                                 \
-	NGP_TUNING_FIELD(encode_dense_records) NGP_TUNING_FIELD(mlp_workgroups_per_cu) NGP_TUNING_FIELD(debug)                          \
-	NGP_TUNING_FIELD(encode_levels_per_thread) NGP_TUNING_FIELD(encode_streaming)                          \
-	NGP_TUNING_FIELD(render_network) NGP_TUNING_FIELD(render_net_workgroups_per_cu)                          \
-	NGP_TUNING_FIELD(train_chain_walk) NGP_TUNING_FIELD(grid_unsorted) NGP_TUNING_FIELD(render_mlp_tile) NGP_TUNING_FIELD(encode_xcd_regions) \
-	NGP_TUNING_FIELD(render_pass_order) NGP_TUNING_FIELD(render_encode_wgs_per_cu) \
-	NGP_TUNING_FIELD(mlp_train_schedule) NGP_TUNING_FIELD(render_slot_compaction) NGP_TUNING_FIELD(render_skip_unfilled) NGP_TUNING_FIELD(render_tail_rays)
+	NGP_TUNING_FIELD(render_budget_scale) NGP_TUNING_FIELD(render_composite_block) NGP_TUNING_FIELD(render_generate_block) \
+	NGP_TUNING_FIELD(encode_dense_records) NGP_TUNING_FIELD(mlp_workgroups_per_cu) NGP_TUNING_FIELD(debug)           \
+	NGP_TUNING_FIELD(encode_streaming) NGP_TUNING_FIELD(grid_unsorted) NGP_TUNING_FIELD(render_mlp_tile)             \
+	NGP_TUNING_FIELD(encode_xcd_regions) NGP_TUNING_FIELD(render_skip_unfilled) NGP_TUNING_FIELD(render_exit_cap)
 
 namespace {
 
@@ -645,6 +641,7 @@ PYBIND11_MODULE(pyngp, m) {
 			d["rays_per_batch"] = t.nerf.training.counters_rgb.rays_per_batch;
 			d["n_rays"] = s.n_rays;
 			d["forward_early_stop_violations"] = s.forward_early_stop_violations;
+			d["sample_capacity_overflow"] = s.sample_capacity_overflow;
 			d["forward_early_stop_violations_total"] = t.forward_early_stop_violations;
 			return d;
 		})

@@ -55,9 +55,7 @@ struct RenderK {
 	uint32_t drx, dry;
 	uint32_t h_local, tiles_x;  // local rows; 8x8 pixel tiles per row of tiles
 	uint32_t pipe_index, pipe_count;  // this pipeline's 8-row blocks of the shard's rows
-	const uint8_t* bitfield;
-	const uint8_t* summary;
-	const uint8_t* df;  // octant distance fields (null: occupancy-summary block skipping)
+	const uint8_t* df;  // octant distance fields [mip][octant][cell] (ngp_math.h lattice_step_df)
 	int budget;         // per-ray sample budgets (sample_budget); 0: every ray gets n_steps
 	float budget_scale;
 	uint32_t* dbg;  // ngp_tuning.debug bit 0: [init lattice steps, init alive, generate iterations, samples, samples composited]
@@ -67,6 +65,7 @@ struct RenderK {
 	float aperture, focus_z;  // depth of field (uv_to_ray, common_device.cuh:450-456)
 	const float* normals;     // Normals mode: d(raw density)/d(warped position) per sample slot of the pass, [slot][3]
 	int mark_unfilled;        // unfilled slots get SH row NO_SH_ROW (the render MLP skips tiles of them)
+	int exit_cap;             // a ray's per-pass budget is capped by the lattice points left to its exit
 };
 
 // square2disk_shirley (random_val.cuh:112-128)
@@ -110,19 +109,9 @@ __device__ __forceinline__ uint32_t local_to_global_row(const RenderK& k, uint32
 	return (blk * k.shard_count + k.shard_index) * k.shard_rows + within;
 }
 
-// Copies the summaries of mips [0, max_mip] into LDS (all threads of the block).
-__device__ __forceinline__ const uint8_t* stage_summary(const uint8_t* __restrict__ g, uint32_t max_mip) {
-	extern __shared__ uint4 s_summary[];
-	const uint32_t n16 = (max_mip + 1) * OCC_SUMMARY_BYTES / 16;
-	const uint4* src = reinterpret_cast<const uint4*>(g);
-	for (uint32_t k = threadIdx.x; k < n16; k += blockDim.x) s_summary[k] = src[k];
-	__syncthreads();
-	return reinterpret_cast<const uint8_t*>(s_summary);
-}
-
 template <bool LENS>
-__device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
-                                              Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer);
+__device__ __forceinline__ bool init_ray_body(const RenderK& k, uint32_t x, uint32_t yl, Payload* pp, float4* __restrict__ frame,
+                                              float* __restrict__ depth_buffer);
 
 // Stream compaction slot for a 256-thread block: ballot per wave, LDS prefix over the four
 // waves, ONE global atomic per block and flag (instead of one per wave).  Returns the
@@ -220,14 +209,13 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
                                                      float* __restrict__ depth, float4* __restrict__ frame,
                                                      float* __restrict__ depth_buffer, uint32_t* __restrict__ counters,
                                                      uint4* __restrict__ shrows) {
-	const uint8_t* summary = stage_summary(k.summary, k.max_mip);
 	// rays are numbered in 8x8 pixel tiles: a wave's 64 rays are a square patch, so at a
 	// given step their samples are close in space (hash-grid gathers share cache lines)
 	const uint32_t r = blockIdx.x * blockDim.x + threadIdx.x;
 	const uint32_t tile = r >> 6, x = (tile % k.tiles_x) * 8u + (r & 7u), yl = (tile / k.tiles_x) * 8u + ((r >> 3) & 7u);
 	Payload p;
 	bool alive = false;
-	if (x < k.W && yl < k.h_local) alive = init_ray_body<LENS>(k, summary, x, yl, &p, frame, depth_buffer);
+	if (x < k.W && yl < k.h_local) alive = init_ray_body<LENS>(k, x, yl, &p, frame, depth_buffer);
 	uint32_t slot, unused;
 	block_append2(alive, false, &counters[0], &counters[3], &slot, &unused);
 	if (alive) {
@@ -246,8 +234,8 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 
 // init_rays_with_payload_kernel_nerf + advance_pos_nerf for pixel x of local row yl
 template <bool LENS>
-__device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* summary, uint32_t x, uint32_t yl,
-                                              Payload* pp, float4* __restrict__ frame, float* __restrict__ depth_buffer) {
+__device__ __forceinline__ bool init_ray_body(const RenderK& k, uint32_t x, uint32_t yl, Payload* pp, float4* __restrict__ frame,
+                                              float* __restrict__ depth_buffer) {
 	const uint32_t y = local_to_global_row(k, yl);
 	const uint32_t idx = x + k.W * y;
 	frame[idx] = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -292,13 +280,11 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, const uint8_t* s
 		// advance_pos_nerf: jitter the start and skip empty space
 		const v3 idir = mk3(1.0f / dir.x, 1.0f / dir.y, 1.0f / dir.z);
 		float n = step_to(k.st, t) + ld_random_val(k.sample_index, idx * 786433u);
-		OccCache occ = occ_cache_init();
 		const uint32_t oct = ray_octant(dir);
 		int st;
 		uint32_t steps = 0;
 		do {
-			st = k.df ? lattice_step_df(&n, k.st, origin, dir, idir, oct, k.df, k.max_mip, k.aabb)
-			          : lattice_step(&n, k.st, origin, dir, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
+			st = lattice_step_df(&n, k.st, origin, dir, idir, oct, k.df, k.max_mip, k.aabb);
 			++steps;
 		} while (st == LATTICE_SKIPPED);
 		alive = st == LATTICE_OCCUPIED;
@@ -374,36 +360,6 @@ __global__ void __launch_bounds__(256) k_slice_shade(RenderK k, uint32_t n, cons
 	const float4 f = frame[idx];
 	frame[idx] = make_float4(t.x + f.x * (1.0f - t.w), t.y + f.y * (1.0f - t.w), t.z + f.z * (1.0f - t.w), t.w + f.w * (1.0f - t.w));
 }
-
-// Occupancy summary (ngp_math.h OCC_SUMMARY_*): one workgroup of 512 threads per 32^3
-// block = 512 bitfield words; a wave's 64 words are eight 8^3 blocks, so levels A and B
-// come from one ballot and level C from the eight waves' ballots in LDS.  Block 0 also
-// zeroes the tracer's counters (this kernel runs first in every render).
-__global__ void __launch_bounds__(512) k_occupancy_summary(const uint8_t* __restrict__ bitfield, uint8_t* __restrict__ summary,
-                                                           uint32_t* __restrict__ counters) {
-	__shared__ uint32_t any_wave[8];
-	const uint32_t g = blockIdx.x * 512u + threadIdx.x;  // [mip][32768 words]
-	const uint32_t mip = g >> 15, wi = g & 32767u, lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
-	if (g < 8) counters[g] = 0;
-	const uint64_t word = reinterpret_cast<const uint64_t*>(bitfield + (size_t)mip * (NERF_GRID_N_CELLS / 8))[wi];
-	const unsigned long long a = __ballot(word != 0ull);
-	uint8_t* sm = summary + (size_t)OCC_SUMMARY_BYTES * mip;
-	if (lane == 0) {
-		*reinterpret_cast<unsigned long long*>(sm + OCC_SUMMARY_A + (wi >> 3)) = a;
-		uint8_t b = 0;
-		for (uint32_t k = 0; k < 8; ++k) b |= ((a >> (8 * k)) & 0xffull) ? (uint8_t)(1u << k) : (uint8_t)0;
-		sm[OCC_SUMMARY_B + (wi >> 6)] = b;
-		any_wave[w] = a != 0ull;
-	}
-	__syncthreads();
-	if (threadIdx.x == 0) {
-		uint32_t c = 0;
-		for (uint32_t k = 0; k < 8; ++k) c |= any_wave[k];
-		sm[OCC_SUMMARY_C + (wi >> 9)] = (uint8_t)c;
-	}
-}
-
-
 
 // Octant distance fields (ngp_math.h lattice_step_df), three separable exact passes of the
 // Chebyshev transform restricted to an orthant: D = min over occupied c' of max_k |c'_k - c_k|
@@ -513,6 +469,16 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 	return b >= (float)n_steps ? n_steps : (uint32_t)fmaxf(b, 1.0f);
 }
 
+// Lattice points a ray at stepping-space position n can still sample before it leaves the render
+// box: floor(n_exit - n) + 1 points at or before the exit, plus one of margin for the rounding of
+// n_exit (a bound only: a ray whose budget runs out before its exit simply continues next pass).
+__device__ __forceinline__ uint32_t points_to_exit(const RenderK& k, v3 o, v3 d, float n) {
+	float t0, t1;
+	ray_intersect(k.aabb.box, rbox_local(k.aabb, o), rbox_local(k.aabb, d), &t0, &t1);
+	const float left = step_to(k.st, fminf(t1, MAX_DEPTH)) - n;
+	return left < 0.0f ? 1u : (left > 1048576.0f ? 1048576u : (uint32_t)left + 2u);
+}
+
 // generate_next_nerf_network_inputs (testbed_nerf.cu:421-469): the next samples of every
 // alive ray.  Each ray first reserves its budget of sample slots (one atomic per block),
 // so the pass's samples are ray-major and packed; the encode and MLP read the total from
@@ -520,18 +486,14 @@ __device__ __forceinline__ uint32_t sample_budget(const RenderK& k, float T, flo
 // lattice points at once (ballots give the occupied ones in order and the first exit),
 // and an all-empty round jumps on from the last lane's verified skip.  G = 1 for the big
 // early passes (one lane per ray, flat loop), up to 64 for the last few thousand rays,
-// whose long serial marches otherwise dominate the tail passes.
-//
-// COMPACT (slot compaction, ngp_tuning.render_slot_compaction = 1, opt-in): a ray marches into its own
-// staging range [i * n_steps, i * n_steps + budget) first, then reserves exactly the samples it found
-// and copies them (L2-resident) to the pass's packed rows -- no reserved-but-unfilled slots (about
-// half the slots of a volumetric scene's pass: rays leave the volume inside their budget).  Measured
-// 3 % slower per frame than the up-front reservation: the unfilled slots cost the encoder (which
-// skips them) and the MLP less than the copy turn costs the latency-bound march.
-template <uint32_t G, bool COMPACT>
+// whose long serial marches otherwise dominate the tail passes.  A ray's budget is its
+// transmittance budget (sample_budget), capped by the lattice points left to its exit
+// (k.exit_cap): the slots a ray reserves but does not fill still cost a 20-B row store,
+// the encoder's zero features and, in mixed tiles, the MLP.
+template <uint32_t G>
 __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
                                                   Payload* __restrict__ payloads, const float4* __restrict__ rgba,
-                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray, float4* __restrict__ stage,
+                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray,
                                                   uint32_t target, uint32_t max_steps,
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
@@ -548,33 +510,29 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 		*next_alive_counter = 0;  // filled by this pass's k_composite
 		*steps_out = n_alive ? n_steps : 0u;
 	}
-	const uint8_t* summary = k.df ? nullptr : stage_summary(k.summary, k.max_mip);
 	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
 	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
 	const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
 	const bool valid = i < n_alive;  // group-uniform
 	Payload* p = payloads + (valid ? i : 0);
-	uint32_t budget = 0;
-	if (valid) budget = sample_budget(k, 1.0f - rgba[i].w, p->alpha_last, n_steps);
-	uint32_t base = 0;
-	if constexpr (!COMPACT) {
-		base = block_reserve(r == 0 ? budget : 0u, sample_counter);
-		if (G > 1) base = __shfl(base, g0, 64);
-	}
-	float4* const out_rows = COMPACT ? stage + (size_t)i * n_steps : posdt + base;
 	bool running = valid;
 	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f);
 	float n = 0.0f;
 	uint32_t row = 0;  // the ray's SH row (its pixel index; written once per frame by k_render_init)
+	uint32_t budget = 0;
 	if (running) {
 		o = mk3(p->o[0], p->o[1], p->o[2]);
 		d = mk3(p->d[0], p->d[1], p->d[2]);
 		idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		n = p->n;
 		row = p->idx;
+		budget = sample_budget(k, 1.0f - rgba[i].w, p->alpha_last, n_steps);
+		if (k.exit_cap) budget = min(budget, points_to_exit(k, o, d, n));
 	}
-	OccCache occ = occ_cache_init();
+	uint32_t base = block_reserve(r == 0 ? budget : 0u, sample_counter);
+	if (G > 1) base = __shfl(base, g0, 64);
+	float4* const out_rows = posdt + base;
 	const uint32_t oct = ray_octant(d);
 	uint32_t j = 0, iters = 0;
 	bool exited = false;
@@ -583,8 +541,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 		float nr = n + (float)r;
 		int st = LATTICE_EXIT;
 		if (running)
-			st = k.df ? lattice_step_df(&nr, k.st, o, d, idir, oct, k.df, k.max_mip, k.aabb)
-			          : lattice_step(&nr, k.st, o, d, idir, k.bitfield, summary, k.max_mip, k.aabb, occ);
+			st = lattice_step_df(&nr, k.st, o, d, idir, oct, k.df, k.max_mip, k.aabb);
 		const unsigned long long m_exit = __ballot(running && st == LATTICE_EXIT) & gmask;
 		const unsigned long long m_occ = __ballot(running && st == LATTICE_OCCUPIED) & gmask;
 		const float n_last = __shfl(st == LATTICE_SKIPPED ? nr : n + (float)G, g0 + G - 1, 64);
@@ -600,7 +557,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 				const float dt = step_from(k.st, pn + 1.0f) - t;
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 				out_rows[j + rank] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				if constexpr (!COMPACT) sray[(size_t)base + j + rank] = row;
+				sray[(size_t)base + j + rank] = row;
 			}
 		}
 		if (cnt >= room) {
@@ -619,24 +576,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 			}
 		}
 	}
-	if constexpr (COMPACT) {
-		// exactly the samples found: packed rows in ray order within the block
-		base = block_reserve(valid && r == 0 ? j : 0u, sample_counter);
-		if (G > 1) base = __shfl(base, g0, 64);
-		if (valid) {
-			const float4* src = stage + (size_t)i * n_steps;
-			uint32_t q = r;
-			for (; q + 3u * G < j; q += 4u * G) {
-				const float4 a0 = src[q], a1 = src[q + G], a2 = src[q + 2u * G], a3 = src[q + 3u * G];
-				posdt[(size_t)base + q] = a0;
-				posdt[(size_t)base + q + G] = a1;
-				posdt[(size_t)base + q + 2u * G] = a2;
-				posdt[(size_t)base + q + 3u * G] = a3;
-			}
-			for (; q < j; q += G) posdt[(size_t)base + q] = src[q];
-			for (q = r; q < j; q += G) sray[(size_t)base + q] = row;
-		}
-	} else if (valid) {
+	if (valid) {
 		// reserved slots the ray did not fill (it left the volume) still go through the encoder
 		// and the MLP: x = -1 marks them for the encoder to skip (zero features)
 		const uint32_t tail_row = k.mark_unfilled ? NO_SH_ROW : row;
@@ -657,11 +597,9 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 	}
 }
 
-// samples loaded ahead of their use in k_composite
-constexpr uint32_t COMPOSITE_AHEAD = 4;  // 8 measured no better (same-weights A/B)
-// the tail passes (few rays, up to 32 samples each): every sample of the pass loaded at once, so a ray's
-// composite waits for one load round trip instead of eight (the same serial arithmetic: same image)
-constexpr uint32_t COMPOSITE_AHEAD_TAIL = 32;
+// samples loaded ahead of their use in k_composite (8 measured no better, same-weights A/B; so did all
+// of a tail pass's samples at once, profiles/r03_tail_composite_ab.txt)
+constexpr uint32_t COMPOSITE_AHEAD = 4;
 
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
@@ -670,7 +608,7 @@ constexpr uint32_t COMPOSITE_AHEAD_TAIL = 32;
 // Positions / Depth: its position / camera depth, Normals: the normalised negative density
 // gradient; Cost counts the ray's composited samples in c.x (shade_kernel_nerf turns it into a
 // grey level, :1327-1330) as payload.n_steps = j + current_step does (:664-667).
-template <bool MODES, uint32_t AHEAD = COMPOSITE_AHEAD>
+template <bool MODES>
 __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
                                                    const Payload* __restrict__ sp, const float4* __restrict__ srgba,
                                                    const float* __restrict__ sdepth, const float4* __restrict__ posdt,
@@ -701,18 +639,18 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		filled = actual;
 		const size_t sbase = p.base;
 		// samples are loaded 4 ahead of their use (the loop is otherwise one dependent
-		// global-load latency per sample; the tail passes run up to 32 per ray)
+		// global-load latency per sample)
 		bool done = false;
 		uint32_t used = actual;
 		float alpha_last = p.alpha_last;
 		// only each sample's dt is read in the loop (4 B instead of the 16-B row); the position of
 		// the max-weight sample -- the depth -- is read once after it
 		size_t s_max = ~(size_t)0;
-		for (uint32_t j0 = 0; j0 < actual && !done; j0 += AHEAD) {
-			uint2 o2[AHEAD];
-			float wdt[AHEAD];
+		for (uint32_t j0 = 0; j0 < actual && !done; j0 += COMPOSITE_AHEAD) {
+			uint2 o2[COMPOSITE_AHEAD];
+			float wdt[COMPOSITE_AHEAD];
 #pragma unroll
-			for (uint32_t u = 0; u < AHEAD; ++u) {
+			for (uint32_t u = 0; u < COMPOSITE_AHEAD; ++u) {
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
@@ -720,7 +658,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				}
 			}
 #pragma unroll
-			for (uint32_t u = 0; u < AHEAD; ++u) {
+			for (uint32_t u = 0; u < COMPOSITE_AHEAD; ++u) {
 				if (done || j0 + u >= actual) continue;
 				const __half2 rg = *reinterpret_cast<const __half2*>(&o2[u].x), bs = *reinterpret_cast<const __half2*>(&o2[u].y);
 				const float T = 1.0f - c.w;
@@ -934,9 +872,6 @@ static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_c
 // (texture-addresser bound) and MLP (matrix cores).  Every ray composites its own samples in
 // order, so the image does not depend on the split.
 static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard) {
-#ifdef NGP_DIAGNOSTICS
-	if (getenv("NGP_RENDER_DUMP")) return 1;  // the diagnostic dump covers one pipeline's pass 0
-#endif
 	uint32_t p = n >= (1u << 16) ? 2u : 1u;
 	if (t.render_pipelines) p = std::min<uint32_t>(t.render_pipelines, RenderScratch::MAX_PIPES);
 	return std::max(1u, std::min(p, div_up(h_shard, 8u)));  // every pipeline gets rows
@@ -946,10 +881,6 @@ static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard) 
 // read-back lag, ngp_tuning.render_lag, is at most HC_SLOTS passes), a copy-back slot, and the words the
 // kernels publish.
 constexpr uint32_t HC_SLOTS = 4, HC_COPYBACK = 16 * HC_SLOTS, HC_PUBLISHED = 128, HC_WORDS = HC_PUBLISHED + 16 * HC_SLOTS;
-
-// ngp_tuning.render_pass_order: 1 free-running pipelines, 2 encoder launches chained across them, 3 encoder +
-// MLP chained
-static uint32_t render_pass_order(const ngp_tuning& t) { return t.render_pass_order ? t.render_pass_order : 1u; }
 
 // passes a pipeline runs ahead of its counter read-backs (ngp_tuning.render_lag, 2 .. HC_SLOTS)
 static uint32_t render_lag(const ngp_tuning& t) {
@@ -968,7 +899,6 @@ struct PipeRun {
 	uint32_t pass = 0, steps_done = 0, n_alive_ub = 0, base_tag = 0;
 	bool marching = false;
 	float4* posdt = nullptr;
-	float4* stage = nullptr;
 	uint32_t* sray = nullptr;
 	uint4* shrows = nullptr;
 	Payload* P(int b) const { return reinterpret_cast<Payload*>(ps->payload[b].ptr); }
@@ -1052,10 +982,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.shard_count = std::max(a->shard_count, 1u);
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);
-	k.bitfield = m->gs.bitfield.ptr;
 	k.tiles_x = div_up(k.W, 8u);
-	rs.summary.reserve(OCC_SUMMARY_BYTES * NERF_CASCADES / 4);
-	k.summary = reinterpret_cast<const uint8_t*>(rs.summary.ptr);
 	const uint32_t H_shard = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	if (k.W * H_shard == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");
@@ -1082,20 +1009,14 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// per-ray sample budgets: headroom factor (default 1.0: measured 1 % faster than 1.5), < 0 = off
 	k.budget = !(tu.render_budget_scale < 0.0f);
 	k.budget_scale = tu.render_budget_scale > 0.0f ? tu.render_budget_scale : 1.0f;
-	const bool block_skipping = tu.render_block_skipping != 0;
-	// the fused encoding + network kernel where it applies (Normals needs the encodings for its backward)
-	const bool fused = tu.render_network == 1 && k.mode != NGP_RENDER_MODE_NORMALS && render_net_supported(m);
-	// slot compaction (ngp_tuning.render_slot_compaction: 1 on, 2 off; 0 the default: off -- 14.37 vs 13.96 ms per
-	// 1080p frame in a same-box A/B: the copy turn costs the march more than the encoder and MLP save)
-	const bool compact = tu.render_slot_compaction == 1;
+	// per-pass budgets capped by the lattice points left to the ray's exit (ngp_tuning.render_exit_cap: 1 on, 2 off)
+	k.exit_cap = tu.render_exit_cap != 2 ? 1 : 0;
 	// unfilled slots marked for the render MLP to skip (ngp_tuning.render_skip_unfilled: 1 on, 2 off; 0 the
 	// default); Normals runs the MLP backward over every slot, so it keeps real rows
 	const bool skip_unfilled = tu.render_skip_unfilled != 2 && k.mode != NGP_RENDER_MODE_NORMALS;
 	k.mark_unfilled = skip_unfilled ? 1 : 0;
 
 	if (!rs.fork) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.fork, hipEventDisableTiming));
-	for (uint32_t j = 0; j < n_pipes; ++j)
-		if (!rs.chain[j]) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.chain[j], hipEventDisableTiming));
 	for (uint32_t j = 1; j < n_pipes; ++j) {
 		if (rs.streams[j]) continue;
 		NGP_HIP_CHECK(hipStreamCreateWithFlags(&rs.streams[j], hipStreamNonBlocking));
@@ -1125,8 +1046,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH rows (pixel indices)
 		ps.coords.reserve(5 * pr.max_samples);
-		if (compact) ps.stage.reserve(4 * pr.max_samples);
-		if (!fused) ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
+		ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
 		if (!ps.host_counter.ptr) {
@@ -1143,7 +1063,6 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // the encoder reads 16-B position rows once per level
 		pr.sray = reinterpret_cast<uint32_t*>(ps.coords.ptr + 4 * pr.max_samples);
-		pr.stage = compact ? reinterpret_cast<float4*>(ps.stage.ptr) : nullptr;
 		pr.shrows = rs.shrows.ptr;
 		pr.base_tag = ps.pass_tag;
 		pr.n_alive_ub = pr.n;
@@ -1153,13 +1072,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	tm.begin(NGP_TIMER_RENDER_MARCH, s);
 	uint32_t* dbg = debug ? rs.pipe[0].counters.ptr + 8 : nullptr;
 	if (debug) NGP_HIP_CHECK(hipMemsetAsync(dbg, 0, 8 * sizeof(uint32_t), s));
-	if (!block_skipping) {
-		build_distance_fields(m, k.max_mip, s);
-		k.df = rs.df.ptr;
-	}
-	// the summary kernel also zeroes pipeline 0's counters
-	k_occupancy_summary<<<NERF_CASCADES * 32768 / 512, 512, 0, s>>>(k.bitfield, reinterpret_cast<uint8_t*>(rs.summary.ptr),
-	                                                                rs.pipe[0].counters.ptr);
+	build_distance_fields(m, k.max_mip, s);
+	k.df = rs.df.ptr;
+	NGP_HIP_CHECK(hipMemsetAsync(rs.pipe[0].counters.ptr, 0, 8 * sizeof(uint32_t), s));
 	// the encoder's table, and corner records of its dense levels (read by every pipeline)
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
@@ -1192,13 +1107,12 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			joiner.n = j + 1;
 		}
 	}
-	const size_t lds = k.df ? 0 : (size_t)(k.max_mip + 1) * OCC_SUMMARY_BYTES;
 	for (uint32_t j = 0; j < n_pipes; ++j) {
 		PipeRun& pr = pipes[j];
 		pr.k.df = k.df;
 		pr.k.dbg = dbg;
 		if (pr.n == 0) continue;
-		(k.lens_mode != LENS_PERSPECTIVE || k.dmap ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, lds, pr.s>>>(
+		(k.lens_mode != LENS_PERSPECTIVE || k.dmap ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, 0, pr.s>>>(
 		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, pr.ps->counters.ptr, rs.shrows.ptr);
 		pr.marching = true;
 	}
@@ -1220,25 +1134,6 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// 512 (256 measured 4.5 % slower)
 	const uint32_t comp_block = tu.render_composite_block ? tu.render_composite_block : 512u;
 	const uint32_t gen_block = tu.render_generate_block ? tu.render_generate_block : 512u;
-	// network launches chained across the pipelines (ngp_tuning.render_pass_order): each pipeline's
-	// encoder (2) or encoder + MLP (3) waits for the one enqueued before it, so the pipelines take
-	// turns on the encoder instead of running their passes in lockstep
-	const uint32_t order = n_pipes > 1 ? render_pass_order(tu) : 1u;
-	int chain_last = -1;
-	// the render encoder's persistent grid (ngp_tuning.render_encode_wgs_per_cu): chunks per level group such
-	// that the launch holds that many workgroups per CU (F = 2, four levels per thread: L/4 groups)
-	const uint32_t enc_chunk_cap = tu.render_encode_wgs_per_cu
-	                                   ? std::max(8u, tu.render_encode_wgs_per_cu * (uint32_t)cu_count() / std::max(1u, m->lt.n_levels / 4) / 8u * 8u)
-	                                   : 0u;
-	auto chain_wait = [&](PipeRun& pr) {
-		const int j = (int)pr.k.pipe_index;
-		if (order >= 2 && chain_last >= 0 && chain_last != j) NGP_HIP_CHECK(hipStreamWaitEvent(pr.s, rs.chain[chain_last], 0));
-	};
-	auto chain_mark = [&](PipeRun& pr) {
-		const int j = (int)pr.k.pipe_index;
-		NGP_HIP_CHECK(hipEventRecord(rs.chain[j], pr.s));
-		chain_last = j;
-	};
 	auto enqueue_pass = [&](PipeRun& pr) {
 		const hipStream_t ps = pr.s;
 		uint32_t* counters = pr.ps->counters.ptr;
@@ -1257,16 +1152,12 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		unsigned long long* host_prev = pass > 0 ? pr.pub_dev() + 8 * ((pass - 1) % HC_SLOTS) : nullptr;
 		const uint32_t tag_prev = pr.base_tag + pass;  // = tag of pass - 1
 		const uint32_t cap_p = pass >= 8 ? cap : std::min(cap, cap0 << pass);
-#define NGP_GEN(GG, CC) k_generate<GG, CC><<<gblocks, gen_block, lds, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, pr.stage, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev)
-		switch (G * 2 + (compact ? 1 : 0)) {
-			case 2: NGP_GEN(1, false); break;
-			case 3: NGP_GEN(1, true); break;
-			case 8: NGP_GEN(4, false); break;
-			case 9: NGP_GEN(4, true); break;
-			case 32: NGP_GEN(16, false); break;
-			case 33: NGP_GEN(16, true); break;
-			case 128: NGP_GEN(64, false); break;
-			default: NGP_GEN(64, true); break;
+#define NGP_GEN(GG) k_generate<GG><<<gblocks, gen_block, 0, ps>>>(pr.k, alive_in, pr.P(cur), pr.C(cur), pr.posdt, pr.sray, target, cap_p, alive_out, samples, steps_out, counters, host_prev, tag_prev)
+		switch (G) {
+			case 1: NGP_GEN(1); break;
+			case 4: NGP_GEN(4); break;
+			case 16: NGP_GEN(16); break;
+			default: NGP_GEN(64); break;
 		}
 #undef NGP_GEN
 		tm.end(NGP_TIMER_RENDER_MARCH, ps);
@@ -1274,69 +1165,31 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const uint64_t bound = std::min<uint64_t>((uint64_t)pr.n_alive_ub * cap_p, std::max(target, pr.n_alive_ub));
 		const uint32_t n_elements = next_multiple((uint32_t)std::max<uint64_t>(bound, 1), BATCH_SIZE_GRANULARITY);
 		tm.begin_kernel(NGP_TIMER_RENDER_ENCODE);
-#ifdef NGP_DIAGNOSTICS
-		static const char* dump = getenv("NGP_RENDER_DUMP");  // diagnostic builds only: pass-0 samples + alive payloads
-		if (dump && pass == 0) {
-			uint32_t c[8];
-			NGP_HIP_CHECK(hipMemcpyAsync(c, counters, sizeof(c), hipMemcpyDeviceToHost, ps));
-			NGP_HIP_CHECK(hipStreamSynchronize(ps));
-			std::vector<float> pd((size_t)c[4] * 4);
-			std::vector<Payload> pl(c[0]);
-			NGP_HIP_CHECK(hipMemcpy(pd.data(), pr.posdt, pd.size() * 4, hipMemcpyDeviceToHost));
-			NGP_HIP_CHECK(hipMemcpy(pl.data(), pr.P(cur), pl.size() * sizeof(Payload), hipMemcpyDeviceToHost));
-			FILE* f = fopen(dump, "wb");
-			if (f) {
-				fwrite(c, 4, 8, f);
-				fwrite(pd.data(), 4, pd.size(), f);
-				fwrite(pl.data(), sizeof(Payload), pl.size(), f);
-				fclose(f);
-			}
-		}
-#endif
-		chain_wait(pr);
-		if (fused) {
-			// one kernel: encoding + network (k_render_net), the features never leave the CU
-			launch_render_net(m, frags, lt_render, table, reinterpret_cast<const float*>(pr.posdt), n_elements, pr.ps->out.ptr, ps,
-			                  samples, reinterpret_cast<const __half*>(pr.shrows), pr.sray, sh_rows);
-			tm.end(NGP_TIMER_RENDER_ENCODE, ps);
-			if (order >= 2) chain_mark(pr);
-		} else {
-			launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
-			                    internal_layout(m, n_elements), ps, samples, 1, enc_chunk_cap);
-			tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
-			if (order == 2) chain_mark(pr);
-			tm.begin_kernel(NGP_TIMER_RENDER_MLP);
-			launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
-			                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows, skip_unfilled);
-			tm.end(NGP_TIMER_RENDER_MLP, ps);
-			if (order == 3) chain_mark(pr);
-		}
+		launch_hashgrid_fwd(lt_render, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, table, pr.ps->enc.ptr,
+		                    internal_layout(m, n_elements), ps, samples, 1);
+		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
+		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
+		launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
+		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows, skip_unfilled);
+		tm.end(NGP_TIMER_RENDER_MLP, ps);
 		if (pr.k.mode == NGP_RENDER_MODE_NORMALS) {
 			// Normals (NerfTracer::trace, testbed_nerf.cu:1715-1717, network->input_gradient): the gradient of
 			// the raw density w.r.t. the warped position of every sample -- the fused MLP backward from
-			// dL/dout = (0, 0, 0, 1) (weight gradients into scratch), then the grid's input gradient
+			// dL/dout = (0, 0, 0, 1) without weight gradients (the rgb rows are zero, so the direction does not
+			// enter), then the grid's input gradient
 			RenderPipeScratch& sc = *pr.ps;
 			sc.nrm_dloss.reserve(4 * (size_t)n_elements);
 			sc.nrm_denc.reserve((size_t)m->lt.n_levels * n_elements * m->lt.F);
 			sc.nrm.reserve(3 * (size_t)n_elements);
-			sc.nrm_grads.reserve(m->n_mlp_params);
 			k_density_unit_dloss<<<div_up(n_elements, 256u), 256, 0, ps>>>(samples, n_elements, sc.nrm_dloss.ptr);
-			launch_mlp_train(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), reinterpret_cast<const float*>(pr.posdt), 4,
-			                 n_elements, sc.nrm_dloss.ptr, nullptr, sc.nrm_grads.ptr, sc.nrm_denc.ptr, ps, samples);
+			launch_mlp_train(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, sc.nrm_dloss.ptr,
+			                 nullptr, nullptr, sc.nrm_denc.ptr, ps, samples);
 			launch_hashgrid_input_grad(m->lt, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, sc.nrm_denc.ptr,
 			                           EncLayout{n_elements, 0}, table, nullptr, sc.nrm.ptr, ps, samples);
 			pr.k.normals = sc.nrm.ptr;
 		}
 		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
-		// ngp_tuning.render_tail_rays (opt-in): passes with at most this many alive rays (and a cap of >= 16 samples
-		// per ray) composite with every sample of the pass prefetched; 0: never (2^16 measured 13.62 vs 13.56 ms
-		// per frame, 2^18 13.68: the tail's composites are not what its passes wait on)
-		const uint32_t tail_rays = tu.render_tail_rays;
-		if (pr.k.mode == NGP_RENDER_MODE_SHADE && pr.n_alive_ub <= tail_rays && cap_p >= 16)
-			k_composite<false, COMPOSITE_AHEAD_TAIL><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
-			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
-			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);
-		else if (pr.k.mode == NGP_RENDER_MODE_SHADE)
+		if (pr.k.mode == NGP_RENDER_MODE_SHADE)
 			k_composite<false><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
 			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
 			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);

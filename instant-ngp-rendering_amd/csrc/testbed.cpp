@@ -17,7 +17,9 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cerrno>
 #include <cstring>
+#include <unistd.h>
 #include <dirent.h>
 #include <fstream>
 #include <sstream>
@@ -182,8 +184,16 @@ Testbed::Testbed(ETestbedMode m) {
 	int device = 0;
 	if (const char* lr = std::getenv("LOCAL_RANK")) device = std::atoi(lr);
 	int n_dev = 0;
-	hk(hipGetDeviceCount(&n_dev), "hipGetDeviceCount");
-	if (n_dev <= 0) throw std::runtime_error("Testbed requires an AMD GPU (no HIP device found).");
+	const hipError_t de = hipGetDeviceCount(&n_dev);
+	if (de != hipSuccess || n_dev <= 0) {
+		// name what the HIP runtime saw: the device-visibility variables and whether the process may open
+		// the kernel driver's device nodes (a runtime that finds no GPU agent reports "no ROCm-capable device")
+		auto env = [](const char* k) { const char* v = std::getenv(k); return std::string(k) + "=" + (v ? v : "(unset)"); };
+		std::string msg = std::string("Testbed requires an AMD GPU: hipGetDeviceCount: ") + hipGetErrorString(de) + " (" +
+		                  env("HIP_VISIBLE_DEVICES") + ", " + env("ROCR_VISIBLE_DEVICES") + ", " + env("CUDA_VISIBLE_DEVICES") +
+		                  ", /dev/kfd " + (access("/dev/kfd", R_OK | W_OK) == 0 ? "accessible" : std::strerror(errno)) + ")";
+		throw std::runtime_error(msg);
+	}
 	device = device % n_dev;
 	hk(hipSetDevice(device), "hipSetDevice");
 	hipStream_t s;
@@ -956,8 +966,15 @@ void Testbed::build_model(const Json& cfg) {
 		ck(ngp_model_destroy(m_model));
 		m_model = nullptr;
 	}
-	ck(ngp_model_create(device, &c, seed, &m_model));
-	ck(ngp_model_set_tuning(m_model, &m_tuning));
+	// the tuning is applied before the model is published, so a failure leaves no model half set up
+	ngp_model* model = nullptr;
+	ck(ngp_model_create(device, &c, seed, &model));
+	if (ngp_model_set_tuning(model, &m_tuning) != NGP_OK) {
+		const std::string msg = ngp_last_error();
+		(void)ngp_model_destroy(model);
+		throw std::runtime_error(msg);
+	}
+	m_model = model;
 	m_net_cfg = c;
 }
 
@@ -965,7 +982,8 @@ void Testbed::build_model(const Json& cfg) {
 // Training
 // ---------------------------------------------------------------------------
 void Testbed::set_tuning(const ngp_tuning& t) {
-	if (m_model) ck(ngp_model_set_tuning(m_model, &t));  // validates
+	ck(ngp_tuning_validate(&t));  // also before a model exists: an invalid value never reaches build_model
+	if (m_model) ck(ngp_model_set_tuning(m_model, &t));
 	m_tuning = t;
 }
 
@@ -1195,25 +1213,30 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 				allreduce_dev(g, info.n_mlp_params, 0, false);
 				allreduce_dev(gg, info.n_grid_params, deterministic ? 3 : 1, false);
 			}
-			if (!a.full_forward) {
-				void* viol = nullptr;
-				ck(ngp_train_scratch(m_model, NGP_SCRATCH_VIOLATIONS, &viol, nullptr));
-				if (viol) allreduce_dev(viol, 1, 2, true);
-			}
+			// the violation word (early stops of the chunked forward, a rank's sample capacity) gates the
+			// optimizer; every rank takes the max over the ranks, so all of them skip or all of them step
+			void* viol = nullptr;
+			ck(ngp_train_scratch(m_model, NGP_SCRATCH_VIOLATIONS, &viol, nullptr));
+			if (viol) allreduce_dev(viol, 1, 2, true);
 			ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 		}
 		// NerfCounters::update_after_training (src/testbed_nerf.cu:2422-2446)
 		ck(ngp_train_read_stats(m_model, &st, m_stream));
-		if (!st.forward_early_stop_violations || a.full_forward) break;
-		// the chunked forward stopped a ray before a sample its loss needed: the step's update was
-		// skipped on the device; drop its gradients and run the step again with the full forward (its
-		// error-map / camera-gradient deposits of the first attempt stay -- such steps have not been seen)
-		forward_early_stop_violations += st.forward_early_stop_violations;
-		std::fprintf(stderr, "Nerf training: the chunked forward missed samples of %u rays; re-running the step with the full "
-		             "forward and keeping it from now on.\n", st.forward_early_stop_violations);
-		train_full_forward = true;
+		const bool early_stop = st.forward_early_stop_violations && !a.full_forward;
+		if (!early_stop && !st.sample_capacity_overflow) break;
+		if (attempt >= 4) throw std::runtime_error("Nerf training: the step could not be completed after 4 retries");
+		// the step's update and its error-map, exposure, camera, distortion and sharpness deposits were skipped
+		// on the device (every rank sees the violations of all ranks); drop its gradients and run it again --
+		// with the full forward when the chunked forward stopped a ray before a sample its loss needed, with
+		// buffers grown to the need when a rank's share of the samples did not fit
 		ck(ngp_train_discard(m_model, m_stream));
-		a.full_forward = 1;
+		if (early_stop) {
+			forward_early_stop_violations += st.forward_early_stop_violations;
+			std::fprintf(stderr, "Nerf training: the chunked forward missed samples of %u rays; re-running the step with the full "
+			             "forward and keeping it from now on.\n", st.forward_early_stop_violations);
+			train_full_forward = true;
+			a.full_forward = 1;
+		}
 	}
 	++training_step;
 	// CDFs from the error map, every n_steps_between_error_map_updates (x1.5 each time)

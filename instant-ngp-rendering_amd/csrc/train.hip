@@ -515,6 +515,7 @@ struct ChunkArgs {
 	uint32_t eval_offset;      // evaluation row of the next chunk's first claim
 	int first, last;
 	int density_act;
+	float stop_T;              // transmittance below which a ray stops (TRAIN_CHUNK_STOP_T; ngp_tuning.debug bit 2: 0.999)
 };
 
 // One chunk step: composite the previous chunk's outputs (transmittance only) and scatter
@@ -576,7 +577,7 @@ __global__ void __launch_bounds__(1024) k_train_chunk(ChunkArgs a) {
 				}
 				const float prev = __shfl_up(incl, 1, G);
 				const float Tb = r == 0 ? T : T * prev;  // transmittance before sample jj
-				const unsigned long long below = __ballot(jj < end && Tb < TRAIN_CHUNK_STOP_T) & gmask;
+				const unsigned long long below = __ballot(jj < end && Tb < a.stop_T) & gmask;
 				if (below) {  // the loss kernel stops at or before the first such sample
 					const uint32_t k = (uint32_t)(__ffsll((long long)below) - 1) - g0;
 					T = __shfl(Tb, g0 + k, 64);
@@ -593,7 +594,7 @@ __global__ void __launch_bounds__(1024) k_train_chunk(ChunkArgs a) {
 		const uint32_t scatter = j - a.prev_lo;
 		ev = j;
 		// stopped inside the chunk, at its end with T already below the margin, or out of samples
-		if (j < end || T < TRAIN_CHUNK_STOP_T || end == n) alive = false;
+		if (j < end || T < a.stop_T || end == n) alive = false;
 		// the chunk's outputs back to the sampler layout (rows [prev_lo, j))
 		for (uint32_t k = r; k < scatter; k += G) {
 			const uint32_t src = base + a.prev_lo + k, e = ebase + k;
@@ -685,6 +686,7 @@ struct LossArgs {
 	const float* mean_density;
 	const uint32_t* ray_eval;  // [R] samples the chunked forward evaluated (null: all of them)
 	uint32_t* violations;      // rays whose composite reached past the evaluated samples (must stay 0)
+	const uint32_t* viol_gate; // the step's violations over all ranks: non-zero = no deposits (the step re-runs)
 	int store_uv_pdf;          // camera gradients: ray_aux[i].w = the pixel's pdf
 	float depth_lambda;        // depth supervision (0: off)
 	int depth_loss_type;
@@ -735,7 +737,8 @@ __device__ __forceinline__ LossSample loss_sample(const LossArgs& a, size_t src)
 }
 
 // decay_sharpness_grid_nerf (src/testbed_nerf.cu:278-282)
-__global__ void __launch_bounds__(256) k_scale_floats(float* __restrict__ x, size_t n, float f) {
+__global__ void __launch_bounds__(256) k_scale_floats(float* __restrict__ x, size_t n, float f, const uint32_t* __restrict__ gate) {
+	if (gate && *gate) return;
 	const size_t i = (size_t)blockIdx.x * 256u + threadIdx.x;
 	if (i < n) x[i] *= f;
 }
@@ -932,14 +935,16 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		if (lane == 0) a.loss_out[i] = 0.0f;
 		return;
 	}
-	if (a.exposure_grad && lane == 0) {
+	// a step the chunked forward got wrong makes no deposits: it is discarded and run again (Testbed)
+	const bool deposit = !(a.viol_gate && *a.viol_gate);
+	if (a.exposure_grad && lane == 0 && deposit) {
 		const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
 		const float4 g = a.ray_aux[i];
 		atomicAdd(&a.exposure_grad[3 * (size_t)img + 0], g.x);
 		atomicAdd(&a.exposure_grad[3 * (size_t)img + 1], g.y);
 		atomicAdd(&a.exposure_grad[3 * (size_t)img + 2], g.z);
 	}
-	if (a.error_map && lane == 0) {
+	if (a.error_map && lane == 0 && deposit) {
 		// bilinear deposit of the ray's mean loss (src/testbed_nerf.cu:1028-1054; rays without
 		// compacted samples returned before it); the corner clamp uses the image
 		// resolution, as the reference does
@@ -1092,6 +1097,7 @@ struct CamGradArgs {
 	float* cam_pos_gradient;     // [n_images][3] (null: off)
 	float* cam_rot_gradient;     // [n_images][3]
 	const ngp_image* images;     // the images' current transforms (distortion gradient)
+	const uint32_t* viol_gate;   // non-zero: the step is discarded and re-run -- no deposits
 	float* dgrad;                // distortion map gradient / weight [dry][drx][2] (null: off)
 	float* dgrad_w;
 	uint32_t drx, dry;
@@ -1120,7 +1126,7 @@ __device__ __forceinline__ void deposit_image_gradient(float gx, float gy, float
 
 __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
-	if (i >= a.n_rays) return;
+	if (i >= a.n_rays || (a.viol_gate && *a.viol_gate)) return;
 	const uint32_t cn = a.compacted[2 * i], cbase = a.compacted[2 * i + 1];
 	if (cn == 0) return;
 	const float* rs = a.ray_state + 8 * (size_t)i;
@@ -1220,13 +1226,18 @@ __global__ void k_clamp_count(const uint32_t* __restrict__ in, uint32_t cap, con
 // Data parallelism (ngp_train_args.world_size > 1): each rank writes its total into its slot of
 // [world] words (the others zero), the caller's all-reduce sums them, and every rank derives the
 // same global prefix -- so caps and rollover follow the global ray order of one process.
-__global__ void k_dp_publish(const uint32_t* __restrict__ total, int32_t* __restrict__ slots, uint32_t world, uint32_t rank) {
+// extra (optional): one more word summed over the ranks, in slots[world] (the chunked forward's violations)
+__global__ void k_dp_publish(const uint32_t* __restrict__ total, int32_t* __restrict__ slots, uint32_t world, uint32_t rank,
+                             const uint32_t* __restrict__ extra) {
 	for (uint32_t q = threadIdx.x; q < world; q += blockDim.x) slots[q] = q == rank ? (int32_t)*total : 0;
+	if (extra && threadIdx.x == 0) slots[world] = (int32_t)*extra;
 }
 // DpCaps: [0] this rank's first global index, [1] min(global total, cap), [2] this rank's share of
-// the cap (cap - base, 0 once the ranks before it filled it)
+// the cap (cap - base, 0 once the ranks before it filled it).  local_cap: the rank's buffer capacity;
+// a share it cannot hold (min(own total, share) > local_cap) flags the step (VIOL_CAPACITY in *viol,
+// the need in *need): the Testbed discards it and runs it again with buffers grown to the need.
 __global__ void k_dp_caps(const int32_t* __restrict__ slots, uint32_t world, uint32_t rank, uint32_t cap,
-                          uint32_t* __restrict__ out) {
+                          uint32_t* __restrict__ out, uint32_t local_cap, uint32_t* __restrict__ viol, uint32_t* __restrict__ need) {
 	if (threadIdx.x || blockIdx.x) return;
 	uint64_t base = 0, total = 0;
 	for (uint32_t q = 0; q < world; ++q) {
@@ -1237,6 +1248,14 @@ __global__ void k_dp_caps(const int32_t* __restrict__ slots, uint32_t world, uin
 	out[0] = (uint32_t)min<uint64_t>(base, 0xffffffffull);
 	out[1] = (uint32_t)min<uint64_t>(total, cap);
 	out[2] = base >= cap ? 0u : (uint32_t)(cap - base);
+	if (viol) {
+		const uint32_t want = min((uint32_t)slots[rank], out[2]);
+		if (want > local_cap) {
+			*viol |= VIOL_CAPACITY;
+			*need = want;
+			out[2] = local_cap;  // stay inside the buffers; the step is discarded
+		}
+	}
 }
 
 // Sum of per-ray losses (deterministic two-level reduction).
@@ -1570,8 +1589,24 @@ void run_error_map_cdf(const float* error_map, uint32_t n_images, uint32_t rx, u
 
 void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	TrainScratch& ts = m->ts;
-	const uint32_t R = t->n_rays, B = t->target_batch_size, MS = t->max_samples;
+	const uint32_t R = t->n_rays, B = t->target_batch_size, MS_global = t->max_samples;
 	const uint32_t L = m->lt.n_levels, F = m->lt.F;
+	// data parallelism: caps and rollover over the global ray order (ngp_train_args.world_size)
+	const uint32_t world = t->world_size > 1 && t->allreduce_i32 ? t->world_size : 1u;
+	if (world > 1 && t->rank >= world) throw std::invalid_argument("rank must be < world_size");
+	// the sample buffers of this rank: the global cap in one process; with data parallelism about the rank's
+	// share (twice the even split, or the need of a step that did not fit -- k_dp_caps flags it), so per-rank
+	// memory does not grow with the world size
+	// (ngp_tuning.debug bit 3: an eighth of the even split, forcing the overflow and the retry)
+	const uint32_t even = (m->tuning.debug & 8u) ? MS_global / world / 8u : 2u * (MS_global / world);
+	const uint32_t MS = world > 1 ? std::min(MS_global, std::max(next_multiple(even, 4096u), ts.rank_cap_hint)) : MS_global;
+	{
+		// 32-bit byte offsets: the MLP's raw encoding buffers and the encoder's planes
+		const uint64_t rows = (uint64_t)MS + 48ull * R;  // the chunked forward's evaluation rows (at most)
+		if ((uint64_t)m->enc_pad * 2 * rows >= (1ull << 32) || 32ull * rows >= (1ull << 32))
+			throw std::invalid_argument("training: max_samples too large for one rank's 32-bit sample buffers "
+			                            "(lower the batch per rank)");
+	}
 	ts.ray_numsteps.reserve(2 * (size_t)R);
 	ts.ray_compacted.reserve(2 * (size_t)R);
 	ts.ray_state.reserve(8 * (size_t)R);
@@ -1598,21 +1633,21 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.last_max_samples = MS;
 	ts.gated_optimizer_ran = false;
 
-	// data parallelism: caps and rollover over the global ray order (ngp_train_args.world_size)
-	const uint32_t world = t->world_size > 1 && t->allreduce_i32 ? t->world_size : 1u;
-	if (world > 1 && t->rank >= world) throw std::invalid_argument("rank must be < world_size");
 	uint32_t* dp_samples = nullptr;  // DpCaps of the sampler / the compaction (device)
 	uint32_t* dp_compact = nullptr;
-	auto dp_exchange = [&](const uint32_t* total, uint32_t* caps, int32_t* slots, uint32_t cap) {
-		k_dp_publish<<<1, 64, 0, s>>>(total, slots, world, t->rank);
+	auto dp_exchange = [&](const uint32_t* total, uint32_t* caps, int32_t* slots, uint32_t cap, const uint32_t* extra,
+	                       uint32_t local_cap) {
+		k_dp_publish<<<1, 64, 0, s>>>(total, slots, world, t->rank, extra);
 		NGP_HIP_CHECK(hipGetLastError());
-		if (t->allreduce_i32(t->allreduce_user, slots, world, s) != NGP_OK)
+		if (t->allreduce_i32(t->allreduce_user, slots, world + (extra ? 1u : 0u), s) != NGP_OK)
 			throw std::runtime_error("data-parallel training: the all-reduce of the per-rank totals failed");
-		k_dp_caps<<<1, 64, 0, s>>>(slots, world, t->rank, cap, caps);
+		const bool sized = local_cap < cap;
+		k_dp_caps<<<1, 64, 0, s>>>(slots, world, t->rank, cap, caps, local_cap, sized ? ts.counters.ptr + 9 : nullptr,
+		                           sized ? ts.counters.ptr + 10 : nullptr);
 		NGP_HIP_CHECK(hipGetLastError());
 	};
 	if (world > 1) {
-		ts.dp.reserve(8 + 2 * (size_t)world);
+		ts.dp.reserve(8 + 2 * (size_t)world + 2);
 		dp_samples = ts.dp.ptr;
 		dp_compact = ts.dp.ptr + 4;
 	}
@@ -1644,7 +1679,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.max_level_rand = t->max_level_rand_training != 0;
 	// aabb_scale 1: cross empty space through the octant distance fields (shared with the renderer,
 	// rebuilt when the bitfield changed); the chain walk otherwise
-	if (t->max_cascade == 0 && m->tuning.train_chain_walk == 0) {
+	if (t->max_cascade == 0) {
 		build_distance_fields(m, 0, s);
 		sa.df = m->rs.df.ptr;
 	}
@@ -1668,7 +1703,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	else k_sample_count<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
 	// the global sample cap (src/testbed_nerf.cu:779-781 drops rays past max_samples) over all ranks
-	if (world > 1) dp_exchange(ts.counters.ptr + 0, dp_samples, reinterpret_cast<int32_t*>(ts.dp.ptr + 8), MS);
+	if (world > 1) dp_exchange(ts.counters.ptr + 0, dp_samples, reinterpret_cast<int32_t*>(ts.dp.ptr + 8), MS_global, nullptr, MS);
 	if (general) k_sample_write<true><<<div_up(R, 4), 256, 0, s>>>(sa);
 	else k_sample_write<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	NGP_HIP_CHECK(hipGetLastError());
@@ -1722,6 +1757,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		c.ray_eval = ts.ray_eval.ptr;
 		c.ray_ebase = ts.ray_ebase.ptr;
 		c.density_act = m->cfg.density_activation;
+		c.stop_T = (m->tuning.debug & 4u) ? 0.999f : TRAIN_CHUNK_STOP_T;
 		for (uint32_t p = 0; p <= TRAIN_CHUNKS; ++p) {
 			c.first = p == 0;
 			c.last = p == TRAIN_CHUNKS;
@@ -1815,7 +1851,6 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		// train_nerf (src/testbed_nerf.cu:2453-2464): clear at step 0, else decay by 0.95
 		const size_t n_cells = (size_t)NERF_GRID_N_CELLS * NERF_CASCADES;
 		if (t->sharpness_grid_clear) NGP_HIP_CHECK(hipMemsetAsync(t->sharpness_grid, 0, n_cells * sizeof(float), s));
-		else k_scale_floats<<<div_up(n_cells, 256), 256, 0, s>>>(t->sharpness_grid, n_cells, 0.95f);
 		la.sharp_data = t->sharpness_data;
 		la.sharp_rx = t->sharpness_res[0];
 		la.sharp_ry = t->sharpness_res[1];
@@ -1832,11 +1867,18 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
 	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
-	// the global compaction cap (src/testbed_nerf.cu:997-1003) over all ranks
+	// the global compaction cap (src/testbed_nerf.cu:997-1003) over all ranks, and the chunked forward's
+	// violations summed over the ranks: every rank skips the step's deposits when any rank saw one
+	la.viol_gate = la.violations;
 	if (world > 1) {
-		dp_exchange(ts.counters.ptr + 1, dp_compact, reinterpret_cast<int32_t*>(ts.dp.ptr + 8 + world), B);
+		int32_t* slots = reinterpret_cast<int32_t*>(ts.dp.ptr + 8 + world);
+		dp_exchange(ts.counters.ptr + 1, dp_compact, slots, B, la.violations, B);
 		la.max_compacted_dev = dp_compact + 2;
+		la.viol_gate = reinterpret_cast<const uint32_t*>(slots + world);
 	}
+	if (la.sharp_grid && !t->sharpness_grid_clear)  // train_nerf's decay by 0.95 (src/testbed_nerf.cu:2453-2464)
+		k_scale_floats<<<div_up((size_t)NERF_GRID_N_CELLS * NERF_CASCADES, 256), 256, 0, s>>>(
+		    la.sharp_grid, (size_t)NERF_GRID_N_CELLS * NERF_CASCADES, 0.95f, la.viol_gate);
 	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
 	NGP_HIP_CHECK(hipGetLastError());
 	const bool train_debug = (m->tuning.debug & 2u) != 0;
@@ -1915,6 +1957,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		ca.cam_rot_gradient = t->cam_rot_gradient;
 		if (!(t->cam_pos_gradient && t->cam_rot_gradient)) ca.cam_pos_gradient = ca.cam_rot_gradient = nullptr;
 		ca.images = t->images;
+		ca.viol_gate = la.viol_gate;
 		if (dist_grad) {
 			ca.dgrad = t->distortion_gradient;
 			ca.dgrad_w = t->distortion_gradient_weight;

@@ -76,7 +76,7 @@ class TrainStats(C.Structure):
     _fields_ = [
         ("n_rays", C.c_uint32), ("n_rays_with_samples", C.c_uint32),
         ("measured_batch_size_before_compaction", C.c_uint32), ("measured_batch_size", C.c_uint32),
-        ("loss", C.c_float), ("forward_early_stop_violations", C.c_uint32),
+        ("loss", C.c_float), ("forward_early_stop_violations", C.c_uint32), ("sample_capacity_overflow", C.c_uint32),
     ]
 
 
@@ -111,18 +111,10 @@ class Tuning(C.Structure):
     _fields_ = [
         ("render_pipelines", C.c_uint32), ("render_pass_samples", C.c_uint32), ("render_lanes", C.c_uint32),
         ("render_first_steps", C.c_uint32), ("render_max_steps", C.c_uint32), ("render_lag", C.c_uint32),
-        ("render_budget_scale", C.c_float), ("render_block_skipping", C.c_uint32),
-        ("render_composite_block", C.c_uint32), ("render_generate_block", C.c_uint32),
+        ("render_budget_scale", C.c_float), ("render_composite_block", C.c_uint32), ("render_generate_block", C.c_uint32),
         ("encode_dense_records", C.c_uint32), ("mlp_workgroups_per_cu", C.c_uint32), ("debug", C.c_uint32),
-        ("encode_levels_per_thread", C.c_uint32), ("encode_streaming", C.c_uint32),
-        ("render_network", C.c_uint32), ("render_net_workgroups_per_cu", C.c_uint32),
-        ("train_chain_walk", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
-        ("encode_xcd_regions", C.c_uint32), ("render_pass_order", C.c_uint32),
-        ("render_encode_wgs_per_cu", C.c_uint32),
-        ("mlp_train_schedule", C.c_uint32),
-        ("render_slot_compaction", C.c_uint32),
-        ("render_skip_unfilled", C.c_uint32),
-        ("render_tail_rays", C.c_uint32),
+        ("encode_streaming", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
+        ("encode_xcd_regions", C.c_uint32), ("render_skip_unfilled", C.c_uint32), ("render_exit_cap", C.c_uint32),
     ]
 
 
@@ -142,6 +134,7 @@ EXPORTS = {
     "ngp_model_create": (C.c_int, [C.c_int, C.POINTER(NetworkConfig), C.c_uint64, C.POINTER(C.c_void_p)]),
     "ngp_model_destroy": (C.c_int, [C.c_void_p]),
     "ngp_model_set_tuning": (C.c_int, [C.c_void_p, C.POINTER(Tuning)]),
+    "ngp_tuning_validate": (C.c_int, [C.POINTER(Tuning)]),
     "ngp_model_get_tuning": (C.c_int, [C.c_void_p, C.POINTER(Tuning)]),
     "ngp_model_get_info": (C.c_int, [C.c_void_p, C.POINTER(ModelInfo)]),
     "ngp_model_buffer": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),

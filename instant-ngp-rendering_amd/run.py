@@ -63,12 +63,27 @@ def write_image(path, img):
             f.write(struct.pack("ii", h, w))
             f.write(img.astype(np.float16).tobytes())
         return
-    import synthetic
-
     rgb, a = img[..., :3], img[..., 3:4]
     straight = np.divide(rgb, a, out=np.zeros_like(rgb), where=a != 0)
     out = np.concatenate([metrics.linear_to_srgb(np.clip(straight, 0, None)), a], axis=-1)
-    synthetic.write_png(path, (np.clip(out, 0, 1) * 255 + 0.5).astype(np.uint8))
+    write_png(path, (np.clip(out, 0, 1) * 255 + 0.5).astype(np.uint8))
+
+
+def write_png(path, rgba):
+    """RGBA8 [H][W][4] -> PNG (zlib, filter 0)."""
+    import zlib
+
+    h, w, _ = rgba.shape
+    raw = b"".join(b"\x00" + rgba[y].tobytes() for y in range(h))
+
+    def chunk(t, body):
+        return struct.pack(">I", len(body)) + t + body + struct.pack(">I", zlib.crc32(t + body) & 0xFFFFFFFF)
+
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n")
+        f.write(chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 6, 0, 0, 0)))
+        f.write(chunk(b"IDAT", zlib.compress(raw, 6)))
+        f.write(chunk(b"IEND", b""))
 
 
 def evaluate(testbed, test_transforms, spp=8, log=print):

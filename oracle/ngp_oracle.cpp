@@ -314,30 +314,12 @@ static bool occupied(V3 p, const uint8_t* bits, uint32_t mip) {
 	if (i == 0xFFFFFFFFu) return false;
 	return bits[i / 8 + CELLS / 8 * mip] & (1u << (i % 8));
 }
-// Occupancy summary per mip (ngp_math.h OCC_SUMMARY_*): level A 32768 bits (4^3 blocks,
-// cell >> 6), level B 4096 bits (8^3 blocks, cell >> 9), level C 64 bits (32^3, cell >> 15).
-static const uint32_t SUM_A = 0, SUM_B = 4096, SUM_C = 4096 + 512, SUMMARY_BYTES = 4096 + 512 + 8;
-static std::vector<uint8_t> occ_summary(const uint8_t* bits) {
-	std::vector<uint8_t> sm((size_t)SUMMARY_BYTES * CASCADES, 0);
-	for (uint32_t mip = 0; mip < CASCADES; ++mip)
-		for (uint32_t w = 0; w < 32768; ++w) {
-			bool any = false;
-			for (uint32_t k = 0; k < 8; ++k) any |= bits[(size_t)CELLS / 8 * mip + w * 8 + k] != 0;
-			if (!any) continue;
-			uint8_t* s = &sm[(size_t)SUMMARY_BYTES * mip];
-			s[SUM_A + (w >> 3)] |= (uint8_t)(1u << (w & 7));
-			s[SUM_B + (w >> 6)] |= (uint8_t)(1u << ((w >> 3) & 7));
-			s[SUM_C + (w >> 12)] |= (uint8_t)(1u << ((w >> 9) & 7));
-		}
-	return sm;
-}
-static bool sum_bit(const uint8_t* sm, uint32_t base, uint32_t b) { return (sm[base + (b >> 3)] >> (b & 7u)) & 1u; }
-
-// First occupied lattice point at or after *n (render march); an empty cell is jumped over
-// only when the lattice point before the landing point is still inside it.
+// First occupied lattice point at or after *n (render march, if_unoccupied_advance_to_next_occupied_voxel
+// nerf_device.cuh:462-494 on the lattice): the cell at clamp(mip_from_pos, 0, maxm); an empty one is left
+// past its far face at the coarsest empty mip (the reference's climb), the jump taken only when the
+// lattice point before the landing point is still in the skipped cell (or already outside the box).
 template <class B>
-static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, const uint8_t* bits,
-                          const uint8_t* summary, uint32_t maxm, const B& b) {
+static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, const uint8_t* bits, uint32_t maxm, const B& b) {
 	float n = *n_io;
 	while (true) {
 		const float t = lat_from(st, n);
@@ -346,24 +328,12 @@ static bool next_occupied(float* n_io, const Stepping& st, V3 o, V3 d, V3 idir, 
 		uint32_t mip = std::min(mip_pos(pos), maxm);
 		if (occupied(pos, bits, mip)) { *n_io = n; return true; }
 		while (mip < maxm && !occupied(pos, bits, mip + 1)) ++mip;
-		// largest empty aligned Morton block around pos at `mip`: 1, 4^3, 8^3 or 32^3 cells
 		const uint32_t cell = grid_idx(pos, mip);
-		uint32_t shift = 0;
-		if (cell != 0xFFFFFFFFu) {
-			const uint8_t* sm = summary + (size_t)SUMMARY_BYTES * mip;
-			if (!sum_bit(sm, SUM_A, cell >> 6)) {
-				shift = 6;
-				if (!sum_bit(sm, SUM_B, cell >> 9)) {
-					shift = 9;
-					if (!sum_bit(sm, SUM_C, cell >> 15)) shift = 15;
-				}
-			}
-		}
-		const float n_far = lat_to(st, t + dist_next_cell(pos, d, idir, mip + shift / 3u));
+		const float n_far = lat_to(st, t + dist_next_cell(pos, d, idir, mip));
 		float nn = n + std::ceil(std::max(n_far - n, 0.5f));
 		if (nn - n > 1.0f) {
 			const V3 last = o + d * lat_from(st, nn - 1.0f);
-			if (b.contains(last) && (grid_idx(last, mip) >> shift) != (cell >> shift)) nn = n + 1.0f;
+			if (b.contains(last) && grid_idx(last, mip) != cell) nn = n + 1.0f;
 		}
 		n = nn;
 	}
@@ -1140,6 +1110,68 @@ static float ref_advance_to_next_voxel(float t, float cone, V3 pos, V3 dir, V3 i
 	return ref_from_stepping_space(ts + std::ceil(std::fmax(tt - ts, 0.5f)), cone);
 }
 
+// if_unoccupied_advance_to_next_occupied_voxel<MIP_FROM_DT = false> (nerf_device.cuh:462-494), the
+// renderer's form, literally: the cell at clamp(mip_from_pos(pos), min_mip, max_mip); an empty cell climbs to
+// the coarsest empty mip and advance_to_next_voxel jumps the chained t past its far face.
+// Distance (in cells of that mip) from pos to the nearest face of the cascade-mip cell grid.
+static float face_distance(V3 pos, uint32_t mip) {
+	const float res = std::scalbn((float)GRID, -(int)mip);
+	float best = 1.0f;
+	for (float c : {pos.x, pos.y, pos.z}) {
+		const float p = (c - 0.5f) * res;
+		best = std::min(best, std::fabs(p - std::round(p)));
+	}
+	return best;
+}
+// trace (tests): every point the march visits -- its stepping-space position, the face distance at the mip
+// it was decided at (the climbed mip for an empty one) and whether it is occupied
+struct MarchTrace {
+	std::vector<float> n, face;
+	std::vector<uint8_t> occ;
+};
+static float ref_if_unoccupied_advance(float t, float cone, V3 o, V3 d, V3 idir, const uint8_t* bits, uint32_t min_mip,
+                                       uint32_t max_mip, const RBox& box, MarchTrace* tr = nullptr) {
+	while (true) {
+		const V3 pos = o + d * t;
+		if (t >= MAXD || !box.contains(pos)) return MAXD;
+		uint32_t mip = std::min(std::max(mip_pos(pos), min_mip), max_mip);
+		if (!bits || occupied(pos, bits, mip)) {
+			if (tr) { tr->n.push_back(ref_to_stepping_space(t, cone)); tr->face.push_back(face_distance(pos, mip)); tr->occ.push_back(1); }
+			return t;
+		}
+		while (mip < max_mip && !occupied(pos, bits, mip + 1)) ++mip;
+		if (tr) { tr->n.push_back(ref_to_stepping_space(t, cone)); tr->face.push_back(face_distance(pos, mip)); tr->occ.push_back(0); }
+		t = ref_advance_to_next_voxel(t, cone, pos, d, idir, mip);
+	}
+}
+
+// One ray of NerfTracer::trace, literally: advance_pos_nerf (src/testbed_nerf.cu:333-362) from the
+// payload's t = max(t_entry, 0) + 1e-6 (:1465-1475), then generate_next_nerf_network_inputs passes
+// (:421-469) of n_steps samples each, t += dt chained through payload.t across passes.  visit(t, dt) per
+// sample until it returns false (the composite's stop) or the ray leaves the box; returns the samples.
+template <class Visit>
+static uint32_t ref_render_ray(float t_start, float jitter, float cone, V3 o, V3 d, const uint8_t* bits, uint32_t max_mip,
+                               const RBox& box, uint32_t n_steps, uint32_t cap, Visit visit, MarchTrace* tr = nullptr) {
+	const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	// advance_pos_nerf
+	float t = ref_advance_n_steps(t_start, cone, jitter);
+	t = ref_if_unoccupied_advance(t, cone, o, d, idir, bits, 0, max_mip, box, tr);
+	if (t >= MAXD) return 0;
+	uint32_t count = 0;
+	for (uint32_t pass = 0; count < cap; ++pass) {
+		// generate_next_nerf_network_inputs: payload.t -> n_steps samples -> payload.t
+		for (uint32_t j = 0; j < n_steps; ++j) {
+			t = ref_if_unoccupied_advance(t, cone, o, d, idir, bits, 0, max_mip, box, tr);
+			if (t >= MAXD) return count;
+			const float dt = ref_calc_dt(t, cone);
+			++count;
+			if (!visit(t, dt) || count >= cap) return count;
+			t += dt;
+		}
+	}
+	return count;
+}
+
 // Data parallelism (ngp_train_args.world_size): every rank learns all ranks' totals
 // through the caller's all-reduce (sum of [world] slots, its own slot set) and caps its share of
 // the global order: out = {first global index of this rank, min(global total, cap)}; returns the
@@ -1620,6 +1652,9 @@ static void grid_finish(Model& M, const ngp_grid_args& a) {
 }
 
 // ---- tracer (render_nerf, NerfTracer::trace; per ray, chunking-invariant) ---------------------
+// 0: the lattice march (the HIP path's formulation, exact per sample); 1: the reference's literal
+// float-chained march (ref_render_ray) -- oref_set_render_literal
+static int g_render_literal = 0;
 // square2disk_shirley (random_val.cuh:112-128)
 static void disk_shirley(float a, float b, float* x, float* y) {
 	const float PI = 3.14159265358979323846f;
@@ -1647,6 +1682,44 @@ static V3 density_gradient(const Model& M, const uint16_t* P, const float* coord
 	return v(g[0], g[1], g[2]);
 }
 
+// uv_to_ray + init_rays_with_payload_kernel_nerf's ray (src/testbed_nerf.cu:1408-1441, common_device.cuh:441-459)
+// of pixel (x, y): lens, learned distortion, the pixel's (rolling-shutter) camera, depth of field, near
+// distance; the direction is not normalised.  false: the lens has no ray for the pixel.
+static bool pixel_camera_ray(const ngp_render_args& a, const Cam& cam, uint32_t x, uint32_t y, float ox, float oy, float aperture,
+                             V3* o_out, V3* d_out) {
+	const uint32_t idx = x + a.width * y;
+	const float u = ((float)x + ox) / (float)a.width, vv = ((float)y + oy) / (float)a.height;
+	V3 d;
+	if (!lens_dir(u, vv, (float)a.width, (float)a.height, a.focal_length[0], a.focal_length[1], a.screen_center[0],
+	              a.screen_center[1], a.lens_mode, a.lens_params, &d))
+		return false;
+	if (a.distortion_map && a.distortion_res[0] && a.distortion_res[1]) {
+		float ddx, ddy;
+		distortion_lerp(a.distortion_map, a.distortion_res[0], a.distortion_res[1], u, vv, &ddx, &ddy);
+		d.x += ddx;
+		d.y += ddy;
+	}
+	// the pixel's camera (src/testbed_nerf.cu:1416)
+	const Cam pc = rs_on(a.rolling_shutter)
+	                   ? slerp_cam(cam, cam_of(a.camera_end), a.rolling_shutter[0] + a.rolling_shutter[1] * u + a.rolling_shutter[2] * vv +
+	                                                              a.rolling_shutter[3] * ldval(a.sample_index, idx * 72239731u, 0))
+	                   : cam;
+	d = rot(pc, d);
+	V3 o = pc.c[3];
+	if (aperture != 0.0f) {  // depth of field (uv_to_ray, common_device.cuh:450-456)
+		const V3 lookat = o + d * a.focus_z;
+		const uint32_t px = (uint32_t)(int)(u * (float)a.width), py = (uint32_t)(int)(vv * (float)a.height);
+		const uint32_t seed = px * 19349663u + py * 96925573u;
+		float dx, dy;
+		disk_shirley(ldval(a.sample_index, seed, 0) * 2.0f - 1.0f, ldval(a.sample_index, seed, 1) * 2.0f - 1.0f, &dx, &dy);
+		o = o + pc.c[0] * (aperture * dx) + pc.c[1] * (aperture * dy);
+		d = (lookat - o) * (1.0f / a.focus_z);
+	}
+	*o_out = o + d * a.near_distance;
+	*d_out = d;
+	return true;
+}
+
 // render_nerf (src/testbed_nerf.cu:1827-1987): per pixel, the NerfTracer march and composite of every
 // render mode but Distortion / EncodingVis, then shade_kernel_nerf; Slice evaluates one point per pixel.
 static void render(const Model& M, const ngp_render_args& a, float* frame, float* depthbuf) {
@@ -1656,7 +1729,6 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 	const Cam cam = cam_of(a.camera);
 	const uint16_t* P = a.use_inference_params ? M.inf16.data() : M.p16.data();
 	const Stepping stp = make_stepping(a.cone_angle_constant);
-	const std::vector<uint8_t> summary = occ_summary(M.bits.data());
 	const int ract = M.cfg.rgb_activation, dact = M.cfg.density_activation;
 	const int mode = a.render_mode;
 	const float aperture = mode == NGP_RENDER_MODE_SLICE ? 0.0f : a.aperture_size;
@@ -1675,34 +1747,8 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			float* fb = frame + 4 * (size_t)idx;
 			fb[0] = fb[1] = fb[2] = fb[3] = 0.0f;
 			depthbuf[idx] = MAXD;
-			const float u = ((float)x + ox) / (float)a.width, vv = ((float)y + oy) / (float)a.height;
-			V3 d;
-			if (!lens_dir(u, vv, (float)a.width, (float)a.height, a.focal_length[0], a.focal_length[1], a.screen_center[0],
-			              a.screen_center[1], a.lens_mode, a.lens_params, &d))
-				continue;  // invalid ray: the pixel stays empty
-			if (a.distortion_map && a.distortion_res[0] && a.distortion_res[1]) {
-				float ddx, ddy;
-				distortion_lerp(a.distortion_map, a.distortion_res[0], a.distortion_res[1], u, vv, &ddx, &ddy);
-				d.x += ddx;
-				d.y += ddy;
-			}
-			// the pixel's camera (src/testbed_nerf.cu:1416)
-			const Cam pc = rs_on(a.rolling_shutter)
-			                   ? slerp_cam(cam, cam_of(a.camera_end), a.rolling_shutter[0] + a.rolling_shutter[1] * u + a.rolling_shutter[2] * vv +
-			                                                              a.rolling_shutter[3] * ldval(a.sample_index, idx * 72239731u, 0))
-			                   : cam;
-			d = rot(pc, d);
-			V3 o = pc.c[3];
-			if (aperture != 0.0f) {  // depth of field (uv_to_ray, common_device.cuh:450-456)
-				const V3 lookat = o + d * a.focus_z;
-				const uint32_t px = (uint32_t)(int)(u * (float)a.width), py = (uint32_t)(int)(vv * (float)a.height);
-				const uint32_t seed = px * 19349663u + py * 96925573u;
-				float dx, dy;
-				disk_shirley(ldval(a.sample_index, seed, 0) * 2.0f - 1.0f, ldval(a.sample_index, seed, 1) * 2.0f - 1.0f, &dx, &dy);
-				o = o + pc.c[0] * (aperture * dx) + pc.c[1] * (aperture * dy);
-				d = (lookat - o) * (1.0f / a.focus_z);
-			}
-			o = o + d * a.near_distance;
+			V3 o, d;
+			if (!pixel_camera_ray(a, cam, x, y, ox, oy, aperture, &o, &d)) continue;  // invalid ray: the pixel stays empty
 			if (mode == NGP_RENDER_MODE_SLICE) {
 				// one point per pixel at camera depth focus_z, compute_nerf_rgba with depth 0.01, shade (Slice)
 				const V3 pos = o + d * a.focus_z;
@@ -1724,26 +1770,21 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 			float t = std::max(t0, 0.0f) + 1e-6f;
 			if (!box.contains(o + d * t)) continue;
 			const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-			float n = lat_to(stp, t) + ldval(a.sample_index, idx * 786433u, 0);
-			if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), summary.data(), a.max_cascade, box)) continue;
+			const float jitter = ldval(a.sample_index, idx * 786433u, 0);
 			float c[4] = {0, 0, 0, 0}, maxw = 0.0f, dep = 0.0f;
 			float cost = 0.0f;
 			uint32_t j = 0;
 			const V3 wd = v((d.x + 1) * 0.5f, (d.y + 1) * 0.5f, (d.z + 1) * 0.5f);
-			bool broke = false;
-			for (uint32_t step = 0; step < 10000; ++step) {
-				if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), summary.data(), a.max_cascade, box)) break;
-				const float t = lat_from(stp, n);
-				const float dt = lat_from(stp, n + 1.0f) - t;
-				const V3 w = tbox.rel(o + d * t);
+			// composite_kernel_nerf for one sample at (t, dt); false once the ray is opaque enough
+			auto composite = [&](float ts, float dt) -> bool {
+				const V3 w = tbox.rel(o + d * ts);
 				float coord[8] = {w.x, w.y, w.z, warp_dt(dt), wd.x, wd.y, wd.z, 0.0f};
 				hg_forward(M, P, coord, 8, 1, enc.data());
 				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data());
-				n += 1.0f;
 				const V3 pos = tbox.mn + v(coord[0] * (tbox.mx.x - tbox.mn.x), coord[1] * (tbox.mx.y - tbox.mn.y), coord[2] * (tbox.mx.z - tbox.mn.z));
 				const float T = 1.0f - c[3];
 				const float alpha = 1.0f - std::exp(-to_density(out[3], dact) * unwarp_dt(coord[3]));
-				const float wgt = alpha * T;
+				float wgt = alpha * T;
 				V3 rgb = v(to_rgb(out[0], ract), to_rgb(out[1], ract), to_rgb(out[2], ract));
 				if (mode == NGP_RENDER_MODE_NORMALS) {
 					const V3 g = density_gradient(M, P, coord, gscratch) * -to_density_d(out[3], dact);
@@ -1767,15 +1808,28 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 					const float inv = 1.0f / c[3];
 					if (mode != NGP_RENDER_MODE_COST) for (int k = 0; k < 3; ++k) c[k] *= inv;
 					c[3] *= inv;
-					broke = true;
-					break;
+					return false;
 				}
 				++j;
+				return true;
+			};
+			if (g_render_literal) {
+				// the reference's own float-chained march (ref_render_ray), 8 samples per pass
+				if (ref_render_ray(t, jitter, a.cone_angle_constant, o, d, M.bits.data(), a.max_cascade, box, 8, 10000, composite) == 0) continue;
+			} else {
+				float n = lat_to(stp, t) + jitter;
+				if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), a.max_cascade, box)) continue;
+				for (uint32_t step = 0; step < 10000; ++step) {
+					if (!next_occupied(&n, stp, o, d, idir, M.bits.data(), a.max_cascade, box)) break;
+					const float ts = lat_from(stp, n);
+					const float dt = lat_from(stp, n + 1.0f) - ts;
+					n += 1.0f;
+					if (!composite(ts, dt)) break;
+				}
 			}
 			// Cost: the reference's payload.n_steps -- the index of the terminating sample, or every
 			// composited sample of a ray that left the volume (src/testbed_nerf.cu:664-667)
 			cost = (float)j;
-			(void)broke;
 			if (!(c[3] > 0.001f)) continue;  // compact_kernel_nerf drops near-transparent rays
 			// shade_kernel_nerf (src/testbed_nerf.cu:1309-1349)
 			if (mode == NGP_RENDER_MODE_NORMALS) {
@@ -2044,6 +2098,58 @@ uint32_t oref_train_ray_samples(void* m, const ngp_train_args* a, uint32_t i, in
 		}
 	}
 	return j;
+}
+
+void oref_set_render_literal(int on) { g_render_literal = on ? 1 : 0; }
+// Test hook: the render march of pixel (x, y) -- mode 0: the lattice march render() uses, as stepping-space
+// positions n; mode 1: the reference's literal march (ref_render_ray, n_steps samples per pass), as
+// to_stepping_space(t).  Both march to the box exit (no composite stop).  Returns the sample count
+// (<= cap), writes min(count, cap) values and the lattice origin n0 = to_stepping_space(t_start) + jitter.
+// trace_out (mode 1, optional): every point the literal march visits, [k][3] = stepping position, distance
+// to the nearest cell face at the mip the point was decided at (in cells), occupied; *trace_n in: capacity,
+// out: points written.
+uint32_t oref_render_ray_samples(void* m, const ngp_render_args* a, uint32_t x, uint32_t y, int mode, uint32_t n_steps,
+                                 float* out, uint32_t cap, float* n0_out, float* trace_out, uint32_t* trace_n) {
+	Model& M = *static_cast<Model*>(m);
+	const RBox box = rbox_of(Box{v(a->aabb_min[0], a->aabb_min[1], a->aabb_min[2]), v(a->aabb_max[0], a->aabb_max[1], a->aabb_max[2])},
+	                         a->render_aabb_to_local);
+	const Stepping stp = make_stepping(a->cone_angle_constant);
+	float ox, oy;
+	pixel_offset(a->snap_to_pixel_centers ? 0 : a->sample_index, &ox, &oy);
+	V3 o, d;
+	if (!pixel_camera_ray(*a, cam_of(a->camera), x, y, ox, oy, a->aperture_size, &o, &d)) { if (trace_n) *trace_n = 0; return 0; }
+	d = normalize(d);
+	float t0, t1;
+	box.b.intersect(box.local(o), box.local(d), &t0, &t1);
+	const float t = std::max(t0, 0.0f) + 1e-6f;
+	if (!box.contains(o + d * t)) { if (trace_n) *trace_n = 0; return 0; }
+	const float jitter = ldval(a->sample_index, (x + a->width * y) * 786433u, 0);
+	if (n0_out) *n0_out = lat_to(stp, t) + jitter;
+	if (mode == 1) {
+		MarchTrace tr;
+		const uint32_t c = ref_render_ray(t, jitter, a->cone_angle_constant, o, d, M.bits.data(), a->max_cascade, box, std::max(n_steps, 1u),
+		                                  cap, [&](float ts, float) { *out++ = ref_to_stepping_space(ts, a->cone_angle_constant); return true; },
+		                                  trace_out ? &tr : nullptr);
+		if (trace_out && trace_n) {
+			const size_t nt = std::min<size_t>(tr.n.size(), *trace_n);
+			for (size_t k = 0; k < nt; ++k) {
+				trace_out[3 * k] = tr.n[k];
+				trace_out[3 * k + 1] = tr.face[k];
+				trace_out[3 * k + 2] = (float)tr.occ[k];
+			}
+			*trace_n = (uint32_t)nt;
+		}
+		return c;
+	}
+	if (trace_n) *trace_n = 0;
+	const V3 idir = v(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+	float n = lat_to(stp, t) + jitter;
+	uint32_t count = 0;
+	while (count < cap && next_occupied(&n, stp, o, d, idir, M.bits.data(), a->max_cascade, box)) {
+		out[count++] = n;
+		n += 1.0f;
+	}
+	return count;
 }
 
 int oref_train_step(void* m, const ngp_train_args* a) { return guard([&] { train_step(*static_cast<Model*>(m), *a); }); }

@@ -61,6 +61,10 @@ _PROTOS = {
     "oref_density_grid_get": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "oref_set_bitfield": (None, [C.c_void_p, C.c_void_p]),
     "oref_render": (C.c_int, [C.c_void_p, C.POINTER(A.RenderArgs), C.c_void_p, C.c_void_p]),
+    "oref_set_render_literal": (None, [C.c_int]),
+    "oref_render_ray_samples": (C.c_uint32, [C.c_void_p, C.POINTER(A.RenderArgs), C.c_uint32, C.c_uint32, C.c_int, C.c_uint32,
+                                             C.c_void_p, C.c_uint32, C.POINTER(C.c_float), C.c_void_p,
+                                             C.POINTER(C.c_uint32)]),
     "oref_accumulate_tonemap": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32,
                                        C.c_int, C.c_float, C.c_void_p, C.c_int]),
     "oref_last_error": (C.c_char_p, []),
@@ -257,6 +261,25 @@ class Oracle:
     def set_bitfield(self, bits):
         bits = np.ascontiguousarray(bits, np.uint8)
         self.lib.oref_set_bitfield(self.h, ptr(bits))
+
+    def render_ray_samples(self, args, x, y, literal=False, n_steps=8, cap=4096, trace=False):
+        """Stepping-space positions of pixel (x, y)'s render samples (marched to the box exit): the lattice
+        march of render(), or the reference's literal float-chained march with n_steps samples per pass;
+        and the ray's lattice origin n0.  trace=True (literal): also every visited point, [k][3] = stepping
+        position, distance to the nearest cell face at its decision mip (cells), occupied."""
+        out = np.zeros(cap, np.float32)
+        n0 = C.c_float()
+        tr = np.zeros((4 * cap, 3), np.float32)
+        tn = C.c_uint32(4 * cap)
+        n = self.lib.oref_render_ray_samples(self.h, C.byref(args), x, y, int(literal), n_steps, ptr(out), cap, C.byref(n0),
+                                             ptr(tr) if trace else None, C.byref(tn) if trace else None)
+        if trace:
+            return out[:n].copy(), n0.value, tr[:tn.value].copy()
+        return out[:n].copy(), n0.value
+
+    def set_render_literal(self, on):
+        """render() marches with the reference's literal float chain (True) or the lattice (False)."""
+        self.lib.oref_set_render_literal(int(bool(on)))
 
     def render(self, args):
         frame = np.zeros((args.height, args.width, 4), np.float32)

@@ -56,11 +56,11 @@ def _params(tb):
     return out.cpu().numpy()
 
 
-def _testbed(scene_dir):
+def _testbed(scene_dir, config="tiny_L4F2.json"):
     import pyngp as ngp
     tb = ngp.Testbed()
     tb.load_training_data(os.path.join(scene_dir, "transforms_train.json"))
-    tb.reload_network_from_file("tiny_L4F2.json")
+    tb.reload_network_from_file(config)
     tb.training_batch_size = BATCH
     return tb
 
@@ -82,7 +82,7 @@ EQ_STEPS = 24
 EQ_EXACT = (1, 2)  # frames after which the two sides are compared to rounding
 
 
-def _equivalence_worker(rank, world, port, scene_dir, q):
+def _equivalence_worker(rank, world, port, scene_dir, q, config="tiny_L4F2.json", tuning=None):
     """Deterministic data-parallel training: state after the first frame and after EQ_STEPS."""
     import torch.distributed as dist
     os.environ["MASTER_ADDR"] = "127.0.0.1"
@@ -90,7 +90,9 @@ def _equivalence_worker(rank, world, port, scene_dir, q):
     dist.init_process_group("gloo", rank=rank, world_size=world)
     try:
         torch.cuda.set_device(0)
-        tb = _testbed(scene_dir)
+        tb = _testbed(scene_dir, config)
+        if tuning:
+            tb.set_tuning(tuning)
         tb.init_distributed_host(rank, world, _host_allreduce(dist))
         tb.deterministic = True
         tb.shall_train = True
@@ -100,6 +102,7 @@ def _equivalence_worker(rank, world, port, scene_dir, q):
             if tb.training_step in EQ_EXACT + (EQ_STEPS,):
                 out[tb.training_step] = dict(params=_params(tb), grid=tb.density_grid(), bits=tb.density_grid_bitfield(),
                                              stats=tb.last_train_stats(), loss=tb.loss)
+        out["violations_total"] = tb.last_train_stats()["forward_early_stop_violations_total"]
         q.put(out)
     finally:
         dist.destroy_process_group()
@@ -145,11 +148,11 @@ def scene(tmp_path_factory):
     return str(root)
 
 
-def _spawn(target, scene, world=2):
+def _spawn(target, scene, world=2, *extra):
     ctx = mp.get_context("spawn")
     q = ctx.Queue()
     port = _free_port()
-    procs = [ctx.Process(target=target, args=(r, world, port, scene, q)) for r in range(world)]
+    procs = [ctx.Process(target=target, args=(r, world, port, scene, q) + tuple(extra)) for r in range(world)]
     for p in procs:
         p.start()
     res = {}
@@ -196,7 +199,17 @@ def test_data_parallel_testbed_two_processes_one_gpu(scene):
     assert r0["local"][..., 3].max() > 0.5
 
 
-def test_two_ranks_train_like_one_process_with_twice_the_batch(scene):
+@pytest.mark.parametrize("world,config,tuning", [
+    (2, "tiny_L4F2.json", None),
+    # config D at its own shape: the config-B network (L16 F2 T2^19, 64-wide MLPs)
+    (2, "lego_L16F2.json", None),
+    (4, "lego_L16F2.json", None),
+    # 4 ranks whose sample buffers start too small (debug bit 3: every rank's share overflows, the step is
+    # discarded and re-run with grown buffers) and whose chunked forward stops rays far too early (bit 2:
+    # violations on the first step, discarded and re-run with the full forward): the same training
+    (4, "lego_L16F2.json", {"debug": 12}),
+], ids=["2-tiny", "2-lego", "4-lego", "4-lego-retries"])
+def test_ranks_train_like_one_process_with_world_times_the_batch(scene, world, config, tuning):
     """rank r of N owns global rays [r R, (r+1) R) of one batch; with the exact
     decomposition the N ranks' step is one process's step of N x the batch.  Deterministic mode on
     both sides: the hash-grid gradients are integer sums (identical), the MLP gradients sums over
@@ -204,10 +217,12 @@ def test_two_ranks_train_like_one_process_with_twice_the_batch(scene):
     to rounding and the batch statistics, density grid and bitfield exactly; later, a training
     trajectory amplifies the association differences (a ray's compacted count can move by one
     sample), so at EQ_STEPS only the statistics and losses are compared, within a percent."""
-    res = _spawn(_equivalence_worker, scene)
+    res = _spawn(_equivalence_worker, scene, world, config, tuning)
+    if tuning and tuning.get("debug", 0) & 4:
+        assert all(res[r]["violations_total"] > 0 for r in range(world))  # the retry path ran
     torch.cuda.set_device(0)
-    tb = _testbed(scene)
-    tb.training_batch_size = 2 * BATCH
+    tb = _testbed(scene, config)
+    tb.training_batch_size = world * BATCH
     tb.deterministic = True
     tb.shall_train = True
     single = {}
@@ -219,7 +234,7 @@ def test_two_ranks_train_like_one_process_with_twice_the_batch(scene):
     n_mlp = _n_mlp(tb)
     for step in EQ_EXACT:
         s = single[step]
-        for r in (0, 1):
+        for r in range(world):
             d = res[r][step]
             # the global batch statistics are the single process's
             for k in ("measured_batch_size", "measured_batch_size_before_compaction", "rays_per_batch"):
@@ -233,15 +248,17 @@ def test_two_ranks_train_like_one_process_with_twice_the_batch(scene):
             np.testing.assert_allclose(d["params"][:n_mlp], s["params"][:n_mlp], rtol=1e-3, atol=1e-6)
             # step 2 runs on step-1 MLP weights that differ in association: a grid gradient sum close to zero
             # can change sign, and Adam's early steps turn that into a full step (lr) of the other sign
+            # (two ranks: < 0.5 % of the grid; four ranks' partitions differ more: measured 0.65 %)
             far = ~np.isclose(d["params"][n_mlp:], s["params"][n_mlp:], rtol=1e-3, atol=1e-6)
-            assert far.mean() < 5e-3, (step, far.mean())
+            assert far.mean() < (5e-3 if world == 2 else 1e-2), (step, far.mean())
     # after the first step the hash-grid parameters are bit-identical (integer-summed gradients, the
     # same Adam step); the step-1 MLP gradients only differ in association
     np.testing.assert_array_equal(res[0][1]["params"][n_mlp:], single[1]["params"][n_mlp:])
     s, d = single[EQ_STEPS], res[0][EQ_STEPS]
+    # (the trajectories drift apart with the association of the MLP sums: measured 1.6 % at four ranks)
     for k in ("measured_batch_size", "measured_batch_size_before_compaction"):
-        assert d["stats"][k] == pytest.approx(s["stats"][k], rel=1e-2), k
-    assert d["loss"] == pytest.approx(s["loss"], rel=2e-2)
+        assert d["stats"][k] == pytest.approx(s["stats"][k], rel=1e-2 if world == 2 else 3e-2), k
+    assert d["loss"] == pytest.approx(s["loss"], rel=2e-2 if world == 2 else 4e-2)
 
 
 def _n_mlp(tb):

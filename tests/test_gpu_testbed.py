@@ -162,14 +162,79 @@ def test_render_1080p_rows_match_oracle(scene, config):
     assert (r.max(-1) > 0.02).mean() > 0.05  # the object is in the sampled rows
     l1 = np.abs(g - r).mean()
     assert l1 < 1e-3, l1
-    # the whole 1080p frame is the same with the passes' sample slots compacted or reserved up front
-    # (every lane-per-ray width of k_generate runs in a 1080p march: 1, 4, 16 and 64)
-    # and with the render MLP computing every reserved slot (default: tiles of unfilled slots skipped)
-    for kw in ({"render_slot_compaction": 1}, {"render_slot_compaction": 2}, {"render_slot_compaction": 0, "render_skip_unfilled": 2},
-               {"render_skip_unfilled": 0, "render_tail_rays": 65536}, {"render_tail_rays": 4194304}):
+    # the whole 1080p frame is the same with and without the per-ray exit cap on the passes' budgets
+    # (every lane-per-ray width of k_generate runs in a 1080p march: 1, 4, 16 and 64) and with the render
+    # MLP computing every reserved slot (default: tiles of unfilled slots skipped)
+    for kw in ({"render_exit_cap": 2}, {"render_exit_cap": 1, "render_skip_unfilled": 2},
+               {"render_exit_cap": 0, "render_skip_unfilled": 0, "render_pipelines": 1}):
         tb.set_tuning(kw)
         np.testing.assert_array_equal(tb.render(W, H, 1, True), img, err_msg=str(kw))
-    tb.set_tuning({"render_tail_rays": 0})
+    tb.set_tuning({"render_pipelines": 0})
+
+
+def test_config_c_eight_way_row_shards_assemble_the_1080p_frame(scene):
+    """BASELINE config C at its own shape on one GPU: one 1920x1080 frame of the config-B network
+    (L16 F2 T2^19, 64-wide MLPs) rendered unsharded, then as the 8 row shards the 8 ranks of config C
+    render (render_shard(r, 8, 8): interleaved 8-row blocks, global pixel keys for the jitter and the
+    ray index -- src/testbed_nerf.cu:1408, 1416 and :355's per-ray advance).  The assembled shards are
+    the unsharded frame bit for bit; one 8-row block of every shard is checked against the oracle."""
+    from scene_util import oracle_frame_rows, testbed_oracle
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("lego_L16F2.json")
+    tb.shall_train = True
+    while tb.training_step < 200:
+        tb.frame()
+    tb.background_color = [0.0, 0.0, 0.0, 1.0]
+    tb.set_camera_to_training_view(4)
+    W, H, N, ROWS = 1920, 1080, 8, 8
+    full = tb.render(W, H, 1, True)
+    assembled = np.zeros_like(full)
+    owner = (np.arange(H) // ROWS) % N
+    for r in range(N):
+        shard = tb.render_shard(W, H, 1, True, r, N, ROWS)
+        mine = owner == r
+        assembled[mine] = shard[mine]
+    assert full[..., 3].max() > 0.5
+    np.testing.assert_array_equal(assembled, full)
+    # 8-row blocks of four of the shards (block b belongs to shard b % 8) against the oracle
+    o = testbed_oracle(tb)
+    blocks = (60, 61, 66, 67)
+    ref = oracle_frame_rows(o, tb, W, H, blocks)
+    ys = sorted(ref)
+    l1 = np.abs(full[ys, :, :3] - np.stack([ref[y] for y in ys])[..., :3]).mean()
+    assert l1 < 1e-3, l1
+
+
+def test_pyngp_in_a_process_without_torch(scene):
+    """pyngp on its own, as the reference's scripts/run.py uses it: a fresh interpreter that never imports
+    torch (so the only HIP runtime in the process is the one libngp_hip.so links) creates a Testbed,
+    trains and renders."""
+    import subprocess
+    import sys
+    root, cams, imgs = scene
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "instant-ngp-rendering_amd")
+    code = f"""
+import sys
+sys.path.insert(0, {pkg!r})
+import numpy as np
+import pyngp as ngp
+tb = ngp.Testbed(ngp.TestbedMode.Nerf)
+tb.load_training_data({os.path.join(root, "transforms_train.json")!r})
+tb.reload_network_from_file("tiny_L4F2.json")
+tb.shall_train = True
+while tb.training_step < 30:
+    tb.frame()
+tb.set_camera_to_training_view(0)
+img = tb.render(64, 48, 1, True)
+assert "torch" not in sys.modules
+assert np.isfinite(tb.loss) and img.shape == (48, 64, 4) and img[..., 3].max() > 0
+print("ok", tb.training_step, float(tb.loss))
+"""
+    r = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert r.stdout.startswith("ok 30")
 
 
 def test_network_config_parent_merge(tmp_path):
@@ -243,6 +308,86 @@ def test_exposure_optimisation(scene):
     tr.optimize_extra_dims = True
     with pytest.raises(RuntimeError):
         tb.frame()
+
+
+def _model_buffer(tb, kind):
+    import ctypes as C
+    import ngp_abi as A
+    import torch
+    lib = A.load()
+    p, n = C.c_void_p(), C.c_size_t()
+    A.check(lib.ngp_model_buffer(C.c_void_p(tb.model_handle), kind, C.byref(p), C.byref(n)))
+    out = torch.empty(n.value // 4, dtype=torch.float32, device="cuda")
+    tb.sync()
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(C.c_void_p(out.data_ptr()), p, n.value, 3) == 0
+    return out.cpu().numpy()
+
+
+def test_forced_early_stop_retry_equals_full_forward_training(scene):
+    """The discard-and-retry path of the chunked forward: ngp_tuning.debug bit 2 makes the
+    chunked forward stop rays at transmittance 0.999, so the loss needs samples it skipped.  The step's
+    violation word gates the optimizer and every deposit (error map, sharpness grid, exposure gradient)
+    on the device; the Testbed discards the step (ngp_train_discard) and runs it again with the full
+    forward.  Afterwards the training is the one of a Testbed that ran the full forward from the start:
+    parameters, Adam moments and EMA weights bit for bit (deterministic hash-grid gradients), the error
+    map and exposures to the order of their float atomics (a doubled first-step deposit would be a
+    percent-level difference)."""
+    root, cams, imgs = scene
+    import ngp_abi as A
+    out = {}
+    for forced in (True, False):
+        ngp, tb = new_testbed()
+        tb.load_training_data(os.path.join(root, "transforms_train.json"))
+        tb.reload_network_from_file("tiny_L4F2.json")
+        tb.deterministic = True
+        tr = tb.nerf.training
+        tr.include_sharpness_in_error = True
+        if forced:
+            tb.set_tuning({"debug": 4})
+        else:
+            tb.train_full_forward = True
+        tb.shall_train = True
+        while tb.training_step < 12:
+            tb.frame()
+        out[forced] = dict(viol=tb.last_train_stats()["forward_early_stop_violations_total"],
+                           full=tb.train_full_forward, em=np.asarray(tr.error_map).copy(),
+                           **{k: _model_buffer(tb, kind) for k, kind in (("p", A.PARAMS_FP32), ("m", A.ADAM_M), ("v", A.ADAM_V),
+                                                                        ("ema", A.PARAMS_EMA_FP32))})
+    f, ref = out[True], out[False]
+    assert f["viol"] > 0 and f["full"] and ref["viol"] == 0
+    for k in ("p", "m", "v", "ema"):
+        np.testing.assert_array_equal(f[k], ref[k], err_msg=k)
+    assert ref["em"].sum() > 0
+    np.testing.assert_allclose(f["em"], ref["em"], rtol=1e-4, atol=1e-7)
+
+
+def test_forced_early_stop_retry_keeps_exposure_deposits_single(scene):
+    """The same retry with per-image exposure optimisation: the first attempt's dL/dexposure deposits are
+    gated on the device, so the exposures after the camera updates are the full-forward run's."""
+    root, cams, imgs = scene
+    out = {}
+    for forced in (True, False):
+        ngp, tb = new_testbed()
+        tb.load_training_data(os.path.join(root, "transforms_train.json"))
+        tb.reload_network_from_file("tiny_L4F2.json")
+        tb.deterministic = True
+        tr = tb.nerf.training
+        tr.optimize_exposure = True
+        tr.n_steps_between_cam_updates = 1
+        if forced:
+            tb.set_tuning({"debug": 4})
+        else:
+            tb.train_full_forward = True
+        tb.shall_train = True
+        while tb.training_step < 3:
+            tb.frame()
+        out[forced] = np.asarray(tr.cam_exposure).copy()
+        if forced:
+            assert tb.last_train_stats()["forward_early_stop_violations_total"] > 0
+    assert np.abs(out[False]).max() > 0
+    np.testing.assert_allclose(out[True], out[False], rtol=1e-4, atol=1e-7)
 
 
 def _rotvec(R):
