@@ -305,6 +305,10 @@ typedef struct ngp_render_args {
 	 * slice_plane_z + scale); Slice mode renders the density / colour slice at depth focus_z instead of tracing */
 	float aperture_size;
 	float focus_z;
+	/* Nerf::glow_mode / glow_y_cutoff (composite_kernel_nerf's glow, src/testbed_nerf.cu:540-628): bit 0 green grid,
+	 * bit 1 green cut line, bit 2 mask to alpha, bit 3 radial distance, bit 4 grid mode; 0 = off */
+	int32_t glow_mode;
+	float glow_y_cutoff;
 } ngp_render_args;
 
 /* ngp_render_args.render_mode (the reference's ERenderMode; Distortion and EncodingVis are GUI

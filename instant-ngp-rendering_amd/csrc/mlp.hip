@@ -422,19 +422,24 @@ __device__ __forceinline__ void sh4_slice(const float* dw, int g, float (&o)[4])
 	for (int r = 0; r < 4; ++r) o[r] = g == 0 ? v[r] : g == 1 ? v[4 + r] : g == 2 ? v[8 + r] : v[12 + r];
 }
 
-// one layer: B operands in (KS steps) -> C tiles out (MT tiles), weights w[frag]
-// live: wave-uniform mask of the column tiles to compute (render slots no ray filled are skipped)
+// one layer: B operands in (KS steps) -> C tiles out (MT tiles), weights w[frag].  Every weight fragment
+// is read from LDS once and feeds the CT column tiles' MFMAs; there is no per-tile branch (a branch
+// around each MFMA keeps the compiler from sharing the fragment reads: one LDS round trip per MFMA)
 template <class N, int l, int CT_>
-__device__ __forceinline__ void rf_layer(const h8* w, const h8 (&bin)[CT_][2], f4 (&cout)[CT_][4], uint32_t live) {
+__device__ __forceinline__ void rf_layer(const h8* w, const h8 (&bin)[CT_][2], f4 (&cout)[CT_][4]) {
 	constexpr int MT = N::Mt(l), KS = N::Ks(l), F0 = N::fwd_frags_upto(l);
+	h8 a[MT][KS];
+#pragma unroll
+	for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+		for (int s = 0; s < KS; ++s) a[mt][s] = w[(F0 + mt * KS + s) * 64];
 #pragma unroll
 	for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
 		for (int c = 0; c < CT_; ++c) {
-			if (!((live >> c) & 1u)) continue;
 			f4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-			for (int s = 0; s < KS; ++s) acc = mfma(w[(F0 + mt * KS + s) * 64], bin[c][s], acc);
+			for (int s = 0; s < KS; ++s) acc = mfma(a[mt][s], bin[c][s], acc);
 			cout[c][mt] = acc;  // ReLU (hidden layers) is applied by rf_chain on the packed halves
 		}
 }
@@ -463,11 +468,11 @@ __device__ __forceinline__ void rf_chain(const f4 (&cin)[CT_][4], h8 (&bout)[CT_
 }
 
 template <class N, int l, int END, int CT_>
-__device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4 (&c)[CT_][4], uint32_t live) {
+__device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4 (&c)[CT_][4]) {
 	if constexpr (l < END) {
-		rf_layer<N, l, CT_>(w, b, c, live);
+		rf_layer<N, l, CT_>(w, b, c);
 		rf_chain<N::Mt(l), CT_>(c, b);
-		rf_hidden_range<N, l + 1, END, CT_>(w, b, c, live);
+		rf_hidden_range<N, l + 1, END, CT_>(w, b, c);
 	}
 }
 
@@ -485,8 +490,9 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 #pragma unroll
 		for (int s = 0; s < N::KE; ++s)
 			b[cc][s] = pack_h8(cur.e[cc][4 * s], cur.e[cc][4 * s + 1], cur.e[cc][4 * s + 2], cur.e[cc][4 * s + 3]);
-	// SH-row inputs (renderer): a 16-sample column tile whose slots no ray filled (k_generate marks them
-	// with row NO_SH_ROW) is not computed -- k_composite reads a ray's filled samples only
+	// SH-row inputs (renderer): a wave step whose slots no ray filled (k_generate marks them with row
+	// NO_SH_ROW) is not computed -- k_composite reads a ray's filled samples only.  A step with any filled
+	// slot computes all its tiles (branch-free MFMA chains)
 	uint32_t live = (1u << CT_) - 1u;
 	if constexpr (SHIN && !DENSITY_ONLY) {
 		if (a.skip_unfilled) {
@@ -496,8 +502,8 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 			if (live == 0) return;
 		}
 	}
-	rf_hidden_range<N, 0, N::DH, CT_>(w, b, c, live);
-	rf_layer<N, N::DH, CT_>(w, b, c, live);
+	rf_hidden_range<N, 0, N::DH, CT_>(w, b, c);
+	rf_layer<N, N::DH, CT_>(w, b, c);
 	if constexpr (DENSITY_ONLY) {
 		if (g == 0) {
 #pragma unroll
@@ -522,8 +528,8 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 				b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
 			}
 		}
-		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c, live);
-		rf_layer<N, N::NL - 1, CT_>(w, b, c, live);
+		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
+		rf_layer<N, N::NL - 1, CT_>(w, b, c);
 		if (a.out_mode == 0) {
 			if (g == 0) {
 #pragma unroll
@@ -1147,11 +1153,7 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		// render MLP steps of 64 samples per wave (4 column tiles share each weight fragment read from LDS:
 		// the 16-sample steps were LDS-bandwidth bound, 20 ds_read_b128 per 20 MFMAs); -4 % frame time
 		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : 4u;
-		if (sh && a.F == 2 && pl && tile == 2)
-			launch_timed(k_mlp_infer_rf<N, 2, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
-		else if (sh && a.F == 2 && pl && tile == 3)
-			launch_timed(k_mlp_infer_rf<N, 2, 2, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
-		else if (sh && a.F == 2 && pl && tile == 4)
+		if (sh && a.F == 2 && pl && tile == 4)
 			launch_timed(k_mlp_infer_rf<N, 4, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 64 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);
 		else if (sh && a.F == 4 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 14, true>, grid, BLOCK, lds, s, a);

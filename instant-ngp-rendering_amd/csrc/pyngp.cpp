@@ -377,6 +377,8 @@ PYBIND11_MODULE(pyngp, m) {
 		     },
 		     py::arg("frame_idx"), py::arg("camera_to_world_start"), py::arg("camera_to_world_end"), py::arg("rolling_shutter"),
 		     py::arg("convert_to_ngp") = true)
+		.def("get_extra_dims", [](const TrainingView& v, int i) { return v.tb->training_extra_dims(i); },
+		     "Get the extra dims (including trained latent code) for a specified training view.")
 		.def("get_camera_extrinsics", [](TrainingView& v, int i) { return mat43_to_numpy(v.tb->get_camera_extrinsics(i)); },
 		     py::arg("frame_idx"))
 		.def("set_image",
@@ -410,7 +412,18 @@ PYBIND11_MODULE(pyngp, m) {
 		NV_RW("rendering_min_transmittance", render_min_transmittance)
 		NV_RW("cone_angle_constant", cone_angle_constant)
 		NV_RW("visualize_cameras", visualize_cameras)
+		NV_RW("glow_y_cutoff", glow_y_cutoff)
+		NV_RW("glow_mode", glow_mode)
 #undef NV_RW
+		.def("find_closest_training_view", [](const NerfView& v) { return v.tb->find_closest_training_view(); },
+		     "Obtain the training view that is closest to the current camera.")
+		// extra dims (per-image latent codes) of the rendered rays (Nerf::rendering_extra_dims, src/testbed_nerf.cu:3246-3280)
+		.def_property("rendering_extra_dims_from_training_view",
+		              [](const NerfView& v) { return v.tb->rendering_extra_dims_from_training_view; },
+		              [](NerfView& v, int i) { v.tb->set_rendering_extra_dims_from_training_view(i); })
+		.def("set_rendering_extra_dims_from_training_view", [](NerfView& v, int i) { v.tb->set_rendering_extra_dims_from_training_view(i); })
+		.def("set_rendering_extra_dims", [](NerfView& v, const std::vector<float>& x) { v.tb->set_rendering_extra_dims(x); })
+		.def("get_rendering_extra_dims", [](const NerfView& v) { return v.tb->rendering_extra_dims(); })
 		.def_property_readonly("max_cascade", [](const NerfView& v) { return v.tb->nerf.max_cascade; })
 		.def_property_readonly("training", py::cpp_function([](NerfView& v) { return TrainingView{v.tb}; }, py::keep_alive<0, 1>()));
 
@@ -541,6 +554,22 @@ PYBIND11_MODULE(pyngp, m) {
 			              t.aabb_max = b.max;
 		              })
 		.def_property("fov", &Testbed::fov, &Testbed::set_fov)
+		.def_property("fov_xy", &Testbed::fov_xy, &Testbed::set_fov_xy)
+		.def_property("raw_aabb", [](const Testbed& t) { return BoundingBox{t.raw_aabb_min, t.raw_aabb_max}; },
+		              [](Testbed& t, const BoundingBox& b) {
+			              t.raw_aabb_min = b.min;
+			              t.raw_aabb_max = b.max;
+		              })
+		.def_readwrite("up_dir", &Testbed::up_dir)
+		.def("crop_box", [](const Testbed& t, bool nerf_space) { return mat43_to_numpy(t.crop_box(nerf_space)); },
+		     py::arg("nerf_space") = true)
+		.def("set_crop_box",
+		     [](Testbed& t, py::array_t<float, py::array::c_style | py::array::forcecast> m, bool nerf_space) {
+			     t.set_crop_box(numpy_to_mat43(m), nerf_space);
+		     },
+		     py::arg("matrix"), py::arg("nerf_space") = true)
+		.def("crop_box_corners", &Testbed::crop_box_corners, py::arg("nerf_space") = true)
+		.def("compute_image_mse", &Testbed::compute_image_mse, py::arg("quantize") = false)
 		.def_readwrite("fov_axis", &Testbed::fov_axis)
 		.def_readwrite("zoom", &Testbed::zoom)
 		.def_readwrite("screen_center", &Testbed::screen_center)

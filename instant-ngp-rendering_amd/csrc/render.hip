@@ -66,6 +66,8 @@ struct RenderK {
 	const float* normals;     // Normals mode: d(raw density)/d(warped position) per sample slot of the pass, [slot][3]
 	int mark_unfilled;        // unfilled slots get SH row NO_SH_ROW (the render MLP skips tiles of them)
 	int exit_cap;             // a ray's per-pass budget is capped by the lattice points left to its exit
+	int glow_mode;            // Nerf::glow_mode (composite_kernel_nerf's glow; 0 = off)
+	float glow_y_cutoff;
 };
 
 // square2disk_shirley (random_val.cuh:112-128)
@@ -601,6 +603,46 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 // of a tail pass's samples at once, profiles/r03_tail_composite_ab.txt)
 constexpr uint32_t COMPOSITE_AHEAD = 4;
 
+// composite_kernel_nerf's glow (testbed_nerf.cu:540-628): grid lines and a cut line below glow_y_cutoff
+// added to the sample's colour (or replacing it, grid mode); mask_to_alpha scales the sample's weight
+__device__ __forceinline__ void apply_glow(const RenderK& k, v3 pos, v3 cam_pos, v3* rgb, float* weight) {
+	const int gm = k.glow_mode;
+	const bool green_grid = gm & 1, green_cutline = gm & 2, mask_to_alpha = gm & 4, radial = gm & 8, grid_mode = gm & 16;
+	float glow = 0.0f;
+	float dist = pos.y;
+	if (radial) dist = fminf(length(pos - cam_pos), (4.5f - pos.y) * 0.333f);
+	if (grid_mode) {
+		glow = 1.0f / fmaxf(1.0f, dist);
+	} else {
+		float y = k.glow_y_cutoff - dist, mask = 0.0f;
+		if (y > 0.0f) {
+			y *= 80.0f;
+			mask = fminf(1.0f, y);
+			if (green_cutline) glow += fmaxf(0.0f, 1.0f - fabsf(1.0f - y)) * 4.0f;
+			if (y > 1.0f) y = 1.0f - (y - 1.0f) * 0.05f;
+			if (green_grid) glow += fmaxf(0.0f, y / fmaxf(1.0f, dist));
+		}
+		if (mask_to_alpha) *weight *= mask;
+	}
+	if (glow > 0.0f) {
+		const float PI = 3.141592653589793f;
+		float line = 0.0f;
+#pragma unroll
+		for (int f = 2; f <= 16; f *= 2) {  // the reference's products, left to right: pos * f * pi * 16
+			line += fmaxf(0.0f, cosf(pos.y * (float)f * PI * 16.0f) - 0.975f);
+			line += fmaxf(0.0f, cosf(pos.x * (float)f * PI * 16.0f) - 0.975f);
+			line += fmaxf(0.0f, cosf(pos.z * (float)f * PI * 16.0f) - 0.975f);
+		}
+		if (grid_mode) {
+			glow = glow * line * 15.0f;
+			*rgb = mk3(glow * 0.25f, glow, glow * 0.5f);
+		} else {
+			glow = glow * glow * 0.25f + glow * line * 15.0f;
+			*rgb = mk3(rgb->x + glow * 0.25f, rgb->y + glow, rgb->z + glow * 0.5f);
+		}
+	}
+}
+
 // composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
 // each thread composites its ray's samples of this pass in order, then the block appends the
 // ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
@@ -664,11 +706,15 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				const float T = 1.0f - c.w;
 				const float dt = unwarp_dt(wdt[u]);
 				const float alpha = 1.0f - __expf(-network_to_density(__high2float(bs), k.density_act) * dt);
-				const float weight = alpha * T;
+				float weight = alpha * T;
 				v3 rgb = mk3(network_to_rgb(__low2float(rg), k.rgb_act), network_to_rgb(__high2float(rg), k.rgb_act),
 				             network_to_rgb(__low2float(bs), k.rgb_act));
 				if constexpr (MODES) {
 					const size_t s = sbase + j0 + u;
+					if (k.glow_mode) {
+						const float4 crd = posdt[s];
+						apply_glow(k, unwarp_position(mk3(crd.x, crd.y, crd.z), k.train_aabb), cam_pos, &rgb, &weight);
+					}
 					if (k.mode == NGP_RENDER_MODE_NORMALS) {
 						// the reference replaces the network input by its gradient (input_gradient, :1715-1717)
 						const float* g = k.normals + 3 * s;
@@ -956,6 +1002,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.depth_scale = a->depth_scale;
 	k.hard_edges = a->gbuffer_hard_edges;
 	k.aperture = k.mode == NGP_RENDER_MODE_SLICE ? 0.0f : a->aperture_size;  // init_rays_with_payload_kernel_nerf:1427-1429
+	k.glow_mode = a->glow_mode;
+	k.glow_y_cutoff = a->glow_y_cutoff;
 	k.focus_z = a->focus_z;
 	if (k.aperture != 0.0f && !(k.focus_z > 0.0f)) throw std::invalid_argument("depth of field needs focus_z > 0");
 	k.train_aabb.min = mk3(a->train_aabb_min[0], a->train_aabb_min[1], a->train_aabb_min[2]);
@@ -1189,7 +1237,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			pr.k.normals = sc.nrm.ptr;
 		}
 		tm.begin(NGP_TIMER_RENDER_MARCH, ps);
-		if (pr.k.mode == NGP_RENDER_MODE_SHADE)
+		if (pr.k.mode == NGP_RENDER_MODE_SHADE && !pr.k.glow_mode)
 			k_composite<false><<<std::max(1u, div_up(pr.n_alive_ub, comp_block)), comp_block, 0, ps>>>(
 			    pr.k, alive_in, pr.P(cur), pr.C(cur), pr.ps->depth[cur].ptr, pr.posdt, pr.ps->out.ptr, pr.P(1 - cur), pr.C(1 - cur),
 			    pr.ps->depth[1 - cur].ptr, pr.P(2), pr.C(2), pr.ps->depth[2].ptr, alive_out, counters + 2, samples_next, counters + 3);

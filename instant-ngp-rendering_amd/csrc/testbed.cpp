@@ -11,6 +11,7 @@
 #include <algorithm>
 #include <cctype>
 #include <iterator>
+#include <limits>
 #include <map>
 #include <mutex>
 #include <chrono>
@@ -538,6 +539,9 @@ void Testbed::load_nerf_post() {
 			render_aabb_min[k] = std::max(ds.render_aabb_min[k], aabb_min[k]);
 			render_aabb_max[k] = std::min(ds.render_aabb_max[k], aabb_max[k]);
 		}
+	raw_aabb_min = aabb_min;  // m_raw_aabb = m_aabb (src/testbed_nerf.cu:2221)
+	raw_aabb_max = aabb_max;
+	up_dir = ds.up;           // m_up_dir = dataset.up (:2237)
 	nerf.max_cascade = 0;
 	while ((1 << nerf.max_cascade) < ds.aabb_scale) ++nerf.max_cascade;
 	nerf.cone_angle_constant = ds.aabb_scale <= 1 ? 0.0f : (1.0f / 256.0f);
@@ -1529,6 +1533,114 @@ void Testbed::set_fov(float degrees) {
 	const float f = fov_to_focal_length(1, degrees);
 	relative_focal_length = {f, f};
 }
+vec2 Testbed::fov_xy() const {
+	return {focal_length_to_fov(1.0f, relative_focal_length[0]), focal_length_to_fov(1.0f, relative_focal_length[1])};
+}
+void Testbed::set_fov_xy(const vec2& degrees) {
+	relative_focal_length = {fov_to_focal_length(1, degrees[0]), fov_to_focal_length(1, degrees[1])};
+}
+
+// crop_box (src/testbed.cu:618-633): axes = the rows of render_aabb_to_local scaled by the half extents, centre
+// = transpose(render_aabb_to_local) * the box centre (the box lives in the local frame)
+Mat43 Testbed::crop_box(bool nerf_space) const {
+	const mat3& R = render_aabb_to_local;  // row-major
+	vec3 cen_local, radius;
+	for (int k = 0; k < 3; ++k) {
+		cen_local[k] = 0.5f * (render_aabb_min[k] + render_aabb_max[k]);
+		radius[k] = 0.5f * (render_aabb_max[k] - render_aabb_min[k]);
+	}
+	Mat43 rv;
+	for (int a = 0; a < 3; ++a)
+		rv.set_col(a, {R[3 * a + 0] * radius[a], R[3 * a + 1] * radius[a], R[3 * a + 2] * radius[a]});
+	vec3 cen;
+	for (int j = 0; j < 3; ++j) cen[j] = R[0 * 3 + j] * cen_local[0] + R[1 * 3 + j] * cen_local[1] + R[2 * 3 + j] * cen_local[2];
+	rv.set_col(3, cen);
+	return nerf_space ? nerf.training.dataset.ngp_matrix_to_nerf(rv, true) : rv;
+}
+
+// set_crop_box (src/testbed.cu:635-649): the inverse -- rows of the frame = the normalised axes, box = centre
+// (in the local frame) +- the axes' lengths
+void Testbed::set_crop_box(Mat43 m, bool nerf_space) {
+	if (nerf_space) {
+		float r[12];  // row-major 3x4 of the NeRF-space matrix
+		for (int row = 0; row < 3; ++row)
+			for (int col = 0; col < 4; ++col) r[row * 4 + col] = m.m[3 * col + row];
+		m = nerf.training.dataset.nerf_matrix_to_ngp(r, true);
+	}
+	vec3 radius;
+	for (int a = 0; a < 3; ++a) {
+		const vec3 c = m.col(a);
+		radius[a] = std::sqrt(c[0] * c[0] + c[1] * c[1] + c[2] * c[2]);
+		if (!(radius[a] > 0.f)) throw std::runtime_error("set_crop_box: the box axes must be non-zero");
+		for (int k = 0; k < 3; ++k) render_aabb_to_local[3 * a + k] = c[k] / radius[a];
+	}
+	const vec3 c3 = m.col(3);
+	for (int a = 0; a < 3; ++a) {
+		const float cl = render_aabb_to_local[3 * a + 0] * c3[0] + render_aabb_to_local[3 * a + 1] * c3[1] +
+		                 render_aabb_to_local[3 * a + 2] * c3[2];
+		render_aabb_min[a] = cl - radius[a];
+		render_aabb_max[a] = cl + radius[a];
+	}
+	m_spp = 0;
+}
+
+// crop_box_corners (src/testbed.cu:651-670): the 8 corners m * (+-1, +-1, +-1, 1), x fastest
+std::vector<vec3> Testbed::crop_box_corners(bool nerf_space) const {
+	const Mat43 m = crop_box(nerf_space);
+	std::vector<vec3> rv(8);
+	for (int i = 0; i < 8; ++i) {
+		const float sx = (i & 1) ? 1.f : -1.f, sy = (i & 2) ? 1.f : -1.f, sz = (i & 4) ? 1.f : -1.f;
+		for (int k = 0; k < 3; ++k) rv[i][k] = m.m[k] * sx + m.m[3 + k] * sy + m.m[6 + k] * sz + m.m[9 + k];
+	}
+	return rv;
+}
+
+float Testbed::compute_image_mse(bool) const {
+	// the Image mode's image is empty in a NeRF testbed: reduce_sum over 0 elements / 0 (src/testbed_image.cu:517)
+	return std::numeric_limits<float>::quiet_NaN();
+}
+
+int Nerf::find_closest_training_view(const Mat43& pose, const std::function<Mat43(size_t)>& transform) const {
+	int best = training.view;
+	float best_score = std::numeric_limits<float>::infinity();
+	auto dist = [](const vec3& a, const vec3& b) {
+		const float x = a[0] - b[0], y = a[1] - b[1], z = a[2] - b[2];
+		return std::sqrt(x * x + y * y + z * z);
+	};
+	for (int i = 0; i < training.n_images_for_training; ++i) {
+		const Mat43 t = transform((size_t)i);
+		float score = dist(t.col(3), pose.col(3));
+		score += 0.25f * dist(t.col(2), pose.col(2));
+		if (score < best_score) {
+			best_score = score;
+			best = i;
+		}
+	}
+	return best;
+}
+
+void Testbed::set_rendering_extra_dims_from_training_view(int trainview) {
+	if (!n_extra_dims()) throw std::runtime_error("Dataset does not have extra dims.");
+	if (trainview < 0 || (size_t)trainview >= nerf.training.dataset.n_images) throw std::runtime_error("Invalid training view.");
+	rendering_extra_dims_from_training_view = trainview;
+}
+
+void Testbed::set_rendering_extra_dims(const std::vector<float>& vals) {
+	if (vals.size() != n_extra_dims())
+		throw std::runtime_error("Invalid number of extra dims. Got " + std::to_string(vals.size()) + " but must be " +
+		                         std::to_string(n_extra_dims()) + ".");
+	rendering_extra_dims_from_training_view = -1;
+}
+
+std::vector<float> Testbed::training_extra_dims(int trainview) const {
+	if (n_extra_dims() == 0) return {};  // Nerf::Training::get_extra_dims_cpu (src/testbed_nerf.cu:1797-1800)
+	if (trainview < 0 || (size_t)trainview >= nerf.training.dataset.n_images) throw std::runtime_error("Invalid training view.");
+	return {};
+}
+
+int Testbed::find_closest_training_view() const {
+	return nerf.find_closest_training_view(camera, [this](size_t i) { return training_transform(i); });
+}
 
 void Testbed::set_camera_to_training_view(int trainview) {
 	const NerfDataset& ds = nerf.training.dataset;
@@ -1681,6 +1793,8 @@ void Testbed::render_into(float* host_dst, int width, int height, int spp, bool 
 		default: throw std::runtime_error("render: render mode Distortion is a GUI visualisation and not supported by this build");
 	}
 	r.depth_scale = 1.0f / nerf.training.dataset.scale;  // src/testbed_nerf.cu:1905
+	r.glow_mode = nerf.glow_mode;
+	r.glow_y_cutoff = nerf.glow_y_cutoff;
 	r.gbuffer_hard_edges = nerf.render_gbuffer_hard_edges;
 	// plane_z = m_slice_plane_z + m_scale (src/testbed_nerf.cu:1842): the Slice plane, or the focus plane of the
 	// depth of field (init_rays_with_payload_kernel_nerf drops the aperture when plane_z < 0, :1427-1429)
@@ -1875,6 +1989,7 @@ void Testbed::save_snapshot(const std::string& path, bool include_optimizer_stat
 	snap["aabb"] = aabb;
 	snap["exposure"] = Json((double)exposure);
 	snap["background_color"] = vec_json(background_color.data(), 4);
+	snap["up_dir"] = vec_json(up_dir.data(), 3);  // src/testbed.cu:4804
 	Json cam = Json::object();
 	Json mat = Json::array();
 	for (int c = 0; c < 4; ++c) mat.push_back(vec_json(&camera.m[3 * c], 3));  // 4 columns of 3 (mat4x3)
@@ -1955,6 +2070,8 @@ void Testbed::load_snapshot(const std::string& path) {
 	exposure = (float)snap.value("exposure", (double)exposure);
 	if (snap.contains("background_color"))
 		for (int k = 0; k < 4; ++k) background_color[k] = (float)snap["background_color"][k].num();
+	if (snap.contains("up_dir"))
+		for (int k = 0; k < 3; ++k) up_dir[k] = (float)snap["up_dir"][k].num();
 	if (snap.contains("camera")) {
 		const Json& cam = snap["camera"];
 		if (cam.contains("matrix") && cam["matrix"].size() == 4)

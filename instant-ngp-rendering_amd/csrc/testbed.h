@@ -164,6 +164,12 @@ struct Nerf {
 	float sharpen = 0.f;
 	uint32_t density_grid_ema_step = 0;
 	bool visualize_cameras = false;
+	// composite_kernel_nerf's glow (nerf.h:176-177, src/testbed_nerf.cu:540-628)
+	float glow_y_cutoff = 0.f;
+	int glow_mode = 0;
+	// Nerf::find_closest_training_view (src/testbed_nerf.cu:3231-3244): the training view whose camera is
+	// nearest to pose (distance of the origins + 0.25 x distance of the forward axes); training.view if none
+	int find_closest_training_view(const Mat43& pose, const std::function<Mat43(size_t)>& transform) const;
 };
 
 class Testbed {
@@ -216,6 +222,27 @@ public:
 	void reset_camera();
 	float fov() const;
 	void set_fov(float degrees);
+	// fov_xy / set_fov_xy (src/testbed.cu:3538-3544): per-axis field of view in degrees
+	vec2 fov_xy() const;
+	void set_fov_xy(const vec2& degrees);
+	// the render crop box as a 4x3 frame (axes scaled by the half extents, centre), NGP or NeRF space
+	// (crop_box / set_crop_box / crop_box_corners, src/testbed.cu:618-670)
+	Mat43 crop_box(bool nerf_space = true) const;
+	void set_crop_box(Mat43 m, bool nerf_space = true);
+	std::vector<vec3> crop_box_corners(bool nerf_space = true) const;
+	// compute_image_mse (src/testbed_image.cu:455-518): the Image mode's network against its image; a NeRF
+	// testbed has no image (the reference divides an empty sum by zero elements: NaN)
+	float compute_image_mse(bool quantize_to_byte = false) const;
+	int find_closest_training_view() const;
+	// extra dims (per-image latent codes) of the rendered rays (Nerf::rendering_extra_dims, src/testbed_nerf.cu:1797-1812,
+	// 3246-3280).  This build trains without them (NerfDataset::n_extra_dims() == 0, optimize_extra_dims refused),
+	// so the reference's n_extra_dims() == 0 behaviour applies: empty vectors, "Dataset does not have extra dims."
+	uint32_t n_extra_dims() const { return 0; }
+	int rendering_extra_dims_from_training_view = -1;
+	void set_rendering_extra_dims_from_training_view(int trainview);
+	void set_rendering_extra_dims(const std::vector<float>& vals);
+	std::vector<float> rendering_extra_dims() const { return {}; }
+	std::vector<float> training_extra_dims(int trainview) const;
 
 	// --- snapshots (save_snapshot src/testbed.cu:4775, load_snapshot :4841) ---
 	void save_snapshot(const std::string& path, bool include_optimizer_state = false, bool compress = true);
@@ -291,6 +318,10 @@ public:
 	std::string network_config_path = "base.json";
 	bool training_data_available = false;
 	vec3 aabb_min = {0.f, 0.f, 0.f}, aabb_max = {1.f, 1.f, 1.f};
+	// m_raw_aabb (testbed.h:926): the dataset's aabb as loaded (src/testbed_nerf.cu:2221)
+	vec3 raw_aabb_min = {-10.f, -10.f, -10.f}, raw_aabb_max = {10.f, 10.f, 10.f};
+	// m_up_dir (testbed.h:732): the dataset's up direction (src/testbed_nerf.cu:2237); kept in snapshots
+	vec3 up_dir = {0.f, 1.f, 0.f};
 	// the render crop box (m_render_aabb, m_render_aabb_to_local; src/testbed_nerf.cu:2219-2225) and modes
 	vec3 render_aabb_min = {0.f, 0.f, 0.f}, render_aabb_max = {1.f, 1.f, 1.f};
 	mat3 render_aabb_to_local = MAT3_IDENTITY;

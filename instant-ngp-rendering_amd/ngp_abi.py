@@ -103,6 +103,7 @@ class RenderArgs(C.Structure):
         ("distortion_map", C.c_void_p), ("distortion_res", C.c_uint32 * 2),
         ("render_aabb_to_local", C.c_float * 9), ("render_mode", C.c_int32), ("depth_scale", C.c_float),
         ("gbuffer_hard_edges", C.c_int32), ("aperture_size", C.c_float), ("focus_z", C.c_float),
+        ("glow_mode", C.c_int32), ("glow_y_cutoff", C.c_float),
     ]
 
 

@@ -1682,6 +1682,51 @@ static V3 density_gradient(const Model& M, const uint16_t* P, const float* coord
 	return v(g[0], g[1], g[2]);
 }
 
+// composite_kernel_nerf's glow (src/testbed_nerf.cu:540-628, the active branch): a grid and a cut line
+// below glow_y_cutoff added to the colour (replacing it in grid mode); mask_to_alpha scales the weight.
+static void glow(const ngp_render_args& a, V3 pos, V3 cam_pos, V3* rgb, float* weight) {
+	const int gm = a.glow_mode;
+	const bool green_grid = gm & 1, green_cutline = gm & 2, mask_to_alpha = gm & 4, radial_mode = gm & 8, grid_mode = gm & 16;
+	float g = 0.0f;
+	float dist;
+	if (radial_mode) {
+		dist = len(pos - cam_pos);
+		dist = std::min(dist, (4.5f - pos.y) * 0.333f);
+	} else {
+		dist = pos.y;
+	}
+	if (grid_mode) {
+		g = 1.0f / std::max(1.0f, dist);
+	} else {
+		float y = a.glow_y_cutoff - dist;
+		float mask = 0.0f;
+		if (y > 0.0f) {
+			y *= 80.0f;
+			mask = std::min(1.0f, y);
+			if (green_cutline) g += std::max(0.0f, 1.0f - std::fabs(1.0f - y)) * 4.0f;
+			if (y > 1.0f) y = 1.0f - (y - 1.0f) * 0.05f;
+			if (green_grid) g += std::max(0.0f, y / std::max(1.0f, dist));
+		}
+		if (mask_to_alpha) *weight *= mask;
+	}
+	if (g > 0.0f) {
+		const float PI = 3.141592653589793f;
+		float line = 0.0f;
+		for (float f : {2.0f, 4.0f, 8.0f, 16.0f}) {
+			line += std::max(0.0f, std::cos(pos.y * f * PI * 16.0f) - 0.975f);
+			line += std::max(0.0f, std::cos(pos.x * f * PI * 16.0f) - 0.975f);
+			line += std::max(0.0f, std::cos(pos.z * f * PI * 16.0f) - 0.975f);
+		}
+		if (grid_mode) {
+			g = g * line * 15.0f;
+			*rgb = v(g * 0.25f, g, g * 0.5f);
+		} else {
+			g = g * g * 0.25f + g * line * 15.0f;
+			*rgb = v(rgb->x + g * 0.25f, rgb->y + g, rgb->z + g * 0.5f);
+		}
+	}
+}
+
 // uv_to_ray + init_rays_with_payload_kernel_nerf's ray (src/testbed_nerf.cu:1408-1441, common_device.cuh:441-459)
 // of pixel (x, y): lens, learned distortion, the pixel's (rolling-shutter) camera, depth of field, near
 // distance; the direction is not normalised.  false: the lens has no ray for the pixel.
@@ -1786,6 +1831,7 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 				const float alpha = 1.0f - std::exp(-to_density(out[3], dact) * unwarp_dt(coord[3]));
 				float wgt = alpha * T;
 				V3 rgb = v(to_rgb(out[0], ract), to_rgb(out[1], ract), to_rgb(out[2], ract));
+				if (a.glow_mode) glow(a, pos, cam.c[3], &rgb, &wgt);
 				if (mode == NGP_RENDER_MODE_NORMALS) {
 					const V3 g = density_gradient(M, P, coord, gscratch) * -to_density_d(out[3], dact);
 					rgb = normalize(g);

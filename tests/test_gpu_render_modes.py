@@ -6,7 +6,9 @@
   1327-1338): AO, Normals (the density gradient through the network, :1715-1717), Positions,
   Depth (soft and with render_gbuffer_hard_edges), Cost, and Slice (render_nerf's 2-D path,
   :1842-1845, 1908-1932);
-* depth of field (uv_to_ray, common_device.cuh:450-456).
+* depth of field (uv_to_ray, common_device.cuh:450-456);
+* the glow of composite_kernel_nerf (nerf.glow_mode / glow_y_cutoff, src/testbed_nerf.cu:540-628): grid and
+  cut lines below the cutoff, mask to alpha, radial distance, grid mode.
 
 Every case renders a 72 x 66 frame of a config-A/B network over a sphere of occupancy and compares
 RGBA with the oracle within the north-star 1e-3 mean L1 (Normals, a gradient through fp16
@@ -54,6 +56,12 @@ CASES = {
     "slice": dict(mode=A.RENDER_SLICE, focus=1.3),
     "dof": dict(aperture=0.04, focus=2.4, spp=3),
     "dof_crop": dict(aperture=0.04, focus=2.4, crop=((0.25, 0.25, 0.25), (0.75, 0.7, 0.75)), R=rot_z(-20)),
+    # Nerf::glow_mode / glow_y_cutoff (composite_kernel_nerf's glow, src/testbed_nerf.cu:540-628)
+    "glow_grid_cutline": dict(glow=1 | 2, cutoff=0.55),
+    "glow_mask_to_alpha": dict(glow=1 | 2 | 4, cutoff=0.5),
+    "glow_radial": dict(glow=1 | 8, cutoff=0.4),
+    "glow_grid_mode": dict(glow=16),
+    "glow_positions": dict(glow=1 | 4, cutoff=0.6, mode=A.RENDER_POSITIONS),
 }
 
 
@@ -71,6 +79,8 @@ def test_render_mode_matches_oracle(case):
         ra.gbuffer_hard_edges = c.get("hard", 0)
         ra.aperture_size = c.get("aperture", 0.0)
         ra.focus_z = c.get("focus", 0.0)
+        ra.glow_mode = c.get("glow", 0)
+        ra.glow_y_cutoff = c.get("cutoff", 0.0)
         if "crop" in c:
             lo, hi = c["crop"]
             for k in range(3):
@@ -90,6 +100,11 @@ def test_render_mode_matches_oracle(case):
             assert err < c.get("tol", 1e-3), err
         if ra.render_mode == A.RENDER_SLICE:
             np.testing.assert_array_equal(gd[gd < 1e4], np.float32(ra.focus_z))
+        if ra.glow_mode:
+            # the glow changes the frame
+            ra.glow_mode = 0
+            plain, _, _, _ = _render(g, o, ra)
+            assert np.abs(plain - gf).mean() > 1e-3
         if "crop" in c:
             # the crop removes part of the sphere: fewer covered pixels than the uncropped render
             ra2 = render_args(W, H, cam, focal, spp=c.get("spp", 1), snap=0)

@@ -237,6 +237,85 @@ print("ok", tb.training_step, float(tb.loss))
     assert r.stdout.startswith("ok 30")
 
 
+def test_testbed_camera_and_crop_box_api(scene):
+    """The remaining pyngp names on the path (src/python_api.cu:506-523, 560-562, 594-600, 672):
+    crop_box / set_crop_box / crop_box_corners (src/testbed.cu:618-670), fov_xy, raw_aabb, up_dir (loaded from
+    the dataset, kept in snapshots), nerf.find_closest_training_view (src/testbed_nerf.cu:3231-3244),
+    compute_image_mse (the Image mode's: NaN on a NeRF testbed), the extra-dims accessors (n_extra_dims 0)."""
+    import pyngp as ngp
+    root, cams, imgs = scene
+    _, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("tiny_L4F2.json")
+    # raw_aabb = aabb at load; up_dir = the dataset's up
+    assert np.allclose(tb.raw_aabb.min, tb.aabb.min) and np.allclose(tb.raw_aabb.max, tb.aabb.max)
+    assert np.allclose(np.linalg.norm(tb.up_dir), 1.0, atol=1e-5)
+    # fov_xy: per-axis degrees of the relative focal length
+    tb.fov_xy = [40.0, 30.0]
+    np.testing.assert_allclose(tb.fov_xy, [40.0, 30.0], rtol=1e-5)
+    np.testing.assert_allclose(tb.relative_focal_length, [0.5 / np.tan(np.deg2rad(20.0)), 0.5 / np.tan(np.deg2rad(15.0))], rtol=1e-5)
+    # the default crop box is the render aabb: axes = half extents, centre = box centre (NGP space)
+    m = np.asarray(tb.crop_box(False))
+    lo, hi = np.asarray(tb.render_aabb.min), np.asarray(tb.render_aabb.max)
+    np.testing.assert_allclose(m[:, :3], np.diag((hi - lo) / 2), atol=1e-6)
+    np.testing.assert_allclose(m[:, 3], (hi + lo) / 2, atol=1e-6)
+    corners = np.asarray(tb.crop_box_corners(False))
+    assert corners.shape == (8, 3)
+    np.testing.assert_allclose(corners[0], lo, atol=1e-6)
+    np.testing.assert_allclose(corners[7], hi, atol=1e-6)
+    np.testing.assert_allclose(corners[1], [hi[0], lo[1], lo[2]], atol=1e-6)
+    # a rotated box set in NeRF space comes back as set, and its corners are the frame's
+    th = 0.3
+    R = np.array([[np.cos(th), -np.sin(th), 0], [np.sin(th), np.cos(th), 0], [0, 0, 1]], np.float32)
+    box = np.zeros((3, 4), np.float32)
+    box[:, :3] = R * np.array([0.4, 0.3, 0.5], np.float32)
+    box[:, 3] = [0.1, -0.2, 0.05]
+    tb.set_crop_box(box, True)
+    np.testing.assert_allclose(np.asarray(tb.crop_box(True)), box, atol=1e-5)
+    c = np.asarray(tb.crop_box_corners(True))
+    for i in range(8):
+        s_ = np.array([1 if i & 1 else -1, 1 if i & 2 else -1, 1 if i & 4 else -1, 1], np.float32)
+        np.testing.assert_allclose(c[i], box @ s_, atol=1e-5)
+    # the NGP-space box is in the frame render_aabb_to_local: its rows are the box's normalised axes
+    to_local = np.asarray(tb.render_aabb_to_local)
+    np.testing.assert_allclose(to_local @ to_local.T, np.eye(3), atol=1e-5)
+    # find_closest_training_view: the training view a camera sits at
+    for i in (0, 5, 11):
+        tb.set_camera_to_training_view(i)
+        assert tb.nerf.find_closest_training_view() == i
+    # up_dir round-trips through a snapshot
+    tb.up_dir = [0.0, 0.0, 1.0]
+    snap = os.path.join(root, "up.ingp")
+    tb.save_snapshot(snap, False)
+    _, tb2 = new_testbed()
+    tb2.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb2.load_snapshot(snap)
+    np.testing.assert_allclose(tb2.up_dir, [0.0, 0.0, 1.0])
+    # the Image mode's metric on a NeRF testbed; extra dims off
+    assert np.isnan(tb.compute_image_mse(False))
+    assert tb.nerf.training.get_extra_dims(0) == []
+    assert tb.nerf.get_rendering_extra_dims() == []
+    tb.nerf.set_rendering_extra_dims([])
+    assert tb.nerf.rendering_extra_dims_from_training_view == -1
+    with pytest.raises(RuntimeError, match="extra dims"):
+        tb.nerf.set_rendering_extra_dims([1.0])
+    with pytest.raises(RuntimeError, match="does not have extra dims"):
+        tb.nerf.set_rendering_extra_dims_from_training_view(0)
+    # glow renders through the Testbed (nerf.glow_mode / glow_y_cutoff)
+    tb.render_aabb = ngp.BoundingBox(list(lo), list(hi))
+    tb.render_aabb_to_local = np.eye(3, dtype=np.float32)
+    tb.shall_train = True
+    while tb.training_step < 40:
+        tb.frame()
+    tb.set_camera_to_training_view(2)
+    plain = tb.render(48, 48, 1, True)
+    tb.nerf.glow_mode = 1 | 2
+    tb.nerf.glow_y_cutoff = 0.6
+    assert tb.nerf.glow_mode == 3 and tb.nerf.glow_y_cutoff == pytest.approx(0.6)
+    glow = tb.render(48, 48, 1, True)
+    assert np.isfinite(glow).all() and np.abs(glow - plain).mean() > 0
+
+
 def test_network_config_parent_merge(tmp_path):
     ngp, tb = new_testbed()
     tb.create_empty_nerf_dataset(2, aabb_scale=1)

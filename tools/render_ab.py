@@ -26,6 +26,7 @@ def main():
     p.add_argument("--config", default=os.path.join(ROOT, "instant-ngp-rendering_amd", "configs", "nerf", "lego_L16F2.json"))
     p.add_argument("--snapshot", default=None, help="load this snapshot if it exists, else train and save it")
     p.add_argument("--pkg", default=None, help="directory holding another build of pyngp + libngp_hip (tools/ab_build_old.sh)")
+    p.add_argument("--stats", action="store_true", help="one frame per setting with the march statistics (debug bit 0)")
     p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
     a = p.parse_args()
     if a.pkg:
@@ -52,8 +53,10 @@ def main():
         tb.load_snapshot(a.snapshot)  # the same weights and grid as the run that wrote it
     else:
         tb.shall_train = True
+        tb.deterministic = True  # bench.py's reproducible pretraining: the same volume on every box
         for i in range(a.pretrain):
             tb.train(1 << 18)
+        tb.deterministic = False
         if a.snapshot:
             tb.save_snapshot(a.snapshot, False)
     n_views = tb.nerf.training.dataset.n_images
@@ -73,6 +76,17 @@ def main():
                 tb.render_to_device(1920, 1080, 1, True)
             times[s].append((time.perf_counter() - t0) / a.frames * 1e3)
         print(f"# round {r + 1}/{a.rounds}", file=sys.stderr, flush=True)
+    if a.stats:
+        for s in a.settings:
+            setting = dict(base)
+            for kv in s.split():
+                k, v = kv.split("=", 1)
+                setting[k] = float(v) if k == "render_budget_scale" else int(v)
+            setting["debug"] = 1  # per-frame march statistics on stderr
+            tb.set_tuning(setting)
+            print(f"# stats: {s or 'default'}", file=sys.stderr, flush=True)
+            tb.render_to_device(1920, 1080, 1, True)
+        tb.set_tuning(base)
     for s in a.settings:
         t = times[s]
         print(f"{s or 'default':55s} median {statistics.median(t):7.3f} ms/frame  min {min(t):7.3f}  "
