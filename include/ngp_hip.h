@@ -107,8 +107,9 @@ enum {
 	                             [0, n_mlp_params) is used, hash-grid gradients live in GRID_FP16 */
 	NGP_ADAM_M = 5,
 	NGP_ADAM_V = 6,
-	NGP_GRADS_GRID_FP16 = 7,  /* hash-grid gradients [n_params - n_mlp_params], fp16, accumulated with
-	                             packed half2 atomics like tcnn's GridEncoding backward */
+	NGP_GRADS_GRID_FP16 = 7,  /* hash-grid gradients [n_params - n_mlp_params], fp16 as tcnn's GridEncoding
+	                             backward keeps them; each backward adds into it (binned LDS sums, or packed
+	                             half2 atomics with ngp_tuning.encode_bwd_binned = 1) */
 	NGP_GRADS_GRID_FIXED64 = 8/* the same in deterministic steps: int64 fixed point, value = v * 2^-40 (allocated on the
 	                             first deterministic step; null before) */
 };
@@ -354,6 +355,10 @@ typedef struct ngp_tuning {
 	                                    by k_generate), 2 = computes every reserved slot; 0: the default (1) */
 	uint32_t render_exit_cap;        /* 1 = a ray reserves at most the lattice points left to its AABB exit in a march
 	                                    pass, 2 = the per-ray cap alone; 0: the default */
+	uint32_t encode_bwd_binned;      /* hash-grid backward (F = 2): 1 = packed half2 (fixed point: 64-bit) atomics per corner
+	                                    run (the default, 0), 2 = the hashed levels binned (corner contributions
+	                                    partitioned by table bin, summed in LDS) and the dense ones atomic, 3 = every
+	                                    level binned (measured slower: DESIGN.md §3) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -586,7 +586,11 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(SHIN ? (const void*)a.sh_ray : (const void*)a.coords, DENSITY_ONLY ? 0u : a.coord_bytes);
 	const __amdgpu_buffer_rsrc_t sh_rs = make_rsrc(a.sh, SHIN && !DENSITY_ONLY ? a.sh_bytes : 0u);
 	constexpr bool SHR = SHIN && !DENSITY_ONLY;
-	RawTile<N, CT_> ring[PF];
+	// PF tiles' loads in flight in a ring of PF + 1 slots, the loop unrolled PF + 1 times so every slot
+	// index is static: step q consumes slot q and loads tile t + PF stride into the slot step q - 1
+	// consumed -- no register copies between the ring and the tile being computed
+	constexpr int R = PF + 1;
+	RawTile<N, CT_> ring[R];
 #pragma unroll
 	for (int q = 0; q < PF; ++q) {
 		const uint32_t t = t0 + q * stride;
@@ -595,21 +599,19 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	if constexpr (SHR) {
 		if (t0 < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[0]);
 	}
-	for (uint32_t tb = t0; tb < n_tiles; tb += PF * stride) {
+	for (uint32_t tb = t0; tb < n_tiles; tb += R * stride) {
 #pragma unroll
-		for (int q = 0; q < PF; ++q) {
+		for (int q = 0; q < R; ++q) {
 			const uint32_t t = tb + q * stride;
-			if (t < n_tiles) {
-				RawTile<N, CT_> cur = ring[q];
-				const uint32_t tn = t + PF * stride;
-				if (tn < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, tn * TS, g, n, ring[q], !DENSITY_ONLY);
-				if constexpr (SHR) {
-					// SH rows of the next tile to consume (its row indices arrived a stage ago); with
-					// PF = 1 that is the tile just loaded into this slot
-					if (t + stride < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[(q + 1) % PF]);
-				}
-				rf_tile<N, CT_, PF, DENSITY_ONLY, SHIN>(a, wl, cur, t * TS, g, n);
+			if (t >= n_tiles) break;
+			const uint32_t tn = t + PF * stride;
+			if (tn < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, tn * TS, g, n, ring[(q + PF) % R], !DENSITY_ONLY);
+			if constexpr (SHR) {
+				// SH rows of the next tile to consume (its row indices were issued with its encoding; with
+				// PF = 1 that is the tile just loaded)
+				if (t + stride < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[(q + 1) % R]);
 			}
+			rf_tile<N, CT_, PF, DENSITY_ONLY, SHIN>(a, wl, ring[q], t * TS, g, n);
 		}
 	}
 }

@@ -1932,11 +1932,13 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, internal_layout(m, B), ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
-	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
+	// the binned backward is several kernels: timed with event records around them
+	if (hashgrid_bwd_binned(lt_c, B, ts.fixed)) tm.begin(NGP_TIMER_TRAIN_ENCODE_BWD, s);
+	else tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
 	// data parallel: launched for about this rank's share of the global batch (blocks loop past it)
 	const uint32_t bwd_chunks = world > 1 ? div_up(B / world + B / (4 * world), 128u) + 16 : 0u;
 	launch_hashgrid_bwd(lt_c, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->grid_grads16.ptr, s,
-	                    ts.counters.ptr + 5, ts.fixed ? m->grid_grads64.ptr : nullptr, bwd_chunks);
+	                    ts.counters.ptr + 5, ts.fixed ? m->grid_grads64.ptr : nullptr, bwd_chunks, &m->bins);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	if (cam) {
 		// input gradients of the compacted samples (Trainer::training_step with dL_dinput), then

@@ -59,7 +59,9 @@ CASES = {
     # Nerf::glow_mode / glow_y_cutoff (composite_kernel_nerf's glow, src/testbed_nerf.cu:540-628)
     "glow_grid_cutline": dict(glow=1 | 2, cutoff=0.55),
     "glow_mask_to_alpha": dict(glow=1 | 2 | 4, cutoff=0.5),
-    "glow_radial": dict(glow=1 | 8, cutoff=0.4),
+    # radial: dist = min(|pos - camera|, (4.5 - y) / 3), 1.03-1.33 on the sphere's visible side; the glow lives in
+    # the shell dist in (cutoff - 21/80, cutoff)
+    "glow_radial": dict(glow=1 | 2 | 8, cutoff=1.3),
     "glow_grid_mode": dict(glow=16),
     "glow_positions": dict(glow=1 | 4, cutoff=0.6, mode=A.RENDER_POSITIONS),
 }

@@ -3,7 +3,7 @@ every kernel timer on and prints the mean launch time of each timer class.  Run 
 (--pkg: a directory with another build of pyngp + libngp_hip, tools/ab_build_old.sh) to compare
 kernels on one box.
 
-Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400] [--settings "mlp_train_schedule=1" "mlp_train_schedule=2"]
+Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400] [--settings "" "encode_bwd_binned=1"]
 (--settings: ngp_tuning fields per setting, timed round-robin on the same trained model)
 """
 import argparse
@@ -22,6 +22,7 @@ def main():
     p.add_argument("--timed", type=int, default=100)
     p.add_argument("--rounds", type=int, default=3)
     p.add_argument("--settings", nargs="*", default=[""])
+    p.add_argument("--deterministic", action="store_true", help="fixed-point hash-grid gradients in every step")
     p.add_argument("--config", default=os.path.join(ROOT, "instant-ngp-rendering_amd", "configs", "nerf", "lego_L16F2.json"))
     p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
     a = p.parse_args()
@@ -34,6 +35,7 @@ def main():
     tb.load_training_data(a.scene)
     tb.reload_network_from_file(a.config)
     tb.shall_train = True
+    tb.deterministic = a.deterministic
     for _ in range(a.steps):
         tb.train(1 << 18)
     lib = A.load(os.path.join(os.path.abspath(a.pkg), "libngp_hip.so")) if a.pkg else A.load()
