@@ -12,7 +12,7 @@ for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name, q,
                  int(r.get("Grid_Size_X", r.get("Grid_Size", 0)) or 0)))
 rows.sort()
-starts = [i for i, r in enumerate(rows) if "k_occupancy_summary" in r[2]]
+starts = [i for i, r in enumerate(rows) if "k_dense_records" in r[2]]
 seg = rows[starts[-2]:starts[-1]]
 last = max(i for i, r in enumerate(seg) if "k_shade" in r[2])
 seg = seg[:last + 1]

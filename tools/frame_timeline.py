@@ -1,5 +1,5 @@
 """Summarise a rocprofv3 kernel trace of tools/probe_render.py-style runs: for the last
-render frame (k_occupancy_summary .. k_accum_tonemap), list every kernel with its start
+render frame (k_dense_records .. k_accum_tonemap), list every kernel with its start
 offset, duration and the idle gap before it (diagnostic).
 Usage: python tools/frame_timeline.py <kernel_trace.csv> [out.txt]"""
 import csv
@@ -9,7 +9,7 @@ rows = []
 for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"].split("(")[0].replace("void ", "")))
 rows.sort()
-starts = [i for i, r in enumerate(rows) if "k_occupancy_summary" in r[2]]
+starts = [i for i, r in enumerate(rows) if "k_dense_records" in r[2]]
 s = starts[-2] if len(starts) > 1 else starts[-1]
 e = next(i for i in range(s, len(rows)) if "k_shade" in rows[i][2] or "k_accum_tonemap" in rows[i][2])
 out = []

@@ -1,5 +1,5 @@
 """Overlap of the render's kernels on the GPU from a rocprofv3 kernel trace (diagnostic): for each
-of the last frames (k_occupancy_summary .. the last k_shade), the frame span, the time with 0, 1,
+of the last frames (k_dense_records .. the last k_shade), the frame span, the time with 0, 1,
 2, 3+ kernels in flight, and per kernel class the summed duration and the time it ran alone.
 Usage: python tools/render_timeline.py <kernel_trace.csv> [frames] [out.txt]"""
 import collections
@@ -12,7 +12,7 @@ for r in csv.DictReader(open(sys.argv[1])):
     rows.append((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), name))
 rows.sort()
 nf = int(sys.argv[2]) if len(sys.argv) > 2 else 3
-starts = [i for i, r in enumerate(rows) if "k_occupancy_summary" in r[2]]
+starts = [i for i, r in enumerate(rows) if "k_dense_records" in r[2]]
 out = []
 
 
