@@ -348,7 +348,7 @@ typedef struct ngp_tuning {
 	uint32_t encode_streaming;       /* hash encoder (F = 2 planes): 0 = non-temporal encoding stores (the default), 1 = plain */
 	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
 	                                    by cell, coherent gathers; same grid) */
-	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16, 4 = 64; 0: 4 */
+	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16, 2 = 32, 4 = 64; 0: 2 */
 	uint32_t encode_xcd_regions;     /* four-levels-per-thread hash encoder: 0 = each XCD encodes one contiguous eighth of
 	                                    the samples (the default), 1 = XCD x takes every eighth chunk */
 	uint32_t render_skip_unfilled;   /* 1 = the render MLP skips 16-sample column tiles of slots no ray filled (marked

@@ -1150,13 +1150,17 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		const uint32_t wg_per_cu = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : 8u;
 		const uint32_t grid = std::min<uint32_t>(div_up(n, 16 * WAVES), cu_count() * wg_per_cu);
 		const bool pl = a.enc_lsh == 2;
-		// the renderer's path: one 16-sample tile per wave step, prefetch two ahead (2-tile steps and
-		// prefetch depths 1 / 3 measured slower)
-		// render MLP steps of 64 samples per wave (4 column tiles share each weight fragment read from LDS:
-		// the 16-sample steps were LDS-bandwidth bound, 20 ds_read_b128 per 20 MFMAs); -4 % frame time
-		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : 4u;
+		// the renderer's path.  Wave steps of 16 * CT samples: the CT column tiles share each weight fragment
+		// read from LDS (16-sample steps were LDS-bandwidth bound, 20 ds_read_b128 per 20 MFMAs).  64-sample
+		// steps (CT = 4, -4 % frame time against 16 in round 3) hold 194 VGPRs: 2 waves per SIMD, MFMA busy
+		// 0.40 of the CU cycles (profiles/r04_pmc_mlp.txt); 32-sample steps (CT = 2, the default since round 4)
+		// 110 VGPRs: 4 waves per SIMD, MFMA busy 0.46, frame time equal on the fire scene and -2.5 % on the
+		// surface scene (profiles/r04_mlp_tile_ab.txt)
+		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : 2u;
 		if (sh && a.F == 2 && pl && tile == 4)
 			launch_timed(k_mlp_infer_rf<N, 4, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 64 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
+		else if (sh && a.F == 2 && pl && tile == 2)
+			launch_timed(k_mlp_infer_rf<N, 2, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);
 		else if (sh && a.F == 4 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 14, true>, grid, BLOCK, lds, s, a);
 		// element-wise loads read K in natural order: only valid where k_pack did not permute the

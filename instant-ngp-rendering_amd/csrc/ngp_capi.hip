@@ -78,7 +78,8 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->mlp_workgroups_per_cu <= 32, "mlp_workgroups_per_cu must be <= 32");
 	require(t->encode_streaming <= 1, "encode_streaming must be 0 or 1");
 	require(t->grid_unsorted <= 1, "grid_unsorted must be 0 or 1");
-	require(t->render_mlp_tile == 0 || t->render_mlp_tile == 1 || t->render_mlp_tile == 4, "render_mlp_tile must be 0, 1 or 4");
+	require(t->render_mlp_tile == 0 || t->render_mlp_tile == 1 || t->render_mlp_tile == 2 || t->render_mlp_tile == 4,
+	        "render_mlp_tile must be 0, 1, 2 or 4");
 	require(t->encode_xcd_regions <= 1, "encode_xcd_regions must be 0 or 1");
 	require(t->render_skip_unfilled <= 2, "render_skip_unfilled must be 0, 1 or 2");
 	require(t->render_exit_cap <= 2, "render_exit_cap must be 0, 1 or 2");

@@ -364,6 +364,7 @@ struct RenderScratch {
 	uint64_t df_version = ~0ull;
 	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;
+	float last_samples_per_ray = 0.0f;  // network samples per ray of the last full Shade frame (0: none yet)
 	void release() {
 		for (auto& p : pipe) p.release();
 		dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();

@@ -916,9 +916,14 @@ static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_c
 // rays).  The pipelines take interleaved 8-row blocks of the frame and run their passes on their
 // own streams: one pipeline's latency-bound march kernels overlap another's encoder
 // (texture-addresser bound) and MLP (matrix cores).  Every ray composites its own samples in
-// order, so the image does not depend on the split.
-static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard) {
-	uint32_t p = n >= (1u << 16) ? 2u : 1u;
+// order, so the image does not depend on the split.  A scene whose rays stop after a few samples
+// (surfaces: the lego-shaped scene's frames carry ~4 network samples per ray) has little encoder
+// and MLP work to overlap with: there one pipeline measured 2.7 % faster per 1080p frame against two
+// (profiles/r04_mlp_tile_ab.txt), a ~45-sample volume 6 % slower, so the default follows the
+// samples per ray of the model's last frame.
+constexpr float ONE_PIPE_SAMPLES_PER_RAY = 12.0f;
+static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard, float last_spr) {
+	uint32_t p = n >= (1u << 16) && !(last_spr > 0.0f && last_spr < ONE_PIPE_SAMPLES_PER_RAY) ? 2u : 1u;
 	if (t.render_pipelines) p = std::min<uint32_t>(t.render_pipelines, RenderScratch::MAX_PIPES);
 	return std::max(1u, std::min(p, div_up(h_shard, 8u)));  // every pipeline gets rows
 }
@@ -1050,7 +1055,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		return;
 	}
 	const ngp_tuning& tu = m->tuning;
-	const uint32_t n_pipes = render_pipes(tu, k.W * H_shard, H_shard);
+	const uint32_t n_pipes = render_pipes(tu, k.W * H_shard, H_shard, rs.last_samples_per_ray);
 
 	const uint32_t target = pass_sample_target(tu), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu), cap);
 	const bool debug = (tu.debug & 1u) != 0;
@@ -1267,6 +1272,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 	}
 
+	uint64_t filled_total = 0;
 	for (uint32_t j = 0; j < n_pipes; ++j) {
 		PipeRun& pr = pipes[j];
 		if (pr.pass == 0) continue;  // no rays
@@ -1279,6 +1285,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		// [3]: filled samples of the pipeline's rays (the encoder / MLP skip the unfilled slots' work)
 		tm.add_units(NGP_TIMER_RENDER_ENCODE, last[3]);
 		tm.add_units(NGP_TIMER_RENDER_MLP, last[3]);
+		filled_total += last[3];
 		if (n_alive > 0) {
 			// march budget exhausted: still-alive rays are shaded with what they accumulated
 			k_retire<<<div_up(n_alive, 256), 256, 0, pr.s>>>(n_alive, pr.P(pr.cur), pr.C(pr.cur), pr.ps->depth[pr.cur].ptr,
@@ -1299,6 +1306,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		NGP_HIP_CHECK(hipGetLastError());
 	}
 	joiner.join();
+	// the next frame's default pipeline count (render_pipes) follows this one's samples per ray
+	if (k.mode == NGP_RENDER_MODE_SHADE && k.W * H_shard >= (1u << 16)) rs.last_samples_per_ray = (float)filled_total / (float)(k.W * H_shard);
 	if (debug) {
 		uint32_t d[8];
 		NGP_HIP_CHECK(hipMemcpyAsync(d, dbg, sizeof(d), hipMemcpyDeviceToHost, s));

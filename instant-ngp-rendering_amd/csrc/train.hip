@@ -1503,8 +1503,10 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 	a.grad = m->grads.ptr;
 	a.grad16 = m->grid_grads16.ptr;
 	a.grad64 = m->ts.fixed ? m->grid_grads64.ptr : nullptr;
-	// a chunked training step's violation word gates its update (ngp_train_discard re-runs it)
-	a.skip = m->ts.chunked && m->ts.counters.ptr ? m->ts.counters.ptr + 9 : nullptr;
+	// the step's violation word gates its update (ngp_train_discard re-runs it): the chunked forward's early
+	// stops and, in data-parallel training, VIOL_CAPACITY (a rank's share did not fit its buffers) -- which the
+	// full forward can raise too, so the gate does not depend on the forward's mode
+	a.skip = m->ts.counters.ptr ? m->ts.counters.ptr + 9 : nullptr;
 	if (a.skip) m->ts.gated_optimizer_ran = true;
 	a.m = m->adam_m.ptr;
 	a.v = m->adam_v.ptr;

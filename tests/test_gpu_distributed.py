@@ -261,15 +261,28 @@ def test_ranks_train_like_one_process_with_world_times_the_batch(scene, world, c
     # same Adam step); the step-1 MLP gradients only differ in association
     np.testing.assert_array_equal(res[0][1]["params"][n_mlp:], single[1]["params"][n_mlp:])
     s, d = single[EQ_STEPS], res[0][EQ_STEPS]
+    if tuning:
+        # the retried steps are the steps a run without retries takes: the same ranks, partition and integer /
+        # fixed-order sums, so after EQ_STEPS the parameters, statistics and losses are bit-identical to it (the
+        # retry-free four-rank run is compared with one process by the 4-lego case)
+        plain = _spawn(_equivalence_worker, scene, world, config, None)
+        for r in range(world):
+            for step in EQ_EXACT + (EQ_STEPS,):
+                np.testing.assert_array_equal(res[r][step]["params"], plain[r][step]["params"], err_msg=f"rank {r} step {step}")
+                np.testing.assert_array_equal(res[r][step]["bits"], plain[r][step]["bits"])
+                assert res[r][step]["stats"]["measured_batch_size"] == plain[r][step]["stats"]["measured_batch_size"]
+            np.testing.assert_array_equal(res[r]["losses"], plain[r]["losses"])
+        return
     # the trajectories drift apart with the association of the MLP sums (measured 1.6 % in the batch sizes at four
     # ranks); one frame's loss is one batch's and moves with the drift (a single step read 19 % apart at four
     # ranks), so the losses are compared as the mean over the last EQ_WINDOW frames' global batches
+    losses = res[0]["losses"]
     print("batch", [(d["stats"][k], s["stats"][k]) for k in ("measured_batch_size", "measured_batch_size_before_compaction")],
-          "window loss", np.mean(d["losses"]), np.mean(single_losses))
+          "window loss", np.mean(losses), np.mean(single_losses))
     for k in ("measured_batch_size", "measured_batch_size_before_compaction"):
         assert d["stats"][k] == pytest.approx(s["stats"][k], rel=1e-2 if world == 2 else 3e-2), k
-    assert len(d["losses"]) == len(single_losses) == EQ_WINDOW
-    assert np.mean(d["losses"]) == pytest.approx(np.mean(single_losses), rel=3e-2 if world == 2 else 8e-2)
+    assert len(losses) == len(single_losses) == EQ_WINDOW
+    assert np.mean(losses) == pytest.approx(np.mean(single_losses), rel=3e-2 if world == 2 else 8e-2)
 
 
 def _n_mlp(tb):

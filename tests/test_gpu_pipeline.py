@@ -587,7 +587,7 @@ def test_render_config_e_full_network_matches_oracle():
         assert (of[..., 3] > 0.01).mean() > 0.1
         l1 = np.abs(gf - of).mean()
         assert l1 < 1e-3, l1
-        # the render MLP's 16- and 64-sample steps (render_mlp_tile), the encoder's XCD-region mapping and plain
+        # the render MLP's 16-, 32- and 64-sample steps (render_mlp_tile), the encoder's XCD-region mapping and plain
         # stores, one to four ray pipelines, the per-ray exit cap and the render MLP computing every reserved slot
         # instead of skipping tiles no ray filled render the same frame bit for bit
         for kw in (dict(render_mlp_tile=1), dict(render_mlp_tile=4, encode_xcd_regions=1),
@@ -595,7 +595,7 @@ def test_render_config_e_full_network_matches_oracle():
                    dict(encode_streaming=0, render_pipelines=3), dict(render_pipelines=4, render_exit_cap=2),
                    dict(render_pipelines=0, render_exit_cap=1), dict(render_skip_unfilled=2),
                    dict(render_skip_unfilled=1, render_mlp_tile=1), dict(render_skip_unfilled=0, render_mlp_tile=0),
-                   dict(render_exit_cap=0)):
+                   dict(render_exit_cap=0), dict(render_mlp_tile=4), dict(render_mlp_tile=2, render_skip_unfilled=2)):
             g.set_tuning(**kw)
             frame.zero_()
             A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
