@@ -108,8 +108,7 @@ enum {
 	NGP_ADAM_M = 5,
 	NGP_ADAM_V = 6,
 	NGP_GRADS_GRID_FP16 = 7,  /* hash-grid gradients [n_params - n_mlp_params], fp16 as tcnn's GridEncoding
-	                             backward keeps them; each backward adds into it (binned LDS sums, or packed
-	                             half2 atomics with ngp_tuning.encode_bwd_binned = 1) */
+	                             backward keeps them; each backward adds into it (packed half2 atomics) */
 	NGP_GRADS_GRID_FIXED64 = 8/* the same in deterministic steps: int64 fixed point, value = v * 2^-40 (allocated on the
 	                             first deterministic step; null before) */
 };
@@ -348,17 +347,14 @@ typedef struct ngp_tuning {
 	uint32_t encode_streaming;       /* hash encoder (F = 2 planes): 0 = non-temporal encoding stores (the default), 1 = plain */
 	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
 	                                    by cell, coherent gathers; same grid) */
-	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16, 2 = 32, 4 = 64; 0: 2 */
+	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16, 2 = 32, 4 = 64; 0: 64 with two or more
+	                                    ray pipelines, 32 with one */
 	uint32_t encode_xcd_regions;     /* four-levels-per-thread hash encoder: 0 = each XCD encodes one contiguous eighth of
 	                                    the samples (the default), 1 = XCD x takes every eighth chunk */
 	uint32_t render_skip_unfilled;   /* 1 = the render MLP skips 16-sample column tiles of slots no ray filled (marked
 	                                    by k_generate), 2 = computes every reserved slot; 0: the default (1) */
 	uint32_t render_exit_cap;        /* 1 = a ray reserves at most the lattice points left to its AABB exit in a march
 	                                    pass, 2 = the per-ray cap alone; 0: the default */
-	uint32_t encode_bwd_binned;      /* hash-grid backward (F = 2): 1 = packed half2 (fixed point: 64-bit) atomics per corner
-	                                    run (the default, 0), 2 = the hashed levels binned (corner contributions
-	                                    partitioned by table bin, summed in LDS) and the dense ones atomic, 3 = every
-	                                    level binned (measured slower: DESIGN.md §3) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -263,195 +263,6 @@ __global__ void __launch_bounds__(256) k_hashgrid_bwd(uint32_t n, const float* _
 }
 
 
-// ---- Binned backward (F = 2; ngp_tuning.encode_bwd_binned) -----------------------------------
-// The atomics above are memory-side: every corner contribution is a device-scope read-modify-write
-// into the table, which bounds that kernel far below HBM bandwidth.  Instead, per level, the
-// contributions are partitioned by table bin (an LDS-sized slice of the level's gradient table):
-//   1. k_bwd_bins<false>: per workgroup, LDS counts of its contributions per bin -> hist[bin][group]
-//   2. exclusive scan of hist (bin-major): each (bin, group) gets its range of the pair array
-//   3. k_bwd_bins<true>: the same walk again, each contribution written as an (entry, value) pair
-//      at its LDS cursor -- the pairs a workgroup sends to one bin are contiguous in HBM
-//   4. k_bwd_bin_sum: one workgroup per bin sums the bin's pairs in an LDS tile and adds the tile
-//      into the table with coalesced loads and stores -- no global atomics
-// fp16 gradients: (entry, half2) pairs -- each contribution rounded to fp16, as the atomics' operands
-// are -- 2 x 8 B per corner plus one pass over the table, all streaming; 8192-entry bins summed in fp32
-// (ds_add_f32) and rounded once, at least as exact as the atomics' fp16 running sums.  Deterministic
-// mode (FIXED): (entry, float2) pairs of 16 B; 4096-entry bins summed as 2^-40 fixed point with 64-bit
-// LDS integer adds (ds_add_u64) of each contribution rounded exactly as the atomic path rounds it
-// (to_fixed), so the sums are the atomic path's bit for bit and independent of the pairs' order.
-constexpr uint32_t BIN_MAX = 4096;    // bins per level: tables up to 2^24 entries
-constexpr uint32_t BIN_GROUPS = 256;  // workgroups per level in the count and partition passes
-template <bool FIXED>
-struct BinGeom {
-	static constexpr uint32_t BITS = FIXED ? 12 : 13, ENTRIES = 1u << BITS;
-};
-
-struct BinPlan {
-	uint32_t first, n_lv, bits;        // binned levels [first, first + n_lv); log2 entries per bin
-	uint32_t bin0[MAX_LEVELS + 1];     // first global bin of binned level h (prefix; [n_lv] = total)
-};
-
-static BinPlan make_bin_plan(const LevelTable& lt, uint32_t first, uint32_t bits) {
-	BinPlan p{};
-	p.first = first;
-	p.n_lv = lt.n_levels - first;
-	p.bits = bits;
-	for (uint32_t h = 0; h < p.n_lv; ++h) p.bin0[h + 1] = p.bin0[h] + div_up(lt.size[first + h], 1u << bits);
-	return p;
-}
-
-typedef _Float16 half2_t __attribute__((ext_vector_type(2)));
-
-template <bool PARTITION, bool WIDE>
-__global__ void __launch_bounds__(256) k_bwd_bins(uint32_t n, const float* __restrict__ pos, uint32_t stride,
-                                                  const __half* __restrict__ denc, EncLayout lay, const LevelTable lt,
-                                                  const BinPlan plan, uint32_t* __restrict__ hist,
-                                                  uint2* __restrict__ pairs, const uint32_t* __restrict__ n_dev) {
-	__shared__ uint32_t cnt[BIN_MAX];
-	const uint32_t grp = blockIdx.x % BIN_GROUPS, h = blockIdx.x / BIN_GROUPS, level = plan.first + h;
-	const uint32_t nb = plan.bin0[h + 1] - plan.bin0[h], bits = plan.bits;
-	uint32_t* hrow = hist + (size_t)plan.bin0[h] * BIN_GROUPS + grp;  // entry of bin b: hrow[b * BIN_GROUPS]
-	for (uint32_t b = threadIdx.x; b < nb; b += 256u) cnt[b] = PARTITION ? hrow[(size_t)b * BIN_GROUPS] : 0u;
-	__syncthreads();
-	if (n_dev) n = min(n, *n_dev);
-	const float scale = lt.scale[level];
-	const uint32_t res = lt.res[level], size = lt.size[level], hashed = lt.hashed[level];
-	for (uint32_t c = grp; c * 256u < n; c += BIN_GROUPS) {  // block-uniform
-		const uint32_t i = c * 256u + threadIdx.x;
-		if (i >= n || lt.level_cut(level, i)) continue;
-		float g[2];
-		unpack<2>(reinterpret_cast<const uint32_t*>(denc)[lay.vec(level, i)], g);
-		if (g[0] == 0.0f && g[1] == 0.0f) continue;
-		float fx, fy, fz;
-		uint32_t gx, gy, gz;
-		pos_fract(pos[(size_t)i * stride + 0], scale, &fx, &gx);
-		pos_fract(pos[(size_t)i * stride + 1], scale, &fy, &gy);
-		pos_fract(pos[(size_t)i * stride + 2], scale, &fz, &gz);
-#pragma unroll
-		for (uint32_t k = 0; k < 8; ++k) {
-			const uint32_t idx = grid_index(hashed, size, res, gx + (k & 1u), gy + ((k >> 1) & 1u), gz + (k >> 2));
-			if constexpr (PARTITION) {
-				float w = (k & 1u) ? fx : 1.0f - fx;
-				w *= (k & 2u) ? fy : 1.0f - fy;
-				w *= (k & 4u) ? fz : 1.0f - fz;
-				const uint32_t at = atomicAdd(&cnt[idx >> bits], 1u);
-				if constexpr (WIDE) {
-					reinterpret_cast<uint4*>(pairs)[at] =
-					    make_uint4(idx, __float_as_uint(w * g[0]), __float_as_uint(w * g[1]), 0u);
-				} else {
-					const half2_t v = {(_Float16)(w * g[0]), (_Float16)(w * g[1])};
-					pairs[at] = make_uint2(idx, __builtin_bit_cast(uint32_t, v));
-				}
-			} else {
-				atomicAdd(&cnt[idx >> bits], 1u);
-			}
-		}
-	}
-	if constexpr (!PARTITION) {
-		__syncthreads();
-		for (uint32_t b = threadIdx.x; b < nb; b += 256u) hrow[(size_t)b * BIN_GROUPS] = cnt[b];
-	}
-}
-
-constexpr uint32_t BIN_SUM_THREADS = 512;
-template <bool FIXED>
-__global__ void __launch_bounds__(BIN_SUM_THREADS) k_bwd_bin_sum(const uint32_t* __restrict__ scan,
-                                                                 const uint2* __restrict__ pairs, const LevelTable lt,
-                                                                 const BinPlan plan, __half* __restrict__ grad,
-                                                                 long long* __restrict__ grad64) {
-	using G = BinGeom<FIXED>;
-	using Acc = typename std::conditional<FIXED, unsigned long long, float>::type;
-	__shared__ Acc tile[2 * G::ENTRIES];  // 64 KiB: entry e's features at 2e, 2e + 1
-	const uint32_t gb = blockIdx.x;
-	uint32_t h = 0;
-	while (gb >= plan.bin0[h + 1]) ++h;
-	const uint32_t level = plan.first + h, e0 = (gb - plan.bin0[h]) << G::BITS;
-	const uint32_t begin = scan[(size_t)gb * BIN_GROUPS], end = scan[(size_t)(gb + 1) * BIN_GROUPS];
-	for (uint32_t e = threadIdx.x; e < 2 * G::ENTRIES; e += BIN_SUM_THREADS) tile[e] = Acc(0);
-	__syncthreads();
-	constexpr uint32_t U = 4;  // pairs in flight per thread
-	for (uint32_t p0 = begin; p0 < end; p0 += U * BIN_SUM_THREADS) {
-		uint4 r[U];
-#pragma unroll
-		for (uint32_t u = 0; u < U; ++u) {
-			const uint32_t p = p0 + u * BIN_SUM_THREADS + threadIdx.x;
-			if constexpr (FIXED) {
-				r[u] = p < end ? reinterpret_cast<const uint4*>(pairs)[p] : make_uint4(0u, 0u, 0u, 0u);
-			} else {
-				const uint2 q = p < end ? pairs[p] : make_uint2(0u, 0u);
-				r[u] = make_uint4(q.x, q.y, 0u, 0u);
-			}
-		}
-#pragma unroll
-		for (uint32_t u = 0; u < U; ++u) {
-			if (p0 + u * BIN_SUM_THREADS + threadIdx.x >= end) break;
-			Acc* t = &tile[2 * (r[u].x & (G::ENTRIES - 1u))];
-			if constexpr (FIXED) {
-				atomicAdd(t, (unsigned long long)to_fixed(__uint_as_float(r[u].y)));
-				atomicAdd(t + 1, (unsigned long long)to_fixed(__uint_as_float(r[u].z)));
-			} else {
-				const half2_t v = __builtin_bit_cast(half2_t, r[u].y);
-				atomicAdd(t, (float)v.x);
-				atomicAdd(t + 1, (float)v.y);
-			}
-		}
-	}
-	__syncthreads();
-	const uint32_t ne = min(G::ENTRIES, lt.size[level] - e0);
-	for (uint32_t e = threadIdx.x; e < ne; e += BIN_SUM_THREADS) {
-		const Acc tx = tile[2 * e], ty = tile[2 * e + 1];
-		if (tx == Acc(0) && ty == Acc(0)) continue;
-		if constexpr (FIXED) {
-			long long* g = grad64 + (size_t)(lt.offset[level] + e0 + e) * 2;
-			const longlong2 o = *reinterpret_cast<const longlong2*>(g);
-			*reinterpret_cast<longlong2*>(g) = make_longlong2(o.x + (long long)tx, o.y + (long long)ty);
-		} else {
-			half2_t* g = reinterpret_cast<half2_t*>(grad) + lt.offset[level] + e0 + e;
-			const half2_t o = *g;
-			*g = half2_t{(_Float16)((float)o.x + tx), (_Float16)((float)o.y + ty)};
-		}
-	}
-}
-
-// first level the binned backward covers (lt.binned_bwd 1: all levels, 2: the hashed levels only), or
-// n_levels when it does not apply
-static uint32_t binned_first_level(const LevelTable& lt, uint32_t n, uint32_t bits) {
-	if (!lt.binned_bwd || lt.F != 2) return lt.n_levels;
-	uint32_t first = 0;
-	if (lt.binned_bwd == 2)
-		while (first < lt.n_levels && !lt.hashed[first]) ++first;
-	uint32_t bins = 0;
-	for (uint32_t l = first; l < lt.n_levels; ++l) {
-		if (lt.size[l] > (BIN_MAX << bits)) return lt.n_levels;
-		bins += div_up(lt.size[l], 1u << bits);
-	}
-	// pair positions and the scan are 32-bit
-	if ((uint64_t)n * 8u * (lt.n_levels - first) >= (1ull << 32) || (uint64_t)bins * BIN_GROUPS >= (1u << 24))
-		return lt.n_levels;
-	return first;
-}
-
-bool hashgrid_bwd_binned(const LevelTable& lt, uint32_t n, bool fixed) {
-	return binned_first_level(lt, n, fixed ? BinGeom<true>::BITS : BinGeom<false>::BITS) < lt.n_levels;
-}
-
-template <bool FIXED>
-static void launch_bwd_binned(const LevelTable& lt, uint32_t first, const float* pos, uint32_t stride, uint32_t n,
-                              const __half* denc, EncLayout lay, __half* grad16, long long* grad64, hipStream_t s,
-                              const uint32_t* n_dev, BinScratch& bs) {
-	const BinPlan plan = make_bin_plan(lt, first, BinGeom<FIXED>::BITS);
-	const uint32_t bins = plan.bin0[plan.n_lv], nh = bins * BIN_GROUPS;
-	bs.hist.reserve(nh);
-	bs.scan.reserve((size_t)nh + 1);
-	bs.block_sums.reserve(div_up(nh, 1024) + 16);
-	bs.pairs.reserve((size_t)n * 8u * plan.n_lv * (FIXED ? 2u : 1u));  // FIXED: 16-B pairs
-	const uint32_t groups = BIN_GROUPS * plan.n_lv;
-	k_bwd_bins<false, FIXED><<<groups, 256, 0, s>>>(n, pos, stride, denc, lay, lt, plan, bs.hist.ptr, nullptr, n_dev);
-	launch_exclusive_scan(bs.hist.ptr, bs.scan.ptr, nh, bs.block_sums.ptr, bs.scan.ptr + nh, s);
-	k_bwd_bins<true, FIXED><<<groups, 256, 0, s>>>(n, pos, stride, denc, lay, lt, plan, bs.scan.ptr, bs.pairs.ptr, n_dev);
-	k_bwd_bin_sum<FIXED><<<bins, BIN_SUM_THREADS, 0, s>>>(bs.scan.ptr, bs.pairs.ptr, lt, plan, grad16, grad64);
-}
-
 // dL/d(position) through the grid (tcnn GridEncoding backward with input gradients, used by the
 // camera gradients): dL/dx_d = sum_l scale_l sum_c dw_c/df_d sum_f dL/denc[l][f] table[c][f].
 // One thread per sample, the training-parameter table; divided by the sample's rollover weight
@@ -634,19 +445,12 @@ static void launch_bwd(const LevelTable& lt, const float* pos, uint32_t stride, 
 
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                          EncLayout enc_plane, __half* grad_table, hipStream_t s, const uint32_t* n_dev, long long* grad64,
-                         uint32_t max_chunks, BinScratch* bins) {
+                         uint32_t max_chunks) {
 	if (n == 0) return;
 	uint32_t n_chunks = div_up(n, BWD_SAMPLES_PER_BLOCK);
 	if (n_dev && max_chunks) n_chunks = std::min(n_chunks, max_chunks);
-	const bool fixed = grad64 != nullptr;
-	const uint32_t first = bins ? binned_first_level(lt, n, fixed ? BinGeom<true>::BITS : BinGeom<false>::BITS) : lt.n_levels;
-	if (fixed) {
-		if (first > 0) launch_bwd<true>(lt, pos, stride, n, denc, enc_plane, nullptr, grad64, s, n_dev, n_chunks, first);
-		if (first < lt.n_levels) launch_bwd_binned<true>(lt, first, pos, stride, n, denc, enc_plane, nullptr, grad64, s, n_dev, *bins);
-	} else {
-		if (first > 0) launch_bwd<false>(lt, pos, stride, n, denc, enc_plane, grad_table, nullptr, s, n_dev, n_chunks, first);
-		if (first < lt.n_levels) launch_bwd_binned<false>(lt, first, pos, stride, n, denc, enc_plane, grad_table, nullptr, s, n_dev, *bins);
-	}
+	if (grad64) launch_bwd<true>(lt, pos, stride, n, denc, enc_plane, nullptr, grad64, s, n_dev, n_chunks, lt.n_levels);
+	else launch_bwd<false>(lt, pos, stride, n, denc, enc_plane, grad_table, nullptr, s, n_dev, n_chunks, lt.n_levels);
 	NGP_HIP_CHECK(hipGetLastError());
 }
 

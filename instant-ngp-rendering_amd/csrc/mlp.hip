@@ -1153,10 +1153,11 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		// the renderer's path.  Wave steps of 16 * CT samples: the CT column tiles share each weight fragment
 		// read from LDS (16-sample steps were LDS-bandwidth bound, 20 ds_read_b128 per 20 MFMAs).  64-sample
 		// steps (CT = 4, -4 % frame time against 16 in round 3) hold 194 VGPRs: 2 waves per SIMD, MFMA busy
-		// 0.40 of the CU cycles (profiles/r04_pmc_mlp.txt); 32-sample steps (CT = 2, the default since round 4)
-		// 110 VGPRs: 4 waves per SIMD, MFMA busy 0.46, frame time equal on the fire scene and -2.5 % on the
-		// surface scene (profiles/r04_mlp_tile_ab.txt)
-		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : 2u;
+		// 0.40 of the CU cycles (profiles/r04_pmc_mlp.txt); 32-sample steps (CT = 2) 110 VGPRs: 4 waves per
+		// SIMD, MFMA busy 0.46.  With two ray pipelines the other pipeline's encoder shares the CUs and the
+		// 64-sample steps measured 0-2 % faster per frame; with one (surface scenes) the 32-sample steps 1-2 %
+		// (profiles/r04_mlp_tile_ab.txt): the renderer picks per frame (RenderScratch::mlp_tile)
+		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : m->rs.mlp_tile;
 		if (sh && a.F == 2 && pl && tile == 4)
 			launch_timed(k_mlp_infer_rf<N, 4, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 64 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl && tile == 2)

@@ -61,7 +61,6 @@ static hipStream_t S(ngp_stream s) { return reinterpret_cast<hipStream_t>(s); }
 static void apply_encode_tuning(LevelTable& lt, const ngp_tuning& t) {
 	lt.streaming = t.encode_streaming == 0 ? 1u : 0u;
 	lt.regions = t.encode_xcd_regions == 0 ? 1u : 0u;
-	lt.binned_bwd = t.encode_bwd_binned == 3 ? 1u : (t.encode_bwd_binned == 2 ? 2u : 0u);
 }
 
 static void validate_tuning(const ngp_tuning* t) {
@@ -83,7 +82,6 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->encode_xcd_regions <= 1, "encode_xcd_regions must be 0 or 1");
 	require(t->render_skip_unfilled <= 2, "render_skip_unfilled must be 0, 1 or 2");
 	require(t->render_exit_cap <= 2, "render_exit_cap must be 0, 1 or 2");
-	require(t->encode_bwd_binned <= 3, "encode_bwd_binned must be 0..3");
 }
 
 // tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.
@@ -259,7 +257,6 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
 		g.skeys.release(); g.perm_in.release(); g.perm.release(); g.sort_tmp.release(); g.spos.release();
 		m->rs.release();
-		m->bins.release();
 		m->timers.release();
 		delete m;
 	});
@@ -435,7 +432,7 @@ ngp_status ngp_model_encode_backward(ngp_model* m, const float* pos, uint32_t st
 	return guarded([&] {
 		require(m && (n == 0 || (pos && denc)), "null argument");
 		launch_hashgrid_bwd(m->lt, pos, stride, n, reinterpret_cast<const __half*>(denc), EncLayout{n, 0},
-		                    m->grid_grads16.ptr, S(s), nullptr, nullptr, 0, &m->bins);
+		                    m->grid_grads16.ptr, S(s));
 	});
 }
 

@@ -156,9 +156,6 @@ struct LevelTable {
 	// 1: each XCD encodes a contiguous eighth of the chunks, level group by level group (four levels per
 	// thread; ngp_tuning.encode_xcd_regions = 0); 0: XCD x takes every eighth chunk
 	uint32_t regions = 0;
-	// backward (F = 2): 1 = every level's corner contributions partitioned by table bin and summed in LDS
-	// (ngp_tuning.encode_bwd_binned = 3), 2 = the hashed levels only (= 2), 0 = atomics (the default)
-	uint32_t binned_bwd = 0;
 	__host__ __device__ bool level_cut(uint32_t level, uint32_t i) const {
 		if (!max_level) return false;
 		// tcnn: max_level = (max_level_gpu[i] * num_grid_features) / N_FEATURES_PER_LEVEL; level >= max_level + 1e-3f
@@ -294,16 +291,6 @@ struct TrainScratch {
 	uint32_t rank_cap_hint = 0;
 };
 
-// Binned hash-grid backward (launch_hashgrid_bwd, hashgrid.hip): per-workgroup bin counts, their exclusive scan
-// (one sentinel past the end: the total), the scan's block sums, and the partitioned (entry, half2 value) pairs
-struct BinScratch {
-	DevBuf<uint32_t> hist, scan, block_sums;
-	DevBuf<uint2> pairs;
-	void release() {
-		hist.release(); scan.release(); block_sums.release(); pairs.release();
-	}
-};
-
 struct GridState {
 	DevBuf<float> grid;        // [n_cascades][N]
 	DevBuf<float> tmp;         // [n_cascades][N]
@@ -365,6 +352,7 @@ struct RenderScratch {
 	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;
 	float last_samples_per_ray = 0.0f;  // network samples per ray of the last full Shade frame (0: none yet)
+	uint32_t mlp_tile = 4;              // the render MLP's default wave step (16-sample tiles) for this frame
 	void release() {
 		for (auto& p : pipe) p.release();
 		dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();
@@ -412,7 +400,6 @@ struct ngp_model {
 	ngp::TrainScratch ts;
 	ngp::GridState gs;
 	ngp::RenderScratch rs;
-	ngp::BinScratch bins;
 	ngp_train_stats last_stats{};
 	bool stats_pending = false;
 	ngp::KernelTimers timers;
@@ -449,13 +436,10 @@ void launch_hashgrid_fwd(const LevelTable& lt, const float* pos, uint32_t stride
 // CUs of the current device (cached)
 int cu_count();
 
-// max_chunks > 0: blocks loop over the device count past max_chunks 128-sample chunks.  bins (with
-// lt.binned_bwd, F = 2, fp16 gradients): scratch of the binned backward of the hashed levels; null: atomics only.
+// max_chunks > 0: blocks loop over the device count past max_chunks 128-sample chunks.
 void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                          EncLayout enc_layout, __half* grad_table16, hipStream_t s, const uint32_t* n_dev = nullptr,
-                         long long* grad64 = nullptr, uint32_t max_chunks = 0, BinScratch* bins = nullptr);
-// the backward of n samples runs binned (several kernels: time it with event records, not launch_timed)
-bool hashgrid_bwd_binned(const LevelTable& lt, uint32_t n, bool fixed);
+                         long long* grad64 = nullptr, uint32_t max_chunks = 0);
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
                              float* w, hipStream_t s);
 // mlp.hip

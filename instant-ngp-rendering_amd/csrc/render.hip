@@ -1056,6 +1056,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	}
 	const ngp_tuning& tu = m->tuning;
 	const uint32_t n_pipes = render_pipes(tu, k.W * H_shard, H_shard, rs.last_samples_per_ray);
+	// render-MLP wave steps (ngp_tuning.render_mlp_tile 0): 64 samples while another pipeline's encoder shares
+	// the CUs (194 VGPRs: 2 waves per SIMD leave it room), 32 with one pipeline (110 VGPRs, 4 waves per SIMD)
+	rs.mlp_tile = n_pipes > 1 ? 4u : 2u;
 
 	const uint32_t target = pass_sample_target(tu), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu), cap);
 	const bool debug = (tu.debug & 1u) != 0;

@@ -1353,10 +1353,14 @@ __device__ __forceinline__ void optimize_one(const OptArgs& a, uint64_t i) {
 		a.w32[i] = w;
 		a.w16[i] = __float2half(w);
 	}
-	if (graw != 0.0f) {  // GradientMode::Overwrite for the next step
-		if (is_mlp) a.grad[i] = 0.0f;
-		else if (a.grad64) a.grad64[i - a.n_mlp] = 0;
-		else a.grad16[i - a.n_mlp] = __float2half(0.0f);
+	// GradientMode::Overwrite for the next step; a fixed-point sum that rounds to fp16 zero is cleared too (its
+	// residue must not carry into the next step's sum)
+	if (is_mlp) {
+		if (graw != 0.0f) a.grad[i] = 0.0f;
+	} else if (a.grad64) {
+		if (a.grad64[i - a.n_mlp] != 0) a.grad64[i - a.n_mlp] = 0;
+	} else if (graw != 0.0f) {
+		a.grad16[i - a.n_mlp] = __float2half(0.0f);
 	}
 	const float e = ema_update(a, a.ema32[i], w);
 	a.ema32[i] = e;
@@ -1406,6 +1410,7 @@ __global__ void __launch_bounds__(256) k_optimizer8(OptArgs a) {
 	const bool is_mlp = i0 < a.n_mlp;
 	const uint64_t gi = i0 - a.n_mlp;
 	float g[8];
+	bool q_nz = false;  // fixed point: any raw sum non-zero (one that rounds to fp16 zero is cleared as well)
 	if (is_mlp) {
 		ld8(a.grad + i0, g);
 	} else if (a.grad64) {
@@ -1415,6 +1420,7 @@ __global__ void __launch_bounds__(256) k_optimizer8(OptArgs a) {
 			const longlong2 t = q[k];
 			g[2 * k] = fixed_grad(t.x);
 			g[2 * k + 1] = fixed_grad(t.y);
+			q_nz |= (t.x | t.y) != 0;
 		}
 	} else {
 		const uint4 u = *reinterpret_cast<const uint4*>(a.grad16 + gi);
@@ -1455,7 +1461,7 @@ __global__ void __launch_bounds__(256) k_optimizer8(OptArgs a) {
 			*reinterpret_cast<uint4*>(a.w16 + i0) = old;
 		}
 	}
-	if (nz) {  // GradientMode::Overwrite for the next step (zeros where they already are change nothing)
+	if (nz || q_nz) {  // GradientMode::Overwrite for the next step (zeros where they already are change nothing)
 		if (is_mlp) reinterpret_cast<float4*>(a.grad + i0)[0] = reinterpret_cast<float4*>(a.grad + i0)[1] = make_float4(0.f, 0.f, 0.f, 0.f);
 		else if (a.grad64) {
 #pragma unroll
@@ -1934,13 +1940,11 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, internal_layout(m, B), ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
 	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr);
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
-	// the binned backward is several kernels: timed with event records around them
-	if (hashgrid_bwd_binned(lt_c, B, ts.fixed)) tm.begin(NGP_TIMER_TRAIN_ENCODE_BWD, s);
-	else tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
+	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
 	// data parallel: launched for about this rank's share of the global batch (blocks loop past it)
 	const uint32_t bwd_chunks = world > 1 ? div_up(B / world + B / (4 * world), 128u) + 16 : 0u;
 	launch_hashgrid_bwd(lt_c, ts.cpos4.ptr, 4, B, ts.denc.ptr, EncLayout{B, 0}, m->grid_grads16.ptr, s,
-	                    ts.counters.ptr + 5, ts.fixed ? m->grid_grads64.ptr : nullptr, bwd_chunks, &m->bins);
+	                    ts.counters.ptr + 5, ts.fixed ? m->grid_grads64.ptr : nullptr, bwd_chunks);
 	tm.end(NGP_TIMER_TRAIN_ENCODE_BWD, s);
 	if (cam) {
 		// input gradients of the compacted samples (Trainer::training_step with dL_dinput), then

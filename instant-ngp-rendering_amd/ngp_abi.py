@@ -116,7 +116,6 @@ class Tuning(C.Structure):
         ("encode_dense_records", C.c_uint32), ("mlp_workgroups_per_cu", C.c_uint32), ("debug", C.c_uint32),
         ("encode_streaming", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
         ("encode_xcd_regions", C.c_uint32), ("render_skip_unfilled", C.c_uint32), ("render_exit_cap", C.c_uint32),
-        ("encode_bwd_binned", C.c_uint32),
     ]
 
 

@@ -234,8 +234,7 @@ def test_deterministic_train_step_gradients_match_oracle_elementwise(cfg_kw):
         assert mlp_rel < 1e-3, mlp_rel
         assert grid_rel < 1e-3, grid_rel
         assert nz.sum() > 1000 and within > 0.999, within
-        # the binned fixed-point backward sums each contribution exactly as the atomic path (default) does
-        g.set_tuning(encode_bwd_binned=2)
+        # integer sums: the same step again gives the same fixed-point gradients bit for bit
         g.zero_grads()
         cuda_memset(gp, nb)
         A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))

@@ -3,7 +3,7 @@ every kernel timer on and prints the mean launch time of each timer class.  Run 
 (--pkg: a directory with another build of pyngp + libngp_hip, tools/ab_build_old.sh) to compare
 kernels on one box.
 
-Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400] [--settings "" "encode_bwd_binned=1"]
+Usage: python tools/train_kernels_ab.py [--pkg DIR] [--steps 400] [--settings "" "mlp_workgroups_per_cu=4"] [--scene synthetic]
 (--settings: ngp_tuning fields per setting, timed round-robin on the same trained model)
 """
 import argparse
@@ -28,11 +28,22 @@ def main():
     a = p.parse_args()
     if a.pkg:
         sys.path.insert(0, os.path.abspath(a.pkg))
+    if a.scene == "synthetic":
+        import torch  # renders the scene's views: its HIP runtime has to start before pyngp's library loads
+
+        torch.cuda.set_device(0)
     import ngp_abi as A
     import pyngp as ngp
 
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
-    tb.load_training_data(a.scene)
+    if a.scene == "synthetic":
+        # bench.py's procedural lego-shaped surface scene (100 views 800x800)
+        sys.path.insert(0, ROOT)
+        sys.path.insert(0, os.path.join(ROOT, "tests"))
+        import bench
+        bench.make_dataset(ngp, tb, argparse.Namespace(scene="synthetic", views=100, train_res=800), "cuda:0")
+    else:
+        tb.load_training_data(a.scene)
     tb.reload_network_from_file(a.config)
     tb.shall_train = True
     tb.deterministic = a.deterministic
