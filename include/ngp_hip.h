@@ -73,9 +73,10 @@ typedef struct ngp_network_config {
 	float ema_decay;
 	uint32_t decay_start, decay_interval;
 	float decay_base;
-	/* NerfNetwork's n_extra_dims (nerf_network.h:81, the dataset's per-image latent code width,
-	 * appended to the rgb network's input): must be 0 -- extra-dims optimisation
-	 * (optimize_extra_dims, default off) is not implemented (ngp_model_create fails otherwise) */
+	/* NerfNetwork's n_extra_dims (nerf_network.h:81-84, NerfDataset::n_extra_dims(): light directions and the
+	 * per-image latent code): the dir encoding's Identity part, appended to the rgb network's input after the
+	 * SH (rgb input width next_multiple(32 + n_extra_dims, 16)).  0..16; > 0 needs the 64-neuron network with
+	 * one density and two rgb hidden layers and an encoding of <= 32 features (base.json / lego_L16F2.json). */
 	uint32_t n_extra_dims;
 } ngp_network_config;
 
@@ -228,6 +229,14 @@ typedef struct ngp_train_args {
 	 * of its samples encode to zero and receive no gradient (tcnn GridEncoding::set_max_level_gpu);
 	 * the value rides in the pad float of the sample's coordinate row.  0: all levels. */
 	int32_t max_level_rand_training;
+	/* n_extra_dims > 0 (per-image latent codes, Nerf::Training::extra_dims_gpu, src/testbed_nerf.cu:706-730, 824):
+	 * extra_dims = device fp32 [n_images][16], image i's code in row i (zero past n_extra_dims); every sample of
+	 * a ray from image i carries row i (NerfCoordinate::set_with_optional_extra_dims); null = zeros.
+	 * extra_dims_gradient (optional, device fp32 [n_images][16]) += sum over the kept rays' compacted samples of
+	 * dL/d(code) (compute_extra_dims_gradient_train_nerf, src/testbed_nerf.cu:1271-1306; loss-scaled, as the
+	 * reference's gradient before its division by LOSS_SCALE at :2588) */
+	const float* extra_dims;
+	float* extra_dims_gradient;
 } ngp_train_args;
 
 typedef struct ngp_train_stats {
@@ -309,6 +318,9 @@ typedef struct ngp_render_args {
 	 * bit 1 green cut line, bit 2 mask to alpha, bit 3 radial distance, bit 4 grid mode; 0 = off */
 	int32_t glow_mode;
 	float glow_y_cutoff;
+	/* n_extra_dims > 0: the latent code every rendered sample carries (Nerf::get_rendering_extra_dims,
+	 * src/testbed_nerf.cu:3206-3228): device fp32 [16], zero past n_extra_dims; null = zeros */
+	const float* extra_dims;
 } ngp_render_args;
 
 /* ngp_render_args.render_mode (the reference's ERenderMode; Distortion and EncodingVis are GUI
@@ -377,7 +389,8 @@ ngp_status ngp_model_encode(ngp_model* model, const float* pos, uint32_t stride,
 /* Debug/parity: corner indices [n][n_levels][8] and trilinear weights [n][n_levels][8]. */
 ngp_status ngp_model_encode_indices(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
                                     uint32_t* idx_out, float* w_out, ngp_stream stream);
-/* coords: NerfCoordinate records (pos[3], dt, dir[3], extra...) of `floats_per_coord` floats.
+/* coords: NerfCoordinate records (pos[3], dt, dir[3], extra...) of `floats_per_coord` floats (n_extra_dims > 0: the
+ * sample's latent code at floats 7 .. 7 + n_extra_dims, floats_per_coord >= 7 + n_extra_dims).
  * out: [n][4] fp16 = (rgb raw x3, density raw) (the 16-row padded output of the reference, rows 0-3). */
 ngp_status ngp_model_infer(ngp_model* model, const float* coords, uint32_t floats_per_coord, uint32_t n,
                            uint16_t* out, int use_inference_params, ngp_stream stream);
@@ -399,6 +412,12 @@ ngp_status ngp_model_density(ngp_model* model, const float* pos, uint32_t stride
 ngp_status ngp_model_backward(ngp_model* model, const uint16_t* enc, const float* dirs, uint32_t n,
                               const uint16_t* dL_dout, const float* sample_weight, uint16_t* dL_denc,
                               ngp_stream stream);
+/* The same with the rgb network's extra inputs (n_extra_dims > 0): extra [n][16] fp32 latent codes of the samples
+ * (zero past n_extra_dims); dL_dextra (optional) [n][16] fp32 = dL/d(code) of each sample's own row (the network's
+ * input gradient that compute_extra_dims_gradient_train_nerf sums, divided by sample_weight). */
+ngp_status ngp_model_backward_extra(ngp_model* model, const uint16_t* enc, const float* dirs, const float* extra, uint32_t n,
+                                    const uint16_t* dL_dout, const float* sample_weight, uint16_t* dL_denc,
+                                    float* dL_dextra, ngp_stream stream);
 /* Parity entry for the hash-grid backward scatter: dL_denc [n_levels][n][F] fp16 -> grads. */
 ngp_status ngp_model_encode_backward(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
                                      const uint16_t* dL_denc, ngp_stream stream);

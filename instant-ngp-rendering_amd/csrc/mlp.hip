@@ -47,14 +47,20 @@ constexpr int TCT = TSPW / 16;
 constexpr int TBLOCK = TWAVES * 64;
 static_assert(TWAVES * TSPW == SAMPLES_PER_BLOCK, "the training images hold one chunk");
 
-template <int W_, int DH_, int RH_, int KE_>
+// XE = 1: the rgb network's input carries the per-image latent code (NerfNetwork's n_extra_dims <= 16, the
+// dir encoding's Identity part): [density out 16 | SH 16 | extra 16] = 48 rows, read as two 32-row K steps whose
+// last 16 rows meet zero weights.  The training images then keep the rgb input segment last in a sample's row,
+// 48 rows long: the second K step's rows 48..63 are the row's zeroed pad and the next row's first halves
+// (finite values times zero weights), so the 160 KiB LDS budget holds.
+template <int W_, int DH_, int RH_, int KE_, int XE_ = 0>
 struct Net {
-	static constexpr int W = W_, DH = DH_, RH = RH_, KE = KE_;
+	static constexpr int W = W_, DH = DH_, RH = RH_, KE = KE_, XE = XE_;
 	static constexpr int Wp = (W + 31) / 32 * 32;
 	static constexpr int NL = DH + RH + 2;
 	static constexpr int ENC_ROWS = 32 * KE;
+	static constexpr int XROWS = XE ? 48 : 32;  // rgb input rows kept in the training images
 	static constexpr int out_dim(int l) { return (l == DH || l == NL - 1) ? 16 : W; }
-	static constexpr int in_rows(int l) { return l == 0 ? ENC_ROWS : (l == DH + 1 ? 32 : Wp); }
+	static constexpr int in_rows(int l) { return l == 0 ? ENC_ROWS : (l == DH + 1 ? 32 * (1 + XE) : Wp); }
 	static constexpr bool relu_out(int l) { return !(l == DH || l == NL - 1); }
 	static constexpr bool relu_in(int l) { return !(l == 0 || l == DH + 1); }
 	static constexpr int Mt(int l) { return out_dim(l) / 16; }
@@ -63,13 +69,15 @@ struct Net {
 	static constexpr int Kt(int l) { return in_rows(l) / 16; }
 	// LDS image layouts (rows per sample); TRAIN keeps every activation for wgrad.
 	template <bool TRAIN>
-	static constexpr int rows() { return TRAIN ? ENC_ROWS + (DH + RH) * Wp + 32 : ENC_ROWS + 2 * Wp + 32; }
+	static constexpr int rows() { return TRAIN ? ENC_ROWS + (DH + RH) * Wp + XROWS : ENC_ROWS + 2 * Wp + 32; }
 	template <bool TRAIN>
-	static constexpr int x_seg() { return TRAIN ? ENC_ROWS + DH * Wp : ENC_ROWS + 2 * Wp; }
+	static constexpr int x_seg() { return TRAIN ? (XE ? ENC_ROWS + (DH + RH) * Wp : ENC_ROWS + DH * Wp) : ENC_ROWS + 2 * Wp; }
 	template <bool TRAIN>
 	static constexpr int dens_hidden(int h) { return TRAIN ? ENC_ROWS + h * Wp : ENC_ROWS + (h % 2) * Wp; }
 	template <bool TRAIN>
-	static constexpr int rgb_hidden(int r) { return TRAIN ? ENC_ROWS + DH * Wp + 32 + r * Wp : ENC_ROWS + (r % 2) * Wp; }
+	static constexpr int rgb_hidden(int r) {
+		return TRAIN ? ENC_ROWS + DH * Wp + (XE ? 0 : 32) + r * Wp : ENC_ROWS + (r % 2) * Wp;
+	}
 	template <bool TRAIN>
 	static constexpr int seg_in(int l) {
 		return l == 0 ? 0 : (l <= DH ? dens_hidden<TRAIN>(l - 1) : (l == DH + 1 ? x_seg<TRAIN>() : rgb_hidden<TRAIN>(l - DH - 2)));
@@ -152,6 +160,11 @@ struct MlpArgs {
 	float* partials;                  // k_mlp_train: [workgroup][n_mlp_params] weight-gradient partials
 	uint32_t n_mlp;                   // MLP parameter count (partials row pitch)
 	uint32_t skip_unfilled;           // SH-row inference: skip column tiles whose rows are all NO_SH_ROW
+	// Net::XE (n_extra_dims > 0): the latent codes, fp32 rows of 16 (zero past n_extra_dims); sample i reads row
+	// sample_img[i] (training: the sample's image), or row 0 without sample_img (rendering: the rendering code)
+	const float* extra;
+	const uint32_t* sample_img;
+	float* dextra;  // optional [n][16] dL/d(latent code) of each sample's own row (the extra dims' gradient)
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -308,6 +321,7 @@ struct RawTile {
 	float d[CT_][3];             // warped direction, or
 	uint32_t h[CT_][2];          // SH inputs 4g .. 4g+3 (precomputed rows)
 	uint32_t ri[CT_];            // SHIN: the samples' SH row indices
+	uint32_t x[CT_][2];          // Net::XE: latent-code components 4g .. 4g+3 (fp16 pairs)
 };
 
 // Buffer resource over a device array (raw buffer, 32-bit byte offsets; reads past
@@ -391,6 +405,16 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 					}
 					r.e[c][4 * s + q] = pair;
 				}
+			}
+		}
+		if constexpr (N::XE) {
+			if (want_dir) {
+				const uint32_t row = a.sample_img && i < a.n ? a.sample_img[i] : 0u;
+				const float4 v = *reinterpret_cast<const float4*>(a.extra + (size_t)row * 16 + 4 * g);
+				const h4 hv = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+				const uint2 u = __builtin_bit_cast(uint2, hv);
+				r.x[c][0] = u.x;
+				r.x[c][1] = u.y;
 			}
 		}
 		if (want_dir && SHIN) {
@@ -527,6 +551,8 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 				const f4 shv = {sh[0], sh[1], sh[2], sh[3]};
 				b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
 			}
+			// the latent code (rgb input rows 32..47; the K permutation puts rows 32 + 4g .. +3 in slots 0..3)
+			if constexpr (N::XE) b[cc][1] = pack_h8(cur.x[cc][0], cur.x[cc][1], 0u, 0u);
 		}
 		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
 		rf_layer<N, N::NL - 1, CT_>(w, b, c);
@@ -636,6 +662,7 @@ __device__ __forceinline__ void wgrad_layer(const _Float16* imgs, const _Float16
 		const int mt = t / KTN, kt = t % KTN;
 		if (gt % TWAVES != wave) continue;
 		if (l == 0 && (uint32_t)(16 * kt) >= enc_pad) continue;
+		if (N::XE && l == N::DH + 1 && kt == 3) continue;  // the latent code's zero padding rows
 		const int slot = gt / TWAVES;
 		f4 c = acc[slot];
 #pragma unroll
@@ -672,7 +699,10 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	const _Float16* fr = frags + N::bwd_off(l);
 #pragma unroll
 	for (int mt = 0; mt < KT; ++mt) {
-		if (l == N::DH + 1 && mt == 1 && !a.dsh) break;
+		// rgb input rows: 16..31 SH (camera gradients), 32..47 the latent code (extra dims), 48..63 padding
+		if (l == N::DH + 1 && mt == 1 && !a.dsh) continue;
+		if (l == N::DH + 1 && mt == 2 && !a.dextra) continue;
+		if (l == N::DH + 1 && mt >= 3) continue;
 		h8 af[MS];
 #pragma unroll
 		for (int s = 0; s < MS; ++s) af[s] = lds_h8(fr + ((mt * MS + s) * 64 + lane) * 8);
@@ -695,11 +725,12 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 					acc[0] += (float)__half2float(a.dloss[(size_t)i * 4 + 3]) * w;
 				}
 			}
-			if (l == N::DH + 1 && mt == 1) {
-				// dL/d(SH) of the sample's own row: the deltas carry its rollover weight
+			if (l == N::DH + 1 && mt >= 1) {
+				// dL/d(SH) or dL/d(latent code) of the sample's own row: the deltas carry its rollover weight
 				if (i < a.n) {
 					const float inv = a.weight ? 1.0f / a.weight[i] : 1.0f;
-					*reinterpret_cast<float4*>(a.dsh + (size_t)i * 16 + 4 * g) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+					float* dst = mt == 1 ? a.dsh : a.dextra;
+					*reinterpret_cast<float4*>(dst + (size_t)i * 16 + 4 * g) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
 				}
 			} else if constexpr (l > 0) {
 				h4 o = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
@@ -803,7 +834,23 @@ struct TrainPrefetch {
 	float d[3];
 	uint2 dl;
 	float w;
+	float4 x[2];  // Net::XE: latent-code components 8 (lane / SPW - 2) .. +7 of this lane's sample
 };
+
+// the latent code of sample i (Net::XE), components 8h .. 8h + 7 as fp16 (tcnn's Identity encoding: the float
+// input converted to the network's half type); zeros past the batch
+__device__ __forceinline__ void load_extra8(const MlpArgs& a, uint32_t i, int h, float4 (&x)[2]) {
+	x[0] = x[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+	if (i >= a.n) return;
+	const uint32_t row = a.sample_img ? a.sample_img[i] : 0u;
+	const float4* src = reinterpret_cast<const float4*>(a.extra + (size_t)row * 16 + 8 * h);
+	x[0] = src[0];
+	x[1] = src[1];
+}
+__device__ __forceinline__ h8 extra_h8(const float4 (&x)[2]) {
+	return h8{(_Float16)x[0].x, (_Float16)x[0].y, (_Float16)x[0].z, (_Float16)x[0].w,
+	          (_Float16)x[1].x, (_Float16)x[1].y, (_Float16)x[1].z, (_Float16)x[1].w};
+}
 
 template <class N, int SPW_ = TSPW>
 __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int lane, TrainPrefetch& p) {
@@ -823,6 +870,9 @@ __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int
 	const float* c = a.coords + (size_t)(in ? i : 0) * a.coord_stride;
 #pragma unroll
 	for (int k = 0; k < 3; ++k) p.d[k] = in ? c[4 + k] : 0.5f;
+	if constexpr (N::XE) {
+		if (lane >= 2 * SPW_ && lane < 4 * SPW_) load_extra8(a, i, lane / SPW_ - 2, p.x);
+	}
 	p.dl = make_uint2(0u, 0u);
 	p.w = 1.0f;
 	if (lane < SPW_ && in) {
@@ -861,6 +911,10 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 #pragma unroll
 		for (int k = 0; k < 8; ++k) o[k] = in ? (_Float16)(half ? v[8 + k] : v[k]) : (_Float16)0;
 		if (half < 2) lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, o);
+		if constexpr (N::XE) {
+			// the latent code: rgb input rows 32..47
+			if (half >= 2 && half < 4) lds_st_h8(img + smp * STRIDE + x_seg + 32 + 8 * (half - 2), extra_h8(p.x));
+		}
 	}
 	for (int t = lane; t < SPW_ * 4; t += 64) {
 		const int smp = t % SPW_, ch = t / SPW_;
@@ -915,6 +969,13 @@ __global__ void __launch_bounds__(TBLOCK) k_mlp_train(MlpArgs a) {
 		} else {
 			load_encoding<N, STRIDE, TSPW>(a, img, base, lane);
 			load_sh<STRIDE, TSPW>(a, img, N::template x_seg<true>(), base, lane);
+			if constexpr (N::XE) {
+				for (int t = lane; t < TSPW * 2; t += 64) {
+					float4 x[2];
+					load_extra8(a, base + t % TSPW, t / TSPW, x);
+					lds_st_h8(img + (t % TSPW) * STRIDE + N::template x_seg<true>() + 32 + 8 * (t / TSPW), extra_h8(x));
+				}
+			}
 			// delta of the rgb output layer: rows 0..2 = dL/drgb_raw (loss-scaled, rollover-weighted)
 			for (int t = lane; t < TSPW * 4; t += 64) {
 				const int smp = t % TSPW, ch = t / TSPW;
@@ -1027,9 +1088,11 @@ using V3 = Net<32, 1, 2, 1>;
 using V4 = Net<64, 2, 2, 1>;
 using V5 = Net<64, 1, 1, 1>;
 using V6 = Net<64, 1, 3, 1>;
+using V7 = Net<64, 1, 2, 1, 1>;  // lego / base.json with per-image latent codes (n_extra_dims 1..16)
 
-int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad) {
+int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad, uint32_t n_extra_dims) {
 	const uint32_t ke = enc_pad <= 32 ? 1 : (enc_pad <= 64 ? 2 : 0);
+	if (n_extra_dims) return width == 64 && dh == 1 && rh == 2 && ke == 1 && n_extra_dims <= 16 ? 7 : -1;
 	if (width == 64 && dh == 1 && rh == 2 && ke == 1) return 0;
 	if (width == 64 && dh == 1 && rh == 2 && ke == 2) return 1;
 	if (width == 16 && dh == 1 && rh == 2 && ke == 1) return 2;
@@ -1068,6 +1131,7 @@ static void layer_geometry(const ngp_model* m, PackArgs& p) {
 		case 4: { using N = V4; __VA_ARGS__; } break;           \
 		case 5: { using N = V5; __VA_ARGS__; } break;           \
 		case 6: { using N = V6; __VA_ARGS__; } break;           \
+		case 7: { using N = V7; __VA_ARGS__; } break;           \
 		default: throw std::runtime_error("unsupported MLP configuration"); \
 	}
 
@@ -1118,7 +1182,7 @@ static void set_lds(K kernel, size_t bytes) {
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev, uint32_t dir_offset, const __half* sh, uint32_t out_mode, uint32_t out_stride,
-                      const uint32_t* sh_ray, uint32_t sh_rows, bool skip_unfilled) {
+                      const uint32_t* sh_ray, uint32_t sh_rows, bool skip_unfilled, const MlpExtra& x) {
 	if (n == 0) return;
 	if (enc_layout.lsh != m->enc_lsh) throw std::runtime_error("encoding layout differs from the packed first layer's");
 	MlpArgs a = base_args(m);
@@ -1142,6 +1206,8 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.out_mode = out_mode;
 	a.out_stride = out_stride;
 	a.skip_unfilled = skip_unfilled && sh_ray && out_mode == 0;
+	a.extra = x.extra ? x.extra : m->zero_extra.ptr;
+	a.sample_img = x.extra ? x.sample_img : nullptr;
 	NGP_DISPATCH(m->mlp_variant, {
 		const size_t lds = (size_t)N::fwd_frags() * FRAG_HALVES * 2;
 		// workgroups per CU (ngp_tuning.mlp_workgroups_per_cu; 8 measured 0.6 % faster per frame than
@@ -1210,10 +1276,13 @@ void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* e
 void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
-                      const uint32_t* n_dev, float* dsh) {
+                      const uint32_t* n_dev, float* dsh, const MlpExtra& x) {
 	if (n == 0) return;
 	MlpArgs a = base_args(m);
 	a.dsh = dsh;
+	a.extra = x.extra ? x.extra : m->zero_extra.ptr;
+	a.sample_img = x.extra ? x.sample_img : nullptr;
+	a.dextra = m->cfg.n_extra_dims ? x.dextra : nullptr;
 	a.frags = frags;
 	a.enc = enc;
 	a.enc_plane = enc_layout.plane;

@@ -119,7 +119,9 @@ static void build_layers(ngp_model* m) {
 	for (uint32_t h = 1; h < c.density_hidden_layers; ++h) dims.push_back({W, W});
 	dims.push_back({16, W});
 	m->n_density_layers = (uint32_t)dims.size();
-	dims.push_back({W, 32});  // rgb_network_input_width = next_multiple(16 + 16, 16) (nerf_network.h:93)
+	// rgb_network_input_width = next_multiple(density out 16 + dir encoding (SH 16 + n_extra_dims Identity), 16)
+	// (nerf_network.h:84, 93)
+	dims.push_back({W, next_multiple(32u + c.n_extra_dims, 16u)});
 	for (uint32_t h = 1; h < c.rgb_hidden_layers; ++h) dims.push_back({W, W});
 	dims.push_back({16, W});  // 3 used, padded to 16 (tcnn output alignment)
 	require(dims.size() <= MAX_LAYERS, "too many MLP layers");
@@ -178,7 +180,7 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 		        "n_features_per_level must be 1, 2, 4 or 8");
 		require(cfg->log2_hashmap_size >= 4 && cfg->log2_hashmap_size <= 30, "log2_hashmap_size out of range");
 		require(cfg->per_level_scale > 0.0f, "per_level_scale must be positive");
-		require(cfg->n_extra_dims == 0, "n_extra_dims > 0 (per-image latent codes, optimize_extra_dims) is not supported");
+		require(cfg->n_extra_dims <= 16, "n_extra_dims must be <= 16 (the rgb network's input holds one 16-wide latent code)");
 		NGP_HIP_CHECK(hipSetDevice(hip_device));
 		auto* m = new ngp_model();
 		try {
@@ -193,8 +195,16 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 				m->enc_gsh = m->enc_lsh ? (uint32_t)__builtin_ctz(G) : 0u;
 			}
 			require(m->enc_pad <= 64, "encoding width (n_levels * F) must be <= 64");
-			m->mlp_variant = mlp_variant_for(cfg->n_neurons, cfg->density_hidden_layers, cfg->rgb_hidden_layers, m->enc_pad);
-			if (m->mlp_variant < 0) throw std::invalid_argument("unsupported MLP shape (n_neurons / hidden layers)");
+			m->mlp_variant = mlp_variant_for(cfg->n_neurons, cfg->density_hidden_layers, cfg->rgb_hidden_layers, m->enc_pad,
+			                                 cfg->n_extra_dims);
+			if (m->mlp_variant < 0)
+				throw std::invalid_argument(cfg->n_extra_dims ? "n_extra_dims > 0 needs the 64-neuron network with 1 density and 2 rgb hidden "
+				                                                "layers and an encoding of <= 32 features"
+				                                              : "unsupported MLP shape (n_neurons / hidden layers)");
+			if (cfg->n_extra_dims) {
+				m->zero_extra.reserve(16);
+				NGP_HIP_CHECK(hipMemset(m->zero_extra.ptr, 0, 16 * sizeof(float)));
+			}
 			build_level_table(m);
 			build_layers(m);
 			m->n_params = m->n_mlp_params + m->n_grid_params;
@@ -252,12 +262,14 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		t.counters.release(); t.scan_a.release(); t.scan_b.release(); t.dp.release();
 		t.epos.release(); t.edir.release(); t.eenc.release(); t.eout.release(); t.eidx.release();
 		t.ray_T.release(); t.ray_eval.release(); t.ray_ebase.release(); t.dsh.release(); t.dpos.release();
+		t.simg.release(); t.eimg.release(); t.cimg.release(); t.dextra.release(); t.api_extra.release(); t.api_extra_idx.release();
 		GridState& g = m->gs;
 		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
 		g.skeys.release(); g.perm_in.release(); g.perm.release(); g.sort_tmp.release(); g.spos.release();
 		m->rs.release();
 		m->timers.release();
+		m->zero_extra.release();
 		delete m;
 	});
 }
@@ -358,18 +370,42 @@ ngp_status ngp_model_encode_indices(ngp_model* m, const float* pos, uint32_t str
 	});
 }
 
+// The latent codes NerfCoordinate records carry after their 7 floats (set_with_optional_extra_dims,
+// nerf_device.cuh:177-195) -> rows of 16 (zero-padded) and row indices i (MlpExtra with one row per sample)
+__global__ void k_extra_rows(const float* __restrict__ src, uint32_t stride, uint32_t offset, uint32_t E, uint32_t n,
+                             float* __restrict__ rows, uint32_t* __restrict__ idx) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	for (uint32_t k = 0; k < 16; ++k) rows[16 * (size_t)i + k] = k < E ? src[(size_t)i * stride + offset + k] : 0.0f;
+	idx[i] = i;
+}
+
+static MlpExtra coord_extras(ngp_model* m, const float* src, uint32_t stride, uint32_t offset, uint32_t n, hipStream_t s) {
+	MlpExtra x;
+	if (!m->cfg.n_extra_dims || n == 0) return x;
+	TrainScratch& ts = m->ts;
+	ts.api_extra.reserve(16 * (size_t)n);
+	ts.api_extra_idx.reserve(n);
+	k_extra_rows<<<div_up(n, 256u), 256, 0, s>>>(src, stride, offset, m->cfg.n_extra_dims, n, ts.api_extra.ptr, ts.api_extra_idx.ptr);
+	NGP_HIP_CHECK(hipGetLastError());
+	x.extra = ts.api_extra.ptr;
+	x.sample_img = ts.api_extra_idx.ptr;
+	return x;
+}
+
 ngp_status ngp_model_infer(ngp_model* m, const float* coords, uint32_t fpc, uint32_t n, uint16_t* out, int use_inf,
                            ngp_stream s) {
 	return guarded([&] {
 		require(m && (n == 0 || (coords && out)), "null argument");
-		require(fpc >= 7, "floats_per_coord must be >= 7 (NerfCoordinate)");
+		require(fpc >= 7 + m->cfg.n_extra_dims, "floats_per_coord must be >= 7 + n_extra_dims (NerfCoordinate + extra dims)");
 		if (n == 0) return;
 		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
 		TrainScratch& ts = m->ts;
 		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
 		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, internal_layout(m, n), S(s));
-		launch_mlp_infer(m, frags, ts.enc.ptr, internal_layout(m, n), coords, fpc, n, reinterpret_cast<__half*>(out), S(s));
+		launch_mlp_infer(m, frags, ts.enc.ptr, internal_layout(m, n), coords, fpc, n, reinterpret_cast<__half*>(out), S(s),
+		                 nullptr, 4, nullptr, 0, 4, nullptr, 0, false, coord_extras(m, coords, fpc, 7, n, S(s)));
 	});
 }
 
@@ -377,7 +413,7 @@ ngp_status ngp_model_infer_padded(ngp_model* m, const float* coords, uint32_t fp
                                   uint32_t out_stride, int layout_rm, int use_inf, ngp_stream s) {
 	return guarded([&] {
 		require(m && (n == 0 || (coords && out)), "null argument");
-		require(fpc >= 7, "floats_per_coord must be >= 7 (NerfCoordinate)");
+		require(fpc >= 7 + m->cfg.n_extra_dims, "floats_per_coord must be >= 7 + n_extra_dims (NerfCoordinate + extra dims)");
 		require(layout_rm ? out_stride >= n : out_stride >= 16, "out_stride too small for 16 output rows");
 		if (n == 0) return;
 		const __half* table = (use_inf ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
@@ -386,7 +422,7 @@ ngp_status ngp_model_infer_padded(ngp_model* m, const float* coords, uint32_t fp
 		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
 		launch_hashgrid_fwd(m->lt, coords, fpc, n, table, ts.enc.ptr, internal_layout(m, n), S(s));
 		launch_mlp_infer(m, frags, ts.enc.ptr, internal_layout(m, n), coords, fpc, n, reinterpret_cast<__half*>(out), S(s),
-		                 nullptr, 4, nullptr, layout_rm ? 2u : 1u, out_stride);
+		                 nullptr, 4, nullptr, layout_rm ? 2u : 1u, out_stride, nullptr, 0, false, coord_extras(m, coords, fpc, 7, n, S(s)));
 	});
 }
 
@@ -405,9 +441,26 @@ ngp_status ngp_model_density(ngp_model* m, const float* pos, uint32_t stride, ui
 	});
 }
 
+static void model_backward(ngp_model* m, const uint16_t* enc, const float* dirs, const float* extra, uint32_t n,
+                           const uint16_t* dloss, const float* weight, uint16_t* denc, float* dextra, ngp_stream s);
+
 ngp_status ngp_model_backward(ngp_model* m, const uint16_t* enc, const float* dirs, uint32_t n, const uint16_t* dloss,
                               const float* weight, uint16_t* denc, ngp_stream s) {
+	return guarded([&] { model_backward(m, enc, dirs, nullptr, n, dloss, weight, denc, nullptr, s); });
+}
+
+ngp_status ngp_model_backward_extra(ngp_model* m, const uint16_t* enc, const float* dirs, const float* extra, uint32_t n,
+                                    const uint16_t* dloss, const float* weight, uint16_t* denc, float* dextra, ngp_stream s) {
 	return guarded([&] {
+		require(m && (n == 0 || extra), "null argument");
+		require(m->cfg.n_extra_dims > 0, "the model has no extra dims (n_extra_dims = 0)");
+		model_backward(m, enc, dirs, extra, n, dloss, weight, denc, dextra, s);
+	});
+}
+
+static void model_backward(ngp_model* m, const uint16_t* enc, const float* dirs, const float* extra, uint32_t n,
+                           const uint16_t* dloss, const float* weight, uint16_t* denc, float* dextra, ngp_stream s) {
+	{
 		require(m && (n == 0 || (enc && dirs && dloss && denc)), "null argument");
 		if (n == 0) return;
 		// dirs are passed as [n][3]; the MLP kernel reads NerfCoordinate-like records (dir at offset 4)
@@ -420,11 +473,13 @@ ngp_status ngp_model_backward(ngp_model* m, const uint16_t* enc, const float* di
 		for (size_t i = 0; i < n; ++i)
 			for (int k = 0; k < 3; ++k) tmp[8 * i + 4 + k] = d[3 * i + k];
 		NGP_HIP_CHECK(hipMemcpyAsync(ts.ccoords.ptr, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, S(s)));
+		MlpExtra x = extra ? coord_extras(m, extra, 16, 0, n, S(s)) : MlpExtra{};
+		x.dextra = dextra;
 		launch_mlp_train(m, m->frag_train.ptr, reinterpret_cast<const __half*>(enc), EncLayout{n, 0}, ts.ccoords.ptr, 8, n,
 		                 reinterpret_cast<const __half*>(dloss), weight, m->grads.ptr, reinterpret_cast<__half*>(denc),
-		                 S(s));
+		                 S(s), nullptr, nullptr, x);
 		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
-	});
+	}
 }
 
 ngp_status ngp_model_encode_backward(ngp_model* m, const float* pos, uint32_t stride, uint32_t n, const uint16_t* denc,

@@ -281,6 +281,12 @@ struct TrainScratch {
 	DevBuf<uint32_t> ray_eval, ray_ebase;  // [R]
 	DevBuf<float> dsh;                 // [B][16] dL/d(SH inputs) of the compacted batch (extrinsics)
 	DevBuf<float> dpos;                // [B][3] dL/d(warped position) of the compacted batch (extrinsics)
+	// n_extra_dims > 0: each sample's image (the row of its latent code) in the sampler's, the evaluation rows'
+	// and the compacted batch's order, and dL/d(code) of the compacted samples
+	DevBuf<uint32_t> simg, eimg, cimg;
+	DevBuf<float> dextra;              // [B][16]
+	DevBuf<float> api_extra;           // C-ABI entries: the latent codes of coordinate records, rows of 16
+	DevBuf<uint32_t> api_extra_idx;
 	DevBuf<uint32_t> dp;               // data parallel: [0,3) sample DpCaps, [4,7) compaction DpCaps, then 2 x [world] slots
 	bool chunked = false;              // last step ran the chunked forward
 	bool fixed = false;                // last step accumulated hash-grid gradients in fixed point (deterministic)
@@ -395,6 +401,7 @@ struct ngp_model {
 	float adam_corr_b1 = 0.0f, adam_corr_b2 = 0.0f;
 	ngp::DevBuf<__half> frag_train, frag_infer;  // packed MFMA fragments of params16 / infer16
 	mutable ngp::DevBuf<float> mlp_partials;      // [workgroup][n_mlp_params] weight-gradient partials of k_mlp_train
+	ngp::DevBuf<float> zero_extra;                // n_extra_dims > 0: one all-zero latent-code row (no codes given)
 	uint32_t ema_step = 0;
 
 	ngp::TrainScratch ts;
@@ -443,16 +450,24 @@ void launch_hashgrid_bwd(const LevelTable& lt, const float* pos, uint32_t stride
 void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, uint32_t* idx,
                              float* w, hipStream_t s);
 // mlp.hip
-int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad);
+int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad, uint32_t n_extra_dims = 0);
 uint32_t mlp_frag_halves(const ngp_model* m);
 void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s);
+// The latent codes of a model with n_extra_dims > 0 (the rgb network's extra inputs): extra = fp32 rows of 16
+// (zero past n_extra_dims), sample i reads row sample_img[i], or row 0 without sample_img; extra null: zeros.
+// dextra (training): [n][16] dL/d(latent code) of each sample's own row.
+struct MlpExtra {
+	const float* extra = nullptr;
+	const uint32_t* sample_img = nullptr;
+	float* dextra = nullptr;
+};
 // coords: per-sample records of coord_stride floats holding the warped direction at
 // dir_offset (NerfCoordinate: 4); sh (optional): [n][16] fp16 SH rows used instead
 void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, __half* out, hipStream_t s,
                       const uint32_t* n_dev = nullptr, uint32_t dir_offset = 4, const __half* sh = nullptr,
                       uint32_t out_mode = 0, uint32_t out_stride = 4, const uint32_t* sh_ray = nullptr, uint32_t sh_rows = 0,
-                      bool skip_unfilled = false);
+                      bool skip_unfilled = false, const MlpExtra& x = MlpExtra{});
 // render.hip: the octant distance fields of the bitfield's mips [0, max_mip] into m->rs.df (rebuilt only
 // when the bitfield changed); the renderer's march and the training sampler (aabb_scale 1) read them
 void build_distance_fields(ngp_model* m, uint32_t max_mip, hipStream_t s);
@@ -464,7 +479,7 @@ void launch_mlp_density(const ngp_model* m, const __half* frags, const __half* e
 void launch_mlp_train(const ngp_model* m, const __half* frags, const __half* enc, EncLayout enc_layout,
                       const float* coords, uint32_t coord_stride, uint32_t n, const __half* dloss,
                       const float* weight, float* grads_mlp, __half* denc, hipStream_t s,
-                      const uint32_t* n_dev = nullptr, float* dsh = nullptr);
+                      const uint32_t* n_dev = nullptr, float* dsh = nullptr, const MlpExtra& x = MlpExtra{});
 // dL/d(warped position) through the grid of the first *n_dev samples (dpos [n][3]), divided by weight
 void launch_hashgrid_input_grad(const LevelTable& lt, const float* pos, uint32_t stride, uint32_t n, const __half* denc,
                                 EncLayout enc_layout, const __half* table, const float* weight, float* dpos, hipStream_t s,

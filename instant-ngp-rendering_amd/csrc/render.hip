@@ -1049,7 +1049,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		const __half* tab = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 		const __half* fr = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
 		launch_hashgrid_fwd(m->lt, rs.slice_coords.ptr, 8, n, tab, rs.slice_enc.ptr, internal_layout(m, n), s);
-		launch_mlp_infer(m, fr, rs.slice_enc.ptr, internal_layout(m, n), rs.slice_coords.ptr, 8, n, rs.slice_out.ptr, s);
+		launch_mlp_infer(m, fr, rs.slice_enc.ptr, internal_layout(m, n), rs.slice_coords.ptr, 8, n, rs.slice_out.ptr, s, nullptr,
+		                 4, nullptr, 0, 4, nullptr, 0, false, MlpExtra{a->extra_dims, nullptr, nullptr});
 		k_slice_shade<<<div_up(n, 256u), 256, 0, s>>>(k, n, rs.slice_coords.ptr, rs.slice_out.ptr, reinterpret_cast<float4*>(frame));
 		NGP_HIP_CHECK(hipGetLastError());
 		return;
@@ -1226,7 +1227,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.end(NGP_TIMER_RENDER_ENCODE, ps);  // units: the pass's sample count, added at its read-back
 		tm.begin_kernel(NGP_TIMER_RENDER_MLP);
 		launch_mlp_infer(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, pr.ps->out.ptr, ps,
-		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows, skip_unfilled);
+		                 samples, 0, reinterpret_cast<const __half*>(pr.shrows), 0, 4, pr.sray, sh_rows, skip_unfilled,
+		                 MlpExtra{a->extra_dims, nullptr, nullptr});
 		tm.end(NGP_TIMER_RENDER_MLP, ps);
 		if (pr.k.mode == NGP_RENDER_MODE_NORMALS) {
 			// Normals (NerfTracer::trace, testbed_nerf.cu:1715-1717, network->input_gradient): the gradient of
@@ -1239,7 +1241,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			sc.nrm.reserve(3 * (size_t)n_elements);
 			k_density_unit_dloss<<<div_up(n_elements, 256u), 256, 0, ps>>>(samples, n_elements, sc.nrm_dloss.ptr);
 			launch_mlp_train(m, frags, pr.ps->enc.ptr, internal_layout(m, n_elements), nullptr, 0, n_elements, sc.nrm_dloss.ptr,
-			                 nullptr, nullptr, sc.nrm_denc.ptr, ps, samples);
+			                 nullptr, nullptr, sc.nrm_denc.ptr, ps, samples, nullptr, MlpExtra{a->extra_dims, nullptr, nullptr});
 			launch_hashgrid_input_grad(m->lt, reinterpret_cast<const float*>(pr.posdt), 4, n_elements, sc.nrm_denc.ptr,
 			                           EncLayout{n_elements, 0}, table, nullptr, sc.nrm.ptr, ps, samples);
 			pr.k.normals = sc.nrm.ptr;

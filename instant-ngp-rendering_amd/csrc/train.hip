@@ -210,6 +210,7 @@ struct SamplerArgs {
 	float* ray_state;    // [R][8]
 	float* coords;       // [max][8]
 	float4* pos4;        // [max]: pos + warped dt again, 16-B rows the encoder reads once per level
+	uint32_t* simg;      // [max] n_extra_dims > 0: the sample's image (its latent-code row); null otherwise
 	const float* dmap;   // learned distortion map [dry][drx][2] (null: off; general instance only)
 	uint32_t drx, dry;
 	const uint8_t* df;   // octant distance fields of mip 0 (aabb_scale 1 only; null: the jump chain)
@@ -256,11 +257,12 @@ __device__ __forceinline__ uint32_t training_pixel(const ngp_image* images, uint
 // max level (2 u with max_level_rand_training, drawn before motionblur_time; else 0 = unused).
 template <bool GENERAL>
 __device__ __forceinline__ bool training_ray(const SamplerArgs& a, uint32_t gi, v3* o, v3* d, float* n0,
-                                             float* max_level = nullptr) {
+                                             float* max_level = nullptr, uint32_t* img_out = nullptr) {
 	pcg32 rng = a.rng;
 	rng.advance((int64_t)gi * N_MAX_RANDOM_SAMPLES_PER_RAY);
 	float u, v;
 	const uint32_t img = training_pixel<GENERAL>(a.images, a.n_images, gi, a.n_rays_global, a.cdf, a.snap, rng, &u, &v);
+	if (img_out) *img_out = img;
 	const ngp_image im = a.images[img];
 	float rgba[4];
 	texel_rgba(read_texel(im, u, v), rgba);
@@ -434,7 +436,8 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	}
 	v3 o, d;
 	float n0, max_level;
-	training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0, &max_level);
+	uint32_t img = 0;
+	training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0, &max_level, &img);
 	if (lane == 0) {
 		a.numsteps[2 * i + 0] = n;
 		a.numsteps[2 * i + 1] = base;
@@ -456,6 +459,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 			c[0] = pd;
 			c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);
 			a.pos4[base + r] = pd;
+			if (a.simg) a.simg[base + r] = img;
 		});
 		return;
 	}
@@ -475,6 +479,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 				c[0] = pd;
 				c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);  // the pad float carries the max level
 				a.pos4[base + r] = pd;
+				if (a.simg) a.simg[base + r] = img;
 			}
 		}
 		j += __popcll(m);
@@ -516,6 +521,8 @@ struct ChunkArgs {
 	int first, last;
 	int density_act;
 	float stop_T;              // transmittance below which a ray stops (TRAIN_CHUNK_STOP_T; ngp_tuning.debug bit 2: 0.999)
+	const uint32_t* simg;      // [MS] n_extra_dims > 0: each sample's image, copied with its evaluation row into
+	uint32_t* eimg;            // [MSE]; null otherwise
 };
 
 // One chunk step: composite the previous chunk's outputs (transmittance only) and scatter
@@ -639,6 +646,7 @@ __global__ void __launch_bounds__(1024) k_train_chunk(ChunkArgs a) {
 		const uint32_t src = base + a.lo + k;
 		a.epos[e0 + k] = a.pos4[src];
 		a.edir[e0 + k] = reinterpret_cast<const float4*>(a.coords + 8 * (size_t)src)[1];
+		if (a.eimg) a.eimg[e0 + k] = a.simg[src];
 	}
 }
 
@@ -1163,6 +1171,35 @@ __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 	atomicAdd(&a.cam_rot_gradient[3 * (size_t)img + 2], aa.z * inv_pdf);
 }
 
+// compute_extra_dims_gradient_train_nerf (src/testbed_nerf.cu:1271-1306): the ray's compacted samples' dL/d(latent
+// code) summed into its image's gradient (one thread per ray, E float atomics; loss-scaled like the reference's)
+__global__ void __launch_bounds__(256) k_extra_gradient(uint32_t n_rays, const uint32_t* __restrict__ compacted,
+                                                        const float* __restrict__ loss_state, const float* __restrict__ dextra,
+                                                        uint32_t E, float* __restrict__ grad, const uint32_t* __restrict__ viol_gate) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n_rays || (viol_gate && *viol_gate)) return;
+	const uint32_t cn = compacted[2 * i], cbase = compacted[2 * i + 1];
+	if (cn == 0) return;
+	float g[16];
+#pragma unroll
+	for (uint32_t k = 0; k < 16; ++k) g[k] = 0.0f;
+	for (uint32_t j = 0; j < cn; ++j) {
+		const float4* src = reinterpret_cast<const float4*>(dextra + 16 * ((size_t)cbase + j));
+#pragma unroll
+		for (uint32_t q = 0; q < 4; ++q) {
+			const float4 v = src[q];
+			g[4 * q] += v.x;
+			g[4 * q + 1] += v.y;
+			g[4 * q + 2] += v.z;
+			g[4 * q + 3] += v.w;
+		}
+	}
+	const uint32_t img = __float_as_uint(loss_state[8 * (size_t)i + 7]);
+#pragma unroll
+	for (uint32_t k = 0; k < 16; ++k)
+		if (k < E) atomicAdd(&grad[16 * (size_t)img + k], g[k]);
+}
+
 // Gather the compacted batch (coords + per-level features) in compacted order: one
 // thread per compacted sample, so every level plane is written by contiguous lanes.
 template <uint32_t F>
@@ -1170,10 +1207,12 @@ __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __rest
                                                           const float* __restrict__ coords, const __half* __restrict__ enc,
                                                           EncLayout src_layout, EncLayout dst_layout, uint32_t n_levels, float* __restrict__ ccoords,
                                                           float4* __restrict__ cpos4, __half* __restrict__ cenc, uint32_t target,
-                                                          const uint32_t* __restrict__ eidx) {
+                                                          const uint32_t* __restrict__ eidx, const uint32_t* __restrict__ simg,
+                                                          uint32_t* __restrict__ cimg) {
 	const uint32_t dst = blockIdx.x * 256u + threadIdx.x;
 	if (dst >= *n_ptr) return;
 	const uint32_t src = csrc[dst];
+	if (cimg) cimg[dst] = simg[src];  // n_extra_dims > 0: the sample's image (latent-code row)
 	const uint32_t esrc = eidx ? eidx[src] : src;  // row of the sample's encoding
 	const float4* ci = reinterpret_cast<const float4*>(coords + 8 * (size_t)src);
 	float4* co = reinterpret_cast<float4*>(ccoords + 8 * (size_t)dst);
@@ -1625,6 +1664,13 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.mlp_out.reserve(4 * (size_t)MS);
 	ts.ccoords.reserve(8 * (size_t)B);
 	ts.pos4.reserve(4 * (size_t)MS);
+	// n_extra_dims > 0: each sample's image picks its latent-code row (NerfCoordinate extra dims, src/testbed_nerf.cu:824)
+	const bool xd = m->cfg.n_extra_dims > 0;
+	if (xd) {
+		ts.simg.reserve(MS);
+		ts.cimg.reserve(B);
+		if (t->extra_dims_gradient) ts.dextra.reserve(16 * (size_t)B);
+	}
 	ts.cpos4.reserve(4 * (size_t)B);
 	ts.cenc.reserve((size_t)L * B * F);
 	ts.dloss.reserve(4 * (size_t)B);
@@ -1699,6 +1745,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
 	sa.pos4 = reinterpret_cast<float4*>(ts.pos4.ptr);
+	sa.simg = xd ? ts.simg.ptr : nullptr;
 	if (t->distortion_map && t->distortion_res[0] && t->distortion_res[1]) {
 		sa.dmap = t->distortion_map;
 		sa.drx = t->distortion_res[0];
@@ -1736,7 +1783,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 		tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
 		launch_mlp_infer(m, m->frag_train.ptr, ts.enc.ptr, enc_layout, ts.coords.ptr, 8, MS, ts.mlp_out.ptr, s,
-		                 ts.counters.ptr + 4);
+		                 ts.counters.ptr + 4, 4, nullptr, 0, 4, nullptr, 0, false, MlpExtra{t->extra_dims, sa.simg, nullptr});
 		tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
 	} else {
 		// evaluation rows: chunk p of every ray lands in [off[p], off[p] + cap[p])
@@ -1748,6 +1795,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		ts.eenc.reserve((size_t)L * MSE * F);
 		ts.eout.reserve(4 * (size_t)MSE);
 		ts.eidx.reserve(MS);
+		if (xd) ts.eimg.reserve(MSE);
 		ts.ray_T.reserve(R);
 		ts.ray_eval.reserve(R);
 		ts.ray_ebase.reserve(R);
@@ -1766,6 +1814,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		c.ray_ebase = ts.ray_ebase.ptr;
 		c.density_act = m->cfg.density_activation;
 		c.stop_T = (m->tuning.debug & 4u) ? 0.999f : TRAIN_CHUNK_STOP_T;
+		c.simg = sa.simg;
+		c.eimg = xd ? ts.eimg.ptr : nullptr;
 		for (uint32_t p = 0; p <= TRAIN_CHUNKS; ++p) {
 			c.first = p == 0;
 			c.last = p == TRAIN_CHUNKS;
@@ -1794,7 +1844,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 			tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
 			launch_mlp_infer(m, m->frag_train.ptr, eenc_p, internal_layout(m, MSE), ts.edir.ptr + 4 * (size_t)off[p], 4,
-			                 cap[p], ts.eout.ptr + 4 * (size_t)off[p], s, c.rows, 0);
+			                 cap[p], ts.eout.ptr + 4 * (size_t)off[p], s, c.rows, 0, nullptr, 0, 4, nullptr, 0, false,
+			                 MlpExtra{t->extra_dims, xd ? ts.eimg.ptr + off[p] : nullptr, nullptr});
 			tm.end(NGP_TIMER_TRAIN_MLP_INFER, s);
 		}
 		enc_rows = ts.eenc.ptr;
@@ -1922,10 +1973,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// compacted batch size c = min(total, B); rollover multiplicity
 	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, la.max_compacted_dev, ts.counters.ptr + 5);
 	switch (F) {
-		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
-		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
-		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
-		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx); break;
+		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
+		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
+		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
+		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
 	}
 	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, dp_compact, ts.cweight.ptr);
 	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
@@ -1937,8 +1988,15 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		ts.dsh.reserve(16 * (size_t)B);
 		ts.dpos.reserve(3 * (size_t)B);
 	}
+	const bool xgrad = xd && t->extra_dims_gradient;
 	launch_mlp_train(m, m->frag_train.ptr, ts.cenc.ptr, internal_layout(m, B), ts.ccoords.ptr, 8, B, ts.dloss.ptr, ts.cweight.ptr,
-	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr);
+	                 m->grads.ptr, ts.denc.ptr, s, ts.counters.ptr + 5, cam ? ts.dsh.ptr : nullptr,
+	                 MlpExtra{t->extra_dims, xd ? ts.cimg.ptr : nullptr, xgrad ? ts.dextra.ptr : nullptr});
+	if (xgrad) {
+		k_extra_gradient<<<div_up(R, 256u), 256, 0, s>>>(R, ts.ray_compacted.ptr, ts.ray_loss_state.ptr, ts.dextra.ptr,
+		                                                 m->cfg.n_extra_dims, t->extra_dims_gradient, la.viol_gate);
+		NGP_HIP_CHECK(hipGetLastError());
+	}
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
 	tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE_BWD);
 	// data parallel: launched for about this rank's share of the global batch (blocks loop past it)

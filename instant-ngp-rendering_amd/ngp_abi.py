@@ -69,6 +69,7 @@ class TrainArgs(C.Structure):
         ("rank", C.c_uint32), ("world_size", C.c_uint32), ("allreduce_i32", C.c_void_p), ("allreduce_user", C.c_void_p),
         ("deterministic", C.c_int32),
         ("max_level_rand_training", C.c_int32),
+        ("extra_dims", C.c_void_p), ("extra_dims_gradient", C.c_void_p),
     ]
 
 
@@ -104,6 +105,7 @@ class RenderArgs(C.Structure):
         ("render_aabb_to_local", C.c_float * 9), ("render_mode", C.c_int32), ("depth_scale", C.c_float),
         ("gbuffer_hard_edges", C.c_int32), ("aperture_size", C.c_float), ("focus_z", C.c_float),
         ("glow_mode", C.c_int32), ("glow_y_cutoff", C.c_float),
+        ("extra_dims", C.c_void_p),
     ]
 
 
@@ -150,6 +152,8 @@ EXPORTS = {
     "ngp_model_density": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]),
     "ngp_model_backward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
+    "ngp_model_backward_extra": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngp_model_encode_backward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p]),
     "ngp_train_step": (C.c_int, [C.c_void_p, C.POINTER(TrainArgs), C.c_void_p]),
     "ngp_optimizer_step": (C.c_int, [C.c_void_p, C.c_uint32, C.c_int, C.c_int, C.c_void_p]),
@@ -200,7 +204,7 @@ def check(status):
 
 
 def default_config(n_levels=16, F=2, log2_T=19, base_res=16, per_level_scale=None, n_neurons=64,
-                   density_hidden=1, rgb_hidden=2, aabb_scale=1):
+                   density_hidden=1, rgb_hidden=2, aabb_scale=1, n_extra_dims=0):
     """Network config with the reference's auto-derived per_level_scale (src/testbed.cu:3709-3713)."""
     import numpy as np
     if per_level_scale is None:
@@ -213,4 +217,5 @@ def default_config(n_levels=16, F=2, log2_T=19, base_res=16, per_level_scale=Non
     c.rgb_activation, c.density_activation = 2, 3  # Logistic (LDR), Exponential
     c.learning_rate, c.beta1, c.beta2, c.epsilon, c.l2_reg = 1e-2, 0.9, 0.99, 1e-15, 1e-6
     c.ema_decay, c.decay_start, c.decay_interval, c.decay_base = 0.95, 20000, 10000, 0.33
+    c.n_extra_dims = n_extra_dims
     return c

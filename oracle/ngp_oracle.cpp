@@ -459,7 +459,9 @@ static void build(Model& M) {
 	for (uint32_t h = 1; h < c.density_hidden_layers; ++h) add(W, W, true, true);
 	add(16, W, false, true);
 	M.n_density_layers = (uint32_t)M.layers.size();
-	add(W, 32, true, false);
+	// rgb input: density out 16 | dir encoding (SH 16, then the n_extra_dims Identity inputs), padded to 16
+	// (nerf_network.h:84, 93)
+	add(W, (32 + c.n_extra_dims + 15) / 16 * 16, true, false);
 	for (uint32_t h = 1; h < c.rgb_hidden_layers; ++h) add(W, W, true, true);
 	add(16, W, false, true);
 	uint64_t o = 0;
@@ -647,19 +649,23 @@ static void layer_fwd(const Model& M, const uint16_t* P, const Layer& Ly, const 
 		out[r] = round ? rh(acc) : acc;
 	}
 }
-static void mlp_forward_one(const Model& M, const uint16_t* P, const float* enc_col /*E*/, const float* wdir, Acts& A) {
+// code (n_extra_dims > 0): the sample's latent code, n_extra_dims floats (NerfCoordinate's extra dims), rounded to
+// fp16 as tcnn's Identity encoding outputs them; null = zeros
+static void mlp_forward_one(const Model& M, const uint16_t* P, const float* enc_col /*E*/, const float* wdir, Acts& A,
+                            const float* code = nullptr) {
 	const uint32_t NL = (uint32_t)M.layers.size();
 	A.a.assign(NL + 1, {});
 	A.a[0].assign(M.Epad, 0.0f);
 	for (uint32_t k = 0; k < M.E; ++k) A.a[0][k] = enc_col[k];
 	for (uint32_t l = 0; l < NL; ++l) {
 		if (l == M.n_density_layers) {
-			// rgb input = [density_out(16) | SH(16)]
-			std::vector<float> x(32);
+			// rgb input = [density_out(16) | SH(16) | extra dims | zero padding]
+			std::vector<float> x(M.layers[l].in, 0.0f);
 			for (int k = 0; k < 16; ++k) x[k] = A.a[l][k];
 			float sh[16];
 			sh4(wdir, sh);
 			for (int k = 0; k < 16; ++k) x[16 + k] = sh[k];
+			for (uint32_t k = 0; k < M.cfg.n_extra_dims && code; ++k) x[32 + k] = rh(code[k]);
 			A.a[l] = x;
 		}
 		layer_fwd(M, P, M.layers[l], A.a[l], A.a[l + 1], true);
@@ -669,8 +675,9 @@ static void gather_enc(const Model& M, const float* enc, uint32_t n, uint32_t i,
 	for (uint32_t k = 0; k < M.E; ++k) col[k] = enc[((size_t)(k / M.F) * n + i) * M.F + (k % M.F)];
 }
 // out: [n][4] = rgb raw (3) + density raw (fp16-rounded)
+// codes: sample i's latent code at codes + i * code_stride (code_stride 0: one code for all; null: none)
 static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, const float* coords, uint32_t cs, uint32_t n,
-                        float* out) {
+                        float* out, const float* codes = nullptr, uint32_t code_stride = 0) {
 #pragma omp parallel
 	{
 	std::vector<float> col(M.E);
@@ -678,7 +685,7 @@ static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, con
 #pragma omp for schedule(static)
 	for (uint32_t i = 0; i < n; ++i) {
 		gather_enc(M, enc, n, i, col.data());
-		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A);
+		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A, codes ? codes + (size_t)i * code_stride : nullptr);
 		const uint32_t NL = (uint32_t)M.layers.size();
 		out[4 * i + 0] = A.a[NL][0];
 		out[4 * i + 1] = A.a[NL][1];
@@ -690,15 +697,17 @@ static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, con
 // NerfNetwork::backward_impl (nerf_network.h:189-268): rgb MLP bwd -> add_density_gradient -> density MLP bwd
 // dsh (optional, [n][16]): dL/d(SH inputs) of the sample's own row (÷ its rollover weight), for the
 // camera gradients (tcnn's input gradient through the Composite encoding's SH part)
+// codes / code_stride: the samples' latent codes (mlp_forward); dextra (optional, [n][16]): dL/d(rgb input rows
+// 32..47) of the sample's own row (÷ its rollover weight) -- the extra dims' input gradient
 static void mlp_backward(const Model& M, float* grads, const uint16_t* P, const float* enc, const float* coords, uint32_t cs,
                          uint32_t n, const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc,
-                         float* dsh = nullptr) {
+                         float* dsh = nullptr, const float* codes = nullptr, uint32_t code_stride = 0, float* dextra = nullptr) {
 	const uint32_t NL = (uint32_t)M.layers.size();
 	std::vector<float> col(M.E);
 	Acts A;
 	for (uint32_t i = 0; i < n; ++i) {
 		gather_enc(M, enc, n, i, col.data());
-		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A);
+		mlp_forward_one(M, P, col.data(), coords + (size_t)i * cs + 4, A, codes ? codes + (size_t)i * code_stride : nullptr);
 		const float w = weight ? weight[i] : 1.0f;
 		std::vector<float> delta(16, 0.0f);
 		for (int r = 0; r < 3; ++r) delta[r] = rh(dl[4 * i + r] * w);
@@ -723,6 +732,13 @@ static void mlp_backward(const Model& M, float* grads, const uint16_t* P, const 
 					float acc = 0.0f;
 					for (uint32_t r = 0; r < Ly.out; ++r) acc += h2f(W[(size_t)r * Ly.in + k]) * delta[r];
 					dsh[16 * (size_t)i + (k - 16)] = acc / w;
+				}
+			if (dextra && l == (int)M.n_density_layers)
+				for (uint32_t k = 32; k < 48; ++k) {
+					float acc = 0.0f;
+					if (k < Ly.in)
+						for (uint32_t r = 0; r < Ly.out; ++r) acc += h2f(W[(size_t)r * Ly.in + k]) * delta[r];
+					dextra[16 * (size_t)i + (k - 32)] = acc / w;
 				}
 			if (l == 0) {
 				for (uint32_t k = 0; k < M.E; ++k) denc[((size_t)(k / M.F) * n + i) * M.F + (k % M.F)] = nd[k];
@@ -1007,13 +1023,15 @@ static uint32_t pick_pixel(const ngp_train_args& a, uint32_t gi, uint32_t nrg, P
 // first lattice point n0 = to_stepping_space(t_entry) + random; t_entry and the random offset
 // are returned too (the literal transcription below starts from them).
 static bool train_ray(const ngp_train_args& a, uint32_t gi, uint32_t nrg, V3* o, V3* d, float* st, float* t_entry = nullptr,
-                      float* jitter = nullptr, float* dlen = nullptr, float* max_level = nullptr) {
+                      float* jitter = nullptr, float* dlen = nullptr, float* max_level = nullptr, uint32_t* img_out = nullptr) {
 	Pcg rng;
 	rng.state = a.rng_state;
 	rng.inc = a.rng_inc;
 	rng.advance((int64_t)gi * 16);
 	float u, vv;
-	const ngp_image& im = a.images[pick_pixel(a, gi, nrg, rng, &u, &vv, nullptr)];
+	const uint32_t img = pick_pixel(a, gi, nrg, rng, &u, &vv, nullptr);
+	if (img_out) *img_out = img;
+	const ngp_image& im = a.images[img];
 	float rgba[4];
 	rgba_of(texel(im, u, vv), rgba);
 	if (rgba[0] < 0.0f) return false;
@@ -1205,10 +1223,11 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	std::vector<uint32_t> cnt(R, 0);
 	std::vector<V3> ro(R), rd(R);
 	std::vector<float> rst(R), rdl(R, 1.0f), rml(R, 0.0f);
+	std::vector<uint32_t> rimg(R, 0);
 	for (uint32_t i = 0; i < R; ++i) {
 		V3 o, d;
 		float t;
-		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t, nullptr, nullptr, &rdl[i], &rml[i])) continue;
+		if (!train_ray(a, a.ray_index_offset + i, nrg, &o, &d, &t, nullptr, nullptr, &rdl[i], &rml[i], &rimg[i])) continue;
 		ro[i] = o; rd[i] = d; rst[i] = t;
 		cnt[i] = training_walk(stp, box, M.bits.data(), a.max_cascade, o, d, t, STEPS,
 		                       [](uint32_t, uint32_t, float, float, V3) {});
@@ -1242,11 +1261,19 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	}
 	M.total_samples = base;
 	const uint32_t S = std::min(base, MS);
+	// n_extra_dims > 0: every sample carries its image's latent code (generate_training_samples_nerf, :730, 824:
+	// extra_dims_gpu + img * n_extra_dims; here rows of 16)
+	const uint32_t XD = M.cfg.n_extra_dims;
+	std::vector<float> scodes(XD ? 16 * (size_t)S : 0, 0.0f);
+	if (XD && a.extra_dims)
+		for (uint32_t i = 0; i < R; ++i)
+			for (uint32_t j = 0; j < M.ray_numsteps[2 * i]; ++j)
+				for (uint32_t k = 0; k < 16; ++k) scodes[16 * ((size_t)M.ray_numsteps[2 * i + 1] + j) + k] = a.extra_dims[16 * (size_t)rimg[i] + k];
 	// inference over the emitted samples with the training params (testbed_nerf.cu:2800-2802)
 	std::vector<float> enc((size_t)M.L * S * M.F), out(4 * (size_t)S);
 	const bool ml_on = a.max_level_rand_training != 0;
 	hg_forward(M, M.p16.data(), M.coords.data(), 8, S, enc.data(), ml_on ? M.coords.data() + 7 : nullptr, 8);
-	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data());
+	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data(), XD ? scodes.data() : nullptr, 16);
 	M.mlp_out.assign(4 * (size_t)a.max_samples, 0);
 	for (size_t k = 0; k < out.size(); ++k) M.mlp_out[k] = f2h(out[k]);
 
@@ -1362,6 +1389,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	M.ccoords.assign(8 * (size_t)B, 0.0f);
 	M.dloss.assign(4 * (size_t)B, 0);
 	std::vector<float> cenc((size_t)M.L * B * M.F, 0.0f);
+	std::vector<float> ccodes(XD ? 16 * (size_t)B : 0, 0.0f);  // the compacted samples' latent codes
 	const float loss_scale = 128.0f / (float)nrg;
 	const float l2r = ract == 3 ? 1e-4f : 0.0f;
 	const float l1d = M.mean < 0.01f ? 1e-4f : 0.0f;
@@ -1421,6 +1449,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		for (uint32_t j = 0; j < cn; ++j) {
 			const size_t s = b0 + j, dst = cb + j;
 			for (int k = 0; k < 8; ++k) M.ccoords[8 * dst + k] = M.coords[8 * s + k];
+			for (uint32_t k = 0; k < (XD ? 16u : 0u); ++k) ccodes[16 * dst + k] = scodes[16 * s + k];
 			for (uint32_t l = 0; l < M.L; ++l)
 				for (uint32_t f = 0; f < M.F; ++f) cenc[((size_t)l * B + dst) * M.F + f] = enc[((size_t)l * S + s) * M.F + f];
 			const float* cw = &M.coords[8 * s];
@@ -1460,8 +1489,24 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	                  a.distortion_gradient_weight;
 	const bool cam = ext || dist;
 	std::vector<float> dsh(cam ? 16 * (size_t)C : 0), dpos(cam ? 3 * (size_t)C : 0);
+	const bool xgrad = XD && a.extra_dims_gradient;
+	std::vector<float> dextra(xgrad ? 16 * (size_t)C : 0);
 	mlp_backward(M, M.grads.data(), M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
-	             cam ? dsh.data() : nullptr);
+	             cam ? dsh.data() : nullptr, XD ? ccodes.data() : nullptr, 16, xgrad ? dextra.data() : nullptr);
+	if (xgrad) {
+		// compute_extra_dims_gradient_train_nerf (src/testbed_nerf.cu:1271-1306): each kept ray's compacted samples'
+		// dL/d(code) into its image's gradient
+		for (uint32_t i = 0; i < R; ++i) {
+			const uint32_t cn = M.ray_compacted[2 * i], cb = M.ray_compacted[2 * i + 1];
+			if (cn == 0) continue;
+			const uint32_t img = (uint32_t)lstate[8 * (size_t)i + 7];
+			for (uint32_t k = 0; k < XD; ++k) {
+				float g = 0.0f;
+				for (uint32_t j = 0; j < cn; ++j) g += dextra[16 * ((size_t)cb + j) + k];
+				a.extra_dims_gradient[16 * (size_t)img + k] += g;
+			}
+		}
+	}
 	const float* cml = ml_on ? M.ccoords.data() + 7 : nullptr;
 	if (cam) hg_input_grad(M, M.p16.data(), M.ccoords.data(), 8, C, denc.data(), wts.data(), dpos.data(), cml, 8);
 	hg_backward(M, M.ccoords.data(), 8, C, denc.data(), cml, 8);
@@ -1801,7 +1846,7 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 				const V3 w = tbox.rel(pos);
 				float coord[8] = {w.x, w.y, w.z, warp_dt(MIN_STEP), (dn.x + 1) * 0.5f, (dn.y + 1) * 0.5f, (dn.z + 1) * 0.5f, 0.0f};
 				hg_forward(M, P, coord, 8, 1, enc.data());
-				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data());
+				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data(), a.extra_dims, 0);
 				const float alpha = std::min(std::max(1.0f - std::exp(-to_density(out[3], dact) * 0.01f), 0.0f), 1.0f);
 				float c[4] = {to_rgb(out[0], ract) * alpha, to_rgb(out[1], ract) * alpha, to_rgb(out[2], ract) * alpha, alpha};
 				if (!a.train_in_linear_colors) for (int k = 0; k < 3; ++k) c[k] = s2l(c[k]);
@@ -1825,7 +1870,7 @@ static void render(const Model& M, const ngp_render_args& a, float* frame, float
 				const V3 w = tbox.rel(o + d * ts);
 				float coord[8] = {w.x, w.y, w.z, warp_dt(dt), wd.x, wd.y, wd.z, 0.0f};
 				hg_forward(M, P, coord, 8, 1, enc.data());
-				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data());
+				mlp_forward(M, P, enc.data(), coord, 8, 1, out.data(), a.extra_dims, 0);
 				const V3 pos = tbox.mn + v(coord[0] * (tbox.mx.x - tbox.mn.x), coord[1] * (tbox.mx.y - tbox.mn.y), coord[2] * (tbox.mx.z - tbox.mn.z));
 				const float T = 1.0f - c[3];
 				const float alpha = 1.0f - std::exp(-to_density(out[3], dact) * unwarp_dt(coord[3]));
@@ -2068,7 +2113,8 @@ void oref_infer(void* m, const float* coords, uint32_t fpc, uint32_t n, float* o
 	const uint16_t* P = use_inf ? M.inf16.data() : M.p16.data();
 	std::vector<float> enc((size_t)M.L * n * M.F);
 	hg_forward(M, P, coords, fpc, n, enc.data());
-	mlp_forward(M, P, enc.data(), coords, fpc, n, out);
+	// n_extra_dims > 0: the records' extra dims (floats 7 .. 7 + n_extra_dims) are the latent codes
+	mlp_forward(M, P, enc.data(), coords, fpc, n, out, M.cfg.n_extra_dims ? coords + 7 : nullptr, fpc);
 }
 // the reference's padded network output: 16 rows per sample, row 3 = density (extract_density)
 void oref_infer_padded(void* m, const float* coords, uint32_t fpc, uint32_t n, float* out16, int use_inf) {
@@ -2080,7 +2126,7 @@ void oref_infer_padded(void* m, const float* coords, uint32_t fpc, uint32_t n, f
 	const uint32_t NL = (uint32_t)M.layers.size();
 	for (uint32_t i = 0; i < n; ++i) {
 		gather_enc(M, enc.data(), n, i, col.data());
-		mlp_forward_one(M, P, col.data(), coords + (size_t)i * fpc + 4, A);
+		mlp_forward_one(M, P, col.data(), coords + (size_t)i * fpc + 4, A, M.cfg.n_extra_dims ? coords + (size_t)i * fpc + 7 : nullptr);
 		for (uint32_t r = 0; r < 16; ++r) out16[16 * (size_t)i + r] = A.a[NL][r];
 		out16[16 * (size_t)i + 3] = A.a[M.n_density_layers][0];
 	}
@@ -2108,6 +2154,14 @@ void oref_backward(void* m, const float* enc, const float* dirs, uint32_t n, con
 	std::vector<float> coords(8 * (size_t)n, 0.0f);
 	for (uint32_t i = 0; i < n; ++i) for (int k = 0; k < 3; ++k) coords[8 * i + 4 + k] = dirs[3 * i + k];
 	mlp_backward(M, M.grads.data(), M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc);
+}
+// the same with latent codes extra [n][16] and their input gradient dextra [n][16] (optional)
+void oref_backward_extra(void* m, const float* enc, const float* dirs, const float* extra, uint32_t n, const float* dloss,
+                         const float* weight, float* denc, float* dextra) {
+	Model& M = *static_cast<Model*>(m);
+	std::vector<float> coords(8 * (size_t)n, 0.0f);
+	for (uint32_t i = 0; i < n; ++i) for (int k = 0; k < 3; ++k) coords[8 * i + 4 + k] = dirs[3 * i + k];
+	mlp_backward(M, M.grads.data(), M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc, nullptr, extra, 16, dextra);
 }
 void oref_encode_backward(void* m, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
 	hg_backward(*static_cast<Model*>(m), pos, stride, n, denc);

@@ -45,6 +45,8 @@ _PROTOS = {
     "oref_mlp_forward_enc": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     "oref_density": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int]),
     "oref_backward": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p]),
+    "oref_backward_extra": (None, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                   C.c_void_p, C.c_void_p]),
     "oref_encode_backward": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p]),
     "oref_train_step": (C.c_int, [C.c_void_p, C.POINTER(A.TrainArgs)]),
     "oref_train_ray_samples": (C.c_uint32, [C.c_void_p, C.POINTER(A.TrainArgs), C.c_uint32, C.c_int, C.c_void_p,
@@ -191,6 +193,20 @@ class Oracle:
         w = None if weight is None else np.ascontiguousarray(weight, np.float32)
         self.lib.oref_backward(self.h, ptr(enc), ptr(dirs), n, ptr(dloss), None if w is None else ptr(w), ptr(denc))
         return denc
+
+    def backward_extra(self, enc, dirs, extra, dloss, weight=None):
+        """backward() with the samples' latent codes extra [n][16]; returns (dL/denc, dL/dextra [n][16])."""
+        enc = np.ascontiguousarray(enc, np.float32)
+        dirs = np.ascontiguousarray(dirs, np.float32)
+        extra = np.ascontiguousarray(extra, np.float32)
+        dloss = np.ascontiguousarray(dloss, np.float32)
+        n = dirs.shape[0]
+        denc = np.zeros((self.L, n, self.F), np.float32)
+        dx = np.zeros((n, 16), np.float32)
+        w = None if weight is None else np.ascontiguousarray(weight, np.float32)
+        self.lib.oref_backward_extra(self.h, ptr(enc), ptr(dirs), ptr(extra), n, ptr(dloss), None if w is None else ptr(w),
+                                     ptr(denc), ptr(dx))
+        return denc, dx
 
     def encode_backward(self, pos, denc):
         pos = np.ascontiguousarray(pos, np.float32)

@@ -107,13 +107,86 @@ def test_infer_padded_output_matches_oracle(name, layout_rm):
         g.close()
 
 
-def test_extra_dims_are_refused():
-    """n_extra_dims > 0 (per-image latent codes) is not implemented: model creation fails loudly."""
-    from gpu_util import GpuModel
-    cfg = A.default_config(**CONFIGS["A_L4F2T14"])
-    cfg.n_extra_dims = 4
-    with pytest.raises(RuntimeError, match="n_extra_dims"):
-        GpuModel(cfg)
+def make_extra(n_extra, seed=3):
+    from gpu_util import GpuModel, random_params
+    cfg = A.default_config(**CONFIGS["B_L16F2T19"], n_extra_dims=n_extra)
+    g = GpuModel(cfg)
+    o = Oracle(cfg)
+    rng = np.random.default_rng(seed)
+    p = random_params(g.n_params, g.n_mlp, g.info, rng, 0.5)
+    g.set_params(p)
+    o.set_params(p)
+    return g, o, rng
+
+
+@pytest.mark.parametrize("n_extra", [16, 3])
+def test_extra_dims_infer_matches_oracle(n_extra):
+    """NerfNetwork with n_extra_dims (nerf_network.h:81-93): the records' extra dims (floats 7 .. 7 + E, the latent
+    code) enter the rgb network after the SH (rgb input next_multiple(32 + E, 16) = 48 wide); against the oracle, and
+    a zero code differs from a random one only in the rgb outputs."""
+    g, o, rng = make_extra(n_extra)
+    try:
+        assert g.info.layer_in[2] == 48
+        n = 3000
+        coords = np.zeros((n, 7 + n_extra), np.float32)
+        coords[:, :7] = random_coords(rng, n)
+        coords[:, 7:] = rng.normal(0, 1, (n, n_extra))
+        go = g.infer(coords)
+        oo = o.infer(coords)
+        err = np.abs(go - oo)
+        tol = 4e-3 + 8e-3 * np.abs(oo)
+        assert (err <= tol).mean() > 0.999, f"max err {err.max()}"
+        assert err.mean() < 1e-3
+        zero = coords.copy()
+        zero[:, 7:] = 0
+        gz = g.infer(zero)
+        np.testing.assert_array_equal(gz[:, 3], go[:, 3])  # density does not see the code
+        assert np.abs(gz[:, :3] - go[:, :3]).mean() > 1e-3
+        gp = g.infer_padded(coords, 1)
+        np.testing.assert_array_equal(gp[:, :4], go)
+        with pytest.raises(RuntimeError, match="floats_per_coord"):
+            g.infer(coords[:, :7])
+    finally:
+        g.close()
+
+
+def test_extra_dims_mlp_backward_matches_oracle():
+    """The fused training MLP with the latent-code rows (Net XE: 48-row rgb input, the images' code segment last):
+    weight gradients (incl. the rgb first layer's code columns) and dL/denc against the oracle, and dL/d(code) of
+    each sample's own row (the input gradient compute_extra_dims_gradient_train_nerf sums)."""
+    g, o, rng = make_extra(16)
+    try:
+        n = 1000
+        coords = random_coords(rng, n)
+        enc = o.encode(coords[:, :3])
+        extra = rng.normal(0, 1, (n, 16)).astype(np.float32)
+        dl = (rng.normal(0, 1e-2, (n, 4))).astype(np.float16).astype(np.float32)
+        w = rng.uniform(1, 2, n).astype(np.float32)
+        g.zero_grads()
+        gd, gx = g.backward_extra(enc, coords[:, 4:7], extra, dl, w)
+        od, ox = o.backward_extra(enc, coords[:, 4:7], extra, dl, w)
+        gg = g.get(A.GRADS_FP32)[: g.n_mlp]
+        og = o.get(A.GRADS_FP32)[: o.n_mlp]
+        rel = np.linalg.norm(gg - og) / np.linalg.norm(og)
+        assert rel < 1e-2, rel
+        # the rgb first layer's code columns (32..47 of its 48) carry gradient
+        off, lin = g.info.layer_param_offset[2], g.info.layer_in[2]
+        wcode = gg[off:off + 64 * lin].reshape(64, lin)[:, 32:48]
+        assert np.abs(wcode).max() > 0
+        dr = np.linalg.norm(gd - od) / max(np.linalg.norm(od), 1e-12)
+        assert dr < 1e-2, dr
+        xr = np.linalg.norm(gx - ox) / max(np.linalg.norm(ox), 1e-12)
+        assert np.abs(ox).max() > 0 and xr < 1e-2, xr
+        # without extra dims the same call is refused; n_extra_dims > 16 too
+        from gpu_util import GpuModel
+        cfg = A.default_config(**CONFIGS["A_L4F2T14"], n_extra_dims=4)
+        with pytest.raises(RuntimeError, match="n_extra_dims"):
+            GpuModel(cfg)
+        cfg = A.default_config(**CONFIGS["B_L16F2T19"], n_extra_dims=17)
+        with pytest.raises(RuntimeError, match="n_extra_dims"):
+            GpuModel(cfg)
+    finally:
+        g.close()
 
 
 @pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
