@@ -232,7 +232,8 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readwrite("resolution", &TrainingImageMetadata::resolution)
 		.def_readwrite("principal_point", &TrainingImageMetadata::principal_point)
 		.def_readwrite("focal_length", &TrainingImageMetadata::focal_length)
-		.def_readwrite("rolling_shutter", &TrainingImageMetadata::rolling_shutter);
+		.def_readwrite("rolling_shutter", &TrainingImageMetadata::rolling_shutter)
+		.def_readwrite("light_dir", &TrainingImageMetadata::light_dir);
 
 	py::class_<NerfDataset>(m, "NerfDataset")
 		.def_readonly("metadata", &NerfDataset::metadata)
@@ -255,6 +256,9 @@ PYBIND11_MODULE(pyngp, m) {
 		.def_readonly("aabb_scale", &NerfDataset::aabb_scale)
 		.def_readonly("from_mitsuba", &NerfDataset::from_mitsuba)
 		.def_readonly("is_hdr", &NerfDataset::is_hdr)
+		.def_readwrite("n_extra_learnable_dims", &NerfDataset::n_extra_learnable_dims)
+		.def_readonly("has_light_dirs", &NerfDataset::has_light_dirs)
+		.def("n_extra_dims", &NerfDataset::n_extra_dims)
 		.def("image", [](const NerfDataset& d, size_t i) {
 			if (i >= d.n_images) throw std::runtime_error("Invalid frame index");
 			const auto& md = d.metadata[i];
@@ -414,6 +418,7 @@ PYBIND11_MODULE(pyngp, m) {
 		NV_RW("visualize_cameras", visualize_cameras)
 		NV_RW("glow_y_cutoff", glow_y_cutoff)
 		NV_RW("glow_mode", glow_mode)
+		NV_RW("light_dir", light_dir)
 #undef NV_RW
 		.def("find_closest_training_view", [](const NerfView& v) { return v.tb->find_closest_training_view(); },
 		     "Obtain the training view that is closest to the current camera.")

@@ -222,7 +222,7 @@ Testbed::~Testbed() {
 		if (p) (void)hipFree(p);
 	if (m_red_buf) (void)hipFree(m_red_buf);
 	if (m_pack) (void)hipFree(m_pack);
-	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid, m_dist, m_dist_grad})
+	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid, m_dist, m_dist_grad, m_extra, m_extra_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
@@ -288,6 +288,7 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 		const std::string base = parent_path(jp);
 		if (j.contains("scale")) ds.scale = (float)j["scale"].num();
 		if (j.contains("aabb_scale")) ds.aabb_scale = (int)j["aabb_scale"].num();
+		if (j.contains("n_extra_learnable_dims")) ds.n_extra_learnable_dims = (uint32_t)j["n_extra_learnable_dims"].num();  // :478-480
 		if (j.contains("offset")) {
 			if (j["offset"].is_array()) ds.offset = {(float)j["offset"][0].num(), (float)j["offset"][1].num(), (float)j["offset"][2].num()};
 			else ds.offset = {(float)j["offset"].num(), (float)j["offset"].num(), (float)j["offset"].num()};
@@ -423,6 +424,17 @@ NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder
 				}
 			ds.xforms.push_back(ds.nerf_matrix_to_ngp(r));
 			ds.xforms_end.push_back(ds.nerf_matrix_to_ngp(re));  // = start without transform_matrix_end
+			// the frame's light direction (nerf_loader.cu:666-675, nerf_direction_to_ngp nerf_loader.h:91-99): an extra
+			// network input; such datasets carry no learnable code
+			if (fr.contains("driver_parameters")) {
+				const Json& dp = fr["driver_parameters"];
+				const vec3 l = {(float)dp.value("LightX", 0.0), (float)dp.value("LightY", 0.0), (float)dp.value("LightZ", 0.0)};
+				const float n = std::sqrt(l[0] * l[0] + l[1] * l[1] + l[2] * l[2]);
+				const vec3 ln = n > 0.f ? vec3{l[0] / n, l[1] / n, l[2] / n} : l;
+				md.light_dir = ds.from_mitsuba ? vec3{-ln[0], -ln[1], -ln[2]} : vec3{ln[1], ln[2], ln[0]};
+				ds.has_light_dirs = true;
+				ds.n_extra_learnable_dims = 0;
+			}
 			ds.metadata.push_back(md);
 			ds.paths.push_back(fp);
 			ds.pixels.push_back(std::move(rgba));
@@ -546,6 +558,21 @@ void Testbed::load_nerf_post() {
 	while ((1 << nerf.max_cascade) < ds.aabb_scale) ++nerf.max_cascade;
 	nerf.cone_angle_constant = ds.aabb_scale <= 1 ? 0.0f : (1.0f / 256.0f);
 	m_dataset_dirty = true;
+	// load_nerf (src/testbed_nerf.cu:2176-2177): fresh latent codes, optimised when the dataset asks for them
+	if (ds.n_extra_dims()) {
+		pcg32 r(seed);
+		if (m_rng_inc) {
+			r.state = m_rng_state;
+			r.inc = m_rng_inc;
+		}
+		reset_extra_dims(&r);
+		m_rng_state = r.state;
+		m_rng_inc = r.inc;
+	} else {
+		reset_extra_dims(nullptr);  // no codes: nothing is drawn
+	}
+	nerf.training.optimize_extra_dims = ds.n_extra_learnable_dims > 0;
+	if (m_model && m_net_cfg.n_extra_dims != ds.n_extra_dims()) reset_network();
 }
 
 void Testbed::set_image_rgba8(int frame_idx, const uint8_t* rgba, int width, int height) {
@@ -861,6 +888,7 @@ void Testbed::reset_network(bool clear_density_grid) {
 	nerf.training.cam_focal_length_offset = NerfTraining::Adam2{};
 	if (training_data_available) m_dataset_dirty = true;
 	pcg32 grid_rng(rng.next_uint());
+	reset_extra_dims(&rng);  // src/testbed.cu:3736
 	m_rng_state = rng.state;
 	m_rng_inc = rng.inc;
 	nerf.training.density_grid_rng_state = grid_rng.state;
@@ -902,6 +930,8 @@ void Testbed::build_model(const Json& cfg) {
 		throw std::runtime_error("density and rgb MLPs must share n_neurons on this build");
 	c.rgb_activation = (int32_t)nerf.rgb_activation;
 	c.density_activation = (int32_t)nerf.density_activation;
+	// NerfNetwork(n_pos_dims, n_dir_dims, n_extra_dims = dataset.n_extra_dims(), ...) (src/testbed.cu:3742-3756)
+	c.n_extra_dims = nerf.training.dataset.n_extra_dims();
 	// optimizer chain: [Ema] -> [ExponentialDecay] -> Adam (configs/nerf/base.json:5-22)
 	c.ema_decay = 0.0f;
 	c.decay_start = 0xFFFFFFFFu;
@@ -1143,6 +1173,17 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	}
 	a.deterministic = deterministic ? 1 : 0;
 	a.max_level_rand_training = m_max_level_rand_training ? 1 : 0;
+	// per-image latent codes (src/testbed_nerf.cu:2478-2484, 2792-2793): the table, and its gradient (cleared per step)
+	// while they are optimised
+	const bool train_extra_dims = tr.dataset.n_extra_learnable_dims > 0 && tr.optimize_extra_dims;
+	if (n_extra_dims()) {
+		if (!m_extra) upload_extra_dims();
+		a.extra_dims = m_extra;
+		if (train_extra_dims) {
+			hk(hipMemsetAsync(m_extra_grad, 0, (m_extra_rows - 1) * 16 * sizeof(float), (hipStream_t)m_stream), "extra dims gradient clear");
+			a.extra_dims_gradient = m_extra_grad;
+		}
+	}
 	for (int k = 0; k < 3; ++k) { a.aabb_min[k] = aabb_min[k]; a.aabb_max[k] = aabb_max[k]; }
 	a.cone_angle_constant = nerf.cone_angle_constant;
 	a.max_cascade = nerf.max_cascade;
@@ -1241,6 +1282,11 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 			train_full_forward = true;
 			a.full_forward = 1;
 		}
+	}
+	// the latent codes' Adam step on every step (src/testbed_nerf.cu:2580-2599); data parallel: their gradient summed
+	if (train_extra_dims) {
+		if (distributed()) allreduce_f32(m_extra_grad, (m_extra_rows - 1) * 16, false);
+		update_extra_dims_step();
 	}
 	++training_step;
 	// CDFs from the error map, every n_steps_between_error_map_updates (x1.5 each time)
@@ -1488,6 +1534,12 @@ void Testbed::train(uint32_t batch_size) {
 		reload_network_from_file();
 		if (!m_model) throw std::runtime_error("Unable to create a neural network trainer.");
 	}
+	// Testbed::train (src/testbed.cu:4046-4053): per-image latents requested without a learnable code -> 16 dims
+	if (nerf.training.optimize_extra_dims && nerf.training.dataset.n_extra_learnable_dims == 0) {
+		nerf.training.dataset.n_extra_learnable_dims = 16;
+		reset_network();
+	}
+	if (m_net_cfg.n_extra_dims != n_extra_dims()) reset_network();  // the network's input width follows the dataset
 	reset_accumulation();
 	// density-grid cadence (src/testbed.cu:4060) + training_prep_nerf (src/testbed_nerf.cu:2933-2946)
 	const uint32_t n_prep_to_skip = std::min(std::max(training_step / 16u, 1u), 16u);
@@ -1630,12 +1682,126 @@ void Testbed::set_rendering_extra_dims(const std::vector<float>& vals) {
 		throw std::runtime_error("Invalid number of extra dims. Got " + std::to_string(vals.size()) + " but must be " +
 		                         std::to_string(n_extra_dims()) + ".");
 	rendering_extra_dims_from_training_view = -1;
+	m_rendering_extra_dims = vals;
 }
 
+// Nerf::get_rendering_extra_dims_cpu: the code set with set_rendering_extra_dims (the training view's code when
+// rendering_extra_dims_from_training_view selects one is what the renderer uses, not this buffer)
+std::vector<float> Testbed::rendering_extra_dims() const { return m_rendering_extra_dims; }
+
 std::vector<float> Testbed::training_extra_dims(int trainview) const {
-	if (n_extra_dims() == 0) return {};  // Nerf::Training::get_extra_dims_cpu (src/testbed_nerf.cu:1797-1800)
+	if (n_extra_dims() == 0) return {};  // Nerf::Training::get_extra_dims_cpu (src/testbed_nerf.cu:1797-1812)
 	if (trainview < 0 || (size_t)trainview >= nerf.training.dataset.n_images) throw std::runtime_error("Invalid training view.");
-	return {};
+	if ((size_t)trainview >= nerf.training.extra_dims_opt.size()) return std::vector<float>(n_extra_dims(), 0.0f);
+	return nerf.training.extra_dims_opt[trainview].variable;
+}
+
+// VarAdamOptimizer::step (adam_optimizer.h:41-51)
+void NerfTraining::VarAdam::step(const std::vector<float>& g) {
+	++iter;
+	const float lr = learning_rate * std::sqrt(1.0f - std::pow(beta2, (float)iter)) / (1.0f - std::pow(beta1, (float)iter));
+	for (size_t i = 0; i < m.size(); ++i) {
+		m[i] = beta1 * m[i] + (1.0f - beta1) * g[i];
+		v[i] = beta2 * v[i] + (1.0f - beta2) * g[i] * g[i];
+		variable[i] -= lr * m[i] / (std::sqrt(v[i]) + epsilon);
+	}
+}
+
+// Nerf::reset_extra_dims (src/testbed_nerf.cu:3181-3204): per image a fresh VarAdamOptimizer(n_extra_dims, 1e-4) whose
+// variable starts at the frame's light direction (first 3, datasets with light dirs) and uniform [-1, 1) values
+// (random_val(rng) * 2 - 1) after it; the rendered code starts as image 0's
+void Testbed::reset_extra_dims(pcg32* rng) {
+	NerfTraining& tr = nerf.training;
+	const uint32_t E = tr.dataset.n_extra_dims();
+	tr.extra_dims_opt.clear();
+	m_rendering_extra_dims.assign(E, 0.0f);
+	if (!E) return;
+	if (E > 16) throw std::runtime_error("n_extra_dims > 16 is not supported (light directions + latent code)");
+	const size_t n = tr.dataset.n_images;
+	tr.extra_dims_opt.resize(n);
+	for (size_t i = 0; i < n; ++i) {
+		NerfTraining::VarAdam& o = tr.extra_dims_opt[i];
+		o.variable.assign(E, 0.0f);
+		o.m.assign(E, 0.0f);
+		o.v.assign(E, 0.0f);
+		for (uint32_t j = 0; j < E; ++j) {
+			if (tr.dataset.has_light_dirs && j < 3 && i < tr.dataset.metadata.size()) {
+				const vec3 ld = tr.dataset.metadata[i].light_dir;
+				const float l = std::sqrt(ld[0] * ld[0] + ld[1] * ld[1] + ld[2] * ld[2]);
+				o.variable[j] = l > 0.f ? (ld[j] / l + 1.0f) * 0.5f : 0.5f;  // warp_direction(normalize(light_dir))
+			} else {
+				o.variable[j] = rng->next_float() * 2.0f - 1.0f;
+			}
+		}
+	}
+	if (n) m_rendering_extra_dims = tr.extra_dims_opt[0].variable;
+	upload_extra_dims();
+}
+
+// Nerf::Training::update_extra_dims (src/testbed_nerf.cu:1814-1825): the codes into the device table, rows of 16
+void Testbed::upload_extra_dims() {
+	const NerfTraining& tr = nerf.training;
+	const uint32_t E = tr.dataset.n_extra_dims();
+	if (!E) return;
+	const size_t rows = std::max(tr.dataset.n_images, tr.extra_dims_opt.size()) + 1;  // + the rendered code's row
+	if (m_extra_rows != rows) {
+		sync();
+		for (float* p : {m_extra, m_extra_grad})
+			if (p) (void)hipFree(p);
+		m_extra = m_extra_grad = nullptr;
+		hk(hipMalloc((void**)&m_extra, rows * 16 * sizeof(float)), "hipMalloc extra dims");
+		hk(hipMalloc((void**)&m_extra_grad, rows * 16 * sizeof(float)), "hipMalloc extra dims gradient");
+		hk(hipMemset(m_extra, 0, rows * 16 * sizeof(float)), "hipMemset extra dims");
+		m_extra_rows = rows;
+	}
+	m_extra_host.assign(rows * 16, 0.0f);
+	for (size_t i = 0; i < tr.extra_dims_opt.size(); ++i)
+		for (uint32_t j = 0; j < E; ++j) m_extra_host[16 * i + j] = tr.extra_dims_opt[i].variable[j];
+	hk(hipMemcpy(m_extra, m_extra_host.data(), (rows - 1) * 16 * sizeof(float), hipMemcpyHostToDevice), "upload extra dims");
+}
+
+// Nerf::get_rendering_extra_dims (src/testbed_nerf.cu:3206-3228): a training view's code or the set one, with the
+// light direction first for datasets with light dirs -- written into the table's spare last row
+const float* Testbed::rendering_extra_dims_device() {
+	const NerfTraining& tr = nerf.training;
+	const uint32_t E = tr.dataset.n_extra_dims();
+	if (!E) return nullptr;
+	if (!m_extra) upload_extra_dims();
+	std::vector<float> row(16, 0.0f);
+	const int v = rendering_extra_dims_from_training_view;
+	const std::vector<float>& src = v >= 0 && (size_t)v < tr.extra_dims_opt.size() ? tr.extra_dims_opt[v].variable : m_rendering_extra_dims;
+	for (uint32_t j = 0; j < E && j < src.size(); ++j) row[j] = src[j];
+	if (tr.dataset.has_light_dirs) {
+		const vec3 ld = nerf.light_dir;
+		const float l = std::sqrt(ld[0] * ld[0] + ld[1] * ld[1] + ld[2] * ld[2]);
+		for (int j = 0; j < 3; ++j) row[j] = l > 0.f ? (ld[j] / l + 1.0f) * 0.5f : 0.5f;
+	}
+	const size_t n = m_extra_rows - 1;
+	std::copy(row.begin(), row.end(), m_extra_host.begin() + 16 * n);
+	hk(hipMemcpyAsync(m_extra + 16 * n, m_extra_host.data() + 16 * n, 16 * sizeof(float), hipMemcpyHostToDevice,
+	                  (hipStream_t)m_stream), "upload rendering extra dims");
+	return m_extra + 16 * n;
+}
+
+// train_nerf's latent-code step (src/testbed_nerf.cu:2580-2599): the codes' gradient (loss-scaled sums over the
+// kept rays' samples) to the host, / LOSS_SCALE, one VarAdam step per training image at the network's current
+// learning rate, then the codes back to the device
+void Testbed::update_extra_dims_step() {
+	NerfTraining& tr = nerf.training;
+	const uint32_t E = tr.dataset.n_extra_dims();
+	const size_t n = m_extra_rows - 1;
+	std::vector<float> g(n * 16);
+	hk(hipMemcpyAsync(g.data(), m_extra_grad, n * 16 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream),
+	   "extra dims gradient d2h");
+	sync();
+	const float lr = current_learning_rate();
+	for (int i = 0; i < tr.n_images_for_training && (size_t)i < tr.extra_dims_opt.size(); ++i) {
+		std::vector<float> gi(E);
+		for (uint32_t j = 0; j < E; ++j) gi[j] = g[16 * (size_t)i + j] / 128.0f;
+		tr.extra_dims_opt[i].learning_rate = lr;
+		tr.extra_dims_opt[i].step(gi);
+	}
+	upload_extra_dims();
 }
 
 int Testbed::find_closest_training_view() const {
@@ -1659,6 +1825,7 @@ void Testbed::set_camera_to_training_view(int trainview) {
 	nerf.render_lens = md.lens;  // src/testbed.cu:477-478
 	screen_center = {1.0f - md.principal_point[0], 1.0f - md.principal_point[1]};
 	nerf.training.view = trainview;
+	if (n_extra_dims()) set_rendering_extra_dims_from_training_view(trainview);  // src/testbed.cu:2207-2209
 	m_spp = 0;
 }
 
@@ -1795,6 +1962,7 @@ void Testbed::render_into(float* host_dst, int width, int height, int spp, bool 
 	r.depth_scale = 1.0f / nerf.training.dataset.scale;  // src/testbed_nerf.cu:1905
 	r.glow_mode = nerf.glow_mode;
 	r.glow_y_cutoff = nerf.glow_y_cutoff;
+	r.extra_dims = rendering_extra_dims_device();  // NerfTracer's extra_dims_gpu (src/testbed_nerf.cu:1848, 1922)
 	r.gbuffer_hard_edges = nerf.render_gbuffer_hard_edges;
 	// plane_z = m_slice_plane_z + m_scale (src/testbed_nerf.cu:1842): the Slice plane, or the focus plane of the
 	// depth of field (init_rays_with_payload_kernel_nerf drops the aperture when plane_z < 0, :1427-1429)
@@ -1956,7 +2124,25 @@ void Testbed::save_snapshot(const std::string& path, bool include_optimizer_stat
 	ds["up"] = vec_json(nerf.training.dataset.up.data(), 3);
 	ds["is_hdr"] = Json(nerf.training.dataset.is_hdr);
 	ds["n_images"] = Json((double)nerf.training.dataset.n_images);
+	ds["n_extra_learnable_dims"] = Json((double)nerf.training.dataset.n_extra_learnable_dims);
 	nj["dataset"] = ds;
+	// the latent codes' optimisers (src/testbed.cu:4795, VarAdamOptimizer::to_json adam_optimizer.h:73-82)
+	{
+		Json a = Json::array();
+		for (const auto& o : nerf.training.extra_dims_opt) {
+			Json j = Json::object();
+			j["iter"] = Json((double)o.iter);
+			j["first_moment"] = vec_json(o.m.data(), o.m.size());
+			j["second_moment"] = vec_json(o.v.data(), o.v.size());
+			j["variable"] = vec_json(o.variable.data(), o.variable.size());
+			j["learning_rate"] = Json((double)o.learning_rate);
+			j["epsilon"] = Json((double)o.epsilon);
+			j["beta1"] = Json((double)o.beta1);
+			j["beta2"] = Json((double)o.beta2);
+			a.push_back(std::move(j));
+		}
+		nj["extra_dims_opt"] = a;
+	}
 	// per-image extrinsic offsets as the reference's AdamOptimizer to_json objects
 	// (src/testbed.cu:4793-4794, adam_optimizer.h:172-183)
 	auto adam_json = [](const std::vector<NerfTraining::Adam3>& v) {
@@ -2049,6 +2235,9 @@ void Testbed::load_snapshot(const std::string& path) {
 			for (int k = 0; k < 3; ++k) nerf.training.dataset.offset[k] = (float)ds["offset"][k].num();
 		nerf.training.dataset.is_hdr = ds.value("is_hdr", false);
 	}
+	if (nj.contains("dataset"))  // src/testbed.cu:4879
+		nerf.training.dataset.n_extra_learnable_dims =
+		    (uint32_t)nj["dataset"].value("n_extra_learnable_dims", (double)nerf.training.dataset.n_extra_learnable_dims);
 	{  // load_nerf_post: aabb, cascades, cone angle, activations
 		const int s = nerf.training.dataset.aabb_scale;
 		const float half = 0.5f * (float)std::min(128, s);
@@ -2093,6 +2282,31 @@ void Testbed::load_snapshot(const std::string& path) {
 	root.erase("snapshot");
 	m_network_config = root;
 	reset_network(false);
+	if (nj.contains("extra_dims_opt") && nj["extra_dims_opt"].is_array() && n_extra_dims()) {  // src/testbed.cu:4948-4950
+		const Json& xa = nj["extra_dims_opt"];
+		auto& opt = nerf.training.extra_dims_opt;
+		opt.resize(xa.size());
+		for (size_t i = 0; i < xa.size(); ++i) {
+			const Json& j = xa[i];
+			auto vec = [&](const char* k) {
+				std::vector<float> v;
+				if (j.contains(k))
+					for (size_t q = 0; q < j[k].size(); ++q) v.push_back((float)j[k][q].num());
+				return v;
+			};
+			opt[i].iter = (uint32_t)j.value("iter", 0.0);
+			opt[i].m = vec("first_moment");
+			opt[i].v = vec("second_moment");
+			opt[i].variable = vec("variable");
+			opt[i].learning_rate = (float)j.value("learning_rate", 1e-4);
+			opt[i].epsilon = (float)j.value("epsilon", 1e-8);
+			opt[i].beta1 = (float)j.value("beta1", 0.9);
+			opt[i].beta2 = (float)j.value("beta2", 0.99);
+			if (opt[i].variable.size() != n_extra_dims() || opt[i].m.size() != n_extra_dims() || opt[i].v.size() != n_extra_dims())
+				throw std::runtime_error("snapshot: extra_dims_opt entries do not match n_extra_dims");
+		}
+		upload_extra_dims();
+	}
 	nerf.training.counters_rgb = saved_counters;
 	nerf.training.counters_rgb.rays_per_batch = saved_counters_rpb;
 	// dataset-specific optimised extrinsics (src/testbed.cu:4940-4951): restored when the

@@ -24,6 +24,7 @@ void pinned_host_release(void* p, size_t bytes);
 #include "json.h"
 
 namespace ngp {
+struct pcg32;
 
 enum class ETestbedMode : int { Nerf, Sdf, Image, Volume, Geometry, None };
 enum class EColorSpace : int { Linear, SRGB, VisPosNeg };
@@ -59,6 +60,7 @@ struct TrainingImageMetadata {
 	vec2 principal_point = {0.5f, 0.5f};
 	Lens lens;
 	vec4 rolling_shutter = {0.f, 0.f, 0.f, 0.f};  // pixel time A + B u + C v + D motionblur_time (nerf_loader.cu:204-216)
+	vec3 light_dir = {0.f, 0.f, 0.f};  // NGP space (frames with "driver_parameters", nerf_loader.cu:666-675)
 };
 
 struct NerfDataset {
@@ -80,6 +82,12 @@ struct NerfDataset {
 	bool is_hdr = false;
 	bool from_mitsuba = false;
 	size_t n_images = 0;
+	// per-image extra network inputs (nerf_loader.h:82-87): a learnable latent code of n_extra_learnable_dims
+	// (transforms.json "n_extra_learnable_dims", or 16 once optimize_extra_dims is set), preceded by the frame's
+	// light direction when frames carry "driver_parameters" (nerf_loader.cu:478-480, 666-675)
+	uint32_t n_extra_learnable_dims = 0;
+	bool has_light_dirs = false;
+	uint32_t n_extra_dims() const { return (has_light_dirs ? 3u : 0u) + n_extra_learnable_dims; }
 	// nerf_loader.h:95-116
 	Mat43 nerf_matrix_to_ngp(const float* nerf_3x4_rowmajor, bool scale_columns = false) const;
 	// compute_sharpness (src/nerf_loader.cu:111-151) of image i: [72][128] variance of the Laplacian of
@@ -144,6 +152,15 @@ struct NerfTraining {
 		uint32_t iter = 0;
 	} cam_focal_length_offset;
 	float intrinsic_l2_reg = 1e-4f;
+	// per-image latent codes (Nerf::Training::extra_dims_opt, nerf.h:82-86): one VarAdamOptimizer per image
+	// (adam_optimizer.h:25-117: lr 1e-4 until the first step takes the network's, eps 1e-8, beta 0.9 / 0.99)
+	struct VarAdam {
+		std::vector<float> variable, m, v;
+		uint32_t iter = 0;
+		float learning_rate = 1e-4f, epsilon = 1e-8f, beta1 = 0.9f, beta2 = 0.99f;
+		void step(const std::vector<float>& g);
+	};
+	std::vector<VarAdam> extra_dims_opt;
 	uint32_t n_steps_between_cam_updates = 16;
 	uint32_t n_steps_since_cam_update = 0;
 	uint32_t n_steps_between_error_map_updates = 128;
@@ -167,6 +184,7 @@ struct Nerf {
 	// composite_kernel_nerf's glow (nerf.h:176-177, src/testbed_nerf.cu:540-628)
 	float glow_y_cutoff = 0.f;
 	int glow_mode = 0;
+	vec3 light_dir = {0.5f, 0.5f, 0.5f};  // nerf.h:155: the rendered light direction of datasets with light dirs
 	// Nerf::find_closest_training_view (src/testbed_nerf.cu:3231-3244): the training view whose camera is
 	// nearest to pose (distance of the origins + 0.25 x distance of the forward axes); training.view if none
 	int find_closest_training_view(const Mat43& pose, const std::function<Mat43(size_t)>& transform) const;
@@ -234,14 +252,15 @@ public:
 	// testbed has no image (the reference divides an empty sum by zero elements: NaN)
 	float compute_image_mse(bool quantize_to_byte = false) const;
 	int find_closest_training_view() const;
-	// extra dims (per-image latent codes) of the rendered rays (Nerf::rendering_extra_dims, src/testbed_nerf.cu:1797-1812,
-	// 3246-3280).  This build trains without them (NerfDataset::n_extra_dims() == 0, optimize_extra_dims refused),
-	// so the reference's n_extra_dims() == 0 behaviour applies: empty vectors, "Dataset does not have extra dims."
-	uint32_t n_extra_dims() const { return 0; }
-	int rendering_extra_dims_from_training_view = -1;
+	// extra dims (per-image latent codes, NerfNetwork's n_extra_dims): the dataset's width, the codes of the
+	// training views (Nerf::Training::get_extra_dims_cpu, src/testbed_nerf.cu:1797-1812) and the code rendered rays
+	// carry -- a training view's (rendering_extra_dims_from_training_view >= 0, the default 0, nerf.h:157) or one set
+	// with set_rendering_extra_dims (src/testbed_nerf.cu:3206-3280)
+	uint32_t n_extra_dims() const { return nerf.training.dataset.n_extra_dims(); }
+	int rendering_extra_dims_from_training_view = 0;
 	void set_rendering_extra_dims_from_training_view(int trainview);
 	void set_rendering_extra_dims(const std::vector<float>& vals);
-	std::vector<float> rendering_extra_dims() const { return {}; }
+	std::vector<float> rendering_extra_dims() const;
 	std::vector<float> training_extra_dims(int trainview) const;
 
 	// --- snapshots (save_snapshot src/testbed.cu:4775, load_snapshot :4841) ---
@@ -370,6 +389,17 @@ private:
 		uint32_t optimizer_step = 0;
 		bool active = false;  // applied to training rays once optimize_distortion was set (a zero map is the identity)
 	} m_distortion;
+	// latent codes on the device: [n_images + 1][16] (the last row: the rendered code), their gradient
+	// [n_images][16]; rendering_extra_dims set by the caller (host, n_extra_dims values)
+	float* m_extra = nullptr;
+	float* m_extra_grad = nullptr;
+	size_t m_extra_rows = 0;
+	std::vector<float> m_rendering_extra_dims;
+	std::vector<float> m_extra_host;  // staging of the device table (the rendered row is copied asynchronously)
+	void reset_extra_dims(pcg32* rng);  // Nerf::reset_extra_dims (src/testbed_nerf.cu:3181-3204; rng: n_extra_dims > 0)
+	void upload_extra_dims();           // Nerf::Training::update_extra_dims (src/testbed_nerf.cu:1814-1825)
+	const float* rendering_extra_dims_device();  // Nerf::get_rendering_extra_dims (src/testbed_nerf.cu:3206-3228)
+	void update_extra_dims_step();      // the per-step latent-code Adam (src/testbed_nerf.cu:2580-2599)
 	float* m_dist = nullptr;       // device params [ry][rx][2]
 	float* m_dist_grad = nullptr;  // device [2][ry][rx][2]: gradient, gradient weight
 	void update_distortion_map();

@@ -1176,3 +1176,97 @@ def test_render_pipelines_match_oracle(pipes, shard):
         assert (np.abs(gd[rows][hit] - od[rows][hit]) <= 1e-3 * np.abs(od[rows][hit]) + 1e-4).mean() > 0.99
     finally:
         g.close()
+
+
+@pytest.mark.parametrize("n_extra", [16, 5])
+def test_train_step_extra_dims_matches_oracle(n_extra):
+    """Per-image latent codes (NerfNetwork n_extra_dims, src/testbed_nerf.cu:706-730, 824, 1271-1306): every sample of
+    a ray from image i carries code row i into the rgb network; the step's outputs and gradients match the oracle,
+    and extra_dims_gradient holds, per image, the sum of its kept rays' compacted samples' dL/d(code)."""
+    g, o, rng = pair(dict(CFG_B, n_extra_dims=n_extra))
+    try:
+        imgs, cams, focal = make_views(6, 24, 24)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        set_bitfield_both(g, o, sphere_bitfield(0.32), 0)
+        codes = np.zeros((6, 16), np.float32)
+        codes[:, :n_extra] = rng.uniform(-1, 1, (6, n_extra))
+        d_codes = torch.from_numpy(codes).cuda()
+        d_grad = torch.zeros(6 * 16, dtype=torch.float32, device="cuda")
+        h_grad = np.zeros(6 * 16, np.float32)
+        R, B, MS = 384, 4096, 1 << 15
+        ga = train_args(dd.ptr, dd.n, R, B, MS)
+        oa = train_args(hd.ptr, hd.n, R, B, MS)
+        ga.extra_dims, ga.extra_dims_gradient = d_codes.data_ptr(), d_grad.data_ptr()
+        oa.extra_dims = codes.ctypes.data_as(C.c_void_p).value
+        oa.extra_dims_gradient = h_grad.ctypes.data_as(C.c_void_p).value
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        o.train_step(oa)
+        g_ns = gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        o_ns = o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        np.testing.assert_array_equal(g_ns, o_ns)
+        ev = gpu_scratch(g, A.SCRATCH_RAY_EVALUATED, np.uint32) & 0x7FFFFFFF
+        evaluated = np.zeros(MS, bool)
+        for r, (n, b) in enumerate(o_ns):
+            evaluated[b:b + min(n, ev[r])] = True
+        g_out = gpu_scratch(g, A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][evaluated].astype(np.float32)
+        o_out = o.scratch(A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][evaluated].astype(np.float32)
+        assert evaluated.sum() > 500 and np.abs(g_out - o_out).mean() < 2e-3
+        gst, ost = A.TrainStats(), o.stats()
+        A.check(g.lib.ngp_train_read_stats(g.h, C.byref(gst), stream()))
+        np.testing.assert_allclose(gst.loss, ost.loss, rtol=2e-2)
+        gg, og = g.grads(), o.get(A.GRADS_FP32)
+        for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
+            rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
+            assert rel < 5e-2, rel
+        gx = d_grad.cpu().numpy().reshape(6, 16)
+        ox = h_grad.reshape(6, 16)
+        assert np.abs(ox[:, :n_extra]).max() > 0 and np.all(gx[:, n_extra:] == 0)
+        rel = np.linalg.norm(gx - ox) / np.linalg.norm(ox)
+        print(f"extra-dims gradient rel {rel:.2e}")
+        assert rel < 5e-2, rel
+        # a different code changes the rgb outputs (the network reads it)
+        codes2 = codes.copy()
+        codes2[:, :n_extra] = -codes2[:, :n_extra]
+        d_codes.copy_(torch.from_numpy(codes2))
+        g.zero_grads()
+        A.check(g.lib.ngp_train_step(g.h, C.byref(ga), stream()))
+        torch.cuda.synchronize()
+        g_out2 = gpu_scratch(g, A.SCRATCH_MLP_OUT, np.float16).reshape(-1, 4)[:MS][evaluated].astype(np.float32)
+        np.testing.assert_array_equal(g_out2[:, 3], g_out[:, 3])  # density does not see the code
+        assert np.abs(g_out2[:, :3] - g_out[:, :3]).mean() > 1e-3
+    finally:
+        g.close()
+
+
+def test_render_extra_dims_matches_oracle():
+    """The rendered samples carry the rendering code (Nerf::get_rendering_extra_dims, src/testbed_nerf.cu:3206-3228):
+    frame against the oracle's with the same code; a null code renders as zeros."""
+    g, o, rng = pair(dict(CFG_B, n_extra_dims=16), grid_scale=1.0)
+    try:
+        set_bitfield_both(g, o, sphere_bitfield(0.3))
+        W, H = 40, 32
+        cam = make_views(1, 8, 8)[1][0]
+        focal = 0.5 * W / np.tan(0.5 * 0.69)
+        code = rng.uniform(-1, 1, 16).astype(np.float32)
+        d_code = torch.from_numpy(code).cuda()
+        frames = []
+        for use in (True, False):
+            ra = render_args(W, H, cam, focal)
+            ra.extra_dims = d_code.data_ptr() if use else None
+            frame = torch.zeros(H * W * 4, dtype=torch.float32, device="cuda")
+            depth = torch.zeros(H * W, dtype=torch.float32, device="cuda")
+            A.check(g.lib.ngp_render(g.h, C.byref(ra), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
+            torch.cuda.synchronize()
+            gf = frame.cpu().numpy().reshape(H, W, 4)
+            rb = render_args(W, H, cam, focal)
+            rb.extra_dims = code.ctypes.data_as(C.c_void_p).value if use else None
+            of, _ = o.render(rb)
+            assert (of[..., 3] > 0.01).mean() > 0.2
+            l1 = np.abs(gf - of).mean()
+            assert l1 < 1e-3, (use, l1)
+            frames.append(gf)
+        assert np.abs(frames[0][..., :3] - frames[1][..., :3]).mean() > 1e-3
+    finally:
+        g.close()

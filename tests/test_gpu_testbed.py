@@ -384,8 +384,9 @@ def test_exposure_optimisation(scene):
     assert e.shape == (12, 3) and np.abs(e).max() > 0
     np.testing.assert_allclose(e.mean(axis=0), 0.0, atol=1e-5)
     assert np.isfinite(losses).all() and np.mean(losses[-16:]) < 0.6 * np.mean(losses[:16])
+    # per-image latents need the 64-neuron network (the tiny 16-wide one has no latent-code instance)
     tr.optimize_extra_dims = True
-    with pytest.raises(RuntimeError):
+    with pytest.raises(RuntimeError, match="n_extra_dims"):
         tb.frame()
 
 
@@ -661,3 +662,53 @@ def test_distortion_map_optimisation(scene):
     assert tb.nerf.render_with_lens_distortion
     f = tb.render(64, 64, 1, True)
     assert np.isfinite(f).all() and f[..., 3].max() > 0.1
+
+
+def test_optimize_extra_dims_trains_per_image_codes(scene, tmp_path):
+    """optimize_extra_dims (Testbed::train src/testbed.cu:4046-4053 -> 16 learnable dims and a network reset; the
+    per-step VarAdam of each image's code, src/testbed_nerf.cu:2580-2599): the codes start uniform in [-1, 1) and
+    move, rendering follows the training view's code (set_camera_to_training_view, src/testbed.cu:2207) or a set one,
+    and a snapshot carries the codes (extra_dims_opt, src/testbed.cu:4795, 4948) so the resumed Testbed renders the
+    same frame bit for bit."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("lego_L16F2.json")
+    tr = tb.nerf.training
+    assert tr.dataset.n_extra_dims() == 0 and not tr.optimize_extra_dims
+    tr.optimize_extra_dims = True
+    tb.shall_train = True
+    tb.frame()
+    assert tr.dataset.n_extra_learnable_dims == 16 and tr.dataset.n_extra_dims() == 16
+    c0 = [np.asarray(tr.get_extra_dims(i)) for i in range(12)]
+    assert all(c.shape == (16,) for c in c0) and max(np.abs(c).max() for c in c0) <= 1.0
+    while tb.training_step < 150:
+        tb.frame()
+    assert np.isfinite(tb.loss)
+    c1 = [np.asarray(tr.get_extra_dims(i)) for i in range(12)]
+    assert max(np.abs(a - b).max() for a, b in zip(c0, c1)) > 1e-4  # the codes train
+    tb.shall_train = False
+    tb.background_color = [0.0, 0.0, 0.0, 1.0]
+    tb.set_camera_to_training_view(3)
+    assert tb.nerf.rendering_extra_dims_from_training_view == 3
+    f3 = tb.render(48, 48, 1, True)
+    tb.nerf.set_rendering_extra_dims([float(x) for x in c1[7]])
+    assert tb.nerf.rendering_extra_dims_from_training_view == -1
+    np.testing.assert_allclose(tb.nerf.get_rendering_extra_dims(), c1[7])
+    f7 = tb.render(48, 48, 1, True)
+    tb.nerf.rendering_extra_dims_from_training_view = 7
+    np.testing.assert_array_equal(tb.render(48, 48, 1, True), f7)  # the same code either way
+    assert np.abs(f3 - f7).max() > 0  # another view's code changes the colours
+    with pytest.raises(RuntimeError, match="Invalid number of extra dims"):
+        tb.nerf.set_rendering_extra_dims([0.0] * 3)
+    snap = str(tmp_path / "extra.ingp")
+    tb.save_snapshot(snap, False)
+    _, tb2 = new_testbed()
+    tb2.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb2.load_snapshot(snap)
+    assert tb2.nerf.training.dataset.n_extra_dims() == 16
+    for i in range(12):
+        np.testing.assert_array_equal(np.asarray(tb2.nerf.training.get_extra_dims(i)), c1[i])
+    tb2.background_color = [0.0, 0.0, 0.0, 1.0]
+    tb2.set_camera_to_training_view(3)
+    np.testing.assert_array_equal(tb2.render(48, 48, 1, True), f3)
