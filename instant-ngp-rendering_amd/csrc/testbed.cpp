@@ -1062,10 +1062,6 @@ void Testbed::update_density_grid(uint32_t n_uniform, uint32_t n_nonuniform) {
 
 void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	if (nerf.training.n_images_for_training == 0) return;
-	{
-		const NerfTraining& t = nerf.training;
-		if (t.optimize_extra_dims) throw std::runtime_error("latent (extra dims) optimisation is not implemented by this build");
-	}
 	upload_dataset();
 	NerfCounters& ctr = nerf.training.counters_rgb;
 	// data parallelism: the ranks train one global batch of world x batch samples over
