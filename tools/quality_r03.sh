@@ -4,9 +4,9 @@
 #  * data/nerf/fox: every 8th frame held out (tools/split_scene.py), base.json (the fork's default);
 #  * the procedural lego-shaped scene: 100 train / 200 test views (tools/make_synthetic_scene.py),
 #    lego_L16F2.json (BASELINE config B).
-# Usage (GPU box, repo root): tools/quality_r03.sh [n_steps]
+# Usage (GPU box, repo root): tools/quality_r03.sh [n_steps] [tag]
 N=${1:-35000}
-OUT=gpurun_out/quality_r03
+OUT=gpurun_out/quality_${2:-r03}
 T=${TMPDIR:-/tmp}
 mkdir -p "$OUT"
 python3 tools/split_scene.py data/nerf/fox/transforms.json 8 "$T/fox_split" 2> "$OUT/split.log" || exit $?
