@@ -144,6 +144,31 @@ def _worker(rank, world, port, scene_dir, q):
         dist.destroy_process_group()
 
 
+def _extra_dims_worker(rank, world, port, scene_dir, q):
+    """optimize_extra_dims under data parallelism: every rank all-reduces the per-image code gradients and applies
+    the same VarAdam step, so codes and parameters stay identical on the ranks."""
+    import torch.distributed as dist
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        tb = _testbed(scene_dir, "lego_L16F2.json")
+        tb.init_distributed_host(rank, world, _host_allreduce(dist))
+        tr = tb.nerf.training
+        tr.optimize_extra_dims = True
+        tb.shall_train = True
+        tb.frame()
+        n = tr.dataset.n_images
+        c0 = np.stack([np.asarray(tr.get_extra_dims(i)) for i in range(n)])
+        while tb.training_step < 16:
+            tb.frame()
+        c1 = np.stack([np.asarray(tr.get_extra_dims(i)) for i in range(n)])
+        q.put(dict(rank=rank, c0=c0, c1=c1, params=_params(tb), loss=tb.loss, dims=tr.dataset.n_extra_dims()))
+    finally:
+        dist.destroy_process_group()
+
+
 @pytest.fixture(scope="module")
 def scene(tmp_path_factory):
     root = tmp_path_factory.mktemp("dp_scene")
@@ -385,3 +410,16 @@ def test_deterministic_mode_switches_off_between_steps(scene):
     assert np.isfinite(out[1][1]).all() and np.isfinite(out[1][2])
     assert out[1][2] == pytest.approx(out[0][2], rel=0.25)
 
+
+
+def test_extra_dims_train_identically_on_every_rank(scene):
+    """The per-image latent codes (extra dims) under data parallelism: the ranks draw the same initial codes, sum
+    their code gradients and take the same VarAdam step, so after 16 steps codes and parameters are bit-identical
+    on both ranks, and the codes have moved."""
+    res = _spawn(_extra_dims_worker, scene, 2)
+    r0, r1 = res[0], res[1]
+    assert r0["dims"] == r1["dims"] == 16
+    np.testing.assert_array_equal(r0["c0"], r1["c0"])
+    np.testing.assert_array_equal(r0["c1"], r1["c1"])
+    np.testing.assert_array_equal(r0["params"], r1["params"])
+    assert np.isfinite(r0["loss"]) and np.abs(r0["c1"] - r0["c0"]).max() > 1e-4
