@@ -343,7 +343,7 @@ typedef struct ngp_tuning {
 	uint32_t render_pipelines;       /* ray pipelines on their own streams, 1..4; 0: 2 for frames of >= 2^16 rays */
 	uint32_t render_pass_samples;    /* a pipeline's sample-slot budget per march pass (<= 2^24); 0: 5 * 2^20 */
 	uint32_t render_lanes;           /* lane budget from which k_generate picks lanes per ray; 0: 2^22 */
-	uint32_t render_first_steps;     /* per-ray sample cap of the first pass (doubling per pass); 0: 4 */
+	uint32_t render_first_steps;     /* per-ray sample cap of the first pass (doubling per pass); 0: 8 after a frame of >= 12 samples per ray, else 4 */
 	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 */
 	uint32_t render_lag;             /* passes a pipeline runs ahead of its counter read-backs, 2..4; 0: 3 */
 	float render_budget_scale;       /* headroom of the per-ray transmittance budget; 0: 1.0; < 0: no budget */

@@ -901,7 +901,12 @@ static uint32_t pass_sample_target(const ngp_tuning& t) {
 	// 5 M: 13.78 vs 13.96 ms per frame against 4 M (6 M 13.82, 8 M 13.99; same weights, profiles/r03_pass_size_ab.txt)
 	return std::min<uint32_t>(t.render_pass_samples ? t.render_pass_samples : 5u << 20, 16u << 20);
 }
-static uint32_t first_pass_steps(const ngp_tuning& t) { return t.render_first_steps ? t.render_first_steps : 4u; }
+// A volume's rays (the model's last frame above VOLUME_SAMPLES_PER_RAY network samples per ray) start with 8:
+// 13.69 vs 13.82 ms per fire frame; a surface scene's keep 4 (8: 2.19 vs 2.11 ms; profiles/r04_first_steps_ab.txt)
+constexpr float VOLUME_SAMPLES_PER_RAY = 12.0f;
+static uint32_t first_pass_steps(const ngp_tuning& t, float last_spr) {
+	return t.render_first_steps ? t.render_first_steps : (last_spr >= VOLUME_SAMPLES_PER_RAY ? 8u : 4u);
+}
 static uint32_t max_steps_per_pass(const ngp_tuning& t) { return t.render_max_steps ? t.render_max_steps : 32u; }
 
 // rows r < h_shard of a shard with (r / 8) % pipe_count == pipe_index
@@ -921,7 +926,7 @@ static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_c
 // and MLP work to overlap with: there one pipeline measured 2.7 % faster per 1080p frame against two
 // (profiles/r04_mlp_tile_ab.txt), a ~45-sample volume 6 % slower, so the default follows the
 // samples per ray of the model's last frame.
-constexpr float ONE_PIPE_SAMPLES_PER_RAY = 12.0f;
+constexpr float ONE_PIPE_SAMPLES_PER_RAY = VOLUME_SAMPLES_PER_RAY;
 static uint32_t render_pipes(const ngp_tuning& t, uint32_t n, uint32_t h_shard, float last_spr) {
 	uint32_t p = n >= (1u << 16) && !(last_spr > 0.0f && last_spr < ONE_PIPE_SAMPLES_PER_RAY) ? 2u : 1u;
 	if (t.render_pipelines) p = std::min<uint32_t>(t.render_pipelines, RenderScratch::MAX_PIPES);
@@ -1061,7 +1066,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// the CUs (194 VGPRs: 2 waves per SIMD leave it room), 32 with one pipeline (110 VGPRs, 4 waves per SIMD)
 	rs.mlp_tile = n_pipes > 1 ? 4u : 2u;
 
-	const uint32_t target = pass_sample_target(tu), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu), cap);
+	const uint32_t target = pass_sample_target(tu), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu, rs.last_samples_per_ray), cap);
 	const bool debug = (tu.debug & 1u) != 0;
 	// per-ray sample budgets: headroom factor (default 1.0: measured 1 % faster than 1.5), < 0 = off
 	k.budget = !(tu.render_budget_scale < 0.0f);
