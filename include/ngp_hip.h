@@ -234,7 +234,7 @@ typedef struct ngp_train_args {
 	 * a ray from image i carries row i (NerfCoordinate::set_with_optional_extra_dims); null = zeros.
 	 * extra_dims_gradient (optional, device fp32 [n_images][16]) += sum over the kept rays' compacted samples of
 	 * dL/d(code) (compute_extra_dims_gradient_train_nerf, src/testbed_nerf.cu:1271-1306; loss-scaled, as the
-	 * reference's gradient before its division by LOSS_SCALE at :2588) */
+	 * reference's gradient before its division by LOSS_SCALE at :2588).  Both 16-byte aligned (float4 rows). */
 	const float* extra_dims;
 	float* extra_dims_gradient;
 } ngp_train_args;
@@ -319,7 +319,7 @@ typedef struct ngp_render_args {
 	int32_t glow_mode;
 	float glow_y_cutoff;
 	/* n_extra_dims > 0: the latent code every rendered sample carries (Nerf::get_rendering_extra_dims,
-	 * src/testbed_nerf.cu:3206-3228): device fp32 [16], zero past n_extra_dims; null = zeros */
+	 * src/testbed_nerf.cu:3206-3228): device fp32 [16], zero past n_extra_dims; null = zeros; 16-byte aligned */
 	const float* extra_dims;
 } ngp_render_args;
 

@@ -497,6 +497,9 @@ ngp_status ngp_train_step(ngp_model* m, const ngp_train_args* a, ngp_stream s) {
 		require(a->images && a->n_images > 0, "training requires at least one image");
 		require(a->n_rays > 0 && a->target_batch_size > 0 && a->max_samples > 0, "empty batch");
 		require(m->gs.bitfield.ptr != nullptr, "density grid not initialised");
+		// the latent-code rows are read and written as float4s (mlp.hip load_extra8, k_extra_gradient)
+		require(((uintptr_t)a->extra_dims % 16) == 0 && ((uintptr_t)a->extra_dims_gradient % 16) == 0,
+		        "extra_dims / extra_dims_gradient must be 16-byte aligned");
 		run_train_step(m, a, S(s));
 	});
 }
@@ -658,6 +661,7 @@ ngp_status ngp_render(ngp_model* m, const ngp_render_args* a, float* frame, floa
 	return guarded([&] {
 		require(m && a && frame && depth, "null argument");
 		require(a->width > 0 && a->height > 0, "empty render target");
+		require(((uintptr_t)a->extra_dims % 16) == 0, "extra_dims must be 16-byte aligned");
 		run_render(m, a, frame, depth, S(s));
 	});
 }
