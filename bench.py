@@ -59,7 +59,7 @@ def parse():
                    help="N=1: also time the procedural lego-shaped SURFACE scene (train + 1080p render) -> surface_scene")
     p.add_argument("--render-to-cpu", type=int, default=5,
                    help="N=1: 1080p renders timed through render() with the read-back to host memory -> render_to_cpu")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r03_pmc_traffic.json"),
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
 
