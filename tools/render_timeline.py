@@ -38,6 +38,7 @@ for fi in range(max(0, len(starts) - nf - 1), len(starts) - 1):
     alone = collections.Counter()
     total = collections.Counter()
     running = collections.Counter()
+    pairs = collections.Counter()  # time with exactly this multiset of classes in flight (two kernels)
     prev = t0
     for t, d, n in ev:
         k = sum(running.values())
@@ -45,6 +46,8 @@ for fi in range(max(0, len(starts) - nf - 1), len(starts) - 1):
         if k == 1:
             (only,) = [x for x, c in running.items() if c]
             alone[only] += t - prev
+        elif k == 2:
+            pairs[" + ".join(sorted(x for x, c in running.items() for _ in range(c)))] += t - prev
         prev = t
         running[cls(n)] += d
     for s, e, n in seg:
@@ -53,6 +56,8 @@ for fi in range(max(0, len(starts) - nf - 1), len(starts) - 1):
     out.append(f"frame {fi}: {span / 1e3:.1f} us; in flight 0: {conc[0] / 1e3:.1f}  1: {conc[1] / 1e3:.1f}  2: {conc[2] / 1e3:.1f}  3+: {conc[3] / 1e3:.1f} us")
     for k, v in total.most_common():
         out.append(f"    {k:20s} sum {v / 1e3:8.1f} us  alone {alone[k] / 1e3:8.1f} us")
+    for k, v in pairs.most_common(8):
+        out.append(f"    pair {k:40s} {v / 1e3:8.1f} us")
 txt = "\n".join(out)
 print(txt)
 if len(sys.argv) > 3:
