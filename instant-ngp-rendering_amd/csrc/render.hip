@@ -64,6 +64,7 @@ struct RenderK {
 	int hard_edges;
 	float aperture, focus_z;  // depth of field (uv_to_ray, common_device.cuh:450-456)
 	const float* normals;     // Normals mode: d(raw density)/d(warped position) per sample slot of the pass, [slot][3]
+	float* sdt;               // optional [slot] warped dt, written by k_generate beside the row, read by k_composite (volumes)
 	int mark_unfilled;        // unfilled slots get SH row NO_SH_ROW (the render MLP skips tiles of them)
 	int exit_cap;             // a ray's per-pass budget is capped by the lattice points left to its exit
 	int glow_mode;            // Nerf::glow_mode (composite_kernel_nerf's glow; 0 = off)
@@ -559,6 +560,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 				const float dt = step_from(k.st, pn + 1.0f) - t;
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 				out_rows[j + rank] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
+				if (k.sdt) k.sdt[(size_t)base + j + rank] = warp_dt(dt);
 				sray[(size_t)base + j + rank] = row;
 			}
 		}
@@ -685,7 +687,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		bool done = false;
 		uint32_t used = actual;
 		float alpha_last = p.alpha_last;
-		// only each sample's dt is read in the loop (4 B instead of the 16-B row); the position of
+		// only each sample's dt is read in the loop (4 B: the dt array for volumes, else the row's w); the position of
 		// the max-weight sample -- the depth -- is read once after it
 		size_t s_max = ~(size_t)0;
 		for (uint32_t j0 = 0; j0 < actual && !done; j0 += COMPOSITE_AHEAD) {
@@ -696,7 +698,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
-					wdt[u] = reinterpret_cast<const float*>(posdt)[4 * s + 3];
+					wdt[u] = k.sdt ? k.sdt[s] : reinterpret_cast<const float*>(posdt)[4 * s + 3];
 				}
 			}
 #pragma unroll
@@ -1107,7 +1109,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 			ps.depth[b].reserve(pr.n);
 		}
 		// [0, 4 max): position + warped dt rows, [4 max, 5 max): the samples' SH rows (pixel indices)
-		ps.coords.reserve(5 * pr.max_samples);
+		ps.coords.reserve(6 * pr.max_samples);  // rows [4 max] | SH rows [max] | dt [max]
 		ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
 		ps.counters.reserve(16);
@@ -1125,6 +1127,11 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		}
 		pr.posdt = reinterpret_cast<float4*>(ps.coords.ptr);  // the encoder reads 16-B position rows once per level
 		pr.sray = reinterpret_cast<uint32_t*>(ps.coords.ptr + 4 * pr.max_samples);
+		// volumes (the last frame >= VOLUME_SAMPLES_PER_RAY samples per ray): each slot's warped dt also goes to its
+		// own array, so k_composite fetches 4 B per sample instead of sharing the 16-B row's line -- 13.33 vs
+		// 13.66 ms per fire frame; a surface scene's few samples per ray do not repay the extra store (2.12 vs
+		// 2.07 ms), profiles/r04_dt_array_ab.txt
+		pr.k.sdt = rs.last_samples_per_ray >= VOLUME_SAMPLES_PER_RAY ? ps.coords.ptr + 5 * pr.max_samples : nullptr;
 		pr.shrows = rs.shrows.ptr;
 		pr.base_tag = ps.pass_tag;
 		pr.n_alive_ub = pr.n;
