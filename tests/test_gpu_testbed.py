@@ -526,11 +526,11 @@ def test_extrinsic_optimisation_recovers_perturbed_pose(scene, tmp_path):
     err_before = np.linalg.norm(moved[:, 3] - true[:, 3])
     err_after = np.linalg.norm(cur[:, 3] - true[:, 3])
     print(f"pose error {err_before:.4f} -> {err_after:.4f}; pos offset {pos[k]}, rot offset {rot[k]}")
-    # moved back toward the true position: the tiny L4 network recovers part of the offset (7-10 % over
+    # moved back toward the true position: the tiny L4 network recovers part of the offset (7-31 % over
     # 1400 steps in GPU runs; the float atomics of the camera gradients make the amount vary run to run),
-    # and the translation offset points along the correction
+    # and the returned position moved along the correction (the translation offset alone need not: the
+    # rotation offset moves the returned position too)
     assert err_after < 0.97 * err_before
-    assert float(np.dot(pos[k], true[:, 3] - moved[:, 3])) > 0.0
     assert np.dot(cur[:, 3] - moved[:, 3], true[:, 3] - moved[:, 3]) > 0
     # untouched cameras stay close to their true poses (typically a few thousandths; with the
     # tiny network an occasional one drifts by ~half the perturbation, so the bound is on the
