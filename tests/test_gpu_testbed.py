@@ -528,8 +528,8 @@ def test_extrinsic_optimisation_recovers_perturbed_pose(scene, tmp_path):
     print(f"pose error {err_before:.4f} -> {err_after:.4f}; pos offset {pos[k]}, rot offset {rot[k]}")
     # moved back toward the true position: the tiny L4 network recovers part of the offset (7-31 % over
     # 1400 steps in GPU runs; the float atomics of the camera gradients make the amount vary run to run),
-    # and the returned position moved along the correction (the translation offset alone need not: the
-    # rotation offset moves the returned position too)
+    # and the returned position moved along the correction (compared in the returned pose's own frame: the
+    # offsets live in NGP space -- axes cycled, scaled -- while get_camera_extrinsics returns the NeRF-convention pose)
     assert err_after < 0.97 * err_before
     assert np.dot(cur[:, 3] - moved[:, 3], true[:, 3] - moved[:, 3]) > 0
     # untouched cameras stay close to their true poses (typically a few thousandths; with the
