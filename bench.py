@@ -3,9 +3,10 @@ nerf_synthetic/lego-shaped scene (BASELINE.json configs[1]: L=16 F=2 T=2^19,
 density 1x64 + rgb 2x64 MLPs) through the pyngp Testbed on MI355X.
 
 One "step" = Testbed.train(2^18) (density-grid update at the reference cadence,
-sampler, fused MLP fwd/bwd, hash-grid scatter, Adam) + one 1920x1080 spp=1
-render kept in HBM.  value = (training rays + rendered rays, all ranks) / max
-over ranks of the timed wall time.  N>1: one process per GPU (torchrun), each
+sampler, fused MLP fwd/bwd, hash-grid scatter, Adam) + one Testbed.render(1920,
+1080, spp=1) -- the float frame read back to host memory, as BASELINE.md counts
+inference.  value = (training rays + rendered rays, all ranks) / max over ranks
+of the timed wall time.  N>1: one process per GPU (torchrun), each
 rank trains on its own rays with the gradients all-reduced over RCCL every step
 and renders its own 1080p view (weak scaling).
 
@@ -57,8 +58,8 @@ def parse():
     p.add_argument("--cpu-rays", type=int, default=512, help="training rays in the CPU oracle sample")
     p.add_argument("--surface-scene", type=int, default=1,
                    help="N=1: also time the procedural lego-shaped SURFACE scene (train + 1080p render) -> surface_scene")
-    p.add_argument("--render-to-cpu", type=int, default=5,
-                   help="N=1: 1080p renders timed through render() with the read-back to host memory -> render_to_cpu")
+    p.add_argument("--render-in-hbm", type=int, default=5,
+                   help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
@@ -234,7 +235,8 @@ def surface_scene(args, ngp):
         tb.train(args.batch)
         t1 = time.perf_counter()
         tb.set_camera_to_training_view(view)
-        tb.render_to_device(W, H, 1, True)
+        img = tb.render(W, H, 1, True)  # to host memory, as the headline step
+        del img
         return tb.last_train_stats()["n_rays"], t1 - t0, time.perf_counter() - t1
 
     for _ in range(args.warmup):
@@ -252,7 +254,7 @@ def surface_scene(args, ngp):
             "train_ms_per_step": round(1e3 * train_s / args.steps, 3), "render_ms_per_frame": round(1e3 * render_s / args.steps, 3),
             "render_Mrays_s": round(W * H * args.steps / render_s / 1e6, 3),
             "workload": f"synthetic lego-shaped surface scene ({args.views} views {args.train_res}x{args.train_res}), same network, "
-                        f"{args.pretrain} pretrain steps, then train(2^18) + {W}x{H} spp1 render per step"}
+                        f"{args.pretrain} pretrain steps, then train(2^18) + render({W}, {H}, spp 1) to host memory per step"}
 
 
 def launch_ranks(args):
@@ -329,7 +331,10 @@ def main():
         t1 = time.perf_counter()
         rays = tb.last_train_stats()["n_rays"]
         tb.set_camera_to_training_view(view)
-        tb.render_to_device(W, H, 1, True)  # synchronised as well
+        # render() as BASELINE.md:30-31 counts inference: the float frame read back to host memory (render_to_cpu,
+        # src/python_api.cu:124-202; here into pooled page-locked numpy arrays)
+        img = tb.render(W, H, 1, True)
+        del img
         t2 = time.perf_counter()
         split["train_s"] += t1 - t0
         split["render_s"] += t2 - t1
@@ -449,29 +454,28 @@ def main():
         roofline["per_frame"] = {"bytes": round(per_frame), "frame_ms": round(1e3 * frame_s, 3),
                                  "GB/s": round(per_frame / frame_s / 1e9, 1),
                                  "frac": round(per_frame / frame_s / 1e9 / HBM_PEAK_GBS, 4),
-                                 "note": "algorithmic encode bytes of one 1080p frame / its render() wall time in HBM"}
+                                 "note": "algorithmic encode bytes of one 1080p frame / its render() wall time (host copy included)"}
 
-    # render() as BASELINE.md:30 counts inference: the wall time of render(1920, 1080, spp) including the
-    # read-back of the float frame to host memory (render_to_cpu, src/python_api.cu:124-202) -- here into
-    # pooled page-locked numpy arrays; reported beside value, which keeps the frame in HBM
-    render_to_cpu = None
-    if world == 1 and args.render_to_cpu > 0:
+    # the same view through render() (the timed step's call) and render_to_device() (the frame stays in HBM):
+    # the read-back's share of a frame, reported beside value
+    render_in_hbm = None
+    if world == 1 and args.render_in_hbm > 0:
         tb.set_camera_to_training_view(view)
         tb.render(W, H, 1, True)
         t0 = time.perf_counter()
-        for _ in range(args.render_to_cpu):
+        for _ in range(args.render_in_hbm):
             img = tb.render(W, H, 1, True)
             del img
-        tr = (time.perf_counter() - t0) / args.render_to_cpu
+        tr = (time.perf_counter() - t0) / args.render_in_hbm
         t0 = time.perf_counter()
-        for _ in range(args.render_to_cpu):
+        for _ in range(args.render_in_hbm):
             tb.render_to_device(W, H, 1, True)
-        td = (time.perf_counter() - t0) / args.render_to_cpu
-        render_to_cpu = {"ms_per_frame": round(1e3 * tr, 3), "Mrays_s": round(W * H / tr / 1e6, 3),
-                         "ms_per_frame_in_hbm": round(1e3 * td, 3), "readback_ms": round(1e3 * (tr - td), 3),
+        td = (time.perf_counter() - t0) / args.render_in_hbm
+        render_in_hbm = {"ms_per_frame": round(1e3 * td, 3), "Mrays_s": round(W * H / td / 1e6, 3),
+                         "ms_per_frame_render": round(1e3 * tr, 3), "readback_ms": round(1e3 * (tr - td), 3),
                          "readback_GB_s": round(W * H * 16 / max(tr - td, 1e-9) / 1e9, 1),
-                         "note": f"{args.render_to_cpu} renders of the bench view through render() (numpy float32 "
-                                 "[H,W,4] on pooled pinned host memory) vs render_to_device()"}
+                         "note": f"{args.render_in_hbm} renders of the bench view through render_to_device() (frame kept in "
+                                 "HBM) vs render() (numpy float32 [H,W,4] on pooled pinned host memory, the timed step's call)"}
 
     cpu = parity = None
     if rank == 0 and world == 1 and args.cpu_baseline:
@@ -504,7 +508,7 @@ def main():
                     + (" (bit-reproducible hash-grid gradients: the same trained scene every run; timed steps on the "
                        "default fp16-atomic path)" if args.deterministic_pretrain else ""),
             "config": {"workload": "lego L16F2T19 MLP 64 (1x density + 2x rgb hidden): Testbed.train(2^18) "
-                                   f"+ {W}x{H} spp1 render per step", "batch": args.batch, "config_file": args.config,
+                                   f"+ Testbed.render({W}, {H}, spp 1) to host memory per step", "batch": args.batch, "config_file": args.config,
                        "parallelism": f"dp{world} (RCCL grad all-reduce) + per-rank 1080p view"},
             "roofline": roofline,
             "cpu_baseline": cpu,
@@ -515,7 +519,7 @@ def main():
                       "render_ms_per_frame": round(1e3 * split["render_s"] / args.steps, 3),
                       "note": "rank 0; per-part wall time inside the timed region (SURVEY 8(d) counts train and inference separately)"},
             "kernels_calibration": kernels,
-            "render_to_cpu": render_to_cpu,
+            "render_in_hbm": render_in_hbm,
             "surface_scene": surface,
             "config_c": config_c,
         }

@@ -271,6 +271,19 @@ typedef struct ngp_grid_args {
 	uint32_t rank, world_size;       /* data-parallel: evaluate a 1/world_size slice, caller all-reduces (max) tmp */
 } ngp_grid_args;
 
+/* A uniform lattice over a box, evaluated by the density network (Testbed::get_density_on_grid,
+ * src/testbed_nerf.cu:3026-3075, which compute_and_save_png_slices writes out, src/testbed.cu:534-559). */
+typedef struct ngp_grid_query {
+	uint32_t res[3];                 /* lattice points per axis (x fastest in the output) */
+	float box_min[3], box_max[3];    /* the lattice's box (m_render_aabb by default) */
+	float box_to_local[9];           /* row-major; lattice point p is placed at transpose(M) * p (all-zero = identity) */
+	float aabb_min[3], aabb_max[3];  /* m_aabb: the network input warp and the density-grid lookup */
+	uint32_t max_cascade;
+	int32_t mask_with_grid;          /* 1: -10000 where the density grid at mip_from_pos is below
+	                                    NERF_MIN_OPTICAL_THICKNESS (grid_samples_half_to_float, :234-250) */
+	int32_t use_inference_params;    /* 1: the EMA parameters, as NerfNetwork::density does */
+} ngp_grid_query;
+
 typedef struct ngp_render_args {
 	uint32_t width, height;
 	uint32_t sample_index;   /* spp index of this frame */
@@ -463,6 +476,10 @@ ngp_status ngp_density_grid_bitfield(ngp_model* model, uint32_t max_cascade, ngp
 /* grid: [n_cascades][128^3] f32 (Morton order); bitfield: [8][128^3/8] u8; tmp: evaluation buffer;
  * mean: 1 f32 (device). */
 ngp_status ngp_density_grid_buffers(ngp_model* model, float** grid, uint8_t** bitfield, float** tmp, float** mean);
+/* Testbed::get_density_on_grid (src/testbed_nerf.cu:3026-3075): out[x + y*res.x + z*res.x*res.y] (device, f32) =
+ * the raw density-network output (the fp16 value, widened) at lattice point (x, y, z) / (res - 1) of the box
+ * (generate_grid_samples_nerf_uniform, :147-160), evaluated in batches of 2^20 points. */
+ngp_status ngp_density_on_grid(ngp_model* model, const ngp_grid_query* query, float* out, ngp_stream stream);
 
 /* --- error map ------------------------------------------------------------------------ */
 /* construct_cdf_2d + construct_cdf_1d (src/testbed_nerf.cu:1493-1546): per image, the row-wise

@@ -297,6 +297,84 @@ void run_grid_bitfield(ngp_model* m, uint32_t max_cascade, hipStream_t s) {
 	NGP_HIP_CHECK(hipGetLastError());
 }
 
+// generate_grid_samples_nerf_uniform (src/testbed_nerf.cu:147-160) for lattice points [first, first + n): point
+// (x, y, z) / (res - 1) of the box, placed by transpose(box_to_local), warped into the training aabb.
+struct LatticeBox {
+	uint32_t rx, ry, rz;
+	aabb3 box, train;
+	float R[9];  // row-major box_to_local
+	int rot;
+};
+
+__global__ void __launch_bounds__(256) k_lattice_points(uint32_t first, uint32_t n, LatticeBox L, float4* __restrict__ out) {
+	const uint32_t j = blockIdx.x * 256u + threadIdx.x;
+	if (j >= n) return;
+	const uint32_t i = first + j;
+	const uint32_t x = i % L.rx, y = (i / L.rx) % L.ry, z = i / (L.rx * L.ry);
+	v3 p = mk3((float)x, (float)y, (float)z) / mk3((float)(L.rx - 1), (float)(L.ry - 1), (float)(L.rz - 1));
+	p = p * (L.box.max - L.box.min) + L.box.min;
+	if (L.rot) {
+		// transpose(M) * p: component c is column c of M (row-major M[r][c] = R[3r + c]) dotted with p
+		const float* R = L.R;
+		p = mk3(R[0] * p.x + R[3] * p.y + R[6] * p.z, R[1] * p.x + R[4] * p.y + R[7] * p.z,
+		        R[2] * p.x + R[5] * p.y + R[8] * p.z);
+	}
+	const v3 w = aabb_relative(L.train, p);
+	out[j] = make_float4(w.x, w.y, w.z, warp_dt(MIN_CONE_STEPSIZE));
+}
+
+// grid_samples_half_to_float (:234-250): the raw (not activated) density output, -10000 where the cascaded
+// density grid at the point's mip_from_pos cell is below NERF_MIN_OPTICAL_THICKNESS (outside the grid: 0).
+__global__ void __launch_bounds__(256) k_grid_density_out(uint32_t n, const float4* __restrict__ rows,
+                                                          const __half* __restrict__ mlp, aabb3 train,
+                                                          const float* __restrict__ grid, uint32_t max_cascade,
+                                                          float* __restrict__ dst) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	float v = __half2float(mlp[i]);
+	if (grid) {
+		const float4 r = rows[i];
+		const v3 pos = unwarp_position(mk3(r.x, r.y, r.z), train);
+		const uint32_t mip = mip_from_pos(pos, max_cascade);
+		const uint32_t idx = cascaded_grid_idx_at(pos, mip);
+		const float g = idx == 0xFFFFFFFFu ? 0.0f : grid[idx + (size_t)mip * NERF_GRID_N_CELLS];
+		if (g < NERF_MIN_OPTICAL_THICKNESS) v = -10000.0f;
+	}
+	dst[i] = v;
+}
+
+void run_density_on_grid(ngp_model* m, const ngp_grid_query* q, float* out, hipStream_t s) {
+	GridState& g = m->gs;
+	LatticeBox L;
+	L.rx = q->res[0];
+	L.ry = q->res[1];
+	L.rz = q->res[2];
+	L.box.min = mk3(q->box_min[0], q->box_min[1], q->box_min[2]);
+	L.box.max = mk3(q->box_max[0], q->box_max[1], q->box_max[2]);
+	L.train.min = mk3(q->aabb_min[0], q->aabb_min[1], q->aabb_min[2]);
+	L.train.max = mk3(q->aabb_max[0], q->aabb_max[1], q->aabb_max[2]);
+	const RenderBox rb = make_render_box(L.box, q->box_to_local);
+	for (int k = 0; k < 9; ++k) L.R[k] = rb.R[k];
+	L.rot = rb.rot;
+	const uint64_t n_total = (uint64_t)L.rx * L.ry * L.rz;
+	const uint32_t batch = (uint32_t)std::min<uint64_t>(n_total, 1u << 20);  // the reference's 1M-point batches
+	g.positions.reserve(4 * (size_t)batch);
+	g.enc.reserve((size_t)m->lt.n_levels * batch * m->lt.F);
+	g.out.reserve(batch);
+	const __half* table = (q->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
+	const __half* frags = q->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
+	const float* grid = q->mask_with_grid ? g.grid.ptr : nullptr;
+	for (uint64_t first = 0; first < n_total; first += batch) {
+		const uint32_t cnt = (uint32_t)std::min<uint64_t>(n_total - first, batch);
+		float4* rows = reinterpret_cast<float4*>(g.positions.ptr);
+		k_lattice_points<<<div_up(cnt, 256), 256, 0, s>>>((uint32_t)first, cnt, L, rows);
+		launch_hashgrid_fwd(m->lt, g.positions.ptr, 4, cnt, table, g.enc.ptr, internal_layout(m, cnt), s);
+		launch_mlp_density(m, frags, g.enc.ptr, internal_layout(m, cnt), cnt, g.out.ptr, s);
+		k_grid_density_out<<<div_up(cnt, 256), 256, 0, s>>>(cnt, rows, g.out.ptr, L.train, grid, q->max_cascade, out + first);
+		NGP_HIP_CHECK(hipGetLastError());
+	}
+}
+
 void run_grid_finish(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 	GridState& g = m->gs;
 	const uint32_t n_elements = NERF_GRID_N_CELLS * (a->max_cascade + 1);

@@ -19,6 +19,7 @@
 namespace ngp {
 void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s);
 void run_grid_finish(ngp_model* m, const ngp_grid_args* a, hipStream_t s);
+void run_density_on_grid(ngp_model* m, const ngp_grid_query* q, float* out, hipStream_t s);
 void run_grid_bitfield(ngp_model* m, uint32_t max_cascade, hipStream_t s);
 void grid_reserve(ngp_model* m, uint32_t n_cascades, uint32_t n_samples);
 void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* depth_buffer, hipStream_t s);
@@ -646,6 +647,21 @@ ngp_status ngp_density_grid_buffers(ngp_model* m, float** grid, uint8_t** bitfie
 		}
 		if (tmp) *tmp = m->gs.tmp.ptr;
 		if (mean) *mean = m->gs.mean.ptr;
+	});
+}
+
+ngp_status ngp_density_on_grid(ngp_model* m, const ngp_grid_query* q, float* out, ngp_stream s) {
+	return guarded([&] {
+		require(m && q, "null argument");
+		const uint64_t n = (uint64_t)q->res[0] * q->res[1] * q->res[2];
+		require(n == 0 || out, "null output");
+		require(n < (1ull << 32), "lattice too large (at most 2^32 points)");
+		require(q->max_cascade < NERF_CASCADES, "max_cascade must be < 8");
+		if (q->mask_with_grid)
+			require(m->gs.grid.ptr != nullptr && m->gs.n_cascades > q->max_cascade,
+			        "density grid not initialised for max_cascade (mask_with_grid)");
+		if (n == 0) return;
+		run_density_on_grid(m, q, out, S(s));
 	});
 }
 

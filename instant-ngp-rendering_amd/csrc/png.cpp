@@ -160,4 +160,72 @@ bool decode_png_file(const std::string& path, std::vector<uint8_t>& rgba, int& w
 	return decode_png_memory(buf.data(), buf.size(), rgba, width, height, err);
 }
 
+// PNG encoder (write_stbi's png branch, src/common_host.cu:234-248): 8-bit gray / GA / RGB / RGBA, filter 0 on every
+// row, one zlib stream in one IDAT chunk.
+static void put_be32(std::vector<uint8_t>& o, uint32_t v) {
+	o.push_back((uint8_t)(v >> 24));
+	o.push_back((uint8_t)(v >> 16));
+	o.push_back((uint8_t)(v >> 8));
+	o.push_back((uint8_t)v);
+}
+
+static void put_chunk(std::vector<uint8_t>& o, const char* type, const uint8_t* data, size_t n) {
+	put_be32(o, (uint32_t)n);
+	const size_t start = o.size();
+	o.insert(o.end(), type, type + 4);
+	if (n) o.insert(o.end(), data, data + n);
+	put_be32(o, (uint32_t)crc32(0L, o.data() + start, (uInt)(n + 4)));
+}
+
+bool encode_png_memory(const uint8_t* pixels, int width, int height, int comp, std::vector<uint8_t>& out, std::string& err) {
+	static const uint8_t ctypes[5] = {0, 0, 4, 2, 6};
+	if (width <= 0 || height <= 0 || comp < 1 || comp > 4) {
+		err = "encode_png: invalid image shape";
+		return false;
+	}
+	const size_t row = (size_t)width * comp;
+	std::vector<uint8_t> raw((row + 1) * (size_t)height);
+	for (int y = 0; y < height; ++y) {
+		raw[(row + 1) * y] = 0;
+		std::memcpy(&raw[(row + 1) * y + 1], pixels + row * y, row);
+	}
+	uLongf zn = compressBound((uLong)raw.size());
+	std::vector<uint8_t> z(zn);
+	if (compress2(z.data(), &zn, raw.data(), (uLong)raw.size(), 6) != Z_OK) {
+		err = "encode_png: zlib deflate failed";
+		return false;
+	}
+	out.clear();
+	static const uint8_t sig[8] = {0x89, 'P', 'N', 'G', '\r', '\n', 0x1a, '\n'};
+	out.insert(out.end(), sig, sig + 8);
+	std::vector<uint8_t> ihdr;
+	put_be32(ihdr, (uint32_t)width);
+	put_be32(ihdr, (uint32_t)height);
+	ihdr.push_back(8);
+	ihdr.push_back(ctypes[comp]);
+	ihdr.push_back(0);
+	ihdr.push_back(0);
+	ihdr.push_back(0);
+	put_chunk(out, "IHDR", ihdr.data(), ihdr.size());
+	put_chunk(out, "IDAT", z.data(), zn);
+	put_chunk(out, "IEND", nullptr, 0);
+	return true;
+}
+
+bool encode_png_file(const std::string& path, const uint8_t* pixels, int width, int height, int comp, std::string& err) {
+	std::vector<uint8_t> buf;
+	if (!encode_png_memory(pixels, width, height, comp, buf, err)) return false;
+	std::ofstream f(path, std::ios::binary);
+	if (!f) {
+		err = "encode_png: cannot open " + path;
+		return false;
+	}
+	f.write(reinterpret_cast<const char*>(buf.data()), (std::streamsize)buf.size());
+	if (!f) {
+		err = "encode_png: write failed for " + path;
+		return false;
+	}
+	return true;
+}
+
 }  // namespace ngp

@@ -135,8 +135,10 @@ struct NerfView {
 	Testbed* tb;
 };
 
+// bounding_box.cuh:45-263: default-constructed empty (min = +inf, max = -inf)
 struct BoundingBox {
-	vec3 min, max;
+	vec3 min = {INFINITY, INFINITY, INFINITY}, max = {-INFINITY, -INFINITY, -INFINITY};
+	bool is_empty() const { return max[0] < min[0] || max[1] < min[1] || max[2] < min[2]; }
 };
 
 }  // namespace
@@ -210,6 +212,7 @@ PYBIND11_MODULE(pyngp, m) {
 			return vec3{0.5f * (b.min[0] + b.max[0]), 0.5f * (b.min[1] + b.max[1]), 0.5f * (b.min[2] + b.max[2])};
 		})
 		.def("diag", [](const BoundingBox& b) { return vec3{b.max[0] - b.min[0], b.max[1] - b.min[1], b.max[2] - b.min[2]}; })
+		.def("is_empty", &BoundingBox::is_empty)
 		.def("contains", [](const BoundingBox& b, vec3 p) {
 			for (int k = 0; k < 3; ++k)
 				if (p[k] < b.min[k] || p[k] > b.max[k]) return false;
@@ -662,6 +665,45 @@ PYBIND11_MODULE(pyngp, m) {
 			auto g = t.density_grid();
 			return py::array_t<float>(g.size(), g.data());
 		})
+		// compute_and_save_png_slices (src/python_api.cu:451-459): the density mosaic of NerfNetwork::density on a lattice
+		// over aabb (empty: the render aabb), written to filename + ".density_slices_{x}x{y}x{z}.png"; returns the lattice
+		.def("compute_and_save_png_slices",
+		     [](Testbed& t, const std::string& filename, int res, const BoundingBox& aabb, float thresh, float density_range,
+		        bool flip) {
+			     std::array<int, 3> r;
+			     {
+				     py::gil_scoped_release rel;
+				     r = t.compute_and_save_png_slices(filename, res, aabb.min, aabb.max, thresh, density_range, flip);
+			     }
+			     py::array_t<int> a(3);
+			     std::copy(r.begin(), r.end(), a.mutable_data());
+			     return a;
+		     },
+		     py::arg("filename"), py::arg("resolution") = 256, py::arg("aabb") = BoundingBox{},
+		     py::arg("thresh") = std::numeric_limits<float>::max(), py::arg("density_range") = 4.f,
+		     py::arg("flip_y_and_z_axes") = false,
+		     "Compute & save a PNG file representing the 3D density field from the current NeRF model.")
+		// get_density_on_grid (src/testbed_nerf.cu:3026-3075) as a [z][y][x] array (an MI355X-side accessor for tests)
+		.def("density_on_grid",
+		     [](Testbed& t, std::array<int, 3> res3d, const BoundingBox& aabb) {
+			     vec3 lo = aabb.min, hi = aabb.max;
+			     mat3 to_local = MAT3_IDENTITY;
+			     if (aabb.is_empty()) {
+				     lo = t.render_aabb_min;
+				     hi = t.render_aabb_max;
+				     to_local = t.render_aabb_to_local;
+			     }
+			     std::vector<float> d;
+			     {
+				     py::gil_scoped_release rel;
+				     d = t.density_on_grid(res3d, lo, hi, to_local);
+			     }
+			     py::array_t<float> a({(py::ssize_t)res3d[2], (py::ssize_t)res3d[1], (py::ssize_t)res3d[0]});
+			     std::memcpy(a.mutable_data(), d.data(), d.size() * sizeof(float));
+			     return a;
+		     },
+		     py::arg("resolution"), py::arg("aabb") = BoundingBox{})
+		.def_readwrite("mesh_thresh", &Testbed::mesh_thresh)
 		.def("density_grid_bitfield", [](const Testbed& t) {
 			auto b = t.density_grid_bitfield();
 			return py::array_t<uint8_t>(b.size(), b.data());

@@ -2064,6 +2064,129 @@ static Json vec_json(const float* v, int n) {
 	return a;
 }
 
+std::array<int, 3> marching_cubes_res(int res_1d, const vec3& box_min, const vec3& box_max) {
+	const vec3 d = {box_max[0] - box_min[0], box_max[1] - box_min[1], box_max[2] - box_min[2]};
+	const float scale = (float)res_1d / std::max(d[0], std::max(d[1], d[2]));
+	std::array<int, 3> r;
+	for (int k = 0; k < 3; ++k) {
+		const unsigned v = (unsigned)(int)(d[k] * scale + 0.5f);  // ivec3(vec3) truncates
+		r[k] = (int)((v + 15u) / 16u * 16u);                        // next_multiple(v, 16u)
+	}
+	return r;
+}
+
+std::vector<uint8_t> density_slices_mosaic(const std::vector<float>& density, std::array<int, 3> res3d, float thresh,
+                                           bool swap_y_z, float density_range, int* width, int* height,
+                                           uint32_t* zero_x_voxels, uint32_t* near_zero_lattice) {
+	const int RX = res3d[0], RY = res3d[1], RZ = res3d[2];
+	if ((size_t)RX * RY * RZ != density.size()) throw std::runtime_error("density_slices_mosaic: grid size mismatch");
+	const float density_scale = 128.f / density_range;
+	auto at = [&](int x, int y, int z) { return density[(size_t)x + (size_t)y * RX + (size_t)z * RX * RY]; };
+	// the log line's statistics (marching_cubes.cu:965-996): voxels whose 8 corners straddle thresh, and interior
+	// lattice points with a 6-neighbour on the other side
+	uint32_t nv = 0, nz = 0;
+	for (int z = 1; z < RZ - 1; ++z)
+		for (int y = 1; y < RY - 1; ++y)
+			for (int x = 1; x < RX - 1; ++x) {
+				int count = 0;
+				for (int k = 0; k < 8; ++k) count += at(x + (k & 1), y + ((k >> 1) & 1), z + (k >> 2)) < thresh;
+				if (count > 0 && count < 8) ++nv;
+				const bool s0 = at(x, y, z) < thresh;
+				bool c = (at(x + 1, y, z) < thresh) != s0;
+				c |= (at(x - 1, y, z) < thresh) != s0;
+				c |= (at(x, y + 1, z) < thresh) != s0;
+				c |= (at(x, y - 1, z) < thresh) != s0;
+				c |= (at(x, y, z + 1) < thresh) != s0;
+				c |= (at(x, y, z - 1) < thresh) != s0;
+				if (c) ++nz;
+			}
+	if (zero_x_voxels) *zero_x_voxels = nv;
+	if (near_zero_lattice) *near_zero_lattice = nz;
+	int rx = RX, ry = RY, rz = RZ;
+	if (swap_y_z) std::swap(ry, rz);
+	const uint32_t ndown = (uint32_t)std::sqrt((float)rz);
+	const uint32_t nacross = ((uint32_t)rz + ndown - 1) / ndown;
+	const uint32_t w = (uint32_t)rx * nacross, h = (uint32_t)ry * ndown;
+	std::vector<uint8_t> px((size_t)w * h);
+	uint8_t* dst = px.data();
+	for (uint32_t v = 0; v < h; ++v)
+		for (uint32_t u = 0; u < w; ++u) {
+			const int x = (int)(u % (uint32_t)rx), y = (int)(v % (uint32_t)ry);
+			const int z = (int)(u / (uint32_t)rx + (v / (uint32_t)ry) * nacross);
+			if (z < rz) {
+				// swapped: the grid's (x, y, z) is the image's (x, z, y), unflipped; otherwise y is flipped
+				const float d = swap_y_z ? density[(size_t)x + (size_t)z * rx + (size_t)y * rx * rz]
+				                         : at(x, ry - 1 - y, z);
+				*dst++ = (uint8_t)std::min(std::max((d - thresh) * density_scale + 128.5f, 0.f), 255.f);
+			} else {
+				*dst++ = 0;
+			}
+		}
+	*width = (int)w;
+	*height = (int)h;
+	return px;
+}
+
+std::vector<float> Testbed::density_on_grid(const std::array<int, 3>& res3d, const vec3& box_min, const vec3& box_max,
+                                            const mat3& box_to_local) const {
+	if (!m_model) throw std::runtime_error("density_on_grid: no network (load a dataset or a snapshot first)");
+	for (int k = 0; k < 3; ++k)
+		if (res3d[k] <= 0) throw std::runtime_error("density_on_grid: the resolution must be positive");
+	ngp_grid_query q{};
+	for (int k = 0; k < 3; ++k) {
+		q.res[k] = (uint32_t)res3d[k];
+		q.box_min[k] = box_min[k];
+		q.box_max[k] = box_max[k];
+		q.aabb_min[k] = aabb_min[k];
+		q.aabb_max[k] = aabb_max[k];
+	}
+	std::memcpy(q.box_to_local, box_to_local.data(), sizeof(q.box_to_local));
+	q.max_cascade = nerf.max_cascade;
+	q.mask_with_grid = mode == ETestbedMode::Nerf ? 1 : 0;
+	q.use_inference_params = 1;
+	const size_t n = (size_t)res3d[0] * res3d[1] * res3d[2];
+	std::vector<float> out(n);
+	float* dev = nullptr;
+	hk(hipMalloc(&dev, n * sizeof(float)), "density_on_grid alloc");
+	try {
+		ck(ngp_density_on_grid(m_model, &q, dev, m_stream));
+		sync();
+		hk(hipMemcpy(out.data(), dev, n * sizeof(float), hipMemcpyDeviceToHost), "density_on_grid d2h");
+	} catch (...) {
+		(void)hipFree(dev);
+		throw;
+	}
+	(void)hipFree(dev);
+	return out;
+}
+
+std::array<int, 3> Testbed::compute_and_save_png_slices(const std::string& filename, int res, vec3 box_min, vec3 box_max,
+                                                        float thresh, float density_range, bool flip_y_and_z_axes) {
+	mat3 to_local = MAT3_IDENTITY;
+	const bool empty = box_max[0] < box_min[0] || box_max[1] < box_min[1] || box_max[2] < box_min[2];
+	if (empty) {
+		box_min = render_aabb_min;
+		box_max = render_aabb_max;
+		to_local = render_aabb_to_local;
+	}
+	if (thresh == std::numeric_limits<float>::max()) thresh = mesh_thresh;
+	if (res <= 0) throw std::runtime_error("compute_and_save_png_slices: the resolution must be positive");
+	const std::array<int, 3> res3d = marching_cubes_res(res, box_min, box_max);
+	const std::vector<float> density = density_on_grid(res3d, box_min, box_max, to_local);
+	int w = 0, h = 0;
+	uint32_t nv = 0, nz = 0;
+	const std::vector<uint8_t> px =
+	    density_slices_mosaic(density, res3d, thresh, flip_y_and_z_axes, density_range, &w, &h, &nv, &nz);
+	const std::string path = filename + ".density_slices_" + std::to_string(res3d[0]) + "x" + std::to_string(res3d[1]) + "x" +
+	                         std::to_string(res3d[2]) + ".png";
+	std::string err;
+	if (!encode_png_file(path, px.data(), w, h, 1, err)) throw std::runtime_error(err);
+	const double N = (double)res3d[0] * res3d[1] * res3d[2];
+	std::fprintf(stderr, "Wrote density PNG to %s\n  #lattice points=%.0f #zero-x voxels=%u (%g%%) #lattice near zero-x=%u (%g%%)\n",
+	             path.c_str(), N, nv, nv * 100.0 / N, nz, nz * 100.0 / N);
+	return res3d;
+}
+
 void Testbed::save_snapshot(const std::string& path, bool include_optimizer_state, bool compress) {
 	if (!m_model) throw std::runtime_error("save_snapshot: no network");
 	sync();

@@ -303,6 +303,16 @@ public:
 	ngp_train_stats last_stats() const { return m_last_stats; }
 	std::vector<float> density_grid() const;
 	std::vector<uint8_t> density_grid_bitfield() const;
+	// get_density_on_grid (src/testbed_nerf.cu:3026-3075): the raw density output on a res3d lattice over the box
+	// (x fastest), -10000 where the density grid is below NERF_MIN_OPTICAL_THICKNESS
+	std::vector<float> density_on_grid(const std::array<int, 3>& res3d, const vec3& box_min, const vec3& box_max,
+	                                   const mat3& box_to_local) const;
+	// compute_and_save_png_slices (src/testbed.cu:534-559): an empty box (min > max) means the render aabb with its
+	// rotation; thresh = FLT_MAX means mesh_thresh.  Writes filename + ".density_slices_{x}x{y}x{z}.png" and
+	// returns the lattice resolution.
+	std::array<int, 3> compute_and_save_png_slices(const std::string& filename, int res, vec3 box_min, vec3 box_max,
+	                                               float thresh, float density_range, bool flip_y_and_z_axes);
+	float mesh_thresh = 2.5f;  // m_mesh.thresh (testbed.h:660)
 
 	// --- state (public like the reference's pybind-exposed members) ---
 	ETestbedMode mode = ETestbedMode::None;
@@ -436,6 +446,14 @@ private:
 };
 
 std::string natural_sort_key(const std::string& s);
+// get_marching_cubes_res (src/marching_cubes.cu:40-47): res_1d along the box's longest side, each axis rounded up to 16
+std::array<int, 3> marching_cubes_res(int res_1d, const vec3& box_min, const vec3& box_max);
+// save_density_grid_to_png's mosaic (src/marching_cubes.cu:957-1020): the res.z slices (res.y with swap_y_z) of a
+// [z][y][x] grid tiled sqrt(res.z) rows down, y flipped, byte = clamp((v - thresh) * 128 / density_range + 128.5);
+// returns the 8-bit gray image and its size; zero_x_voxels / near_zero_lattice get the log line's two counts
+std::vector<uint8_t> density_slices_mosaic(const std::vector<float>& density, std::array<int, 3> res3d, float thresh,
+                                           bool swap_y_z, float density_range, int* width, int* height,
+                                           uint32_t* zero_x_voxels = nullptr, uint32_t* near_zero_lattice = nullptr);
 // non-PNG images (JPG, ...): decoder(path, rgba8_out, width, height) -> success
 using ImageDecoder = std::function<bool(const std::string&, std::vector<uint8_t>&, int&, int&)>;
 NerfDataset load_nerf(const std::string& path, const ImageDecoder& image_decoder = nullptr);

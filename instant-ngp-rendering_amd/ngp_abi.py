@@ -91,6 +91,15 @@ class GridArgs(C.Structure):
     ]
 
 
+class GridQuery(C.Structure):
+    """ngp_grid_query: the lattice of get_density_on_grid (src/testbed_nerf.cu:3026-3075)."""
+    _fields_ = [
+        ("res", C.c_uint32 * 3), ("box_min", C.c_float * 3), ("box_max", C.c_float * 3), ("box_to_local", C.c_float * 9),
+        ("aabb_min", C.c_float * 3), ("aabb_max", C.c_float * 3), ("max_cascade", C.c_uint32),
+        ("mask_with_grid", C.c_int32), ("use_inference_params", C.c_int32),
+    ]
+
+
 class RenderArgs(C.Structure):
     _fields_ = [
         ("width", C.c_uint32), ("height", C.c_uint32), ("sample_index", C.c_uint32), ("camera", C.c_float * 12),
@@ -167,6 +176,7 @@ EXPORTS = {
     "ngp_density_grid_bitfield": (C.c_int, [C.c_void_p, C.c_uint32, C.c_void_p]),
     "ngp_density_grid_buffers": (C.c_int, [C.c_void_p, C.POINTER(C.c_void_p), C.POINTER(C.c_void_p),
                                            C.POINTER(C.c_void_p), C.POINTER(C.c_void_p)]),
+    "ngp_density_on_grid": (C.c_int, [C.c_void_p, C.POINTER(GridQuery), C.c_void_p, C.c_void_p]),
     "ngp_error_map_build_cdf": (C.c_int, [C.c_void_p, C.c_uint32, C.c_uint32, C.c_uint32, C.c_void_p, C.c_void_p,
                                           C.c_void_p, C.c_void_p]),
     "ngp_render": (C.c_int, [C.c_void_p, C.POINTER(RenderArgs), C.c_void_p, C.c_void_p, C.c_void_p]),

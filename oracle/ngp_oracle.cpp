@@ -2332,4 +2332,100 @@ void oref_accumulate_tonemap(const float* frame, float* accum, float* out, uint3
 	}
 }
 
+
+// Testbed::get_density_on_grid (src/testbed_nerf.cu:3026-3075): generate_grid_samples_nerf_uniform (:147-160) places
+// lattice point (x, y, z) / (res - 1) of the box, rotated by transpose(render_aabb_to_local) and warped into the
+// training aabb; NerfNetwork::density gives the raw output (fp16); grid_samples_half_to_float (:234-250) unwarps
+// the position and replaces the value by -10000 where the cascaded density grid at mip_from_pos is below 0.01
+// (a point outside the grid reads 0).  grid: [n_cascades][128^3] host floats, null = no masking.
+void oref_density_on_grid(void* m, const ngp_grid_query* q, const float* grid, float* out) {
+	const uint32_t rx = q->res[0], ry = q->res[1], rz = q->res[2];
+	const size_t n = (size_t)rx * ry * rz;
+	const Box box{v(q->box_min[0], q->box_min[1], q->box_min[2]), v(q->box_max[0], q->box_max[1], q->box_max[2])};
+	const Box train{v(q->aabb_min[0], q->aabb_min[1], q->aabb_min[2]), v(q->aabb_max[0], q->aabb_max[1], q->aabb_max[2])};
+	const RBox rb = rbox_of(box, q->box_to_local);
+	const V3 den = v((float)(rx - 1), (float)(ry - 1), (float)(rz - 1));
+	std::vector<float> rows(4 * n);
+	for (size_t i = 0; i < n; ++i) {
+		const uint32_t x = (uint32_t)(i % rx), y = (uint32_t)((i / rx) % ry), z = (uint32_t)(i / ((size_t)rx * ry));
+		V3 p = v((float)x, (float)y, (float)z) / den;
+		p = V3{p.x * (box.mx.x - box.mn.x), p.y * (box.mx.y - box.mn.y), p.z * (box.mx.z - box.mn.z)} + box.mn;
+		if (rb.rot) {
+			const float* R = rb.R;  // transpose(R) * p
+			p = V3{R[0] * p.x + R[3] * p.y + R[6] * p.z, R[1] * p.x + R[4] * p.y + R[7] * p.z, R[2] * p.x + R[5] * p.y + R[8] * p.z};
+		}
+		const V3 w = train.rel(p);
+		rows[4 * i + 0] = w.x;
+		rows[4 * i + 1] = w.y;
+		rows[4 * i + 2] = w.z;
+		rows[4 * i + 3] = warp_dt(MIN_STEP);
+	}
+	const size_t chunk = 4096;
+#pragma omp parallel for schedule(dynamic)
+	for (size_t c = 0; c < n; c += chunk) {
+		const uint32_t cnt = (uint32_t)std::min(chunk, n - c);
+		std::vector<float> raw(cnt);
+		oref_density(m, rows.data() + 4 * c, 4, cnt, raw.data(), q->use_inference_params);
+		for (uint32_t j = 0; j < cnt; ++j) {
+			const size_t i = c + j;
+			float val = h2f(f2h(raw[j]));
+			if (grid && q->mask_with_grid) {
+				const V3 w = v(rows[4 * i], rows[4 * i + 1], rows[4 * i + 2]);
+				const V3 pos = V3{w.x * (train.mx.x - train.mn.x), w.y * (train.mx.y - train.mn.y), w.z * (train.mx.z - train.mn.z)} + train.mn;
+				const uint32_t mip = mip_pos(pos, q->max_cascade);
+				const uint32_t gi = grid_idx(pos, mip);
+				const float gd = gi == 0xFFFFFFFFu ? 0.0f : grid[gi + (size_t)CELLS * mip];
+				if (gd < 0.01f) val = -10000.0f;
+			}
+			out[i] = val;
+		}
+	}
+}
+
+// save_density_grid_to_png (src/marching_cubes.cu:957-1020): density [z][y][x] (res3d), mosaic of ceil(rz / ndown) x
+// ndown tiles with ndown = floor(sqrt(rz)) (rz, ry swapped when swap_y_z); tile z at column z % nacross, row
+// z / nacross; unswapped rows are flipped (y = ry - 1 - v); byte = (uint8)clamp((d - thresh) * 128 / range + 128.5, 0, 255);
+// unused tiles are 0.  *w, *h: the mosaic size; out: w * h bytes (null: size only).  The log line's counts
+// (:965-996) go to counts[0] (voxels with 1..7 of 8 corners below thresh) and counts[1] (interior points with a
+// 6-neighbour on the other side of thresh).
+void oref_density_slices_mosaic(const float* d, const int* res3d, float thresh, int swap_y_z, float range, uint8_t* out,
+                                int* w, int* h, uint32_t* counts) {
+	const int X = res3d[0], Y = res3d[1], Z = res3d[2];
+	auto below = [&](int x, int y, int z) { return d[((size_t)z * Y + y) * X + x] < thresh; };
+	if (counts) {
+		counts[0] = counts[1] = 0;
+		for (int z = 1; z + 1 < Z; ++z)
+			for (int y = 1; y + 1 < Y; ++y)
+				for (int x = 1; x + 1 < X; ++x) {
+					int c = 0;
+					for (int dz = 0; dz < 2; ++dz)
+						for (int dy = 0; dy < 2; ++dy)
+							for (int dx = 0; dx < 2; ++dx) c += below(x + dx, y + dy, z + dz);
+					counts[0] += (c > 0 && c < 8);
+					const bool me = below(x, y, z);
+					const bool diff = below(x + 1, y, z) != me || below(x - 1, y, z) != me || below(x, y + 1, z) != me ||
+					                  below(x, y - 1, z) != me || below(x, y, z + 1) != me || below(x, y, z - 1) != me;
+					counts[1] += diff;
+				}
+	}
+	const int ty = swap_y_z ? Z : Y, tz = swap_y_z ? Y : Z;  // tile height and tile count
+	const int ndown = (int)std::sqrt((float)tz), nacross = (tz + ndown - 1) / ndown;
+	*w = X * nacross;
+	*h = ty * ndown;
+	if (!out) return;
+	const float scale = 128.0f / range;
+	std::memset(out, 0, (size_t)(*w) * (*h));
+	for (int t = 0; t < tz; ++t) {
+		const int u0 = (t % nacross) * X, v0 = (t / nacross) * ty;
+		for (int r = 0; r < ty; ++r)
+			for (int x = 0; x < X; ++x) {
+				// swapped: image row r of tile t is grid (y = t, z = r); otherwise grid (y = ty - 1 - r, z = t)
+				const float val = swap_y_z ? d[((size_t)r * Y + t) * X + x] : d[((size_t)t * Y + (ty - 1 - r)) * X + x];
+				float b = (val - thresh) * scale + 128.5f;
+				b = b < 0.0f ? 0.0f : (b > 255.0f ? 255.0f : b);
+				out[(size_t)(v0 + r) * (*w) + u0 + x] = (uint8_t)b;
+			}
+	}
+}
+
 }  // extern "C"

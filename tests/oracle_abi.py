@@ -56,6 +56,9 @@ _PROTOS = {
     "oref_train_scratch": (C.c_size_t, [C.c_void_p, C.c_int, C.c_void_p]),
     "oref_density_grid_update": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
     "oref_density_grid_bitfield": (None, [C.c_void_p, C.c_uint32]),
+    "oref_density_on_grid": (None, [C.c_void_p, C.POINTER(A.GridQuery), C.c_void_p, C.c_void_p]),
+    "oref_density_slices_mosaic": (None, [C.c_void_p, C.c_void_p, C.c_float, C.c_int, C.c_float, C.c_void_p, C.c_void_p,
+                                          C.c_void_p, C.c_void_p]),
     "oref_density_grid_evaluate": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
     "oref_density_grid_finish": (C.c_int, [C.c_void_p, C.POINTER(A.GridArgs)]),
     "oref_density_grid_tmp": (None, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int]),
@@ -95,6 +98,20 @@ def load():
 
 def ptr(a):
     return a.ctypes.data_as(C.c_void_p)
+
+
+def density_slices_mosaic(density, thresh=2.5, swap_y_z=False, density_range=4.0):
+    """save_density_grid_to_png's mosaic of a [z][y][x] grid -> (uint8 [h][w], (zero-x voxels, near-zero points))."""
+    d = np.ascontiguousarray(density, np.float32)
+    res = np.array([d.shape[2], d.shape[1], d.shape[0]], np.int32)
+    w, h = C.c_int(0), C.c_int(0)
+    lib = load()
+    lib.oref_density_slices_mosaic(ptr(d), ptr(res), thresh, int(swap_y_z), density_range, None, C.byref(w), C.byref(h), None)
+    out = np.zeros((h.value, w.value), np.uint8)
+    counts = np.zeros(2, np.uint32)
+    lib.oref_density_slices_mosaic(ptr(d), ptr(res), thresh, int(swap_y_z), density_range, ptr(out), C.byref(w), C.byref(h),
+                                   ptr(counts))
+    return out, (int(counts[0]), int(counts[1]))
 
 
 class Oracle:
@@ -182,6 +199,14 @@ class Oracle:
         n, stride = pos.shape
         out = np.zeros(n, np.float32)
         self.lib.oref_density(self.h, ptr(pos), stride, n, ptr(out), int(use_inf))
+        return out
+
+    def density_on_grid(self, query, grid=None):
+        """get_density_on_grid on an A.GridQuery lattice -> [z][y][x] float32 (grid: host density grid or None)."""
+        rx, ry, rz = (int(v) for v in query.res)
+        out = np.zeros((rz, ry, rx), np.float32)
+        g = None if grid is None else np.ascontiguousarray(grid, np.float32)
+        self.lib.oref_density_on_grid(self.h, C.byref(query), None if g is None else ptr(g), ptr(out))
         return out
 
     def backward(self, enc, dirs, dloss, weight=None):

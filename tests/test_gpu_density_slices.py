@@ -1,0 +1,114 @@
+"""Testbed.compute_and_save_png_slices / get_density_on_grid on the GPU (src/python_api.cu:451-459,
+src/testbed.cu:534-559, src/testbed_nerf.cu:147-160, 234-250, 3026-3075, src/marching_cubes.cu:40-47, 957-1020):
+the lattice densities against the oracle with the same weights and density grid, the written mosaic byte for byte
+against the oracle's mosaic of the same densities."""
+import os
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+FOX = os.path.join(ROOT, "data", "nerf", "fox", "transforms.json")
+
+
+@pytest.fixture(scope="module")
+def fox():
+    """base.json trained 300 steps on the fox (aabb_scale 4: three occupancy cascades, OpenCV lens)."""
+    import pyngp as ngp
+    tb = ngp.Testbed()
+    tb.load_training_data(FOX)
+    tb.reload_network_from_file("base.json")
+    tb.shall_train = True
+    while tb.training_step < 300:
+        tb.frame()
+    assert tb.nerf.max_cascade == 2
+    return ngp, tb
+
+
+def _query(tb, res, lo, hi, to_local=None):
+    import ngp_abi as A
+    q = A.GridQuery()
+    for k in range(3):
+        q.res[k] = res[k]
+        q.box_min[k], q.box_max[k] = lo[k], hi[k]
+        q.aabb_min[k], q.aabb_max[k] = tb.aabb.min[k], tb.aabb.max[k]
+    m = np.eye(3, dtype=np.float32) if to_local is None else np.asarray(to_local, np.float32)
+    for k in range(9):
+        q.box_to_local[k] = float(m.reshape(-1)[k])
+    q.max_cascade = int(tb.nerf.max_cascade)
+    q.mask_with_grid = 1
+    q.use_inference_params = 1
+    return q
+
+
+def _rot(axis, angle):
+    c, s = np.cos(angle), np.sin(angle)
+    i, j = [k for k in range(3) if k != axis]
+    R = np.eye(3, dtype=np.float32)
+    R[i, i], R[i, j], R[j, i], R[j, j] = c, -s, s, c
+    return R
+
+
+@pytest.mark.parametrize("box", ["render_aabb", "sub_box", "rotated"])
+def test_density_on_grid_matches_oracle(fox, box):
+    """get_density_on_grid: raw density outputs within the fp16 tolerance of the MLP parity tests, the -10000 mask
+    of cells the cascaded density grid holds below NERF_MIN_OPTICAL_THICKNESS identical."""
+    from scene_util import testbed_oracle
+    ngp, tb = fox
+    res = (40, 36, 28)
+    bb = ngp.BoundingBox()
+    orig_box, orig_local = tb.render_aabb, np.array(tb.render_aabb_to_local, np.float32)
+    if box == "sub_box":
+        bb = ngp.BoundingBox([-0.4, 0.1, 0.0], [1.7, 1.2, 0.9])
+    if box == "rotated":
+        tb.render_aabb = ngp.BoundingBox([-0.5, -0.5, -0.5], [1.5, 1.5, 1.5])
+        tb.render_aabb_to_local = _rot(1, 0.3) @ _rot(0, -0.2)
+    try:
+        g = tb.density_on_grid(list(res), bb)
+        if bb.is_empty():
+            lo, hi, R = tb.render_aabb.min, tb.render_aabb.max, np.asarray(tb.render_aabb_to_local)
+        else:
+            lo, hi, R = bb.min, bb.max, None
+        o = testbed_oracle(tb)
+        r = o.density_on_grid(_query(tb, res, lo, hi, R), tb.density_grid())
+    finally:
+        tb.render_aabb = orig_box
+        tb.render_aabb_to_local = orig_local
+    assert g.shape == (res[2], res[1], res[0])
+    masked_g, masked_r = g == -10000.0, r == -10000.0
+    np.testing.assert_array_equal(masked_g, masked_r)
+    assert 0.02 < masked_g.mean() < 0.98, masked_g.mean()  # both kinds of lattice points occur
+    np.testing.assert_allclose(g[~masked_g], r[~masked_r], atol=4e-3, rtol=8e-3)
+
+
+def test_png_slices_are_the_oracle_mosaic(fox, tmp_path):
+    """The written file: filename + '.density_slices_{x}x{y}x{z}.png', 8-bit gray, byte-identical to the oracle's
+    save_density_grid_to_png mosaic of the same lattice densities, for the defaults (render aabb, thresh =
+    mesh_thresh 2.5, range 4), a non-cubic box (get_marching_cubes_res rounds each axis up to 16), another
+    threshold / range and flip_y_and_z_axes; the return value is the lattice resolution."""
+    from oracle_abi import density_slices_mosaic
+    from density_slices_util import read_png_gray
+    ngp, tb = fox
+    cases = [
+        (dict(), None, (64, 64, 64)),
+        (dict(aabb=ngp.BoundingBox([-0.4, 0.2, 0.1], [1.6, 1.1, 1.3])), ngp.BoundingBox([-0.4, 0.2, 0.1], [1.6, 1.1, 1.3]),
+         (64, 32, 48)),
+        (dict(thresh=1.0, density_range=8.0), None, (64, 64, 64)),
+        (dict(flip_y_and_z_axes=True, aabb=ngp.BoundingBox([0.0, 0.0, 0.0], [1.0, 0.5, 1.0])),
+         ngp.BoundingBox([0.0, 0.0, 0.0], [1.0, 0.5, 1.0]), (64, 32, 64)),
+    ]
+    assert tb.mesh_thresh == 2.5
+    for i, (kw, bb, want) in enumerate(cases):
+        prefix = str(tmp_path / f"slices{i}")
+        res = tuple(int(v) for v in tb.compute_and_save_png_slices(prefix, 64, **kw))
+        assert res == want, (kw, res)
+        path = prefix + ".density_slices_{}x{}x{}.png".format(*res)
+        assert os.path.exists(path), path
+        png = read_png_gray(path)
+        d = tb.density_on_grid(list(res), bb if bb is not None else ngp.BoundingBox())
+        ref, _ = density_slices_mosaic(d, kw.get("thresh", 2.5), kw.get("flip_y_and_z_axes", False),
+                                       kw.get("density_range", 4.0))
+        np.testing.assert_array_equal(png, ref, err_msg=str(kw))
+        assert (png >= 129).any() and (png == 0).any()

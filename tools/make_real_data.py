@@ -6,6 +6,12 @@ container, where /root/reference exists; the outputs are committed and travel to
   stored as RGB PNG (lossless for an opaque image), intrinsics (fl_x/fl_y/cx/cy/w/h) halved.
   Split for the quality protocol: every 10th frame (0005, 0015, ...) -> transforms_test.json,
   the other 45 -> transforms_train.json.
+* data/nerf/test2/images: the reference's second BlenderNeRF scene (data/nerf/test2/images, 300 RGBA 720x1280
+  frames, alpha 255 everywhere, aabb_scale 1) at quarter resolution (180x320, Lanczos, RGB PNG), all 300 views,
+  intrinsics quartered; transforms_train.json lists every frame as the reference's does.  With
+  data/nerf/test/dataset it is one of the two scenes whose CUDA-trained density mosaics the reference ships
+  (data/nerf/test.density_slices_256x256x256.png, data/nerf/test2/images.density_slices_256x256x256.png), which
+  tests/golden/ref_density_slices/ holds byte for byte.
 * data/nerf/fox: the reference's transforms.json verbatim and its 50 JPG frames as shipped (17
   listed frames are absent from the reference checkout; the loader skips them exactly as
   nerf_loader.cu:364-387 does for files that do not exist).
@@ -45,6 +51,30 @@ def make_test():
     shutil.copy(os.path.join(src, "log.txt"), os.path.join(dst, "log.txt"))
 
 
+def make_test2():
+    src = os.path.join(REF, "test2", "images")
+    dst = os.path.join(OUT, "test2", "images")
+    os.makedirs(os.path.join(dst, "train"), exist_ok=True)
+    meta = json.load(open(os.path.join(src, "transforms_train.json")))
+    for k in ("fl_x", "fl_y", "cx", "cy", "w", "h"):
+        meta[k] = meta[k] * 0.25
+    for fr in meta["frames"]:
+        name = os.path.basename(fr["file_path"])
+        im = Image.open(os.path.join(src, fr["file_path"]))
+        w, h = im.size
+        im = im.resize((w // 4, h // 4), Image.LANCZOS).convert("RGB")
+        im.save(os.path.join(dst, "train", name), "PNG", optimize=True)
+    json.dump(meta, open(os.path.join(dst, "transforms_train.json"), "w"), indent=1)
+    shutil.copy(os.path.join(src, "log.txt"), os.path.join(dst, "log.txt"))
+
+
+def copy_reference_slices():
+    dst = os.path.join(ROOT, "tests", "golden", "ref_density_slices")
+    os.makedirs(dst, exist_ok=True)
+    shutil.copy(os.path.join(REF, "test.density_slices_256x256x256.png"), os.path.join(dst, "test.png"))
+    shutil.copy(os.path.join(REF, "test2", "images.density_slices_256x256x256.png"), os.path.join(dst, "test2.png"))
+
+
 def make_fox():
     src = os.path.join(REF, "fox")
     dst = os.path.join(OUT, "fox")
@@ -57,5 +87,12 @@ def make_fox():
 if __name__ == "__main__":
     if not os.path.isdir(REF):
         sys.exit("the reference checkout is not here (build container only)")
-    make_test()
-    make_fox()
+    which = sys.argv[1:] or ["test", "test2", "fox", "slices"]
+    if "test" in which:
+        make_test()
+    if "test2" in which:
+        make_test2()
+    if "fox" in which:
+        make_fox()
+    if "slices" in which:
+        copy_reference_slices()
