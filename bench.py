@@ -58,8 +58,13 @@ def parse():
     p.add_argument("--cpu-rays", type=int, default=512, help="training rays in the CPU oracle sample")
     p.add_argument("--surface-scene", type=int, default=1,
                    help="N=1: also time the procedural lego-shaped SURFACE scene (train + 1080p render) -> surface_scene")
+    p.add_argument("--config-e", type=int, default=1,
+                   help="N=1: also time BASELINE config E's shape (T=2^22 L16F2 network, aabb_scale 64 scene) -> config_e")
+    p.add_argument("--config-e-pretrain", type=int, default=500)
     p.add_argument("--render-in-hbm", type=int, default=5,
                    help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
+    p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r05_surface_pmc_traffic.json"),
+                   help="PMC traffic summary of the surface-scene bench (tools/pmc_traffic.py)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r04_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
@@ -165,6 +170,80 @@ def read_timers(abi, lib, handle):
     return out
 
 
+def kernel_table(calib, models):
+    """Per timer: time, launches, units and the roofline fraction of its algorithmic bytes / flops."""
+    kernels = {}
+    for name, (ms, units, launches) in calib.items():
+        if launches == 0:
+            continue
+        entry = {"ms_total": round(ms, 3), "launches": launches, "units": units,
+                 "us_per_launch": round(1000.0 * ms / launches, 2)}
+        if name in models and ms > 0:
+            bound, per_unit = models[name]
+            rate = model_bytes(name, per_unit, units, calib) / (ms / 1000.0)
+            if bound == "hbm":
+                entry["GB/s"] = round(rate / 1e9, 1)
+                entry["frac"] = round(rate / 1e9 / HBM_PEAK_GBS, 4)
+            else:
+                entry["TFLOP/s"] = round(rate / 1e12, 2)
+                entry["frac"] = round(rate / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)
+        kernels[name] = entry
+    return kernels
+
+
+def roofline_of(dom, tsrc, models):
+    """The roofline block of timer `dom` from (ms, units, launches) timers: algorithmic work per launch / launch time."""
+    bound, per_unit = models[dom]
+    ms, units, launches = tsrc[dom]
+    work = model_bytes(dom, per_unit, units, tsrc)
+    achieved = work / launches / (ms / launches / 1000.0)
+    r = {"kernel": dom, "bound": bound, "achieved": round(achieved / (1e9 if bound == "hbm" else 1e12), 2),
+         "peak": HBM_PEAK_GBS if bound == "hbm" else MFMA_F16_PEAK_TFLOPS,
+         "unit": "GB/s" if bound == "hbm" else "TFLOP/s", "traffic": None,
+         "per_unit": per_unit if per_unit is not None else f"{MARCH_B_PER_SAMPLE} B/filled sample + {MARCH_B_PER_RAY} B/ray",
+         "units_per_launch": round(units / launches), "bytes_or_flops_per_launch": round(work / launches),
+         "us_per_launch": round(1000.0 * ms / launches, 2)}
+    r["frac"] = round(r["achieved"] / r["peak"], 4)
+    return r, work
+
+
+def testbed_models(tb):
+    cfg = tb.network_config
+    enc = cfg["encoding"]
+    return kernel_models({"n_levels": int(enc["n_levels"]), "F": int(enc["n_features_per_level"]),
+                          "W": int(cfg["network"]["n_neurons"]), "dh": int(cfg["network"]["n_hidden_layers"]),
+                          "rh": int(cfg["rgb_network"]["n_hidden_layers"])})
+
+
+def timed_leg(args, tb, step):
+    """Warmup (its last calibration steps with every kernel timer on), then args.steps timed steps with only the
+    dominant kernel's timer; returns (seconds, step results, kernel table, roofline of the dominant kernel)."""
+    import ngp_abi as A
+    lib = A.load()
+    h = C.c_void_p(tb.model_handle)
+    models = testbed_models(tb)
+    n_cal = min(args.warmup, 3)
+    for i in range(args.warmup):
+        if i == args.warmup - n_cal:
+            A.check(lib.ngp_timing_enable(h, -1))
+            read_timers(A, lib, tb.model_handle)
+        step()
+    calib = read_timers(A, lib, tb.model_handle)
+    modeled = [k for k in models if calib.get(k, (0, 0, 0))[2] > 0 and k != "render_march"]
+    dom = max(modeled, key=lambda k: calib[k][0]) if modeled else "render_encode"
+    A.check(lib.ngp_timing_enable(h, 1 << A.TIMER[dom]))
+    read_timers(A, lib, tb.model_handle)
+    tb.sync()
+    t0 = time.perf_counter()
+    out = [step() for _ in range(args.steps)]
+    tb.sync()
+    elapsed = time.perf_counter() - t0
+    timers = read_timers(A, lib, tb.model_handle)
+    A.check(lib.ngp_timing_enable(h, 0))
+    roof, _ = roofline_of(dom, timers, models)
+    return elapsed, out, kernel_table(calib, models), roof
+
+
 def cpu_baseline(args, tb, cams, imgs, focal, view, W, H, calib, n_cal):
     """The scalar C++ oracle (tests/cpu_baseline.py) on bounded samples, timed single-threaded and
     with OpenMP on min(16, hardware_concurrency) threads (the GPU box's CPU share):
@@ -239,22 +318,64 @@ def surface_scene(args, ngp):
         del img
         return tb.last_train_stats()["n_rays"], t1 - t0, time.perf_counter() - t1
 
-    for _ in range(args.warmup):
-        step()
-    tb.sync()
-    rays = train_s = render_s = 0
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        r, a, b = step()
-        rays += r + W * H
-        train_s += a
-        render_s += b
-    elapsed = time.perf_counter() - t0
+    elapsed, out, kernels, roof = timed_leg(args, tb, step)
+    rays = sum(r + W * H for r, _, _ in out)
+    train_s = sum(a for _, a, _ in out)
+    render_s = sum(b for _, _, b in out)
+    roof["traffic"] = pmc_traffic(args.surface_traffic_json, roof["kernel"], roof["units_per_launch"])
     return {"Mrays_s": round(rays / elapsed / 1e6, 3), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "roofline": roof, "kernels_calibration": kernels,
             "train_ms_per_step": round(1e3 * train_s / args.steps, 3), "render_ms_per_frame": round(1e3 * render_s / args.steps, 3),
             "render_Mrays_s": round(W * H * args.steps / render_s / 1e6, 3),
             "workload": f"synthetic lego-shaped surface scene ({args.views} views {args.train_res}x{args.train_res}), same network, "
                         f"{args.pretrain} pretrain steps, then train(2^18) + render({W}, {H}, spp 1) to host memory per step"}
+
+
+def config_e(args, ngp):
+    """BASELINE config E's shape on one GPU: the T=2^22 L16F2 network (configs/nerf/bicycle_L16F2T22.json) on a scene
+    with aabb_scale 64 (the fox's real photos with aabb_scale raised to 64: mip-nerf360/bicycle is not available
+    offline), pretrained, then args.steps of train(2^18) + render(1920, 1080, spp 1) to host memory."""
+    import tempfile
+
+    sys.path.insert(0, TESTS)
+    from test_gpu_config_e import fox_aabb64
+
+    hip = C.CDLL("libamdhip64.so")
+
+    def used():
+        free, total = C.c_size_t(), C.c_size_t()
+        hip.hipMemGetInfo(C.byref(free), C.byref(total))
+        return total.value - free.value
+
+    used0 = used()
+    with tempfile.TemporaryDirectory() as d:
+        tb = ngp.Testbed(ngp.TestbedMode.Nerf)
+        tb.load_training_data(fox_aabb64(d))
+        tb.reload_network_from_file("bicycle_L16F2T22.json")
+        tb.shall_train = True
+        for _ in range(args.config_e_pretrain):
+            tb.train(args.batch)
+        W, H = args.width, args.height
+
+        def step():
+            t0 = time.perf_counter()
+            tb.train(args.batch)
+            t1 = time.perf_counter()
+            tb.set_camera_to_training_view(3)
+            img = tb.render(W, H, 1, True)
+            del img
+            return tb.last_train_stats()["n_rays"], t1 - t0, time.perf_counter() - t1
+
+        elapsed, out, kernels, roof = timed_leg(args, tb, step)
+        mem = used() - used0
+        del tb
+    rays = sum(r + W * H for r, _, _ in out)
+    return {"Mrays_s": round(rays / elapsed / 1e6, 3), "ms_per_step": round(1e3 * elapsed / args.steps, 3),
+            "train_ms_per_step": round(1e3 * sum(a for _, a, _ in out) / args.steps, 3),
+            "render_ms_per_frame": round(1e3 * sum(b for _, _, b in out) / args.steps, 3),
+            "device_memory_GiB": round(mem / 2**30, 3), "roofline": roof, "kernels_calibration": kernels,
+            "workload": f"T=2^22 L16F2 64-wide MLPs, fox photos with aabb_scale 64 (max_cascade 6), {args.config_e_pretrain} "
+                        f"pretrain steps, then train(2^18) + render({W}, {H}, spp 1) to host memory per step"}
 
 
 def launch_ranks(args):
@@ -410,22 +531,7 @@ def main():
                     "Mrays_s": round(W * H * args.steps / tc / 1e6, 3), "ms_per_frame": round(1e3 * tc / args.steps, 3),
                     "scaling": "strong"}
 
-    kernels = {}
-    for name, (ms, units, launches) in calib.items():
-        if launches == 0:
-            continue
-        entry = {"ms_total": round(ms, 3), "launches": launches, "units": units,
-                 "us_per_launch": round(1000.0 * ms / launches, 2)}
-        if name in models and ms > 0:
-            bound, per_unit = models[name]
-            rate = model_bytes(name, per_unit, units, calib) / (ms / 1000.0)
-            if bound == "hbm":
-                entry["GB/s"] = round(rate / 1e9, 1)
-                entry["frac"] = round(rate / 1e9 / HBM_PEAK_GBS, 4)
-            else:
-                entry["TFLOP/s"] = round(rate / 1e12, 2)
-                entry["frac"] = round(rate / 1e12 / MFMA_F16_PEAK_TFLOPS, 4)
-        kernels[name] = entry
+    kernels = kernel_table(calib, models)
     bound, per_unit = models[dom]
     tsrc = timers if args.kernel_timer else calib
     ms, units, launches = tsrc[dom]
@@ -481,10 +587,13 @@ def main():
     if rank == 0 and world == 1 and args.cpu_baseline:
         cpu, parity = cpu_baseline(args, tb, cams, imgs, focal, view, W, H, calib, n_cal)
 
-    surface = None
-    if world == 1 and args.surface_scene:
+    surface = cfg_e = None
+    if world == 1 and (args.surface_scene or args.config_e):
         del tb
+    if world == 1 and args.surface_scene:
         surface = surface_scene(args, ngp)
+    if world == 1 and args.config_e:
+        cfg_e = config_e(args, ngp)
 
     value = rays / elapsed / 1e6
     if rank == 0:
@@ -521,6 +630,7 @@ def main():
             "kernels_calibration": kernels,
             "render_in_hbm": render_in_hbm,
             "surface_scene": surface,
+            "config_e": cfg_e,
             "config_c": config_c,
         }
         print(json.dumps(line), flush=True)

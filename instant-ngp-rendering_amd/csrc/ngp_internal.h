@@ -285,6 +285,9 @@ struct TrainScratch {
 	// and the compacted batch's order, and dL/d(code) of the compacted samples
 	DevBuf<uint32_t> simg, eimg, cimg;
 	DevBuf<float> dextra;              // [B][16]
+	// deterministic steps: per-image fixed-point gradient sums [n_images][IMG_FIX_STRIDE]: exposure 0-2, camera
+	// translation 3-5, rotation 6-8, latent code 9-24 (train.hip img_deposit_fixed)
+	DevBuf<unsigned long long> img_fix;
 	DevBuf<float> api_extra;           // C-ABI entries: the latent codes of coordinate records, rows of 16
 	DevBuf<uint32_t> api_extra_idx;
 	DevBuf<uint32_t> dp;               // data parallel: [0,3) sample DpCaps, [4,7) compaction DpCaps, then 2 x [world] slots
@@ -296,6 +299,8 @@ struct TrainScratch {
 	// data parallelism: the sample capacity a step that did not fit asked for (grown on the retry)
 	uint32_t rank_cap_hint = 0;
 };
+
+constexpr uint32_t IMG_FIX_STRIDE = 25;
 
 struct GridState {
 	DevBuf<float> grid;        // [n_cascades][N]

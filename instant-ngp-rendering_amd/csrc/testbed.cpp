@@ -225,6 +225,7 @@ Testbed::~Testbed() {
 	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid, m_dist, m_dist_grad, m_extra, m_extra_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
+	if (m_extra_stage) pinned_host_release(m_extra_stage, 16 * sizeof(float));
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
 }
 
@@ -1254,11 +1255,27 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 				allreduce_dev(g, info.n_mlp_params, 0, false);
 				allreduce_dev(gg, info.n_grid_params, deterministic ? 3 : 1, false);
 			}
-			// the violation word (early stops of the chunked forward, a rank's sample capacity) gates the
-			// optimizer; every rank takes the max over the ranks, so all of them skip or all of them step
+			// the violation word (early stops of the chunked forward in the low bits, a rank's sample capacity in
+			// VIOL_CAPACITY, ngp_internal.h) gates the optimizer; its two parts are reduced separately (a max of
+			// the packed word would hide one rank's early stops behind another's capacity flag), so every rank
+			// sees any rank's early stops and any rank's overflow, and all of them skip or all of them step
 			void* viol = nullptr;
 			ck(ngp_train_scratch(m_model, NGP_SCRATCH_VIOLATIONS, &viol, nullptr));
-			if (viol) allreduce_dev(viol, 1, 2, true);
+			if (viol) {
+				constexpr uint32_t kViolCapacity = 1u << 20;
+				uint32_t w = 0;
+				hk(hipMemcpyAsync(&w, viol, 4, hipMemcpyDeviceToHost, (hipStream_t)m_stream), "violations d2h");
+				sync();
+				int32_t parts[2] = {(int32_t)(w & (kViolCapacity - 1u)), (w & kViolCapacity) ? 1 : 0};
+				int32_t* dp = (int32_t*)m_red_buf + 8;
+				hk(hipMemcpyAsync(dp, parts, sizeof(parts), hipMemcpyHostToDevice, (hipStream_t)m_stream), "violations h2d");
+				allreduce_dev(dp, 2, 2, true);
+				hk(hipMemcpyAsync(parts, dp, sizeof(parts), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "violations d2h");
+				sync();
+				w = (parts[1] ? kViolCapacity : 0u) | std::min<uint32_t>((uint32_t)parts[0], kViolCapacity - 1u);
+				hk(hipMemcpyAsync(viol, &w, 4, hipMemcpyHostToDevice, (hipStream_t)m_stream), "violations h2d");
+				sync();
+			}
 			ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 		}
 		// NerfCounters::update_after_training (src/testbed_nerf.cu:2422-2446)
@@ -1683,7 +1700,24 @@ void Testbed::set_rendering_extra_dims(const std::vector<float>& vals) {
 
 // Nerf::get_rendering_extra_dims_cpu: the code set with set_rendering_extra_dims (the training view's code when
 // rendering_extra_dims_from_training_view selects one is what the renderer uses, not this buffer)
-std::vector<float> Testbed::rendering_extra_dims() const { return m_rendering_extra_dims; }
+// Nerf::get_rendering_extra_dims_cpu (src/testbed_nerf.cu:3269-3280): the code rendered rays carry -- the trained code of
+// rendering_extra_dims_from_training_view when it names a view (the default 0), the set one otherwise -- with the warped
+// light direction in the first three entries for datasets with light dirs (get_rendering_extra_dims, :3206-3228)
+std::vector<float> Testbed::rendering_extra_dims() const {
+	const NerfTraining& tr = nerf.training;
+	const uint32_t E = tr.dataset.n_extra_dims();
+	if (!E) return {};
+	std::vector<float> row(E, 0.0f);
+	const int v = rendering_extra_dims_from_training_view;
+	const std::vector<float>& src = v >= 0 && (size_t)v < tr.extra_dims_opt.size() ? tr.extra_dims_opt[v].variable : m_rendering_extra_dims;
+	for (uint32_t j = 0; j < E && j < src.size(); ++j) row[j] = src[j];
+	if (tr.dataset.has_light_dirs) {
+		const vec3 ld = nerf.light_dir;
+		const float l = std::sqrt(ld[0] * ld[0] + ld[1] * ld[1] + ld[2] * ld[2]);
+		for (uint32_t j = 0; j < 3 && j < E; ++j) row[j] = l > 0.f ? (ld[j] / l + 1.0f) * 0.5f : 0.5f;
+	}
+	return row;
+}
 
 std::vector<float> Testbed::training_extra_dims(int trainview) const {
 	if (n_extra_dims() == 0) return {};  // Nerf::Training::get_extra_dims_cpu (src/testbed_nerf.cu:1797-1812)
@@ -1763,19 +1797,15 @@ const float* Testbed::rendering_extra_dims_device() {
 	const uint32_t E = tr.dataset.n_extra_dims();
 	if (!E) return nullptr;
 	if (!m_extra) upload_extra_dims();
-	std::vector<float> row(16, 0.0f);
-	const int v = rendering_extra_dims_from_training_view;
-	const std::vector<float>& src = v >= 0 && (size_t)v < tr.extra_dims_opt.size() ? tr.extra_dims_opt[v].variable : m_rendering_extra_dims;
-	for (uint32_t j = 0; j < E && j < src.size(); ++j) row[j] = src[j];
-	if (tr.dataset.has_light_dirs) {
-		const vec3 ld = nerf.light_dir;
-		const float l = std::sqrt(ld[0] * ld[0] + ld[1] * ld[1] + ld[2] * ld[2]);
-		for (int j = 0; j < 3; ++j) row[j] = l > 0.f ? (ld[j] / l + 1.0f) * 0.5f : 0.5f;
-	}
+	const std::vector<float> row = rendering_extra_dims();
+	// staged in a page-locked row of its own: the copy is still in flight when this returns, and render() synchronises
+	// the stream before the next call writes the row again
+	if (!m_extra_stage) m_extra_stage = static_cast<float*>(pinned_host_alloc(16 * sizeof(float)));
+	std::fill(m_extra_stage, m_extra_stage + 16, 0.0f);
+	std::copy(row.begin(), row.end(), m_extra_stage);
 	const size_t n = m_extra_rows - 1;
-	std::copy(row.begin(), row.end(), m_extra_host.begin() + 16 * n);
-	hk(hipMemcpyAsync(m_extra + 16 * n, m_extra_host.data() + 16 * n, 16 * sizeof(float), hipMemcpyHostToDevice,
-	                  (hipStream_t)m_stream), "upload rendering extra dims");
+	hk(hipMemcpyAsync(m_extra + 16 * n, m_extra_stage, 16 * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream),
+	   "upload rendering extra dims");
 	return m_extra + 16 * n;
 }
 

@@ -405,7 +405,8 @@ private:
 	float* m_extra_grad = nullptr;
 	size_t m_extra_rows = 0;
 	std::vector<float> m_rendering_extra_dims;
-	std::vector<float> m_extra_host;  // staging of the device table (the rendered row is copied asynchronously)
+	std::vector<float> m_extra_host;  // staging of the device table (uploaded synchronously)
+	float* m_extra_stage = nullptr;   // pinned 16-float staging of the rendered row (copied asynchronously)
 	void reset_extra_dims(pcg32* rng);  // Nerf::reset_extra_dims (src/testbed_nerf.cu:3181-3204; rng: n_extra_dims > 0)
 	void upload_extra_dims();           // Nerf::Training::update_extra_dims (src/testbed_nerf.cu:1814-1825)
 	const float* rendering_extra_dims_device();  // Nerf::get_rendering_extra_dims (src/testbed_nerf.cu:3206-3228)

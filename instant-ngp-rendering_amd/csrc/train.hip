@@ -658,6 +658,7 @@ struct LossArgs {
 	ErrorCdf cdf;
 	const float* exposure;     // [n_images][3] log2 exposure (null: 0)
 	float* exposure_grad;      // [n_images][3] (null: off)
+	unsigned long long* exposure_fix;  // deterministic steps: the exposure deposits in 2^-32 fixed point (null: float atomics)
 	float4* ray_aux;           // [R]: the ray's dL/dexposure, deposited by k_loss_emit if the ray is kept
 	float* error_map;
 	uint32_t error_map_rx, error_map_ry;
@@ -925,6 +926,26 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	a.ccounts[i] = c;
 }
 
+// Deterministic steps (ngp_train_args.deterministic): per-image gradient deposits (exposure, camera extrinsics,
+// latent codes) are summed as 64-bit integers in 2^-32 units, so the sums do not depend on the order of the rays'
+// atomics; k_img_fix_flush adds each step's sum to the float gradient once and clears it.  A contribution is
+// clamped at +-2^62 units (+-1.07e9), far beyond any loss-scaled per-ray gradient.
+constexpr double IMG_FIXED_SCALE = 4294967296.0;  // 2^32
+__device__ __forceinline__ void img_deposit_fixed(unsigned long long* dst, float v) {
+	const double x = fmin(fmax((double)v * IMG_FIXED_SCALE, -4.6e18), 4.6e18);
+	atomicAdd(dst, (unsigned long long)(long long)rint(x));
+}
+
+__global__ void __launch_bounds__(256) k_img_fix_flush(uint32_t n, uint32_t stride, uint32_t first, uint32_t width,
+                                                       unsigned long long* __restrict__ fix, float* __restrict__ dst) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n * width) return;
+	const size_t src = (size_t)(i / width) * stride + first + i % width;
+	const long long v = (long long)fix[src];
+	fix[src] = 0ull;
+	if (v) dst[i] += (float)((double)v * (1.0 / IMG_FIXED_SCALE));
+}
+
 // pass 2: recomposite the kept samples of the ray (one wave, 64 per iteration) and write
 // dL/d(raw network output) with the suffix trick (testbed_nerf.cu:1061-1119) plus the
 // compacted-slot -> source-sample map; consecutive lanes write consecutive slots.
@@ -948,9 +969,15 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 	if (a.exposure_grad && lane == 0 && deposit) {
 		const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
 		const float4 g = a.ray_aux[i];
-		atomicAdd(&a.exposure_grad[3 * (size_t)img + 0], g.x);
-		atomicAdd(&a.exposure_grad[3 * (size_t)img + 1], g.y);
-		atomicAdd(&a.exposure_grad[3 * (size_t)img + 2], g.z);
+		if (a.exposure_fix) {
+			img_deposit_fixed(&a.exposure_fix[3 * (size_t)img + 0], g.x);
+			img_deposit_fixed(&a.exposure_fix[3 * (size_t)img + 1], g.y);
+			img_deposit_fixed(&a.exposure_fix[3 * (size_t)img + 2], g.z);
+		} else {
+			atomicAdd(&a.exposure_grad[3 * (size_t)img + 0], g.x);
+			atomicAdd(&a.exposure_grad[3 * (size_t)img + 1], g.y);
+			atomicAdd(&a.exposure_grad[3 * (size_t)img + 2], g.z);
+		}
 	}
 	if (a.error_map && lane == 0 && deposit) {
 		// bilinear deposit of the ray's mean loss (src/testbed_nerf.cu:1028-1054; rays without
@@ -1104,6 +1131,7 @@ struct CamGradArgs {
 	const float* dsh;            // [B][16]
 	float* cam_pos_gradient;     // [n_images][3] (null: off)
 	float* cam_rot_gradient;     // [n_images][3]
+	unsigned long long* cam_fix; // deterministic steps: [n_images][IMG_FIX_STRIDE], pos at 3, rot at 6 (null: float atomics)
 	const ngp_image* images;     // the images' current transforms (distortion gradient)
 	const uint32_t* viol_gate;   // non-zero: the step is discarded and re-run -- no deposits
 	float* dgrad;                // distortion map gradient / weight [dry][drx][2] (null: off)
@@ -1163,6 +1191,16 @@ __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 	}
 	if (!a.cam_pos_gradient) return;
 	const v3 aa = mk3(d.y * gd.z - d.z * gd.y, d.z * gd.x - d.x * gd.z, d.x * gd.y - d.y * gd.x);
+	if (a.cam_fix) {
+		unsigned long long* f = a.cam_fix + IMG_FIX_STRIDE * (size_t)img;
+		img_deposit_fixed(f + 3, go.x * inv_pdf);
+		img_deposit_fixed(f + 4, go.y * inv_pdf);
+		img_deposit_fixed(f + 5, go.z * inv_pdf);
+		img_deposit_fixed(f + 6, aa.x * inv_pdf);
+		img_deposit_fixed(f + 7, aa.y * inv_pdf);
+		img_deposit_fixed(f + 8, aa.z * inv_pdf);
+		return;
+	}
 	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 0], go.x * inv_pdf);
 	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 1], go.y * inv_pdf);
 	atomicAdd(&a.cam_pos_gradient[3 * (size_t)img + 2], go.z * inv_pdf);
@@ -1175,7 +1213,8 @@ __global__ void __launch_bounds__(256) k_cam_gradient(CamGradArgs a) {
 // code) summed into its image's gradient (one thread per ray, E float atomics; loss-scaled like the reference's)
 __global__ void __launch_bounds__(256) k_extra_gradient(uint32_t n_rays, const uint32_t* __restrict__ compacted,
                                                         const float* __restrict__ loss_state, const float* __restrict__ dextra,
-                                                        uint32_t E, float* __restrict__ grad, const uint32_t* __restrict__ viol_gate) {
+                                                        uint32_t E, float* __restrict__ grad, const uint32_t* __restrict__ viol_gate,
+                                                        unsigned long long* __restrict__ fix) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= n_rays || (viol_gate && *viol_gate)) return;
 	const uint32_t cn = compacted[2 * i], cbase = compacted[2 * i + 1];
@@ -1196,8 +1235,11 @@ __global__ void __launch_bounds__(256) k_extra_gradient(uint32_t n_rays, const u
 	}
 	const uint32_t img = __float_as_uint(loss_state[8 * (size_t)i + 7]);
 #pragma unroll
-	for (uint32_t k = 0; k < 16; ++k)
-		if (k < E) atomicAdd(&grad[16 * (size_t)img + k], g[k]);
+	for (uint32_t k = 0; k < 16; ++k) {
+		if (k >= E) continue;
+		if (fix) img_deposit_fixed(&fix[IMG_FIX_STRIDE * (size_t)img + 9 + k], g[k]);
+		else atomicAdd(&grad[16 * (size_t)img + k], g[k]);
+	}
 }
 
 // Gather the compacted batch (coords + per-level features) in compacted order: one
@@ -1708,6 +1750,11 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	// deterministic hash-grid gradients: the fixed-point buffer, zeroed once (the optimizer clears
 	// what it consumed, as for the fp16 buffer)
 	ts.fixed = t->deterministic != 0;
+	if (ts.fixed && ts.img_fix.n < (size_t)IMG_FIX_STRIDE * t->n_images) {
+		ts.img_fix.release();
+		ts.img_fix.reserve((size_t)IMG_FIX_STRIDE * t->n_images);
+		NGP_HIP_CHECK(hipMemsetAsync(ts.img_fix.ptr, 0, ts.img_fix.bytes(), s));
+	}
 	if (ts.fixed && !m->grid_grads64.ptr) {
 		m->grid_grads64.reserve(m->n_grid_params);
 		NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads64.ptr, 0, m->n_grid_params * sizeof(long long), s));
@@ -1867,6 +1914,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.error_map = t->error_map;
 	la.exposure = t->exposure;
 	la.exposure_grad = t->exposure_gradient;
+	la.exposure_fix = ts.fixed && t->exposure_gradient ? ts.img_fix.ptr : nullptr;
 	ts.ray_aux.reserve(4 * (size_t)R);
 	la.ray_aux = reinterpret_cast<float4*>(ts.ray_aux.ptr);
 	la.error_map_rx = t->error_map_res[0];
@@ -1994,7 +2042,8 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	                 MlpExtra{t->extra_dims, xd ? ts.cimg.ptr : nullptr, xgrad ? ts.dextra.ptr : nullptr});
 	if (xgrad) {
 		k_extra_gradient<<<div_up(R, 256u), 256, 0, s>>>(R, ts.ray_compacted.ptr, ts.ray_loss_state.ptr, ts.dextra.ptr,
-		                                                 m->cfg.n_extra_dims, t->extra_dims_gradient, la.viol_gate);
+		                                                 m->cfg.n_extra_dims, t->extra_dims_gradient, la.viol_gate,
+		                                                 ts.fixed ? ts.img_fix.ptr : nullptr);
 		NGP_HIP_CHECK(hipGetLastError());
 	}
 	tm.end(NGP_TIMER_TRAIN_MLP_BWD, s);
@@ -2022,6 +2071,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		ca.cam_pos_gradient = t->cam_pos_gradient;
 		ca.cam_rot_gradient = t->cam_rot_gradient;
 		if (!(t->cam_pos_gradient && t->cam_rot_gradient)) ca.cam_pos_gradient = ca.cam_rot_gradient = nullptr;
+		ca.cam_fix = ts.fixed && ca.cam_pos_gradient ? ts.img_fix.ptr : nullptr;
 		ca.images = t->images;
 		ca.viol_gate = la.viol_gate;
 		if (dist_grad) {
@@ -2032,6 +2082,21 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		}
 		k_cam_gradient<<<div_up(R, 256), 256, 0, s>>>(ca);
 		NGP_HIP_CHECK(hipGetLastError());
+	}
+	if (ts.fixed) {
+		// the step's fixed-point per-image sums into the float gradients, in image order
+		const uint32_t NI = t->n_images;
+		auto flush = [&](uint32_t first, uint32_t width, float* dst) {
+			if (!dst || !width) return;
+			k_img_fix_flush<<<div_up(NI * width, 256u), 256, 0, s>>>(NI, IMG_FIX_STRIDE, first, width, ts.img_fix.ptr, dst);
+			NGP_HIP_CHECK(hipGetLastError());
+		};
+		flush(0, 3, t->exposure_gradient);
+		if (cam && t->cam_pos_gradient && t->cam_rot_gradient) {
+			flush(3, 3, t->cam_pos_gradient);
+			flush(6, 3, t->cam_rot_gradient);
+		}
+		if (xgrad) flush(9, 16, t->extra_dims_gradient);  // rows of 16, the first E written
 	}
 	tm.train_units_pending = tm.mask != 0;
 

@@ -236,7 +236,11 @@ def test_data_parallel_testbed_two_processes_one_gpu(scene):
     # discarded and re-run with grown buffers) and whose chunked forward stops rays far too early (bit 2:
     # violations on the first step, discarded and re-run with the full forward): the same training
     (4, "lego_L16F2.json", {"debug": 12}),
-], ids=["2-tiny", "2-lego", "4-lego", "4-lego-retries"])
+    # config D's full width: eight ranks (the per-rank sample caps at twice the even share of 1/8 of the global cap,
+    # and the capacity-overflow regrowth, at the world size the node runs)
+    (8, "lego_L16F2.json", None),
+    (8, "lego_L16F2.json", {"debug": 12}),
+], ids=["2-tiny", "2-lego", "4-lego", "4-lego-retries", "8-lego", "8-lego-retries"])
 def test_ranks_train_like_one_process_with_world_times_the_batch(scene, world, config, tuning):
     """rank r of N owns global rays [r R, (r+1) R) of one batch; with the exact
     decomposition the N ranks' step is one process's step of N x the batch.  Deterministic mode on
@@ -281,7 +285,8 @@ def test_ranks_train_like_one_process_with_world_times_the_batch(scene, world, c
             # can change sign, and Adam's early steps turn that into a full step (lr) of the other sign
             # (two ranks: < 0.5 % of the grid; four ranks' partitions differ more: measured 0.65 %)
             far = ~np.isclose(d["params"][n_mlp:], s["params"][n_mlp:], rtol=1e-3, atol=1e-6)
-            assert far.mean() < (5e-3 if world == 2 else 1e-2), (step, far.mean())
+            print("world", world, "step", step, "grid params off", far.mean())
+            assert far.mean() < {2: 5e-3, 4: 1e-2}.get(world, 2e-2), (step, far.mean())
     # after the first step the hash-grid parameters are bit-identical (integer-summed gradients, the
     # same Adam step); the step-1 MLP gradients only differ in association
     np.testing.assert_array_equal(res[0][1]["params"][n_mlp:], single[1]["params"][n_mlp:])
@@ -305,9 +310,9 @@ def test_ranks_train_like_one_process_with_world_times_the_batch(scene, world, c
     print("batch", [(d["stats"][k], s["stats"][k]) for k in ("measured_batch_size", "measured_batch_size_before_compaction")],
           "window loss", np.mean(losses), np.mean(single_losses))
     for k in ("measured_batch_size", "measured_batch_size_before_compaction"):
-        assert d["stats"][k] == pytest.approx(s["stats"][k], rel=1e-2 if world == 2 else 3e-2), k
+        assert d["stats"][k] == pytest.approx(s["stats"][k], rel={2: 1e-2, 4: 3e-2}.get(world, 5e-2)), k
     assert len(losses) == len(single_losses) == EQ_WINDOW
-    assert np.mean(losses) == pytest.approx(np.mean(single_losses), rel=3e-2 if world == 2 else 8e-2)
+    assert np.mean(losses) == pytest.approx(np.mean(single_losses), rel={2: 3e-2, 4: 8e-2}.get(world, 1.2e-1))
 
 
 def _n_mlp(tb):

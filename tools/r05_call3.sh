@@ -10,3 +10,13 @@ timeout -k 10 400 python -u tools/density_slices_probe.py --scene $sc --seeds 13
 grep -v "^Wrote\|#lattice" gpurun_out/r05c/ds_${sc}.log | cut -c1-250
 done
 echo "== done $(date +%T)"
+echo "== camera / exposure / extra-dims tests $(date +%T)"
+timeout -k 10 600 python -u -m pytest tests -m gpu -v -s -k "extrinsic or exposure or cam_gradient or extra_dims or deterministic or config_e_trains" \
+  --timeout 300 --timeout-method thread > gpurun_out/r05c/cam_tests.log 2>&1 \
+  || { echo "tests rc=$?"; grep -E "pose error|PASS|FAIL|Error" gpurun_out/r05c/cam_tests.log | tail -20; exit 1; }
+grep -E "pose error|config E|passed|failed" gpurun_out/r05c/cam_tests.log | tail -5
+echo "== 8-rank DP tests $(date +%T)"
+timeout -k 10 700 python -u -m pytest tests/test_gpu_distributed.py -v -s -k "8-lego" --timeout 600 --timeout-method thread \
+  > gpurun_out/r05c/dp8_tests.log 2>&1 || { echo "tests rc=$?"; grep -E "world|passed|failed|Error" gpurun_out/r05c/dp8_tests.log | tail -20; exit 1; }
+grep -E "world|batch|passed|failed" gpurun_out/r05c/dp8_tests.log | tail -12
+echo "== done $(date +%T)"
