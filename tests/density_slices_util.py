@@ -106,3 +106,28 @@ def testbed_volume(tb, save_prefix=None, resolution=256):
         return mosaic_to_volume(read_png_gray(path), tuple(int(r) for r in res))
     with tempfile.TemporaryDirectory() as d:
         return testbed_volume(tb, os.path.join(d, "field"), resolution)
+
+
+def coarse(mask, block=8):
+    """Fraction of set voxels per block^3 block of a cubic mask."""
+    n = mask.shape[0] // block
+    return mask.astype(np.float32).reshape(n, block, n, block, n, block).mean((1, 3, 5))
+
+
+def orientation_ranking(ours, ref):
+    """Correlation of two coarse occupancy grids under each of the 48 axis permutations / flips of `ref`; returns
+    (correlation at the identity, its rank among the 48: 0 = best)."""
+    import itertools
+    cs = []
+    ident = None
+    for perm in itertools.permutations(range(3)):
+        for flips in itertools.product((0, 1), repeat=3):
+            r = ref.transpose(perm)
+            for ax, f in enumerate(flips):
+                if f:
+                    r = np.flip(r, ax)
+            c = float(np.corrcoef(r.ravel(), ours.ravel())[0, 1])
+            cs.append(c)
+            if perm == (0, 1, 2) and flips == (0, 0, 0):
+                ident = c
+    return ident, sorted(cs, reverse=True).index(ident)

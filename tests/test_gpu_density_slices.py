@@ -112,3 +112,38 @@ def test_png_slices_are_the_oracle_mosaic(fox, tmp_path):
                                        kw.get("density_range", 4.0))
         np.testing.assert_array_equal(png, ref, err_msg=str(kw))
         assert (png >= 129).any() and (png == 0).any()
+
+
+def test_trained_field_against_the_reference_density_mosaic():
+    """The reference ships the density mosaic its CUDA build wrote after training on data/nerf/test2/images
+    (images.density_slices_256x256x256.png; the data path in the name is the scene's).  base.json trained 35k steps
+    on the same scene (quarter resolution, tools/make_real_data.py) with two seeds, compared at the scale the scene
+    determines -- it is a flame animated over the 300 frames in front of an opaque black background, so no two
+    trainings agree voxel by voxel (seed vs seed IoU of the >= 2.5 raw-density masks 0.29-0.40, this build vs the
+    reference 0.11-0.14; profiles/r05_density_slices.json) -- through the 32^3 grid of per-block occupied fractions:
+      * the reference's field correlates with ours best in the identity frame among the 48 axis permutations / flips
+        (measured first for every pair of four seeds): same world axes, same placement in the render aabb;
+      * that correlation is positive (0.11-0.18 measured) and the two seeds agree with each other (0.44-0.70);
+      * the occupied volume is of the reference's order (ours 17-31 %, the reference's 13.3 %).
+    The other mosaic (data/nerf/test.density_slices_...) names the data path data/nerf/test, not test/dataset where the
+    fire scene now sits, and matches no orientation of fields trained on it: it is not compared."""
+    import density_slices_util as D
+    import pyngp as ngp
+    ref = D.reference_volume("test2") >= 129
+    occ = {}
+    for seed in (1337, 42):
+        tb = D.new_testbed(ngp, "test2", "base.json", seed)
+        D.train_to(tb, 35000)
+        occ[seed] = D.testbed_volume(tb) >= 129
+        del tb
+    ours = (D.coarse(occ[1337]) + D.coarse(occ[42])) / 2
+    cref = D.coarse(ref)
+    ident, rank = D.orientation_ranking(ours, cref)
+    seeds_corr = float(np.corrcoef(D.coarse(occ[1337]).ravel(), D.coarse(occ[42]).ravel())[0, 1])
+    ratio = float(ours.mean() / cref.mean())
+    print(f"test2: corr vs reference {ident:.3f} (rank {rank} of 48), seed vs seed {seeds_corr:.3f}, occupied ratio {ratio:.2f}, "
+          f"IoU vs reference {[round(D.compare(o.astype(np.uint8) * 200, ref.astype(np.uint8) * 200)['iou'], 3) for o in occ.values()]}")
+    assert rank == 0, (ident, rank)
+    assert ident > 0.05
+    assert seeds_corr > 0.3
+    assert 0.5 < ratio < 3.0

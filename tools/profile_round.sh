@@ -1,13 +1,17 @@
 #!/bin/bash
 # Round profile set: bench line, kernel-trace stats, FETCH_SIZE calibration, PMC HBM traffic
 # (separate FETCH / WRITE passes), MFMA counters.  Usage (GPU box, repo root): tools/profile_round.sh r02
+# Extra bench.py arguments (e.g. the surface scene: BENCH_EXTRA="--scene synthetic") come from $BENCH_EXTRA;
+# SKIP_CALIB=1 reuses an existing FETCH calibration (gpurun_out/fetch_calib/fetch_calib.json).
 R=${1:-r02}
 OUT=$PWD/gpurun_out/prof_$R
 mkdir -p "$OUT"
 REPO=$PWD
 export TMPDIR=/tmp
-STEPS="--steps 10 --warmup 3 --pretrain 1500 --cpu-baseline 0 --surface-scene 0 --render-to-cpu 0"
-tools/fetch_calib.sh > "$OUT/fetch_calib.log" 2>&1 || exit $?
+STEPS="--steps 10 --warmup 3 --pretrain 1500 --cpu-baseline 0 --surface-scene 0 --config-e 0 --render-in-hbm 0 $BENCH_EXTRA"
+if [ "${SKIP_CALIB:-0}" != 1 ] || [ ! -f gpurun_out/fetch_calib/fetch_calib.json ]; then
+  tools/fetch_calib.sh > "$OUT/fetch_calib.log" 2>&1 || exit $?
+fi
 cp gpurun_out/fetch_calib/fetch_calib.json "$OUT/fetch_calib.json"
 cd /tmp
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d "$OUT/kt" -o run -- \
