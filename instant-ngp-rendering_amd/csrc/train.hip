@@ -710,22 +710,40 @@ struct LossArgs {
 	uint32_t max_mip;
 };
 
-// Wave scans over the 64 lanes (inclusive).
-__device__ __forceinline__ float wave_scan_add(float v, uint32_t lane) {
+// Scans over the G lanes of a ray's group (inclusive; G = 64: the whole wave).  Lane r of a group takes the
+// same sequence of operations for every G > its rank, so a ray whose samples fit one group gets the same bits
+// whatever G is.
+template <uint32_t G>
+__device__ __forceinline__ float group_scan_add(float v, uint32_t r) {
 #pragma unroll
-	for (uint32_t off = 1; off < 64; off <<= 1) {
-		const float t = __shfl_up(v, off, 64);
-		if (lane >= off) v += t;
+	for (uint32_t off = 1; off < G; off <<= 1) {
+		const float t = __shfl_up(v, off, G);
+		if (r >= off) v += t;
 	}
 	return v;
 }
-__device__ __forceinline__ float wave_scan_mul(float v, uint32_t lane) {
+template <uint32_t G>
+__device__ __forceinline__ float group_scan_mul(float v, uint32_t r) {
 #pragma unroll
-	for (uint32_t off = 1; off < 64; off <<= 1) {
-		const float t = __shfl_up(v, off, 64);
-		if (lane >= off) v *= t;
+	for (uint32_t off = 1; off < G; off <<= 1) {
+		const float t = __shfl_up(v, off, G);
+		if (r >= off) v *= t;
 	}
 	return v;
+}
+// the ballot bits of the lane's group, shifted to bit 0
+template <uint32_t G>
+__device__ __forceinline__ unsigned long long group_ballot(bool p, uint32_t lane) {
+	const unsigned long long b = __ballot(p);
+	return G == 64 ? b : (b >> (lane & ~(G - 1u))) & ((1ull << G) - 1ull);
+}
+
+// The loss kernels' lanes per ray: the average kept samples per ray of the global batch (target_batch /
+// n_rays_global, the same on every data-parallel rank and in one process with the whole batch), rounded up to
+// the group that holds 1.5x it -- 16 for a surface scene's ~8, 64 for a volume's ~100.
+inline uint32_t loss_lanes_per_ray(uint32_t target_batch, uint32_t n_rays_global) {
+	const float avg = 1.5f * (float)target_batch / (float)std::max(n_rays_global, 1u);
+	return avg <= 8.0f ? 8u : avg <= 16.0f ? 16u : avg <= 32.0f ? 32u : 64u;
 }
 
 // One compacted-batch sample as the compositor sees it.
@@ -772,18 +790,18 @@ __device__ __forceinline__ float unnormalized_dir_length(const ngp_image& im, fl
 	return length(dir);
 }
 
-// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1160), pass 1: one wave per ray,
-// 64 samples per iteration.  Transmittance T_j = prod_{i<j}(1 - alpha_i) comes from a
-// multiplicative wave scan, the colour from an additive one; the ray stops at the first
+// compute_loss_kernel_train_nerf (testbed_nerf.cu:841-1160), pass 1: G lanes per ray (loss_lanes_per_ray),
+// G samples per iteration.  Transmittance T_j = prod_{i<j}(1 - alpha_i) comes from a
+// multiplicative group scan, the colour from an additive one; the ray stops at the first
 // sample with T_j < 1e-4 (the reference's sequential test), found with a ballot.
-template <bool GENERAL>
+template <bool GENERAL, uint32_t G>
 __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
-	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
-	const uint32_t lane = threadIdx.x & 63u;
-	if (i >= a.n_rays) return;  // wave-uniform
+	const uint32_t i = blockIdx.x * (256u / G) + threadIdx.x / G;
+	const uint32_t lane = threadIdx.x & 63u, r = threadIdx.x % G;
+	if (i >= a.n_rays) return;  // group-uniform
 	const uint32_t numsteps = a.numsteps[2 * i + 0], base = a.numsteps[2 * i + 1];
 	if (numsteps == 0) {
-		if (lane == 0) a.ccounts[i] = 0;
+		if (r == 0) a.ccounts[i] = 0;
 		return;
 	}
 	float T = 1.0f;
@@ -796,31 +814,31 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 	uint32_t c = numsteps;
 	// the chunked forward evaluated at least every sample before this ray's stop
 	const uint32_t evaluated = a.ray_eval ? (a.ray_eval[i] & ~RAY_EVAL_DONE) : numsteps;
-	for (uint32_t kb = 0; kb < numsteps; kb += 64) {
-		const uint32_t j = kb + lane;
+	for (uint32_t kb = 0; kb < numsteps; kb += G) {
+		const uint32_t j = kb + r;
 		const bool active = j < numsteps;
 		LossSample q;
 		if (active && j < evaluated) q = loss_sample(a, (size_t)base + j);
 		else { q.alpha = 0.0f; q.rgb = mk3(0.0f); }
-		const float incl = wave_scan_mul(1.0f - q.alpha, lane);
-		float excl = __shfl_up(incl, 1, 64);
-		if (lane == 0) excl = 1.0f;
+		const float incl = group_scan_mul<G>(1.0f - q.alpha, r);
+		float excl = __shfl_up(incl, 1, G);
+		if (r == 0) excl = 1.0f;
 		const float Tj = T * excl;
-		const unsigned long long term = __ballot(active && Tj < 1e-4f);
+		const unsigned long long term = group_ballot<G>(active && Tj < 1e-4f, lane);
 		const uint32_t first = term ? (uint32_t)(__ffsll((long long)term) - 1) : 64u;
-		const float w = (active && lane < first) ? q.alpha * Tj : 0.0f;
-		rgb_ray.x += __shfl(wave_scan_add(q.rgb.x * w, lane), 63, 64);
-		rgb_ray.y += __shfl(wave_scan_add(q.rgb.y * w, lane), 63, 64);
-		rgb_ray.z += __shfl(wave_scan_add(q.rgb.z * w, lane), 63, 64);
+		const float w = (active && r < first) ? q.alpha * Tj : 0.0f;
+		rgb_ray.x += __shfl(group_scan_add<G>(q.rgb.x * w, r), G - 1, G);
+		rgb_ray.y += __shfl(group_scan_add<G>(q.rgb.y * w, r), G - 1, G);
+		rgb_ray.z += __shfl(group_scan_add<G>(q.rgb.z * w, r), G - 1, G);
 		if (a.sharp_data) {
 			v3 wp = mk3(0.0f);
 			if (w != 0.0f) {
 				const size_t src = (size_t)base + j;
 				wp = unwarp_position(mk3(a.coords[8 * src], a.coords[8 * src + 1], a.coords[8 * src + 2]), a.aabb) * w;
 			}
-			hit.x += __shfl(wave_scan_add(wp.x, lane), 63, 64);
-			hit.y += __shfl(wave_scan_add(wp.y, lane), 63, 64);
-			hit.z += __shfl(wave_scan_add(wp.z, lane), 63, 64);
+			hit.x += __shfl(group_scan_add<G>(wp.x, r), G - 1, G);
+			hit.y += __shfl(group_scan_add<G>(wp.y, r), G - 1, G);
+			hit.z += __shfl(group_scan_add<G>(wp.z, r), G - 1, G);
 		}
 		if (depth_on) {
 			float wd = 0.0f;
@@ -829,16 +847,16 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 				const v3 pos = unwarp_position(mk3(a.coords[8 * src], a.coords[8 * src + 1], a.coords[8 * src + 2]), a.aabb);
 				wd = w * length(pos - ray_o);
 			}
-			depth_ray += __shfl(wave_scan_add(wd, lane), 63, 64);
+			depth_ray += __shfl(group_scan_add<G>(wd, r), G - 1, G);
 		}
 		if (term) {
 			c = kb + first;
 			break;
 		}
-		T *= __shfl(incl, 63, 64);
+		T *= __shfl(incl, G - 1, G);
 	}
 	// runtime guard of the chunked forward: every sample before the stop must have been evaluated
-	if (lane == 0 && a.ray_eval && evaluated < c) atomicAdd(a.violations, 1u);
+	if (r == 0 && a.ray_eval && evaluated < c) atomicAdd(a.violations, 1u);
 
 	// Same RNG stream as the sampler -> same pixel and background colour (testbed_nerf.cu:938-955).
 	const uint32_t gi = a.ray_offset + i;
@@ -883,7 +901,7 @@ __global__ void __launch_bounds__(256) k_loss_composite(LossArgs a) {
 		}
 	}
 	if (c == numsteps) rgb_ray = rgb_ray + bg * T;
-	if (lane != 0) return;
+	if (r != 0) return;
 	float lx, ly, lz, gx, gy, gz;
 	loss_and_gradient(target.x, rgb_ray.x, a.loss_type, &lx, &gx);
 	loss_and_gradient(target.y, rgb_ray.y, a.loss_type, &ly, &gy);
@@ -946,12 +964,13 @@ __global__ void __launch_bounds__(256) k_img_fix_flush(uint32_t n, uint32_t stri
 	if (v) dst[i] += (float)((double)v * (1.0 / IMG_FIXED_SCALE));
 }
 
-// pass 2: recomposite the kept samples of the ray (one wave, 64 per iteration) and write
+// pass 2: recomposite the kept samples of the ray (G lanes, G per iteration) and write
 // dL/d(raw network output) with the suffix trick (testbed_nerf.cu:1061-1119) plus the
 // compacted-slot -> source-sample map; consecutive lanes write consecutive slots.
+template <uint32_t G>
 __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
-	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
-	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t i = blockIdx.x * (256u / G) + threadIdx.x / G;
+	const uint32_t lane = threadIdx.x % G;  // the lane's rank in the ray's group
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.ccounts[i], cbase = a.cbases[i];
 	const uint32_t mc = a.max_compacted_dev ? *a.max_compacted_dev : a.max_compacted;
@@ -1030,20 +1049,20 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 	// depth supervision: the ray's composited depth and lambda * dloss/ddepth (0: no term)
 	const float2 rdep = a.depth_lambda > 0.0f ? a.ray_depth[i] : make_float2(0.0f, 0.0f);
 	float dacc = 0.0f;
-	for (uint32_t kb = 0; kb < cn; kb += 64) {
+	for (uint32_t kb = 0; kb < cn; kb += G) {
 		const uint32_t j = kb + lane;
 		const bool active = j < cn;
 		const size_t src = (size_t)base + j, dst = (size_t)cbase + j;
 		LossSample q;
 		if (active) q = loss_sample(a, src);
 		else { q.alpha = 0.0f; q.rgb = mk3(0.0f); q.dt = 0.0f; q.raw[0] = q.raw[1] = q.raw[2] = q.raw[3] = 0.0f; }
-		const float incl = wave_scan_mul(1.0f - q.alpha, lane);
-		float excl = __shfl_up(incl, 1, 64);
+		const float incl = group_scan_mul<G>(1.0f - q.alpha, lane);
+		float excl = __shfl_up(incl, 1, G);
 		if (lane == 0) excl = 1.0f;
 		const float Tj = T * excl, Tnext = T * incl;
 		const float weight = q.alpha * Tj;
-		const v3 pre = mk3(wave_scan_add(q.rgb.x * weight, lane), wave_scan_add(q.rgb.y * weight, lane),
-		                   wave_scan_add(q.rgb.z * weight, lane));
+		const v3 pre = mk3(group_scan_add<G>(q.rgb.x * weight, lane), group_scan_add<G>(q.rgb.y * weight, lane),
+		                   group_scan_add<G>(q.rgb.z * weight, lane));
 		const v3 rgb_ray2 = acc + pre;
 		float depth = 0.0f;
 		if (active) {
@@ -1051,7 +1070,7 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 			depth = length(unwarp_position(mk3(c0.x, c0.y, c0.z), a.aabb) - ray_o);
 		}
 		// depth supervision: inclusive prefix of weight x depth over the ray's samples (depth_ray2)
-		const float dpre = rdep.y != 0.0f ? wave_scan_add(weight * depth, lane) : 0.0f;
+		const float dpre = rdep.y != 0.0f ? group_scan_add<G>(weight * depth, lane) : 0.0f;
 		if (active) {
 			a.csrc[dst] = (uint32_t)src;
 			const v3 suffix = rgb_ray - rgb_ray2;
@@ -1070,9 +1089,9 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 			                     (o3 > -10.0f && depth < a.near_distance ? 1e-4f : 0.0f));
 			*reinterpret_cast<uint2*>(a.dloss + 4 * dst) = *reinterpret_cast<const uint2*>(dl);
 		}
-		acc = acc + mk3(__shfl(pre.x, 63, 64), __shfl(pre.y, 63, 64), __shfl(pre.z, 63, 64));
-		if (rdep.y != 0.0f) dacc += __shfl(dpre, 63, 64);
-		T *= __shfl(incl, 63, 64);
+		acc = acc + mk3(__shfl(pre.x, G - 1, G), __shfl(pre.y, G - 1, G), __shfl(pre.z, G - 1, G));
+		if (rdep.y != 0.0f) dacc += __shfl(dpre, G - 1, G);
+		T *= __shfl(incl, G - 1, G);
 	}
 }
 
@@ -1971,8 +1990,19 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		la.ray_depth = reinterpret_cast<float2*>(ts.ray_depth.ptr);
 	}
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);
-	if (general) k_loss_composite<true><<<div_up(R, 4), 256, 0, s>>>(la);
-	else k_loss_composite<false><<<div_up(R, 4), 256, 0, s>>>(la);
+	const uint32_t LG = loss_lanes_per_ray(t->target_batch_size, la.n_rays_global);
+#define NGP_LOSS(GG)                                                                       \
+	do {                                                                                   \
+		if (general) k_loss_composite<true, GG><<<div_up(R, 256u / GG), 256, 0, s>>>(la);  \
+		else k_loss_composite<false, GG><<<div_up(R, 256u / GG), 256, 0, s>>>(la);         \
+	} while (0)
+	switch (LG) {
+		case 8: NGP_LOSS(8); break;
+		case 16: NGP_LOSS(16); break;
+		case 32: NGP_LOSS(32); break;
+		default: NGP_LOSS(64); break;
+	}
+#undef NGP_LOSS
 	launch_exclusive_scan(la.ccounts, la.cbases, R, ts.block_sums.ptr, ts.counters.ptr + 1, s);
 	// the global compaction cap (src/testbed_nerf.cu:997-1003) over all ranks, and the chunked forward's
 	// violations summed over the ranks: every rank skips the step's deposits when any rank saw one
@@ -1986,7 +2016,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	if (la.sharp_grid && !t->sharpness_grid_clear)  // train_nerf's decay by 0.95 (src/testbed_nerf.cu:2453-2464)
 		k_scale_floats<<<div_up((size_t)NERF_GRID_N_CELLS * NERF_CASCADES, 256), 256, 0, s>>>(
 		    la.sharp_grid, (size_t)NERF_GRID_N_CELLS * NERF_CASCADES, 0.95f, la.viol_gate);
-	k_loss_emit<<<div_up(R, 4), 256, 0, s>>>(la);
+	switch (LG) {
+		case 8: k_loss_emit<8><<<div_up(R, 32u), 256, 0, s>>>(la); break;
+		case 16: k_loss_emit<16><<<div_up(R, 16u), 256, 0, s>>>(la); break;
+		case 32: k_loss_emit<32><<<div_up(R, 8u), 256, 0, s>>>(la); break;
+		default: k_loss_emit<64><<<div_up(R, 4u), 256, 0, s>>>(la); break;
+	}
 	NGP_HIP_CHECK(hipGetLastError());
 	const bool train_debug = (m->tuning.debug & 2u) != 0;
 	if (train_debug) {
