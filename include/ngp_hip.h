@@ -334,6 +334,19 @@ typedef struct ngp_render_args {
 	/* n_extra_dims > 0: the latent code every rendered sample carries (Nerf::get_rendering_extra_dims,
 	 * src/testbed_nerf.cu:3206-3228): device fp32 [16], zero past n_extra_dims; null = zeros; 16-byte aligned */
 	const float* extra_dims;
+	/* optional (render(): one spp, Shade mode without glow, unsharded): the frame's tonemapped pixels streamed into
+	 * caller-owned page-locked host memory [H][W][4] by the kernels that finish their rays, while the march goes
+	 * on -- the value ngp_accumulate_tonemap(frame, accum, out, W, H, 0, host_color_space, host_exposure,
+	 * host_background, host_output_srgb) leaves in `out`, bit for bit, without the read-back after the frame
+	 * (render_to_cpu's copy, src/python_api.cu:124-202).  *host_frame_complete (host memory) is set to 1 when every
+	 * pixel was written, 0 when some rays ran out of march iterations (k_retire) and the caller copies the frame
+	 * instead.  null = off. */
+	float* host_frame;
+	int32_t* host_frame_complete;
+	float host_background[4];
+	float host_exposure;
+	int32_t host_color_space;
+	int32_t host_output_srgb;
 } ngp_render_args;
 
 /* ngp_render_args.render_mode (the reference's ERenderMode; Distortion and EncodingVis are GUI
@@ -380,6 +393,10 @@ typedef struct ngp_tuning {
 	                                    by k_generate), 2 = computes every reserved slot; 0: the default (1) */
 	uint32_t render_exit_cap;        /* 1 = a ray reserves at most the lattice points left to its AABB exit in a march
 	                                    pass, 2 = the per-ray cap alone; 0: the default */
+	uint32_t render_priority;        /* wave issue priority (s_setprio 0..3) of the render kernels sharing the CUs:
+	                                    bits 0-1 the encoder, 2-3 the MLP, 4-5 the march kernels; 0: all 0 */
+	uint32_t render_host_frame;      /* Testbed::render into host memory: 1 = pixels streamed by the kernels
+	                                    (ngp_render_args.host_frame), 2 = tonemap then one read-back; 0: the default */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

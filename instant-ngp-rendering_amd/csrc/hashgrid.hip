@@ -61,6 +61,7 @@ __global__ void __launch_bounds__(256) k_hashgrid_fwd(uint32_t n, const float* _
                                                       const __half* __restrict__ table, const LevelTable lt,
                                                       __half* __restrict__ enc, EncLayout lay, uint32_t n_chunks,
                                                       const uint32_t* __restrict__ n_dev) {
+	if (SITE == 1) set_wave_priority(lt.prio);
 	uint32_t grp, chunk0 = 0;
 	const uint32_t groups = lt.n_levels / LPT;
 	if (n_dev) n = min(n, *n_dev);

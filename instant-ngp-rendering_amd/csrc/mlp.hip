@@ -160,6 +160,7 @@ struct MlpArgs {
 	float* partials;                  // k_mlp_train: [workgroup][n_mlp_params] weight-gradient partials
 	uint32_t n_mlp;                   // MLP parameter count (partials row pitch)
 	uint32_t skip_unfilled;           // SH-row inference: skip column tiles whose rows are all NO_SH_ROW
+	uint32_t prio;                    // SH-row inference (renderer): wave issue priority (ngp_tuning.render_priority bits 2-3)
 	// Net::XE (n_extra_dims > 0): the latent codes, fp32 rows of 16 (zero past n_extra_dims); sample i reads row
 	// sample_img[i] (training: the sample's image), or row 0 without sample_img (rendering: the rendering code)
 	const float* extra;
@@ -593,6 +594,7 @@ template <class N, int CT_, int PF, bool DENSITY_ONLY, int FF, bool SHIN = false
 __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	static_assert(N::KE <= 2 && N::Wp <= 64, "register layout assumes <= 2 K-steps per layer");
 	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	if constexpr (SHIN) set_wave_priority(a.prio);
 	constexpr int NF = DENSITY_ONLY ? N::fwd_frags_upto(N::DH + 1) : N::fwd_frags();
 	extern __shared__ __attribute__((aligned(16))) char smem[];
 	h8* w = reinterpret_cast<h8*>(smem);  // [frag][lane]
@@ -1206,6 +1208,7 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 	a.out_mode = out_mode;
 	a.out_stride = out_stride;
 	a.skip_unfilled = skip_unfilled && sh_ray && out_mode == 0;
+	a.prio = sh_ray ? (m->tuning.render_priority >> 2) & 3u : 0u;
 	a.extra = x.extra ? x.extra : m->zero_extra.ptr;
 	a.sample_img = x.extra ? x.sample_img : nullptr;
 	NGP_DISPATCH(m->mlp_variant, {

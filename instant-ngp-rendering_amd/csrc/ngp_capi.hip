@@ -83,6 +83,8 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->encode_xcd_regions <= 1, "encode_xcd_regions must be 0 or 1");
 	require(t->render_skip_unfilled <= 2, "render_skip_unfilled must be 0, 1 or 2");
 	require(t->render_exit_cap <= 2, "render_exit_cap must be 0, 1 or 2");
+	require(t->render_priority < 64, "render_priority must be < 64 (three 2-bit priorities)");
+	require(t->render_host_frame <= 2, "render_host_frame must be 0, 1 or 2");
 }
 
 // tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.

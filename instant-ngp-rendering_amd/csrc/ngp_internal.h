@@ -156,6 +156,8 @@ struct LevelTable {
 	// 1: each XCD encodes a contiguous eighth of the chunks, level group by level group (four levels per
 	// thread; ngp_tuning.encode_xcd_regions = 0); 0: XCD x takes every eighth chunk
 	uint32_t regions = 0;
+	// wave issue priority of the encoder's waves (s_setprio; ngp_tuning.render_priority bits 0-1, render site)
+	uint32_t prio = 0;
 	__host__ __device__ bool level_cut(uint32_t level, uint32_t i) const {
 		if (!max_level) return false;
 		// tcnn: max_level = (max_level_gpu[i] * num_grid_features) / N_FEATURES_PER_LEVEL; level >= max_level + 1e-3f
@@ -300,6 +302,13 @@ struct TrainScratch {
 	uint32_t rank_cap_hint = 0;
 };
 
+// s_setprio takes an immediate: the wave's issue priority from a kernel argument (0..3)
+__device__ __forceinline__ void set_wave_priority(uint32_t p) {
+	if (p == 1) __builtin_amdgcn_s_setprio(1);
+	else if (p == 2) __builtin_amdgcn_s_setprio(2);
+	else if (p >= 3) __builtin_amdgcn_s_setprio(3);
+}
+
 constexpr uint32_t IMG_FIX_STRIDE = 25;
 
 struct GridState {
@@ -359,6 +368,11 @@ struct RenderScratch {
 	DevBuf<uint8_t> df_x, df_xy;  // separable passes: [mip][2][N], [mip][4][N]
 	DevBuf<float> slice_coords;   // Slice mode: [pixels][8] NerfCoordinate rows (pos.x NaN: no ray)
 	DevBuf<__half> slice_enc, slice_out;
+	// streamed host frame (ngp_render_args.host_frame): pixels whose ray never marched (1 per pixel, k_render_init),
+	// written to the host by k_host_background on its own stream while the passes run
+	DevBuf<uint8_t> hmask;
+	hipStream_t host_stream = nullptr;
+	hipEvent_t host_ev[MAX_PIPES] = {}, host_join = nullptr;
 	uint64_t df_version = ~0ull;
 	uint32_t df_max_mip = ~0u;
 	size_t cap = 0;
@@ -367,7 +381,13 @@ struct RenderScratch {
 	void release() {
 		for (auto& p : pipe) p.release();
 		dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();
-		slice_coords.release(); slice_enc.release(); slice_out.release();
+		slice_coords.release(); slice_enc.release(); slice_out.release(); hmask.release();
+		for (auto& e : host_ev)
+			if (e) (void)hipEventDestroy(e), e = nullptr;
+		if (host_join) (void)hipEventDestroy(host_join);
+		host_join = nullptr;
+		if (host_stream) (void)hipStreamDestroy(host_stream);
+		host_stream = nullptr;
 		if (fork) (void)hipEventDestroy(fork);
 		fork = nullptr;
 		for (int j = 0; j < MAX_PIPES; ++j) {

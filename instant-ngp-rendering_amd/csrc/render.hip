@@ -31,6 +31,7 @@ constexpr uint32_t PAYLOAD_EXITED = 0x80000000u;
 static_assert(sizeof(Payload) == 48, "payload layout");
 
 struct RenderK {
+	uint32_t prio;  // wave issue priority of the march kernels (ngp_tuning.render_priority bits 4-5)
 	uint32_t W, H;
 	uint32_t sample_index;
 	m43 cam;
@@ -69,7 +70,61 @@ struct RenderK {
 	int exit_cap;             // a ray's per-pass budget is capped by the lattice points left to its exit
 	int glow_mode;            // Nerf::glow_mode (composite_kernel_nerf's glow; 0 = off)
 	float glow_y_cutoff;
+	// ngp_render_args.host_frame (device-mapped), with the tonemap's parameters: finished rays' pixels go straight to it
+	float4* hframe;
+	uint8_t* hmask;  // [W * H]: 1 = the pixel's ray never marched (its background pixel is written by k_host_background)
+	float4 hbg;
+	float hexposure;
+	int hcolor_space, hsrgb;
 };
+
+// tonemap_kernel's per-pixel body (render_buffer.cu:533-565) after the accumulation: background, exposure, sRGB
+__device__ __forceinline__ float4 tonemap_pixel(float4 c, int color_space, float exposure, float4 bg, int output_srgb) {
+	if (color_space != 1) {
+		bg.x = srgb_to_linear(bg.x);
+		bg.y = srgb_to_linear(bg.y);
+		bg.z = srgb_to_linear(bg.z);
+	}
+	const float weight = (1.0f - c.w) * bg.w;
+	c.x += bg.x * weight;
+	c.y += bg.y * weight;
+	c.z += bg.z * weight;
+	c.w += weight;
+	if (color_space == 1) {
+		c.x = srgb_to_linear(c.x);
+		c.y = srgb_to_linear(c.y);
+		c.z = srgb_to_linear(c.z);
+	}
+	const float e = powf(2.0f, exposure);
+	c.x *= e;
+	c.y *= e;
+	c.z *= e;
+	if (output_srgb) {
+		c.x = linear_to_srgb(c.x);
+		c.y = linear_to_srgb(c.y);
+		c.z = linear_to_srgb(c.z);
+	}
+	return c;
+}
+
+// The finished pixel as render() returns it for one spp: shade_kernel_nerf's Shade colour over the cleared frame
+// (t + 0 * (1 - t.w) = t), accumulate_kernel's first sample ((0 * 0 + c) / (0 + 1) = c, after linear_to_srgb in an
+// sRGB buffer), then tonemap_pixel -- the arithmetic of k_shade + k_accum_tonemap, so the bits agree.  hit: the ray
+// composited colour (c.w > 0.001); otherwise the pixel stays cleared.
+__device__ __forceinline__ void write_host_pixel(const RenderK& k, uint32_t idx, float4 c, bool hit) {
+	float4 t = hit ? c : make_float4(0.f, 0.f, 0.f, 0.f);
+	if (hit && !k.linear_colors) {
+		t.x = srgb_to_linear(t.x);
+		t.y = srgb_to_linear(t.y);
+		t.z = srgb_to_linear(t.z);
+	}
+	if (k.hcolor_space == 1) {
+		t.x = linear_to_srgb(t.x);
+		t.y = linear_to_srgb(t.y);
+		t.z = linear_to_srgb(t.z);
+	}
+	k.hframe[idx] = tonemap_pixel(t, k.hcolor_space, k.hexposure, k.hbg, k.hsrgb);
+}
 
 // square2disk_shirley (random_val.cuh:112-128)
 __device__ __forceinline__ void square2disk_shirley(float a, float b, float* x, float* y) {
@@ -218,7 +273,12 @@ __global__ void __launch_bounds__(256) k_render_init(RenderK k, Payload* __restr
 	const uint32_t tile = r >> 6, x = (tile % k.tiles_x) * 8u + (r & 7u), yl = (tile / k.tiles_x) * 8u + ((r >> 3) & 7u);
 	Payload p;
 	bool alive = false;
-	if (x < k.W && yl < k.h_local) alive = init_ray_body<LENS>(k, x, yl, &p, frame, depth_buffer);
+	const bool inside = x < k.W && yl < k.h_local;
+	if (inside) alive = init_ray_body<LENS>(k, x, yl, &p, frame, depth_buffer);
+	// the pixels of rays that never march are written to the host by k_host_background on a side stream, spread
+	// over the frame's passes (written here, a frame's background pixels were a burst of PCIe stores that held
+	// this launch up)
+	if (k.hframe && inside) k.hmask[p.idx] = alive ? 0 : 1;
 	uint32_t slot, unused;
 	block_append2(alive, false, &counters[0], &counters[3], &slot, &unused);
 	if (alive) {
@@ -444,6 +504,14 @@ __global__ void __launch_bounds__(256) k_retire(uint32_t n, const Payload* __res
 	}
 }
 
+// The background pixels of a streamed host frame (rays that never marched: k_render_init's mask), on a side
+// stream concurrent with the march passes; a modest grid (grid-stride) so it takes few CU slots.
+__global__ void __launch_bounds__(256) k_host_background(RenderK k, uint32_t n) {
+	const float4 bgpix = make_float4(0.f, 0.f, 0.f, 0.f);
+	for (uint32_t i = blockIdx.x * 256u + threadIdx.x; i < n; i += gridDim.x * 256u)
+		if (k.hmask[i]) write_host_pixel(k, i, bgpix, false);
+}
+
 // Publishes the tracer's counters [0, 8) of the previous pass to pinned host memory, so the
 // host learns a pass's sizes by polling instead of enqueueing a copy and an event after
 // every pass (each costs a queue drain).  Called by the first 8 threads of the first
@@ -501,6 +569,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
                                                   uint32_t* __restrict__ next_alive_counter,
                                                   uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
                                                   const uint32_t* counters, unsigned long long* host_prev, uint32_t tag_prev) {
+	set_wave_priority(k.prio);
 	// the previous pass's counters, before this block zeroes next_alive_counter / steps_out
 	if (host_prev && blockIdx.x == 0 && threadIdx.x < 8) publish_counters(counters, host_prev, tag_prev);
 	__syncthreads();
@@ -663,6 +732,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
                                                    uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter,
                                                    uint32_t* __restrict__ next_sample_counter,
                                                    uint32_t* __restrict__ filled_counter) {
+	set_wave_priority(k.prio);
 	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
 	const uint32_t n_alive = *alive_in;
 	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -770,6 +840,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		if (done || (p.n_steps & PAYLOAD_EXITED)) alive = false;
 	}
 	const bool hit = i < n_alive && !alive && c.w > 0.001f;
+	if (!MODES && k.hframe && i < n_alive && !alive) write_host_pixel(k, p.idx, c, hit);
 	// samples the rays actually filled this pass (reserved slots past an exit are not counted):
 	// the frame's network-evaluated sample count for the roofline
 	block_add(filled, filled_counter);
@@ -853,32 +924,7 @@ __global__ void __launch_bounds__(256) k_accum_tonemap(uint32_t W, uint32_t H, c
 	tmp.w = (tmp.w * sample_count + color.w) / (sample_count + 1.0f);
 	accum[i] = tmp;
 	if (!out) return;
-	if (color_space != 1) {
-		bg.x = srgb_to_linear(bg.x);
-		bg.y = srgb_to_linear(bg.y);
-		bg.z = srgb_to_linear(bg.z);
-	}
-	float4 c = tmp;
-	const float weight = (1.0f - c.w) * bg.w;
-	c.x += bg.x * weight;
-	c.y += bg.y * weight;
-	c.z += bg.z * weight;
-	c.w += weight;
-	if (color_space == 1) {
-		c.x = srgb_to_linear(c.x);
-		c.y = srgb_to_linear(c.y);
-		c.z = srgb_to_linear(c.z);
-	}
-	const float e = powf(2.0f, exposure);
-	c.x *= e;
-	c.y *= e;
-	c.z *= e;
-	if (output_srgb) {
-		c.x = linear_to_srgb(c.x);
-		c.y = linear_to_srgb(c.y);
-		c.z = linear_to_srgb(c.z);
-	}
-	out[i] = c;
+	out[i] = tonemap_pixel(tmp, color_space, exposure, bg, output_srgb);
 }
 
 static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t rows) {
@@ -1011,6 +1057,22 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	if (a->render_mode < NGP_RENDER_MODE_SHADE || a->render_mode > NGP_RENDER_MODE_SLICE)
 		throw std::invalid_argument("render_mode must be one of NGP_RENDER_MODE_* (Distortion / EncodingVis are not supported)");
 	k.mode = a->render_mode;
+	k.prio = (m->tuning.render_priority >> 4) & 3u;
+	if (a->host_frame) {
+		if (a->render_mode != NGP_RENDER_MODE_SHADE || a->glow_mode || a->shard_count > 1 || a->sample_index != 0 ||
+		    !a->host_frame_complete)
+			throw std::invalid_argument("host_frame needs one spp of a Shade-mode unsharded frame without glow, and host_frame_complete");
+		void* dp = nullptr;
+		NGP_HIP_CHECK(hipHostGetDevicePointer(&dp, a->host_frame, 0));
+		k.hframe = reinterpret_cast<float4*>(dp);
+		k.hbg = make_float4(a->host_background[0], a->host_background[1], a->host_background[2], a->host_background[3]);
+		k.hexposure = a->host_exposure;
+		k.hcolor_space = a->host_color_space;
+		k.hsrgb = a->host_output_srgb;
+		rs.hmask.reserve((size_t)k.W * k.H);
+		k.hmask = rs.hmask.ptr;
+		*a->host_frame_complete = 1;
+	}
 	k.depth_scale = a->depth_scale;
 	k.hard_edges = a->gbuffer_hard_edges;
 	k.aperture = k.mode == NGP_RENDER_MODE_SLICE ? 0.0f : a->aperture_size;  // init_rays_with_payload_kernel_nerf:1427-1429
@@ -1147,7 +1209,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// the encoder's table, and corner records of its dense levels (read by every pipeline)
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
-	const LevelTable lt_render = build_dense_records(m, table, s);
+	LevelTable lt_render = build_dense_records(m, table, s);
+	lt_render.prio = tu.render_priority & 3u;
 	// joins the pipeline streams back to s, also when a throw leaves this function early (work the
 	// caller enqueues on s next shares the frame, dense records and scratch with them)
 	struct StreamJoin {
@@ -1187,6 +1250,21 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	}
 	tm.end(NGP_TIMER_RENDER_MARCH, s, k.W * H_shard);
 	NGP_HIP_CHECK(hipGetLastError());
+	if (k.hframe) {
+		// the background pixels stream to the host beside the passes, once every pipeline's init has run
+		if (!rs.host_stream) {
+			NGP_HIP_CHECK(hipStreamCreateWithFlags(&rs.host_stream, hipStreamNonBlocking));
+			NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.host_join, hipEventDisableTiming));
+		}
+		for (uint32_t j = 0; j < n_pipes; ++j) {
+			if (!rs.host_ev[j]) NGP_HIP_CHECK(hipEventCreateWithFlags(&rs.host_ev[j], hipEventDisableTiming));
+			NGP_HIP_CHECK(hipEventRecord(rs.host_ev[j], pipes[j].s));
+			NGP_HIP_CHECK(hipStreamWaitEvent(rs.host_stream, rs.host_ev[j], 0));
+		}
+		k_host_background<<<128, 256, 0, rs.host_stream>>>(k, k.W * k.H);
+		NGP_HIP_CHECK(hipGetLastError());
+		NGP_HIP_CHECK(hipEventRecord(rs.host_join, rs.host_stream));
+	}
 
 	// NerfTracer::trace (testbed_nerf.cu:1639-1755): generate -> infer -> composite(+compact),
 	// alive rays ping-pong between buffers 0/1, finished rays with colour append to buffer 2.
@@ -1304,6 +1382,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		tm.add_units(NGP_TIMER_RENDER_MLP, last[3]);
 		filled_total += last[3];
 		if (n_alive > 0) {
+			if (a->host_frame) *a->host_frame_complete = 0;  // their pixels were not streamed: the caller copies the frame
 			// march budget exhausted: still-alive rays are shaded with what they accumulated
 			k_retire<<<div_up(n_alive, 256), 256, 0, pr.s>>>(n_alive, pr.P(pr.cur), pr.C(pr.cur), pr.ps->depth[pr.cur].ptr,
 			                                                 pr.P(2), pr.C(2), pr.ps->depth[2].ptr, counters);
@@ -1323,6 +1402,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		NGP_HIP_CHECK(hipGetLastError());
 	}
 	joiner.join();
+	if (k.hframe) NGP_HIP_CHECK(hipStreamWaitEvent(s, rs.host_join, 0));
 	// the next frame's default pipeline count (render_pipes) follows this one's samples per ray
 	if (k.mode == NGP_RENDER_MODE_SHADE && k.W * H_shard >= (1u << 16)) rs.last_samples_per_ray = (float)filled_total / (float)(k.W * H_shard);
 	if (debug) {

@@ -2014,6 +2014,20 @@ void Testbed::render_into(float* host_dst, int width, int height, int spp, bool 
 		}
 	}
 	const float bg[4] = {background_color[0], background_color[1], background_color[2], background_color[3]};
+	// one spp of a whole Shade-mode frame into host memory: the kernels that finish the rays stream their tonemapped
+	// pixels to host_dst while the march goes on (ngp_render_args.host_frame), so no read-back follows the frame
+	// (ngp_tuning.render_host_frame 2: tonemap, then copy).  The device frame and m_out are produced as before.
+	int32_t host_complete = 0;
+	const bool stream_pixels = host_dst && std::max(spp, 1) == 1 && r.shard_count == 1 && r.render_mode == NGP_RENDER_MODE_SHADE &&
+	                           r.glow_mode == 0 && m_tuning.render_host_frame != 2;
+	if (stream_pixels) {
+		r.host_frame = host_dst;
+		r.host_frame_complete = &host_complete;
+		for (int k = 0; k < 4; ++k) r.host_background[k] = bg[k];
+		r.host_exposure = exposure;
+		r.host_color_space = (int32_t)color_space;
+		r.host_output_srgb = linear ? 0 : 1;
+	}
 	m_spp = 0;
 	for (int i = 0; i < std::max(spp, 1); ++i) {
 		r.sample_index = (uint32_t)i;
@@ -2023,7 +2037,8 @@ void Testbed::render_into(float* host_dst, int width, int height, int spp, bool 
 		                          (int)color_space, exposure, bg, linear ? 0 : 1, m_stream));
 		++m_spp;
 	}
-	if (host_dst) hk(hipMemcpyAsync(host_dst, m_out, n * 4 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "render d2h");
+	if (host_dst && !(stream_pixels && host_complete))
+		hk(hipMemcpyAsync(host_dst, m_out, n * 4 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "render d2h");
 	sync();
 	render_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
 }

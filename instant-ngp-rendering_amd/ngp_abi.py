@@ -115,6 +115,8 @@ class RenderArgs(C.Structure):
         ("gbuffer_hard_edges", C.c_int32), ("aperture_size", C.c_float), ("focus_z", C.c_float),
         ("glow_mode", C.c_int32), ("glow_y_cutoff", C.c_float),
         ("extra_dims", C.c_void_p),
+        ("host_frame", C.c_void_p), ("host_frame_complete", C.c_void_p), ("host_background", C.c_float * 4),
+        ("host_exposure", C.c_float), ("host_color_space", C.c_int32), ("host_output_srgb", C.c_int32),
     ]
 
 
@@ -127,6 +129,7 @@ class Tuning(C.Structure):
         ("encode_dense_records", C.c_uint32), ("mlp_workgroups_per_cu", C.c_uint32), ("debug", C.c_uint32),
         ("encode_streaming", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
         ("encode_xcd_regions", C.c_uint32), ("render_skip_unfilled", C.c_uint32), ("render_exit_cap", C.c_uint32),
+        ("render_priority", C.c_uint32), ("render_host_frame", C.c_uint32),
     ]
 
 

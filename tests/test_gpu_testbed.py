@@ -166,10 +166,51 @@ def test_render_1080p_rows_match_oracle(scene, config):
     # (every lane-per-ray width of k_generate runs in a 1080p march: 1, 4, 16 and 64) and with the render
     # MLP computing every reserved slot (default: tiles of unfilled slots skipped)
     for kw in ({"render_exit_cap": 2}, {"render_exit_cap": 1, "render_skip_unfilled": 2},
-               {"render_exit_cap": 0, "render_skip_unfilled": 0, "render_pipelines": 1}):
+               {"render_exit_cap": 0, "render_skip_unfilled": 0, "render_pipelines": 1},
+               {"render_host_frame": 2, "render_pipelines": 0}):
         tb.set_tuning(kw)
         np.testing.assert_array_equal(tb.render(W, H, 1, True), img, err_msg=str(kw))
-    tb.set_tuning({"render_pipelines": 0})
+    tb.set_tuning({"render_pipelines": 0, "render_host_frame": 0})
+
+
+@pytest.mark.parametrize("linear,color_space,bg,exposure", [(True, 0, [0.0, 0.0, 0.0, 1.0], 0.0),
+                                                            (False, 0, [0.3, 0.6, 0.9, 1.0], 0.5),
+                                                            (False, 1, [0.8, 0.2, 0.1, 0.7], -0.25)])
+def test_render_streams_tonemapped_pixels_to_host_bit_exactly(scene, linear, color_space, bg, exposure):
+    """render(): one spp of a Shade frame streams each finished ray's tonemapped pixel into the returned host array
+    from k_render_init / k_composite (ngp_render_args.host_frame) instead of a read-back after the frame; the array
+    must equal the device frame render_to_device leaves (tonemap_kernel, render_buffer.cu:533-565) and the copy path
+    (ngp_tuning.render_host_frame 2) bit for bit, for linear / sRGB output, both colour spaces, a background with
+    alpha and exposure.  Two spp, another render mode or a shard take the copy path."""
+    import ctypes as C
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("lego_L16F2.json")
+    tb.shall_train = True
+    while tb.training_step < 100:
+        tb.frame()
+    tb.background_color = bg
+    tb.exposure = exposure
+    tb.color_space = ngp.ColorSpace.SRGB if color_space == 1 else ngp.ColorSpace.Linear
+    tb.set_camera_to_training_view(2)
+    W, H = 640, 360
+    streamed = tb.render(W, H, 1, linear)
+    addr = tb.render_to_device(W, H, 1, linear)
+    tb.sync()
+    dev = np.zeros((H, W, 4), np.float32)
+    hip = C.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [C.c_void_p, C.c_void_p, C.c_size_t, C.c_int]
+    assert hip.hipMemcpy(dev.ctypes.data_as(C.c_void_p), C.c_void_p(addr), dev.nbytes, 2) == 0
+    tb.set_tuning({"render_host_frame": 2})
+    copied = tb.render(W, H, 1, linear)
+    tb.set_tuning({"render_host_frame": 0})
+    np.testing.assert_array_equal(streamed, copied)
+    np.testing.assert_array_equal(streamed[..., 3] >= 0, True)
+    assert np.abs(streamed[..., :3] - streamed[0, 0, :3]).max() > 0  # the object is in the frame
+    np.testing.assert_array_equal(streamed, dev)
+    # two spp accumulate on the device and copy
+    np.testing.assert_array_equal(tb.render(W, H, 2, linear), tb.render(W, H, 2, linear))
 
 
 def test_config_c_eight_way_row_shards_assemble_the_1080p_frame(scene):

@@ -27,6 +27,8 @@ def main():
     p.add_argument("--snapshot", default=None, help="load this snapshot if it exists, else train and save it")
     p.add_argument("--pkg", default=None, help="directory holding another build of pyngp + libngp_hip (tools/ab_build_old.sh)")
     p.add_argument("--stats", action="store_true", help="one frame per setting with the march statistics (debug bit 0)")
+    p.add_argument("--host", action="store_true", help="time render() into host memory instead of render_to_device(); a "
+                   "setting 'hbm' times render_to_device()")
     p.add_argument("--scene", default=os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"))
     a = p.parse_args()
     if a.pkg:
@@ -66,14 +68,23 @@ def main():
     for r in range(a.rounds):
         for s in a.settings:
             setting = dict(base)
-            for kv in s.split():
+            kvs = [kv for kv in s.split() if kv != "hbm"]
+            for kv in kvs:
                 k, v = kv.split("=", 1)
                 setting[k] = float(v) if k == "render_budget_scale" else int(v)
             tb.set_tuning(setting)
-            tb.render_to_device(1920, 1080, 1, True)  # warm this setting's buffers
+            host = a.host and "hbm" not in s.split()
+
+            def frame():
+                if host:
+                    img = tb.render(1920, 1080, 1, True)
+                    del img
+                else:
+                    tb.render_to_device(1920, 1080, 1, True)
+            frame()  # warm this setting's buffers
             t0 = time.perf_counter()
             for _ in range(a.frames):
-                tb.render_to_device(1920, 1080, 1, True)
+                frame()
             times[s].append((time.perf_counter() - t0) / a.frames * 1e3)
         print(f"# round {r + 1}/{a.rounds}", file=sys.stderr, flush=True)
     if a.stats:
