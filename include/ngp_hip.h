@@ -397,6 +397,8 @@ typedef struct ngp_tuning {
 	                                    bits 0-1 the encoder, 2-3 the MLP, 4-5 the march kernels; 0: all 0 */
 	uint32_t render_host_frame;      /* Testbed::render into host memory: 1 = pixels streamed by the kernels
 	                                    (ngp_render_args.host_frame), 2 = tonemap then one read-back; 0: the default */
+	uint32_t train_chunk_lanes;      /* lanes per ray of the chunked training forward's k_train_chunk (4, 8, 16, 32 or 64);
+	                                    0: 64 for batches of <= 4096 rays, else 16 */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -85,6 +85,9 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->render_exit_cap <= 2, "render_exit_cap must be 0, 1 or 2");
 	require(t->render_priority < 64, "render_priority must be < 64 (three 2-bit priorities)");
 	require(t->render_host_frame <= 2, "render_host_frame must be 0, 1 or 2");
+	require(t->train_chunk_lanes == 0 || (t->train_chunk_lanes >= 4 && t->train_chunk_lanes <= 64 &&
+	                                      (t->train_chunk_lanes & (t->train_chunk_lanes - 1)) == 0),
+	        "train_chunk_lanes must be 0 or a power of two in [4, 64]");
 }
 
 // tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.

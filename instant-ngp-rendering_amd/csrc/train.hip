@@ -2,7 +2,7 @@
 //
 //  k_sample_count / k_sample_write   generate_training_samples_nerf   src/testbed_nerf.cu:679-838
 //  k_loss_composite / k_loss_emit    compute_loss_kernel_train_nerf   src/testbed_nerf.cu:841-1160
-//  k_rollover_weight                 tcnn fill_rollover_and_rescale   src/testbed_nerf.cu:2862-2870
+//  rollover_weight (gather kernel)   tcnn fill_rollover_and_rescale   src/testbed_nerf.cu:2862-2870
 //  k_optimizer                       tcnn Ema∘ExponentialDecay∘Adam   src/testbed_nerf.cu:2502
 //
 // The reference claims output slots with global atomicAdd (numsteps_counter,
@@ -214,6 +214,8 @@ struct SamplerArgs {
 	const float* dmap;   // learned distortion map [dry][drx][2] (null: off; general instance only)
 	uint32_t drx, dry;
 	const uint8_t* df;   // octant distance fields of mip 0 (aabb_scale 1 only; null: the jump chain)
+	const uint32_t* total;   // the scan's sample total
+	uint32_t* total_capped;  // k_sample_write: min(total, cap) for the kernels after the sampler
 };
 
 // Image and pixel of global training ray gi from its pcg32 stream (already advanced to
@@ -363,12 +365,14 @@ __device__ __forceinline__ unsigned long long training_walk_batch(const LatticeP
 // through the octant distance fields -- a surface scene's rays cross most of the volume empty, one
 // voxel per jump in the chain walk.  visit(rank, k) for every sample in order (rank < cap); returns
 // the ray's sample count, capped.
+// kb: the lattice point the walk starts from (0, or the round k_sample_count saw emit the ray's first
+// sample: the walk from there is the same); *first (if set) = the start of the first emitting round.
 template <class Visit>
 __device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3 idir, float n0, uint32_t cap, uint32_t lane,
-                                            Visit visit) {
+                                            uint32_t kb, uint32_t* first, Visit visit) {
 	const uint32_t oct = ray_octant(d);
 	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
-	uint32_t kb = 0, j = 0;
+	uint32_t j = 0;
 	while (true) {  // wave-uniform: one ray per wave
 		uint32_t k = kb + lane;
 		const int st = train_step_df(&k, n0, a.st, o, d, idir, oct, a.df, a.aabb);
@@ -381,6 +385,7 @@ __device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3
 			const uint32_t r = j + __popcll(emit & below);
 			if (r < cap) visit(r, kb + lane);
 		}
+		if (first && j == 0 && emit) *first = kb;
 		j += __popcll(emit);
 		if (j >= cap) return cap;
 		if (m_exit) return j;
@@ -388,7 +393,9 @@ __device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3
 	}
 }
 
-// pass 1: count the ray's samples (<= NERF_STEPS), one wave per ray.
+// pass 1: count the ray's samples (<= NERF_STEPS), one wave per ray.  The point the walk
+// reached when it emitted its first sample goes to ray_state[8 i + 6] (overwritten by the loss
+// kernel later), so pass 2 starts there instead of crossing the empty space before it again.
 template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -396,18 +403,20 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	if (i >= a.n_rays) return;  // wave-uniform
 	v3 o, d;
 	float n0;
-	uint32_t count = 0;
+	uint32_t count = 0, first = 0;
 	if (!training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0)) {
 	} else if (a.df) {
 		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-		count = df_walk(a, o, d, idir, n0, NERF_STEPS, lane, [](uint32_t, uint32_t) {});
+		count = df_walk(a, o, d, idir, n0, NERF_STEPS, lane, 0u, &first, [](uint32_t, uint32_t) {});
 	} else {
 		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		bool exited = false;
 		for (uint32_t kb = 0, cur = 0; !exited; kb += 64, cur -= 64) {
 			if (cur >= 64u) continue;  // a jump past this whole batch
+			const uint32_t cur0 = cur;
 			const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + lane);
 			const uint32_t c = __popcll(training_walk_batch(p, lane, &cur, &exited));
+			if (count == 0 && c) first = kb | cur0;  // kb is a multiple of 64, cur0 < 64
 			if (count + c >= NERF_STEPS) {
 				count = NERF_STEPS;
 				break;
@@ -415,7 +424,10 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 			count += c;
 		}
 	}
-	if (lane == 0) a.counts[i] = count;
+	if (lane == 0) {
+		a.counts[i] = count;
+		reinterpret_cast<uint32_t*>(a.ray_state)[8 * (size_t)i + 6] = first;
+	}
 }
 
 // pass 2: same walk, each sample written at base + (its rank among the ray's samples);
@@ -424,9 +436,10 @@ template <bool GENERAL>
 __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
 	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t cap = a.max_samples_dev ? *a.max_samples_dev : a.max_samples;
+	if (i == 0 && lane == 0) *a.total_capped = min(*a.total, cap);  // (no reader in this launch)
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.counts[i], base = a.bases[i];
-	const uint32_t cap = a.max_samples_dev ? *a.max_samples_dev : a.max_samples;
 	if (n == 0 || base + n > cap) {
 		if (lane == 0) {
 			a.numsteps[2 * i + 0] = 0;
@@ -434,6 +447,8 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 		}
 		return;
 	}
+	// k_sample_count's resume point, read before lane 0 rewrites the ray's state below
+	const uint32_t first = reinterpret_cast<const uint32_t*>(a.ray_state)[8 * (size_t)i + 6];
 	v3 o, d;
 	float n0, max_level;
 	uint32_t img = 0;
@@ -448,7 +463,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	const v3 wdir = warp_direction(d);
 	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 	if (a.df) {
-		df_walk(a, o, d, idir, n0, n, lane, [&](uint32_t r, uint32_t k) {
+		df_walk(a, o, d, idir, n0, n, lane, first, nullptr, [&](uint32_t r, uint32_t k) {
 			// the chain walk's training_lattice_point for lattice point k, bit for bit
 			const float nk = n0 + (float)k;
 			const float t = step_from(a.st, nk);
@@ -466,7 +481,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
 	uint32_t j = 0;
 	bool exited = false;
-	for (uint32_t kb = 0, cur = 0; j < n && !exited; kb += 64, cur -= 64) {
+	for (uint32_t kb = first & ~63u, cur = first & 63u; j < n && !exited; kb += 64, cur -= 64) {
 		if (cur >= 64u) continue;
 		const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + lane);
 		const unsigned long long m = training_walk_batch(p, lane, &cur, &exited);
@@ -1261,17 +1276,65 @@ __global__ void __launch_bounds__(256) k_extra_gradient(uint32_t n_rays, const u
 	}
 }
 
-// Gather the compacted batch (coords + per-level features) in compacted order: one
-// thread per compacted sample, so every level plane is written by contiguous lanes.
+// Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
+// c < B is repeated floor((B-1-j)/c) more times, each copy scaled by c/B.  Data parallel (dp =
+// DpCaps of the compaction): the rank's sample j is global sample base + j of the global batch.
+__device__ __forceinline__ float rollover_weight(uint32_t j, uint32_t n, uint32_t target, const uint32_t* __restrict__ dp) {
+	const uint32_t c = dp ? dp[1] : n, g = dp ? dp[0] + j : j;
+	const uint32_t copies = (target - 1 - g) / c;
+	return 1.0f + (float)copies * ((float)c / (float)target);
+}
+
+// Sum of per-ray losses by one 256-thread workgroup, in the order of a 1024-thread two-level
+// reduction (thread t of 1024 sums v[t], v[t + 1024], ...; then a halving tree), so the result
+// does not depend on the launch.
+__device__ void block_sum_losses(const float* __restrict__ v, uint32_t n, float* __restrict__ out) {
+	__shared__ float part[1024];
+	for (uint32_t q = 0; q < 4; ++q) {
+		const uint32_t t = threadIdx.x + 256u * q;
+		float s = 0.0f;
+		for (uint32_t i = t; i < n; i += 1024) s += v[i];
+		part[t] = s;
+	}
+	__syncthreads();
+	for (uint32_t d = 512; d > 0; d >>= 1) {
+		for (uint32_t t = threadIdx.x; t < d; t += 256u) part[t] += part[t + d];
+		__syncthreads();
+	}
+	if (threadIdx.x == 0) *out = part[0];
+}
+
+struct CompactFinish {
+	const uint32_t* total;    // compacted samples (the loss kernels' count)
+	const uint32_t* cap_dev;  // data parallel: the rank's share of the cap (device); null: target
+	uint32_t* n_out;          // min(total, cap): the count the kernels after the gather read
+	const uint32_t* dp;       // DpCaps of the compaction (data parallel) or null
+	float* weight;            // [B] rollover weight per compacted sample
+	const float* loss;        // [R] per-ray losses
+	uint32_t n_rays;
+	float* loss_sum;
+};
+
+// The end of the loss stage in one launch: the compacted count, the gather of the compacted batch
+// (coords + per-level features) in compacted order -- one thread per compacted sample, so every level
+// plane is written by contiguous lanes -- with each sample's rollover weight, and, in the extra last
+// workgroup, the sum of the per-ray losses.
 template <uint32_t F>
-__global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __restrict__ n_ptr, const uint32_t* __restrict__ csrc,
+__global__ void __launch_bounds__(256) k_gather_compacted(CompactFinish cf, const uint32_t* __restrict__ csrc,
                                                           const float* __restrict__ coords, const __half* __restrict__ enc,
                                                           EncLayout src_layout, EncLayout dst_layout, uint32_t n_levels, float* __restrict__ ccoords,
                                                           float4* __restrict__ cpos4, __half* __restrict__ cenc, uint32_t target,
                                                           const uint32_t* __restrict__ eidx, const uint32_t* __restrict__ simg,
                                                           uint32_t* __restrict__ cimg) {
+	if (blockIdx.x == gridDim.x - 1) {
+		block_sum_losses(cf.loss, cf.n_rays, cf.loss_sum);
+		return;
+	}
+	const uint32_t n = min(*cf.total, cf.cap_dev ? *cf.cap_dev : target);
 	const uint32_t dst = blockIdx.x * 256u + threadIdx.x;
-	if (dst >= *n_ptr) return;
+	if (dst == 0) *cf.n_out = n;  // (no reader in this launch)
+	if (dst >= n) return;
+	cf.weight[dst] = rollover_weight(dst, n, target, cf.dp);
 	const uint32_t src = csrc[dst];
 	if (cimg) cimg[dst] = simg[src];  // n_extra_dims > 0: the sample's image (latent-code row)
 	const uint32_t esrc = eidx ? eidx[src] : src;  // row of the sample's encoding
@@ -1295,32 +1358,6 @@ __global__ void __launch_bounds__(256) k_gather_compacted(const uint32_t* __rest
 	} else {
 		for (uint32_t l = 0; l < n_levels; ++l) ed[dst_layout.vec(l, dst)] = es[src_layout.vec(l, esrc)];
 	}
-}
-
-// Rollover multiplicity (tcnn fill_rollover_and_rescale, folded): compacted sample j of
-// c < B is repeated floor((B-1-j)/c) more times, each copy scaled by c/B.  Data parallel (dp =
-// DpCaps of the compaction): the rank's sample j is global sample base + j of the global batch.
-__global__ void k_rollover_weight(const uint32_t* __restrict__ total_ptr, uint32_t target, const uint32_t* __restrict__ dp,
-                                  float* __restrict__ w) {
-	const uint32_t j = blockIdx.x * blockDim.x + threadIdx.x;
-	uint32_t c, g, n;
-	if (dp) {
-		c = dp[1];
-		g = dp[0] + j;
-		n = min(*total_ptr, dp[2]);
-	} else {
-		c = min(*total_ptr, target);
-		g = j;
-		n = c;
-	}
-	if (j >= n) return;
-	const uint32_t copies = (target - 1 - g) / c;
-	w[j] = 1.0f + (float)copies * ((float)c / (float)target);
-}
-
-__global__ void k_clamp_count(const uint32_t* __restrict__ in, uint32_t cap, const uint32_t* __restrict__ cap_dev,
-                              uint32_t* __restrict__ out) {
-	if (threadIdx.x == 0 && blockIdx.x == 0) *out = min(*in, cap_dev ? *cap_dev : cap);
 }
 
 // Data parallelism (ngp_train_args.world_size > 1): each rank writes its total into its slot of
@@ -1356,20 +1393,6 @@ __global__ void k_dp_caps(const int32_t* __restrict__ slots, uint32_t world, uin
 			out[2] = local_cap;  // stay inside the buffers; the step is discarded
 		}
 	}
-}
-
-// Sum of per-ray losses (deterministic two-level reduction).
-__global__ void __launch_bounds__(1024) k_sum_floats(const float* __restrict__ v, uint32_t n, float* __restrict__ out) {
-	__shared__ float part[1024];
-	float s = 0.0f;
-	for (uint32_t i = threadIdx.x; i < n; i += 1024) s += v[i];
-	part[threadIdx.x] = s;
-	__syncthreads();
-	for (int d = 512; d > 0; d >>= 1) {
-		if ((int)threadIdx.x < d) part[threadIdx.x] += part[threadIdx.x + d];
-		__syncthreads();
-	}
-	if (threadIdx.x == 0) *out = part[0];
 }
 
 // ---------------------------------------------------------------------------
@@ -1630,9 +1653,12 @@ void launch_optimizer(ngp_model* m, uint32_t step, int opt_mlp, int opt_enc, hip
 				m->adam_corr.reserve((size_t)std::max<uint32_t>(need * 2u, 1u << 16) * 2);  // grows: refill all
 				lo = 0;
 			}
-			k_adam_corr<<<div_up(need - lo, 256u), 256, 0, s>>>(c.beta1, c.beta2, lo, need, reinterpret_cast<float2*>(m->adam_corr.ptr));
+			// 4096 steps ahead (entries past a parameter's count are never read), so the table is
+			// extended once per 4096 optimizer steps instead of once per step
+			const uint32_t fill = std::min<uint32_t>((need + 4095u) & ~4095u, (uint32_t)(m->adam_corr.n / 2));
+			k_adam_corr<<<div_up(fill - lo, 256u), 256, 0, s>>>(c.beta1, c.beta2, lo, fill, reinterpret_cast<float2*>(m->adam_corr.ptr));
 			NGP_HIP_CHECK(hipGetLastError());
-			m->adam_corr_n = need;
+			m->adam_corr_n = fill;
 			m->adam_corr_b1 = c.beta1;
 			m->adam_corr_b2 = c.beta2;
 		}
@@ -1825,10 +1851,11 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
 	// the global sample cap (src/testbed_nerf.cu:779-781 drops rays past max_samples) over all ranks
 	if (world > 1) dp_exchange(ts.counters.ptr + 0, dp_samples, reinterpret_cast<int32_t*>(ts.dp.ptr + 8), MS_global, nullptr, MS);
+	sa.total = ts.counters.ptr + 0;
+	sa.total_capped = ts.counters.ptr + 4;
 	if (general) k_sample_write<true><<<div_up(R, 4), 256, 0, s>>>(sa);
 	else k_sample_write<false><<<div_up(R, 4), 256, 0, s>>>(sa);
 	NGP_HIP_CHECK(hipGetLastError());
-	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 0, MS, sa.max_samples_dev, ts.counters.ptr + 4);
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 
 	// network inference with the training params (NerfNetwork::inference_mixed_precision): over
@@ -1890,10 +1917,18 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			c.hi = p < TRAIN_CHUNKS ? TRAIN_CHUNK_END[p] : c.lo;
 			c.rows = ts.counters.ptr + 12 + std::min(p, TRAIN_CHUNKS - 1);
 			c.eval_offset = p < TRAIN_CHUNKS ? off[p] : 0u;
-			// lanes per ray: ~100k+ lanes per launch (2k rays of a volume scene: 64; 35k rays of a surface scene: 4)
-			if (R <= 4096) k_train_chunk<64><<<div_up(R, 16), 1024, 0, s>>>(c);
-			else if (R <= 16384) k_train_chunk<16><<<div_up(R, 64), 1024, 0, s>>>(c);
-			else k_train_chunk<4><<<div_up(R, 256), 1024, 0, s>>>(c);
+			// lanes per ray: 64 for the ~2k long rays of a volume scene's batch, 16 for the 20-60k rays of a surface
+			// scene (its rays that pass 16 samples composite and scatter 32 per chunk: 2 rounds instead of 8 at 4
+			// lanes; surface step 1037 vs 1073 us, profiles/r05_train_chunk_lanes_ab.txt)
+			uint32_t G = m->tuning.train_chunk_lanes;
+			if (G == 0) G = R <= 4096 ? 64u : 16u;
+			switch (G) {
+			case 64: k_train_chunk<64><<<div_up(R, 16), 1024, 0, s>>>(c); break;
+			case 32: k_train_chunk<32><<<div_up(R, 32), 1024, 0, s>>>(c); break;
+			case 16: k_train_chunk<16><<<div_up(R, 64), 1024, 0, s>>>(c); break;
+			case 8: k_train_chunk<8><<<div_up(R, 128), 1024, 0, s>>>(c); break;
+			default: k_train_chunk<4><<<div_up(R, 256), 1024, 0, s>>>(c); break;
+			}
 			NGP_HIP_CHECK(hipGetLastError());
 			if (p == TRAIN_CHUNKS) break;
 			// launch about as many encoder chunks as the last step's rows needed; blocks loop
@@ -2053,16 +2088,20 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		        (unsigned long long)ev[0], (unsigned long long)ev[1], (unsigned long long)ev[2], (unsigned long long)ev[3]);
 	}
 
-	// compacted batch size c = min(total, B); rollover multiplicity
-	k_clamp_count<<<1, 1, 0, s>>>(ts.counters.ptr + 1, B, la.max_compacted_dev, ts.counters.ptr + 5);
+	// compacted batch size c = min(total, B), gather, rollover multiplicity, loss sum: one launch
+	const CompactFinish cf{ts.counters.ptr + 1, la.max_compacted_dev, ts.counters.ptr + 5, dp_compact, ts.cweight.ptr,
+	                       ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8)};
+	const uint32_t gather_blocks = div_up(B, 256) + 1;
+#define NGP_GATHER(FF) k_gather_compacted<FF><<<gather_blocks, 256, 0, s>>>(cf, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, \
+		internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr)
 	switch (F) {
-		case 1: k_gather_compacted<1><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
-		case 2: k_gather_compacted<2><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
-		case 4: k_gather_compacted<4><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
-		default: k_gather_compacted<8><<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 5, ts.csrc.ptr, ts.coords.ptr, enc_rows, enc_layout, internal_layout(m, B), L, ts.ccoords.ptr, reinterpret_cast<float4*>(ts.cpos4.ptr), ts.cenc.ptr, B, eidx, sa.simg, xd ? ts.cimg.ptr : nullptr); break;
+		case 1: NGP_GATHER(1); break;
+		case 2: NGP_GATHER(2); break;
+		case 4: NGP_GATHER(4); break;
+		default: NGP_GATHER(8); break;
 	}
-	k_rollover_weight<<<div_up(B, 256), 256, 0, s>>>(ts.counters.ptr + 1, B, dp_compact, ts.cweight.ptr);
-	k_sum_floats<<<1, 1024, 0, s>>>(ts.loss.ptr, R, reinterpret_cast<float*>(ts.counters.ptr + 8));
+#undef NGP_GATHER
+	NGP_HIP_CHECK(hipGetLastError());
 	tm.end(NGP_TIMER_TRAIN_LOSS, s, R);
 
 	// fused MLP forward+backward, then hash-grid scatter (Trainer::training_step)

@@ -277,12 +277,15 @@ def test_sampler_distance_field_walk_matches_chain_walk(density):
         g.close()
 
 
-def test_chunked_forward_matches_full_forward():
+@pytest.mark.parametrize("lanes", [0, 4, 8, 32])
+def test_chunked_forward_matches_full_forward(lanes):
     """The early-terminated (chunked) forward leaves the loss, the compaction and dL/dout
     bit-identical to evaluating every sample (the reference's inference over the whole
-    pre-compaction batch); gradients agree up to float-atomic ordering."""
+    pre-compaction batch); gradients agree up to float-atomic ordering.  lanes: k_train_chunk's
+    lanes per ray (ngp_tuning.train_chunk_lanes; 0 = the default for the batch, 64 at R = 2048)."""
     g, o, rng = pair(CFG_B, grid_scale=2.0)  # dense enough that most rays stop early
     try:
+        g.set_tuning(train_chunk_lanes=lanes)
         imgs, cams, focal = make_views(6, 32, 32)
         dd = DeviceDataset(imgs, cams, focal)
         set_bitfield_both(g, o, sphere_bitfield(0.35))

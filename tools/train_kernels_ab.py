@@ -10,6 +10,7 @@ import argparse
 import ctypes as C
 import os
 import sys
+import time
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, os.path.join(ROOT, "instant-ngp-rendering_amd"))
@@ -63,6 +64,12 @@ def main():
             tb.set_tuning(setting)
             tb.train(1 << 18)
             tb.sync()
+            # the step's wall time with the timers off, then the per-kernel pass with them on
+            t0 = time.perf_counter()
+            for _ in range(a.timed):
+                tb.train(1 << 18)
+            tb.sync()
+            acc[st].setdefault("step_wall", []).append(1e6 * (time.perf_counter() - t0) / a.timed)
             A.check(lib.ngp_timing_enable(h, -1))
             for idx in A.TIMER.values():  # discard what the warm-up step accumulated
                 A.check(lib.ngp_timing_read(h, idx, None, None, None, 1))
@@ -74,6 +81,7 @@ def main():
                 A.check(lib.ngp_timing_read(h, idx, C.byref(ms), C.byref(units), C.byref(launches), 1))
                 if launches.value:
                     acc[st].setdefault(name, []).append(1000.0 * ms.value / launches.value)
+            A.check(lib.ngp_timing_enable(h, 0))
     for st in a.settings:
         print(f"## {st or 'default'}")
         for name, v in acc[st].items():
