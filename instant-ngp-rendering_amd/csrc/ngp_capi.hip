@@ -263,7 +263,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		TrainScratch& t = m->ts;
 		t.ray_numsteps.release(); t.ray_compacted.release(); t.ray_state.release(); t.ray_loss_state.release(); t.ray_depth.release();
 		t.coords.release(); t.enc.release(); t.mlp_out.release(); t.ccoords.release(); t.cenc.release();
-		t.pos4.release(); t.cpos4.release(); t.ray_aux.release();
+		t.cpos4.release(); t.ray_aux.release();
 		t.dloss.release(); t.cweight.release(); t.csrc.release(); t.denc.release(); t.loss.release(); t.block_sums.release();
 		t.counters.release(); t.scan_a.release(); t.scan_b.release(); t.dp.release();
 		t.epos.release(); t.edir.release(); t.eenc.release(); t.eout.release(); t.eidx.release();

@@ -261,7 +261,6 @@ struct TrainScratch {
 	DevBuf<__half> enc;                // [L][max_samples][F]
 	DevBuf<__half> mlp_out;            // [max_samples][4]
 	DevBuf<float> ccoords;             // [B][8] compacted
-	DevBuf<float> pos4;                // [max_samples][4]: pos + dt rows for the encoder
 	DevBuf<float> cpos4;               // [B][4] compacted, for the encoder backward
 	DevBuf<__half> cenc;               // [L][B][F]
 	DevBuf<__half> dloss;              // [B][4]

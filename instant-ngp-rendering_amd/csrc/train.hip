@@ -209,7 +209,6 @@ struct SamplerArgs {
 	uint32_t* bases;     // [R]
 	float* ray_state;    // [R][8]
 	float* coords;       // [max][8]
-	float4* pos4;        // [max]: pos + warped dt again, 16-B rows the encoder reads once per level
 	uint32_t* simg;      // [max] n_extra_dims > 0: the sample's image (its latent-code row); null otherwise
 	const float* dmap;   // learned distortion map [dry][drx][2] (null: off; general instance only)
 	uint32_t drx, dry;
@@ -473,7 +472,6 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 			const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
 			c[0] = pd;
 			c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);
-			a.pos4[base + r] = pd;
 			if (a.simg) a.simg[base + r] = img;
 		});
 		return;
@@ -493,8 +491,7 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 				const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
 				c[0] = pd;
 				c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);  // the pad float carries the max level
-				a.pos4[base + r] = pd;
-				if (a.simg) a.simg[base + r] = img;
+					if (a.simg) a.simg[base + r] = img;
 			}
 		}
 		j += __popcll(m);
@@ -521,7 +518,6 @@ struct ChunkArgs {
 	uint32_t n_rays;
 	const uint32_t* numsteps;  // [R][2] samples, first sample (sampler)
 	const float* coords;       // [MS][8] sampler rows
-	const float4* pos4;        // [MS]
 	float4* epos;              // [MSE] evaluation rows: pos + warped dt
 	float4* edir;              // [MSE] warped direction
 	const __half* eout;        // [MSE][4] network outputs of the evaluation rows
@@ -659,8 +655,9 @@ __global__ void __launch_bounds__(1024) k_train_chunk(ChunkArgs a) {
 	if (r == 0) a.ray_ebase[i] = e0;
 	for (uint32_t k = r; k < claim; k += G) {
 		const uint32_t src = base + a.lo + k;
-		a.epos[e0 + k] = a.pos4[src];
-		a.edir[e0 + k] = reinterpret_cast<const float4*>(a.coords + 8 * (size_t)src)[1];
+		const float4* row = reinterpret_cast<const float4*>(a.coords + 8 * (size_t)src);
+		a.epos[e0 + k] = row[0];
+		a.edir[e0 + k] = row[1];
 		if (a.eimg) a.eimg[e0 + k] = a.simg[src];
 	}
 }
@@ -1750,7 +1747,6 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.enc.reserve((size_t)L * MS * F);
 	ts.mlp_out.reserve(4 * (size_t)MS);
 	ts.ccoords.reserve(8 * (size_t)B);
-	ts.pos4.reserve(4 * (size_t)MS);
 	// n_extra_dims > 0: each sample's image picks its latent-code row (NerfCoordinate extra dims, src/testbed_nerf.cu:824)
 	const bool xd = m->cfg.n_extra_dims > 0;
 	if (xd) {
@@ -1836,7 +1832,6 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.bases = counts.ptr + R;
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
-	sa.pos4 = reinterpret_cast<float4*>(ts.pos4.ptr);
 	sa.simg = xd ? ts.simg.ptr : nullptr;
 	if (t->distortion_map && t->distortion_res[0] && t->distortion_res[1]) {
 		sa.dmap = t->distortion_map;
@@ -1871,7 +1866,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.chunked = !chunk_off;
 	if (chunk_off) {
 		tm.begin_kernel(NGP_TIMER_TRAIN_ENCODE);
-		launch_hashgrid_fwd(ml_on ? m->lt.with_max_level(ts.coords.ptr + 7, 8) : m->lt, ts.pos4.ptr, 4, MS, table, ts.enc.ptr,
+		launch_hashgrid_fwd(ml_on ? m->lt.with_max_level(ts.coords.ptr + 7, 8) : m->lt, ts.coords.ptr, 8, MS, table, ts.enc.ptr,
 		                    enc_layout, s, ts.counters.ptr + 4, 0);
 		tm.end(NGP_TIMER_TRAIN_ENCODE, s);
 		tm.begin_kernel(NGP_TIMER_TRAIN_MLP_INFER);
@@ -1896,7 +1891,6 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		c.n_rays = R;
 		c.numsteps = ts.ray_numsteps.ptr;
 		c.coords = ts.coords.ptr;
-		c.pos4 = reinterpret_cast<const float4*>(ts.pos4.ptr);
 		c.epos = reinterpret_cast<float4*>(ts.epos.ptr);
 		c.edir = reinterpret_cast<float4*>(ts.edir.ptr);
 		c.eout = ts.eout.ptr;
