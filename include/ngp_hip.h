@@ -399,6 +399,7 @@ typedef struct ngp_tuning {
 	                                    (ngp_render_args.host_frame), 2 = tonemap then one read-back; 0: the default */
 	uint32_t train_chunk_lanes;      /* lanes per ray of the chunked training forward's k_train_chunk (4, 8, 16, 32 or 64);
 	                                    0: 64 for batches of <= 4096 rays, else 16 */
+	uint32_t train_sampler_lanes;    /* lanes per ray of the training sampler's two passes (8, 16, 32 or 64); 0: 64 */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */

@@ -88,6 +88,9 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->train_chunk_lanes == 0 || (t->train_chunk_lanes >= 4 && t->train_chunk_lanes <= 64 &&
 	                                      (t->train_chunk_lanes & (t->train_chunk_lanes - 1)) == 0),
 	        "train_chunk_lanes must be 0 or a power of two in [4, 64]");
+	require(t->train_sampler_lanes == 0 || (t->train_sampler_lanes >= 8 && t->train_sampler_lanes <= 64 &&
+	                                        (t->train_sampler_lanes & (t->train_sampler_lanes - 1)) == 0),
+	        "train_sampler_lanes must be 0 or a power of two in [8, 64]");
 }
 
 // tcnn GridEncodingTemplated constructor (level table); per_level_scale resolved on the host.

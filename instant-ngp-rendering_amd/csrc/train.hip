@@ -328,61 +328,69 @@ __device__ __forceinline__ LatticePoint training_lattice_point(const SamplerArgs
 	return p;
 }
 
-// generate_training_samples_nerf's walk (testbed_nerf.cu:779-795, 814-830) over 64 lattice
+// The sampler runs G lanes per ray (G = 8 ... 64, a power of two; one ray per G-lane group of a wave, groups
+// independent: every branch below is group-uniform, ballots are taken over the group's bits only).
+template <uint32_t G>
+__device__ __forceinline__ unsigned long long group_bits(unsigned long long wave_bits, uint32_t g0) {
+	return G == 64 ? wave_bits : (wave_bits >> g0) & ((1ull << G) - 1ull);
+}
+
+// generate_training_samples_nerf's walk (testbed_nerf.cu:779-795, 814-830) over G lattice
 // points of one ray at a time (one per lane): the reference's chain -- a sample at every
 // occupied point it visits, a jump past the cell of every empty one, stop at the first
 // visited point outside the AABB -- run as a scalar loop over the batch's ballots (one
-// iteration per run of samples or per jump).  Returns the batch's sample lanes; *cur = the
-// lattice offset (from this batch's first point) of the next point to visit; *exited once
-// the ray has left the AABB.
-__device__ __forceinline__ unsigned long long training_walk_batch(const LatticePoint& p, uint32_t lane, uint32_t* cur_io,
+// iteration per run of samples or per jump).  Returns the batch's sample lanes (bits relative to
+// the group's first lane g0); *cur = the lattice offset (from this batch's first point) of the
+// next point to visit; *exited once the ray has left the AABB.
+template <uint32_t G>
+__device__ __forceinline__ unsigned long long training_walk_batch(const LatticePoint& p, uint32_t g0, uint32_t* cur_io,
                                                                   bool* exited) {
-	const unsigned long long occ = __ballot(p.occupied), in = __ballot(p.inside);
+	const unsigned long long occ = group_bits<G>(__ballot(p.occupied), g0), in = group_bits<G>(__ballot(p.inside), g0);
 	unsigned long long samp = 0;
 	uint32_t cur = *cur_io;
-	while (cur < 64u) {
+	while (cur < G) {
 		if (!((in >> cur) & 1ull)) {
 			*exited = true;
 			break;
 		}
 		if ((occ >> cur) & 1ull) {
-			const unsigned long long rest = ~occ >> cur;  // run of occupied points from cur
-			const uint32_t run = rest ? (uint32_t)(__ffsll((long long)rest) - 1) : 64u - cur;
+			const unsigned long long rest = (~occ >> cur) & (G == 64 ? ~0ull : ((1ull << (G - cur)) - 1ull));
+			const uint32_t run = rest ? (uint32_t)(__ffsll((long long)rest) - 1) : G - cur;  // occupied points from cur
 			samp |= (run >= 64u ? ~0ull : ((1ull << run) - 1ull)) << cur;
 			cur += run;
 		} else {
-			cur += (uint32_t)__builtin_amdgcn_readlane((int)p.jump, (int)cur);
+			cur += (uint32_t)__shfl((int)p.jump, (int)(g0 + cur), 64);
 		}
 	}
 	*cur_io = cur;
-	(void)lane;
 	return samp;
 }
 
 // aabb_scale 1 (a.df set): the ray's samples are the occupied lattice points inside the AABB (see
-// train_step_df), found 64 lattice points per round with the empty space between them crossed
+// train_step_df), found G lattice points per round with the empty space between them crossed
 // through the octant distance fields -- a surface scene's rays cross most of the volume empty, one
 // voxel per jump in the chain walk.  visit(rank, k) for every sample in order (rank < cap); returns
 // the ray's sample count, capped.
 // kb: the lattice point the walk starts from (0, or the round k_sample_count saw emit the ray's first
 // sample: the walk from there is the same); *first (if set) = the start of the first emitting round.
-template <class Visit>
-__device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3 idir, float n0, uint32_t cap, uint32_t lane,
-                                            uint32_t kb, uint32_t* first, Visit visit) {
+template <uint32_t G, class Visit>
+__device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3 idir, float n0, uint32_t cap, uint32_t r,
+                                            uint32_t g0, uint32_t kb, uint32_t* first, Visit visit) {
 	const uint32_t oct = ray_octant(d);
-	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+	const unsigned long long below = (1ull << r) - 1ull;
 	uint32_t j = 0;
-	while (true) {  // wave-uniform: one ray per wave
-		uint32_t k = kb + lane;
+	while (true) {  // group-uniform
+		uint32_t k = kb + r;
 		const int st = train_step_df(&k, n0, a.st, o, d, idir, oct, a.df, a.aabb);
-		const unsigned long long m_exit = __ballot(st == LATTICE_EXIT), m_occ = __ballot(st == LATTICE_OCCUPIED);
-		// an all-empty round goes on from the last lane's verified skip
-		const uint32_t k_next = (uint32_t)__builtin_amdgcn_readlane((int)(st == LATTICE_SKIPPED ? k : kb + 64u), 63);
+		const unsigned long long m_exit = group_bits<G>(__ballot(st == LATTICE_EXIT), g0);
+		const unsigned long long m_occ = group_bits<G>(__ballot(st == LATTICE_OCCUPIED), g0);
+		// an all-empty round goes on from the group's last lane's verified skip
+		const uint32_t k_next = (uint32_t)__shfl((int)(st == LATTICE_SKIPPED ? k : kb + G), (int)(g0 + G - 1), 64);
 		const uint32_t fe = m_exit ? (uint32_t)(__ffsll((long long)m_exit) - 1) : 64u;
 		const unsigned long long emit = m_occ & (fe >= 64 ? ~0ull : ((1ull << fe) - 1ull));
-		if ((emit >> lane) & 1ull) {
-			const uint32_t r = j + __popcll(emit & below);
-			if (r < cap) visit(r, kb + lane);
+		if ((emit >> r) & 1ull) {
+			const uint32_t rank = j + __popcll(emit & below);
+			if (rank < cap) visit(rank, kb + r);
 		}
 		if (first && j == 0 && emit) *first = kb;
 		j += __popcll(emit);
@@ -392,30 +400,30 @@ __device__ __forceinline__ uint32_t df_walk(const SamplerArgs& a, v3 o, v3 d, v3
 	}
 }
 
-// pass 1: count the ray's samples (<= NERF_STEPS), one wave per ray.  The point the walk
-// reached when it emitted its first sample goes to ray_state[8 i + 6] (overwritten by the loss
-// kernel later), so pass 2 starts there instead of crossing the empty space before it again.
-template <bool GENERAL>
+// pass 1: count the ray's samples (<= NERF_STEPS), G lanes per ray.  The point the walk reached
+// when it emitted its first sample goes to ray_state[8 i + 6] (overwritten by the loss kernel
+// later), so pass 2 starts there instead of crossing the empty space before it again.
+template <bool GENERAL, uint32_t G>
 __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
-	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
-	const uint32_t lane = threadIdx.x & 63u;
-	if (i >= a.n_rays) return;  // wave-uniform
+	const uint32_t lane = threadIdx.x & 63u, r = lane % G, g0 = lane - r;
+	const uint32_t i = blockIdx.x * (256u / G) + threadIdx.x / G;
+	if (i >= a.n_rays) return;  // group-uniform
 	v3 o, d;
 	float n0;
 	uint32_t count = 0, first = 0;
 	if (!training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0)) {
 	} else if (a.df) {
 		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-		count = df_walk(a, o, d, idir, n0, NERF_STEPS, lane, 0u, &first, [](uint32_t, uint32_t) {});
+		count = df_walk<G>(a, o, d, idir, n0, NERF_STEPS, r, g0, 0u, &first, [](uint32_t, uint32_t) {});
 	} else {
 		const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 		bool exited = false;
-		for (uint32_t kb = 0, cur = 0; !exited; kb += 64, cur -= 64) {
-			if (cur >= 64u) continue;  // a jump past this whole batch
+		for (uint32_t kb = 0, cur = 0; !exited; kb += G, cur -= G) {
+			if (cur >= G) continue;  // a jump past this whole batch
 			const uint32_t cur0 = cur;
-			const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + lane);
-			const uint32_t c = __popcll(training_walk_batch(p, lane, &cur, &exited));
-			if (count == 0 && c) first = kb | cur0;  // kb is a multiple of 64, cur0 < 64
+			const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + r);
+			const uint32_t c = __popcll(training_walk_batch<G>(p, g0, &cur, &exited));
+			if (count == 0 && c) first = kb | cur0;  // kb is a multiple of G, cur0 < G
 			if (count + c >= NERF_STEPS) {
 				count = NERF_STEPS;
 				break;
@@ -423,7 +431,7 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 			count += c;
 		}
 	}
-	if (lane == 0) {
+	if (r == 0) {
 		a.counts[i] = count;
 		reinterpret_cast<uint32_t*>(a.ray_state)[8 * (size_t)i + 6] = first;
 	}
@@ -431,28 +439,28 @@ __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 
 // pass 2: same walk, each sample written at base + (its rank among the ray's samples);
 // consecutive lanes write consecutive 32-byte coordinates.
-template <bool GENERAL>
+template <bool GENERAL, uint32_t G>
 __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
-	const uint32_t i = blockIdx.x * 4u + (threadIdx.x >> 6);
-	const uint32_t lane = threadIdx.x & 63u;
+	const uint32_t lane = threadIdx.x & 63u, r = lane % G, g0 = lane - r;
+	const uint32_t i = blockIdx.x * (256u / G) + threadIdx.x / G;
 	const uint32_t cap = a.max_samples_dev ? *a.max_samples_dev : a.max_samples;
-	if (i == 0 && lane == 0) *a.total_capped = min(*a.total, cap);  // (no reader in this launch)
+	if (i == 0 && r == 0) *a.total_capped = min(*a.total, cap);  // (no reader in this launch)
 	if (i >= a.n_rays) return;
 	const uint32_t n = a.counts[i], base = a.bases[i];
 	if (n == 0 || base + n > cap) {
-		if (lane == 0) {
+		if (r == 0) {
 			a.numsteps[2 * i + 0] = 0;
 			a.numsteps[2 * i + 1] = 0;
 		}
 		return;
 	}
-	// k_sample_count's resume point, read before lane 0 rewrites the ray's state below
+	// k_sample_count's resume point, read before lane 0 of the group rewrites the ray's state below
 	const uint32_t first = reinterpret_cast<const uint32_t*>(a.ray_state)[8 * (size_t)i + 6];
 	v3 o, d;
 	float n0, max_level;
 	uint32_t img = 0;
 	training_ray<GENERAL>(a, a.ray_offset + i, &o, &d, &n0, &max_level, &img);
-	if (lane == 0) {
+	if (r == 0) {
 		a.numsteps[2 * i + 0] = n;
 		a.numsteps[2 * i + 1] = base;
 		float* rs = a.ray_state + 8 * (size_t)i;
@@ -462,36 +470,34 @@ __global__ void __launch_bounds__(256) k_sample_write(SamplerArgs a) {
 	const v3 wdir = warp_direction(d);
 	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 	if (a.df) {
-		df_walk(a, o, d, idir, n0, n, lane, first, nullptr, [&](uint32_t r, uint32_t k) {
+		df_walk<G>(a, o, d, idir, n0, n, r, g0, first, nullptr, [&](uint32_t rank, uint32_t k) {
 			// the chain walk's training_lattice_point for lattice point k, bit for bit
 			const float nk = n0 + (float)k;
 			const float t = step_from(a.st, nk);
 			const float dt = step_from(a.st, nk + 1.0f) - t;
 			const v3 wp = aabb_relative(a.aabb, o + d * t);
-			float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + r));
-			const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-			c[0] = pd;
+			float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + rank));
+			c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
 			c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);
-			if (a.simg) a.simg[base + r] = img;
+			if (a.simg) a.simg[base + rank] = img;
 		});
 		return;
 	}
-	const unsigned long long below = lane == 0 ? 0ull : (~0ull >> (64 - lane));
+	const unsigned long long below = (1ull << r) - 1ull;
 	uint32_t j = 0;
 	bool exited = false;
-	for (uint32_t kb = first & ~63u, cur = first & 63u; j < n && !exited; kb += 64, cur -= 64) {
-		if (cur >= 64u) continue;
-		const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + lane);
-		const unsigned long long m = training_walk_batch(p, lane, &cur, &exited);
-		if ((m >> lane) & 1ull) {
-			const uint32_t r = j + __popcll(m & below);
-			if (r < n) {
+	for (uint32_t kb = first & ~(G - 1u), cur = first & (G - 1u); j < n && !exited; kb += G, cur -= G) {
+		if (cur >= G) continue;
+		const LatticePoint p = training_lattice_point(a, o, d, idir, n0, kb + r);
+		const unsigned long long m = training_walk_batch<G>(p, g0, &cur, &exited);
+		if ((m >> r) & 1ull) {
+			const uint32_t rank = j + __popcll(m & below);
+			if (rank < n) {
 				const v3 wp = aabb_relative(a.aabb, p.pos);
-				float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + r));
-				const float4 pd = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
-				c[0] = pd;
+				float4* c = reinterpret_cast<float4*>(a.coords + 8 * (size_t)(base + rank));
+				c[0] = make_float4(wp.x, wp.y, wp.z, warp_dt(p.dt));
 				c[1] = make_float4(wdir.x, wdir.y, wdir.z, max_level);  // the pad float carries the max level
-					if (a.simg) a.simg[base + r] = img;
+				if (a.simg) a.simg[base + rank] = img;
 			}
 		}
 		j += __popcll(m);
@@ -1841,15 +1847,24 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	KernelTimers& tm = m->timers;
 	tm.begin(NGP_TIMER_TRAIN_SAMPLER, s);
 	const bool general = t->cdf_img || t->cdf_x_cond_y || t->has_lens || sa.dmap;
-	if (general) k_sample_count<true><<<div_up(R, 4), 256, 0, s>>>(sa);
-	else k_sample_count<false><<<div_up(R, 4), 256, 0, s>>>(sa);
+	// lanes per ray of the two sampler passes (a wave per ray for the ~2k rays of a volume scene's batch)
+	uint32_t sl = m->tuning.train_sampler_lanes;
+	if (sl == 0) sl = 64u;
+#define NGP_SAMPLER(KERNEL)                                                                                        \
+	switch (sl) {                                                                                                  \
+		case 8: if (general) KERNEL<true, 8><<<div_up(R, 32), 256, 0, s>>>(sa); else KERNEL<false, 8><<<div_up(R, 32), 256, 0, s>>>(sa); break; \
+		case 16: if (general) KERNEL<true, 16><<<div_up(R, 16), 256, 0, s>>>(sa); else KERNEL<false, 16><<<div_up(R, 16), 256, 0, s>>>(sa); break; \
+		case 32: if (general) KERNEL<true, 32><<<div_up(R, 8), 256, 0, s>>>(sa); else KERNEL<false, 32><<<div_up(R, 8), 256, 0, s>>>(sa); break; \
+		default: if (general) KERNEL<true, 64><<<div_up(R, 4), 256, 0, s>>>(sa); else KERNEL<false, 64><<<div_up(R, 4), 256, 0, s>>>(sa); break; \
+	}
+	NGP_SAMPLER(k_sample_count)
 	launch_exclusive_scan(sa.counts, sa.bases, R, ts.block_sums.ptr, ts.counters.ptr + 0, s);
 	// the global sample cap (src/testbed_nerf.cu:779-781 drops rays past max_samples) over all ranks
 	if (world > 1) dp_exchange(ts.counters.ptr + 0, dp_samples, reinterpret_cast<int32_t*>(ts.dp.ptr + 8), MS_global, nullptr, MS);
 	sa.total = ts.counters.ptr + 0;
 	sa.total_capped = ts.counters.ptr + 4;
-	if (general) k_sample_write<true><<<div_up(R, 4), 256, 0, s>>>(sa);
-	else k_sample_write<false><<<div_up(R, 4), 256, 0, s>>>(sa);
+	NGP_SAMPLER(k_sample_write)
+#undef NGP_SAMPLER
 	NGP_HIP_CHECK(hipGetLastError());
 	tm.end(NGP_TIMER_TRAIN_SAMPLER, s, R);
 

@@ -130,7 +130,7 @@ class Tuning(C.Structure):
         ("encode_streaming", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
         ("encode_xcd_regions", C.c_uint32), ("render_skip_unfilled", C.c_uint32), ("render_exit_cap", C.c_uint32),
         ("render_priority", C.c_uint32), ("render_host_frame", C.c_uint32),
-        ("train_chunk_lanes", C.c_uint32),
+        ("train_chunk_lanes", C.c_uint32), ("train_sampler_lanes", C.c_uint32),
     ]
 
 

@@ -277,6 +277,54 @@ def test_sampler_distance_field_walk_matches_chain_walk(density):
         g.close()
 
 
+@pytest.mark.parametrize("lanes", [8, 16, 32])
+@pytest.mark.parametrize("aabb_scale", [1, 8])
+def test_sampler_lanes_per_ray_match_oracle(aabb_scale, lanes):
+    """The training sampler with G lanes per ray (ngp_tuning.train_sampler_lanes; G-lane groups of a wave walk
+    their rays independently) emits the same samples as one wave per ray, bit for bit -- counts, bases,
+    coordinates -- and the reference's (the oracle): for the distance-field walk (aabb_scale 1) and the jump
+    chain through cascades (aabb_scale 8; cone stepping's expf/logf differ from the host's in the last ulp, as in
+    test_train_step_matches_oracle)."""
+    g, o, rng = pair(dict(CFG_A, aabb_scale=aabb_scale))
+    try:
+        imgs, cams, focal = make_views(6, 32, 32)
+        hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
+        max_cascade = int(np.log2(aabb_scale))
+        if aabb_scale == 1:
+            grid = np.maximum(np.where(rng.random(CELLS) < 0.05, 1.0, 0.0).astype(np.float32), sphere_bitfield(0.2))
+        else:
+            grid = cascaded_grid(rng, max_cascade)
+        set_bitfield_both(g, o, grid, max_cascade)
+        R, B, MS = 2048, 1 << 14, 1 << 18
+        out = {}
+        for G in (64, lanes):
+            g.set_tuning(train_sampler_lanes=G)
+            g.zero_grads()
+            A.check(g.lib.ngp_train_step(g.h, C.byref(train_args(dd.ptr, dd.n, R, B, MS, aabb_scale=aabb_scale)), stream()))
+            torch.cuda.synchronize()
+            out[G] = (gpu_scratch(g, A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2).copy(),
+                      gpu_scratch(g, A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS].copy())
+        o.train_step(train_args(hd.ptr, hd.n, R, B, MS, aabb_scale=aabb_scale))
+        o_ns = o.scratch(A.SCRATCH_RAY_NUMSTEPS, np.uint32).reshape(-1, 2)
+        np.testing.assert_array_equal(out[lanes][0], out[64][0])
+        np.testing.assert_array_equal(out[lanes][0], o_ns)
+        assert int(o_ns[:, 0].sum()) > 1000
+        owned = np.zeros(MS, bool)
+        for n, b in o_ns:
+            owned[b:b + n] = True
+        g_c, g64_c = out[lanes][1][owned, :7], out[64][1][owned, :7]
+        o_c = o.scratch(A.SCRATCH_COORDS, np.float32).reshape(-1, 8)[:MS][owned, :7]
+        np.testing.assert_array_equal(g_c, g64_c)
+        if aabb_scale == 1:
+            np.testing.assert_array_equal(g_c, o_c)
+        else:
+            np.testing.assert_allclose(g_c[:, :3], o_c[:, :3], rtol=0, atol=1e-6)
+            np.testing.assert_allclose(g_c[:, 3], o_c[:, 3], rtol=0, atol=5e-5)
+            np.testing.assert_array_equal(g_c[:, 4:], o_c[:, 4:])
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("lanes", [0, 4, 8, 32])
 def test_chunked_forward_matches_full_forward(lanes):
     """The early-terminated (chunked) forward leaves the loss, the compaction and dL/dout
