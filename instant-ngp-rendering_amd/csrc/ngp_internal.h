@@ -58,8 +58,11 @@ struct KernelTimers {
 
 	hipEvent_t take() {
 		if (pool.empty()) {
+			// timing-only events: no system-scope fence when they complete (the default one writes back and
+			// invalidates the caches around every timed launch -- ~10 us of idle GPU per event pair, measured in
+			// profiles/r05_timer_gaps.txt); the host reads them after a stream synchronisation
 			hipEvent_t e;
-			NGP_HIP_CHECK(hipEventCreate(&e));
+			NGP_HIP_CHECK(hipEventCreateWithFlags(&e, hipEventDisableSystemFence));
 			return e;
 		}
 		hipEvent_t e = pool.back();

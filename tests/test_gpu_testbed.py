@@ -774,3 +774,52 @@ def test_optimize_extra_dims_trains_per_image_codes(scene, tmp_path):
     tb2.background_color = [0.0, 0.0, 0.0, 1.0]
     tb2.set_camera_to_training_view(3)
     np.testing.assert_array_equal(tb2.render(48, 48, 1, True), f3)
+
+
+def test_kernel_timers_measure_every_class(scene):
+    """The kernel timers bench.py's roofline reads (ngp_timing_enable / ngp_timing_read; timing-only events without the
+    system-scope fence): with every timer on, 16 training steps (one with a density-grid update) and a 1080p frame give
+    each class launches, time and units, within the wall time they were measured in; timers off leave nothing to read."""
+    import ctypes as C
+    import time
+    import ngp_abi as A
+    root, _, _ = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(root)
+    tb.reload_network_from_file("lego_L16F2.json")
+    tb.shall_train = True
+    for _ in range(20):
+        tb.train(1 << 16)
+    tb.set_camera_to_training_view(0)
+    tb.render(256, 256, 1, True)
+    tb.sync()
+    lib = A.load()
+    h = C.c_void_p(tb.model_handle)
+    A.check(lib.ngp_timing_enable(h, -1))
+    for idx in A.TIMER.values():
+        A.check(lib.ngp_timing_read(h, idx, None, None, None, 1))
+    t0 = time.perf_counter()
+    for _ in range(16):  # one density-grid update every 16 steps
+        tb.train(1 << 16)
+    tb.render(1920, 1080, 1, True)
+    tb.sync()
+    wall_ms = 1e3 * (time.perf_counter() - t0)
+    got = {}
+    for name, idx in A.TIMER.items():
+        ms, units, launches = C.c_double(), C.c_uint64(), C.c_uint32()
+        A.check(lib.ngp_timing_read(h, idx, C.byref(ms), C.byref(units), C.byref(launches), 1))
+        got[name] = (ms.value, units.value, launches.value)
+    A.check(lib.ngp_timing_enable(h, 0))
+    for name, (ms, units, launches) in got.items():
+        assert launches > 0 and ms > 0.0, (name, got[name])
+        assert ms < 2.0 * wall_ms, (name, ms, wall_ms)  # (the two ray pipelines' launches overlap)
+    for name in ("train_encode", "train_mlp_infer", "train_mlp_bwd", "train_encode_bwd", "render_encode", "render_mlp",
+                 "render_march", "optimizer"):
+        assert got[name][1] > 0, (name, got[name])
+    assert got["render_encode"][1] == got["render_mlp"][1]  # the frame's filled samples
+    assert got["train_encode_bwd"][1] == got["train_mlp_bwd"][1] <= 16 * (1 << 16)  # the compacted batches
+    tb.train(1 << 16)
+    tb.sync()
+    ms, units, launches = C.c_double(), C.c_uint64(), C.c_uint32()
+    A.check(lib.ngp_timing_read(h, A.TIMER["train_encode"], C.byref(ms), C.byref(units), C.byref(launches), 1))
+    assert launches.value == 0 and ms.value == 0.0
