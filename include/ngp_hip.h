@@ -381,7 +381,8 @@ typedef struct ngp_tuning {
 	                                    bit 2: the chunked training forward stops rays at transmittance 0.999 (forces
 	                                    forward_early_stop_violations: exercises the discard-and-retry path);
 	                                    bit 3: data-parallel sample buffers start at an eighth of a rank's even share
-	                                    (forces sample_capacity_overflow and the retry with grown buffers) */
+	                                    (forces sample_capacity_overflow and the retry with grown buffers);
+	                                    bit 4: renders stop marching after 40 lattice steps per ray (the retire path) */
 	uint32_t encode_streaming;       /* hash encoder (F = 2 planes): 0 = non-temporal encoding stores (the default), 1 = plain */
 	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
 	                                    by cell, coherent gathers; same grid) */

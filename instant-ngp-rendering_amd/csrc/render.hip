@@ -561,53 +561,30 @@ __device__ __forceinline__ uint32_t points_to_exit(const RenderK& k, v3 o, v3 d,
 // transmittance budget (sample_budget), capped by the lattice points left to its exit
 // (k.exit_cap): the slots a ray reserves but does not fill still cost a 20-B row store,
 // the encoder's zero features and, in mixed tiles, the MLP.
+// One ray's march of a pass (the body of generate_next_nerf_network_inputs for G lanes per ray): reserves the ray's
+// budget of slots (block_reserve: every thread of the workgroup calls this, running = false for idle lanes), writes
+// its samples from lattice point *n on (positions + warped dt rows, SH row indices, optional dt array), pads the
+// slots it did not fill, and returns the samples written; *n / *exited / *base are the ray's next state.  cap_slots:
+// the slot arrays' extent (a reservation past it is cut; the ray continues next pass).
 template <uint32_t G>
-__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
-                                                  Payload* __restrict__ payloads, const float4* __restrict__ rgba,
-                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray,
-                                                  uint32_t target, uint32_t max_steps,
-                                                  uint32_t* __restrict__ next_alive_counter,
-                                                  uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
-                                                  const uint32_t* counters, unsigned long long* host_prev, uint32_t tag_prev) {
-	set_wave_priority(k.prio);
-	// the previous pass's counters, before this block zeroes next_alive_counter / steps_out
-	if (host_prev && blockIdx.x == 0 && threadIdx.x < 8) publish_counters(counters, host_prev, tag_prev);
-	__syncthreads();
-	// the pass is sized on the device: the host enqueues passes ahead of their read-backs
-	const uint32_t n_alive = *alive_counter;
-	// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
-	// every ray composites its own samples in order and stops at the same one whatever the chunking
-	const uint32_t n_steps = min(max(target / max(n_alive, 1u), 1u), max_steps);
-	if (blockIdx.x == 0 && threadIdx.x == 0) {
-		*next_alive_counter = 0;  // filled by this pass's k_composite
-		*steps_out = n_alive ? n_steps : 0u;
-	}
+__device__ __forceinline__ uint32_t march_ray(const RenderK& k, bool valid, v3 o, v3 d, float* n_io, uint32_t row, uint32_t budget,
+                                              float4* __restrict__ posdt, uint32_t* __restrict__ sray, float* __restrict__ sdt,
+                                              uint32_t* __restrict__ sample_counter, uint32_t cap_slots, uint32_t* base_out,
+                                              bool* exited_out) {
 	const uint32_t lane = threadIdx.x & 63u;
 	const uint32_t r = lane % G, g0 = lane - r;  // rank in the ray's group, first lane of the group
 	const unsigned long long gmask = G == 64 ? ~0ull : (((1ull << G) - 1ull) << g0);
-	const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
-	const bool valid = i < n_alive;  // group-uniform
-	Payload* p = payloads + (valid ? i : 0);
 	bool running = valid;
-	v3 o = mk3(0.0f), d = mk3(1.0f), idir = mk3(1.0f);
-	float n = 0.0f;
-	uint32_t row = 0;  // the ray's SH row (its pixel index; written once per frame by k_render_init)
-	uint32_t budget = 0;
-	if (running) {
-		o = mk3(p->o[0], p->o[1], p->o[2]);
-		d = mk3(p->d[0], p->d[1], p->d[2]);
-		idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-		n = p->n;
-		row = p->idx;
-		budget = sample_budget(k, 1.0f - rgba[i].w, p->alpha_last, n_steps);
-		if (k.exit_cap) budget = min(budget, points_to_exit(k, o, d, n));
-	}
+	float n = *n_io;
+	const v3 idir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
 	uint32_t base = block_reserve(r == 0 ? budget : 0u, sample_counter);
 	if (G > 1) base = __shfl(base, g0, 64);
+	if (valid && base + budget > cap_slots) budget = base < cap_slots ? cap_slots - base : 0u;
 	float4* const out_rows = posdt + base;
 	const uint32_t oct = ray_octant(d);
 	uint32_t j = 0, iters = 0;
 	bool exited = false;
+	if (budget == 0) running = false;
 	while (__ballot(running) != 0ull) {
 		iters += running;
 		float nr = n + (float)r;
@@ -629,7 +606,7 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 				const float dt = step_from(k.st, pn + 1.0f) - t;
 				const v3 wp = aabb_relative(k.train_aabb, o + d * t);
 				out_rows[j + rank] = make_float4(wp.x, wp.y, wp.z, warp_dt(dt));
-				if (k.sdt) k.sdt[(size_t)base + j + rank] = warp_dt(dt);
+				if (sdt) sdt[(size_t)base + j + rank] = warp_dt(dt);
 				sray[(size_t)base + j + rank] = row;
 			}
 		}
@@ -663,7 +640,58 @@ __global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k
 		atomicAdd(&k.dbg[3], j);
 		atomicAdd(&k.dbg[5], budget);
 	}
-	if (valid && r == 0) {
+	*n_io = n;
+	*base_out = base;
+	*exited_out = exited;
+	return j;
+}
+
+// The ray's slot budget of a pass: sample_budget of its transmittance, capped by the points left to its exit.
+__device__ __forceinline__ uint32_t ray_budget(const RenderK& k, float T, float alpha_last, uint32_t n_steps, v3 o, v3 d, float n) {
+	uint32_t budget = sample_budget(k, T, alpha_last, n_steps);
+	if (k.exit_cap) budget = min(budget, points_to_exit(k, o, d, n));
+	return budget;
+}
+
+template <uint32_t G>
+__global__ void __launch_bounds__(512) __attribute__((amdgpu_waves_per_eu(8))) k_generate(RenderK k, const uint32_t* __restrict__ alive_counter,
+                                                  Payload* __restrict__ payloads, const float4* __restrict__ rgba,
+                                                  float4* __restrict__ posdt, uint32_t* __restrict__ sray,
+                                                  uint32_t target, uint32_t max_steps,
+                                                  uint32_t* __restrict__ next_alive_counter,
+                                                  uint32_t* __restrict__ sample_counter, uint32_t* __restrict__ steps_out,
+                                                  const uint32_t* counters, unsigned long long* host_prev, uint32_t tag_prev) {
+	set_wave_priority(k.prio);
+	// the previous pass's counters, before this block zeroes next_alive_counter / steps_out
+	if (host_prev && blockIdx.x == 0 && threadIdx.x < 8) publish_counters(counters, host_prev, tag_prev);
+	__syncthreads();
+	// the pass is sized on the device: the host enqueues passes ahead of their read-backs
+	const uint32_t n_alive = *alive_counter;
+	// samples per ray per pass (the reference caps this at 8): a free schedule parameter, since
+	// every ray composites its own samples in order and stops at the same one whatever the chunking
+	const uint32_t n_steps = min(max(target / max(n_alive, 1u), 1u), max_steps);
+	if (blockIdx.x == 0 && threadIdx.x == 0) {
+		*next_alive_counter = 0;  // filled by this pass's k_composite
+		*steps_out = n_alive ? n_steps : 0u;
+	}
+	const uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / G;
+	const bool valid = i < n_alive;  // group-uniform
+	Payload* p = payloads + (valid ? i : 0);
+	v3 o = mk3(0.0f), d = mk3(1.0f);
+	float n = 0.0f;
+	uint32_t row = 0;  // the ray's SH row (its pixel index; written once per frame by k_render_init)
+	uint32_t budget = 0;
+	if (valid) {
+		o = mk3(p->o[0], p->o[1], p->o[2]);
+		d = mk3(p->d[0], p->d[1], p->d[2]);
+		n = p->n;
+		row = p->idx;
+		budget = ray_budget(k, 1.0f - rgba[i].w, p->alpha_last, n_steps, o, d, n);
+	}
+	uint32_t base;
+	bool exited;
+	const uint32_t j = march_ray<G>(k, valid, o, d, &n, row, budget, posdt, sray, k.sdt, sample_counter, 0xffffffffu, &base, &exited);
+	if (valid && (threadIdx.x % G) == 0) {
 		p->n_steps = j | (exited ? PAYLOAD_EXITED : 0u);
 		p->base = base;
 		if (!exited) p->n = n;
@@ -714,43 +742,16 @@ __device__ __forceinline__ void apply_glow(const RenderK& k, v3 pos, v3 cam_pos,
 	}
 }
 
-// composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
-// each thread composites its ray's samples of this pass in order, then the block appends the
-// ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
-// MODES: the render modes other than Shade (:626-638) replace a sample's colour -- AO: its alpha,
-// Positions / Depth: its position / camera depth, Normals: the normalised negative density
-// gradient; Cost counts the ray's composited samples in c.x (shade_kernel_nerf turns it into a
-// grey level, :1327-1330) as payload.n_steps = j + current_step does (:664-667).
+// composite_kernel_nerf's per-ray loop over one pass's samples of the ray (its n_steps slots from p.base): updates
+// p (max weight, alpha of the last sample), c and local_depth; returns whether the ray goes on -- neither opaque
+// (c.w > 1 - min_transmittance) nor out of the volume during the pass.  sdt: the pass's dt array (null: the rows' w).
 template <bool MODES>
-__global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
-                                                   const Payload* __restrict__ sp, const float4* __restrict__ srgba,
-                                                   const float* __restrict__ sdepth, const float4* __restrict__ posdt,
-                                                   const __half* __restrict__ out,
-                                                   Payload* __restrict__ dp, float4* __restrict__ drgba,
-                                                   float* __restrict__ ddepth, Payload* __restrict__ hp,
-                                                   float4* __restrict__ hrgba, float* __restrict__ hdepth,
-                                                   uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter,
-                                                   uint32_t* __restrict__ next_sample_counter,
-                                                   uint32_t* __restrict__ filled_counter) {
-	set_wave_priority(k.prio);
-	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
-	const uint32_t n_alive = *alive_in;
-	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-	Payload p;
-	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
-	float local_depth = 0.0f;
-	bool alive = false;
-	uint32_t filled = 0;
-	if (i < n_alive) {
-		p = sp[i];
-		c = srgba[i];
-		local_depth = sdepth[i];
-		alive = true;
-	}
-	if (alive) {
+__device__ __forceinline__ bool composite_ray(const RenderK& k, Payload& p, float4& c, float& local_depth,
+                                              const float4* __restrict__ posdt, const float* __restrict__ sdt,
+                                              const __half* __restrict__ out) {
+	{
 		const v3 cam_fwd = k.cam.c[2], cam_pos = k.cam.c[3];
 		const uint32_t actual = p.n_steps & ~PAYLOAD_EXITED;
-		filled = actual;
 		const size_t sbase = p.base;
 		// samples are loaded 4 ahead of their use (the loop is otherwise one dependent
 		// global-load latency per sample)
@@ -768,7 +769,7 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 				if (j0 + u < actual) {
 					const size_t s = sbase + j0 + u;
 					o2[u] = *reinterpret_cast<const uint2*>(out + 4 * s);
-					wdt[u] = k.sdt ? k.sdt[s] : reinterpret_cast<const float*>(posdt)[4 * s + 3];
+					wdt[u] = sdt ? sdt[s] : reinterpret_cast<const float*>(posdt)[4 * s + 3];
 				}
 			}
 #pragma unroll
@@ -837,7 +838,46 @@ __global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* _
 		if (MODES && k.mode == NGP_RENDER_MODE_COST && !done) c.x += (float)actual;
 		p.alpha_last = alpha_last;
 		// finished: opaque enough, or the ray left the volume during this pass
-		if (done || (p.n_steps & PAYLOAD_EXITED)) alive = false;
+		return !(done || (p.n_steps & PAYLOAD_EXITED));
+	}
+}
+
+// composite_kernel_nerf (testbed_nerf.cu:471-677) fused with compact_kernel_nerf (:1351-1374):
+// each thread composites its ray's samples of this pass in order, then the block appends the
+// ray to the next pass's alive buffer, or (finished with colour) to the hit buffer.
+// MODES: the render modes other than Shade (:626-638) replace a sample's colour -- AO: its alpha,
+// Positions / Depth: its position / camera depth, Normals: the normalised negative density
+// gradient; Cost counts the ray's composited samples in c.x (shade_kernel_nerf turns it into a
+// grey level, :1327-1330) as payload.n_steps = j + current_step does (:664-667).
+template <bool MODES>
+__global__ void __launch_bounds__(1024) k_composite(RenderK k, const uint32_t* __restrict__ alive_in,
+                                                   const Payload* __restrict__ sp, const float4* __restrict__ srgba,
+                                                   const float* __restrict__ sdepth, const float4* __restrict__ posdt,
+                                                   const __half* __restrict__ out,
+                                                   Payload* __restrict__ dp, float4* __restrict__ drgba,
+                                                   float* __restrict__ ddepth, Payload* __restrict__ hp,
+                                                   float4* __restrict__ hrgba, float* __restrict__ hdepth,
+                                                   uint32_t* __restrict__ alive_counter, uint32_t* __restrict__ hit_counter,
+                                                   uint32_t* __restrict__ next_sample_counter,
+                                                   uint32_t* __restrict__ filled_counter) {
+	set_wave_priority(k.prio);
+	if (blockIdx.x == 0 && threadIdx.x == 0) *next_sample_counter = 0;  // the next pass's k_generate reserves from it
+	const uint32_t n_alive = *alive_in;
+	const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+	Payload p;
+	float4 c = make_float4(0.f, 0.f, 0.f, 0.f);
+	float local_depth = 0.0f;
+	bool alive = false;
+	uint32_t filled = 0;
+	if (i < n_alive) {
+		p = sp[i];
+		c = srgba[i];
+		local_depth = sdepth[i];
+		alive = true;
+	}
+	if (alive) {
+		filled = p.n_steps & ~PAYLOAD_EXITED;
+		alive = composite_ray<MODES>(k, p, c, local_depth, posdt, k.sdt, out);
 	}
 	const bool hit = i < n_alive && !alive && c.w > 0.001f;
 	if (!MODES && k.hframe && i < n_alive && !alive) write_host_pixel(k, p.idx, c, hit);
@@ -1174,7 +1214,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		ps.coords.reserve(6 * pr.max_samples);  // rows [4 max] | SH rows [max] | dt [max]
 		ps.enc.reserve((size_t)m->lt.n_levels * pr.max_samples * m->lt.F);
 		ps.out.reserve(4 * pr.max_samples);
-		ps.counters.reserve(16);
+		ps.counters.reserve(16);  // [0, 8) the pass counters, [8, 16) debug (pipeline 0)
 		if (!ps.host_counter.ptr) {
 			// [HC_SLOTS][16] unpacked pass counters, [HC_COPYBACK, +8) copy-back slot,
 			// [HC_PUBLISHED, +HC_SLOTS * 16) the published words ([slot][8] x (tag << 32 | value));
@@ -1206,6 +1246,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	build_distance_fields(m, k.max_mip, s);
 	k.df = rs.df.ptr;
 	NGP_HIP_CHECK(hipMemsetAsync(rs.pipe[0].counters.ptr, 0, 8 * sizeof(uint32_t), s));
+
 	// the encoder's table, and corner records of its dense levels (read by every pipeline)
 	const __half* table = (a->use_inference_params ? m->infer16.ptr : m->params16.ptr) + m->n_mlp_params;
 	const __half* frags = a->use_inference_params ? m->frag_infer.ptr : m->frag_train.ptr;
@@ -1245,7 +1286,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		pr.k.dbg = dbg;
 		if (pr.n == 0) continue;
 		(k.lens_mode != LENS_PERSPECTIVE || k.dmap ? k_render_init<true> : k_render_init<false>)<<<div_up(pr.n_tiled, 256u), 256, 0, pr.s>>>(
-		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer, pr.ps->counters.ptr, rs.shrows.ptr);
+		    pr.k, pr.P(0), pr.C(0), pr.ps->depth[0].ptr, reinterpret_cast<float4*>(frame), depth_buffer,
+		    pr.ps->counters.ptr, rs.shrows.ptr);
 		pr.marching = true;
 	}
 	tm.end(NGP_TIMER_RENDER_MARCH, s, k.W * H_shard);
@@ -1275,7 +1317,8 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// pipeline stops once a read-back shows no alive rays (the pass enqueued meanwhile runs
 	// empty).  With two pipelines the host alternates between them, so each stream holds up
 	// to two enqueued passes while the host waits on the other's read-back.
-	const uint32_t MARCH_ITER = 10000;
+	// ngp_tuning.debug bit 4: a 40-step march budget (exercises the retire path of rays that run out of it)
+	const uint32_t MARCH_ITER = (tu.debug & 16u) ? 40u : 10000u;
 	const uint32_t lag = render_lag(tu);
 	// workgroup sizes: k_composite 512 (measured 0.5 % faster than 1024, 256 2 % slower), k_generate
 	// 512 (256 measured 4.5 % slower)
@@ -1383,16 +1426,19 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 		filled_total += last[3];
 		if (n_alive > 0) {
 			if (a->host_frame) *a->host_frame_complete = 0;  // their pixels were not streamed: the caller copies the frame
+			auto wait_copy = [&](void* dst, const void* src, size_t bytes) {
+				NGP_HIP_CHECK(hipMemcpyAsync(dst, src, bytes, hipMemcpyDeviceToHost, pr.s));
+				NGP_HIP_CHECK(hipEventRecord(pr.ps->events[0], pr.s));
+				hipError_t e;
+				while ((e = hipEventQuery(pr.ps->events[0])) == hipErrorNotReady) {
+				}
+				NGP_HIP_CHECK(e);
+			};
 			// march budget exhausted: still-alive rays are shaded with what they accumulated
 			k_retire<<<div_up(n_alive, 256), 256, 0, pr.s>>>(n_alive, pr.P(pr.cur), pr.C(pr.cur), pr.ps->depth[pr.cur].ptr,
 			                                                 pr.P(2), pr.C(2), pr.ps->depth[2].ptr, counters);
-			// copy-back of the counters -> slot [32, 40), then an event
-			NGP_HIP_CHECK(hipMemcpyAsync(pr.hc() + HC_COPYBACK, counters, 8 * sizeof(uint32_t), hipMemcpyDeviceToHost, pr.s));
-			NGP_HIP_CHECK(hipEventRecord(pr.ps->events[0], pr.s));
-			hipError_t e;
-			while ((e = hipEventQuery(pr.ps->events[0])) == hipErrorNotReady) {
-			}
-			NGP_HIP_CHECK(e);
+			// copy-back of the counters -> slot [HC_COPYBACK, +8), then an event
+			wait_copy(pr.hc() + HC_COPYBACK, counters, 8 * sizeof(uint32_t));
 			n_hit = pr.hc()[HC_COPYBACK + 2];
 		}
 		pr.ps->pass_tag = pr.base_tag + pr.pass;

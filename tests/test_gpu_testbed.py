@@ -823,3 +823,25 @@ def test_kernel_timers_measure_every_class(scene):
     ms, units, launches = C.c_double(), C.c_uint64(), C.c_uint32()
     A.check(lib.ngp_timing_read(h, A.TIMER["train_encode"], C.byref(ms), C.byref(units), C.byref(launches), 1))
     assert launches.value == 0 and ms.value == 0.0
+
+
+def test_render_retires_rays_out_of_march_budget(scene):
+    """With a 40-step march budget (ngp_tuning.debug bit 4) the rays still marching are retired with what they
+    accumulated (k_retire; the reference's NerfTracer stops after MARCH_ITER steps): the frame is finite, its pixels
+    equal the full render's wherever the ray finished inside the budget (render() copies the frame instead of streaming
+    it when rays were retired)."""
+    root, _, _ = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(root)
+    tb.reload_network_from_file("lego_L16F2.json")
+    tb.shall_train = True
+    for _ in range(60):
+        tb.train(1 << 16)
+    tb.set_camera_to_training_view(1)
+    full = tb.render(640, 360, 1, True).copy()
+    tb.set_tuning({"debug": 16})
+    cut = tb.render(640, 360, 1, True).copy()
+    tb.set_tuning({"debug": 0})
+    assert np.isfinite(cut).all()
+    same = (cut == full).all(-1)
+    assert 0.5 < same.mean() < 1.0, same.mean()  # some rays ran out of the budget, most finished inside it
