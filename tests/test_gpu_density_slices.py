@@ -144,7 +144,7 @@ def test_trained_field_against_the_reference_density_mosaic():
         D.train_to(tb, 35000)
         occ[seed] = D.testbed_volume(tb) >= 129
         del tb
-    ours = (D.coarse(occ[1337]) + D.coarse(occ[42])) / 2
+    ours = (D.coarse(occ[1337]) + D.coarse(occ[2024])) / 2
     cref = D.coarse(ref)
     ident, rank = D.orientation_ranking(ours, cref)
     seeds_corr = float(np.corrcoef(D.coarse(occ[1337]).ravel(), D.coarse(occ[2024]).ravel())[0, 1])
