@@ -367,7 +367,8 @@ enum {
  * default.  Per model; ngp_model_create starts from all zeros. */
 typedef struct ngp_tuning {
 	uint32_t render_pipelines;       /* ray pipelines on their own streams, 1..4; 0: 2 for frames of >= 2^16 rays */
-	uint32_t render_pass_samples;    /* a pipeline's sample-slot budget per march pass (<= 2^24); 0: 5 * 2^20 */
+	uint32_t render_pass_samples;    /* a pipeline's sample-slot budget per march pass (<= 2^24); 0: 6 * 2^20 for a volume
+	                                    (the last frame >= 12 samples per ray), else 3 * 2^20 */
 	uint32_t render_lanes;           /* lane budget from which k_generate picks lanes per ray; 0: 2^22 */
 	uint32_t render_first_steps;     /* per-ray sample cap of the first pass (doubling per pass); 0: 8 after a frame of >= 12 samples per ray, else 4 */
 	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 */
@@ -376,7 +377,7 @@ typedef struct ngp_tuning {
 	uint32_t render_composite_block; /* k_composite workgroup size (256, 512, 1024); 0: 512 */
 	uint32_t render_generate_block;  /* k_generate workgroup size (256, 512); 0: 512 */
 	uint32_t encode_dense_records;   /* render-site corner records of the dense levels: 0 on, 1 off */
-	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: 8 */
+	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: 6 for the render MLP's 64-sample steps, else 8 */
 	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics;
 	                                    bit 2: the chunked training forward stops rays at transmittance 0.999 (forces
 	                                    forward_early_stop_violations: exercises the discard-and-retry path);

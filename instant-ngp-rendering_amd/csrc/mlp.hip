@@ -1227,8 +1227,11 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		// 64-sample steps measured 0-2 % faster per frame; with one (surface scenes) the 32-sample steps 1-2 %
 		// (profiles/r04_mlp_tile_ab.txt): the renderer picks per frame (RenderScratch::mlp_tile)
 		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : m->rs.mlp_tile;
+		// the 64-sample steps beside the other pipeline's encoder: 6 workgroups per CU (13.60 vs 13.67 ms per fire frame
+		// against 8 with 6 M passes; profiles/r05_schedule_sweep.txt)
+		const uint32_t wg_render = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : 6u;
 		if (sh && a.F == 2 && pl && tile == 4)
-			launch_timed(k_mlp_infer_rf<N, 4, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 64 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
+			launch_timed(k_mlp_infer_rf<N, 4, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 64 * WAVES), cu_count() * wg_render), BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl && tile == 2)
 			launch_timed(k_mlp_infer_rf<N, 2, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl) launch_timed(k_mlp_infer_rf<N, 1, 2, false, 12, true>, grid, BLOCK, lds, s, a);

@@ -976,7 +976,7 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 
 // The march schedule (ngp_tuning; results do not depend on it):
 //  * lanes_target: the lane budget that picks lanes-per-ray in k_generate (4M);
-//  * pass_sample_target: a pipeline's sample slots per pass (5M; <= 16M: the MLP reads the
+//  * pass_sample_target: a pipeline's sample slots per pass (6M volumes, 3M surfaces; <= 16M: the MLP reads the
 //    encodings through raw buffers with 32-bit byte offsets, 64 B/sample);
 //  * first_pass_steps / max_steps_per_pass: the per-ray cap of the first pass doubles every pass
 //    up to the maximum (4 -> 32).  A ray's slots past its termination are wasted encoder and MLP
@@ -985,13 +985,16 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 //    waste and the pass count both low.  Inside the cap each ray's budget also follows its
 //    transmittance and the opacity of its last sample (sample_budget).
 static uint32_t lanes_target(const ngp_tuning& t) { return t.render_lanes ? t.render_lanes : 4u << 20; }
-static uint32_t pass_sample_target(const ngp_tuning& t) {
-	// 5 M: 13.78 vs 13.96 ms per frame against 4 M (6 M 13.82, 8 M 13.99; same weights, profiles/r03_pass_size_ab.txt)
-	return std::min<uint32_t>(t.render_pass_samples ? t.render_pass_samples : 5u << 20, 16u << 20);
-}
 // A volume's rays (the model's last frame above VOLUME_SAMPLES_PER_RAY network samples per ray) start with 8:
 // 13.69 vs 13.82 ms per fire frame; a surface scene's keep 4 (8: 2.19 vs 2.11 ms; profiles/r04_first_steps_ab.txt)
 constexpr float VOLUME_SAMPLES_PER_RAY = 12.0f;
+// A pipeline's sample slots per pass: 6 M for a volume (the model's last frame >= VOLUME_SAMPLES_PER_RAY samples per
+// ray), 3 M for a surface scene -- 13.67 vs 13.81 ms per fire frame against 5 M (7 M 13.69), 2.67 vs 2.73 ms on the
+// surface scene (4 M 2.71; profiles/r05_schedule_sweep.txt; round 3 had measured 5 M best for both)
+static uint32_t pass_sample_target(const ngp_tuning& t, float last_spr) {
+	const uint32_t def = last_spr >= VOLUME_SAMPLES_PER_RAY ? 6u << 20 : 3u << 20;
+	return std::min<uint32_t>(t.render_pass_samples ? t.render_pass_samples : def, 16u << 20);
+}
 static uint32_t first_pass_steps(const ngp_tuning& t, float last_spr) {
 	return t.render_first_steps ? t.render_first_steps : (last_spr >= VOLUME_SAMPLES_PER_RAY ? 8u : 4u);
 }
@@ -1170,7 +1173,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// the CUs (194 VGPRs: 2 waves per SIMD leave it room), 32 with one pipeline (110 VGPRs, 4 waves per SIMD)
 	rs.mlp_tile = n_pipes > 1 ? 4u : 2u;
 
-	const uint32_t target = pass_sample_target(tu), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu, rs.last_samples_per_ray), cap);
+	const uint32_t target = pass_sample_target(tu, rs.last_samples_per_ray), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu, rs.last_samples_per_ray), cap);
 	const bool debug = (tu.debug & 1u) != 0;
 	// per-ray sample budgets: headroom factor (default 1.0: measured 1 % faster than 1.5), < 0 = off
 	k.budget = !(tu.render_budget_scale < 0.0f);
