@@ -371,7 +371,7 @@ typedef struct ngp_tuning {
 	                                    (the last frame >= 12 samples per ray), else 3 * 2^20 */
 	uint32_t render_lanes;           /* lane budget from which k_generate picks lanes per ray; 0: 2^22 */
 	uint32_t render_first_steps;     /* per-ray sample cap of the first pass (doubling per pass); 0: 8 after a frame of >= 12 samples per ray, else 4 */
-	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 */
+	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 for a volume, 24 for a surface scene */
 	uint32_t render_lag;             /* passes a pipeline runs ahead of its counter read-backs, 2..4; 0: 3 */
 	float render_budget_scale;       /* headroom of the per-ray transmittance budget; 0: 1.0; < 0: no budget */
 	uint32_t render_composite_block; /* k_composite workgroup size (256, 512, 1024); 0: 512 */

@@ -979,7 +979,7 @@ static uint32_t rows_owned(uint32_t H, uint32_t idx, uint32_t count, uint32_t ro
 //  * pass_sample_target: a pipeline's sample slots per pass (6M volumes, 3M surfaces; <= 16M: the MLP reads the
 //    encodings through raw buffers with 32-bit byte offsets, 64 B/sample);
 //  * first_pass_steps / max_steps_per_pass: the per-ray cap of the first pass doubles every pass
-//    up to the maximum (4 -> 32).  A ray's slots past its termination are wasted encoder and MLP
+//    up to the maximum (surfaces 4 -> 24, volumes 8 -> 32).  A ray's slots past its termination are wasted encoder and MLP
 //    work: most rays of a surface scene stop within a few samples of their first occupied one,
 //    while rays through a volume need many, so short first passes and geometric growth keep the
 //    waste and the pass count both low.  Inside the cap each ray's budget also follows its
@@ -998,7 +998,11 @@ static uint32_t pass_sample_target(const ngp_tuning& t, float last_spr) {
 static uint32_t first_pass_steps(const ngp_tuning& t, float last_spr) {
 	return t.render_first_steps ? t.render_first_steps : (last_spr >= VOLUME_SAMPLES_PER_RAY ? 8u : 4u);
 }
-static uint32_t max_steps_per_pass(const ngp_tuning& t) { return t.render_max_steps ? t.render_max_steps : 32u; }
+// the per-ray cap of any pass: 32 for a volume, 24 for a surface scene (2.63 vs 2.66 ms per frame; 16: 2.69;
+// profiles/r05_schedule_sweep.txt)
+static uint32_t max_steps_per_pass(const ngp_tuning& t, float last_spr) {
+	return t.render_max_steps ? t.render_max_steps : (last_spr >= VOLUME_SAMPLES_PER_RAY ? 32u : 24u);
+}
 
 // rows r < h_shard of a shard with (r / 8) % pipe_count == pipe_index
 static uint32_t pipe_rows(uint32_t h_shard, uint32_t pipe_index, uint32_t pipe_count) {
@@ -1173,7 +1177,7 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// the CUs (194 VGPRs: 2 waves per SIMD leave it room), 32 with one pipeline (110 VGPRs, 4 waves per SIMD)
 	rs.mlp_tile = n_pipes > 1 ? 4u : 2u;
 
-	const uint32_t target = pass_sample_target(tu, rs.last_samples_per_ray), cap = max_steps_per_pass(tu), cap0 = std::min(first_pass_steps(tu, rs.last_samples_per_ray), cap);
+	const uint32_t target = pass_sample_target(tu, rs.last_samples_per_ray), cap = max_steps_per_pass(tu, rs.last_samples_per_ray), cap0 = std::min(first_pass_steps(tu, rs.last_samples_per_ray), cap);
 	const bool debug = (tu.debug & 1u) != 0;
 	// per-ray sample budgets: headroom factor (default 1.0: measured 1 % faster than 1.5), < 0 = off
 	k.budget = !(tu.render_budget_scale < 0.0f);
