@@ -372,7 +372,7 @@ typedef struct ngp_tuning {
 	uint32_t render_lanes;           /* lane budget from which k_generate picks lanes per ray; 0: 2^22 */
 	uint32_t render_first_steps;     /* per-ray sample cap of the first pass (doubling per pass); 0: 8 after a frame of >= 12 samples per ray, else 4 */
 	uint32_t render_max_steps;       /* per-ray sample cap of any pass; 0: 32 for a volume, 24 for a surface scene */
-	uint32_t render_lag;             /* passes a pipeline runs ahead of its counter read-backs, 2..4; 0: 3 */
+	uint32_t render_lag;             /* passes a pipeline runs ahead of its counter read-backs, 2..4; 0: 2 */
 	float render_budget_scale;       /* headroom of the per-ray transmittance budget; 0: 1.0; < 0: no budget */
 	uint32_t render_composite_block; /* k_composite workgroup size (256, 512, 1024); 0: 512 */
 	uint32_t render_generate_block;  /* k_generate workgroup size (256, 512); 0: 512 */
@@ -394,7 +394,7 @@ typedef struct ngp_tuning {
 	uint32_t render_skip_unfilled;   /* 1 = the render MLP skips 16-sample column tiles of slots no ray filled (marked
 	                                    by k_generate), 2 = computes every reserved slot; 0: the default (1) */
 	uint32_t render_exit_cap;        /* 1 = a ray reserves at most the lattice points left to its AABB exit in a march
-	                                    pass, 2 = the per-ray cap alone; 0: the default */
+	                                    pass, 2 = the per-ray cap alone; 0: the default (2) */
 	uint32_t render_priority;        /* wave issue priority (s_setprio 0..3) of the render kernels sharing the CUs:
 	                                    bits 0-1 the encoder, 2-3 the MLP, 4-5 the march kernels; 0: all 0 */
 	uint32_t render_host_frame;      /* Testbed::render into host memory: 1 = pixels streamed by the kernels

@@ -1035,7 +1035,9 @@ constexpr uint32_t HC_SLOTS = 4, HC_COPYBACK = 16 * HC_SLOTS, HC_PUBLISHED = 128
 
 // passes a pipeline runs ahead of its counter read-backs (ngp_tuning.render_lag, 2 .. HC_SLOTS)
 static uint32_t render_lag(const ngp_tuning& t) {
-	return t.render_lag >= 2 ? std::min<uint32_t>(t.render_lag, HC_SLOTS) : 3u;  // 3: -0.6 % against 2 (same weights)
+	// 2: 13.58 vs 13.66 ms per fire frame against 3, 2.60 vs 2.66 on the surface scene (round 5's schedule; round 3 had
+	// measured 3 0.6 % faster; profiles/r05_schedule_sweep.txt)
+	return t.render_lag >= 2 ? std::min<uint32_t>(t.render_lag, HC_SLOTS) : 2u;
 }
 
 namespace {
@@ -1182,8 +1184,9 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	// per-ray sample budgets: headroom factor (default 1.0: measured 1 % faster than 1.5), < 0 = off
 	k.budget = !(tu.render_budget_scale < 0.0f);
 	k.budget_scale = tu.render_budget_scale > 0.0f ? tu.render_budget_scale : 1.0f;
-	// per-pass budgets capped by the lattice points left to the ray's exit (ngp_tuning.render_exit_cap: 1 on, 2 off)
-	k.exit_cap = tu.render_exit_cap != 2 ? 1 : 0;
+	// per-pass budgets capped by the lattice points left to the ray's exit (ngp_tuning.render_exit_cap: 1 on, 2 off; off
+	// by default since round 5's schedule: with read-back lag 2, 13.51 vs 13.58 ms per fire frame, 2.597 vs 2.603 surface)
+	k.exit_cap = tu.render_exit_cap == 1 ? 1 : 0;
 	// unfilled slots marked for the render MLP to skip (ngp_tuning.render_skip_unfilled: 1 on, 2 off; 0 the
 	// default); Normals runs the MLP backward over every slot, so it keeps real rows
 	const bool skip_unfilled = tu.render_skip_unfilled != 2 && k.mode != NGP_RENDER_MODE_NORMALS;
