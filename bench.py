@@ -63,9 +63,9 @@ def parse():
     p.add_argument("--config-e-pretrain", type=int, default=500)
     p.add_argument("--render-in-hbm", type=int, default=5,
                    help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
-    p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r05_final2_surface_pmc_traffic.json"),
+    p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r05_final3_surface_pmc_traffic.json"),
                    help="PMC traffic summary of the surface-scene bench (tools/pmc_traffic.py)")
-    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05_final2_pmc_traffic.json"),
+    p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05_final3_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
 
