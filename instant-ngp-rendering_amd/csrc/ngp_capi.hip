@@ -257,6 +257,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		m->grid_grads16.release();
 		m->grid_grads64.release();
 		if (m->sync_event) (void)hipEventDestroy(m->sync_event);
+		if (m->stats_host) (void)hipHostFree(m->stats_host);
 		m->params16.release();
 		m->infer16.release();
 		m->adam_steps.release();
@@ -559,8 +560,11 @@ ngp_status ngp_train_read_stats(ngp_model* m, ngp_train_stats* st, ngp_stream s)
 		require(m && st, "null argument");
 		std::memset(st, 0, sizeof(*st));
 		if (!m->ts.counters.ptr) return;
-		uint32_t c[16];
-		NGP_HIP_CHECK(hipMemcpyAsync(c, m->ts.counters.ptr, sizeof(c), hipMemcpyDeviceToHost, S(s)));
+		// into pinned memory: a pageable destination is staged and copied by the runtime before the
+		// call returns, which the step's critical path paid every step
+		if (!m->stats_host) NGP_HIP_CHECK(hipHostMalloc((void**)&m->stats_host, 16 * sizeof(uint32_t), hipHostMallocDefault));
+		const uint32_t* c = m->stats_host;
+		NGP_HIP_CHECK(hipMemcpyAsync(m->stats_host, m->ts.counters.ptr, 16 * sizeof(uint32_t), hipMemcpyDeviceToHost, S(s)));
 		wait_stream(m, S(s));
 		st->n_rays = m->ts.last_n_rays;
 		st->measured_batch_size_before_compaction = c[0];

@@ -234,6 +234,13 @@ struct DevBuf {
 		NGP_HIP_CHECK(hipMalloc((void**)&ptr, std::max<size_t>(count, 1) * sizeof(T)));
 		n = count;
 	}
+	// per-step scratch whose size follows the adaptive ray / sample counts: grow with an eighth of
+	// headroom, so a count that creeps upward does not free and reallocate (a hipFree waits for the
+	// device) every time it sets a new maximum
+	void grow(size_t count) {
+		if (count <= n) return;
+		reserve((count + count / 8 + 4095) & ~(size_t)4095);
+	}
 	void release() {
 		if (ptr) (void)hipFree(ptr);
 		ptr = nullptr;
@@ -438,6 +445,7 @@ struct ngp_model {
 	bool stats_pending = false;
 	ngp::KernelTimers timers;
 	hipEvent_t sync_event = nullptr;  // host read-backs spin on it (ngp::wait_stream)
+	uint32_t* stats_host = nullptr;   // pinned (hipHostMalloc): the training counters' read-back
 	uint32_t last_n_rays = 0;
 };
 

@@ -1744,19 +1744,19 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			throw std::invalid_argument("training: max_samples too large for one rank's 32-bit sample buffers "
 			                            "(lower the batch per rank)");
 	}
-	ts.ray_numsteps.reserve(2 * (size_t)R);
-	ts.ray_compacted.reserve(2 * (size_t)R);
-	ts.ray_state.reserve(8 * (size_t)R);
-	ts.ray_loss_state.reserve(8 * (size_t)R);
-	ts.loss.reserve(R);
-	ts.coords.reserve(8 * (size_t)MS);
-	ts.enc.reserve((size_t)L * MS * F);
-	ts.mlp_out.reserve(4 * (size_t)MS);
+	ts.ray_numsteps.grow(2 * (size_t)R);
+	ts.ray_compacted.grow(2 * (size_t)R);
+	ts.ray_state.grow(8 * (size_t)R);
+	ts.ray_loss_state.grow(8 * (size_t)R);
+	ts.loss.grow(R);
+	ts.coords.grow(8 * (size_t)MS);
+	ts.enc.grow((size_t)L * MS * F);
+	ts.mlp_out.grow(4 * (size_t)MS);
 	ts.ccoords.reserve(8 * (size_t)B);
 	// n_extra_dims > 0: each sample's image picks its latent-code row (NerfCoordinate extra dims, src/testbed_nerf.cu:824)
 	const bool xd = m->cfg.n_extra_dims > 0;
 	if (xd) {
-		ts.simg.reserve(MS);
+		ts.simg.grow(MS);
 		ts.cimg.reserve(B);
 		if (t->extra_dims_gradient) ts.dextra.reserve(16 * (size_t)B);
 	}
@@ -1766,10 +1766,10 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	ts.cweight.reserve(B);
 	ts.csrc.reserve(B);
 	ts.denc.reserve((size_t)L * B * F);
-	ts.block_sums.reserve(div_up(std::max(R, 1u), 1024) + 16);
+	ts.block_sums.grow(div_up(std::max(R, 1u), 1024) + 16);
 	ts.counters.reserve(16);
-	ts.scan_a.reserve(2 * (size_t)R);
-	ts.scan_b.reserve(2 * (size_t)R);
+	ts.scan_a.grow(2 * (size_t)R);
+	ts.scan_b.grow(2 * (size_t)R);
 	DevBuf<uint32_t>& counts = ts.scan_a;
 	ts.last_n_rays = R;
 	ts.last_target = B;
@@ -1893,15 +1893,15 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		const uint32_t cap[TRAIN_CHUNKS] = {std::min(16 * R, MS), std::min(32 * R, MS), MS};
 		const uint32_t off[TRAIN_CHUNKS] = {0, cap[0], cap[0] + cap[1]};
 		const uint32_t MSE = off[2] + cap[2];
-		ts.epos.reserve(4 * (size_t)MSE);
-		ts.edir.reserve(4 * (size_t)MSE);
-		ts.eenc.reserve((size_t)L * MSE * F);
-		ts.eout.reserve(4 * (size_t)MSE);
-		ts.eidx.reserve(MS);
-		if (xd) ts.eimg.reserve(MSE);
-		ts.ray_T.reserve(R);
-		ts.ray_eval.reserve(R);
-		ts.ray_ebase.reserve(R);
+		ts.epos.grow(4 * (size_t)MSE);
+		ts.edir.grow(4 * (size_t)MSE);
+		ts.eenc.grow((size_t)L * MSE * F);
+		ts.eout.grow(4 * (size_t)MSE);
+		ts.eidx.grow(MS);
+		if (xd) ts.eimg.grow(MSE);
+		ts.ray_T.grow(R);
+		ts.ray_eval.grow(R);
+		ts.ray_ebase.grow(R);
 		ChunkArgs c{};
 		c.n_rays = R;
 		c.numsteps = ts.ray_numsteps.ptr;
@@ -1978,7 +1978,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	la.exposure = t->exposure;
 	la.exposure_grad = t->exposure_gradient;
 	la.exposure_fix = ts.fixed && t->exposure_gradient ? ts.img_fix.ptr : nullptr;
-	ts.ray_aux.reserve(4 * (size_t)R);
+	ts.ray_aux.grow(4 * (size_t)R);
 	la.ray_aux = reinterpret_cast<float4*>(ts.ray_aux.ptr);
 	la.error_map_rx = t->error_map_res[0];
 	la.error_map_ry = t->error_map_res[1];
@@ -2025,12 +2025,12 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		la.sharp_rx = t->sharpness_res[0];
 		la.sharp_ry = t->sharpness_res[1];
 		la.sharp_grid = t->sharpness_grid;
-		ts.ray_hit.reserve(4 * (size_t)R);
+		ts.ray_hit.grow(4 * (size_t)R);
 		la.ray_hit = reinterpret_cast<float4*>(ts.ray_hit.ptr);
 	}
 	la.depth_loss_type = t->depth_loss_type;
 	if (la.depth_lambda > 0.0f) {
-		ts.ray_depth.reserve(2 * (size_t)R);
+		ts.ray_depth.grow(2 * (size_t)R);
 		la.ray_depth = reinterpret_cast<float2*>(ts.ray_depth.ptr);
 	}
 	tm.begin(NGP_TIMER_TRAIN_LOSS, s);

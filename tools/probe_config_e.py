@@ -19,12 +19,16 @@ from test_gpu_config_e import fox_aabb64  # noqa: E402
 
 def frame(tb, lib, h, label, n=3):
     tb.render_to_device(1920, 1080, 1, True)
-    for name in A.TIMERS:
-        lib.ngp_timing_read(h, A.TIMER[name], None, None, None, 1)
+    A.check(lib.ngp_timing_enable(h, 0))  # frame time without the per-dispatch timer events
     t0 = time.perf_counter()
     for _ in range(n):
         tb.render_to_device(1920, 1080, 1, True)
     dt = (time.perf_counter() - t0) / n
+    A.check(lib.ngp_timing_enable(h, -1))
+    for name in A.TIMERS:
+        lib.ngp_timing_read(h, A.TIMER[name], None, None, None, 1)
+    for _ in range(n):
+        tb.render_to_device(1920, 1080, 1, True)
     res = {}
     for name in ("render_march", "render_encode", "render_mlp"):
         ms, u, k = C.c_double(), C.c_uint64(), C.c_uint32()
@@ -51,8 +55,11 @@ def main():
         tb.set_tuning({"debug": 0})
         A.check(lib.ngp_timing_enable(h, -1))
         frame(tb, lib, h, "default")
-        for kw in ({"render_pipelines": 1}, {"render_pipelines": 3}, {"render_lanes": 1 << 24}, {"render_lanes": 1 << 20},
-                   {"render_max_steps": 64}, {"render_first_steps": 16}, {"render_pass_samples": 10 << 20}):
+        variants = ({"render_pipelines": 1}, {"render_pipelines": 3}, {"render_lanes": 1 << 23}, {"render_lanes": 1 << 21},
+                    {"render_max_steps": 64}, {"render_max_steps": 16}, {"render_first_steps": 16}, {"render_pass_samples": 10 << 20},
+                    {"render_pass_samples": 4 << 20}, {"render_lag": 3}, {"render_exit_cap": 1}, {"mlp_workgroups_per_cu": 8})
+        for kw in variants + variants:  # twice: the second round shows the spread
+            frame(tb, lib, h, "default")
             tb.set_tuning(kw)
             frame(tb, lib, h, str(kw))
             tb.set_tuning({k: 0 for k in kw})

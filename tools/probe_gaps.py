@@ -1,7 +1,7 @@
 """Probe (GPU, diagnostic, run under rocprofv3 --kernel-trace): idle gaps between a 1080p frame's kernels with the kernel
 timers off or on (ngp_timing_enable), on bench.py's surface scene (one ray pipeline).  Renders 4 frames; summarise the
-trace with tools/gap_summary.py.
-  python tools/probe_gaps.py [--timers MASK]"""
+trace with tools/gap_summary.py.  --train: 8 training steps instead (gap_summary.py ... k_sample_count).
+  python tools/probe_gaps.py [--timers MASK] [--train]"""
 import argparse
 import ctypes as C
 import os
@@ -16,6 +16,7 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--timers", type=int, default=0)
     p.add_argument("--scene", default="synthetic")
+    p.add_argument("--train", action="store_true", help="trace 8 training steps instead of frames")
     a = p.parse_args()
     import torch
     torch.cuda.set_device(0)
@@ -31,11 +32,19 @@ def main():
     tb.shall_train = True
     for _ in range(300):
         tb.train(1 << 18)
-    tb.shall_train = False
-    tb.set_camera_to_training_view(3)
     lib = A.load()
     h = C.c_void_p(tb.model_handle)
     A.check(lib.ngp_timing_enable(h, a.timers))
+    if a.train:
+        tb.sync()
+        t0 = time.perf_counter()
+        for _ in range(8):
+            tb.train(1 << 18)
+        tb.sync()
+        print(f"timers {a.timers}: {(time.perf_counter() - t0) / 8 * 1e6:.1f} us per training step", flush=True)
+        return
+    tb.shall_train = False
+    tb.set_camera_to_training_view(3)
     tb.render_to_device(1920, 1080, 1, True)
     tb.sync()
     t0 = time.perf_counter()
