@@ -215,6 +215,7 @@ struct SamplerArgs {
 	const uint8_t* df;   // octant distance fields of mip 0 (aabb_scale 1 only; null: the jump chain)
 	const uint32_t* total;   // the scan's sample total
 	uint32_t* total_capped;  // k_sample_write: min(total, cap) for the kernels after the sampler
+	uint32_t* clear16;       // k_sample_count: the step's 16 counter words, zeroed (no memset dispatch in front of the step)
 };
 
 // Image and pixel of global training ray gi from its pcg32 stream (already advanced to
@@ -407,6 +408,8 @@ template <bool GENERAL, uint32_t G>
 __global__ void __launch_bounds__(256) k_sample_count(SamplerArgs a) {
 	const uint32_t lane = threadIdx.x & 63u, r = lane % G, g0 = lane - r;
 	const uint32_t i = blockIdx.x * (256u / G) + threadIdx.x / G;
+	// the step's first kernel: every later user of the counters runs after it in stream order
+	if (blockIdx.x == 0 && threadIdx.x < 16u) a.clear16[threadIdx.x] = 0u;
 	if (i >= a.n_rays) return;  // group-uniform
 	v3 o, d;
 	float n0;
@@ -1807,7 +1810,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 		NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads64.ptr, 0, m->n_grid_params * sizeof(long long), s));
 	}
 
-	NGP_HIP_CHECK(hipMemsetAsync(ts.counters.ptr, 0, 16 * sizeof(uint32_t), s));
+	// the step's counters are zeroed by k_sample_count, its first kernel (sa.clear16)
 
 	SamplerArgs sa{};
 	sa.images = t->images;
@@ -1839,6 +1842,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	sa.ray_state = ts.ray_state.ptr;
 	sa.coords = ts.coords.ptr;
 	sa.simg = xd ? ts.simg.ptr : nullptr;
+	sa.clear16 = ts.counters.ptr;
 	if (t->distortion_map && t->distortion_res[0] && t->distortion_res[1]) {
 		sa.dmap = t->distortion_map;
 		sa.drx = t->distortion_res[0];

@@ -32,3 +32,12 @@ for a in anchors[-steps:]:
     for st, en, fn in api:
         if prev_end - 20000 <= st <= first[0]:
             print(f"   {(st - prev_end) / 1e3:8.1f} us  {(en - st) / 1e3:7.1f} us  {fn}")
+
+# the last full step as one timeline: GPU operations (start, duration, idle gap before) and HIP API calls
+a, b = anchors[-2], anchors[-1]
+t0 = gpu[a][0]
+ev = [(g[0], "GPU", f"{(g[1] - g[0]) / 1e3:7.1f} us  {g[2]}") for g in gpu[a - 3:b + 1]]
+ev += [(st, "API", f"{(en - st) / 1e3:7.1f} us  {fn}") for st, en, fn in api if gpu[a - 3][0] <= st <= gpu[b][0]]
+print("== last step timeline (us from its k_sample_count)")
+for t, kind, txt in sorted(ev):
+    print(f"{(t - t0) / 1e3:9.1f}  {kind}  {txt}")
