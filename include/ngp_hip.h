@@ -385,8 +385,9 @@ typedef struct ngp_tuning {
 	                                    (forces sample_capacity_overflow and the retry with grown buffers);
 	                                    bit 4: renders stop marching after 40 lattice steps per ray (the retire path) */
 	uint32_t encode_streaming;       /* hash encoder (F = 2 planes): 0 = non-temporal encoding stores (the default), 1 = plain */
-	uint32_t grid_unsorted;          /* 1: the density-grid update encodes its samples in drawing order (0: sorted
-	                                    by cell, coherent gathers; same grid) */
+	uint32_t grid_unsorted;          /* density-grid update sample order (the same grid either way): 0 = bucketed by
+	                                    cell (top 14 Morton bits; coherent gathers), 1 = drawing order, 2 = fully sorted
+	                                    by cell (hipCUB radix sort) */
 	uint32_t render_mlp_tile;        /* render MLP samples per wave step: 1 = 16, 2 = 32, 4 = 64; 0: 64 with two or more
 	                                    ray pipelines, 32 with one */
 	uint32_t encode_xcd_regions;     /* four-levels-per-thread hash encoder: 0 = each XCD encodes one contiguous eighth of

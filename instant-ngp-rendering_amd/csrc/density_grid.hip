@@ -215,6 +215,60 @@ __global__ void k_gather_rows(uint32_t n, const uint32_t* __restrict__ perm, con
 	if (i < n) dst[i] = src[perm[i]];
 }
 
+// Bucketed cell sort (ngp_tuning.grid_unsorted 0): the samples only need neighbouring lanes in neighbouring cells, not a
+// total order, so they are bucketed by the top 14 bits of the cascade-major Morton key (2^21 / 2^14 = 128 cells, an
+// 8x4x4 block of the finest cascade per bucket) in three kernels -- ranks from returning atomics, one-block scan, scatter
+// -- instead of a full radix sort (~20 launches, ~200 us per update).  The order inside a bucket follows the atomics'
+// arrival; the splat is a max per cell, so the grid does not depend on it.
+constexpr uint32_t GRID_BUCKET_BITS = 14, GRID_BUCKETS = 1u << GRID_BUCKET_BITS;
+
+__global__ void __launch_bounds__(256) k_bucket_rank(uint32_t n, const uint32_t* __restrict__ keys, uint32_t shift,
+                                                     uint32_t* __restrict__ hist, uint32_t* __restrict__ rank) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i < n) rank[i] = atomicAdd(hist + (keys[i] >> shift), 1u);
+}
+
+// exclusive scan of the bucket counts (one block, 16 buckets per thread); leaves the counts zero for the next update
+__global__ void __launch_bounds__(1024) k_bucket_scan(uint32_t* __restrict__ hist, uint32_t* __restrict__ base) {
+	constexpr uint32_t PER = GRID_BUCKETS / 1024u;
+	__shared__ uint32_t wave_sum[16];
+	const uint32_t t = threadIdx.x, lane = t & 63u, w = t >> 6;
+	uint32_t c[PER], sum = 0;
+#pragma unroll
+	for (uint32_t k = 0; k < PER; ++k) {
+		c[k] = hist[t * PER + k];
+		hist[t * PER + k] = 0u;
+		sum += c[k];
+	}
+	uint32_t incl = sum;  // inclusive scan over the wave
+#pragma unroll
+	for (uint32_t off = 1; off < 64; off <<= 1) {
+		const uint32_t v = __shfl_up(incl, off, 64);
+		if (lane >= off) incl += v;
+	}
+	if (lane == 63) wave_sum[w] = incl;
+	__syncthreads();
+	uint32_t prefix = 0;
+	for (uint32_t k = 0; k < w; ++k) prefix += wave_sum[k];
+	uint32_t run = prefix + incl - sum;
+#pragma unroll
+	for (uint32_t k = 0; k < PER; ++k) {
+		base[t * PER + k] = run;
+		run += c[k];
+	}
+}
+
+__global__ void __launch_bounds__(256) k_bucket_scatter(uint32_t n, const uint32_t* __restrict__ keys, uint32_t shift,
+                                                        const uint32_t* __restrict__ base, const uint32_t* __restrict__ rank,
+                                                        const float4* __restrict__ pos, uint32_t* __restrict__ skeys,
+                                                        float4* __restrict__ spos) {
+	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
+	if (i >= n) return;
+	const uint32_t key = keys[i], dst = base[key >> shift] + rank[i];
+	skeys[dst] = key;
+	spos[dst] = pos[i];
+}
+
 void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 	GridState& g = m->gs;
 	const uint32_t n_cascades = a->max_cascade + 1;
@@ -254,11 +308,28 @@ void run_grid_evaluate(ngp_model* m, const ngp_grid_args* a, hipStream_t s) {
 	if (cnt) {
 		const float* pos = g.positions.ptr + 4 * (size_t)first;
 		const uint32_t* idx = g.indices.ptr + first;
+		// the samples are drawn in hash order, so the encoder's gathers were incoherent (2.6x the
+		// algorithmic fetch, r02); sorted by cell index (cascade-major Morton order) neighbouring lanes
+		// share corners.  The splat is a max per cell: the result does not depend on the order.
+		const uint32_t bits = 21u + (uint32_t)std::ceil(std::log2((double)n_cascades));
 		if (m->tuning.grid_unsorted == 0) {
-			// the samples are drawn in hash order, so the encoder's gathers were incoherent (2.6x the
-			// algorithmic fetch, r02); sorted by cell index (cascade-major Morton order) neighbouring lanes
-			// share corners.  The splat is a max per cell: the result does not depend on the order.
-			const uint32_t bits = 21u + (uint32_t)std::ceil(std::log2((double)n_cascades));
+			g.skeys.reserve(cnt);
+			g.perm_in.reserve(cnt);
+			g.spos.reserve(4 * (size_t)cnt);
+			if (!g.bucket_hist.ptr) {
+				g.bucket_hist.reserve(GRID_BUCKETS);
+				NGP_HIP_CHECK(hipMemsetAsync(g.bucket_hist.ptr, 0, GRID_BUCKETS * sizeof(uint32_t), s));
+			}
+			g.bucket_base.reserve(GRID_BUCKETS);
+			const uint32_t shift = bits - GRID_BUCKET_BITS;
+			k_bucket_rank<<<div_up(cnt, 256), 256, 0, s>>>(cnt, idx, shift, g.bucket_hist.ptr, g.perm_in.ptr);
+			k_bucket_scan<<<1, 1024, 0, s>>>(g.bucket_hist.ptr, g.bucket_base.ptr);
+			k_bucket_scatter<<<div_up(cnt, 256), 256, 0, s>>>(cnt, idx, shift, g.bucket_base.ptr, g.perm_in.ptr,
+			                                                  reinterpret_cast<const float4*>(pos), g.skeys.ptr,
+			                                                  reinterpret_cast<float4*>(g.spos.ptr));
+			pos = g.spos.ptr;
+			idx = g.skeys.ptr;
+		} else if (m->tuning.grid_unsorted == 2) {
 			g.skeys.reserve(cnt);
 			g.perm_in.reserve(cnt);
 			g.perm.reserve(cnt);

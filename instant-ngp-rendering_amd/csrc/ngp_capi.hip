@@ -77,7 +77,7 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->encode_dense_records <= 1, "encode_dense_records must be 0 or 1");
 	require(t->mlp_workgroups_per_cu <= 32, "mlp_workgroups_per_cu must be <= 32");
 	require(t->encode_streaming <= 1, "encode_streaming must be 0 or 1");
-	require(t->grid_unsorted <= 1, "grid_unsorted must be 0 or 1");
+	require(t->grid_unsorted <= 2, "grid_unsorted must be 0, 1 or 2");
 	require(t->render_mlp_tile == 0 || t->render_mlp_tile == 1 || t->render_mlp_tile == 2 || t->render_mlp_tile == 4,
 	        "render_mlp_tile must be 0, 1, 2 or 4");
 	require(t->encode_xcd_regions <= 1, "encode_xcd_regions must be 0 or 1");
@@ -277,6 +277,7 @@ ngp_status ngp_model_destroy(ngp_model* m) {
 		g.grid.release(); g.tmp.release(); g.bitfield.release(); g.mean.release(); g.sum.release();
 		g.positions.release(); g.indices.release(); g.enc.release(); g.out.release();
 		g.skeys.release(); g.perm_in.release(); g.perm.release(); g.sort_tmp.release(); g.spos.release();
+		g.bucket_hist.release(); g.bucket_base.release();
 		m->rs.release();
 		m->timers.release();
 		m->zero_extra.release();

@@ -333,6 +333,7 @@ struct GridState {
 	// the evaluated samples in cell (Morton) order: sort keys / permutation in and out, the
 	// positions gathered in that order, radix-sort scratch
 	DevBuf<uint32_t> skeys, perm_in, perm, sort_tmp;
+	DevBuf<uint32_t> bucket_hist, bucket_base;  // the bucketed cell sort (GRID_BUCKETS; hist kept zero between updates)
 	DevBuf<float> spos;        // [n][4]
 	uint32_t n_cascades = 0;
 	uint64_t version = 0;  // bumped whenever the bitfield may have changed (render caches derive from it)

@@ -479,11 +479,11 @@ def test_density_grid_update_matches_oracle(cfg_kw, aabb_scale, lens):
 
 @pytest.mark.parametrize("aabb_scale", [1, 16])
 def test_density_grid_update_sorted_samples_match_drawing_order(aabb_scale):
-    """The grid update encodes its samples sorted by cell (coherent gathers; ngp_tuning.grid_unsorted = 0)
-    -- the splat is a max per cell, so the grid, mean and bitfield are bit-identical to evaluating them in
-    drawing order (grid_unsorted = 1)."""
+    """The grid update encodes its samples bucketed by cell (coherent gathers; ngp_tuning.grid_unsorted = 0) or
+    fully sorted (2) -- the splat is a max per cell, so the grid, mean and bitfield are bit-identical to evaluating
+    them in drawing order (grid_unsorted = 1)."""
     out = {}
-    for unsorted in (1, 0):
+    for unsorted in (1, 0, 2):
         g, o, rng = pair(dict(CFG_B, aabb_scale=aabb_scale), grid_scale=1.0)
         try:
             g.set_tuning(grid_unsorted=unsorted)
@@ -503,8 +503,9 @@ def test_density_grid_update_sorted_samples_match_drawing_order(aabb_scale):
             out[unsorted] = (gg, gb)
         finally:
             g.close()
-    np.testing.assert_array_equal(out[0][0], out[1][0])
-    np.testing.assert_array_equal(out[0][1], out[1][1])
+    for k in (0, 2):
+        np.testing.assert_array_equal(out[k][0], out[1][0])
+        np.testing.assert_array_equal(out[k][1], out[1][1])
     assert (out[0][0] > 0).mean() > 0.01  # the update wrote densities
 
 
