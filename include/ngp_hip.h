@@ -403,6 +403,9 @@ typedef struct ngp_tuning {
 	uint32_t train_chunk_lanes;      /* lanes per ray of the chunked training forward's k_train_chunk (4, 8, 16, 32 or 64);
 	                                    0: 64 for batches of <= 4096 rays, else 16 */
 	uint32_t train_sampler_lanes;    /* lanes per ray of the training sampler's two passes (8, 16, 32 or 64); 0: 64 */
+	uint32_t render_mlp_pipeline;    /* render MLP load pipeline: 1 = round-5 ring (a tile's SH rows fetched right after its
+	                                    row indices), 2 = decoupled (row indices two tiles ahead, encodings one, SH rows
+	                                    one), 3 = decoupled with encodings two tiles ahead; 0: the default (2) */
 } ngp_tuning;
 
 /* --- lifecycle -------------------------------------------------------------------- */
@@ -438,6 +441,14 @@ ngp_status ngp_model_infer(ngp_model* model, const float* coords, uint32_t float
 ngp_status ngp_model_infer_padded(ngp_model* model, const float* coords, uint32_t floats_per_coord, uint32_t n,
                                   uint16_t* out, uint32_t out_stride, int layout_rm, int use_inference_params,
                                   ngp_stream stream);
+/* The renderer's network call (NerfTracer's inference_mixed_precision on the compacted samples,
+ * src/testbed_nerf.cu:1720): enc [n_levels][n][F] fp16 (level-major, as ngp_model_encode writes), sh_rows
+ * [n_rows][16] fp16 = the degree-4 SH of each ray's warped direction (the dir encoding, computed once per ray),
+ * sh_row_of_sample [n] u32 = the row of each sample.  out: [n][4] fp16 as ngp_model_infer.  Timed by
+ * NGP_TIMER_RENDER_MLP (the MLP dispatch alone).  Networks without extra dims. */
+ngp_status ngp_model_infer_sh_rows(ngp_model* model, const uint16_t* enc, const uint16_t* sh_rows,
+                                   const uint32_t* sh_row_of_sample, uint32_t n, uint32_t n_rows, uint16_t* out,
+                                   int use_inference_params, ngp_stream stream);
 /* pos: n positions (stride floats). out: [n] fp16 raw density (row 0 of the density MLP output). */
 ngp_status ngp_model_density(ngp_model* model, const float* pos, uint32_t stride, uint32_t n,
                              uint16_t* out, int use_inference_params, ngp_stream stream);
@@ -488,6 +499,11 @@ ngp_status ngp_train_scratch(ngp_model* model, int kind, void** dev_ptr, size_t*
 /* Drops the last step's gradients (MLP and hash grid) before the step is run again -- after a chunked
  * forward reported forward_early_stop_violations, which made its optimizer step a no-op. */
 ngp_status ngp_train_discard(ngp_model* model, ngp_stream stream);
+/* Data-parallel: the violation word (NGP_SCRATCH_VIOLATIONS) as two int32 parts on the device, so a caller can
+ * max-reduce them over the ranks without a host round trip.  to_parts = 1: parts[0] = early-stop count,
+ * parts[1] = 1 when this rank's samples overflowed its capacity; to_parts = 0: the word is rebuilt from the
+ * (reduced) parts.  parts: 2 int32 of device memory; stream-ordered. */
+ngp_status ngp_train_violation_parts(ngp_model* model, int32_t* parts, int to_parts, ngp_stream stream);
 
 /* --- occupancy grid ------------------------------------------------------------------ */
 ngp_status ngp_density_grid_update(ngp_model* model, const ngp_grid_args* args, ngp_stream stream);

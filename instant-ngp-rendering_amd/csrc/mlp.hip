@@ -507,7 +507,7 @@ __device__ __forceinline__ void rf_hidden_range(const h8* w, h8 (&b)[CT_][2], f4
 // fragments are read from LDS (one copy per workgroup) to leave the VGPRs to the ring.
 template <class N, int CT_, int PF, bool DENSITY_ONLY, bool SHIN>
 __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const RawTile<N, CT_>& cur, uint32_t base, int g,
-                                        int n) {
+                                        int n, int32_t live_pre = -1) {
 	h8 b[CT_][2];
 	f4 c[CT_][4];
 #pragma unroll
@@ -521,9 +521,13 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 	uint32_t live = (1u << CT_) - 1u;
 	if constexpr (SHIN && !DENSITY_ONLY) {
 		if (a.skip_unfilled) {
-			live = 0;
+			if (live_pre >= 0) {
+				live = (uint32_t)live_pre;  // computed when the tile's SH rows were fetched (k_mlp_infer_sh)
+			} else {
+				live = 0;
 #pragma unroll
-			for (int cc = 0; cc < CT_; ++cc) live |= (__ballot(cur.ri[cc] != NO_SH_ROW) != 0ull ? 1u : 0u) << cc;
+				for (int cc = 0; cc < CT_; ++cc) live |= (__ballot(cur.ri[cc] != NO_SH_ROW) != 0ull ? 1u : 0u) << cc;
+			}
 			if (live == 0) return;
 		}
 	}
@@ -640,6 +644,84 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 				if (t + stride < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[(q + 1) % R]);
 			}
 			rf_tile<N, CT_, PF, DENSITY_ONLY, SHIN>(a, wl, ring[q], t * TS, g, n);
+		}
+	}
+}
+
+// ---------------------------------------------------------------------------
+// The renderer's network call with a decoupled load pipeline (ngp_tuning.render_mlp_pipeline 2 / 3).
+// k_mlp_infer_rf's SH-row path fetches a tile's SH rows right after issuing its row indices, so every wave
+// step waits one full memory latency for the indices before it computes (round 5: the waves were parked at
+// s_waitcnt 55 % of their cycles in the standalone 2^21-sample microbench, profiles/r06_mlp_microbench_*).
+// Here every load a step waits for was issued at least one step earlier: at the step computing tile t a
+// wave issues the SH rows of tile t+1 (their row indices came PF steps earlier), the row indices of tile
+// t+PF+1 and the encodings of tile t+PF, then computes tile t.  A tile's live mask (column tiles holding a
+// filled slot) is taken when its SH rows are fetched, so its row-index registers are free for the indices
+// of the tile PF+1 steps ahead.  Same arithmetic as k_mlp_infer_rf (bit-identical outputs).
+// ---------------------------------------------------------------------------
+template <class N, int CT_>
+__device__ __forceinline__ void ri_load(__amdgpu_buffer_rsrc_t crd_rs, uint32_t base, int n, RawTile<N, CT_>& r) {
+#pragma unroll
+	for (int c = 0; c < CT_; ++c) r.ri[c] = __builtin_amdgcn_raw_buffer_load_b32(crd_rs, 4 * (base + 16 * c + n), 0, 0);
+}
+
+template <class N, int CT_>
+__device__ __forceinline__ uint32_t sh_load_live(__amdgpu_buffer_rsrc_t sh_rs, int g, RawTile<N, CT_>& r, bool skip) {
+	sh_load<N, CT_>(sh_rs, g, r);
+	uint32_t live = (1u << CT_) - 1u;
+	if (skip) {
+		live = 0;
+#pragma unroll
+		for (int cc = 0; cc < CT_; ++cc) live |= (__ballot(r.ri[cc] != NO_SH_ROW) != 0ull ? 1u : 0u) << cc;
+	}
+	return __builtin_amdgcn_readfirstlane(live);
+}
+
+template <class N, int CT_, int PF, int FF>
+__global__ void __launch_bounds__(BLOCK) k_mlp_infer_sh(MlpArgs a) {
+	static_assert(N::KE <= 2 && N::Wp <= 64 && N::XE == 0, "register layout assumes <= 2 K-steps per layer, no extra dims");
+	if (a.n_dev) a.n = min(a.n, *a.n_dev);
+	set_wave_priority(a.prio);
+	constexpr int NF = N::fwd_frags();
+	extern __shared__ __attribute__((aligned(16))) char smem[];
+	h8* w = reinterpret_cast<h8*>(smem);  // [frag][lane]
+	{
+		const h8* src = reinterpret_cast<const h8*>(a.frags + N::rfwd_off(0));
+		for (int t = threadIdx.x; t < NF * 64; t += BLOCK) w[t] = src[t];
+	}
+	__syncthreads();
+	const int lane = threadIdx.x & 63, g = lane >> 4, n = lane & 15;
+	const h8* wl = w + lane;
+	constexpr uint32_t TS = 16 * CT_;
+	const uint32_t n_tiles = (a.n + TS - 1) / TS;
+	const uint32_t stride = gridDim.x * WAVES;
+	const uint32_t t0 = __builtin_amdgcn_readfirstlane(blockIdx.x * WAVES + (threadIdx.x >> 6));
+	const __amdgpu_buffer_rsrc_t enc_rs = make_rsrc(a.enc, a.enc_bytes);
+	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.sh_ray, a.coord_bytes);
+	const __amdgpu_buffer_rsrc_t sh_rs = make_rsrc(a.sh, a.sh_bytes);
+	const bool skip = a.skip_unfilled != 0;
+	// slot of tile t0 + k * stride: k % R (the loop is unrolled R times, so every slot index is static)
+	constexpr int R = PF + 1;
+	RawTile<N, CT_> ring[R];
+	uint32_t live[R];
+	// The loads are issued unconditionally: a tile past the end reads past the buffers' extents (the raw
+	// buffer loads return 0; a row index of 0 fetches SH row 0) and is never computed.  Guarding them with
+	// branches made the compiler's s_waitcnt bookkeeping conservative at the merges (vmcnt(0) before every
+	// SH fetch and every tile: the pipeline drained each step)
+#pragma unroll
+	for (int k = 0; k <= PF; ++k) ri_load<N, CT_>(crd_rs, (t0 + k * stride) * TS, n, ring[k % R]);
+#pragma unroll
+	for (int k = 0; k < PF; ++k) rf_load<N, CT_, FF, true>(a, enc_rs, crd_rs, (t0 + k * stride) * TS, g, n, ring[k], false);
+	live[0] = sh_load_live<N, CT_>(sh_rs, g, ring[0], skip);
+	for (uint32_t tb = t0; tb < n_tiles; tb += R * stride) {
+#pragma unroll
+		for (int q = 0; q < R; ++q) {
+			const uint32_t t = tb + q * stride;
+			if (t >= n_tiles) break;
+			live[(q + 1) % R] = sh_load_live<N, CT_>(sh_rs, g, ring[(q + 1) % R], skip);
+			ri_load<N, CT_>(crd_rs, (t + (PF + 1) * stride) * TS, n, ring[q]);
+			rf_load<N, CT_, FF, true>(a, enc_rs, crd_rs, (t + PF * stride) * TS, g, n, ring[(q + PF) % R], false);
+			rf_tile<N, CT_, PF, false, true>(a, wl, ring[q], t * TS, g, n, (int32_t)live[q]);
 		}
 	}
 }
@@ -1230,7 +1312,25 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		// the 64-sample steps beside the other pipeline's encoder: 6 workgroups per CU (13.60 vs 13.67 ms per fire frame
 		// against 8 with 6 M passes; profiles/r05_schedule_sweep.txt)
 		const uint32_t wg_render = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : 6u;
-		if (sh && a.F == 2 && pl && tile == 4)
+		// the decoupled load pipeline (k_mlp_infer_sh, ngp_tuning.render_mlp_pipeline 2 / 3; 1 = the round-5 ring)
+		const uint32_t pipe = m->tuning.render_mlp_pipeline ? m->tuning.render_mlp_pipeline : 2u;
+		bool done = false;
+		if constexpr (N::XE == 0) {
+			if (sh && a.F == 2 && pl && pipe >= 2) {
+				const uint32_t wg = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : (tile == 4 ? 6u : 8u);
+				const uint32_t ts = 16 * (tile == 4 ? 4 : tile == 2 ? 2 : 1);
+				const uint32_t grid_sh = std::min<uint32_t>(div_up(n, ts * WAVES), cu_count() * wg);
+				if (tile == 4 && pipe == 2) launch_timed(k_mlp_infer_sh<N, 4, 1, 12>, grid_sh, BLOCK, lds, s, a);
+				else if (tile == 4) launch_timed(k_mlp_infer_sh<N, 4, 2, 12>, grid_sh, BLOCK, lds, s, a);
+				else if (tile == 2 && pipe == 2) launch_timed(k_mlp_infer_sh<N, 2, 1, 12>, grid_sh, BLOCK, lds, s, a);
+				else if (tile == 2) launch_timed(k_mlp_infer_sh<N, 2, 2, 12>, grid_sh, BLOCK, lds, s, a);
+				else if (pipe == 2) launch_timed(k_mlp_infer_sh<N, 1, 2, 12>, grid_sh, BLOCK, lds, s, a);
+				else launch_timed(k_mlp_infer_sh<N, 1, 3, 12>, grid_sh, BLOCK, lds, s, a);
+				done = true;
+			}
+		}
+		if (done) {
+		} else if (sh && a.F == 2 && pl && tile == 4)
 			launch_timed(k_mlp_infer_rf<N, 4, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 64 * WAVES), cu_count() * wg_render), BLOCK, lds, s, a);
 		else if (sh && a.F == 2 && pl && tile == 2)
 			launch_timed(k_mlp_infer_rf<N, 2, 1, false, 12, true>, std::min<uint32_t>(div_up(n, 32 * WAVES), cu_count() * wg_per_cu), BLOCK, lds, s, a);

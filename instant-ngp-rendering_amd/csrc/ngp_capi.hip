@@ -88,6 +88,7 @@ static void validate_tuning(const ngp_tuning* t) {
 	require(t->train_chunk_lanes == 0 || (t->train_chunk_lanes >= 4 && t->train_chunk_lanes <= 64 &&
 	                                      (t->train_chunk_lanes & (t->train_chunk_lanes - 1)) == 0),
 	        "train_chunk_lanes must be 0 or a power of two in [4, 64]");
+	require(t->render_mlp_pipeline <= 3, "render_mlp_pipeline must be 0, 1, 2 or 3");
 	require(t->train_sampler_lanes == 0 || (t->train_sampler_lanes >= 8 && t->train_sampler_lanes <= 64 &&
 	                                        (t->train_sampler_lanes & (t->train_sampler_lanes - 1)) == 0),
 	        "train_sampler_lanes must be 0 or a power of two in [8, 64]");
@@ -437,6 +438,37 @@ ngp_status ngp_model_infer_padded(ngp_model* m, const float* coords, uint32_t fp
 	});
 }
 
+// level-major [L][n][F] encodings -> the pipelines' EncLayout (the layout the encoder writes inside the renderer)
+__global__ void k_enc_relayout(const uint16_t* __restrict__ src, uint16_t* __restrict__ dst, uint32_t L, uint32_t F, uint32_t n,
+                               EncLayout lay) {
+	const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+	if (t >= L * n) return;
+	const uint32_t lvl = t / n, i = t % n;
+	const size_t d = lay.vec(lvl, i) * F;
+	for (uint32_t f = 0; f < F; ++f) dst[d + f] = src[(size_t)t * F + f];
+}
+
+ngp_status ngp_model_infer_sh_rows(ngp_model* m, const uint16_t* enc, const uint16_t* sh_rows, const uint32_t* sh_row_of_sample,
+                                   uint32_t n, uint32_t n_rows, uint16_t* out, int use_inf, ngp_stream s) {
+	return guarded([&] {
+		require(m && (n == 0 || (enc && sh_rows && sh_row_of_sample && out)), "null argument");
+		require(m->cfg.n_extra_dims == 0, "ngp_model_infer_sh_rows: networks with extra dims take ngp_model_infer");
+		if (n == 0) return;
+		const __half* frags = use_inf ? m->frag_infer.ptr : m->frag_train.ptr;
+		TrainScratch& ts = m->ts;
+		const EncLayout lay = internal_layout(m, n);
+		ts.enc.reserve((size_t)m->lt.n_levels * n * m->lt.F);
+		k_enc_relayout<<<div_up(m->lt.n_levels * n, 256u), 256, 0, S(s)>>>(enc, reinterpret_cast<uint16_t*>(ts.enc.ptr), m->lt.n_levels,
+		                                                                  m->lt.F, n, lay);
+		NGP_HIP_CHECK(hipGetLastError());
+		// the renderer's network call: its timer (NGP_TIMER_RENDER_MLP) rides on the MLP dispatch alone
+		m->timers.begin_kernel(NGP_TIMER_RENDER_MLP);
+		launch_mlp_infer(m, frags, ts.enc.ptr, lay, nullptr, 0, n, reinterpret_cast<__half*>(out), S(s), nullptr, 4,
+		                 reinterpret_cast<const __half*>(sh_rows), 0, 4, sh_row_of_sample, n_rows, false, MlpExtra{});
+		m->timers.end(NGP_TIMER_RENDER_MLP, S(s), n);
+	});
+}
+
 ngp_status ngp_model_density(ngp_model* m, const float* pos, uint32_t stride, uint32_t n, uint16_t* out, int use_inf,
                              ngp_stream s) {
 	return guarded([&] {
@@ -486,9 +518,11 @@ static void model_backward(ngp_model* m, const uint16_t* enc, const float* dirs,
 		NGP_HIP_CHECK(hipMemcpyAsync(ts.ccoords.ptr, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, S(s)));
 		MlpExtra x = extra ? coord_extras(m, extra, 16, 0, n, S(s)) : MlpExtra{};
 		x.dextra = dextra;
+		m->timers.begin_kernel(NGP_TIMER_TRAIN_MLP_BWD);
 		launch_mlp_train(m, m->frag_train.ptr, reinterpret_cast<const __half*>(enc), EncLayout{n, 0}, ts.ccoords.ptr, 8, n,
 		                 reinterpret_cast<const __half*>(dloss), weight, m->grads.ptr, reinterpret_cast<__half*>(denc),
 		                 S(s), nullptr, nullptr, x);
+		m->timers.end(NGP_TIMER_TRAIN_MLP_BWD, S(s), n);
 		NGP_HIP_CHECK(hipStreamSynchronize(S(s)));
 	}
 }
@@ -553,6 +587,28 @@ ngp_status ngp_train_discard(ngp_model* m, ngp_stream s) {
 		NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads16.ptr, 0, m->n_grid_params * sizeof(__half), S(s)));
 		if (m->grid_grads64.ptr) NGP_HIP_CHECK(hipMemsetAsync(m->grid_grads64.ptr, 0, m->n_grid_params * sizeof(long long), S(s)));
 		if (m->ts.counters.ptr) NGP_HIP_CHECK(hipMemsetAsync(m->ts.counters.ptr + 9, 0, sizeof(uint32_t), S(s)));
+	});
+}
+
+// the violation word <-> its two reducible parts (one thread; a data-parallel step's only per-step exchange
+// besides the gradients, kept on the stream so an RCCL max-reduce of the parts stays asynchronous)
+__global__ void k_violation_parts(uint32_t* word, int32_t* parts, int to_parts) {
+	if (to_parts) {
+		const uint32_t w = *word;
+		parts[0] = (int32_t)(w & (VIOL_CAPACITY - 1u));
+		parts[1] = (w & VIOL_CAPACITY) ? 1 : 0;
+	} else {
+		const uint32_t c = (uint32_t)max(parts[0], 0);
+		*word = (parts[1] ? VIOL_CAPACITY : 0u) | min(c, VIOL_CAPACITY - 1u);
+	}
+}
+
+ngp_status ngp_train_violation_parts(ngp_model* m, int32_t* parts, int to_parts, ngp_stream s) {
+	return guarded([&] {
+		require(m && parts, "null argument");
+		require(m->ts.counters.ptr, "no training step has run");
+		k_violation_parts<<<1, 1, 0, S(s)>>>(m->ts.counters.ptr + 9, parts, to_parts);
+		NGP_HIP_CHECK(hipGetLastError());
 	});
 }
 

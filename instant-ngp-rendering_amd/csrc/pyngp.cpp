@@ -39,7 +39,7 @@ static py::array_t<float> pinned_frame(int height, int width) {
 	NGP_TUNING_FIELD(encode_dense_records) NGP_TUNING_FIELD(mlp_workgroups_per_cu) NGP_TUNING_FIELD(debug)           \
 	NGP_TUNING_FIELD(encode_streaming) NGP_TUNING_FIELD(grid_unsorted) NGP_TUNING_FIELD(render_mlp_tile)             \
 	NGP_TUNING_FIELD(encode_xcd_regions) NGP_TUNING_FIELD(render_skip_unfilled) NGP_TUNING_FIELD(render_exit_cap) \
-	NGP_TUNING_FIELD(render_priority) NGP_TUNING_FIELD(render_host_frame) NGP_TUNING_FIELD(train_chunk_lanes) NGP_TUNING_FIELD(train_sampler_lanes)
+	NGP_TUNING_FIELD(render_priority) NGP_TUNING_FIELD(render_host_frame) NGP_TUNING_FIELD(train_chunk_lanes) NGP_TUNING_FIELD(train_sampler_lanes) NGP_TUNING_FIELD(render_mlp_pipeline)
 
 namespace {
 
@@ -467,7 +467,7 @@ PYBIND11_MODULE(pyngp, m) {
 			     py::array_t<float> a = pinned_frame(height, width);
 			     {
 				     py::gil_scoped_release rel;
-				     t.render_into(a.mutable_data(), width, height, spp, linear);
+				     t.render_into(a.mutable_data(), width, height, spp, linear, 0, 1, 8, true);
 			     }
 			     return a;
 		     },

@@ -1266,22 +1266,15 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 			// VIOL_CAPACITY, ngp_internal.h) gates the optimizer; its two parts are reduced separately (a max of
 			// the packed word would hide one rank's early stops behind another's capacity flag), so every rank
 			// sees any rank's early stops and any rank's overflow, and all of them skip or all of them step
+			// (split and rebuilt on the device: the max-reduce of the parts stays on the stream -- asynchronous over
+			// RCCL -- instead of three blocking host round trips per step)
 			void* viol = nullptr;
 			ck(ngp_train_scratch(m_model, NGP_SCRATCH_VIOLATIONS, &viol, nullptr));
 			if (viol) {
-				constexpr uint32_t kViolCapacity = 1u << 20;
-				uint32_t w = 0;
-				hk(hipMemcpyAsync(&w, viol, 4, hipMemcpyDeviceToHost, (hipStream_t)m_stream), "violations d2h");
-				sync();
-				int32_t parts[2] = {(int32_t)(w & (kViolCapacity - 1u)), (w & kViolCapacity) ? 1 : 0};
 				int32_t* dp = (int32_t*)m_red_buf + 8;
-				hk(hipMemcpyAsync(dp, parts, sizeof(parts), hipMemcpyHostToDevice, (hipStream_t)m_stream), "violations h2d");
+				ck(ngp_train_violation_parts(m_model, dp, 1, m_stream));
 				allreduce_dev(dp, 2, 2, true);
-				hk(hipMemcpyAsync(parts, dp, sizeof(parts), hipMemcpyDeviceToHost, (hipStream_t)m_stream), "violations d2h");
-				sync();
-				w = (parts[1] ? kViolCapacity : 0u) | std::min<uint32_t>((uint32_t)parts[0], kViolCapacity - 1u);
-				hk(hipMemcpyAsync(viol, &w, 4, hipMemcpyHostToDevice, (hipStream_t)m_stream), "violations h2d");
-				sync();
+				ck(ngp_train_violation_parts(m_model, dp, 0, m_stream));
 			}
 			ck(ngp_optimizer_step(m_model, training_step, train_network, train_encoding, m_stream));
 		}
@@ -1910,7 +1903,7 @@ std::vector<float> Testbed::render(int width, int height, int spp, bool linear, 
 }
 
 void Testbed::render_into(float* host_dst, int width, int height, int spp, bool linear, uint32_t shard_index,
-                          uint32_t shard_count, uint32_t shard_rows) {
+                          uint32_t shard_count, uint32_t shard_rows, bool host_dst_pinned) {
 	if (width <= 0 || height <= 0) throw std::runtime_error("render: invalid resolution");
 	const size_t n = (size_t)width * height;
 	const vec2 sc = {(0.5f - screen_center[0]) * zoom + 0.5f, (0.5f - screen_center[1]) * zoom + 0.5f};
@@ -2024,8 +2017,10 @@ void Testbed::render_into(float* host_dst, int width, int height, int spp, bool 
 	// one spp of a whole Shade-mode frame into host memory: the kernels that finish the rays stream their tonemapped
 	// pixels to host_dst while the march goes on (ngp_render_args.host_frame), so no read-back follows the frame
 	// (ngp_tuning.render_host_frame 2: tonemap, then copy).  The device frame and m_out are produced as before.
+	// Only a page-locked, device-mapped destination can be written by the kernels (render() and
+	// render_shard() hand in a pageable std::vector, which takes the read-back).
 	int32_t host_complete = 0;
-	const bool stream_pixels = host_dst && std::max(spp, 1) == 1 && r.shard_count == 1 && r.render_mode == NGP_RENDER_MODE_SHADE &&
+	const bool stream_pixels = host_dst && host_dst_pinned && std::max(spp, 1) == 1 && r.shard_count == 1 && r.render_mode == NGP_RENDER_MODE_SHADE &&
 	                           r.glow_mode == 0 && m_tuning.render_host_frame != 2;
 	if (stream_pixels) {
 		r.host_frame = host_dst;

@@ -232,9 +232,11 @@ public:
 	std::vector<float> render(int width, int height, int spp, bool linear, uint32_t shard_index = 0,
 	                          uint32_t shard_count = 1, uint32_t shard_rows = 8, bool copy_to_host = true);
 	// the same into caller-owned host memory of width * height * 4 floats (null: stay in HBM); with a
-	// pinned buffer (pinned_host_alloc) the read-back runs at PCIe DMA rate
+	// pinned buffer (pinned_host_alloc) the read-back runs at PCIe DMA rate.  host_dst_pinned: the caller
+	// guarantees host_dst is page-locked and device-mapped (pinned_host_alloc), so the render kernels may
+	// stream finished pixels into it; pageable memory (a std::vector) takes the read-back after the frame
 	void render_into(float* host_dst, int width, int height, int spp, bool linear, uint32_t shard_index = 0,
-	                 uint32_t shard_count = 1, uint32_t shard_rows = 8);
+	                 uint32_t shard_count = 1, uint32_t shard_rows = 8, bool host_dst_pinned = false);
 	const float* render_frame_buffer() const { return m_out; }
 	void set_camera_to_training_view(int trainview);
 	void reset_camera();

@@ -1010,9 +1010,9 @@ __global__ void __launch_bounds__(256) k_loss_emit(LossArgs a) {
 		const uint32_t img = __float_as_uint(a.loss_state[8 * (size_t)i + 7]);
 		const float4 g = a.ray_aux[i];
 		if (a.exposure_fix) {
-			img_deposit_fixed(&a.exposure_fix[3 * (size_t)img + 0], g.x);
-			img_deposit_fixed(&a.exposure_fix[3 * (size_t)img + 1], g.y);
-			img_deposit_fixed(&a.exposure_fix[3 * (size_t)img + 2], g.z);
+			img_deposit_fixed(&a.exposure_fix[IMG_FIX_STRIDE * (size_t)img + 0], g.x);
+			img_deposit_fixed(&a.exposure_fix[IMG_FIX_STRIDE * (size_t)img + 1], g.y);
+			img_deposit_fixed(&a.exposure_fix[IMG_FIX_STRIDE * (size_t)img + 2], g.z);
 		} else {
 			atomicAdd(&a.exposure_grad[3 * (size_t)img + 0], g.x);
 			atomicAdd(&a.exposure_grad[3 * (size_t)img + 1], g.y);

@@ -130,7 +130,7 @@ class Tuning(C.Structure):
         ("encode_streaming", C.c_uint32), ("grid_unsorted", C.c_uint32), ("render_mlp_tile", C.c_uint32),
         ("encode_xcd_regions", C.c_uint32), ("render_skip_unfilled", C.c_uint32), ("render_exit_cap", C.c_uint32),
         ("render_priority", C.c_uint32), ("render_host_frame", C.c_uint32),
-        ("train_chunk_lanes", C.c_uint32), ("train_sampler_lanes", C.c_uint32),
+        ("train_chunk_lanes", C.c_uint32), ("train_sampler_lanes", C.c_uint32), ("render_mlp_pipeline", C.c_uint32),
     ]
 
 
@@ -162,6 +162,8 @@ EXPORTS = {
     "ngp_model_infer": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]),
     "ngp_model_infer_padded": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_uint32, C.c_int,
                                          C.c_int, C.c_void_p]),
+    "ngp_model_infer_sh_rows": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32,
+                                          C.c_void_p, C.c_int, C.c_void_p]),
     "ngp_model_density": (C.c_int, [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint32, C.c_void_p, C.c_int, C.c_void_p]),
     "ngp_model_backward": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                      C.c_void_p, C.c_void_p]),
@@ -174,6 +176,7 @@ EXPORTS = {
     "ngp_allreduce_grads": (C.c_int, [C.c_void_p, C.c_void_p, C.c_void_p]),
     "ngp_train_scratch": (C.c_int, [C.c_void_p, C.c_int, C.POINTER(C.c_void_p), C.POINTER(C.c_size_t)]),
     "ngp_train_discard": (C.c_int, [C.c_void_p, C.c_void_p]),
+    "ngp_train_violation_parts": (C.c_int, [C.c_void_p, C.c_void_p, C.c_int, C.c_void_p]),
     "ngp_density_grid_update": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),
     "ngp_density_grid_evaluate": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),
     "ngp_density_grid_finish": (C.c_int, [C.c_void_p, C.POINTER(GridArgs), C.c_void_p]),

@@ -11,6 +11,7 @@ Three measurements, all on bounded samples so the default bench finishes in minu
     extrapolated linearly to one bench step (labelled "extrapolated").
 Only bench.py's cpu_baseline leg calls this; the oracle is never the thing measured as `value`.
 """
+import os
 import time
 
 import numpy as np
@@ -25,6 +26,17 @@ def threads_for_box(cap=16):
     """All-core thread count: the host's hardware concurrency, capped at the GPU box's CPU share."""
     hw = int(load().oref_hardware_concurrency())
     return hw, max(1, min(cap, hw))
+
+
+def cpu_share():
+    """The CPUs this process may actually run on: its affinity mask and the cgroup CPU quota (cpu.max), if any."""
+    out = {"affinity_cpus": len(os.sched_getaffinity(0))}
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        out["cgroup_cpu_quota"] = None if q == "max" else round(int(q) / int(period), 2)
+    except (OSError, ValueError):
+        out["cgroup_cpu_quota"] = None
+    return out
 
 
 def _timed(fn):

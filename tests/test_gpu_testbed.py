@@ -213,6 +213,25 @@ def test_render_streams_tonemapped_pixels_to_host_bit_exactly(scene, linear, col
     np.testing.assert_array_equal(tb.render(W, H, 2, linear), tb.render(W, H, 2, linear))
 
 
+def test_single_shard_and_local_render_distributed_read_back_into_pageable_memory(scene):
+    """render_shard(..., shard_index=0, shard_count=1) and render_distributed(copy_to_host=True)
+    on a Testbed without a communicator render into a pageable std::vector.  Only pyngp's render() hands in
+    page-locked memory the kernels may stream pixels into; these paths take the read-back and equal render()."""
+    root, cams, imgs = scene
+    ngp, tb = new_testbed()
+    tb.load_training_data(os.path.join(root, "transforms_train.json"))
+    tb.reload_network_from_file("lego_L16F2.json")
+    tb.shall_train = True
+    while tb.training_step < 50:
+        tb.frame()
+    tb.set_camera_to_training_view(1)
+    W, H = 320, 200
+    ref = tb.render(W, H, 1, True)
+    assert np.abs(ref[..., :3]).max() > 0
+    np.testing.assert_array_equal(tb.render_shard(W, H, 1, True, 0, 1), ref)
+    np.testing.assert_array_equal(tb.render_distributed(W, H, 1, True, True), ref)
+
+
 def test_config_c_eight_way_row_shards_assemble_the_1080p_frame(scene):
     """BASELINE config C at its own shape on one GPU: one 1920x1080 frame of the config-B network
     (L16 F2 T2^19, 64-wide MLPs) rendered unsharded, then as the 8 row shards the 8 ranks of config C
@@ -429,6 +448,34 @@ def test_exposure_optimisation(scene):
     tr.optimize_extra_dims = True
     with pytest.raises(RuntimeError, match="n_extra_dims"):
         tb.frame()
+
+
+def test_deterministic_exposure_gradients_land_on_their_own_images(scene):
+    """in deterministic mode k_loss_emit deposits dL/dexposure as 64-bit fixed point into the
+    per-image [n_images][IMG_FIX_STRIDE] sums (exposure slots 0-2 of each image's row).  The exposures after a few
+    camera updates must agree with the float-atomic path's for EVERY image (a wrong row stride gives image 0 every
+    gradient and leaves images 1.. at the re-centring offset, all equal)."""
+    root, cams, imgs = scene
+    out = {}
+    for det in (True, False):
+        ngp, tb = new_testbed()
+        tb.load_training_data(os.path.join(root, "transforms_train.json"))
+        tb.reload_network_from_file("tiny_L4F2.json")
+        tb.deterministic = det
+        tr = tb.nerf.training
+        tr.optimize_exposure = True
+        tr.n_steps_between_cam_updates = 1
+        tb.shall_train = True
+        while tb.training_step < 4:
+            tb.frame()
+        out[det] = np.asarray(tr.cam_exposure).copy()
+    d, f = out[True], out[False]
+    assert d.shape == (12, 3) and np.abs(f).max() > 0
+    # images 1..11 carry their own gradients: their exposures differ from one another
+    assert np.ptp(d[1:], axis=0).max() > 0.1 * np.abs(f).max()
+    # the fixed-point sums and the float atomics differ by summation order only (and the hash-grid gradients by
+    # fp16 atomics rounding): a few Adam steps of per-image sign-like updates agree closely
+    assert np.abs(d - f).max() <= 0.05 * np.abs(f).max(), (d, f)
 
 
 def _model_buffer(tb, kind):
