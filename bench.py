@@ -65,6 +65,8 @@ def parse():
                    help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
     p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r05_final3_surface_pmc_traffic.json"),
                    help="PMC traffic summary of the surface-scene bench (tools/pmc_traffic.py)")
+    p.add_argument("--config-e-traffic-json", default=os.path.join(ROOT, "profiles", "r06_config_e_pmc_traffic.json"),
+                   help="PMC FETCH/WRITE summary of the config-E leg alone (tools/config_e_leg.py under tools/profile_round.sh)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r05_final3_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
     return p.parse_args()
@@ -137,7 +139,7 @@ def make_dataset(ngp, tb, args, device):
 # timer -> kernel (name pattern) whose PMC counters describe it
 TIMER_KERNEL = {"train_encode": r"k_hashgrid_fwd<\d+u, 0[,>]", "render_encode": r"k_hashgrid_fwd<\d+u, 1[,>]",
                 "train_encode_bwd": r"k_hashgrid_bwd<", "train_mlp_infer": r"k_mlp_infer_rf<.*, false, \d+, false>$",
-                "render_mlp": r"k_mlp_infer_rf<.*, true>$", "train_mlp_bwd": r"k_mlp_train<",
+                "render_mlp": r"k_mlp_infer_(rf<.*, true>|sh<.*>)$", "train_mlp_bwd": r"k_mlp_train<",
                 "optimizer": r"k_optimizer"}
 
 
@@ -370,6 +372,7 @@ def config_e(args, ngp):
             return tb.last_train_stats()["n_rays"], t1 - t0, time.perf_counter() - t1
 
         elapsed, out, kernels, roof = timed_leg(args, tb, step)
+        roof["traffic"] = pmc_traffic(args.config_e_traffic_json, roof["kernel"], roof["units_per_launch"])
         mem = used() - used0
         del tb
     rays = sum(r + W * H for r, _, _ in out)

@@ -12,6 +12,7 @@ container, where /root/reference exists; the outputs are committed and travel to
   data/nerf/test/dataset it is one of the two scenes whose CUDA-trained density mosaics the reference ships
   (data/nerf/test.density_slices_256x256x256.png, data/nerf/test2/images.density_slices_256x256x256.png), which
   tests/golden/ref_density_slices/ holds byte for byte.
+* data/nerf/test2_half/images: the same scene at half resolution (360x640; `python tools/make_real_data.py test2_half`).
 * data/nerf/fox: the reference's transforms.json verbatim and its 50 JPG frames as shipped (17
   listed frames are absent from the reference checkout; the loader skips them exactly as
   nerf_loader.cu:364-387 does for files that do not exist).
@@ -51,18 +52,20 @@ def make_test():
     shutil.copy(os.path.join(src, "log.txt"), os.path.join(dst, "log.txt"))
 
 
-def make_test2():
+def make_test2(div=4, out="test2"):
+    """div 4 -> data/nerf/test2 (180x320); div 2 -> data/nerf/test2_half (360x640, VERDICT r05 item 2: the
+    reference trained at 720x1280)."""
     src = os.path.join(REF, "test2", "images")
-    dst = os.path.join(OUT, "test2", "images")
+    dst = os.path.join(OUT, out, "images")
     os.makedirs(os.path.join(dst, "train"), exist_ok=True)
     meta = json.load(open(os.path.join(src, "transforms_train.json")))
     for k in ("fl_x", "fl_y", "cx", "cy", "w", "h"):
-        meta[k] = meta[k] * 0.25
+        meta[k] = meta[k] / div
     for fr in meta["frames"]:
         name = os.path.basename(fr["file_path"])
         im = Image.open(os.path.join(src, fr["file_path"]))
         w, h = im.size
-        im = im.resize((w // 4, h // 4), Image.LANCZOS).convert("RGB")
+        im = im.resize((w // div, h // div), Image.LANCZOS).convert("RGB")
         im.save(os.path.join(dst, "train", name), "PNG", optimize=True)
     json.dump(meta, open(os.path.join(dst, "transforms_train.json"), "w"), indent=1)
     shutil.copy(os.path.join(src, "log.txt"), os.path.join(dst, "log.txt"))
@@ -92,6 +95,8 @@ if __name__ == "__main__":
         make_test()
     if "test2" in which:
         make_test2()
+    if "test2_half" in which:
+        make_test2(2, "test2_half")
     if "fox" in which:
         make_fox()
     if "slices" in which:

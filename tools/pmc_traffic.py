@@ -31,7 +31,7 @@ KERNELS = [
     (r"k_hashgrid_fwd<\d+u, 1[,>]", "render_encode", "k_gather16"),
     (r"k_hashgrid_fwd<\d+u, 0[,>]", "train_encode", "k_gather16"),
     (r"k_hashgrid_bwd<", "train_encode_bwd", "k_gather4"),
-    (r"k_mlp_infer_rf<.*, true>$", "render_mlp", "k_stream16"),
+    (r"k_mlp_infer_(rf<.*, true>|sh<.*>)$", "render_mlp", "k_stream16"),
     (r"k_mlp_infer_rf<.*, false, 12, false>$", "train_mlp_infer", "k_stream16"),
     (r"k_mlp_train<", "train_mlp_bwd", "k_stream4"),
     (r"k_optimizer", "optimizer", "k_stream16"),
@@ -49,10 +49,11 @@ def load(path):
 def bench_units(log):
     if not log:
         return {}
-    line = [l for l in open(log) if l.startswith('{"metric"')]
+    line = [l for l in open(log) if l.startswith('{"metric"') or l.startswith('{"config_e"')]
     if not line:
         return {}
-    k = json.loads(line[-1]).get("kernels_calibration", {})
+    d = json.loads(line[-1])
+    k = d.get("kernels_calibration") or d.get("config_e", {}).get("kernels_calibration", {})
     return {name: e["units"] / e["launches"] for name, e in k.items() if e.get("launches")}
 
 
