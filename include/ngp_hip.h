@@ -36,6 +36,10 @@
 #ifndef NGP_HIP_H
 #define NGP_HIP_H
 
+/* per-sample / per-image latent-code rows (n_extra_dims > 0): NGP_EXTRA_ROW floats, zero past n_extra_dims */
+#define NGP_EXTRA_DIMS_MAX 32
+#define NGP_EXTRA_ROW 32
+
 #include <stddef.h>
 #include <stdint.h>
 
@@ -75,8 +79,10 @@ typedef struct ngp_network_config {
 	float decay_base;
 	/* NerfNetwork's n_extra_dims (nerf_network.h:81-84, NerfDataset::n_extra_dims(): light directions and the
 	 * per-image latent code): the dir encoding's Identity part, appended to the rgb network's input after the
-	 * SH (rgb input width next_multiple(32 + n_extra_dims, 16)).  0..16; > 0 needs the 64-neuron network with
-	 * one density and two rgb hidden layers and an encoding of <= 32 features (base.json / lego_L16F2.json). */
+	 * SH (rgb input width next_multiple(32 + n_extra_dims, 16)).  0..NGP_EXTRA_DIMS_MAX (32: light directions
+	 * 3 + the 16-wide learnable code of optimize_extra_dims, src/testbed.cu:4046-4053, fit); > 0 needs the
+	 * 64-neuron network with one density and two rgb hidden layers and an encoding of <= 32 features
+	 * (base.json / lego_L16F2.json).  Latent codes travel in rows of NGP_EXTRA_ROW floats. */
 	uint32_t n_extra_dims;
 } ngp_network_config;
 
@@ -230,9 +236,9 @@ typedef struct ngp_train_args {
 	 * the value rides in the pad float of the sample's coordinate row.  0: all levels. */
 	int32_t max_level_rand_training;
 	/* n_extra_dims > 0 (per-image latent codes, Nerf::Training::extra_dims_gpu, src/testbed_nerf.cu:706-730, 824):
-	 * extra_dims = device fp32 [n_images][16], image i's code in row i (zero past n_extra_dims); every sample of
+	 * extra_dims = device fp32 [n_images][NGP_EXTRA_ROW], image i's code in row i (zero past n_extra_dims); every sample of
 	 * a ray from image i carries row i (NerfCoordinate::set_with_optional_extra_dims); null = zeros.
-	 * extra_dims_gradient (optional, device fp32 [n_images][16]) += sum over the kept rays' compacted samples of
+	 * extra_dims_gradient (optional, device fp32 [n_images][NGP_EXTRA_ROW]) += sum over the kept rays' compacted samples of
 	 * dL/d(code) (compute_extra_dims_gradient_train_nerf, src/testbed_nerf.cu:1271-1306; loss-scaled, as the
 	 * reference's gradient before its division by LOSS_SCALE at :2588).  Both 16-byte aligned (float4 rows). */
 	const float* extra_dims;
@@ -332,7 +338,7 @@ typedef struct ngp_render_args {
 	int32_t glow_mode;
 	float glow_y_cutoff;
 	/* n_extra_dims > 0: the latent code every rendered sample carries (Nerf::get_rendering_extra_dims,
-	 * src/testbed_nerf.cu:3206-3228): device fp32 [16], zero past n_extra_dims; null = zeros; 16-byte aligned */
+	 * src/testbed_nerf.cu:3206-3228): device fp32 [NGP_EXTRA_ROW], zero past n_extra_dims; null = zeros; 16-byte aligned */
 	const float* extra_dims;
 	/* optional (render(): one spp, Shade mode without glow, unsharded): the frame's tonemapped pixels streamed into
 	 * caller-owned page-locked host memory [H][W][4] by the kernels that finish their rays, while the march goes
@@ -459,8 +465,8 @@ ngp_status ngp_model_density(ngp_model* model, const float* pos, uint32_t stride
 ngp_status ngp_model_backward(ngp_model* model, const uint16_t* enc, const float* dirs, uint32_t n,
                               const uint16_t* dL_dout, const float* sample_weight, uint16_t* dL_denc,
                               ngp_stream stream);
-/* The same with the rgb network's extra inputs (n_extra_dims > 0): extra [n][16] fp32 latent codes of the samples
- * (zero past n_extra_dims); dL_dextra (optional) [n][16] fp32 = dL/d(code) of each sample's own row (the network's
+/* The same with the rgb network's extra inputs (n_extra_dims > 0): extra [n][NGP_EXTRA_ROW] fp32 latent codes of the
+ * samples (zero past n_extra_dims); dL_dextra (optional) [n][NGP_EXTRA_ROW] fp32 = dL/d(code) of each sample's own row (the network's
  * input gradient that compute_extra_dims_gradient_train_nerf sums, divided by sample_weight). */
 ngp_status ngp_model_backward_extra(ngp_model* model, const uint16_t* enc, const float* dirs, const float* extra, uint32_t n,
                                     const uint16_t* dL_dout, const float* sample_weight, uint16_t* dL_denc,

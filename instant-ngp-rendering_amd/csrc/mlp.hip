@@ -32,6 +32,7 @@ typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
 typedef short s4 __attribute__((ext_vector_type(4)));
 typedef float f4 __attribute__((ext_vector_type(4)));
+typedef unsigned int v2u __attribute__((ext_vector_type(2)));
 
 constexpr int SPW = 32;         // samples per wave
 constexpr int CT = SPW / 16;    // 16-sample column tiles per wave
@@ -47,6 +48,7 @@ constexpr int TCT = TSPW / 16;
 constexpr int TBLOCK = TWAVES * 64;
 static_assert(TWAVES * TSPW == SAMPLES_PER_BLOCK, "the training images hold one chunk");
 
+// XE = 2: n_extra_dims 17..32 fill rows 32..63 (both K steps whole; the training images keep 64 rows).
 // XE = 1: the rgb network's input carries the per-image latent code (NerfNetwork's n_extra_dims <= 16, the
 // dir encoding's Identity part): [density out 16 | SH 16 | extra 16] = 48 rows, read as two 32-row K steps whose
 // last 16 rows meet zero weights.  The training images then keep the rgb input segment last in a sample's row,
@@ -58,9 +60,9 @@ struct Net {
 	static constexpr int Wp = (W + 31) / 32 * 32;
 	static constexpr int NL = DH + RH + 2;
 	static constexpr int ENC_ROWS = 32 * KE;
-	static constexpr int XROWS = XE ? 48 : 32;  // rgb input rows kept in the training images
+	static constexpr int XROWS = XE == 2 ? 64 : (XE ? 48 : 32);  // rgb input rows kept in the training images
 	static constexpr int out_dim(int l) { return (l == DH || l == NL - 1) ? 16 : W; }
-	static constexpr int in_rows(int l) { return l == 0 ? ENC_ROWS : (l == DH + 1 ? 32 * (1 + XE) : Wp); }
+	static constexpr int in_rows(int l) { return l == 0 ? ENC_ROWS : (l == DH + 1 ? (XE ? 64 : 32) : Wp); }
 	static constexpr bool relu_out(int l) { return !(l == DH || l == NL - 1); }
 	static constexpr bool relu_in(int l) { return !(l == 0 || l == DH + 1); }
 	static constexpr int Mt(int l) { return out_dim(l) / 16; }
@@ -161,11 +163,11 @@ struct MlpArgs {
 	uint32_t n_mlp;                   // MLP parameter count (partials row pitch)
 	uint32_t skip_unfilled;           // SH-row inference: skip column tiles whose rows are all NO_SH_ROW
 	uint32_t prio;                    // SH-row inference (renderer): wave issue priority (ngp_tuning.render_priority bits 2-3)
-	// Net::XE (n_extra_dims > 0): the latent codes, fp32 rows of 16 (zero past n_extra_dims); sample i reads row
+	// Net::XE (n_extra_dims > 0): the latent codes, fp32 rows of NGP_EXTRA_ROW (zero past n_extra_dims); sample i reads row
 	// sample_img[i] (training: the sample's image), or row 0 without sample_img (rendering: the rendering code)
 	const float* extra;
 	const uint32_t* sample_img;
-	float* dextra;  // optional [n][16] dL/d(latent code) of each sample's own row (the extra dims' gradient)
+	float* dextra;  // optional [n][NGP_EXTRA_ROW] dL/d(latent code) of each sample's own row (the extra dims' gradient)
 };
 
 __device__ __forceinline__ f4 mfma(h8 a, h8 b, f4 c) { return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0); }
@@ -322,7 +324,7 @@ struct RawTile {
 	float d[CT_][3];             // warped direction, or
 	uint32_t h[CT_][2];          // SH inputs 4g .. 4g+3 (precomputed rows)
 	uint32_t ri[CT_];            // SHIN: the samples' SH row indices
-	uint32_t x[CT_][2];          // Net::XE: latent-code components 4g .. 4g+3 (fp16 pairs)
+	uint32_t x[CT_][N::XE == 2 ? 4 : 2];  // Net::XE: latent-code components 4g .. 4g+3 (and 16 + 4g .. +3: XE 2), fp16 pairs
 };
 
 // Buffer resource over a device array (raw buffer, 32-bit byte offsets; reads past
@@ -411,11 +413,14 @@ __device__ __forceinline__ void rf_load(const MlpArgs& a, __amdgpu_buffer_rsrc_t
 		if constexpr (N::XE) {
 			if (want_dir) {
 				const uint32_t row = a.sample_img && i < a.n ? a.sample_img[i] : 0u;
-				const float4 v = *reinterpret_cast<const float4*>(a.extra + (size_t)row * 16 + 4 * g);
-				const h4 hv = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
-				const uint2 u = __builtin_bit_cast(uint2, hv);
-				r.x[c][0] = u.x;
-				r.x[c][1] = u.y;
+#pragma unroll
+				for (int hh = 0; hh < N::XE; ++hh) {
+					const float4 v = *reinterpret_cast<const float4*>(a.extra + (size_t)row * NGP_EXTRA_ROW + 16 * hh + 4 * g);
+					const h4 hv = {(_Float16)v.x, (_Float16)v.y, (_Float16)v.z, (_Float16)v.w};
+					const uint2 u = __builtin_bit_cast(uint2, hv);
+					r.x[c][2 * hh] = u.x;
+					r.x[c][2 * hh + 1] = u.y;
+				}
 			}
 		}
 		if (want_dir && SHIN) {
@@ -557,7 +562,9 @@ __device__ __forceinline__ void rf_tile(const MlpArgs& a, const h8* w, const Raw
 				b[cc][0] = c_to_b(c[cc][0], shv);  // rgb input: [density out 16 | SH 16]
 			}
 			// the latent code (rgb input rows 32..47; the K permutation puts rows 32 + 4g .. +3 in slots 0..3)
-			if constexpr (N::XE) b[cc][1] = pack_h8(cur.x[cc][0], cur.x[cc][1], 0u, 0u);
+			if constexpr (N::XE == 1) b[cc][1] = pack_h8(cur.x[cc][0], cur.x[cc][1], 0u, 0u);
+			// XE 2: slots 4..7 of the second K step are rgb input rows 48 + 4g .. +3 = code components 16 + 4g .. +3
+			if constexpr (N::XE == 2) b[cc][1] = pack_h8(cur.x[cc][0], cur.x[cc][1], cur.x[cc][2], cur.x[cc][3]);
 		}
 		rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
 		rf_layer<N, N::NL - 1, CT_>(w, b, c);
@@ -677,6 +684,43 @@ __device__ __forceinline__ uint32_t sh_load_live(__amdgpu_buffer_rsrc_t sh_rs, i
 	return __builtin_amdgcn_readfirstlane(live);
 }
 
+// One wave step of k_mlp_infer_sh: rf_tile's SH-row path with the renderer's [n][4] output only, stored through a
+// buffer resource whose extent is the device-side sample count (the stores past it are dropped by the hardware:
+// no per-sample compare, 32-bit offsets instead of 64-bit address arithmetic per column tile)
+template <class N, int CT_>
+__device__ __forceinline__ void sh_tile(const h8* w, const RawTile<N, CT_>& cur, __amdgpu_buffer_rsrc_t out_rs, uint32_t base,
+                                        int g, int n, uint32_t live) {
+	if (live == 0) return;
+	h8 b[CT_][2];
+	f4 c[CT_][4];
+#pragma unroll
+	for (int cc = 0; cc < CT_; ++cc)
+#pragma unroll
+		for (int s = 0; s < N::KE; ++s)
+			b[cc][s] = pack_h8(cur.e[cc][4 * s], cur.e[cc][4 * s + 1], cur.e[cc][4 * s + 2], cur.e[cc][4 * s + 3]);
+	rf_hidden_range<N, 0, N::DH, CT_>(w, b, c);
+	rf_layer<N, N::DH, CT_>(w, b, c);
+	h4 dens[CT_];
+#pragma unroll
+	for (int cc = 0; cc < CT_; ++cc) {
+		dens[cc] = h4{(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], (_Float16)c[cc][0][3]};
+		const uint2 lu = __builtin_bit_cast(uint2, dens[cc]);
+		b[cc][0] = pack_h8(lu.x, lu.y, cur.h[cc][0], cur.h[cc][1]);  // rgb input: [density out 16 | SH 16]
+	}
+	rf_hidden_range<N, N::DH + 1, N::NL - 1, CT_>(w, b, c);
+	rf_layer<N, N::NL - 1, CT_>(w, b, c);
+	if (g == 0) {
+#pragma unroll
+		for (int cc = 0; cc < CT_; ++cc) {
+			if ((live >> cc) & 1u) {
+				const h4 o = {(_Float16)c[cc][0][0], (_Float16)c[cc][0][1], (_Float16)c[cc][0][2], dens[cc][0]};
+				const uint2 u = __builtin_bit_cast(uint2, o);
+				__builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(v2u, u), out_rs, 8 * (base + 16 * cc + n), 0, 0);
+			}
+		}
+	}
+}
+
 template <class N, int CT_, int PF, int FF>
 __global__ void __launch_bounds__(BLOCK) k_mlp_infer_sh(MlpArgs a) {
 	static_assert(N::KE <= 2 && N::Wp <= 64 && N::XE == 0, "register layout assumes <= 2 K-steps per layer, no extra dims");
@@ -700,6 +744,7 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_sh(MlpArgs a) {
 	const __amdgpu_buffer_rsrc_t crd_rs = make_rsrc(a.sh_ray, a.coord_bytes);
 	const __amdgpu_buffer_rsrc_t sh_rs = make_rsrc(a.sh, a.sh_bytes);
 	const bool skip = a.skip_unfilled != 0;
+	const __amdgpu_buffer_rsrc_t out_rs = make_rsrc(a.out, 8u * a.n);  // a.n: the device-side count
 	// slot of tile t0 + k * stride: k % R (the loop is unrolled R times, so every slot index is static)
 	constexpr int R = PF + 1;
 	RawTile<N, CT_> ring[R];
@@ -721,7 +766,7 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_sh(MlpArgs a) {
 			live[(q + 1) % R] = sh_load_live<N, CT_>(sh_rs, g, ring[(q + 1) % R], skip);
 			ri_load<N, CT_>(crd_rs, (t + (PF + 1) * stride) * TS, n, ring[q]);
 			rf_load<N, CT_, FF, true>(a, enc_rs, crd_rs, (t + PF * stride) * TS, g, n, ring[(q + PF) % R], false);
-			rf_tile<N, CT_, PF, false, true>(a, wl, ring[q], t * TS, g, n, (int32_t)live[q]);
+			sh_tile<N, CT_>(wl, ring[q], out_rs, t * TS, g, n, live[q]);
 		}
 	}
 }
@@ -746,7 +791,7 @@ __device__ __forceinline__ void wgrad_layer(const _Float16* imgs, const _Float16
 		const int mt = t / KTN, kt = t % KTN;
 		if (gt % TWAVES != wave) continue;
 		if (l == 0 && (uint32_t)(16 * kt) >= enc_pad) continue;
-		if (N::XE && l == N::DH + 1 && kt == 3) continue;  // the latent code's zero padding rows
+		if (N::XE == 1 && l == N::DH + 1 && kt == 3) continue;  // the latent code's zero padding rows
 		const int slot = gt / TWAVES;
 		f4 c = acc[slot];
 #pragma unroll
@@ -785,8 +830,8 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 	for (int mt = 0; mt < KT; ++mt) {
 		// rgb input rows: 16..31 SH (camera gradients), 32..47 the latent code (extra dims), 48..63 padding
 		if (l == N::DH + 1 && mt == 1 && !a.dsh) continue;
-		if (l == N::DH + 1 && mt == 2 && !a.dextra) continue;
-		if (l == N::DH + 1 && mt >= 3) continue;
+		if (l == N::DH + 1 && mt >= 2 && !a.dextra) continue;
+		if (l == N::DH + 1 && mt >= 2 + N::XE) continue;  // XE 1: rows 48..63 are padding
 		h8 af[MS];
 #pragma unroll
 		for (int s = 0; s < MS; ++s) af[s] = lds_h8(fr + ((mt * MS + s) * 64 + lane) * 8);
@@ -813,8 +858,8 @@ __device__ __forceinline__ void dgrad_layer(const MlpArgs& a, const _Float16* fr
 				// dL/d(SH) or dL/d(latent code) of the sample's own row: the deltas carry its rollover weight
 				if (i < a.n) {
 					const float inv = a.weight ? 1.0f / a.weight[i] : 1.0f;
-					float* dst = mt == 1 ? a.dsh : a.dextra;
-					*reinterpret_cast<float4*>(dst + (size_t)i * 16 + 4 * g) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
+					float* dst = mt == 1 ? a.dsh + (size_t)i * 16 : a.dextra + (size_t)i * NGP_EXTRA_ROW + 16 * (mt - 2);
+					*reinterpret_cast<float4*>(dst + 4 * g) = make_float4(acc[0] * inv, acc[1] * inv, acc[2] * inv, acc[3] * inv);
 				}
 			} else if constexpr (l > 0) {
 				h4 o = {(_Float16)acc[0], (_Float16)acc[1], (_Float16)acc[2], (_Float16)acc[3]};
@@ -918,19 +963,22 @@ struct TrainPrefetch {
 	float d[3];
 	uint2 dl;
 	float w;
-	float4 x[2];  // Net::XE: latent-code components 8 (lane / SPW - 2) .. +7 of this lane's sample
+	float4 x[4];  // Net::XE: latent-code components 8h .. 8h + 7 (XE 1) / 16h .. 16h + 15 (XE 2), h = lane / SPW - 2
 };
 
-// the latent code of sample i (Net::XE), components 8h .. 8h + 7 as fp16 (tcnn's Identity encoding: the float
-// input converted to the network's half type); zeros past the batch
-__device__ __forceinline__ void load_extra8(const MlpArgs& a, uint32_t i, int h, float4 (&x)[2]) {
-	x[0] = x[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+// the latent code of sample i (Net::XE), components 4Q h .. 4Q h + 4Q - 1 (Q float4s) as fp32 -- converted to fp16
+// (tcnn's Identity encoding: the float input in the network's half type) by extra_h8; zeros past the batch
+template <int Q, int NX>
+__device__ __forceinline__ void load_extra(const MlpArgs& a, uint32_t i, int h, float4 (&x)[NX]) {
+#pragma unroll
+	for (int q = 0; q < Q; ++q) x[q] = make_float4(0.f, 0.f, 0.f, 0.f);
 	if (i >= a.n) return;
 	const uint32_t row = a.sample_img ? a.sample_img[i] : 0u;
-	const float4* src = reinterpret_cast<const float4*>(a.extra + (size_t)row * 16 + 8 * h);
-	x[0] = src[0];
-	x[1] = src[1];
+	const float4* src = reinterpret_cast<const float4*>(a.extra + (size_t)row * NGP_EXTRA_ROW + 4 * Q * h);
+#pragma unroll
+	for (int q = 0; q < Q; ++q) x[q] = src[q];
 }
+__device__ __forceinline__ void load_extra8(const MlpArgs& a, uint32_t i, int h, float4 (&x)[2]) { load_extra<2>(a, i, h, x); }
 __device__ __forceinline__ h8 extra_h8(const float4 (&x)[2]) {
 	return h8{(_Float16)x[0].x, (_Float16)x[0].y, (_Float16)x[0].z, (_Float16)x[0].w,
 	          (_Float16)x[1].x, (_Float16)x[1].y, (_Float16)x[1].z, (_Float16)x[1].w};
@@ -955,7 +1003,7 @@ __device__ __forceinline__ void train_fetch(const MlpArgs& a, uint32_t base, int
 #pragma unroll
 	for (int k = 0; k < 3; ++k) p.d[k] = in ? c[4 + k] : 0.5f;
 	if constexpr (N::XE) {
-		if (lane >= 2 * SPW_ && lane < 4 * SPW_) load_extra8(a, i, lane / SPW_ - 2, p.x);
+		if (lane >= 2 * SPW_ && lane < 4 * SPW_) load_extra<2 * N::XE>(a, i, lane / SPW_ - 2, p.x);
 	}
 	p.dl = make_uint2(0u, 0u);
 	p.w = 1.0f;
@@ -996,8 +1044,15 @@ __device__ __forceinline__ void train_commit(const MlpArgs& a, const TrainPrefet
 		for (int k = 0; k < 8; ++k) o[k] = in ? (_Float16)(half ? v[8 + k] : v[k]) : (_Float16)0;
 		if (half < 2) lds_st_h8(img + smp * STRIDE + x_seg + 16 + 8 * half, o);
 		if constexpr (N::XE) {
-			// the latent code: rgb input rows 32..47
-			if (half >= 2 && half < 4) lds_st_h8(img + smp * STRIDE + x_seg + 32 + 8 * (half - 2), extra_h8(p.x));
+			// the latent code: rgb input rows 32..47 (XE 2: 32..63, 16 per lane)
+			if (half >= 2 && half < 4) {
+				const float4 x0[2] = {p.x[0], p.x[1]};
+				lds_st_h8(img + smp * STRIDE + x_seg + 32 + 8 * N::XE * (half - 2), extra_h8(x0));
+				if constexpr (N::XE == 2) {
+					const float4 x1[2] = {p.x[2], p.x[3]};
+					lds_st_h8(img + smp * STRIDE + x_seg + 32 + 16 * (half - 2) + 8, extra_h8(x1));
+				}
+			}
 		}
 	}
 	for (int t = lane; t < SPW_ * 4; t += 64) {
@@ -1054,7 +1109,7 @@ __global__ void __launch_bounds__(TBLOCK) k_mlp_train(MlpArgs a) {
 			load_encoding<N, STRIDE, TSPW>(a, img, base, lane);
 			load_sh<STRIDE, TSPW>(a, img, N::template x_seg<true>(), base, lane);
 			if constexpr (N::XE) {
-				for (int t = lane; t < TSPW * 2; t += 64) {
+				for (int t = lane; t < TSPW * 2 * N::XE; t += 64) {
 					float4 x[2];
 					load_extra8(a, base + t % TSPW, t / TSPW, x);
 					lds_st_h8(img + (t % TSPW) * STRIDE + N::template x_seg<true>() + 32 + 8 * (t / TSPW), extra_h8(x));
@@ -1173,10 +1228,11 @@ using V4 = Net<64, 2, 2, 1>;
 using V5 = Net<64, 1, 1, 1>;
 using V6 = Net<64, 1, 3, 1>;
 using V7 = Net<64, 1, 2, 1, 1>;  // lego / base.json with per-image latent codes (n_extra_dims 1..16)
+using V8 = Net<64, 1, 2, 1, 2>;  // the same with n_extra_dims 17..32 (light directions + a 16-wide code)
 
 int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad, uint32_t n_extra_dims) {
 	const uint32_t ke = enc_pad <= 32 ? 1 : (enc_pad <= 64 ? 2 : 0);
-	if (n_extra_dims) return width == 64 && dh == 1 && rh == 2 && ke == 1 && n_extra_dims <= 16 ? 7 : -1;
+	if (n_extra_dims) return width == 64 && dh == 1 && rh == 2 && ke == 1 && n_extra_dims <= 32 ? (n_extra_dims <= 16 ? 7 : 8) : -1;
 	if (width == 64 && dh == 1 && rh == 2 && ke == 1) return 0;
 	if (width == 64 && dh == 1 && rh == 2 && ke == 2) return 1;
 	if (width == 16 && dh == 1 && rh == 2 && ke == 1) return 2;
@@ -1216,6 +1272,7 @@ static void layer_geometry(const ngp_model* m, PackArgs& p) {
 		case 5: { using N = V5; __VA_ARGS__; } break;           \
 		case 6: { using N = V6; __VA_ARGS__; } break;           \
 		case 7: { using N = V7; __VA_ARGS__; } break;           \
+		case 8: { using N = V8; __VA_ARGS__; } break;           \
 		default: throw std::runtime_error("unsupported MLP configuration"); \
 	}
 
@@ -1316,7 +1373,7 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		const uint32_t pipe = m->tuning.render_mlp_pipeline ? m->tuning.render_mlp_pipeline : 2u;
 		bool done = false;
 		if constexpr (N::XE == 0) {
-			if (sh && a.F == 2 && pl && pipe >= 2) {
+			if (sh && a.F == 2 && pl && pipe >= 2 && out_mode == 0) {
 				const uint32_t wg = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : (tile == 4 ? 6u : 8u);
 				const uint32_t ts = 16 * (tile == 4 ? 4 : tile == 2 ? 2 : 1);
 				const uint32_t grid_sh = std::min<uint32_t>(div_up(n, ts * WAVES), cu_count() * wg);

@@ -190,7 +190,7 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 		        "n_features_per_level must be 1, 2, 4 or 8");
 		require(cfg->log2_hashmap_size >= 4 && cfg->log2_hashmap_size <= 30, "log2_hashmap_size out of range");
 		require(cfg->per_level_scale > 0.0f, "per_level_scale must be positive");
-		require(cfg->n_extra_dims <= 16, "n_extra_dims must be <= 16 (the rgb network's input holds one 16-wide latent code)");
+		require(cfg->n_extra_dims <= NGP_EXTRA_DIMS_MAX, "n_extra_dims must be <= 32 (light directions + a 16-wide latent code fit)");
 		NGP_HIP_CHECK(hipSetDevice(hip_device));
 		auto* m = new ngp_model();
 		try {
@@ -212,8 +212,8 @@ ngp_status ngp_model_create(int hip_device, const ngp_network_config* cfg, uint6
 				                                                "layers and an encoding of <= 32 features"
 				                                              : "unsupported MLP shape (n_neurons / hidden layers)");
 			if (cfg->n_extra_dims) {
-				m->zero_extra.reserve(16);
-				NGP_HIP_CHECK(hipMemset(m->zero_extra.ptr, 0, 16 * sizeof(float)));
+				m->zero_extra.reserve(NGP_EXTRA_ROW);
+				NGP_HIP_CHECK(hipMemset(m->zero_extra.ptr, 0, NGP_EXTRA_ROW * sizeof(float)));
 			}
 			build_level_table(m);
 			build_layers(m);
@@ -383,12 +383,12 @@ ngp_status ngp_model_encode_indices(ngp_model* m, const float* pos, uint32_t str
 }
 
 // The latent codes NerfCoordinate records carry after their 7 floats (set_with_optional_extra_dims,
-// nerf_device.cuh:177-195) -> rows of 16 (zero-padded) and row indices i (MlpExtra with one row per sample)
+// nerf_device.cuh:177-195) -> rows of NGP_EXTRA_ROW (zero-padded) and row indices i (MlpExtra with one row per sample)
 __global__ void k_extra_rows(const float* __restrict__ src, uint32_t stride, uint32_t offset, uint32_t E, uint32_t n,
                              float* __restrict__ rows, uint32_t* __restrict__ idx) {
 	const uint32_t i = blockIdx.x * 256u + threadIdx.x;
 	if (i >= n) return;
-	for (uint32_t k = 0; k < 16; ++k) rows[16 * (size_t)i + k] = k < E ? src[(size_t)i * stride + offset + k] : 0.0f;
+	for (uint32_t k = 0; k < NGP_EXTRA_ROW; ++k) rows[NGP_EXTRA_ROW * (size_t)i + k] = k < E ? src[(size_t)i * stride + offset + k] : 0.0f;
 	idx[i] = i;
 }
 
@@ -396,7 +396,7 @@ static MlpExtra coord_extras(ngp_model* m, const float* src, uint32_t stride, ui
 	MlpExtra x;
 	if (!m->cfg.n_extra_dims || n == 0) return x;
 	TrainScratch& ts = m->ts;
-	ts.api_extra.reserve(16 * (size_t)n);
+	ts.api_extra.reserve(NGP_EXTRA_ROW * (size_t)n);
 	ts.api_extra_idx.reserve(n);
 	k_extra_rows<<<div_up(n, 256u), 256, 0, s>>>(src, stride, offset, m->cfg.n_extra_dims, n, ts.api_extra.ptr, ts.api_extra_idx.ptr);
 	NGP_HIP_CHECK(hipGetLastError());
@@ -516,7 +516,7 @@ static void model_backward(ngp_model* m, const uint16_t* enc, const float* dirs,
 		for (size_t i = 0; i < n; ++i)
 			for (int k = 0; k < 3; ++k) tmp[8 * i + 4 + k] = d[3 * i + k];
 		NGP_HIP_CHECK(hipMemcpyAsync(ts.ccoords.ptr, tmp.data(), tmp.size() * 4, hipMemcpyHostToDevice, S(s)));
-		MlpExtra x = extra ? coord_extras(m, extra, 16, 0, n, S(s)) : MlpExtra{};
+		MlpExtra x = extra ? coord_extras(m, extra, NGP_EXTRA_ROW, 0, n, S(s)) : MlpExtra{};
 		x.dextra = dextra;
 		m->timers.begin_kernel(NGP_TIMER_TRAIN_MLP_BWD);
 		launch_mlp_train(m, m->frag_train.ptr, reinterpret_cast<const __half*>(enc), EncLayout{n, 0}, ts.ccoords.ptr, 8, n,

@@ -297,9 +297,9 @@ struct TrainScratch {
 	DevBuf<uint32_t> simg, eimg, cimg;
 	DevBuf<float> dextra;              // [B][16]
 	// deterministic steps: per-image fixed-point gradient sums [n_images][IMG_FIX_STRIDE]: exposure 0-2, camera
-	// translation 3-5, rotation 6-8, latent code 9-24 (train.hip img_deposit_fixed)
+	// translation 3-5, rotation 6-8, latent code 9-40 (train.hip img_deposit_fixed)
 	DevBuf<unsigned long long> img_fix;
-	DevBuf<float> api_extra;           // C-ABI entries: the latent codes of coordinate records, rows of 16
+	DevBuf<float> api_extra;           // C-ABI entries: the latent codes of coordinate records, rows of NGP_EXTRA_ROW
 	DevBuf<uint32_t> api_extra_idx;
 	DevBuf<uint32_t> dp;               // data parallel: [0,3) sample DpCaps, [4,7) compaction DpCaps, then 2 x [world] slots
 	bool chunked = false;              // last step ran the chunked forward
@@ -318,7 +318,7 @@ __device__ __forceinline__ void set_wave_priority(uint32_t p) {
 	else if (p >= 3) __builtin_amdgcn_s_setprio(3);
 }
 
-constexpr uint32_t IMG_FIX_STRIDE = 25;
+constexpr uint32_t IMG_FIX_STRIDE = 9 + NGP_EXTRA_ROW;
 
 struct GridState {
 	DevBuf<float> grid;        // [n_cascades][N]
@@ -489,7 +489,7 @@ void launch_hashgrid_indices(const LevelTable& lt, const float* pos, uint32_t st
 int mlp_variant_for(uint32_t width, uint32_t dh, uint32_t rh, uint32_t enc_pad, uint32_t n_extra_dims = 0);
 uint32_t mlp_frag_halves(const ngp_model* m);
 void pack_mlp_fragments(const ngp_model* m, const __half* params16, __half* frags, hipStream_t s);
-// The latent codes of a model with n_extra_dims > 0 (the rgb network's extra inputs): extra = fp32 rows of 16
+// The latent codes of a model with n_extra_dims > 0 (the rgb network's extra inputs): extra = fp32 rows of NGP_EXTRA_ROW
 // (zero past n_extra_dims), sample i reads row sample_img[i], or row 0 without sample_img; extra null: zeros.
 // dextra (training): [n][16] dL/d(latent code) of each sample's own row.
 struct MlpExtra {

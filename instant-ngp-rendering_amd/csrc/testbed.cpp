@@ -225,7 +225,7 @@ Testbed::~Testbed() {
 	for (float* p : {m_err, m_cdf_x, m_cdf_y, m_cdf_img, m_exp, m_exp_grad, m_cam_grad, m_sharp_grid, m_dist, m_dist_grad, m_extra, m_extra_grad})
 		if (p) (void)hipFree(p);
 	if (m_comm) ncclCommDestroy((ncclComm_t)m_comm);
-	if (m_extra_stage) pinned_host_release(m_extra_stage, 16 * sizeof(float));
+	if (m_extra_stage) pinned_host_release(m_extra_stage, NGP_EXTRA_ROW * sizeof(float));
 	if (m_stream) (void)hipStreamDestroy((hipStream_t)m_stream);
 }
 
@@ -1184,7 +1184,8 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 		if (!m_extra) upload_extra_dims();
 		a.extra_dims = m_extra;
 		if (train_extra_dims) {
-			hk(hipMemsetAsync(m_extra_grad, 0, (m_extra_rows - 1) * 16 * sizeof(float), (hipStream_t)m_stream), "extra dims gradient clear");
+			hk(hipMemsetAsync(m_extra_grad, 0, (m_extra_rows - 1) * NGP_EXTRA_ROW * sizeof(float), (hipStream_t)m_stream),
+			   "extra dims gradient clear");
 			a.extra_dims_gradient = m_extra_grad;
 		}
 	}
@@ -1298,7 +1299,7 @@ void Testbed::train_nerf(uint32_t batch, bool get_loss_scalar) {
 	}
 	// the latent codes' Adam step on every step (src/testbed_nerf.cu:2580-2599); data parallel: their gradient summed
 	if (train_extra_dims) {
-		if (distributed()) allreduce_f32(m_extra_grad, (m_extra_rows - 1) * 16, false);
+		if (distributed()) allreduce_f32(m_extra_grad, (m_extra_rows - 1) * NGP_EXTRA_ROW, false);
 		update_extra_dims_step();
 	}
 	++training_step;
@@ -1746,7 +1747,7 @@ void Testbed::reset_extra_dims(pcg32* rng) {
 	tr.extra_dims_opt.clear();
 	m_rendering_extra_dims.assign(E, 0.0f);
 	if (!E) return;
-	if (E > 16) throw std::runtime_error("n_extra_dims > 16 is not supported (light directions + latent code)");
+	if (E > NGP_EXTRA_DIMS_MAX) throw std::runtime_error("n_extra_dims > 32 is not supported (light directions + latent code)");
 	const size_t n = tr.dataset.n_images;
 	tr.extra_dims_opt.resize(n);
 	for (size_t i = 0; i < n; ++i) {
@@ -1768,7 +1769,7 @@ void Testbed::reset_extra_dims(pcg32* rng) {
 	upload_extra_dims();
 }
 
-// Nerf::Training::update_extra_dims (src/testbed_nerf.cu:1814-1825): the codes into the device table, rows of 16
+// Nerf::Training::update_extra_dims (src/testbed_nerf.cu:1814-1825): the codes into the device table, rows of NGP_EXTRA_ROW
 void Testbed::upload_extra_dims() {
 	const NerfTraining& tr = nerf.training;
 	const uint32_t E = tr.dataset.n_extra_dims();
@@ -1779,15 +1780,15 @@ void Testbed::upload_extra_dims() {
 		for (float* p : {m_extra, m_extra_grad})
 			if (p) (void)hipFree(p);
 		m_extra = m_extra_grad = nullptr;
-		hk(hipMalloc((void**)&m_extra, rows * 16 * sizeof(float)), "hipMalloc extra dims");
-		hk(hipMalloc((void**)&m_extra_grad, rows * 16 * sizeof(float)), "hipMalloc extra dims gradient");
-		hk(hipMemset(m_extra, 0, rows * 16 * sizeof(float)), "hipMemset extra dims");
+		hk(hipMalloc((void**)&m_extra, rows * NGP_EXTRA_ROW * sizeof(float)), "hipMalloc extra dims");
+		hk(hipMalloc((void**)&m_extra_grad, rows * NGP_EXTRA_ROW * sizeof(float)), "hipMalloc extra dims gradient");
+		hk(hipMemset(m_extra, 0, rows * NGP_EXTRA_ROW * sizeof(float)), "hipMemset extra dims");
 		m_extra_rows = rows;
 	}
-	m_extra_host.assign(rows * 16, 0.0f);
+	m_extra_host.assign(rows * NGP_EXTRA_ROW, 0.0f);
 	for (size_t i = 0; i < tr.extra_dims_opt.size(); ++i)
-		for (uint32_t j = 0; j < E; ++j) m_extra_host[16 * i + j] = tr.extra_dims_opt[i].variable[j];
-	hk(hipMemcpy(m_extra, m_extra_host.data(), (rows - 1) * 16 * sizeof(float), hipMemcpyHostToDevice), "upload extra dims");
+		for (uint32_t j = 0; j < E; ++j) m_extra_host[NGP_EXTRA_ROW * i + j] = tr.extra_dims_opt[i].variable[j];
+	hk(hipMemcpy(m_extra, m_extra_host.data(), (rows - 1) * NGP_EXTRA_ROW * sizeof(float), hipMemcpyHostToDevice), "upload extra dims");
 }
 
 // Nerf::get_rendering_extra_dims (src/testbed_nerf.cu:3206-3228): a training view's code or the set one, with the
@@ -1800,13 +1801,14 @@ const float* Testbed::rendering_extra_dims_device() {
 	const std::vector<float> row = rendering_extra_dims();
 	// staged in a page-locked row of its own: the copy is still in flight when this returns, and render() synchronises
 	// the stream before the next call writes the row again
-	if (!m_extra_stage) m_extra_stage = static_cast<float*>(pinned_host_alloc(16 * sizeof(float)));
-	std::fill(m_extra_stage, m_extra_stage + 16, 0.0f);
+	if (!m_extra_stage) m_extra_stage = static_cast<float*>(pinned_host_alloc(NGP_EXTRA_ROW * sizeof(float)));
+	std::fill(m_extra_stage, m_extra_stage + NGP_EXTRA_ROW, 0.0f);
 	std::copy(row.begin(), row.end(), m_extra_stage);
 	const size_t n = m_extra_rows - 1;
-	hk(hipMemcpyAsync(m_extra + 16 * n, m_extra_stage, 16 * sizeof(float), hipMemcpyHostToDevice, (hipStream_t)m_stream),
+	hk(hipMemcpyAsync(m_extra + NGP_EXTRA_ROW * n, m_extra_stage, NGP_EXTRA_ROW * sizeof(float), hipMemcpyHostToDevice,
+	                  (hipStream_t)m_stream),
 	   "upload rendering extra dims");
-	return m_extra + 16 * n;
+	return m_extra + NGP_EXTRA_ROW * n;
 }
 
 // train_nerf's latent-code step (src/testbed_nerf.cu:2580-2599): the codes' gradient (loss-scaled sums over the
@@ -1816,14 +1818,14 @@ void Testbed::update_extra_dims_step() {
 	NerfTraining& tr = nerf.training;
 	const uint32_t E = tr.dataset.n_extra_dims();
 	const size_t n = m_extra_rows - 1;
-	std::vector<float> g(n * 16);
-	hk(hipMemcpyAsync(g.data(), m_extra_grad, n * 16 * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream),
+	std::vector<float> g(n * NGP_EXTRA_ROW);
+	hk(hipMemcpyAsync(g.data(), m_extra_grad, n * NGP_EXTRA_ROW * sizeof(float), hipMemcpyDeviceToHost, (hipStream_t)m_stream),
 	   "extra dims gradient d2h");
 	sync();
 	const float lr = current_learning_rate();
 	for (int i = 0; i < tr.n_images_for_training && (size_t)i < tr.extra_dims_opt.size(); ++i) {
 		std::vector<float> gi(E);
-		for (uint32_t j = 0; j < E; ++j) gi[j] = g[16 * (size_t)i + j] / 128.0f;
+		for (uint32_t j = 0; j < E; ++j) gi[j] = g[NGP_EXTRA_ROW * (size_t)i + j] / 128.0f;
 		tr.extra_dims_opt[i].learning_rate = lr;
 		tr.extra_dims_opt[i].step(gi);
 	}

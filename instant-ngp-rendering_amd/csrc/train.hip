@@ -1259,13 +1259,15 @@ __global__ void __launch_bounds__(256) k_extra_gradient(uint32_t n_rays, const u
 	if (i >= n_rays || (viol_gate && *viol_gate)) return;
 	const uint32_t cn = compacted[2 * i], cbase = compacted[2 * i + 1];
 	if (cn == 0) return;
-	float g[16];
+	float g[NGP_EXTRA_ROW];
 #pragma unroll
-	for (uint32_t k = 0; k < 16; ++k) g[k] = 0.0f;
+	for (uint32_t k = 0; k < NGP_EXTRA_ROW; ++k) g[k] = 0.0f;
+	const uint32_t nq = E > 16 ? NGP_EXTRA_ROW / 4 : 4;  // float4s of a row holding the E components
 	for (uint32_t j = 0; j < cn; ++j) {
-		const float4* src = reinterpret_cast<const float4*>(dextra + 16 * ((size_t)cbase + j));
+		const float4* src = reinterpret_cast<const float4*>(dextra + NGP_EXTRA_ROW * ((size_t)cbase + j));
 #pragma unroll
-		for (uint32_t q = 0; q < 4; ++q) {
+		for (uint32_t q = 0; q < NGP_EXTRA_ROW / 4; ++q) {
+			if (q >= nq) break;
 			const float4 v = src[q];
 			g[4 * q] += v.x;
 			g[4 * q + 1] += v.y;
@@ -1275,10 +1277,10 @@ __global__ void __launch_bounds__(256) k_extra_gradient(uint32_t n_rays, const u
 	}
 	const uint32_t img = __float_as_uint(loss_state[8 * (size_t)i + 7]);
 #pragma unroll
-	for (uint32_t k = 0; k < 16; ++k) {
+	for (uint32_t k = 0; k < NGP_EXTRA_ROW; ++k) {
 		if (k >= E) continue;
 		if (fix) img_deposit_fixed(&fix[IMG_FIX_STRIDE * (size_t)img + 9 + k], g[k]);
-		else atomicAdd(&grad[16 * (size_t)img + k], g[k]);
+		else atomicAdd(&grad[NGP_EXTRA_ROW * (size_t)img + k], g[k]);
 	}
 }
 
@@ -1761,7 +1763,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 	if (xd) {
 		ts.simg.grow(MS);
 		ts.cimg.reserve(B);
-		if (t->extra_dims_gradient) ts.dextra.reserve(16 * (size_t)B);
+		if (t->extra_dims_gradient) ts.dextra.reserve(NGP_EXTRA_ROW * (size_t)B);
 	}
 	ts.cpos4.reserve(4 * (size_t)B);
 	ts.cenc.reserve((size_t)L * B * F);
@@ -2183,7 +2185,7 @@ void run_train_step(ngp_model* m, const ngp_train_args* t, hipStream_t s) {
 			flush(3, 3, t->cam_pos_gradient);
 			flush(6, 3, t->cam_rot_gradient);
 		}
-		if (xgrad) flush(9, 16, t->extra_dims_gradient);  // rows of 16, the first E written
+		if (xgrad) flush(9, NGP_EXTRA_ROW, t->extra_dims_gradient);  // rows of NGP_EXTRA_ROW, the first E written
 	}
 	tm.train_units_pending = tm.mask != 0;
 

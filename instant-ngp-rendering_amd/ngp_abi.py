@@ -134,6 +134,10 @@ class Tuning(C.Structure):
     ]
 
 
+# latent-code rows (include/ngp_hip.h NGP_EXTRA_ROW / NGP_EXTRA_DIMS_MAX)
+EXTRA_ROW = 32
+EXTRA_DIMS_MAX = 32
+
 # enums (include/ngp_hip.h)
 PARAMS_FP32, PARAMS_FP16, PARAMS_EMA_FP32, PARAMS_INFER_FP16, GRADS_FP32, ADAM_M, ADAM_V, GRADS_GRID_FP16, \
     GRADS_GRID_FIXED64 = range(9)

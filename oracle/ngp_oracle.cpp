@@ -697,7 +697,7 @@ static void mlp_forward(const Model& M, const uint16_t* P, const float* enc, con
 // NerfNetwork::backward_impl (nerf_network.h:189-268): rgb MLP bwd -> add_density_gradient -> density MLP bwd
 // dsh (optional, [n][16]): dL/d(SH inputs) of the sample's own row (÷ its rollover weight), for the
 // camera gradients (tcnn's input gradient through the Composite encoding's SH part)
-// codes / code_stride: the samples' latent codes (mlp_forward); dextra (optional, [n][16]): dL/d(rgb input rows
+// codes / code_stride: the samples' latent codes (mlp_forward); dextra (optional, [n][NGP_EXTRA_ROW]): dL/d(rgb input rows
 // 32..47) of the sample's own row (÷ its rollover weight) -- the extra dims' input gradient
 static void mlp_backward(const Model& M, float* grads, const uint16_t* P, const float* enc, const float* coords, uint32_t cs,
                          uint32_t n, const float* dl /*[n][4] fp16 values*/, const float* weight, float* denc,
@@ -734,11 +734,11 @@ static void mlp_backward(const Model& M, float* grads, const uint16_t* P, const 
 					dsh[16 * (size_t)i + (k - 16)] = acc / w;
 				}
 			if (dextra && l == (int)M.n_density_layers)
-				for (uint32_t k = 32; k < 48; ++k) {
+				for (uint32_t k = 32; k < 32 + NGP_EXTRA_ROW; ++k) {
 					float acc = 0.0f;
 					if (k < Ly.in)
 						for (uint32_t r = 0; r < Ly.out; ++r) acc += h2f(W[(size_t)r * Ly.in + k]) * delta[r];
-					dextra[16 * (size_t)i + (k - 32)] = acc / w;
+					dextra[NGP_EXTRA_ROW * (size_t)i + (k - 32)] = acc / w;
 				}
 			if (l == 0) {
 				for (uint32_t k = 0; k < M.E; ++k) denc[((size_t)(k / M.F) * n + i) * M.F + (k % M.F)] = nd[k];
@@ -1262,18 +1262,19 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	M.total_samples = base;
 	const uint32_t S = std::min(base, MS);
 	// n_extra_dims > 0: every sample carries its image's latent code (generate_training_samples_nerf, :730, 824:
-	// extra_dims_gpu + img * n_extra_dims; here rows of 16)
+	// extra_dims_gpu + img * n_extra_dims; here rows of NGP_EXTRA_ROW)
 	const uint32_t XD = M.cfg.n_extra_dims;
-	std::vector<float> scodes(XD ? 16 * (size_t)S : 0, 0.0f);
+	std::vector<float> scodes(XD ? NGP_EXTRA_ROW * (size_t)S : 0, 0.0f);
 	if (XD && a.extra_dims)
 		for (uint32_t i = 0; i < R; ++i)
 			for (uint32_t j = 0; j < M.ray_numsteps[2 * i]; ++j)
-				for (uint32_t k = 0; k < 16; ++k) scodes[16 * ((size_t)M.ray_numsteps[2 * i + 1] + j) + k] = a.extra_dims[16 * (size_t)rimg[i] + k];
+				for (uint32_t k = 0; k < NGP_EXTRA_ROW; ++k)
+					scodes[NGP_EXTRA_ROW * ((size_t)M.ray_numsteps[2 * i + 1] + j) + k] = a.extra_dims[NGP_EXTRA_ROW * (size_t)rimg[i] + k];
 	// inference over the emitted samples with the training params (testbed_nerf.cu:2800-2802)
 	std::vector<float> enc((size_t)M.L * S * M.F), out(4 * (size_t)S);
 	const bool ml_on = a.max_level_rand_training != 0;
 	hg_forward(M, M.p16.data(), M.coords.data(), 8, S, enc.data(), ml_on ? M.coords.data() + 7 : nullptr, 8);
-	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data(), XD ? scodes.data() : nullptr, 16);
+	mlp_forward(M, M.p16.data(), enc.data(), M.coords.data(), 8, S, out.data(), XD ? scodes.data() : nullptr, NGP_EXTRA_ROW);
 	M.mlp_out.assign(4 * (size_t)a.max_samples, 0);
 	for (size_t k = 0; k < out.size(); ++k) M.mlp_out[k] = f2h(out[k]);
 
@@ -1389,7 +1390,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	M.ccoords.assign(8 * (size_t)B, 0.0f);
 	M.dloss.assign(4 * (size_t)B, 0);
 	std::vector<float> cenc((size_t)M.L * B * M.F, 0.0f);
-	std::vector<float> ccodes(XD ? 16 * (size_t)B : 0, 0.0f);  // the compacted samples' latent codes
+	std::vector<float> ccodes(XD ? NGP_EXTRA_ROW * (size_t)B : 0, 0.0f);  // the compacted samples' latent codes
 	const float loss_scale = 128.0f / (float)nrg;
 	const float l2r = ract == 3 ? 1e-4f : 0.0f;
 	const float l1d = M.mean < 0.01f ? 1e-4f : 0.0f;
@@ -1449,7 +1450,7 @@ static void train_step(Model& M, const ngp_train_args& a) {
 		for (uint32_t j = 0; j < cn; ++j) {
 			const size_t s = b0 + j, dst = cb + j;
 			for (int k = 0; k < 8; ++k) M.ccoords[8 * dst + k] = M.coords[8 * s + k];
-			for (uint32_t k = 0; k < (XD ? 16u : 0u); ++k) ccodes[16 * dst + k] = scodes[16 * s + k];
+			for (uint32_t k = 0; k < (XD ? (uint32_t)NGP_EXTRA_ROW : 0u); ++k) ccodes[NGP_EXTRA_ROW * dst + k] = scodes[NGP_EXTRA_ROW * s + k];
 			for (uint32_t l = 0; l < M.L; ++l)
 				for (uint32_t f = 0; f < M.F; ++f) cenc[((size_t)l * B + dst) * M.F + f] = enc[((size_t)l * S + s) * M.F + f];
 			const float* cw = &M.coords[8 * s];
@@ -1490,9 +1491,9 @@ static void train_step(Model& M, const ngp_train_args& a) {
 	const bool cam = ext || dist;
 	std::vector<float> dsh(cam ? 16 * (size_t)C : 0), dpos(cam ? 3 * (size_t)C : 0);
 	const bool xgrad = XD && a.extra_dims_gradient;
-	std::vector<float> dextra(xgrad ? 16 * (size_t)C : 0);
+	std::vector<float> dextra(xgrad ? NGP_EXTRA_ROW * (size_t)C : 0);
 	mlp_backward(M, M.grads.data(), M.p16.data(), ce.data(), M.ccoords.data(), 8, C, dlf.data(), wts.data(), denc.data(),
-	             cam ? dsh.data() : nullptr, XD ? ccodes.data() : nullptr, 16, xgrad ? dextra.data() : nullptr);
+	             cam ? dsh.data() : nullptr, XD ? ccodes.data() : nullptr, NGP_EXTRA_ROW, xgrad ? dextra.data() : nullptr);
 	if (xgrad) {
 		// compute_extra_dims_gradient_train_nerf (src/testbed_nerf.cu:1271-1306): each kept ray's compacted samples'
 		// dL/d(code) into its image's gradient
@@ -1502,8 +1503,8 @@ static void train_step(Model& M, const ngp_train_args& a) {
 			const uint32_t img = (uint32_t)lstate[8 * (size_t)i + 7];
 			for (uint32_t k = 0; k < XD; ++k) {
 				float g = 0.0f;
-				for (uint32_t j = 0; j < cn; ++j) g += dextra[16 * ((size_t)cb + j) + k];
-				a.extra_dims_gradient[16 * (size_t)img + k] += g;
+				for (uint32_t j = 0; j < cn; ++j) g += dextra[NGP_EXTRA_ROW * ((size_t)cb + j) + k];
+				a.extra_dims_gradient[NGP_EXTRA_ROW * (size_t)img + k] += g;
 			}
 		}
 	}
@@ -2155,13 +2156,13 @@ void oref_backward(void* m, const float* enc, const float* dirs, uint32_t n, con
 	for (uint32_t i = 0; i < n; ++i) for (int k = 0; k < 3; ++k) coords[8 * i + 4 + k] = dirs[3 * i + k];
 	mlp_backward(M, M.grads.data(), M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc);
 }
-// the same with latent codes extra [n][16] and their input gradient dextra [n][16] (optional)
+// the same with latent codes extra [n][NGP_EXTRA_ROW] and their input gradient dextra [n][NGP_EXTRA_ROW] (optional)
 void oref_backward_extra(void* m, const float* enc, const float* dirs, const float* extra, uint32_t n, const float* dloss,
                          const float* weight, float* denc, float* dextra) {
 	Model& M = *static_cast<Model*>(m);
 	std::vector<float> coords(8 * (size_t)n, 0.0f);
 	for (uint32_t i = 0; i < n; ++i) for (int k = 0; k < 3; ++k) coords[8 * i + 4 + k] = dirs[3 * i + k];
-	mlp_backward(M, M.grads.data(), M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc, nullptr, extra, 16, dextra);
+	mlp_backward(M, M.grads.data(), M.p16.data(), enc, coords.data(), 8, n, dloss, weight, denc, nullptr, extra, NGP_EXTRA_ROW, dextra);
 }
 void oref_encode_backward(void* m, const float* pos, uint32_t stride, uint32_t n, const float* denc) {
 	hg_backward(*static_cast<Model*>(m), pos, stride, n, denc);

@@ -161,19 +161,22 @@ class GpuModel:
         return denc.float().cpu().numpy().reshape(self.L, n, self.F)
 
     def backward_extra(self, enc16, dirs, extra, dloss16, weight=None):
-        """ngp_model_backward_extra: (dL/denc, dL/dextra [n][16])."""
+        """ngp_model_backward_extra: extra [n][<= EXTRA_ROW] (padded to rows of A.EXTRA_ROW);
+        returns (dL/denc, dL/dextra [n][A.EXTRA_ROW])."""
         n = dirs.shape[0]
         e = dev(enc16.astype(np.float16))
         d = dev(np.ascontiguousarray(dirs, np.float32))
-        x = dev(np.ascontiguousarray(extra, np.float32))
+        xr = np.zeros((n, A.EXTRA_ROW), np.float32)
+        xr[:, :extra.shape[1]] = extra
+        x = dev(xr)
         dl = dev(dloss16.astype(np.float16))
         w = None if weight is None else dev(np.ascontiguousarray(weight, np.float32))
         denc = torch.zeros(self.L * n * self.F, dtype=torch.float16, device="cuda")
-        dx = torch.zeros(n * 16, dtype=torch.float32, device="cuda")
+        dx = torch.zeros(n * A.EXTRA_ROW, dtype=torch.float32, device="cuda")
         A.check(self.lib.ngp_model_backward_extra(self.h, vp(e), vp(d), vp(x), n, vp(dl), None if w is None else vp(w),
                                                   vp(denc), vp(dx), stream()))
         torch.cuda.synchronize()
-        return denc.float().cpu().numpy().reshape(self.L, n, self.F), dx.cpu().numpy().reshape(n, 16)
+        return denc.float().cpu().numpy().reshape(self.L, n, self.F), dx.cpu().numpy().reshape(n, A.EXTRA_ROW)
 
     def encode_backward(self, pos, denc16):
         pos = np.ascontiguousarray(pos, np.float32)

@@ -220,14 +220,17 @@ class Oracle:
         return denc
 
     def backward_extra(self, enc, dirs, extra, dloss, weight=None):
-        """backward() with the samples' latent codes extra [n][16]; returns (dL/denc, dL/dextra [n][16])."""
+        """backward() with the samples' latent codes extra [n][<= EXTRA_ROW] (padded to rows of EXTRA_ROW = 32);
+        returns (dL/denc, dL/dextra [n][EXTRA_ROW])."""
         enc = np.ascontiguousarray(enc, np.float32)
         dirs = np.ascontiguousarray(dirs, np.float32)
-        extra = np.ascontiguousarray(extra, np.float32)
+        xr = np.zeros((dirs.shape[0], 32), np.float32)
+        xr[:, :extra.shape[1]] = extra
+        extra = xr
         dloss = np.ascontiguousarray(dloss, np.float32)
         n = dirs.shape[0]
         denc = np.zeros((self.L, n, self.F), np.float32)
-        dx = np.zeros((n, 16), np.float32)
+        dx = np.zeros((n, 32), np.float32)
         w = None if weight is None else np.ascontiguousarray(weight, np.float32)
         self.lib.oref_backward_extra(self.h, ptr(enc), ptr(dirs), ptr(extra), n, ptr(dloss), None if w is None else ptr(w),
                                      ptr(denc), ptr(dx))

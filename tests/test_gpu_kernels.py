@@ -119,14 +119,15 @@ def make_extra(n_extra, seed=3):
     return g, o, rng
 
 
-@pytest.mark.parametrize("n_extra", [16, 3])
+@pytest.mark.parametrize("n_extra", [16, 3, 19, 32])
 def test_extra_dims_infer_matches_oracle(n_extra):
     """NerfNetwork with n_extra_dims (nerf_network.h:81-93): the records' extra dims (floats 7 .. 7 + E, the latent
-    code) enter the rgb network after the SH (rgb input next_multiple(32 + E, 16) = 48 wide); against the oracle, and
-    a zero code differs from a random one only in the rgb outputs."""
+    code) enter the rgb network after the SH (rgb input next_multiple(32 + E, 16) = 48 or 64 wide; 19 = light
+    direction + the 16-wide code of optimize_extra_dims, src/testbed.cu:4046-4053); against the oracle, and a zero
+    code differs from a random one only in the rgb outputs."""
     g, o, rng = make_extra(n_extra)
     try:
-        assert g.info.layer_in[2] == 48
+        assert g.info.layer_in[2] == (48 if n_extra <= 16 else 64)
         n = 3000
         coords = np.zeros((n, 7 + n_extra), np.float32)
         coords[:, :7] = random_coords(rng, n)
@@ -150,16 +151,17 @@ def test_extra_dims_infer_matches_oracle(n_extra):
         g.close()
 
 
-def test_extra_dims_mlp_backward_matches_oracle():
-    """The fused training MLP with the latent-code rows (Net XE: 48-row rgb input, the images' code segment last):
-    weight gradients (incl. the rgb first layer's code columns) and dL/denc against the oracle, and dL/d(code) of
-    each sample's own row (the input gradient compute_extra_dims_gradient_train_nerf sums)."""
-    g, o, rng = make_extra(16)
+@pytest.mark.parametrize("n_extra", [16, 19, 32])
+def test_extra_dims_mlp_backward_matches_oracle(n_extra):
+    """The fused training MLP with the latent-code rows (Net XE 1: 48-row rgb input, XE 2: 64 rows; the images' code
+    segment last): weight gradients (incl. the rgb first layer's code columns) and dL/denc against the oracle, and
+    dL/d(code) of each sample's own row (the input gradient compute_extra_dims_gradient_train_nerf sums)."""
+    g, o, rng = make_extra(n_extra)
     try:
         n = 1000
         coords = random_coords(rng, n)
         enc = o.encode(coords[:, :3])
-        extra = rng.normal(0, 1, (n, 16)).astype(np.float32)
+        extra = rng.normal(0, 1, (n, n_extra)).astype(np.float32)
         dl = (rng.normal(0, 1e-2, (n, 4))).astype(np.float16).astype(np.float32)
         w = rng.uniform(1, 2, n).astype(np.float32)
         g.zero_grads()
@@ -169,20 +171,20 @@ def test_extra_dims_mlp_backward_matches_oracle():
         og = o.get(A.GRADS_FP32)[: o.n_mlp]
         rel = np.linalg.norm(gg - og) / np.linalg.norm(og)
         assert rel < 1e-2, rel
-        # the rgb first layer's code columns (32..47 of its 48) carry gradient
+        # the rgb first layer's code columns (32 .. 32 + E of its 48 / 64) carry gradient, every one of them
         off, lin = g.info.layer_param_offset[2], g.info.layer_in[2]
-        wcode = gg[off:off + 64 * lin].reshape(64, lin)[:, 32:48]
-        assert np.abs(wcode).max() > 0
+        wcode = gg[off:off + 64 * lin].reshape(64, lin)[:, 32:32 + n_extra]
+        assert np.abs(wcode).max(axis=0).min() > 0
         dr = np.linalg.norm(gd - od) / max(np.linalg.norm(od), 1e-12)
         assert dr < 1e-2, dr
         xr = np.linalg.norm(gx - ox) / max(np.linalg.norm(ox), 1e-12)
         assert np.abs(ox).max() > 0 and xr < 1e-2, xr
-        # without extra dims the same call is refused; n_extra_dims > 16 too
+        # the tiny network has no latent-code instance; n_extra_dims > 32 is refused
         from gpu_util import GpuModel
         cfg = A.default_config(**CONFIGS["A_L4F2T14"], n_extra_dims=4)
         with pytest.raises(RuntimeError, match="n_extra_dims"):
             GpuModel(cfg)
-        cfg = A.default_config(**CONFIGS["B_L16F2T19"], n_extra_dims=17)
+        cfg = A.default_config(**CONFIGS["B_L16F2T19"], n_extra_dims=33)
         with pytest.raises(RuntimeError, match="n_extra_dims"):
             GpuModel(cfg)
     finally:

@@ -1230,7 +1230,7 @@ def test_render_pipelines_match_oracle(pipes, shard):
         g.close()
 
 
-@pytest.mark.parametrize("n_extra", [16, 5])
+@pytest.mark.parametrize("n_extra", [16, 5, 19])
 def test_train_step_extra_dims_matches_oracle(n_extra):
     """Per-image latent codes (NerfNetwork n_extra_dims, src/testbed_nerf.cu:706-730, 824, 1271-1306): every sample of
     a ray from image i carries code row i into the rgb network; the step's outputs and gradients match the oracle,
@@ -1240,11 +1240,12 @@ def test_train_step_extra_dims_matches_oracle(n_extra):
         imgs, cams, focal = make_views(6, 24, 24)
         hd, dd = HostDataset(imgs, cams, focal), DeviceDataset(imgs, cams, focal)
         set_bitfield_both(g, o, sphere_bitfield(0.32), 0)
-        codes = np.zeros((6, 16), np.float32)
+        XR = A.EXTRA_ROW  # latent-code rows of 32 floats
+        codes = np.zeros((6, XR), np.float32)
         codes[:, :n_extra] = rng.uniform(-1, 1, (6, n_extra))
         d_codes = torch.from_numpy(codes).cuda()
-        d_grad = torch.zeros(6 * 16, dtype=torch.float32, device="cuda")
-        h_grad = np.zeros(6 * 16, np.float32)
+        d_grad = torch.zeros(6 * XR, dtype=torch.float32, device="cuda")
+        h_grad = np.zeros(6 * XR, np.float32)
         R, B, MS = 384, 4096, 1 << 15
         ga = train_args(dd.ptr, dd.n, R, B, MS)
         oa = train_args(hd.ptr, hd.n, R, B, MS)
@@ -1272,8 +1273,8 @@ def test_train_step_extra_dims_matches_oracle(n_extra):
         for sl in (slice(0, g.n_mlp), slice(g.n_mlp, None)):
             rel = np.linalg.norm(gg[sl] - og[sl]) / np.linalg.norm(og[sl])
             assert rel < 5e-2, rel
-        gx = d_grad.cpu().numpy().reshape(6, 16)
-        ox = h_grad.reshape(6, 16)
+        gx = d_grad.cpu().numpy().reshape(6, XR)
+        ox = h_grad.reshape(6, XR)
         assert np.abs(ox[:, :n_extra]).max() > 0 and np.all(gx[:, n_extra:] == 0)
         rel = np.linalg.norm(gx - ox) / np.linalg.norm(ox)
         print(f"extra-dims gradient rel {rel:.2e}")
@@ -1295,13 +1296,14 @@ def test_train_step_extra_dims_matches_oracle(n_extra):
 def test_render_extra_dims_matches_oracle():
     """The rendered samples carry the rendering code (Nerf::get_rendering_extra_dims, src/testbed_nerf.cu:3206-3228):
     frame against the oracle's with the same code; a null code renders as zeros."""
-    g, o, rng = pair(dict(CFG_B, n_extra_dims=16), grid_scale=1.0)
+    g, o, rng = pair(dict(CFG_B, n_extra_dims=19), grid_scale=1.0)
     try:
         set_bitfield_both(g, o, sphere_bitfield(0.3))
         W, H = 40, 32
         cam = make_views(1, 8, 8)[1][0]
         focal = 0.5 * W / np.tan(0.5 * 0.69)
-        code = rng.uniform(-1, 1, 16).astype(np.float32)
+        code = np.zeros(A.EXTRA_ROW, np.float32)
+        code[:19] = rng.uniform(-1, 1, 19)
         d_code = torch.from_numpy(code).cuda()
         frames = []
         for use in (True, False):

@@ -823,6 +823,52 @@ def test_optimize_extra_dims_trains_per_image_codes(scene, tmp_path):
     np.testing.assert_array_equal(tb2.render(48, 48, 1, True), f3)
 
 
+def test_optimize_extra_dims_on_a_light_direction_dataset(scene, tmp_path):
+    """A dataset whose frames carry light directions (driver_parameters LightX/Y/Z, src/nerf_loader.cu:666-675) has 3
+    extra network inputs; optimize_extra_dims adds the 16 learnable ones (src/testbed.cu:4046-4053), so the rgb network
+    takes 16 + 16 + 19 -> 64 inputs (refused before).  Each image's code starts with its warped
+    light direction (Nerf::reset_extra_dims, src/testbed_nerf.cu:3181-3204), all 19 dims train, and a render with the
+    rendering light direction is finite and follows it."""
+    root, cams, imgs = scene
+    meta = json.load(open(os.path.join(root, "transforms_train.json")))
+    rng = np.random.default_rng(5)
+    for fr in meta["frames"]:
+        l = rng.normal(size=3)
+        fr["driver_parameters"] = {"LightX": float(l[0]), "LightY": float(l[1]), "LightZ": float(l[2])}
+        fr["file_path"] = os.path.join(root, fr["file_path"]) if not os.path.isabs(fr["file_path"]) else fr["file_path"]
+    path = str(tmp_path / "transforms_light.json")
+    json.dump(meta, open(path, "w"))
+    ngp, tb = new_testbed()
+    tb.load_training_data(path)
+    tr = tb.nerf.training
+    assert tr.dataset.has_light_dirs and tr.dataset.n_extra_dims() == 3
+    tb.reload_network_from_file("lego_L16F2.json")
+    tr.optimize_extra_dims = True
+    tb.shall_train = True
+    tb.frame()
+    assert tr.dataset.n_extra_dims() == 19
+    c0 = [np.asarray(tr.get_extra_dims(i)) for i in range(12)]
+    for i in range(12):
+        ld = np.asarray(tr.dataset.metadata[i].light_dir, np.float64)
+        np.testing.assert_allclose(c0[i][:3], (ld / np.linalg.norm(ld) + 1) * 0.5, atol=1e-5)
+    while tb.training_step < 150:
+        tb.frame()
+    assert np.isfinite(tb.loss)
+    c1 = [np.asarray(tr.get_extra_dims(i)) for i in range(12)]
+    assert max(np.abs(a[3:] - b[3:]).max() for a, b in zip(c0, c1)) > 1e-4
+    tb.shall_train = False
+    tb.background_color = [0.0, 0.0, 0.0, 1.0]
+    tb.set_camera_to_training_view(2)
+    tb.nerf.rendering_extra_dims_from_training_view = -1
+    tb.nerf.set_rendering_extra_dims([float(x) for x in c1[2]])
+    tb.nerf.light_dir = [0.0, 0.0, 1.0]
+    fa = tb.render(48, 48, 1, True)
+    tb.nerf.light_dir = [1.0, 0.0, 0.0]
+    fb = tb.render(48, 48, 1, True)
+    assert np.isfinite(fa).all() and fa[..., 3].max() > 0.1
+    assert np.abs(fa[..., :3] - fb[..., :3]).max() > 0  # the light direction is a network input
+
+
 def test_kernel_timers_measure_every_class(scene):
     """The kernel timers bench.py's roofline reads (ngp_timing_enable / ngp_timing_read; timing-only events without the
     system-scope fence): with every timer on, 16 training steps (one with a density-grid update) and a 1080p frame give
