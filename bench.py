@@ -61,6 +61,8 @@ def parse():
     p.add_argument("--config-e", type=int, default=1,
                    help="N=1: also time BASELINE config E's shape (T=2^22 L16F2 network, aabb_scale 64 scene) -> config_e")
     p.add_argument("--config-e-pretrain", type=int, default=500)
+    p.add_argument("--mlp-microbench", type=int, default=1,
+                   help="time the fused MLPs alone at 2^21 / 2^18 samples after the timed region (tools/mlp_microbench.py)")
     p.add_argument("--render-in-hbm", type=int, default=5,
                    help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
     p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r05_final3_surface_pmc_traffic.json"),
@@ -600,6 +602,13 @@ def main():
         surface = surface_scene(args, ngp)
     if world == 1 and args.config_e:
         cfg_e = config_e(args, ngp)
+    mlp_standalone = None
+    if world == 1 and args.mlp_microbench:
+        # the fused MLPs alone at SURVEY 8(d)'s sizes (tools/mlp_microbench.py): the render MLP over 2^21 samples under
+        # the frame's tunings and the training MLP over 2^18, after the timed region
+        sys.path.insert(0, os.path.join(ROOT, "tools"))
+        import mlp_microbench
+        mlp_standalone = mlp_microbench.measure(iters=20)
 
     value = rays / elapsed / 1e6
     if rank == 0:
@@ -638,6 +647,7 @@ def main():
             "surface_scene": surface,
             "config_e": cfg_e,
             "config_c": config_c,
+            "mlp_standalone": mlp_standalone,
         }
         print(json.dumps(line), flush=True)
     if world > 1:

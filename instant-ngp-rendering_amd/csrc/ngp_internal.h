@@ -388,7 +388,14 @@ struct RenderScratch {
 	size_t cap = 0;
 	float last_samples_per_ray = 0.0f;  // network samples per ray of the last full Shade frame (0: none yet)
 	uint32_t mlp_tile = 4;              // the render MLP's default wave step (16-sample tiles) for this frame
+	// per-pixel undistorted directions of an OpenCV / fisheye lens (render.hip RenderK::lens_xy) and what they hold
+	DevBuf<float2> lens_xy;
+	std::vector<float> lens_key;
+	const float2* lens_xy_filled = nullptr;
 	void release() {
+		lens_xy.release();
+		lens_key.clear();
+		lens_xy_filled = nullptr;
 		for (auto& p : pipe) p.release();
 		dense_rec.release(); shrows.release(); df.release(); df_x.release(); df_xy.release();
 		slice_coords.release(); slice_enc.release(); slice_out.release(); hmask.release();

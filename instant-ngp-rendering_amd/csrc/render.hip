@@ -76,6 +76,11 @@ struct RenderK {
 	float4 hbg;
 	float hexposure;
 	int hcolor_space, hsrgb;
+	// OpenCV / OpenCV-fisheye lenses: the undistorted camera-space direction (x, y, 1) of every pixel, a function of the
+	// pixel, its jitter (sample_index / snap) and the intrinsics only -- cached across frames (RenderScratch::lens_key):
+	// lens_fill = 1 computes and stores it (iterative_lens_undistortion, 100 Newton steps at most), 0 reads it back
+	float2* lens_xy;
+	int lens_fill;
 };
 
 // tonemap_kernel's per-pixel body (render_buffer.cu:533-565) after the accumulation: background, exposure, sRGB
@@ -311,10 +316,15 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, uint32_t x, uint
 	// get_xform_given_rolling_shutter (src/testbed_nerf.cu:1416)
 	const m43 cam = k.rs_on ? xform_given_rolling_shutter(k.cam, k.cam_end, k.rs, u, v, ld_random_val(k.sample_index, idx * 72239731u))
 	                        : k.cam;
-	if (LENS && !lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
+	if (LENS && k.lens_xy && !k.lens_fill) {
+		const float2 c = k.lens_xy[idx];  // the same bits lens_direction returned when the entry was filled
+		dir = mk3(c.x, c.y, 1.0f);
+	} else if (LENS && !lens_direction(u, v, (float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, k.lens_mode, k.lens_params, &dir)) {
 		*pp = Payload{};  // uv_to_ray returned Ray::invalid(): the pixel stays empty
 		pp->idx = idx;
 		return false;
+	} else if (LENS && k.lens_xy) {
+		k.lens_xy[idx] = make_float2(dir.x, dir.y);  // (the cached modes always return a ray with z = 1)
 	}
 	if (LENS && k.dmap) {  // uv_to_ray: dir.xy += distortion.at_lerp(uv) (common_device.cuh:441-443)
 		float ddx, ddy;
@@ -1154,6 +1164,21 @@ void run_render(ngp_model* m, const ngp_render_args* a, float* frame, float* dep
 	k.shard_index = a->shard_index % k.shard_count;
 	k.shard_rows = std::max(a->shard_rows, 1u);
 	k.tiles_x = div_up(k.W, 8u);
+	if (k.mode != NGP_RENDER_MODE_SLICE && (k.lens_mode == LENS_OPENCV || k.lens_mode == LENS_OPENCV_FISHEYE)) {
+		// the per-pixel undistortion cache (RenderK::lens_xy): valid while every input of lens_direction and the
+		// pixel jitter are the ones it was filled with; the shard geometry decides which rows were filled
+		const float key[] = {(float)k.W, (float)k.H, k.fx, k.fy, k.scx, k.scy, (float)k.lens_mode, k.lens_params[0],
+		                     k.lens_params[1], k.lens_params[2], k.lens_params[3], k.lens_params[4], k.lens_params[5],
+		                     k.lens_params[6], (float)(k.snap ? 0u : k.sample_index), (float)k.shard_index,
+		                     (float)k.shard_count, (float)k.shard_rows};
+		const std::vector<float> kv(key, key + sizeof(key) / sizeof(key[0]));
+		rs.lens_xy.reserve((size_t)k.W * k.H);
+		k.lens_xy = rs.lens_xy.ptr;
+		k.lens_fill = std::memcmp(kv.data(), rs.lens_key.data(), std::min(kv.size(), rs.lens_key.size()) * sizeof(float)) != 0 ||
+		              kv.size() != rs.lens_key.size() || rs.lens_xy_filled != rs.lens_xy.ptr;
+		rs.lens_key = kv;
+		rs.lens_xy_filled = rs.lens_xy.ptr;
+	}
 	const uint32_t H_shard = rows_owned(k.H, k.shard_index, k.shard_count, k.shard_rows);
 	if (k.W * H_shard == 0) return;
 	if (!m->gs.bitfield.ptr) throw std::runtime_error("render: density grid bitfield not initialised");

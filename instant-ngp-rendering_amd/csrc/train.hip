@@ -96,11 +96,23 @@ __global__ void __launch_bounds__(1024) k_scan_one_block(const uint32_t* __restr
 	uint32_t* st = reinterpret_cast<uint32_t*>(stage);
 	const uint32_t lane = threadIdx.x & 63u, w = threadIdx.x >> 6;
 	uint32_t carry = 0;
+	// the next tile's elements are loaded into registers while this one is scanned (a surface scene's ~35 k rays
+	// are three tiles: one global-load latency instead of three)
+	uint32_t nxt[PER];
+#pragma unroll
+	for (uint32_t k = 0; k < PER; ++k) {
+		const uint32_t e = k * 1024u + threadIdx.x;
+		nxt[k] = e < n ? in[e] : 0u;
+	}
 	for (uint32_t t0 = 0; t0 < n; t0 += TILE) {
 #pragma unroll
-		for (uint32_t k = 0; k < PER; ++k) {
-			const uint32_t e = k * 1024u + threadIdx.x;
-			st[e] = t0 + e < n ? in[t0 + e] : 0u;
+		for (uint32_t k = 0; k < PER; ++k) st[k * 1024u + threadIdx.x] = nxt[k];
+		if (t0 + TILE < n) {
+#pragma unroll
+			for (uint32_t k = 0; k < PER; ++k) {
+				const uint32_t e = t0 + TILE + k * 1024u + threadIdx.x;
+				nxt[k] = e < n ? in[e] : 0u;
+			}
 		}
 		__syncthreads();
 		uint32_t v[PER], tsum = 0;

@@ -782,6 +782,35 @@ def test_render_lens_matches_oracle():
         of, od = o.render(ra)
         assert (of[..., 3] > 0.01).mean() > 0.2
         assert np.abs(gf - of).mean() < 1e-3
+
+        # the per-pixel undistortion cache (RenderScratch::lens_xy): the next frame with the same intrinsics, lens and
+        # jitter reads the directions back -- bit-identical to the frame that computed them, also from another pose --
+        # and a changed lens parameter or jitter recomputes them (against the oracle again)
+        def render(r):
+            A.check(g.lib.ngp_render(g.h, C.byref(r), C.c_void_p(frame.data_ptr()), C.c_void_p(depth.data_ptr()), stream()))
+            torch.cuda.synchronize()
+            return frame.cpu().numpy().reshape(H, W, 4).copy()
+        np.testing.assert_array_equal(render(ra), gf)
+        cam2 = make_views(2, 8, 8)[1][1]
+        rb = render_args(W, H, cam2, focal, spp=0, snap=1)
+        rb.lens_mode = 1
+        for k in range(7):
+            rb.lens_params[k] = ra.lens_params[k]
+        f2 = render(rb)  # cached directions, another camera
+        ob, _ = o.render(rb)
+        assert np.abs(f2 - ob).mean() < 1e-3
+        ra.lens_params[0] = -0.12
+        f3 = render(ra)
+        oc, _ = o.render(ra)
+        assert np.abs(f3 - oc).mean() < 1e-3 and np.abs(f3 - gf).max() > 0
+        for si in (1, 2):  # jittered spp: each sample index its own pixel offsets
+            rj = render_args(W, H, cam, focal, spp=si, snap=0)
+            rj.lens_mode = 1
+            for k in range(7):
+                rj.lens_params[k] = ra.lens_params[k]
+            fj = render(rj)
+            oj, _ = o.render(rj)
+            assert np.abs(fj - oj).mean() < 1e-3, si
     finally:
         g.close()
 
@@ -1293,17 +1322,18 @@ def test_train_step_extra_dims_matches_oracle(n_extra):
         g.close()
 
 
-def test_render_extra_dims_matches_oracle():
+@pytest.mark.parametrize("n_extra", [16, 19])
+def test_render_extra_dims_matches_oracle(n_extra):
     """The rendered samples carry the rendering code (Nerf::get_rendering_extra_dims, src/testbed_nerf.cu:3206-3228):
     frame against the oracle's with the same code; a null code renders as zeros."""
-    g, o, rng = pair(dict(CFG_B, n_extra_dims=19), grid_scale=1.0)
+    g, o, rng = pair(dict(CFG_B, n_extra_dims=n_extra), grid_scale=1.0)
     try:
         set_bitfield_both(g, o, sphere_bitfield(0.3))
         W, H = 40, 32
         cam = make_views(1, 8, 8)[1][0]
         focal = 0.5 * W / np.tan(0.5 * 0.69)
         code = np.zeros(A.EXTRA_ROW, np.float32)
-        code[:19] = rng.uniform(-1, 1, 19)
+        code[:n_extra] = rng.uniform(-1, 1, n_extra)
         d_code = torch.from_numpy(code).cuda()
         frames = []
         for use in (True, False):
@@ -1321,6 +1351,7 @@ def test_render_extra_dims_matches_oracle():
             l1 = np.abs(gf - of).mean()
             assert l1 < 1e-3, (use, l1)
             frames.append(gf)
-        assert np.abs(frames[0][..., :3] - frames[1][..., :3]).mean() > 1e-3
+        # the code is read: the frames differ (a smoke check; each frame's parity is the oracle comparison above)
+        assert np.abs(frames[0][..., :3] - frames[1][..., :3]).mean() > 1e-4
     finally:
         g.close()

@@ -34,7 +34,7 @@ SCENES = {
 }
 
 
-def load(ngp, scene, seed, config):
+def load(ngp, scene, seed, config, random_bg=True):
     tb = ngp.Testbed(ngp.TestbedMode.Nerf)
     tb.seed = seed
     if scene == "synthetic":
@@ -44,6 +44,7 @@ def load(ngp, scene, seed, config):
     else:
         tb.load_training_data(SCENES[scene])
     tb.reload_network_from_file(config)
+    tb.nerf.training.random_bg_color = random_bg
     tb.shall_train = True
     return tb
 
@@ -74,6 +75,7 @@ def main():
     ap.add_argument("--config", default="base.json")
     ap.add_argument("--views", type=int, default=4)
     ap.add_argument("--trajectory", type=int, default=0, help="also print a line every this many steps")
+    ap.add_argument("--random-bg", type=int, default=1, help="nerf.training.random_bg_color (the reference's default: 1)")
     ap.add_argument("--mosaic-dir", default="", help="test2 / test2_half / fire: compare the trained field's density "
                     "mosaic with the reference's and save its packed >= 2.5 mask here (seed-versus-seed IoU later)")
     args = ap.parse_args()
@@ -85,7 +87,7 @@ def main():
     for scene in args.scenes.split(","):
         for seed in (int(s) for s in args.seeds.split(",")):
             t0 = time.time()
-            tb = load(ngp, scene, seed, args.config)
+            tb = load(ngp, scene, seed, args.config, bool(args.random_bg))
             losses = []
             while tb.training_step < args.steps:
                 tb.frame()
@@ -100,7 +102,7 @@ def main():
             st = tb.last_train_stats()
             g = np.asarray(tb.density_grid())
             bits = np.unpackbits(np.asarray(tb.density_grid_bitfield(), np.uint8)[:128 ** 3 // 8])
-            rec = {"scene": scene, "seed": seed, "steps": tb.training_step, "mode": "default",
+            rec = {"scene": scene, "seed": seed, "steps": tb.training_step, "mode": "default", "random_bg": args.random_bg,
                    "loss": float(np.mean(losses[-64:])), "grid_max": float(g.max()), "grid_mean": float(g[:128 ** 3].mean()),
                    "occupied": float(bits.mean()), "batch": int(st["measured_batch_size"]), "rays": int(st["n_rays"]),
                    "psnr": psnr_views(tb, args.views), "seconds": round(time.time() - t0, 1)}
@@ -114,7 +116,8 @@ def main():
                 rec.update({"ref_corr": corr, "ref_rank": rank,
                             "occupied_ratio": float((vol >= 129).mean() / max((ref >= 129).mean(), 1e-9))})
                 os.makedirs(args.mosaic_dir, exist_ok=True)
-                np.savez_compressed(os.path.join(args.mosaic_dir, f"{scene}_seed{seed}.npz"), mask=np.packbits(vol >= 129))
+                np.savez_compressed(os.path.join(args.mosaic_dir, f"{scene}_bg{args.random_bg}_seed{seed}.npz"),
+                                    mask=np.packbits(vol >= 129))
             print(json.dumps(rec), flush=True)
             del tb
 

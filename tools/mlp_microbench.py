@@ -48,45 +48,34 @@ def timer(lib, h, idx):
     return ms.value, units.value, launches.value
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--n-render", type=int, default=1 << 21)
-    ap.add_argument("--n-train", type=int, default=1 << 18)
-    ap.add_argument("--iters", type=int, default=40)
-    ap.add_argument("--tiles", default="4,2,1")
-    ap.add_argument("--wg", default="0", help="render-MLP workgroups per CU to sweep (0 = default)")
-    ap.add_argument("--pipes", default="1,2,3", help="ngp_tuning.render_mlp_pipeline values to sweep (1 = round 5)")
-    ap.add_argument("--samples-per-ray", type=int, default=32)
-    args = ap.parse_args()
-    torch.cuda.set_device(0)
+def measure(configs=((2, 2, 4), (2, 4, 2), (2, 4, 0), (1, 4, 0)), n_render=1 << 21, n_train=1 << 18, iters=40,
+            samples_per_ray=32, device=0):
+    """The render MLP under each (render_mlp_pipeline, render_mlp_tile, mlp_workgroups_per_cu) and the training MLP;
+    returns the result dict (see the module docstring).  Every render configuration's output must be bit-identical."""
+    torch.cuda.set_device(device)
     lib = A.load()
     cfg = A.default_config()
     h = C.c_void_p()
-    A.check(lib.ngp_model_create(0, C.byref(cfg), 1337, C.byref(h)))
+    A.check(lib.ngp_model_create(device, C.byref(cfg), 1337, C.byref(h)))
     s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
     rng = np.random.default_rng(1337)
     L, F = cfg.n_levels, cfg.n_features_per_level
-    out = {"config": "L16F2T19 density 32-64-16 rgb 32-64-64-16, Xavier weights, enc N(0,0.1^2) fp16",
-           "peak_tflops": PEAK / 1e12, "render": {}, "train": {}}
-
-    # --- render MLP ---------------------------------------------------------------------------------------
-    n = args.n_render
-    rays = (n + args.samples_per_ray - 1) // args.samples_per_ray
-    enc = torch.from_numpy((rng.standard_normal((L, n, F)) * 0.1).astype(np.float16)).cuda()
-    d = rng.standard_normal((rays, 3))
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    shr = torch.from_numpy(sh_deg4((d + 1) * 0.5)).cuda()
-    ri = torch.from_numpy((np.arange(n) // args.samples_per_ray).astype(np.int32)).cuda()
-    o = torch.zeros(n * 4, dtype=torch.float16, device="cuda")
-    ref = None
-    for wg, pipe, tile in [(int(w), int(p), int(t)) for w in args.wg.split(",") for p in args.pipes.split(",")
-                           for t in args.tiles.split(",")]:
-        if True:
+    out = {"config": "L16F2T19 density 32-64-16 rgb 32-64-64-16, Xavier weights, enc N(0,0.1^2) fp16, "
+                     f"{samples_per_ray} samples per SH row", "peak_tflops": PEAK / 1e12, "render": {}, "train": {}}
+    try:
+        n = n_render
+        rays = (n + samples_per_ray - 1) // samples_per_ray
+        enc = torch.from_numpy((rng.standard_normal((L, n, F)) * 0.1).astype(np.float16)).cuda()
+        d = rng.standard_normal((rays, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        shr = torch.from_numpy(sh_deg4((d + 1) * 0.5)).cuda()
+        ri = torch.from_numpy((np.arange(n) // samples_per_ray).astype(np.int32)).cuda()
+        o = torch.zeros(n * 4, dtype=torch.float16, device="cuda")
+        ref = None
+        for pipe, tile, wg in configs:
             t = A.Tuning()
             A.check(lib.ngp_model_get_tuning(h, C.byref(t)))
-            t.render_mlp_tile = tile
-            t.mlp_workgroups_per_cu = wg
-            t.render_mlp_pipeline = pipe
+            t.render_mlp_tile, t.mlp_workgroups_per_cu, t.render_mlp_pipeline = tile, wg, pipe
             A.check(lib.ngp_model_set_tuning(h, C.byref(t)))
             call = lambda: A.check(lib.ngp_model_infer_sh_rows(h, C.c_void_p(enc.data_ptr()), C.c_void_p(shr.data_ptr()),
                                                                C.c_void_p(ri.data_ptr()), n, rays, C.c_void_p(o.data_ptr()),
@@ -100,7 +89,7 @@ def main():
                 ref = res
             A.check(lib.ngp_timing_enable(h, 1 << A.TIMER["render_mlp"]))
             timer(lib, h, A.TIMER["render_mlp"])  # reset
-            for _ in range(args.iters):
+            for _ in range(iters):
                 call()
             torch.cuda.synchronize()
             ms, units, launches = timer(lib, h, A.TIMER["render_mlp"])
@@ -109,35 +98,53 @@ def main():
             tf = FLOP_FWD * n / (us * 1e-6) / 1e12
             key = f"pipe{pipe}_tile{tile}" + (f"_wg{wg}" if wg else "")
             out["render"][key] = {"n": n, "us": round(us, 2), "tflops": round(tf, 1), "frac": round(tf * 1e12 / PEAK, 4),
-                                  "launches": launches,
-                                  "equal_to_first": bool(torch.equal(res, ref))}
-            print(key, out["render"][key], flush=True)
+                                  "launches": launches, "equal_to_first": bool(torch.equal(res, ref))}
+        best = max(out["render"], key=lambda k: out["render"][k]["frac"])
+        out["render_best"] = dict(out["render"][best], tuning=best)
 
-    # --- training MLP -------------------------------------------------------------------------------------
-    n = args.n_train
-    enc = torch.from_numpy((rng.standard_normal((L, n, F)) * 0.1).astype(np.float16)).cuda()
-    d = rng.standard_normal((n, 3))
-    d /= np.linalg.norm(d, axis=1, keepdims=True)
-    dirs = torch.from_numpy(((d + 1) * 0.5).astype(np.float32)).cuda()
-    dl = torch.from_numpy((rng.standard_normal((n, 4)) * 1e-2).astype(np.float16)).cuda()
-    denc = torch.zeros(L * n * F, dtype=torch.float16, device="cuda")
-    call = lambda: A.check(lib.ngp_model_backward(h, C.c_void_p(enc.data_ptr()), C.c_void_p(dirs.data_ptr()), n,
-                                                  C.c_void_p(dl.data_ptr()), None, C.c_void_p(denc.data_ptr()), s))
-    for _ in range(3):
-        call()
-    A.check(lib.ngp_timing_enable(h, 1 << A.TIMER["train_mlp_bwd"]))
-    timer(lib, h, A.TIMER["train_mlp_bwd"])
-    for _ in range(max(args.iters // 4, 5)):
-        call()
-    torch.cuda.synchronize()
-    ms, units, launches = timer(lib, h, A.TIMER["train_mlp_bwd"])
-    A.check(lib.ngp_timing_enable(h, 0))
-    us = ms / max(launches, 1) * 1e3
-    tf = FLOP_TRAIN * n / (us * 1e-6) / 1e12
-    out["train"] = {"n": n, "us": round(us, 2), "tflops": round(tf, 1), "frac": round(tf * 1e12 / PEAK, 4),
-                    "launches": launches}
+        n = n_train
+        enc = torch.from_numpy((rng.standard_normal((L, n, F)) * 0.1).astype(np.float16)).cuda()
+        d = rng.standard_normal((n, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        dirs = torch.from_numpy(((d + 1) * 0.5).astype(np.float32)).cuda()
+        dl = torch.from_numpy((rng.standard_normal((n, 4)) * 1e-2).astype(np.float16)).cuda()
+        denc = torch.zeros(L * n * F, dtype=torch.float16, device="cuda")
+        call = lambda: A.check(lib.ngp_model_backward(h, C.c_void_p(enc.data_ptr()), C.c_void_p(dirs.data_ptr()), n,
+                                                      C.c_void_p(dl.data_ptr()), None, C.c_void_p(denc.data_ptr()), s))
+        for _ in range(3):
+            call()
+        A.check(lib.ngp_timing_enable(h, 1 << A.TIMER["train_mlp_bwd"]))
+        timer(lib, h, A.TIMER["train_mlp_bwd"])
+        for _ in range(max(iters // 4, 5)):
+            call()
+        torch.cuda.synchronize()
+        ms, units, launches = timer(lib, h, A.TIMER["train_mlp_bwd"])
+        A.check(lib.ngp_timing_enable(h, 0))
+        us = ms / max(launches, 1) * 1e3
+        tf = FLOP_TRAIN * n / (us * 1e-6) / 1e12
+        out["train"] = {"n": n, "us": round(us, 2), "tflops": round(tf, 1), "frac": round(tf * 1e12 / PEAK, 4),
+                        "launches": launches}
+    finally:
+        torch.cuda.synchronize()
+        A.check(lib.ngp_model_destroy(h))
+    return out
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n-render", type=int, default=1 << 21)
+    ap.add_argument("--n-train", type=int, default=1 << 18)
+    ap.add_argument("--iters", type=int, default=40)
+    ap.add_argument("--tiles", default="4,2,1")
+    ap.add_argument("--wg", default="0", help="render-MLP workgroups per CU to sweep (0 = default)")
+    ap.add_argument("--pipes", default="1,2,3", help="ngp_tuning.render_mlp_pipeline values to sweep (1 = round 5)")
+    ap.add_argument("--samples-per-ray", type=int, default=32)
+    args = ap.parse_args()
+    configs = [(int(p), int(t), int(w)) for w in args.wg.split(",") for p in args.pipes.split(",") for t in args.tiles.split(",")]
+    out = measure(configs, args.n_render, args.n_train, args.iters, args.samples_per_ray)
+    for k, v in out["render"].items():
+        print(k, v, flush=True)
     print("train", out["train"], flush=True)
-    A.check(lib.ngp_model_destroy(h))
     print(json.dumps(out))
 
 

@@ -10,7 +10,7 @@ mkdir -p "$OUT"
 REPO=$PWD
 export TMPDIR=/tmp
 SCRIPT=${BENCH_SCRIPT:-bench.py}
-STEPS="--steps 10 --warmup 3 --pretrain 1500 --cpu-baseline 0 --surface-scene 0 --config-e 0 --render-in-hbm 0 $BENCH_EXTRA"
+STEPS="--steps 10 --warmup 3 --pretrain 1500 --cpu-baseline 0 --surface-scene 0 --config-e 0 --render-in-hbm 0 --mlp-microbench 0 $BENCH_EXTRA"
 if [ "${SKIP_CALIB:-0}" != 1 ] || [ ! -f gpurun_out/fetch_calib/fetch_calib.json ]; then
   tools/fetch_calib.sh > "$OUT/fetch_calib.log" 2>&1 || exit $?
 fi
