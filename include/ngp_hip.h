@@ -383,7 +383,8 @@ typedef struct ngp_tuning {
 	uint32_t render_composite_block; /* k_composite workgroup size (256, 512, 1024); 0: 512 */
 	uint32_t render_generate_block;  /* k_generate workgroup size (256, 512); 0: 512 */
 	uint32_t encode_dense_records;   /* render-site corner records of the dense levels: 0 on, 1 off */
-	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: 6 for the render MLP's 64-sample steps, else 8 */
+	uint32_t mlp_workgroups_per_cu;  /* inference-MLP workgroups per CU; 0: the render MLP's resident count (2 at 64-sample
+	                                    steps, 4 at 32), else 8 */
 	uint32_t debug;                  /* bit 0: per-frame march statistics on stderr; bit 1: per-step sampler statistics;
 	                                    bit 2: the chunked training forward stops rays at transmittance 0.999 (forces
 	                                    forward_early_stop_violations: exercises the discard-and-retry path);

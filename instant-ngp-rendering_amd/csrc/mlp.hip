@@ -1374,7 +1374,11 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		bool done = false;
 		if constexpr (N::XE == 0) {
 			if (sh && a.F == 2 && pl && pipe >= 2 && out_mode == 0) {
-				const uint32_t wg = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : (tile == 4 ? 6u : 8u);
+				// workgroups per CU = the resident ones (64-sample steps: 174 VGPRs, 2 waves per SIMD = 2 workgroups;
+				// 32-sample steps: 96 VGPRs, 4 workgroups): no second round of workgroups reloading the weights
+				// (standalone 0.34 -> 0.38 and 0.37 -> 0.39 of the peak, profiles/r06_mlp_microbench_pipelines.txt;
+				// fire frame 13.23 -> 13.18 ms, profiles/r06_render_mlp_pipeline_ab.txt)
+				const uint32_t wg = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : (tile == 4 ? 2u : tile == 2 ? 4u : 8u);
 				const uint32_t ts = 16 * (tile == 4 ? 4 : tile == 2 ? 2 : 1);
 				const uint32_t grid_sh = std::min<uint32_t>(div_up(n, ts * WAVES), cu_count() * wg);
 				if (tile == 4 && pipe == 2) launch_timed(k_mlp_infer_sh<N, 4, 1, 12>, grid_sh, BLOCK, lds, s, a);
