@@ -753,10 +753,14 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_sh(MlpArgs a) {
 	// buffer loads return 0; a row index of 0 fetches SH row 0) and is never computed.  Guarding them with
 	// branches made the compiler's s_waitcnt bookkeeping conservative at the merges (vmcnt(0) before every
 	// SH fetch and every tile: the pipeline drained each step)
+	// (a tile past the end reads through an empty descriptor: its encoding loads would otherwise land in the next
+	// plane's rows -- real traffic, 17 MB per launch at 4 workgroups per CU, a quarter of a surface-scene pass)
+	const __amdgpu_buffer_rsrc_t none_rs = make_rsrc(a.enc, 0u);
 #pragma unroll
 	for (int k = 0; k <= PF; ++k) ri_load<N, CT_>(crd_rs, (t0 + k * stride) * TS, n, ring[k % R]);
 #pragma unroll
-	for (int k = 0; k < PF; ++k) rf_load<N, CT_, FF, true>(a, enc_rs, crd_rs, (t0 + k * stride) * TS, g, n, ring[k], false);
+	for (int k = 0; k < PF; ++k)
+		rf_load<N, CT_, FF, true>(a, t0 + k * stride < n_tiles ? enc_rs : none_rs, crd_rs, (t0 + k * stride) * TS, g, n, ring[k], false);
 	live[0] = sh_load_live<N, CT_>(sh_rs, g, ring[0], skip);
 	for (uint32_t tb = t0; tb < n_tiles; tb += R * stride) {
 #pragma unroll
@@ -765,7 +769,8 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_sh(MlpArgs a) {
 			if (t >= n_tiles) break;
 			live[(q + 1) % R] = sh_load_live<N, CT_>(sh_rs, g, ring[(q + 1) % R], skip);
 			ri_load<N, CT_>(crd_rs, (t + (PF + 1) * stride) * TS, n, ring[q]);
-			rf_load<N, CT_, FF, true>(a, enc_rs, crd_rs, (t + PF * stride) * TS, g, n, ring[(q + PF) % R], false);
+			rf_load<N, CT_, FF, true>(a, t + PF * stride < n_tiles ? enc_rs : none_rs, crd_rs, (t + PF * stride) * TS, g, n,
+			                          ring[(q + PF) % R], false);
 			sh_tile<N, CT_>(wl, ring[q], out_rs, t * TS, g, n, live[q]);
 		}
 	}

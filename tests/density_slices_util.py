@@ -14,10 +14,13 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "ref_density_slices")
 
 # scene -> (training transforms, the reference's mosaic).  The reference trained at full resolution on every
-# frame; these are data/nerf copies at half (test) and quarter (test2) resolution (tools/make_real_data.py).
+# frame; these are data/nerf copies at half (test, test2_half) and quarter (test2) resolution (tools/make_real_data.py).
 SCENES = {
     "test": (os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"), os.path.join(GOLDEN, "test.png")),
     "test2": (os.path.join(ROOT, "data", "nerf", "test2", "images", "transforms_train.json"), os.path.join(GOLDEN, "test2.png")),
+    # the same 300 views at half resolution (360x640; the reference trained at 720x1280)
+    "test2_half": (os.path.join(ROOT, "data", "nerf", "test2_half", "images", "transforms_train.json"),
+                   os.path.join(GOLDEN, "test2.png")),
 }
 # sha256 of the reference's files (data/nerf/test.density_slices_256x256x256.png,
 # data/nerf/test2/images.density_slices_256x256x256.png), checked by tests/test_density_slices.py

@@ -114,44 +114,84 @@ def test_png_slices_are_the_oracle_mosaic(fox, tmp_path):
         assert (png >= 129).any() and (png == 0).any()
 
 
+def _training_view_psnr(tb, views=4):
+    """Mean PSNR of `views` training views rendered at their own resolution against the images (black background)."""
+    ds = tb.nerf.training.dataset
+    tb.background_color = [0.0, 0.0, 0.0, 1.0]
+    out = []
+    for v in np.linspace(0, ds.n_images - 1, views).astype(int):
+        w, h = (int(x) for x in ds.metadata[int(v)].resolution)
+        tb.set_camera_to_training_view(int(v))
+        tb.render_ground_truth = True
+        gt = tb.render(w, h, 1, True)[..., :3]
+        tb.render_ground_truth = False
+        img = tb.render(w, h, 1, True)[..., :3]
+        out.append(-10.0 * np.log10(max(float(np.mean((np.clip(img, 0, 1) - np.clip(gt, 0, 1)) ** 2)), 1e-12)))
+    return float(np.mean(out))
+
+
 def test_trained_field_against_the_reference_density_mosaic():
     """The reference ships the density mosaic its CUDA build wrote after training on data/nerf/test2/images
-    (images.density_slices_256x256x256.png; the data path in the name is the scene's).  base.json trained 35k steps
-    on the same scene (quarter resolution, tools/make_real_data.py) with two seeds, compared at the scale the scene
-    determines -- it is a flame animated over the 300 frames in front of an opaque black background, so no two
-    trainings agree voxel by voxel (seed vs seed IoU of the >= 2.5 raw-density masks 0.29-0.40, this build vs the
-    reference 0.11-0.14; profiles/r05_density_slices.json) -- through the 32^3 grid of per-block occupied fractions:
-      * the reference's field correlates with ours best in the identity frame among the 48 axis permutations / flips
-        (measured first for every pair of four seeds): same world axes, same placement in the render aabb;
-      * that correlation is positive (0.11-0.18 measured) and the two seeds agree with each other (0.22-0.80: the fp16
-        gradient atomics make every run, seed for seed, a different field);
-      * the occupied volume is of the reference's order (ours 17-35 %, the reference's 13.3 %).
-    The views are opaque (alpha 255), so with random background colours every ray that sees the black backdrop needs
-    opaque black density, and about one training in four (nondeterministic or deterministic, any seed) converges
-    instead to painting the views onto the box (loss -> 0, raw density 1e6-1e7 everywhere, occupied ratio ~4.8, no
-    orientation preference; profiles/r05_density_mosaic_seeds.txt).  So the test trains deterministically -- the
-    result is reproducible -- with two seeds that converge to the flame (1337, 2024: pair correlation 0.199 at rank 0,
-    seeds 0.697, ratio 1.45 when measured).
+    (images.density_slices_256x256x256.png; the data path in the name is the scene's): a flame animated over the 300
+    frames in front of an opaque black backdrop, 13.3 % of the lattice at raw density >= 2.5.  base.json, 35 k steps on
+    the scene at half resolution (360x640; the reference trained at 720x1280), the DEFAULT training mode (random
+    background colours, fp16 gradient atomics), seeds 1337 and 1 -- the first two of the sweep's fixed list.
+
+    tools/collapse_sweep.py measured the outcomes first (profiles/r06_collapse_sweep.txt, 8 seeds per scene):
+      * the static scenes never collapse: fire, fox and the lego-shaped surface scene 24 of 24 runs converge (training-
+        view PSNR 36-38 / 33-34 / 44 dB), so the training path has no collapse of its own;
+      * test2's views are opaque, so with random background colours every ray that sees the black backdrop needs
+        opaque density: early on the occupancy grid is full, every ray reserves hundreds of samples and the 16 x 2^18
+        sample cap admits only the first ~12 k rays (the reference drops the rest, src/testbed_nerf.cu:779-781).  At
+        half resolution 6 of 8 runs then form the flame and its backdrop: 1.5-1.9x the reference's occupied volume,
+        the reference's field correlating best with ours in the identity frame of the 48 axis orders / flips
+        (0.18-0.24), IoU of the >= 2.5 masks 0.14-0.16 (0.38-0.41 within one voxel); 2 of 8 stay sample-starved
+        (the ray count pinned at 2^18, 3.0x the volume, rank 1-3).  At quarter resolution the starved mode, which
+        paints the views on the box with view-dependent colour, wins 6 of 8 runs (4.2-4.8x, PSNR 25.4-26.9 dB);
+      * with a black training background instead (random_bg_color False) all 8 quarter-resolution runs converge to
+        the flame alone: seed-versus-seed IoU 0.61-0.72, 0.03x the reference's volume -- the reference's 13.3 % is the
+        flame plus the backdrop density that random-background training builds.
+    So each default-mode run must land in one of the two documented modes, the flame mode pinned against the
+    reference's mosaic; two black-background runs must agree with each other and hold no backdrop density.
+    Thresholds: the measured ranges widened by about a third.
     The other mosaic (data/nerf/test.density_slices_...) names the data path data/nerf/test, not test/dataset where the
-    fire scene now sits, and matches no orientation of fields trained on it: it is not compared."""
+    fire scene now sits, and matches no orientation of fields trained on it (fire runs: correlation <= 0.0, ratio
+    ~21): it is not compared."""
     import density_slices_util as D
     import pyngp as ngp
     ref = D.reference_volume("test2") >= 129
-    occ = {}
-    for seed in (1337, 2024):
-        tb = D.new_testbed(ngp, "test2", "base.json", seed)
-        tb.deterministic = True  # bit-reproducible: the scene's training outcome is bimodal (below)
-        D.train_to(tb, 35000)
-        occ[seed] = D.testbed_volume(tb) >= 129
-        del tb
-    ours = (D.coarse(occ[1337]) + D.coarse(occ[2024])) / 2
     cref = D.coarse(ref)
-    ident, rank = D.orientation_ranking(ours, cref)
-    seeds_corr = float(np.corrcoef(D.coarse(occ[1337]).ravel(), D.coarse(occ[2024]).ravel())[0, 1])
-    ratio = float(ours.mean() / cref.mean())
-    print(f"test2: corr vs reference {ident:.3f} (rank {rank} of 48), seed vs seed {seeds_corr:.3f}, occupied ratio {ratio:.2f}, "
-          f"IoU vs reference {[round(D.compare(o.astype(np.uint8) * 200, ref.astype(np.uint8) * 200)['iou'], 3) for o in occ.values()]}")
-    assert rank == 0, (ident, rank)
-    assert ident > 0.05
-    assert seeds_corr > 0.1
-    assert 0.5 < ratio < 4.0
+    modes = {}
+    for seed in (1337, 1):
+        tb = D.new_testbed(ngp, "test2_half", "base.json", seed)
+        D.train_to(tb, 35000)
+        rays = tb.last_train_stats()["n_rays"]
+        occ = D.testbed_volume(tb) >= 129
+        ident, rank = D.orientation_ranking(D.coarse(occ), cref)
+        ratio = float(occ.mean() / ref.mean())
+        psnr = _training_view_psnr(tb)
+        print(f"test2_half seed {seed}: rays {rays}, occupied ratio {ratio:.2f}, corr vs reference {ident:.3f} "
+              f"(rank {rank} of 48), PSNR {psnr:.2f} dB")
+        if rays >= (1 << 18):  # sample-starved: the views painted on the box (or on its way there)
+            modes[seed] = "starved"
+            assert 2.0 < ratio < 6.5, ratio
+            assert psnr > 23.0, psnr
+        else:
+            modes[seed] = "flame"
+            assert 0.9 < ratio < 2.5, ratio
+            assert rank == 0 and ident > 0.1, (ident, rank)
+            assert psnr > 24.0, psnr
+        del tb
+    occ_black = []
+    for seed in (1337, 1):
+        tb = D.new_testbed(ngp, "test2", "base.json", seed, random_bg_color=False)
+        D.train_to(tb, 35000)
+        occ_black.append(D.testbed_volume(tb) >= 129)
+        assert _training_view_psnr(tb) > 33.0
+        del tb
+    a, b = occ_black
+    iou = float((a & b).sum() / max((a | b).sum(), 1))
+    ratios = [float(o.mean() / ref.mean()) for o in occ_black]
+    print(f"test2 black background: seed vs seed IoU {iou:.3f}, occupied ratios {ratios}, default-mode modes {modes}")
+    assert iou > 0.45, iou
+    assert max(ratios) < 0.1, ratios
