@@ -55,7 +55,7 @@ def test_oracle_mosaic_matches_numpy_restatement(shape, swap):
         assert counts == np_counts(d, thresh)
 
 
-@pytest.mark.parametrize("scene", sorted(D.SCENES))
+@pytest.mark.parametrize("scene", sorted(D.REFERENCE_SHA256))  # the two shipped mosaics (test2_half shares test2's)
 def test_reference_mosaics_are_the_shipped_files_and_round_trip(scene):
     """The fixtures are the reference's files (sha256); each is a 16 x 16 mosaic of 256 slices of 256^2; a volume
     whose bytes map back to the same bytes re-encodes to the identical mosaic (the layout inverse is exact)."""
