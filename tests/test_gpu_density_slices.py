@@ -152,8 +152,8 @@ def test_trained_field_against_the_reference_density_mosaic():
         the flame alone: seed-versus-seed IoU 0.61-0.72, 0.03x the reference's volume -- the reference's 13.3 % is the
         flame plus the backdrop density that random-background training builds.
     So each default-mode run must land in one of the two documented modes, the flame mode pinned against the
-    reference's mosaic; two black-background runs must agree with each other and hold no backdrop density.
-    Thresholds: the measured ranges widened by about a third.
+    reference's mosaic (the black-background control is the next test).  Thresholds: the measured ranges widened by
+    about a third.
     The other mosaic (data/nerf/test.density_slices_...) names the data path data/nerf/test, not test/dataset where the
     fire scene now sits, and matches no orientation of fields trained on it (fire runs: correlation <= 0.0, ratio
     ~21): it is not compared."""
@@ -182,6 +182,17 @@ def test_trained_field_against_the_reference_density_mosaic():
             assert rank == 0 and ident > 0.1, (ident, rank)
             assert psnr > 24.0, psnr
         del tb
+    print(f"test2_half default-mode modes {modes}")
+
+
+def test_black_background_training_on_the_reference_scene_has_no_backdrop():
+    """test_trained_field_against_the_reference_density_mosaic's control: test2 trained with a black background
+    (random_bg_color False; quarter resolution, default mode, seeds 1337 and 1) forms the flame alone in every run of
+    the sweep (8 of 8, seed-versus-seed IoU 0.61-0.72, 0.03x the reference's occupied volume, PSNR 36.4-42.0 dB): the
+    two runs must agree with each other and hold none of the backdrop density random-background training builds."""
+    import density_slices_util as D
+    import pyngp as ngp
+    ref = D.reference_volume("test2") >= 129
     occ_black = []
     for seed in (1337, 1):
         tb = D.new_testbed(ngp, "test2", "base.json", seed, random_bg_color=False)
@@ -192,6 +203,6 @@ def test_trained_field_against_the_reference_density_mosaic():
     a, b = occ_black
     iou = float((a & b).sum() / max((a | b).sum(), 1))
     ratios = [float(o.mean() / ref.mean()) for o in occ_black]
-    print(f"test2 black background: seed vs seed IoU {iou:.3f}, occupied ratios {ratios}, default-mode modes {modes}")
+    print(f"test2 black background: seed vs seed IoU {iou:.3f}, occupied ratios {ratios}")
     assert iou > 0.45, iou
     assert max(ratios) < 0.1, ratios
