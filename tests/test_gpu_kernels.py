@@ -84,6 +84,58 @@ def test_infer_matches_oracle(name):
         g.close()
 
 
+@pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
+def test_infer_sh_rows_matches_oracle_under_every_render_mlp_tuning(name):
+    """ngp_model_infer_sh_rows -- the renderer's network call (src/testbed_nerf.cu:1720) on given encodings with the
+    degree-4 SH of each ray's direction precomputed once per ray (k_mlp_infer_sh / k_mlp_infer_rf's SH-row path) --
+    against the oracle's NerfNetwork::inference of the same samples; the output is bit-identical across the render-MLP
+    load pipelines (round 5's ring and the decoupled one), wave steps and workgroup counts, and a sample count that
+    is not a multiple of any tile (past-the-end tiles read through an empty descriptor) leaves the rows after it
+    untouched."""
+    import torch
+    from gpu_util import dev, stream, vp
+    g, o, rng = make(name)
+    try:
+        n, per_ray = 5001, 7
+        rays = (n + per_ray - 1) // per_ray
+        d = rng.normal(size=(rays, 3))
+        d /= np.linalg.norm(d, axis=1, keepdims=True)
+        wd = ((d + 1) * 0.5).astype(np.float32)
+        coords = random_coords(rng, n)
+        coords[:, 4:7] = wd[np.arange(n) // per_ray]
+        enc = o.encode(coords[:, :3]).astype(np.float16)  # [L][n][F]
+        oo = o.infer(coords)
+        # the rows: the device's own SH of each direction (one ngp_model_infer_sh_rows input per ray)
+        x, y, z = (2 * wd[:, 0] - 1), (2 * wd[:, 1] - 1), (2 * wd[:, 2] - 1)
+        sh = np.stack([np.full_like(x, 0.28209479177387814), -0.48860251190291987 * y, 0.48860251190291987 * z,
+                       -0.48860251190291987 * x, 1.0925484305920792 * x * y, -1.0925484305920792 * y * z,
+                       0.94617469575755997 * z * z - 0.31539156525251999, -1.0925484305920792 * x * z,
+                       0.54627421529603959 * (x * x - y * y), 0.59004358992664352 * y * (-3 * x * x + y * y),
+                       2.8906114426405538 * x * y * z, 0.45704579946446572 * y * (1 - 5 * z * z),
+                       0.3731763325901154 * z * (5 * z * z - 3), 0.45704579946446572 * x * (1 - 5 * z * z),
+                       1.4453057213202769 * z * (x * x - y * y), 0.59004358992664352 * x * (-x * x + 3 * y * y)],
+                      1).astype(np.float16)
+        e, r, ri = dev(enc.view(np.int16)), dev(sh.view(np.int16)), dev((np.arange(n) // per_ray).astype(np.int32))
+        outs = {}
+        for pipe, tile, wg in ((1, 4, 0), (2, 4, 0), (2, 4, 2), (2, 2, 0), (2, 1, 0), (3, 4, 0), (3, 2, 4)):
+            g.set_tuning(render_mlp_pipeline=pipe, render_mlp_tile=tile, mlp_workgroups_per_cu=wg)
+            out = torch.full((n + 64) * 4, -7.0, dtype=torch.float16, device="cuda")
+            A.check(g.lib.ngp_model_infer_sh_rows(g.h, vp(e), vp(r), vp(ri), n, rays, vp(out), 0, stream()))
+            torch.cuda.synchronize()
+            h = out.float().cpu().numpy().reshape(n + 64, 4)
+            assert np.all(h[n:] == -7.0), (pipe, tile, wg)  # nothing written past the n samples
+            outs[(pipe, tile, wg)] = h[:n]
+        first = next(iter(outs.values()))
+        for k, v in outs.items():
+            np.testing.assert_array_equal(v, first, err_msg=str(k))
+        err = np.abs(first - oo)
+        tol = 4e-3 + 8e-3 * np.abs(oo)
+        assert (err <= tol).mean() > 0.999, f"max err {err.max()}"
+        assert err.mean() < 1e-3
+    finally:
+        g.close()
+
+
 @pytest.mark.parametrize("layout_rm", [0, 1])
 @pytest.mark.parametrize("name", ["B_L16F2T19", "A_L4F2T14"])
 def test_infer_padded_output_matches_oracle(name, layout_rm):
