@@ -119,7 +119,7 @@ def test_infer_sh_rows_matches_oracle_under_every_render_mlp_tuning(name):
         outs = {}
         for pipe, tile, wg in ((1, 4, 0), (2, 4, 0), (2, 4, 2), (2, 2, 0), (2, 1, 0), (3, 4, 0), (3, 2, 4)):
             g.set_tuning(render_mlp_pipeline=pipe, render_mlp_tile=tile, mlp_workgroups_per_cu=wg)
-            out = torch.full((n + 64) * 4, -7.0, dtype=torch.float16, device="cuda")
+            out = torch.full(((n + 64) * 4,), -7.0, dtype=torch.float16, device="cuda")
             A.check(g.lib.ngp_model_infer_sh_rows(g.h, vp(e), vp(r), vp(ri), n, rays, vp(out), 0, stream()))
             torch.cuda.synchronize()
             h = out.float().cpu().numpy().reshape(n + 64, 4)
