@@ -630,25 +630,31 @@ __global__ void __launch_bounds__(BLOCK) k_mlp_infer_rf(MlpArgs a) {
 	// consumed -- no register copies between the ring and the tile being computed
 	constexpr int R = PF + 1;
 	RawTile<N, CT_> ring[R];
+	// The ring's loads are issued unconditionally (k_mlp_infer_sh, round 6): a branch around them made the compiler's
+	// s_waitcnt bookkeeping fall back at the merges -- each step waited for the loads it had just issued (the
+	// training forward and the density-grid evaluation: vmcnt(1) right after the next tile's direction and
+	// encoding loads).  A tile past the end reads through descriptors of zero extent (no traffic; zeros) and is
+	// never computed.  FF 0 / 2 / 4 (the element-wise and level-major loads) keep their own guards.
+	const __amdgpu_buffer_rsrc_t none_rs = make_rsrc(a.enc, 0u);
 #pragma unroll
 	for (int q = 0; q < PF; ++q) {
 		const uint32_t t = t0 + q * stride;
-		if (t < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, t * TS, g, n, ring[q], !DENSITY_ONLY);
+		rf_load<N, CT_, FF, SHIN>(a, t < n_tiles ? enc_rs : none_rs, t < n_tiles ? crd_rs : none_rs, t * TS, g, n, ring[q],
+		                          !DENSITY_ONLY);
 	}
-	if constexpr (SHR) {
-		if (t0 < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[0]);
-	}
+	if constexpr (SHR) sh_load<N, CT_>(sh_rs, g, ring[0]);
 	for (uint32_t tb = t0; tb < n_tiles; tb += R * stride) {
 #pragma unroll
 		for (int q = 0; q < R; ++q) {
 			const uint32_t t = tb + q * stride;
 			if (t >= n_tiles) break;
 			const uint32_t tn = t + PF * stride;
-			if (tn < n_tiles) rf_load<N, CT_, FF, SHIN>(a, enc_rs, crd_rs, tn * TS, g, n, ring[(q + PF) % R], !DENSITY_ONLY);
+			rf_load<N, CT_, FF, SHIN>(a, tn < n_tiles ? enc_rs : none_rs, tn < n_tiles ? crd_rs : none_rs, tn * TS, g, n,
+			                          ring[(q + PF) % R], !DENSITY_ONLY);
 			if constexpr (SHR) {
 				// SH rows of the next tile to consume (its row indices were issued with its encoding; with
 				// PF = 1 that is the tile just loaded)
-				if (t + stride < n_tiles) sh_load<N, CT_>(sh_rs, g, ring[(q + 1) % R]);
+				sh_load<N, CT_>(sh_rs, g, ring[(q + 1) % R]);
 			}
 			rf_tile<N, CT_, PF, DENSITY_ONLY, SHIN>(a, wl, ring[q], t * TS, g, n);
 		}

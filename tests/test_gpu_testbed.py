@@ -849,8 +849,10 @@ def test_optimize_extra_dims_on_a_light_direction_dataset(scene, tmp_path):
     assert tr.dataset.n_extra_dims() == 19
     c0 = [np.asarray(tr.get_extra_dims(i)) for i in range(12)]
     for i in range(12):
+        # the frame that reset the codes also took the first VarAdam step on them: at most one learning rate (1e-2,
+        # Adam's first step is lr * sign) from the warped light direction they started at
         ld = np.asarray(tr.dataset.metadata[i].light_dir, np.float64)
-        np.testing.assert_allclose(c0[i][:3], (ld / np.linalg.norm(ld) + 1) * 0.5, atol=1e-5)
+        np.testing.assert_allclose(c0[i][:3], (ld / np.linalg.norm(ld) + 1) * 0.5, atol=1.01e-2)
     while tb.training_step < 150:
         tb.frame()
     assert np.isfinite(tb.loss)
