@@ -429,7 +429,9 @@ PYBIND11_MODULE(pyngp, m) {
 		// extra dims (per-image latent codes) of the rendered rays (Nerf::rendering_extra_dims, src/testbed_nerf.cu:3246-3280)
 		.def_property("rendering_extra_dims_from_training_view",
 		              [](const NerfView& v) { return v.tb->rendering_extra_dims_from_training_view; },
-		              [](NerfView& v, int i) { v.tb->set_rendering_extra_dims_from_training_view(i); })
+		              // a plain field write (def_readwrite, src/python_api.cu:596): -1 selects the set code; a view past
+		              // the trained codes reads the set code too (Testbed::rendering_extra_dims)
+		              [](NerfView& v, int i) { v.tb->rendering_extra_dims_from_training_view = i; })
 		.def("set_rendering_extra_dims_from_training_view", [](NerfView& v, int i) { v.tb->set_rendering_extra_dims_from_training_view(i); })
 		.def("set_rendering_extra_dims", [](NerfView& v, const std::vector<float>& x) { v.tb->set_rendering_extra_dims(x); })
 		.def("get_rendering_extra_dims", [](const NerfView& v) { return v.tb->rendering_extra_dims(); })
