@@ -31,6 +31,7 @@ SCENES = {
     "fox": os.path.join(ROOT, "data", "nerf", "fox"),
     "test2": os.path.join(ROOT, "data", "nerf", "test2", "images", "transforms_train.json"),
     "test2_half": os.path.join(ROOT, "data", "nerf", "test2_half", "images", "transforms_train.json"),
+    "test2_full": os.path.join(ROOT, "data", "nerf", "test2_full", "images", "transforms_train.json"),
 }
 
 
@@ -106,7 +107,7 @@ def main():
                    "loss": float(np.mean(losses[-64:])), "grid_max": float(g.max()), "grid_mean": float(g[:128 ** 3].mean()),
                    "occupied": float(bits.mean()), "batch": int(st["measured_batch_size"]), "rays": int(st["n_rays"]),
                    "psnr": psnr_views(tb, args.views), "seconds": round(time.time() - t0, 1)}
-            ref_scene = {"test2": "test2", "test2_half": "test2", "fire": "test"}.get(scene)
+            ref_scene = {"test2": "test2", "test2_half": "test2", "test2_full": "test2", "fire": "test"}.get(scene)
             if args.mosaic_dir and ref_scene:
                 import density_slices_util as D
                 vol = D.testbed_volume(tb)

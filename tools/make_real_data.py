@@ -65,7 +65,9 @@ def make_test2(div=4, out="test2"):
         name = os.path.basename(fr["file_path"])
         im = Image.open(os.path.join(src, fr["file_path"]))
         w, h = im.size
-        im = im.resize((w // div, h // div), Image.LANCZOS).convert("RGB")
+        if div > 1:
+            im = im.resize((w // div, h // div), Image.LANCZOS)
+        im = im.convert("RGB")
         im.save(os.path.join(dst, "train", name), "PNG", optimize=True)
     json.dump(meta, open(os.path.join(dst, "transforms_train.json"), "w"), indent=1)
     shutil.copy(os.path.join(src, "log.txt"), os.path.join(dst, "log.txt"))
@@ -97,6 +99,8 @@ if __name__ == "__main__":
         make_test2()
     if "test2_half" in which:
         make_test2(2, "test2_half")
+    if "test2_full" in which:
+        make_test2(1, "test2_full")  # 720x1280 (the reference's training resolution; not committed, ~150 MB)
     if "fox" in which:
         make_fox()
     if "slices" in which:
