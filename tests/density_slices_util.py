@@ -14,12 +14,16 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 GOLDEN = os.path.join(ROOT, "tests", "golden", "ref_density_slices")
 
 # scene -> (training transforms, the reference's mosaic).  The reference trained at full resolution on every
-# frame; these are data/nerf copies at half (test, test2_half) and quarter (test2) resolution (tools/make_real_data.py).
+# frame; these are data/nerf copies at half (test, test2_half), quarter (test2) and full (test2_full) resolution
+# (tools/make_real_data.py).
 SCENES = {
     "test": (os.path.join(ROOT, "data", "nerf", "test", "dataset", "transforms_all.json"), os.path.join(GOLDEN, "test.png")),
     "test2": (os.path.join(ROOT, "data", "nerf", "test2", "images", "transforms_train.json"), os.path.join(GOLDEN, "test2.png")),
     # the same 300 views at half resolution (360x640; the reference trained at 720x1280)
     "test2_half": (os.path.join(ROOT, "data", "nerf", "test2_half", "images", "transforms_train.json"),
+                   os.path.join(GOLDEN, "test2.png")),
+    # ... and at the reference's own training resolution (720x1280, lossless RGB)
+    "test2_full": (os.path.join(ROOT, "data", "nerf", "test2_full", "images", "transforms_train.json"),
                    os.path.join(GOLDEN, "test2.png")),
 }
 # sha256 of the reference's files (data/nerf/test.density_slices_256x256x256.png,

@@ -185,6 +185,42 @@ def test_trained_field_against_the_reference_density_mosaic():
     print(f"test2_half default-mode modes {modes}")
 
 
+def test_trained_field_at_the_reference_resolution_against_its_density_mosaic():
+    """The same pin at the resolution the reference trained at (720x1280, data/nerf/test2_full): there the default mode
+    has one outcome.  tools/collapse_sweep.py, 8 fixed seeds, base.json, 35 k steps, random background colours
+    (profiles/r06_collapse_sweep_test2_full.jsonl, last section of r06_collapse_sweep.txt): 8 of 8 form the flame and
+    its backdrop (three starved at 5 k steps and recovered by 15 k): occupied volume 1.50-1.80x the reference's, the
+    reference's field correlating best with ours in the identity frame of the 48 axis orders / flips (0.17-0.23), IoU
+    of the >= 2.5 masks 0.13-0.16 against the reference and 0.38-0.45 seed versus seed.  Seeds 1337 and 1 (the sweep's
+    first two, fixed before measuring); thresholds: the measured ranges widened by about a third.  Voxel-level
+    agreement with the reference's single run at the seed-versus-seed level is not claimed (0.14 vs 0.42)."""
+    import density_slices_util as D
+    import pyngp as ngp
+    ref = D.reference_volume("test2") >= 129
+    cref = D.coarse(ref)
+    occs = []
+    for seed in (1337, 1):
+        tb = D.new_testbed(ngp, "test2_full", "base.json", seed)
+        D.train_to(tb, 35000)
+        rays = tb.last_train_stats()["n_rays"]
+        occ = D.testbed_volume(tb) >= 129
+        ident, rank = D.orientation_ranking(D.coarse(occ), cref)
+        ratio = float(occ.mean() / ref.mean())
+        iou = float((occ & ref).sum() / max((occ | ref).sum(), 1))
+        print(f"test2_full seed {seed}: rays {rays}, occupied ratio {ratio:.2f}, corr vs reference {ident:.3f} "
+              f"(rank {rank} of 48), IoU vs reference {iou:.3f}")
+        assert rays < (1 << 18), rays  # not sample-starved
+        assert 1.0 < ratio < 2.4, ratio
+        assert rank == 0 and ident > 0.11, (ident, rank)
+        assert iou > 0.09, iou
+        occs.append(occ)
+        del tb
+    a, b = occs
+    iou_seeds = float((a & b).sum() / max((a | b).sum(), 1))
+    print(f"test2_full seed vs seed IoU {iou_seeds:.3f}")
+    assert iou_seeds > 0.25, iou_seeds
+
+
 def test_black_background_training_on_the_reference_scene_has_no_backdrop():
     """test_trained_field_against_the_reference_density_mosaic's control: test2 trained with a black background
     (random_bg_color False; quarter resolution, default mode, seeds 1337 and 1) forms the flame alone in every run

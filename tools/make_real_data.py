@@ -100,7 +100,7 @@ if __name__ == "__main__":
     if "test2_half" in which:
         make_test2(2, "test2_half")
     if "test2_full" in which:
-        make_test2(1, "test2_full")  # 720x1280 (the reference's training resolution; not committed, ~150 MB)
+        make_test2(1, "test2_full")  # 720x1280, the reference's training resolution (82 MB)
     if "fox" in which:
         make_fox()
     if "slices" in which:
