@@ -65,7 +65,7 @@ def parse():
                    help="time the fused MLPs alone at 2^21 / 2^18 samples after the timed region (tools/mlp_microbench.py)")
     p.add_argument("--render-in-hbm", type=int, default=5,
                    help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
-    p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r05_final3_surface_pmc_traffic.json"),
+    p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r06_final_surface_pmc_traffic.json"),
                    help="PMC traffic summary of the surface-scene bench (tools/pmc_traffic.py)")
     p.add_argument("--config-e-traffic-json", default=os.path.join(ROOT, "profiles", "r06_config_e_pmc_traffic.json"),
                    help="PMC FETCH/WRITE summary of the config-E leg alone (tools/config_e_leg.py under tools/profile_round.sh)")
