@@ -560,7 +560,9 @@ def main():
         "us_per_launch": round(1000.0 * ms / launches, 2),
     }
     roofline["frac"] = round(roofline["achieved"] / roofline["peak"], 4)
-    roofline["traffic"] = pmc_traffic(args.traffic_json, dom, units / launches)
+    # the PMC summary of the same scene (bench.py --scene synthetic profiles the surface scene)
+    roofline["traffic"] = pmc_traffic(args.surface_traffic_json if args.scene == "synthetic" else args.traffic_json,
+                                      dom, units / launches)
     if dom == "render_encode" and split["render_s"] > 0:
         # the same algorithmic bytes over a whole frame: one frame's encode bytes / the frame's wall time
         frame_s = split["render_s"] / args.steps
