@@ -67,7 +67,7 @@ def parse():
                    help="N=1: 1080p renders timed through render_to_device() (the frame stays in HBM) -> render_in_hbm")
     p.add_argument("--surface-traffic-json", default=os.path.join(ROOT, "profiles", "r06_final_surface_pmc_traffic.json"),
                    help="PMC traffic summary of the surface-scene bench (tools/pmc_traffic.py)")
-    p.add_argument("--config-e-traffic-json", default=os.path.join(ROOT, "profiles", "r06_config_e_pmc_traffic.json"),
+    p.add_argument("--config-e-traffic-json", default=os.path.join(ROOT, "profiles", "r06_config_e_final_pmc_traffic.json"),
                    help="PMC FETCH/WRITE summary of the config-E leg alone (tools/config_e_leg.py under tools/profile_round.sh)")
     p.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r06_final_pmc_traffic.json"),
                    help="per-kernel HBM bytes from rocprofv3 --pmc FETCH_SIZE/WRITE_SIZE passes (tools/pmc_traffic.py)")
