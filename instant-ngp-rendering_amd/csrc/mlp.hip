@@ -1376,12 +1376,16 @@ void launch_mlp_infer(const ngp_model* m, const __half* frags, const __half* enc
 		// SIMD, MFMA busy 0.46.  With two ray pipelines the other pipeline's encoder shares the CUs and the
 		// 64-sample steps measured 0-2 % faster per frame; with one (surface scenes) the 32-sample steps 1-2 %
 		// (profiles/r04_mlp_tile_ab.txt): the renderer picks per frame (RenderScratch::mlp_tile)
-		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : m->rs.mlp_tile;
+		// (the network alone, ngp_model_infer_sh_rows: 32-sample steps, see the decoupled pipeline below)
+		const uint32_t tile = m->tuning.render_mlp_tile ? m->tuning.render_mlp_tile : (x.standalone ? 2u : m->rs.mlp_tile);
 		// the 64-sample steps beside the other pipeline's encoder: 6 workgroups per CU (13.60 vs 13.67 ms per fire frame
 		// against 8 with 6 M passes; profiles/r05_schedule_sweep.txt)
 		const uint32_t wg_render = m->tuning.mlp_workgroups_per_cu ? m->tuning.mlp_workgroups_per_cu : 6u;
 		// the decoupled load pipeline (k_mlp_infer_sh, ngp_tuning.render_mlp_pipeline 2 / 3; 1 = the round-5 ring)
-		const uint32_t pipe = m->tuning.render_mlp_pipeline ? m->tuning.render_mlp_pipeline : 2u;
+		// alone on the GPU the two-tile-deep ring (3) at 32-sample steps and 4 workgroups per CU measured best (0.40 of
+		// the fp16 peak vs 0.39 for 2; in frame 3 is 0.5 % slower per fire frame: profiles/r06_mlp_microbench_wg_sweep.txt,
+		// r06_render_mlp_pipeline_ab.txt)
+		const uint32_t pipe = m->tuning.render_mlp_pipeline ? m->tuning.render_mlp_pipeline : (x.standalone ? 3u : 2u);
 		bool done = false;
 		if constexpr (N::XE == 0) {
 			if (sh && a.F == 2 && pl && pipe >= 2 && out_mode == 0) {

@@ -462,9 +462,11 @@ ngp_status ngp_model_infer_sh_rows(ngp_model* m, const uint16_t* enc, const uint
 		                                                                  m->lt.F, n, lay);
 		NGP_HIP_CHECK(hipGetLastError());
 		// the renderer's network call: its timer (NGP_TIMER_RENDER_MLP) rides on the MLP dispatch alone
+		MlpExtra standalone;
+		standalone.standalone = true;
 		m->timers.begin_kernel(NGP_TIMER_RENDER_MLP);
 		launch_mlp_infer(m, frags, ts.enc.ptr, lay, nullptr, 0, n, reinterpret_cast<__half*>(out), S(s), nullptr, 4,
-		                 reinterpret_cast<const __half*>(sh_rows), 0, 4, sh_row_of_sample, n_rows, false, MlpExtra{});
+		                 reinterpret_cast<const __half*>(sh_rows), 0, 4, sh_row_of_sample, n_rows, false, standalone);
 		m->timers.end(NGP_TIMER_RENDER_MLP, S(s), n);
 	});
 }

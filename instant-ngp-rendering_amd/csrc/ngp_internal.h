@@ -503,6 +503,9 @@ struct MlpExtra {
 	const float* extra = nullptr;
 	const uint32_t* sample_img = nullptr;
 	float* dextra = nullptr;
+	// the network alone on the GPU (ngp_model_infer_sh_rows), not beside the renderer's other ray pipeline: the
+	// untuned render-MLP schedule defaults to the standalone optimum (launch_mlp_infer)
+	bool standalone = false;
 };
 // coords: per-sample records of coord_stride floats holding the warped direction at
 // dir_offset (NerfCoordinate: 4); sh (optional): [n][16] fp16 SH rows used instead

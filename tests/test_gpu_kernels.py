@@ -117,7 +117,7 @@ def test_infer_sh_rows_matches_oracle_under_every_render_mlp_tuning(name):
                       1).astype(np.float16)
         e, r, ri = dev(enc.view(np.int16)), dev(sh.view(np.int16)), dev((np.arange(n) // per_ray).astype(np.int32))
         outs = {}
-        for pipe, tile, wg in ((1, 4, 0), (2, 4, 0), (2, 4, 2), (2, 2, 0), (2, 1, 0), (3, 4, 0), (3, 2, 4)):
+        for pipe, tile, wg in ((0, 0, 0), (1, 4, 0), (2, 4, 0), (2, 4, 2), (2, 2, 0), (2, 1, 0), (3, 4, 0), (3, 2, 4)):
             g.set_tuning(render_mlp_pipeline=pipe, render_mlp_tile=tile, mlp_workgroups_per_cu=wg)
             out = torch.full(((n + 64) * 4,), -7.0, dtype=torch.float16, device="cuda")
             A.check(g.lib.ngp_model_infer_sh_rows(g.h, vp(e), vp(r), vp(ri), n, rays, vp(out), 0, stream()))
