@@ -222,28 +222,32 @@ def test_trained_field_at_the_reference_resolution_against_its_density_mosaic():
 
 
 def test_black_background_training_on_the_reference_scene_has_no_backdrop():
-    """test_trained_field_against_the_reference_density_mosaic's control: test2 trained with a black background
-    (random_bg_color False; quarter resolution, default mode, seeds 1337 and 1) forms the flame alone in every run
-    measured (13 of 13 at 35 k steps: seed-versus-seed IoU 0.61-0.73, 0.03-0.04x the reference's occupied volume;
-    profiles/r06_collapse_sweep.txt and r06_collapse_sweep_test2_black_bg_trajectory.txt): the two runs must agree with
-    each other and hold none of the backdrop density random-background training builds.
-    The training-view PSNR is printed, not asserted: black-background runs pass through transient density excursions
-    (2 of 5 trajectory runs: density-grid max up to 1e14 between 5 k and 30 k steps, then recovered), and a run that
-    ends inside one renders at ~21 dB while its network's field is already the flame again -- this test asserted
-    PSNR > 33 dB and measured 21.0 dB once (the round-6 suite run); the other 13 ended at 36.4-42.0 dB."""
+    """The mosaic pins' control: test2 at the reference's resolution (720x1280) trained with a black background
+    (random_bg_color False, default mode, seeds 1337 and 1) forms the flame alone -- the reference's 13.3 % is the flame
+    plus the backdrop density random-background training builds.  The sweep measured it first (8 of 8 seeds, no density
+    excursion on the way: occupied volume 0.037-0.039x the reference's, seed-versus-seed IoU 0.85-0.89, training-view
+    PSNR 32.1-35.8 dB; profiles/r06_collapse_sweep_test2_full_black_bg.jsonl, r06_collapse_sweep.txt).  Thresholds: the
+    measured ranges widened by about a third.
+    This control first trained the quarter-resolution copy, where black-background runs are not stable: they pass
+    through transient density excursions (2 of 5 trajectories) and 2 of 17 ended inside one or painted on the box
+    (21.0 dB; ratio 6.9 at 25.6 dB -- the round-6 suite runs, profiles/r06_gpu_tests_suite*.txt), as random-background
+    runs do more often at low resolution."""
     import density_slices_util as D
     import pyngp as ngp
     ref = D.reference_volume("test2") >= 129
     occ_black, psnr = [], []
     for seed in (1337, 1):
-        tb = D.new_testbed(ngp, "test2", "base.json", seed, random_bg_color=False)
+        tb = D.new_testbed(ngp, "test2_full", "base.json", seed, random_bg_color=False)
         D.train_to(tb, 35000)
+        rays = tb.last_train_stats()["n_rays"]
         occ_black.append(D.testbed_volume(tb) >= 129)
         psnr.append(round(_training_view_psnr(tb), 2))
+        assert rays < (1 << 18), rays
         del tb
     a, b = occ_black
     iou = float((a & b).sum() / max((a | b).sum(), 1))
     ratios = [float(o.mean() / ref.mean()) for o in occ_black]
-    print(f"test2 black background: seed vs seed IoU {iou:.3f}, occupied ratios {ratios}, training-view PSNR {psnr}")
-    assert iou > 0.45, iou
+    print(f"test2_full black background: seed vs seed IoU {iou:.3f}, occupied ratios {ratios}, training-view PSNR {psnr}")
+    assert iou > 0.55, iou
     assert max(ratios) < 0.1, ratios
+    assert min(psnr) > 24.0, psnr
