@@ -452,7 +452,9 @@ ngp_status ngp_model_infer_padded(ngp_model* model, const float* coords, uint32_
  * src/testbed_nerf.cu:1720): enc [n_levels][n][F] fp16 (level-major, as ngp_model_encode writes), sh_rows
  * [n_rows][16] fp16 = the degree-4 SH of each ray's warped direction (the dir encoding, computed once per ray),
  * sh_row_of_sample [n] u32 = the row of each sample.  out: [n][4] fp16 as ngp_model_infer.  Timed by
- * NGP_TIMER_RENDER_MLP (the MLP dispatch alone).  Networks without extra dims. */
+ * NGP_TIMER_RENDER_MLP (the MLP dispatch alone).  Networks without extra dims.  Untuned (ngp_tuning render_mlp_pipeline /
+ * render_mlp_tile / mlp_workgroups_per_cu 0) it runs the schedule measured best for the network alone on the GPU
+ * (the two-tile-deep ring at 32-sample steps, 4 workgroups per CU), not the renderer's. */
 ngp_status ngp_model_infer_sh_rows(ngp_model* model, const uint16_t* enc, const uint16_t* sh_rows,
                                    const uint32_t* sh_row_of_sample, uint32_t n, uint32_t n_rows, uint16_t* out,
                                    int use_inference_params, ngp_stream stream);
