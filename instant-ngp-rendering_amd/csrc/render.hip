@@ -469,14 +469,25 @@ __global__ void __launch_bounds__(256) k_df_yz(const uint8_t* __restrict__ fin, 
 	const int c0 = AXIS == 1 ? (int)y : (int)z;
 	const uint32_t stride = AXIS == 1 ? NERF_GRIDSIZE : NERF_GRIDSIZE * NERF_GRIDSIZE;
 	uint32_t h = f[cell];
-	for (uint32_t k = 1; k < h; ++k) {
-		const int c = neg ? c0 - (int)k : c0 + (int)k;
-		if (c < 0 || c >= (int)NERF_GRIDSIZE) {
+	// k = 1, 2, ... while k < h, eight lattice steps per round: the eight byte loads of a round are independent
+	// (one serial load per step made the pass latency-bound: ~300 us per pass on mostly empty grids).  Steps of a
+	// round at or past the final h change nothing (max(k, f) >= k >= h), so the result is the step-by-step one.
+	const uint32_t lim = neg ? (uint32_t)c0 : NERF_GRIDSIZE - 1u - (uint32_t)c0;  // steps before leaving the grid
+	const int sstride = neg ? -(int)stride : (int)stride;
+	uint32_t k = 1;
+	while (k < h) {
+		if (k > lim) {  // the next step leaves the grid: occupied below max_mip (the next mip), outside the AABB at it
 			if (mip < max_mip) h = k;
 			break;
 		}
-		const uint32_t fk = f[(uint32_t)((int)cell + (c - c0) * (int)stride)];
-		h = min(h, max(k, fk));
+		const uint32_t kend = min(k + 8u, lim + 1u);
+		uint32_t fk[8];
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u) fk[u] = k + u < kend ? f[(uint32_t)((int)cell + (int)(k + u) * sstride)] : 255u;
+#pragma unroll
+		for (uint32_t u = 0; u < 8; ++u)
+			if (k + u < kend) h = min(h, max(k + u, fk[u]));
+		k = kend;
 	}
 	fout[(size_t)(mip * 2u * NV_IN + v) * DF_BYTES_PER_FIELD + cell] = (uint8_t)h;
 	(void)x;
