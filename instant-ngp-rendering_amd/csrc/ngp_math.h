@@ -594,6 +594,7 @@ NGP_HD uint32_t df_index(uint32_t mip, uint32_t oct, int ix, int iy, int iz) {
 // lattice_step through the octant distance fields: same result as lattice_step (the point is
 // occupied iff D = 0 at its mip; the coarsest empty mip is climbed as the reference does), but
 // an empty cell is left through the far faces of its empty D-box in one verified jump.
+template <bool PARALLEL_CLIMB = false>
 NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir, uint32_t oct, const uint8_t* df,
                            uint32_t max_mip, const RenderBox& aabb) {
 	const float n = *n_io;
@@ -608,8 +609,37 @@ NGP_HD int lattice_step_df(float* n_io, const Stepping& st, v3 o, v3 d, v3 idir,
 		return LATTICE_SKIPPED;
 	}
 	uint32_t D = df[df_index(mip, oct, cx, cy, cz)];
+	if (PARALLEL_CLIMB) {
+		// coarsest empty mip, as the reference climbs, with every mip's distance fetched at once -- this mip's and the
+		// coarser ones' (their cells depend on the position only) -- and climbed in registers: one load latency per
+		// lattice step instead of one per mip visited.  Used by k_render_init, whose skip to the first sample crosses
+		// config E's seven cascades; the march kernels run at 64 VGPRs, where these registers spill, and keep the
+		// serial climb below.  The chosen mip's cell is recomputed.
+		constexpr uint32_t MAXQ = NERF_CASCADES - 1;
+		uint32_t Du[MAXQ], inmask = 0;
+#pragma unroll
+		for (uint32_t q = 0; q < MAXQ; ++q) {
+			const uint32_t mq = mip + 1u + q;
+			int ux, uy, uz;
+			const bool in = mq <= max_mip && cascaded_cell_at(pos, mq, &ux, &uy, &uz);
+			inmask |= (in ? 1u : 0u) << q;
+			Du[q] = in ? df[df_index(mq, oct, ux, uy, uz)] : 0u;
+		}
+		if (D == 0u) return LATTICE_OCCUPIED;
+		uint32_t top = mip;
+#pragma unroll
+		for (uint32_t q = 0; q < MAXQ; ++q) {
+			if (!((inmask >> q) & 1u) || Du[q] == 0u) break;
+			top = mip + 1u + q;
+			D = Du[q];
+		}
+		if (top != mip) {
+			mip = top;
+			cascaded_cell_at(pos, mip, &cx, &cy, &cz);
+		}
+	}
 	if (D == 0u) return LATTICE_OCCUPIED;
-	while (mip < max_mip) {  // coarsest empty mip, as the reference climbs
+	while (!PARALLEL_CLIMB && mip < max_mip) {  // coarsest empty mip, as the reference climbs
 		int ux, uy, uz;
 		if (!cascaded_cell_at(pos, mip + 1, &ux, &uy, &uz)) break;
 		const uint32_t Du = df[df_index(mip + 1, oct, ux, uy, uz)];
