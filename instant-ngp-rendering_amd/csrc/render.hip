@@ -357,7 +357,9 @@ __device__ __forceinline__ bool init_ray_body(const RenderK& k, uint32_t x, uint
 		int st;
 		uint32_t steps = 0;
 		do {
-			st = lattice_step_df<true>(&n, k.st, origin, dir, idir, oct, k.df, k.max_mip, k.aabb);
+			// several cascades (aabb_scale > 1): every mip's distance fetched at once; one cascade: nothing to climb
+			st = k.max_mip ? lattice_step_df<true>(&n, k.st, origin, dir, idir, oct, k.df, k.max_mip, k.aabb)
+			               : lattice_step_df<false>(&n, k.st, origin, dir, idir, oct, k.df, k.max_mip, k.aabb);
 			++steps;
 		} while (st == LATTICE_SKIPPED);
 		alive = st == LATTICE_OCCUPIED;
